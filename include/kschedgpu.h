@@ -1,0 +1,206 @@
+/*
+ * kschedgpu.h — C ABI of libkschedgpu.so, the MI355X-native Filter/Score pass of
+ * the kube-scheduler generic scheduler (smarterclayton/kubernetes v0.13.0-dev).
+ *
+ * What this ABI replaces (reference file:line, all under /root/reference):
+ *   algorithm.Scheduler.Schedule(pod, minionLister)      pkg/scheduler/scheduler.go:25-27
+ *     implemented by genericScheduler.Schedule           pkg/scheduler/generic_scheduler.go:54-80
+ *       findNodesThatFit                                 pkg/scheduler/generic_scheduler.go:100-128
+ *       prioritizeNodes                                  pkg/scheduler/generic_scheduler.go:136-165
+ *       selectHost / getBestHosts                        pkg/scheduler/generic_scheduler.go:84-96,167-177
+ *   SystemModeler.AssumePod (the commit)                 plugin/pkg/scheduler/scheduler.go:42-47,115-118
+ *   NewGenericScheduler(predicates, prioritizers, ...)   pkg/scheduler/generic_scheduler.go:197-204
+ *     built by ConfigFactory.CreateFromKeys              plugin/pkg/scheduler/factory/factory.go:107-172
+ *
+ * Conventions
+ *   - Strings never cross this ABI. The caller (the Go cgo shim, or the Python
+ *     mirror in kubernetes_amd/) interns node names, label (key,value) pairs,
+ *     label keys, host ports, GCE PD names and services to dense ids.
+ *   - Node "rank" = index of the node in byte-wise ascending name order. The
+ *     reference's tie order (score desc, host name desc; types.go:42-47) is
+ *     therefore "rank desc".
+ *   - All input arrays are caller-owned and copied before return. Output
+ *     buffers are caller-allocated.
+ *   - Return codes: KSG_OK (0); KSG_NOFIT (1) = *FitError; KSG_NONODES (2) =
+ *     "no minions available to schedule pods"; negative = internal error, see
+ *     ksg_last_error(). There is NO CPU fallback inside this library: every
+ *     predicate/priority evaluation runs in HIP kernels on the GPU.
+ *   - One scheduling thread per context (the reference calls Schedule from one
+ *     goroutine, plugin/pkg/scheduler/scheduler.go:86-88).
+ */
+#ifndef KSCHEDGPU_H_
+#define KSCHEDGPU_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KSG_ABI_VERSION 1
+
+/* ---- return codes ---------------------------------------------------- */
+#define KSG_OK 0
+#define KSG_NOFIT 1          /* generic_scheduler.go:72-77  *FitError              */
+#define KSG_NONODES 2        /* generic_scheduler.go:59-61  no minions available   */
+#define KSG_ERR_ARG (-1)
+#define KSG_ERR_HIP (-2)
+#define KSG_ERR_CAPACITY (-3)
+#define KSG_ERR_STATE (-4)
+#define KSG_ERR_NOPEER (-5)  /* predicates.go:293-296: service peer's host is not a known node */
+#define KSG_ERR_RCCL (-6)
+
+/* out_nodes[] codes of ksg_schedule_batch (>= 0 is a node rank) */
+#define KSG_OUT_NOFIT (-1)
+#define KSG_OUT_ERROR (-2)
+#define KSG_OUT_NONODES (-3)
+
+/* ---- predicates (FitPredicate registry names, factory/plugins.go:63-117) */
+#define KSG_PRED_PODFITSPORTS      (1u << 0) /* predicates.go:326-350 */
+#define KSG_PRED_PODFITSRESOURCES  (1u << 1) /* predicates.go:94-145  */
+#define KSG_PRED_NODISKCONFLICT    (1u << 2) /* predicates.go:52-83   */
+#define KSG_PRED_MATCHNODESELECTOR (1u << 3) /* predicates.go:161-179 */
+#define KSG_PRED_HOSTNAME          (1u << 4) /* predicates.go:181-186 */
+#define KSG_PRED_SERVICEAFFINITY   (1u << 5) /* predicates.go:231-324 (policy) */
+#define KSG_PRED_LABELSPRESENCE    (1u << 6) /* predicates.go:188-229 (policy) */
+
+/* fail codes written per node by ksg_schedule_begin/ksg_evaluate:
+ * 0 = fits, otherwise the first failing predicate in this fixed order. */
+#define KSG_FAIL_NONE 0
+#define KSG_FAIL_HOSTNAME 1
+#define KSG_FAIL_LABELSPRESENCE 2
+#define KSG_FAIL_MATCHNODESELECTOR 3
+#define KSG_FAIL_NODISKCONFLICT 4
+#define KSG_FAIL_PODFITSPORTS 5
+#define KSG_FAIL_PODFITSRESOURCES 6
+#define KSG_FAIL_SERVICEAFFINITY 7
+
+#define KSG_MAX_ANTI 4          /* ServiceAntiAffinity priorities (policy)      */
+#define KSG_MAX_LABEL_PREF 8    /* LabelPreference priorities (policy)          */
+#define KSG_MAX_PRESENCE 8      /* LabelsPresence predicates (policy)           */
+#define KSG_MAX_PRESENCE_KEYS 8 /* labels per LabelsPresence predicate          */
+#define KSG_MAX_AFF 4           /* ServiceAffinity labels (union of predicates) */
+
+/* Scheduler configuration: the compiled form of map[string]FitPredicate +
+ * []PriorityConfig that NewGenericScheduler receives (factory.go:149). */
+typedef struct ksg_config {
+  uint32_t predicates;          /* KSG_PRED_* bitmask                                   */
+  uint32_t n_priority_configs;  /* len(priorityConfigs); 0 => EqualPriority fallback
+                                   (generic_scheduler.go:141-143)                       */
+  int32_t w_least_requested;    /* LeastRequestedPriority weight, 0 = absent/skipped    */
+  int32_t w_service_spreading;  /* ServiceSpreadingPriority weight                       */
+  int32_t w_equal;              /* EqualPriority weight (DefaultProvider: 0, skipped)    */
+  uint32_t n_anti;              /* ServiceAntiAffinity priorities                        */
+  uint32_t anti_key[KSG_MAX_ANTI];   /* label-key id of each                           */
+  int32_t w_anti[KSG_MAX_ANTI];
+  uint32_t n_label_pref;        /* LabelPreference priorities                            */
+  uint32_t pref_key[KSG_MAX_LABEL_PREF];
+  uint32_t pref_presence[KSG_MAX_LABEL_PREF];
+  int32_t w_pref[KSG_MAX_LABEL_PREF];
+  uint32_t n_presence;          /* LabelsPresence predicates                             */
+  uint32_t presence_n_keys[KSG_MAX_PRESENCE];
+  uint32_t presence_keys[KSG_MAX_PRESENCE][KSG_MAX_PRESENCE_KEYS];
+  uint32_t presence_flag[KSG_MAX_PRESENCE];
+  uint32_t n_aff_labels;        /* ServiceAffinity: label-key ids (union over predicates) */
+  uint32_t aff_key[KSG_MAX_AFF];
+  uint32_t max_conflict_keys;   /* capacity for interned host-port + GCE-PD ids          */
+  uint32_t max_domains;         /* capacity for anti-affinity label values (pair ids)    */
+} ksg_config;
+
+/* One node, rank-ordered. Capacity is node.Spec.Capacity converted with
+ * Quantity.MilliValue (cpu) / Value (memory) (resource_helpers.go:29-42). */
+typedef struct ksg_node {
+  int64_t cap_milli_cpu;
+  int64_t cap_memory;
+  uint32_t label_off;   /* offset into node_pairs[] of this node's label pair ids */
+  uint32_t n_labels;
+} ksg_node;
+
+/* One pod (pending or existing). Variable-length lists are (offset, count)
+ * into a caller-supplied uint32 id array passed alongside. */
+typedef struct ksg_pod {
+  uint64_t uid;         /* caller-unique id (namespace/name) for ksg_remove_pod     */
+  int64_t milli_cpu;    /* getResourceRequest: sum of container Limits cpu (milli)  */
+  int64_t memory;       /* ... and memory (bytes) (predicates.go:94-102)            */
+  int32_t host;         /* Spec.Host: -1 empty, -2 names no node, else node rank    */
+  int32_t service;      /* services[0] of GetPodServices, -1 none                   */
+  uint32_t ports_off, n_ports;  /* conflict-key ids of HostPorts != 0               */
+  uint32_t pds_off, n_pds;      /* conflict-key ids of GCE PD names                 */
+  uint32_t sel_off, n_sel;      /* nodeSelector pair ids; 0 = pair no node has;
+                                   n_sel == 0 => selector matches everything        */
+  uint32_t svcs_off, n_svcs;    /* every service whose selector matches the pod     */
+  int32_t aff_pair[KSG_MAX_AFF];/* ServiceAffinity: pair id of the pod's own
+                                   nodeSelector value for aff label j; -1 = the pod
+                                   does not specify it; 0 = value no node has        */
+} ksg_pod;
+
+typedef struct ksg_ctx ksg_ctx;
+
+/* Create a context on HIP device `device`. Single-GPU form. */
+int ksg_create(const ksg_config* cfg, int device, ksg_ctx** out);
+
+/* Node-sharded form: `world` processes, one per GPU, each owning node ranks
+ * [rank*N/world, (rank+1)*N/world). Node state is replicated; evaluation is
+ * sharded; the per-pod winner is exchanged with RCCL (all-gather of a packed
+ * {score, tie count} word). `nccl_id` is the 128-byte ncclUniqueId from rank 0. */
+int ksg_create_sharded(const ksg_config* cfg, int device, int rank, int world,
+                       const void* nccl_id, ksg_ctx** out);
+/* Fill a fresh ncclUniqueId (128 bytes) for ksg_create_sharded on rank 0. */
+int ksg_nccl_unique_id(void* out128);
+
+int ksg_destroy(ksg_ctx* ctx);
+const char* ksg_last_error(ksg_ctx* ctx);
+
+/* Replace the node set (MinionLister.List()). Resets all pod state.
+ * pair_keys[p] = label-key id of label pair p (pair 0 is reserved: "no node has
+ * it"). node_pairs holds each node's label pair ids. */
+int ksg_set_cluster(ksg_ctx* ctx, const ksg_node* nodes, uint32_t n_nodes,
+                    const uint32_t* node_pairs, uint32_t n_node_pairs,
+                    const uint32_t* pair_keys, uint32_t n_pairs,
+                    uint32_t n_services);
+
+/* Existing / assumed pods (SimpleModeler.AssumePod + scheduled-pod store).
+ * host_id < n_nodes is a node rank (Status.Host); host_id >= n_nodes is a host
+ * that is not in the node list (still counted by ServiceSpreading's maxCount,
+ * spreading.go:73-80). */
+int ksg_add_pod(ksg_ctx* ctx, uint32_t host_id, const ksg_pod* pod, const uint32_t* ids);
+int ksg_remove_pod(ksg_ctx* ctx, uint64_t uid);
+
+/* Split Schedule: begin evaluates every node and reports the best combined
+ * score and the number of nodes tied at it (0 => KSG_NOFIT). The caller draws
+ * r = rand.Int() iff tie_count > 0 and calls commit(r % tie_count), which picks
+ * the tie_index-th tie in descending name order (generic_scheduler.go:88-95)
+ * and applies AssumePod's delta. fail_codes (optional, n_nodes bytes) gets the
+ * per-node KSG_FAIL_* code to rebuild FailedPredicateMap. */
+int ksg_schedule_begin(ksg_ctx* ctx, const ksg_pod* pod, const uint32_t* ids,
+                       int64_t* max_score, uint32_t* tie_count, uint8_t* fail_codes);
+int ksg_schedule_commit(ksg_ctx* ctx, uint32_t tie_index, int32_t* out_node);
+
+/* Schedule n pods in order, committing each before the next, entirely on the
+ * device. Tie-break source: splitmix64 with state *rng_state; one Int63 draw
+ * (next() >> 1) per successful schedule only (generic_scheduler.go:94).
+ * out_nodes[i] = node rank or KSG_OUT_*. *rng_state is advanced. */
+int ksg_schedule_batch(ksg_ctx* ctx, const ksg_pod* pods, uint32_t n,
+                       const uint32_t* ids, uint32_t n_ids,
+                       uint64_t* rng_state, int32_t* out_nodes);
+
+/* Introspection (HostPriorityList): per-node fail code and combined score for
+ * a pod, without committing. score_out[i] is meaningful where fail_out[i]==0. */
+int ksg_evaluate(ksg_ctx* ctx, const ksg_pod* pod, const uint32_t* ids,
+                 uint8_t* fail_out, int64_t* score_out);
+
+/* Device time (ms) of the last ksg_schedule_batch's kernels, from HIP events
+ * recorded on the stream the kernels ran on. */
+int ksg_last_batch_ms(ksg_ctx* ctx, double* ms);
+
+/* Node shard owned by this context: [lo, hi). */
+int ksg_shard(ksg_ctx* ctx, uint32_t* lo, uint32_t* hi);
+
+/* Copy the committed per-node requested totals (sum of limits of all pods on
+ * the node) back to the host, for state checks. */
+int ksg_read_requested(ksg_ctx* ctx, int64_t* milli_cpu, int64_t* memory);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KSCHEDGPU_H_ */

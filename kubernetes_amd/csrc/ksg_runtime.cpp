@@ -1,0 +1,844 @@
+// ksg_runtime.cpp — host runtime of libkschedgpu.so: the C ABI in
+// include/kschedgpu.h, the device-state mirror, and the RCCL exchange.
+//
+// Reference behaviour mirrored here (under /root/reference):
+//   genericScheduler.Schedule / selectHost     pkg/scheduler/generic_scheduler.go:54-96
+//   MapPodsToMachines (pods keyed by Status.Host)  pkg/scheduler/predicates.go:354-375
+//   SimpleModeler.AssumePod / listPods        plugin/pkg/scheduler/modeler.go:77-139
+//   ServiceSpread maxCount over all hosts     pkg/scheduler/spreading.go:72-80
+//
+// The library keeps a host mirror of the mutable per-node state (requested
+// totals, conflict-key reference counts, per-service pod counts and peers) so
+// ksg_remove_pod can undo exactly; the device copy is authoritative for
+// scheduling and is patched from the mirror. All scheduling decisions run in
+// the HIP kernels (ksg_kernels.hip); there is no CPU evaluation path.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "ksg_internal.h"
+
+
+hipError_t ksg_launch_batch(int R, bool anti, const KsgDev& d, const ksg_pod* pods,
+                            const uint32_t* ids, uint32_t n, uint64_t* rng, int32_t* out,
+                            size_t lds, hipStream_t st);
+hipError_t ksg_launch_scan(int R, bool anti, const KsgDev& d, const ksg_pod* pods,
+                           const uint32_t* ids, int mode, int phase, uint8_t* fail_out,
+                           int64_t* score_out, uint8_t* record, int32_t* dpart,
+                           const int32_t* dglobal, size_t lds, hipStream_t st);
+hipError_t ksg_launch_decide(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids,
+                             const uint8_t* records, uint32_t rec_bytes, uint32_t world,
+                             const uint32_t* shard_wlo, int mode, uint64_t tie_index,
+                             uint64_t* rng, int32_t* out, uint32_t out_idx, int64_t* summary,
+                             hipStream_t st);
+hipError_t ksg_launch_static(const KsgStaticCfg& sc, uint32_t n_nodes, const ksg_node* nodes,
+                             const uint32_t* node_pairs, const uint32_t* pair_keys,
+                             const int32_t* dom_of_pair, uint32_t n_pairs, uint32_t nw,
+                             uint64_t* static_fit, int32_t* static_score, int32_t* anti_domain,
+                             int32_t* aff_pair, unsigned long long* pairmap, hipStream_t st);
+hipError_t ksg_launch_patch(const KsgPatch* patches, uint32_t n, hipStream_t st);
+
+namespace {
+
+struct PodRec {
+  uint32_t host;
+  int64_t cpu, mem;
+  std::vector<uint32_t> keys;  // ports + PDs
+  std::vector<uint32_t> svcs;
+  uint64_t seq;
+};
+
+constexpr uint32_t kMaxNodesPerShard = 32 * KSG_NT;
+
+}  // namespace
+
+struct ksg_ctx {
+  ksg_config cfg{};
+  int device = 0, rank = 0, world = 1;
+  hipStream_t st = nullptr;
+  ncclComm_t comm = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  double last_ms = 0.0;
+  std::string err;
+
+  // cluster
+  bool have_cluster = false;
+  uint32_t N = 0, nw = 0, n_pairs = 0, S = 0, D = 0;
+  uint32_t lo = 0, hi = 0, wlo = 0, nwords = 0, nwords_max = 0;
+  std::vector<uint32_t> shard_wlo_h;
+  int R = 1;
+  size_t lds = 0;
+  KsgDev dev{};
+  std::vector<void*> cluster_allocs;
+  uint32_t* d_shard_wlo = nullptr;
+
+  // scratch
+  ksg_pod* d_pods = nullptr;
+  size_t pods_cap = 0;
+  uint32_t* d_ids = nullptr;
+  size_t ids_cap = 0;
+  uint8_t* d_fail = nullptr;
+  int64_t* d_score = nullptr;
+  uint8_t* d_rec_send = nullptr;
+  uint8_t* d_rec_recv = nullptr;
+  uint32_t rec_bytes = 0;
+  int32_t* d_dpart = nullptr;
+  int32_t* d_dglobal = nullptr;
+  int32_t* d_out = nullptr;
+  size_t out_cap = 0;
+  uint64_t* d_rng = nullptr;
+  int64_t* d_summary = nullptr;
+  KsgPatch* d_patch = nullptr;
+  size_t patch_cap = 0;
+  std::vector<KsgPatch> patches;
+
+  // host mirror
+  std::vector<int64_t> used_c, used_m;
+  std::unordered_map<uint64_t, uint32_t> key_ref;  // (key << 32) | node
+  std::vector<int32_t> svc_cnt;                    // S*N
+  std::vector<std::unordered_map<uint32_t, int32_t>> svc_ext;
+  std::vector<int32_t> svc_max, svc_total, svc_peer;
+  std::vector<std::map<uint64_t, uint32_t>> svc_members;  // seq -> host
+  std::unordered_map<uint64_t, PodRec> pods;
+  uint64_t seq = 0;
+
+  // begin/commit
+  bool pending = false;
+  uint64_t pending_k = 0;
+  ksg_pod pend{};
+  std::vector<uint32_t> pend_ids;
+};
+
+namespace {
+
+int fail(ksg_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIPCHK(c, x)                                                                 \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess)                                                            \
+      return fail((c), KSG_ERR_HIP, "%s:%d %s: %s", __FILE__, __LINE__, #x,          \
+                  hipGetErrorString(e_));                                            \
+  } while (0)
+
+#define NCCLCHK(c, x)                                                                \
+  do {                                                                               \
+    ncclResult_t r_ = (x);                                                           \
+    if (r_ != ncclSuccess)                                                           \
+      return fail((c), KSG_ERR_RCCL, "%s:%d %s: %s", __FILE__, __LINE__, #x,         \
+                  ncclGetErrorString(r_));                                           \
+  } while (0)
+
+template <typename T>
+int dalloc(ksg_ctx* c, T** p, size_t count, std::vector<void*>* owner) {
+  void* q = nullptr;
+  HIPCHK(c, hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T)));
+  HIPCHK(c, hipMemsetAsync(q, 0, std::max<size_t>(count, 1) * sizeof(T), c->st));
+  *p = static_cast<T*>(q);
+  if (owner) owner->push_back(q);
+  return KSG_OK;
+}
+
+void free_cluster(ksg_ctx* c) {
+  for (void* p : c->cluster_allocs) (void)hipFree(p);
+  c->cluster_allocs.clear();
+  c->have_cluster = false;
+}
+
+int grow(ksg_ctx* c, void** p, size_t* cap, size_t need, size_t elem) {
+  if (need <= *cap && *p) return KSG_OK;
+  size_t nc = std::max<size_t>(need, std::max<size_t>(*cap * 2, 64));
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  HIPCHK(c, hipMalloc(p, nc * elem));
+  *cap = nc;
+  return KSG_OK;
+}
+
+int pick_R(uint32_t shard_nodes) {
+  const uint32_t r = (shard_nodes + KSG_NT - 1) / KSG_NT;
+  int R = 1;
+  while ((uint32_t)R < r) R <<= 1;
+  return R;
+}
+
+// ---- patches: host-mirror deltas applied on the device in order ----------
+void patch32(ksg_ctx* c, const void* addr, int32_t v) {
+  c->patches.push_back(KsgPatch{(uint64_t)(uintptr_t)addr, (uint64_t)(uint32_t)v, 0, 0});
+}
+void patch64(ksg_ctx* c, const void* addr, int64_t v) {
+  c->patches.push_back(KsgPatch{(uint64_t)(uintptr_t)addr, (uint64_t)v, 1, 0});
+}
+void patch_or(ksg_ctx* c, const void* addr, uint64_t v) {
+  c->patches.push_back(KsgPatch{(uint64_t)(uintptr_t)addr, v, 2, 0});
+}
+void patch_andnot(ksg_ctx* c, const void* addr, uint64_t v) {
+  c->patches.push_back(KsgPatch{(uint64_t)(uintptr_t)addr, v, 3, 0});
+}
+
+int flush_patches(ksg_ctx* c) {
+  if (c->patches.empty()) return KSG_OK;
+  int rc = grow(c, (void**)&c->d_patch, &c->patch_cap, c->patches.size(), sizeof(KsgPatch));
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->d_patch, c->patches.data(), c->patches.size() * sizeof(KsgPatch),
+                           hipMemcpyHostToDevice, c->st));
+  HIPCHK(c, ksg_launch_patch(c->d_patch, (uint32_t)c->patches.size(), c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));  // host vector is reused
+  c->patches.clear();
+  return KSG_OK;
+}
+
+int32_t peer_code(ksg_ctx* c, uint32_t s) {
+  if (c->svc_members[s].empty()) return -1;
+  const uint32_t h = c->svc_members[s].begin()->second;
+  return h < c->N ? (int32_t)h : -2;
+}
+
+int32_t recompute_max(ksg_ctx* c, uint32_t s) {
+  int32_t m = 0;
+  const int32_t* row = c->svc_cnt.data() + (size_t)s * c->N;
+  for (uint32_t n = 0; n < c->N; ++n) m = std::max(m, row[n]);
+  for (auto& kv : c->svc_ext[s]) m = std::max(m, kv.second);
+  return m;
+}
+
+// Mirror update for one pod placed on host h. emit=false when the device has
+// already applied the same delta (batch commit).
+int mirror_add(ksg_ctx* c, uint32_t h, const ksg_pod* p, const uint32_t* ids, bool emit) {
+  if (c->pods.count(p->uid)) return fail(c, KSG_ERR_ARG, "duplicate pod uid %llu", (unsigned long long)p->uid);
+  PodRec r;
+  r.host = h;
+  r.cpu = p->milli_cpu;
+  r.mem = p->memory;
+  r.seq = ++c->seq;
+  for (uint32_t i = 0; i < p->n_ports; ++i) r.keys.push_back(ids[p->ports_off + i]);
+  for (uint32_t i = 0; i < p->n_pds; ++i) r.keys.push_back(ids[p->pds_off + i]);
+  for (uint32_t i = 0; i < p->n_svcs; ++i) r.svcs.push_back(ids[p->svcs_off + i]);
+  for (uint32_t k : r.keys)
+    if (k >= c->cfg.max_conflict_keys)
+      return fail(c, KSG_ERR_CAPACITY, "conflict key %u >= max_conflict_keys %u", k, c->cfg.max_conflict_keys);
+  for (uint32_t s : r.svcs)
+    if (s >= c->S) return fail(c, KSG_ERR_ARG, "service %u >= n_services %u", s, c->S);
+  if (h < c->N) {
+    c->used_c[h] = (int64_t)((uint64_t)c->used_c[h] + (uint64_t)r.cpu);
+    c->used_m[h] = (int64_t)((uint64_t)c->used_m[h] + (uint64_t)r.mem);
+    if (emit) {
+      patch64(c, c->dev.used_cpu + h, c->used_c[h]);
+      patch64(c, c->dev.used_mem + h, c->used_m[h]);
+    }
+    for (uint32_t k : r.keys) {
+      const uint32_t ref = ++c->key_ref[((uint64_t)k << 32) | h];
+      if (ref == 1 && emit) patch_or(c, c->dev.keymap + (size_t)k * c->nw + (h >> 6), 1ULL << (h & 63));
+    }
+  }
+  for (uint32_t s : r.svcs) {
+    int32_t v;
+    if (h < c->N) {
+      v = ++c->svc_cnt[(size_t)s * c->N + h];
+      if (emit) patch32(c, c->dev.svc_cnt + (size_t)s * c->N + h, v);
+    } else {
+      v = ++c->svc_ext[s][h];
+    }
+    if (v > c->svc_max[s]) {
+      c->svc_max[s] = v;
+      if (emit) patch32(c, c->dev.svc_max + s, v);
+    }
+    ++c->svc_total[s];
+    if (emit) patch32(c, c->dev.svc_total + s, c->svc_total[s]);
+    c->svc_members[s][r.seq] = h;
+    const int32_t pc = peer_code(c, s);
+    if (pc != c->svc_peer[s]) {
+      c->svc_peer[s] = pc;
+      if (emit) patch32(c, c->dev.svc_peer + s, pc);
+    }
+  }
+  c->pods.emplace(p->uid, std::move(r));
+  return KSG_OK;
+}
+
+void reset_mirror(ksg_ctx* c) {
+  c->used_c.assign(c->N, 0);
+  c->used_m.assign(c->N, 0);
+  c->key_ref.clear();
+  c->svc_cnt.assign((size_t)c->S * c->N, 0);
+  c->svc_ext.assign(c->S, {});
+  c->svc_max.assign(c->S, 0);
+  c->svc_total.assign(c->S, 0);
+  c->svc_peer.assign(c->S, -1);
+  c->svc_members.assign(c->S, {});
+  c->pods.clear();
+  c->seq = 0;
+  c->patches.clear();
+  c->pending = false;
+}
+
+int check_pod(ksg_ctx* c, const ksg_pod* p, const uint32_t* ids, size_t n_ids) {
+  auto in = [&](uint32_t off, uint32_t n) { return (size_t)off + n <= n_ids; };
+  if (!in(p->ports_off, p->n_ports) || !in(p->pds_off, p->n_pds) || !in(p->sel_off, p->n_sel) ||
+      !in(p->svcs_off, p->n_svcs))
+    return fail(c, KSG_ERR_ARG, "pod id list out of range");
+  if (p->host < -2 || p->host >= (int32_t)c->N) return fail(c, KSG_ERR_ARG, "pod host %d out of range", p->host);
+  if (p->service < -1 || p->service >= (int32_t)c->S) return fail(c, KSG_ERR_ARG, "pod service out of range");
+  for (uint32_t i = 0; i < p->n_ports; ++i)
+    if (ids[p->ports_off + i] >= c->cfg.max_conflict_keys) return fail(c, KSG_ERR_CAPACITY, "port key out of range");
+  for (uint32_t i = 0; i < p->n_pds; ++i)
+    if (ids[p->pds_off + i] >= c->cfg.max_conflict_keys) return fail(c, KSG_ERR_CAPACITY, "pd key out of range");
+  for (uint32_t i = 0; i < p->n_sel; ++i)
+    if (ids[p->sel_off + i] >= c->n_pairs) return fail(c, KSG_ERR_ARG, "selector pair out of range");
+  for (uint32_t i = 0; i < p->n_svcs; ++i)
+    if (ids[p->svcs_off + i] >= c->S) return fail(c, KSG_ERR_ARG, "service id out of range");
+  for (uint32_t j = 0; j < c->cfg.n_aff_labels; ++j)
+    if (p->aff_pair[j] >= (int32_t)c->n_pairs) return fail(c, KSG_ERR_ARG, "affinity pair out of range");
+  return KSG_OK;
+}
+
+// upload one pod + its id list into the single-pod scratch slots
+int upload_pods(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32_t* ids, size_t n_ids) {
+  int rc = grow(c, (void**)&c->d_pods, &c->pods_cap, n, sizeof(ksg_pod));
+  if (rc) return rc;
+  rc = grow(c, (void**)&c->d_ids, &c->ids_cap, std::max<size_t>(n_ids, 1), sizeof(uint32_t));
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->d_pods, pods, (size_t)n * sizeof(ksg_pod), hipMemcpyHostToDevice, c->st));
+  if (n_ids) HIPCHK(c, hipMemcpyAsync(c->d_ids, ids, n_ids * sizeof(uint32_t), hipMemcpyHostToDevice, c->st));
+  return KSG_OK;
+}
+
+size_t pod_ids_extent(const ksg_pod* p) {
+  size_t e = 0;
+  e = std::max<size_t>(e, (size_t)p->ports_off + p->n_ports);
+  e = std::max<size_t>(e, (size_t)p->pds_off + p->n_pds);
+  e = std::max<size_t>(e, (size_t)p->sel_off + p->n_sel);
+  e = std::max<size_t>(e, (size_t)p->svcs_off + p->n_svcs);
+  return e;
+}
+
+bool anti_on(const ksg_ctx* c) { return c->cfg.n_anti > 0 && c->dev.n_domains_total > 0; }
+
+// one pod through scan [+ dcount all-reduce] + record all-gather (device only)
+int scan_exchange(ksg_ctx* c, const ksg_pod* dpod, const uint32_t* dids, int mode, uint8_t* fail_out,
+                  int64_t* score_out) {
+  const bool anti = anti_on(c);
+  if (anti && c->world > 1) {
+    HIPCHK(c, ksg_launch_scan(c->R, true, c->dev, dpod, dids, mode, 1, nullptr, nullptr, c->d_rec_send,
+                              c->d_dpart, nullptr, c->lds, c->st));
+    NCCLCHK(c, ncclAllReduce(c->d_dpart, c->d_dglobal, c->dev.n_domains_total, ncclInt32, ncclSum, c->comm,
+                             c->st));
+    HIPCHK(c, ksg_launch_scan(c->R, true, c->dev, dpod, dids, mode, 2, fail_out, score_out, c->d_rec_send,
+                              nullptr, c->d_dglobal, c->lds, c->st));
+  } else {
+    HIPCHK(c, ksg_launch_scan(c->R, anti, c->dev, dpod, dids, mode, 0, fail_out, score_out, c->d_rec_send,
+                              nullptr, nullptr, c->lds, c->st));
+  }
+  if (mode == KSG_MODE_BEGIN) {
+    if (c->world > 1) {
+      NCCLCHK(c, ncclAllGather(c->d_rec_send, c->d_rec_recv, c->rec_bytes, ncclUint8, c->comm, c->st));
+    } else {
+      HIPCHK(c, hipMemcpyAsync(c->d_rec_recv, c->d_rec_send, c->rec_bytes, hipMemcpyDeviceToDevice, c->st));
+    }
+  }
+  return KSG_OK;
+}
+
+int ensure_out(ksg_ctx* c, size_t n) { return grow(c, (void**)&c->d_out, &c->out_cap, n, sizeof(int32_t)); }
+
+}  // namespace
+
+extern "C" {
+
+int ksg_nccl_unique_id(void* out128) {
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return KSG_ERR_RCCL;
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  memcpy(out128, &id, sizeof id);
+  return KSG_OK;
+}
+
+static int create_impl(const ksg_config* cfg, int device, int rank, int world, const void* nccl_id,
+                       ksg_ctx** out) {
+  if (!cfg || !out || world < 1 || rank < 0 || rank >= world) return KSG_ERR_ARG;
+  if (cfg->n_anti > KSG_MAX_ANTI || cfg->n_label_pref > KSG_MAX_LABEL_PREF ||
+      cfg->n_presence > KSG_MAX_PRESENCE || cfg->n_aff_labels > KSG_MAX_AFF)
+    return KSG_ERR_ARG;
+  for (uint32_t q = 0; q < cfg->n_presence; ++q)
+    if (cfg->presence_n_keys[q] > KSG_MAX_PRESENCE_KEYS) return KSG_ERR_ARG;
+  ksg_ctx* c = new ksg_ctx();
+  c->cfg = *cfg;
+  if (c->cfg.max_conflict_keys == 0) c->cfg.max_conflict_keys = 1024;
+  if (c->cfg.max_domains == 0) c->cfg.max_domains = 4096;
+  c->device = device;
+  c->rank = rank;
+  c->world = world;
+  auto bail = [&](int rc) {
+    if (rc != KSG_OK) {
+      fprintf(stderr, "ksg_create: %s\n", c->err.c_str());
+      delete c;
+    }
+    return rc;
+  };
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return bail(fail(c, KSG_ERR_HIP, "hipSetDevice(%d): %s", device, hipGetErrorString(e)));
+  if ((e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess)
+    return bail(fail(c, KSG_ERR_HIP, "stream/event: %s", hipGetErrorString(e)));
+  if (world > 1) {
+    if (!nccl_id) return bail(fail(c, KSG_ERR_ARG, "nccl_id required for world > 1"));
+    ncclUniqueId id;
+    memcpy(&id, nccl_id, sizeof id);
+    ncclResult_t r = ncclCommInitRank(&c->comm, world, id, rank);
+    if (r != ncclSuccess) return bail(fail(c, KSG_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r)));
+  }
+  int rc;
+  if ((rc = dalloc(c, &c->d_rng, 1, nullptr)) || (rc = dalloc(c, &c->d_summary, 4, nullptr)))
+    return bail(rc);
+  *out = c;
+  return KSG_OK;
+}
+
+int ksg_create(const ksg_config* cfg, int device, ksg_ctx** out) {
+  return create_impl(cfg, device, 0, 1, nullptr, out);
+}
+
+int ksg_create_sharded(const ksg_config* cfg, int device, int rank, int world, const void* nccl_id,
+                       ksg_ctx** out) {
+  return create_impl(cfg, device, rank, world, nccl_id, out);
+}
+
+int ksg_destroy(ksg_ctx* c) {
+  if (!c) return KSG_OK;
+  (void)hipSetDevice(c->device);
+  if (c->st) (void)hipStreamSynchronize(c->st);
+  free_cluster(c);
+  void* scratch[] = {c->d_pods, c->d_ids, c->d_fail, c->d_score, c->d_rec_send, c->d_rec_recv, c->d_dpart,
+                     c->d_dglobal, c->d_out, c->d_rng, c->d_summary, c->d_patch, c->d_shard_wlo};
+  for (void* p : scratch)
+    if (p) (void)hipFree(p);
+  if (c->comm) ncclCommDestroy(c->comm);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->st) (void)hipStreamDestroy(c->st);
+  delete c;
+  return KSG_OK;
+}
+
+const char* ksg_last_error(ksg_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const uint32_t* node_pairs,
+                    uint32_t n_node_pairs, const uint32_t* pair_keys, uint32_t n_pairs, uint32_t n_services) {
+  if (!c) return KSG_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  if (n_nodes && !nodes) return fail(c, KSG_ERR_ARG, "nodes == NULL");
+  if (n_pairs == 0) n_pairs = 1;  // pair 0 always exists (empty)
+  for (uint32_t i = 0; i < n_nodes; ++i) {
+    if ((size_t)nodes[i].label_off + nodes[i].n_labels > n_node_pairs)
+      return fail(c, KSG_ERR_ARG, "node %u label range out of bounds", i);
+    for (uint32_t k = 0; k < nodes[i].n_labels; ++k)
+      if (node_pairs[nodes[i].label_off + k] >= n_pairs || node_pairs[nodes[i].label_off + k] == 0)
+        return fail(c, KSG_ERR_ARG, "node %u has invalid pair id", i);
+  }
+  free_cluster(c);
+  c->N = n_nodes;
+  c->nw = (n_nodes + 63) / 64;
+  c->n_pairs = n_pairs;
+  c->S = n_services;
+  // shard by 64-node words
+  c->shard_wlo_h.resize(c->world);
+  c->nwords_max = 0;
+  uint32_t max_shard_nodes = 0;
+  for (int g = 0; g < c->world; ++g) {
+    const uint32_t a = (uint32_t)((uint64_t)g * c->nw / c->world);
+    const uint32_t b = (uint32_t)((uint64_t)(g + 1) * c->nw / c->world);
+    c->shard_wlo_h[g] = a;
+    c->nwords_max = std::max(c->nwords_max, b - a);
+    max_shard_nodes = std::max(max_shard_nodes, std::min(b * 64, n_nodes) - std::min(a * 64, n_nodes));
+    if (g == c->rank) {
+      c->wlo = a;
+      c->nwords = b - a;
+      c->lo = std::min(a * 64, n_nodes);
+      c->hi = std::min(b * 64, n_nodes);
+    }
+  }
+  if (max_shard_nodes > kMaxNodesPerShard)
+    return fail(c, KSG_ERR_CAPACITY, "shard of %u nodes exceeds %u (use more GPUs)", max_shard_nodes,
+                kMaxNodesPerShard);
+  c->R = pick_R(std::max<uint32_t>(max_shard_nodes, 1));
+
+  // anti-affinity domains: dense index of each pair whose key is the label
+  std::vector<int32_t> dom_of_pair((size_t)std::max<uint32_t>(c->cfg.n_anti, 1) * n_pairs, -1);
+  c->D = 0;
+  KsgDev& d = c->dev;
+  d = KsgDev{};
+  for (uint32_t a = 0; a < c->cfg.n_anti; ++a) {
+    d.anti_dom_off[a] = c->D;
+    uint32_t nd = 0;
+    for (uint32_t p = 1; p < n_pairs; ++p)
+      if (pair_keys[p] == c->cfg.anti_key[a]) dom_of_pair[(size_t)a * n_pairs + p] = (int32_t)nd++;
+    c->D += nd;
+  }
+  if (c->D > c->cfg.max_domains)
+    return fail(c, KSG_ERR_CAPACITY, "%u anti-affinity domains > max_domains %u", c->D, c->cfg.max_domains);
+  c->lds = (size_t)c->D * sizeof(int32_t);
+
+  auto* owner = &c->cluster_allocs;
+  int rc;
+  int64_t *cap_c, *cap_m;
+  uint64_t *sfit, *keymap, *pairmap;
+  int32_t *sscore, *anti_dom, *aff_pair;
+  const size_t NN = std::max<uint32_t>(n_nodes, 1);
+  if ((rc = dalloc(c, &cap_c, NN, owner)) || (rc = dalloc(c, &cap_m, NN, owner)) ||
+      (rc = dalloc(c, &d.used_cpu, NN, owner)) || (rc = dalloc(c, &d.used_mem, NN, owner)) ||
+      (rc = dalloc(c, &sfit, std::max<uint32_t>(c->nw, 1), owner)) ||
+      (rc = dalloc(c, &sscore, NN, owner)) ||
+      (rc = dalloc(c, &keymap, (size_t)c->cfg.max_conflict_keys * std::max<uint32_t>(c->nw, 1), owner)) ||
+      (rc = dalloc(c, &pairmap, (size_t)n_pairs * std::max<uint32_t>(c->nw, 1), owner)) ||
+      (rc = dalloc(c, &d.svc_cnt, (size_t)std::max<uint32_t>(n_services, 1) * NN, owner)) ||
+      (rc = dalloc(c, &d.svc_max, std::max<uint32_t>(n_services, 1), owner)) ||
+      (rc = dalloc(c, &d.svc_total, std::max<uint32_t>(n_services, 1), owner)) ||
+      (rc = dalloc(c, &d.svc_peer, std::max<uint32_t>(n_services, 1), owner)) ||
+      (rc = dalloc(c, &anti_dom, (size_t)std::max<uint32_t>(c->cfg.n_anti, 1) * NN, owner)) ||
+      (rc = dalloc(c, &aff_pair, (size_t)std::max<uint32_t>(c->cfg.n_aff_labels, 1) * NN, owner)))
+    return rc;
+  if (n_services) HIPCHK(c, hipMemsetAsync(d.svc_peer, 0xff, n_services * sizeof(int32_t), c->st));
+
+  // upload nodes + static tables
+  std::vector<int64_t> hc(NN, 0), hm(NN, 0);
+  for (uint32_t i = 0; i < n_nodes; ++i) {
+    hc[i] = nodes[i].cap_milli_cpu;
+    hm[i] = nodes[i].cap_memory;
+  }
+  HIPCHK(c, hipMemcpyAsync(cap_c, hc.data(), NN * 8, hipMemcpyHostToDevice, c->st));
+  HIPCHK(c, hipMemcpyAsync(cap_m, hm.data(), NN * 8, hipMemcpyHostToDevice, c->st));
+  ksg_node* dn = nullptr;
+  uint32_t *dnp = nullptr, *dpk = nullptr;
+  int32_t* ddom = nullptr;
+  std::vector<void*> tmp;
+  if ((rc = dalloc(c, &dn, NN, &tmp)) || (rc = dalloc(c, &dnp, std::max<uint32_t>(n_node_pairs, 1), &tmp)) ||
+      (rc = dalloc(c, &dpk, n_pairs, &tmp)) || (rc = dalloc(c, &ddom, dom_of_pair.size(), &tmp)))
+    return rc;
+  if (n_nodes) HIPCHK(c, hipMemcpyAsync(dn, nodes, n_nodes * sizeof(ksg_node), hipMemcpyHostToDevice, c->st));
+  if (n_node_pairs)
+    HIPCHK(c, hipMemcpyAsync(dnp, node_pairs, n_node_pairs * 4, hipMemcpyHostToDevice, c->st));
+  std::vector<uint32_t> pk(n_pairs, 0xffffffffu);
+  if (pair_keys)
+    for (uint32_t p = 1; p < n_pairs; ++p) pk[p] = pair_keys[p];
+  HIPCHK(c, hipMemcpyAsync(dpk, pk.data(), n_pairs * 4, hipMemcpyHostToDevice, c->st));
+  HIPCHK(c, hipMemcpyAsync(ddom, dom_of_pair.data(), dom_of_pair.size() * 4, hipMemcpyHostToDevice, c->st));
+  KsgStaticCfg sc{};
+  sc.n_presence = c->cfg.n_presence;
+  memcpy(sc.presence_n_keys, c->cfg.presence_n_keys, sizeof sc.presence_n_keys);
+  memcpy(sc.presence_keys, c->cfg.presence_keys, sizeof sc.presence_keys);
+  memcpy(sc.presence_flag, c->cfg.presence_flag, sizeof sc.presence_flag);
+  sc.n_pref = c->cfg.n_label_pref;
+  memcpy(sc.pref_key, c->cfg.pref_key, sizeof sc.pref_key);
+  memcpy(sc.pref_presence, c->cfg.pref_presence, sizeof sc.pref_presence);
+  memcpy(sc.w_pref, c->cfg.w_pref, sizeof sc.w_pref);
+  sc.w_equal = c->cfg.w_equal;
+  sc.n_anti = c->cfg.n_anti;
+  memcpy(sc.anti_key, c->cfg.anti_key, sizeof sc.anti_key);
+  sc.n_aff = c->cfg.n_aff_labels;
+  memcpy(sc.aff_key, c->cfg.aff_key, sizeof sc.aff_key);
+  HIPCHK(c, ksg_launch_static(sc, n_nodes, dn, dnp, dpk, ddom, n_pairs, c->nw, sfit, sscore, anti_dom, aff_pair,
+                              (unsigned long long*)pairmap, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  for (void* p : tmp) (void)hipFree(p);
+
+  d.n_nodes = n_nodes;
+  d.nw = c->nw;
+  d.lo = c->lo;
+  d.hi = c->hi;
+  d.wlo = c->wlo;
+  d.nwords = c->nwords;
+  d.n_pairs = n_pairs;
+  d.n_services = n_services;
+  d.max_keys = c->cfg.max_conflict_keys;
+  d.n_domains_total = c->D;
+  d.preds = c->cfg.predicates;
+  d.n_aff = (c->cfg.predicates & KSG_PRED_SERVICEAFFINITY) ? c->cfg.n_aff_labels : 0;
+  d.equal_fallback = c->cfg.n_priority_configs == 0;
+  // prioritizeNodes skips weight-0 configs; if every config has weight 0 the
+  // HostPriorityList is empty and Schedule returns *FitError.
+  bool any_weight = c->cfg.w_least_requested || c->cfg.w_service_spreading || c->cfg.w_equal;
+  for (uint32_t a = 0; a < c->cfg.n_anti; ++a) any_weight |= c->cfg.w_anti[a] != 0;
+  for (uint32_t q = 0; q < c->cfg.n_label_pref; ++q) any_weight |= c->cfg.w_pref[q] != 0;
+  d.empty_priorities = (!d.equal_fallback && !any_weight) ? 1 : 0;
+  d.w_lr = c->cfg.w_least_requested;
+  d.w_spread = c->cfg.w_service_spreading;
+  d.n_anti = 0;
+  for (uint32_t a = 0; a < c->cfg.n_anti; ++a) {
+    d.w_anti[a] = c->cfg.w_anti[a];
+    if (c->cfg.w_anti[a]) d.n_anti = a + 1;
+  }
+  if (d.n_anti == 0) d.n_domains_total = 0;
+  bool any_pref = false;
+  for (uint32_t q = 0; q < c->cfg.n_label_pref; ++q) any_pref |= c->cfg.w_pref[q] != 0;
+  d.has_static_score = (c->cfg.w_equal != 0 || any_pref) ? 1 : 0;
+  d.has_static_fit = ((c->cfg.predicates & KSG_PRED_LABELSPRESENCE) && c->cfg.n_presence > 0) ? 1 : 0;
+  d.cap_cpu = cap_c;
+  d.cap_mem = cap_m;
+  d.static_fit = sfit;
+  d.static_score = sscore;
+  d.keymap = keymap;
+  d.pairmap = pairmap;
+  d.anti_domain = anti_dom;
+  d.aff_pair = aff_pair;
+  c->lds = (size_t)d.n_domains_total * sizeof(int32_t);
+
+  // scratch sized for the shard
+  c->rec_bytes = (uint32_t)(sizeof(KsgRecordHdr) + (size_t)std::max<uint32_t>(c->nwords_max, 1) * 8);
+  if (c->d_rec_send) (void)hipFree(c->d_rec_send);
+  if (c->d_rec_recv) (void)hipFree(c->d_rec_recv);
+  if (c->d_fail) (void)hipFree(c->d_fail);
+  if (c->d_score) (void)hipFree(c->d_score);
+  if (c->d_dpart) (void)hipFree(c->d_dpart);
+  if (c->d_dglobal) (void)hipFree(c->d_dglobal);
+  if (c->d_shard_wlo) (void)hipFree(c->d_shard_wlo);
+  c->d_rec_send = c->d_rec_recv = c->d_fail = nullptr;
+  c->d_score = nullptr;
+  c->d_dpart = c->d_dglobal = nullptr;
+  c->d_shard_wlo = nullptr;
+  if ((rc = dalloc(c, &c->d_rec_send, c->rec_bytes, nullptr)) ||
+      (rc = dalloc(c, &c->d_rec_recv, (size_t)c->rec_bytes * c->world, nullptr)) ||
+      (rc = dalloc(c, &c->d_fail, NN, nullptr)) || (rc = dalloc(c, &c->d_score, NN, nullptr)) ||
+      (rc = dalloc(c, &c->d_dpart, std::max<uint32_t>(c->D, 1), nullptr)) ||
+      (rc = dalloc(c, &c->d_dglobal, std::max<uint32_t>(c->D, 1), nullptr)) ||
+      (rc = dalloc(c, &c->d_shard_wlo, c->world, nullptr)))
+    return rc;
+  HIPCHK(c, hipMemcpyAsync(c->d_shard_wlo, c->shard_wlo_h.data(), c->world * 4, hipMemcpyHostToDevice, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  reset_mirror(c);
+  c->have_cluster = true;
+  return KSG_OK;
+}
+
+int ksg_add_pod(ksg_ctx* c, uint32_t host_id, const ksg_pod* pod, const uint32_t* ids) {
+  if (!c || !pod) return KSG_ERR_ARG;
+  if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
+  if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
+  int rc = check_pod(c, pod, ids, pod_ids_extent(pod));
+  if (rc) return rc;
+  rc = mirror_add(c, host_id, pod, ids, true);
+  if (rc) return rc;
+  if (c->patches.size() > 4096) return flush_patches(c);
+  return KSG_OK;
+}
+
+int ksg_remove_pod(ksg_ctx* c, uint64_t uid) {
+  if (!c) return KSG_ERR_ARG;
+  if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
+  auto it = c->pods.find(uid);
+  if (it == c->pods.end()) return fail(c, KSG_ERR_ARG, "unknown pod uid %llu", (unsigned long long)uid);
+  PodRec r = std::move(it->second);
+  c->pods.erase(it);
+  const uint32_t h = r.host;
+  if (h < c->N) {
+    c->used_c[h] = (int64_t)((uint64_t)c->used_c[h] - (uint64_t)r.cpu);
+    c->used_m[h] = (int64_t)((uint64_t)c->used_m[h] - (uint64_t)r.mem);
+    patch64(c, c->dev.used_cpu + h, c->used_c[h]);
+    patch64(c, c->dev.used_mem + h, c->used_m[h]);
+    for (uint32_t k : r.keys) {
+      auto kit = c->key_ref.find(((uint64_t)k << 32) | h);
+      if (kit != c->key_ref.end() && --kit->second == 0) {
+        c->key_ref.erase(kit);
+        patch_andnot(c, c->dev.keymap + (size_t)k * c->nw + (h >> 6), 1ULL << (h & 63));
+      }
+    }
+  }
+  for (uint32_t s : r.svcs) {
+    int32_t before;
+    if (h < c->N) {
+      int32_t& v = c->svc_cnt[(size_t)s * c->N + h];
+      before = v--;
+      patch32(c, c->dev.svc_cnt + (size_t)s * c->N + h, v);
+    } else {
+      auto& m = c->svc_ext[s];
+      before = m[h]--;
+      if (m[h] == 0) m.erase(h);
+    }
+    if (before == c->svc_max[s]) {
+      c->svc_max[s] = recompute_max(c, s);
+      patch32(c, c->dev.svc_max + s, c->svc_max[s]);
+    }
+    --c->svc_total[s];
+    patch32(c, c->dev.svc_total + s, c->svc_total[s]);
+    c->svc_members[s].erase(r.seq);
+    const int32_t pc = peer_code(c, s);
+    if (pc != c->svc_peer[s]) {
+      c->svc_peer[s] = pc;
+      patch32(c, c->dev.svc_peer + s, pc);
+    }
+  }
+  if (c->patches.size() > 4096) return flush_patches(c);
+  return KSG_OK;
+}
+
+int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int64_t* max_score,
+                       uint32_t* tie_count, uint8_t* fail_codes) {
+  if (!c || !pod) return KSG_ERR_ARG;
+  if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
+  HIPCHK(c, hipSetDevice(c->device));
+  c->pending = false;
+  if (c->N == 0) return KSG_NONODES;
+  const size_t ext = pod_ids_extent(pod);
+  int rc = check_pod(c, pod, ids, ext);
+  if (rc) return rc;
+  if ((rc = flush_patches(c))) return rc;
+  if ((rc = upload_pods(c, pod, 1, ids, ext))) return rc;
+  if ((rc = scan_exchange(c, c->d_pods, c->d_ids, KSG_MODE_BEGIN, fail_codes ? c->d_fail : nullptr, nullptr)))
+    return rc;
+  HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods, c->d_ids, c->d_rec_recv, c->rec_bytes, c->world,
+                              c->d_shard_wlo, 0, 0, c->d_rng, nullptr, 0, c->d_summary, c->st));
+  int64_t summ[3];
+  HIPCHK(c, hipMemcpyAsync(summ, c->d_summary, sizeof summ, hipMemcpyDeviceToHost, c->st));
+  if (fail_codes && c->hi > c->lo)
+    HIPCHK(c, hipMemcpyAsync(fail_codes, c->d_fail, c->hi - c->lo, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  if (summ[2]) return fail(c, KSG_ERR_NOPEER, "service affinity peer is not on a known node");
+  if (max_score) *max_score = summ[1] > 0 ? summ[0] : 0;
+  if (tie_count) *tie_count = (uint32_t)summ[1];
+  if (summ[1] == 0) return KSG_NOFIT;
+  c->pending = true;
+  c->pending_k = (uint64_t)summ[1];
+  c->pend = *pod;
+  c->pend_ids.assign(ids, ids + ext);
+  return KSG_OK;
+}
+
+int ksg_schedule_commit(ksg_ctx* c, uint32_t tie_index, int32_t* out_node) {
+  if (!c) return KSG_ERR_ARG;
+  if (!c->pending) return fail(c, KSG_ERR_STATE, "no schedule_begin pending");
+  if (tie_index >= c->pending_k) return fail(c, KSG_ERR_ARG, "tie_index %u >= tie_count %llu", tie_index,
+                                             (unsigned long long)c->pending_k);
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = ensure_out(c, 1);
+  if (rc) return rc;
+  HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods, c->d_ids, c->d_rec_recv, c->rec_bytes, c->world,
+                              c->d_shard_wlo, 2, tie_index, c->d_rng, c->d_out, 0, c->d_summary, c->st));
+  int32_t node = -1;
+  HIPCHK(c, hipMemcpyAsync(&node, c->d_out, 4, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  c->pending = false;
+  if (node < 0) return fail(c, KSG_ERR_STATE, "commit selected no node (%d)", node);
+  rc = mirror_add(c, (uint32_t)node, &c->pend, c->pend_ids.data(), false);
+  if (rc) return rc;
+  if (out_node) *out_node = node;
+  return KSG_OK;
+}
+
+int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32_t* ids, uint32_t n_ids,
+                       uint64_t* rng_state, int32_t* out_nodes) {
+  if (!c || (n && (!pods || !out_nodes)) || !rng_state) return KSG_ERR_ARG;
+  if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
+  if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
+  HIPCHK(c, hipSetDevice(c->device));
+  c->last_ms = 0.0;
+  if (n == 0) return KSG_OK;
+  if (c->N == 0) {
+    for (uint32_t i = 0; i < n; ++i) out_nodes[i] = KSG_OUT_NONODES;
+    return KSG_OK;
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    int rc = check_pod(c, pods + i, ids, n_ids);
+    if (rc) return rc;
+    if (c->pods.count(pods[i].uid)) return fail(c, KSG_ERR_ARG, "pod %u: duplicate uid", i);
+  }
+  int rc;
+  if ((rc = flush_patches(c))) return rc;
+  if ((rc = upload_pods(c, pods, n, ids, n_ids))) return rc;
+  if ((rc = ensure_out(c, n))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->d_rng, rng_state, 8, hipMemcpyHostToDevice, c->st));
+  HIPCHK(c, hipEventRecord(c->ev0, c->st));
+  if (c->world == 1) {
+    HIPCHK(c, ksg_launch_batch(c->R, anti_on(c), c->dev, c->d_pods, c->d_ids, n, c->d_rng, c->d_out, c->lds,
+                               c->st));
+  } else {
+    for (uint32_t i = 0; i < n; ++i) {
+      if ((rc = scan_exchange(c, c->d_pods + i, c->d_ids, KSG_MODE_BEGIN, nullptr, nullptr))) return rc;
+      HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods + i, c->d_ids, c->d_rec_recv, c->rec_bytes, c->world,
+                                  c->d_shard_wlo, 1, 0, c->d_rng, c->d_out, i, c->d_summary, c->st));
+    }
+  }
+  HIPCHK(c, hipEventRecord(c->ev1, c->st));
+  HIPCHK(c, hipMemcpyAsync(out_nodes, c->d_out, (size_t)n * 4, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipMemcpyAsync(rng_state, c->d_rng, 8, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  float ms = 0.f;
+  HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  c->last_ms = ms;
+  // the device applied every commit; replay them into the host mirror
+  for (uint32_t i = 0; i < n; ++i) {
+    if (out_nodes[i] >= 0) {
+      if ((rc = mirror_add(c, (uint32_t)out_nodes[i], pods + i, ids, false))) return rc;
+    }
+  }
+  return KSG_OK;
+}
+
+int ksg_evaluate(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, uint8_t* fail_out, int64_t* score_out) {
+  if (!c || !pod) return KSG_ERR_ARG;
+  if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
+  if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (c->N == 0) return KSG_NONODES;
+  const size_t ext = pod_ids_extent(pod);
+  int rc = check_pod(c, pod, ids, ext);
+  if (rc) return rc;
+  if ((rc = flush_patches(c))) return rc;
+  if ((rc = upload_pods(c, pod, 1, ids, ext))) return rc;
+  // errors surface through the BEGIN record, so run BEGIN first for the flag
+  if ((rc = scan_exchange(c, c->d_pods, c->d_ids, KSG_MODE_BEGIN, nullptr, nullptr))) return rc;
+  HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods, c->d_ids, c->d_rec_recv, c->rec_bytes, c->world,
+                              c->d_shard_wlo, 0, 0, c->d_rng, nullptr, 0, c->d_summary, c->st));
+  if ((rc = scan_exchange(c, c->d_pods, c->d_ids, KSG_MODE_EVAL, c->d_fail, c->d_score))) return rc;
+  int64_t summ[3];
+  HIPCHK(c, hipMemcpyAsync(summ, c->d_summary, sizeof summ, hipMemcpyDeviceToHost, c->st));
+  const size_t ns = c->hi - c->lo;
+  if (fail_out && ns) HIPCHK(c, hipMemcpyAsync(fail_out, c->d_fail, ns, hipMemcpyDeviceToHost, c->st));
+  if (score_out && ns) HIPCHK(c, hipMemcpyAsync(score_out, c->d_score, ns * 8, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  if (summ[2]) return fail(c, KSG_ERR_NOPEER, "service affinity peer is not on a known node");
+  return KSG_OK;
+}
+
+int ksg_last_batch_ms(ksg_ctx* c, double* ms) {
+  if (!c || !ms) return KSG_ERR_ARG;
+  *ms = c->last_ms;
+  return KSG_OK;
+}
+
+int ksg_shard(ksg_ctx* c, uint32_t* lo, uint32_t* hi) {
+  if (!c) return KSG_ERR_ARG;
+  if (lo) *lo = c->lo;
+  if (hi) *hi = c->hi;
+  return KSG_OK;
+}
+
+int ksg_read_requested(ksg_ctx* c, int64_t* milli_cpu, int64_t* memory) {
+  if (!c || !c->have_cluster) return KSG_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = flush_patches(c);
+  if (rc) return rc;
+  if (c->N) {
+    if (milli_cpu) HIPCHK(c, hipMemcpyAsync(milli_cpu, c->dev.used_cpu, c->N * 8, hipMemcpyDeviceToHost, c->st));
+    if (memory) HIPCHK(c, hipMemcpyAsync(memory, c->dev.used_mem, c->N * 8, hipMemcpyDeviceToHost, c->st));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  return KSG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,188 @@
+"""Thin object wrapper over one libkschedgpu.so context.
+
+`DeviceScheduler` owns a `ksg_ctx` (device memory, HIP stream, optional RCCL
+communicator) and speaks in the interned numpy arrays of kubernetes_amd.ingest.
+Every method maps 1:1 onto a C-ABI entry point of include/kschedgpu.h; any
+non-OK return that is not a scheduling outcome raises KsgError. There is no
+host-side evaluation here — the HIP kernels are the only implementation.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import abi
+
+
+class KsgError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"ksg error {code}: {msg}")
+        self.code = code
+
+
+@dataclass
+class ClusterArrays:
+    """Interned node set: rank-ordered nodes, their label pair ids, pair->key."""
+
+    nodes: np.ndarray  # NODE_DTYPE[N]
+    node_pairs: np.ndarray  # uint32
+    pair_keys: np.ndarray  # uint32[n_pairs] (entry 0 unused)
+    n_services: int
+    names: list = field(default_factory=list)  # node names in rank order (optional)
+
+    @property
+    def n_nodes(self) -> int:
+        return int(self.nodes.shape[0])
+
+
+@dataclass
+class PodBatch:
+    """Interned pods (POD_DTYPE) with their shared id list."""
+
+    pods: np.ndarray
+    ids: np.ndarray  # uint32
+
+    def __len__(self):
+        return int(self.pods.shape[0])
+
+    def one(self, i: int) -> "PodBatch":
+        return PodBatch(self.pods[i : i + 1].copy(), self.ids)
+
+
+def _u32(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.uint32)
+
+
+class DeviceScheduler:
+    """One scheduling context on one GPU (or one shard of a node-sharded set)."""
+
+    def __init__(self, cfg: abi.KsgConfig, device: int = 0, rank: int = 0, world: int = 1,
+                 nccl_id: bytes | None = None):
+        self._lib = abi.load_library()
+        self._ctx = C.c_void_p()
+        if world == 1:
+            rc = self._lib.ksg_create(C.byref(cfg), device, C.byref(self._ctx))
+        else:
+            idbuf = C.create_string_buffer(nccl_id, 128)
+            rc = self._lib.ksg_create_sharded(C.byref(cfg), device, rank, world, idbuf, C.byref(self._ctx))
+        if rc != abi.KSG_OK:
+            raise KsgError(rc, "ksg_create failed (see stderr)")
+        self.cfg = cfg
+        self.n_nodes = 0
+        self.world = world
+        self.rank = rank
+
+    @staticmethod
+    def nccl_unique_id() -> bytes:
+        lib = abi.load_library()
+        buf = C.create_string_buffer(128)
+        rc = lib.ksg_nccl_unique_id(buf)
+        if rc != abi.KSG_OK:
+            raise KsgError(rc, "ncclGetUniqueId failed")
+        return buf.raw
+
+    def close(self):
+        if self._ctx:
+            self._lib.ksg_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _err(self, rc: int):
+        msg = self._lib.ksg_last_error(self._ctx)
+        raise KsgError(rc, msg.decode() if msg else "")
+
+    # ---- cluster / pod state ---------------------------------------------
+    def set_cluster(self, cl: ClusterArrays):
+        nodes = np.ascontiguousarray(cl.nodes, dtype=abi.NODE_DTYPE)
+        np_ = _u32(cl.node_pairs if len(cl.node_pairs) else np.zeros(1, np.uint32))
+        pk = _u32(cl.pair_keys if len(cl.pair_keys) else np.zeros(1, np.uint32))
+        rc = self._lib.ksg_set_cluster(self._ctx, abi.ptr(nodes), len(nodes), abi.ptr(np_), len(cl.node_pairs),
+                                       abi.ptr(pk), len(pk), int(cl.n_services))
+        if rc != abi.KSG_OK:
+            self._err(rc)
+        self.n_nodes = len(nodes)
+
+    def add_pod(self, host_id: int, batch: PodBatch, i: int = 0):
+        pod = np.ascontiguousarray(batch.pods[i : i + 1])
+        ids = _u32(batch.ids if len(batch.ids) else np.zeros(1, np.uint32))
+        rc = self._lib.ksg_add_pod(self._ctx, int(host_id), abi.ptr(pod), abi.ptr(ids))
+        if rc != abi.KSG_OK:
+            self._err(rc)
+
+    def remove_pod(self, uid: int):
+        rc = self._lib.ksg_remove_pod(self._ctx, int(uid))
+        if rc != abi.KSG_OK:
+            self._err(rc)
+
+    # ---- scheduling ---------------------------------------------------------
+    def begin(self, batch: PodBatch, i: int = 0, want_fail: bool = False):
+        """-> (rc, max_score, tie_count, fail_codes|None); rc in {OK, NOFIT, NONODES}."""
+        pod = np.ascontiguousarray(batch.pods[i : i + 1])
+        ids = _u32(batch.ids if len(batch.ids) else np.zeros(1, np.uint32))
+        m = C.c_int64(0)
+        k = C.c_uint32(0)
+        lo, hi = self.shard()
+        fails = np.zeros(max(hi - lo, 1), np.uint8) if want_fail else None
+        rc = self._lib.ksg_schedule_begin(self._ctx, abi.ptr(pod), abi.ptr(ids), C.byref(m), C.byref(k),
+                                          abi.ptr(fails))
+        if rc not in (abi.KSG_OK, abi.KSG_NOFIT, abi.KSG_NONODES):
+            self._err(rc)
+        return rc, m.value, k.value, (fails[: hi - lo] if fails is not None else None)
+
+    def commit(self, tie_index: int) -> int:
+        out = C.c_int32(-1)
+        rc = self._lib.ksg_schedule_commit(self._ctx, int(tie_index), C.byref(out))
+        if rc != abi.KSG_OK:
+            self._err(rc)
+        return out.value
+
+    def batch(self, batch: PodBatch, rng_state: int):
+        """Schedule every pod of the batch in order on the device. -> (out, rng_state)."""
+        n = len(batch)
+        pods = np.ascontiguousarray(batch.pods, dtype=abi.POD_DTYPE)
+        ids = _u32(batch.ids if len(batch.ids) else np.zeros(1, np.uint32))
+        out = np.empty(max(n, 1), np.int32)
+        st = C.c_uint64(rng_state)
+        rc = self._lib.ksg_schedule_batch(self._ctx, abi.ptr(pods), n, abi.ptr(ids), len(batch.ids), C.byref(st),
+                                          abi.ptr(out))
+        if rc != abi.KSG_OK:
+            self._err(rc)
+        return out[:n], st.value
+
+    def evaluate(self, batch: PodBatch, i: int = 0):
+        """Per-node (fail code, combined score) of the shard, no commit."""
+        pod = np.ascontiguousarray(batch.pods[i : i + 1])
+        ids = _u32(batch.ids if len(batch.ids) else np.zeros(1, np.uint32))
+        lo, hi = self.shard()
+        fails = np.zeros(max(hi - lo, 1), np.uint8)
+        scores = np.zeros(max(hi - lo, 1), np.int64)
+        rc = self._lib.ksg_evaluate(self._ctx, abi.ptr(pod), abi.ptr(ids), abi.ptr(fails), abi.ptr(scores))
+        if rc not in (abi.KSG_OK, abi.KSG_NONODES):
+            self._err(rc)
+        return rc, fails[: hi - lo], scores[: hi - lo]
+
+    def last_batch_ms(self) -> float:
+        ms = C.c_double(0)
+        self._lib.ksg_last_batch_ms(self._ctx, C.byref(ms))
+        return ms.value
+
+    def shard(self):
+        lo = C.c_uint32(0)
+        hi = C.c_uint32(0)
+        self._lib.ksg_shard(self._ctx, C.byref(lo), C.byref(hi))
+        return lo.value, hi.value
+
+    def read_requested(self):
+        c = np.zeros(max(self.n_nodes, 1), np.int64)
+        m = np.zeros(max(self.n_nodes, 1), np.int64)
+        rc = self._lib.ksg_read_requested(self._ctx, abi.ptr(c), abi.ptr(m))
+        if rc != abi.KSG_OK:
+            self._err(rc)
+        return c[: self.n_nodes], m[: self.n_nodes]

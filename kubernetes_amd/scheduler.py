@@ -1,0 +1,231 @@
+"""The drop-in `algorithm.Scheduler` backed by the HIP Filter/Score pass.
+
+Reference interface (pkg/scheduler):
+  type Scheduler interface { Schedule(api.Pod, MinionLister) (string, error) }   scheduler.go:25-27
+  NewGenericScheduler(predicates, prioritizers, pods PodLister, random)           generic_scheduler.go:197-204
+  FitError{Pod, FailedPredicates}                                                  generic_scheduler.go:30-44
+  MinionLister / PodLister / ServiceLister and their fakes                         listers.go:27-93
+
+`GPUScheduler.schedule(pod, minion_lister)` keeps the reference's contract:
+  * no nodes -> NoMinionsError("no minions available to schedule pods");
+  * nothing fits (or the priority list is empty) -> FitError with a
+    FailedPredicateMap (one failing predicate name per node);
+  * otherwise exactly one `random.int()` draw and the ix-th host, ix = r % ties,
+    in (score desc, name desc) order.
+The pods the scheduler sees are exactly what `pod_lister.list()` returns at each
+call (as MapPodsToMachines re-lists them, predicates.go:354-375): the device
+state is reconciled against the lister by namespace/name before each pod.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+from . import abi
+from .api import Node, Pod, Service
+from .engine import DeviceScheduler, PodBatch
+from .factory import SchedulerConfig
+from .ingest import ClusterView, Interner, PodBatchBuilder
+from .labels import everything, selector_from_set
+
+
+class FitError(Exception):
+    """*FitError (generic_scheduler.go:30-44)."""
+
+    def __init__(self, pod: Pod, failed_predicates: Dict[str, set]):
+        self.pod = pod
+        self.failed_predicates = failed_predicates
+        out = f"failed to find fit for pod: {pod.metadata.namespace}/{pod.metadata.name}"
+        for node in sorted(failed_predicates):
+            out += f"Node {node}: {','.join(sorted(failed_predicates[node]))}"
+        super().__init__(out)
+
+
+class NoMinionsError(Exception):
+    def __init__(self):
+        super().__init__("no minions available to schedule pods")
+
+
+class SchedulingError(Exception):
+    """Non-fit errors from a predicate (e.g. ServiceAffinity's peer lookup)."""
+
+
+# ---- listers (listers.go:27-93) ----------------------------------------------
+class FakeMinionLister:
+    def __init__(self, nodes: Sequence[Node]):
+        self.nodes = list(nodes)
+
+    def list(self) -> List[Node]:
+        return list(self.nodes)
+
+
+class FakePodLister:
+    def __init__(self, pods: Sequence[Pod]):
+        self.pods = list(pods)
+
+    def list(self, selector=None) -> List[Pod]:
+        sel = selector or everything()
+        return [p for p in self.pods if sel.matches(p.metadata.labels)]
+
+
+class FakeServiceLister:
+    def __init__(self, services: Sequence[Service]):
+        self.services = list(services)
+
+    def list(self) -> List[Service]:
+        return list(self.services)
+
+    def get_pod_services(self, pod: Pod) -> List[Service]:
+        out = [s for s in self.services
+               if s.metadata.namespace == pod.metadata.namespace
+               and selector_from_set(s.spec.selector).matches(pod.metadata.labels)]
+        if not out:
+            raise LookupError(f"Could not find service for pod {pod.metadata.name} in namespace "
+                              f"{pod.metadata.namespace} with labels: {pod.metadata.labels}")
+        return out
+
+
+class SplitMix64Rand:
+    """Injected deterministic source: Int() = splitmix64 >> 1.
+    Go's `*rand.Rand` stream cannot be reproduced without the Go stdlib; the
+    caller's own source can be passed instead (anything with .int())."""
+
+    MASK = (1 << 64) - 1
+
+    def __init__(self, seed: int = 0):
+        self.state = seed & self.MASK
+
+    def next(self) -> int:
+        self.state = (self.state + 0x9E3779B97F4A7C15) & self.MASK
+        z = self.state
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & self.MASK
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & self.MASK
+        return z ^ (z >> 31)
+
+    def int(self) -> int:
+        return self.next() >> 1
+
+
+class GPUScheduler:
+    """algorithm.Scheduler on the MI355X (NewGenericScheduler's drop-in)."""
+
+    def __init__(self, config: SchedulerConfig, pod_lister, service_lister=None, random=None,
+                 device: int = 0):
+        self.config = config
+        self.pod_lister = pod_lister
+        self.service_lister = service_lister or FakeServiceLister([])
+        self.random = random if random is not None else SplitMix64Rand(0)
+        self.interner = Interner()
+        for k in config.label_keys():
+            self.interner.key_id(k)
+        self.aff_labels = config.affinity_labels()
+        self.engine = DeviceScheduler(config.compile(self.interner.key_id), device=device)
+        self.fail_names = config.fail_code_names()
+        self.view: Optional[ClusterView] = None
+        self._node_sig = None
+        self._svc_sig = None
+        self._mirror: Dict[str, tuple] = {}  # pod key -> (uid, host_id, id(pod))
+        self._next_uid = 1
+
+    def close(self):
+        self.engine.close()
+
+    # ---- state reconciliation ----------------------------------------------
+    def _uid(self) -> int:
+        u = self._next_uid
+        self._next_uid += 1
+        return u
+
+    def _sync(self, nodes: Sequence[Node]):
+        services = self.service_lister.list()
+        nsig = tuple(id(n) for n in nodes)
+        ssig = tuple(id(s) for s in services)
+        if nsig != self._node_sig or ssig != self._svc_sig or self.view is None:
+            self.view = ClusterView(nodes, services, self.interner)
+            self.engine.set_cluster(self.view.arrays)
+            self._node_sig, self._svc_sig = nsig, ssig
+            self._mirror = {}
+        pods = self.pod_lister.list(everything())
+        want = {}
+        for p in pods:
+            want[p.key()] = p
+        for k, (uid, host, pid) in list(self._mirror.items()):
+            # a pod this scheduler assumed, now reported by the lister on the same host
+            if pid is None and k in want and self.view.host_id(want[k].status.host) == host:
+                self._mirror[k] = (uid, host, id(want[k]))
+        for key in [k for k, (uid, host, pid) in self._mirror.items()
+                    if k not in want or id(want[k]) != pid or self.view.host_id(want[k].status.host) != host]:
+            self.engine.remove_pod(self._mirror.pop(key)[0])
+        add = [p for k, p in want.items() if k not in self._mirror]
+        if add:
+            b = PodBatchBuilder(self.view, self.aff_labels)
+            uids = []
+            for p in add:
+                uid = self._uid()
+                uids.append(uid)
+                b.add(p, uid)
+            batch = b.build()
+            for i, p in enumerate(add):
+                h = self.view.host_id(p.status.host)
+                self.engine.add_pod(h, batch, i)
+                self._mirror[p.key()] = (uids[i], h, id(p))
+
+    # ---- Schedule -------------------------------------------------------------
+    def schedule(self, pod: Pod, minion_lister) -> str:
+        nodes = minion_lister.list()
+        if len(nodes) == 0:
+            raise NoMinionsError()
+        self._sync(nodes)
+        uid = self._uid()
+        b = PodBatchBuilder(self.view, self.aff_labels)
+        b.add(pod, uid)
+        batch = b.build()
+        try:
+            rc, _, k, fails = self.engine.begin(batch, 0, want_fail=True)
+        except Exception as e:  # ServiceAffinity peer on an unknown node, etc.
+            if getattr(e, "code", None) == abi.KSG_ERR_NOPEER:
+                raise SchedulingError(str(e)) from e
+            raise
+        if rc == abi.KSG_NONODES:
+            raise NoMinionsError()
+        if rc == abi.KSG_NOFIT:
+            failed = {}
+            for n, code in enumerate(fails):
+                if code:
+                    failed[self.view.names[n]] = {self.fail_names[int(code)]}
+            raise FitError(pod, failed)
+        r = self.random.int()
+        node = self.engine.commit(r % k)
+        # the device now assumes the pod on `node` (AssumePod); the next _sync keeps it
+        # iff the pod lister reports it there too.
+        host = self.view.names[node]
+        self._mirror[pod.key()] = (uid, node, None)
+        return host
+
+    # ---- batch path (persistent kernel) -------------------------------------
+    def schedule_batch(self, pods: Sequence[Pod], minion_lister, rng_state: int):
+        """Schedule pods in order without host round-trips; each success is assumed
+        (committed) before the next pod. -> (hosts or None per pod, rng_state)."""
+        nodes = minion_lister.list()
+        if len(nodes) == 0:
+            return [None] * len(pods), rng_state
+        self._sync(nodes)
+        b = PodBatchBuilder(self.view, self.aff_labels)
+        uids = []
+        for p in pods:
+            uids.append(self._uid())
+            b.add(p, uids[-1])
+        out, rng_state = self.engine.batch(b.build(), rng_state)
+        hosts = []
+        for i, p in enumerate(pods):
+            if out[i] >= 0:
+                hosts.append(self.view.names[out[i]])
+                self._mirror[p.key()] = (uids[i], int(out[i]), None)
+            else:
+                hosts.append(None)
+        return hosts, rng_state
+
+
+def new_gpu_scheduler(config: SchedulerConfig, pod_lister, service_lister=None, random=None,
+                      device: int = 0) -> GPUScheduler:
+    """Counterpart of NewGenericScheduler at factory.go:149."""
+    return GPUScheduler(config, pod_lister, service_lister, random, device)

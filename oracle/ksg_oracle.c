@@ -1,0 +1,791 @@
+/*
+ * ksg_oracle.c — CPU restatement of the kube-scheduler generic scheduler
+ * (smarterclayton/kubernetes v0.13.0-dev) over the interned inputs of
+ * include/kschedgpu.h.
+ *
+ * TEST INFRASTRUCTURE ONLY. This file is the checker for the HIP path and the
+ * `cpu_baseline` leg of bench.py. Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline may load liboracle.so. The product library
+ * (kubernetes_amd/libkschedgpu.so) never links or calls it.
+ *
+ * Parity pinning: the restatement is checked against the golden vectors
+ * transcribed from the reference's own Go tests (tests/golden/, via the
+ * object-level model oracle/ref_model.py and the Python ingest), see
+ * tests/test_oracle_golden.py and tests/test_oracle_crosscheck.py. The Go
+ * stdlib math/rand stream is not reproducible here (no Go toolchain); the
+ * tie-break source is the injected splitmix64 stream.
+ *
+ * Two modes that must agree bit-for-bit (tests/test_oracle_crosscheck.py):
+ *   faithful    — the reference's cost structure: every Schedule regroups all
+ *                 placed pods by host (MapPodsToMachines, predicates.go:354-375),
+ *                 runs each predicate per node rescanning that node's pods,
+ *                 re-derives every priority from the pod list, builds a
+ *                 HostPriorityList and sorts it (generic_scheduler.go:84-96).
+ *   incremental — per-node totals/bitsets updated on commit, closed forms.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/kschedgpu.h"
+
+typedef struct {
+  uint64_t uid;
+  uint32_t host;
+  int64_t cpu, mem;
+  uint32_t *keys_port, n_port;
+  uint32_t *keys_pd, n_pd;
+  uint32_t *svcs, n_svcs;
+  uint64_t seq;
+  int alive;
+} opod;
+
+typedef struct orc {
+  ksg_config cfg;
+  int faithful;
+  /* cluster */
+  uint32_t N, n_pairs, S;
+  int64_t *cap_c, *cap_m;
+  uint32_t **node_pairs; /* per node list */
+  uint32_t *node_np;
+  uint32_t *pair_keys;
+  /* placed pods, in insertion order (the lister order we canonicalize to) */
+  opod *pods;
+  uint32_t n_pods, cap_pods;
+  uint64_t seq;
+  /* incremental state */
+  int64_t *used_c, *used_m;
+  uint32_t *key_ref; /* max_conflict_keys x N refcounts */
+  int32_t *svc_cnt;  /* S x N */
+  int32_t *svc_max, *svc_total;
+  /* pending begin */
+  int pending;
+  ksg_pod pend;
+  uint32_t *pend_ids;
+  size_t pend_n_ids;
+  uint64_t pend_k;
+  int64_t pend_M;
+  int64_t *scores; /* N */
+  uint8_t *fails;  /* N */
+} orc;
+
+#define NONE_SCORE (-0x7fffffffffffffffLL - 1)
+
+/* ------------------------------------------------------------------ utils */
+static uint64_t splitmix_next(uint64_t *s) {
+  uint64_t z = (*s += 0x9E3779B97F4A7C15ULL);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+static int64_t go_div(int64_t a, int64_t b) {
+  if (b == -1) return (int64_t)(0ULL - (uint64_t)a);
+  return a / b;
+}
+
+/* calculateScore, priorities.go:27-37 (Go int64: wrapping multiply) */
+static int64_t calculate_score(int64_t requested, int64_t capacity) {
+  if (capacity == 0) return 0;
+  if (requested > capacity) return 0;
+  int64_t diff = (int64_t)((uint64_t)capacity - (uint64_t)requested);
+  int64_t prod = (int64_t)((uint64_t)diff * 10ULL);
+  return go_div(prod, capacity);
+}
+
+/* int(10 * (float32(num) / float32(den))), spreading.go:79-83,156-160 */
+static int64_t frac10_f32(int64_t num, int64_t den) {
+  volatile float a = (float)num;
+  volatile float b = (float)den;
+  volatile float q = a / b;
+  volatile float s = 10.0f * q;
+  return (int64_t)s;
+}
+
+static int node_has_key(const orc *o, uint32_t n, uint32_t key) {
+  for (uint32_t i = 0; i < o->node_np[n]; ++i)
+    if (o->pair_keys[o->node_pairs[n][i]] == key) return 1;
+  return 0;
+}
+
+static int node_has_pair(const orc *o, uint32_t n, uint32_t pair) {
+  if (pair == 0) return 0;
+  for (uint32_t i = 0; i < o->node_np[n]; ++i)
+    if (o->node_pairs[n][i] == pair) return 1;
+  return 0;
+}
+
+/* pair id of the node's value for label key, or -1 */
+static int32_t node_pair_for_key(const orc *o, uint32_t n, uint32_t key) {
+  int32_t pr = -1;
+  for (uint32_t i = 0; i < o->node_np[n]; ++i)
+    if (o->pair_keys[o->node_pairs[n][i]] == key) pr = (int32_t)o->node_pairs[n][i];
+  return pr;
+}
+
+static int pod_in_service(const opod *p, uint32_t s) {
+  for (uint32_t i = 0; i < p->n_svcs; ++i)
+    if (p->svcs[i] == s) return 1;
+  return 0;
+}
+
+/* --------------------------------------------------------------- lifecycle */
+orc *orc_create(const ksg_config *cfg, int faithful) {
+  orc *o = (orc *)calloc(1, sizeof(orc));
+  o->cfg = *cfg;
+  if (o->cfg.max_conflict_keys == 0) o->cfg.max_conflict_keys = 1024;
+  o->faithful = faithful;
+  return o;
+}
+
+static void free_pods(orc *o) {
+  for (uint32_t i = 0; i < o->n_pods; ++i) {
+    free(o->pods[i].keys_port);
+    free(o->pods[i].keys_pd);
+    free(o->pods[i].svcs);
+  }
+  free(o->pods);
+  o->pods = NULL;
+  o->n_pods = o->cap_pods = 0;
+}
+
+static void free_cluster(orc *o) {
+  for (uint32_t n = 0; n < o->N; ++n) free(o->node_pairs[n]);
+  free(o->node_pairs);
+  free(o->node_np);
+  free(o->cap_c);
+  free(o->cap_m);
+  free(o->pair_keys);
+  free(o->used_c);
+  free(o->used_m);
+  free(o->key_ref);
+  free(o->svc_cnt);
+  free(o->svc_max);
+  free(o->svc_total);
+  free(o->scores);
+  free(o->fails);
+  free_pods(o);
+  o->node_pairs = NULL;
+  o->node_np = NULL;
+  o->cap_c = o->cap_m = NULL;
+  o->pair_keys = NULL;
+  o->used_c = o->used_m = NULL;
+  o->key_ref = NULL;
+  o->svc_cnt = o->svc_max = o->svc_total = NULL;
+  o->scores = NULL;
+  o->fails = NULL;
+}
+
+void orc_destroy(orc *o) {
+  if (!o) return;
+  free_cluster(o);
+  free(o->pend_ids);
+  free(o);
+}
+
+int orc_set_cluster(orc *o, const ksg_node *nodes, uint32_t n_nodes, const uint32_t *node_pairs,
+                    uint32_t n_node_pairs, const uint32_t *pair_keys, uint32_t n_pairs,
+                    uint32_t n_services) {
+  (void)n_node_pairs;
+  free_cluster(o);
+  if (n_pairs == 0) n_pairs = 1;
+  o->N = n_nodes;
+  o->n_pairs = n_pairs;
+  o->S = n_services;
+  size_t NN = n_nodes ? n_nodes : 1;
+  o->cap_c = (int64_t *)calloc(NN, 8);
+  o->cap_m = (int64_t *)calloc(NN, 8);
+  o->node_pairs = (uint32_t **)calloc(NN, sizeof(uint32_t *));
+  o->node_np = (uint32_t *)calloc(NN, 4);
+  o->pair_keys = (uint32_t *)calloc(n_pairs, 4);
+  o->pair_keys[0] = 0xffffffffu;
+  for (uint32_t p = 1; p < n_pairs; ++p) o->pair_keys[p] = pair_keys[p];
+  for (uint32_t n = 0; n < n_nodes; ++n) {
+    o->cap_c[n] = nodes[n].cap_milli_cpu;
+    o->cap_m[n] = nodes[n].cap_memory;
+    o->node_np[n] = nodes[n].n_labels;
+    o->node_pairs[n] = (uint32_t *)calloc(nodes[n].n_labels ? nodes[n].n_labels : 1, 4);
+    memcpy(o->node_pairs[n], node_pairs + nodes[n].label_off, (size_t)nodes[n].n_labels * 4);
+  }
+  o->used_c = (int64_t *)calloc(NN, 8);
+  o->used_m = (int64_t *)calloc(NN, 8);
+  o->key_ref = (uint32_t *)calloc((size_t)o->cfg.max_conflict_keys * NN, 4);
+  o->svc_cnt = (int32_t *)calloc((size_t)(n_services ? n_services : 1) * NN, 4);
+  o->svc_max = (int32_t *)calloc(n_services ? n_services : 1, 4);
+  o->svc_total = (int32_t *)calloc(n_services ? n_services : 1, 4);
+  o->scores = (int64_t *)calloc(NN, 8);
+  o->fails = (uint8_t *)calloc(NN, 1);
+  o->seq = 0;
+  o->pending = 0;
+  return KSG_OK;
+}
+
+/* ------------------------------------------------------------- pod store */
+static uint32_t *dup_ids(const uint32_t *ids, uint32_t off, uint32_t n) {
+  uint32_t *r = (uint32_t *)malloc((n ? n : 1) * 4);
+  if (n) memcpy(r, ids + off, (size_t)n * 4);
+  return r;
+}
+
+static int32_t ext_count(const orc *o, uint32_t s, uint32_t host) {
+  int32_t c = 0;
+  for (uint32_t i = 0; i < o->n_pods; ++i)
+    if (o->pods[i].alive && o->pods[i].host == host && pod_in_service(&o->pods[i], s)) ++c;
+  return c;
+}
+
+static void recompute_svc_max(orc *o, uint32_t s) {
+  /* maxCount over all hosts incl. hosts not in the node list (spreading.go:73-80) */
+  int32_t m = 0;
+  for (uint32_t n = 0; n < o->N; ++n)
+    if (o->svc_cnt[(size_t)s * o->N + n] > m) m = o->svc_cnt[(size_t)s * o->N + n];
+  for (uint32_t i = 0; i < o->n_pods; ++i) {
+    const opod *p = &o->pods[i];
+    if (p->alive && p->host >= o->N && pod_in_service(p, s)) {
+      int32_t c = ext_count(o, s, p->host);
+      if (c > m) m = c;
+    }
+  }
+  o->svc_max[s] = m;
+}
+
+int orc_add_pod(orc *o, uint32_t host_id, const ksg_pod *p, const uint32_t *ids) {
+  if (o->n_pods == o->cap_pods) {
+    o->cap_pods = o->cap_pods ? o->cap_pods * 2 : 256;
+    o->pods = (opod *)realloc(o->pods, (size_t)o->cap_pods * sizeof(opod));
+  }
+  opod *q = &o->pods[o->n_pods++];
+  q->uid = p->uid;
+  q->host = host_id;
+  q->cpu = p->milli_cpu;
+  q->mem = p->memory;
+  q->keys_port = dup_ids(ids, p->ports_off, p->n_ports);
+  q->n_port = p->n_ports;
+  q->keys_pd = dup_ids(ids, p->pds_off, p->n_pds);
+  q->n_pd = p->n_pds;
+  q->svcs = dup_ids(ids, p->svcs_off, p->n_svcs);
+  q->n_svcs = p->n_svcs;
+  q->seq = ++o->seq;
+  q->alive = 1;
+  if (host_id < o->N) {
+    o->used_c[host_id] = (int64_t)((uint64_t)o->used_c[host_id] + (uint64_t)q->cpu);
+    o->used_m[host_id] = (int64_t)((uint64_t)o->used_m[host_id] + (uint64_t)q->mem);
+    for (uint32_t i = 0; i < q->n_port; ++i) o->key_ref[(size_t)q->keys_port[i] * o->N + host_id]++;
+    for (uint32_t i = 0; i < q->n_pd; ++i) o->key_ref[(size_t)q->keys_pd[i] * o->N + host_id]++;
+  }
+  for (uint32_t i = 0; i < q->n_svcs; ++i) {
+    uint32_t s = q->svcs[i];
+    int32_t v;
+    if (host_id < o->N)
+      v = ++o->svc_cnt[(size_t)s * o->N + host_id];
+    else
+      v = ext_count(o, s, host_id);
+    if (v > o->svc_max[s]) o->svc_max[s] = v;
+    o->svc_total[s]++;
+  }
+  return KSG_OK;
+}
+
+int orc_remove_pod(orc *o, uint64_t uid) {
+  for (uint32_t i = 0; i < o->n_pods; ++i) {
+    opod *q = &o->pods[i];
+    if (!q->alive || q->uid != uid) continue;
+    q->alive = 0;
+    uint32_t h = q->host;
+    if (h < o->N) {
+      o->used_c[h] = (int64_t)((uint64_t)o->used_c[h] - (uint64_t)q->cpu);
+      o->used_m[h] = (int64_t)((uint64_t)o->used_m[h] - (uint64_t)q->mem);
+      for (uint32_t k = 0; k < q->n_port; ++k) o->key_ref[(size_t)q->keys_port[k] * o->N + h]--;
+      for (uint32_t k = 0; k < q->n_pd; ++k) o->key_ref[(size_t)q->keys_pd[k] * o->N + h]--;
+    }
+    for (uint32_t k = 0; k < q->n_svcs; ++k) {
+      uint32_t s = q->svcs[k];
+      if (h < o->N) o->svc_cnt[(size_t)s * o->N + h]--;
+      o->svc_total[s]--;
+      recompute_svc_max(o, s);
+    }
+    return KSG_OK;
+  }
+  return KSG_ERR_ARG;
+}
+
+/* first service peer = earliest-added live pod matching service s
+ * (canonical order for nsServicePods[0], predicates.go:293) */
+static const opod *first_peer(const orc *o, uint32_t s) {
+  const opod *best = NULL;
+  for (uint32_t i = 0; i < o->n_pods; ++i) {
+    const opod *p = &o->pods[i];
+    if (p->alive && pod_in_service(p, s) && (!best || p->seq < best->seq)) best = p;
+  }
+  return best;
+}
+
+/* ------------------------------------------------------- pod-level context */
+typedef struct {
+  const ksg_pod *p;
+  const uint32_t *ids;
+  int32_t req_aff[KSG_MAX_AFF];
+  int error;
+} pctx;
+
+static void resolve_affinity(const orc *o, pctx *c) {
+  c->error = 0;
+  for (int j = 0; j < KSG_MAX_AFF; ++j) c->req_aff[j] = -1;
+  if (!(o->cfg.predicates & KSG_PRED_SERVICEAFFINITY)) return;
+  int all_given = 1;
+  for (uint32_t j = 0; j < o->cfg.n_aff_labels; ++j) {
+    c->req_aff[j] = c->p->aff_pair[j];
+    if (c->p->aff_pair[j] < 0) all_given = 0;
+  }
+  if (all_given || c->p->service < 0) return;
+  const opod *peer = first_peer(o, (uint32_t)c->p->service);
+  if (!peer) return;
+  if (peer->host >= o->N) {
+    c->error = 1; /* GetNodeInfo(peer's Status.Host) fails, predicates.go:293-296 */
+    return;
+  }
+  for (uint32_t j = 0; j < o->cfg.n_aff_labels; ++j)
+    if (c->req_aff[j] < 0) c->req_aff[j] = node_pair_for_key(o, peer->host, o->cfg.aff_key[j]);
+}
+
+/* ================================================================ FAITHFUL */
+/* MapPodsToMachines: group every placed pod by Status.Host (predicates.go:354-375) */
+typedef struct {
+  uint32_t **lists; /* per node: indices into o->pods */
+  uint32_t *len;
+} machine_map;
+
+static void map_pods_to_machines(const orc *o, machine_map *m) {
+  m->len = (uint32_t *)calloc(o->N ? o->N : 1, 4);
+  for (uint32_t i = 0; i < o->n_pods; ++i)
+    if (o->pods[i].alive && o->pods[i].host < o->N) m->len[o->pods[i].host]++;
+  m->lists = (uint32_t **)calloc(o->N ? o->N : 1, sizeof(uint32_t *));
+  for (uint32_t n = 0; n < o->N; ++n) m->lists[n] = (uint32_t *)malloc((m->len[n] ? m->len[n] : 1) * 4);
+  uint32_t *fillc = (uint32_t *)calloc(o->N ? o->N : 1, 4);
+  for (uint32_t i = 0; i < o->n_pods; ++i)
+    if (o->pods[i].alive && o->pods[i].host < o->N) {
+      uint32_t h = o->pods[i].host;
+      m->lists[h][fillc[h]++] = i;
+    }
+  free(fillc);
+}
+
+static void free_machine_map(const orc *o, machine_map *m) {
+  for (uint32_t n = 0; n < o->N; ++n) free(m->lists[n]);
+  free(m->lists);
+  free(m->len);
+}
+
+/* PodFitsPorts / getUsedPorts (predicates.go:326-350) */
+static int f_fits_ports(const orc *o, const pctx *c, const machine_map *m, uint32_t n) {
+  for (uint32_t w = 0; w < c->p->n_ports; ++w) {
+    uint32_t want = c->ids[c->p->ports_off + w];
+    for (uint32_t e = 0; e < m->len[n]; ++e) {
+      const opod *q = &o->pods[m->lists[n][e]];
+      for (uint32_t k = 0; k < q->n_port; ++k)
+        if (q->keys_port[k] == want) return 0;
+    }
+  }
+  return 1;
+}
+
+/* NoDiskConflict / isVolumeConflict (predicates.go:52-83) */
+static int f_no_disk_conflict(const orc *o, const pctx *c, const machine_map *m, uint32_t n) {
+  for (uint32_t v = 0; v < c->p->n_pds; ++v) {
+    uint32_t pd = c->ids[c->p->pds_off + v];
+    for (uint32_t e = 0; e < m->len[n]; ++e) {
+      const opod *q = &o->pods[m->lists[n][e]];
+      for (uint32_t k = 0; k < q->n_pd; ++k)
+        if (q->keys_pd[k] == pd) return 0;
+    }
+  }
+  return 1;
+}
+
+/* PodFitsResources / CheckPodsExceedingCapacity (predicates.go:104-145): greedy */
+static int f_fits_resources(const orc *o, const pctx *c, const machine_map *m, uint32_t n) {
+  if (c->p->milli_cpu == 0 && c->p->memory == 0) return 1;
+  int64_t totalC = o->cap_c[n], totalM = o->cap_m[n];
+  int64_t reqC = 0, reqM = 0;
+  for (uint32_t e = 0; e <= m->len[n]; ++e) {
+    int64_t pc, pm;
+    if (e < m->len[n]) {
+      const opod *q = &o->pods[m->lists[n][e]];
+      pc = q->cpu;
+      pm = q->mem;
+    } else {
+      pc = c->p->milli_cpu;
+      pm = c->p->memory;
+    }
+    int fitsC = totalC == 0 || (int64_t)((uint64_t)totalC - (uint64_t)reqC) >= pc;
+    int fitsM = totalM == 0 || (int64_t)((uint64_t)totalM - (uint64_t)reqM) >= pm;
+    if (!fitsC || !fitsM) return 0; /* exceeding non-empty */
+    reqC = (int64_t)((uint64_t)reqC + (uint64_t)pc);
+    reqM = (int64_t)((uint64_t)reqM + (uint64_t)pm);
+  }
+  return 1;
+}
+
+/* PodSelectorMatches (predicates.go:161-179) */
+static int f_selector(const orc *o, const pctx *c, uint32_t n) {
+  for (uint32_t i = 0; i < c->p->n_sel; ++i)
+    if (!node_has_pair(o, n, c->ids[c->p->sel_off + i])) return 0;
+  return 1;
+}
+
+/* CheckNodeLabelPresence (predicates.go:215-229), AND over LabelsPresence predicates */
+static int f_labels_presence(const orc *o, uint32_t n) {
+  for (uint32_t q = 0; q < o->cfg.n_presence; ++q)
+    for (uint32_t i = 0; i < o->cfg.presence_n_keys[q]; ++i) {
+      int exists = node_has_key(o, n, o->cfg.presence_keys[q][i]);
+      if ((exists && !o->cfg.presence_flag[q]) || (!exists && o->cfg.presence_flag[q])) return 0;
+    }
+  return 1;
+}
+
+static int f_service_affinity(const orc *o, const pctx *c, uint32_t n) {
+  for (uint32_t j = 0; j < o->cfg.n_aff_labels; ++j)
+    if (c->req_aff[j] >= 0 && !node_has_pair(o, n, (uint32_t)c->req_aff[j])) return 0;
+  return 1;
+}
+
+static int faithful_fail_code(const orc *o, const pctx *c, const machine_map *m, uint32_t n) {
+  uint32_t P = o->cfg.predicates;
+  if ((P & KSG_PRED_HOSTNAME) && c->p->host != -1 && (int32_t)n != c->p->host) return KSG_FAIL_HOSTNAME;
+  if ((P & KSG_PRED_LABELSPRESENCE) && o->cfg.n_presence && !f_labels_presence(o, n))
+    return KSG_FAIL_LABELSPRESENCE;
+  if ((P & KSG_PRED_MATCHNODESELECTOR) && !f_selector(o, c, n)) return KSG_FAIL_MATCHNODESELECTOR;
+  if ((P & KSG_PRED_NODISKCONFLICT) && !f_no_disk_conflict(o, c, m, n)) return KSG_FAIL_NODISKCONFLICT;
+  if ((P & KSG_PRED_PODFITSPORTS) && !f_fits_ports(o, c, m, n)) return KSG_FAIL_PODFITSPORTS;
+  if ((P & KSG_PRED_PODFITSRESOURCES) && !f_fits_resources(o, c, m, n)) return KSG_FAIL_PODFITSRESOURCES;
+  if ((P & KSG_PRED_SERVICEAFFINITY) && !f_service_affinity(o, c, n)) return KSG_FAIL_SERVICEAFFINITY;
+  return KSG_FAIL_NONE;
+}
+
+/* prioritizeNodes over the filtered nodes (generic_scheduler.go:136-165).
+ * score[n] valid where fails[n]==0. Returns 0 if the HostPriorityList is empty. */
+static int faithful_prioritize(orc *o, const pctx *c, const uint8_t *fails, int64_t *score) {
+  const ksg_config *cf = &o->cfg;
+  uint32_t nfilt = 0;
+  for (uint32_t n = 0; n < o->N; ++n) nfilt += fails[n] == 0;
+  if (cf->n_priority_configs == 0) { /* EqualPriority */
+    for (uint32_t n = 0; n < o->N; ++n) score[n] = 1;
+    return nfilt > 0;
+  }
+  int any = 0;
+  for (uint32_t n = 0; n < o->N; ++n) score[n] = 0;
+  if (cf->w_least_requested) { /* LeastRequestedPriority, priorities.go:43-91 */
+    any = 1;
+    machine_map m;
+    map_pods_to_machines(o, &m);
+    for (uint32_t n = 0; n < o->N; ++n) {
+      if (fails[n]) continue;
+      int64_t tc = 0, tm = 0;
+      for (uint32_t e = 0; e < m.len[n]; ++e) {
+        const opod *q = &o->pods[m.lists[n][e]];
+        tc = (int64_t)((uint64_t)tc + (uint64_t)q->cpu);
+        tm = (int64_t)((uint64_t)tm + (uint64_t)q->mem);
+      }
+      tc = (int64_t)((uint64_t)tc + (uint64_t)c->p->milli_cpu);
+      tm = (int64_t)((uint64_t)tm + (uint64_t)c->p->memory);
+      int64_t cs = calculate_score(tc, o->cap_c[n]);
+      int64_t ms = calculate_score(tm, o->cap_m[n]);
+      score[n] += (int64_t)cf->w_least_requested * ((cs + ms) / 2);
+    }
+    free_machine_map(o, &m);
+  }
+  if (cf->w_service_spreading) { /* CalculateSpreadPriority, spreading.go:37-86 */
+    any = 1;
+    int32_t *counts = (int32_t *)calloc(o->N ? o->N : 1, 4);
+    int32_t maxCount = 0;
+    if (c->p->service >= 0) {
+      uint32_t s = (uint32_t)c->p->service;
+      /* counts by Status.Host over all hosts (incl. unknown ones) */
+      for (uint32_t i = 0; i < o->n_pods; ++i) {
+        const opod *q = &o->pods[i];
+        if (!q->alive || !pod_in_service(q, s)) continue;
+        int32_t cnt;
+        if (q->host < o->N)
+          cnt = ++counts[q->host];
+        else {
+          cnt = 0;
+          for (uint32_t k = 0; k <= i; ++k)
+            if (o->pods[k].alive && o->pods[k].host == q->host && pod_in_service(&o->pods[k], s)) ++cnt;
+        }
+        if (cnt > maxCount) maxCount = cnt;
+      }
+    }
+    for (uint32_t n = 0; n < o->N; ++n) {
+      if (fails[n]) continue;
+      int64_t sc = maxCount > 0 ? frac10_f32((int64_t)maxCount - counts[n], maxCount) : 10;
+      score[n] += (int64_t)cf->w_service_spreading * sc;
+    }
+    free(counts);
+  }
+  for (uint32_t a = 0; a < cf->n_anti; ++a) { /* CalculateAntiAffinityPriority, spreading.go:104-168 */
+    if (!cf->w_anti[a]) continue;
+    any = 1;
+    int32_t *podCounts = (int32_t *)calloc(o->n_pairs, 4); /* by pair id of the label value */
+    int64_t nsp = 0;
+    if (c->p->service >= 0) {
+      uint32_t s = (uint32_t)c->p->service;
+      for (uint32_t i = 0; i < o->n_pods; ++i) {
+        const opod *q = &o->pods[i];
+        if (!q->alive || !pod_in_service(q, s)) continue;
+        nsp++;
+        if (q->host < o->N && !fails[q->host]) { /* labeledMinions built from filtered nodes */
+          int32_t pr = node_pair_for_key(o, q->host, cf->anti_key[a]);
+          if (pr >= 0) podCounts[pr]++;
+        }
+      }
+    }
+    for (uint32_t n = 0; n < o->N; ++n) {
+      if (fails[n]) continue;
+      int32_t pr = node_pair_for_key(o, n, cf->anti_key[a]);
+      int64_t sc = 0;
+      if (pr >= 0) sc = nsp > 0 ? frac10_f32(nsp - podCounts[pr], nsp) : 10;
+      score[n] += (int64_t)cf->w_anti[a] * sc;
+    }
+    free(podCounts);
+  }
+  for (uint32_t q = 0; q < cf->n_label_pref; ++q) { /* CalculateNodeLabelPriority, priorities.go:109-134 */
+    if (!cf->w_pref[q]) continue;
+    any = 1;
+    for (uint32_t n = 0; n < o->N; ++n) {
+      if (fails[n]) continue;
+      int exists = node_has_key(o, n, cf->pref_key[q]);
+      int ok = (exists && cf->pref_presence[q]) || (!exists && !cf->pref_presence[q]);
+      score[n] += (int64_t)cf->w_pref[q] * (ok ? 10 : 0);
+    }
+  }
+  if (cf->w_equal) {
+    any = 1;
+    for (uint32_t n = 0; n < o->N; ++n)
+      if (!fails[n]) score[n] += (int64_t)cf->w_equal;
+  }
+  return any && nfilt > 0;
+}
+
+/* ============================================================= INCREMENTAL */
+static int incr_fail_code(const orc *o, const pctx *c, uint32_t n) {
+  uint32_t P = o->cfg.predicates;
+  if ((P & KSG_PRED_HOSTNAME) && c->p->host != -1 && (int32_t)n != c->p->host) return KSG_FAIL_HOSTNAME;
+  if ((P & KSG_PRED_LABELSPRESENCE) && o->cfg.n_presence && !f_labels_presence(o, n))
+    return KSG_FAIL_LABELSPRESENCE;
+  if ((P & KSG_PRED_MATCHNODESELECTOR) && !f_selector(o, c, n)) return KSG_FAIL_MATCHNODESELECTOR;
+  if (P & KSG_PRED_NODISKCONFLICT)
+    for (uint32_t i = 0; i < c->p->n_pds; ++i)
+      if (o->key_ref[(size_t)c->ids[c->p->pds_off + i] * o->N + n]) return KSG_FAIL_NODISKCONFLICT;
+  if (P & KSG_PRED_PODFITSPORTS)
+    for (uint32_t i = 0; i < c->p->n_ports; ++i)
+      if (o->key_ref[(size_t)c->ids[c->p->ports_off + i] * o->N + n]) return KSG_FAIL_PODFITSPORTS;
+  if ((P & KSG_PRED_PODFITSRESOURCES) && !(c->p->milli_cpu == 0 && c->p->memory == 0)) {
+    int fc = o->cap_c[n] == 0 || (int64_t)((uint64_t)o->cap_c[n] - (uint64_t)o->used_c[n]) >= c->p->milli_cpu;
+    int fm = o->cap_m[n] == 0 || (int64_t)((uint64_t)o->cap_m[n] - (uint64_t)o->used_m[n]) >= c->p->memory;
+    if (!(fc && fm)) return KSG_FAIL_PODFITSRESOURCES;
+  }
+  if ((P & KSG_PRED_SERVICEAFFINITY) && !f_service_affinity(o, c, n)) return KSG_FAIL_SERVICEAFFINITY;
+  return KSG_FAIL_NONE;
+}
+
+static int incr_prioritize(orc *o, const pctx *c, const uint8_t *fails, int64_t *score) {
+  const ksg_config *cf = &o->cfg;
+  uint32_t nfilt = 0;
+  for (uint32_t n = 0; n < o->N; ++n) nfilt += fails[n] == 0;
+  if (cf->n_priority_configs == 0) {
+    for (uint32_t n = 0; n < o->N; ++n) score[n] = 1;
+    return nfilt > 0;
+  }
+  int any = cf->w_least_requested || cf->w_service_spreading || cf->w_equal;
+  for (uint32_t q = 0; q < cf->n_label_pref; ++q) any |= cf->w_pref[q] != 0;
+  for (uint32_t a = 0; a < cf->n_anti; ++a) any |= cf->w_anti[a] != 0;
+  int32_t s = c->p->service;
+  int32_t maxc = s >= 0 ? o->svc_max[s] : 0;
+  int64_t tot = s >= 0 ? o->svc_total[s] : 0;
+  /* anti-affinity domain counts over filtered labelled nodes */
+  int32_t *dcount[KSG_MAX_ANTI] = {0};
+  for (uint32_t a = 0; a < cf->n_anti; ++a) {
+    if (!cf->w_anti[a]) continue;
+    dcount[a] = (int32_t *)calloc(o->n_pairs, 4);
+    if (s >= 0)
+      for (uint32_t n = 0; n < o->N; ++n) {
+        if (fails[n]) continue;
+        int32_t pr = node_pair_for_key(o, n, cf->anti_key[a]);
+        if (pr >= 0) dcount[a][pr] += o->svc_cnt[(size_t)s * o->N + n];
+      }
+  }
+  for (uint32_t n = 0; n < o->N; ++n) {
+    if (fails[n]) continue;
+    int64_t sc = 0;
+    if (cf->w_least_requested) {
+      int64_t tc = (int64_t)((uint64_t)o->used_c[n] + (uint64_t)c->p->milli_cpu);
+      int64_t tm = (int64_t)((uint64_t)o->used_m[n] + (uint64_t)c->p->memory);
+      sc += (int64_t)cf->w_least_requested * ((calculate_score(tc, o->cap_c[n]) + calculate_score(tm, o->cap_m[n])) / 2);
+    }
+    if (cf->w_service_spreading) {
+      int32_t cnt = s >= 0 ? o->svc_cnt[(size_t)s * o->N + n] : 0;
+      sc += (int64_t)cf->w_service_spreading * (maxc > 0 ? frac10_f32((int64_t)maxc - cnt, maxc) : 10);
+    }
+    for (uint32_t a = 0; a < cf->n_anti; ++a) {
+      if (!cf->w_anti[a]) continue;
+      int32_t pr = node_pair_for_key(o, n, cf->anti_key[a]);
+      int64_t v = 0;
+      if (pr >= 0) v = tot > 0 ? frac10_f32(tot - dcount[a][pr], tot) : 10;
+      sc += (int64_t)cf->w_anti[a] * v;
+    }
+    for (uint32_t q = 0; q < cf->n_label_pref; ++q) {
+      if (!cf->w_pref[q]) continue;
+      int exists = node_has_key(o, n, cf->pref_key[q]);
+      int ok = (exists && cf->pref_presence[q]) || (!exists && !cf->pref_presence[q]);
+      sc += (int64_t)cf->w_pref[q] * (ok ? 10 : 0);
+    }
+    sc += (int64_t)cf->w_equal;
+    score[n] = sc;
+  }
+  for (uint32_t a = 0; a < cf->n_anti; ++a) free(dcount[a]);
+  return any && nfilt > 0;
+}
+
+/* ============================================================== Schedule */
+/* evaluate: fills o->fails / o->scores; returns 1 if the priority list is
+ * non-empty, 0 if empty, <0 on error */
+static int evaluate(orc *o, const ksg_pod *p, const uint32_t *ids) {
+  pctx c;
+  c.p = p;
+  c.ids = ids;
+  resolve_affinity(o, &c);
+  if (c.error) return KSG_ERR_NOPEER;
+  if (o->faithful) {
+    machine_map m;
+    map_pods_to_machines(o, &m);
+    for (uint32_t n = 0; n < o->N; ++n) o->fails[n] = (uint8_t)faithful_fail_code(o, &c, &m, n);
+    free_machine_map(o, &m);
+    return faithful_prioritize(o, &c, o->fails, o->scores);
+  }
+  for (uint32_t n = 0; n < o->N; ++n) o->fails[n] = (uint8_t)incr_fail_code(o, &c, n);
+  return incr_prioritize(o, &c, o->fails, o->scores);
+}
+
+typedef struct {
+  int64_t score;
+  uint32_t rank;
+} hp;
+
+/* HostPriorityList.Less (types.go:42-47) under sort.Reverse: score desc, host desc */
+static int hp_cmp_desc(const void *a, const void *b) {
+  const hp *x = (const hp *)a, *y = (const hp *)b;
+  if (x->score != y->score) return x->score > y->score ? -1 : 1;
+  return x->rank > y->rank ? -1 : (x->rank < y->rank ? 1 : 0);
+}
+
+/* selectHost / getBestHosts: returns ties count; *best_rank_for(ix) resolves later */
+static uint64_t count_ties(orc *o, int64_t *M) {
+  int64_t best = NONE_SCORE;
+  for (uint32_t n = 0; n < o->N; ++n)
+    if (!o->fails[n] && o->scores[n] > best) best = o->scores[n];
+  uint64_t k = 0;
+  for (uint32_t n = 0; n < o->N; ++n)
+    if (!o->fails[n] && o->scores[n] == best) k++;
+  *M = best;
+  return k;
+}
+
+static int32_t pick(orc *o, uint64_t ix) {
+  if (o->faithful) { /* sort.Sort(sort.Reverse(priorityList)) then hosts[ix] */
+    uint32_t cnt = 0;
+    hp *list = (hp *)malloc((o->N ? o->N : 1) * sizeof(hp));
+    for (uint32_t n = 0; n < o->N; ++n)
+      if (!o->fails[n]) list[cnt++] = (hp){o->scores[n], n};
+    qsort(list, cnt, sizeof(hp), hp_cmp_desc);
+    int32_t r = (int32_t)list[ix].rank;
+    free(list);
+    return r;
+  }
+  int64_t M;
+  count_ties(o, &M);
+  uint64_t seen = 0;
+  for (int64_t n = (int64_t)o->N - 1; n >= 0; --n)
+    if (!o->fails[n] && o->scores[n] == M) {
+      if (seen == ix) return (int32_t)n;
+      seen++;
+    }
+  return -1;
+}
+
+static void commit(orc *o, const ksg_pod *p, const uint32_t *ids, uint32_t node) { orc_add_pod(o, node, p, ids); }
+
+int orc_evaluate(orc *o, const ksg_pod *p, const uint32_t *ids, uint8_t *fail_out, int64_t *score_out) {
+  if (o->N == 0) return KSG_NONODES;
+  int r = evaluate(o, p, ids);
+  if (r < 0) return r;
+  if (fail_out) memcpy(fail_out, o->fails, o->N);
+  if (score_out)
+    for (uint32_t n = 0; n < o->N; ++n) score_out[n] = o->fails[n] ? 0 : o->scores[n];
+  return KSG_OK;
+}
+
+int orc_schedule_begin(orc *o, const ksg_pod *p, const uint32_t *ids, size_t n_ids, int64_t *max_score,
+                       uint32_t *tie_count, uint8_t *fail_codes) {
+  o->pending = 0;
+  if (o->N == 0) return KSG_NONODES;
+  int r = evaluate(o, p, ids);
+  if (r < 0) return r;
+  if (fail_codes) memcpy(fail_codes, o->fails, o->N);
+  int64_t M = 0;
+  uint64_t k = r ? count_ties(o, &M) : 0;
+  if (max_score) *max_score = k ? M : 0;
+  if (tie_count) *tie_count = (uint32_t)k;
+  if (!k) return KSG_NOFIT;
+  o->pending = 1;
+  o->pend = *p;
+  free(o->pend_ids);
+  o->pend_ids = (uint32_t *)malloc((n_ids ? n_ids : 1) * 4);
+  if (n_ids) memcpy(o->pend_ids, ids, n_ids * 4);
+  o->pend_n_ids = n_ids;
+  o->pend_k = k;
+  o->pend_M = M;
+  return KSG_OK;
+}
+
+int orc_schedule_commit(orc *o, uint32_t tie_index, int32_t *out_node) {
+  if (!o->pending || tie_index >= o->pend_k) return KSG_ERR_STATE;
+  int32_t node = pick(o, tie_index);
+  o->pending = 0;
+  if (node < 0) return KSG_ERR_STATE;
+  commit(o, &o->pend, o->pend_ids, (uint32_t)node);
+  if (out_node) *out_node = node;
+  return KSG_OK;
+}
+
+/* the same loop the device runs: begin, draw Int63 iff something fits, commit */
+int orc_schedule_batch(orc *o, const ksg_pod *pods, uint32_t n, const uint32_t *ids, uint32_t n_ids,
+                       uint64_t *rng_state, int32_t *out_nodes) {
+  (void)n_ids;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (o->N == 0) {
+      out_nodes[i] = KSG_OUT_NONODES;
+      continue;
+    }
+    int r = evaluate(o, pods + i, ids);
+    if (r < 0) {
+      out_nodes[i] = KSG_OUT_ERROR;
+      continue;
+    }
+    int64_t M = 0;
+    uint64_t k = r ? count_ties(o, &M) : 0;
+    if (!k) {
+      out_nodes[i] = KSG_OUT_NOFIT;
+      continue;
+    }
+    uint64_t rr = splitmix_next(rng_state) >> 1;
+    int32_t node = pick(o, rr % k);
+    commit(o, pods + i, ids, (uint32_t)node);
+    out_nodes[i] = node;
+  }
+  return KSG_OK;
+}
+
+void orc_read_requested(orc *o, int64_t *c, int64_t *m) {
+  if (c) memcpy(c, o->used_c, (size_t)o->N * 8);
+  if (m) memcpy(m, o->used_m, (size_t)o->N * 8);
+}

@@ -1,0 +1,120 @@
+"""GPU parity: the HIP path (through the C ABI) vs the C oracle, bit-exact.
+
+Compared: pod -> node assignments (incl. FitError / error outcomes), the tie-break
+RNG stream position, per-node fail codes and integer scores, and the committed
+per-node requested totals. Sizes exercise every kernel variant (nodes per thread
+R = 1..32) and every BASELINE config's predicate/priority set.
+"""
+import numpy as np
+import pytest
+
+from kubernetes_amd import abi
+from kubernetes_amd.engine import DeviceScheduler, PodBatch
+from oracle.pyoracle import OracleScheduler
+from tests.helpers import Case, run_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(case):
+    return DeviceScheduler(case.cfg, device=0), OracleScheduler(case.cfg)
+
+
+@pytest.mark.parametrize("name,nn,npods", [
+    ("config1", 500, 1000),      # BASELINE config 1 at full size
+    ("config2", 700, 1500),
+    ("config2", 2000, 3000),
+    ("config4", 900, 1500),
+    ("config2", 5000, 2000),     # config 2 node count
+    ("config2", 9000, 800),      # R = 16 (memory-resident node state)
+    ("config4", 20000, 300),     # R = 32, anti-affinity
+])
+def test_batch_matches_oracle(name, nn, npods):
+    case = Case(name, nn, npods)
+    dev, orc = _pair(case)
+    got, sg = run_batch(dev, case)
+    want, sw = run_batch(orc, case)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"first mismatches at {bad[:8]}: gpu {got[bad[:8]]} oracle {want[bad[:8]]}"
+    assert sg == sw
+    gc, gm = dev.read_requested()
+    wc, wm = orc.read_requested()
+    assert np.array_equal(gc, wc) and np.array_equal(gm, wm)
+    dev.close()
+
+
+def test_batch_chunks_equal_one_batch():
+    """Batch boundaries must not change outcomes (state persists across launches)."""
+    case = Case("config2", 1500, 1200)
+    dev, orc = _pair(case)
+    got, sg = run_batch(dev, case, chunk=97)
+    want, sw = run_batch(orc, case)
+    assert np.array_equal(got, want) and sg == sw
+    dev.close()
+
+
+def test_begin_commit_and_evaluate_match_oracle():
+    case = Case("config4", 800, 300)
+    dev, orc = _pair(case)
+    dev.set_cluster(case.view.arrays)
+    orc.set_cluster(case.view.arrays)
+    rng = np.random.default_rng(7)
+    for i in range(len(case.batch)):
+        if i % 25 == 0:
+            rcg, fg, sg = dev.evaluate(case.batch, i)
+            rco, fo, so = orc.evaluate(case.batch, i)
+            assert rcg == rco
+            assert np.array_equal(fg, fo)
+            fit = fg == 0
+            assert np.array_equal(sg[fit], so[fit])
+        rg, mg, kg, failg = dev.begin(case.batch, i, want_fail=True)
+        ro, mo, ko, failo = orc.begin(case.batch, i, want_fail=True)
+        assert (rg, kg) == (ro, ko), i
+        assert np.array_equal(failg, failo)
+        if rg == abi.KSG_OK:
+            assert mg == mo
+            ix = int(rng.integers(0, kg))
+            assert dev.commit(ix) == orc.commit(ix)
+    dev.close()
+
+
+def test_existing_pods_add_remove():
+    """ksg_add_pod / ksg_remove_pod incl. pods on hosts outside the node list."""
+    case = Case("config2", 600, 900)
+    dev, orc = _pair(case)
+    dev.set_cluster(case.view.arrays)
+    orc.set_cluster(case.view.arrays)
+    n = case.view.arrays.n_nodes
+    rng = np.random.default_rng(3)
+    pre = 400
+    for i in range(pre):
+        host = int(rng.integers(0, n + 5))  # some hosts are not nodes
+        for s in (dev, orc):
+            s.add_pod(host, case.batch, i)
+    for i in range(0, pre, 3):
+        uid = int(case.batch.pods[i]["uid"])
+        for s in (dev, orc):
+            s.remove_pod(uid)
+    rest = PodBatch(case.batch.pods[pre:], case.batch.ids)
+    got, sg = dev.batch(rest, 99)
+    want, sw = orc.batch(rest, 99)
+    assert np.array_equal(got, want) and sg == sw
+    dev.close()
+
+
+def test_no_nodes_and_empty_priorities():
+    case = Case("config2", 64, 10)
+    # all-zero weights: prioritizeNodes returns an empty list -> FitError for every pod
+    from kubernetes_amd import factory
+    cfgz = factory.create_from_keys(["PodFitsResources"], ["EqualPriority"]).compile(case.it.key_id)
+    dev = DeviceScheduler(cfgz)
+    dev.set_cluster(case.view.arrays)
+    out, st = dev.batch(case.batch, 5)
+    assert (out == abi.KSG_OUT_NOFIT).all() and st == 5
+    # no nodes
+    empty = type(case.view.arrays)(case.view.arrays.nodes[:0], case.view.arrays.node_pairs[:0],
+                                   case.view.arrays.pair_keys, case.view.arrays.n_services)
+    dev.set_cluster(empty)
+    out, _ = dev.batch(case.batch, 5)
+    assert (out == abi.KSG_OUT_NONODES).all()
+    dev.close()
