@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""bench.py — pods scheduled/sec of the MI355X Filter/Score pass (BASELINE.json metric).
+
+A "step" is one batch of `--batch` pods scheduled in order through the hot path
+(filter every node, score, argmax + reference tie-break, commit) by the
+persistent HIP kernel; pods are resident in HBM state before the timed region
+(the C ABI copies the batch descriptors in, ~B*88 bytes, inside the step).
+
+  N=1 : BASELINE config 2 — 5,000 nodes / 10,000 pods, DefaultProvider
+        (PodFitsPorts, PodFitsResources, NoDiskConflict, MatchNodeSelector,
+        HostName + LeastRequested(1), ServiceSpreading(1), Equal(0)).
+  N>1 : BASELINE config 3 — 15,000 nodes node-sharded across N GPUs, per-pod
+        winner exchange with RCCL all-gather over xGMI (strong scaling: the
+        total node count is fixed).
+
+Roofline: bound "hbm"; achieved = algorithmic bytes per launch / kernel time,
+with SURVEY.md 8(d)'s 60 B/node/pod for this predicate+priority set
+(resources 32 + ports 8 + PD 8 + labels 8 + spread count 4) x nodes x pods per
+launch; kernel time from HIP events on the library's stream. cpu_baseline: the
+C restatement in faithful mode (the reference's per-pod MapPodsToMachines
+regroup + per-node rescans + sort; single thread like the reference's one
+scheduling goroutine) timed on this host over a bounded prefix of the same
+workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip-level parameters
+BYTES_PER_NODE = {"config1": 32, "config2": 60, "config3": 60, "config4": 64, "config5": 84}
+
+
+def _dist_env():
+    return int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")), int(
+        os.environ.get("LOCAL_RANK", "0"))
+
+
+def _torch_sync():
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+    except Exception:
+        pass
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1000, help="pods per step")
+    ap.add_argument("--workload", default=None, help="config1..config5 (default: config2 at N=1, config3 at N>1)")
+    ap.add_argument("--nodes", type=int, default=None)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the cpu_baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--window", type=int, default=None,
+                    help="pods per speculative window (0 = exact one-pod-at-a-time kernel)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-derived HBM bytes per launch (profiles/), keyed by workload")
+    args = ap.parse_args()
+
+    world, rank, local_rank = _dist_env()
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"WORLD_SIZE={world} but --gpus={args.gpus}")
+    wl = args.workload or ("config2" if world == 1 else "config3")
+    n_pods = (args.warmup + args.steps) * args.batch
+
+    from kubernetes_amd import ingest, workload
+    from kubernetes_amd.engine import DeviceScheduler, PodBatch
+
+    t0 = time.time()
+    w = workload.build(wl, n_nodes=args.nodes, n_pods=n_pods)
+    it = ingest.Interner()
+    for k in w.config.label_keys():
+        it.key_id(k)
+    view = ingest.ClusterView(w.nodes, w.services, it)
+    batch = ingest.ingest_pods(view, w.pods, aff_labels=w.config.affinity_labels())
+    cfg = w.config.compile(it.key_id)
+    n_nodes = view.arrays.n_nodes
+    if rank == 0:
+        print(f"[bench] {wl}: {n_nodes} nodes, {n_pods} pods, ingest {time.time() - t0:.1f}s", file=sys.stderr,
+              flush=True)
+
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_mod
+
+        dist = dist_mod
+        dist.init_process_group("gloo")
+        idb = DeviceScheduler.nccl_unique_id() if rank == 0 else bytes(128)
+        obj = [idb]
+        dist.broadcast_object_list(obj, src=0)
+        sched = DeviceScheduler(cfg, device=local_rank, rank=rank, world=world, nccl_id=obj[0])
+    else:
+        sched = DeviceScheduler(cfg, device=0)
+    if args.window is not None:
+        sched.set_window(args.window)
+    sched.set_cluster(view.arrays)
+
+    def step_batch(s):
+        sl = slice(s * args.batch, (s + 1) * args.batch)
+        return PodBatch(batch.pods[sl], batch.ids)
+
+    rng = workload.TIEBREAK_SEED
+    outs = []
+    for s in range(args.warmup):
+        o, rng = sched.batch(step_batch(s), rng)
+        outs.append(o)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        _torch_sync()
+
+    barrier()
+    t_start = time.perf_counter()
+    kern_ms = []
+    wstats = {"windows": 0, "stops_service": 0, "stops_exhausted": 0, "stops_cache": 0}
+    for s in range(args.warmup, args.warmup + args.steps):
+        o, rng = sched.batch(step_batch(s), rng)
+        kern_ms.append(sched.last_batch_ms())
+        for k_, v_ in sched.last_batch_stats().items():
+            wstats[k_] += v_
+        outs.append(o)
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    out = np.concatenate(outs)
+    timed = out[args.warmup * args.batch:]
+    pods_timed = args.steps * args.batch
+    value = pods_timed / elapsed
+
+    if rank != 0:
+        sched.close()
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    # ---- roofline of the dominant kernel (the persistent batch kernel) --------
+    kavg_s = float(np.mean(kern_ms)) / 1e3 if kern_ms else float("nan")
+    bpn = BYTES_PER_NODE.get(wl, 60)
+    alg_bytes = bpn * n_nodes * args.batch  # per launch (world=1) / per step (world>1)
+    achieved = alg_bytes / kavg_s
+    traffic = None
+    try:
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        ent = tj.get(f"{wl}:{n_nodes}:{args.batch}")
+        if ent:
+            traffic = ent["hbm_bytes_per_launch"]
+    except (OSError, ValueError):
+        pass
+    roofline = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK, "traffic": traffic,
+                "kernel": "ksg_batch_kernel" if world == 1 else "ksg_scan_kernel+ksg_decide_kernel+rccl",
+                "kernel_ms_avg": kavg_s * 1e3, "bytes_per_node_pod": bpn}
+
+    # ---- CPU baseline: faithful restatement, single thread, bounded prefix ------
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        from oracle.pyoracle import OracleScheduler
+
+        orc = OracleScheduler(cfg, faithful=True)
+        orc.set_cluster(view.arrays)
+        r = workload.TIEBREAK_SEED
+        done = 0
+        t_c = time.perf_counter()
+        chunk = 50
+        cpu_out = []
+        while done < n_pods and time.perf_counter() - t_c < args.cpu_seconds:
+            sub = PodBatch(batch.pods[done:done + chunk], batch.ids)
+            o, r = orc.batch(sub, r)
+            cpu_out.append(o)
+            done += len(sub)
+        cpu_s = time.perf_counter() - t_c
+        cpu_out = np.concatenate(cpu_out)
+        agree = bool(np.array_equal(cpu_out, out[:done]))
+        cpu = {"value": done / cpu_s, "unit": "pods/s", "cores": 1, "kind": "port",
+               "sample": f"first {done} pods of the same {wl} workload on {n_nodes} nodes from an empty cluster "
+                         f"({cpu_s:.1f}s, faithful mode: per-pod MapPodsToMachines regroup, per-node predicate "
+                         f"rescans, HostPriorityList sort); decisions identical to GPU: {agree}",
+               "cpu_model": _cpu_model(), "nproc": os.cpu_count()}
+
+    line = {
+        "metric": "pods scheduled/sec",
+        "value": value,
+        "unit": "pods/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (seeded splitmix64 scheduler_perf-style cluster; SURVEY.md 8(d))",
+        "config": {"workload": f"{wl}: {n_nodes} nodes, {n_pods} pods, "
+                               + ("DefaultProvider" if wl in ("config2", "config3", "config5") else wl),
+                   "nodes": n_nodes, "pods_per_step": args.batch,
+                   "placed_in_timed": int((timed >= 0).sum()), "fit_errors_in_timed": int((timed == -1).sum()),
+                   "snapshots_in_timed": wstats,
+                   "parallelism": "single workgroup persistent kernel" if world == 1
+                   else f"node-sharded x{world}, RCCL all-gather per pod"},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    sched.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for l in f:
+                if l.startswith("model name"):
+                    return l.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+if __name__ == "__main__":
+    main()

@@ -189,6 +189,18 @@ int ksg_schedule_batch(ksg_ctx* ctx, const ksg_pod* pods, uint32_t n,
 int ksg_evaluate(ksg_ctx* ctx, const ksg_pod* pod, const uint32_t* ids,
                  uint8_t* fail_out, int64_t* score_out);
 
+/* Batch execution strategy. window > 0 (default 1024, env KSG_WINDOW): pods
+ * are filtered/scored a window at a time against one snapshot on all CUs and
+ * then resolved in order by one wave (exact; see ksg_window.hip). window = 0:
+ * the persistent one-pod-at-a-time kernel. Both give identical results; the
+ * window path is used only when it is exact (no ServiceAntiAffinity). */
+int ksg_set_window(ksg_ctx* ctx, uint32_t window);
+/* Window statistics of the last ksg_schedule_batch: stats4[0] = windows
+ * (snapshots), [1] = windows ended because a service scalar changed, [2] =
+ * windows ended because every snapshot tie of a pod got worse, [3] = windows
+ * ended by the per-node window cache filling up or an oversized pod. */
+int ksg_last_batch_stats(ksg_ctx* ctx, uint32_t* stats4);
+
 /* Device time (ms) of the last ksg_schedule_batch's kernels, from HIP events
  * recorded on the stream the kernels ran on. */
 int ksg_last_batch_ms(ksg_ctx* ctx, double* ms);

@@ -150,6 +150,8 @@ EXPORTS = [
     "ksg_schedule_commit",
     "ksg_schedule_batch",
     "ksg_evaluate",
+    "ksg_set_window",
+    "ksg_last_batch_stats",
     "ksg_last_batch_ms",
     "ksg_shard",
     "ksg_read_requested",
@@ -189,6 +191,8 @@ def load_library() -> C.CDLL:
         "ksg_schedule_commit": (C.c_int, [vp, U32, P(I32)]),
         "ksg_schedule_batch": (C.c_int, [vp, vp, U32, vp, U32, P(U64), vp]),
         "ksg_evaluate": (C.c_int, [vp, vp, vp, vp, vp]),
+        "ksg_set_window": (C.c_int, [vp, U32]),
+        "ksg_last_batch_stats": (C.c_int, [vp, vp]),
         "ksg_last_batch_ms": (C.c_int, [vp, P(C.c_double)]),
         "ksg_shard": (C.c_int, [vp, P(U32), P(U32)]),
         "ksg_read_requested": (C.c_int, [vp, vp, vp]),

@@ -27,8 +27,12 @@
 #define KSG_MODE_EVAL 0      // write fail codes + scores for every node
 #define KSG_MODE_BEGIN 1     // write {M, k, tie words} record (+ optional fail codes)
 
-// score sentinel for nodes that do not fit
+// score sentinels for nodes that do not fit (int64 records / int32 LDS scores)
 #define KSG_SCORE_NONE (-0x7fffffffffffffffLL - 1)
+#define KSG_S32_NONE ((int32_t)0x80000000)
+// combined scores are kept in int32 on the device; the host rejects weight
+// sets whose |score| could reach this bound
+#define KSG_SCORE_BOUND (1LL << 30)
 
 struct KsgDev {
   // cluster geometry
@@ -47,6 +51,8 @@ struct KsgDev {
   int32_t empty_priorities;   // configs present but all weights 0: always FitError
   int32_t has_static_score;
   int32_t has_static_fit;
+  int32_t dbg;                // debug switches (KSG_DEBUG env), 0 in production
+  int32_t* dbgbuf;            // KSG_DEBUG & 4: per-pod resolver trace
   // arrays
   const int64_t* cap_cpu;
   const int64_t* cap_mem;
@@ -81,6 +87,30 @@ struct KsgStaticCfg {
   uint32_t n_aff;
   uint32_t aff_key[KSG_MAX_AFF];
 };
+
+// window path, phase A output per pod (see ksg_window.hip). Everything phase B
+// needs for one pod in one 192-byte record, so the sequential resolver streams
+// one record per pod instead of chasing the pod descriptor and id lists.
+#define KSG_WIN_INLINE 24
+struct KsgWinSum {
+  int32_t m0;          // best combined score at the snapshot (KSG_S32_NONE: nothing fits)
+  uint32_t k0;         // nodes at m0 (bits of the pod's T0 bitmap)
+  int32_t error;       // ServiceAffinity peer on an unknown node
+  int32_t service;     // primary service
+  int32_t host;        // PodFitsHost target
+  int32_t spread_max;  // svc_max[primary] at the snapshot
+  int32_t svc_total;   // svc_total[primary] at the snapshot
+  uint32_t n_inline;   // total list entries; > KSG_WIN_INLINE: lists read from pods/ids
+  int64_t milli_cpu;
+  int64_t memory;
+  int32_t req_aff[KSG_MAX_AFF];  // resolved ServiceAffinity pairs
+  uint16_t n_ports, n_pds, n_sel, n_svcs;
+  uint32_t pad;
+  uint32_t ids[KSG_WIN_INLINE];  // ports, pds, sel, svcs (in that order)
+  uint32_t pad2[5];
+};
+static_assert(sizeof(KsgWinSum) == 192, "KsgWinSum layout");
+#define KSG_WIN_SUM_DWORDS (sizeof(KsgWinSum) / 4)
 
 // one record of the per-pod winner exchange (all-gathered across ranks)
 struct KsgRecordHdr {

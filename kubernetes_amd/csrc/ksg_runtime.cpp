@@ -29,11 +29,17 @@
 
 hipError_t ksg_launch_batch(int R, bool anti, const KsgDev& d, const ksg_pod* pods,
                             const uint32_t* ids, uint32_t n, uint64_t* rng, int32_t* out,
-                            size_t lds, hipStream_t st);
+                            hipStream_t st);
 hipError_t ksg_launch_scan(int R, bool anti, const KsgDev& d, const ksg_pod* pods,
                            const uint32_t* ids, int mode, int phase, uint8_t* fail_out,
                            int64_t* score_out, uint8_t* record, int32_t* dpart,
-                           const int32_t* dglobal, size_t lds, hipStream_t st);
+                           const int32_t* dglobal, hipStream_t st);
+hipError_t ksg_launch_win_eval(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids, uint32_t n,
+                               KsgWinSum* sums, uint64_t* t0words, hipStream_t st);
+hipError_t ksg_launch_win_resolve(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids, uint32_t n,
+                                  const KsgWinSum* sums, const uint64_t* t0words, uint64_t* rng, int32_t* out,
+                                  uint32_t* resolved, hipStream_t st);
+uint32_t ksg_win_max_window(const KsgDev& d);
 hipError_t ksg_launch_decide(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids,
                              const uint8_t* records, uint32_t rec_bytes, uint32_t world,
                              const uint32_t* shard_wlo, int mode, uint64_t tie_index,
@@ -109,6 +115,15 @@ struct ksg_ctx {
   std::vector<std::map<uint64_t, uint32_t>> svc_members;  // seq -> host
   std::unordered_map<uint64_t, PodRec> pods;
   uint64_t seq = 0;
+
+  // window (speculative) path
+  uint32_t window = 1024;       // 0 = exact one-pod-at-a-time kernel
+  KsgWinSum* d_winsum = nullptr;
+  uint64_t* d_t0 = nullptr;
+  size_t win_cap = 0, t0_cap = 0;
+  uint32_t* d_resolved = nullptr;  // {resolved, stop reason}
+  uint32_t last_stats[4] = {0, 0, 0, 0};  // windows, stops (service scalar), stops (ties exhausted)
+  int64_t max_cap = 0;
 
   // begin/commit
   bool pending = false;
@@ -336,14 +351,14 @@ int scan_exchange(ksg_ctx* c, const ksg_pod* dpod, const uint32_t* dids, int mod
   const bool anti = anti_on(c);
   if (anti && c->world > 1) {
     HIPCHK(c, ksg_launch_scan(c->R, true, c->dev, dpod, dids, mode, 1, nullptr, nullptr, c->d_rec_send,
-                              c->d_dpart, nullptr, c->lds, c->st));
+                              c->d_dpart, nullptr, c->st));
     NCCLCHK(c, ncclAllReduce(c->d_dpart, c->d_dglobal, c->dev.n_domains_total, ncclInt32, ncclSum, c->comm,
                              c->st));
     HIPCHK(c, ksg_launch_scan(c->R, true, c->dev, dpod, dids, mode, 2, fail_out, score_out, c->d_rec_send,
-                              nullptr, c->d_dglobal, c->lds, c->st));
+                              nullptr, c->d_dglobal, c->st));
   } else {
     HIPCHK(c, ksg_launch_scan(c->R, anti, c->dev, dpod, dids, mode, 0, fail_out, score_out, c->d_rec_send,
-                              nullptr, nullptr, c->lds, c->st));
+                              nullptr, nullptr, c->st));
   }
   if (mode == KSG_MODE_BEGIN) {
     if (c->world > 1) {
@@ -353,6 +368,25 @@ int scan_exchange(ksg_ctx* c, const ksg_pod* dpod, const uint32_t* dids, int mod
     }
   }
   return KSG_OK;
+}
+
+// The window path needs monotone scores under commits (see ksg_window.hip):
+// no ServiceAntiAffinity, and int64 totals far from wrapping.
+bool use_window(ksg_ctx* c, const ksg_pod* pods, uint32_t n) {
+  if (c->window == 0 || anti_on(c) || c->nwords > 8 * 64 || ksg_win_max_window(c->dev) == 0) return false;
+  // monotonicity under commits needs non-negative pod-dependent weights
+  if (c->cfg.w_least_requested < 0 || c->cfg.w_service_spreading < 0) return false;
+  const int64_t lim = 1LL << 58;
+  if (c->max_cap > lim) return false;
+  int64_t mu = 0;
+  for (uint32_t i = 0; i < c->N; ++i) mu = std::max<int64_t>(mu, std::max<int64_t>(std::llabs(c->used_c[i]), std::llabs(c->used_m[i])));
+  int64_t sum = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (pods[i].milli_cpu < 0 || pods[i].memory < 0) return false;
+    sum += std::min<int64_t>(pods[i].milli_cpu + pods[i].memory, lim);
+    if (sum > lim) return false;
+  }
+  return mu + sum <= lim;
 }
 
 int ensure_out(ksg_ctx* c, size_t n) { return grow(c, (void**)&c->d_out, &c->out_cap, n, sizeof(int32_t)); }
@@ -377,6 +411,16 @@ static int create_impl(const ksg_config* cfg, int device, int rank, int world, c
     return KSG_ERR_ARG;
   for (uint32_t q = 0; q < cfg->n_presence; ++q)
     if (cfg->presence_n_keys[q] > KSG_MAX_PRESENCE_KEYS) return KSG_ERR_ARG;
+  {  // combined scores are int32 on the device
+    int64_t bound = 10LL * (std::llabs((int64_t)cfg->w_least_requested) + std::llabs((int64_t)cfg->w_service_spreading)) +
+                    std::llabs((int64_t)cfg->w_equal);
+    for (uint32_t a = 0; a < cfg->n_anti; ++a) bound += 10LL * std::llabs((int64_t)cfg->w_anti[a]);
+    for (uint32_t q = 0; q < cfg->n_label_pref; ++q) bound += 10LL * std::llabs((int64_t)cfg->w_pref[q]);
+    if (bound >= KSG_SCORE_BOUND) {
+      fprintf(stderr, "ksg_create: priority weights too large (|score| bound %lld)\n", (long long)bound);
+      return KSG_ERR_ARG;
+    }
+  }
   ksg_ctx* c = new ksg_ctx();
   c->cfg = *cfg;
   if (c->cfg.max_conflict_keys == 0) c->cfg.max_conflict_keys = 1024;
@@ -404,7 +448,9 @@ static int create_impl(const ksg_config* cfg, int device, int rank, int world, c
     if (r != ncclSuccess) return bail(fail(c, KSG_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r)));
   }
   int rc;
-  if ((rc = dalloc(c, &c->d_rng, 1, nullptr)) || (rc = dalloc(c, &c->d_summary, 4, nullptr)))
+  if (const char* wenv = getenv("KSG_WINDOW")) c->window = (uint32_t)atoi(wenv);
+  if ((rc = dalloc(c, &c->d_rng, 1, nullptr)) || (rc = dalloc(c, &c->d_summary, 4, nullptr)) ||
+      (rc = dalloc(c, &c->d_resolved, 4, nullptr)))
     return bail(rc);
   *out = c;
   return KSG_OK;
@@ -421,11 +467,18 @@ int ksg_create_sharded(const ksg_config* cfg, int device, int rank, int world, c
 
 int ksg_destroy(ksg_ctx* c) {
   if (!c) return KSG_OK;
+  if (c->dev.dbgbuf) {  // debug stamps (KSG_DEBUG & 8): cycles/64 per resolver section
+    int32_t h[8];
+    (void)hipMemcpy(h, c->dev.dbgbuf, sizeof h, hipMemcpyDeviceToHost);
+    fprintf(stderr, "ksg stamps (x64 cycles): prefetch-issue %d retire %d head %d recheck %d select %d commit %d loop-end %d candidates %d\n",
+            h[0], h[1], h[6], h[2] - h[6], h[3], h[4], h[5], h[7]);
+  }
   (void)hipSetDevice(c->device);
   if (c->st) (void)hipStreamSynchronize(c->st);
   free_cluster(c);
   void* scratch[] = {c->d_pods, c->d_ids, c->d_fail, c->d_score, c->d_rec_send, c->d_rec_recv, c->d_dpart,
-                     c->d_dglobal, c->d_out, c->d_rng, c->d_summary, c->d_patch, c->d_shard_wlo};
+                     c->d_dglobal, c->d_out, c->d_rng, c->d_summary, c->d_patch, c->d_shard_wlo,
+                     c->d_winsum, c->d_t0, c->d_resolved};
   for (void* p : scratch)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -518,9 +571,11 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
 
   // upload nodes + static tables
   std::vector<int64_t> hc(NN, 0), hm(NN, 0);
+  c->max_cap = 0;
   for (uint32_t i = 0; i < n_nodes; ++i) {
     hc[i] = nodes[i].cap_milli_cpu;
     hm[i] = nodes[i].cap_memory;
+    c->max_cap = std::max<int64_t>(c->max_cap, std::max<int64_t>(std::llabs(hc[i]), std::llabs(hm[i])));
   }
   HIPCHK(c, hipMemcpyAsync(cap_c, hc.data(), NN * 8, hipMemcpyHostToDevice, c->st));
   HIPCHK(c, hipMemcpyAsync(cap_m, hm.data(), NN * 8, hipMemcpyHostToDevice, c->st));
@@ -588,6 +643,11 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   bool any_pref = false;
   for (uint32_t q = 0; q < c->cfg.n_label_pref; ++q) any_pref |= c->cfg.w_pref[q] != 0;
   d.has_static_score = (c->cfg.w_equal != 0 || any_pref) ? 1 : 0;
+  d.dbg = getenv("KSG_DEBUG") ? atoi(getenv("KSG_DEBUG")) : 0;
+  if (d.dbg & 8) {
+    (void)hipMalloc(&d.dbgbuf, 64);
+    (void)hipMemset(d.dbgbuf, 0, 64);
+  }
   d.has_static_fit = ((c->cfg.predicates & KSG_PRED_LABELSPRESENCE) && c->cfg.n_presence > 0) ? 1 : 0;
   d.cap_cpu = cap_c;
   d.cap_mem = cap_m;
@@ -763,9 +823,38 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
   if ((rc = ensure_out(c, n))) return rc;
   HIPCHK(c, hipMemcpyAsync(c->d_rng, rng_state, 8, hipMemcpyHostToDevice, c->st));
   HIPCHK(c, hipEventRecord(c->ev0, c->st));
-  if (c->world == 1) {
-    HIPCHK(c, ksg_launch_batch(c->R, anti_on(c), c->dev, c->d_pods, c->d_ids, n, c->d_rng, c->d_out, c->lds,
-                               c->st));
+  c->last_stats[0] = c->last_stats[1] = c->last_stats[2] = c->last_stats[3] = 0;
+  if (c->world == 1 && use_window(c, pods, n)) {
+    const uint32_t W = std::min(c->window, ksg_win_max_window(c->dev));
+    if ((rc = grow(c, (void**)&c->d_winsum, &c->win_cap, W, sizeof(KsgWinSum)))) return rc;
+    if ((rc = grow(c, (void**)&c->d_t0, &c->t0_cap, (size_t)W * c->nwords, sizeof(uint64_t)))) return rc;
+    uint32_t pos = 0;
+    while (pos < n) {
+      const uint32_t w = std::min(W, n - pos);
+      HIPCHK(c, ksg_launch_win_eval(c->dev, c->d_pods + pos, c->d_ids, w, c->d_winsum, c->d_t0, c->st));
+      HIPCHK(c, ksg_launch_win_resolve(c->dev, c->d_pods + pos, c->d_ids, w, c->d_winsum, c->d_t0, c->d_rng,
+                                       c->d_out + pos, c->d_resolved, c->st));
+      uint32_t st2[2] = {0, 0};
+      HIPCHK(c, hipMemcpyAsync(st2, c->d_resolved, 8, hipMemcpyDeviceToHost, c->st));
+      HIPCHK(c, hipStreamSynchronize(c->st));
+      const uint32_t res = st2[0];
+      ++c->last_stats[0];
+      if (st2[1] == 4) {
+        // a pod whose id lists exceed the window record: exact per-pod kernel
+        HIPCHK(c, ksg_launch_batch(c->R, false, c->dev, c->d_pods + pos, c->d_ids, 1, c->d_rng, c->d_out + pos,
+                                   c->st));
+        pos += 1;
+        ++c->last_stats[3];
+        continue;
+      }
+      if (res == 0 || res > w) return fail(c, KSG_ERR_STATE, "window resolved %u of %u pods", res, w);
+      pos += res;
+      if (st2[1] == 1) ++c->last_stats[1];
+      if (st2[1] == 2) ++c->last_stats[2];
+      if (st2[1] == 3) ++c->last_stats[3];
+    }
+  } else if (c->world == 1) {
+    HIPCHK(c, ksg_launch_batch(c->R, anti_on(c), c->dev, c->d_pods, c->d_ids, n, c->d_rng, c->d_out, c->st));
   } else {
     for (uint32_t i = 0; i < n; ++i) {
       if ((rc = scan_exchange(c, c->d_pods + i, c->d_ids, KSG_MODE_BEGIN, nullptr, nullptr))) return rc;
@@ -812,6 +901,18 @@ int ksg_evaluate(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, uint8_t* f
   if (score_out && ns) HIPCHK(c, hipMemcpyAsync(score_out, c->d_score, ns * 8, hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
   if (summ[2]) return fail(c, KSG_ERR_NOPEER, "service affinity peer is not on a known node");
+  return KSG_OK;
+}
+
+int ksg_set_window(ksg_ctx* c, uint32_t window) {
+  if (!c) return KSG_ERR_ARG;
+  c->window = window;
+  return KSG_OK;
+}
+
+int ksg_last_batch_stats(ksg_ctx* c, uint32_t* stats4) {
+  if (!c || !stats4) return KSG_ERR_ARG;
+  for (int i = 0; i < 4; ++i) stats4[i] = c->last_stats[i];
   return KSG_OK;
 }
 

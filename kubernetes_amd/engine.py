@@ -168,6 +168,21 @@ class DeviceScheduler:
             self._err(rc)
         return rc, fails[: hi - lo], scores[: hi - lo]
 
+    def set_window(self, window: int):
+        """Pods per speculative window (0 = exact one-pod-at-a-time kernel)."""
+        rc = self._lib.ksg_set_window(self._ctx, int(window))
+        if rc != abi.KSG_OK:
+            self._err(rc)
+
+    def last_batch_stats(self) -> dict:
+        st = np.zeros(4, np.uint32)
+        self._lib.ksg_last_batch_stats(self._ctx, abi.ptr(st))
+        return {"windows": int(st[0]), "stops_service": int(st[1]), "stops_exhausted": int(st[2]),
+                "stops_cache": int(st[3])}
+
+    def last_batch_windows(self) -> int:
+        return self.last_batch_stats()["windows"]
+
     def last_batch_ms(self) -> float:
         ms = C.c_double(0)
         self._lib.ksg_last_batch_ms(self._ctx, C.byref(ms))

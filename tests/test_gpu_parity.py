@@ -16,10 +16,14 @@ from tests.helpers import Case, run_batch
 pytestmark = pytest.mark.gpu
 
 
-def _pair(case):
-    return DeviceScheduler(case.cfg, device=0), OracleScheduler(case.cfg)
+def _pair(case, window=None):
+    dev = DeviceScheduler(case.cfg, device=0)
+    if window is not None:
+        dev.set_window(window)
+    return dev, OracleScheduler(case.cfg)
 
 
+@pytest.mark.parametrize("window", [0, 1024, 37])
 @pytest.mark.parametrize("name,nn,npods", [
     ("config1", 500, 1000),      # BASELINE config 1 at full size
     ("config2", 700, 1500),
@@ -29,9 +33,10 @@ def _pair(case):
     ("config2", 9000, 800),      # R = 16 (memory-resident node state)
     ("config4", 20000, 300),     # R = 32, anti-affinity
 ])
-def test_batch_matches_oracle(name, nn, npods):
+def test_batch_matches_oracle(name, nn, npods, window):
+    """window=0: exact one-pod-at-a-time kernel; >0: speculative window path."""
     case = Case(name, nn, npods)
-    dev, orc = _pair(case)
+    dev, orc = _pair(case, window)
     got, sg = run_batch(dev, case)
     want, sw = run_batch(orc, case)
     bad = np.nonzero(got != want)[0]
@@ -43,10 +48,11 @@ def test_batch_matches_oracle(name, nn, npods):
     dev.close()
 
 
-def test_batch_chunks_equal_one_batch():
+@pytest.mark.parametrize("window", [0, 256])
+def test_batch_chunks_equal_one_batch(window):
     """Batch boundaries must not change outcomes (state persists across launches)."""
     case = Case("config2", 1500, 1200)
-    dev, orc = _pair(case)
+    dev, orc = _pair(case, window)
     got, sg = run_batch(dev, case, chunk=97)
     want, sw = run_batch(orc, case)
     assert np.array_equal(got, want) and sg == sw
