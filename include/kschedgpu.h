@@ -189,7 +189,7 @@ int ksg_schedule_batch(ksg_ctx* ctx, const ksg_pod* pods, uint32_t n,
 int ksg_evaluate(ksg_ctx* ctx, const ksg_pod* pod, const uint32_t* ids,
                  uint8_t* fail_out, int64_t* score_out);
 
-/* Batch execution strategy. window > 0 (default 1024, env KSG_WINDOW): pods
+/* Batch execution strategy. window > 0 (default 128, env KSG_WINDOW): pods
  * are filtered/scored a window at a time against one snapshot on all CUs and
  * then resolved in order by one wave (exact; see ksg_window.hip). window = 0:
  * the persistent one-pod-at-a-time kernel. Both give identical results; the
@@ -204,6 +204,12 @@ int ksg_last_batch_stats(ksg_ctx* ctx, uint32_t* stats4);
 /* Device time (ms) of the last ksg_schedule_batch's kernels, from HIP events
  * recorded on the stream the kernels ran on. */
 int ksg_last_batch_ms(ksg_ctx* ctx, double* ms);
+
+/* Window path of the last ksg_schedule_batch: out3[0] = device ms in the
+ * snapshot-scoring kernel (ksg_win_eval_kernel), out3[1] = device ms in the
+ * resolver (ksg_win_resolve_kernel), out3[2] = number of windows; from HIP
+ * events recorded around each launch on the context's stream. */
+int ksg_last_batch_kernel_ms(ksg_ctx* ctx, double* out3);
 
 /* Node shard owned by this context: [lo, hi). */
 int ksg_shard(ksg_ctx* ctx, uint32_t* lo, uint32_t* hi);

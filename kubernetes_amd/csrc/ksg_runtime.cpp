@@ -117,12 +117,14 @@ struct ksg_ctx {
   uint64_t seq = 0;
 
   // window (speculative) path
-  uint32_t window = 1024;       // 0 = exact one-pod-at-a-time kernel
+  uint32_t window = 128;        // 0 = exact one-pod-at-a-time kernel
   KsgWinSum* d_winsum = nullptr;
   uint64_t* d_t0 = nullptr;
   size_t win_cap = 0, t0_cap = 0;
   uint32_t* d_resolved = nullptr;  // {resolved, stop reason}
   uint32_t last_stats[4] = {0, 0, 0, 0};  // windows, stops (service scalar), stops (ties exhausted)
+  hipEvent_t kev[4] = {nullptr, nullptr, nullptr, nullptr};
+  double last_kms[3] = {0, 0, 0};  // phase A ms, phase B ms, launches (window path)
   int64_t max_cap = 0;
 
   // begin/commit
@@ -484,6 +486,8 @@ int ksg_destroy(ksg_ctx* c) {
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  for (auto& e : c->kev)
+    if (e) (void)hipEventDestroy(e);
   if (c->st) (void)hipStreamDestroy(c->st);
   delete c;
   return KSG_OK;
@@ -829,16 +833,31 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     if ((rc = grow(c, (void**)&c->d_winsum, &c->win_cap, W, sizeof(KsgWinSum)))) return rc;
     if ((rc = grow(c, (void**)&c->d_t0, &c->t0_cap, (size_t)W * c->nwords, sizeof(uint64_t)))) return rc;
     uint32_t pos = 0;
+    if (!c->kev[0])
+      for (auto& e : c->kev) HIPCHK(c, hipEventCreate(&e));
+    c->last_kms[0] = c->last_kms[1] = c->last_kms[2] = 0;
     while (pos < n) {
       const uint32_t w = std::min(W, n - pos);
+      // HIP events on this stream around each kernel (per-kernel device time)
+      HIPCHK(c, hipEventRecord(c->kev[0], c->st));
       HIPCHK(c, ksg_launch_win_eval(c->dev, c->d_pods + pos, c->d_ids, w, c->d_winsum, c->d_t0, c->st));
+      HIPCHK(c, hipEventRecord(c->kev[1], c->st));
       HIPCHK(c, ksg_launch_win_resolve(c->dev, c->d_pods + pos, c->d_ids, w, c->d_winsum, c->d_t0, c->d_rng,
                                        c->d_out + pos, c->d_resolved, c->st));
+      HIPCHK(c, hipEventRecord(c->kev[2], c->st));
       uint32_t st2[2] = {0, 0};
       HIPCHK(c, hipMemcpyAsync(st2, c->d_resolved, 8, hipMemcpyDeviceToHost, c->st));
       HIPCHK(c, hipStreamSynchronize(c->st));
       const uint32_t res = st2[0];
       ++c->last_stats[0];
+      {
+        float a = 0.f, b = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&a, c->kev[0], c->kev[1]));
+        HIPCHK(c, hipEventElapsedTime(&b, c->kev[1], c->kev[2]));
+        c->last_kms[0] += a;
+        c->last_kms[1] += b;
+        c->last_kms[2] += 1;
+      }
       if (st2[1] == 4) {
         // a pod whose id lists exceed the window record: exact per-pod kernel
         HIPCHK(c, ksg_launch_batch(c->R, false, c->dev, c->d_pods + pos, c->d_ids, 1, c->d_rng, c->d_out + pos,
@@ -913,6 +932,12 @@ int ksg_set_window(ksg_ctx* c, uint32_t window) {
 int ksg_last_batch_stats(ksg_ctx* c, uint32_t* stats4) {
   if (!c || !stats4) return KSG_ERR_ARG;
   for (int i = 0; i < 4; ++i) stats4[i] = c->last_stats[i];
+  return KSG_OK;
+}
+
+int ksg_last_batch_kernel_ms(ksg_ctx* c, double* out3) {
+  if (!c || !out3) return KSG_ERR_ARG;
+  for (int i = 0; i < 3; ++i) out3[i] = c->last_kms[i];
   return KSG_OK;
 }
 

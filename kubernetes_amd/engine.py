@@ -183,6 +183,12 @@ class DeviceScheduler:
     def last_batch_windows(self) -> int:
         return self.last_batch_stats()["windows"]
 
+    def last_batch_kernel_ms(self) -> dict:
+        """Window path: device ms of the snapshot kernel, of the resolver, windows."""
+        o = np.zeros(3, np.float64)
+        self._lib.ksg_last_batch_kernel_ms(self._ctx, abi.ptr(o))
+        return {"eval_ms": float(o[0]), "resolve_ms": float(o[1]), "launches": int(o[2])}
+
     def last_batch_ms(self) -> float:
         ms = C.c_double(0)
         self._lib.ksg_last_batch_ms(self._ctx, C.byref(ms))
