@@ -9,7 +9,11 @@ host ingest (tests/test_oracle_crosscheck.py).
 
 Go map iteration order is the only nondeterminism in the reference on this
 path; it is canonicalised here as in the product:
-  * predicates run in sorted-name order (findNodesThatFit, generic_scheduler.go:109);
+  * predicates run in sorted-name order (findNodesThatFit, generic_scheduler.go:109),
+    except that predicates which can return an error (ServiceAffinity's peer
+    lookup, predicates.go:293-297) run first: when the first service peer sits
+    on a host outside the node list, Schedule returns that error (one of the
+    outcomes Go's random map order allows, and the one the kernels implement);
   * services[0] = first matching service in ServiceLister order (spreading.go:54);
   * nsServicePods[0] = first matching pod in PodLister order (predicates.go:293).
 """
@@ -186,6 +190,7 @@ def new_service_affinity_predicate(pod_lister: PodLister, service_lister: Servic
                             affinity[l] = set_get(other.metadata.labels, l)
         sel = everything() if not affinity else selector_from_set(affinity)
         return sel.matches(info.get(node).metadata.labels)
+    check_service_affinity.may_error = True
     return check_service_affinity
 
 
@@ -330,7 +335,7 @@ def find_nodes_that_fit(pod: Pod, pod_lister: PodLister, predicates: Dict[str, P
     m = map_pods_to_machines(pod_lister)
     for n in nodes:
         fits = True
-        for name in sorted(predicates):
+        for name in sorted(predicates, key=lambda k: (not getattr(predicates[k], "may_error", False), k)):
             if not predicates[name](pod, m.get(n.metadata.name, []), n.metadata.name):
                 fits = False
                 failed.setdefault(n.metadata.name, set()).add(name)
@@ -398,4 +403,44 @@ def default_provider(nodes: Sequence[Node], pod_lister: PodLister, service_liste
     }
     # priorities in sorted name order (plugins.go:235-248)
     prios = [(equal_priority, 0), (least_requested_priority, 1), (new_service_spread_priority(service_lister), 1)]
+    return preds, prios
+
+
+def from_config(config, nodes: Sequence[Node], pod_lister: PodLister, service_lister: ServiceLister):
+    """Bind a kubernetes_amd.factory.SchedulerConfig to these functions, as the factory's
+    getFitPredicateFunctions / getPriorityFunctionConfigs do (plugins.go:220-248)."""
+    info = NodeInfo(nodes)
+    preds: Dict[str, Predicate] = {}
+    for name, d in config.predicates.items():
+        if d.kind == "PodFitsPorts":
+            preds[name] = pod_fits_ports
+        elif d.kind == "PodFitsResources":
+            preds[name] = new_resource_fit_predicate(info)
+        elif d.kind == "NoDiskConflict":
+            preds[name] = no_disk_conflict
+        elif d.kind == "MatchNodeSelector":
+            preds[name] = new_selector_match_predicate(info)
+        elif d.kind == "HostName":
+            preds[name] = pod_fits_host
+        elif d.kind == "ServiceAffinity":
+            preds[name] = new_service_affinity_predicate(pod_lister, service_lister, info, d.labels)
+        elif d.kind == "LabelsPresence":
+            preds[name] = new_node_label_predicate(info, d.labels, d.presence)
+        else:
+            raise ValueError(d.kind)
+    prios: List[Tuple[PriorityFn, int]] = []
+    for d in config.priorities:
+        if d.kind == "LeastRequestedPriority":
+            fn = least_requested_priority
+        elif d.kind == "ServiceSpreadingPriority":
+            fn = new_service_spread_priority(service_lister)
+        elif d.kind == "EqualPriority":
+            fn = equal_priority
+        elif d.kind == "ServiceAntiAffinity":
+            fn = new_service_anti_affinity_priority(service_lister, d.label)
+        elif d.kind == "LabelPreference":
+            fn = new_node_label_priority(d.label, d.presence)
+        else:
+            raise ValueError(d.kind)
+        prios.append((fn, d.weight))
     return preds, prios

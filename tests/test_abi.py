@@ -1,0 +1,90 @@
+"""The drop-in boundary without a GPU: libkschedgpu.so loads, exports every entry point
+include/kschedgpu.h declares, and the ctypes/numpy mirrors match the C struct layouts
+(checked by compiling the header with gcc). No compute call is made here."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from kubernetes_amd import abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "kschedgpu.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^[A-Za-z_][\w \*]*?\b(ksg_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_the_abi():
+    d = _declared()
+    assert "ksg_schedule_begin" in d and "ksg_schedule_batch" in d
+    assert sorted(abi.EXPORTS) == d
+
+
+def test_library_exports_every_declared_symbol():
+    path = abi.lib_path()
+    assert os.path.exists(path), "build() must produce the in-tree library"
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    exported = {l.split()[-1] for l in out.splitlines() if l.strip()}
+    missing = [s for s in _declared() if s not in exported]
+    assert not missing, missing
+    lib = abi.load_library()  # dlopen + signatures; no HIP call is made
+    for s in _declared():
+        assert getattr(lib, s) is not None
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    monkeypatch.setattr(abi, "_lib", None)
+    monkeypatch.setattr(abi, "lib_path", lambda: str(tmp_path / "nope.so"))
+    with pytest.raises(RuntimeError, match="missing"):
+        abi.load_library()
+
+
+_LAYOUT_C = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "kschedgpu.h"
+#define P(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
+int main(void) {
+  printf("ksg_config %zu\nksg_node %zu\nksg_pod %zu\n", sizeof(ksg_config), sizeof(ksg_node), sizeof(ksg_pod));
+  %FIELDS%
+  return 0;
+}
+"""
+
+
+def test_struct_layouts_match_header(tmp_path):
+    fields = []
+    for T, cls in (("ksg_config", abi.KsgConfig), ("ksg_node", abi.KsgNode), ("ksg_pod", abi.KsgPod)):
+        for name, _ in cls._fields_:
+            fields.append(f"P({T}, {name})")
+    src = tmp_path / "layout.c"
+    src.write_text(_LAYOUT_C.replace("%FIELDS%", "\n  ".join(fields)))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                          check=True).stdout.splitlines())
+    assert int(got["ksg_config"]) == C.sizeof(abi.KsgConfig)
+    assert int(got["ksg_node"]) == C.sizeof(abi.KsgNode) == abi.NODE_DTYPE.itemsize
+    assert int(got["ksg_pod"]) == C.sizeof(abi.KsgPod) == abi.POD_DTYPE.itemsize
+    for T, cls in (("ksg_config", abi.KsgConfig), ("ksg_node", abi.KsgNode), ("ksg_pod", abi.KsgPod)):
+        for name, _ in cls._fields_:
+            assert int(got[f"{T}.{name}"]) == getattr(cls, name).offset, (T, name)
+    for name in abi.POD_DTYPE.names:
+        assert abi.POD_DTYPE.fields[name][1] == getattr(abi.KsgPod, name).offset
+
+
+def test_product_never_imports_the_oracle():
+    """The oracle is test infrastructure: nothing under kubernetes_amd/ may reference it."""
+    pkg = os.path.join(ROOT, "kubernetes_amd")
+    for dp, _, fs in os.walk(pkg):
+        for f in fs:
+            if f.endswith((".py", ".cpp", ".hip", ".h")):
+                txt = open(os.path.join(dp, f), encoding="utf-8").read()
+                assert not re.search(r"^\s*(from|import)\s+oracle\b", txt, flags=re.M), f
+                assert "liboracle" not in txt and "ksg_oracle" not in txt, f
