@@ -211,6 +211,36 @@ int ksg_last_batch_ms(ksg_ctx* ctx, double* ms);
  * events recorded around each launch on the context's stream. */
 int ksg_last_batch_kernel_ms(ksg_ctx* ctx, double* out3);
 
+/* ---- node sharding (multi-GPU) ------------------------------
+ * Nodes are split into contiguous runs of 64-node words in name-rank order.
+ * Per pod every shard produces one record: this header followed by the shard's
+ * tie bitmap (uint64 words, bit j of word w = node 64*(shard_first_word+w)+j
+ * scores max_score). The winner rule over all records is the reference's
+ * selectHost (generic_scheduler.go:84-96): global max, k = sum of the shards'
+ * counts at the max, ix = Int63() % k, ix-th tie counted from the highest name
+ * rank. ksg_schedule_batch/begin/commit apply it on the device after an RCCL
+ * all-gather; these two host functions expose the same rule (same code) for a
+ * caller that exchanges records over its own transport. */
+typedef struct ksg_shard_record {
+  int64_t max_score;  /* INT64_MIN if nothing fits in the shard */
+  uint64_t tie_count; /* nodes of the shard at max_score */
+  int32_t error;      /* nonzero: the pod errors (ServiceAffinity peer not a node) */
+  int32_t pad;
+  uint64_t pad2;
+} ksg_shard_record;
+
+/* Node range [lo, hi) of shard `rank` of `world` over n_nodes rank-ordered nodes. */
+int ksg_shard_range(uint32_t n_nodes, int rank, int world, uint32_t* lo, uint32_t* hi);
+
+/* Merge `world` records of rec_bytes each (header + ceil-words tie bitmap).
+ * rng_state != NULL: draw Int63 from the splitmix64 stream only if k > 0 (as the
+ * batch path); else use tie_index % k (as ksg_schedule_commit). Returns KSG_OK
+ * with *out_node = global node rank, KSG_NOFIT (no draw), or KSG_ERR_NOPEER.
+ * empty_priorities: the config has priority configs but all weights are 0. */
+int ksg_merge_records(const void* records, uint32_t rec_bytes, uint32_t world, uint32_t n_nodes,
+                      int empty_priorities, uint64_t* rng_state, uint64_t tie_index, int32_t* out_node,
+                      int64_t* max_score, uint64_t* tie_count);
+
 /* Node shard owned by this context: [lo, hi). */
 int ksg_shard(ksg_ctx* ctx, uint32_t* lo, uint32_t* hi);
 

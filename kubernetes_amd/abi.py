@@ -109,6 +109,10 @@ class KsgPod(C.Structure):
     ]
 
 
+class KsgShardRecord(C.Structure):
+    _fields_ = [("max_score", I64), ("tie_count", U64), ("error", I32), ("pad", I32), ("pad2", U64)]
+
+
 # numpy mirrors of the C structs (batched construction without Python loops)
 NODE_DTYPE = np.dtype(
     [("cap_milli_cpu", "<i8"), ("cap_memory", "<i8"), ("label_off", "<u4"), ("n_labels", "<u4")],
@@ -156,6 +160,8 @@ EXPORTS = [
     "ksg_last_batch_kernel_ms",
     "ksg_shard",
     "ksg_read_requested",
+    "ksg_shard_range",
+    "ksg_merge_records",
 ]
 
 LIB_NAME = "libkschedgpu.so"
@@ -198,6 +204,8 @@ def load_library() -> C.CDLL:
         "ksg_last_batch_kernel_ms": (C.c_int, [vp, vp]),
         "ksg_shard": (C.c_int, [vp, P(U32), P(U32)]),
         "ksg_read_requested": (C.c_int, [vp, vp, vp]),
+        "ksg_shard_range": (C.c_int, [U32, C.c_int, C.c_int, P(U32), P(U32)]),
+        "ksg_merge_records": (C.c_int, [vp, U32, U32, U32, C.c_int, P(U64), U64, P(I32), P(I64), P(U64)]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)

@@ -113,13 +113,7 @@ static_assert(sizeof(KsgWinSum) == 192, "KsgWinSum layout");
 #define KSG_WIN_SUM_DWORDS (sizeof(KsgWinSum) / 4)
 
 // one record of the per-pod winner exchange (all-gathered across ranks)
-struct KsgRecordHdr {
-  int64_t max_score;   // KSG_SCORE_NONE if nothing fits in this shard
-  uint64_t tie_count;  // nodes of this shard at max_score
-  int32_t error;       // nonzero: pod errors (ServiceAffinity peer missing)
-  int32_t pad;
-  uint64_t pad2;
-};
+typedef ksg_shard_record KsgRecordHdr;  // public layout (include/kschedgpu.h)
 // followed by nwords_max uint64 tie words (bit set = node at max_score)
 
 struct KsgPatch {

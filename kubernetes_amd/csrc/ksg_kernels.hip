@@ -23,6 +23,7 @@
 #include "ksg_internal.h"
 
 #include "ksg_device.h"
+#include "ksg_shard.h"
 
 // ============================================================================
 // Exact per-pod path. One workgroup of 1024 threads (16 waves); thread t owns
@@ -324,28 +325,18 @@ __global__ __launch_bounds__(64) void ksg_decide_kernel(KsgDev d, const ksg_pod*
                                                        uint64_t* rng_io, int32_t* out,
                                                        uint32_t out_idx, int64_t* summary) {
   const uint32_t lane = threadIdx.x;
-  int64_t M = KSG_SCORE_NONE;
-  int err = 0;
-  for (uint32_t g = 0; g < world; ++g) {
-    const KsgRecordHdr* h = reinterpret_cast<const KsgRecordHdr*>(records + (size_t)g * rec_bytes);
-    if (h->error) err = 1;
-    if (h->tie_count > 0 && h->max_score > M) M = h->max_score;
-  }
-  uint64_t k = 0;
-  for (uint32_t g = 0; g < world; ++g) {
-    const KsgRecordHdr* h = reinterpret_cast<const KsgRecordHdr*>(records + (size_t)g * rec_bytes);
-    if (h->tie_count > 0 && h->max_score == M) k += h->tie_count;
-  }
-  if (d.empty_priorities) k = 0;  // all priority weights 0: empty HostPriorityList
+  const KsgMerged mg = ksg_merge_summary(records, rec_bytes, world, d.empty_priorities);
+  const int64_t M = mg.max_score;
+  const uint64_t k = mg.tie_count;
   if (mode == 0) {
     if (lane == 0) {
       summary[0] = M;
       summary[1] = (int64_t)k;
-      summary[2] = err;
+      summary[2] = mg.error;
     }
     return;
   }
-  if (err) {
+  if (mg.error) {
     if (lane == 0) out[out_idx] = KSG_OUT_ERROR;
     return;
   }
@@ -362,20 +353,8 @@ __global__ __launch_bounds__(64) void ksg_decide_kernel(KsgDev d, const ksg_pod*
     ix = tie_index % k;
   }
   // descending rank order: highest shard first (generic_scheduler.go:88-95)
-  int32_t owner = -1;
   uint64_t lix = 0, kg = 0;
-  for (int32_t g = (int32_t)world - 1; g >= 0; --g) {
-    const KsgRecordHdr* h = reinterpret_cast<const KsgRecordHdr*>(records + (size_t)g * rec_bytes);
-    if (h->tie_count > 0 && h->max_score == M) {
-      if (ix < h->tie_count) {
-        owner = g;
-        lix = ix;
-        kg = h->tie_count;
-        break;
-      }
-      ix -= h->tie_count;
-    }
-  }
+  const int32_t owner = ksg_merge_owner(records, rec_bytes, world, M, ix, &lix, &kg);
   if (owner < 0) {
     if (lane == 0) out[out_idx] = KSG_OUT_ERROR;
     return;

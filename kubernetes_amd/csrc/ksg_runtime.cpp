@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "ksg_internal.h"
+#include "ksg_shard.h"
 
 
 hipError_t ksg_launch_batch(int R, bool anti, const KsgDev& d, const ksg_pod* pods,
@@ -397,6 +398,50 @@ int ensure_out(ksg_ctx* c, size_t n) { return grow(c, (void**)&c->d_out, &c->out
 
 extern "C" {
 
+int ksg_shard_range(uint32_t n_nodes, int rank, int world, uint32_t* lo, uint32_t* hi) {
+  if (world < 1 || rank < 0 || rank >= world || !lo || !hi) return KSG_ERR_ARG;
+  uint32_t a, b;
+  ksg_shard_words((n_nodes + 63) / 64, (uint32_t)rank, (uint32_t)world, &a, &b);
+  *lo = std::min(a * 64, n_nodes);
+  *hi = std::min(b * 64, n_nodes);
+  return KSG_OK;
+}
+
+int ksg_merge_records(const void* records, uint32_t rec_bytes, uint32_t world, uint32_t n_nodes,
+                      int empty_priorities, uint64_t* rng_state, uint64_t tie_index, int32_t* out_node,
+                      int64_t* max_score, uint64_t* tie_count) {
+  if (!records || world < 1 || rec_bytes < sizeof(KsgRecordHdr) || !out_node) return KSG_ERR_ARG;
+  const uint8_t* rec = static_cast<const uint8_t*>(records);
+  const KsgMerged m = ksg_merge_summary(rec, rec_bytes, world, empty_priorities);
+  if (max_score) *max_score = m.max_score;
+  if (tie_count) *tie_count = m.tie_count;
+  *out_node = -1;
+  if (m.error) return KSG_ERR_NOPEER;
+  if (m.tie_count == 0) return KSG_NOFIT;
+  const uint64_t ix = rng_state ? (ksg_splitmix_next(rng_state) >> 1) % m.tie_count : tie_index % m.tie_count;
+  uint64_t lix = 0, kg = 0;
+  const int32_t g = ksg_merge_owner(rec, rec_bytes, world, m.max_score, ix, &lix, &kg);
+  if (g < 0) return KSG_ERR_ARG;
+  uint32_t a, b;
+  ksg_shard_words((n_nodes + 63) / 64, (uint32_t)g, world, &a, &b);
+  const uint32_t nwords = (rec_bytes - (uint32_t)sizeof(KsgRecordHdr)) / 8;
+  const uint64_t* words = reinterpret_cast<const uint64_t*>(rec + (size_t)g * rec_bytes + sizeof(KsgRecordHdr));
+  // the lix-th tie from the top = the (kg-1-lix)-th set bit from the bottom
+  uint64_t target = kg - 1 - lix;
+  for (uint32_t w = 0; w < std::min(nwords, b - a); ++w) {
+    uint64_t x = words[w];
+    const uint32_t cnt = (uint32_t)__builtin_popcountll(x);
+    if (target >= cnt) {
+      target -= cnt;
+      continue;
+    }
+    for (; target; --target) x &= x - 1;
+    *out_node = (int32_t)((a + w) * 64 + (uint32_t)__builtin_ctzll(x));
+    return *out_node < (int32_t)n_nodes ? KSG_OK : KSG_ERR_ARG;
+  }
+  return KSG_ERR_ARG;  // record's count and bitmap disagree
+}
+
 int ksg_nccl_unique_id(void* out128) {
   ncclUniqueId id;
   if (ncclGetUniqueId(&id) != ncclSuccess) return KSG_ERR_RCCL;
@@ -519,8 +564,8 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   c->nwords_max = 0;
   uint32_t max_shard_nodes = 0;
   for (int g = 0; g < c->world; ++g) {
-    const uint32_t a = (uint32_t)((uint64_t)g * c->nw / c->world);
-    const uint32_t b = (uint32_t)((uint64_t)(g + 1) * c->nw / c->world);
+    uint32_t a, b;
+    ksg_shard_words(c->nw, (uint32_t)g, (uint32_t)c->world, &a, &b);
     c->shard_wlo_h[g] = a;
     c->nwords_max = std::max(c->nwords_max, b - a);
     max_shard_nodes = std::max(max_shard_nodes, std::min(b * 64, n_nodes) - std::min(a * 64, n_nodes));

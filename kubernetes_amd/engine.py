@@ -207,3 +207,58 @@ class DeviceScheduler:
         if rc != abi.KSG_OK:
             self._err(rc)
         return c[: self.n_nodes], m[: self.n_nodes]
+
+
+# ---- node sharding (host side of the multi-GPU exchange; include/kschedgpu.h) ----
+REC_HDR_BYTES = C.sizeof(abi.KsgShardRecord)
+
+
+def shard_range(n_nodes: int, rank: int, world: int):
+    """ksg_shard_range: node range [lo, hi) of `rank`'s shard."""
+    lib = abi.load_library()
+    lo, hi = C.c_uint32(0), C.c_uint32(0)
+    rc = lib.ksg_shard_range(int(n_nodes), int(rank), int(world), C.byref(lo), C.byref(hi))
+    if rc != abi.KSG_OK:
+        raise KsgError(rc, "ksg_shard_range")
+    return lo.value, hi.value
+
+
+def merge_records(records: np.ndarray, n_nodes: int, empty_priorities: bool = False,
+                  rng_state: int | None = None, tie_index: int = 0):
+    """ksg_merge_records over a uint8[world, rec_bytes] array of shard records.
+    -> (rc, node, max_score, tie_count, rng_state)."""
+    lib = abi.load_library()
+    rec = np.ascontiguousarray(records, dtype=np.uint8)
+    world, rec_bytes = rec.shape
+    node = C.c_int32(-1)
+    m = C.c_int64(0)
+    k = C.c_uint64(0)
+    st = C.c_uint64(rng_state or 0)
+    rc = lib.ksg_merge_records(abi.ptr(rec), rec_bytes, world, int(n_nodes), 1 if empty_priorities else 0,
+                               C.byref(st) if rng_state is not None else None, int(tie_index), C.byref(node),
+                               C.byref(m), C.byref(k))
+    if rc not in (abi.KSG_OK, abi.KSG_NOFIT, abi.KSG_ERR_NOPEER):
+        raise KsgError(rc, "ksg_merge_records")
+    return rc, node.value, m.value, k.value, (st.value if rng_state is not None else None)
+
+
+def make_shard_record(fails: np.ndarray, scores: np.ndarray, lo: int, word_lo: int, nwords_max: int,
+                      error: bool = False) -> np.ndarray:
+    """Pack one shard's record (header + tie bitmap) from its per-node fail codes and scores
+    (the layout ksg_scan_kernel writes; used by callers that evaluate shards themselves)."""
+    out = np.zeros(REC_HDR_BYTES + 8 * nwords_max, np.uint8)
+    hdr = abi.KsgShardRecord.from_buffer(out)
+    fit = fails == 0
+    hdr.error = 1 if error else 0
+    if fit.any() and not error:
+        m = int(scores[fit].max())
+        ties = np.nonzero(fit & (scores == m))[0] + lo
+        hdr.max_score = m
+        hdr.tie_count = len(ties)
+        words = out[REC_HDR_BYTES:].view(np.uint64)
+        rel = ties - word_lo * 64
+        np.bitwise_or.at(words, rel // 64, (np.uint64(1) << (rel % 64).astype(np.uint64)))
+    else:
+        hdr.max_score = -(1 << 63)
+        hdr.tie_count = 0
+    return out

@@ -45,13 +45,17 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
         abi.load_library()
 
 
+STRUCTS = (("ksg_config", abi.KsgConfig), ("ksg_node", abi.KsgNode), ("ksg_pod", abi.KsgPod),
+           ("ksg_shard_record", abi.KsgShardRecord))
+
 _LAYOUT_C = r"""
 #include <stdio.h>
 #include <stddef.h>
 #include "kschedgpu.h"
 #define P(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
 int main(void) {
-  printf("ksg_config %zu\nksg_node %zu\nksg_pod %zu\n", sizeof(ksg_config), sizeof(ksg_node), sizeof(ksg_pod));
+  printf("ksg_config %zu\nksg_node %zu\nksg_pod %zu\nksg_shard_record %zu\n", sizeof(ksg_config),
+         sizeof(ksg_node), sizeof(ksg_pod), sizeof(ksg_shard_record));
   %FIELDS%
   return 0;
 }
@@ -60,7 +64,7 @@ int main(void) {
 
 def test_struct_layouts_match_header(tmp_path):
     fields = []
-    for T, cls in (("ksg_config", abi.KsgConfig), ("ksg_node", abi.KsgNode), ("ksg_pod", abi.KsgPod)):
+    for T, cls in STRUCTS:
         for name, _ in cls._fields_:
             fields.append(f"P({T}, {name})")
     src = tmp_path / "layout.c"
@@ -72,7 +76,8 @@ def test_struct_layouts_match_header(tmp_path):
     assert int(got["ksg_config"]) == C.sizeof(abi.KsgConfig)
     assert int(got["ksg_node"]) == C.sizeof(abi.KsgNode) == abi.NODE_DTYPE.itemsize
     assert int(got["ksg_pod"]) == C.sizeof(abi.KsgPod) == abi.POD_DTYPE.itemsize
-    for T, cls in (("ksg_config", abi.KsgConfig), ("ksg_node", abi.KsgNode), ("ksg_pod", abi.KsgPod)):
+    for T, cls in STRUCTS:
+        assert int(got[T]) == C.sizeof(cls), T
         for name, _ in cls._fields_:
             assert int(got[f"{T}.{name}"]) == getattr(cls, name).offset, (T, name)
     for name in abi.POD_DTYPE.names:
