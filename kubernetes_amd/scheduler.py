@@ -146,8 +146,14 @@ class GPUScheduler:
             self._mirror = {}
         pods = self.pod_lister.list(everything())
         want = {}
-        for p in pods:
-            want[p.key()] = p
+        for p in pods:  # unnamed / duplicate keys (fake listers) stay distinct pods
+            k = p.key()
+            if k in want:
+                j = 1
+                while f"{k}#{j}" in want:
+                    j += 1
+                k = f"{k}#{j}"
+            want[k] = p
         for k, (uid, host, pid) in list(self._mirror.items()):
             # a pod this scheduler assumed, now reported by the lister on the same host
             if pid is None and k in want and self.view.host_id(want[k].status.host) == host:
