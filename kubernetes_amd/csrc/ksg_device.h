@@ -56,6 +56,27 @@ __device__ __forceinline__ int64_t lr_calc(int64_t requested, int64_t capacity) 
   return go_div64((int64_t)(x * 10ULL), capacity);
 }
 
+// calculateScore for the window path, whose host guard (use_window) holds
+// 0 <= cap <= 2^49 and 0 <= requested < 2^50: q = 10u/cap (u = cap - requested)
+// through a per-node f64 reciprocal inv10 = 10.0/cap. |q - 10u/cap| <= ~2.2e-15,
+// so trunc(q) can differ from the exact floor only when q lies within that of
+// an integer; every q within 1e-9 of an integer takes the exact integer fix-up
+// (10u < 2^53, (q+1)*cap < 2^53: no overflow), so the result equals lr_calc.
+__device__ __forceinline__ int32_t lr_win(int64_t requested, int64_t cap, double inv10) {
+  if (requested > cap || cap == 0) return 0;  // priorities.go:29-35
+  const int64_t u = cap - requested;
+  const double q = (double)u * inv10;
+  int32_t qi = (int32_t)q;
+  const double fr = q - (double)qi;
+  if (fr < 1e-9 || fr > 1.0 - 1e-9) {
+    const uint64_t y = (uint64_t)u * 10ULL;
+    if ((uint64_t)(qi + 1) * (uint64_t)cap <= y) qi += 1;
+    else if ((uint64_t)qi * (uint64_t)cap > y) qi -= 1;
+  }
+  return qi;
+}
+__device__ __forceinline__ double lr_inv10(int64_t cap) { return cap > 0 ? 10.0 / (double)cap : 0.0; }
+
 // int(10 * (float32(num) / float32(den))) with IEEE f32 divide and multiply,
 // no contraction (spreading.go:79-83, 156-160).
 __device__ __forceinline__ int64_t frac10_f32(int64_t num, int64_t den) {
@@ -95,6 +116,86 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, uint32_t lane
     if (lane >= (uint32_t)off) v += o;
   }
   return v;
+}
+
+// ---- DPP wave scans (GFX9 row_shr + row_bcast; no LDS round trip) ----------
+// Inclusive prefix over the 64 lanes; lane 63 holds the wave total. Lanes whose
+// DPP source falls outside the row (or whose row is masked) receive `old`,
+// the identity of the operator.
+#define KSG_DPP(old, v, ctrl, rmask) __builtin_amdgcn_update_dpp((old), (v), (ctrl), (rmask), 0xf, false)
+
+__device__ __forceinline__ uint32_t dpp_scan_add(uint32_t v) {
+  int x = (int)v;
+  x += KSG_DPP(0, x, 0x111, 0xf);  // row_shr:1
+  x += KSG_DPP(0, x, 0x112, 0xf);  // row_shr:2
+  x += KSG_DPP(0, x, 0x114, 0xf);  // row_shr:4
+  x += KSG_DPP(0, x, 0x118, 0xf);  // row_shr:8
+  x += KSG_DPP(0, x, 0x142, 0xa);  // row_bcast:15 -> rows 1, 3
+  x += KSG_DPP(0, x, 0x143, 0xc);  // row_bcast:31 -> rows 2, 3
+  return (uint32_t)x;
+}
+
+__device__ __forceinline__ int32_t dpp_scan_max(int32_t x) {
+  const int lo = (int)0x80000000;
+  x = max(x, KSG_DPP(lo, x, 0x111, 0xf));
+  x = max(x, KSG_DPP(lo, x, 0x112, 0xf));
+  x = max(x, KSG_DPP(lo, x, 0x114, 0xf));
+  x = max(x, KSG_DPP(lo, x, 0x118, 0xf));
+  x = max(x, KSG_DPP(lo, x, 0x142, 0xa));
+  x = max(x, KSG_DPP(lo, x, 0x143, 0xc));
+  return x;
+}
+
+__device__ __forceinline__ uint32_t dpp_scan_or(uint32_t v) {
+  int x = (int)v;
+  x |= KSG_DPP(0, x, 0x111, 0xf);
+  x |= KSG_DPP(0, x, 0x112, 0xf);
+  x |= KSG_DPP(0, x, 0x114, 0xf);
+  x |= KSG_DPP(0, x, 0x118, 0xf);
+  x |= KSG_DPP(0, x, 0x142, 0xa);
+  x |= KSG_DPP(0, x, 0x143, 0xc);
+  return (uint32_t)x;
+}
+
+// wave-uniform results of the scans
+__device__ __forceinline__ uint32_t wave_or_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)dpp_scan_or(v), 63);
+}
+__device__ __forceinline__ uint32_t wave_total_add(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)dpp_scan_add(v), 63);
+}
+__device__ __forceinline__ int32_t wave_total_max(int32_t v) {
+  return __builtin_amdgcn_readlane(dpp_scan_max(v), 63);
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane)) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane) << 32);
+}
+
+// register copy the compiler cannot see through: the s_waitcnt for a pending
+// load into `x` lands here, not at a later use
+__device__ __forceinline__ uint32_t opaque_v(uint32_t x) {
+  uint32_t y;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
+  return y;
+}
+__device__ __forceinline__ uint64_t opaque_v64(uint64_t x) {
+  return ((uint64_t)opaque_v((uint32_t)(x >> 32)) << 32) | opaque_v((uint32_t)x);
+}
+
+// r % k for r < 2^64, 0 < k < 2^32, without the 64-bit division routine:
+// hi % k in 32 bits, then (rem * 2^32 + lo) / k through one f64 divide whose
+// quotient is off by at most one (x < k * 2^32 <= 2^64, 53-bit mantissa), fixed
+// with exact integer arithmetic.
+__device__ __forceinline__ uint32_t umod64_32(uint64_t r, uint32_t k) {
+  const uint32_t hi = (uint32_t)(r >> 32), lo = (uint32_t)r;
+  const uint64_t x = ((uint64_t)(hi % k) << 32) | lo;
+  uint64_t q = (uint64_t)((double)x / (double)k);
+  if (q > 0) q -= 1;  // never overshoot: x - q*k >= 0
+  uint64_t rem = x - q * (uint64_t)k;
+  while (rem >= k) rem -= k;  // at most 3 steps
+  return (uint32_t)rem;
 }
 
 // position of the m-th (0-based) set bit of w, ascending

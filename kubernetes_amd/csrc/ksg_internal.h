@@ -33,6 +33,9 @@
 // combined scores are kept in int32 on the device; the host rejects weight
 // sets whose |score| could reach this bound
 #define KSG_SCORE_BOUND (1LL << 30)
+// largest capacity / requested total the window path accepts (lr_win's bound,
+// ksg_device.h)
+#define KSG_WIN_LR_BOUND (1LL << 49)
 
 struct KsgDev {
   // cluster geometry

@@ -36,10 +36,10 @@ hipError_t ksg_launch_scan(int R, bool anti, const KsgDev& d, const ksg_pod* pod
                            int64_t* score_out, uint8_t* record, int32_t* dpart,
                            const int32_t* dglobal, hipStream_t st);
 hipError_t ksg_launch_win_eval(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids, uint32_t n,
-                               KsgWinSum* sums, uint64_t* t0words, hipStream_t st);
-hipError_t ksg_launch_win_resolve(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids, uint32_t n,
-                                  const KsgWinSum* sums, const uint64_t* t0words, uint64_t* rng, int32_t* out,
-                                  uint32_t* resolved, hipStream_t st);
+                               KsgWinSum* sums, uint64_t* wbits, int32_t* wmax, hipStream_t st);
+hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t n, const KsgWinSum* sums, const uint64_t* wbits,
+                                  const int32_t* wmax, uint64_t* rng, int32_t* out, uint32_t* stat,
+                                  hipStream_t st);
 uint32_t ksg_win_max_window(const KsgDev& d);
 hipError_t ksg_launch_decide(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids,
                              const uint8_t* records, uint32_t rec_bytes, uint32_t world,
@@ -120,13 +120,14 @@ struct ksg_ctx {
   // window (speculative) path
   uint32_t window = 128;        // 0 = exact one-pod-at-a-time kernel
   KsgWinSum* d_winsum = nullptr;
-  uint64_t* d_t0 = nullptr;
-  size_t win_cap = 0, t0_cap = 0;
+  uint64_t* d_t0 = nullptr;     // [W][nwords] per-word best-score node bitmaps (phase A)
+  int32_t* d_wmax = nullptr;    // [W][nwords] per-word best scores (phase A)
+  size_t win_cap = 0, t0_cap = 0, wmax_cap = 0;
   uint32_t* d_resolved = nullptr;  // {resolved, stop reason}
   uint32_t last_stats[4] = {0, 0, 0, 0};  // windows, stops (service scalar), stops (ties exhausted)
   hipEvent_t kev[4] = {nullptr, nullptr, nullptr, nullptr};
   double last_kms[3] = {0, 0, 0};  // phase A ms, phase B ms, launches (window path)
-  int64_t max_cap = 0;
+  int64_t max_cap = 0, min_cap = 0;
 
   // begin/commit
   bool pending = false;
@@ -376,13 +377,17 @@ int scan_exchange(ksg_ctx* c, const ksg_pod* dpod, const uint32_t* dids, int mod
 // The window path needs monotone scores under commits (see ksg_window.hip):
 // no ServiceAntiAffinity, and int64 totals far from wrapping.
 bool use_window(ksg_ctx* c, const ksg_pod* pods, uint32_t n) {
-  if (c->window == 0 || anti_on(c) || c->nwords > 8 * 64 || ksg_win_max_window(c->dev) == 0) return false;
+  if (c->window == 0 || anti_on(c) || c->nwords > 8 * 64 || ksg_win_max_window(c->dev) < 8) return false;
   // monotonicity under commits needs non-negative pod-dependent weights
   if (c->cfg.w_least_requested < 0 || c->cfg.w_service_spreading < 0) return false;
-  const int64_t lim = 1LL << 58;
-  if (c->max_cap > lim) return false;
+  // lr_win (ksg_device.h) is exact for 0 <= capacity, requested totals <= 2^49
+  const int64_t lim = KSG_WIN_LR_BOUND;
+  if (c->max_cap > lim || c->min_cap < 0) return false;
   int64_t mu = 0;
-  for (uint32_t i = 0; i < c->N; ++i) mu = std::max<int64_t>(mu, std::max<int64_t>(std::llabs(c->used_c[i]), std::llabs(c->used_m[i])));
+  for (uint32_t i = 0; i < c->N; ++i) {
+    if (c->used_c[i] < 0 || c->used_m[i] < 0) return false;
+    mu = std::max<int64_t>(mu, std::max<int64_t>(c->used_c[i], c->used_m[i]));
+  }
   int64_t sum = 0;
   for (uint32_t i = 0; i < n; ++i) {
     if (pods[i].milli_cpu < 0 || pods[i].memory < 0) return false;
@@ -515,17 +520,18 @@ int ksg_create_sharded(const ksg_config* cfg, int device, int rank, int world, c
 int ksg_destroy(ksg_ctx* c) {
   if (!c) return KSG_OK;
   if (c->dev.dbgbuf) {  // debug stamps (KSG_DEBUG & 8): cycles/64 per resolver section
-    int32_t h[8];
+    int32_t h[16];
     (void)hipMemcpy(h, c->dev.dbgbuf, sizeof h, hipMemcpyDeviceToHost);
-    fprintf(stderr, "ksg stamps (x64 cycles): prefetch-issue %d retire %d head %d recheck %d select %d commit %d loop-end %d candidates %d\n",
-            h[0], h[1], h[6], h[2] - h[6], h[3], h[4], h[5], h[7]);
+    fprintf(stderr, "ksg stamps (x64 cycles): ring-wait %d head %d recheck[retire %d list %d check %d collect %d] "
+            "select %d commit %d loop-end %d | candidates %d head-retires %d recheck-retires %d cache-misses %d\n",
+            h[0], h[1], h[6], h[8], h[11], h[2], h[3], h[4], h[5], h[7], h[9], h[10], h[12]);
   }
   (void)hipSetDevice(c->device);
   if (c->st) (void)hipStreamSynchronize(c->st);
   free_cluster(c);
   void* scratch[] = {c->d_pods, c->d_ids, c->d_fail, c->d_score, c->d_rec_send, c->d_rec_recv, c->d_dpart,
                      c->d_dglobal, c->d_out, c->d_rng, c->d_summary, c->d_patch, c->d_shard_wlo,
-                     c->d_winsum, c->d_t0, c->d_resolved};
+                     c->d_winsum, c->d_t0, c->d_wmax, c->d_resolved};
   for (void* p : scratch)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -621,10 +627,12 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   // upload nodes + static tables
   std::vector<int64_t> hc(NN, 0), hm(NN, 0);
   c->max_cap = 0;
+  c->min_cap = 0;
   for (uint32_t i = 0; i < n_nodes; ++i) {
     hc[i] = nodes[i].cap_milli_cpu;
     hm[i] = nodes[i].cap_memory;
     c->max_cap = std::max<int64_t>(c->max_cap, std::max<int64_t>(std::llabs(hc[i]), std::llabs(hm[i])));
+    c->min_cap = std::min<int64_t>(c->min_cap, std::min<int64_t>(hc[i], hm[i]));
   }
   HIPCHK(c, hipMemcpyAsync(cap_c, hc.data(), NN * 8, hipMemcpyHostToDevice, c->st));
   HIPCHK(c, hipMemcpyAsync(cap_m, hm.data(), NN * 8, hipMemcpyHostToDevice, c->st));
@@ -694,8 +702,8 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   d.has_static_score = (c->cfg.w_equal != 0 || any_pref) ? 1 : 0;
   d.dbg = getenv("KSG_DEBUG") ? atoi(getenv("KSG_DEBUG")) : 0;
   if (d.dbg & 8) {
-    (void)hipMalloc(&d.dbgbuf, 64);
-    (void)hipMemset(d.dbgbuf, 0, 64);
+    (void)hipMalloc(&d.dbgbuf, 128);
+    (void)hipMemset(d.dbgbuf, 0, 128);
   }
   d.has_static_fit = ((c->cfg.predicates & KSG_PRED_LABELSPRESENCE) && c->cfg.n_presence > 0) ? 1 : 0;
   d.cap_cpu = cap_c;
@@ -877,6 +885,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     const uint32_t W = std::min(c->window, ksg_win_max_window(c->dev));
     if ((rc = grow(c, (void**)&c->d_winsum, &c->win_cap, W, sizeof(KsgWinSum)))) return rc;
     if ((rc = grow(c, (void**)&c->d_t0, &c->t0_cap, (size_t)W * c->nwords, sizeof(uint64_t)))) return rc;
+    if ((rc = grow(c, (void**)&c->d_wmax, &c->wmax_cap, (size_t)W * c->nwords, sizeof(int32_t)))) return rc;
     uint32_t pos = 0;
     if (!c->kev[0])
       for (auto& e : c->kev) HIPCHK(c, hipEventCreate(&e));
@@ -885,10 +894,11 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       const uint32_t w = std::min(W, n - pos);
       // HIP events on this stream around each kernel (per-kernel device time)
       HIPCHK(c, hipEventRecord(c->kev[0], c->st));
-      HIPCHK(c, ksg_launch_win_eval(c->dev, c->d_pods + pos, c->d_ids, w, c->d_winsum, c->d_t0, c->st));
+      HIPCHK(c, ksg_launch_win_eval(c->dev, c->d_pods + pos, c->d_ids, w, c->d_winsum, c->d_t0, c->d_wmax,
+                                    c->st));
       HIPCHK(c, hipEventRecord(c->kev[1], c->st));
-      HIPCHK(c, ksg_launch_win_resolve(c->dev, c->d_pods + pos, c->d_ids, w, c->d_winsum, c->d_t0, c->d_rng,
-                                       c->d_out + pos, c->d_resolved, c->st));
+      HIPCHK(c, ksg_launch_win_resolve(c->dev, w, c->d_winsum, c->d_t0, c->d_wmax, c->d_rng, c->d_out + pos,
+                                       c->d_resolved, c->st));
       HIPCHK(c, hipEventRecord(c->kev[2], c->st));
       uint32_t st2[2] = {0, 0};
       HIPCHK(c, hipMemcpyAsync(st2, c->d_resolved, 8, hipMemcpyDeviceToHost, c->st));
@@ -911,6 +921,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
         ++c->last_stats[3];
         continue;
       }
+      if (st2[1] == 9) return fail(c, KSG_ERR_STATE, "window resolver: ring wait timed out at pod %u", pos + res);
       if (res == 0 || res > w) return fail(c, KSG_ERR_STATE, "window resolved %u of %u pods", res, w);
       pos += res;
       if (st2[1] == 1) ++c->last_stats[1];

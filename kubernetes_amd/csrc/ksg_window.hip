@@ -5,36 +5,51 @@
 // that exact sequential semantics while moving almost all of the work off the
 // sequential chain:
 //
-//  phase A (ksg_win_eval_kernel, one 256-thread workgroup per pod, all CUs):
-//    every pod of a window is filtered and scored against ONE snapshot of the
-//    node state; per pod it stores the best score M0, the tie count k0, the tie
-//    bitmap T0 (bit n = node n scores M0) and two spreading scalars.
+//  phase A (ksg_win_score_kernel, all CUs, node-major): one wave owns one
+//    64-node word of the shard (lane = node) and scores a group of KSG_PG
+//    window pods against ONE snapshot of the node state. The pod-side work of
+//    the predicates (nodeSelector pairs, host ports, GCE PDs, ServiceAffinity,
+//    LabelsPresence, HostName) collapses into one 64-bit fit word per (pod,
+//    word), built by lane j for pod j; the node state (capacity, requested
+//    totals) is loaded once per wave and reused for every pod of the group.
+//    Per (pod, word) it stores the word's best score and the bitmap of nodes at
+//    that score; the wave that owns word 0 also writes each pod's 192-byte
+//    resolver record (KsgWinSum).
 //  phase B (ksg_win_resolve_kernel, one wave): walks the window in order and
-//    reproduces the sequential result from the snapshot. For a "clean" pod —
-//    one whose service scalars (ServiceSpreading maxCount, ServiceAffinity
-//    peer) no earlier pod of the window changed — a commit can only make the
-//    committed node WORSE (requested totals grow: LeastRequested falls and
-//    PodFitsResources can flip to false; host ports / PDs only get added;
-//    service counts grow under a fixed maxCount), and every other node is
-//    untouched. So the sequential max is still M0 unless all of T0 was made
-//    worse, and the sequential tie set is T0 minus the nodes committed earlier
-//    in the window (set C) whose re-evaluated score dropped. Phase B re-scores
-//    only T0 ∩ C, draws the same Int63 the reference draws, selects the ix-th
-//    tie in descending name order, commits, and continues. A pod that is not
-//    clean, or whose whole T0 dropped, ends the window; the host starts the next
-//    window (new snapshot) at that pod. Results are bit-identical to the
-//    one-pod-at-a-time path (tests/test_gpu_parity.py compares both).
+//    reproduces the sequential result. M0 = max over the words of the best
+//    scores, T0 = nodes at M0. For a "clean" pod — one whose service scalars
+//    (ServiceSpreading maxCount, ServiceAffinity peer) no earlier pod of the
+//    window changed — a commit can only make the committed node WORSE
+//    (requested totals grow: LeastRequested falls and PodFitsResources can flip
+//    to false; host ports / PDs only get added; service counts grow under a
+//    fixed maxCount), and every other node is untouched. So the sequential max
+//    is still M0 unless all of T0 was made worse, and the sequential tie set is
+//    T0 minus the nodes committed earlier in the window (set C) whose
+//    re-evaluated score dropped. Phase B re-scores only T0 ∩ C from LDS copies
+//    of the committed nodes ("slots"), draws the Int63 the reference draws
+//    (generic_scheduler.go:94), selects the ix-th tie in descending name order,
+//    commits into the slot, and continues. A pod that is not clean, or whose
+//    whole T0 dropped, ends the window; the host starts the next window (new
+//    snapshot) at that pod. Results are bit-identical to the one-pod-at-a-time
+//    path (tests/test_gpu_parity.py compares both with the oracle).
+//
+// Latency is everything in phase B (one wave, one pod after another): the
+// committed-node mask C and the pod's T0 live in registers (lane l owns words
+// [l*P, l*P+P)), prefix counts are DPP row scans, candidates are compacted
+// through LDS so one pass of 64 lanes re-checks them, and the snapshot loads
+// of a newly committed node are retired lazily (only when a later pod needs
+// that node, else at the next commit).
 //
 // ServiceAntiAffinity changes a service-wide scalar on every commit and is
 // served by the exact per-pod kernel instead (ksg_kernels.hip).
 #include "ksg_device.h"
 
-#define KSG_WIN_NT 256
-#define KSG_WIN_NWAVE (KSG_WIN_NT / 64)
+#include <algorithm>
+
+#define KSG_SC_NT 256  // phase A: 4 waves, one 64-node word each
+#define KSG_PG 8       // phase A: pods per wave
 
 // dword offsets inside KsgWinSum (lane j of the resolver holds dword j)
-#define WS_M0 0
-#define WS_K0 1
 #define WS_ERR 2
 #define WS_SVC 3
 #define WS_HOST 4
@@ -48,280 +63,542 @@
 #define WS_NSS 17
 #define WS_IDS 19
 
-// phase A: one workgroup per pod of the window. The node state is read-only
-// while phase A runs, so every load is a plain (cacheable) load.
-__global__ __launch_bounds__(KSG_WIN_NT) void ksg_win_eval_kernel(KsgDev d, const ksg_pod* __restrict__ pods,
-                                                                 const uint32_t* __restrict__ ids,
+// ---------------------------------------------------------------------------
+// phase A
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, const ksg_pod* __restrict__ pods,
+                                                                 const uint32_t* __restrict__ ids, uint32_t n_pods,
                                                                  KsgWinSum* __restrict__ sums,
-                                                                 uint64_t* __restrict__ t0words) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  int32_t* s_sc = reinterpret_cast<int32_t*>(smem);  // one score per node of the shard
-  __shared__ int32_t s_red[KSG_WIN_NWAVE];
-  __shared__ uint32_t s_cnt[KSG_WIN_NWAVE];
+                                                                 uint64_t* __restrict__ wbits,
+                                                                 int32_t* __restrict__ wmax) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (KSG_SC_NT / 64) + (threadIdx.x >> 6));
+  const uint32_t p0 = blockIdx.y * KSG_PG;
+  if (w >= d.nwords || p0 >= n_pods) return;  // wave-uniform
+  const uint32_t np = min((uint32_t)KSG_PG, n_pods - p0);
+  const uint32_t gw = d.wlo + w;  // global word
+  const uint32_t n = gw * 64 + lane;
+  const bool valid = n < d.hi;
+  const uint32_t P = d.preds;
 
-  const uint32_t i = blockIdx.x;
-  const uint32_t tid = threadIdx.x;
-  const uint32_t lane = tid & 63;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint64_t bit = 1ULL << lane;
-  const ksg_pod& p = pods[i];
+  // ---- node state, once per wave (read-only while phase A runs)
+  int64_t capc = 0, capm = 0, usedc = 0, usedm = 0;
+  int32_t sst = 0;
+  if (valid) {
+    capc = d.cap_cpu[n];
+    capm = d.cap_mem[n];
+    usedc = d.used_cpu[n];
+    usedm = d.used_mem[n];
+    if (d.has_static_score) sst = d.static_score[n];
+  }
+  const double inv_c = lr_inv10(capc), inv_m = lr_inv10(capm);
+
+  // ---- lane j < np: pod p0+j's context and its fit word for this node word
+  uint64_t fm = 0;
+  int64_t rc = 0, rm = 0;
+  int32_t svc = -1, smax = 0, zr = 0;
   PodCtx c;
-  pod_resolve<false>(d, p, ids, c);
-  KsgWinSum* S = sums + i;
-  uint64_t* T0 = t0words + (size_t)i * d.nwords;
-  int32_t M = KSG_S32_NONE;
-  uint32_t k = 0;
-  if (!c.error) {
-    const bool need_cnt = d.w_spread != 0 && c.svc >= 0;
-    const uint32_t span = d.nwords * 64;
-    int32_t m = KSG_S32_NONE;
-    for (uint32_t off = tid; off < span; off += KSG_WIN_NT) {
-      const uint32_t n = d.lo + off;
-      const uint32_t wi = (d.lo >> 6) + (off >> 6);
-      int32_t sc = KSG_S32_NONE;
-      if (n < d.hi) {
-        const int64_t capc = d.cap_cpu[n], capm = d.cap_mem[n];
-        const int64_t usedc = (d.dbg & 2) ? ld_mut(d.used_cpu + n) : d.used_cpu[n];
-        const int64_t usedm = (d.dbg & 2) ? ld_mut(d.used_mem + n) : d.used_mem[n];
-        const int32_t cnt = need_cnt ? d.svc_cnt[(size_t)c.svc * d.n_nodes + n] : 0;
-        if (node_fail<false>(d, c, n, wi, bit, capc, capm, usedc, usedm) == KSG_FAIL_NONE)
-          sc = (int32_t)node_score(d, c, n, capc, capm, usedc, usedm, cnt);
+  if (lane < np) {
+    const ksg_pod& p = pods[p0 + lane];
+    pod_resolve<false>(d, p, ids, c);
+    uint64_t m = gw * 64 + 64 <= d.hi ? ~0ULL : ((1ULL << (d.hi - gw * 64)) - 1);  // nodes of the shard
+    if (d.has_static_fit) m &= d.static_fit[gw];  // LabelsPresence (predicates.go:215-229)
+    if ((P & KSG_PRED_HOSTNAME) && c.host != -1) {  // PodFitsHost (predicates.go:181-186)
+      m &= (c.host >= 0 && (uint32_t)c.host >> 6 == gw) ? (1ULL << (c.host & 63)) : 0ULL;
+    }
+    if (P & KSG_PRED_MATCHNODESELECTOR)  // PodMatchesNodeLabels (predicates.go:161-167)
+      for (uint32_t t = 0; t < c.n_sel; ++t) m &= d.pairmap[(size_t)c.sel[t] * d.nw + gw];
+    if (P & KSG_PRED_NODISKCONFLICT)  // NoDiskConflict (predicates.go:73-83)
+      for (uint32_t t = 0; t < c.n_pds; ++t) m &= ~d.keymap[(size_t)c.pds[t] * d.nw + gw];
+    if (P & KSG_PRED_PODFITSPORTS)  // PodFitsPorts (predicates.go:326-338)
+      for (uint32_t t = 0; t < c.n_ports; ++t) m &= ~d.keymap[(size_t)c.ports[t] * d.nw + gw];
+    if (P & KSG_PRED_SERVICEAFFINITY) {  // CheckServiceAffinity (predicates.go:257-324)
+#pragma unroll
+      for (uint32_t j = 0; j < KSG_MAX_AFF; ++j)
+        if (j < d.n_aff && c.req_aff[j] >= 0) m &= d.pairmap[(size_t)c.req_aff[j] * d.nw + gw];
+    }
+    fm = m;
+    rc = c.req_cpu;
+    rm = c.req_mem;
+    zr = c.zero_req;
+    svc = c.svc;
+    smax = c.spread_max;
+  }
+
+  // ---- per-pod service counts of this lane's node, all issued up front
+  const bool need_cnt = d.w_spread != 0;
+  int32_t cnt[KSG_PG];
+#pragma unroll
+  for (int j = 0; j < KSG_PG; ++j) {
+    const int32_t s = __builtin_amdgcn_readlane(svc, j);
+    cnt[j] = (need_cnt && valid && (uint32_t)j < np && s >= 0) ? d.svc_cnt[(size_t)s * d.n_nodes + n] : 0;
+  }
+
+  // ---- score every pod of the group on this word
+  int32_t my_max = KSG_S32_NONE;
+  uint64_t my_bits = 0;
+  const bool res_on = (P & KSG_PRED_PODFITSRESOURCES) != 0;
+#pragma unroll
+  for (int j = 0; j < KSG_PG; ++j) {
+    if ((uint32_t)j < np) {
+      const uint64_t fmj = readlane64(fm, j);
+      const int64_t rcj = (int64_t)readlane64((uint64_t)rc, j);
+      const int64_t rmj = (int64_t)readlane64((uint64_t)rm, j);
+      bool fit = (fmj >> lane) & 1ULL;
+      if (res_on && !__builtin_amdgcn_readlane(zr, j)) {
+        // CheckPodsExceedingCapacity over existing+pod in closed form (predicates.go:104-145)
+        const bool fc = capc == 0 || (int64_t)((uint64_t)capc - (uint64_t)usedc) >= rcj;
+        const bool fmm = capm == 0 || (int64_t)((uint64_t)capm - (uint64_t)usedm) >= rmj;
+        fit = fit && fc && fmm;
       }
-      s_sc[off] = sc;
-      m = sc > m ? sc : m;
+      int32_t sc = KSG_S32_NONE;
+      if (fit) {
+        if (d.equal_fallback) {
+          sc = 1;  // EqualPriority (generic_scheduler.go:141-143,180-195)
+        } else {
+          int64_t s = sst;
+          if (d.w_lr) {  // calculateOccupancy (priorities.go:43-76)
+            const int64_t tc = (int64_t)((uint64_t)usedc + (uint64_t)rcj);
+            const int64_t tm = (int64_t)((uint64_t)usedm + (uint64_t)rmj);
+            s += (int64_t)d.w_lr * ((lr_win(tc, capc, inv_c) + lr_win(tm, capm, inv_m)) >> 1);
+          }
+          if (d.w_spread) {  // CalculateSpreadPriority (spreading.go:72-86)
+            const int32_t mx = __builtin_amdgcn_readlane(smax, j);
+            const int64_t ss = mx > 0 ? frac10_f32((int64_t)mx - cnt[j], mx) : 10;
+            s += (int64_t)d.w_spread * ss;
+          }
+          sc = (int32_t)s;
+        }
+      }
+      int32_t m = wave_total_max(sc);
+      if (d.empty_priorities) m = KSG_S32_NONE;  // prioritizeNodes returns nothing
+      const uint64_t b = __ballot(m != KSG_S32_NONE && sc == m);
+      if (lane == (uint32_t)j) {
+        my_max = m;
+        my_bits = b;
+      }
     }
-    m = wave_max_i32(m);
-    if (lane == 0) s_red[wave] = m;
-    __syncthreads();
-    M = s_red[0];
+  }
+  if (lane < np) {
+    wmax[(size_t)(p0 + lane) * d.nwords + w] = my_max;
+    wbits[(size_t)(p0 + lane) * d.nwords + w] = my_bits;
+  }
+
+  // ---- the resolver's record of each pod (one wave per pod group)
+  if (w == 0) {
+    if (lane < np) {
+      const ksg_pod& p = pods[p0 + lane];
+      KsgWinSum* S = sums + p0 + lane;
+      S->m0 = 0;
+      S->k0 = 0;
+      S->error = c.error;
+      S->service = c.svc;
+      S->host = c.host;
+      S->spread_max = c.spread_max;
+      S->svc_total = c.svc_total;
+      S->n_inline = p.n_ports + p.n_pds + p.n_sel + p.n_svcs;
+      S->milli_cpu = c.req_cpu;
+      S->memory = c.req_mem;
 #pragma unroll
-    for (int w = 1; w < KSG_WIN_NWAVE; ++w) M = s_red[w] > M ? s_red[w] : M;
-    if (d.empty_priorities) M = KSG_S32_NONE;
-    uint32_t cntk = 0;
-    for (uint32_t off = tid; off < span; off += KSG_WIN_NT) {
-      const uint64_t b = __ballot(M != KSG_S32_NONE && s_sc[off] == M);
-      if (lane == 0) T0[off >> 6] = b;
-      cntk += __popcll(b);
+      for (int j = 0; j < KSG_MAX_AFF; ++j) S->req_aff[j] = c.req_aff[j];
+      S->n_ports = (uint16_t)p.n_ports;
+      S->n_pds = (uint16_t)p.n_pds;
+      S->n_sel = (uint16_t)p.n_sel;
+      S->n_svcs = (uint16_t)p.n_svcs;
     }
-    if (lane == 0) s_cnt[wave] = cntk;
-    __syncthreads();
-#pragma unroll
-    for (int w = 0; w < KSG_WIN_NWAVE; ++w) k += s_cnt[w];
-  }
-  // the record phase B streams for this pod
-  const uint32_t ninl = p.n_ports + p.n_pds + p.n_sel + p.n_svcs;
-  if (tid < KSG_WIN_INLINE && tid < ninl) {
-    uint32_t t = tid, v;
-    if (t < p.n_ports) v = ids[p.ports_off + t];
-    else if ((t -= p.n_ports) < p.n_pds) v = ids[p.pds_off + t];
-    else if ((t -= p.n_pds) < p.n_sel) v = ids[p.sel_off + t];
-    else v = ids[p.svcs_off + (t - p.n_sel)];
-    S->ids[tid] = v;
-  }
-  if (tid == 0) {
-    S->m0 = M;
-    S->k0 = M == KSG_S32_NONE ? 0 : k;
-    S->error = c.error;
-    S->service = c.svc;
-    S->host = c.host;
-    S->spread_max = c.spread_max;
-    S->svc_total = c.svc_total;
-    S->n_inline = ninl;
-    S->milli_cpu = c.req_cpu;
-    S->memory = c.req_mem;
-#pragma unroll
-    for (int j = 0; j < KSG_MAX_AFF; ++j) S->req_aff[j] = c.req_aff[j];
-    S->n_ports = (uint16_t)p.n_ports;
-    S->n_pds = (uint16_t)p.n_pds;
-    S->n_sel = (uint16_t)p.n_sel;
-    S->n_svcs = (uint16_t)p.n_svcs;
+    for (uint32_t j = 0; j < np; ++j) {
+      const ksg_pod& p = pods[p0 + j];
+      const uint32_t ninl = p.n_ports + p.n_pds + p.n_sel + p.n_svcs;
+      if (lane < KSG_WIN_INLINE && lane < ninl) {
+        uint32_t t = lane, v;
+        if (t < p.n_ports) v = ids[p.ports_off + t];
+        else if ((t -= p.n_ports) < p.n_pds) v = ids[p.pds_off + t];
+        else if ((t -= p.n_pds) < p.n_sel) v = ids[p.sel_off + t];
+        else v = ids[p.svcs_off + (t - p.n_sel)];
+        sums[p0 + j].ids[lane] = v;
+      }
+    }
   }
 }
 
-// list entries straight from the record register (readlane: uniform index;
-// v_readlane ignores EXEC, so it is safe inside divergent code)
-struct RecLists {
-  uint32_t rec, o_pd, o_sel;
-  __device__ __forceinline__ uint32_t port(uint32_t i) const { return __builtin_amdgcn_readlane(rec, WS_IDS + i); }
-  __device__ __forceinline__ uint32_t pd(uint32_t i) const { return __builtin_amdgcn_readlane(rec, WS_IDS + o_pd + i); }
-  __device__ __forceinline__ uint32_t sel(uint32_t i) const { return __builtin_amdgcn_readlane(rec, WS_IDS + o_sel + i); }
-};
-
-// Per-window cache of a node committed in the window (set C). The node state in
-// HBM stays a pristine snapshot while the window resolves; the window's deltas
-// live here and are written back once, at the end of the window.
+// ---------------------------------------------------------------------------
+// phase B
+// ---------------------------------------------------------------------------
+// One workgroup. Wave 0 is the RESOLVER: the sequential chain, LDS and ALU
+// only. Waves 1..KSG_RES_NPW are PRODUCERS: pod j of the window is staged by
+// producer (j mod NPW) into ring entry j mod KSG_RING — its record, its T0
+// bitmap (nodes at the snapshot max M0, from phase A's per-word maxima), k0 =
+// |T0|, its tie-break draw r (the splitmix64 output at the pod's draw index,
+// which is the number of earlier window pods that draw: those that neither
+// error nor find no fit) and r mod (k0 - d) for d = 0..63 dropped ties. The
+// pod staging latency, the RNG and the modulo are thus off the resolver's
+// chain. At kernel start the producers also pull the shard's node state
+// (capacity, requested totals) into this XCD's L2, so the resolver's one
+// snapshot load per newly committed node is an L2 hit.
+//
+// Per-window cache of the nodes committed in the window (set C): structure of
+// arrays in LDS indexed by slot (order of first commit). The node state in HBM
+// stays a pristine snapshot while the window resolves; the window's deltas live
+// here and are written back once, at the end of the window.
+#define KSG_RES_NT 512
+#define KSG_RES_NPW (KSG_RES_NT / 64 - 1)
+#define KSG_RING 16
 #define KSG_SLOT_KEYS 8
 #define KSG_SLOT_SVCS 12
-struct WinSlot {
-  int64_t cap_c, cap_m, snap_c, snap_m;  // snapshot capacity / requested totals
-  int64_t dc, dm;                        // requested added by the window
-  uint32_t node, nk, ns, pad;
-  uint32_t keys[KSG_SLOT_KEYS];          // conflict keys added by the window
-  uint32_t svcs[KSG_SLOT_SVCS];          // one entry per committed pod x service
-  int32_t scnt[KSG_SLOT_SVCS];           // svc_cnt[svcs[a]][node] at the snapshot
+
+struct alignas(16) I64x2 {
+  int64_t c, m;
+};
+struct alignas(16) F64x2 {
+  double c, m;
+};
+struct alignas(16) SlotMeta {
+  uint32_t node;    // shard offset of the node
+  uint16_t nk, ns;  // conflict keys / service entries added by the window
+  uint32_t smask;   // OR of 1 << (service & 31) over the service entries
+  uint32_t pad;
+};
+struct alignas(16) RingHdr {
+  int32_t m0;
+  uint32_t k0;
+  uint64_t r;         // Int63 draw of the pod
+  uint32_t ready;     // pod index + 1 once the entry is complete
+  uint32_t drawable;
+  uint32_t pad[2];
+};
+struct alignas(16) WinCtl {
+  uint32_t consumed;    // pods the resolver is done with (ring entries free)
+  uint32_t stop;        // the window ended early: producers exit
+  uint32_t draw_next;   // next pod allowed to take a draw index
+  uint32_t draw_count;  // draws of pods [0, draw_next)
+  uint32_t cache_n;     // (unused)
+  uint32_t pad[3];
 };
 
-__host__ __device__ constexpr uint32_t win_even(uint32_t x) { return (x + 1) & ~1u; }
-__host__ __device__ constexpr size_t win_lds_fixed(uint32_t P, uint32_t nflag, uint32_t nshard) {
-  return (size_t)P * 64 * 8 + (size_t)win_even(nflag) * 4 * 2 + (((size_t)nshard * 2 + 15) & ~(size_t)15);
+// byte offsets of the resolver's dynamic LDS arrays (host and device agree)
+struct WinLdsOff {
+  uint32_t ctl, r_hdr, r_t0, r_rec, r_mod;  // ring
+  uint32_t cap, snap, dlt, inv, meta, keys, svcs, scnt;  // slots
+  uint32_t peer, list, out, flag, peerset, slot_of, drop;
+  uint32_t total;
+};
+
+__host__ __device__ constexpr uint32_t win_al16(size_t x) { return (uint32_t)((x + 15) & ~(size_t)15); }
+
+__host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag, uint32_t nshard, uint32_t W) {
+  WinLdsOff o;
+  uint32_t at = 0;
+  o.ctl = at;     at += win_al16(sizeof(WinCtl));
+  o.r_hdr = at;   at += win_al16((size_t)KSG_RING * sizeof(RingHdr));
+  o.r_t0 = at;    at += win_al16((size_t)KSG_RING * P * 64 * 8);
+  o.r_rec = at;   at += win_al16((size_t)KSG_RING * KSG_WIN_SUM_DWORDS * 4);
+  o.r_mod = at;   at += win_al16((size_t)KSG_RING * 64 * 4);
+  o.cap = at;     at += win_al16((size_t)W * sizeof(I64x2));
+  o.snap = at;    at += win_al16((size_t)W * sizeof(I64x2));
+  o.dlt = at;     at += win_al16((size_t)W * sizeof(I64x2));
+  o.inv = at;     at += win_al16((size_t)W * sizeof(F64x2));
+  o.meta = at;    at += win_al16((size_t)W * sizeof(SlotMeta));
+  o.keys = at;    at += win_al16((size_t)W * KSG_SLOT_KEYS * 4);
+  o.svcs = at;    at += win_al16((size_t)W * KSG_SLOT_SVCS * 4);
+  o.scnt = at;    at += win_al16((size_t)W * KSG_SLOT_SVCS * 4);
+  o.peer = at;    at += win_al16((size_t)W * 2 * 4);
+  o.list = at;    at += win_al16((size_t)W * 4);
+  o.out = at;     at += win_al16((size_t)W * 4);
+  o.flag = at;    at += win_al16((size_t)nflag * 4);
+  o.peerset = at; at += win_al16((size_t)nflag * 4);
+  o.slot_of = at; at += win_al16((size_t)nshard * 2);
+  o.drop = at;    at += win_al16((size_t)P * 64 * 8);
+  o.total = at;
+  return o;
 }
-__host__ __device__ constexpr size_t win_lds_per_slot() { return sizeof(WinSlot) + 4 + 8 + 1; }
 
 #define KSG_STOP_SERVICE 1
 #define KSG_STOP_EXHAUSTED 2
 #define KSG_STOP_SLOT 3
 #define KSG_STOP_OVERSIZE 4
+#define KSG_STOP_HANG 9        // a ring/draw wait exceeded KSG_SPIN_LIMIT polls (a bug): the host fails
+#define KSG_SPIN_LIMIT (1u << 22)
 
-__device__ __forceinline__ int64_t rl64(int64_t v, int lane) {
-  return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane)) |
-                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), lane) << 32));
+__device__ __forceinline__ void lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+__device__ __forceinline__ uint32_t ld_acq(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void st_rel(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// phase B: one wave resolves the window sequentially. P = words of T0 per lane.
-template <int P>
-__global__ __launch_bounds__(64) void ksg_win_resolve_kernel(KsgDev d, const ksg_pod* __restrict__ pods,
-                                                            const uint32_t* __restrict__ ids, uint32_t n_pods,
-                                                            const KsgWinSum* __restrict__ sums,
-                                                            const uint64_t* __restrict__ t0words,
-                                                            uint64_t* rng_io, int32_t* __restrict__ out,
-                                                            uint32_t* stat_out) {
+template <int P, bool STAMP>
+__global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, uint32_t n_pods,
+                                                                    const KsgWinSum* __restrict__ sums,
+                                                                    const uint64_t* __restrict__ wbits,
+                                                                    const int32_t* __restrict__ wmax,
+                                                                    uint64_t* rng_io, int32_t* __restrict__ out,
+                                                                    uint32_t* stat_out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const uint32_t lane = threadIdx.x;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t nflag = (d.n_services + 31) / 32;
   const uint32_t nshard = d.hi - d.lo;
-  uint64_t* s_cmask = reinterpret_cast<uint64_t*>(smem);               // nodes committed in this window
-  uint32_t* s_flag = reinterpret_cast<uint32_t*>(s_cmask + P * 64);    // services whose scalars changed
-  uint32_t* s_peerset = s_flag + win_even(nflag);                      // services whose peer the window set
-  uint16_t* s_slot_of = reinterpret_cast<uint16_t*>(s_peerset + win_even(nflag));
-  WinSlot* s_slots = reinterpret_cast<WinSlot*>(reinterpret_cast<char*>(s_slot_of) +
-                                                (((size_t)nshard * 2 + 15) & ~(size_t)15));
-  uint32_t* s_peer = reinterpret_cast<uint32_t*>(s_slots + n_pods);    // (service, node) pairs
-  uint32_t* s_list = s_peer + 2 * n_pods;                              // candidate node offsets
-  uint8_t* s_dflag = reinterpret_cast<uint8_t*>(s_list + n_pods);      // candidate dropped?
-  for (uint32_t w = lane; w < P * 64u; w += 64) s_cmask[w] = 0;
-  for (uint32_t w = lane; w < 2 * win_even(nflag); w += 64) s_flag[w] = 0;
+  const uint32_t nwords = d.nwords;
+  const WinLdsOff o = win_lds_offsets(P, nflag, nshard, n_pods);
+  WinCtl* ctl = reinterpret_cast<WinCtl*>(smem + o.ctl);
+  RingHdr* r_hdr = reinterpret_cast<RingHdr*>(smem + o.r_hdr);
+  uint64_t* r_t0 = reinterpret_cast<uint64_t*>(smem + o.r_t0);
+  uint32_t* r_rec = reinterpret_cast<uint32_t*>(smem + o.r_rec);
+  uint32_t* r_mod = reinterpret_cast<uint32_t*>(smem + o.r_mod);
+
+  for (uint32_t t = tid; t < KSG_RING; t += KSG_RES_NT) r_hdr[t].ready = 0;
+  if (tid == 0) *ctl = WinCtl{0, 0, 0, 0, 0, {0, 0, 0}};
+  if (wave == 0) {
+    uint64_t* drop = reinterpret_cast<uint64_t*>(smem + o.drop);
+    uint32_t* flag = reinterpret_cast<uint32_t*>(smem + o.flag);
+    uint32_t* peerset = reinterpret_cast<uint32_t*>(smem + o.peerset);
+    for (uint32_t w = lane; w < P * 64u; w += 64) drop[w] = 0;
+    for (uint32_t w = lane; w < nflag; w += 64) {
+      flag[w] = 0;
+      peerset[w] = 0;
+    }
+  }
+  __syncthreads();
+  const uint64_t rng0 = *rng_io;
+
+  // =========================================================================
+  // producers
+  // =========================================================================
+  if (wave != 0) {
+    // warm this XCD's L2 with the shard's node state: the resolver's snapshot
+    // loads of committed nodes (same CU, same L2) then hit L2 instead of HBM
+    {
+      const uint32_t pw = wave - 1, nt = KSG_RES_NPW * 64;
+      const uint32_t n16 = (nshard + 1) / 2;  // 16-byte chunks of one int64 array
+      uint64_t acc = 0;
+      const int64_t* arr[4] = {d.cap_cpu + d.lo, d.cap_mem + d.lo, d.used_cpu + d.lo, d.used_mem + d.lo};
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        for (uint32_t t = pw * 64 + lane; t < n16; t += nt) {
+          const uint32_t idx = 2 * t + 1 < nshard ? 2 * t + 1 : 2 * t;
+          acc ^= (uint64_t)arr[a][idx];
+        }
+      if (acc == 0x5bd1e995a5a5a5a5ULL) ctl->pad[0] = 1;  // keeps the loads
+    }
+    const uint32_t* recs = reinterpret_cast<const uint32_t*>(sums);
+    for (uint32_t j = wave - 1; j < n_pods; j += KSG_RES_NPW) {
+      const uint32_t e = j % KSG_RING;
+      for (uint32_t spin = 0;; ++spin) {  // ring entry free: the resolver is done with pod j - KSG_RING
+        if (ld_acq(&ctl->stop) || spin > KSG_SPIN_LIMIT) return;
+        if (ld_acq(&ctl->consumed) + KSG_RING > j) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      const uint32_t rec = lane < KSG_WIN_SUM_DWORDS ? recs[(size_t)j * KSG_WIN_SUM_DWORDS + lane] : 0u;
+      uint64_t t0[P];
+      int32_t mw[P];
+      int32_t lm = KSG_S32_NONE;
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        const uint32_t wq = lane * P + q;
+        t0[q] = wq < nwords ? wbits[(size_t)j * nwords + wq] : 0ULL;
+        mw[q] = wq < nwords ? wmax[(size_t)j * nwords + wq] : KSG_S32_NONE;
+        lm = mw[q] > lm ? mw[q] : lm;
+      }
+      const int32_t m0 = wave_total_max(lm);
+      uint32_t cnt = 0;
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        t0[q] = (m0 != KSG_S32_NONE && mw[q] == m0) ? t0[q] : 0ULL;
+        cnt += __popcll(t0[q]);
+      }
+      const uint32_t k0 = wave_total_add(cnt);
+      const bool drawable = __builtin_amdgcn_readlane(rec, WS_ERR) == 0 && m0 != KSG_S32_NONE;
+
+      // draw index = draws of the window pods before j (taken before the cache
+      // fill so the chain between producers stays short)
+      for (uint32_t spin = 0;; ++spin) {
+        if (ld_acq(&ctl->stop) || spin > KSG_SPIN_LIMIT) return;
+        if (ld_acq(&ctl->draw_next) == j) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      const uint32_t idx = __builtin_amdgcn_readfirstlane(ctl->draw_count);
+      if (lane == 0) {
+        ctl->draw_count = idx + (drawable ? 1u : 0u);
+        st_rel(&ctl->draw_next, j + 1);
+      }
+      uint64_t sm = rng0 + (uint64_t)idx * 0x9E3779B97F4A7C15ULL;
+      const uint64_t r = ksg_splitmix_next(&sm) >> 1;  // rand.Int() (generic_scheduler.go:94)
+
+      uint32_t mv = 0;
+      if (drawable && lane < k0) mv = umod64_32(r, k0 - lane);
+
+      // publish the entry
+      r_mod[e * 64 + lane] = mv;
+      if (lane < KSG_WIN_SUM_DWORDS) r_rec[e * KSG_WIN_SUM_DWORDS + lane] = rec;
+#pragma unroll
+      for (int q = 0; q < P; ++q) r_t0[(size_t)e * P * 64 + lane * P + q] = t0[q];
+      if (lane == 0) {
+        r_hdr[e].m0 = m0;
+        r_hdr[e].k0 = k0;
+        r_hdr[e].r = r;
+        r_hdr[e].drawable = drawable;
+        st_rel(&r_hdr[e].ready, j + 1);
+      }
+    }
+    return;
+  }
+
+  // =========================================================================
+  // resolver (wave 0)
+  // =========================================================================
+  __builtin_amdgcn_s_setprio(3);
+  struct {
+    I64x2 *cap, *snap, *dlt;
+    F64x2* inv;
+    SlotMeta* meta;
+    uint32_t *keys, *svcs;
+    int32_t* scnt;
+    uint32_t *peer, *list;
+    int32_t* out;
+    uint32_t *flag, *peerset;
+    uint16_t* slot_of;
+    uint64_t* drop;
+  } L = {reinterpret_cast<I64x2*>(smem + o.cap),      reinterpret_cast<I64x2*>(smem + o.snap),
+         reinterpret_cast<I64x2*>(smem + o.dlt),      reinterpret_cast<F64x2*>(smem + o.inv),
+         reinterpret_cast<SlotMeta*>(smem + o.meta),  reinterpret_cast<uint32_t*>(smem + o.keys),
+         reinterpret_cast<uint32_t*>(smem + o.svcs),  reinterpret_cast<int32_t*>(smem + o.scnt),
+         reinterpret_cast<uint32_t*>(smem + o.peer),  reinterpret_cast<uint32_t*>(smem + o.list),
+         reinterpret_cast<int32_t*>(smem + o.out),    reinterpret_cast<uint32_t*>(smem + o.flag),
+         reinterpret_cast<uint32_t*>(smem + o.peerset), reinterpret_cast<uint16_t*>(smem + o.slot_of),
+         reinterpret_cast<uint64_t*>(smem + o.drop)};
   const bool spread_on = d.w_spread != 0;
   const bool aff_on = (d.preds & KSG_PRED_SERVICEAFFINITY) && d.n_aff > 0;
   const bool res_on = (d.preds & KSG_PRED_PODFITSRESOURCES) != 0;
   const bool ports_on = (d.preds & KSG_PRED_PODFITSPORTS) != 0;
   const bool disk_on = (d.preds & KSG_PRED_NODISKCONFLICT) != 0;
-  uint64_t rng = *rng_io;
-  uint32_t resolved = n_pods, reason = 0, n_slots = 0, n_peer = 0;
+  uint32_t resolved = n_pods, reason = 0, n_slots = 0, n_peer = 0, n_draws = 0;
 
-  // pending snapshot loads of the last commit, retired at the next pod
-  bool p_active = false, p_new = false;
+  uint64_t cm[P];  // C: nodes committed in this window (lane owns words lane*P + q)
+#pragma unroll
+  for (int q = 0; q < P; ++q) cm[q] = 0;
+
+  // pending global loads of the last commit (retired lazily): the snapshot of
+  // a newly committed node (issued first, so waiting for it does not wait for
+  // the service loads), then the committing pod's service scalars
+  bool p_snap = false, p_svc = false;
   uint32_t p_slot = 0, p_base = 0, p_nsv = 0, p_node = 0;
-  int64_t p_v = 0;                     // lanes 0..3: cap_c, cap_m, used_c, used_m
+  int64_t p_v = 0;                           // lanes 0..3: cap_c, cap_m, used_c, used_m
   int32_t p_cnt = 0, p_max = 0, p_peer = 0;  // service lanes 32+t
-  auto retire = [&]() {
-    if (!p_active) return;
-    WinSlot& S = s_slots[p_slot];
-    if (p_new) {
-      const int64_t cc = rl64(p_v, 0), cm = rl64(p_v, 1), uc = rl64(p_v, 2), um = rl64(p_v, 3);
-      if (lane == 0) {
-        S.cap_c = cc;
-        S.cap_m = cm;
-        S.snap_c = uc;
-        S.snap_m = um;
-      }
+  uint32_t p_sv = 0xffffffffu;               // service lanes 32+t
+  auto retire_snap = [&]() {
+    if (!p_snap) return;
+    p_snap = false;
+    if (lane < 4) {
+      int64_t* dst = lane < 2 ? &L.cap[p_slot].c : &L.snap[p_slot].c;
+      dst[lane & 1] = p_v;
     }
+    const int64_t cc = readlane64((uint64_t)p_v, 0), cmm = readlane64((uint64_t)p_v, 1);
+    if (lane == 0) L.inv[p_slot] = F64x2{lr_inv10(cc), lr_inv10(cmm)};
+    lds_fence();
+  };
+  auto retire_svc = [&]() {
+    if (!p_svc) return;
+    p_svc = false;
     const uint32_t t = lane - 32;
+    const bool mine = lane >= 32 && t < p_nsv;
     bool changed = false;
-    uint32_t sv = 0;
-    if (lane >= 32 && t < p_nsv) {
+    if (mine) {
       const uint32_t a = p_base + t;
-      sv = S.svcs[a];
-      uint32_t before = 0;  // in-window commits of sv on this node before this one
-      for (uint32_t b = 0; b < a; ++b) before += S.svcs[b] == sv;
-      S.scnt[a] = p_cnt;
+      const uint32_t* sl = L.svcs + (size_t)p_slot * KSG_SLOT_SVCS;
+      uint32_t before = 0;  // in-window commits of this service on this node before this one
+      for (uint32_t b = 0; b < a; ++b) before += sl[b] == p_sv;
+      L.scnt[(size_t)p_slot * KSG_SLOT_SVCS + a] = p_cnt;
       if (spread_on && p_cnt + (int32_t)before + 1 > p_max) changed = true;  // maxCount rises
-      if (p_peer == -1 && !((s_peerset[sv >> 5] >> (sv & 31)) & 1u)) changed |= aff_on;
+      if (p_peer == -1 && !((L.peerset[p_sv >> 5] >> (p_sv & 31)) & 1u)) changed |= aff_on;
     }
-    // first commit of a service with no peer yet: record the peer (ballot, lane 0 applies)
-    uint64_t pm = __ballot(lane >= 32 && t < p_nsv && p_peer == -1);
+    // first commit of a service with no peer yet: record the peer (lane 0 applies, in order)
+    uint64_t pm = __ballot(mine && p_peer == -1);
     while (pm) {
       const uint32_t b = __builtin_ctzll(pm);
       pm &= pm - 1;
-      const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)sv, (int)b);
-      const bool fresh = !((s_peerset[fsv >> 5] >> (fsv & 31)) & 1u);  // same LDS word for all lanes
+      const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)p_sv, (int)b);
+      const bool fresh = !((L.peerset[fsv >> 5] >> (fsv & 31)) & 1u);
       if (fresh) {
         if (lane == 0) {
-          s_peerset[fsv >> 5] |= 1u << (fsv & 31);
-          s_peer[2 * n_peer] = fsv;
-          s_peer[2 * n_peer + 1] = p_node;
+          L.peerset[fsv >> 5] |= 1u << (fsv & 31);
+          L.peer[2 * n_peer] = fsv;
+          L.peer[2 * n_peer + 1] = d.lo + p_node;
         }
         ++n_peer;
+        lds_fence();
       }
     }
-    uint64_t fm = __ballot(changed);
-    while (fm) {
-      const uint32_t b = __builtin_ctzll(fm);
-      fm &= fm - 1;
-      const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)sv, (int)b);
-      if (lane == 0) s_flag[fsv >> 5] |= 1u << (fsv & 31);
-    }
-    p_active = false;
+    if (changed) atomicOr(&L.flag[p_sv >> 5], 1u << (p_sv & 31));
+    lds_fence();
+  };
+  auto retire = [&]() {
+    retire_snap();
+    retire_svc();
   };
 
-  // software pipeline: pod i+1's record and T0 words load while pod i resolves
-  const uint32_t* recs = reinterpret_cast<const uint32_t*>(sums);
-  uint32_t rec = (n_pods > 0 && lane < KSG_WIN_SUM_DWORDS) ? recs[lane] : 0u;
-  uint64_t tw[P], twn[P];
-#pragma unroll
-  for (int q = 0; q < P; ++q) {
-    const uint32_t w = q * 64 + lane;
-    tw[q] = (n_pods > 0 && w < d.nwords) ? t0words[w] : 0ULL;
-  }
-  uint64_t t_last = 0, t_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const bool stamp = (d.dbg & 8) != 0;
+  // KSG_DEBUG & 8: the STAMP instantiation accumulates s_memtime per section
+  uint64_t t_last = 0, t_acc[STAMP ? 16 : 1] = {};
+  constexpr bool stamp = STAMP;
 #define KSG_STAMP(k)                                     \
-  if (stamp) {                                           \
+  if constexpr (STAMP) {                                 \
     const uint64_t t_now = __builtin_amdgcn_s_memtime(); \
     t_acc[k] += t_now - t_last;                          \
     t_last = t_now;                                      \
   }
-  if (stamp) t_last = __builtin_amdgcn_s_memtime();
+  if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
+
   for (uint32_t i = 0; i < n_pods; ++i) {
-    uint32_t recn = 0;
-    if (i + 1 < n_pods) {
-      if (lane < KSG_WIN_SUM_DWORDS) recn = recs[(size_t)(i + 1) * KSG_WIN_SUM_DWORDS + lane];
-      const uint64_t* nx = t0words + (size_t)(i + 1) * d.nwords;
-#pragma unroll
-      for (int q = 0; q < P; ++q) {
-        const uint32_t w = q * 64 + lane;
-        twn[q] = w < d.nwords ? nx[w] : 0ULL;
+    const uint32_t e = i % KSG_RING;
+    bool hung = false;
+    for (uint32_t spin = 0; ld_acq(&r_hdr[e].ready) != i + 1; ++spin) {
+      if (spin > 16 * KSG_SPIN_LIMIT) {
+        hung = true;
+        break;
       }
     }
-    KSG_STAMP(0)
-    retire();
-    KSG_STAMP(1)
-    const int32_t m0 = (int32_t)__builtin_amdgcn_readlane(rec, WS_M0);
-    const uint32_t k0 = __builtin_amdgcn_readlane(rec, WS_K0);
-    const int32_t s = (int32_t)__builtin_amdgcn_readlane(rec, WS_SVC);
-    if (s >= 0 && (spread_on || aff_on) && ((s_flag[s >> 5] >> (s & 31)) & 1u)) {
-      resolved = i;  // a service scalar this pod reads changed in the window
-      reason = KSG_STOP_SERVICE;
+    if (hung) {
+      resolved = i;
+      reason = KSG_STOP_HANG;
       break;
     }
+    KSG_STAMP(0)
+    // ---- head
+    const uint32_t rec = lane < KSG_WIN_SUM_DWORDS ? r_rec[e * KSG_WIN_SUM_DWORDS + lane] : 0u;
+    uint64_t t0[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) t0[q] = r_t0[(size_t)e * P * 64 + lane * P + q];
+    const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
+    const uint32_t k0 = __builtin_amdgcn_readfirstlane(r_hdr[e].k0);
+    const int32_t s = (int32_t)__builtin_amdgcn_readlane(rec, WS_SVC);
+    if (s >= 0 && (spread_on || aff_on)) {
+      // the last commit's services may flag this pod's service: retire it first
+      if (p_svc && __ballot(lane >= 32 && lane - 32 < p_nsv && p_sv == (uint32_t)s)) {
+        if constexpr (STAMP) t_acc[9] += 64;
+        retire_svc();
+      }
+      if ((L.flag[s >> 5] >> (s & 31)) & 1u) {
+        resolved = i;  // a service scalar this pod reads changed in the window
+        reason = KSG_STOP_SERVICE;
+        break;
+      }
+    }
+    KSG_STAMP(1)
     if (__builtin_amdgcn_readlane(rec, WS_ERR)) {
-      if (lane == 0) out[i] = KSG_OUT_ERROR;
-    } else if (m0 == KSG_S32_NONE || k0 == 0) {
-      if (lane == 0) out[i] = KSG_OUT_NOFIT;  // nothing fit at the snapshot; commits only remove fits
+      if (lane == 0) L.out[i] = KSG_OUT_ERROR;
+    } else if (m0 == KSG_S32_NONE) {
+      if (lane == 0) L.out[i] = KSG_OUT_NOFIT;  // nothing fit at the snapshot; commits only remove fits
     } else {
       const uint32_t npp = __builtin_amdgcn_readlane(rec, WS_NPP), nss = __builtin_amdgcn_readlane(rec, WS_NSS);
-      PodCtx c;
-      // readlane returns int: widen through uint32_t (no sign extension of the low dword)
-      c.req_cpu = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_CPU) |
-                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_CPU + 1) << 32));
-      c.req_mem = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_MEM) |
-                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_MEM + 1) << 32));
-      c.zero_req = c.req_cpu == 0 && c.req_mem == 0;
-      c.spread_max = (int32_t)__builtin_amdgcn_readlane(rec, WS_SMAX);
-      c.n_ports = npp & 0xffff;
-      c.n_pds = npp >> 16;
-      c.n_sel = nss & 0xffff;
-      const uint32_t n_svcs = nss >> 16;
-      const uint32_t nk = c.n_ports + c.n_pds;
+      const int64_t req_c = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_CPU) |
+                                      ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_CPU + 1) << 32));
+      const int64_t req_m = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_MEM) |
+                                      ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_MEM + 1) << 32));
+      const bool zero_req = req_c == 0 && req_m == 0;
+      const int32_t smax = (int32_t)__builtin_amdgcn_readlane(rec, WS_SMAX);
+      const uint32_t n_ports = npp & 0xffff, n_pds = npp >> 16, n_sel = nss & 0xffff, n_svcs = nss >> 16;
+      const uint32_t nk = n_ports + n_pds;
       if (__builtin_amdgcn_readlane(rec, WS_NINL) > KSG_WIN_INLINE || nk > KSG_SLOT_KEYS ||
           n_svcs > KSG_SLOT_SVCS) {
         // lists longer than the record / a slot: the exact per-pod kernel takes it
@@ -329,272 +606,345 @@ __global__ __launch_bounds__(64) void ksg_win_resolve_kernel(KsgDev d, const ksg
         reason = i == 0 ? KSG_STOP_OVERSIZE : KSG_STOP_SLOT;
         break;
       }
-      const RecLists RL{rec, c.n_ports, c.n_ports + c.n_pds};
-      KSG_STAMP(6)
 
-      // ---- candidates: snapshot ties committed earlier in this window (T0 ∩ C),
-      //      compacted so that 64 lanes re-check 64 of them at a time
+      // ---- candidates: snapshot ties committed earlier in the window (T0 ∩ C)
+      uint64_t cand[P];
       uint32_t cnt = 0;
-      uint64_t dmr[P];
 #pragma unroll
       for (int q = 0; q < P; ++q) {
-        const uint32_t w = q * 64 + lane;
-        cnt += __popcll(tw[q] & (w < d.nwords ? s_cmask[w] : 0ULL));
-        dmr[q] = 0;
+        cand[q] = t0[q] & cm[q];
+        cnt += __popcll(cand[q]);
       }
-      const uint32_t incl = wave_incl_scan_u32(cnt, lane);
-      const uint32_t total = __shfl(incl, 63, 64);
-      if (stamp) t_acc[7] += total * 64;
+      uint64_t dw[P];
+#pragma unroll
+      for (int q = 0; q < P; ++q) dw[q] = 0;
+      const uint32_t incl_c = dpp_scan_add(cnt);
+      const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl_c, 63);
+      if constexpr (STAMP) t_acc[7] += total * 64;
       if (total) {
-        uint32_t pos = incl - cnt;
+        if (p_snap || p_svc) {
+          // the last committed node is a candidate and a value it needs is in flight
+          const uint32_t pw = p_node >> 6, po = pw / P, pq = pw % P;
+          bool hit = false;
+#pragma unroll
+          for (int q = 0; q < P; ++q)
+            if ((uint32_t)q == pq) hit = (cand[q] >> (p_node & 63)) & 1ULL;
+          if (__builtin_amdgcn_readlane((int)hit, (int)po)) {
+            if constexpr (STAMP) t_acc[10] += 64;
+            retire_snap();
+            if (p_svc && spread_on && s >= 0 &&
+                __ballot(lane >= 32 && lane - 32 < p_nsv && p_sv == (uint32_t)s) != 0)
+              retire_svc();
+          }
+        }
+        KSG_STAMP(6)
+        uint32_t pos = incl_c - cnt;
 #pragma unroll
         for (int q = 0; q < P; ++q) {
-          const uint32_t w = q * 64 + lane;
-          uint64_t x = tw[q] & (w < d.nwords ? s_cmask[w] : 0ULL);
+          uint64_t x = cand[q];
           while (x) {
-            s_list[pos++] = w * 64 + __builtin_ctzll(x);
+            L.list[pos++] = (lane * P + q) * 64 + __builtin_ctzll(x);
             x &= x - 1;
           }
         }
+        lds_fence();
+        KSG_STAMP(8)
         for (uint32_t base = 0; base < total; base += 64) {
           const uint32_t t = base + lane;
           if (t < total) {
             // the node fit the pod at the snapshot; only the window's deltas can change that
-            const WinSlot& S = s_slots[s_slot_of[s_list[t]]];
-            const int64_t now_c = (int64_t)((uint64_t)S.snap_c + (uint64_t)S.dc);
-            const int64_t now_m = (int64_t)((uint64_t)S.snap_m + (uint64_t)S.dm);
+            const uint32_t woff = L.list[t];
+            const uint32_t sl = L.slot_of[woff];
+            const I64x2 cap = L.cap[sl], snp = L.snap[sl], dl = L.dlt[sl];
+            const int64_t now_c = (int64_t)((uint64_t)snp.c + (uint64_t)dl.c);
+            const int64_t now_m = (int64_t)((uint64_t)snp.m + (uint64_t)dl.m);
+            const SlotMeta me = L.meta[sl];
             bool drop = false;
-            if (res_on && !c.zero_req) {  // PodFitsResources
-              const bool fc = S.cap_c == 0 || (int64_t)((uint64_t)S.cap_c - (uint64_t)now_c) >= c.req_cpu;
-              const bool fm = S.cap_m == 0 || (int64_t)((uint64_t)S.cap_m - (uint64_t)now_m) >= c.req_mem;
+            if (res_on && !zero_req) {  // PodFitsResources
+              const bool fc = cap.c == 0 || cap.c - now_c >= req_c;
+              const bool fm = cap.m == 0 || cap.m - now_m >= req_m;
               drop = !(fc && fm);
             }
-            for (uint32_t a = 0; a < S.nk && !drop; ++a) {  // PodFitsPorts / NoDiskConflict
-              const uint32_t key = S.keys[a];
-              if (ports_on)
-                for (uint32_t b = 0; b < c.n_ports; ++b) drop |= RL.port(b) == key;
-              if (disk_on)
-                for (uint32_t b = 0; b < c.n_pds; ++b) drop |= RL.pd(b) == key;
-            }
-            if (!drop && d.w_lr) {  // LeastRequested can only fall as requested grows
-              const int64_t lr_now = lr_calc((int64_t)((uint64_t)now_c + (uint64_t)c.req_cpu), S.cap_c) +
-                                     lr_calc((int64_t)((uint64_t)now_m + (uint64_t)c.req_mem), S.cap_m);
-              const int64_t lr_snap = lr_calc((int64_t)((uint64_t)S.snap_c + (uint64_t)c.req_cpu), S.cap_c) +
-                                      lr_calc((int64_t)((uint64_t)S.snap_m + (uint64_t)c.req_mem), S.cap_m);
-              drop = lr_now / 2 != lr_snap / 2;
-            }
-            if (!drop && spread_on && s >= 0) {  // ServiceSpreading under an unchanged maxCount
-              int32_t delta = 0, snapc = 0;
-              for (uint32_t a = 0; a < S.ns; ++a)
-                if (S.svcs[a] == (uint32_t)s) {
-                  snapc = S.scnt[a];
-                  ++delta;
-                }
-              if (delta) {
-                const int64_t mx = c.spread_max;
-                drop = frac10_f32(mx - snapc - delta, mx) != frac10_f32(mx - snapc, mx);
+            if (nk && !drop) {  // PodFitsPorts / NoDiskConflict against the window's keys
+              const uint32_t* ks = L.keys + (size_t)sl * KSG_SLOT_KEYS;
+              for (uint32_t a = 0; a < me.nk; ++a) {
+                const uint32_t key = ks[a];
+                if (ports_on)
+                  for (uint32_t b = 0; b < n_ports; ++b)
+                    drop |= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + b) == key;
+                if (disk_on)
+                  for (uint32_t b = 0; b < n_pds; ++b)
+                    drop |= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + n_ports + b) == key;
               }
             }
-            s_dflag[t] = drop ? 1 : 0;
+            if (!drop && d.w_lr) {  // LeastRequested can only fall as requested grows
+              const F64x2 iv = L.inv[sl];
+              const int32_t lr_now = lr_win(now_c + req_c, cap.c, iv.c) + lr_win(now_m + req_m, cap.m, iv.m);
+              const int32_t lr_snap = lr_win(snp.c + req_c, cap.c, iv.c) + lr_win(snp.m + req_m, cap.m, iv.m);
+              drop = (lr_now >> 1) != (lr_snap >> 1);
+            }
+            if (!drop && spread_on && s >= 0 && ((me.smask >> (s & 31)) & 1u)) {
+              // ServiceSpreading under an unchanged maxCount
+              const uint32_t* sv = L.svcs + (size_t)sl * KSG_SLOT_SVCS;
+              int32_t delta = 0, snapc = 0;
+              for (uint32_t a = 0; a < me.ns; ++a)
+                if (sv[a] == (uint32_t)s) {
+                  snapc = L.scnt[(size_t)sl * KSG_SLOT_SVCS + a];
+                  ++delta;
+                }
+              if (delta) drop = frac10_f32((int64_t)smax - snapc - delta, smax) != frac10_f32((int64_t)smax - snapc, smax);
+            }
+            if (drop) atomicOr(reinterpret_cast<unsigned long long*>(L.drop + (woff >> 6)), 1ULL << (woff & 63));
           }
         }
-        // each lane rebuilds the dropped bits of its own T0 words: its candidates
-        // sit at [incl - cnt, incl) of the list in bit order
-        uint32_t idx = incl - cnt;
+        lds_fence();
+        KSG_STAMP(11)
+        // each lane collects the dropped bits of its own words and clears them
+        if (cnt) {
 #pragma unroll
-        for (int q = 0; q < P; ++q) {
-          const uint32_t w = q * 64 + lane;
-          uint64_t x = tw[q] & (w < d.nwords ? s_cmask[w] : 0ULL);
-          while (x) {
-            const uint32_t b = __builtin_ctzll(x);
-            x &= x - 1;
-            if (s_dflag[idx++]) dmr[q] |= 1ULL << b;
-          }
+          for (int q = 0; q < P; ++q)
+            if (cand[q]) {
+              dw[q] = L.drop[lane * P + q];
+              L.drop[lane * P + q] = 0;
+            }
         }
       }
       KSG_STAMP(2)
-      uint32_t dropped = 0;
+      // ---- selection: k live ties, ix-th in descending rank = (k-1-ix)-th ascending
       uint64_t live[P];
+      uint32_t cl = 0;
 #pragma unroll
       for (int q = 0; q < P; ++q) {
-        live[q] = tw[q] & ~dmr[q];
-        dropped += __popcll(dmr[q]);
+        live[q] = t0[q] & ~dw[q];
+        cl += __popcll(live[q]);
       }
-      dropped = wave_sum_u32(dropped);
-      const uint64_t k = (uint64_t)k0 - dropped;
+      const uint32_t incl = dpp_scan_add(cl);
+      const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
       if (k == 0) {
         resolved = i;  // every snapshot tie got worse: needs a fresh snapshot
         reason = KSG_STOP_EXHAUSTED;
         break;
       }
-      const uint64_t rng_before = rng;
-      const uint64_t r = ksg_splitmix_next(&rng) >> 1;  // rand.Int() (generic_scheduler.go:94)
-      const uint64_t target = k - 1 - (r % k);           // ix-th host in descending name order
-      uint64_t acc = 0;
-      int32_t win = -1;
+      const uint32_t dropped = k0 - k;
+      uint32_t ix;
+      if (dropped < 64 && !(d.dbg & 32)) {  // KSG_DEBUG & 32: always the direct modulo
+        ix = __builtin_amdgcn_readfirstlane(r_mod[e * 64 + dropped]);
+      } else {
+        // (readfirstlane returns int: widen through uint32_t, no sign extension)
+        const uint64_t r = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(r_hdr[e].r >> 32)) << 32) |
+                           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r_hdr[e].r);
+        ix = umod64_32(r, k);
+      }
+      const uint32_t target = k - 1 - ix;
+      const uint32_t excl = incl - cl;
+      const int ol = (int)__builtin_ctzll(__ballot(excl <= target && target < incl));
+      // the owner lane's words, in scalar registers; then the bit by mbcnt rank
+      uint32_t local = target - (uint32_t)__builtin_amdgcn_readlane((int)excl, ol);
+      uint64_t wsel = 0;
+      uint32_t qsel = 0;
 #pragma unroll
       for (int q = 0; q < P; ++q) {
-        const uint32_t cq = __popcll(live[q]);
-        const uint32_t iq = wave_incl_scan_u32(cq, lane);
-        const uint32_t tot = __shfl(iq, 63, 64);
-        if (win < 0 && target < acc + tot) {
-          const uint32_t excl = iq - cq;
-          int32_t cand = -1;
-          if (acc + excl <= target && target < acc + iq)
-            cand = (int32_t)(d.lo + (q * 64 + lane) * 64 + select_bit(live[q], (uint32_t)(target - acc - excl)));
-          const uint64_t own = __ballot(cand >= 0);
-          win = __shfl(cand, (int)__builtin_ctzll(own), 64);
+        const uint64_t wq = readlane64(live[q], ol);
+        const uint32_t pc = __popcll(wq);
+        if (qsel == (uint32_t)q) {
+          if (local < pc) {
+            wsel = wq;
+          } else {
+            local -= pc;
+            qsel = q + 1;
+          }
         }
-        acc += tot;
       }
+      const uint32_t rank =
+          __builtin_amdgcn_mbcnt_hi((uint32_t)(wsel >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wsel, 0u));
+      const uint32_t bsel = (uint32_t)__builtin_ctzll(__ballot(((wsel >> lane) & 1ULL) && rank == local));
+      const uint32_t woff = ((uint32_t)ol * P + qsel) * 64 + bsel;
+      const uint32_t wn = d.lo + woff;
       KSG_STAMP(3)
-      const uint32_t wn = (uint32_t)win;
-      const uint32_t woff = wn - d.lo;
-      const bool in_c = (s_cmask[woff >> 6] >> (woff & 63)) & 1ULL;
-      const uint32_t slot = in_c ? s_slot_of[woff] : n_slots;
-      WinSlot& S = s_slots[slot];
-      if (in_c && (S.nk + nk > KSG_SLOT_KEYS || S.ns + n_svcs > KSG_SLOT_SVCS)) {
-        rng = rng_before;  // this pod is redone (with the same draw) in the next window
-        resolved = i;
-        reason = KSG_STOP_SLOT;
-        break;
-      }
       // ---- AssumePod into the window cache; HBM is written back at window end
-      const uint32_t base_ns = in_c ? S.ns : 0u;
-      if (!in_c) {
+      retire();  // the previous commit's loads land before this commit reuses the registers
+      const uint32_t cw = woff >> 6, co = cw / P, cq = cw % P;
+      uint64_t cmw = 0;
+#pragma unroll
+      for (int q = 0; q < P; ++q)
+        if ((uint32_t)q == cq) cmw = cm[q];
+      const bool in_c = (readlane64(cmw, (int)co) >> (woff & 63)) & 1ULL;
+      uint32_t slot = n_slots, base_nk = 0, base_ns = 0, smask_old = 0;
+      bool snap_pending = false;
+      if (in_c) {
+        slot = L.slot_of[woff];
+        const SlotMeta me = L.meta[slot];
+        base_nk = me.nk;
+        base_ns = me.ns;
+        smask_old = me.smask;
+        if (base_nk + nk > KSG_SLOT_KEYS || base_ns + n_svcs > KSG_SLOT_SVCS) {
+          resolved = i;  // this pod is redone (with the same draw) in the next window
+          reason = KSG_STOP_SLOT;
+          break;
+        }
+      } else {
         ++n_slots;
-        // snapshot loads, retired at the next pod
+        // snapshot loads (L2-warm), retired lazily
+        snap_pending = true;
         if (lane == 0) p_v = d.cap_cpu[wn];
         else if (lane == 1) p_v = d.cap_mem[wn];
         else if (lane == 2) p_v = d.used_cpu[wn];
         else if (lane == 3) p_v = d.used_mem[wn];
+#pragma unroll
+        for (int q = 0; q < P; ++q)
+          if ((uint32_t)q == cq && lane == co) cm[q] |= 1ULL << (woff & 63);
       }
       const uint32_t t32 = lane - 32;
-      // every lane takes part in the shuffle (bpermute reads inactive lanes as garbage)
-      const uint32_t idx_sv = WS_IDS + nk + c.n_sel + (t32 < n_svcs ? t32 : 0u);
-      const uint32_t my_sv = (uint32_t)__shfl(rec, (int)(idx_sv < 64 ? idx_sv : 0u), 64);
+      // every lane takes part in the shuffles (bpermute reads inactive lanes as garbage)
+      const uint32_t idx_sv = WS_IDS + nk + n_sel + (t32 < n_svcs ? t32 : 0u);
+      const uint32_t my_sv = (uint32_t)__shfl((int)rec, (int)(idx_sv < 64 ? idx_sv : 0u), 64);
+      const uint32_t smask_new =
+          smask_old | (uint32_t)__builtin_amdgcn_readfirstlane(
+                          (int)wave_or_u32(lane >= 32 && t32 < n_svcs ? (1u << (my_sv & 31)) : 0u));
       if (lane >= 32 && t32 < n_svcs) {
-        const uint32_t sv = my_sv;
-        p_cnt = d.svc_cnt[(size_t)sv * d.n_nodes + wn];
-        p_max = d.svc_max[sv];
-        p_peer = d.svc_peer[sv];
+        p_cnt = d.svc_cnt[(size_t)my_sv * d.n_nodes + wn];
+        p_max = d.svc_max[my_sv];
+        p_peer = d.svc_peer[my_sv];
+        p_sv = my_sv;
+        L.svcs[(size_t)slot * KSG_SLOT_SVCS + base_ns + t32] = my_sv;
       }
+      // ports then PDs sit at record dwords WS_IDS + [0, nk)
+      const uint32_t my_key = (uint32_t)__shfl((int)rec, (int)(WS_IDS + (lane < nk ? lane : 0u)), 64);
+      if (lane < nk) L.keys[(size_t)slot * KSG_SLOT_KEYS + base_nk + lane] = my_key;
       if (lane == 0) {
         if (!in_c) {
-          S.node = wn;
-          S.nk = 0;
-          S.ns = 0;
-          S.dc = 0;
-          S.dm = 0;
-          s_slot_of[woff] = (uint16_t)slot;
-          s_cmask[woff >> 6] |= 1ULL << (wn & 63);
+          L.slot_of[woff] = (uint16_t)slot;
+          L.dlt[slot] = I64x2{req_c, req_m};
+        } else {
+          const I64x2 ov = L.dlt[slot];
+          L.dlt[slot] = I64x2{ov.c + req_c, ov.m + req_m};
         }
-        S.dc = (int64_t)((uint64_t)S.dc + (uint64_t)c.req_cpu);
-        S.dm = (int64_t)((uint64_t)S.dm + (uint64_t)c.req_mem);
-        for (uint32_t t = 0; t < nk; ++t) S.keys[S.nk++] = t < c.n_ports ? RL.port(t) : RL.pd(t - c.n_ports);
-        for (uint32_t t = 0; t < n_svcs; ++t) S.svcs[S.ns++] = __builtin_amdgcn_readlane(rec, WS_IDS + nk + c.n_sel + t);
-        out[i] = win;
+        L.meta[slot] = SlotMeta{woff, (uint16_t)(base_nk + nk), (uint16_t)(base_ns + n_svcs), smask_new, 0u};
+        L.out[i] = (int32_t)wn;
       }
-      p_active = true;
-      p_new = !in_c;
+      ++n_draws;
+      lds_fence();
+      p_snap = snap_pending;
+      p_svc = n_svcs > 0;
       p_slot = slot;
       p_base = base_ns;
       p_nsv = n_svcs;
-      p_node = wn;
+      p_node = woff;
       KSG_STAMP(4)
     }
-    rec = recn;
-#pragma unroll
-    for (int q = 0; q < P; ++q) tw[q] = twn[q];
+    if (lane == 0) st_rel(&ctl->consumed, i + 1);
     KSG_STAMP(5)
   }
+  if (resolved < n_pods && lane == 0) st_rel(&ctl->stop, 1u);
   retire();
-  if (stamp && lane == 0)
-    for (int k = 0; k < 8; ++k) atomicAdd(d.dbgbuf + k, (int32_t)(t_acc[k] / 64));
+  if constexpr (STAMP) {
+    if (lane == 0)
+      for (int k = 0; k < 16; ++k) atomicAdd(d.dbgbuf + k, (int32_t)(t_acc[k] / 64));
+  }
 #undef KSG_STAMP
 
   // ---- write the window's deltas back to HBM (the next snapshot) -------------
   for (uint32_t t = lane; t < n_slots; t += 64) {
-    const WinSlot& S = s_slots[t];
-    const uint32_t n = S.node;
-    d.used_cpu[n] = (int64_t)((uint64_t)S.snap_c + (uint64_t)S.dc);
-    d.used_mem[n] = (int64_t)((uint64_t)S.snap_m + (uint64_t)S.dm);
-    for (uint32_t a = 0; a < S.nk; ++a)
-      __hip_atomic_fetch_or(d.keymap + (size_t)S.keys[a] * d.nw + (n >> 6), 1ULL << (n & 63), __ATOMIC_RELAXED,
+    const SlotMeta me = L.meta[t];
+    const uint32_t n = d.lo + me.node;
+    const I64x2 snp = L.snap[t], dl = L.dlt[t];
+    d.used_cpu[n] = snp.c + dl.c;
+    d.used_mem[n] = snp.m + dl.m;
+    const uint32_t* ks = L.keys + (size_t)t * KSG_SLOT_KEYS;
+    for (uint32_t a = 0; a < me.nk; ++a)
+      __hip_atomic_fetch_or(d.keymap + (size_t)ks[a] * d.nw + (n >> 6), 1ULL << (n & 63), __ATOMIC_RELAXED,
                             __HIP_MEMORY_SCOPE_AGENT);
-    for (uint32_t a = 0; a < S.ns; ++a) {
-      const uint32_t sv = S.svcs[a];
+    const uint32_t* sv = L.svcs + (size_t)t * KSG_SLOT_SVCS;
+    const int32_t* sc = L.scnt + (size_t)t * KSG_SLOT_SVCS;
+    for (uint32_t a = 0; a < me.ns; ++a) {
+      const uint32_t s = sv[a];
       bool first = true;
       int32_t count = 0;
-      for (uint32_t b = 0; b < S.ns; ++b) {
-        if (S.svcs[b] == sv) {
+      for (uint32_t b = 0; b < me.ns; ++b) {
+        if (sv[b] == s) {
           if (b < a) first = false;
           ++count;
         }
       }
-      __hip_atomic_fetch_add(d.svc_total + sv, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(d.svc_total + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (first) {
-        const int32_t fin = S.scnt[a] + count;
-        d.svc_cnt[(size_t)sv * d.n_nodes + n] = fin;
-        __hip_atomic_fetch_max(d.svc_max + sv, fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int32_t fin = sc[a] + count;
+        d.svc_cnt[(size_t)s * d.n_nodes + n] = fin;
+        __hip_atomic_fetch_max(d.svc_max + s, fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
   for (uint32_t t = lane; t < n_peer; t += 64) {
-    const uint32_t sv = s_peer[2 * t];
+    const uint32_t sv = L.peer[2 * t];
     int32_t expect = -1;
-    __hip_atomic_compare_exchange_strong(d.svc_peer + sv, &expect, (int32_t)s_peer[2 * t + 1], __ATOMIC_RELAXED,
+    __hip_atomic_compare_exchange_strong(d.svc_peer + sv, &expect, (int32_t)L.peer[2 * t + 1], __ATOMIC_RELAXED,
                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  for (uint32_t t = lane; t < resolved; t += 64) out[t] = L.out[t];
   if (lane == 0) {
-    *rng_io = rng;
+    *rng_io = rng0 + (uint64_t)n_draws * 0x9E3779B97F4A7C15ULL;
     stat_out[0] = resolved;
     stat_out[1] = reason;
   }
 }
 
+// ---------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------
+static uint32_t win_P(const KsgDev& d) {
+  const uint32_t P = (d.nwords + 63) / 64;
+  return P <= 1 ? 1 : P <= 2 ? 2 : P <= 4 ? 4 : P <= 8 ? 8 : 0;
+}
+
+static const size_t kWinLdsBudget = 156 * 1024;
+
 hipError_t ksg_launch_win_eval(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids, uint32_t n,
-                               KsgWinSum* sums, uint64_t* t0words, hipStream_t st) {
-  const size_t lds = (size_t)d.nwords * 64 * sizeof(int32_t);
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_eval_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8 * 1024);
-    (void)hipGetLastError();  // do not leave a sticky error behind
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(ksg_win_eval_kernel, dim3(n), dim3(KSG_WIN_NT), lds, st, d, pods, ids, sums, t0words);
+                               KsgWinSum* sums, uint64_t* wbits, int32_t* wmax, hipStream_t st) {
+  const dim3 grid((d.nwords + KSG_SC_NT / 64 - 1) / (KSG_SC_NT / 64), (n + KSG_PG - 1) / KSG_PG);
+  hipLaunchKernelGGL(ksg_win_score_kernel, grid, dim3(KSG_SC_NT), 0, st, d, pods, ids, n, sums, wbits, wmax);
   return hipGetLastError();
 }
 
-// largest window the resolver's LDS holds for this shard (slots + candidate list)
+// largest window the resolver's LDS holds for this shard
 uint32_t ksg_win_max_window(const KsgDev& d) {
-  const uint32_t P = (d.nwords + 63) / 64;
-  const size_t fixed = win_lds_fixed(P < 1 ? 1 : P, (d.n_services + 31) / 32, d.hi - d.lo);
-  const size_t budget = 150 * 1024;
-  if (fixed >= budget) return 0;
-  const size_t n = (budget - fixed) / win_lds_per_slot();
-  return (uint32_t)(n > 4096 ? 4096 : n);
+  const uint32_t P = win_P(d);
+  if (P == 0) return 0;
+  const uint32_t nflag = (d.n_services + 31) / 32, nshard = d.hi - d.lo;
+  uint32_t lo = 0, hi = 4096;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) / 2;
+    if (win_lds_offsets(P, nflag, nshard, mid).total <= kWinLdsBudget) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
 }
 
-hipError_t ksg_launch_win_resolve(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids, uint32_t n,
-                                  const KsgWinSum* sums, const uint64_t* t0words, uint64_t* rng, int32_t* out,
-                                  uint32_t* stat, hipStream_t st) {
-  const uint32_t P = (d.nwords + 63) / 64;
-#define KSG_RES_CASE(PP)                                                                                  \
-  if (P <= PP) {                                                                                          \
-    static bool once = false;                                                                             \
-    if (!once) {                                                                                          \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_resolve_kernel<PP>),               \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 8 * 1024);       \
-      (void)hipGetLastError();                                                                            \
-      once = true;                                                                                        \
-    }                                                                                                     \
-    const size_t lds = win_lds_fixed(PP, (d.n_services + 31) / 32, d.hi - d.lo) + (size_t)n * win_lds_per_slot(); \
-    hipLaunchKernelGGL(ksg_win_resolve_kernel<PP>, dim3(1), dim3(64), lds, st, d, pods, ids, n, sums, t0words, \
-                       rng, out, stat);                                                                   \
-    return hipGetLastError();                                                                             \
+template <int PP, bool ST>
+static hipError_t win_resolve_launch(const KsgDev& d, uint32_t n, size_t lds, const KsgWinSum* sums,
+                                     const uint64_t* wbits, const int32_t* wmax, uint64_t* rng, int32_t* out,
+                                     uint32_t* stat, hipStream_t st) {
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_resolve_kernel<PP, ST>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipGetLastError();  // do not leave a sticky error behind
+    once = true;
   }
+  hipLaunchKernelGGL((ksg_win_resolve_kernel<PP, ST>), dim3(1), dim3(KSG_RES_NT), lds, st, d, n, sums, wbits, wmax,
+                     rng, out, stat);
+  return hipGetLastError();
+}
+
+hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t n, const KsgWinSum* sums, const uint64_t* wbits,
+                                  const int32_t* wmax, uint64_t* rng, int32_t* out, uint32_t* stat,
+                                  hipStream_t st) {
+  const uint32_t P = win_P(d);
+  const size_t lds = win_lds_offsets(P, (d.n_services + 31) / 32, d.hi - d.lo, n).total;
+  const bool stamp = (d.dbg & 8) != 0;  // KSG_DEBUG & 8: per-section s_memtime stamps
+#define KSG_RES_CASE(PP)                                                                              \
+  if (P == PP)                                                                                        \
+    return stamp ? win_resolve_launch<PP, true>(d, n, lds, sums, wbits, wmax, rng, out, stat, st)     \
+                 : win_resolve_launch<PP, false>(d, n, lds, sums, wbits, wmax, rng, out, stat, st);
   KSG_RES_CASE(1)
   KSG_RES_CASE(2)
   KSG_RES_CASE(4)
