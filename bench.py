@@ -11,9 +11,11 @@ batch descriptors in, ~B*88 bytes, inside the step).
   N=1 : BASELINE config 2 — 5,000 nodes / 10,000 pods, DefaultProvider
         (PodFitsPorts, PodFitsResources, NoDiskConflict, MatchNodeSelector,
         HostName + LeastRequested(1), ServiceSpreading(1), Equal(0)).
-  N>1 : BASELINE config 3 — 15,000 nodes node-sharded across N GPUs, per-pod
-        winner exchange with RCCL all-gather over xGMI (strong scaling: the
-        total node count is fixed).
+  N>1 : BASELINE config 3 — 15,000 nodes node-sharded across N GPUs: each GPU
+        scores its shard for a window of pods, the shards' per-word results are
+        all-gathered with RCCL over xGMI once per window, and every GPU resolves
+        the window identically over its replica of the node state (strong
+        scaling: the total node count is fixed).
 
 Roofline: bound "hbm"; achieved = algorithmic bytes per launch / kernel time,
 with SURVEY.md 8(d)'s 60 B/node/pod for this predicate+priority set
@@ -165,14 +167,16 @@ def main():
     # from the HIP events the library records around each resolver launch.
     # exact path (--window 0) / sharded: the one batch kernel per step.
     bpn = BYTES_PER_NODE.get(wl, 60)
-    if kk["launches"] > 0 and world == 1:
+    if kk["launches"] > 0:
         launches = kk["launches"]
         pods_per_launch = pods_timed / launches
         kavg_s = kk["resolve_ms"] / launches / 1e3
         kname = "ksg_win_resolve_kernel"
+        # phase A scores this rank's shard (N/world nodes); with world > 1 its
+        # event window also holds the per-window all-gather
         extra = {"launches": launches, "pods_per_launch": pods_per_launch,
                  "win_eval_ms_avg": kk["eval_ms"] / launches,
-                 "win_eval_GBps": bpn * n_nodes * pods_per_launch / (kk["eval_ms"] / launches / 1e3) / 1e9}
+                 "win_eval_GBps": bpn * (n_nodes / world) * pods_per_launch / (kk["eval_ms"] / launches / 1e3) / 1e9}
     else:
         pods_per_launch = args.batch
         kavg_s = float(np.mean(kern_ms)) / 1e3 if kern_ms else float("nan")
@@ -240,7 +244,8 @@ def main():
                    "snapshots_in_timed": wstats,
                    "parallelism": ("speculative windows: all-CU snapshot scoring + in-order exact resolver"
                                    if kk["launches"] else "single workgroup persistent kernel") if world == 1
-                   else f"node-sharded x{world}, RCCL all-gather per pod"},
+                   else (f"node-sharded x{world}: shard scoring, RCCL all-gather per window, replicated resolver"
+                         if kk["launches"] else f"node-sharded x{world}, RCCL all-gather per pod")},
         "roofline": roofline,
         "cpu_baseline": cpu,
     }

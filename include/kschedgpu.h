@@ -139,12 +139,26 @@ typedef struct ksg_ctx ksg_ctx;
 /* Create a context on HIP device `device`. Single-GPU form. */
 int ksg_create(const ksg_config* cfg, int device, ksg_ctx** out);
 
-/* Node-sharded form: `world` processes, one per GPU, each owning node ranks
- * [rank*N/world, (rank+1)*N/world). Node state is replicated; evaluation is
- * sharded; the per-pod winner is exchanged with RCCL (all-gather of a packed
- * {score, tie count} word). `nccl_id` is the 128-byte ncclUniqueId from rank 0. */
+/* Node-sharded form: `world` (<= 16) processes, one per GPU, each owning the
+ * node ranks of its run of 64-node words (ksg_shard_range). Node state is
+ * replicated; filter/score evaluation is sharded. Window path: the shards'
+ * per-word results for a window of pods are all-gathered once per window and
+ * every rank resolves the window identically. Per-pod path (begin/commit,
+ * ServiceAntiAffinity): the shard records are all-gathered per pod. `nccl_id`
+ * is the 128-byte ncclUniqueId from rank 0 (RCCL over xGMI), or NULL to use a
+ * host transport installed with ksg_set_allgather. */
 int ksg_create_sharded(const ksg_config* cfg, int device, int rank, int world,
                        const void* nccl_id, ksg_ctx** out);
+/* Host transport for a sharded context created with nccl_id == NULL: the
+ * library calls fn(user, send, recv, bytes) with host buffers and fn must
+ * all-gather `bytes` from every rank into recv, rank-major (world * bytes),
+ * returning 0 on success. Every rank must make the same sequence of calls.
+ * This is how a caller that owns its own transport (or a test that runs
+ * several ranks on one GPU, where RCCL refuses duplicate devices) drives the
+ * same sharded kernels; with an RCCL communicator the exchange stays on the
+ * device stream. */
+typedef int (*ksg_allgather_fn)(void* user, const void* send, void* recv, uint64_t bytes);
+int ksg_set_allgather(ksg_ctx* ctx, ksg_allgather_fn fn, void* user);
 /* Fill a fresh ncclUniqueId (128 bytes) for ksg_create_sharded on rank 0. */
 int ksg_nccl_unique_id(void* out128);
 

@@ -162,7 +162,11 @@ EXPORTS = [
     "ksg_read_requested",
     "ksg_shard_range",
     "ksg_merge_records",
+    "ksg_set_allgather",
 ]
+
+# int (*ksg_allgather_fn)(void* user, const void* send, void* recv, uint64_t bytes)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64)
 
 LIB_NAME = "libkschedgpu.so"
 _lib = None
@@ -206,6 +210,7 @@ def load_library() -> C.CDLL:
         "ksg_read_requested": (C.c_int, [vp, vp, vp]),
         "ksg_shard_range": (C.c_int, [U32, C.c_int, C.c_int, P(U32), P(U32)]),
         "ksg_merge_records": (C.c_int, [vp, U32, U32, U32, C.c_int, P(U64), U64, P(I32), P(I64), P(U64)]),
+        "ksg_set_allgather": (C.c_int, [vp, ALLGATHER_FN, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)

@@ -115,6 +115,22 @@ struct KsgWinSum {
 static_assert(sizeof(KsgWinSum) == 192, "KsgWinSum layout");
 #define KSG_WIN_SUM_DWORDS (sizeof(KsgWinSum) / 4)
 
+// Where the resolver finds phase A's per-word results (ksg_window.hip). Phase A
+// on each rank writes one block for its shard: best-score bitmaps
+// uint64[wcap][ostride], then best scores int32[wcap][ostride], row = window
+// pod, column = word of the shard. With world > 1 the blocks are all-gathered
+// rank-major (block g at buf + g * blk); global word w lives in the block of
+// the rank whose [wlo, wlo + nw) holds it.
+#define KSG_MAX_WORLD 16
+struct KsgWinXchg {
+  const uint8_t* buf;
+  uint64_t blk;       // bytes per rank block
+  uint32_t ostride;   // words per row (>= every shard's word count)
+  uint32_t wcap;      // rows per block (window capacity)
+  uint32_t world, pad;
+  uint32_t wlo[KSG_MAX_WORLD], nw[KSG_MAX_WORLD];
+};
+
 // one record of the per-pod winner exchange (all-gathered across ranks)
 typedef ksg_shard_record KsgRecordHdr;  // public layout (include/kschedgpu.h)
 // followed by nwords_max uint64 tie words (bit set = node at max_score)

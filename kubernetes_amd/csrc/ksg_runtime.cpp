@@ -36,10 +36,10 @@ hipError_t ksg_launch_scan(int R, bool anti, const KsgDev& d, const ksg_pod* pod
                            int64_t* score_out, uint8_t* record, int32_t* dpart,
                            const int32_t* dglobal, hipStream_t st);
 hipError_t ksg_launch_win_eval(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids, uint32_t n,
-                               KsgWinSum* sums, uint64_t* wbits, int32_t* wmax, hipStream_t st);
-hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t n, const KsgWinSum* sums, const uint64_t* wbits,
-                                  const int32_t* wmax, uint64_t* rng, int32_t* out, uint32_t* stat,
-                                  hipStream_t st);
+                               KsgWinSum* sums, uint64_t* wbits, int32_t* wmax, uint32_t ostride,
+                               hipStream_t st);
+hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t n, const KsgWinSum* sums, const KsgWinXchg& x,
+                                  uint64_t* rng, int32_t* out, uint32_t* stat, hipStream_t st);
 uint32_t ksg_win_max_window(const KsgDev& d);
 hipError_t ksg_launch_decide(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids,
                              const uint8_t* records, uint32_t rec_bytes, uint32_t world,
@@ -72,6 +72,11 @@ struct ksg_ctx {
   int device = 0, rank = 0, world = 1;
   hipStream_t st = nullptr;
   ncclComm_t comm = nullptr;
+  // host-staged exchange (ksg_set_allgather) for sharded contexts without RCCL
+  ksg_allgather_fn xfn = nullptr;
+  void* xuser = nullptr;
+  uint8_t *h_xsend = nullptr, *h_xrecv = nullptr;
+  size_t h_xsend_cap = 0, h_xrecv_cap = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   double last_ms = 0.0;
   std::string err;
@@ -120,9 +125,9 @@ struct ksg_ctx {
   // window (speculative) path
   uint32_t window = 128;        // 0 = exact one-pod-at-a-time kernel
   KsgWinSum* d_winsum = nullptr;
-  uint64_t* d_t0 = nullptr;     // [W][nwords] per-word best-score node bitmaps (phase A)
-  int32_t* d_wmax = nullptr;    // [W][nwords] per-word best scores (phase A)
-  size_t win_cap = 0, t0_cap = 0, wmax_cap = 0;
+  uint8_t* d_xsend = nullptr;   // phase A block of this shard (KsgWinXchg layout)
+  uint8_t* d_xrecv = nullptr;   // all-gathered blocks of every shard (world > 1)
+  size_t win_cap = 0, xsend_cap = 0, xrecv_cap = 0;
   uint32_t* d_resolved = nullptr;  // {resolved, stop reason}
   uint32_t last_stats[4] = {0, 0, 0, 0};  // windows, stops (service scalar), stops (ties exhausted)
   hipEvent_t kev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -349,6 +354,62 @@ size_t pod_ids_extent(const ksg_pod* p) {
 
 bool anti_on(const ksg_ctx* c) { return c->cfg.n_anti > 0 && c->dev.n_domains_total > 0; }
 
+// ---- cross-rank exchange: RCCL over xGMI, or the caller's host transport ----
+int grow_host(ksg_ctx* c, uint8_t** p, size_t* cap, size_t need) {
+  if (*cap >= need) return KSG_OK;
+  if (*p) (void)hipHostFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  HIPCHK(c, hipHostMalloc((void**)p, need, hipHostMallocDefault));
+  *cap = need;
+  return KSG_OK;
+}
+
+// recv[g * bytes, (g + 1) * bytes) = rank g's send, on c->st
+int allgather(ksg_ctx* c, const void* dsend, void* drecv, size_t bytes) {
+  if (c->comm) {
+    NCCLCHK(c, ncclAllGather(dsend, drecv, bytes, ncclUint8, c->comm, c->st));
+    return KSG_OK;
+  }
+  if (!c->xfn) return fail(c, KSG_ERR_STATE, "sharded context has neither an RCCL communicator nor ksg_set_allgather");
+  int rc;
+  if ((rc = grow_host(c, &c->h_xsend, &c->h_xsend_cap, bytes)) ||
+      (rc = grow_host(c, &c->h_xrecv, &c->h_xrecv_cap, bytes * c->world)))
+    return rc;
+  HIPCHK(c, hipMemcpyAsync(c->h_xsend, dsend, bytes, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  if ((rc = c->xfn(c->xuser, c->h_xsend, c->h_xrecv, (uint64_t)bytes)) != 0)
+    return fail(c, KSG_ERR_RCCL, "allgather callback returned %d", rc);
+  HIPCHK(c, hipMemcpyAsync(drecv, c->h_xrecv, bytes * c->world, hipMemcpyHostToDevice, c->st));
+  return KSG_OK;
+}
+
+int allreduce_sum_i32(ksg_ctx* c, const int32_t* dsend, int32_t* drecv, uint32_t n) {
+  if (c->comm) {
+    NCCLCHK(c, ncclAllReduce(dsend, drecv, n, ncclInt32, ncclSum, c->comm, c->st));
+    return KSG_OK;
+  }
+  if (!c->xfn) return fail(c, KSG_ERR_STATE, "sharded context has neither an RCCL communicator nor ksg_set_allgather");
+  const size_t bytes = (size_t)n * 4;
+  int rc;
+  if ((rc = grow_host(c, &c->h_xsend, &c->h_xsend_cap, bytes)) ||
+      (rc = grow_host(c, &c->h_xrecv, &c->h_xrecv_cap, bytes * (c->world + 1))))
+    return rc;
+  HIPCHK(c, hipMemcpyAsync(c->h_xsend, dsend, bytes, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  if ((rc = c->xfn(c->xuser, c->h_xsend, c->h_xrecv, (uint64_t)bytes)) != 0)
+    return fail(c, KSG_ERR_RCCL, "allgather callback returned %d", rc);
+  int32_t* all = reinterpret_cast<int32_t*>(c->h_xrecv);
+  int32_t* sum = all + (size_t)n * c->world;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t acc = 0;  // wrapping, as ncclSum on int32
+    for (int g = 0; g < c->world; ++g) acc += (uint32_t)all[(size_t)g * n + i];
+    sum[i] = (int32_t)acc;
+  }
+  HIPCHK(c, hipMemcpyAsync(drecv, sum, bytes, hipMemcpyHostToDevice, c->st));
+  return KSG_OK;
+}
+
 // one pod through scan [+ dcount all-reduce] + record all-gather (device only)
 int scan_exchange(ksg_ctx* c, const ksg_pod* dpod, const uint32_t* dids, int mode, uint8_t* fail_out,
                   int64_t* score_out) {
@@ -356,8 +417,8 @@ int scan_exchange(ksg_ctx* c, const ksg_pod* dpod, const uint32_t* dids, int mod
   if (anti && c->world > 1) {
     HIPCHK(c, ksg_launch_scan(c->R, true, c->dev, dpod, dids, mode, 1, nullptr, nullptr, c->d_rec_send,
                               c->d_dpart, nullptr, c->st));
-    NCCLCHK(c, ncclAllReduce(c->d_dpart, c->d_dglobal, c->dev.n_domains_total, ncclInt32, ncclSum, c->comm,
-                             c->st));
+    int rc = allreduce_sum_i32(c, c->d_dpart, c->d_dglobal, c->dev.n_domains_total);
+    if (rc) return rc;
     HIPCHK(c, ksg_launch_scan(c->R, true, c->dev, dpod, dids, mode, 2, fail_out, score_out, c->d_rec_send,
                               nullptr, c->d_dglobal, c->st));
   } else {
@@ -366,7 +427,8 @@ int scan_exchange(ksg_ctx* c, const ksg_pod* dpod, const uint32_t* dids, int mod
   }
   if (mode == KSG_MODE_BEGIN) {
     if (c->world > 1) {
-      NCCLCHK(c, ncclAllGather(c->d_rec_send, c->d_rec_recv, c->rec_bytes, ncclUint8, c->comm, c->st));
+      int rc = allgather(c, c->d_rec_send, c->d_rec_recv, c->rec_bytes);
+      if (rc) return rc;
     } else {
       HIPCHK(c, hipMemcpyAsync(c->d_rec_recv, c->d_rec_send, c->rec_bytes, hipMemcpyDeviceToDevice, c->st));
     }
@@ -376,8 +438,18 @@ int scan_exchange(ksg_ctx* c, const ksg_pod* dpod, const uint32_t* dids, int mod
 
 // The window path needs monotone scores under commits (see ksg_window.hip):
 // no ServiceAntiAffinity, and int64 totals far from wrapping.
+// The resolver walks the whole node set on every rank (state is replicated).
+KsgDev full_geometry(const ksg_ctx* c) {
+  KsgDev f = c->dev;
+  f.lo = 0;
+  f.hi = c->N;
+  f.wlo = 0;
+  f.nwords = c->nw;
+  return f;
+}
+
 bool use_window(ksg_ctx* c, const ksg_pod* pods, uint32_t n) {
-  if (c->window == 0 || anti_on(c) || c->nwords > 8 * 64 || ksg_win_max_window(c->dev) < 8) return false;
+  if (c->window == 0 || anti_on(c) || c->nw > 8 * 64 || ksg_win_max_window(full_geometry(c)) < 8) return false;
   // monotonicity under commits needs non-negative pod-dependent weights
   if (c->cfg.w_least_requested < 0 || c->cfg.w_service_spreading < 0) return false;
   // lr_win (ksg_device.h) is exact for 0 <= capacity, requested totals <= 2^49
@@ -493,11 +565,13 @@ static int create_impl(const ksg_config* cfg, int device, int rank, int world, c
       (e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess)
     return bail(fail(c, KSG_ERR_HIP, "stream/event: %s", hipGetErrorString(e)));
   if (world > 1) {
-    if (!nccl_id) return bail(fail(c, KSG_ERR_ARG, "nccl_id required for world > 1"));
-    ncclUniqueId id;
-    memcpy(&id, nccl_id, sizeof id);
-    ncclResult_t r = ncclCommInitRank(&c->comm, world, id, rank);
-    if (r != ncclSuccess) return bail(fail(c, KSG_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r)));
+    if (world > KSG_MAX_WORLD) return bail(fail(c, KSG_ERR_ARG, "world %d > %d", world, KSG_MAX_WORLD));
+    if (nccl_id) {  // else: the caller installs a host transport with ksg_set_allgather
+      ncclUniqueId id;
+      memcpy(&id, nccl_id, sizeof id);
+      ncclResult_t r = ncclCommInitRank(&c->comm, world, id, rank);
+      if (r != ncclSuccess) return bail(fail(c, KSG_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r)));
+    }
   }
   int rc;
   if (const char* wenv = getenv("KSG_WINDOW")) c->window = (uint32_t)atoi(wenv);
@@ -531,10 +605,12 @@ int ksg_destroy(ksg_ctx* c) {
   free_cluster(c);
   void* scratch[] = {c->d_pods, c->d_ids, c->d_fail, c->d_score, c->d_rec_send, c->d_rec_recv, c->d_dpart,
                      c->d_dglobal, c->d_out, c->d_rng, c->d_summary, c->d_patch, c->d_shard_wlo,
-                     c->d_winsum, c->d_t0, c->d_wmax, c->d_resolved};
+                     c->d_winsum, c->d_xsend, c->d_xrecv, c->d_resolved};
   for (void* p : scratch)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
+  if (c->h_xsend) (void)hipHostFree(c->h_xsend);
+  if (c->h_xrecv) (void)hipHostFree(c->h_xrecv);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   for (auto& e : c->kev)
@@ -881,11 +957,30 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
   HIPCHK(c, hipMemcpyAsync(c->d_rng, rng_state, 8, hipMemcpyHostToDevice, c->st));
   HIPCHK(c, hipEventRecord(c->ev0, c->st));
   c->last_stats[0] = c->last_stats[1] = c->last_stats[2] = c->last_stats[3] = 0;
-  if (c->world == 1 && use_window(c, pods, n)) {
-    const uint32_t W = std::min(c->window, ksg_win_max_window(c->dev));
+  if (use_window(c, pods, n)) {
+    // Window path. Phase A scores the window on this rank's shard; with world > 1
+    // the per-word results are all-gathered once per window (not per pod) and
+    // every rank runs the same resolver over the whole replicated node state, so
+    // every rank commits the same pods to the same nodes.
+    const KsgDev full = full_geometry(c);
+    const uint32_t W = std::min(c->window, ksg_win_max_window(full));
+    KsgWinXchg x{};
+    x.ostride = std::max<uint32_t>(c->nwords_max, 1);
+    x.wcap = W;
+    x.world = (uint32_t)c->world;
+    for (int g = 0; g < c->world; ++g) {
+      uint32_t a, b;
+      ksg_shard_words(c->nw, (uint32_t)g, (uint32_t)c->world, &a, &b);
+      x.wlo[g] = a;
+      x.nw[g] = b - a;
+    }
+    x.blk = ((size_t)W * x.ostride * 12 + 255) & ~(size_t)255;
     if ((rc = grow(c, (void**)&c->d_winsum, &c->win_cap, W, sizeof(KsgWinSum)))) return rc;
-    if ((rc = grow(c, (void**)&c->d_t0, &c->t0_cap, (size_t)W * c->nwords, sizeof(uint64_t)))) return rc;
-    if ((rc = grow(c, (void**)&c->d_wmax, &c->wmax_cap, (size_t)W * c->nwords, sizeof(int32_t)))) return rc;
+    if ((rc = grow(c, (void**)&c->d_xsend, &c->xsend_cap, x.blk, 1))) return rc;
+    if (c->world > 1 && (rc = grow(c, (void**)&c->d_xrecv, &c->xrecv_cap, x.blk * c->world, 1))) return rc;
+    x.buf = c->world > 1 ? c->d_xrecv : c->d_xsend;
+    uint64_t* wbits = reinterpret_cast<uint64_t*>(c->d_xsend);
+    int32_t* wmax = reinterpret_cast<int32_t*>(c->d_xsend + (size_t)W * x.ostride * 8);
     uint32_t pos = 0;
     if (!c->kev[0])
       for (auto& e : c->kev) HIPCHK(c, hipEventCreate(&e));
@@ -894,11 +989,11 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       const uint32_t w = std::min(W, n - pos);
       // HIP events on this stream around each kernel (per-kernel device time)
       HIPCHK(c, hipEventRecord(c->kev[0], c->st));
-      HIPCHK(c, ksg_launch_win_eval(c->dev, c->d_pods + pos, c->d_ids, w, c->d_winsum, c->d_t0, c->d_wmax,
+      HIPCHK(c, ksg_launch_win_eval(c->dev, c->d_pods + pos, c->d_ids, w, c->d_winsum, wbits, wmax, x.ostride,
                                     c->st));
+      if (c->world > 1 && (rc = allgather(c, c->d_xsend, c->d_xrecv, x.blk))) return rc;
       HIPCHK(c, hipEventRecord(c->kev[1], c->st));
-      HIPCHK(c, ksg_launch_win_resolve(c->dev, w, c->d_winsum, c->d_t0, c->d_wmax, c->d_rng, c->d_out + pos,
-                                       c->d_resolved, c->st));
+      HIPCHK(c, ksg_launch_win_resolve(full, w, c->d_winsum, x, c->d_rng, c->d_out + pos, c->d_resolved, c->st));
       HIPCHK(c, hipEventRecord(c->kev[2], c->st));
       uint32_t st2[2] = {0, 0};
       HIPCHK(c, hipMemcpyAsync(st2, c->d_resolved, 8, hipMemcpyDeviceToHost, c->st));
@@ -914,9 +1009,15 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
         c->last_kms[2] += 1;
       }
       if (st2[1] == 4) {
-        // a pod whose id lists exceed the window record: exact per-pod kernel
-        HIPCHK(c, ksg_launch_batch(c->R, false, c->dev, c->d_pods + pos, c->d_ids, 1, c->d_rng, c->d_out + pos,
-                                   c->st));
+        // a pod whose id lists exceed the window record: the exact per-pod path
+        if (c->world == 1) {
+          HIPCHK(c, ksg_launch_batch(c->R, false, c->dev, c->d_pods + pos, c->d_ids, 1, c->d_rng,
+                                     c->d_out + pos, c->st));
+        } else {
+          if ((rc = scan_exchange(c, c->d_pods + pos, c->d_ids, KSG_MODE_BEGIN, nullptr, nullptr))) return rc;
+          HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods + pos, c->d_ids, c->d_rec_recv, c->rec_bytes, c->world,
+                                      c->d_shard_wlo, 1, 0, c->d_rng, c->d_out, pos, c->d_summary, c->st));
+        }
         pos += 1;
         ++c->last_stats[3];
         continue;
@@ -976,6 +1077,14 @@ int ksg_evaluate(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, uint8_t* f
   if (score_out && ns) HIPCHK(c, hipMemcpyAsync(score_out, c->d_score, ns * 8, hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
   if (summ[2]) return fail(c, KSG_ERR_NOPEER, "service affinity peer is not on a known node");
+  return KSG_OK;
+}
+
+int ksg_set_allgather(ksg_ctx* c, ksg_allgather_fn fn, void* user) {
+  if (!c) return KSG_ERR_ARG;
+  if (c->comm) return fail(c, KSG_ERR_STATE, "context already exchanges over RCCL");
+  c->xfn = fn;
+  c->xuser = user;
   return KSG_OK;
 }
 

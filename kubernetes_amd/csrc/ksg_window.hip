@@ -70,15 +70,19 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
                                                                  const uint32_t* __restrict__ ids, uint32_t n_pods,
                                                                  KsgWinSum* __restrict__ sums,
                                                                  uint64_t* __restrict__ wbits,
-                                                                 int32_t* __restrict__ wmax) {
+                                                                 int32_t* __restrict__ wmax, uint32_t ostride) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (KSG_SC_NT / 64) + (threadIdx.x >> 6));
   const uint32_t p0 = blockIdx.y * KSG_PG;
-  if (w >= d.nwords || p0 >= n_pods) return;  // wave-uniform
+  // the wave of local word 0 also writes the pods' resolver records, so it runs
+  // even on a rank whose shard is empty (every rank resolves every pod)
+  if ((w >= d.nwords && w != 0) || p0 >= n_pods) return;  // wave-uniform
+  const bool has_word = w < d.nwords;
   const uint32_t np = min((uint32_t)KSG_PG, n_pods - p0);
   const uint32_t gw = d.wlo + w;  // global word
   const uint32_t n = gw * 64 + lane;
-  const bool valid = n < d.hi;
+  const bool valid = has_word && n < d.hi;
+  const uint64_t shard_m = __ballot(valid);  // nodes of the shard in this word
   const uint32_t P = d.preds;
 
   // ---- node state, once per wave (read-only while phase A runs)
@@ -101,11 +105,13 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
   if (lane < np) {
     const ksg_pod& p = pods[p0 + lane];
     pod_resolve<false>(d, p, ids, c);
-    uint64_t m = gw * 64 + 64 <= d.hi ? ~0ULL : ((1ULL << (d.hi - gw * 64)) - 1);  // nodes of the shard
-    if (d.has_static_fit) m &= d.static_fit[gw];  // LabelsPresence (predicates.go:215-229)
+    uint64_t m = shard_m;
+    if (!has_word) m = 0;  // (no bitmap word to read)
+    else if (d.has_static_fit) m &= d.static_fit[gw];  // LabelsPresence (predicates.go:215-229)
     if ((P & KSG_PRED_HOSTNAME) && c.host != -1) {  // PodFitsHost (predicates.go:181-186)
       m &= (c.host >= 0 && (uint32_t)c.host >> 6 == gw) ? (1ULL << (c.host & 63)) : 0ULL;
     }
+    if (has_word) {
     if (P & KSG_PRED_MATCHNODESELECTOR)  // PodMatchesNodeLabels (predicates.go:161-167)
       for (uint32_t t = 0; t < c.n_sel; ++t) m &= d.pairmap[(size_t)c.sel[t] * d.nw + gw];
     if (P & KSG_PRED_NODISKCONFLICT)  // NoDiskConflict (predicates.go:73-83)
@@ -116,6 +122,7 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
 #pragma unroll
       for (uint32_t j = 0; j < KSG_MAX_AFF; ++j)
         if (j < d.n_aff && c.req_aff[j] >= 0) m &= d.pairmap[(size_t)c.req_aff[j] * d.nw + gw];
+    }
     }
     fm = m;
     rc = c.req_cpu;
@@ -179,9 +186,9 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
       }
     }
   }
-  if (lane < np) {
-    wmax[(size_t)(p0 + lane) * d.nwords + w] = my_max;
-    wbits[(size_t)(p0 + lane) * d.nwords + w] = my_bits;
+  if (lane < np && has_word) {
+    wmax[(size_t)(p0 + lane) * ostride + w] = my_max;
+    wbits[(size_t)(p0 + lane) * ostride + w] = my_bits;
   }
 
   // ---- the resolver's record of each pod (one wave per pod group)
@@ -330,9 +337,8 @@ __device__ __forceinline__ void st_rel(uint32_t* p, uint32_t v) {
 template <int P, bool STAMP>
 __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, uint32_t n_pods,
                                                                     const KsgWinSum* __restrict__ sums,
-                                                                    const uint64_t* __restrict__ wbits,
-                                                                    const int32_t* __restrict__ wmax,
-                                                                    uint64_t* rng_io, int32_t* __restrict__ out,
+                                                                    const KsgWinXchg x, uint64_t* rng_io,
+                                                                    int32_t* __restrict__ out,
                                                                     uint32_t* stat_out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const uint32_t tid = threadIdx.x;
@@ -383,6 +389,22 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
       if (acc == 0x5bd1e995a5a5a5a5ULL) ctl->pad[0] = 1;  // keeps the loads
     }
     const uint32_t* recs = reinterpret_cast<const uint32_t*>(sums);
+    // this lane's words lane*P + q: the rank block and row offset phase A wrote them at
+    // (byte offsets into x.buf; ~0u = no such word)
+    uint32_t wb_at[P], wm_at[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      const uint32_t wq = lane * P + q;
+      uint32_t g = 0;
+      for (uint32_t r = 1; r < x.world; ++r)
+        if (wq >= x.wlo[r] && x.nw[r] > 0) g = r;
+      const uint32_t i = wq - x.wlo[g];
+      const bool ok = wq < nwords && i < x.nw[g];
+      const uint32_t base = (uint32_t)(g * x.blk);
+      wb_at[q] = ok ? base + i * 8 : ~0u;
+      wm_at[q] = ok ? base + x.wcap * x.ostride * 8 + i * 4 : ~0u;
+    }
+    const uint32_t row_b = x.ostride * 8, row_m = x.ostride * 4;
     for (uint32_t j = wave - 1; j < n_pods; j += KSG_RES_NPW) {
       const uint32_t e = j % KSG_RING;
       for (uint32_t spin = 0;; ++spin) {  // ring entry free: the resolver is done with pod j - KSG_RING
@@ -396,9 +418,8 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
       int32_t lm = KSG_S32_NONE;
 #pragma unroll
       for (int q = 0; q < P; ++q) {
-        const uint32_t wq = lane * P + q;
-        t0[q] = wq < nwords ? wbits[(size_t)j * nwords + wq] : 0ULL;
-        mw[q] = wq < nwords ? wmax[(size_t)j * nwords + wq] : KSG_S32_NONE;
+        t0[q] = wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + j * row_b) : 0ULL;
+        mw[q] = wm_at[q] != ~0u ? *reinterpret_cast<const int32_t*>(x.buf + wm_at[q] + j * row_m) : KSG_S32_NONE;
         lm = mw[q] > lm ? mw[q] : lm;
       }
       const int32_t m0 = wave_total_max(lm);
@@ -899,9 +920,12 @@ static uint32_t win_P(const KsgDev& d) {
 static const size_t kWinLdsBudget = 156 * 1024;
 
 hipError_t ksg_launch_win_eval(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids, uint32_t n,
-                               KsgWinSum* sums, uint64_t* wbits, int32_t* wmax, hipStream_t st) {
-  const dim3 grid((d.nwords + KSG_SC_NT / 64 - 1) / (KSG_SC_NT / 64), (n + KSG_PG - 1) / KSG_PG);
-  hipLaunchKernelGGL(ksg_win_score_kernel, grid, dim3(KSG_SC_NT), 0, st, d, pods, ids, n, sums, wbits, wmax);
+                               KsgWinSum* sums, uint64_t* wbits, int32_t* wmax, uint32_t ostride,
+                               hipStream_t st) {
+  const uint32_t gx = std::max<uint32_t>(1, (d.nwords + KSG_SC_NT / 64 - 1) / (KSG_SC_NT / 64));
+  const dim3 grid(gx, (n + KSG_PG - 1) / KSG_PG);
+  hipLaunchKernelGGL(ksg_win_score_kernel, grid, dim3(KSG_SC_NT), 0, st, d, pods, ids, n, sums, wbits, wmax,
+                     ostride);
   return hipGetLastError();
 }
 
@@ -921,8 +945,8 @@ uint32_t ksg_win_max_window(const KsgDev& d) {
 
 template <int PP, bool ST>
 static hipError_t win_resolve_launch(const KsgDev& d, uint32_t n, size_t lds, const KsgWinSum* sums,
-                                     const uint64_t* wbits, const int32_t* wmax, uint64_t* rng, int32_t* out,
-                                     uint32_t* stat, hipStream_t st) {
+                                     const KsgWinXchg& x, uint64_t* rng, int32_t* out, uint32_t* stat,
+                                     hipStream_t st) {
   static bool once = false;
   if (!once) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_resolve_kernel<PP, ST>),
@@ -930,21 +954,20 @@ static hipError_t win_resolve_launch(const KsgDev& d, uint32_t n, size_t lds, co
     (void)hipGetLastError();  // do not leave a sticky error behind
     once = true;
   }
-  hipLaunchKernelGGL((ksg_win_resolve_kernel<PP, ST>), dim3(1), dim3(KSG_RES_NT), lds, st, d, n, sums, wbits, wmax,
-                     rng, out, stat);
+  hipLaunchKernelGGL((ksg_win_resolve_kernel<PP, ST>), dim3(1), dim3(KSG_RES_NT), lds, st, d, n, sums, x, rng, out,
+                     stat);
   return hipGetLastError();
 }
 
-hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t n, const KsgWinSum* sums, const uint64_t* wbits,
-                                  const int32_t* wmax, uint64_t* rng, int32_t* out, uint32_t* stat,
-                                  hipStream_t st) {
+hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t n, const KsgWinSum* sums, const KsgWinXchg& x,
+                                  uint64_t* rng, int32_t* out, uint32_t* stat, hipStream_t st) {
   const uint32_t P = win_P(d);
   const size_t lds = win_lds_offsets(P, (d.n_services + 31) / 32, d.hi - d.lo, n).total;
   const bool stamp = (d.dbg & 8) != 0;  // KSG_DEBUG & 8: per-section s_memtime stamps
 #define KSG_RES_CASE(PP)                                                                              \
   if (P == PP)                                                                                        \
-    return stamp ? win_resolve_launch<PP, true>(d, n, lds, sums, wbits, wmax, rng, out, stat, st)     \
-                 : win_resolve_launch<PP, false>(d, n, lds, sums, wbits, wmax, rng, out, stat, st);
+    return stamp ? win_resolve_launch<PP, true>(d, n, lds, sums, x, rng, out, stat, st)               \
+                 : win_resolve_launch<PP, false>(d, n, lds, sums, x, rng, out, stat, st);
   KSG_RES_CASE(1)
   KSG_RES_CASE(2)
   KSG_RES_CASE(4)

@@ -59,13 +59,19 @@ class DeviceScheduler:
     """One scheduling context on one GPU (or one shard of a node-sharded set)."""
 
     def __init__(self, cfg: abi.KsgConfig, device: int = 0, rank: int = 0, world: int = 1,
-                 nccl_id: bytes | None = None):
+                 nccl_id: bytes | None = None, allgather=None):
+        """world > 1: exchange over RCCL (`nccl_id` from rank 0's nccl_unique_id()),
+        or over the caller's transport `allgather(send: bytes) -> bytes` (the
+        rank-major concatenation of every rank's `send`; ksg_set_allgather)."""
         self._lib = abi.load_library()
         self._ctx = C.c_void_p()
+        self._xfn = None
         if world == 1:
             rc = self._lib.ksg_create(C.byref(cfg), device, C.byref(self._ctx))
         else:
-            idbuf = C.create_string_buffer(nccl_id, 128)
+            if (nccl_id is None) == (allgather is None):
+                raise ValueError("world > 1 needs exactly one of nccl_id / allgather")
+            idbuf = C.create_string_buffer(nccl_id, 128) if nccl_id is not None else None
             rc = self._lib.ksg_create_sharded(C.byref(cfg), device, rank, world, idbuf, C.byref(self._ctx))
         if rc != abi.KSG_OK:
             raise KsgError(rc, "ksg_create failed (see stderr)")
@@ -73,6 +79,29 @@ class DeviceScheduler:
         self.n_nodes = 0
         self.world = world
         self.rank = rank
+        if world > 1 and allgather is not None:
+            self._install_allgather(allgather)
+
+    def _install_allgather(self, allgather):
+        world = self.world
+
+        def cb(_user, send, recv, nbytes):
+            try:
+                got = allgather(C.string_at(send, nbytes))
+                if len(got) != world * nbytes:
+                    return -1
+                C.memmove(recv, got, world * nbytes)
+                return 0
+            except Exception:  # an exception must not unwind through C
+                import traceback
+
+                traceback.print_exc()
+                return -1
+
+        self._xfn = abi.ALLGATHER_FN(cb)  # kept alive with the context
+        rc = self._lib.ksg_set_allgather(self._ctx, self._xfn, None)
+        if rc != abi.KSG_OK:
+            self._err(rc)
 
     @staticmethod
     def nccl_unique_id() -> bytes:
@@ -207,6 +236,21 @@ class DeviceScheduler:
         if rc != abi.KSG_OK:
             self._err(rc)
         return c[: self.n_nodes], m[: self.n_nodes]
+
+
+def gloo_allgather(group=None):
+    """allgather callable for DeviceScheduler over a torch.distributed process
+    group (host transport; e.g. gloo ranks sharing one GPU in tests)."""
+    import torch
+    import torch.distributed as dist
+
+    def ag(send: bytes) -> bytes:
+        t = torch.frombuffer(bytearray(send), dtype=torch.uint8)
+        outs = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+        dist.all_gather(outs, t, group=group)
+        return b"".join(o.numpy().tobytes() for o in outs)
+
+    return ag
 
 
 # ---- node sharding (host side of the multi-GPU exchange; include/kschedgpu.h) ----

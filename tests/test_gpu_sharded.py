@@ -1,0 +1,115 @@
+"""Node-sharded HIP path on one GPU: `world` ranks, each a separate process with
+its own sharded ksg context on cuda:0, exchanging over gloo through
+ksg_set_allgather (RCCL refuses two ranks on one device; with RCCL the same
+kernels run and only the transport of the all-gather changes).
+
+Each rank filters/scores only its node shard; the window path all-gathers the
+shards' per-word results once per window and every rank resolves the window
+over the replicated state; the per-pod path (window 0, ServiceAntiAffinity)
+all-gathers shard records per pod (generic_scheduler.go:54-96 pod by pod).
+Every rank's pod -> node sequence, RNG position and committed requested
+totals must equal the C oracle's single-process schedule.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, name, nn, npods, window, chunk, seed, q):
+    import torch.distributed as dist
+
+    from kubernetes_amd.engine import DeviceScheduler, gloo_allgather
+    from tests.helpers import Case, run_batch
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        case = Case(name, nn, npods)
+        dev = DeviceScheduler(case.cfg, device=0, rank=rank, world=world, allgather=gloo_allgather())
+        dev.set_window(window)
+        out, rng = run_batch(dev, case, rng=seed, chunk=chunk)
+        used_c, used_m = dev.read_requested()
+        lo, hi = dev.shard()
+        stats = dev.last_batch_stats()
+        dev.close()
+        q.put((rank, out.tolist(), rng, used_c.tolist(), used_m.tolist(), lo, hi, stats, None))
+    except Exception as e:  # report instead of hanging the parent
+        import traceback
+
+        q.put((rank, None, None, None, None, None, None, None, traceback.format_exc() + repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(name, nn, npods, window, world=2, chunk=None, seed=1234):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, nn, npods, window, chunk, seed, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = []
+    try:
+        for _ in range(world):
+            res.append(q.get(timeout=110))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    res.sort(key=lambda r: r[0])
+    for r in res:
+        assert r[8] is None, r[8]
+    return res
+
+
+def _oracle(name, nn, npods, seed=1234):
+    from oracle.pyoracle import OracleScheduler
+    from tests.helpers import Case, run_batch
+
+    case = Case(name, nn, npods)
+    orc = OracleScheduler(case.cfg)
+    want, st = run_batch(orc, case, rng=seed)
+    wc, wm = orc.read_requested()
+    return want, st, wc, wm
+
+
+@pytest.mark.parametrize("name,nn,npods,window,world,chunk", [
+    ("config2", 700, 1500, 128, 2, None),    # window path, both shards non-empty
+    ("config2", 5000, 2000, 1024, 2, None),  # config 2 node count, large windows
+    ("config2", 1500, 900, 37, 3, 211),      # three ranks, ragged shards, windows cut by batches
+    ("config2", 60, 300, 128, 2, None),      # one 64-node word: rank 0's shard is empty
+    ("config2", 700, 400, 0, 2, None),       # per-pod exchange path
+    ("config4", 900, 500, 128, 2, None),     # ServiceAntiAffinity: per-pod path + domain all-reduce
+    ("config1", 500, 1000, 128, 2, None),    # BASELINE config 1
+])
+def test_sharded_batch_matches_oracle(name, nn, npods, window, world, chunk):
+    want, st, wc, wm = _oracle(name, nn, npods)
+    res = _run(name, nn, npods, window, world=world, chunk=chunk)
+    spans = [(r[5], r[6]) for r in res]
+    assert spans[0][0] == 0 and spans[-1][1] == nn
+    for rank, out, rng, uc, um, lo, hi, stats, _ in res:
+        got = np.asarray(out)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, f"rank {rank}: first mismatches at {bad[:8]}: {got[bad[:8]]} vs {want[bad[:8]]}"
+        assert rng == st
+        assert np.array_equal(np.asarray(uc), wc) and np.array_equal(np.asarray(um), wm)
+    if world == 2 and all(b > a for a, b in spans):
+        lo1 = spans[1][0]  # both shards must have produced winners
+        assert (want >= lo1).any() and ((want >= 0) & (want < lo1)).any()
