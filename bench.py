@@ -70,6 +70,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--window", type=int, default=None,
                     help="pods per speculative window (0 = exact one-pod-at-a-time kernel)")
+    ap.add_argument("--transport", choices=("rccl", "gloo"), default="rccl",
+                    help="N>1 exchange: RCCL over xGMI (default), or host-staged over the gloo group "
+                         "(rehearsal of the sharded path with several ranks on one GPU)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (profiles/), keyed by workload")
     args = ap.parse_args()
@@ -103,10 +106,17 @@ def main():
 
         dist = dist_mod
         dist.init_process_group("gloo")
-        idb = DeviceScheduler.nccl_unique_id() if rank == 0 else bytes(128)
-        obj = [idb]
-        dist.broadcast_object_list(obj, src=0)
-        sched = DeviceScheduler(cfg, device=local_rank, rank=rank, world=world, nccl_id=obj[0])
+        if args.transport == "rccl":
+            idb = DeviceScheduler.nccl_unique_id() if rank == 0 else bytes(128)
+            obj = [idb]
+            dist.broadcast_object_list(obj, src=0)
+            sched = DeviceScheduler(cfg, device=local_rank, rank=rank, world=world, nccl_id=obj[0])
+        else:
+            from kubernetes_amd.engine import gloo_allgather
+
+            ndev = max(torch.cuda.device_count(), 1)
+            sched = DeviceScheduler(cfg, device=local_rank % ndev, rank=rank, world=world,
+                                    allgather=gloo_allgather())
     else:
         sched = DeviceScheduler(cfg, device=0)
     if args.window is not None:
@@ -232,6 +242,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
+        "device_ms_per_step": float(np.mean(kern_ms)) if kern_ms else None,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -242,6 +253,7 @@ def main():
                    "nodes": n_nodes, "pods_per_step": args.batch,
                    "placed_in_timed": int((timed >= 0).sum()), "fit_errors_in_timed": int((timed == -1).sum()),
                    "snapshots_in_timed": wstats,
+                   "exchange": None if world == 1 else args.transport,
                    "parallelism": ("speculative windows: all-CU snapshot scoring + in-order exact resolver"
                                    if kk["launches"] else "single workgroup persistent kernel") if world == 1
                    else (f"node-sharded x{world}: shard scoring, RCCL all-gather per window, replicated resolver"

@@ -131,6 +131,20 @@ struct KsgWinXchg {
   uint32_t wlo[KSG_MAX_WORLD], nw[KSG_MAX_WORLD];
 };
 
+// Device-side progress of a chain of windows (ksg_window.hip): the host enqueues
+// several windows back to back and each kernel reads where the previous one
+// stopped, so there is no host round trip between windows.
+#define KSG_HALT_OVERSIZE 4  // pod `pos` needs the exact per-pod path
+#define KSG_HALT_BADCOUNT 8  // resolver reported an impossible count (a bug)
+#define KSG_HALT_HANG 9      // a ring/draw wait timed out (a bug)
+struct KsgWinRun {
+  uint32_t pos;       // first pod of the next window
+  uint32_t n;         // pods in the batch
+  uint32_t halt;      // KSG_HALT_*: later windows of the chain do nothing
+  uint32_t windows;   // windows resolved
+  uint32_t stops[4];  // windows ended early, by stop reason 1..3
+};
+
 // one record of the per-pod winner exchange (all-gathered across ranks)
 typedef ksg_shard_record KsgRecordHdr;  // public layout (include/kschedgpu.h)
 // followed by nwords_max uint64 tie words (bit set = node at max_score)

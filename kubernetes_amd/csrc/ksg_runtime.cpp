@@ -35,11 +35,11 @@ hipError_t ksg_launch_scan(int R, bool anti, const KsgDev& d, const ksg_pod* pod
                            const uint32_t* ids, int mode, int phase, uint8_t* fail_out,
                            int64_t* score_out, uint8_t* record, int32_t* dpart,
                            const int32_t* dglobal, hipStream_t st);
-hipError_t ksg_launch_win_eval(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids, uint32_t n,
-                               KsgWinSum* sums, uint64_t* wbits, int32_t* wmax, uint32_t ostride,
+hipError_t ksg_launch_win_eval(const KsgDev& d, const ksg_pod* batch, const uint32_t* ids, const KsgWinRun* run,
+                               uint32_t wcap, KsgWinSum* sums, uint64_t* wbits, int32_t* wmax, uint32_t ostride,
                                hipStream_t st);
-hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t n, const KsgWinSum* sums, const KsgWinXchg& x,
-                                  uint64_t* rng, int32_t* out, uint32_t* stat, hipStream_t st);
+hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
+                                  const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st);
 uint32_t ksg_win_max_window(const KsgDev& d);
 hipError_t ksg_launch_decide(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids,
                              const uint8_t* records, uint32_t rec_bytes, uint32_t world,
@@ -128,9 +128,10 @@ struct ksg_ctx {
   uint8_t* d_xsend = nullptr;   // phase A block of this shard (KsgWinXchg layout)
   uint8_t* d_xrecv = nullptr;   // all-gathered blocks of every shard (world > 1)
   size_t win_cap = 0, xsend_cap = 0, xrecv_cap = 0;
-  uint32_t* d_resolved = nullptr;  // {resolved, stop reason}
+  KsgWinRun* d_run = nullptr;      // progress of the window chain (device)
+  KsgWinRun* h_run = nullptr;      // pinned host copy
   uint32_t last_stats[4] = {0, 0, 0, 0};  // windows, stops (service scalar), stops (ties exhausted)
-  hipEvent_t kev[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::vector<hipEvent_t> wev;     // event pairs around the chained window kernels
   double last_kms[3] = {0, 0, 0};  // phase A ms, phase B ms, launches (window path)
   int64_t max_cap = 0, min_cap = 0;
 
@@ -576,8 +577,10 @@ static int create_impl(const ksg_config* cfg, int device, int rank, int world, c
   int rc;
   if (const char* wenv = getenv("KSG_WINDOW")) c->window = (uint32_t)atoi(wenv);
   if ((rc = dalloc(c, &c->d_rng, 1, nullptr)) || (rc = dalloc(c, &c->d_summary, 4, nullptr)) ||
-      (rc = dalloc(c, &c->d_resolved, 4, nullptr)))
+      (rc = dalloc(c, &c->d_run, 1, nullptr)))
     return bail(rc);
+  if ((e = hipHostMalloc((void**)&c->h_run, sizeof(KsgWinRun), hipHostMallocDefault)) != hipSuccess)
+    return bail(fail(c, KSG_ERR_HIP, "hipHostMalloc: %s", hipGetErrorString(e)));
   *out = c;
   return KSG_OK;
 }
@@ -605,15 +608,16 @@ int ksg_destroy(ksg_ctx* c) {
   free_cluster(c);
   void* scratch[] = {c->d_pods, c->d_ids, c->d_fail, c->d_score, c->d_rec_send, c->d_rec_recv, c->d_dpart,
                      c->d_dglobal, c->d_out, c->d_rng, c->d_summary, c->d_patch, c->d_shard_wlo,
-                     c->d_winsum, c->d_xsend, c->d_xrecv, c->d_resolved};
+                     c->d_winsum, c->d_xsend, c->d_xrecv, c->d_run};
   for (void* p : scratch)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->h_xsend) (void)hipHostFree(c->h_xsend);
+  if (c->h_run) (void)hipHostFree(c->h_run);
   if (c->h_xrecv) (void)hipHostFree(c->h_xrecv);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
-  for (auto& e : c->kev)
+  for (auto& e : c->wev)
     if (e) (void)hipEventDestroy(e);
   if (c->st) (void)hipStreamDestroy(c->st);
   delete c;
@@ -981,34 +985,49 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     x.buf = c->world > 1 ? c->d_xrecv : c->d_xsend;
     uint64_t* wbits = reinterpret_cast<uint64_t*>(c->d_xsend);
     int32_t* wmax = reinterpret_cast<int32_t*>(c->d_xsend + (size_t)W * x.ostride * 8);
-    uint32_t pos = 0;
-    if (!c->kev[0])
-      for (auto& e : c->kev) HIPCHK(c, hipEventCreate(&e));
+    // Windows are chained on the device: each kernel reads the window's start
+    // from d_run (written by the previous resolver), so the host enqueues a
+    // round of windows and synchronises once per round, not once per window.
+    uint32_t pos = 0, K = (uint32_t)(((uint64_t)n * 5 + (uint64_t)W * 4 - 1) / ((uint64_t)W * 4)) + 1;
     c->last_kms[0] = c->last_kms[1] = c->last_kms[2] = 0;
     while (pos < n) {
-      const uint32_t w = std::min(W, n - pos);
-      // HIP events on this stream around each kernel (per-kernel device time)
-      HIPCHK(c, hipEventRecord(c->kev[0], c->st));
-      HIPCHK(c, ksg_launch_win_eval(c->dev, c->d_pods + pos, c->d_ids, w, c->d_winsum, wbits, wmax, x.ostride,
-                                    c->st));
-      if (c->world > 1 && (rc = allgather(c, c->d_xsend, c->d_xrecv, x.blk))) return rc;
-      HIPCHK(c, hipEventRecord(c->kev[1], c->st));
-      HIPCHK(c, ksg_launch_win_resolve(full, w, c->d_winsum, x, c->d_rng, c->d_out + pos, c->d_resolved, c->st));
-      HIPCHK(c, hipEventRecord(c->kev[2], c->st));
-      uint32_t st2[2] = {0, 0};
-      HIPCHK(c, hipMemcpyAsync(st2, c->d_resolved, 8, hipMemcpyDeviceToHost, c->st));
+      if (c->wev.size() < 2 * (size_t)K + 1) {
+        const size_t old = c->wev.size();
+        c->wev.resize(2 * (size_t)K + 1, nullptr);
+        for (size_t i = old; i < c->wev.size(); ++i) HIPCHK(c, hipEventCreate(&c->wev[i]));
+      }
+      *c->h_run = KsgWinRun{pos, n, 0, 0, {0, 0, 0, 0}};
+      HIPCHK(c, hipMemcpyAsync(c->d_run, c->h_run, sizeof(KsgWinRun), hipMemcpyHostToDevice, c->st));
+      HIPCHK(c, hipEventRecord(c->wev[0], c->st));
+      for (uint32_t k = 0; k < K; ++k) {
+        // HIP events on this stream around each kernel (per-kernel device time)
+        HIPCHK(c, ksg_launch_win_eval(c->dev, c->d_pods, c->d_ids, c->d_run, W, c->d_winsum, wbits, wmax,
+                                      x.ostride, c->st));
+        if (c->world > 1 && (rc = allgather(c, c->d_xsend, c->d_xrecv, x.blk))) return rc;
+        HIPCHK(c, hipEventRecord(c->wev[2 * k + 1], c->st));
+        HIPCHK(c, ksg_launch_win_resolve(full, W, c->d_run, c->d_winsum, x, c->d_rng, c->d_out, c->st));
+        HIPCHK(c, hipEventRecord(c->wev[2 * k + 2], c->st));
+      }
+      HIPCHK(c, hipMemcpyAsync(c->h_run, c->d_run, sizeof(KsgWinRun), hipMemcpyDeviceToHost, c->st));
       HIPCHK(c, hipStreamSynchronize(c->st));
-      const uint32_t res = st2[0];
-      ++c->last_stats[0];
-      {
+      const KsgWinRun r = *c->h_run;
+      // windows that did work come first in the chain; the rest returned at once
+      const uint32_t eff = std::min(r.windows, K);
+      for (uint32_t k = 0; k < eff; ++k) {
         float a = 0.f, b = 0.f;
-        HIPCHK(c, hipEventElapsedTime(&a, c->kev[0], c->kev[1]));
-        HIPCHK(c, hipEventElapsedTime(&b, c->kev[1], c->kev[2]));
+        HIPCHK(c, hipEventElapsedTime(&a, c->wev[2 * k], c->wev[2 * k + 1]));
+        HIPCHK(c, hipEventElapsedTime(&b, c->wev[2 * k + 1], c->wev[2 * k + 2]));
         c->last_kms[0] += a;
         c->last_kms[1] += b;
-        c->last_kms[2] += 1;
       }
-      if (st2[1] == 4) {
+      c->last_kms[2] += eff;
+      c->last_stats[0] += r.windows;
+      for (int q = 1; q <= 3; ++q) c->last_stats[q] += r.stops[q];
+      if (r.halt == KSG_HALT_HANG) return fail(c, KSG_ERR_STATE, "window resolver: ring wait timed out at pod %u", r.pos);
+      if (r.halt == KSG_HALT_BADCOUNT || r.pos < pos || r.pos > n)
+        return fail(c, KSG_ERR_STATE, "window resolver: bad progress (halt %u, pos %u -> %u)", r.halt, pos, r.pos);
+      pos = r.pos;
+      if (r.halt == KSG_HALT_OVERSIZE) {
         // a pod whose id lists exceed the window record: the exact per-pod path
         if (c->world == 1) {
           HIPCHK(c, ksg_launch_batch(c->R, false, c->dev, c->d_pods + pos, c->d_ids, 1, c->d_rng,
@@ -1020,14 +1039,9 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
         }
         pos += 1;
         ++c->last_stats[3];
-        continue;
       }
-      if (st2[1] == 9) return fail(c, KSG_ERR_STATE, "window resolver: ring wait timed out at pod %u", pos + res);
-      if (res == 0 || res > w) return fail(c, KSG_ERR_STATE, "window resolved %u of %u pods", res, w);
-      pos += res;
-      if (st2[1] == 1) ++c->last_stats[1];
-      if (st2[1] == 2) ++c->last_stats[2];
-      if (st2[1] == 3) ++c->last_stats[3];
+      // next round (rare: stops shortened this round's windows): the rest at W/2 pods per window
+      K = (uint32_t)(((uint64_t)(n - std::min(pos, n)) * 2 + W - 1) / W) + 1;
     }
   } else if (c->world == 1) {
     HIPCHK(c, ksg_launch_batch(c->R, anti_on(c), c->dev, c->d_pods, c->d_ids, n, c->d_rng, c->d_out, c->st));

@@ -66,14 +66,20 @@
 // ---------------------------------------------------------------------------
 // phase A
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, const ksg_pod* __restrict__ pods,
-                                                                 const uint32_t* __restrict__ ids, uint32_t n_pods,
+__global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, const ksg_pod* __restrict__ batch,
+                                                                 const uint32_t* __restrict__ ids,
+                                                                 const KsgWinRun* __restrict__ run, uint32_t wcap,
                                                                  KsgWinSum* __restrict__ sums,
                                                                  uint64_t* __restrict__ wbits,
                                                                  int32_t* __restrict__ wmax, uint32_t ostride) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (KSG_SC_NT / 64) + (threadIdx.x >> 6));
   const uint32_t p0 = blockIdx.y * KSG_PG;
+  // this window = pods [pos, pos + n_pods) of the batch (set by the previous resolver)
+  const uint32_t pos = run->pos, n_batch = run->n;
+  if (run->halt || pos >= n_batch) return;
+  const uint32_t n_pods = min(wcap, n_batch - pos);
+  const ksg_pod* __restrict__ pods = batch + pos;
   // the wave of local word 0 also writes the pods' resolver records, so it runs
   // even on a rank whose shard is empty (every rank resolves every pod)
   if ((w >= d.nwords && w != 0) || p0 >= n_pods) return;  // wave-uniform
@@ -335,19 +341,22 @@ __device__ __forceinline__ void st_rel(uint32_t* p, uint32_t v) {
 }
 
 template <int P, bool STAMP>
-__global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, uint32_t n_pods,
+__global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
                                                                     const KsgWinSum* __restrict__ sums,
                                                                     const KsgWinXchg x, uint64_t* rng_io,
-                                                                    int32_t* __restrict__ out,
-                                                                    uint32_t* stat_out) {
+                                                                    int32_t* __restrict__ out_batch) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t pos = run->pos, n_batch = run->n;
+  if (run->halt || pos >= n_batch) return;  // the chain is done (uniform, before any barrier)
+  const uint32_t n_pods = min(wcap, n_batch - pos);
+  int32_t* __restrict__ out = out_batch + pos;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t nflag = (d.n_services + 31) / 32;
   const uint32_t nshard = d.hi - d.lo;
   const uint32_t nwords = d.nwords;
-  const WinLdsOff o = win_lds_offsets(P, nflag, nshard, n_pods);
+  const WinLdsOff o = win_lds_offsets(P, nflag, nshard, wcap);
   WinCtl* ctl = reinterpret_cast<WinCtl*>(smem + o.ctl);
   RingHdr* r_hdr = reinterpret_cast<RingHdr*>(smem + o.r_hdr);
   uint64_t* r_t0 = reinterpret_cast<uint64_t*>(smem + o.r_t0);
@@ -561,7 +570,6 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
 
   // KSG_DEBUG & 8: the STAMP instantiation accumulates s_memtime per section
   uint64_t t_last = 0, t_acc[STAMP ? 16 : 1] = {};
-  constexpr bool stamp = STAMP;
 #define KSG_STAMP(k)                                     \
   if constexpr (STAMP) {                                 \
     const uint64_t t_now = __builtin_amdgcn_s_memtime(); \
@@ -904,8 +912,17 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
   for (uint32_t t = lane; t < resolved; t += 64) out[t] = L.out[t];
   if (lane == 0) {
     *rng_io = rng0 + (uint64_t)n_draws * 0x9E3779B97F4A7C15ULL;
-    stat_out[0] = resolved;
-    stat_out[1] = reason;
+    if (reason == KSG_STOP_HANG) {
+      run->halt = KSG_HALT_HANG;
+    } else if (reason == KSG_STOP_OVERSIZE) {
+      run->halt = KSG_HALT_OVERSIZE;  // pod pos: the host runs the exact per-pod path, then resumes
+    } else if (resolved == 0 || resolved > n_pods) {
+      run->halt = KSG_HALT_BADCOUNT;
+    } else {
+      run->pos = pos + resolved;
+      run->windows += 1;
+      if (reason >= 1 && reason <= 3) run->stops[reason] += 1;
+    }
   }
 }
 
@@ -919,13 +936,13 @@ static uint32_t win_P(const KsgDev& d) {
 
 static const size_t kWinLdsBudget = 156 * 1024;
 
-hipError_t ksg_launch_win_eval(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids, uint32_t n,
-                               KsgWinSum* sums, uint64_t* wbits, int32_t* wmax, uint32_t ostride,
+hipError_t ksg_launch_win_eval(const KsgDev& d, const ksg_pod* batch, const uint32_t* ids, const KsgWinRun* run,
+                               uint32_t wcap, KsgWinSum* sums, uint64_t* wbits, int32_t* wmax, uint32_t ostride,
                                hipStream_t st) {
   const uint32_t gx = std::max<uint32_t>(1, (d.nwords + KSG_SC_NT / 64 - 1) / (KSG_SC_NT / 64));
-  const dim3 grid(gx, (n + KSG_PG - 1) / KSG_PG);
-  hipLaunchKernelGGL(ksg_win_score_kernel, grid, dim3(KSG_SC_NT), 0, st, d, pods, ids, n, sums, wbits, wmax,
-                     ostride);
+  const dim3 grid(gx, (wcap + KSG_PG - 1) / KSG_PG);
+  hipLaunchKernelGGL(ksg_win_score_kernel, grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, run, wcap, sums, wbits,
+                     wmax, ostride);
   return hipGetLastError();
 }
 
@@ -944,8 +961,8 @@ uint32_t ksg_win_max_window(const KsgDev& d) {
 }
 
 template <int PP, bool ST>
-static hipError_t win_resolve_launch(const KsgDev& d, uint32_t n, size_t lds, const KsgWinSum* sums,
-                                     const KsgWinXchg& x, uint64_t* rng, int32_t* out, uint32_t* stat,
+static hipError_t win_resolve_launch(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run,
+                                     const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
                                      hipStream_t st) {
   static bool once = false;
   if (!once) {
@@ -954,20 +971,20 @@ static hipError_t win_resolve_launch(const KsgDev& d, uint32_t n, size_t lds, co
     (void)hipGetLastError();  // do not leave a sticky error behind
     once = true;
   }
-  hipLaunchKernelGGL((ksg_win_resolve_kernel<PP, ST>), dim3(1), dim3(KSG_RES_NT), lds, st, d, n, sums, x, rng, out,
-                     stat);
+  hipLaunchKernelGGL((ksg_win_resolve_kernel<PP, ST>), dim3(1), dim3(KSG_RES_NT), lds, st, d, wcap, run, sums, x,
+                     rng, out);
   return hipGetLastError();
 }
 
-hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t n, const KsgWinSum* sums, const KsgWinXchg& x,
-                                  uint64_t* rng, int32_t* out, uint32_t* stat, hipStream_t st) {
+hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
+                                  const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
   const uint32_t P = win_P(d);
-  const size_t lds = win_lds_offsets(P, (d.n_services + 31) / 32, d.hi - d.lo, n).total;
+  const size_t lds = win_lds_offsets(P, (d.n_services + 31) / 32, d.hi - d.lo, wcap).total;
   const bool stamp = (d.dbg & 8) != 0;  // KSG_DEBUG & 8: per-section s_memtime stamps
 #define KSG_RES_CASE(PP)                                                                              \
   if (P == PP)                                                                                        \
-    return stamp ? win_resolve_launch<PP, true>(d, n, lds, sums, x, rng, out, stat, st)               \
-                 : win_resolve_launch<PP, false>(d, n, lds, sums, x, rng, out, stat, st);
+    return stamp ? win_resolve_launch<PP, true>(d, wcap, lds, run, sums, x, rng, out, st)             \
+                 : win_resolve_launch<PP, false>(d, wcap, lds, run, sums, x, rng, out, st);
   KSG_RES_CASE(1)
   KSG_RES_CASE(2)
   KSG_RES_CASE(4)
