@@ -5,6 +5,7 @@
 // node-major bit vectors of nw = ceil(N/64) uint64 words, bit n%64 of word n/64):
 //
 //   cap_cpu[N], cap_mem[N]        int64   static   node.Spec.Capacity (milli / bytes)
+//   inv10_cpu[N], inv10_mem[N]    f64     static   10.0 / capacity (window path's LeastRequested)
 //   used_cpu[N], used_mem[N]      int64   mutable  sum of limits of ALL pods on node
 //   static_fit[nw]                uint64  static   AND of LabelsPresence predicates
 //   static_score[N]               int32   static   sum of w * score of pod-independent
@@ -59,6 +60,8 @@ struct KsgDev {
   // arrays
   const int64_t* cap_cpu;
   const int64_t* cap_mem;
+  const double* inv10_cpu;    // 10.0 / cap (0 if cap <= 0): lr_win's reciprocal, static
+  const double* inv10_mem;
   int64_t* used_cpu;
   int64_t* used_mem;
   const uint64_t* static_fit;

@@ -22,6 +22,7 @@
 #include <map>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "ksg_internal.h"
@@ -134,6 +135,16 @@ struct ksg_ctx {
   std::vector<hipEvent_t> wev;     // event pairs around the chained window kernels
   double last_kms[3] = {0, 0, 0};  // phase A ms, phase B ms, launches (window path)
   int64_t max_cap = 0, min_cap = 0;
+
+  // Commits of the last ksg_schedule_batch not yet replayed into the host
+  // mirror: replayed while the next batch runs on the device, or before any
+  // call that reads the mirror (flush_deferred).
+  std::vector<ksg_pod> dfr_pods;
+  std::vector<uint32_t> dfr_ids;
+  std::vector<int32_t> dfr_out;
+  std::unordered_set<uint64_t> dfr_uids;
+  int64_t dfr_sum = 0;   // sum of the deferred pods' requests (cpu + memory), capped
+  bool dfr_neg = false;  // a deferred pod has a negative request
 
   // begin/commit
   bool pending = false;
@@ -461,13 +472,31 @@ bool use_window(ksg_ctx* c, const ksg_pod* pods, uint32_t n) {
     if (c->used_c[i] < 0 || c->used_m[i] < 0) return false;
     mu = std::max<int64_t>(mu, std::max<int64_t>(c->used_c[i], c->used_m[i]));
   }
-  int64_t sum = 0;
+  // commits not yet in the mirror (non-negative: checked by the caller) only add
+  int64_t sum = c->dfr_sum;
   for (uint32_t i = 0; i < n; ++i) {
     if (pods[i].milli_cpu < 0 || pods[i].memory < 0) return false;
     sum += std::min<int64_t>(pods[i].milli_cpu + pods[i].memory, lim);
     if (sum > lim) return false;
   }
   return mu + sum <= lim;
+}
+
+void drop_deferred(ksg_ctx* c) {
+  c->dfr_pods.clear();
+  c->dfr_ids.clear();
+  c->dfr_out.clear();
+  c->dfr_uids.clear();
+  c->dfr_sum = 0;
+  c->dfr_neg = false;
+}
+
+int flush_deferred(ksg_ctx* c) {
+  int rc = KSG_OK;
+  for (size_t i = 0; i < c->dfr_out.size() && rc == KSG_OK; ++i)
+    if (c->dfr_out[i] >= 0) rc = mirror_add(c, (uint32_t)c->dfr_out[i], &c->dfr_pods[i], c->dfr_ids.data(), false);
+  drop_deferred(c);
+  return rc;
 }
 
 int ensure_out(ksg_ctx* c, size_t n) { return grow(c, (void**)&c->d_out, &c->out_cap, n, sizeof(int32_t)); }
@@ -599,9 +628,9 @@ int ksg_destroy(ksg_ctx* c) {
   if (c->dev.dbgbuf) {  // debug stamps (KSG_DEBUG & 8): cycles/64 per resolver section
     int32_t h[16];
     (void)hipMemcpy(h, c->dev.dbgbuf, sizeof h, hipMemcpyDeviceToHost);
-    fprintf(stderr, "ksg stamps (x64 cycles): ring-wait %d head %d recheck[retire %d list %d check %d collect %d] "
-            "select %d commit %d loop-end %d | candidates %d head-retires %d recheck-retires %d cache-misses %d\n",
-            h[0], h[1], h[6], h[8], h[11], h[2], h[3], h[4], h[5], h[7], h[9], h[10], h[12]);
+    fprintf(stderr, "ksg stamps (x64 cycles): ring-wait %d head %d candidates+recheck %d select %d commit %d | "
+            "candidates %d drop-path pods %d unpredicted commits %d | commit: retire %d slot %d services %d rest %d\n",
+            h[0], h[1], h[2], h[3], h[4] + h[10] + h[11] + h[12], h[7], h[8], h[9], h[12], h[10], h[11], h[4]);
   }
   (void)hipSetDevice(c->device);
   if (c->st) (void)hipStreamSynchronize(c->st);
@@ -641,6 +670,7 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
         return fail(c, KSG_ERR_ARG, "node %u has invalid pair id", i);
   }
   free_cluster(c);
+  drop_deferred(c);
   c->N = n_nodes;
   c->nw = (n_nodes + 63) / 64;
   c->n_pairs = n_pairs;
@@ -686,10 +716,12 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   auto* owner = &c->cluster_allocs;
   int rc;
   int64_t *cap_c, *cap_m;
+  double *inv_c, *inv_m;
   uint64_t *sfit, *keymap, *pairmap;
   int32_t *sscore, *anti_dom, *aff_pair;
   const size_t NN = std::max<uint32_t>(n_nodes, 1);
   if ((rc = dalloc(c, &cap_c, NN, owner)) || (rc = dalloc(c, &cap_m, NN, owner)) ||
+      (rc = dalloc(c, &inv_c, NN, owner)) || (rc = dalloc(c, &inv_m, NN, owner)) ||
       (rc = dalloc(c, &d.used_cpu, NN, owner)) || (rc = dalloc(c, &d.used_mem, NN, owner)) ||
       (rc = dalloc(c, &sfit, std::max<uint32_t>(c->nw, 1), owner)) ||
       (rc = dalloc(c, &sscore, NN, owner)) ||
@@ -716,6 +748,14 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   }
   HIPCHK(c, hipMemcpyAsync(cap_c, hc.data(), NN * 8, hipMemcpyHostToDevice, c->st));
   HIPCHK(c, hipMemcpyAsync(cap_m, hm.data(), NN * 8, hipMemcpyHostToDevice, c->st));
+  // correctly rounded on host and device alike (lr_inv10, ksg_device.h)
+  std::vector<double> ic(NN, 0.0), im(NN, 0.0);
+  for (uint32_t i = 0; i < n_nodes; ++i) {
+    ic[i] = hc[i] > 0 ? 10.0 / (double)hc[i] : 0.0;
+    im[i] = hm[i] > 0 ? 10.0 / (double)hm[i] : 0.0;
+  }
+  HIPCHK(c, hipMemcpyAsync(inv_c, ic.data(), NN * 8, hipMemcpyHostToDevice, c->st));
+  HIPCHK(c, hipMemcpyAsync(inv_m, im.data(), NN * 8, hipMemcpyHostToDevice, c->st));
   ksg_node* dn = nullptr;
   uint32_t *dnp = nullptr, *dpk = nullptr;
   int32_t* ddom = nullptr;
@@ -788,6 +828,8 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   d.has_static_fit = ((c->cfg.predicates & KSG_PRED_LABELSPRESENCE) && c->cfg.n_presence > 0) ? 1 : 0;
   d.cap_cpu = cap_c;
   d.cap_mem = cap_m;
+  d.inv10_cpu = inv_c;
+  d.inv10_mem = inv_m;
   d.static_fit = sfit;
   d.static_score = sscore;
   d.keymap = keymap;
@@ -825,6 +867,7 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
 
 int ksg_add_pod(ksg_ctx* c, uint32_t host_id, const ksg_pod* pod, const uint32_t* ids) {
   if (!c || !pod) return KSG_ERR_ARG;
+  if (int rc0 = flush_deferred(c)) return rc0;
   if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
   if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
   int rc = check_pod(c, pod, ids, pod_ids_extent(pod));
@@ -837,6 +880,7 @@ int ksg_add_pod(ksg_ctx* c, uint32_t host_id, const ksg_pod* pod, const uint32_t
 
 int ksg_remove_pod(ksg_ctx* c, uint64_t uid) {
   if (!c) return KSG_ERR_ARG;
+  if (int rc0 = flush_deferred(c)) return rc0;
   if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
   auto it = c->pods.find(uid);
   if (it == c->pods.end()) return fail(c, KSG_ERR_ARG, "unknown pod uid %llu", (unsigned long long)uid);
@@ -887,6 +931,7 @@ int ksg_remove_pod(ksg_ctx* c, uint64_t uid) {
 int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int64_t* max_score,
                        uint32_t* tie_count, uint8_t* fail_codes) {
   if (!c || !pod) return KSG_ERR_ARG;
+  if (int rc0 = flush_deferred(c)) return rc0;
   if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
   HIPCHK(c, hipSetDevice(c->device));
   c->pending = false;
@@ -952,9 +997,11 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
   for (uint32_t i = 0; i < n; ++i) {
     int rc = check_pod(c, pods + i, ids, n_ids);
     if (rc) return rc;
-    if (c->pods.count(pods[i].uid)) return fail(c, KSG_ERR_ARG, "pod %u: duplicate uid", i);
+    if (c->pods.count(pods[i].uid) || c->dfr_uids.count(pods[i].uid))
+      return fail(c, KSG_ERR_ARG, "pod %u: duplicate uid", i);
   }
   int rc;
+  if (c->dfr_neg && (rc = flush_deferred(c))) return rc;
   if ((rc = flush_patches(c))) return rc;
   if ((rc = upload_pods(c, pods, n, ids, n_ids))) return rc;
   if ((rc = ensure_out(c, n))) return rc;
@@ -1009,6 +1056,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
         HIPCHK(c, hipEventRecord(c->wev[2 * k + 2], c->st));
       }
       HIPCHK(c, hipMemcpyAsync(c->h_run, c->d_run, sizeof(KsgWinRun), hipMemcpyDeviceToHost, c->st));
+      if ((rc = flush_deferred(c))) return rc;  // the host mirror catches up while the device works
       HIPCHK(c, hipStreamSynchronize(c->st));
       const KsgWinRun r = *c->h_run;
       // windows that did work come first in the chain; the rest returned at once
@@ -1055,21 +1103,31 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
   HIPCHK(c, hipEventRecord(c->ev1, c->st));
   HIPCHK(c, hipMemcpyAsync(out_nodes, c->d_out, (size_t)n * 4, hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipMemcpyAsync(rng_state, c->d_rng, 8, hipMemcpyDeviceToHost, c->st));
+  if ((rc = flush_deferred(c))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->st));
   float ms = 0.f;
   HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
   c->last_ms = ms;
-  // the device applied every commit; replay them into the host mirror
+  // the device applied every commit; the host mirror replays them later
+  // (flush_deferred), overlapped with the next batch's device work
+  c->dfr_pods.assign(pods, pods + n);
+  c->dfr_ids.assign(ids, ids + n_ids);
+  c->dfr_out.assign(out_nodes, out_nodes + n);
+  c->dfr_uids.reserve(2 * (size_t)n);
   for (uint32_t i = 0; i < n; ++i) {
-    if (out_nodes[i] >= 0) {
-      if ((rc = mirror_add(c, (uint32_t)out_nodes[i], pods + i, ids, false))) return rc;
-    }
+    if (out_nodes[i] < 0) continue;
+    if (!c->dfr_uids.insert(pods[i].uid).second)  // (mirror_add reports it as before, at the replay)
+      return fail(c, KSG_ERR_ARG, "pod %u: duplicate uid within the batch", i);
+    if (pods[i].milli_cpu < 0 || pods[i].memory < 0) c->dfr_neg = true;
+    else c->dfr_sum = std::min<int64_t>(c->dfr_sum + std::min<int64_t>(pods[i].milli_cpu + pods[i].memory,
+                                                                        KSG_WIN_LR_BOUND), KSG_WIN_LR_BOUND + 1);
   }
   return KSG_OK;
 }
 
 int ksg_evaluate(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, uint8_t* fail_out, int64_t* score_out) {
   if (!c || !pod) return KSG_ERR_ARG;
+  if (int rc0 = flush_deferred(c)) return rc0;
   if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
   if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
   HIPCHK(c, hipSetDevice(c->device));

@@ -237,68 +237,70 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
 // ---------------------------------------------------------------------------
 // phase B
 // ---------------------------------------------------------------------------
-// One workgroup. Wave 0 is the RESOLVER: the sequential chain, LDS and ALU
-// only. Waves 1..KSG_RES_NPW are PRODUCERS: pod j of the window is staged by
-// producer (j mod NPW) into ring entry j mod KSG_RING — its record, its T0
-// bitmap (nodes at the snapshot max M0, from phase A's per-word maxima), k0 =
-// |T0|, its tie-break draw r (the splitmix64 output at the pod's draw index,
-// which is the number of earlier window pods that draw: those that neither
-// error nor find no fit) and r mod (k0 - d) for d = 0..63 dropped ties. The
-// pod staging latency, the RNG and the modulo are thus off the resolver's
-// chain. At kernel start the producers also pull the shard's node state
-// (capacity, requested totals) into this XCD's L2, so the resolver's one
-// snapshot load per newly committed node is an L2 hit.
+// One workgroup. Wave 0 is the RESOLVER: the sequential chain, registers and
+// LDS only on its common path. Waves 1..KSG_RES_NPW are PRODUCERS: pod j of the
+// window is staged by producer (j mod NPW) into ring entry j mod KSG_RING —
+// its record, its T0 bitmap (nodes at the snapshot max M0, from phase A's
+// per-word maxima), k0 = |T0|, its tie-break draw r (the splitmix64 output at
+// the pod's draw index = the number of earlier window pods that draw: those
+// that neither error nor find no fit), r mod (k0 - d) for d = 0..63 dropped
+// ties, and the PREDICTED node: the (r mod k0)-th tie of T0 from the top,
+// which is the answer whenever no tie dropped. The producer also loads the
+// predicted node's snapshot state (capacity, requested totals, 10/capacity,
+// the pod's service counts on it) and the pod's service scalars, so a commit
+// to the predicted node needs no global memory access on the chain.
 //
-// Per-window cache of the nodes committed in the window (set C): structure of
-// arrays in LDS indexed by slot (order of first commit). The node state in HBM
-// stays a pristine snapshot while the window resolves; the window's deltas live
-// here and are written back once, at the end of the window.
+// Nodes committed in the window ("slots", set C, at most KSG_MAX_SLOTS) live
+// in the resolver's registers: lane l holds slots l and 64 + l (node, snapshot
+// capacity / requested totals, window delta, 10/capacity, key and service
+// counts). A pod's candidates — slots whose node is in its T0 — are found by
+// each slot lane testing its node's bit in the staged T0 (one LDS read); the
+// re-check then runs on the slot lanes out of registers. The node state in HBM
+// stays the pristine snapshot while the window resolves; the window's deltas
+// are written back once, at the end of the window.
 #define KSG_RES_NT 512
 #define KSG_RES_NPW (KSG_RES_NT / 64 - 1)
 #define KSG_RING 16
 #define KSG_SLOT_KEYS 8
 #define KSG_SLOT_SVCS 12
+#define KSG_MAX_SLOTS 128  // two per resolver lane
 
-struct alignas(16) I64x2 {
-  int64_t c, m;
-};
-struct alignas(16) F64x2 {
-  double c, m;
-};
-struct alignas(16) SlotMeta {
-  uint32_t node;    // shard offset of the node
-  uint16_t nk, ns;  // conflict keys / service entries added by the window
-  uint32_t smask;   // OR of 1 << (service & 31) over the service entries
-  uint32_t pad;
-};
 struct alignas(16) RingHdr {
   int32_t m0;
   uint32_t k0;
-  uint64_t r;         // Int63 draw of the pod
-  uint32_t ready;     // pod index + 1 once the entry is complete
+  uint64_t r;          // Int63 draw of the pod
+  uint32_t ready;      // pod index + 1 once the entry is complete
   uint32_t drawable;
-  uint32_t pad[2];
+  int32_t pred;        // (r mod k0)-th tie of T0 from the top (shard offset), -1: none
+  uint32_t pad;
+  int64_t cap_c, cap_m, used_c, used_m;  // snapshot of pred
+  double inv_c, inv_m;                   // lr_inv10 of pred's capacities
+};
+struct alignas(16) RingSvc {  // per service entry t of the pod (t < n_svcs)
+  int32_t cnt[KSG_SLOT_SVCS];   // svc_cnt[sv][pred] at the snapshot
+  int32_t max[KSG_SLOT_SVCS];   // svc_max[sv]
+  int32_t peer[KSG_SLOT_SVCS];  // svc_peer[sv]
+  int32_t pad[4];
 };
 struct alignas(16) WinCtl {
   uint32_t consumed;    // pods the resolver is done with (ring entries free)
   uint32_t stop;        // the window ended early: producers exit
   uint32_t draw_next;   // next pod allowed to take a draw index
   uint32_t draw_count;  // draws of pods [0, draw_next)
-  uint32_t cache_n;     // (unused)
-  uint32_t pad[3];
+  uint32_t pad[4];
 };
 
 // byte offsets of the resolver's dynamic LDS arrays (host and device agree)
 struct WinLdsOff {
-  uint32_t ctl, r_hdr, r_t0, r_rec, r_mod;  // ring
-  uint32_t cap, snap, dlt, inv, meta, keys, svcs, scnt;  // slots
-  uint32_t peer, list, out, flag, peerset, slot_of, drop;
+  uint32_t ctl, r_hdr, r_t0, r_rec, r_mod, r_svc;  // ring
+  uint32_t keys, svcs, scnt;                       // slots
+  uint32_t peer, out, flag, peerset, drop;
   uint32_t total;
 };
 
 __host__ __device__ constexpr uint32_t win_al16(size_t x) { return (uint32_t)((x + 15) & ~(size_t)15); }
 
-__host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag, uint32_t nshard, uint32_t W) {
+__host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag, uint32_t W) {
   WinLdsOff o;
   uint32_t at = 0;
   o.ctl = at;     at += win_al16(sizeof(WinCtl));
@@ -306,20 +308,14 @@ __host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag,
   o.r_t0 = at;    at += win_al16((size_t)KSG_RING * P * 64 * 8);
   o.r_rec = at;   at += win_al16((size_t)KSG_RING * KSG_WIN_SUM_DWORDS * 4);
   o.r_mod = at;   at += win_al16((size_t)KSG_RING * 64 * 4);
-  o.cap = at;     at += win_al16((size_t)W * sizeof(I64x2));
-  o.snap = at;    at += win_al16((size_t)W * sizeof(I64x2));
-  o.dlt = at;     at += win_al16((size_t)W * sizeof(I64x2));
-  o.inv = at;     at += win_al16((size_t)W * sizeof(F64x2));
-  o.meta = at;    at += win_al16((size_t)W * sizeof(SlotMeta));
-  o.keys = at;    at += win_al16((size_t)W * KSG_SLOT_KEYS * 4);
-  o.svcs = at;    at += win_al16((size_t)W * KSG_SLOT_SVCS * 4);
-  o.scnt = at;    at += win_al16((size_t)W * KSG_SLOT_SVCS * 4);
+  o.r_svc = at;   at += win_al16((size_t)KSG_RING * sizeof(RingSvc));
+  o.keys = at;    at += win_al16((size_t)KSG_MAX_SLOTS * KSG_SLOT_KEYS * 4);
+  o.svcs = at;    at += win_al16((size_t)KSG_MAX_SLOTS * KSG_SLOT_SVCS * 4);
+  o.scnt = at;    at += win_al16((size_t)KSG_MAX_SLOTS * KSG_SLOT_SVCS * 4);
   o.peer = at;    at += win_al16((size_t)W * 2 * 4);
-  o.list = at;    at += win_al16((size_t)W * 4);
   o.out = at;     at += win_al16((size_t)W * 4);
   o.flag = at;    at += win_al16((size_t)nflag * 4);
   o.peerset = at; at += win_al16((size_t)nflag * 4);
-  o.slot_of = at; at += win_al16((size_t)nshard * 2);
   o.drop = at;    at += win_al16((size_t)P * 64 * 8);
   o.total = at;
   return o;
@@ -340,6 +336,37 @@ __device__ __forceinline__ void st_rel(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// The target-th set bit (ascending, 0-based) of the P-word-per-lane bitmap
+// `bits` (lane l owns words l*P + q), given each lane's popcount `cl` and its
+// inclusive prefix `incl`. Wave-uniform result: the word-major bit offset.
+template <int P>
+__device__ __forceinline__ uint32_t select_in_lanes(const uint64_t (&bits)[P], uint32_t cl, uint32_t incl,
+                                                    uint32_t target, uint32_t lane) {
+  const uint32_t excl = incl - cl;
+  const int ol = (int)__builtin_ctzll(__ballot(excl <= target && target < incl));
+  // the owner lane's words, in scalar registers; then the bit by mbcnt rank
+  uint32_t local = target - (uint32_t)__builtin_amdgcn_readlane((int)excl, ol);
+  uint64_t wsel = 0;
+  uint32_t qsel = 0;
+#pragma unroll
+  for (int q = 0; q < P; ++q) {
+    const uint64_t wq = readlane64(bits[q], ol);
+    const uint32_t pc = __popcll(wq);
+    if (qsel == (uint32_t)q) {
+      if (local < pc) {
+        wsel = wq;
+      } else {
+        local -= pc;
+        qsel = q + 1;
+      }
+    }
+  }
+  const uint32_t rank =
+      __builtin_amdgcn_mbcnt_hi((uint32_t)(wsel >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wsel, 0u));
+  const uint32_t bsel = (uint32_t)__builtin_ctzll(__ballot(((wsel >> lane) & 1ULL) && rank == local));
+  return ((uint32_t)ol * P + qsel) * 64 + bsel;
+}
+
 template <int P, bool STAMP>
 __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
                                                                     const KsgWinSum* __restrict__ sums,
@@ -356,24 +383,25 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
   const uint32_t nflag = (d.n_services + 31) / 32;
   const uint32_t nshard = d.hi - d.lo;
   const uint32_t nwords = d.nwords;
-  const WinLdsOff o = win_lds_offsets(P, nflag, nshard, wcap);
+  const WinLdsOff o = win_lds_offsets(P, nflag, wcap);
   WinCtl* ctl = reinterpret_cast<WinCtl*>(smem + o.ctl);
   RingHdr* r_hdr = reinterpret_cast<RingHdr*>(smem + o.r_hdr);
   uint64_t* r_t0 = reinterpret_cast<uint64_t*>(smem + o.r_t0);
   uint32_t* r_rec = reinterpret_cast<uint32_t*>(smem + o.r_rec);
   uint32_t* r_mod = reinterpret_cast<uint32_t*>(smem + o.r_mod);
+  RingSvc* r_svc = reinterpret_cast<RingSvc*>(smem + o.r_svc);
 
   for (uint32_t t = tid; t < KSG_RING; t += KSG_RES_NT) r_hdr[t].ready = 0;
-  if (tid == 0) *ctl = WinCtl{0, 0, 0, 0, 0, {0, 0, 0}};
+  if (tid == 0) *ctl = WinCtl{0, 0, 0, 0, {0, 0, 0, 0}};
   if (wave == 0) {
-    uint64_t* drop = reinterpret_cast<uint64_t*>(smem + o.drop);
     uint32_t* flag = reinterpret_cast<uint32_t*>(smem + o.flag);
     uint32_t* peerset = reinterpret_cast<uint32_t*>(smem + o.peerset);
-    for (uint32_t w = lane; w < P * 64u; w += 64) drop[w] = 0;
+    uint64_t* drop = reinterpret_cast<uint64_t*>(smem + o.drop);
     for (uint32_t w = lane; w < nflag; w += 64) {
       flag[w] = 0;
       peerset[w] = 0;
     }
+    for (uint32_t w = lane; w < P * 64u; w += 64) drop[w] = 0;
   }
   __syncthreads();
   const uint64_t rng0 = *rng_io;
@@ -382,24 +410,25 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
   // producers
   // =========================================================================
   if (wave != 0) {
-    // warm this XCD's L2 with the shard's node state: the resolver's snapshot
-    // loads of committed nodes (same CU, same L2) then hit L2 instead of HBM
+    // warm this XCD's L2 with the node state: the producers' loads of each
+    // pod's predicted node (and the resolver's rare loads) then hit L2
     {
       const uint32_t pw = wave - 1, nt = KSG_RES_NPW * 64;
       const uint32_t n16 = (nshard + 1) / 2;  // 16-byte chunks of one int64 array
       uint64_t acc = 0;
-      const int64_t* arr[4] = {d.cap_cpu + d.lo, d.cap_mem + d.lo, d.used_cpu + d.lo, d.used_mem + d.lo};
+      const int64_t* arr[6] = {d.cap_cpu + d.lo, d.cap_mem + d.lo, d.used_cpu + d.lo, d.used_mem + d.lo,
+                               reinterpret_cast<const int64_t*>(d.inv10_cpu) + d.lo,
+                               reinterpret_cast<const int64_t*>(d.inv10_mem) + d.lo};
+      for (uint32_t t = pw * 64 + lane; t < n16; t += nt) {
+        const uint32_t idx = 2 * t + 1 < nshard ? 2 * t + 1 : 2 * t;
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
-        for (uint32_t t = pw * 64 + lane; t < n16; t += nt) {
-          const uint32_t idx = 2 * t + 1 < nshard ? 2 * t + 1 : 2 * t;
-          acc ^= (uint64_t)arr[a][idx];
-        }
+        for (int a = 0; a < 6; ++a) acc ^= (uint64_t)arr[a][idx];  // six loads in flight
+      }
       if (acc == 0x5bd1e995a5a5a5a5ULL) ctl->pad[0] = 1;  // keeps the loads
     }
     const uint32_t* recs = reinterpret_cast<const uint32_t*>(sums);
-    // this lane's words lane*P + q: the rank block and row offset phase A wrote them at
-    // (byte offsets into x.buf; ~0u = no such word)
+    // this lane's words lane*P + q: byte offsets of the rank block and row phase
+    // A wrote them at (~0u = no such word)
     uint32_t wb_at[P], wm_at[P];
 #pragma unroll
     for (int q = 0; q < P; ++q) {
@@ -438,11 +467,11 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
         t0[q] = (m0 != KSG_S32_NONE && mw[q] == m0) ? t0[q] : 0ULL;
         cnt += __popcll(t0[q]);
       }
-      const uint32_t k0 = wave_total_add(cnt);
+      const uint32_t incl = dpp_scan_add(cnt);
+      const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
       const bool drawable = __builtin_amdgcn_readlane(rec, WS_ERR) == 0 && m0 != KSG_S32_NONE;
 
-      // draw index = draws of the window pods before j (taken before the cache
-      // fill so the chain between producers stays short)
+      // draw index = draws of the window pods before j
       for (uint32_t spin = 0;; ++spin) {
         if (ld_acq(&ctl->stop) || spin > KSG_SPIN_LIMIT) return;
         if (ld_acq(&ctl->draw_next) == j) break;
@@ -459,16 +488,54 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
       uint32_t mv = 0;
       if (drawable && lane < k0) mv = umod64_32(r, k0 - lane);
 
+      // predicted node: the (r mod k0)-th tie from the top (nothing dropped)
+      int32_t pred = -1;
+      int64_t pv = 0;  // lanes 0..3: cap_c, cap_m, used_c, used_m of pred
+      double pinv = 0.0;
+      const uint32_t n_svcs = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NSS) >> 16;
+      const uint32_t nk = ((uint32_t)__builtin_amdgcn_readlane(rec, WS_NPP) & 0xffff) +
+                          ((uint32_t)__builtin_amdgcn_readlane(rec, WS_NPP) >> 16);
+      const uint32_t n_sel = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NSS) & 0xffff;
+      const bool inl = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NINL) <= KSG_WIN_INLINE &&
+                       n_svcs <= KSG_SLOT_SVCS;
+      // the pod's services are record dwords WS_IDS + nk + n_sel + t (all lanes shuffle)
+      const uint32_t t_sv = lane < n_svcs ? lane : 0u;
+      const uint32_t my_sv = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + t_sv, 63u), 64);
+      int32_t s_cnt = 0, s_max = 0, s_peer = 0;
+      if (drawable) {
+        const uint32_t ix0 = __builtin_amdgcn_readfirstlane(mv);  // lane 0: r mod k0
+        pred = (int32_t)select_in_lanes<P>(t0, cnt, incl, k0 - 1 - ix0, lane);
+        const uint32_t pn = d.lo + (uint32_t)pred;
+        if (lane == 0) pv = d.cap_cpu[pn];
+        else if (lane == 1) pv = d.cap_mem[pn];
+        else if (lane == 2) pv = d.used_cpu[pn];
+        else if (lane == 3) pv = d.used_mem[pn];
+        if (inl && lane < n_svcs) {
+          s_cnt = d.svc_cnt[(size_t)my_sv * d.n_nodes + pn];
+          s_max = d.svc_max[my_sv];
+          s_peer = d.svc_peer[my_sv];
+        }
+        pinv = lr_inv10(pv);
+      }
+
       // publish the entry
       r_mod[e * 64 + lane] = mv;
       if (lane < KSG_WIN_SUM_DWORDS) r_rec[e * KSG_WIN_SUM_DWORDS + lane] = rec;
 #pragma unroll
       for (int q = 0; q < P; ++q) r_t0[(size_t)e * P * 64 + lane * P + q] = t0[q];
+      if (inl && lane < n_svcs) {
+        r_svc[e].cnt[lane] = s_cnt;
+        r_svc[e].max[lane] = s_max;
+        r_svc[e].peer[lane] = s_peer;
+      }
+      if (lane < 4) (&r_hdr[e].cap_c)[lane] = pv;
+      if (lane < 2) (&r_hdr[e].inv_c)[lane] = pinv;
       if (lane == 0) {
         r_hdr[e].m0 = m0;
         r_hdr[e].k0 = k0;
         r_hdr[e].r = r;
         r_hdr[e].drawable = drawable;
+        r_hdr[e].pred = pred;
         st_rel(&r_hdr[e].ready, j + 1);
       }
     }
@@ -479,25 +546,14 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
   // resolver (wave 0)
   // =========================================================================
   __builtin_amdgcn_s_setprio(3);
-  struct {
-    I64x2 *cap, *snap, *dlt;
-    F64x2* inv;
-    SlotMeta* meta;
-    uint32_t *keys, *svcs;
-    int32_t* scnt;
-    uint32_t *peer, *list;
-    int32_t* out;
-    uint32_t *flag, *peerset;
-    uint16_t* slot_of;
-    uint64_t* drop;
-  } L = {reinterpret_cast<I64x2*>(smem + o.cap),      reinterpret_cast<I64x2*>(smem + o.snap),
-         reinterpret_cast<I64x2*>(smem + o.dlt),      reinterpret_cast<F64x2*>(smem + o.inv),
-         reinterpret_cast<SlotMeta*>(smem + o.meta),  reinterpret_cast<uint32_t*>(smem + o.keys),
-         reinterpret_cast<uint32_t*>(smem + o.svcs),  reinterpret_cast<int32_t*>(smem + o.scnt),
-         reinterpret_cast<uint32_t*>(smem + o.peer),  reinterpret_cast<uint32_t*>(smem + o.list),
-         reinterpret_cast<int32_t*>(smem + o.out),    reinterpret_cast<uint32_t*>(smem + o.flag),
-         reinterpret_cast<uint32_t*>(smem + o.peerset), reinterpret_cast<uint16_t*>(smem + o.slot_of),
-         reinterpret_cast<uint64_t*>(smem + o.drop)};
+  uint32_t* const L_keys = reinterpret_cast<uint32_t*>(smem + o.keys);
+  uint32_t* const L_svcs = reinterpret_cast<uint32_t*>(smem + o.svcs);
+  int32_t* const L_scnt = reinterpret_cast<int32_t*>(smem + o.scnt);
+  uint32_t* const L_peer = reinterpret_cast<uint32_t*>(smem + o.peer);
+  int32_t* const L_out = reinterpret_cast<int32_t*>(smem + o.out);
+  uint64_t* const L_drop = reinterpret_cast<uint64_t*>(smem + o.drop);
+  uint32_t* const L_flag = reinterpret_cast<uint32_t*>(smem + o.flag);
+  uint32_t* const L_peerset = reinterpret_cast<uint32_t*>(smem + o.peerset);
   const bool spread_on = d.w_spread != 0;
   const bool aff_on = (d.preds & KSG_PRED_SERVICEAFFINITY) && d.n_aff > 0;
   const bool res_on = (d.preds & KSG_PRED_PODFITSRESOURCES) != 0;
@@ -505,62 +561,73 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
   const bool disk_on = (d.preds & KSG_PRED_NODISKCONFLICT) != 0;
   uint32_t resolved = n_pods, reason = 0, n_slots = 0, n_peer = 0, n_draws = 0;
 
-  uint64_t cm[P];  // C: nodes committed in this window (lane owns words lane*P + q)
-#pragma unroll
-  for (int q = 0; q < P; ++q) cm[q] = 0;
+  // slots h*64 + lane (h = 0, 1) of this lane
+  uint32_t sn[2] = {0, 0};                // node (shard offset)
+  int64_t cap_c[2] = {0, 0}, cap_m[2] = {0, 0};
+  int64_t snp_c[2] = {0, 0}, snp_m[2] = {0, 0};
+  int64_t dl_c[2] = {0, 0}, dl_m[2] = {0, 0};
+  double inv_c[2] = {0.0, 0.0}, inv_m[2] = {0.0, 0.0};
+  uint32_t s_nk[2] = {0, 0}, s_ns[2] = {0, 0}, s_mask[2] = {0, 0};
 
-  // pending global loads of the last commit (retired lazily): the snapshot of
-  // a newly committed node (issued first, so waiting for it does not wait for
-  // the service loads), then the committing pod's service scalars
+  // Values a commit loads from HBM when the node was not the predicted one:
+  // the node's snapshot (owner lane) and the pod's service counts on it
+  // (service lanes); retire_* moves them into the slot state once they land.
   bool p_snap = false, p_svc = false;
-  uint32_t p_slot = 0, p_base = 0, p_nsv = 0, p_node = 0;
-  int64_t p_v = 0;                           // lanes 0..3: cap_c, cap_m, used_c, used_m
-  int32_t p_cnt = 0, p_max = 0, p_peer = 0;  // service lanes 32+t
-  uint32_t p_sv = 0xffffffffu;               // service lanes 32+t
+  uint32_t p_slot = 0, p_node = 0, p_base = 0, p_nsv = 0;
+  int64_t pl_cc = 0, pl_cm = 0, pl_uc = 0, pl_um = 0;
+  double pl_ic = 0.0, pl_im = 0.0;
+  int32_t pl_cnt = 0, pl_max = 0, pl_peer = 0;
+  uint32_t pl_sv = 0;
   auto retire_snap = [&]() {
     if (!p_snap) return;
     p_snap = false;
-    if (lane < 4) {
-      int64_t* dst = lane < 2 ? &L.cap[p_slot].c : &L.snap[p_slot].c;
-      dst[lane & 1] = p_v;
+    if (lane == (p_slot & 63)) {
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+        if (hh == (int)(p_slot >> 6)) {
+          cap_c[hh] = pl_cc;
+          cap_m[hh] = pl_cm;
+          snp_c[hh] = pl_uc;
+          snp_m[hh] = pl_um;
+          inv_c[hh] = pl_ic;
+          inv_m[hh] = pl_im;
+        }
     }
-    const int64_t cc = readlane64((uint64_t)p_v, 0), cmm = readlane64((uint64_t)p_v, 1);
-    if (lane == 0) L.inv[p_slot] = F64x2{lr_inv10(cc), lr_inv10(cmm)};
-    lds_fence();
   };
+  // service entries of the last commit: snapshot counts, the maxCount /
+  // ServiceAffinity-peer flags later pods of those services stop on, peers
   auto retire_svc = [&]() {
     if (!p_svc) return;
     p_svc = false;
-    const uint32_t t = lane - 32;
-    const bool mine = lane >= 32 && t < p_nsv;
+    const bool sv_lane = lane < p_nsv;
     bool changed = false;
-    if (mine) {
-      const uint32_t a = p_base + t;
-      const uint32_t* sl = L.svcs + (size_t)p_slot * KSG_SLOT_SVCS;
-      uint32_t before = 0;  // in-window commits of this service on this node before this one
-      for (uint32_t b = 0; b < a; ++b) before += sl[b] == p_sv;
-      L.scnt[(size_t)p_slot * KSG_SLOT_SVCS + a] = p_cnt;
-      if (spread_on && p_cnt + (int32_t)before + 1 > p_max) changed = true;  // maxCount rises
-      if (p_peer == -1 && !((L.peerset[p_sv >> 5] >> (p_sv & 31)) & 1u)) changed |= aff_on;
+    if (sv_lane) {
+      // in-window commits of this service on this node before this one
+      const uint32_t* sl = L_svcs + (size_t)p_slot * KSG_SLOT_SVCS;
+      uint32_t before = 0;
+      for (uint32_t b = 0; b < p_base; ++b) before += sl[b] == pl_sv;
+      if (spread_on && pl_cnt + (int32_t)before + 1 > pl_max) changed = true;  // maxCount rises
+      if (aff_on && pl_peer == -1 && !((L_peerset[pl_sv >> 5] >> (pl_sv & 31)) & 1u)) changed = true;
+      L_scnt[(size_t)p_slot * KSG_SLOT_SVCS + p_base + lane] = pl_cnt;
     }
     // first commit of a service with no peer yet: record the peer (lane 0 applies, in order)
-    uint64_t pm = __ballot(mine && p_peer == -1);
+    uint64_t pm = __ballot(sv_lane && pl_peer == -1);
     while (pm) {
       const uint32_t b = __builtin_ctzll(pm);
       pm &= pm - 1;
-      const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)p_sv, (int)b);
-      const bool fresh = !((L.peerset[fsv >> 5] >> (fsv & 31)) & 1u);
+      const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)pl_sv, (int)b);
+      const bool fresh = !((L_peerset[fsv >> 5] >> (fsv & 31)) & 1u);
       if (fresh) {
         if (lane == 0) {
-          L.peerset[fsv >> 5] |= 1u << (fsv & 31);
-          L.peer[2 * n_peer] = fsv;
-          L.peer[2 * n_peer + 1] = d.lo + p_node;
+          L_peerset[fsv >> 5] |= 1u << (fsv & 31);
+          L_peer[2 * n_peer] = fsv;
+          L_peer[2 * n_peer + 1] = d.lo + p_node;
         }
         ++n_peer;
         lds_fence();
       }
     }
-    if (changed) atomicOr(&L.flag[p_sv >> 5], 1u << (p_sv & 31));
+    if (changed) atomicOr(&L_flag[pl_sv >> 5], 1u << (pl_sv & 31));
     lds_fence();
   };
   auto retire = [&]() {
@@ -569,12 +636,17 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
   };
 
   // KSG_DEBUG & 8: the STAMP instantiation accumulates s_memtime per section
-  uint64_t t_last = 0, t_acc[STAMP ? 16 : 1] = {};
-#define KSG_STAMP(k)                                     \
-  if constexpr (STAMP) {                                 \
-    const uint64_t t_now = __builtin_amdgcn_s_memtime(); \
-    t_acc[k] += t_now - t_last;                          \
-    t_last = t_now;                                      \
+  // (lane k accumulates section k in a VGPR: no scalar registers taken from the chain)
+  uint64_t t_last = 0, t_acc = 0;
+#define KSG_STAMP(k)                                         \
+  if constexpr (STAMP) {                                     \
+    const uint64_t t_now = __builtin_amdgcn_s_memtime();     \
+    t_acc += lane == (uint32_t)(k) ? t_now - t_last : 0ULL;  \
+    t_last = t_now;                                          \
+  }
+#define KSG_COUNT(k, v)                              \
+  if constexpr (STAMP) {                             \
+    t_acc += lane == (uint32_t)(k) ? (uint64_t)(v) : 0ULL; \
   }
   if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
 
@@ -595,166 +667,110 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
     KSG_STAMP(0)
     // ---- head
     const uint32_t rec = lane < KSG_WIN_SUM_DWORDS ? r_rec[e * KSG_WIN_SUM_DWORDS + lane] : 0u;
-    uint64_t t0[P];
-#pragma unroll
-    for (int q = 0; q < P; ++q) t0[q] = r_t0[(size_t)e * P * 64 + lane * P + q];
     const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
     const uint32_t k0 = __builtin_amdgcn_readfirstlane(r_hdr[e].k0);
     const int32_t s = (int32_t)__builtin_amdgcn_readlane(rec, WS_SVC);
-    if (s >= 0 && (spread_on || aff_on)) {
-      // the last commit's services may flag this pod's service: retire it first
-      if (p_svc && __ballot(lane >= 32 && lane - 32 < p_nsv && p_sv == (uint32_t)s)) {
-        if constexpr (STAMP) t_acc[9] += 64;
-        retire_svc();
-      }
-      if ((L.flag[s >> 5] >> (s & 31)) & 1u) {
-        resolved = i;  // a service scalar this pod reads changed in the window
-        reason = KSG_STOP_SERVICE;
-        break;
-      }
+    if (s >= 0 && (spread_on || aff_on) && ((L_flag[s >> 5] >> (s & 31)) & 1u)) {
+      resolved = i;  // a service scalar this pod reads changed in the window
+      reason = KSG_STOP_SERVICE;
+      break;
+    }
+    if (__builtin_amdgcn_readlane(rec, WS_ERR)) {
+      if (lane == 0) L_out[i] = KSG_OUT_ERROR;
+      if (lane == 0) st_rel(&ctl->consumed, i + 1);
+      continue;
+    }
+    if (m0 == KSG_S32_NONE) {
+      if (lane == 0) L_out[i] = KSG_OUT_NOFIT;  // nothing fit at the snapshot; commits only remove fits
+      if (lane == 0) st_rel(&ctl->consumed, i + 1);
+      continue;
+    }
+    const uint32_t npp = __builtin_amdgcn_readlane(rec, WS_NPP), nss = __builtin_amdgcn_readlane(rec, WS_NSS);
+    const int64_t req_c = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_CPU) |
+                                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_CPU + 1) << 32));
+    const int64_t req_m = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_MEM) |
+                                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_MEM + 1) << 32));
+    const bool zero_req = req_c == 0 && req_m == 0;
+    const int32_t smax = (int32_t)__builtin_amdgcn_readlane(rec, WS_SMAX);
+    const uint32_t n_ports = npp & 0xffff, n_pds = npp >> 16, n_sel = nss & 0xffff, n_svcs = nss >> 16;
+    const uint32_t nk = n_ports + n_pds;
+    if (__builtin_amdgcn_readlane(rec, WS_NINL) > KSG_WIN_INLINE || nk > KSG_SLOT_KEYS ||
+        n_svcs > KSG_SLOT_SVCS) {
+      // lists longer than the record / a slot: the exact per-pod kernel takes it
+      resolved = i;
+      reason = i == 0 ? KSG_STOP_OVERSIZE : KSG_STOP_SLOT;
+      break;
     }
     KSG_STAMP(1)
-    if (__builtin_amdgcn_readlane(rec, WS_ERR)) {
-      if (lane == 0) L.out[i] = KSG_OUT_ERROR;
-    } else if (m0 == KSG_S32_NONE) {
-      if (lane == 0) L.out[i] = KSG_OUT_NOFIT;  // nothing fit at the snapshot; commits only remove fits
-    } else {
-      const uint32_t npp = __builtin_amdgcn_readlane(rec, WS_NPP), nss = __builtin_amdgcn_readlane(rec, WS_NSS);
-      const int64_t req_c = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_CPU) |
-                                      ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_CPU + 1) << 32));
-      const int64_t req_m = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_MEM) |
-                                      ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_MEM + 1) << 32));
-      const bool zero_req = req_c == 0 && req_m == 0;
-      const int32_t smax = (int32_t)__builtin_amdgcn_readlane(rec, WS_SMAX);
-      const uint32_t n_ports = npp & 0xffff, n_pds = npp >> 16, n_sel = nss & 0xffff, n_svcs = nss >> 16;
-      const uint32_t nk = n_ports + n_pds;
-      if (__builtin_amdgcn_readlane(rec, WS_NINL) > KSG_WIN_INLINE || nk > KSG_SLOT_KEYS ||
-          n_svcs > KSG_SLOT_SVCS) {
-        // lists longer than the record / a slot: the exact per-pod kernel takes it
-        resolved = i;
-        reason = i == 0 ? KSG_STOP_OVERSIZE : KSG_STOP_SLOT;
-        break;
-      }
 
-      // ---- candidates: snapshot ties committed earlier in the window (T0 ∩ C)
-      uint64_t cand[P];
-      uint32_t cnt = 0;
+    // ---- candidates: slots whose node is a snapshot tie (T0 ∩ C); re-check them
+    const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
+    uint64_t dmask[2] = {0, 0};
 #pragma unroll
-      for (int q = 0; q < P; ++q) {
-        cand[q] = t0[q] & cm[q];
-        cnt += __popcll(cand[q]);
-      }
-      uint64_t dw[P];
-#pragma unroll
-      for (int q = 0; q < P; ++q) dw[q] = 0;
-      const uint32_t incl_c = dpp_scan_add(cnt);
-      const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl_c, 63);
-      if constexpr (STAMP) t_acc[7] += total * 64;
-      if (total) {
-        if (p_snap || p_svc) {
-          // the last committed node is a candidate and a value it needs is in flight
-          const uint32_t pw = p_node >> 6, po = pw / P, pq = pw % P;
-          bool hit = false;
-#pragma unroll
-          for (int q = 0; q < P; ++q)
-            if ((uint32_t)q == pq) hit = (cand[q] >> (p_node & 63)) & 1ULL;
-          if (__builtin_amdgcn_readlane((int)hit, (int)po)) {
-            if constexpr (STAMP) t_acc[10] += 64;
-            retire_snap();
-            if (p_svc && spread_on && s >= 0 &&
-                __ballot(lane >= 32 && lane - 32 < p_nsv && p_sv == (uint32_t)s) != 0)
-              retire_svc();
+    for (int h = 0; h < 2; ++h) {
+      if (h * 64 >= (int)n_slots) break;
+      bool cand = false;
+      if ((uint32_t)h * 64 + lane < n_slots) cand = (t0e[sn[h] >> 6] >> (sn[h] & 63)) & 1ULL;
+      if (__ballot(cand) == 0) continue;
+      bool drop = false;
+      if (cand) {
+        // the node fit the pod at the snapshot; only the window's deltas can change that
+        const int64_t now_c = (int64_t)((uint64_t)snp_c[h] + (uint64_t)dl_c[h]);
+        const int64_t now_m = (int64_t)((uint64_t)snp_m[h] + (uint64_t)dl_m[h]);
+        if (res_on && !zero_req) {  // PodFitsResources
+          const bool fc = cap_c[h] == 0 || cap_c[h] - now_c >= req_c;
+          const bool fm = cap_m[h] == 0 || cap_m[h] - now_m >= req_m;
+          drop = !(fc && fm);
+        }
+        if (nk && !drop && s_nk[h]) {  // PodFitsPorts / NoDiskConflict against the window's keys
+          const uint32_t* ks = L_keys + (size_t)(h * 64 + lane) * KSG_SLOT_KEYS;
+          for (uint32_t a = 0; a < s_nk[h]; ++a) {
+            const uint32_t key = ks[a];
+            if (ports_on)
+              for (uint32_t b = 0; b < n_ports; ++b)
+                drop |= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + b) == key;
+            if (disk_on)
+              for (uint32_t b = 0; b < n_pds; ++b)
+                drop |= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + n_ports + b) == key;
           }
         }
-        KSG_STAMP(6)
-        uint32_t pos = incl_c - cnt;
-#pragma unroll
-        for (int q = 0; q < P; ++q) {
-          uint64_t x = cand[q];
-          while (x) {
-            L.list[pos++] = (lane * P + q) * 64 + __builtin_ctzll(x);
-            x &= x - 1;
-          }
+        if (!drop && d.w_lr) {  // LeastRequested can only fall as requested grows
+          const int32_t lr_now = lr_win(now_c + req_c, cap_c[h], inv_c[h]) + lr_win(now_m + req_m, cap_m[h], inv_m[h]);
+          const int32_t lr_snap =
+              lr_win(snp_c[h] + req_c, cap_c[h], inv_c[h]) + lr_win(snp_m[h] + req_m, cap_m[h], inv_m[h]);
+          drop = (lr_now >> 1) != (lr_snap >> 1);
         }
-        lds_fence();
-        KSG_STAMP(8)
-        for (uint32_t base = 0; base < total; base += 64) {
-          const uint32_t t = base + lane;
-          if (t < total) {
-            // the node fit the pod at the snapshot; only the window's deltas can change that
-            const uint32_t woff = L.list[t];
-            const uint32_t sl = L.slot_of[woff];
-            const I64x2 cap = L.cap[sl], snp = L.snap[sl], dl = L.dlt[sl];
-            const int64_t now_c = (int64_t)((uint64_t)snp.c + (uint64_t)dl.c);
-            const int64_t now_m = (int64_t)((uint64_t)snp.m + (uint64_t)dl.m);
-            const SlotMeta me = L.meta[sl];
-            bool drop = false;
-            if (res_on && !zero_req) {  // PodFitsResources
-              const bool fc = cap.c == 0 || cap.c - now_c >= req_c;
-              const bool fm = cap.m == 0 || cap.m - now_m >= req_m;
-              drop = !(fc && fm);
+        if (!drop && spread_on && s >= 0 && ((s_mask[h] >> (s & 31)) & 1u)) {
+          // ServiceSpreading under an unchanged maxCount
+          const uint32_t* sv = L_svcs + (size_t)(h * 64 + lane) * KSG_SLOT_SVCS;
+          const int32_t* sc = L_scnt + (size_t)(h * 64 + lane) * KSG_SLOT_SVCS;
+          int32_t delta = 0, snapc = 0;
+          for (uint32_t a = 0; a < s_ns[h]; ++a)
+            if (sv[a] == (uint32_t)s) {
+              snapc = sc[a];
+              ++delta;
             }
-            if (nk && !drop) {  // PodFitsPorts / NoDiskConflict against the window's keys
-              const uint32_t* ks = L.keys + (size_t)sl * KSG_SLOT_KEYS;
-              for (uint32_t a = 0; a < me.nk; ++a) {
-                const uint32_t key = ks[a];
-                if (ports_on)
-                  for (uint32_t b = 0; b < n_ports; ++b)
-                    drop |= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + b) == key;
-                if (disk_on)
-                  for (uint32_t b = 0; b < n_pds; ++b)
-                    drop |= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + n_ports + b) == key;
-              }
-            }
-            if (!drop && d.w_lr) {  // LeastRequested can only fall as requested grows
-              const F64x2 iv = L.inv[sl];
-              const int32_t lr_now = lr_win(now_c + req_c, cap.c, iv.c) + lr_win(now_m + req_m, cap.m, iv.m);
-              const int32_t lr_snap = lr_win(snp.c + req_c, cap.c, iv.c) + lr_win(snp.m + req_m, cap.m, iv.m);
-              drop = (lr_now >> 1) != (lr_snap >> 1);
-            }
-            if (!drop && spread_on && s >= 0 && ((me.smask >> (s & 31)) & 1u)) {
-              // ServiceSpreading under an unchanged maxCount
-              const uint32_t* sv = L.svcs + (size_t)sl * KSG_SLOT_SVCS;
-              int32_t delta = 0, snapc = 0;
-              for (uint32_t a = 0; a < me.ns; ++a)
-                if (sv[a] == (uint32_t)s) {
-                  snapc = L.scnt[(size_t)sl * KSG_SLOT_SVCS + a];
-                  ++delta;
-                }
-              if (delta) drop = frac10_f32((int64_t)smax - snapc - delta, smax) != frac10_f32((int64_t)smax - snapc, smax);
-            }
-            if (drop) atomicOr(reinterpret_cast<unsigned long long*>(L.drop + (woff >> 6)), 1ULL << (woff & 63));
-          }
-        }
-        lds_fence();
-        KSG_STAMP(11)
-        // each lane collects the dropped bits of its own words and clears them
-        if (cnt) {
-#pragma unroll
-          for (int q = 0; q < P; ++q)
-            if (cand[q]) {
-              dw[q] = L.drop[lane * P + q];
-              L.drop[lane * P + q] = 0;
-            }
+          if (delta) drop = frac10_f32((int64_t)smax - snapc - delta, smax) != frac10_f32((int64_t)smax - snapc, smax);
         }
       }
-      KSG_STAMP(2)
-      // ---- selection: k live ties, ix-th in descending rank = (k-1-ix)-th ascending
-      uint64_t live[P];
-      uint32_t cl = 0;
-#pragma unroll
-      for (int q = 0; q < P; ++q) {
-        live[q] = t0[q] & ~dw[q];
-        cl += __popcll(live[q]);
-      }
-      const uint32_t incl = dpp_scan_add(cl);
-      const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-      if (k == 0) {
-        resolved = i;  // every snapshot tie got worse: needs a fresh snapshot
-        reason = KSG_STOP_EXHAUSTED;
-        break;
-      }
-      const uint32_t dropped = k0 - k;
+      dmask[h] = __ballot(drop);
+      if (drop) atomicOr(reinterpret_cast<unsigned long long*>(L_drop + (sn[h] >> 6)), 1ULL << (sn[h] & 63));
+      KSG_COUNT(7, __popcll(__ballot(cand)) * 64)
+    }
+    KSG_STAMP(2)
+    // ---- selection: k live ties, ix-th in descending rank = (k-1-ix)-th ascending
+    const uint32_t dropped = __popcll(dmask[0]) + __popcll(dmask[1]);
+    if (dropped >= k0) {
+      resolved = i;  // every snapshot tie got worse: needs a fresh snapshot
+      reason = KSG_STOP_EXHAUSTED;
+      break;
+    }
+    const uint32_t k = k0 - dropped;
+    uint32_t woff;
+    if (dropped == 0) {
+      woff = (uint32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].pred);  // staged by the producer
+    } else {
+      KSG_COUNT(8, 64)
       uint32_t ix;
       if (dropped < 64 && !(d.dbg & 32)) {  // KSG_DEBUG & 32: always the direct modulo
         ix = __builtin_amdgcn_readfirstlane(r_mod[e * 64 + dropped]);
@@ -764,152 +780,187 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
                            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r_hdr[e].r);
         ix = umod64_32(r, k);
       }
-      const uint32_t target = k - 1 - ix;
-      const uint32_t excl = incl - cl;
-      const int ol = (int)__builtin_ctzll(__ballot(excl <= target && target < incl));
-      // the owner lane's words, in scalar registers; then the bit by mbcnt rank
-      uint32_t local = target - (uint32_t)__builtin_amdgcn_readlane((int)excl, ol);
-      uint64_t wsel = 0;
-      uint32_t qsel = 0;
+      // live ties: T0 minus the dropped slot nodes, scattered into L_drop by the
+      // dropping lanes (lane l owns words l*P + q and clears them for the next pod)
+      lds_fence();
+      uint64_t live[P];
 #pragma unroll
       for (int q = 0; q < P; ++q) {
-        const uint64_t wq = readlane64(live[q], ol);
-        const uint32_t pc = __popcll(wq);
-        if (qsel == (uint32_t)q) {
-          if (local < pc) {
-            wsel = wq;
-          } else {
-            local -= pc;
-            qsel = q + 1;
-          }
-        }
+        live[q] = t0e[lane * P + q] & ~L_drop[lane * P + q];
+        L_drop[lane * P + q] = 0;
       }
-      const uint32_t rank =
-          __builtin_amdgcn_mbcnt_hi((uint32_t)(wsel >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wsel, 0u));
-      const uint32_t bsel = (uint32_t)__builtin_ctzll(__ballot(((wsel >> lane) & 1ULL) && rank == local));
-      const uint32_t woff = ((uint32_t)ol * P + qsel) * 64 + bsel;
-      const uint32_t wn = d.lo + woff;
-      KSG_STAMP(3)
-      // ---- AssumePod into the window cache; HBM is written back at window end
-      retire();  // the previous commit's loads land before this commit reuses the registers
-      const uint32_t cw = woff >> 6, co = cw / P, cq = cw % P;
-      uint64_t cmw = 0;
+      uint32_t cl = 0;
 #pragma unroll
-      for (int q = 0; q < P; ++q)
-        if ((uint32_t)q == cq) cmw = cm[q];
-      const bool in_c = (readlane64(cmw, (int)co) >> (woff & 63)) & 1ULL;
-      uint32_t slot = n_slots, base_nk = 0, base_ns = 0, smask_old = 0;
-      bool snap_pending = false;
-      if (in_c) {
-        slot = L.slot_of[woff];
-        const SlotMeta me = L.meta[slot];
-        base_nk = me.nk;
-        base_ns = me.ns;
-        smask_old = me.smask;
-        if (base_nk + nk > KSG_SLOT_KEYS || base_ns + n_svcs > KSG_SLOT_SVCS) {
-          resolved = i;  // this pod is redone (with the same draw) in the next window
-          reason = KSG_STOP_SLOT;
-          break;
-        }
-      } else {
-        ++n_slots;
-        // snapshot loads (L2-warm), retired lazily
-        snap_pending = true;
-        if (lane == 0) p_v = d.cap_cpu[wn];
-        else if (lane == 1) p_v = d.cap_mem[wn];
-        else if (lane == 2) p_v = d.used_cpu[wn];
-        else if (lane == 3) p_v = d.used_mem[wn];
-#pragma unroll
-        for (int q = 0; q < P; ++q)
-          if ((uint32_t)q == cq && lane == co) cm[q] |= 1ULL << (woff & 63);
-      }
-      const uint32_t t32 = lane - 32;
-      // every lane takes part in the shuffles (bpermute reads inactive lanes as garbage)
-      const uint32_t idx_sv = WS_IDS + nk + n_sel + (t32 < n_svcs ? t32 : 0u);
-      const uint32_t my_sv = (uint32_t)__shfl((int)rec, (int)(idx_sv < 64 ? idx_sv : 0u), 64);
-      const uint32_t smask_new =
-          smask_old | (uint32_t)__builtin_amdgcn_readfirstlane(
-                          (int)wave_or_u32(lane >= 32 && t32 < n_svcs ? (1u << (my_sv & 31)) : 0u));
-      if (lane >= 32 && t32 < n_svcs) {
-        p_cnt = d.svc_cnt[(size_t)my_sv * d.n_nodes + wn];
-        p_max = d.svc_max[my_sv];
-        p_peer = d.svc_peer[my_sv];
-        p_sv = my_sv;
-        L.svcs[(size_t)slot * KSG_SLOT_SVCS + base_ns + t32] = my_sv;
-      }
-      // ports then PDs sit at record dwords WS_IDS + [0, nk)
-      const uint32_t my_key = (uint32_t)__shfl((int)rec, (int)(WS_IDS + (lane < nk ? lane : 0u)), 64);
-      if (lane < nk) L.keys[(size_t)slot * KSG_SLOT_KEYS + base_nk + lane] = my_key;
-      if (lane == 0) {
-        if (!in_c) {
-          L.slot_of[woff] = (uint16_t)slot;
-          L.dlt[slot] = I64x2{req_c, req_m};
-        } else {
-          const I64x2 ov = L.dlt[slot];
-          L.dlt[slot] = I64x2{ov.c + req_c, ov.m + req_m};
-        }
-        L.meta[slot] = SlotMeta{woff, (uint16_t)(base_nk + nk), (uint16_t)(base_ns + n_svcs), smask_new, 0u};
-        L.out[i] = (int32_t)wn;
-      }
-      ++n_draws;
-      lds_fence();
-      p_snap = snap_pending;
-      p_svc = n_svcs > 0;
-      p_slot = slot;
-      p_base = base_ns;
-      p_nsv = n_svcs;
-      p_node = woff;
-      KSG_STAMP(4)
+      for (int q = 0; q < P; ++q) cl += __popcll(live[q]);
+      const uint32_t incl = dpp_scan_add(cl);
+      woff = select_in_lanes<P>(live, cl, incl, k - 1 - ix, lane);
     }
+    const uint32_t wn = d.lo + woff;
+    KSG_STAMP(3)
+
+    // ---- AssumePod into the window's slots; HBM is written back at window end
+    const bool is_pred = (int32_t)woff == (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].pred);
+    const uint64_t hit0 = __ballot(lane < n_slots && sn[0] == woff);
+    const uint64_t hit1 = __ballot(64 + lane < n_slots && sn[1] == woff);
+    uint32_t slot, base_nk = 0, base_ns = 0;
+    const bool in_c = (hit0 | hit1) != 0;
+    if (in_c) {
+      slot = hit0 ? (uint32_t)__builtin_ctzll(hit0) : 64u + (uint32_t)__builtin_ctzll(hit1);
+      const int sl = (int)(slot & 63);
+      base_nk = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? s_nk[0] : s_nk[1]), sl);
+      base_ns = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? s_ns[0] : s_ns[1]), sl);
+      if (base_nk + nk > KSG_SLOT_KEYS || base_ns + n_svcs > KSG_SLOT_SVCS) {
+        resolved = i;  // this pod is redone (with the same draw) in the next window
+        reason = KSG_STOP_SLOT;
+        break;
+      }
+    } else {
+      if (n_slots == KSG_MAX_SLOTS) {
+        resolved = i;
+        reason = KSG_STOP_SLOT;
+        break;
+      }
+      slot = n_slots++;
+      const int h = slot >> 6;
+      const bool owner = lane == (slot & 63);
+      // snapshot of the node: staged by the producer when it is the predicted
+      // node; otherwise the owner lane loads it and it is retired lazily
+      int64_t vc = 0, vm = 0, uc = 0, um = 0;
+      double ic = 0.0, im = 0.0;
+      if (is_pred) {
+        vc = r_hdr[e].cap_c;
+        vm = r_hdr[e].cap_m;
+        uc = r_hdr[e].used_c;
+        um = r_hdr[e].used_m;
+        ic = r_hdr[e].inv_c;
+        im = r_hdr[e].inv_m;
+      } else {
+        KSG_COUNT(9, 64)
+        if (owner) {
+          pl_cc = d.cap_cpu[wn];
+          pl_cm = d.cap_mem[wn];
+          pl_uc = d.used_cpu[wn];
+          pl_um = d.used_mem[wn];
+          pl_ic = d.inv10_cpu[wn];
+          pl_im = d.inv10_mem[wn];
+        }
+        p_snap = true;
+      }
+      if (owner) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+          if (hh == h) {
+            sn[hh] = woff;
+            if (is_pred) {
+              cap_c[hh] = vc;
+              cap_m[hh] = vm;
+              snp_c[hh] = uc;
+              snp_m[hh] = um;
+              inv_c[hh] = ic;
+              inv_m[hh] = im;
+            }
+            dl_c[hh] = 0;
+            dl_m[hh] = 0;
+            s_nk[hh] = 0;
+            s_ns[hh] = 0;
+            s_mask[hh] = 0;
+          }
+      }
+    }
+    KSG_STAMP(10)
+    // the pod's services (lane t < n_svcs): snapshot count on the node, maxCount, peer
+    const uint32_t t_sv = lane < n_svcs ? lane : 0u;
+    const uint32_t my_sv = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + t_sv, 63u), 64);
+    const bool sv_lane = lane < n_svcs;
+    uint32_t new_mask = 0;
+    if (n_svcs) {
+      if (sv_lane) {
+        pl_max = r_svc[e].max[lane];
+        pl_peer = r_svc[e].peer[lane];
+        pl_sv = my_sv;
+        // (predicted node: staged; else a lazily retired load, L2-warm)
+        pl_cnt = is_pred ? r_svc[e].cnt[lane] : d.svc_cnt[(size_t)my_sv * d.n_nodes + wn];
+        L_svcs[(size_t)slot * KSG_SLOT_SVCS + base_ns + lane] = my_sv;
+      }
+      p_svc = true;
+      new_mask = wave_or_u32(sv_lane ? (1u << (my_sv & 31)) : 0u);
+    }
+    p_slot = slot;
+    p_node = woff;
+    p_base = base_ns;
+    p_nsv = n_svcs;
+    // (the next pod nearly always has this node among its candidates: waiting
+    // here costs the same as waiting there)
+    retire();
+    KSG_STAMP(11)
+    // ports then PDs sit at record dwords WS_IDS + [0, nk)
+    const uint32_t my_key = (uint32_t)__shfl((int)rec, (int)(WS_IDS + (lane < nk ? lane : 0u)), 64);
+    if (lane < nk) L_keys[(size_t)slot * KSG_SLOT_KEYS + base_nk + lane] = my_key;
+    if (lane == (slot & 63)) {
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+        if (hh == (int)(slot >> 6)) {
+          dl_c[hh] = (int64_t)((uint64_t)dl_c[hh] + (uint64_t)req_c);
+          dl_m[hh] = (int64_t)((uint64_t)dl_m[hh] + (uint64_t)req_m);
+          s_nk[hh] += nk;
+          s_ns[hh] += n_svcs;
+          s_mask[hh] |= new_mask;
+        }
+    }
+    if (lane == 0) L_out[i] = (int32_t)wn;
+    ++n_draws;
+    lds_fence();
     if (lane == 0) st_rel(&ctl->consumed, i + 1);
-    KSG_STAMP(5)
+    KSG_STAMP(4)
   }
   if (resolved < n_pods && lane == 0) st_rel(&ctl->stop, 1u);
   retire();
   if constexpr (STAMP) {
-    if (lane == 0)
-      for (int k = 0; k < 16; ++k) atomicAdd(d.dbgbuf + k, (int32_t)(t_acc[k] / 64));
+    if (lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
   }
 #undef KSG_STAMP
+#undef KSG_COUNT
 
   // ---- write the window's deltas back to HBM (the next snapshot) -------------
-  for (uint32_t t = lane; t < n_slots; t += 64) {
-    const SlotMeta me = L.meta[t];
-    const uint32_t n = d.lo + me.node;
-    const I64x2 snp = L.snap[t], dl = L.dlt[t];
-    d.used_cpu[n] = snp.c + dl.c;
-    d.used_mem[n] = snp.m + dl.m;
-    const uint32_t* ks = L.keys + (size_t)t * KSG_SLOT_KEYS;
-    for (uint32_t a = 0; a < me.nk; ++a)
-      __hip_atomic_fetch_or(d.keymap + (size_t)ks[a] * d.nw + (n >> 6), 1ULL << (n & 63), __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t* sv = L.svcs + (size_t)t * KSG_SLOT_SVCS;
-    const int32_t* sc = L.scnt + (size_t)t * KSG_SLOT_SVCS;
-    for (uint32_t a = 0; a < me.ns; ++a) {
-      const uint32_t s = sv[a];
-      bool first = true;
-      int32_t count = 0;
-      for (uint32_t b = 0; b < me.ns; ++b) {
-        if (sv[b] == s) {
-          if (b < a) first = false;
-          ++count;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t t = (uint32_t)h * 64 + lane;
+    if (t < n_slots) {
+      const uint32_t n = d.lo + sn[h];
+      d.used_cpu[n] = (int64_t)((uint64_t)snp_c[h] + (uint64_t)dl_c[h]);
+      d.used_mem[n] = (int64_t)((uint64_t)snp_m[h] + (uint64_t)dl_m[h]);
+      const uint32_t* ks = L_keys + (size_t)t * KSG_SLOT_KEYS;
+      for (uint32_t a = 0; a < s_nk[h]; ++a)
+        __hip_atomic_fetch_or(d.keymap + (size_t)ks[a] * d.nw + (n >> 6), 1ULL << (n & 63), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t* sv = L_svcs + (size_t)t * KSG_SLOT_SVCS;
+      const int32_t* sc = L_scnt + (size_t)t * KSG_SLOT_SVCS;
+      for (uint32_t a = 0; a < s_ns[h]; ++a) {
+        const uint32_t sa = sv[a];
+        bool first = true;
+        int32_t count = 0;
+        for (uint32_t b = 0; b < s_ns[h]; ++b) {
+          if (sv[b] == sa) {
+            if (b < a) first = false;
+            ++count;
+          }
         }
-      }
-      __hip_atomic_fetch_add(d.svc_total + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (first) {
-        const int32_t fin = sc[a] + count;
-        d.svc_cnt[(size_t)s * d.n_nodes + n] = fin;
-        __hip_atomic_fetch_max(d.svc_max + s, fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(d.svc_total + sa, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (first) {
+          const int32_t fin = sc[a] + count;
+          d.svc_cnt[(size_t)sa * d.n_nodes + n] = fin;
+          __hip_atomic_fetch_max(d.svc_max + sa, fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
     }
   }
   for (uint32_t t = lane; t < n_peer; t += 64) {
-    const uint32_t sv = L.peer[2 * t];
+    const uint32_t sv = L_peer[2 * t];
     int32_t expect = -1;
-    __hip_atomic_compare_exchange_strong(d.svc_peer + sv, &expect, (int32_t)L.peer[2 * t + 1], __ATOMIC_RELAXED,
+    __hip_atomic_compare_exchange_strong(d.svc_peer + sv, &expect, (int32_t)L_peer[2 * t + 1], __ATOMIC_RELAXED,
                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  for (uint32_t t = lane; t < resolved; t += 64) out[t] = L.out[t];
+  for (uint32_t t = lane; t < resolved; t += 64) out[t] = L_out[t];
   if (lane == 0) {
     *rng_io = rng0 + (uint64_t)n_draws * 0x9E3779B97F4A7C15ULL;
     if (reason == KSG_STOP_HANG) {
@@ -950,11 +1001,11 @@ hipError_t ksg_launch_win_eval(const KsgDev& d, const ksg_pod* batch, const uint
 uint32_t ksg_win_max_window(const KsgDev& d) {
   const uint32_t P = win_P(d);
   if (P == 0) return 0;
-  const uint32_t nflag = (d.n_services + 31) / 32, nshard = d.hi - d.lo;
+  const uint32_t nflag = (d.n_services + 31) / 32;
   uint32_t lo = 0, hi = 4096;
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1) / 2;
-    if (win_lds_offsets(P, nflag, nshard, mid).total <= kWinLdsBudget) lo = mid;
+    if (win_lds_offsets(P, nflag, mid).total <= kWinLdsBudget) lo = mid;
     else hi = mid - 1;
   }
   return lo;
@@ -979,7 +1030,7 @@ static hipError_t win_resolve_launch(const KsgDev& d, uint32_t wcap, size_t lds,
 hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
                                   const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
   const uint32_t P = win_P(d);
-  const size_t lds = win_lds_offsets(P, (d.n_services + 31) / 32, d.hi - d.lo, wcap).total;
+  const size_t lds = win_lds_offsets(P, (d.n_services + 31) / 32, wcap).total;
   const bool stamp = (d.dbg & 8) != 0;  // KSG_DEBUG & 8: per-section s_memtime stamps
 #define KSG_RES_CASE(PP)                                                                              \
   if (P == PP)                                                                                        \

@@ -124,3 +124,32 @@ def test_no_nodes_and_empty_priorities():
     out, _ = dev.batch(case.batch, 5)
     assert (out == abi.KSG_OUT_NONODES).all()
     dev.close()
+
+
+def test_batch_rejects_duplicate_uids_and_keeps_mirror():
+    """A pod uid already scheduled (replayed into the host mirror lazily) is refused
+    before any device work; remove_pod after a batch sees that batch's commits."""
+    from kubernetes_amd.engine import KsgError
+
+    case = Case("config2", 300, 200)
+    dev, orc = _pair(case, 128)
+    dev.set_cluster(case.view.arrays)
+    orc.set_cluster(case.view.arrays)
+    half = PodBatch(case.batch.pods[:100], case.batch.ids)
+    got, st = dev.batch(half, 7)
+    want, sw = orc.batch(half, 7)
+    assert np.array_equal(got, want) and st == sw
+    with pytest.raises(KsgError):
+        dev.batch(PodBatch(case.batch.pods[50:60], case.batch.ids), st)
+    # removing a pod of the last batch undoes its commit exactly (mirror replay)
+    uid = int(case.batch.pods[0]["uid"])
+    dev.remove_pod(uid)
+    orc.remove_pod(uid)
+    rest = PodBatch(case.batch.pods[100:], case.batch.ids)
+    g2, _ = dev.batch(rest, st)
+    w2, _ = orc.batch(rest, sw)
+    assert np.array_equal(g2, w2)
+    gc, gm = dev.read_requested()
+    wc, wm = orc.read_requested()
+    assert np.array_equal(gc, wc) and np.array_equal(gm, wm)
+    dev.close()
