@@ -221,8 +221,10 @@ int ksg_last_batch_ms(ksg_ctx* ctx, double* ms);
 
 /* Window path of the last ksg_schedule_batch: out3[0] = device ms in the
  * snapshot-scoring kernel (ksg_win_eval_kernel), out3[1] = device ms in the
- * resolver (ksg_win_resolve_kernel), out3[2] = number of windows; from HIP
- * events recorded around each launch on the context's stream. */
+ * resolver (ksg_win_resolve_kernel), out3[2] = resolver launches (windows are
+ * chained on the device, so a round may end with launches that find the batch
+ * done and return at once); from HIP events recorded around each launch on the
+ * context's stream. */
 int ksg_last_batch_kernel_ms(ksg_ctx* ctx, double* out3);
 
 /* ---- node sharding (multi-GPU) ------------------------------

@@ -1059,16 +1059,16 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       if ((rc = flush_deferred(c))) return rc;  // the host mirror catches up while the device works
       HIPCHK(c, hipStreamSynchronize(c->st));
       const KsgWinRun r = *c->h_run;
-      // windows that did work come first in the chain; the rest returned at once
-      const uint32_t eff = std::min(r.windows, K);
-      for (uint32_t k = 0; k < eff; ++k) {
+      // every launch of the round, including the ones after the batch was done
+      // (they return at once), so the mean matches a kernel trace of the run
+      for (uint32_t k = 0; k < K; ++k) {
         float a = 0.f, b = 0.f;
         HIPCHK(c, hipEventElapsedTime(&a, c->wev[2 * k], c->wev[2 * k + 1]));
         HIPCHK(c, hipEventElapsedTime(&b, c->wev[2 * k + 1], c->wev[2 * k + 2]));
         c->last_kms[0] += a;
         c->last_kms[1] += b;
       }
-      c->last_kms[2] += eff;
+      c->last_kms[2] += K;
       c->last_stats[0] += r.windows;
       for (int q = 1; q <= 3; ++q) c->last_stats[q] += r.stops[q];
       if (r.halt == KSG_HALT_HANG) return fail(c, KSG_ERR_STATE, "window resolver: ring wait timed out at pod %u", r.pos);
