@@ -237,34 +237,57 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
 // ---------------------------------------------------------------------------
 // phase B
 // ---------------------------------------------------------------------------
-// One workgroup. Wave 0 is the RESOLVER: the sequential chain, registers and
-// LDS only on its common path. Waves 1..KSG_RES_NPW are PRODUCERS: pod j of the
-// window is staged by producer (j mod NPW) into ring entry j mod KSG_RING —
-// its record, its T0 bitmap (nodes at the snapshot max M0, from phase A's
-// per-word maxima), k0 = |T0|, its tie-break draw r (the splitmix64 output at
-// the pod's draw index = the number of earlier window pods that draw: those
-// that neither error nor find no fit), r mod (k0 - d) for d = 0..63 dropped
-// ties, and the PREDICTED node: the (r mod k0)-th tie of T0 from the top,
-// which is the answer whenever no tie dropped. The producer also loads the
-// predicted node's snapshot state (capacity, requested totals, 10/capacity,
-// the pod's service counts on it) and the pod's service scalars, so a commit
-// to the predicted node needs no global memory access on the chain.
+// One workgroup of 8 waves in three roles, pipelined over the window's pods:
 //
-// Nodes committed in the window ("slots", set C, at most KSG_MAX_SLOTS) live
-// in the resolver's registers: lane l holds slots l and 64 + l (node, snapshot
-// capacity / requested totals, window delta, 10/capacity, key and service
-// counts). A pod's candidates — slots whose node is in its T0 — are found by
-// each slot lane testing its node's bit in the staged T0 (one LDS read); the
-// re-check then runs on the slot lanes out of registers. The node state in HBM
-// stays the pristine snapshot while the window resolves; the window's deltas
-// are written back once, at the end of the window.
+//  PRODUCERS (waves 3..7) stage pod j into ring entry j mod KSG_RING: its
+//    record, its T0 bitmap (nodes at the snapshot max M0, from phase A's
+//    per-word maxima), k0 = |T0|, its tie-break draw r (the splitmix64 output
+//    at the pod's draw index = the number of earlier window pods that draw:
+//    those that neither error nor find no fit), r mod (k0 - d) for d = 0..63
+//    dropped ties, and the PREDICTED node: the (r mod k0)-th tie of T0 from
+//    the top, the answer whenever no tie dropped, with its snapshot state
+//    (capacity, requested totals, 10/capacity) and the pod's service counts
+//    on it and service scalars.
+//  CHECKERS (waves 1, 2) re-check pod i against the nodes committed earlier
+//    in the window ("slots", set C): checker c owns slots 64c..64c+63, one per
+//    lane. A slot is a candidate when its node is in T0 (one LDS read); a
+//    candidate drops when the window's deltas pushed its score below M0
+//    (resources, host ports / PDs, LeastRequested, ServiceSpreading). Dropped
+//    nodes are scattered into an LDS bitmap. Pod i is checked as soon as the
+//    COMMITTER has selected pod i-1's node, against every slot except the one
+//    pod i-1 is committing into.
+//  COMMITTER (wave 0) walks the window in order: for pod i it takes the
+//    checkers' drops, re-checks the one slot pod i-1 just committed into,
+//    selects the ix-th live tie in descending name order (the staged
+//    prediction when nothing dropped), publishes the choice — which releases
+//    the checkers onto pod i+1 — and then commits into the slot.
+//
+// So the checkers' scan of pod i+1 overlaps the commit of pod i, and the
+// sequential chain per pod is select + commit + one slot's re-check. Slot
+// state lives in LDS (structure of arrays by slot, at most KSG_MAX_SLOTS).
+// The node state in HBM stays the pristine snapshot while the window
+// resolves; the window's deltas are written back once, at the end.
 #define KSG_RES_NT 512
-#define KSG_RES_NPW (KSG_RES_NT / 64 - 1)
+#define KSG_RES_NCHK 2                                // checker waves 1, 2
+#define KSG_RES_P0 (1 + KSG_RES_NCHK)                 // first producer wave
+#define KSG_RES_NPW (KSG_RES_NT / 64 - KSG_RES_P0)    // producer waves
 #define KSG_RING 16
 #define KSG_SLOT_KEYS 8
 #define KSG_SLOT_SVCS 12
-#define KSG_MAX_SLOTS 128  // two per resolver lane
+#define KSG_MAX_SLOTS (64 * KSG_RES_NCHK)
+#define KSG_NO_SLOT 0xffffu
 
+struct alignas(16) I64x2 {
+  int64_t c, m;
+};
+struct alignas(16) F64x2 {
+  double c, m;
+};
+struct alignas(16) SlotMeta {
+  uint32_t node;    // shard offset of the node
+  uint32_t nk, ns;  // conflict keys / service entries added by the window
+  uint32_t smask;   // OR of 1 << (service & 31) over the service entries
+};
 struct alignas(16) RingHdr {
   int32_t m0;
   uint32_t k0;
@@ -274,7 +297,7 @@ struct alignas(16) RingHdr {
   int32_t pred;        // (r mod k0)-th tie of T0 from the top (shard offset), -1: none
   uint32_t pad;
   int64_t cap_c, cap_m, used_c, used_m;  // snapshot of pred
-  double inv_c, inv_m;                   // lr_inv10 of pred's capacities
+  double inv_c, inv_m;                   // 10 / capacity of pred
 };
 struct alignas(16) RingSvc {  // per service entry t of the pod (t < n_svcs)
   int32_t cnt[KSG_SLOT_SVCS];   // svc_cnt[sv][pred] at the snapshot
@@ -283,17 +306,24 @@ struct alignas(16) RingSvc {  // per service entry t of the pod (t < n_svcs)
   int32_t pad[4];
 };
 struct alignas(16) WinCtl {
-  uint32_t consumed;    // pods the resolver is done with (ring entries free)
-  uint32_t stop;        // the window ended early: producers exit
+  uint32_t consumed;    // pods the committer is done with (ring entries free)
+  uint32_t stop;        // the window ended early: every other wave exits
   uint32_t draw_next;   // next pod allowed to take a draw index
   uint32_t draw_count;  // draws of pods [0, draw_next)
+  uint32_t sel_seq;     // pods the committer has selected a node for
+  uint32_t xs_slot;     // slot the last selected pod commits into (KSG_NO_SLOT: none)
+  uint32_t xs_nslots;   // slots in use once that pod is committed
+  uint32_t pad0;
+  uint32_t chk_seq[KSG_RES_NCHK];     // pods checker c is done with
+  uint32_t chk_cnt[KSG_RES_NCHK][2];  // checker c's drops for the pod of parity p
   uint32_t pad[4];
 };
 
 // byte offsets of the resolver's dynamic LDS arrays (host and device agree)
 struct WinLdsOff {
-  uint32_t ctl, r_hdr, r_t0, r_rec, r_mod, r_svc;  // ring
-  uint32_t keys, svcs, scnt;                       // slots
+  uint32_t ctl, r_hdr, r_t0, r_rec, r_mod, r_svc;     // ring
+  uint32_t s_meta, s_cap, s_snp, s_dl, s_inv;          // slots
+  uint32_t keys, svcs, scnt;
   uint32_t peer, out, flag, peerset, drop;
   uint32_t total;
 };
@@ -309,6 +339,11 @@ __host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag,
   o.r_rec = at;   at += win_al16((size_t)KSG_RING * KSG_WIN_SUM_DWORDS * 4);
   o.r_mod = at;   at += win_al16((size_t)KSG_RING * 64 * 4);
   o.r_svc = at;   at += win_al16((size_t)KSG_RING * sizeof(RingSvc));
+  o.s_meta = at;  at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(SlotMeta));
+  o.s_cap = at;   at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(I64x2));
+  o.s_snp = at;   at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(I64x2));
+  o.s_dl = at;    at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(I64x2));
+  o.s_inv = at;   at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(F64x2));
   o.keys = at;    at += win_al16((size_t)KSG_MAX_SLOTS * KSG_SLOT_KEYS * 4);
   o.svcs = at;    at += win_al16((size_t)KSG_MAX_SLOTS * KSG_SLOT_SVCS * 4);
   o.scnt = at;    at += win_al16((size_t)KSG_MAX_SLOTS * KSG_SLOT_SVCS * 4);
@@ -316,7 +351,7 @@ __host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag,
   o.out = at;     at += win_al16((size_t)W * 4);
   o.flag = at;    at += win_al16((size_t)nflag * 4);
   o.peerset = at; at += win_al16((size_t)nflag * 4);
-  o.drop = at;    at += win_al16((size_t)P * 64 * 8);
+  o.drop = at;    at += win_al16((size_t)2 * P * 64 * 8);
   o.total = at;
   return o;
 }
@@ -367,6 +402,91 @@ __device__ __forceinline__ uint32_t select_in_lanes(const uint64_t (&bits)[P], u
   return ((uint32_t)ol * P + qsel) * 64 + bsel;
 }
 
+// LDS views of the slots (structure of arrays by slot index)
+struct WinSlots {
+  SlotMeta* meta;
+  I64x2 *cap, *snp, *dl;
+  F64x2* inv;
+  uint32_t* keys;
+  uint32_t* svcs;
+  int32_t* scnt;
+};
+
+// The pod-side inputs of a re-check (wave-uniform, read from the pod's record).
+struct PodView {
+  int64_t req_c, req_m;
+  bool zero_req;
+  uint32_t n_ports, n_pds, nk;
+  int32_t s, smax;
+};
+
+// Does slot `sl` (a snapshot tie of the pod) score below M0 once the window's
+// deltas are applied? The node fit the pod at the snapshot; only those deltas
+// (requested totals, keys, service counts) can change that. `rec` is this
+// lane's dword of the pod's record (the pod's key ids are read from it).
+__device__ __forceinline__ bool slot_drops(const KsgDev& d, const WinSlots& S, uint32_t sl, const PodView& pv,
+                                           uint32_t rec, bool res_on, bool ports_on, bool disk_on,
+                                           bool spread_on) {
+  const I64x2 cap = S.cap[sl], snp = S.snp[sl], dl = S.dl[sl];
+  const SlotMeta me = S.meta[sl];
+  const int64_t now_c = (int64_t)((uint64_t)snp.c + (uint64_t)dl.c);
+  const int64_t now_m = (int64_t)((uint64_t)snp.m + (uint64_t)dl.m);
+  bool drop = false;
+  if (res_on && !pv.zero_req) {  // PodFitsResources (predicates.go:127-145)
+    const bool fc = cap.c == 0 || cap.c - now_c >= pv.req_c;
+    const bool fm = cap.m == 0 || cap.m - now_m >= pv.req_m;
+    drop = !(fc && fm);
+  }
+  if (pv.nk && !drop && me.nk) {  // PodFitsPorts / NoDiskConflict against the window's keys
+    const uint32_t* ks = S.keys + (size_t)sl * KSG_SLOT_KEYS;
+    for (uint32_t a = 0; a < me.nk; ++a) {
+      const uint32_t key = ks[a];
+      if (ports_on)
+        for (uint32_t b = 0; b < pv.n_ports; ++b)
+          drop |= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + b) == key;
+      if (disk_on)
+        for (uint32_t b = 0; b < pv.n_pds; ++b)
+          drop |= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + pv.n_ports + b) == key;
+    }
+  }
+  if (!drop && d.w_lr) {  // LeastRequested (priorities.go:43-76) can only fall as requested grows
+    const F64x2 iv = S.inv[sl];
+    const int32_t lr_now = lr_win(now_c + pv.req_c, cap.c, iv.c) + lr_win(now_m + pv.req_m, cap.m, iv.m);
+    const int32_t lr_snap = lr_win(snp.c + pv.req_c, cap.c, iv.c) + lr_win(snp.m + pv.req_m, cap.m, iv.m);
+    drop = (lr_now >> 1) != (lr_snap >> 1);
+  }
+  if (!drop && spread_on && pv.s >= 0 && ((me.smask >> (pv.s & 31)) & 1u)) {
+    // ServiceSpreading (spreading.go:72-86) under an unchanged maxCount
+    const uint32_t* sv = S.svcs + (size_t)sl * KSG_SLOT_SVCS;
+    const int32_t* sc = S.scnt + (size_t)sl * KSG_SLOT_SVCS;
+    int32_t delta = 0, snapc = 0;
+    for (uint32_t a = 0; a < me.ns; ++a)
+      if (sv[a] == (uint32_t)pv.s) {
+        snapc = sc[a];
+        ++delta;
+      }
+    if (delta)
+      drop = frac10_f32((int64_t)pv.smax - snapc - delta, pv.smax) != frac10_f32((int64_t)pv.smax - snapc, pv.smax);
+  }
+  return drop;
+}
+
+__device__ __forceinline__ PodView pod_view(uint32_t rec) {
+  PodView pv;
+  const uint32_t npp = __builtin_amdgcn_readlane(rec, WS_NPP);
+  pv.req_c = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_CPU) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_CPU + 1) << 32));
+  pv.req_m = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_MEM) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_MEM + 1) << 32));
+  pv.zero_req = pv.req_c == 0 && pv.req_m == 0;
+  pv.n_ports = npp & 0xffff;
+  pv.n_pds = npp >> 16;
+  pv.nk = pv.n_ports + pv.n_pds;
+  pv.s = (int32_t)__builtin_amdgcn_readlane(rec, WS_SVC);
+  pv.smax = (int32_t)__builtin_amdgcn_readlane(rec, WS_SMAX);
+  return pv;
+}
+
 template <int P, bool STAMP>
 __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
                                                                     const KsgWinSum* __restrict__ sums,
@@ -390,30 +510,42 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
   uint32_t* r_rec = reinterpret_cast<uint32_t*>(smem + o.r_rec);
   uint32_t* r_mod = reinterpret_cast<uint32_t*>(smem + o.r_mod);
   RingSvc* r_svc = reinterpret_cast<RingSvc*>(smem + o.r_svc);
+  const WinSlots S{reinterpret_cast<SlotMeta*>(smem + o.s_meta), reinterpret_cast<I64x2*>(smem + o.s_cap),
+                   reinterpret_cast<I64x2*>(smem + o.s_snp),     reinterpret_cast<I64x2*>(smem + o.s_dl),
+                   reinterpret_cast<F64x2*>(smem + o.s_inv),     reinterpret_cast<uint32_t*>(smem + o.keys),
+                   reinterpret_cast<uint32_t*>(smem + o.svcs),   reinterpret_cast<int32_t*>(smem + o.scnt)};
+  uint64_t* const L_drop = reinterpret_cast<uint64_t*>(smem + o.drop);  // [2][P*64] by pod parity
+  const bool spread_on = d.w_spread != 0;
+  const bool aff_on = (d.preds & KSG_PRED_SERVICEAFFINITY) && d.n_aff > 0;
+  const bool res_on = (d.preds & KSG_PRED_PODFITSRESOURCES) != 0;
+  const bool ports_on = (d.preds & KSG_PRED_PODFITSPORTS) != 0;
+  const bool disk_on = (d.preds & KSG_PRED_NODISKCONFLICT) != 0;
 
   for (uint32_t t = tid; t < KSG_RING; t += KSG_RES_NT) r_hdr[t].ready = 0;
-  if (tid == 0) *ctl = WinCtl{0, 0, 0, 0, {0, 0, 0, 0}};
+  if (tid == 0) {
+    *ctl = WinCtl{};
+    ctl->xs_slot = KSG_NO_SLOT;
+  }
   if (wave == 0) {
     uint32_t* flag = reinterpret_cast<uint32_t*>(smem + o.flag);
     uint32_t* peerset = reinterpret_cast<uint32_t*>(smem + o.peerset);
-    uint64_t* drop = reinterpret_cast<uint64_t*>(smem + o.drop);
     for (uint32_t w = lane; w < nflag; w += 64) {
       flag[w] = 0;
       peerset[w] = 0;
     }
-    for (uint32_t w = lane; w < P * 64u; w += 64) drop[w] = 0;
   }
+  for (uint32_t w = tid; w < 2 * P * 64u; w += KSG_RES_NT) L_drop[w] = 0;
   __syncthreads();
   const uint64_t rng0 = *rng_io;
 
   // =========================================================================
   // producers
   // =========================================================================
-  if (wave != 0) {
+  if (wave >= KSG_RES_P0) {
     // warm this XCD's L2 with the node state: the producers' loads of each
-    // pod's predicted node (and the resolver's rare loads) then hit L2
+    // pod's predicted node (and the committer's loads of other nodes) then hit L2
     {
-      const uint32_t pw = wave - 1, nt = KSG_RES_NPW * 64;
+      const uint32_t pw = wave - KSG_RES_P0, nt = KSG_RES_NPW * 64;
       const uint32_t n16 = (nshard + 1) / 2;  // 16-byte chunks of one int64 array
       uint64_t acc = 0;
       const int64_t* arr[6] = {d.cap_cpu + d.lo, d.cap_mem + d.lo, d.used_cpu + d.lo, d.used_mem + d.lo,
@@ -443,7 +575,7 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
       wm_at[q] = ok ? base + x.wcap * x.ostride * 8 + i * 4 : ~0u;
     }
     const uint32_t row_b = x.ostride * 8, row_m = x.ostride * 4;
-    for (uint32_t j = wave - 1; j < n_pods; j += KSG_RES_NPW) {
+    for (uint32_t j = wave - KSG_RES_P0; j < n_pods; j += KSG_RES_NPW) {
       const uint32_t e = j % KSG_RING;
       for (uint32_t spin = 0;; ++spin) {  // ring entry free: the resolver is done with pod j - KSG_RING
         if (ld_acq(&ctl->stop) || spin > KSG_SPIN_LIMIT) return;
@@ -543,100 +675,63 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
   }
 
   // =========================================================================
-  // resolver (wave 0)
+  // checkers (waves 1 .. KSG_RES_NCHK): slot 64c + lane of checker c
+  // =========================================================================
+  if (wave < KSG_RES_P0) {
+    if (wave != 0) {
+      __builtin_amdgcn_s_setprio(2);
+      const uint32_t c = wave - 1;
+      const uint32_t sl = c * 64 + lane;
+      for (uint32_t i = 0; i < n_pods; ++i) {
+        const uint32_t e = i % KSG_RING, par = i & 1;
+        // pod i is staged and the committer has chosen pod i-1's node (while
+        // this checker works on pod i the committer cannot pass pod i-1: it
+        // waits for this checker before selecting pod i)
+        for (uint32_t spin = 0;; ++spin) {
+          if (ld_acq(&ctl->stop) || spin > 16 * KSG_SPIN_LIMIT) return;
+          if (ld_acq(&r_hdr[e].ready) == i + 1 && ld_acq(&ctl->sel_seq) >= i) break;
+        }
+        const uint32_t xs = ctl->xs_slot, ns = ctl->xs_nslots;
+        const uint32_t rec = lane < KSG_WIN_SUM_DWORDS ? r_rec[e * KSG_WIN_SUM_DWORDS + lane] : 0u;
+        const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
+        uint32_t cnt = 0;
+        if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE && c * 64 < ns) {
+          const PodView pv = pod_view(rec);
+          const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
+          bool drop = false;
+          if (sl < ns && sl != xs) {
+            const uint32_t nd = S.meta[sl].node;
+            if ((t0e[nd >> 6] >> (nd & 63)) & 1ULL) {
+              drop = slot_drops(d, S, sl, pv, rec, res_on, ports_on, disk_on, spread_on);
+              if (drop)
+                atomicOr(reinterpret_cast<unsigned long long*>(L_drop + (size_t)par * P * 64 + (nd >> 6)),
+                         1ULL << (nd & 63));
+            }
+          }
+          cnt = __popcll(__ballot(drop));
+        }
+        if (lane == 0) {
+          ctl->chk_cnt[c][par] = cnt;
+          st_rel(&ctl->chk_seq[c], i + 1);
+        }
+      }
+      return;
+    }
+  }
+
+  // =========================================================================
+  // committer (wave 0)
   // =========================================================================
   __builtin_amdgcn_s_setprio(3);
-  uint32_t* const L_keys = reinterpret_cast<uint32_t*>(smem + o.keys);
-  uint32_t* const L_svcs = reinterpret_cast<uint32_t*>(smem + o.svcs);
-  int32_t* const L_scnt = reinterpret_cast<int32_t*>(smem + o.scnt);
   uint32_t* const L_peer = reinterpret_cast<uint32_t*>(smem + o.peer);
   int32_t* const L_out = reinterpret_cast<int32_t*>(smem + o.out);
-  uint64_t* const L_drop = reinterpret_cast<uint64_t*>(smem + o.drop);
   uint32_t* const L_flag = reinterpret_cast<uint32_t*>(smem + o.flag);
   uint32_t* const L_peerset = reinterpret_cast<uint32_t*>(smem + o.peerset);
-  const bool spread_on = d.w_spread != 0;
-  const bool aff_on = (d.preds & KSG_PRED_SERVICEAFFINITY) && d.n_aff > 0;
-  const bool res_on = (d.preds & KSG_PRED_PODFITSRESOURCES) != 0;
-  const bool ports_on = (d.preds & KSG_PRED_PODFITSPORTS) != 0;
-  const bool disk_on = (d.preds & KSG_PRED_NODISKCONFLICT) != 0;
   uint32_t resolved = n_pods, reason = 0, n_slots = 0, n_peer = 0, n_draws = 0;
+  uint32_t last_slot = KSG_NO_SLOT;  // slot the previous pod committed into
 
-  // slots h*64 + lane (h = 0, 1) of this lane
-  uint32_t sn[2] = {0, 0};                // node (shard offset)
-  int64_t cap_c[2] = {0, 0}, cap_m[2] = {0, 0};
-  int64_t snp_c[2] = {0, 0}, snp_m[2] = {0, 0};
-  int64_t dl_c[2] = {0, 0}, dl_m[2] = {0, 0};
-  double inv_c[2] = {0.0, 0.0}, inv_m[2] = {0.0, 0.0};
-  uint32_t s_nk[2] = {0, 0}, s_ns[2] = {0, 0}, s_mask[2] = {0, 0};
-
-  // Values a commit loads from HBM when the node was not the predicted one:
-  // the node's snapshot (owner lane) and the pod's service counts on it
-  // (service lanes); retire_* moves them into the slot state once they land.
-  bool p_snap = false, p_svc = false;
-  uint32_t p_slot = 0, p_node = 0, p_base = 0, p_nsv = 0;
-  int64_t pl_cc = 0, pl_cm = 0, pl_uc = 0, pl_um = 0;
-  double pl_ic = 0.0, pl_im = 0.0;
-  int32_t pl_cnt = 0, pl_max = 0, pl_peer = 0;
-  uint32_t pl_sv = 0;
-  auto retire_snap = [&]() {
-    if (!p_snap) return;
-    p_snap = false;
-    if (lane == (p_slot & 63)) {
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-        if (hh == (int)(p_slot >> 6)) {
-          cap_c[hh] = pl_cc;
-          cap_m[hh] = pl_cm;
-          snp_c[hh] = pl_uc;
-          snp_m[hh] = pl_um;
-          inv_c[hh] = pl_ic;
-          inv_m[hh] = pl_im;
-        }
-    }
-  };
-  // service entries of the last commit: snapshot counts, the maxCount /
-  // ServiceAffinity-peer flags later pods of those services stop on, peers
-  auto retire_svc = [&]() {
-    if (!p_svc) return;
-    p_svc = false;
-    const bool sv_lane = lane < p_nsv;
-    bool changed = false;
-    if (sv_lane) {
-      // in-window commits of this service on this node before this one
-      const uint32_t* sl = L_svcs + (size_t)p_slot * KSG_SLOT_SVCS;
-      uint32_t before = 0;
-      for (uint32_t b = 0; b < p_base; ++b) before += sl[b] == pl_sv;
-      if (spread_on && pl_cnt + (int32_t)before + 1 > pl_max) changed = true;  // maxCount rises
-      if (aff_on && pl_peer == -1 && !((L_peerset[pl_sv >> 5] >> (pl_sv & 31)) & 1u)) changed = true;
-      L_scnt[(size_t)p_slot * KSG_SLOT_SVCS + p_base + lane] = pl_cnt;
-    }
-    // first commit of a service with no peer yet: record the peer (lane 0 applies, in order)
-    uint64_t pm = __ballot(sv_lane && pl_peer == -1);
-    while (pm) {
-      const uint32_t b = __builtin_ctzll(pm);
-      pm &= pm - 1;
-      const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)pl_sv, (int)b);
-      const bool fresh = !((L_peerset[fsv >> 5] >> (fsv & 31)) & 1u);
-      if (fresh) {
-        if (lane == 0) {
-          L_peerset[fsv >> 5] |= 1u << (fsv & 31);
-          L_peer[2 * n_peer] = fsv;
-          L_peer[2 * n_peer + 1] = d.lo + p_node;
-        }
-        ++n_peer;
-        lds_fence();
-      }
-    }
-    if (changed) atomicOr(&L_flag[pl_sv >> 5], 1u << (pl_sv & 31));
-    lds_fence();
-  };
-  auto retire = [&]() {
-    retire_snap();
-    retire_svc();
-  };
-
-  // KSG_DEBUG & 8: the STAMP instantiation accumulates s_memtime per section
-  // (lane k accumulates section k in a VGPR: no scalar registers taken from the chain)
+  // KSG_DEBUG & 8: per-section s_memtime; lane k accumulates section k in a
+  // VGPR (no scalar registers taken from the chain)
   uint64_t t_last = 0, t_acc = 0;
 #define KSG_STAMP(k)                                         \
   if constexpr (STAMP) {                                     \
@@ -644,14 +739,22 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
     t_acc += lane == (uint32_t)(k) ? t_now - t_last : 0ULL;  \
     t_last = t_now;                                          \
   }
-#define KSG_COUNT(k, v)                              \
-  if constexpr (STAMP) {                             \
+#define KSG_COUNT(k, v)                                    \
+  if constexpr (STAMP) {                                   \
     t_acc += lane == (uint32_t)(k) ? (uint64_t)(v) : 0ULL; \
   }
   if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
 
+  auto publish = [&](uint32_t i, uint32_t xs, uint32_t ns) {
+    if (lane == 0) {
+      ctl->xs_slot = xs;
+      ctl->xs_nslots = ns;
+      st_rel(&ctl->sel_seq, i + 1);
+    }
+  };
+
   for (uint32_t i = 0; i < n_pods; ++i) {
-    const uint32_t e = i % KSG_RING;
+    const uint32_t e = i % KSG_RING, par = i & 1;
     bool hung = false;
     for (uint32_t spin = 0; ld_acq(&r_hdr[e].ready) != i + 1; ++spin) {
       if (spin > 16 * KSG_SPIN_LIMIT) {
@@ -675,25 +778,18 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
       reason = KSG_STOP_SERVICE;
       break;
     }
-    if (__builtin_amdgcn_readlane(rec, WS_ERR)) {
-      if (lane == 0) L_out[i] = KSG_OUT_ERROR;
+    if (__builtin_amdgcn_readlane(rec, WS_ERR) || m0 == KSG_S32_NONE) {
+      // ServiceAffinity peer error / nothing fit at the snapshot (commits only
+      // remove fits): no draw, no commit. The checkers skip this pod too.
+      if (lane == 0) L_out[i] = __builtin_amdgcn_readlane(rec, WS_ERR) ? KSG_OUT_ERROR : KSG_OUT_NOFIT;
+      publish(i, KSG_NO_SLOT, n_slots);
+      last_slot = KSG_NO_SLOT;
       if (lane == 0) st_rel(&ctl->consumed, i + 1);
       continue;
     }
-    if (m0 == KSG_S32_NONE) {
-      if (lane == 0) L_out[i] = KSG_OUT_NOFIT;  // nothing fit at the snapshot; commits only remove fits
-      if (lane == 0) st_rel(&ctl->consumed, i + 1);
-      continue;
-    }
-    const uint32_t npp = __builtin_amdgcn_readlane(rec, WS_NPP), nss = __builtin_amdgcn_readlane(rec, WS_NSS);
-    const int64_t req_c = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_CPU) |
-                                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_CPU + 1) << 32));
-    const int64_t req_m = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_MEM) |
-                                    ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_MEM + 1) << 32));
-    const bool zero_req = req_c == 0 && req_m == 0;
-    const int32_t smax = (int32_t)__builtin_amdgcn_readlane(rec, WS_SMAX);
-    const uint32_t n_ports = npp & 0xffff, n_pds = npp >> 16, n_sel = nss & 0xffff, n_svcs = nss >> 16;
-    const uint32_t nk = n_ports + n_pds;
+    const PodView pv = pod_view(rec);
+    const uint32_t nss = __builtin_amdgcn_readlane(rec, WS_NSS);
+    const uint32_t n_sel = nss & 0xffff, n_svcs = nss >> 16, nk = pv.nk;
     if (__builtin_amdgcn_readlane(rec, WS_NINL) > KSG_WIN_INLINE || nk > KSG_SLOT_KEYS ||
         n_svcs > KSG_SLOT_SVCS) {
       // lists longer than the record / a slot: the exact per-pod kernel takes it
@@ -703,63 +799,39 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
     }
     KSG_STAMP(1)
 
-    // ---- candidates: slots whose node is a snapshot tie (T0 ∩ C); re-check them
-    const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
-    uint64_t dmask[2] = {0, 0};
+    // ---- the checkers' drops for this pod (every slot but last_slot)
+    for (uint32_t spin = 0;; ++spin) {
+      bool done = true;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (h * 64 >= (int)n_slots) break;
-      bool cand = false;
-      if ((uint32_t)h * 64 + lane < n_slots) cand = (t0e[sn[h] >> 6] >> (sn[h] & 63)) & 1ULL;
-      if (__ballot(cand) == 0) continue;
-      bool drop = false;
-      if (cand) {
-        // the node fit the pod at the snapshot; only the window's deltas can change that
-        const int64_t now_c = (int64_t)((uint64_t)snp_c[h] + (uint64_t)dl_c[h]);
-        const int64_t now_m = (int64_t)((uint64_t)snp_m[h] + (uint64_t)dl_m[h]);
-        if (res_on && !zero_req) {  // PodFitsResources
-          const bool fc = cap_c[h] == 0 || cap_c[h] - now_c >= req_c;
-          const bool fm = cap_m[h] == 0 || cap_m[h] - now_m >= req_m;
-          drop = !(fc && fm);
-        }
-        if (nk && !drop && s_nk[h]) {  // PodFitsPorts / NoDiskConflict against the window's keys
-          const uint32_t* ks = L_keys + (size_t)(h * 64 + lane) * KSG_SLOT_KEYS;
-          for (uint32_t a = 0; a < s_nk[h]; ++a) {
-            const uint32_t key = ks[a];
-            if (ports_on)
-              for (uint32_t b = 0; b < n_ports; ++b)
-                drop |= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + b) == key;
-            if (disk_on)
-              for (uint32_t b = 0; b < n_pds; ++b)
-                drop |= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + n_ports + b) == key;
-          }
-        }
-        if (!drop && d.w_lr) {  // LeastRequested can only fall as requested grows
-          const int32_t lr_now = lr_win(now_c + req_c, cap_c[h], inv_c[h]) + lr_win(now_m + req_m, cap_m[h], inv_m[h]);
-          const int32_t lr_snap =
-              lr_win(snp_c[h] + req_c, cap_c[h], inv_c[h]) + lr_win(snp_m[h] + req_m, cap_m[h], inv_m[h]);
-          drop = (lr_now >> 1) != (lr_snap >> 1);
-        }
-        if (!drop && spread_on && s >= 0 && ((s_mask[h] >> (s & 31)) & 1u)) {
-          // ServiceSpreading under an unchanged maxCount
-          const uint32_t* sv = L_svcs + (size_t)(h * 64 + lane) * KSG_SLOT_SVCS;
-          const int32_t* sc = L_scnt + (size_t)(h * 64 + lane) * KSG_SLOT_SVCS;
-          int32_t delta = 0, snapc = 0;
-          for (uint32_t a = 0; a < s_ns[h]; ++a)
-            if (sv[a] == (uint32_t)s) {
-              snapc = sc[a];
-              ++delta;
-            }
-          if (delta) drop = frac10_f32((int64_t)smax - snapc - delta, smax) != frac10_f32((int64_t)smax - snapc, smax);
-        }
+      for (int c = 0; c < KSG_RES_NCHK; ++c) done = done && ld_acq(&ctl->chk_seq[c]) >= i + 1;
+      if (done) break;
+      if (spin > 16 * KSG_SPIN_LIMIT) {
+        hung = true;
+        break;
       }
-      dmask[h] = __ballot(drop);
-      if (drop) atomicOr(reinterpret_cast<unsigned long long*>(L_drop + (sn[h] >> 6)), 1ULL << (sn[h] & 63));
-      KSG_COUNT(7, __popcll(__ballot(cand)) * 64)
     }
+    if (hung) {
+      resolved = i;
+      reason = KSG_STOP_HANG;
+      break;
+    }
+    uint32_t chk_drops = 0;
+#pragma unroll
+    for (int c = 0; c < KSG_RES_NCHK; ++c) chk_drops += __builtin_amdgcn_readfirstlane(ctl->chk_cnt[c][par]);
     KSG_STAMP(2)
+    // ---- the slot the previous pod just committed into: re-check it here
+    const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
+    bool a_drop = false;
+    uint32_t a_node = 0;
+    if (last_slot != KSG_NO_SLOT) {
+      a_node = __builtin_amdgcn_readfirstlane(S.meta[last_slot].node);
+      if ((t0e[a_node >> 6] >> (a_node & 63)) & 1ULL)
+        a_drop = __builtin_amdgcn_readfirstlane(
+                     (int)slot_drops(d, S, last_slot, pv, rec, res_on, ports_on, disk_on, spread_on)) != 0;
+    }
+    KSG_STAMP(3)
     // ---- selection: k live ties, ix-th in descending rank = (k-1-ix)-th ascending
-    const uint32_t dropped = __popcll(dmask[0]) + __popcll(dmask[1]);
+    const uint32_t dropped = chk_drops + (a_drop ? 1u : 0u);
     if (dropped >= k0) {
       resolved = i;  // every snapshot tie got worse: needs a fresh snapshot
       reason = KSG_STOP_EXHAUSTED;
@@ -770,7 +842,7 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
     if (dropped == 0) {
       woff = (uint32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].pred);  // staged by the producer
     } else {
-      KSG_COUNT(8, 64)
+      KSG_COUNT(7, 64)
       uint32_t ix;
       if (dropped < 64 && !(d.dbg & 32)) {  // KSG_DEBUG & 32: always the direct modulo
         ix = __builtin_amdgcn_readfirstlane(r_mod[e * 64 + dropped]);
@@ -780,14 +852,18 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
                            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r_hdr[e].r);
         ix = umod64_32(r, k);
       }
-      // live ties: T0 minus the dropped slot nodes, scattered into L_drop by the
-      // dropping lanes (lane l owns words l*P + q and clears them for the next pod)
-      lds_fence();
+      // live ties: T0 minus the checkers' drops (lane l owns words l*P + q and
+      // clears them for the pod two ahead) minus the re-checked slot's node
+      uint64_t* dw = L_drop + (size_t)par * P * 64;
       uint64_t live[P];
 #pragma unroll
       for (int q = 0; q < P; ++q) {
-        live[q] = t0e[lane * P + q] & ~L_drop[lane * P + q];
-        L_drop[lane * P + q] = 0;
+        live[q] = t0e[lane * P + q];
+        if (chk_drops) {
+          live[q] &= ~dw[lane * P + q];
+          dw[lane * P + q] = 0;
+        }
+        if (a_drop && lane * P + q == (a_node >> 6)) live[q] &= ~(1ULL << (a_node & 63));
       }
       uint32_t cl = 0;
 #pragma unroll
@@ -796,19 +872,18 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
       woff = select_in_lanes<P>(live, cl, incl, k - 1 - ix, lane);
     }
     const uint32_t wn = d.lo + woff;
-    KSG_STAMP(3)
+    KSG_STAMP(4)
 
     // ---- AssumePod into the window's slots; HBM is written back at window end
     const bool is_pred = (int32_t)woff == (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].pred);
-    const uint64_t hit0 = __ballot(lane < n_slots && sn[0] == woff);
-    const uint64_t hit1 = __ballot(64 + lane < n_slots && sn[1] == woff);
+    const uint64_t hit0 = __ballot(lane < n_slots && S.meta[lane].node == woff);
+    const uint64_t hit1 = __ballot(64 + lane < n_slots && S.meta[64 + lane].node == woff);
     uint32_t slot, base_nk = 0, base_ns = 0;
     const bool in_c = (hit0 | hit1) != 0;
     if (in_c) {
       slot = hit0 ? (uint32_t)__builtin_ctzll(hit0) : 64u + (uint32_t)__builtin_ctzll(hit1);
-      const int sl = (int)(slot & 63);
-      base_nk = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? s_nk[0] : s_nk[1]), sl);
-      base_ns = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? s_ns[0] : s_ns[1]), sl);
+      base_nk = __builtin_amdgcn_readfirstlane(S.meta[slot].nk);
+      base_ns = __builtin_amdgcn_readfirstlane(S.meta[slot].ns);
       if (base_nk + nk > KSG_SLOT_KEYS || base_ns + n_svcs > KSG_SLOT_SVCS) {
         resolved = i;  // this pod is redone (with the same draw) in the next window
         reason = KSG_STOP_SLOT;
@@ -821,100 +896,86 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
         break;
       }
       slot = n_slots++;
-      const int h = slot >> 6;
-      const bool owner = lane == (slot & 63);
-      // snapshot of the node: staged by the producer when it is the predicted
-      // node; otherwise the owner lane loads it and it is retired lazily
-      int64_t vc = 0, vm = 0, uc = 0, um = 0;
-      double ic = 0.0, im = 0.0;
-      if (is_pred) {
-        vc = r_hdr[e].cap_c;
-        vm = r_hdr[e].cap_m;
-        uc = r_hdr[e].used_c;
-        um = r_hdr[e].used_m;
-        ic = r_hdr[e].inv_c;
-        im = r_hdr[e].inv_m;
-      } else {
-        KSG_COUNT(9, 64)
-        if (owner) {
-          pl_cc = d.cap_cpu[wn];
-          pl_cm = d.cap_mem[wn];
-          pl_uc = d.used_cpu[wn];
-          pl_um = d.used_mem[wn];
-          pl_ic = d.inv10_cpu[wn];
-          pl_im = d.inv10_mem[wn];
-        }
-        p_snap = true;
-      }
-      if (owner) {
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh)
-          if (hh == h) {
-            sn[hh] = woff;
-            if (is_pred) {
-              cap_c[hh] = vc;
-              cap_m[hh] = vm;
-              snp_c[hh] = uc;
-              snp_m[hh] = um;
-              inv_c[hh] = ic;
-              inv_m[hh] = im;
-            }
-            dl_c[hh] = 0;
-            dl_m[hh] = 0;
-            s_nk[hh] = 0;
-            s_ns[hh] = 0;
-            s_mask[hh] = 0;
-          }
-      }
     }
-    KSG_STAMP(10)
+    // the choice is made: the checkers move on to pod i+1 (every slot but this one)
+    publish(i, slot, n_slots);
+    if (!in_c) {
+      // snapshot of the node: staged by the producer when it is the predicted
+      // node, else loaded here (L2-warm)
+      if (lane == 0) {
+        if (is_pred) {
+          S.cap[slot] = I64x2{r_hdr[e].cap_c, r_hdr[e].cap_m};
+          S.snp[slot] = I64x2{r_hdr[e].used_c, r_hdr[e].used_m};
+          S.inv[slot] = F64x2{r_hdr[e].inv_c, r_hdr[e].inv_m};
+        } else {
+          S.cap[slot] = I64x2{d.cap_cpu[wn], d.cap_mem[wn]};
+          S.snp[slot] = I64x2{d.used_cpu[wn], d.used_mem[wn]};
+          S.inv[slot] = F64x2{d.inv10_cpu[wn], d.inv10_mem[wn]};
+        }
+        S.dl[slot] = I64x2{0, 0};
+      }
+      if (!is_pred) KSG_COUNT(8, 64)
+    }
     // the pod's services (lane t < n_svcs): snapshot count on the node, maxCount, peer
     const uint32_t t_sv = lane < n_svcs ? lane : 0u;
     const uint32_t my_sv = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + t_sv, 63u), 64);
     const bool sv_lane = lane < n_svcs;
     uint32_t new_mask = 0;
     if (n_svcs) {
+      int32_t cnt = 0, mx = 0, peer = 0;
+      bool changed = false;
       if (sv_lane) {
-        pl_max = r_svc[e].max[lane];
-        pl_peer = r_svc[e].peer[lane];
-        pl_sv = my_sv;
-        // (predicted node: staged; else a lazily retired load, L2-warm)
-        pl_cnt = is_pred ? r_svc[e].cnt[lane] : d.svc_cnt[(size_t)my_sv * d.n_nodes + wn];
-        L_svcs[(size_t)slot * KSG_SLOT_SVCS + base_ns + lane] = my_sv;
+        mx = r_svc[e].max[lane];
+        peer = r_svc[e].peer[lane];
+        cnt = is_pred ? r_svc[e].cnt[lane] : d.svc_cnt[(size_t)my_sv * d.n_nodes + wn];
+        // in-window commits of this service on this node before this one
+        const uint32_t* sl = S.svcs + (size_t)slot * KSG_SLOT_SVCS;
+        uint32_t before = 0;
+        for (uint32_t b = 0; b < base_ns; ++b) before += sl[b] == my_sv;
+        if (spread_on && cnt + (int32_t)before + 1 > mx) changed = true;  // maxCount rises
+        if (aff_on && peer == -1 && !((L_peerset[my_sv >> 5] >> (my_sv & 31)) & 1u)) changed = true;
       }
-      p_svc = true;
+      // first commit of a service with no peer yet: record the peer (lane 0 applies, in order)
+      uint64_t pm = __ballot(sv_lane && peer == -1);
+      while (pm) {
+        const uint32_t b = __builtin_ctzll(pm);
+        pm &= pm - 1;
+        const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)b);
+        const bool fresh = !((L_peerset[fsv >> 5] >> (fsv & 31)) & 1u);
+        if (fresh) {
+          if (lane == 0) {
+            L_peerset[fsv >> 5] |= 1u << (fsv & 31);
+            L_peer[2 * n_peer] = fsv;
+            L_peer[2 * n_peer + 1] = wn;
+          }
+          ++n_peer;
+          lds_fence();
+        }
+      }
+      if (sv_lane) {
+        S.svcs[(size_t)slot * KSG_SLOT_SVCS + base_ns + lane] = my_sv;
+        S.scnt[(size_t)slot * KSG_SLOT_SVCS + base_ns + lane] = cnt;
+        if (changed) atomicOr(&L_flag[my_sv >> 5], 1u << (my_sv & 31));
+      }
       new_mask = wave_or_u32(sv_lane ? (1u << (my_sv & 31)) : 0u);
     }
-    p_slot = slot;
-    p_node = woff;
-    p_base = base_ns;
-    p_nsv = n_svcs;
-    // (the next pod nearly always has this node among its candidates: waiting
-    // here costs the same as waiting there)
-    retire();
-    KSG_STAMP(11)
     // ports then PDs sit at record dwords WS_IDS + [0, nk)
     const uint32_t my_key = (uint32_t)__shfl((int)rec, (int)(WS_IDS + (lane < nk ? lane : 0u)), 64);
-    if (lane < nk) L_keys[(size_t)slot * KSG_SLOT_KEYS + base_nk + lane] = my_key;
-    if (lane == (slot & 63)) {
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-        if (hh == (int)(slot >> 6)) {
-          dl_c[hh] = (int64_t)((uint64_t)dl_c[hh] + (uint64_t)req_c);
-          dl_m[hh] = (int64_t)((uint64_t)dl_m[hh] + (uint64_t)req_m);
-          s_nk[hh] += nk;
-          s_ns[hh] += n_svcs;
-          s_mask[hh] |= new_mask;
-        }
+    if (lane < nk) S.keys[(size_t)slot * KSG_SLOT_KEYS + base_nk + lane] = my_key;
+    if (lane == 0) {
+      const I64x2 ov = S.dl[slot];
+      S.dl[slot] = I64x2{(int64_t)((uint64_t)ov.c + (uint64_t)pv.req_c), (int64_t)((uint64_t)ov.m + (uint64_t)pv.req_m)};
+      const uint32_t om = in_c ? S.meta[slot].smask : 0u;
+      S.meta[slot] = SlotMeta{woff, base_nk + nk, base_ns + n_svcs, om | new_mask};
+      L_out[i] = (int32_t)wn;
     }
-    if (lane == 0) L_out[i] = (int32_t)wn;
     ++n_draws;
+    last_slot = slot;
     lds_fence();
     if (lane == 0) st_rel(&ctl->consumed, i + 1);
-    KSG_STAMP(4)
+    KSG_STAMP(5)
   }
   if (resolved < n_pods && lane == 0) st_rel(&ctl->stop, 1u);
-  retire();
   if constexpr (STAMP) {
     if (lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
   }
@@ -922,35 +983,33 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
 #undef KSG_COUNT
 
   // ---- write the window's deltas back to HBM (the next snapshot) -------------
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const uint32_t t = (uint32_t)h * 64 + lane;
-    if (t < n_slots) {
-      const uint32_t n = d.lo + sn[h];
-      d.used_cpu[n] = (int64_t)((uint64_t)snp_c[h] + (uint64_t)dl_c[h]);
-      d.used_mem[n] = (int64_t)((uint64_t)snp_m[h] + (uint64_t)dl_m[h]);
-      const uint32_t* ks = L_keys + (size_t)t * KSG_SLOT_KEYS;
-      for (uint32_t a = 0; a < s_nk[h]; ++a)
-        __hip_atomic_fetch_or(d.keymap + (size_t)ks[a] * d.nw + (n >> 6), 1ULL << (n & 63), __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t* sv = L_svcs + (size_t)t * KSG_SLOT_SVCS;
-      const int32_t* sc = L_scnt + (size_t)t * KSG_SLOT_SVCS;
-      for (uint32_t a = 0; a < s_ns[h]; ++a) {
-        const uint32_t sa = sv[a];
-        bool first = true;
-        int32_t count = 0;
-        for (uint32_t b = 0; b < s_ns[h]; ++b) {
-          if (sv[b] == sa) {
-            if (b < a) first = false;
-            ++count;
-          }
+  for (uint32_t t = lane; t < n_slots; t += 64) {
+    const SlotMeta me = S.meta[t];
+    const uint32_t n = d.lo + me.node;
+    const I64x2 snp = S.snp[t], dl = S.dl[t];
+    d.used_cpu[n] = (int64_t)((uint64_t)snp.c + (uint64_t)dl.c);
+    d.used_mem[n] = (int64_t)((uint64_t)snp.m + (uint64_t)dl.m);
+    const uint32_t* ks = S.keys + (size_t)t * KSG_SLOT_KEYS;
+    for (uint32_t a = 0; a < me.nk; ++a)
+      __hip_atomic_fetch_or(d.keymap + (size_t)ks[a] * d.nw + (n >> 6), 1ULL << (n & 63), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t* sv = S.svcs + (size_t)t * KSG_SLOT_SVCS;
+    const int32_t* sc = S.scnt + (size_t)t * KSG_SLOT_SVCS;
+    for (uint32_t a = 0; a < me.ns; ++a) {
+      const uint32_t sa = sv[a];
+      bool first = true;
+      int32_t count = 0;
+      for (uint32_t b = 0; b < me.ns; ++b) {
+        if (sv[b] == sa) {
+          if (b < a) first = false;
+          ++count;
         }
-        __hip_atomic_fetch_add(d.svc_total + sa, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (first) {
-          const int32_t fin = sc[a] + count;
-          d.svc_cnt[(size_t)sa * d.n_nodes + n] = fin;
-          __hip_atomic_fetch_max(d.svc_max + sa, fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+      }
+      __hip_atomic_fetch_add(d.svc_total + sa, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (first) {
+        const int32_t fin = sc[a] + count;
+        d.svc_cnt[(size_t)sa * d.n_nodes + n] = fin;
+        __hip_atomic_fetch_max(d.svc_max + sa, fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
