@@ -24,6 +24,8 @@
 
 #define KSG_NT 1024          // threads of the single-workgroup scan kernels
 #define KSG_NWAVE (KSG_NT / 64)
+#define KSG_R_LDS 32         // largest R whose per-node scores fit the LDS (R * 4 KiB)
+#define KSG_R_MAX 128        // nodes per thread of the exact kernels: shards up to 131072 nodes
 
 #define KSG_MODE_EVAL 0      // write fail codes + scores for every node
 #define KSG_MODE_BEGIN 1     // write {M, k, tie words} record (+ optional fail codes)
@@ -74,6 +76,7 @@ struct KsgDev {
   int32_t* svc_peer;
   const int32_t* anti_domain;
   const int32_t* aff_pair;
+  int32_t* score_scratch;     // exact kernels with R > KSG_R_LDS: per-node scores in HBM, not LDS
 };
 
 // static-table configuration (LabelsPresence, EqualPriority, LabelPreference,

@@ -144,8 +144,10 @@ __global__ __launch_bounds__(KSG_NT) void ksg_batch_kernel(KsgDev d, const ksg_p
                                                           uint32_t n_pods, uint64_t* rng_io,
                                                           int32_t* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  int32_t* s_score = reinterpret_cast<int32_t*>(smem);
-  int32_t* s_dcount = s_score + R * KSG_NT;
+  // per-node scores: LDS up to KSG_R_LDS nodes per thread, else HBM scratch
+  // (each thread only ever reads back its own entries)
+  int32_t* s_score = R > KSG_R_LDS ? d.score_scratch : reinterpret_cast<int32_t*>(smem);
+  int32_t* s_dcount = R > KSG_R_LDS ? reinterpret_cast<int32_t*>(smem) : s_score + R * KSG_NT;
   __shared__ uint64_t s_tie[R * KSG_NWAVE];
   __shared__ int32_t s_wmax[KSG_NWAVE];
   __shared__ uint32_t s_wcnt[KSG_NWAVE];
@@ -235,8 +237,10 @@ __global__ __launch_bounds__(KSG_NT) void ksg_scan_kernel(KsgDev d, const ksg_po
                                                          int32_t* __restrict__ dpart,
                                                          const int32_t* __restrict__ dglobal) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  int32_t* s_score = reinterpret_cast<int32_t*>(smem);
-  int32_t* s_dcount = s_score + R * KSG_NT;
+  // per-node scores: LDS up to KSG_R_LDS nodes per thread, else HBM scratch
+  // (each thread only ever reads back its own entries)
+  int32_t* s_score = R > KSG_R_LDS ? d.score_scratch : reinterpret_cast<int32_t*>(smem);
+  int32_t* s_dcount = R > KSG_R_LDS ? reinterpret_cast<int32_t*>(smem) : s_score + R * KSG_NT;
   __shared__ uint64_t s_tie[R * KSG_NWAVE];
   __shared__ int32_t s_wmax[KSG_NWAVE];
   __shared__ uint32_t s_wcnt[KSG_NWAVE];
@@ -459,7 +463,7 @@ __global__ void ksg_patch_kernel(const KsgPatch* __restrict__ patches, uint32_t 
 // ---- launch wrappers (called from ksg_runtime.cpp) ------------------------
 // dynamic LDS = R*1024 int32 scores + the anti-affinity domain counts
 static size_t lds_bytes(int R, const KsgDev& d) {
-  return (size_t)R * KSG_NT * sizeof(int32_t) + (size_t)d.n_domains_total * sizeof(int32_t);
+  return (R > KSG_R_LDS ? 0 : (size_t)R * KSG_NT * sizeof(int32_t)) + (size_t)d.n_domains_total * sizeof(int32_t);
 }
 
 template <typename K>
@@ -489,6 +493,8 @@ static hipError_t launch_batch_a(int R, const KsgDev& d, const ksg_pod* pods, co
     case 8: return launch_batch_t<8, ANTI, false>(d, pods, ids, n, rng, out, st);
     case 16: return launch_batch_t<16, ANTI, false>(d, pods, ids, n, rng, out, st);
     case 32: return launch_batch_t<32, ANTI, false>(d, pods, ids, n, rng, out, st);
+    case 64: return launch_batch_t<64, ANTI, false>(d, pods, ids, n, rng, out, st);
+    case 128: return launch_batch_t<128, ANTI, false>(d, pods, ids, n, rng, out, st);
   }
   return hipErrorInvalidValue;
 }
@@ -515,6 +521,8 @@ static hipError_t launch_scan_a(int R, const KsgDev& d, const ksg_pod* pods, con
     case 8: return launch_scan_t<8, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, st);
     case 16: return launch_scan_t<16, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, st);
     case 32: return launch_scan_t<32, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, st);
+    case 64: return launch_scan_t<64, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, st);
+    case 128: return launch_scan_t<128, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, st);
   }
   return hipErrorInvalidValue;
 }

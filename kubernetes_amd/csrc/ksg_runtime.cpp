@@ -64,7 +64,7 @@ struct PodRec {
   uint64_t seq;
 };
 
-constexpr uint32_t kMaxNodesPerShard = 32 * KSG_NT;
+constexpr uint32_t kMaxNodesPerShard = KSG_R_MAX * KSG_NT;
 
 }  // namespace
 
@@ -461,7 +461,7 @@ KsgDev full_geometry(const ksg_ctx* c) {
 }
 
 bool use_window(ksg_ctx* c, const ksg_pod* pods, uint32_t n) {
-  if (c->window == 0 || anti_on(c) || c->nw > 8 * 64 || ksg_win_max_window(full_geometry(c)) < 8) return false;
+  if (c->window == 0 || anti_on(c) || c->nw > 32 * 64 || ksg_win_max_window(full_geometry(c)) < 8) return false;
   // monotonicity under commits needs non-negative pod-dependent weights
   if (c->cfg.w_least_requested < 0 || c->cfg.w_service_spreading < 0) return false;
   // lr_win (ksg_device.h) is exact for 0 <= capacity, requested totals <= 2^49
@@ -630,7 +630,9 @@ int ksg_destroy(ksg_ctx* c) {
     (void)hipMemcpy(h, c->dev.dbgbuf, sizeof h, hipMemcpyDeviceToHost);
     fprintf(stderr, "ksg stamps (x64 cycles, committer wave): ring-wait %d head %d wait-checkers %d "
             "recheck-last-slot %d select %d commit %d | drop-path pods %d unpredicted commits %d\n",
-            h[0], h[1], h[2], h[3], h[4], h[5], h[7], h[8]);
+            h[0], h[1], h[2], h[3], h[4], h[5] + h[9] + h[10] + h[11] + h[12], h[7], h[8]);
+    fprintf(stderr, "ksg commit split: slot+publish %d loads-issue %d svc-lds %d svc-finish+snap %d tail %d\n",
+            h[9], h[10], h[11], h[12], h[5]);
   }
   (void)hipSetDevice(c->device);
   if (c->st) (void)hipStreamSynchronize(c->st);
@@ -718,7 +720,7 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   int64_t *cap_c, *cap_m;
   double *inv_c, *inv_m;
   uint64_t *sfit, *keymap, *pairmap;
-  int32_t *sscore, *anti_dom, *aff_pair;
+  int32_t *sscore, *anti_dom, *aff_pair, *gscore = nullptr;
   const size_t NN = std::max<uint32_t>(n_nodes, 1);
   if ((rc = dalloc(c, &cap_c, NN, owner)) || (rc = dalloc(c, &cap_m, NN, owner)) ||
       (rc = dalloc(c, &inv_c, NN, owner)) || (rc = dalloc(c, &inv_m, NN, owner)) ||
@@ -732,7 +734,8 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
       (rc = dalloc(c, &d.svc_total, std::max<uint32_t>(n_services, 1), owner)) ||
       (rc = dalloc(c, &d.svc_peer, std::max<uint32_t>(n_services, 1), owner)) ||
       (rc = dalloc(c, &anti_dom, (size_t)std::max<uint32_t>(c->cfg.n_anti, 1) * NN, owner)) ||
-      (rc = dalloc(c, &aff_pair, (size_t)std::max<uint32_t>(c->cfg.n_aff_labels, 1) * NN, owner)))
+      (rc = dalloc(c, &aff_pair, (size_t)std::max<uint32_t>(c->cfg.n_aff_labels, 1) * NN, owner)) ||
+      (c->R > KSG_R_LDS && (rc = dalloc(c, &gscore, (size_t)c->R * KSG_NT, owner))))
     return rc;
   if (n_services) HIPCHK(c, hipMemsetAsync(d.svc_peer, 0xff, n_services * sizeof(int32_t), c->st));
 
@@ -836,6 +839,7 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   d.pairmap = pairmap;
   d.anti_domain = anti_dom;
   d.aff_pair = aff_pair;
+  d.score_scratch = gscore;
   c->lds = (size_t)d.n_domains_total * sizeof(int32_t);
 
   // scratch sized for the shard

@@ -271,7 +271,8 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
 #define KSG_RES_NCHK 2                                // checker waves 1, 2
 #define KSG_RES_P0 (1 + KSG_RES_NCHK)                 // first producer wave
 #define KSG_RES_NPW (KSG_RES_NT / 64 - KSG_RES_P0)    // producer waves
-#define KSG_RING 16
+// ring entries: 16, or 4 when the T0 words of an entry are large (P > 8: more than 32k nodes)
+__host__ __device__ constexpr uint32_t win_ring(uint32_t P) { return P <= 8 ? 16u : 4u; }
 #define KSG_SLOT_KEYS 8
 #define KSG_SLOT_SVCS 12
 #define KSG_MAX_SLOTS (64 * KSG_RES_NCHK)
@@ -332,6 +333,7 @@ __host__ __device__ constexpr uint32_t win_al16(size_t x) { return (uint32_t)((x
 
 __host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag, uint32_t W) {
   WinLdsOff o;
+  const uint32_t KSG_RING = win_ring(P);
   uint32_t at = 0;
   o.ctl = at;     at += win_al16(sizeof(WinCtl));
   o.r_hdr = at;   at += win_al16((size_t)KSG_RING * sizeof(RingHdr));
@@ -503,6 +505,7 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
   const uint32_t nflag = (d.n_services + 31) / 32;
   const uint32_t nshard = d.hi - d.lo;
   const uint32_t nwords = d.nwords;
+  constexpr uint32_t KSG_RING = win_ring(P);
   const WinLdsOff o = win_lds_offsets(P, nflag, wcap);
   WinCtl* ctl = reinterpret_cast<WinCtl*>(smem + o.ctl);
   RingHdr* r_hdr = reinterpret_cast<RingHdr*>(smem + o.r_hdr);
@@ -899,42 +902,49 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
     }
     // the choice is made: the checkers move on to pod i+1 (every slot but this one)
     publish(i, slot, n_slots);
+    KSG_STAMP(9)
+    const bool fetch = !in_c && !is_pred;  // the node's snapshot must come from HBM
+    if (fetch) KSG_COUNT(8, 64)
+    // Loads first, uses last: lanes 0..5 fetch the node's capacity, requested
+    // totals and 10/capacity (one vector load, per-lane address), service lanes
+    // its service counts, and the LDS work below runs while they are in flight.
+    uint64_t snapv = 0;
     if (!in_c) {
-      // snapshot of the node: staged by the producer when it is the predicted
-      // node, else loaded here (L2-warm)
-      if (lane == 0) {
-        if (is_pred) {
-          S.cap[slot] = I64x2{r_hdr[e].cap_c, r_hdr[e].cap_m};
-          S.snp[slot] = I64x2{r_hdr[e].used_c, r_hdr[e].used_m};
-          S.inv[slot] = F64x2{r_hdr[e].inv_c, r_hdr[e].inv_m};
-        } else {
-          S.cap[slot] = I64x2{d.cap_cpu[wn], d.cap_mem[wn]};
-          S.snp[slot] = I64x2{d.used_cpu[wn], d.used_mem[wn]};
-          S.inv[slot] = F64x2{d.inv10_cpu[wn], d.inv10_mem[wn]};
-        }
-        S.dl[slot] = I64x2{0, 0};
+      if (is_pred) {
+        if (lane < 6) snapv = reinterpret_cast<const uint64_t*>(&r_hdr[e].cap_c)[lane];
+      } else if (lane < 6) {
+        const uint64_t* src = lane == 0   ? reinterpret_cast<const uint64_t*>(d.cap_cpu)
+                              : lane == 1 ? reinterpret_cast<const uint64_t*>(d.cap_mem)
+                              : lane == 2 ? reinterpret_cast<const uint64_t*>(d.used_cpu)
+                              : lane == 3 ? reinterpret_cast<const uint64_t*>(d.used_mem)
+                              : lane == 4 ? reinterpret_cast<const uint64_t*>(d.inv10_cpu)
+                                          : reinterpret_cast<const uint64_t*>(d.inv10_mem);
+        snapv = src[wn];
       }
-      if (!is_pred) KSG_COUNT(8, 64)
     }
     // the pod's services (lane t < n_svcs): snapshot count on the node, maxCount, peer
     const uint32_t t_sv = lane < n_svcs ? lane : 0u;
     const uint32_t my_sv = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + t_sv, 63u), 64);
     const bool sv_lane = lane < n_svcs;
+    int32_t cnt = 0;
+    if (sv_lane) cnt = is_pred ? r_svc[e].cnt[lane] : d.svc_cnt[(size_t)my_sv * d.n_nodes + wn];
+    KSG_STAMP(10)
+    // ports then PDs sit at record dwords WS_IDS + [0, nk)
+    const uint32_t my_key = (uint32_t)__shfl((int)rec, (int)(WS_IDS + (lane < nk ? lane : 0u)), 64);
+    if (lane < nk) S.keys[(size_t)slot * KSG_SLOT_KEYS + base_nk + lane] = my_key;
     uint32_t new_mask = 0;
     if (n_svcs) {
-      int32_t cnt = 0, mx = 0, peer = 0;
-      bool changed = false;
+      int32_t mx = 0, peer = 0;
+      uint32_t before = 0;
       if (sv_lane) {
         mx = r_svc[e].max[lane];
         peer = r_svc[e].peer[lane];
-        cnt = is_pred ? r_svc[e].cnt[lane] : d.svc_cnt[(size_t)my_sv * d.n_nodes + wn];
         // in-window commits of this service on this node before this one
         const uint32_t* sl = S.svcs + (size_t)slot * KSG_SLOT_SVCS;
-        uint32_t before = 0;
         for (uint32_t b = 0; b < base_ns; ++b) before += sl[b] == my_sv;
-        if (spread_on && cnt + (int32_t)before + 1 > mx) changed = true;  // maxCount rises
-        if (aff_on && peer == -1 && !((L_peerset[my_sv >> 5] >> (my_sv & 31)) & 1u)) changed = true;
+        S.svcs[(size_t)slot * KSG_SLOT_SVCS + base_ns + lane] = my_sv;
       }
+      bool changed = sv_lane && aff_on && peer == -1 && !((L_peerset[my_sv >> 5] >> (my_sv & 31)) & 1u);
       // first commit of a service with no peer yet: record the peer (lane 0 applies, in order)
       uint64_t pm = __ballot(sv_lane && peer == -1);
       while (pm) {
@@ -952,16 +962,25 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
           lds_fence();
         }
       }
+      new_mask = wave_or_u32(sv_lane ? (1u << (my_sv & 31)) : 0u);
+      KSG_STAMP(11)
+      // the service counts are needed from here on
       if (sv_lane) {
-        S.svcs[(size_t)slot * KSG_SLOT_SVCS + base_ns + lane] = my_sv;
+        if (spread_on && cnt + (int32_t)before + 1 > mx) changed = true;  // maxCount rises
         S.scnt[(size_t)slot * KSG_SLOT_SVCS + base_ns + lane] = cnt;
         if (changed) atomicOr(&L_flag[my_sv >> 5], 1u << (my_sv & 31));
       }
-      new_mask = wave_or_u32(sv_lane ? (1u << (my_sv & 31)) : 0u);
     }
-    // ports then PDs sit at record dwords WS_IDS + [0, nk)
-    const uint32_t my_key = (uint32_t)__shfl((int)rec, (int)(WS_IDS + (lane < nk ? lane : 0u)), 64);
-    if (lane < nk) S.keys[(size_t)slot * KSG_SLOT_KEYS + base_nk + lane] = my_key;
+    if (!in_c) {
+      // lanes 0..5 -> cap.c, cap.m, snp.c, snp.m, inv.c, inv.m of the slot
+      uint64_t* dst = lane < 2   ? reinterpret_cast<uint64_t*>(&S.cap[slot]) + lane
+                      : lane < 4 ? reinterpret_cast<uint64_t*>(&S.snp[slot]) + (lane - 2)
+                                 : reinterpret_cast<uint64_t*>(&S.inv[slot]) + (lane & 1);
+      if (lane < 6) *dst = snapv;
+      if (lane == 0) S.dl[slot] = I64x2{0, 0};
+    }
+    KSG_STAMP(12)
+    lds_fence();
     if (lane == 0) {
       const I64x2 ov = S.dl[slot];
       S.dl[slot] = I64x2{(int64_t)((uint64_t)ov.c + (uint64_t)pv.req_c), (int64_t)((uint64_t)ov.m + (uint64_t)pv.req_m)};
@@ -1041,7 +1060,7 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
 // ---------------------------------------------------------------------------
 static uint32_t win_P(const KsgDev& d) {
   const uint32_t P = (d.nwords + 63) / 64;
-  return P <= 1 ? 1 : P <= 2 ? 2 : P <= 4 ? 4 : P <= 8 ? 8 : 0;
+  return P <= 1 ? 1 : P <= 2 ? 2 : P <= 4 ? 4 : P <= 8 ? 8 : P <= 16 ? 16 : P <= 32 ? 32 : 0;
 }
 
 static const size_t kWinLdsBudget = 156 * 1024;
@@ -1099,6 +1118,8 @@ hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run
   KSG_RES_CASE(2)
   KSG_RES_CASE(4)
   KSG_RES_CASE(8)
+  KSG_RES_CASE(16)
+  KSG_RES_CASE(32)
 #undef KSG_RES_CASE
   return hipErrorInvalidValue;
 }
