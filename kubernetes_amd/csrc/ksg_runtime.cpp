@@ -628,8 +628,8 @@ int ksg_destroy(ksg_ctx* c) {
   if (c->dev.dbgbuf) {  // debug stamps (KSG_DEBUG & 8): cycles/64 per resolver section
     int32_t h[16];
     (void)hipMemcpy(h, c->dev.dbgbuf, sizeof h, hipMemcpyDeviceToHost);
-    fprintf(stderr, "ksg stamps (x64 cycles, committer wave): ring-wait %d head %d wait-checkers %d "
-            "recheck-last-slot %d select %d commit %d | drop-path pods %d unpredicted commits %d\n",
+    fprintf(stderr, "ksg stamps (x64 cycles, committer wave): ring-wait %d head %d recheck-last-slot %d "
+            "wait-checkers %d select %d commit %d | drop-path pods %d unpredicted commits %d\n",
             h[0], h[1], h[2], h[3], h[4], h[5] + h[9] + h[10] + h[11] + h[12], h[7], h[8]);
     fprintf(stderr, "ksg commit split: slot+publish %d loads-issue %d svc-lds %d svc-finish+snap %d tail %d\n",
             h[9], h[10], h[11], h[12], h[5]);

@@ -732,6 +732,8 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
   uint32_t* const L_peerset = reinterpret_cast<uint32_t*>(smem + o.peerset);
   uint32_t resolved = n_pods, reason = 0, n_slots = 0, n_peer = 0, n_draws = 0;
   uint32_t last_slot = KSG_NO_SLOT;  // slot the previous pod committed into
+  uint32_t last_node = 0;            // and its node
+  uint32_t cn0 = ~0u, cn1 = ~0u;     // nodes of slots lane and 64 + lane (the committer's copy)
 
   // KSG_DEBUG & 8: per-section s_memtime; lane k accumulates section k in a
   // VGPR (no scalar registers taken from the chain)
@@ -802,6 +804,17 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
     }
     KSG_STAMP(1)
 
+    // ---- the slot the previous pod just committed into: re-check it here
+    const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
+    bool a_drop = false;
+    uint32_t a_node = 0;
+    if (last_slot != KSG_NO_SLOT) {
+      a_node = last_node;
+      if ((t0e[a_node >> 6] >> (a_node & 63)) & 1ULL)
+        a_drop = __builtin_amdgcn_readfirstlane(
+                     (int)slot_drops(d, S, last_slot, pv, rec, res_on, ports_on, disk_on, spread_on)) != 0;
+    }
+    KSG_STAMP(2)
     // ---- the checkers' drops for this pod (every slot but last_slot)
     for (uint32_t spin = 0;; ++spin) {
       bool done = true;
@@ -821,17 +834,6 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
     uint32_t chk_drops = 0;
 #pragma unroll
     for (int c = 0; c < KSG_RES_NCHK; ++c) chk_drops += __builtin_amdgcn_readfirstlane(ctl->chk_cnt[c][par]);
-    KSG_STAMP(2)
-    // ---- the slot the previous pod just committed into: re-check it here
-    const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
-    bool a_drop = false;
-    uint32_t a_node = 0;
-    if (last_slot != KSG_NO_SLOT) {
-      a_node = __builtin_amdgcn_readfirstlane(S.meta[last_slot].node);
-      if ((t0e[a_node >> 6] >> (a_node & 63)) & 1ULL)
-        a_drop = __builtin_amdgcn_readfirstlane(
-                     (int)slot_drops(d, S, last_slot, pv, rec, res_on, ports_on, disk_on, spread_on)) != 0;
-    }
     KSG_STAMP(3)
     // ---- selection: k live ties, ix-th in descending rank = (k-1-ix)-th ascending
     const uint32_t dropped = chk_drops + (a_drop ? 1u : 0u);
@@ -879,8 +881,8 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
 
     // ---- AssumePod into the window's slots; HBM is written back at window end
     const bool is_pred = (int32_t)woff == (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].pred);
-    const uint64_t hit0 = __ballot(lane < n_slots && S.meta[lane].node == woff);
-    const uint64_t hit1 = __ballot(64 + lane < n_slots && S.meta[64 + lane].node == woff);
+    const uint64_t hit0 = __ballot(cn0 == woff);
+    const uint64_t hit1 = __ballot(cn1 == woff);
     uint32_t slot, base_nk = 0, base_ns = 0;
     const bool in_c = (hit0 | hit1) != 0;
     if (in_c) {
@@ -899,6 +901,10 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
         break;
       }
       slot = n_slots++;
+      if (lane == (slot & 63)) {
+        if (slot < 64) cn0 = woff;
+        else cn1 = woff;
+      }
     }
     // the choice is made: the checkers move on to pod i+1 (every slot but this one)
     publish(i, slot, n_slots);
@@ -990,6 +996,7 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
     }
     ++n_draws;
     last_slot = slot;
+    last_node = woff;
     lds_fence();
     if (lane == 0) st_rel(&ctl->consumed, i + 1);
     KSG_STAMP(5)
