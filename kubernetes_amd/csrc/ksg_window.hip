@@ -268,8 +268,9 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
 // The node state in HBM stays the pristine snapshot while the window
 // resolves; the window's deltas are written back once, at the end.
 #define KSG_RES_NT 512
-#define KSG_RES_NCHK 2                                // checker waves 1, 2
-#define KSG_RES_P0 (1 + KSG_RES_NCHK)                 // first producer wave
+#define KSG_RES_C0 2                                  // first checker wave (0: committer, 1: scribe)
+#define KSG_RES_NCHK 2                                // checker waves
+#define KSG_RES_P0 (KSG_RES_C0 + KSG_RES_NCHK)        // first producer wave
 #define KSG_RES_NPW (KSG_RES_NT / 64 - KSG_RES_P0)    // producer waves
 // ring entries: 16, or 4 when the T0 words of an entry are large (P > 8: more than 32k nodes)
 __host__ __device__ constexpr uint32_t win_ring(uint32_t P) { return P <= 8 ? 16u : 4u; }
@@ -317,7 +318,21 @@ struct alignas(16) WinCtl {
   uint32_t pad0;
   uint32_t chk_seq[KSG_RES_NCHK];     // pods checker c is done with
   uint32_t chk_cnt[KSG_RES_NCHK][2];  // checker c's drops for the pod of parity p
-  uint32_t pad[4];
+  uint32_t order_seq;                 // orders the committer has issued (one per pod)
+  uint32_t scribe_done;               // orders the scribe has written into the slots
+  uint32_t n_peer;                    // services given their first peer in the window
+  uint32_t pad[1];
+};
+// One pod's outcome, handed from the committer to the scribe (two buffers, by
+// pod parity). The scribe reads the pod itself from its ring entry.
+struct alignas(16) WinOrder {
+  uint32_t kind;     // 0: no commit (error / no fit), 1: commit
+  uint32_t slot, node;
+  int32_t out;       // placement (node rank or KSG_OUT_*)
+  uint32_t e;        // ring entry of the pod
+  uint32_t in_c;     // the slot existed before this commit
+  uint32_t is_pred;  // the node is the producer's predicted node (its snapshot is staged)
+  uint32_t pad;
 };
 
 // byte offsets of the resolver's dynamic LDS arrays (host and device agree)
@@ -325,7 +340,7 @@ struct WinLdsOff {
   uint32_t ctl, r_hdr, r_t0, r_rec, r_mod, r_svc;     // ring
   uint32_t s_meta, s_cap, s_snp, s_dl, s_inv;          // slots
   uint32_t keys, svcs, scnt;
-  uint32_t peer, out, flag, peerset, drop;
+  uint32_t peer, out, flag, peerset, drop, ord;
   uint32_t total;
 };
 
@@ -354,6 +369,7 @@ __host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag,
   o.flag = at;    at += win_al16((size_t)nflag * 4);
   o.peerset = at; at += win_al16((size_t)nflag * 4);
   o.drop = at;    at += win_al16((size_t)2 * P * 64 * 8);
+  o.ord = at;     at += win_al16((size_t)2 * sizeof(WinOrder));
   o.total = at;
   return o;
 }
@@ -678,62 +694,204 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
   }
 
   // =========================================================================
-  // checkers (waves 1 .. KSG_RES_NCHK): slot 64c + lane of checker c
+  // checkers (waves KSG_RES_C0 ..): slot 64c + lane of checker c
   // =========================================================================
-  if (wave < KSG_RES_P0) {
-    if (wave != 0) {
-      __builtin_amdgcn_s_setprio(2);
-      const uint32_t c = wave - 1;
-      const uint32_t sl = c * 64 + lane;
-      for (uint32_t i = 0; i < n_pods; ++i) {
-        const uint32_t e = i % KSG_RING, par = i & 1;
-        // pod i is staged and the committer has chosen pod i-1's node (while
-        // this checker works on pod i the committer cannot pass pod i-1: it
-        // waits for this checker before selecting pod i)
-        for (uint32_t spin = 0;; ++spin) {
-          if (ld_acq(&ctl->stop) || spin > 16 * KSG_SPIN_LIMIT) return;
-          if (ld_acq(&r_hdr[e].ready) == i + 1 && ld_acq(&ctl->sel_seq) >= i) break;
+  if (wave >= KSG_RES_C0) {
+    __builtin_amdgcn_s_setprio(2);
+    const uint32_t c = wave - KSG_RES_C0;
+    const uint32_t sl = c * 64 + lane;
+    for (uint32_t i = 0; i < n_pods; ++i) {
+      const uint32_t e = i % KSG_RING, par = i & 1;
+      // pod i is staged, the committer has chosen pod i-1's node (slot xs,
+      // skipped here), and the scribe has written every commit before pod i-1.
+      // While this checker works on pod i the committer cannot pass pod i-1:
+      // it waits for this checker before selecting pod i.
+      for (uint32_t spin = 0;; ++spin) {
+        if (ld_acq(&ctl->stop) || spin > 16 * KSG_SPIN_LIMIT) return;
+        if (ld_acq(&r_hdr[e].ready) == i + 1 && ld_acq(&ctl->sel_seq) >= i && ld_acq(&ctl->scribe_done) + 1 >= i)
+          break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      const uint32_t xs = ctl->xs_slot, ns = ctl->xs_nslots;
+      const uint32_t rec = lane < KSG_WIN_SUM_DWORDS ? r_rec[e * KSG_WIN_SUM_DWORDS + lane] : 0u;
+      const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
+      uint32_t cnt = 0;
+      if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE && c * 64 < ns) {
+        const PodView pv = pod_view(rec);
+        const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
+        bool drop = false;
+        if (sl < ns && sl != xs) {
+          const uint32_t nd = S.meta[sl].node;
+          if ((t0e[nd >> 6] >> (nd & 63)) & 1ULL) {
+            drop = slot_drops(d, S, sl, pv, rec, res_on, ports_on, disk_on, spread_on);
+            if (drop)
+              atomicOr(reinterpret_cast<unsigned long long*>(L_drop + (size_t)par * P * 64 + (nd >> 6)),
+                       1ULL << (nd & 63));
+          }
         }
-        const uint32_t xs = ctl->xs_slot, ns = ctl->xs_nslots;
+        cnt = __popcll(__ballot(drop));
+      }
+      if (lane == 0) {
+        ctl->chk_cnt[c][par] = cnt;
+        st_rel(&ctl->chk_seq[c], i + 1);
+      }
+    }
+    return;
+  }
+
+  uint32_t* const L_peer = reinterpret_cast<uint32_t*>(smem + o.peer);
+  int32_t* const L_out = reinterpret_cast<int32_t*>(smem + o.out);
+  uint32_t* const L_flag = reinterpret_cast<uint32_t*>(smem + o.flag);
+  uint32_t* const L_peerset = reinterpret_cast<uint32_t*>(smem + o.peerset);
+  WinOrder* const L_ord = reinterpret_cast<WinOrder*>(smem + o.ord);  // [2] by pod parity
+
+  // =========================================================================
+  // scribe (wave 1): applies each commit to the LDS slot state, in order
+  // =========================================================================
+  if (wave == 1) {
+    __builtin_amdgcn_s_setprio(2);
+    uint32_t n_peer = 0;
+    for (uint32_t i = 0;; ++i) {
+      bool have = false;
+      // (no spin limit: the committer's own waits are bounded and it always
+      // raises stop, after its last order)
+      for (;;) {
+        if (ld_acq(&ctl->order_seq) >= i + 1) {
+          have = true;
+          break;
+        }
+        if (ld_acq(&ctl->stop) && ld_acq(&ctl->order_seq) <= i) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (!have) break;
+      const WinOrder& od = L_ord[i & 1];
+      const uint32_t kind = __builtin_amdgcn_readfirstlane(od.kind);
+      const int32_t outv = __builtin_amdgcn_readfirstlane(od.out);
+      if (kind == 1) {
+        const uint32_t slot = __builtin_amdgcn_readfirstlane(od.slot);
+        const uint32_t woff = __builtin_amdgcn_readfirstlane(od.node);
+        const uint32_t e = __builtin_amdgcn_readfirstlane(od.e);
+        const bool in_c = __builtin_amdgcn_readfirstlane(od.in_c) != 0;
+        const bool is_pred = __builtin_amdgcn_readfirstlane(od.is_pred) != 0;
+        const uint32_t wn = d.lo + woff;
+        // the pod, from its ring entry (released to the producers only below)
         const uint32_t rec = lane < KSG_WIN_SUM_DWORDS ? r_rec[e * KSG_WIN_SUM_DWORDS + lane] : 0u;
-        const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
-        uint32_t cnt = 0;
-        if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE && c * 64 < ns) {
-          const PodView pv = pod_view(rec);
-          const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
-          bool drop = false;
-          if (sl < ns && sl != xs) {
-            const uint32_t nd = S.meta[sl].node;
-            if ((t0e[nd >> 6] >> (nd & 63)) & 1ULL) {
-              drop = slot_drops(d, S, sl, pv, rec, res_on, ports_on, disk_on, spread_on);
-              if (drop)
-                atomicOr(reinterpret_cast<unsigned long long*>(L_drop + (size_t)par * P * 64 + (nd >> 6)),
-                         1ULL << (nd & 63));
+        const PodView pv = pod_view(rec);
+        const uint32_t nss = __builtin_amdgcn_readlane(rec, WS_NSS);
+        const uint32_t n_sel = nss & 0xffff, n_svcs = nss >> 16, nk = pv.nk;
+        uint32_t base_nk = 0, base_ns = 0, om = 0;
+        if (in_c) {
+          base_nk = __builtin_amdgcn_readfirstlane(S.meta[slot].nk);
+          base_ns = __builtin_amdgcn_readfirstlane(S.meta[slot].ns);
+          om = __builtin_amdgcn_readfirstlane(S.meta[slot].smask);
+        }
+        // new slot: the node's snapshot (staged for the predicted node, else from HBM)
+        if (!in_c && lane < 6) {
+          uint64_t v;
+          if (is_pred) {
+            v = reinterpret_cast<const uint64_t*>(&r_hdr[e].cap_c)[lane];
+          } else {
+            const uint64_t* src = lane == 0   ? reinterpret_cast<const uint64_t*>(d.cap_cpu)
+                                  : lane == 1 ? reinterpret_cast<const uint64_t*>(d.cap_mem)
+                                  : lane == 2 ? reinterpret_cast<const uint64_t*>(d.used_cpu)
+                                  : lane == 3 ? reinterpret_cast<const uint64_t*>(d.used_mem)
+                                  : lane == 4 ? reinterpret_cast<const uint64_t*>(d.inv10_cpu)
+                                              : reinterpret_cast<const uint64_t*>(d.inv10_mem);
+            v = src[wn];
+          }
+          uint64_t* dst = lane < 2   ? reinterpret_cast<uint64_t*>(&S.cap[slot]) + lane
+                          : lane < 4 ? reinterpret_cast<uint64_t*>(&S.snp[slot]) + (lane - 2)
+                                     : reinterpret_cast<uint64_t*>(&S.inv[slot]) + (lane & 1);
+          *dst = v;
+        }
+        // the pod's keys and service entries, appended to the slot's lists
+        const uint32_t my_key = (uint32_t)__shfl((int)rec, (int)(WS_IDS + (lane < nk ? lane : 0u)), 64);
+        if (lane < nk) S.keys[(size_t)slot * KSG_SLOT_KEYS + base_nk + lane] = my_key;
+        const bool sv_lane = lane < n_svcs;
+        const uint32_t my_sv = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + (sv_lane ? lane : 0u), 63u), 64);
+        uint32_t new_mask = 0;
+        if (n_svcs) {
+          int32_t cnt = 0, mx = 0, peer = 0;
+          uint32_t before = 0;
+          bool changed = false;
+          if (sv_lane) {
+            cnt = is_pred ? r_svc[e].cnt[lane] : d.svc_cnt[(size_t)my_sv * d.n_nodes + wn];
+            mx = r_svc[e].max[lane];
+            peer = r_svc[e].peer[lane];
+            // in-window commits of this service on this node before this one
+            const uint32_t* sl = S.svcs + (size_t)slot * KSG_SLOT_SVCS;
+            for (uint32_t b = 0; b < base_ns; ++b) before += sl[b] == my_sv;
+            changed = aff_on && peer == -1 && !((L_peerset[my_sv >> 5] >> (my_sv & 31)) & 1u);
+          }
+          // first commit of a service with no peer yet: record the peer (in order)
+          uint64_t pm = __ballot(sv_lane && peer == -1);
+          while (pm) {
+            const uint32_t b = __builtin_ctzll(pm);
+            pm &= pm - 1;
+            const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)b);
+            const bool fresh = !((L_peerset[fsv >> 5] >> (fsv & 31)) & 1u);
+            if (fresh) {
+              if (lane == 0) {
+                L_peerset[fsv >> 5] |= 1u << (fsv & 31);
+                L_peer[2 * n_peer] = fsv;
+                L_peer[2 * n_peer + 1] = wn;
+              }
+              ++n_peer;
+              lds_fence();
             }
           }
-          cnt = __popcll(__ballot(drop));
+          new_mask = wave_or_u32(sv_lane ? (1u << (my_sv & 31)) : 0u);
+          if (sv_lane) {
+            if (spread_on && cnt + (int32_t)before + 1 > mx) changed = true;  // maxCount rises
+            S.svcs[(size_t)slot * KSG_SLOT_SVCS + base_ns + lane] = my_sv;
+            S.scnt[(size_t)slot * KSG_SLOT_SVCS + base_ns + lane] = cnt;
+            if (changed) atomicOr(&L_flag[my_sv >> 5], 1u << (my_sv & 31));
+          }
         }
+        lds_fence();
         if (lane == 0) {
-          ctl->chk_cnt[c][par] = cnt;
-          st_rel(&ctl->chk_seq[c], i + 1);
+          const I64x2 ov = in_c ? S.dl[slot] : I64x2{0, 0};
+          S.dl[slot] = I64x2{(int64_t)((uint64_t)ov.c + (uint64_t)pv.req_c), (int64_t)((uint64_t)ov.m + (uint64_t)pv.req_m)};
+          S.meta[slot] = SlotMeta{woff, base_nk + nk, base_ns + n_svcs, om | new_mask};
         }
       }
-      return;
+      if (lane == 0) {
+        L_out[i] = outv;
+        ctl->n_peer = n_peer;
+        st_rel(&ctl->scribe_done, i + 1);
+        st_rel(&ctl->consumed, i + 1);  // the pod's ring entry is free
+      }
     }
+    return;
   }
 
   // =========================================================================
   // committer (wave 0)
   // =========================================================================
   __builtin_amdgcn_s_setprio(3);
-  uint32_t* const L_peer = reinterpret_cast<uint32_t*>(smem + o.peer);
-  int32_t* const L_out = reinterpret_cast<int32_t*>(smem + o.out);
-  uint32_t* const L_flag = reinterpret_cast<uint32_t*>(smem + o.flag);
-  uint32_t* const L_peerset = reinterpret_cast<uint32_t*>(smem + o.peerset);
-  uint32_t resolved = n_pods, reason = 0, n_slots = 0, n_peer = 0, n_draws = 0;
-  uint32_t last_slot = KSG_NO_SLOT;  // slot the previous pod committed into
-  uint32_t last_node = 0;            // and its node
-  uint32_t cn0 = ~0u, cn1 = ~0u;     // nodes of slots lane and 64 + lane (the committer's copy)
+  uint32_t resolved = n_pods, reason = 0, n_slots = 0, n_draws = 0;
+  uint32_t cn0 = ~0u, cn1 = ~0u;  // nodes of slots lane and 64 + lane (the committer's copy)
+  // The slot the previous pod committed into, as it is after that commit, in
+  // registers: the next pod re-checks it here (the checkers skip it) without
+  // waiting for the scribe. Lists: lane t holds key t, service entry t.
+  bool ls_valid = false;
+  uint32_t ls_slot = KSG_NO_SLOT, ls_node = 0, ls_nk = 0, ls_ns = 0, ls_mask = 0;
+  int64_t ls_cap_c = 0, ls_cap_m = 0, ls_snp_c = 0, ls_snp_m = 0, ls_dl_c = 0, ls_dl_m = 0;
+  double ls_inv_c = 0.0, ls_inv_m = 0.0;
+  uint32_t ls_key = 0, ls_sv = 0;
+  int32_t ls_scnt = 0;
+  uint32_t prev_nsv = 0, prev_sv = 0;  // the previous pod's services (lane t < prev_nsv)
+  uint32_t ls_cnt_stale = 0;          // n > 0: ls_scnt misses the counts order n-1 loads
+
+  auto wait_scribe = [&](uint32_t n) -> bool {  // the scribe has written orders [0, n)
+    for (uint32_t spin = 0; ld_acq(&ctl->scribe_done) < n; ++spin)
+      if (spin > 16 * KSG_SPIN_LIMIT) return false;
+    return true;
+  };
+  auto issue = [&](uint32_t i) {  // publish order i (written by the lanes before)
+    lds_fence();
+    if (lane == 0) st_rel(&ctl->order_seq, i + 1);
+  };
 
   // KSG_DEBUG & 8: per-section s_memtime; lane k accumulates section k in a
   // VGPR (no scalar registers taken from the chain)
@@ -750,17 +908,9 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
   }
   if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
 
-  auto publish = [&](uint32_t i, uint32_t xs, uint32_t ns) {
-    if (lane == 0) {
-      ctl->xs_slot = xs;
-      ctl->xs_nslots = ns;
-      st_rel(&ctl->sel_seq, i + 1);
-    }
-  };
-
+  bool hung = false;
   for (uint32_t i = 0; i < n_pods; ++i) {
     const uint32_t e = i % KSG_RING, par = i & 1;
-    bool hung = false;
     for (uint32_t spin = 0; ld_acq(&r_hdr[e].ready) != i + 1; ++spin) {
       if (spin > 16 * KSG_SPIN_LIMIT) {
         hung = true;
@@ -778,18 +928,40 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
     const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
     const uint32_t k0 = __builtin_amdgcn_readfirstlane(r_hdr[e].k0);
     const int32_t s = (int32_t)__builtin_amdgcn_readlane(rec, WS_SVC);
-    if (s >= 0 && (spread_on || aff_on) && ((L_flag[s >> 5] >> (s & 31)) & 1u)) {
-      resolved = i;  // a service scalar this pod reads changed in the window
-      reason = KSG_STOP_SERVICE;
+    if (s >= 0 && (spread_on || aff_on)) {
+      // the flags of every earlier commit that may concern this pod's service
+      const bool prev_has = __ballot(lane < prev_nsv && prev_sv == (uint32_t)s) != 0;
+      if (!wait_scribe(prev_has ? i : (i ? i - 1 : 0))) {
+        resolved = i;
+        reason = KSG_STOP_HANG;
+        break;
+      }
+      if ((L_flag[s >> 5] >> (s & 31)) & 1u) {
+        resolved = i;  // a service scalar this pod reads changed in the window
+        reason = KSG_STOP_SERVICE;
+        break;
+      }
+    }
+    // (the order buffer of parity i was last used by order i-2)
+    if (!wait_scribe(i >= 1 ? i - 1 : 0)) {
+      resolved = i;
+      reason = KSG_STOP_HANG;
       break;
     }
+    WinOrder& od = L_ord[par];
     if (__builtin_amdgcn_readlane(rec, WS_ERR) || m0 == KSG_S32_NONE) {
       // ServiceAffinity peer error / nothing fit at the snapshot (commits only
       // remove fits): no draw, no commit. The checkers skip this pod too.
-      if (lane == 0) L_out[i] = __builtin_amdgcn_readlane(rec, WS_ERR) ? KSG_OUT_ERROR : KSG_OUT_NOFIT;
-      publish(i, KSG_NO_SLOT, n_slots);
-      last_slot = KSG_NO_SLOT;
-      if (lane == 0) st_rel(&ctl->consumed, i + 1);
+      if (lane == 0) {
+        od.kind = 0;
+        od.out = __builtin_amdgcn_readlane(rec, WS_ERR) ? KSG_OUT_ERROR : KSG_OUT_NOFIT;
+        ctl->xs_slot = KSG_NO_SLOT;
+        ctl->xs_nslots = n_slots;
+        st_rel(&ctl->sel_seq, i + 1);
+      }
+      issue(i);
+      prev_nsv = 0;
+      ls_valid = false;  // (the next pod re-checks nothing; the checkers cover every slot)
       continue;
     }
     const PodView pv = pod_view(rec);
@@ -803,19 +975,56 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
       break;
     }
     KSG_STAMP(1)
-
     // ---- the slot the previous pod just committed into: re-check it here
     const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
     bool a_drop = false;
-    uint32_t a_node = 0;
-    if (last_slot != KSG_NO_SLOT) {
-      a_node = last_node;
-      if ((t0e[a_node >> 6] >> (a_node & 63)) & 1ULL)
-        a_drop = __builtin_amdgcn_readfirstlane(
-                     (int)slot_drops(d, S, last_slot, pv, rec, res_on, ports_on, disk_on, spread_on)) != 0;
+    if (ls_valid && ((t0e[ls_node >> 6] >> (ls_node & 63)) & 1ULL)) {
+      const int64_t now_c = (int64_t)((uint64_t)ls_snp_c + (uint64_t)ls_dl_c);
+      const int64_t now_m = (int64_t)((uint64_t)ls_snp_m + (uint64_t)ls_dl_m);
+      if (res_on && !pv.zero_req) {  // PodFitsResources
+        const bool fc = ls_cap_c == 0 || ls_cap_c - now_c >= pv.req_c;
+        const bool fm = ls_cap_m == 0 || ls_cap_m - now_m >= pv.req_m;
+        a_drop = !(fc && fm);
+      }
+      if (nk && !a_drop && ls_nk) {  // PodFitsPorts / NoDiskConflict
+        bool hit = false;
+        if (lane < ls_nk) {
+          if (ports_on)
+            for (uint32_t b = 0; b < pv.n_ports; ++b) hit |= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + b) == ls_key;
+          if (disk_on)
+            for (uint32_t b = 0; b < pv.n_pds; ++b)
+              hit |= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + pv.n_ports + b) == ls_key;
+        }
+        a_drop = __ballot(hit) != 0;
+      }
+      if (!a_drop && d.w_lr) {  // LeastRequested
+        const int32_t lr_now = lr_win(now_c + pv.req_c, ls_cap_c, ls_inv_c) + lr_win(now_m + pv.req_m, ls_cap_m, ls_inv_m);
+        const int32_t lr_snap =
+            lr_win(ls_snp_c + pv.req_c, ls_cap_c, ls_inv_c) + lr_win(ls_snp_m + pv.req_m, ls_cap_m, ls_inv_m);
+        a_drop = (lr_now >> 1) != (lr_snap >> 1);
+      }
+      if (!a_drop && spread_on && pv.s >= 0 && ((ls_mask >> (pv.s & 31)) & 1u)) {  // ServiceSpreading
+        if (ls_cnt_stale) {  // the scribe loaded the counts of the last commit: take them from LDS
+          if (!wait_scribe(ls_cnt_stale)) {
+            resolved = i;
+            reason = KSG_STOP_HANG;
+            break;
+          }
+          ls_scnt = lane < ls_ns ? S.scnt[(size_t)ls_slot * KSG_SLOT_SVCS + lane] : 0;
+          ls_cnt_stale = 0;
+        }
+        const uint64_t mm = __ballot(lane < ls_ns && ls_sv == (uint32_t)pv.s);
+        if (mm) {
+          const int32_t delta = (int32_t)__popcll(mm);
+          const int32_t snapc = __builtin_amdgcn_readlane(ls_scnt, (int)__builtin_ctzll(mm));
+          a_drop = frac10_f32((int64_t)pv.smax - snapc - delta, pv.smax) != frac10_f32((int64_t)pv.smax - snapc, pv.smax);
+        }
+      }
+      a_drop = __builtin_amdgcn_readfirstlane((int)a_drop) != 0;
     }
+    const uint32_t a_node = ls_node;
     KSG_STAMP(2)
-    // ---- the checkers' drops for this pod (every slot but last_slot)
+    // ---- the checkers' drops for this pod (every slot but the last one)
     for (uint32_t spin = 0;; ++spin) {
       bool done = true;
 #pragma unroll
@@ -879,17 +1088,34 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
     const uint32_t wn = d.lo + woff;
     KSG_STAMP(4)
 
-    // ---- AssumePod into the window's slots; HBM is written back at window end
+    // ---- AssumePod: the slot and its state after this commit (registers); the
+    // scribe applies the commit to the LDS slot state from the order
     const bool is_pred = (int32_t)woff == (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].pred);
     const uint64_t hit0 = __ballot(cn0 == woff);
     const uint64_t hit1 = __ballot(cn1 == woff);
-    uint32_t slot, base_nk = 0, base_ns = 0;
     const bool in_c = (hit0 | hit1) != 0;
+    uint32_t slot;
+    bool cnt_wait = false;  // the register copy's counts of this pod's services are still loading
     if (in_c) {
       slot = hit0 ? (uint32_t)__builtin_ctzll(hit0) : 64u + (uint32_t)__builtin_ctzll(hit1);
-      base_nk = __builtin_amdgcn_readfirstlane(S.meta[slot].nk);
-      base_ns = __builtin_amdgcn_readfirstlane(S.meta[slot].ns);
-      if (base_nk + nk > KSG_SLOT_KEYS || base_ns + n_svcs > KSG_SLOT_SVCS) {
+      if (!(ls_valid && slot == ls_slot)) {
+        // an older slot: its LDS state is final once the scribe is past order i-2
+        if (!wait_scribe(i >= 1 ? i - 1 : 0)) {
+          resolved = i;
+          reason = KSG_STOP_HANG;
+          break;
+        }
+        const I64x2 cp = S.cap[slot], sp = S.snp[slot], dl = S.dl[slot];
+        const F64x2 iv = S.inv[slot];
+        const SlotMeta me = S.meta[slot];
+        ls_cap_c = cp.c; ls_cap_m = cp.m; ls_snp_c = sp.c; ls_snp_m = sp.m; ls_dl_c = dl.c; ls_dl_m = dl.m;
+        ls_inv_c = iv.c; ls_inv_m = iv.m;
+        ls_nk = me.nk; ls_ns = me.ns; ls_mask = me.smask;
+        ls_key = lane < ls_nk ? S.keys[(size_t)slot * KSG_SLOT_KEYS + lane] : 0u;
+        ls_sv = lane < ls_ns ? S.svcs[(size_t)slot * KSG_SLOT_SVCS + lane] : 0u;
+        ls_scnt = lane < ls_ns ? S.scnt[(size_t)slot * KSG_SLOT_SVCS + lane] : 0;
+      }
+      if (ls_nk + nk > KSG_SLOT_KEYS || ls_ns + n_svcs > KSG_SLOT_SVCS) {
         resolved = i;  // this pod is redone (with the same draw) in the next window
         reason = KSG_STOP_SLOT;
         break;
@@ -906,107 +1132,76 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
         else cn1 = woff;
       }
     }
-    // the choice is made: the checkers move on to pod i+1 (every slot but this one)
-    publish(i, slot, n_slots);
-    KSG_STAMP(9)
-    const bool fetch = !in_c && !is_pred;  // the node's snapshot must come from HBM
-    if (fetch) KSG_COUNT(8, 64)
-    // Loads first, uses last: lanes 0..5 fetch the node's capacity, requested
-    // totals and 10/capacity (one vector load, per-lane address), service lanes
-    // its service counts, and the LDS work below runs while they are in flight.
-    uint64_t snapv = 0;
-    if (!in_c) {
-      if (is_pred) {
-        if (lane < 6) snapv = reinterpret_cast<const uint64_t*>(&r_hdr[e].cap_c)[lane];
-      } else if (lane < 6) {
-        const uint64_t* src = lane == 0   ? reinterpret_cast<const uint64_t*>(d.cap_cpu)
-                              : lane == 1 ? reinterpret_cast<const uint64_t*>(d.cap_mem)
-                              : lane == 2 ? reinterpret_cast<const uint64_t*>(d.used_cpu)
-                              : lane == 3 ? reinterpret_cast<const uint64_t*>(d.used_mem)
-                              : lane == 4 ? reinterpret_cast<const uint64_t*>(d.inv10_cpu)
-                                          : reinterpret_cast<const uint64_t*>(d.inv10_mem);
-        snapv = src[wn];
-      }
-    }
-    // the pod's services (lane t < n_svcs): snapshot count on the node, maxCount, peer
-    const uint32_t t_sv = lane < n_svcs ? lane : 0u;
-    const uint32_t my_sv = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + t_sv, 63u), 64);
-    const bool sv_lane = lane < n_svcs;
-    int32_t cnt = 0;
-    if (sv_lane) cnt = is_pred ? r_svc[e].cnt[lane] : d.svc_cnt[(size_t)my_sv * d.n_nodes + wn];
-    KSG_STAMP(10)
-    // ports then PDs sit at record dwords WS_IDS + [0, nk)
-    const uint32_t my_key = (uint32_t)__shfl((int)rec, (int)(WS_IDS + (lane < nk ? lane : 0u)), 64);
-    if (lane < nk) S.keys[(size_t)slot * KSG_SLOT_KEYS + base_nk + lane] = my_key;
-    uint32_t new_mask = 0;
-    if (n_svcs) {
-      int32_t mx = 0, peer = 0;
-      uint32_t before = 0;
-      if (sv_lane) {
-        mx = r_svc[e].max[lane];
-        peer = r_svc[e].peer[lane];
-        // in-window commits of this service on this node before this one
-        const uint32_t* sl = S.svcs + (size_t)slot * KSG_SLOT_SVCS;
-        for (uint32_t b = 0; b < base_ns; ++b) before += sl[b] == my_sv;
-        S.svcs[(size_t)slot * KSG_SLOT_SVCS + base_ns + lane] = my_sv;
-      }
-      bool changed = sv_lane && aff_on && peer == -1 && !((L_peerset[my_sv >> 5] >> (my_sv & 31)) & 1u);
-      // first commit of a service with no peer yet: record the peer (lane 0 applies, in order)
-      uint64_t pm = __ballot(sv_lane && peer == -1);
-      while (pm) {
-        const uint32_t b = __builtin_ctzll(pm);
-        pm &= pm - 1;
-        const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)b);
-        const bool fresh = !((L_peerset[fsv >> 5] >> (fsv & 31)) & 1u);
-        if (fresh) {
-          if (lane == 0) {
-            L_peerset[fsv >> 5] |= 1u << (fsv & 31);
-            L_peer[2 * n_peer] = fsv;
-            L_peer[2 * n_peer + 1] = wn;
-          }
-          ++n_peer;
-          lds_fence();
-        }
-      }
-      new_mask = wave_or_u32(sv_lane ? (1u << (my_sv & 31)) : 0u);
-      KSG_STAMP(11)
-      // the service counts are needed from here on
-      if (sv_lane) {
-        if (spread_on && cnt + (int32_t)before + 1 > mx) changed = true;  // maxCount rises
-        S.scnt[(size_t)slot * KSG_SLOT_SVCS + base_ns + lane] = cnt;
-        if (changed) atomicOr(&L_flag[my_sv >> 5], 1u << (my_sv & 31));
-      }
-    }
-    if (!in_c) {
-      // lanes 0..5 -> cap.c, cap.m, snp.c, snp.m, inv.c, inv.m of the slot
-      uint64_t* dst = lane < 2   ? reinterpret_cast<uint64_t*>(&S.cap[slot]) + lane
-                      : lane < 4 ? reinterpret_cast<uint64_t*>(&S.snp[slot]) + (lane - 2)
-                                 : reinterpret_cast<uint64_t*>(&S.inv[slot]) + (lane & 1);
-      if (lane < 6) *dst = snapv;
-      if (lane == 0) S.dl[slot] = I64x2{0, 0};
-    }
-    KSG_STAMP(12)
-    lds_fence();
+    // the choice is made: the checkers move on to pod i+1 (every slot but this
+    // one), the scribe to the order
     if (lane == 0) {
-      const I64x2 ov = S.dl[slot];
-      S.dl[slot] = I64x2{(int64_t)((uint64_t)ov.c + (uint64_t)pv.req_c), (int64_t)((uint64_t)ov.m + (uint64_t)pv.req_m)};
-      const uint32_t om = in_c ? S.meta[slot].smask : 0u;
-      S.meta[slot] = SlotMeta{woff, base_nk + nk, base_ns + n_svcs, om | new_mask};
-      L_out[i] = (int32_t)wn;
+      ctl->xs_slot = slot;
+      ctl->xs_nslots = n_slots;
+      st_rel(&ctl->sel_seq, i + 1);
+      od.kind = 1;
+      od.slot = slot;
+      od.node = woff;
+      od.out = (int32_t)wn;
+      od.e = e;
+      od.in_c = in_c;
+      od.is_pred = is_pred;
     }
+    issue(i);
+    if (!in_c) {
+      // snapshot of the node: staged by the producer when it is the predicted
+      // node, else loaded here (L2-warm); the window's lists start empty
+      if (is_pred) {
+        ls_cap_c = r_hdr[e].cap_c; ls_cap_m = r_hdr[e].cap_m;
+        ls_snp_c = r_hdr[e].used_c; ls_snp_m = r_hdr[e].used_m;
+        ls_inv_c = r_hdr[e].inv_c; ls_inv_m = r_hdr[e].inv_m;
+      } else {
+        KSG_COUNT(8, 64)
+        ls_cap_c = d.cap_cpu[wn]; ls_cap_m = d.cap_mem[wn];
+        ls_snp_c = d.used_cpu[wn]; ls_snp_m = d.used_mem[wn];
+        ls_inv_c = d.inv10_cpu[wn]; ls_inv_m = d.inv10_mem[wn];
+      }
+      ls_dl_c = 0;
+      ls_dl_m = 0;
+      ls_nk = ls_ns = ls_mask = 0;
+      ls_key = ls_sv = 0;
+      ls_scnt = 0;
+    }
+    // this pod's keys and service entries, appended at lanes [ls_nk, +nk), [ls_ns, +n_svcs)
+    const uint32_t base_nk = ls_nk, base_ns = ls_ns;
+    const uint32_t tk = lane - base_nk, ts = lane - base_ns;
+    const bool key_lane = lane >= base_nk && tk < nk, sv_lane = lane >= base_ns && ts < n_svcs;
+    const uint32_t new_key = (uint32_t)__shfl((int)rec, (int)(WS_IDS + (key_lane ? tk : 0u)), 64);
+    const uint32_t new_sv = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + (sv_lane ? ts : 0u), 63u), 64);
+    if (key_lane) ls_key = new_key;
+    if (sv_lane) {
+      ls_sv = new_sv;
+      if (is_pred) ls_scnt = r_svc[e].cnt[ts];
+      else cnt_wait = true;  // (the scribe loads it; read back from LDS if a re-check needs it)
+    }
+    ls_nk = base_nk + nk;
+    ls_ns = base_ns + n_svcs;
+    if (n_svcs) ls_mask |= wave_or_u32(sv_lane ? (1u << (new_sv & 31)) : 0u);
+    ls_dl_c = (int64_t)((uint64_t)ls_dl_c + (uint64_t)pv.req_c);
+    ls_dl_m = (int64_t)((uint64_t)ls_dl_m + (uint64_t)pv.req_m);
+    ls_slot = slot;
+    ls_node = woff;
+    ls_valid = true;
+    ls_cnt_stale = __builtin_amdgcn_readfirstlane((int)cnt_wait) != 0 ? i + 1 : 0u;
+    prev_nsv = n_svcs;
+    prev_sv = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + (lane < n_svcs ? lane : 0u), 63u), 64);
     ++n_draws;
-    last_slot = slot;
-    last_node = woff;
-    lds_fence();
-    if (lane == 0) st_rel(&ctl->consumed, i + 1);
     KSG_STAMP(5)
   }
-  if (resolved < n_pods && lane == 0) st_rel(&ctl->stop, 1u);
+  // every other wave finishes: the scribe drains the orders issued (one per pod < resolved)
+  if (lane == 0) st_rel(&ctl->stop, 1u);
+  const bool drained = wait_scribe(resolved);
+  if (!drained) reason = KSG_STOP_HANG;
   if constexpr (STAMP) {
     if (lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
   }
 #undef KSG_STAMP
 #undef KSG_COUNT
+  const uint32_t n_peer = __builtin_amdgcn_readfirstlane(ctl->n_peer);
 
   // ---- write the window's deltas back to HBM (the next snapshot) -------------
   for (uint32_t t = lane; t < n_slots; t += 64) {
