@@ -630,9 +630,10 @@ int ksg_destroy(ksg_ctx* c) {
     (void)hipMemcpy(h, c->dev.dbgbuf, sizeof h, hipMemcpyDeviceToHost);
     fprintf(stderr, "ksg stamps (x64 cycles, committer wave): ring-wait %d head %d recheck-last-slot %d "
             "wait-checkers %d select %d commit %d | drop-path pods %d unpredicted commits %d\n",
-            h[0], h[1], h[2], h[3], h[4], h[5] + h[9] + h[10] + h[11] + h[12], h[7], h[8]);
-    fprintf(stderr, "ksg commit split: slot+publish %d loads-issue %d svc-lds %d svc-finish+snap %d tail %d\n",
-            h[9], h[10], h[11], h[12], h[5]);
+            h[0], h[1], h[2], h[3], h[4], h[5], h[7], h[8]);
+    fprintf(stderr, "ksg ring-wait split: first 4 pods of each window %d, later pods %d\n", h[10], h[11]);
+    fprintf(stderr, "ksg producers (sum over waves): slot-wait %d loads %d draw-wait %d stage %d\n", h[12], h[13],
+            h[14], h[15]);
   }
   (void)hipSetDevice(c->device);
   if (c->st) (void)hipStreamSynchronize(c->st);

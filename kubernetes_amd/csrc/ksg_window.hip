@@ -267,11 +267,13 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
 // state lives in LDS (structure of arrays by slot, at most KSG_MAX_SLOTS).
 // The node state in HBM stays the pristine snapshot while the window
 // resolves; the window's deltas are written back once, at the end.
-#define KSG_RES_NT 512
+// threads of the resolver workgroup: 8 waves
+// (16 waves for P <= 8 measured no faster than 8: the chain, not the producers, limits)
+__host__ __device__ constexpr uint32_t win_res_nt(uint32_t P) { return P <= 8 ? 512u : 512u; }
 #define KSG_RES_C0 2                                  // first checker wave (0: committer, 1: scribe)
 #define KSG_RES_NCHK 2                                // checker waves
 #define KSG_RES_P0 (KSG_RES_C0 + KSG_RES_NCHK)        // first producer wave
-#define KSG_RES_NPW (KSG_RES_NT / 64 - KSG_RES_P0)    // producer waves
+#define KSG_RES_NPW (KSG_RES_NT / 64 - KSG_RES_P0)    // producer waves (KSG_RES_NT: in the kernel)
 // ring entries: 16, or 4 when the T0 words of an entry are large (P > 8: more than 32k nodes)
 __host__ __device__ constexpr uint32_t win_ring(uint32_t P) { return P <= 8 ? 16u : 4u; }
 #define KSG_SLOT_KEYS 8
@@ -506,7 +508,7 @@ __device__ __forceinline__ PodView pod_view(uint32_t rec) {
 }
 
 template <int P, bool STAMP>
-__global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
+__global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
                                                                     const KsgWinSum* __restrict__ sums,
                                                                     const KsgWinXchg x, uint64_t* rng_io,
                                                                     int32_t* __restrict__ out_batch) {
@@ -522,6 +524,7 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
   const uint32_t nshard = d.hi - d.lo;
   const uint32_t nwords = d.nwords;
   constexpr uint32_t KSG_RING = win_ring(P);
+  constexpr uint32_t KSG_RES_NT = win_res_nt(P);
   const WinLdsOff o = win_lds_offsets(P, nflag, wcap);
   WinCtl* ctl = reinterpret_cast<WinCtl*>(smem + o.ctl);
   RingHdr* r_hdr = reinterpret_cast<RingHdr*>(smem + o.r_hdr);
@@ -563,7 +566,8 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
   if (wave >= KSG_RES_P0) {
     // warm this XCD's L2 with the node state: the producers' loads of each
     // pod's predicted node (and the committer's loads of other nodes) then hit L2
-    {
+    // (KSG_DEBUG & 64: skip, to measure what it buys)
+    if (!(d.dbg & 64)) {
       const uint32_t pw = wave - KSG_RES_P0, nt = KSG_RES_NPW * 64;
       const uint32_t n16 = (nshard + 1) / 2;  // 16-byte chunks of one int64 array
       uint64_t acc = 0;
@@ -594,13 +598,30 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
       wm_at[q] = ok ? base + x.wcap * x.ostride * 8 + i * 4 : ~0u;
     }
     const uint32_t row_b = x.ostride * 8, row_m = x.ostride * 4;
+    // KSG_DEBUG & 8: producer sections (slot wait, loads, draw wait, rest) into dbgbuf[12..15]
+    uint64_t pt_last = 0, pt_acc = 0;
+    auto pstamp = [&](uint32_t k) {
+      if (d.dbg & 8) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        pt_acc += lane == k ? t_now - pt_last : 0ULL;
+        pt_last = t_now;
+      }
+    };
+    auto pflush = [&]() {
+      if ((d.dbg & 8) && lane >= 12 && lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(pt_acc / 64));
+    };
+    if (d.dbg & 8) pt_last = __builtin_amdgcn_s_memtime();
     for (uint32_t j = wave - KSG_RES_P0; j < n_pods; j += KSG_RES_NPW) {
       const uint32_t e = j % KSG_RING;
       for (uint32_t spin = 0;; ++spin) {  // ring entry free: the resolver is done with pod j - KSG_RING
-        if (ld_acq(&ctl->stop) || spin > KSG_SPIN_LIMIT) return;
+        if (ld_acq(&ctl->stop) || spin > KSG_SPIN_LIMIT) {
+          pflush();
+          return;
+        }
         if (ld_acq(&ctl->consumed) + KSG_RING > j) break;
         __builtin_amdgcn_s_sleep(1);
       }
+      pstamp(12);
       const uint32_t rec = lane < KSG_WIN_SUM_DWORDS ? recs[(size_t)j * KSG_WIN_SUM_DWORDS + lane] : 0u;
       uint64_t t0[P];
       int32_t mw[P];
@@ -622,12 +643,17 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
       const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
       const bool drawable = __builtin_amdgcn_readlane(rec, WS_ERR) == 0 && m0 != KSG_S32_NONE;
 
+      pstamp(13);
       // draw index = draws of the window pods before j
       for (uint32_t spin = 0;; ++spin) {
-        if (ld_acq(&ctl->stop) || spin > KSG_SPIN_LIMIT) return;
+        if (ld_acq(&ctl->stop) || spin > KSG_SPIN_LIMIT) {
+          pflush();
+          return;
+        }
         if (ld_acq(&ctl->draw_next) == j) break;
         __builtin_amdgcn_s_sleep(1);
       }
+      pstamp(14);
       const uint32_t idx = __builtin_amdgcn_readfirstlane(ctl->draw_count);
       if (lane == 0) {
         ctl->draw_count = idx + (drawable ? 1u : 0u);
@@ -689,7 +715,9 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
         r_hdr[e].pred = pred;
         st_rel(&r_hdr[e].ready, j + 1);
       }
+      pstamp(15);
     }
+    pflush();
     return;
   }
 
@@ -884,9 +912,16 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
   uint32_t ls_cnt_stale = 0;          // n > 0: ls_scnt misses the counts order n-1 loads
 
   auto wait_scribe = [&](uint32_t n) -> bool {  // the scribe has written orders [0, n)
+    if (ld_acq(&ctl->scribe_done) >= n) return true;
+    __builtin_amdgcn_s_setprio(0);  // (see the ring wait below)
+    bool ok = true;
     for (uint32_t spin = 0; ld_acq(&ctl->scribe_done) < n; ++spin)
-      if (spin > 16 * KSG_SPIN_LIMIT) return false;
-    return true;
+      if (spin > 16 * KSG_SPIN_LIMIT) {
+        ok = false;
+        break;
+      }
+    __builtin_amdgcn_s_setprio(3);
+    return ok;
   };
   auto issue = [&](uint32_t i) {  // publish order i (written by the lanes before)
     lds_fence();
@@ -911,16 +946,26 @@ __global__ __launch_bounds__(KSG_RES_NT) void ksg_win_resolve_kernel(KsgDev d, u
   bool hung = false;
   for (uint32_t i = 0; i < n_pods; ++i) {
     const uint32_t e = i % KSG_RING, par = i & 1;
-    for (uint32_t spin = 0; ld_acq(&r_hdr[e].ready) != i + 1; ++spin) {
-      if (spin > 16 * KSG_SPIN_LIMIT) {
-        hung = true;
-        break;
+    if (ld_acq(&r_hdr[e].ready) != i + 1) {
+      // waiting on a producer, one of which shares this SIMD: drop the issue
+      // priority while spinning so it is not starved
+      __builtin_amdgcn_s_setprio(0);
+      for (uint32_t spin = 0; ld_acq(&r_hdr[e].ready) != i + 1; ++spin) {
+        if (spin > 16 * KSG_SPIN_LIMIT) {
+          hung = true;
+          break;
+        }
       }
+      __builtin_amdgcn_s_setprio(3);
     }
     if (hung) {
       resolved = i;
       reason = KSG_STOP_HANG;
       break;
+    }
+    if constexpr (STAMP) {  // ring wait of the window's first 4 pods (10) vs the rest (11)
+      const uint64_t t_now = __builtin_amdgcn_s_memtime();
+      t_acc += lane == (i < 4 ? 10u : 11u) ? t_now - t_last : 0ULL;
     }
     KSG_STAMP(0)
     // ---- head
@@ -1302,7 +1347,7 @@ static hipError_t win_resolve_launch(const KsgDev& d, uint32_t wcap, size_t lds,
     (void)hipGetLastError();  // do not leave a sticky error behind
     once = true;
   }
-  hipLaunchKernelGGL((ksg_win_resolve_kernel<PP, ST>), dim3(1), dim3(KSG_RES_NT), lds, st, d, wcap, run, sums, x,
+  hipLaunchKernelGGL((ksg_win_resolve_kernel<PP, ST>), dim3(1), dim3(win_res_nt(PP)), lds, st, d, wcap, run, sums, x,
                      rng, out);
   return hipGetLastError();
 }
