@@ -123,8 +123,9 @@ static_assert(sizeof(KsgWinSum) == 192, "KsgWinSum layout");
 
 // Where the resolver finds phase A's per-word results (ksg_window.hip). Phase A
 // on each rank writes one block for its shard: best-score bitmaps
-// uint64[wcap][ostride], then best scores int32[wcap][ostride], row = window
-// pod, column = word of the shard. With world > 1 the blocks are all-gathered
+// uint64[wcap][ostride], then best scores int32[wcap][ostride] (then, with
+// ServiceAntiAffinity, fit bitmaps uint64[wcap][ostride] at fit_off), row =
+// window pod, column = word of the shard. With world > 1 the blocks are all-gathered
 // rank-major (block g at buf + g * blk); global word w lives in the block of
 // the rank whose [wlo, wlo + nw) holds it.
 #define KSG_MAX_WORLD 16
@@ -133,7 +134,9 @@ struct KsgWinXchg {
   uint64_t blk;       // bytes per rank block
   uint32_t ostride;   // words per row (>= every shard's word count)
   uint32_t wcap;      // rows per block (window capacity)
-  uint32_t world, pad;
+  uint32_t world;
+  uint32_t fit_off;   // ServiceAntiAffinity: byte offset in a block of the fit bitmaps
+                      // uint64[wcap][ostride] (nodes the pod fits at the snapshot), else 0
   uint32_t wlo[KSG_MAX_WORLD], nw[KSG_MAX_WORLD];
 };
 

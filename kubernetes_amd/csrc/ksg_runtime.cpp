@@ -36,9 +36,9 @@ hipError_t ksg_launch_scan(int R, bool anti, const KsgDev& d, const ksg_pod* pod
                            const uint32_t* ids, int mode, int phase, uint8_t* fail_out,
                            int64_t* score_out, uint8_t* record, int32_t* dpart,
                            const int32_t* dglobal, hipStream_t st);
-hipError_t ksg_launch_win_eval(const KsgDev& d, const ksg_pod* batch, const uint32_t* ids, const KsgWinRun* run,
-                               uint32_t wcap, KsgWinSum* sums, uint64_t* wbits, int32_t* wmax, uint32_t ostride,
-                               hipStream_t st);
+hipError_t ksg_launch_win_eval(const KsgDev& d, int mode, const ksg_pod* batch, const uint32_t* ids,
+                               const KsgWinRun* run, uint32_t wcap, KsgWinSum* sums, uint64_t* wbits, int32_t* wmax,
+                               uint32_t ostride, int32_t* dcnt, uint64_t* wfit, hipStream_t st);
 hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
                                   const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st);
 uint32_t ksg_win_max_window(const KsgDev& d);
@@ -128,7 +128,8 @@ struct ksg_ctx {
   KsgWinSum* d_winsum = nullptr;
   uint8_t* d_xsend = nullptr;   // phase A block of this shard (KsgWinXchg layout)
   uint8_t* d_xrecv = nullptr;   // all-gathered blocks of every shard (world > 1)
-  size_t win_cap = 0, xsend_cap = 0, xrecv_cap = 0;
+  int32_t* d_dcnt = nullptr;     // [W][D] per-pod anti-affinity domain counts (phase A pre-pass)
+  size_t win_cap = 0, xsend_cap = 0, xrecv_cap = 0, dcnt_cap = 0;
   KsgWinRun* d_run = nullptr;      // progress of the window chain (device)
   KsgWinRun* h_run = nullptr;      // pinned host copy
   uint32_t last_stats[4] = {0, 0, 0, 0};  // windows, stops (service scalar), stops (ties exhausted)
@@ -461,7 +462,7 @@ KsgDev full_geometry(const ksg_ctx* c) {
 }
 
 bool use_window(ksg_ctx* c, const ksg_pod* pods, uint32_t n) {
-  if (c->window == 0 || anti_on(c) || c->nw > 32 * 64 || ksg_win_max_window(full_geometry(c)) < 8) return false;
+  if (c->window == 0 || c->nw > 32 * 64 || ksg_win_max_window(full_geometry(c)) < 8) return false;
   // monotonicity under commits needs non-negative pod-dependent weights
   if (c->cfg.w_least_requested < 0 || c->cfg.w_service_spreading < 0) return false;
   // lr_win (ksg_device.h) is exact for 0 <= capacity, requested totals <= 2^49
@@ -640,7 +641,7 @@ int ksg_destroy(ksg_ctx* c) {
   free_cluster(c);
   void* scratch[] = {c->d_pods, c->d_ids, c->d_fail, c->d_score, c->d_rec_send, c->d_rec_recv, c->d_dpart,
                      c->d_dglobal, c->d_out, c->d_rng, c->d_summary, c->d_patch, c->d_shard_wlo,
-                     c->d_winsum, c->d_xsend, c->d_xrecv, c->d_run};
+                     c->d_winsum, c->d_xsend, c->d_xrecv, c->d_run, c->d_dcnt};
   for (void* p : scratch)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -1030,7 +1031,12 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       x.wlo[g] = a;
       x.nw[g] = b - a;
     }
-    x.blk = ((size_t)W * x.ostride * 12 + 255) & ~(size_t)255;
+    const bool anti = anti_on(c);
+    const size_t fit_off = ((size_t)W * x.ostride * 12 + 7) & ~(size_t)7;
+    x.fit_off = anti ? (uint32_t)fit_off : 0u;
+    x.blk = ((anti ? fit_off + (size_t)W * x.ostride * 8 : (size_t)W * x.ostride * 12) + 255) & ~(size_t)255;
+    const size_t dcnt_n = (size_t)W * std::max<uint32_t>(c->D, 1);
+    if (anti && (rc = grow(c, (void**)&c->d_dcnt, &c->dcnt_cap, dcnt_n, sizeof(int32_t)))) return rc;
     if ((rc = grow(c, (void**)&c->d_winsum, &c->win_cap, W, sizeof(KsgWinSum)))) return rc;
     if ((rc = grow(c, (void**)&c->d_xsend, &c->xsend_cap, x.blk, 1))) return rc;
     if (c->world > 1 && (rc = grow(c, (void**)&c->d_xrecv, &c->xrecv_cap, x.blk * c->world, 1))) return rc;
@@ -1053,8 +1059,16 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       HIPCHK(c, hipEventRecord(c->wev[0], c->st));
       for (uint32_t k = 0; k < K; ++k) {
         // HIP events on this stream around each kernel (per-kernel device time)
-        HIPCHK(c, ksg_launch_win_eval(c->dev, c->d_pods, c->d_ids, c->d_run, W, c->d_winsum, wbits, wmax,
-                                      x.ostride, c->st));
+        if (anti) {
+          // ServiceAntiAffinity: the pods' per-domain counts over their filtered nodes first
+          HIPCHK(c, hipMemsetAsync(c->d_dcnt, 0, dcnt_n * sizeof(int32_t), c->st));
+          HIPCHK(c, ksg_launch_win_eval(c->dev, 1, c->d_pods, c->d_ids, c->d_run, W, c->d_winsum, wbits, wmax,
+                                        x.ostride, c->d_dcnt, nullptr, c->st));
+          if (c->world > 1 && (rc = allreduce_sum_i32(c, c->d_dcnt, c->d_dcnt, (uint32_t)dcnt_n))) return rc;
+        }
+        HIPCHK(c, ksg_launch_win_eval(c->dev, anti ? 2 : 0, c->d_pods, c->d_ids, c->d_run, W, c->d_winsum, wbits,
+                                      wmax, x.ostride, c->d_dcnt,
+                                      anti ? reinterpret_cast<uint64_t*>(c->d_xsend + fit_off) : nullptr, c->st));
         if (c->world > 1 && (rc = allgather(c, c->d_xsend, c->d_xrecv, x.blk))) return rc;
         HIPCHK(c, hipEventRecord(c->wev[2 * k + 1], c->st));
         HIPCHK(c, ksg_launch_win_resolve(full, W, c->d_run, c->d_winsum, x, c->d_rng, c->d_out, c->st));
@@ -1083,7 +1097,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       if (r.halt == KSG_HALT_OVERSIZE) {
         // a pod whose id lists exceed the window record: the exact per-pod path
         if (c->world == 1) {
-          HIPCHK(c, ksg_launch_batch(c->R, false, c->dev, c->d_pods + pos, c->d_ids, 1, c->d_rng,
+          HIPCHK(c, ksg_launch_batch(c->R, anti, c->dev, c->d_pods + pos, c->d_ids, 1, c->d_rng,
                                      c->d_out + pos, c->st));
         } else {
           if ((rc = scan_exchange(c, c->d_pods + pos, c->d_ids, KSG_MODE_BEGIN, nullptr, nullptr))) return rc;

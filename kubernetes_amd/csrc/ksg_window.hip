@@ -66,12 +66,25 @@
 // ---------------------------------------------------------------------------
 // phase A
 // ---------------------------------------------------------------------------
+// MODE 0: filter + score. With ServiceAntiAffinity (calculateAntiAffinityPriority,
+// spreading.go:104-168) a pod's score on a node depends on the pod's service
+// counts summed per label domain over every node that passes its filters, so
+// phase A runs twice: MODE 1 only sums those domain counts (dcnt[pod][domain],
+// all-reduced over the ranks when sharded), MODE 2 scores with the
+// anti-affinity term and also writes each pod's fit bitmap (the resolver needs
+// to know which committed nodes the pod fitted at the snapshot).
+#define KSG_WIN_PLAIN 0
+#define KSG_WIN_COUNT 1
+#define KSG_WIN_ANTI 2
+template <int MODE>
 __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, const ksg_pod* __restrict__ batch,
                                                                  const uint32_t* __restrict__ ids,
                                                                  const KsgWinRun* __restrict__ run, uint32_t wcap,
                                                                  KsgWinSum* __restrict__ sums,
                                                                  uint64_t* __restrict__ wbits,
-                                                                 int32_t* __restrict__ wmax, uint32_t ostride) {
+                                                                 int32_t* __restrict__ wmax, uint32_t ostride,
+                                                                 int32_t* __restrict__ dcnt,
+                                                                 uint64_t* __restrict__ wfit) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (KSG_SC_NT / 64) + (threadIdx.x >> 6));
   const uint32_t p0 = blockIdx.y * KSG_PG;
@@ -139,7 +152,7 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
   }
 
   // ---- per-pod service counts of this lane's node, all issued up front
-  const bool need_cnt = d.w_spread != 0;
+  const bool need_cnt = d.w_spread != 0 || MODE != KSG_WIN_PLAIN;
   int32_t cnt[KSG_PG];
 #pragma unroll
   for (int j = 0; j < KSG_PG; ++j) {
@@ -147,9 +160,19 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
     cnt[j] = (need_cnt && valid && (uint32_t)j < np && s >= 0) ? d.svc_cnt[(size_t)s * d.n_nodes + n] : 0;
   }
 
+  // anti-affinity label domains of this lane's node (dense per priority, -1 unlabelled)
+  int32_t dom[KSG_MAX_ANTI];
+#pragma unroll
+  for (int a = 0; a < KSG_MAX_ANTI; ++a)
+    dom[a] = (MODE != KSG_WIN_PLAIN && valid && (uint32_t)a < d.n_anti && d.w_anti[a] != 0)
+                 ? d.anti_domain[(size_t)a * d.n_nodes + n]
+                 : -1;
+  int32_t tot = 0;  // svc_total of each pod's service (lane j)
+  if (MODE == KSG_WIN_ANTI && lane < np) tot = c.svc_total;
+
   // ---- score every pod of the group on this word
   int32_t my_max = KSG_S32_NONE;
-  uint64_t my_bits = 0;
+  uint64_t my_bits = 0, my_fit = 0;
   const bool res_on = (P & KSG_PRED_PODFITSRESOURCES) != 0;
 #pragma unroll
   for (int j = 0; j < KSG_PG; ++j) {
@@ -163,6 +186,28 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
         const bool fc = capc == 0 || (int64_t)((uint64_t)capc - (uint64_t)usedc) >= rcj;
         const bool fmm = capm == 0 || (int64_t)((uint64_t)capm - (uint64_t)usedm) >= rmj;
         fit = fit && fc && fmm;
+      }
+      if constexpr (MODE == KSG_WIN_COUNT) {
+        // the pod's service pods on filtered labelled nodes, per domain
+        // (calculateAntiAffinityPriority, spreading.go:130-151): summed over the
+        // wave one domain at a time, one atomic per (wave, domain)
+        const int32_t cj = fit ? cnt[j] : 0;
+#pragma unroll
+        for (int a = 0; a < KSG_MAX_ANTI; ++a) {
+          uint64_t pend = __ballot(cj != 0 && dom[a] >= 0);
+          while (pend) {
+            const int32_t dd = __builtin_amdgcn_readlane(dom[a], (int)__builtin_ctzll(pend));
+            const bool mine = ((pend >> lane) & 1ULL) && dom[a] == dd;
+            const uint32_t sum = wave_total_add(mine ? (uint32_t)cj : 0u);
+            if (lane == 0) atomicAdd(dcnt + (size_t)(p0 + j) * d.n_domains_total + d.anti_dom_off[a] + dd, (int32_t)sum);
+            pend &= ~__ballot(mine);
+          }
+        }
+        continue;
+      }
+      if constexpr (MODE == KSG_WIN_ANTI) {
+        const uint64_t fb = __ballot(fit);
+        if (lane == (uint32_t)j) my_fit = fb;
       }
       int32_t sc = KSG_S32_NONE;
       if (fit) {
@@ -180,6 +225,17 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
             const int64_t ss = mx > 0 ? frac10_f32((int64_t)mx - cnt[j], mx) : 10;
             s += (int64_t)d.w_spread * ss;
           }
+          if constexpr (MODE == KSG_WIN_ANTI) {  // CalculateAntiAffinityPriority (spreading.go:152-166)
+            const int32_t tj = __builtin_amdgcn_readlane(tot, j);
+#pragma unroll
+            for (int a = 0; a < KSG_MAX_ANTI; ++a) {
+              if (dom[a] >= 0) {  // unlabelled nodes score 0
+                const int32_t pc = dcnt[(size_t)(p0 + j) * d.n_domains_total + d.anti_dom_off[a] + dom[a]];
+                const int64_t sa = tj > 0 ? frac10_f32((int64_t)tj - pc, tj) : 10;
+                s += (int64_t)d.w_anti[a] * sa;
+              }
+            }
+          }
           sc = (int32_t)s;
         }
       }
@@ -192,9 +248,11 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
       }
     }
   }
+  if constexpr (MODE == KSG_WIN_COUNT) return;
   if (lane < np && has_word) {
     wmax[(size_t)(p0 + lane) * ostride + w] = my_max;
     wbits[(size_t)(p0 + lane) * ostride + w] = my_bits;
+    if constexpr (MODE == KSG_WIN_ANTI) wfit[(size_t)(p0 + lane) * ostride + w] = my_fit;
   }
 
   // ---- the resolver's record of each pod (one wave per pod group)
@@ -320,6 +378,7 @@ struct alignas(16) WinCtl {
   uint32_t pad0;
   uint32_t chk_seq[KSG_RES_NCHK];     // pods checker c is done with
   uint32_t chk_cnt[KSG_RES_NCHK][2];  // checker c's drops for the pod of parity p
+  uint32_t chk_stop[KSG_RES_NCHK][2]; // checker c: the pod's anti-affinity domain counts changed
   uint32_t order_seq;                 // orders the committer has issued (one per pod)
   uint32_t scribe_done;               // orders the scribe has written into the slots
   uint32_t n_peer;                    // services given their first peer in the window
@@ -339,7 +398,7 @@ struct alignas(16) WinOrder {
 
 // byte offsets of the resolver's dynamic LDS arrays (host and device agree)
 struct WinLdsOff {
-  uint32_t ctl, r_hdr, r_t0, r_rec, r_mod, r_svc;     // ring
+  uint32_t ctl, r_hdr, r_t0, r_rec, r_mod, r_svc, r_fit;  // ring
   uint32_t s_meta, s_cap, s_snp, s_dl, s_inv;          // slots
   uint32_t keys, svcs, scnt;
   uint32_t peer, out, flag, peerset, drop, ord;
@@ -348,7 +407,7 @@ struct WinLdsOff {
 
 __host__ __device__ constexpr uint32_t win_al16(size_t x) { return (uint32_t)((x + 15) & ~(size_t)15); }
 
-__host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag, uint32_t W) {
+__host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag, uint32_t W, bool anti) {
   WinLdsOff o;
   const uint32_t KSG_RING = win_ring(P);
   uint32_t at = 0;
@@ -358,6 +417,7 @@ __host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag,
   o.r_rec = at;   at += win_al16((size_t)KSG_RING * KSG_WIN_SUM_DWORDS * 4);
   o.r_mod = at;   at += win_al16((size_t)KSG_RING * 64 * 4);
   o.r_svc = at;   at += win_al16((size_t)KSG_RING * sizeof(RingSvc));
+  o.r_fit = at;   at += anti ? win_al16((size_t)KSG_RING * P * 64 * 8) : 0u;  // fit bitmaps (anti-affinity)
   o.s_meta = at;  at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(SlotMeta));
   o.s_cap = at;   at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(I64x2));
   o.s_snp = at;   at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(I64x2));
@@ -491,6 +551,45 @@ __device__ __forceinline__ bool slot_drops(const KsgDev& d, const WinSlots& S, u
   return drop;
 }
 
+// ServiceAntiAffinity: a node the pod fitted at the snapshot that it no longer
+// fits (the window's commits took its resources or a key) leaves the pod's
+// filtered set; if the node is labelled and holds pods of the pod's service,
+// the pod's per-domain counts and so the scores of a whole domain change
+// (spreading.go:130-151): not a monotone change, the window must end there.
+__device__ __forceinline__ bool anti_counts_move(const KsgDev& d, uint32_t node, int32_t s) {
+  bool labelled = false;
+#pragma unroll
+  for (int a = 0; a < KSG_MAX_ANTI; ++a)
+    if ((uint32_t)a < d.n_anti && d.w_anti[a] != 0 && d.anti_domain[(size_t)a * d.n_nodes + d.lo + node] >= 0)
+      labelled = true;
+  return labelled && d.svc_cnt[(size_t)s * d.n_nodes + d.lo + node] > 0;
+}
+
+// The resource and key parts of the filter against slot sl's current state
+// (the static parts cannot change in a window).
+__device__ __forceinline__ bool slot_fits_now(const WinSlots& S, uint32_t sl, const PodView& pv, uint32_t rec,
+                                              bool res_on, bool ports_on, bool disk_on) {
+  const I64x2 cap = S.cap[sl], snp = S.snp[sl], dl = S.dl[sl];
+  const int64_t now_c = (int64_t)((uint64_t)snp.c + (uint64_t)dl.c);
+  const int64_t now_m = (int64_t)((uint64_t)snp.m + (uint64_t)dl.m);
+  bool fit = true;
+  if (res_on && !pv.zero_req)
+    fit = (cap.c == 0 || cap.c - now_c >= pv.req_c) && (cap.m == 0 || cap.m - now_m >= pv.req_m);
+  const uint32_t nk = S.meta[sl].nk;
+  if (fit && pv.nk && nk) {
+    const uint32_t* ks = S.keys + (size_t)sl * KSG_SLOT_KEYS;
+    for (uint32_t a = 0; a < nk; ++a) {
+      const uint32_t key = ks[a];
+      if (ports_on)
+        for (uint32_t b = 0; b < pv.n_ports; ++b) fit &= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + b) != key;
+      if (disk_on)
+        for (uint32_t b = 0; b < pv.n_pds; ++b)
+          fit &= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + pv.n_ports + b) != key;
+    }
+  }
+  return fit;
+}
+
 __device__ __forceinline__ PodView pod_view(uint32_t rec) {
   PodView pv;
   const uint32_t npp = __builtin_amdgcn_readlane(rec, WS_NPP);
@@ -525,13 +624,15 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
   const uint32_t nwords = d.nwords;
   constexpr uint32_t KSG_RING = win_ring(P);
   constexpr uint32_t KSG_RES_NT = win_res_nt(P);
-  const WinLdsOff o = win_lds_offsets(P, nflag, wcap);
+  const bool anti_on = x.fit_off != 0;  // ServiceAntiAffinity (phase A wrote fit bitmaps)
+  const WinLdsOff o = win_lds_offsets(P, nflag, wcap, anti_on);
   WinCtl* ctl = reinterpret_cast<WinCtl*>(smem + o.ctl);
   RingHdr* r_hdr = reinterpret_cast<RingHdr*>(smem + o.r_hdr);
   uint64_t* r_t0 = reinterpret_cast<uint64_t*>(smem + o.r_t0);
   uint32_t* r_rec = reinterpret_cast<uint32_t*>(smem + o.r_rec);
   uint32_t* r_mod = reinterpret_cast<uint32_t*>(smem + o.r_mod);
   RingSvc* r_svc = reinterpret_cast<RingSvc*>(smem + o.r_svc);
+  uint64_t* r_fit = reinterpret_cast<uint64_t*>(smem + o.r_fit);
   const WinSlots S{reinterpret_cast<SlotMeta*>(smem + o.s_meta), reinterpret_cast<I64x2*>(smem + o.s_cap),
                    reinterpret_cast<I64x2*>(smem + o.s_snp),     reinterpret_cast<I64x2*>(smem + o.s_dl),
                    reinterpret_cast<F64x2*>(smem + o.s_inv),     reinterpret_cast<uint32_t*>(smem + o.keys),
@@ -596,6 +697,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
       const uint32_t base = (uint32_t)(g * x.blk);
       wb_at[q] = ok ? base + i * 8 : ~0u;
       wm_at[q] = ok ? base + x.wcap * x.ostride * 8 + i * 4 : ~0u;
+      // (the fit bitmaps sit at wb_at + fit_off)
     }
     const uint32_t row_b = x.ostride * 8, row_m = x.ostride * 4;
     // KSG_DEBUG & 8: producer sections (slot wait, loads, draw wait, rest) into dbgbuf[12..15]
@@ -700,6 +802,12 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
       if (lane < KSG_WIN_SUM_DWORDS) r_rec[e * KSG_WIN_SUM_DWORDS + lane] = rec;
 #pragma unroll
       for (int q = 0; q < P; ++q) r_t0[(size_t)e * P * 64 + lane * P + q] = t0[q];
+      if (anti_on) {
+#pragma unroll
+        for (int q = 0; q < P; ++q)
+          r_fit[(size_t)e * P * 64 + lane * P + q] =
+              wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + x.fit_off + j * row_b) : 0ULL;
+      }
       if (inl && lane < n_svcs) {
         r_svc[e].cnt[lane] = s_cnt;
         r_svc[e].max[lane] = s_max;
@@ -743,11 +851,11 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
       const uint32_t xs = ctl->xs_slot, ns = ctl->xs_nslots;
       const uint32_t rec = lane < KSG_WIN_SUM_DWORDS ? r_rec[e * KSG_WIN_SUM_DWORDS + lane] : 0u;
       const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
-      uint32_t cnt = 0;
+      uint32_t cnt = 0, astop = 0;
       if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE && c * 64 < ns) {
         const PodView pv = pod_view(rec);
         const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
-        bool drop = false;
+        bool drop = false, moved = false;
         if (sl < ns && sl != xs) {
           const uint32_t nd = S.meta[sl].node;
           if ((t0e[nd >> 6] >> (nd & 63)) & 1ULL) {
@@ -756,11 +864,16 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
               atomicOr(reinterpret_cast<unsigned long long*>(L_drop + (size_t)par * P * 64 + (nd >> 6)),
                        1ULL << (nd & 63));
           }
+          if (anti_on && pv.s >= 0 && ((r_fit[(size_t)e * P * 64 + (nd >> 6)] >> (nd & 63)) & 1ULL) &&
+              !slot_fits_now(S, sl, pv, rec, res_on, ports_on, disk_on))
+            moved = anti_counts_move(d, nd, pv.s);
         }
         cnt = __popcll(__ballot(drop));
+        astop = __ballot(moved) != 0;
       }
       if (lane == 0) {
         ctl->chk_cnt[c][par] = cnt;
+        ctl->chk_stop[c][par] = astop;
         st_rel(&ctl->chk_seq[c], i + 1);
       }
     }
@@ -850,6 +963,8 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
             const uint32_t* sl = S.svcs + (size_t)slot * KSG_SLOT_SVCS;
             for (uint32_t b = 0; b < base_ns; ++b) before += sl[b] == my_sv;
             changed = aff_on && peer == -1 && !((L_peerset[my_sv >> 5] >> (my_sv & 31)) & 1u);
+            // ServiceAntiAffinity divides by the service's pod count: any commit changes it
+            changed |= anti_on;
           }
           // first commit of a service with no peer yet: record the peer (in order)
           uint64_t pm = __ballot(sv_lane && peer == -1);
@@ -973,7 +1088,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
     const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
     const uint32_t k0 = __builtin_amdgcn_readfirstlane(r_hdr[e].k0);
     const int32_t s = (int32_t)__builtin_amdgcn_readlane(rec, WS_SVC);
-    if (s >= 0 && (spread_on || aff_on)) {
+    if (s >= 0 && (spread_on || aff_on || anti_on)) {
       // the flags of every earlier commit that may concern this pod's service
       const bool prev_has = __ballot(lane < prev_nsv && prev_sv == (uint32_t)s) != 0;
       if (!wait_scribe(prev_has ? i : (i ? i - 1 : 0))) {
@@ -1085,9 +1200,38 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
       reason = KSG_STOP_HANG;
       break;
     }
-    uint32_t chk_drops = 0;
+    uint32_t chk_drops = 0, chk_stop = 0;
 #pragma unroll
-    for (int c = 0; c < KSG_RES_NCHK; ++c) chk_drops += __builtin_amdgcn_readfirstlane(ctl->chk_cnt[c][par]);
+    for (int c = 0; c < KSG_RES_NCHK; ++c) {
+      chk_drops += __builtin_amdgcn_readfirstlane(ctl->chk_cnt[c][par]);
+      chk_stop |= __builtin_amdgcn_readfirstlane(ctl->chk_stop[c][par]);
+    }
+    if (anti_on && pv.s >= 0 && !chk_stop && ls_valid &&
+        ((r_fit[(size_t)e * P * 64 + (ls_node >> 6)] >> (ls_node & 63)) & 1ULL)) {
+      // the last slot, from the register copy: does the pod still fit it?
+      const int64_t now_c = (int64_t)((uint64_t)ls_snp_c + (uint64_t)ls_dl_c);
+      const int64_t now_m = (int64_t)((uint64_t)ls_snp_m + (uint64_t)ls_dl_m);
+      bool fit = true;
+      if (res_on && !pv.zero_req)
+        fit = (ls_cap_c == 0 || ls_cap_c - now_c >= pv.req_c) && (ls_cap_m == 0 || ls_cap_m - now_m >= pv.req_m);
+      if (fit && nk && ls_nk) {
+        bool hit = false;
+        if (lane < ls_nk) {
+          if (ports_on)
+            for (uint32_t b = 0; b < pv.n_ports; ++b) hit |= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + b) == ls_key;
+          if (disk_on)
+            for (uint32_t b = 0; b < pv.n_pds; ++b)
+              hit |= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + pv.n_ports + b) == ls_key;
+        }
+        fit = __ballot(hit) == 0;
+      }
+      if (!fit && anti_counts_move(d, ls_node, pv.s)) chk_stop = 1;
+    }
+    if (chk_stop) {
+      resolved = i;  // the pod's anti-affinity domain counts changed in the window
+      reason = KSG_STOP_SERVICE;
+      break;
+    }
     KSG_STAMP(3)
     // ---- selection: k live ties, ix-th in descending rank = (k-1-ix)-th ascending
     const uint32_t dropped = chk_drops + (a_drop ? 1u : 0u);
@@ -1312,13 +1456,20 @@ static uint32_t win_P(const KsgDev& d) {
 
 static const size_t kWinLdsBudget = 156 * 1024;
 
-hipError_t ksg_launch_win_eval(const KsgDev& d, const ksg_pod* batch, const uint32_t* ids, const KsgWinRun* run,
-                               uint32_t wcap, KsgWinSum* sums, uint64_t* wbits, int32_t* wmax, uint32_t ostride,
-                               hipStream_t st) {
+hipError_t ksg_launch_win_eval(const KsgDev& d, int mode, const ksg_pod* batch, const uint32_t* ids,
+                               const KsgWinRun* run, uint32_t wcap, KsgWinSum* sums, uint64_t* wbits, int32_t* wmax,
+                               uint32_t ostride, int32_t* dcnt, uint64_t* wfit, hipStream_t st) {
   const uint32_t gx = std::max<uint32_t>(1, (d.nwords + KSG_SC_NT / 64 - 1) / (KSG_SC_NT / 64));
   const dim3 grid(gx, (wcap + KSG_PG - 1) / KSG_PG);
-  hipLaunchKernelGGL(ksg_win_score_kernel, grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, run, wcap, sums, wbits,
-                     wmax, ostride);
+  if (mode == KSG_WIN_COUNT)
+    hipLaunchKernelGGL(ksg_win_score_kernel<KSG_WIN_COUNT>, grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, run, wcap,
+                       sums, wbits, wmax, ostride, dcnt, wfit);
+  else if (mode == KSG_WIN_ANTI)
+    hipLaunchKernelGGL(ksg_win_score_kernel<KSG_WIN_ANTI>, grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, run, wcap,
+                       sums, wbits, wmax, ostride, dcnt, wfit);
+  else
+    hipLaunchKernelGGL(ksg_win_score_kernel<KSG_WIN_PLAIN>, grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, run, wcap,
+                       sums, wbits, wmax, ostride, dcnt, wfit);
   return hipGetLastError();
 }
 
@@ -1330,7 +1481,7 @@ uint32_t ksg_win_max_window(const KsgDev& d) {
   uint32_t lo = 0, hi = 4096;
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1) / 2;
-    if (win_lds_offsets(P, nflag, mid).total <= kWinLdsBudget) lo = mid;
+    if (win_lds_offsets(P, nflag, mid, d.n_anti > 0).total <= kWinLdsBudget) lo = mid;
     else hi = mid - 1;
   }
   return lo;
@@ -1355,7 +1506,7 @@ static hipError_t win_resolve_launch(const KsgDev& d, uint32_t wcap, size_t lds,
 hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
                                   const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
   const uint32_t P = win_P(d);
-  const size_t lds = win_lds_offsets(P, (d.n_services + 31) / 32, wcap).total;
+  const size_t lds = win_lds_offsets(P, (d.n_services + 31) / 32, wcap, x.fit_off != 0).total;
   const bool stamp = (d.dbg & 8) != 0;  // KSG_DEBUG & 8: per-section s_memtime stamps
 #define KSG_RES_CASE(PP)                                                                              \
   if (P == PP)                                                                                        \
