@@ -1,0 +1,93 @@
+"""Randomised GPU parity: many small seeded clusters that stress the window
+resolver's corner cases against the C oracle, bit-exact.
+
+Knobs drawn per case: node count (incl. one or two 64-node words), tight
+capacities (FitErrors, requested > capacity), dense host ports / GCE PDs (key
+conflicts between pods of one window), few services (service flags, maxCount
+changes, ServiceAffinity peers), zero-request pods, and every policy family
+(DefaultProvider, resources only, ServiceAffinity + ServiceAntiAffinity,
+LabelsPresence / LabelPreference / anti-affinity with weights). Each case runs
+at windows 0 (exact kernel), 5, 64 and 128.
+"""
+import numpy as np
+import pytest
+
+from kubernetes_amd import factory, ingest, workload
+from kubernetes_amd.api import Quantity
+from kubernetes_amd.engine import DeviceScheduler
+from oracle.pyoracle import OracleScheduler
+
+pytestmark = pytest.mark.gpu
+
+POLICIES = {
+    "default": workload.config_default,
+    "basic": workload.config1,
+    "config4": workload.config4,
+    "labels": lambda: factory.create_from_config({
+        "predicates": [{"name": "PodFitsResources"}, {"name": "PodFitsPorts"}, {"name": "MatchNodeSelector"},
+                       {"name": "HasZone", "argument": {"labelsPresence": {"labels": ["zone"], "presence": True}}}],
+        "priorities": [{"name": "LeastRequestedPriority", "weight": 2},
+                       {"name": "ServiceSpreadingPriority", "weight": 3},
+                       {"name": "PreferRack", "weight": 1,
+                        "argument": {"labelPreference": {"label": "rack", "presence": True}}},
+                       {"name": "RackSpread", "weight": 2, "argument": {"serviceAntiAffinity": {"label": "rack"}}}],
+    }),
+}
+
+
+def _case(seed):
+    rng = workload._SM(1000 + seed)
+    nn = [40, 64, 65, 130, 700, 2100][rng.below(6)]
+    npods = 150 + rng.below(250)
+    policy = list(POLICIES)[seed % len(POLICIES)]
+    n_apps = [1, 3, 10, 40][rng.below(4)]
+    port_frac = [0.0, 0.1, 0.6][rng.below(3)]
+    pd_frac = [0.0, 0.05, 0.5][rng.below(3)]
+    sel_frac = [0.0, 0.2, 0.7][rng.below(3)]
+    tight = rng.below(3) == 0
+    nodes = workload.make_nodes(nn, rng)
+    if tight:
+        for n in nodes:
+            n.spec.capacity["cpu"] = Quantity.from_milli(1000 + 500 * rng.below(4))
+    pods = workload.make_pods(npods, rng, n_apps=n_apps, port_frac=port_frac, pd_frac=pd_frac, sel_frac=sel_frac)
+    for i, p in enumerate(pods):  # some zero-request pods (fit anywhere, predicates.go:129-132)
+        if rng.below(20) == 0:
+            c = p.spec.containers[0]
+            c.resources.limits["cpu"] = Quantity.from_milli(0)
+            c.resources.limits["memory"] = Quantity.from_int(0)
+    for p in pods:  # dense keys: a small pool so pods of one window collide
+        for c in p.spec.containers:
+            for cp in c.ports:
+                cp.host_port = 9000 + (cp.host_port % 3)
+        for v in p.spec.volumes:
+            if v.gce_persistent_disk is not None:
+                v.gce_persistent_disk.pd_name = f"pd-{int(v.gce_persistent_disk.pd_name.split('-')[1]) % 5}"
+    cfg = POLICIES[policy]()
+    cfg.max_conflict_keys = 64
+    w = workload.Workload(f"fuzz{seed}", nodes, pods, workload.make_services(n_apps), cfg, [])
+    it = ingest.Interner()
+    for k in w.config.label_keys():
+        it.key_id(k)
+    view = ingest.ClusterView(w.nodes, w.services, it)
+    batch = ingest.ingest_pods(view, w.pods, aff_labels=w.config.affinity_labels())
+    return w.config.compile(it.key_id), view.arrays, batch, (nn, npods, policy, n_apps, port_frac, pd_frac, tight)
+
+
+@pytest.mark.parametrize("seed", range(64))
+def test_fuzz_windows_match_oracle(seed):
+    cfg, arrays, batch, desc = _case(seed)
+    orc = OracleScheduler(cfg)
+    orc.set_cluster(arrays)
+    want, sw = orc.batch(batch, 4242 + seed)
+    wc, wm = orc.read_requested()
+    for window in (0, 5, 64, 128):
+        dev = DeviceScheduler(cfg, device=0)
+        dev.set_window(window)
+        dev.set_cluster(arrays)
+        got, sg = dev.batch(batch, 4242 + seed)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, f"{desc} window {window}: first mismatches at {bad[:6]}: {got[bad[:6]]} vs {want[bad[:6]]}"
+        assert sg == sw, (desc, window)
+        gc, gm = dev.read_requested()
+        assert np.array_equal(gc, wc) and np.array_equal(gm, wm), (desc, window)
+        dev.close()
