@@ -44,7 +44,7 @@ __device__ __forceinline__ int32_t scan_pod(const KsgDev& d, const PodCtx& c, ui
   const bool need_cnt = (d.w_spread != 0 || ANTI) && c.svc >= 0;
   int32_t m = KSG_S32_NONE;
   // register-cached node state needs compile-time j; otherwise keep the loop rolled
-#pragma unroll(REG ? R : 1)
+#pragma unroll REG ? R : 1
   for (int j = 0; j < R; ++j) {
     const uint32_t n = d.lo + j * KSG_NT + tid;
     const uint32_t wi = (d.lo >> 6) + j * KSG_NWAVE + wave;
