@@ -606,7 +606,9 @@ __device__ __forceinline__ PodView pod_view(uint32_t rec) {
   return pv;
 }
 
-template <int P, bool STAMP>
+// ANTI: ServiceAntiAffinity is on (its checks are compiled only into these
+// instantiations: they cost the others scalar registers on the chain)
+template <int P, bool STAMP, bool ANTI>
 __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
                                                                     const KsgWinSum* __restrict__ sums,
                                                                     const KsgWinXchg x, uint64_t* rng_io,
@@ -624,7 +626,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
   const uint32_t nwords = d.nwords;
   constexpr uint32_t KSG_RING = win_ring(P);
   constexpr uint32_t KSG_RES_NT = win_res_nt(P);
-  const bool anti_on = x.fit_off != 0;  // ServiceAntiAffinity (phase A wrote fit bitmaps)
+  constexpr bool anti_on = ANTI;  // (the host passes fit bitmaps, x.fit_off != 0, exactly then)
   const WinLdsOff o = win_lds_offsets(P, nflag, wcap, anti_on);
   WinCtl* ctl = reinterpret_cast<WinCtl*>(smem + o.ctl);
   RingHdr* r_hdr = reinterpret_cast<RingHdr*>(smem + o.r_hdr);
@@ -703,16 +705,17 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
     // KSG_DEBUG & 8: producer sections (slot wait, loads, draw wait, rest) into dbgbuf[12..15]
     uint64_t pt_last = 0, pt_acc = 0;
     auto pstamp = [&](uint32_t k) {
-      if (d.dbg & 8) {
+      if constexpr (STAMP) {
         const uint64_t t_now = __builtin_amdgcn_s_memtime();
         pt_acc += lane == k ? t_now - pt_last : 0ULL;
         pt_last = t_now;
       }
     };
     auto pflush = [&]() {
-      if ((d.dbg & 8) && lane >= 12 && lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(pt_acc / 64));
+      if constexpr (STAMP)
+        if (lane >= 12 && lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(pt_acc / 64));
     };
-    if (d.dbg & 8) pt_last = __builtin_amdgcn_s_memtime();
+    if constexpr (STAMP) pt_last = __builtin_amdgcn_s_memtime();
     for (uint32_t j = wave - KSG_RES_P0; j < n_pods; j += KSG_RES_NPW) {
       const uint32_t e = j % KSG_RING;
       for (uint32_t spin = 0;; ++spin) {  // ring entry free: the resolver is done with pod j - KSG_RING
@@ -1477,6 +1480,7 @@ hipError_t ksg_launch_win_eval(const KsgDev& d, int mode, const ksg_pod* batch, 
 uint32_t ksg_win_max_window(const KsgDev& d) {
   const uint32_t P = win_P(d);
   if (P == 0) return 0;
+  if (d.n_anti > 0 && d.n_domains_total > 0 && P > 8) return 0;  // anti-affinity: up to 32k nodes
   const uint32_t nflag = (d.n_services + 31) / 32;
   uint32_t lo = 0, hi = 4096;
   while (lo < hi) {
@@ -1487,18 +1491,18 @@ uint32_t ksg_win_max_window(const KsgDev& d) {
   return lo;
 }
 
-template <int PP, bool ST>
+template <int PP, bool ST, bool AN>
 static hipError_t win_resolve_launch(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run,
                                      const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
                                      hipStream_t st) {
   static bool once = false;
   if (!once) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_resolve_kernel<PP, ST>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_resolve_kernel<PP, ST, AN>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipGetLastError();  // do not leave a sticky error behind
     once = true;
   }
-  hipLaunchKernelGGL((ksg_win_resolve_kernel<PP, ST>), dim3(1), dim3(win_res_nt(PP)), lds, st, d, wcap, run, sums, x,
+  hipLaunchKernelGGL((ksg_win_resolve_kernel<PP, ST, AN>), dim3(1), dim3(win_res_nt(PP)), lds, st, d, wcap, run, sums, x,
                      rng, out);
   return hipGetLastError();
 }
@@ -1508,16 +1512,21 @@ hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run
   const uint32_t P = win_P(d);
   const size_t lds = win_lds_offsets(P, (d.n_services + 31) / 32, wcap, x.fit_off != 0).total;
   const bool stamp = (d.dbg & 8) != 0;  // KSG_DEBUG & 8: per-section s_memtime stamps
-#define KSG_RES_CASE(PP)                                                                              \
-  if (P == PP)                                                                                        \
-    return stamp ? win_resolve_launch<PP, true>(d, wcap, lds, run, sums, x, rng, out, st)             \
-                 : win_resolve_launch<PP, false>(d, wcap, lds, run, sums, x, rng, out, st);
-  KSG_RES_CASE(1)
-  KSG_RES_CASE(2)
-  KSG_RES_CASE(4)
-  KSG_RES_CASE(8)
-  KSG_RES_CASE(16)
-  KSG_RES_CASE(32)
+  const bool anti = x.fit_off != 0;
+#define KSG_RES_CASE(PP, AN)                                                                          \
+  if (P == PP && anti == AN)                                                                          \
+    return stamp ? win_resolve_launch<PP, true, AN>(d, wcap, lds, run, sums, x, rng, out, st)         \
+                 : win_resolve_launch<PP, false, AN>(d, wcap, lds, run, sums, x, rng, out, st);
+  KSG_RES_CASE(1, false)
+  KSG_RES_CASE(2, false)
+  KSG_RES_CASE(4, false)
+  KSG_RES_CASE(8, false)
+  KSG_RES_CASE(16, false)
+  KSG_RES_CASE(32, false)
+  KSG_RES_CASE(1, true)
+  KSG_RES_CASE(2, true)
+  KSG_RES_CASE(4, true)
+  KSG_RES_CASE(8, true)
 #undef KSG_RES_CASE
   return hipErrorInvalidValue;
 }
