@@ -7,7 +7,7 @@ host-side mirror of the reference's algorithm API:
 
   factory      predicate/priority registry, DefaultProvider, Policy -> ksg_config
   scheduler    GPUScheduler (algorithm.Scheduler drop-in), FitError, listers
-  modeler      SimpleModeler (AssumePod = the commit)
+  modeler      cache.Store, SimpleModeler (AssumePod = the commit), PodMirror (event-driven device state)
   ingest       api objects -> interned SoA arrays
   engine       one libkschedgpu.so context (DeviceScheduler)
   api/resource/labels   the pkg/api, resource.Quantity and labels subset the path reads

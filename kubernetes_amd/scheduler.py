@@ -13,8 +13,11 @@ Reference interface (pkg/scheduler):
   * otherwise exactly one `random.int()` draw and the ix-th host, ix = r % ties,
     in (score desc, name desc) order.
 The pods the scheduler sees are exactly what `pod_lister.list()` returns at each
-call (as MapPodsToMachines re-lists them, predicates.go:354-375): the device
-state is reconciled against the lister by namespace/name before each pod.
+call (as MapPodsToMachines re-lists them, predicates.go:354-375). With a plain
+lister the device state is reconciled against it by namespace/name before each
+pod; with SimpleModeler's lister (kubernetes_amd.modeler) it is kept equal to
+the modeler's stores by their change events (PodMirror), so a Schedule call costs
+O(events + assumed pods) on the host instead of O(all pods).
 """
 from __future__ import annotations
 
@@ -26,6 +29,7 @@ from .engine import DeviceScheduler, PodBatch
 from .factory import SchedulerConfig
 from .ingest import ClusterView, Interner, PodBatchBuilder
 from .labels import everything, selector_from_set
+from .modeler import ModelerPodLister, PodMirror
 
 
 class FitError(Exception):
@@ -125,6 +129,11 @@ class GPUScheduler:
         self._svc_sig = None
         self._mirror: Dict[str, tuple] = {}  # pod key -> (uid, host_id, id(pod))
         self._next_uid = 1
+        # the modeler's PodLister (factory.go: f.PodLister = modeler.PodLister()):
+        # mirror its stores by events instead of re-listing every pod per Schedule
+        self._events: Optional[PodMirror] = None
+        if isinstance(pod_lister, ModelerPodLister):
+            self._events = PodMirror(pod_lister.modeler, self.engine, self._ingest_one, self._uid)
 
     def close(self):
         self.engine.close()
@@ -135,6 +144,11 @@ class GPUScheduler:
         self._next_uid += 1
         return u
 
+    def _ingest_one(self, pod: Pod, uid: int):
+        b = PodBatchBuilder(self.view, self.aff_labels)
+        b.add(pod, uid)
+        return self.view.host_id(pod.status.host), b.build()
+
     def _sync(self, nodes: Sequence[Node]):
         services = self.service_lister.list()
         nsig = tuple(id(n) for n in nodes)
@@ -144,6 +158,12 @@ class GPUScheduler:
             self.engine.set_cluster(self.view.arrays)
             self._node_sig, self._svc_sig = nsig, ssig
             self._mirror = {}
+            if self._events is not None:
+                self._events.reload()
+                return
+        if self._events is not None:
+            self._events.sync()
+            return
         pods = self.pod_lister.list(everything())
         want = {}
         for p in pods:  # unnamed / duplicate keys (fake listers) stay distinct pods
@@ -204,7 +224,10 @@ class GPUScheduler:
         # the device now assumes the pod on `node` (AssumePod); the next _sync keeps it
         # iff the pod lister reports it there too.
         host = self.view.names[node]
-        self._mirror[pod.key()] = (uid, node, None)
+        if self._events is not None:  # adopted when AssumePod reports it, else dropped
+            self._events.committed(pod, uid, node)
+        else:
+            self._mirror[pod.key()] = (uid, node, None)
         return host
 
     # ---- batch path (persistent kernel) -------------------------------------
@@ -225,7 +248,10 @@ class GPUScheduler:
         for i, p in enumerate(pods):
             if out[i] >= 0:
                 hosts.append(self.view.names[out[i]])
-                self._mirror[p.key()] = (uids[i], int(out[i]), None)
+                if self._events is not None:
+                    self._events.committed(p, uids[i], int(out[i]))
+                else:
+                    self._mirror[p.key()] = (uids[i], int(out[i]), None)
             else:
                 hosts.append(None)
         return hosts, rng_state

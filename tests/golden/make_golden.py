@@ -451,6 +451,18 @@ def labels():
     }
 
 
+def modeler():
+    """plugin/pkg/scheduler/modeler_test.go:52-75 (TestModeler): (namespace, name) ids."""
+    return {"source": "plugin/pkg/scheduler/modeler_test.go:52-75", "cases": [
+        {"queued": [], "scheduled": [["default", "foo"], ["custom", "foo"]], "assumed": [["default", "foo"]],
+         "expect": [["default", "foo"], ["custom", "foo"]]},
+        {"queued": [], "scheduled": [["default", "foo"]], "assumed": [["default", "foo"], ["custom", "foo"]],
+         "expect": [["default", "foo"], ["custom", "foo"]]},
+        {"queued": [["custom", "foo"]], "scheduled": [["default", "foo"]],
+         "assumed": [["default", "foo"], ["custom", "foo"]], "expect": [["default", "foo"]]},
+    ]}
+
+
 def main():
     out = {
         "source": "smarterclayton/kubernetes v0.13.0-dev, pkg/scheduler/*_test.go (tables restated as data)",
@@ -476,6 +488,9 @@ def main():
                     node("machine21", labels={"zone": "zone2"}), node("machine22", labels={"zone": "zone2"})])
     with open(os.path.join(HERE, "scheduler_golden.json"), "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
+        f.write("\n")
+    with open(os.path.join(HERE, "modeler_golden.json"), "w") as f:
+        json.dump(modeler(), f, indent=1, sort_keys=True)
         f.write("\n")
     with open(os.path.join(HERE, "quantity_golden.json"), "w") as f:
         json.dump({"source": "pkg/api/resource/quantity_test.go", **quantity()}, f, indent=1, sort_keys=True)
