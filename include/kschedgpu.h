@@ -146,7 +146,8 @@ int ksg_create(const ksg_config* cfg, int device, ksg_ctx** out);
  * every rank resolves the window identically. Per-pod path (begin/commit,
  * ServiceAntiAffinity): the shard records are all-gathered per pod. `nccl_id`
  * is the 128-byte ncclUniqueId from rank 0 (RCCL over xGMI), or NULL to use a
- * host transport installed with ksg_set_allgather. */
+ * host transport installed with ksg_set_allgather. world == 1 with an nccl_id
+ * runs the same exchange path over a 1-rank RCCL communicator. */
 int ksg_create_sharded(const ksg_config* cfg, int device, int rank, int world,
                        const void* nccl_id, ksg_ctx** out);
 /* Host transport for a sharded context created with nccl_id == NULL: the

@@ -73,6 +73,7 @@ struct ksg_ctx {
   int device = 0, rank = 0, world = 1;
   hipStream_t st = nullptr;
   ncclComm_t comm = nullptr;
+  bool xchg = false;  // exchange path: world > 1, or a 1-rank RCCL communicator
   // host-staged exchange (ksg_set_allgather) for sharded contexts without RCCL
   ksg_allgather_fn xfn = nullptr;
   void* xuser = nullptr;
@@ -427,7 +428,7 @@ int allreduce_sum_i32(ksg_ctx* c, const int32_t* dsend, int32_t* drecv, uint32_t
 int scan_exchange(ksg_ctx* c, const ksg_pod* dpod, const uint32_t* dids, int mode, uint8_t* fail_out,
                   int64_t* score_out) {
   const bool anti = anti_on(c);
-  if (anti && c->world > 1) {
+  if (anti && c->xchg) {
     HIPCHK(c, ksg_launch_scan(c->R, true, c->dev, dpod, dids, mode, 1, nullptr, nullptr, c->d_rec_send,
                               c->d_dpart, nullptr, c->st));
     int rc = allreduce_sum_i32(c, c->d_dpart, c->d_dglobal, c->dev.n_domains_total);
@@ -439,7 +440,7 @@ int scan_exchange(ksg_ctx* c, const ksg_pod* dpod, const uint32_t* dids, int mod
                               nullptr, nullptr, c->st));
   }
   if (mode == KSG_MODE_BEGIN) {
-    if (c->world > 1) {
+    if (c->xchg) {
       int rc = allgather(c, c->d_rec_send, c->d_rec_recv, c->rec_bytes);
       if (rc) return rc;
     } else {
@@ -595,7 +596,11 @@ static int create_impl(const ksg_config* cfg, int device, int rank, int world, c
   if ((e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess)
     return bail(fail(c, KSG_ERR_HIP, "stream/event: %s", hipGetErrorString(e)));
-  if (world > 1) {
+  // The exchange path (shard scan, all-gather of per-shard records, replicated
+  // resolve) runs for world > 1, and for a 1-rank RCCL communicator when the caller
+  // passes an nccl_id with world == 1 (RCCL itself exercised on a single GPU).
+  c->xchg = world > 1 || nccl_id != nullptr;
+  if (c->xchg) {
     if (world > KSG_MAX_WORLD) return bail(fail(c, KSG_ERR_ARG, "world %d > %d", world, KSG_MAX_WORLD));
     if (nccl_id) {  // else: the caller installs a host transport with ksg_set_allgather
       ncclUniqueId id;
@@ -1039,8 +1044,8 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     if (anti && (rc = grow(c, (void**)&c->d_dcnt, &c->dcnt_cap, dcnt_n, sizeof(int32_t)))) return rc;
     if ((rc = grow(c, (void**)&c->d_winsum, &c->win_cap, W, sizeof(KsgWinSum)))) return rc;
     if ((rc = grow(c, (void**)&c->d_xsend, &c->xsend_cap, x.blk, 1))) return rc;
-    if (c->world > 1 && (rc = grow(c, (void**)&c->d_xrecv, &c->xrecv_cap, x.blk * c->world, 1))) return rc;
-    x.buf = c->world > 1 ? c->d_xrecv : c->d_xsend;
+    if (c->xchg && (rc = grow(c, (void**)&c->d_xrecv, &c->xrecv_cap, x.blk * c->world, 1))) return rc;
+    x.buf = c->xchg ? c->d_xrecv : c->d_xsend;
     uint64_t* wbits = reinterpret_cast<uint64_t*>(c->d_xsend);
     int32_t* wmax = reinterpret_cast<int32_t*>(c->d_xsend + (size_t)W * x.ostride * 8);
     // Windows are chained on the device: each kernel reads the window's start
@@ -1064,12 +1069,12 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
           HIPCHK(c, hipMemsetAsync(c->d_dcnt, 0, dcnt_n * sizeof(int32_t), c->st));
           HIPCHK(c, ksg_launch_win_eval(c->dev, 1, c->d_pods, c->d_ids, c->d_run, W, c->d_winsum, wbits, wmax,
                                         x.ostride, c->d_dcnt, nullptr, c->st));
-          if (c->world > 1 && (rc = allreduce_sum_i32(c, c->d_dcnt, c->d_dcnt, (uint32_t)dcnt_n))) return rc;
+          if (c->xchg && (rc = allreduce_sum_i32(c, c->d_dcnt, c->d_dcnt, (uint32_t)dcnt_n))) return rc;
         }
         HIPCHK(c, ksg_launch_win_eval(c->dev, anti ? 2 : 0, c->d_pods, c->d_ids, c->d_run, W, c->d_winsum, wbits,
                                       wmax, x.ostride, c->d_dcnt,
                                       anti ? reinterpret_cast<uint64_t*>(c->d_xsend + fit_off) : nullptr, c->st));
-        if (c->world > 1 && (rc = allgather(c, c->d_xsend, c->d_xrecv, x.blk))) return rc;
+        if (c->xchg && (rc = allgather(c, c->d_xsend, c->d_xrecv, x.blk))) return rc;
         HIPCHK(c, hipEventRecord(c->wev[2 * k + 1], c->st));
         HIPCHK(c, ksg_launch_win_resolve(full, W, c->d_run, c->d_winsum, x, c->d_rng, c->d_out, c->st));
         HIPCHK(c, hipEventRecord(c->wev[2 * k + 2], c->st));
@@ -1096,7 +1101,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       pos = r.pos;
       if (r.halt == KSG_HALT_OVERSIZE) {
         // a pod whose id lists exceed the window record: the exact per-pod path
-        if (c->world == 1) {
+        if (!c->xchg) {
           HIPCHK(c, ksg_launch_batch(c->R, anti, c->dev, c->d_pods + pos, c->d_ids, 1, c->d_rng,
                                      c->d_out + pos, c->st));
         } else {
@@ -1110,7 +1115,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       // next round (rare: stops shortened this round's windows): the rest at W/2 pods per window
       K = (uint32_t)(((uint64_t)(n - std::min(pos, n)) * 2 + W - 1) / W) + 1;
     }
-  } else if (c->world == 1) {
+  } else if (!c->xchg) {
     HIPCHK(c, ksg_launch_batch(c->R, anti_on(c), c->dev, c->d_pods, c->d_ids, n, c->d_rng, c->d_out, c->st));
   } else {
     for (uint32_t i = 0; i < n; ++i) {

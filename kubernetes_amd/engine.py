@@ -62,15 +62,17 @@ class DeviceScheduler:
                  nccl_id: bytes | None = None, allgather=None):
         """world > 1: exchange over RCCL (`nccl_id` from rank 0's nccl_unique_id()),
         or over the caller's transport `allgather(send: bytes) -> bytes` (the
-        rank-major concatenation of every rank's `send`; ksg_set_allgather)."""
+        rank-major concatenation of every rank's `send`; ksg_set_allgather).
+        world == 1 with an `nccl_id`: the exchange path over a 1-rank RCCL
+        communicator (RCCL exercised on one GPU)."""
         self._lib = abi.load_library()
         self._ctx = C.c_void_p()
         self._xfn = None
-        if world == 1:
+        if world == 1 and nccl_id is None:
             rc = self._lib.ksg_create(C.byref(cfg), device, C.byref(self._ctx))
         else:
             if (nccl_id is None) == (allgather is None):
-                raise ValueError("world > 1 needs exactly one of nccl_id / allgather")
+                raise ValueError("a sharded context needs exactly one of nccl_id / allgather")
             idbuf = C.create_string_buffer(nccl_id, 128) if nccl_id is not None else None
             rc = self._lib.ksg_create_sharded(C.byref(cfg), device, rank, world, idbuf, C.byref(self._ctx))
         if rc != abi.KSG_OK:

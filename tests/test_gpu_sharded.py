@@ -143,3 +143,62 @@ def test_sharded_fuzz_matches_oracle(fuzz_seed):
         assert bad.size == 0, f"rank {rank}: first mismatches at {bad[:8]}: {got[bad[:8]]} vs {want[bad[:8]]}"
         assert rng == st
         assert np.array_equal(np.asarray(uc), wc) and np.array_equal(np.asarray(um), wm)
+
+
+# ---- RCCL itself on one GPU: the exchange path over a 1-rank communicator ------------
+def _rccl_ctx(cfg):
+    from kubernetes_amd.engine import DeviceScheduler
+
+    return DeviceScheduler(cfg, device=0, rank=0, world=1, nccl_id=DeviceScheduler.nccl_unique_id())
+
+
+@pytest.mark.parametrize("name,nn,npods,window", [
+    ("config2", 1500, 1200, 128),  # window path: ncclAllGather of the per-word block per window
+    ("config2", 700, 300, 0),      # per-pod path: ncclAllGather of the shard record per pod
+    ("config4", 900, 400, 128),    # ServiceAntiAffinity: ncclAllReduce of the domain counts
+])
+def test_rccl_one_rank_batch_matches_oracle(name, nn, npods, window):
+    """ncclCommInitRank / ncclAllGather / ncclAllReduce on the library's stream, through
+    the same sharded code path world > 1 takes (RCCL refuses two ranks on one device)."""
+    from tests.helpers import Case, run_batch
+
+    want, st, wc, wm = _oracle(name, nn, npods)
+    case = Case(name, nn, npods)
+    dev = _rccl_ctx(case.cfg)
+    try:
+        dev.set_window(window)
+        got, rng = run_batch(dev, case, rng=1234)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, f"first mismatches at {bad[:8]}: {got[bad[:8]]} vs {want[bad[:8]]}"
+        assert rng == st
+        uc, um = dev.read_requested()
+        assert np.array_equal(uc, wc) and np.array_equal(um, wm)
+        if window:
+            assert dev.last_batch_stats()["windows"] > 0
+    finally:
+        dev.close()
+
+
+def test_rccl_one_rank_begin_commit_matches_oracle():
+    from kubernetes_amd import abi
+    from oracle.pyoracle import OracleScheduler
+    from tests.helpers import Case
+
+    case = Case("config4", 600, 150)
+    dev, orc = _rccl_ctx(case.cfg), OracleScheduler(case.cfg)
+    try:
+        dev.set_cluster(case.view.arrays)
+        orc.set_cluster(case.view.arrays)
+        rng = np.random.default_rng(3)
+        for i in range(len(case.batch)):
+            rg, mg, kg, failg = dev.begin(case.batch, i, want_fail=True)
+            ro, mo, ko, failo = orc.begin(case.batch, i, want_fail=True)
+            assert (rg, kg) == (ro, ko), i
+            assert np.array_equal(failg, failo)
+            if rg == abi.KSG_OK:
+                assert mg == mo
+                ix = int(rng.integers(0, kg))
+                assert dev.commit(ix) == orc.commit(ix)
+    finally:
+        dev.close()
+        orc.close()
