@@ -26,7 +26,13 @@
  *     ksg_last_error(). There is NO CPU fallback inside this library: every
  *     predicate/priority evaluation runs in HIP kernels on the GPU.
  *   - One scheduling thread per context (the reference calls Schedule from one
- *     goroutine, plugin/pkg/scheduler/scheduler.go:86-88).
+ *     goroutine, plugin/pkg/scheduler/scheduler.go:86-88). Every entry point
+ *     holds the context's mutex, so other threads (the reflectors feeding the
+ *     scheduled-pod store, factory.go:126-145) may call ksg_add_pod /
+ *     ksg_remove_pod at any time: between pods they apply at once (a batch in
+ *     flight finishes first); between ksg_schedule_begin and its commit they
+ *     are validated, queued and applied in arrival order right after the
+ *     commit (or when the begin is abandoned by the next begin).
  */
 #ifndef KSCHEDGPU_H_
 #define KSCHEDGPU_H_

@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
@@ -153,7 +154,25 @@ struct ksg_ctx {
   uint64_t pending_k = 0;
   ksg_pod pend{};
   std::vector<uint32_t> pend_ids;
+
+  // Every entry point holds `mu`, so reflector threads may call ksg_add_pod /
+  // ksg_remove_pod while the scheduling thread schedules. Updates that arrive
+  // between ksg_schedule_begin and its commit are queued (validated first) and
+  // applied, in arrival order, when the pending pod is committed or abandoned:
+  // between pods, never inside one (SURVEY.md 8(b) "Threading").
+  std::recursive_mutex mu;
+  struct Queued {
+    bool add;
+    uint32_t host;
+    ksg_pod pod;
+    std::vector<uint32_t> ids;
+    uint64_t uid;
+  };
+  std::vector<Queued> upd_q;
+  std::unordered_set<uint64_t> q_added, q_removed;
 };
+
+#define KSG_LOCK(c) std::lock_guard<std::recursive_mutex> ksg_lock_((c)->mu)
 
 namespace {
 
@@ -324,6 +343,9 @@ void reset_mirror(ksg_ctx* c) {
   c->seq = 0;
   c->patches.clear();
   c->pending = false;
+  c->upd_q.clear();
+  c->q_added.clear();
+  c->q_removed.clear();
 }
 
 int check_pod(ksg_ctx* c, const ksg_pod* p, const uint32_t* ids, size_t n_ids) {
@@ -641,6 +663,9 @@ int ksg_destroy(ksg_ctx* c) {
     fprintf(stderr, "ksg producers (sum over waves): slot-wait %d loads %d draw-wait %d stage %d\n", h[12], h[13],
             h[14], h[15]);
   }
+  {
+    KSG_LOCK(c);  // waits for a call in flight on another thread
+  }
   (void)hipSetDevice(c->device);
   if (c->st) (void)hipStreamSynchronize(c->st);
   free_cluster(c);
@@ -667,6 +692,7 @@ const char* ksg_last_error(ksg_ctx* c) { return c ? c->err.c_str() : "null conte
 int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const uint32_t* node_pairs,
                     uint32_t n_node_pairs, const uint32_t* pair_keys, uint32_t n_pairs, uint32_t n_services) {
   if (!c) return KSG_ERR_ARG;
+  KSG_LOCK(c);
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->st));
   if (n_nodes && !nodes) return fail(c, KSG_ERR_ARG, "nodes == NULL");
@@ -876,11 +902,9 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   return KSG_OK;
 }
 
-int ksg_add_pod(ksg_ctx* c, uint32_t host_id, const ksg_pod* pod, const uint32_t* ids) {
-  if (!c || !pod) return KSG_ERR_ARG;
+static int add_pod_impl(ksg_ctx* c, uint32_t host_id, const ksg_pod* pod, const uint32_t* ids) {
   if (int rc0 = flush_deferred(c)) return rc0;
   if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
-  if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
   int rc = check_pod(c, pod, ids, pod_ids_extent(pod));
   if (rc) return rc;
   rc = mirror_add(c, host_id, pod, ids, true);
@@ -889,10 +913,8 @@ int ksg_add_pod(ksg_ctx* c, uint32_t host_id, const ksg_pod* pod, const uint32_t
   return KSG_OK;
 }
 
-int ksg_remove_pod(ksg_ctx* c, uint64_t uid) {
-  if (!c) return KSG_ERR_ARG;
+static int remove_pod_impl(ksg_ctx* c, uint64_t uid) {
   if (int rc0 = flush_deferred(c)) return rc0;
-  if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
   auto it = c->pods.find(uid);
   if (it == c->pods.end()) return fail(c, KSG_ERR_ARG, "unknown pod uid %llu", (unsigned long long)uid);
   PodRec r = std::move(it->second);
@@ -939,13 +961,61 @@ int ksg_remove_pod(ksg_ctx* c, uint64_t uid) {
   return KSG_OK;
 }
 
+// apply the updates queued while a schedule_begin was pending (c->mu held)
+static int apply_queued(ksg_ctx* c) {
+  std::vector<ksg_ctx::Queued> q;
+  q.swap(c->upd_q);
+  c->q_added.clear();
+  c->q_removed.clear();
+  for (auto& u : q) {
+    const int rc = u.add ? add_pod_impl(c, u.host, &u.pod, u.ids.data()) : remove_pod_impl(c, u.uid);
+    if (rc) return rc;
+  }
+  return KSG_OK;
+}
+
+int ksg_add_pod(ksg_ctx* c, uint32_t host_id, const ksg_pod* pod, const uint32_t* ids) {
+  if (!c || !pod) return KSG_ERR_ARG;
+  KSG_LOCK(c);
+  HIPCHK(c, hipSetDevice(c->device));  // reflector threads: patches flush on this context's device
+  if (!c->pending) return add_pod_impl(c, host_id, pod, ids);
+  if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
+  const size_t ext = pod_ids_extent(pod);
+  int rc = check_pod(c, pod, ids, ext);
+  if (rc) return rc;
+  const bool live = c->pods.count(pod->uid) && !c->q_removed.count(pod->uid);
+  if (live || c->q_added.count(pod->uid) || pod->uid == c->pend.uid)
+    return fail(c, KSG_ERR_ARG, "duplicate pod uid %llu", (unsigned long long)pod->uid);
+  c->upd_q.push_back({true, host_id, *pod, std::vector<uint32_t>(ids, ids + ext), pod->uid});
+  c->q_added.insert(pod->uid);
+  c->q_removed.erase(pod->uid);
+  return KSG_OK;
+}
+
+int ksg_remove_pod(ksg_ctx* c, uint64_t uid) {
+  if (!c) return KSG_ERR_ARG;
+  KSG_LOCK(c);
+  HIPCHK(c, hipSetDevice(c->device));
+  if (!c->pending) return remove_pod_impl(c, uid);
+  const bool live = (c->pods.count(uid) && !c->q_removed.count(uid)) || c->q_added.count(uid);
+  if (!live) return fail(c, KSG_ERR_ARG, "unknown pod uid %llu", (unsigned long long)uid);
+  c->upd_q.push_back({false, 0, ksg_pod{}, {}, uid});
+  c->q_added.erase(uid);
+  c->q_removed.insert(uid);
+  return KSG_OK;
+}
+
 int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int64_t* max_score,
                        uint32_t* tie_count, uint8_t* fail_codes) {
   if (!c || !pod) return KSG_ERR_ARG;
+  KSG_LOCK(c);
   if (int rc0 = flush_deferred(c)) return rc0;
   if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
   HIPCHK(c, hipSetDevice(c->device));
-  c->pending = false;
+  if (c->pending) {  // the previous begin was abandoned: its queued updates apply now
+    c->pending = false;
+    if (int rq = apply_queued(c)) return rq;
+  }
   if (c->N == 0) return KSG_NONODES;
   const size_t ext = pod_ids_extent(pod);
   int rc = check_pod(c, pod, ids, ext);
@@ -974,6 +1044,7 @@ int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int6
 
 int ksg_schedule_commit(ksg_ctx* c, uint32_t tie_index, int32_t* out_node) {
   if (!c) return KSG_ERR_ARG;
+  KSG_LOCK(c);
   if (!c->pending) return fail(c, KSG_ERR_STATE, "no schedule_begin pending");
   if (tie_index >= c->pending_k) return fail(c, KSG_ERR_ARG, "tie_index %u >= tie_count %llu", tie_index,
                                              (unsigned long long)c->pending_k);
@@ -989,6 +1060,8 @@ int ksg_schedule_commit(ksg_ctx* c, uint32_t tie_index, int32_t* out_node) {
   if (node < 0) return fail(c, KSG_ERR_STATE, "commit selected no node (%d)", node);
   rc = mirror_add(c, (uint32_t)node, &c->pend, c->pend_ids.data(), false);
   if (rc) return rc;
+  c->pend.uid = ~0ULL;
+  if ((rc = apply_queued(c))) return rc;
   if (out_node) *out_node = node;
   return KSG_OK;
 }
@@ -996,6 +1069,7 @@ int ksg_schedule_commit(ksg_ctx* c, uint32_t tie_index, int32_t* out_node) {
 int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32_t* ids, uint32_t n_ids,
                        uint64_t* rng_state, int32_t* out_nodes) {
   if (!c || (n && (!pods || !out_nodes)) || !rng_state) return KSG_ERR_ARG;
+  KSG_LOCK(c);
   if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
   if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
   HIPCHK(c, hipSetDevice(c->device));
@@ -1151,6 +1225,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
 
 int ksg_evaluate(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, uint8_t* fail_out, int64_t* score_out) {
   if (!c || !pod) return KSG_ERR_ARG;
+  KSG_LOCK(c);
   if (int rc0 = flush_deferred(c)) return rc0;
   if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
   if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
@@ -1178,6 +1253,7 @@ int ksg_evaluate(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, uint8_t* f
 
 int ksg_set_allgather(ksg_ctx* c, ksg_allgather_fn fn, void* user) {
   if (!c) return KSG_ERR_ARG;
+  KSG_LOCK(c);
   if (c->comm) return fail(c, KSG_ERR_STATE, "context already exchanges over RCCL");
   c->xfn = fn;
   c->xuser = user;
@@ -1186,30 +1262,35 @@ int ksg_set_allgather(ksg_ctx* c, ksg_allgather_fn fn, void* user) {
 
 int ksg_set_window(ksg_ctx* c, uint32_t window) {
   if (!c) return KSG_ERR_ARG;
+  KSG_LOCK(c);
   c->window = window;
   return KSG_OK;
 }
 
 int ksg_last_batch_stats(ksg_ctx* c, uint32_t* stats4) {
   if (!c || !stats4) return KSG_ERR_ARG;
+  KSG_LOCK(c);
   for (int i = 0; i < 4; ++i) stats4[i] = c->last_stats[i];
   return KSG_OK;
 }
 
 int ksg_last_batch_kernel_ms(ksg_ctx* c, double* out3) {
   if (!c || !out3) return KSG_ERR_ARG;
+  KSG_LOCK(c);
   for (int i = 0; i < 3; ++i) out3[i] = c->last_kms[i];
   return KSG_OK;
 }
 
 int ksg_last_batch_ms(ksg_ctx* c, double* ms) {
   if (!c || !ms) return KSG_ERR_ARG;
+  KSG_LOCK(c);
   *ms = c->last_ms;
   return KSG_OK;
 }
 
 int ksg_shard(ksg_ctx* c, uint32_t* lo, uint32_t* hi) {
   if (!c) return KSG_ERR_ARG;
+  KSG_LOCK(c);
   if (lo) *lo = c->lo;
   if (hi) *hi = c->hi;
   return KSG_OK;
@@ -1217,6 +1298,7 @@ int ksg_shard(ksg_ctx* c, uint32_t* lo, uint32_t* hi) {
 
 int ksg_read_requested(ksg_ctx* c, int64_t* milli_cpu, int64_t* memory) {
   if (!c || !c->have_cluster) return KSG_ERR_ARG;
+  KSG_LOCK(c);
   HIPCHK(c, hipSetDevice(c->device));
   int rc = flush_patches(c);
   if (rc) return rc;

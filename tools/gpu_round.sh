@@ -1,5 +1,6 @@
+# One GPU-box pass: the -m gpu suite, smoke(), the default bench line.
 set -o pipefail
-cd $GRAFT_REPO_ROOT
+cd "$GRAFT_REPO_ROOT"
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
-timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>gpurun_out/bench.err
+timeout -k 10 300 python bench.py > gpurun_out/bench.log 2> gpurun_out/bench.err
