@@ -180,3 +180,26 @@ def test_config5_100k_nodes_matches_oracle(window):
     wc, wm = orc.read_requested()
     assert np.array_equal(gc, wc) and np.array_equal(gm, wm)
     dev.close()
+
+
+def test_config3_full_size_matches_oracle():
+    """BASELINE config 3 at full size on one GPU: 15,000 nodes, 50,000 pods in
+    1,000-pod batches (as bench.py steps), every decision, the RNG position and
+    the committed totals against the oracle; plus the size-independent checksum
+    requested totals == the sum of the placed pods' requests."""
+    case = Case("config3", 15000, 50000)
+    dev, orc = _pair(case)
+    got, sg = run_batch(dev, case, chunk=1000)
+    want, sw = run_batch(orc, case, chunk=1000)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"first mismatches at {bad[:8]}: gpu {got[bad[:8]]} oracle {want[bad[:8]]}"
+    assert sg == sw
+    gc, gm = dev.read_requested()
+    wc, wm = orc.read_requested()
+    assert np.array_equal(gc, wc) and np.array_equal(gm, wm)
+    ok = got >= 0
+    sc = np.zeros_like(gc)
+    np.add.at(sc, got[ok], case.batch.pods["milli_cpu"][ok].astype(np.int64))
+    assert np.array_equal(sc, gc)
+    assert dev.last_batch_stats()["windows"] > 0
+    dev.close()

@@ -114,6 +114,7 @@ def _oracle(name, nn, npods, seed=1234):
     ("config2", 700, 400, 0, 2, None),       # per-pod exchange path
     ("config4", 900, 500, 128, 2, None),     # ServiceAntiAffinity: per-pod path + domain all-reduce
     ("config1", 500, 1000, 128, 2, None),    # BASELINE config 1
+    ("config3", 15000, 50000, 128, 2, 1000), # BASELINE config 3 at full size, 1000-pod batches
 ])
 def test_sharded_batch_matches_oracle(name, nn, npods, window, world, chunk):
     want, st, wc, wm = _oracle(name, nn, npods)
