@@ -443,6 +443,12 @@ __host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag,
 #define KSG_STOP_HANG 9        // a ring/draw wait exceeded KSG_SPIN_LIMIT polls (a bug): the host fails
 #define KSG_SPIN_LIMIT (1u << 22)
 
+// a global-address-space load: global_load (vmcnt only), not flat_load, whose
+// lgkmcnt share would make every later LDS wait also wait for it
+template <typename T>
+__device__ __forceinline__ T gld(const T* p) {
+  return *(const __attribute__((address_space(1))) T*)p;
+}
 __device__ __forceinline__ void lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 __device__ __forceinline__ uint32_t ld_acq(uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -941,7 +947,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
                                   : lane == 3 ? reinterpret_cast<const uint64_t*>(d.used_mem)
                                   : lane == 4 ? reinterpret_cast<const uint64_t*>(d.inv10_cpu)
                                               : reinterpret_cast<const uint64_t*>(d.inv10_mem);
-            v = src[wn];
+            v = gld(src + wn);
           }
           uint64_t* dst = lane < 2   ? reinterpret_cast<uint64_t*>(&S.cap[slot]) + lane
                           : lane < 4 ? reinterpret_cast<uint64_t*>(&S.snp[slot]) + (lane - 2)
@@ -959,7 +965,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
           uint32_t before = 0;
           bool changed = false;
           if (sv_lane) {
-            cnt = is_pred ? r_svc[e].cnt[lane] : d.svc_cnt[(size_t)my_sv * d.n_nodes + wn];
+            cnt = is_pred ? r_svc[e].cnt[lane] : gld(d.svc_cnt + (size_t)my_sv * d.n_nodes + wn);
             mx = r_svc[e].max[lane];
             peer = r_svc[e].peer[lane];
             // in-window commits of this service on this node before this one
@@ -1348,9 +1354,9 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
         ls_inv_c = r_hdr[e].inv_c; ls_inv_m = r_hdr[e].inv_m;
       } else {
         KSG_COUNT(8, 64)
-        ls_cap_c = d.cap_cpu[wn]; ls_cap_m = d.cap_mem[wn];
-        ls_snp_c = d.used_cpu[wn]; ls_snp_m = d.used_mem[wn];
-        ls_inv_c = d.inv10_cpu[wn]; ls_inv_m = d.inv10_mem[wn];
+        ls_cap_c = gld(d.cap_cpu + wn); ls_cap_m = gld(d.cap_mem + wn);
+        ls_snp_c = gld(d.used_cpu + wn); ls_snp_m = gld(d.used_mem + wn);
+        ls_inv_c = gld(d.inv10_cpu + wn); ls_inv_m = gld(d.inv10_mem + wn);
       }
       ls_dl_c = 0;
       ls_dl_m = 0;
