@@ -203,3 +203,40 @@ def test_config3_full_size_matches_oracle():
     assert np.array_equal(sc, gc)
     assert dev.last_batch_stats()["windows"] > 0
     dev.close()
+
+
+def test_config5_full_size_window_equals_exact_path():
+    """BASELINE config 5 at full size: 100k nodes x 100k pods in 1,000-pod batches.
+    The oracle would need ~10^10 node evaluations, so the full run is checked through
+    size-independent properties: the window path and the exact one-pod-at-a-time kernel
+    (two different kernels) agree on every decision and the RNG position; committed
+    totals equal the sum of the placed pods' requests; no node with a capacity ends
+    above it; and the first 2,000 pods match the oracle exactly."""
+    case = Case("config5", 100000, 100000)
+    wind = DeviceScheduler(case.cfg, device=0)
+    got, sg = run_batch(wind, case, chunk=1000)
+    assert wind.last_batch_stats()["windows"] > 0
+    gc, gm = wind.read_requested()
+    wind.close()
+    exact = DeviceScheduler(case.cfg, device=0)
+    exact.set_window(0)
+    ref, sr = run_batch(exact, case, chunk=1000)
+    ec, em = exact.read_requested()
+    exact.close()
+    bad = np.nonzero(got != ref)[0]
+    assert bad.size == 0, f"window vs exact: first mismatches at {bad[:8]}: {got[bad[:8]]} vs {ref[bad[:8]]}"
+    assert sg == sr and np.array_equal(gc, ec) and np.array_equal(gm, em)
+    ok = got >= 0
+    assert ok.sum() > len(got) // 2
+    sc, sm = np.zeros_like(gc), np.zeros_like(gm)
+    np.add.at(sc, got[ok], case.batch.pods["milli_cpu"][ok].astype(np.int64))
+    np.add.at(sm, got[ok], case.batch.pods["memory"][ok].astype(np.int64))
+    assert np.array_equal(sc, gc) and np.array_equal(sm, gm)
+    nodes = case.view.arrays.nodes
+    cap_c, cap_m = nodes["cap_milli_cpu"].astype(np.int64), nodes["cap_memory"].astype(np.int64)
+    assert ((cap_c == 0) | (gc <= cap_c)).all() and ((cap_m == 0) | (gm <= cap_m)).all()
+    orc = OracleScheduler(case.cfg)
+    orc.set_cluster(case.view.arrays)
+    want, _ = orc.batch(PodBatch(case.batch.pods[:2000], case.batch.ids), 1234)
+    orc.close()
+    assert np.array_equal(got[:2000], want)
