@@ -173,7 +173,11 @@ _lib = None
 
 
 def lib_path() -> str:
-    return os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+    """The in-tree library; KSG_LIB may name another in-tree build of it (the
+    host-UBSan variant libkschedgpu_ubsan.so, tests/test_gpu_ubsan_runtime.py)."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    alt = os.environ.get("KSG_LIB")
+    return os.path.join(here, alt) if alt else os.path.join(here, LIB_NAME)
 
 
 def load_library() -> C.CDLL:

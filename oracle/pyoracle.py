@@ -16,7 +16,8 @@ from kubernetes_amd import abi
 from kubernetes_amd.engine import ClusterArrays, PodBatch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "_build", "liboracle.so")
+# KSG_ORACLE_LIB: a sanitizer build of the same restatement (tests/test_sanitizers.py)
+LIB = os.environ.get("KSG_ORACLE_LIB") or os.path.join(HERE, "_build", "liboracle.so")
 _lib = None
 
 
