@@ -37,10 +37,12 @@ class ResourceList(dict):
             self[k] = _q(v)
 
     def cpu(self) -> Quantity:
-        return self.get("cpu", Quantity.zero())
+        q = self.get("cpu")
+        return q if q is not None else Quantity.zero()
 
     def memory(self) -> Quantity:
-        return self.get("memory", Quantity.zero())
+        q = self.get("memory")
+        return q if q is not None else Quantity.zero()
 
 
 @dataclass

@@ -74,7 +74,13 @@ struct ksg_ctx {
   int device = 0, rank = 0, world = 1;
   hipStream_t st = nullptr;
   ncclComm_t comm = nullptr;
-  bool xchg = false;  // exchange path: world > 1, or a 1-rank RCCL communicator
+  bool xchg = false;
+  // pinned staging for the per-call uploads / small read-backs (a pageable
+  // hipMemcpyAsync is a staged, effectively synchronous copy)
+  uint8_t* h_up = nullptr;
+  size_t h_up_cap = 0;
+  uint8_t* h_dn = nullptr;
+  size_t h_dn_cap = 0;  // exchange path: world > 1, or a 1-rank RCCL communicator
   // host-staged exchange (ksg_set_allgather) for sharded contexts without RCCL
   ksg_allgather_fn xfn = nullptr;
   void* xuser = nullptr;
@@ -369,13 +375,21 @@ int check_pod(ksg_ctx* c, const ksg_pod* p, const uint32_t* ids, size_t n_ids) {
 }
 
 // upload one pod + its id list into the single-pod scratch slots
+int grow_host(ksg_ctx* c, uint8_t** p, size_t* cap, size_t need);
+
 int upload_pods(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32_t* ids, size_t n_ids) {
   int rc = grow(c, (void**)&c->d_pods, &c->pods_cap, n, sizeof(ksg_pod));
   if (rc) return rc;
   rc = grow(c, (void**)&c->d_ids, &c->ids_cap, std::max<size_t>(n_ids, 1), sizeof(uint32_t));
   if (rc) return rc;
-  HIPCHK(c, hipMemcpyAsync(c->d_pods, pods, (size_t)n * sizeof(ksg_pod), hipMemcpyHostToDevice, c->st));
-  if (n_ids) HIPCHK(c, hipMemcpyAsync(c->d_ids, ids, n_ids * sizeof(uint32_t), hipMemcpyHostToDevice, c->st));
+  // every caller synchronises the stream before it returns, so the staging
+  // buffer is free again at the next call
+  const size_t pb = (size_t)n * sizeof(ksg_pod), ib = n_ids * sizeof(uint32_t);
+  if ((rc = grow_host(c, &c->h_up, &c->h_up_cap, pb + ib))) return rc;
+  memcpy(c->h_up, pods, pb);
+  if (n_ids) memcpy(c->h_up + pb, ids, ib);
+  HIPCHK(c, hipMemcpyAsync(c->d_pods, c->h_up, pb, hipMemcpyHostToDevice, c->st));
+  if (n_ids) HIPCHK(c, hipMemcpyAsync(c->d_ids, c->h_up + pb, ib, hipMemcpyHostToDevice, c->st));
   return KSG_OK;
 }
 
@@ -387,6 +401,9 @@ size_t pod_ids_extent(const ksg_pod* p) {
   e = std::max<size_t>(e, (size_t)p->svcs_off + p->n_svcs);
   return e;
 }
+
+// the shard records decide reads: all-gathered (exchange path) or this rank's own
+uint8_t* rec_buf(ksg_ctx* c) { return c->xchg ? c->d_rec_recv : c->d_rec_send; }
 
 bool anti_on(const ksg_ctx* c) { return c->cfg.n_anti > 0 && c->dev.n_domains_total > 0; }
 
@@ -465,9 +482,7 @@ int scan_exchange(ksg_ctx* c, const ksg_pod* dpod, const uint32_t* dids, int mod
     if (c->xchg) {
       int rc = allgather(c, c->d_rec_send, c->d_rec_recv, c->rec_bytes);
       if (rc) return rc;
-    } else {
-      HIPCHK(c, hipMemcpyAsync(c->d_rec_recv, c->d_rec_send, c->rec_bytes, hipMemcpyDeviceToDevice, c->st));
-    }
+    }  // (one rank: decide reads the record where the scan wrote it, rec_buf)
   }
   return KSG_OK;
 }
@@ -677,6 +692,8 @@ int ksg_destroy(ksg_ctx* c) {
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->h_xsend) (void)hipHostFree(c->h_xsend);
   if (c->h_run) (void)hipHostFree(c->h_run);
+  if (c->h_up) (void)hipHostFree(c->h_up);
+  if (c->h_dn) (void)hipHostFree(c->h_dn);
   if (c->h_xrecv) (void)hipHostFree(c->h_xrecv);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -1024,13 +1041,16 @@ int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int6
   if ((rc = upload_pods(c, pod, 1, ids, ext))) return rc;
   if ((rc = scan_exchange(c, c->d_pods, c->d_ids, KSG_MODE_BEGIN, fail_codes ? c->d_fail : nullptr, nullptr)))
     return rc;
-  HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods, c->d_ids, c->d_rec_recv, c->rec_bytes, c->world,
+  HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods, c->d_ids, rec_buf(c), c->rec_bytes, c->world,
                               c->d_shard_wlo, 0, 0, c->d_rng, nullptr, 0, c->d_summary, c->st));
   int64_t summ[3];
-  HIPCHK(c, hipMemcpyAsync(summ, c->d_summary, sizeof summ, hipMemcpyDeviceToHost, c->st));
-  if (fail_codes && c->hi > c->lo)
-    HIPCHK(c, hipMemcpyAsync(fail_codes, c->d_fail, c->hi - c->lo, hipMemcpyDeviceToHost, c->st));
+  const size_t nf = fail_codes ? (size_t)(c->hi - c->lo) : 0;
+  if ((rc = grow_host(c, &c->h_dn, &c->h_dn_cap, sizeof summ + nf))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->h_dn, c->d_summary, sizeof summ, hipMemcpyDeviceToHost, c->st));
+  if (nf) HIPCHK(c, hipMemcpyAsync(c->h_dn + sizeof summ, c->d_fail, nf, hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
+  memcpy(summ, c->h_dn, sizeof summ);
+  if (nf) memcpy(fail_codes, c->h_dn + sizeof summ, nf);
   if (summ[2]) return fail(c, KSG_ERR_NOPEER, "service affinity peer is not on a known node");
   if (max_score) *max_score = summ[1] > 0 ? summ[0] : 0;
   if (tie_count) *tie_count = (uint32_t)summ[1];
@@ -1051,11 +1071,13 @@ int ksg_schedule_commit(ksg_ctx* c, uint32_t tie_index, int32_t* out_node) {
   HIPCHK(c, hipSetDevice(c->device));
   int rc = ensure_out(c, 1);
   if (rc) return rc;
-  HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods, c->d_ids, c->d_rec_recv, c->rec_bytes, c->world,
+  HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods, c->d_ids, rec_buf(c), c->rec_bytes, c->world,
                               c->d_shard_wlo, 2, tie_index, c->d_rng, c->d_out, 0, c->d_summary, c->st));
   int32_t node = -1;
-  HIPCHK(c, hipMemcpyAsync(&node, c->d_out, 4, hipMemcpyDeviceToHost, c->st));
+  if ((rc = grow_host(c, &c->h_dn, &c->h_dn_cap, 4))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->h_dn, c->d_out, 4, hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
+  memcpy(&node, c->h_dn, 4);
   c->pending = false;
   if (node < 0) return fail(c, KSG_ERR_STATE, "commit selected no node (%d)", node);
   rc = mirror_add(c, (uint32_t)node, &c->pend, c->pend_ids.data(), false);
@@ -1180,7 +1202,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
                                      c->d_out + pos, c->st));
         } else {
           if ((rc = scan_exchange(c, c->d_pods + pos, c->d_ids, KSG_MODE_BEGIN, nullptr, nullptr))) return rc;
-          HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods + pos, c->d_ids, c->d_rec_recv, c->rec_bytes, c->world,
+          HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods + pos, c->d_ids, rec_buf(c), c->rec_bytes, c->world,
                                       c->d_shard_wlo, 1, 0, c->d_rng, c->d_out, pos, c->d_summary, c->st));
         }
         pos += 1;
@@ -1194,7 +1216,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
   } else {
     for (uint32_t i = 0; i < n; ++i) {
       if ((rc = scan_exchange(c, c->d_pods + i, c->d_ids, KSG_MODE_BEGIN, nullptr, nullptr))) return rc;
-      HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods + i, c->d_ids, c->d_rec_recv, c->rec_bytes, c->world,
+      HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods + i, c->d_ids, rec_buf(c), c->rec_bytes, c->world,
                                   c->d_shard_wlo, 1, 0, c->d_rng, c->d_out, i, c->d_summary, c->st));
     }
   }
@@ -1238,7 +1260,7 @@ int ksg_evaluate(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, uint8_t* f
   if ((rc = upload_pods(c, pod, 1, ids, ext))) return rc;
   // errors surface through the BEGIN record, so run BEGIN first for the flag
   if ((rc = scan_exchange(c, c->d_pods, c->d_ids, KSG_MODE_BEGIN, nullptr, nullptr))) return rc;
-  HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods, c->d_ids, c->d_rec_recv, c->rec_bytes, c->world,
+  HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods, c->d_ids, rec_buf(c), c->rec_bytes, c->world,
                               c->d_shard_wlo, 0, 0, c->d_rng, nullptr, 0, c->d_summary, c->st));
   if ((rc = scan_exchange(c, c->d_pods, c->d_ids, KSG_MODE_EVAL, c->d_fail, c->d_score))) return rc;
   int64_t summ[3];

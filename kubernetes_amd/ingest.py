@@ -68,6 +68,17 @@ class ClusterView:
         self.rank = {name: i for i, name in enumerate(self.names)}
         self.services = list(services)
         self._svc_sel = [(s.metadata.namespace, selector_from_set(s.spec.selector)) for s in self.services]
+        # GetPodServices index: a service can only match a pod that carries its
+        # selector's first requirement; empty selectors (incl. SelectorFromSet's
+        # invalid-label trap) match every pod of the namespace
+        self._svc_first: Dict[tuple, List[int]] = {}
+        self._svc_all: Dict[str, List[int]] = {}
+        for i, (sns, sel) in enumerate(self._svc_sel):
+            if sel.empty():
+                self._svc_all.setdefault(sns, []).append(i)
+            else:
+                k, v = sel.requirements[0]
+                self._svc_first.setdefault((sns, k, v), []).append(i)
         arr = np.zeros(len(self.nodes), dtype=abi.NODE_DTYPE)
         pairs: List[int] = []
         for i, n in enumerate(self.nodes):
@@ -99,9 +110,19 @@ class ClusterView:
         return len(self.names) + ext[host]
 
     def pod_services(self, pod: Pod) -> List[int]:
+        """Indices (service-list order) of the services selecting the pod: same
+        namespace, selector matches its labels (GetPodServices, listers.go:63-91)."""
         ns = pod.metadata.namespace
-        labels = pod.metadata.labels
-        return [i for i, (sns, sel) in enumerate(self._svc_sel) if sns == ns and sel.matches(labels)]
+        labels = pod.metadata.labels or {}
+        cand = list(self._svc_all.get(ns, ()))
+        for k, v in labels.items():
+            c = self._svc_first.get((ns, k, v))
+            if c:
+                cand.extend(c)
+        if not cand:
+            return []
+        sel = self._svc_sel
+        return sorted(i for i in set(cand) if sel[i][1].matches(labels))
 
 
 class PodBatchBuilder:

@@ -183,11 +183,14 @@ class PodMirror:
 
     SCHED, ASSUMED = 0, 1
 
-    def __init__(self, modeler: SimpleModeler, sink, ingest: Callable, new_uid: Callable[[], int]):
+    def __init__(self, modeler: SimpleModeler, sink, ingest: Callable, new_uid: Callable[[], int],
+                 host_of: Optional[Callable] = None):
         self.modeler = modeler
         self.sink = sink
         self.ingest = ingest
         self.new_uid = new_uid
+        # pod -> host id without a full ingest (the adoption check only needs the host)
+        self.host_of = host_of if host_of is not None else (lambda p: ingest(p, 0)[0])
         self._q: deque = deque()
         self._qlock = threading.Lock()
         # (source, key) -> uid on the device
@@ -224,8 +227,7 @@ class PodMirror:
                 src, op, key, pod = self._q.popleft()
             if src == self.ASSUMED and op == ADD and key in self.pending:
                 uid, host_id = self.pending.pop(key)
-                h, _ = self.ingest(pod, 0)
-                if h == host_id:  # AssumePod of the pod we just committed there: adopt it
+                if self.host_of(pod) == host_id:  # AssumePod of the pod we just committed there: adopt it
                     self.on_device[(src, key)] = uid
                     self.stats["adopted"] += 1
                     continue

@@ -40,6 +40,14 @@ def _round_up(x: Fraction, places: int) -> Fraction:
     return Fraction(n if y > 0 else -n, scale)
 
 
+def _ceil_away(n: int, d: int) -> int:
+    """n/d (d > 0) rounded away from zero to an integer: _round_up(Fraction(n, d), 0)'s
+    numerator in integer arithmetic (ingest calls it per container per pod)."""
+    q, r = divmod(abs(n), d)
+    q += r != 0
+    return q if n >= 0 else -q
+
+
 def _go_int64(v: int) -> int:
     """big.Int.Int64(): low 64 bits of |v|, negated for v < 0 (two's complement wrap)."""
     mag = abs(v) & ((1 << 64) - 1)
@@ -102,13 +110,11 @@ class Quantity:
 
     def value(self) -> int:
         """Value(): Round(0, RoundUp) -> Int64 (quantity.go:335-342)."""
-        r = _round_up(self.amount, 0)
-        return _go_int64(r.numerator)
+        return _go_int64(_ceil_away(self.amount.numerator, self.amount.denominator))
 
     def milli_value(self) -> int:
         """MilliValue(): Round(amount*1000, 0, RoundUp) -> Int64 (quantity.go:344-351)."""
-        r = _round_up(self.amount * 1000, 0)
-        return _go_int64(r.numerator)
+        return _go_int64(_ceil_away(self.amount.numerator * 1000, self.amount.denominator))
 
     def __eq__(self, other):
         return isinstance(other, Quantity) and self.amount == other.amount and self.format == other.format

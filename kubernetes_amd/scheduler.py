@@ -133,7 +133,8 @@ class GPUScheduler:
         # mirror its stores by events instead of re-listing every pod per Schedule
         self._events: Optional[PodMirror] = None
         if isinstance(pod_lister, ModelerPodLister):
-            self._events = PodMirror(pod_lister.modeler, self.engine, self._ingest_one, self._uid)
+            self._events = PodMirror(pod_lister.modeler, self.engine, self._ingest_one, self._uid,
+                                     host_of=lambda p: self.view.host_id(p.status.host))
 
     def close(self):
         self.engine.close()
@@ -151,8 +152,10 @@ class GPUScheduler:
 
     def _sync(self, nodes: Sequence[Node]):
         services = self.service_lister.list()
-        nsig = tuple(id(n) for n in nodes)
-        ssig = tuple(id(s) for s in services)
+        # list equality: identity first per element, so an unchanged list is ~10 us at
+        # 5k nodes (an equal-valued replacement object counts as unchanged)
+        nsig = list(nodes)
+        ssig = list(services)
         if nsig != self._node_sig or ssig != self._svc_sig or self.view is None:
             self.view = ClusterView(nodes, services, self.interner)
             self.engine.set_cluster(self.view.arrays)

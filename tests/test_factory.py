@@ -106,3 +106,31 @@ def test_weighted_sum_through_oracle():
     rc, got = run_engine(OracleScheduler, cfg, nodes, [], [], Pod())
     assert rc == abi.KSG_OK
     assert got["a"][1] == 4 * 10 + 10 and got["b"][1] == 10
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_pod_services_index_matches_scan(seed):
+    """ClusterView.pod_services (indexed by each selector's first requirement) equals
+    the plain GetPodServices scan: same namespace, selector matches the pod's labels,
+    service-list order; empty and invalid selectors (SelectorFromSet's trap) match all."""
+    import random
+
+    from kubernetes_amd.api import Service, ServiceSpec
+    from kubernetes_amd.ingest import ClusterView, Interner
+    from kubernetes_amd.labels import selector_from_set
+
+    rng = random.Random(seed)
+    keys, vals = ["app", "tier", "zone", "bad key!"], ["a", "b", "c", "-bad-"]
+    svcs = []
+    for i in range(60):
+        sel = {rng.choice(keys): rng.choice(vals) for _ in range(rng.randrange(0, 3))}
+        svcs.append(Service(metadata=ObjectMeta(name=f"s{i}", namespace=rng.choice(["", "default", "x"])),
+                            spec=ServiceSpec(selector=sel if sel or rng.random() < 0.5 else None)))
+    view = ClusterView([make_node("n0", 1000, 1 << 30)], svcs, Interner())
+    for j in range(300):
+        labels = {k: rng.choice(vals) for k in rng.sample(keys, rng.randrange(0, 4))}
+        pod = Pod(metadata=ObjectMeta(name=f"p{j}", namespace=rng.choice(["", "default", "x"]),
+                                      labels=labels if labels or rng.random() < 0.5 else None))
+        want = [i for i, s in enumerate(svcs) if s.metadata.namespace == pod.metadata.namespace
+                and selector_from_set(s.spec.selector).matches(pod.metadata.labels)]
+        assert view.pod_services(pod) == want
