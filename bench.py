@@ -105,6 +105,8 @@ def main():
         import torch.distributed as dist_mod
 
         dist = dist_mod
+        if torch.cuda.is_available() and torch.cuda.device_count() > local_rank:
+            torch.cuda.set_device(local_rank)  # torch's syncs (barrier()) on this rank's GPU, not GPU 0
         dist.init_process_group("gloo")
         if args.transport == "rccl":
             idb = DeviceScheduler.nccl_unique_id() if rank == 0 else bytes(128)
