@@ -16,6 +16,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -75,6 +76,7 @@ struct ksg_ctx {
   hipStream_t st = nullptr;
   ncclComm_t comm = nullptr;
   bool xchg = false;
+  double ppw_est = 0.0;  // pods resolved per window (window path round sizing)
   // pinned staging for the per-call uploads / small read-backs (a pageable
   // hipMemcpyAsync is a staged, effectively synchronous copy)
   uint8_t* h_up = nullptr;
@@ -1147,7 +1149,16 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     // Windows are chained on the device: each kernel reads the window's start
     // from d_run (written by the previous resolver), so the host enqueues a
     // round of windows and synchronises once per round, not once per window.
-    uint32_t pos = 0, K = (uint32_t)(((uint64_t)n * 5 + (uint64_t)W * 4 - 1) / ((uint64_t)W * 4)) + 1;
+    // Windows per round: from the pods per window the previous rounds resolved
+    // (windows stop early on service / exhaustion / slot events, e.g. every ~13
+    // pods with ServiceAntiAffinity), 10% over; launches past the batch's end
+    // return at once. Fewer rounds = fewer host synchronisations per batch.
+    auto round_k = [&](uint32_t left) -> uint32_t {
+      const double ppw = c->ppw_est > 0.0 ? std::min<double>(std::max(c->ppw_est, 1.0), (double)W) : 0.8 * W;
+      const double k = std::ceil((double)left / ppw * 1.1) + 1.0;
+      return (uint32_t)std::min(k, 8192.0);
+    };
+    uint32_t pos = 0, K = round_k(n);
     c->last_kms[0] = c->last_kms[1] = c->last_kms[2] = 0;
     while (pos < n) {
       if (c->wev.size() < 2 * (size_t)K + 1) {
@@ -1179,6 +1190,10 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       if ((rc = flush_deferred(c))) return rc;  // the host mirror catches up while the device works
       HIPCHK(c, hipStreamSynchronize(c->st));
       const KsgWinRun r = *c->h_run;
+      if (r.windows > 0 && r.pos > pos) {  // pods per window, smoothed over rounds and batches
+        const double ppw = (double)(r.pos - pos) / (double)r.windows;
+        c->ppw_est = c->ppw_est > 0.0 ? 0.5 * c->ppw_est + 0.5 * ppw : ppw;
+      }
       // every launch of the round, including the ones after the batch was done
       // (they return at once), so the mean matches a kernel trace of the run
       for (uint32_t k = 0; k < K; ++k) {
@@ -1209,7 +1224,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
         ++c->last_stats[3];
       }
       // next round (rare: stops shortened this round's windows): the rest at W/2 pods per window
-      K = (uint32_t)(((uint64_t)(n - std::min(pos, n)) * 2 + W - 1) / W) + 1;
+      K = round_k(n - std::min(pos, n));
     }
   } else if (!c->xchg) {
     HIPCHK(c, ksg_launch_batch(c->R, anti_on(c), c->dev, c->d_pods, c->d_ids, n, c->d_rng, c->d_out, c->st));
