@@ -42,7 +42,8 @@ def meta_namespace_key(obj) -> str:
 
 class Store:
     """cache.Store (store.go): a keyed, thread-safe object cache. Listeners get
-    (op, key, old, new) after each change, outside the lock's critical data."""
+    (op, key, old, new) for each change, called under the store's lock so that
+    the event order is the mutation order (listeners must only enqueue)."""
 
     def __init__(self, key_func: Callable = meta_namespace_key):
         self._lock = threading.RLock()
@@ -62,7 +63,7 @@ class Store:
         with self._lock:
             old = self._items.get(k)
             self._items[k] = obj
-        self._emit(ADD if old is None else UPDATE, k, old, obj)
+            self._emit(ADD if old is None else UPDATE, k, old, obj)
 
     def update(self, obj) -> None:  # store.go:148-160
         self.add(obj)
@@ -71,8 +72,8 @@ class Store:
         k = self._key(obj)
         with self._lock:
             old = self._items.pop(k, None)
-        if old is not None:
-            self._emit(DELETE, k, old, None)
+            if old is not None:
+                self._emit(DELETE, k, old, None)
 
     def get(self, obj) -> Tuple[Optional[object], bool]:  # store.go:212-220
         return self.get_by_key(self._key(obj))
@@ -95,11 +96,11 @@ class Store:
         with self._lock:
             old = self._items
             self._items = dict(new)
-        for k, o in old.items():
-            if k not in new:
-                self._emit(DELETE, k, o, None)
-        for k, o in new.items():
-            self._emit(ADD if k not in old else UPDATE, k, old.get(k), o)
+            for k, o in old.items():
+                if k not in new:
+                    self._emit(DELETE, k, o, None)
+            for k, o in new.items():
+                self._emit(ADD if k not in old else UPDATE, k, old.get(k), o)
 
     def __len__(self):
         with self._lock:

@@ -310,3 +310,26 @@ def test_schedule_loop_gpu_modeler(name, nn, npods, tight, existing):
     finally:
         for g in made:
             g.close()
+
+
+def test_store_events_follow_mutation_order_across_threads():
+    """Listeners run under the store lock: replaying the event stream reproduces the
+    store's final state even with several writer threads on the same keys."""
+    import threading
+
+    st = Store()
+    replay = {}
+    st.add_listener(lambda op, k, old, new: replay.pop(k) if op == DELETE else replay.__setitem__(k, new))
+
+    def writer(seed):
+        rng = random.Random(seed)
+        for _ in range(3000):
+            p = Pod(metadata=ObjectMeta(name=f"p{rng.randrange(8)}"), status=PodStatus(host=str(seed)))
+            (st.delete if rng.random() < 0.3 else st.add)(p)
+
+    ts = [threading.Thread(target=writer, args=(s,)) for s in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert {k: id(v) for k, v in replay.items()} == {k: id(st.get_by_key(k)[0]) for k in st.list_keys()}
