@@ -4,7 +4,7 @@
 A "step" is one batch of `--batch` pods scheduled in order through the hot path
 (filter every node, score, argmax + reference tie-break, commit) by
 ksg_schedule_batch: windows of pods are scored against a snapshot on all CUs
-(ksg_win_eval_kernel) and resolved in order, exactly, by ksg_win_resolve_kernel;
+(ksg_win_score_kernel) and resolved in order, exactly, by ksg_win_resolve_kernel;
 node state is resident in HBM before the timed region (the C ABI copies the
 batch descriptors in, ~B*88 bytes, inside the step).
 
@@ -251,6 +251,7 @@ def main():
                                "sample": f"first {done_i} pods, incremental mode (SoA closed forms, "
                                          f"no per-pod re-list), {inc_s:.1f}s"}}
 
+    xname = "RCCL" if args.transport == "rccl" else "host-staged gloo"
     line = {
         "metric": "pods scheduled/sec",
         "value": value,
@@ -273,8 +274,8 @@ def main():
                    "exchange": None if world == 1 else args.transport,
                    "parallelism": ("speculative windows: all-CU snapshot scoring + in-order exact resolver"
                                    if kk["launches"] else "single workgroup persistent kernel") if world == 1
-                   else (f"node-sharded x{world}: shard scoring, RCCL all-gather per window, replicated resolver"
-                         if kk["launches"] else f"node-sharded x{world}, RCCL all-gather per pod")},
+                   else (f"node-sharded x{world}: shard scoring, {xname} all-gather per window, replicated resolver"
+                         if kk["launches"] else f"node-sharded x{world}, {xname} all-gather per pod")},
         "roofline": roofline,
         "cpu_baseline": cpu,
     }

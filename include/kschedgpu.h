@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define KSG_ABI_VERSION 1
+#define KSG_ABI_VERSION 2
 
 /* ---- return codes ---------------------------------------------------- */
 #define KSG_OK 0
@@ -86,9 +86,25 @@ extern "C" {
 #define KSG_MAX_PRESENCE 8      /* LabelsPresence predicates (policy)           */
 #define KSG_MAX_PRESENCE_KEYS 8 /* labels per LabelsPresence predicate          */
 #define KSG_MAX_AFF 4           /* ServiceAffinity labels (union of predicates) */
+#define KSG_MAX_AFF_GROUPS 8    /* ServiceAffinity predicates (label groups)    */
+
+/* Label pair flag in ksg_set_cluster's pair_keys[p]: the pair's key fails
+ * IsQualifiedName or its value fails IsValidLabelValue (pkg/util/validation.go),
+ * so a selector built from it by SelectorFromSet is the empty selector that
+ * matches every node (pkg/labels/selector.go:654-668). The key id is
+ * pair_keys[p] & ~KSG_PAIR_INVALID. */
+#define KSG_PAIR_INVALID 0x80000000u
+/* ksg_pod.aff_pair[j]: the pod's nodeSelector gives ServiceAffinity label j
+ * an invalid value (or label j's key is invalid). */
+#define KSG_AFF_INVALID (-2)
 
 /* Scheduler configuration: the compiled form of map[string]FitPredicate +
- * []PriorityConfig that NewGenericScheduler receives (factory.go:149). */
+ * []PriorityConfig that NewGenericScheduler receives (factory.go:149).
+ *
+ * Weights are int32 (factory.compile refuses anything outside int32), and
+ * ksg_create returns KSG_ERR_ARG when a combined score could reach 2^30 in
+ * magnitude: 10 * (sum of |w| over score-10 priorities) + |w_equal| >= 2^30
+ * (scores are kept in int32 on the device). */
 typedef struct ksg_config {
   uint32_t predicates;          /* KSG_PRED_* bitmask                                   */
   uint32_t n_priority_configs;  /* len(priorityConfigs); 0 => EqualPriority fallback
@@ -111,6 +127,12 @@ typedef struct ksg_config {
   uint32_t aff_key[KSG_MAX_AFF];
   uint32_t max_conflict_keys;   /* capacity for interned host-port + GCE-PD ids          */
   uint32_t max_domains;         /* capacity for anti-affinity label values (pair ids)    */
+  /* ServiceAffinity predicates: bit j of aff_group_mask[g] = aff label j belongs
+   * to predicate g. Each predicate builds its own selector, so SelectorFromSet's
+   * invalid-value trap empties one predicate's selector, not the others'
+   * (predicates.go:311-315). n_aff_groups == 0: one predicate over every label. */
+  uint32_t n_aff_groups;
+  uint32_t aff_group_mask[KSG_MAX_AFF_GROUPS];
 } ksg_config;
 
 /* One node, rank-ordered. Capacity is node.Spec.Capacity converted with
@@ -137,7 +159,8 @@ typedef struct ksg_pod {
   uint32_t svcs_off, n_svcs;    /* every service whose selector matches the pod     */
   int32_t aff_pair[KSG_MAX_AFF];/* ServiceAffinity: pair id of the pod's own
                                    nodeSelector value for aff label j; -1 = the pod
-                                   does not specify it; 0 = value no node has        */
+                                   does not specify it; 0 = value no node has;
+                                   KSG_AFF_INVALID = an invalid value            */
 } ksg_pod;
 
 typedef struct ksg_ctx ksg_ctx;
@@ -173,8 +196,9 @@ int ksg_destroy(ksg_ctx* ctx);
 const char* ksg_last_error(ksg_ctx* ctx);
 
 /* Replace the node set (MinionLister.List()). Resets all pod state.
- * pair_keys[p] = label-key id of label pair p (pair 0 is reserved: "no node has
- * it"). node_pairs holds each node's label pair ids. */
+ * pair_keys[p] = label-key id of label pair p, | KSG_PAIR_INVALID for a pair
+ * SelectorFromSet would reject (pair 0 is reserved: "no node has it").
+ * node_pairs holds each node's label pair ids. */
 int ksg_set_cluster(ksg_ctx* ctx, const ksg_node* nodes, uint32_t n_nodes,
                     const uint32_t* node_pairs, uint32_t n_node_pairs,
                     const uint32_t* pair_keys, uint32_t n_pairs,
@@ -212,9 +236,12 @@ int ksg_evaluate(ksg_ctx* ctx, const ksg_pod* pod, const uint32_t* ids,
 
 /* Batch execution strategy. window > 0 (default 128, env KSG_WINDOW): pods
  * are filtered/scored a window at a time against one snapshot on all CUs and
- * then resolved in order by one wave (exact; see ksg_window.hip). window = 0:
- * the persistent one-pod-at-a-time kernel. Both give identical results; the
- * window path is used only when it is exact (no ServiceAntiAffinity). */
+ * then resolved in order by one workgroup (exact; see ksg_window.hip);
+ * ServiceAntiAffinity adds a per-window domain-count pass. window = 0: the
+ * persistent one-pod-at-a-time kernel. Both give identical results; a batch
+ * takes the window path only where it is exact (non-negative LeastRequested /
+ * ServiceSpreading weights, capacities and requested totals within 2^49, at
+ * most 2048 node words). */
 int ksg_set_window(ksg_ctx* ctx, uint32_t window);
 /* Window statistics of the last ksg_schedule_batch: stats4[0] = windows
  * (snapshots), [1] = windows ended because a service scalar changed, [2] =
@@ -227,7 +254,7 @@ int ksg_last_batch_stats(ksg_ctx* ctx, uint32_t* stats4);
 int ksg_last_batch_ms(ksg_ctx* ctx, double* ms);
 
 /* Window path of the last ksg_schedule_batch: out3[0] = device ms in the
- * snapshot-scoring kernel (ksg_win_eval_kernel), out3[1] = device ms in the
+ * snapshot-scoring kernel(s) (ksg_win_score_kernel), out3[1] = device ms in the
  * resolver (ksg_win_resolve_kernel), out3[2] = resolver launches (windows are
  * chained on the device, so a round may end with launches that find the batch
  * done and return at once); from HIP events recorded around each launch on the

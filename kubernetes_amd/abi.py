@@ -49,6 +49,9 @@ MAX_LABEL_PREF = 8
 MAX_PRESENCE = 8
 MAX_PRESENCE_KEYS = 8
 MAX_AFF = 4
+MAX_AFF_GROUPS = 8
+PAIR_INVALID = 0x80000000  # pair_keys flag: SelectorFromSet rejects the (key, value)
+AFF_INVALID = -2           # ksg_pod.aff_pair: the pod's own value for the label is invalid
 
 U32 = C.c_uint32
 I32 = C.c_int32
@@ -78,6 +81,8 @@ class KsgConfig(C.Structure):
         ("aff_key", U32 * MAX_AFF),
         ("max_conflict_keys", U32),
         ("max_domains", U32),
+        ("n_aff_groups", U32),
+        ("aff_group_mask", U32 * MAX_AFF_GROUPS),
     ]
 
 

@@ -230,6 +230,25 @@ struct PodCtx {
   int32_t req_aff[KSG_MAX_AFF];
 };
 
+// SelectorFromSet's trap per ServiceAffinity predicate (predicates.go:311-315,
+// labels.go:60-61, selector.go:654-668): a predicate whose affinity map holds
+// an invalid (key, value) builds the empty selector and fits every node, so
+// its labels are only required through the predicates that stayed valid.
+// req_aff[j] < 0 afterwards means "no requirement on label j".
+__device__ __forceinline__ void aff_apply_trap(const KsgDev& d, int32_t (&req_aff)[KSG_MAX_AFF]) {
+  uint32_t bad = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < KSG_MAX_AFF; ++j)
+    if (j < d.n_aff && req_aff[j] == KSG_AFF_INVALID) bad |= 1u << j;
+  if (!bad) return;
+  uint32_t active = 0;
+  for (uint32_t g = 0; g < d.n_aff_groups; ++g)
+    if (!(d.aff_group_mask[g] & bad)) active |= d.aff_group_mask[g];
+#pragma unroll
+  for (uint32_t j = 0; j < KSG_MAX_AFF; ++j)
+    if (!((active >> j) & 1u)) req_aff[j] = -1;
+}
+
 template <bool COH = true>
 __device__ __forceinline__ void pod_resolve(const KsgDev& d, const ksg_pod& p, const uint32_t* ids,
                                             PodCtx& c) {
@@ -264,7 +283,7 @@ __device__ __forceinline__ void pod_resolve(const KsgDev& d, const ksg_pod& p, c
     for (uint32_t j = 0; j < KSG_MAX_AFF; ++j) {
       if (j < d.n_aff) {
         c.req_aff[j] = p.aff_pair[j];
-        if (p.aff_pair[j] < 0) all_given = false;
+        if (p.aff_pair[j] == -1) all_given = false;  // (KSG_AFF_INVALID: given, invalid)
       }
     }
     if (!all_given && peer != -1) {
@@ -273,9 +292,10 @@ __device__ __forceinline__ void pod_resolve(const KsgDev& d, const ksg_pod& p, c
       } else {
 #pragma unroll
         for (uint32_t j = 0; j < KSG_MAX_AFF; ++j)
-          if (j < d.n_aff && c.req_aff[j] < 0) c.req_aff[j] = d.aff_pair[(size_t)j * d.n_nodes + peer];
+          if (j < d.n_aff && c.req_aff[j] == -1) c.req_aff[j] = d.aff_pair[(size_t)j * d.n_nodes + peer];
       }
     }
+    aff_apply_trap(d, c.req_aff);
   }
 }
 

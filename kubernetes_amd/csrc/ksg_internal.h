@@ -18,6 +18,8 @@
 //                                                  -2 not a known node)
 //   anti_domain[A][N]             int32   static   dense value index of anti label, -1
 //   aff_pair[J][N]                int32   static   pair id of node's value of aff label j
+//                                                  (-1 none, KSG_AFF_INVALID: SelectorFromSet
+//                                                  would reject the (key, value))
 #pragma once
 #include <stdint.h>
 #include "../../include/kschedgpu.h"
@@ -53,6 +55,8 @@ struct KsgDev {
   int32_t w_anti[KSG_MAX_ANTI];
   uint32_t anti_dom_off[KSG_MAX_ANTI];
   uint32_t n_aff;
+  uint32_t n_aff_groups;      // ServiceAffinity predicates (>= 1 when n_aff > 0)
+  uint32_t aff_group_mask[KSG_MAX_AFF_GROUPS];  // aff labels of each predicate
   int32_t equal_fallback;     // no priority configs: every fitting node scores 1
   int32_t empty_priorities;   // configs present but all weights 0: always FitError
   int32_t has_static_score;

@@ -382,10 +382,15 @@ __global__ __launch_bounds__(64) void ksg_decide_kernel(KsgDev d, const ksg_pod*
 // and ServiceAffinity pair per node. One thread per node.
 // ============================================================================
 
+// pair_keys[p] carries KSG_PAIR_INVALID for pairs SelectorFromSet rejects
+__device__ __forceinline__ uint32_t pair_key_of(const uint32_t* pair_keys, uint32_t p) {
+  return pair_keys[p] & ~KSG_PAIR_INVALID;
+}
+
 __device__ __forceinline__ bool node_has_key(const uint32_t* pairs, uint32_t np,
                                              const uint32_t* pair_keys, uint32_t key) {
   for (uint32_t i = 0; i < np; ++i)
-    if (pair_keys[pairs[i]] == key) return true;
+    if (pair_key_of(pair_keys, pairs[i]) == key) return true;
   return false;
 }
 
@@ -425,7 +430,8 @@ __global__ void ksg_static_kernel(KsgStaticCfg sc, uint32_t n_nodes, const ksg_n
     for (uint32_t j = 0; j < sc.n_aff; ++j) {
       int32_t pr = -1;
       for (uint32_t i = 0; i < np; ++i)
-        if (pair_keys[pairs[i]] == sc.aff_key[j]) pr = (int32_t)pairs[i];
+        if (pair_key_of(pair_keys, pairs[i]) == sc.aff_key[j])
+          pr = (pair_keys[pairs[i]] & KSG_PAIR_INVALID) ? KSG_AFF_INVALID : (int32_t)pairs[i];
       aff_pair[(size_t)j * n_nodes + n] = pr;
     }
   }

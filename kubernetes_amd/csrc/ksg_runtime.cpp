@@ -372,7 +372,8 @@ int check_pod(ksg_ctx* c, const ksg_pod* p, const uint32_t* ids, size_t n_ids) {
   for (uint32_t i = 0; i < p->n_svcs; ++i)
     if (ids[p->svcs_off + i] >= c->S) return fail(c, KSG_ERR_ARG, "service id out of range");
   for (uint32_t j = 0; j < c->cfg.n_aff_labels; ++j)
-    if (p->aff_pair[j] >= (int32_t)c->n_pairs) return fail(c, KSG_ERR_ARG, "affinity pair out of range");
+    if (p->aff_pair[j] >= (int32_t)c->n_pairs || p->aff_pair[j] < KSG_AFF_INVALID)
+      return fail(c, KSG_ERR_ARG, "affinity pair out of range");
   return KSG_OK;
 }
 
@@ -489,8 +490,9 @@ int scan_exchange(ksg_ctx* c, const ksg_pod* dpod, const uint32_t* dids, int mod
   return KSG_OK;
 }
 
-// The window path needs monotone scores under commits (see ksg_window.hip):
-// no ServiceAntiAffinity, and int64 totals far from wrapping.
+// The window path needs scores that commits can only lower (see ksg_window.hip):
+// non-negative LeastRequested / ServiceSpreading weights and int64 totals far
+// from wrapping (ServiceAntiAffinity is handled by its count pass and stops).
 // The resolver walks the whole node set on every rank (state is replicated).
 KsgDev full_geometry(const ksg_ctx* c) {
   KsgDev f = c->dev;
@@ -602,8 +604,11 @@ static int create_impl(const ksg_config* cfg, int device, int rank, int world, c
                        ksg_ctx** out) {
   if (!cfg || !out || world < 1 || rank < 0 || rank >= world) return KSG_ERR_ARG;
   if (cfg->n_anti > KSG_MAX_ANTI || cfg->n_label_pref > KSG_MAX_LABEL_PREF ||
-      cfg->n_presence > KSG_MAX_PRESENCE || cfg->n_aff_labels > KSG_MAX_AFF)
+      cfg->n_presence > KSG_MAX_PRESENCE || cfg->n_aff_labels > KSG_MAX_AFF ||
+      cfg->n_aff_groups > KSG_MAX_AFF_GROUPS)
     return KSG_ERR_ARG;
+  for (uint32_t g = 0; g < cfg->n_aff_groups; ++g)
+    if (cfg->aff_group_mask[g] >> cfg->n_aff_labels) return KSG_ERR_ARG;  // a label the config lacks
   for (uint32_t q = 0; q < cfg->n_presence; ++q)
     if (cfg->presence_n_keys[q] > KSG_MAX_PRESENCE_KEYS) return KSG_ERR_ARG;
   {  // combined scores are int32 on the device
@@ -725,6 +730,7 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   }
   free_cluster(c);
   drop_deferred(c);
+  c->ppw_est = 0.0;
   c->N = n_nodes;
   c->nw = (n_nodes + 63) / 64;
   c->n_pairs = n_pairs;
@@ -760,7 +766,7 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
     d.anti_dom_off[a] = c->D;
     uint32_t nd = 0;
     for (uint32_t p = 1; p < n_pairs; ++p)
-      if (pair_keys[p] == c->cfg.anti_key[a]) dom_of_pair[(size_t)a * n_pairs + p] = (int32_t)nd++;
+      if ((pair_keys[p] & ~KSG_PAIR_INVALID) == c->cfg.anti_key[a]) dom_of_pair[(size_t)a * n_pairs + p] = (int32_t)nd++;
     c->D += nd;
   }
   if (c->D > c->cfg.max_domains)
@@ -857,6 +863,13 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   d.n_domains_total = c->D;
   d.preds = c->cfg.predicates;
   d.n_aff = (c->cfg.predicates & KSG_PRED_SERVICEAFFINITY) ? c->cfg.n_aff_labels : 0;
+  // ServiceAffinity predicates (label groups); none given: one over every label
+  d.n_aff_groups = c->cfg.n_aff_groups;
+  for (uint32_t g = 0; g < d.n_aff_groups; ++g) d.aff_group_mask[g] = c->cfg.aff_group_mask[g];
+  if (d.n_aff_groups == 0 && d.n_aff > 0) {
+    d.n_aff_groups = 1;
+    d.aff_group_mask[0] = (1u << d.n_aff) - 1u;
+  }
   d.equal_fallback = c->cfg.n_priority_configs == 0;
   // prioritizeNodes skips weight-0 configs; if every config has weight 0 the
   // HostPriorityList is empty and Schedule returns *FitError.
@@ -1064,28 +1077,36 @@ int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int6
   return KSG_OK;
 }
 
+// the device half of a commit: decide the tie_index-th tie and apply AssumePod's delta
+static int commit_on_device(ksg_ctx* c, uint32_t tie_index, int32_t* node) {
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = ensure_out(c, 1);
+  if (rc) return rc;
+  HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods, c->d_ids, rec_buf(c), c->rec_bytes, c->world,
+                              c->d_shard_wlo, 2, tie_index, c->d_rng, c->d_out, 0, c->d_summary, c->st));
+  if ((rc = grow_host(c, &c->h_dn, &c->h_dn_cap, 4))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->h_dn, c->d_out, 4, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  memcpy(node, c->h_dn, 4);
+  if (*node < 0) return fail(c, KSG_ERR_STATE, "commit selected no node (%d)", *node);
+  return KSG_OK;
+}
+
 int ksg_schedule_commit(ksg_ctx* c, uint32_t tie_index, int32_t* out_node) {
   if (!c) return KSG_ERR_ARG;
   KSG_LOCK(c);
   if (!c->pending) return fail(c, KSG_ERR_STATE, "no schedule_begin pending");
   if (tie_index >= c->pending_k) return fail(c, KSG_ERR_ARG, "tie_index %u >= tie_count %llu", tie_index,
                                              (unsigned long long)c->pending_k);
-  HIPCHK(c, hipSetDevice(c->device));
-  int rc = ensure_out(c, 1);
-  if (rc) return rc;
-  HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods, c->d_ids, rec_buf(c), c->rec_bytes, c->world,
-                              c->d_shard_wlo, 2, tie_index, c->d_rng, c->d_out, 0, c->d_summary, c->st));
   int32_t node = -1;
-  if ((rc = grow_host(c, &c->h_dn, &c->h_dn_cap, 4))) return rc;
-  HIPCHK(c, hipMemcpyAsync(c->h_dn, c->d_out, 4, hipMemcpyDeviceToHost, c->st));
-  HIPCHK(c, hipStreamSynchronize(c->st));
-  memcpy(&node, c->h_dn, 4);
+  int rc = commit_on_device(c, tie_index, &node);
   c->pending = false;
-  if (node < 0) return fail(c, KSG_ERR_STATE, "commit selected no node (%d)", node);
-  rc = mirror_add(c, (uint32_t)node, &c->pend, c->pend_ids.data(), false);
-  if (rc) return rc;
+  if (rc == KSG_OK) rc = mirror_add(c, (uint32_t)node, &c->pend, c->pend_ids.data(), false);
   c->pend.uid = ~0ULL;
-  if ((rc = apply_queued(c))) return rc;
+  // the updates queued while the begin was pending apply now, whatever the outcome
+  const int rq = apply_queued(c);
+  if (rc) return rc;
+  if (rq) return rq;
   if (out_node) *out_node = node;
   return KSG_OK;
 }
@@ -1153,8 +1174,12 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     // (windows stop early on service / exhaustion / slot events, e.g. every ~13
     // pods with ServiceAntiAffinity), 10% over; launches past the batch's end
     // return at once. Fewer rounds = fewer host synchronisations per batch.
+    // A sharded context issues one collective per launch, so every rank must
+    // enqueue the same number of launches: its estimate starts fresh each batch
+    // and follows only this batch's progress, which every rank resolves alike.
+    double ppw_est = c->xchg ? 0.0 : c->ppw_est;
     auto round_k = [&](uint32_t left) -> uint32_t {
-      const double ppw = c->ppw_est > 0.0 ? std::min<double>(std::max(c->ppw_est, 1.0), (double)W) : 0.8 * W;
+      const double ppw = ppw_est > 0.0 ? std::min<double>(std::max(ppw_est, 1.0), (double)W) : 0.8 * W;
       const double k = std::ceil((double)left / ppw * 1.1) + 1.0;
       return (uint32_t)std::min(k, 8192.0);
     };
@@ -1192,7 +1217,8 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       const KsgWinRun r = *c->h_run;
       if (r.windows > 0 && r.pos > pos) {  // pods per window, smoothed over rounds and batches
         const double ppw = (double)(r.pos - pos) / (double)r.windows;
-        c->ppw_est = c->ppw_est > 0.0 ? 0.5 * c->ppw_est + 0.5 * ppw : ppw;
+        ppw_est = ppw_est > 0.0 ? 0.5 * ppw_est + 0.5 * ppw : ppw;
+        if (!c->xchg) c->ppw_est = ppw_est;
       }
       // every launch of the round, including the ones after the batch was done
       // (they return at once), so the mean matches a kernel trace of the run
@@ -1301,6 +1327,7 @@ int ksg_set_window(ksg_ctx* c, uint32_t window) {
   if (!c) return KSG_ERR_ARG;
   KSG_LOCK(c);
   c->window = window;
+  c->ppw_est = 0.0;
   return KSG_OK;
 }
 

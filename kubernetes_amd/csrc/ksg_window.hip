@@ -40,8 +40,9 @@
 // of a newly committed node are retired lazily (only when a later pod needs
 // that node, else at the next commit).
 //
-// ServiceAntiAffinity changes a service-wide scalar on every commit and is
-// served by the exact per-pod kernel instead (ksg_kernels.hip).
+// ServiceAntiAffinity scores a node by its domain's count of the pod's service
+// pods over the pod's FILTERED nodes: phase A runs a count pass first, and a
+// window stops at a pod whose service count or domain counts moved.
 #include "ksg_device.h"
 
 #include <algorithm>

@@ -27,6 +27,7 @@ from . import abi
 
 DefaultProvider = "DefaultProvider"
 
+_I32_MIN, _I32_MAX = -(1 << 31), (1 << 31) - 1
 _VALID_NAME = re.compile(r"[a-zA-Z0-9]([-a-zA-Z0-9]*[a-zA-Z0-9])")
 
 
@@ -252,8 +253,34 @@ class SchedulerConfig:
         cfg.n_aff_labels = len(aff)
         for j, l in enumerate(aff):
             cfg.aff_key[j] = key_id(l)
+        # one label group per ServiceAffinity predicate: SelectorFromSet's trap
+        # empties one predicate's selector only (predicates.go:311-315)
+        groups = []
+        for name in sorted(self.predicates):
+            d = self.predicates[name]
+            if d.kind == "ServiceAffinity" and d.labels:
+                m = 0
+                for l in d.labels:
+                    m |= 1 << aff.index(l)
+                if m not in groups:
+                    groups.append(m)
+        if len(groups) > abi.MAX_AFF_GROUPS:
+            raise ConfigError("too many ServiceAffinity predicates")
+        cfg.n_aff_groups = len(groups)
+        for g, m in enumerate(groups):
+            cfg.aff_group_mask[g] = m
         cfg.n_priority_configs = len(self.priorities)
         n_anti = n_pref = 0
+        tot = {"LeastRequestedPriority": 0, "ServiceSpreadingPriority": 0, "EqualPriority": 0}
+        for p in self.priorities:
+            # Policy weights are Go ints (plugin/pkg/scheduler/api/types.go:46); the
+            # device keeps them (and their sums) as int32: refuse, never wrap
+            if not (_I32_MIN <= int(p.weight) <= _I32_MAX):
+                raise ConfigError(f"priority weight {p.weight} of {p.kind} is outside int32")
+            if p.kind in tot:
+                tot[p.kind] += int(p.weight)
+                if not (_I32_MIN <= tot[p.kind] <= _I32_MAX):
+                    raise ConfigError(f"summed {p.kind} weight {tot[p.kind]} is outside int32")
         for p in self.priorities:
             if p.kind == "LeastRequestedPriority":
                 cfg.w_least_requested += p.weight

@@ -23,7 +23,12 @@ import numpy as np
 from . import abi
 from .api import Node, Pod, Service
 from .engine import ClusterArrays, PodBatch
-from .labels import selector_from_set
+from .labels import is_qualified_name, is_valid_label_value, selector_from_set
+
+
+def pair_is_valid(key: str, value: str) -> bool:
+    """NewRequirement(key, =, {value}) succeeds (selector.go:91-115, 638-650)."""
+    return is_qualified_name(key) and is_valid_label_value(value)
 
 
 class Interner:
@@ -48,7 +53,12 @@ class Interner:
             if not create:
                 return 0
             pid = self.pairs[(key, value)] = len(self.pair_key)
-            self.pair_key.append(self.key_id(key))
+            kid = self.key_id(key)
+            # SelectorFromSet rejects this (key, value) (selector.go:654-668): flagged so
+            # a ServiceAffinity selector built from a peer node's label matches everything
+            if not pair_is_valid(key, value):
+                kid |= abi.PAIR_INVALID
+            self.pair_key.append(kid)
         return pid
 
     def conflict_id(self, kind: str, value) -> int:
@@ -159,7 +169,8 @@ class PodBatchBuilder:
         aff = [-1] * abi.MAX_AFF
         for j, l in enumerate(self.aff_labels):  # CheckServiceAffinity (predicates.go:261-271)
             if ns and l in ns:
-                aff[j] = it.pair_id(l, ns[l], create=False)
+                # an invalid value empties the predicate's selector (predicates.go:314)
+                aff[j] = it.pair_id(l, ns[l], create=False) if pair_is_valid(l, ns[l]) else abi.AFF_INVALID
         base = len(self.ids)
         self.ids.extend(ports)
         self.ids.extend(pds)

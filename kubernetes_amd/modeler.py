@@ -208,6 +208,7 @@ class PodMirror:
         return fn
 
     def _add(self, src: int, key: str, pod: Pod):
+        self._remove(src, key)  # an ADD for a key already on the device replaces it
         uid = self.new_uid()
         host_id, batch = self.ingest(pod, uid)
         self.sink.add_pod(host_id, batch, 0)
@@ -255,22 +256,23 @@ class PodMirror:
 
     def reload(self) -> None:
         """The device context was re-created from a new ClusterView (node or service
-        change): discard the queue and load the modeler's current pod set."""
-        with self._qlock:
-            self._q.clear()
+        change): discard the queue and load the modeler's current pod set.
+
+        The queue is cleared and both stores are snapshotted while holding the stores'
+        locks (their listeners enqueue under them), so an event is either already in
+        the snapshot or queued after it, never both."""
         self.pending.clear()
         self.on_device.clear()
         self.modeler.prune_assumed()
-        with self._qlock:
-            self._q.clear()
-        for key in self.modeler.scheduled_pods.store.list_keys():
-            p, ok = self.modeler.scheduled_pods.store.get_by_key(key)
+        sched, assumed = self.modeler.scheduled_pods.store, self.modeler.assumed_pods.store
+        with sched._lock, assumed._lock:
+            with self._qlock:
+                self._q.clear()
+            snap = [(self.SCHED, k, sched.get_by_key(k)) for k in sched.list_keys()]
+            snap += [(self.ASSUMED, k, assumed.get_by_key(k)) for k in assumed.list_keys()]
+        for src, key, (p, ok) in snap:
             if ok:
-                self._add(self.SCHED, key, p)
-        for key in self.modeler.assumed_pods.store.list_keys():
-            p, ok = self.modeler.assumed_pods.store.get_by_key(key)
-            if ok:
-                self._add(self.ASSUMED, key, p)
+                self._add(src, key, p)
         self.stats["reloads"] += 1
 
     def committed(self, pod: Pod, uid: int, host_id: int) -> None:

@@ -127,7 +127,8 @@ class GPUScheduler:
         self.view: Optional[ClusterView] = None
         self._node_sig = None
         self._svc_sig = None
-        self._mirror: Dict[str, tuple] = {}  # pod key -> (uid, host_id, id(pod))
+        self._mirror: Dict[str, tuple] = {}  # listed pod's distinct key -> (uid, host_id, id(pod))
+        self._assumed: List[tuple] = []  # (pod key, uid, host_id) committed since the last re-list
         self._next_uid = 1
         # the modeler's PodLister (factory.go: f.PodLister = modeler.PodLister()):
         # mirror its stores by events instead of re-listing every pod per Schedule
@@ -161,6 +162,7 @@ class GPUScheduler:
             self.engine.set_cluster(self.view.arrays)
             self._node_sig, self._svc_sig = nsig, ssig
             self._mirror = {}
+            self._assumed = []
             if self._events is not None:
                 self._events.reload()
                 return
@@ -177,26 +179,37 @@ class GPUScheduler:
                     j += 1
                 k = f"{k}#{j}"
             want[k] = p
-        for k, (uid, host, pid) in list(self._mirror.items()):
-            # a pod this scheduler assumed, now reported by the lister on the same host
-            if pid is None and k in want and self.view.host_id(want[k].status.host) == host:
-                self._mirror[k] = (uid, host, id(want[k]))
+        # pods this scheduler committed since the last call: kept iff the lister now
+        # reports them (under their key, or a #j variant of it) on the same host
+        assumed, self._assumed = self._assumed, []
+        for akey, uid, host in assumed:
+            k, j, match = akey, 0, None
+            while k in want:
+                if k not in self._mirror and self.view.host_id(want[k].status.host) == host:
+                    match = k
+                    break
+                j += 1
+                k = f"{akey}#{j}"
+            if match is None:
+                self.engine.remove_pod(uid)
+            else:
+                self._mirror[match] = (uid, host, id(want[match]))
         for key in [k for k, (uid, host, pid) in self._mirror.items()
                     if k not in want or id(want[k]) != pid or self.view.host_id(want[k].status.host) != host]:
             self.engine.remove_pod(self._mirror.pop(key)[0])
-        add = [p for k, p in want.items() if k not in self._mirror]
+        add = [(k, p) for k, p in want.items() if k not in self._mirror]
         if add:
             b = PodBatchBuilder(self.view, self.aff_labels)
             uids = []
-            for p in add:
+            for _, p in add:
                 uid = self._uid()
                 uids.append(uid)
                 b.add(p, uid)
             batch = b.build()
-            for i, p in enumerate(add):
+            for i, (k, p) in enumerate(add):
                 h = self.view.host_id(p.status.host)
                 self.engine.add_pod(h, batch, i)
-                self._mirror[p.key()] = (uids[i], h, id(p))
+                self._mirror[k] = (uids[i], h, id(p))
 
     # ---- Schedule -------------------------------------------------------------
     def schedule(self, pod: Pod, minion_lister) -> str:
@@ -230,7 +243,7 @@ class GPUScheduler:
         if self._events is not None:  # adopted when AssumePod reports it, else dropped
             self._events.committed(pod, uid, node)
         else:
-            self._mirror[pod.key()] = (uid, node, None)
+            self._assumed.append((pod.key(), uid, node))
         return host
 
     # ---- batch path (persistent kernel) -------------------------------------
@@ -254,7 +267,7 @@ class GPUScheduler:
                 if self._events is not None:
                     self._events.committed(p, uids[i], int(out[i]))
                 else:
-                    self._mirror[p.key()] = (uids[i], int(out[i]), None)
+                    self._assumed.append((p.key(), uids[i], int(out[i])))
             else:
                 hosts.append(None)
         return hosts, rng_state

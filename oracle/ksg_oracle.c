@@ -48,7 +48,8 @@ typedef struct orc {
   int64_t *cap_c, *cap_m;
   uint32_t **node_pairs; /* per node list */
   uint32_t *node_np;
-  uint32_t *pair_keys;
+  uint32_t *pair_keys;   /* label-key id (KSG_PAIR_INVALID stripped) */
+  uint8_t *pair_bad;     /* SelectorFromSet would reject the pair (selector.go:654-668) */
   /* placed pods, in insertion order (the lister order we canonicalize to) */
   opod *pods;
   uint32_t n_pods, cap_pods;
@@ -156,6 +157,7 @@ static void free_cluster(orc *o) {
   free(o->cap_c);
   free(o->cap_m);
   free(o->pair_keys);
+  free(o->pair_bad);
   free(o->used_c);
   free(o->used_m);
   free(o->key_ref);
@@ -169,6 +171,7 @@ static void free_cluster(orc *o) {
   o->node_np = NULL;
   o->cap_c = o->cap_m = NULL;
   o->pair_keys = NULL;
+  o->pair_bad = NULL;
   o->used_c = o->used_m = NULL;
   o->key_ref = NULL;
   o->svc_cnt = o->svc_max = o->svc_total = NULL;
@@ -198,8 +201,12 @@ int orc_set_cluster(orc *o, const ksg_node *nodes, uint32_t n_nodes, const uint3
   o->node_pairs = (uint32_t **)calloc(NN, sizeof(uint32_t *));
   o->node_np = (uint32_t *)calloc(NN, 4);
   o->pair_keys = (uint32_t *)calloc(n_pairs, 4);
+  o->pair_bad = (uint8_t *)calloc(n_pairs, 1);
   o->pair_keys[0] = 0xffffffffu;
-  for (uint32_t p = 1; p < n_pairs; ++p) o->pair_keys[p] = pair_keys[p];
+  for (uint32_t p = 1; p < n_pairs; ++p) {
+    o->pair_keys[p] = pair_keys[p] & ~KSG_PAIR_INVALID;
+    o->pair_bad[p] = (pair_keys[p] & KSG_PAIR_INVALID) != 0;
+  }
   for (uint32_t n = 0; n < n_nodes; ++n) {
     o->cap_c[n] = nodes[n].cap_milli_cpu;
     o->cap_m[n] = nodes[n].cap_memory;
@@ -328,24 +335,53 @@ typedef struct {
   int error;
 } pctx;
 
+/* CheckServiceAffinity (predicates.go:257-324) for every ServiceAffinity
+ * predicate at once: req_aff[j] = the value label j must have (pair id), the
+ * pod's own nodeSelector value first (:261-271), else the first service peer's
+ * node's (:274-307); then SelectorFromSet's trap per predicate (:311-315,
+ * labels.go:60-61, selector.go:654-668): a predicate whose affinity map holds
+ * an invalid (key, value) matches every node, so its labels stay required only
+ * through the predicates that are valid. req_aff[j] < 0: no requirement. */
 static void resolve_affinity(const orc *o, pctx *c) {
   c->error = 0;
   for (int j = 0; j < KSG_MAX_AFF; ++j) c->req_aff[j] = -1;
   if (!(o->cfg.predicates & KSG_PRED_SERVICEAFFINITY)) return;
+  const uint32_t J = o->cfg.n_aff_labels;
   int all_given = 1;
-  for (uint32_t j = 0; j < o->cfg.n_aff_labels; ++j) {
+  for (uint32_t j = 0; j < J; ++j) {
     c->req_aff[j] = c->p->aff_pair[j];
-    if (c->p->aff_pair[j] < 0) all_given = 0;
+    if (c->p->aff_pair[j] == -1) all_given = 0; /* KSG_AFF_INVALID: given (invalid) */
   }
-  if (all_given || c->p->service < 0) return;
-  const opod *peer = first_peer(o, (uint32_t)c->p->service);
-  if (!peer) return;
-  if (peer->host >= o->N) {
-    c->error = 1; /* GetNodeInfo(peer's Status.Host) fails, predicates.go:293-296 */
-    return;
+  if (!all_given && c->p->service >= 0) {
+    const opod *peer = first_peer(o, (uint32_t)c->p->service);
+    if (peer) {
+      if (peer->host >= o->N) {
+        c->error = 1; /* GetNodeInfo(peer's Status.Host) fails, predicates.go:293-296 */
+        return;
+      }
+      for (uint32_t j = 0; j < J; ++j)
+        if (c->req_aff[j] == -1) {
+          int32_t pr = node_pair_for_key(o, peer->host, o->cfg.aff_key[j]);
+          c->req_aff[j] = (pr > 0 && o->pair_bad[pr]) ? KSG_AFF_INVALID : pr;
+        }
+    }
   }
-  for (uint32_t j = 0; j < o->cfg.n_aff_labels; ++j)
-    if (c->req_aff[j] < 0) c->req_aff[j] = node_pair_for_key(o, peer->host, o->cfg.aff_key[j]);
+  /* one predicate per group; n_aff_groups == 0: one predicate over every label */
+  uint32_t ng = o->cfg.n_aff_groups, masks[KSG_MAX_AFF_GROUPS];
+  for (uint32_t g = 0; g < ng; ++g) masks[g] = o->cfg.aff_group_mask[g];
+  if (ng == 0) {
+    ng = 1;
+    masks[0] = (1u << J) - 1u;
+  }
+  uint32_t active = 0;
+  for (uint32_t g = 0; g < ng; ++g) {
+    int trapped = 0;
+    for (uint32_t j = 0; j < J; ++j)
+      if (((masks[g] >> j) & 1u) && c->req_aff[j] == KSG_AFF_INVALID) trapped = 1;
+    if (!trapped) active |= masks[g];
+  }
+  for (uint32_t j = 0; j < J; ++j)
+    if (!((active >> j) & 1u)) c->req_aff[j] = -1;
 }
 
 /* ================================================================ FAITHFUL */

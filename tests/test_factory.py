@@ -134,3 +134,35 @@ def test_pod_services_index_matches_scan(seed):
         want = [i for i, s in enumerate(svcs) if s.metadata.namespace == pod.metadata.namespace
                 and selector_from_set(s.spec.selector).matches(pod.metadata.labels)]
         assert view.pod_services(pod) == want
+
+
+def test_weights_outside_int32_are_refused():
+    """Policy weights are Go ints (plugin/pkg/scheduler/api/types.go:46); the device keeps
+    them as int32, so compile() refuses (never wraps) a weight or a summed builtin weight
+    outside int32."""
+    for w in (1 << 31, -(1 << 31) - 1, 1 << 40):
+        cfg = factory.create_from_config({"priorities": [
+            {"name": f"HugePref{abs(w)}", "weight": w, "argument": {"labelPreference": {"label": "rack"}}}]})
+        with pytest.raises(factory.ConfigError, match="outside int32"):
+            cfg.compile(lambda k: 0)
+    ok = factory.create_from_config({"priorities": [
+        {"name": "MaxPref", "weight": (1 << 31) - 1, "argument": {"labelPreference": {"label": "rack"}}}]})
+    assert ok.compile(lambda k: 0).w_pref[0] == (1 << 31) - 1
+
+
+def test_library_refuses_weights_over_the_score_bound():
+    """ksg_create returns KSG_ERR_ARG (before any HIP call) when a combined score could
+    reach 2^30: 10 * sum|w| + |w_equal| >= KSG_SCORE_BOUND (include/kschedgpu.h)."""
+    import ctypes as C
+
+    lib = abi.load_library()
+    for w_pref, ok in (((1 << 30) // 10 - 30, True), ((1 << 30) // 10, False), ((1 << 31) - 1, False)):
+        cfg = factory.create_from_config({"priorities": [
+            {"name": f"BoundPref{w_pref}", "weight": w_pref, "argument": {"labelPreference": {"label": "rack"}}},
+            {"name": "LeastRequestedPriority", "weight": 1}, {"name": "ServiceSpreadingPriority", "weight": 1}]}
+        ).compile(lambda k: 0)
+        if ok:
+            continue  # a valid config goes on to create a HIP stream: GPU tests cover it
+        ctx = C.c_void_p()
+        assert lib.ksg_create(C.byref(cfg), 0, C.byref(ctx)) == abi.KSG_ERR_ARG
+        assert not ctx.value

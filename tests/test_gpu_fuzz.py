@@ -16,6 +16,7 @@ from kubernetes_amd import factory, ingest, workload
 from kubernetes_amd.api import Quantity
 from kubernetes_amd.engine import DeviceScheduler
 from oracle.pyoracle import OracleScheduler
+from tests.families import FAMILIES, FamilyCase
 
 pytestmark = pytest.mark.gpu
 
@@ -90,4 +91,28 @@ def test_fuzz_windows_match_oracle(seed):
         assert sg == sw, (desc, window)
         gc, gm = dev.read_requested()
         assert np.array_equal(gc, wc) and np.array_equal(gm, wm), (desc, window)
+        dev.close()
+
+
+# ---- input families the BASELINE configs never produce (tests/families.py) ----------
+@pytest.mark.parametrize("family", FAMILIES)
+def test_family_windows_match_oracle(family):
+    case = FamilyCase(family, 700, 500)
+    orc = case.load(OracleScheduler(case.cfg))
+    want, sw = orc.batch(case.batch, 777)
+    wc, wm = orc.read_requested()
+    assert (want >= 0).sum() > len(want) // 2
+    for window in (0, 5, 64, 128):
+        dev = case.load(DeviceScheduler(case.cfg, device=0))
+        dev.set_window(window)
+        got, sg = dev.batch(case.batch, 777)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, f"{family} window {window}: first mismatches at {bad[:6]}: {got[bad[:6]]} vs {want[bad[:6]]}"
+        assert sg == sw, (family, window)
+        gc, gm = dev.read_requested()
+        assert np.array_equal(gc, wc) and np.array_equal(gm, wm), (family, window)
+        if family == "negative" and window:
+            # negative LeastRequested / ServiceSpreading weights break the window path's
+            # monotonicity: every batch must have taken the exact kernel
+            assert dev.last_batch_stats()["windows"] == 0
         dev.close()

@@ -66,3 +66,40 @@ def test_no_minions():
     with pytest.raises(NoMinionsError):
         g.schedule(Pod(), FakeMinionLister([]))
     g.close()
+
+
+def test_unnamed_pods_relist_keeps_device_equal_to_lister():
+    """Fake listers hold unnamed pods (key "/"), as the reference's test tables do. Every
+    Schedule re-lists them (MapPodsToMachines, predicates.go:354-375): the device's
+    requested totals must equal the lister's pods' sums after each call, however many
+    unnamed pods share a key and whatever the scheduler committed in between."""
+    import numpy as np
+
+    from kubernetes_amd import factory
+    from kubernetes_amd.api import Container, ObjectMeta, Pod, PodSpec, ResourceList, ResourceRequirements, make_node
+    from kubernetes_amd.resource import Quantity
+
+    def pod(cpu, host=""):
+        return Pod(metadata=ObjectMeta(),
+                   spec=PodSpec(containers=[Container(resources=ResourceRequirements(ResourceList(
+                       cpu=Quantity.from_milli(cpu), memory=Quantity.from_int(cpu << 20))))]),
+                   status=PodStatus(host=host))
+
+    nodes = [make_node(f"m{i}", 10000, 10 << 30) for i in range(4)]
+    lister = FakePodLister([pod(100, "m0"), pod(200, "m0"), pod(300, "m1"), pod(400, "gone")])
+    g = GPUScheduler(factory.create_from_provider(), lister, FakeServiceLister([]), SplitMix64Rand(5))
+    minions = FakeMinionLister(nodes)
+    try:
+        for step in range(6):
+            host = g.schedule(pod(50 + step), minions)
+            if step % 2:  # the scheduler's commit reported back (AssumePod), unnamed too
+                lister.pods.append(pod(50 + step, host))
+            g._sync(nodes)  # what the next Schedule call sees
+            want = np.zeros(len(nodes), np.int64)
+            for p in lister.pods:
+                if p.status.host in {n.metadata.name for n in nodes}:
+                    want[int(p.status.host[1:])] += p.spec.containers[0].resources.limits.cpu().milli_value()
+            got_c, _ = g.engine.read_requested()
+            assert np.array_equal(got_c, want), (step, got_c, want)
+    finally:
+        g.close()

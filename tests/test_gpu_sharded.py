@@ -38,16 +38,28 @@ class _Fuzz:
 
 
 def _make_case(name, nn, npods):
+    from tests.families import FamilyCase
     from tests.helpers import Case
 
+    if name.startswith("fam:"):
+        return FamilyCase(name[4:], nn, npods)
     return _Fuzz(nn) if name == "fuzz" else Case(name, nn, npods)
+
+
+def _run_case(sched, case, seed, chunk=None):
+    """run_batch, after the case's existing pods for a tests/families.py case."""
+    from tests.helpers import run_batch
+
+    if hasattr(case, "load"):
+        case.load(sched)
+        return sched.batch(case.batch, seed)
+    return run_batch(sched, case, rng=seed, chunk=chunk)
 
 
 def _worker(rank, world, port, name, nn, npods, window, chunk, seed, q):
     import torch.distributed as dist
 
     from kubernetes_amd.engine import DeviceScheduler, gloo_allgather
-    from tests.helpers import run_batch
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -56,7 +68,7 @@ def _worker(rank, world, port, name, nn, npods, window, chunk, seed, q):
         case = _make_case(name, nn, npods)
         dev = DeviceScheduler(case.cfg, device=0, rank=rank, world=world, allgather=gloo_allgather())
         dev.set_window(window)
-        out, rng = run_batch(dev, case, rng=seed, chunk=chunk)
+        out, rng = _run_case(dev, case, seed, chunk)
         used_c, used_m = dev.read_requested()
         lo, hi = dev.shard()
         stats = dev.last_batch_stats()
@@ -97,11 +109,10 @@ def _run(name, nn, npods, window, world=2, chunk=None, seed=1234):
 
 def _oracle(name, nn, npods, seed=1234):
     from oracle.pyoracle import OracleScheduler
-    from tests.helpers import run_batch
 
     case = _make_case(name, nn, npods)
     orc = OracleScheduler(case.cfg)
-    want, st = run_batch(orc, case, rng=seed)
+    want, st = _run_case(orc, case, seed)
     wc, wm = orc.read_requested()
     return want, st, wc, wm
 
@@ -115,7 +126,8 @@ def _oracle(name, nn, npods, seed=1234):
     ("config4", 900, 500, 128, 2, None),     # ServiceAntiAffinity: per-pod path + domain all-reduce
     ("config1", 500, 1000, 128, 2, None),    # BASELINE config 1
     ("config3", 15000, 50000, 128, 2, 1000), # BASELINE config 3 at full size, 1000-pod batches
-])
+] + [(f"fam:{f}", 700, 400, 64, 2, None) for f in ("multi_service", "namespaces", "negative", "big_weights",
+                                                   "existing_hosts", "invalid_selectors")])
 def test_sharded_batch_matches_oracle(name, nn, npods, window, world, chunk):
     want, st, wc, wm = _oracle(name, nn, npods)
     res = _run(name, nn, npods, window, world=world, chunk=chunk)

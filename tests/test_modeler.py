@@ -333,3 +333,41 @@ def test_store_events_follow_mutation_order_across_threads():
     for t in ts:
         t.join()
     assert {k: id(v) for k, v in replay.items()} == {k: id(st.get_by_key(k)[0]) for k in st.list_keys()}
+
+
+def test_reload_races_a_reflector_thread():
+    """A reflector thread adding pods while reload() snapshots the stores: each pod is
+    on the device exactly once afterwards (either in the snapshot or queued after it)."""
+    import threading
+
+    q, s = StoreToPodLister(), StoreToPodLister()
+    m = SimpleModeler(q, s)
+    sink = _RecordingSink()
+    hosts = lambda p: hash(p.status.host) & 0xFFFF  # noqa: E731
+    uids = iter(range(1, 10 ** 9))
+    mir = PodMirror(m, sink, lambda p, uid: (hosts(p), (uid, p)), lambda: next(uids))
+    rng = random.Random(3)
+    for i in range(50):
+        s.store.add(_pod(rng, f"p{i}", "h1"))
+    mir.sync()
+    stop = threading.Event()
+
+    def reflector():
+        j = 0
+        while not stop.is_set() and j < 3000:
+            s.store.add(_pod(random.Random(j), f"r{j % 400}", f"h{j % 3}"))
+            j += 1
+
+    t = threading.Thread(target=reflector)
+    t.start()
+    try:
+        for _ in range(30):
+            sink.live.clear()
+            mir.reload()
+            mir.sync()
+    finally:
+        stop.set()
+        t.join()
+    mir.sync()
+    assert _mirror_state(sink) == _modeler_state(m, hosts)
+    assert len(sink.live) == len(m.list_pods())

@@ -17,6 +17,8 @@ from kubernetes_amd.api import Pod, PodStatus
 from kubernetes_amd.scheduler import SplitMix64Rand
 from oracle import ref_model as R
 from oracle.pyoracle import OracleScheduler
+from tests import families
+from tests.families import FAMILIES
 from tests.helpers import Case
 
 
@@ -144,3 +146,17 @@ def test_faithful_vs_incremental(name, nn, npods):
     assert np.array_equal(oa, ob) and sa == sb
     ra, rb = a.read_requested(), b.read_requested()
     assert all(np.array_equal(x, y) for x, y in zip(ra, rb))
+
+
+@pytest.mark.parametrize("family", FAMILIES)
+def test_families_ref_model_vs_c_oracle(family):
+    """tests/families.py: overlapping services, two namespaces, negative and large
+    weights, pre-existing pods on "" / unknown hosts, invalid ServiceAffinity values."""
+    w = families.build(family, 40, 110)
+    want, st_w = _ref_sequence(w, 31)
+    for faithful in (True, False):
+        got, st_g = _c_sequence(w, 31, faithful)
+        bad = [i for i in range(len(want)) if want[i] != got[i]]
+        assert not bad, f"faithful={faithful} first mismatches {[(i, want[i], got[i]) for i in bad[:5]]}"
+        assert st_g == st_w
+    assert sum(k == "ok" for k, _ in want) > len(want) // 2
