@@ -298,6 +298,44 @@ int ksg_shard(ksg_ctx* ctx, uint32_t* lo, uint32_t* hi);
  * the node) back to the host, for state checks. */
 int ksg_read_requested(ksg_ctx* ctx, int64_t* milli_cpu, int64_t* memory);
 
+/* ---- kubelet admission -------------------------------
+ * The node agent re-checks its own pods with the scheduler's predicates
+ * (handleNotFittingPods, pkg/kubelet/kubelet.go:1716-1771):
+ *   checkNodeSelectorMatching -> PodMatchesNodeLabels          predicates.go:161-167
+ *   checkCapacityExceeded     -> CheckPodsExceedingCapacity on
+ *                                the pods sorted by creation    predicates.go:104-124
+ * These entry points check many nodes' admission sets in one device pass. They
+ * use only the context's device and stream (no ksg_set_cluster needed) and do
+ * not touch its scheduling state. The caller orders each set's pods (creation
+ * order for the capacity check) and interns node label pairs and nodeSelector
+ * pairs in one id space (0 = a pair no node has). */
+typedef struct ksg_admission_set {
+  int64_t cap_milli_cpu;  /* CapacityFromMachineInfo (kubelet/util.go:48-58): NumCores*1000 */
+  int64_t cap_memory;     /* ... MemoryCapacity (bytes); 0 = unlimited, as in the reference */
+  uint32_t pod_off, n_pods;     /* this set's pods: pods[pod_off, pod_off + n_pods)   */
+  uint32_t label_off, n_labels; /* the node's label pair ids: pairs[label_off, ...)   */
+} ksg_admission_set;
+
+#define KSG_ADMIT_OK 0
+#define KSG_ADMIT_NODESELECTOR 1  /* "nodeSelectorMismatching" (kubelet.go:1757-1763) */
+#define KSG_ADMIT_CAPACITY 2      /* "capacityExceeded" (kubelet.go:1765-1770)        */
+
+/* CheckPodsExceedingCapacity per set, greedy in the given order: fits[i] = 1
+ * (fitting) or 0 (notFitting); only fitting pods accumulate. */
+int ksg_check_pods_exceeding_capacity(ksg_ctx* ctx, const ksg_admission_set* sets, uint32_t n_sets,
+                                      const ksg_pod* pods, uint32_t n_pods, uint8_t* fits);
+/* PodMatchesNodeLabels: matches[i] = 1 iff every nodeSelector pair of pod i
+ * (ids[sel_off, sel_off + n_sel)) is one of its set's node label pairs. */
+int ksg_pod_matches_node_labels(ksg_ctx* ctx, const ksg_admission_set* sets, uint32_t n_sets,
+                                const ksg_pod* pods, uint32_t n_pods, const uint32_t* ids, uint32_t n_ids,
+                                const uint32_t* pairs, uint32_t n_pairs, uint8_t* matches);
+/* Both, in the kubelet's order: codes[i] = KSG_ADMIT_NODESELECTOR for a pod
+ * whose selector does not match, else the capacity check over the matching pods
+ * only (KSG_ADMIT_CAPACITY or KSG_ADMIT_OK). */
+int ksg_admit_pods(ksg_ctx* ctx, const ksg_admission_set* sets, uint32_t n_sets, const ksg_pod* pods,
+                   uint32_t n_pods, const uint32_t* ids, uint32_t n_ids, const uint32_t* pairs, uint32_t n_pairs,
+                   uint8_t* codes);
+
 #ifdef __cplusplus
 }
 #endif

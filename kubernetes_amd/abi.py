@@ -114,6 +114,16 @@ class KsgPod(C.Structure):
     ]
 
 
+class KsgAdmissionSet(C.Structure):
+    _fields_ = [("cap_milli_cpu", I64), ("cap_memory", I64), ("pod_off", U32), ("n_pods", U32),
+                ("label_off", U32), ("n_labels", U32)]
+
+
+ADMIT_OK = 0
+ADMIT_NODESELECTOR = 1
+ADMIT_CAPACITY = 2
+
+
 class KsgShardRecord(C.Structure):
     _fields_ = [("max_score", I64), ("tie_count", U64), ("error", I32), ("pad", I32), ("pad2", U64)]
 
@@ -142,6 +152,10 @@ POD_DTYPE = np.dtype(
     ],
     align=True,
 )
+ADMISSION_SET_DTYPE = np.dtype(
+    [("cap_milli_cpu", "<i8"), ("cap_memory", "<i8"), ("pod_off", "<u4"), ("n_pods", "<u4"),
+     ("label_off", "<u4"), ("n_labels", "<u4")], align=True)
+assert ADMISSION_SET_DTYPE.itemsize == C.sizeof(KsgAdmissionSet)
 assert NODE_DTYPE.itemsize == C.sizeof(KsgNode)
 assert POD_DTYPE.itemsize == C.sizeof(KsgPod)
 
@@ -168,6 +182,9 @@ EXPORTS = [
     "ksg_shard_range",
     "ksg_merge_records",
     "ksg_set_allgather",
+    "ksg_check_pods_exceeding_capacity",
+    "ksg_pod_matches_node_labels",
+    "ksg_admit_pods",
 ]
 
 # int (*ksg_allgather_fn)(void* user, const void* send, void* recv, uint64_t bytes)
@@ -220,6 +237,9 @@ def load_library() -> C.CDLL:
         "ksg_shard_range": (C.c_int, [U32, C.c_int, C.c_int, P(U32), P(U32)]),
         "ksg_merge_records": (C.c_int, [vp, U32, U32, U32, C.c_int, P(U64), U64, P(I32), P(I64), P(U64)]),
         "ksg_set_allgather": (C.c_int, [vp, ALLGATHER_FN, vp]),
+        "ksg_check_pods_exceeding_capacity": (C.c_int, [vp, vp, U32, vp, U32, vp]),
+        "ksg_pod_matches_node_labels": (C.c_int, [vp, vp, U32, vp, U32, vp, U32, vp, U32, vp]),
+        "ksg_admit_pods": (C.c_int, [vp, vp, U32, vp, U32, vp, U32, vp, U32, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)

@@ -50,6 +50,7 @@ class ObjectMeta:
     name: str = ""
     namespace: str = ""
     labels: Optional[Dict[str, str]] = None
+    creation_timestamp: float = 0.0  # seconds; the kubelet's admission order (kubelet.go:1692-1694)
 
 
 @dataclass

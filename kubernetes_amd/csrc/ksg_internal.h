@@ -162,6 +162,10 @@ struct KsgWinRun {
 typedef ksg_shard_record KsgRecordHdr;  // public layout (include/kschedgpu.h)
 // followed by nwords_max uint64 tie words (bit set = node at max_score)
 
+// ksg_admit_kernel modes (ksg_admit.hip)
+#define KSG_ADMIT_MODE_CAPACITY 1
+#define KSG_ADMIT_MODE_SELECTOR 2
+
 struct KsgPatch {
   uint64_t addr;   // device address
   uint64_t value;

@@ -55,6 +55,8 @@ hipError_t ksg_launch_static(const KsgStaticCfg& sc, uint32_t n_nodes, const ksg
                              uint64_t* static_fit, int32_t* static_score, int32_t* anti_domain,
                              int32_t* aff_pair, unsigned long long* pairmap, hipStream_t st);
 hipError_t ksg_launch_patch(const KsgPatch* patches, uint32_t n, hipStream_t st);
+hipError_t ksg_launch_admit(const ksg_admission_set* sets, uint32_t n_sets, const ksg_pod* pods,
+                            const uint32_t* ids, const uint32_t* pairs, int mode, uint8_t* out, hipStream_t st);
 
 namespace {
 
@@ -121,6 +123,8 @@ struct ksg_ctx {
   int64_t* d_summary = nullptr;
   KsgPatch* d_patch = nullptr;
   size_t patch_cap = 0;
+  uint8_t* d_admit = nullptr;  // kubelet admission: sets, pods, ids, pairs, codes (one buffer)
+  size_t admit_cap = 0;
   std::vector<KsgPatch> patches;
 
   // host mirror
@@ -693,7 +697,7 @@ int ksg_destroy(ksg_ctx* c) {
   free_cluster(c);
   void* scratch[] = {c->d_pods, c->d_ids, c->d_fail, c->d_score, c->d_rec_send, c->d_rec_recv, c->d_dpart,
                      c->d_dglobal, c->d_out, c->d_rng, c->d_summary, c->d_patch, c->d_shard_wlo,
-                     c->d_winsum, c->d_xsend, c->d_xrecv, c->d_run, c->d_dcnt};
+                     c->d_winsum, c->d_xsend, c->d_xrecv, c->d_run, c->d_dcnt, c->d_admit};
   for (void* p : scratch)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -1372,6 +1376,78 @@ int ksg_read_requested(ksg_ctx* c, int64_t* milli_cpu, int64_t* memory) {
   }
   HIPCHK(c, hipStreamSynchronize(c->st));
   return KSG_OK;
+}
+
+// ---- kubelet admission (ksg_admit.hip) ------------------------------------
+static int admit_impl(ksg_ctx* c, int mode, const ksg_admission_set* sets, uint32_t n_sets, const ksg_pod* pods,
+                      uint32_t n_pods, const uint32_t* ids, uint32_t n_ids, const uint32_t* pairs, uint32_t n_pairs,
+                      uint8_t* out) {
+  if (!c || (n_sets && !sets) || (n_pods && (!pods || !out))) return KSG_ERR_ARG;
+  KSG_LOCK(c);
+  for (uint32_t s = 0; s < n_sets; ++s) {
+    if ((uint64_t)sets[s].pod_off + sets[s].n_pods > n_pods)
+      return fail(c, KSG_ERR_ARG, "admission set %u: pods out of range", s);
+    if ((mode & KSG_ADMIT_MODE_SELECTOR) && (uint64_t)sets[s].label_off + sets[s].n_labels > n_pairs)
+      return fail(c, KSG_ERR_ARG, "admission set %u: labels out of range", s);
+  }
+  if (mode & KSG_ADMIT_MODE_SELECTOR)
+    for (uint32_t i = 0; i < n_pods; ++i)
+      if ((uint64_t)pods[i].sel_off + pods[i].n_sel > n_ids)
+        return fail(c, KSG_ERR_ARG, "pod %u: nodeSelector ids out of range", i);
+  for (uint32_t i = 0; i < n_pods; ++i) out[i] = KSG_ADMIT_OK;  // pods in no set
+  if (n_sets == 0 || n_pods == 0) return KSG_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  const bool sel = (mode & KSG_ADMIT_MODE_SELECTOR) != 0;
+  const size_t b_sets = (size_t)n_sets * sizeof(ksg_admission_set), b_pods = (size_t)n_pods * sizeof(ksg_pod);
+  const size_t b_ids = sel ? (size_t)n_ids * 4 : 0, b_pairs = sel ? (size_t)n_pairs * 4 : 0;
+  const size_t o_pods = (b_sets + 15) & ~(size_t)15, o_ids = o_pods + ((b_pods + 15) & ~(size_t)15);
+  const size_t o_pairs = o_ids + ((b_ids + 15) & ~(size_t)15), o_out = o_pairs + ((b_pairs + 15) & ~(size_t)15);
+  const size_t total = o_out + n_pods;
+  int rc;
+  if ((rc = grow(c, (void**)&c->d_admit, &c->admit_cap, total, 1))) return rc;
+  if ((rc = grow_host(c, &c->h_up, &c->h_up_cap, o_out))) return rc;
+  memcpy(c->h_up, sets, b_sets);
+  memcpy(c->h_up + o_pods, pods, b_pods);
+  if (b_ids) memcpy(c->h_up + o_ids, ids, b_ids);
+  if (b_pairs) memcpy(c->h_up + o_pairs, pairs, b_pairs);
+  HIPCHK(c, hipMemcpyAsync(c->d_admit, c->h_up, o_out, hipMemcpyHostToDevice, c->st));
+  HIPCHK(c, ksg_launch_admit(reinterpret_cast<const ksg_admission_set*>(c->d_admit), n_sets,
+                             reinterpret_cast<const ksg_pod*>(c->d_admit + o_pods),
+                             reinterpret_cast<const uint32_t*>(c->d_admit + o_ids),
+                             reinterpret_cast<const uint32_t*>(c->d_admit + o_pairs), mode, c->d_admit + o_out, c->st));
+  if ((rc = grow_host(c, &c->h_dn, &c->h_dn_cap, n_pods))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->h_dn, c->d_admit + o_out, n_pods, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  // pods outside every set keep KSG_ADMIT_OK; the kernel wrote the others
+  std::vector<uint8_t> in_set(n_pods, 0);
+  for (uint32_t s = 0; s < n_sets; ++s) memset(in_set.data() + sets[s].pod_off, 1, sets[s].n_pods);
+  for (uint32_t i = 0; i < n_pods; ++i)
+    if (in_set[i]) out[i] = c->h_dn[i];
+  return KSG_OK;
+}
+
+int ksg_check_pods_exceeding_capacity(ksg_ctx* c, const ksg_admission_set* sets, uint32_t n_sets,
+                                      const ksg_pod* pods, uint32_t n_pods, uint8_t* fits) {
+  const int rc = admit_impl(c, KSG_ADMIT_MODE_CAPACITY, sets, n_sets, pods, n_pods, nullptr, 0, nullptr, 0, fits);
+  if (rc == KSG_OK)
+    for (uint32_t i = 0; i < n_pods; ++i) fits[i] = fits[i] == KSG_ADMIT_OK;
+  return rc;
+}
+
+int ksg_pod_matches_node_labels(ksg_ctx* c, const ksg_admission_set* sets, uint32_t n_sets, const ksg_pod* pods,
+                                uint32_t n_pods, const uint32_t* ids, uint32_t n_ids, const uint32_t* pairs,
+                                uint32_t n_pairs, uint8_t* matches) {
+  const int rc = admit_impl(c, KSG_ADMIT_MODE_SELECTOR, sets, n_sets, pods, n_pods, ids, n_ids, pairs, n_pairs,
+                            matches);
+  if (rc == KSG_OK)
+    for (uint32_t i = 0; i < n_pods; ++i) matches[i] = matches[i] == KSG_ADMIT_OK;
+  return rc;
+}
+
+int ksg_admit_pods(ksg_ctx* c, const ksg_admission_set* sets, uint32_t n_sets, const ksg_pod* pods, uint32_t n_pods,
+                   const uint32_t* ids, uint32_t n_ids, const uint32_t* pairs, uint32_t n_pairs, uint8_t* codes) {
+  return admit_impl(c, KSG_ADMIT_MODE_SELECTOR | KSG_ADMIT_MODE_CAPACITY, sets, n_sets, pods, n_pods, ids, n_ids,
+                    pairs, n_pairs, codes);
 }
 
 }  // extern "C"

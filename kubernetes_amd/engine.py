@@ -231,6 +231,29 @@ class DeviceScheduler:
         self._lib.ksg_shard(self._ctx, C.byref(lo), C.byref(hi))
         return lo.value, hi.value
 
+    def admit(self, sets: np.ndarray, batch: PodBatch, pairs, mode: int = 3) -> np.ndarray:
+        """Kubelet admission over many nodes' sets (ksg_admit.hip). mode 1:
+        ksg_check_pods_exceeding_capacity (1 = fitting), 2: ksg_pod_matches_node_labels
+        (1 = matches), 3: ksg_admit_pods (KSG_ADMIT_* codes)."""
+        sets = np.ascontiguousarray(sets, dtype=abi.ADMISSION_SET_DTYPE)
+        pods = np.ascontiguousarray(batch.pods, dtype=abi.POD_DTYPE)
+        ids = _u32(batch.ids if len(batch.ids) else np.zeros(1, np.uint32))
+        prs = _u32(pairs if len(pairs) else np.zeros(1, np.uint32))
+        out = np.zeros(max(len(pods), 1), np.uint8)
+        if mode == 1:
+            rc = self._lib.ksg_check_pods_exceeding_capacity(self._ctx, abi.ptr(sets), len(sets), abi.ptr(pods),
+                                                             len(pods), abi.ptr(out))
+        elif mode == 2:
+            rc = self._lib.ksg_pod_matches_node_labels(self._ctx, abi.ptr(sets), len(sets), abi.ptr(pods), len(pods),
+                                                       abi.ptr(ids), len(batch.ids), abi.ptr(prs), len(pairs),
+                                                       abi.ptr(out))
+        else:
+            rc = self._lib.ksg_admit_pods(self._ctx, abi.ptr(sets), len(sets), abi.ptr(pods), len(pods), abi.ptr(ids),
+                                          len(batch.ids), abi.ptr(prs), len(pairs), abi.ptr(out))
+        if rc != abi.KSG_OK:
+            self._err(rc)
+        return out[: len(pods)]
+
     def read_requested(self):
         c = np.zeros(max(self.n_nodes, 1), np.int64)
         m = np.zeros(max(self.n_nodes, 1), np.int64)

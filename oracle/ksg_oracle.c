@@ -825,3 +825,44 @@ void orc_read_requested(orc *o, int64_t *c, int64_t *m) {
   if (c) memcpy(c, o->used_c, (size_t)o->N * 8);
   if (m) memcpy(m, o->used_m, (size_t)o->N * 8);
 }
+
+/* ====================================================== kubelet admission */
+/* handleNotFittingPods' scheduler checks (pkg/kubelet/kubelet.go:1716-1771) over
+ * the ksg_admission_set layout: PodMatchesNodeLabels (predicates.go:161-167),
+ * then CheckPodsExceedingCapacity (predicates.go:104-124) greedily in the given
+ * order over the pods that matched. mode bit 1: capacity, bit 2: selector. */
+void orc_admit_pods(const ksg_admission_set *sets, uint32_t n_sets, const ksg_pod *pods, uint32_t n_pods,
+                    const uint32_t *ids, const uint32_t *pairs, int mode, uint8_t *out) {
+  for (uint32_t i = 0; i < n_pods; ++i) out[i] = KSG_ADMIT_OK;
+  for (uint32_t s = 0; s < n_sets; ++s) {
+    const ksg_admission_set *st = &sets[s];
+    int64_t totalC = st->cap_milli_cpu, totalM = st->cap_memory, reqC = 0, reqM = 0;
+    for (uint32_t i = st->pod_off; i < st->pod_off + st->n_pods; ++i) {
+      const ksg_pod *p = &pods[i];
+      uint8_t code = KSG_ADMIT_OK;
+      if (mode & 2) {
+        for (uint32_t k = 0; k < p->n_sel; ++k) {
+          uint32_t want = ids[p->sel_off + k];
+          int found = 0;
+          for (uint32_t l = 0; l < st->n_labels; ++l)
+            if (want != 0 && pairs[st->label_off + l] == want) found = 1;
+          if (!found) {
+            code = KSG_ADMIT_NODESELECTOR;
+            break;
+          }
+        }
+      }
+      if ((mode & 1) && code == KSG_ADMIT_OK) {
+        int fitsC = totalC == 0 || (int64_t)((uint64_t)totalC - (uint64_t)reqC) >= p->milli_cpu;
+        int fitsM = totalM == 0 || (int64_t)((uint64_t)totalM - (uint64_t)reqM) >= p->memory;
+        if (fitsC && fitsM) {
+          reqC = (int64_t)((uint64_t)reqC + (uint64_t)p->milli_cpu);
+          reqM = (int64_t)((uint64_t)reqM + (uint64_t)p->memory);
+        } else {
+          code = KSG_ADMIT_CAPACITY;
+        }
+      }
+      out[i] = code;
+    }
+  }
+}

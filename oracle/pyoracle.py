@@ -45,6 +45,7 @@ def load():
         "orc_schedule_commit": (C.c_int, [vp, C.c_uint32, P(C.c_int32)]),
         "orc_schedule_batch": (C.c_int, [vp, vp, C.c_uint32, vp, C.c_uint32, P(C.c_uint64), vp]),
         "orc_read_requested": (None, [vp, vp, vp]),
+        "orc_admit_pods": (None, [vp, C.c_uint32, vp, C.c_uint32, vp, vp, C.c_int, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -140,3 +141,15 @@ class OracleScheduler:
         m = np.zeros(max(self.n_nodes, 1), np.int64)
         self._lib.orc_read_requested(self._o, abi.ptr(c), abi.ptr(m))
         return c[: self.n_nodes], m[: self.n_nodes]
+
+
+def admit_pods(sets, batch: PodBatch, pairs, mode: int = 3):
+    """C restatement of the kubelet's admission checks (orc_admit_pods):
+    mode 1 capacity, 2 nodeSelector, 3 both in the kubelet's order -> codes."""
+    lib = load()
+    sets = np.ascontiguousarray(sets, dtype=abi.ADMISSION_SET_DTYPE)
+    pods = np.ascontiguousarray(batch.pods, dtype=abi.POD_DTYPE)
+    out = np.zeros(max(len(pods), 1), np.uint8)
+    lib.orc_admit_pods(abi.ptr(sets), len(sets), abi.ptr(pods), len(pods), abi.ptr(_u32(batch.ids)),
+                       abi.ptr(_u32(pairs)), int(mode), abi.ptr(out))
+    return out[: len(pods)]

@@ -463,6 +463,26 @@ def modeler():
     ]}
 
 
+def kubelet():
+    """pkg/kubelet/kubelet_test.go TestHandleNodeSelector (:2929-2976) and TestHandleMemExceeded
+    (:2979-3032): handleNotFittingPods (kubelet.go:1745-1771) marks the not-fitting pod failed.
+    machine = cadvisor MachineInfo (CapacityFromMachineInfo, kubelet/util.go:48-58); created =
+    CreationTimestamp order key (seconds); rejected = the pods whose status becomes PodFailed."""
+    mem90 = [ctr(memory="90")]
+    return {"source": "pkg/kubelet/kubelet_test.go:2929-3032", "cases": [
+        {"test": "TestHandleNodeSelector", "machine": {"num_cores": 0, "memory_capacity": 0},
+         "node_labels": {"key": "B"},
+         "pods": [dict(pod("podA", "foo", node_selector={"key": "A"}), created=0),
+                  dict(pod("podB", "foo", node_selector={"key": "B"}), created=0)],
+         "rejected": {"foo/podA": "nodeSelectorMismatching"}},
+        {"test": "TestHandleMemExceeded", "machine": {"num_cores": 0, "memory_capacity": 100},
+         "node_labels": None,
+         "pods": [dict(pod("newpod", "foo", containers=mem90), created=1),
+                  dict(pod("oldpod", "foo", containers=mem90), created=0)],
+         "rejected": {"foo/newpod": "capacityExceeded"}},
+    ]}
+
+
 def main():
     out = {
         "source": "smarterclayton/kubernetes v0.13.0-dev, pkg/scheduler/*_test.go (tables restated as data)",
@@ -491,6 +511,9 @@ def main():
         f.write("\n")
     with open(os.path.join(HERE, "modeler_golden.json"), "w") as f:
         json.dump(modeler(), f, indent=1, sort_keys=True)
+        f.write("\n")
+    with open(os.path.join(HERE, "kubelet_golden.json"), "w") as f:
+        json.dump(kubelet(), f, indent=1, sort_keys=True)
         f.write("\n")
     with open(os.path.join(HERE, "quantity_golden.json"), "w") as f:
         json.dump({"source": "pkg/api/resource/quantity_test.go", **quantity()}, f, indent=1, sort_keys=True)

@@ -46,7 +46,7 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
 
 
 STRUCTS = (("ksg_config", abi.KsgConfig), ("ksg_node", abi.KsgNode), ("ksg_pod", abi.KsgPod),
-           ("ksg_shard_record", abi.KsgShardRecord))
+           ("ksg_shard_record", abi.KsgShardRecord), ("ksg_admission_set", abi.KsgAdmissionSet))
 
 _LAYOUT_C = r"""
 #include <stdio.h>
@@ -54,8 +54,8 @@ _LAYOUT_C = r"""
 #include "kschedgpu.h"
 #define P(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
 int main(void) {
-  printf("ksg_config %zu\nksg_node %zu\nksg_pod %zu\nksg_shard_record %zu\n", sizeof(ksg_config),
-         sizeof(ksg_node), sizeof(ksg_pod), sizeof(ksg_shard_record));
+  printf("ksg_config %zu\nksg_node %zu\nksg_pod %zu\nksg_shard_record %zu\nksg_admission_set %zu\n",
+         sizeof(ksg_config), sizeof(ksg_node), sizeof(ksg_pod), sizeof(ksg_shard_record), sizeof(ksg_admission_set));
   %FIELDS%
   return 0;
 }

@@ -182,12 +182,17 @@ def test_config5_100k_nodes_matches_oracle(window):
     dev.close()
 
 
-def test_config3_full_size_matches_oracle():
-    """BASELINE config 3 at full size on one GPU: 15,000 nodes, 50,000 pods in
-    1,000-pod batches (as bench.py steps), every decision, the RNG position and
-    the committed totals against the oracle; plus the size-independent checksum
-    requested totals == the sum of the placed pods' requests."""
-    case = Case("config3", 15000, 50000)
+@pytest.mark.parametrize("name,nn,npods", [
+    ("config2", 5000, 10000),    # BASELINE config 2 at its stated size
+    ("config3", 15000, 50000),   # BASELINE config 3 (one GPU)
+    ("config4", 5000, 10000),    # BASELINE config 4 (ServiceAffinity + ServiceAntiAffinity)
+])
+def test_full_size_matches_oracle(name, nn, npods):
+    """A BASELINE config at its stated size on one GPU, in 1,000-pod batches (as
+    bench.py steps): every decision, the RNG position and the committed totals
+    against the incremental oracle; plus the size-independent checksum requested
+    totals == the sum of the placed pods' requests."""
+    case = Case(name, nn, npods)
     dev, orc = _pair(case)
     got, sg = run_batch(dev, case, chunk=1000)
     want, sw = run_batch(orc, case, chunk=1000)
@@ -203,6 +208,21 @@ def test_config3_full_size_matches_oracle():
     assert np.array_equal(sc, gc)
     assert dev.last_batch_stats()["windows"] > 0
     dev.close()
+
+
+def test_config2_prefix_matches_faithful_restatement():
+    """bench.py's cpu_baseline check as a test: the reference's own cost structure
+    (faithful mode: per-pod MapPodsToMachines regroup, greedy CheckPodsExceedingCapacity,
+    HostPriorityList sort) on the first 6,000 pods of BASELINE config 2 makes the same
+    decisions as the GPU, from an empty cluster, with the same tie-break stream."""
+    case = Case("config2", 5000, 6000)
+    dev = DeviceScheduler(case.cfg, device=0)
+    got, sg = run_batch(dev, case, chunk=1000)
+    dev.close()
+    orc = OracleScheduler(case.cfg, faithful=True)
+    want, sw = run_batch(orc, case)
+    orc.close()
+    assert np.array_equal(got, want) and sg == sw
 
 
 def test_config5_full_size_window_equals_exact_path():
