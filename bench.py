@@ -242,6 +242,22 @@ def main():
             done_i += len(o)
         inc_s = time.perf_counter() - t_i
         inc.close()
+        # ... and node-sharded over this process's CPU share (OMP_NUM_THREADS: 16 on the
+        # GPU box, whose os.cpu_count() is the whole machine's), SURVEY.md 8(d) "CPU timing" ii
+        nthr = max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+        mt = OracleScheduler(cfg, faithful=False)
+        mt.set_cluster(view.arrays)
+        r = workload.TIEBREAK_SEED
+        done_m = 0
+        mt_out = []
+        t_m = time.perf_counter()
+        while done_m < n_pods and time.perf_counter() - t_m < min(args.cpu_seconds, 5.0):
+            o, r = mt.batch_mt(PodBatch(batch.pods[done_m:done_m + 500], batch.ids), r, nthr)
+            mt_out.append(o)
+            done_m += len(o)
+        mt_s = time.perf_counter() - t_m
+        mt.close()
+        mt_agree = bool(np.array_equal(np.concatenate(mt_out), out[:done_m]))
         cpu = {"value": done / cpu_s, "unit": "pods/s", "cores": 1, "kind": "port",
                "sample": f"first {done} pods of the same {wl} workload on {n_nodes} nodes from an empty cluster "
                          f"({cpu_s:.1f}s, faithful mode: per-pod MapPodsToMachines regroup, per-node predicate "
@@ -249,7 +265,12 @@ def main():
                "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
                "incremental": {"value": done_i / inc_s, "unit": "pods/s", "cores": 1,
                                "sample": f"first {done_i} pods, incremental mode (SoA closed forms, "
-                                         f"no per-pod re-list), {inc_s:.1f}s"}}
+                                         f"no per-pod re-list), {inc_s:.1f}s"},
+               "incremental_nproc": {"value": done_m / mt_s, "unit": "pods/s", "cores": nthr,
+                                     "sample": f"first {done_m} pods, incremental mode, each pod's node loop "
+                                               f"split over {nthr} threads (node-rank shards, two spin barriers "
+                                               f"per pod; ServiceAntiAffinity configs run 1 thread), "
+                                               f"{mt_s:.1f}s; decisions identical to GPU: {mt_agree}"}}
 
     xname = "RCCL" if args.transport == "rccl" else "host-staged gloo"
     line = {

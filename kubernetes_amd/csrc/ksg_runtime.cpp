@@ -680,7 +680,7 @@ int ksg_create_sharded(const ksg_config* cfg, int device, int rank, int world, c
 int ksg_destroy(ksg_ctx* c) {
   if (!c) return KSG_OK;
   if (c->dev.dbgbuf) {  // debug stamps (KSG_DEBUG & 8): cycles/64 per resolver section
-    int32_t h[16];
+    int32_t h[32];
     (void)hipMemcpy(h, c->dev.dbgbuf, sizeof h, hipMemcpyDeviceToHost);
     fprintf(stderr, "ksg stamps (x64 cycles, committer wave): ring-wait %d head %d recheck-last-slot %d "
             "wait-checkers %d select %d commit %d | drop-path pods %d unpredicted commits %d\n",
@@ -688,6 +688,9 @@ int ksg_destroy(ksg_ctx* c) {
     fprintf(stderr, "ksg ring-wait split: first 4 pods of each window %d, later pods %d\n", h[10], h[11]);
     fprintf(stderr, "ksg producers (sum over waves): slot-wait %d loads %d draw-wait %d stage %d\n", h[12], h[13],
             h[14], h[15]);
+    fprintf(stderr, "ksg stamps raw:");
+    for (int q = 0; q < 24; ++q) fprintf(stderr, " %d", h[q]);
+    fprintf(stderr, "\n");
   }
   {
     KSG_LOCK(c);  // waits for a call in flight on another thread

@@ -1457,6 +1457,846 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
 }
 
 // ---------------------------------------------------------------------------
+// phase B, register-slot resolver (every configuration without
+// ServiceAntiAffinity; that one keeps the resolver above)
+// ---------------------------------------------------------------------------
+// The window's committed nodes ("slots", at most 128) are owned by two checker
+// waves, one slot per lane: the node's capacity, snapshot and window delta of
+// the requested totals and 10/capacity live in the owner lane's registers; the
+// conflict keys and service entries the window added live in an LDS table by
+// slot (keys and service ids written by the committer at the commit, the
+// services' snapshot counts by the owner checker).
+//  CHECKERS run a pod ahead of the committer: for pod i they apply commit i-2
+//    (a new slot takes the node's snapshot from the producer's staging when it
+//    is the predicted node, else from L2; the service flags and first peers
+//    later pods stop on are set here) and test pod i against every slot as of
+//    commits <= i-2.
+//  COMMITTER (wave 0) re-checks only the slot commit i-1 went into (its window
+//    delta in registers, its lists from the table, the node's snapshot loaded at
+//    the top of the iteration), adds the checkers' drops (a commit can only
+//    make a node worse, so drops as of i-2 stay drops), selects the ix-th live
+//    tie (the staged prediction when nothing dropped), writes the pod's lists
+//    into the table and publishes the commit record.
+//  PRODUCERS stage pods ahead into the ring. The draw index of pod j is the
+//    number of drawable pods before j, read from two LDS bitmaps every producer
+//    fills as soon as it knows its pod's max score (no producer-to-producer
+//    hand-off chain).
+struct alignas(16) WinCommit {
+  uint32_t kind;   // 0: no commit (error / no fit), 1: commit
+  uint32_t slot;
+  uint32_t node;   // shard offset of the node
+  uint32_t flags;  // bit 0: a new slot, bit 1: the node is the producer's predicted node
+};
+struct alignas(16) WinCtl2 {
+  uint32_t stop;      // the committer is done: pods [0, resolved) are decided
+  uint32_t resolved;
+  uint32_t sel_seq;   // commit records published for pods [0, sel_seq)
+  uint32_t n_peer;    // first service peers recorded in the window (L_peer entries)
+  uint32_t chk_seq[KSG_RES_NCHK];     // pods checker c is done with
+  uint32_t chk_cnt[KSG_RES_NCHK][2];  // checker c's drops for the pod of parity p
+  uint32_t fin[KSG_RES_NCHK];         // checker c applied every commit and wrote its slots back
+  uint32_t hang;                      // a wait exceeded its spin limit (a bug)
+  uint32_t pad[1];
+};
+// per-slot list table: [0, 8) conflict keys, [8, 20) service ids, [20, 32) the
+// services' counts on the node at the snapshot
+#define KSG_CL_KEY 0
+#define KSG_CL_SV 8
+#define KSG_CL_SC 20
+#define KSG_CL_W 32
+
+struct WinLdsOff2 {
+  uint32_t ctl, r_hdr, r_t0, r_rec, r_mod, r_svc;
+  uint32_t cm, out, peer, flag, peerset, drop, pub, drw, clist;
+  uint32_t total;
+};
+
+__host__ __device__ inline WinLdsOff2 win2_lds_offsets(uint32_t P, uint32_t nflag, uint32_t W) {
+  WinLdsOff2 o;
+  const uint32_t R = win_ring(P);
+  uint32_t at = 0;
+  o.ctl = at;     at += win_al16(sizeof(WinCtl2));
+  o.r_hdr = at;   at += win_al16((size_t)R * sizeof(RingHdr));
+  o.r_t0 = at;    at += win_al16((size_t)R * P * 64 * 8);
+  o.r_rec = at;   at += win_al16((size_t)R * KSG_WIN_SUM_DWORDS * 4);
+  o.r_mod = at;   at += win_al16((size_t)R * 64 * 4);
+  o.r_svc = at;   at += win_al16((size_t)R * sizeof(RingSvc));
+  o.cm = at;      at += win_al16((size_t)W * sizeof(WinCommit));
+  o.out = at;     at += win_al16((size_t)W * 4);
+  o.peer = at;    at += win_al16((size_t)W * 2 * 4);
+  o.flag = at;    at += win_al16((size_t)nflag * 4);
+  o.peerset = at; at += win_al16((size_t)nflag * 4);
+  o.drop = at;    at += win_al16((size_t)2 * P * 64 * 8);
+  o.pub = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
+  o.drw = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
+  o.clist = at;   at += win_al16((size_t)KSG_MAX_SLOTS * KSG_CL_W * 4);
+  o.total = at;
+  return o;
+}
+
+// One slot in a checker lane's registers.
+struct RegSlot {
+  uint32_t node;  // shard offset; ~0u: the lane owns no slot yet
+  int64_t cap_c, cap_m, snp_c, snp_m, dl_c, dl_m;
+  double inv_c, inv_m;
+  uint32_t nk, ns, smask;  // list lengths as of the commits this checker applied
+};
+
+template <int P, bool STAMP>
+__global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
+                                                               const KsgWinSum* __restrict__ sums,
+                                                               const KsgWinXchg x, uint64_t* rng_io,
+                                                               int32_t* __restrict__ out_batch) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t pos = run->pos, n_batch = run->n;
+  if (run->halt || pos >= n_batch) return;  // the chain is done (uniform, before any barrier)
+  const uint32_t n_pods = min(wcap, n_batch - pos);
+  int32_t* __restrict__ out = out_batch + pos;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t nflag = (d.n_services + 31) / 32;
+  const uint32_t nshard = d.hi - d.lo;
+  const uint32_t nwords = d.nwords;
+  constexpr uint32_t RING = win_ring(P);
+  constexpr uint32_t NT = 512;
+  constexpr uint32_t NPW = NT / 64 - KSG_RES_P0;  // producer waves
+  constexpr uint32_t DW = KSG_WIN_SUM_DWORDS;
+  const WinLdsOff2 o = win2_lds_offsets(P, nflag, wcap);
+  WinCtl2* ctl = reinterpret_cast<WinCtl2*>(smem + o.ctl);
+  RingHdr* r_hdr = reinterpret_cast<RingHdr*>(smem + o.r_hdr);
+  uint64_t* r_t0 = reinterpret_cast<uint64_t*>(smem + o.r_t0);
+  uint32_t* r_rec = reinterpret_cast<uint32_t*>(smem + o.r_rec);
+  uint32_t* r_mod = reinterpret_cast<uint32_t*>(smem + o.r_mod);
+  RingSvc* r_svc = reinterpret_cast<RingSvc*>(smem + o.r_svc);
+  WinCommit* L_cm = reinterpret_cast<WinCommit*>(smem + o.cm);
+  int32_t* L_out = reinterpret_cast<int32_t*>(smem + o.out);
+  uint32_t* L_peer = reinterpret_cast<uint32_t*>(smem + o.peer);
+  uint32_t* L_flag = reinterpret_cast<uint32_t*>(smem + o.flag);
+  uint32_t* L_peerset = reinterpret_cast<uint32_t*>(smem + o.peerset);
+  uint64_t* L_drop = reinterpret_cast<uint64_t*>(smem + o.drop);  // [2][P*64] by pod parity
+  uint32_t* L_pub = reinterpret_cast<uint32_t*>(smem + o.pub);    // pods whose drawable bit is known
+  uint32_t* L_drw = reinterpret_cast<uint32_t*>(smem + o.drw);    // drawable pods
+  uint32_t* L_cl = reinterpret_cast<uint32_t*>(smem + o.clist);   // [slot][KSG_CL_W]
+  const bool spread_on = d.w_spread != 0;
+  const bool aff_on = (d.preds & KSG_PRED_SERVICEAFFINITY) && d.n_aff > 0;
+  const bool res_on = (d.preds & KSG_PRED_PODFITSRESOURCES) != 0;
+  const bool ports_on = (d.preds & KSG_PRED_PODFITSPORTS) != 0;
+  const bool disk_on = (d.preds & KSG_PRED_NODISKCONFLICT) != 0;
+  const uint32_t nbits = (wcap + 31) / 32;
+
+  for (uint32_t t = tid; t < RING; t += NT) r_hdr[t].ready = 0;
+  if (tid == 0) *ctl = WinCtl2{};
+  for (uint32_t w = tid; w < nflag; w += NT) {
+    L_flag[w] = 0;
+    L_peerset[w] = 0;
+  }
+  for (uint32_t w = tid; w < nbits; w += NT) {
+    L_pub[w] = 0;
+    L_drw[w] = 0;
+  }
+  for (uint32_t w = tid; w < 2 * P * 64u; w += NT) L_drop[w] = 0;
+  __syncthreads();
+  const uint64_t rng0 = *rng_io;
+
+  // =========================================================================
+  // producers
+  // =========================================================================
+  if (wave >= KSG_RES_P0) {
+    if (!(d.dbg & 64)) {  // warm this XCD's L2 with the node state (KSG_DEBUG & 64: skip)
+      const uint32_t pw = wave - KSG_RES_P0, nt = NPW * 64;
+      const uint32_t n16 = (nshard + 1) / 2;
+      uint64_t acc = 0;
+      const int64_t* arr[6] = {d.cap_cpu + d.lo, d.cap_mem + d.lo, d.used_cpu + d.lo, d.used_mem + d.lo,
+                               reinterpret_cast<const int64_t*>(d.inv10_cpu) + d.lo,
+                               reinterpret_cast<const int64_t*>(d.inv10_mem) + d.lo};
+      for (uint32_t t = pw * 64 + lane; t < n16; t += nt) {
+        const uint32_t idx = 2 * t + 1 < nshard ? 2 * t + 1 : 2 * t;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) acc ^= (uint64_t)arr[a][idx];
+      }
+      if (acc == 0x5bd1e995a5a5a5a5ULL) ctl->pad[0] = 1;  // keeps the loads
+    }
+    const uint32_t* recs = reinterpret_cast<const uint32_t*>(sums);
+    uint32_t wb_at[P], wm_at[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      const uint32_t wq = lane * P + q;
+      uint32_t g = 0;
+      for (uint32_t r = 1; r < x.world; ++r)
+        if (wq >= x.wlo[r] && x.nw[r] > 0) g = r;
+      const uint32_t i = wq - x.wlo[g];
+      const bool ok = wq < nwords && i < x.nw[g];
+      const uint32_t base = (uint32_t)(g * x.blk);
+      wb_at[q] = ok ? base + i * 8 : ~0u;
+      wm_at[q] = ok ? base + x.wcap * x.ostride * 8 + i * 4 : ~0u;
+    }
+    const uint32_t row_b = x.ostride * 8, row_m = x.ostride * 4;
+    for (uint32_t j = wave - KSG_RES_P0; j < n_pods; j += NPW) {
+      const uint32_t e = j % RING;
+      // ring entry free: the checkers applied the commit of pod j - RING (while
+      // checking pod j - RING + 2), so neither they nor the committer need it
+      for (uint32_t spin = 0;; ++spin) {
+        if (ld_acq(&ctl->stop)) return;
+        if (spin > KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          return;
+        }
+        uint32_t done = ld_acq(&ctl->chk_seq[0]);
+#pragma unroll
+        for (int c = 1; c < KSG_RES_NCHK; ++c) done = min(done, ld_acq(&ctl->chk_seq[c]));
+        if (j < RING || done + RING >= j + 3) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      const uint32_t rec = lane < DW ? recs[(size_t)j * DW + lane] : 0u;
+      uint64_t t0[P];
+      int32_t mw[P];
+      int32_t lm = KSG_S32_NONE;
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        t0[q] = wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + j * row_b) : 0ULL;
+        mw[q] = wm_at[q] != ~0u ? *reinterpret_cast<const int32_t*>(x.buf + wm_at[q] + j * row_m) : KSG_S32_NONE;
+        lm = mw[q] > lm ? mw[q] : lm;
+      }
+      const int32_t m0 = wave_total_max(lm);
+      const bool drawable = __builtin_amdgcn_readlane(rec, WS_ERR) == 0 && m0 != KSG_S32_NONE;
+      const uint32_t wj = j >> 5, bj = 1u << (j & 31);
+      if (lane == 0) {  // the drawable bit first, then "known" (readers read them in that order)
+        if (drawable) atomicOr(&L_drw[wj], bj);
+        atomicOr(&L_pub[wj], bj);
+      }
+      uint32_t cnt = 0;
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        t0[q] = (m0 != KSG_S32_NONE && mw[q] == m0) ? t0[q] : 0ULL;
+        cnt += __popcll(t0[q]);
+      }
+      const uint32_t incl = dpp_scan_add(cnt);
+      const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      // draw index = drawable pods before j (every one of them known)
+      uint32_t idx = 0;
+      for (uint32_t spin = 0;; ++spin) {
+        if (ld_acq(&ctl->stop)) return;
+        if (spin > KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          return;
+        }
+        bool all = true;
+        idx = 0;
+        for (uint32_t w = 0; w <= wj; ++w) {
+          const uint32_t mask = w < wj ? ~0u : bj - 1u;
+          const uint32_t pub = __builtin_amdgcn_readfirstlane(ld_acq(&L_pub[w]));
+          all = all && (pub & mask) == mask;
+          idx += __popc(__builtin_amdgcn_readfirstlane(L_drw[w]) & mask);
+        }
+        if (all) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      uint64_t sm = rng0 + (uint64_t)idx * 0x9E3779B97F4A7C15ULL;
+      const uint64_t r = ksg_splitmix_next(&sm) >> 1;  // rand.Int() (generic_scheduler.go:94)
+      uint32_t mv = 0;
+      if (drawable && lane < k0) mv = umod64_32(r, k0 - lane);
+      int32_t pred = -1;
+      int64_t pv = 0;  // lanes 0..3: cap_c, cap_m, used_c, used_m of pred
+      double pinv = 0.0;
+      const uint32_t n_svcs = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NSS) >> 16;
+      const uint32_t nk = ((uint32_t)__builtin_amdgcn_readlane(rec, WS_NPP) & 0xffff) +
+                          ((uint32_t)__builtin_amdgcn_readlane(rec, WS_NPP) >> 16);
+      const uint32_t n_sel = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NSS) & 0xffff;
+      const bool inl = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NINL) <= KSG_WIN_INLINE && n_svcs <= KSG_SLOT_SVCS;
+      const uint32_t t_sv = lane < n_svcs ? lane : 0u;
+      const uint32_t my_sv = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + t_sv, 63u), 64);
+      int32_t s_cnt = 0, s_max = 0, s_peer = 0;
+      if (drawable) {
+        const uint32_t ix0 = __builtin_amdgcn_readfirstlane(mv);  // lane 0: r mod k0
+        pred = (int32_t)select_in_lanes<P>(t0, cnt, incl, k0 - 1 - ix0, lane);
+        const uint32_t pn = d.lo + (uint32_t)pred;
+        if (lane == 0) pv = d.cap_cpu[pn];
+        else if (lane == 1) pv = d.cap_mem[pn];
+        else if (lane == 2) pv = d.used_cpu[pn];
+        else if (lane == 3) pv = d.used_mem[pn];
+        if (inl && lane < n_svcs) {
+          s_cnt = d.svc_cnt[(size_t)my_sv * d.n_nodes + pn];
+          s_max = d.svc_max[my_sv];
+          s_peer = d.svc_peer[my_sv];
+        }
+        pinv = lr_inv10(pv);
+      }
+      r_mod[e * 64 + lane] = mv;
+      if (lane < DW) r_rec[e * DW + lane] = rec;
+#pragma unroll
+      for (int q = 0; q < P; ++q) r_t0[(size_t)e * P * 64 + lane * P + q] = t0[q];
+      if (inl && lane < n_svcs) {
+        r_svc[e].cnt[lane] = s_cnt;
+        r_svc[e].max[lane] = s_max;
+        r_svc[e].peer[lane] = s_peer;
+      }
+      if (lane < 4) (&r_hdr[e].cap_c)[lane] = pv;
+      if (lane < 2) (&r_hdr[e].inv_c)[lane] = pinv;
+      if (lane == 0) {
+        r_hdr[e].m0 = m0;
+        r_hdr[e].k0 = k0;
+        r_hdr[e].r = r;
+        r_hdr[e].drawable = drawable;
+        r_hdr[e].pred = pred;
+        st_rel(&r_hdr[e].ready, j + 1);
+      }
+    }
+    return;
+  }
+
+  // =========================================================================
+  // checkers (waves KSG_RES_C0 ..): lane l of checker c owns slot 64c + l
+  // =========================================================================
+  if (wave >= KSG_RES_C0) {
+    __builtin_amdgcn_s_setprio(2);
+    const uint32_t c = wave - KSG_RES_C0;
+    const uint32_t my_slot = c * 64 + lane;
+    const uint32_t* my_cl = L_cl + (size_t)my_slot * KSG_CL_W;
+    RegSlot S;
+    S.node = ~0u;
+    S.cap_c = S.cap_m = S.snp_c = S.snp_m = S.dl_c = S.dl_m = 0;
+    S.inv_c = S.inv_m = 0.0;
+    S.nk = S.ns = S.smask = 0;
+    // AssumePod of pod p (plugin/pkg/scheduler/scheduler.go:115-118) into the
+    // owner lane's slot: requested totals, list lengths; the services' snapshot
+    // counts into the table; the service flags (maxCount rises, first peer)
+    // later pods of the window stop on
+    auto apply = [&](uint32_t p) {
+      const uint32_t kind = __builtin_amdgcn_readfirstlane(L_cm[p].kind);
+      const uint32_t slot = __builtin_amdgcn_readfirstlane(L_cm[p].slot);
+      if (kind != 1 || (slot >> 6) != c) return;
+      const uint32_t woff = __builtin_amdgcn_readfirstlane(L_cm[p].node);
+      const uint32_t fl = __builtin_amdgcn_readfirstlane(L_cm[p].flags);
+      const bool fresh = (fl & 1u) != 0, is_pred = (fl & 2u) != 0;
+      const uint32_t ol = slot & 63, ep = p % RING, wn = d.lo + woff;
+      const uint32_t prec = lane < DW ? r_rec[ep * DW + lane] : 0u;
+      const PodView ppv = pod_view(prec);
+      const uint32_t nss = __builtin_amdgcn_readlane(prec, WS_NSS);
+      const uint32_t n_sel = nss & 0xffff, n_svcs = nss >> 16, nk = ppv.nk;
+      const uint32_t base_nk = fresh ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)S.nk, (int)ol);
+      const uint32_t base_ns = fresh ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)S.ns, (int)ol);
+      // the new slot's snapshot: staged for the predicted node, else from L2
+      if (fresh && lane == ol) {
+        if (is_pred) {
+          S.cap_c = r_hdr[ep].cap_c;
+          S.cap_m = r_hdr[ep].cap_m;
+          S.snp_c = r_hdr[ep].used_c;
+          S.snp_m = r_hdr[ep].used_m;
+          S.inv_c = r_hdr[ep].inv_c;
+          S.inv_m = r_hdr[ep].inv_m;
+        } else {
+          S.cap_c = gld(d.cap_cpu + wn);
+          S.cap_m = gld(d.cap_mem + wn);
+          S.snp_c = gld(d.used_cpu + wn);
+          S.snp_m = gld(d.used_mem + wn);
+          S.inv_c = gld(d.inv10_cpu + wn);
+          S.inv_m = gld(d.inv10_mem + wn);
+        }
+        S.node = woff;
+        S.dl_c = S.dl_m = 0;
+        S.smask = 0;
+      }
+      uint32_t new_mask = 0;
+      if (n_svcs) {
+        // the pod's services (lane t < n_svcs): snapshot count on the node, max, peer
+        const bool sv_lane = lane < n_svcs;
+        const uint32_t my_sv =
+            (uint32_t)__shfl((int)prec, (int)min(WS_IDS + nk + n_sel + (sv_lane ? lane : 0u), 63u), 64);
+        int32_t cnt = 0, mx = 0, peer = 0;
+        if (sv_lane) {
+          cnt = is_pred ? r_svc[ep].cnt[lane] : gld(d.svc_cnt + (size_t)my_sv * d.n_nodes + wn);
+          mx = r_svc[ep].max[lane];
+          peer = r_svc[ep].peer[lane];
+        }
+        // earlier window commits of each service on this node (table lanes KSG_CL_SV..)
+        const uint32_t ent = lane - KSG_CL_SV < base_ns ? L_cl[(size_t)slot * KSG_CL_W + lane] : ~0u;
+        uint32_t before = 0;
+        for (uint32_t t = 0; t < n_svcs; ++t) {
+          const uint32_t sv_t = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)t);
+          const uint32_t b_t = (uint32_t)__popcll(__ballot(ent == sv_t));
+          if (lane == t) before = b_t;
+        }
+        bool changed = sv_lane && aff_on && peer == -1 && !((L_peerset[my_sv >> 5] >> (my_sv & 31)) & 1u);
+        // first commit of a service with no peer yet: its first peer, in commit order
+        uint64_t pm = __ballot(sv_lane && peer == -1);
+        if (pm) {
+          uint32_t n_peer = __builtin_amdgcn_readfirstlane(ctl->n_peer);
+          while (pm) {
+            const uint32_t b = __builtin_ctzll(pm);
+            pm &= pm - 1;
+            const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)b);
+            if (!((L_peerset[fsv >> 5] >> (fsv & 31)) & 1u)) {
+              if (lane == 0) {
+                L_peerset[fsv >> 5] |= 1u << (fsv & 31);
+                L_peer[2 * n_peer] = fsv;
+                L_peer[2 * n_peer + 1] = wn;
+              }
+              ++n_peer;
+              lds_fence();
+            }
+          }
+          if (lane == 0) ctl->n_peer = n_peer;
+        }
+        if (sv_lane && spread_on && cnt + (int32_t)before + 1 > mx) changed = true;  // maxCount rises
+        if (changed) atomicOr(&L_flag[my_sv >> 5], 1u << (my_sv & 31));
+        if (sv_lane) L_cl[(size_t)slot * KSG_CL_W + KSG_CL_SC + base_ns + lane] = (uint32_t)cnt;
+        new_mask = wave_or_u32(sv_lane ? (1u << (my_sv & 31)) : 0u);
+      }
+      if (lane == ol) {
+        S.dl_c = (int64_t)((uint64_t)S.dl_c + (uint64_t)ppv.req_c);
+        S.dl_m = (int64_t)((uint64_t)S.dl_m + (uint64_t)ppv.req_m);
+        S.nk = base_nk + nk;
+        S.ns = base_ns + n_svcs;
+        S.smask |= new_mask;
+      }
+    };
+
+    uint64_t t_last = 0, t_acc = 0;
+    auto cstamp = [&](uint32_t k) {
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        t_acc += lane == k ? t_now - t_last : 0ULL;
+        t_last = t_now;
+      }
+    };
+    if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
+    for (uint32_t i = 0;; ++i) {
+      const uint32_t e = i % RING, par = i & 1;
+      bool stopped = false;
+      // pod i is checked against the slots as of commits <= i-2 (the committer
+      // re-checks the slot of commit i-1 itself): it starts once commit i-2 is
+      // published, a whole pod before the committer needs its drops
+      for (uint32_t spin = 0;; ++spin) {
+        if (i < n_pods && ld_acq(&ctl->sel_seq) + 1 >= i && ld_acq(&r_hdr[e].ready) == i + 1) break;
+        if (ld_acq(&ctl->stop)) {
+          stopped = true;
+          break;
+        }
+        if (spin > 16 * KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          stopped = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      cstamp(c == 0 ? 16 : 19);
+      if (stopped) {
+        // pods [0, resolved) are decided: apply the commits this checker has not
+        // (the committer runs ahead of the checkers over pods that do not commit)
+        const uint32_t R = __builtin_amdgcn_readfirstlane(ctl->resolved);
+        for (uint32_t q = i >= 2 ? i - 2 : 0; q < R; ++q) apply(q);
+        break;
+      }
+      if (i >= 2) apply(i - 2);
+      cstamp(c == 0 ? 17 : 20);
+      const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
+      const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
+      uint32_t cntd = 0;
+      if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE) {
+        const PodView pv = pod_view(rec);
+        bool drop = false;
+        if (S.node != ~0u) {
+          const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
+          if ((t0e[S.node >> 6] >> (S.node & 63)) & 1ULL) {
+            // does the slot (a snapshot tie of the pod) score below M0 now?
+            const int64_t now_c = (int64_t)((uint64_t)S.snp_c + (uint64_t)S.dl_c);
+            const int64_t now_m = (int64_t)((uint64_t)S.snp_m + (uint64_t)S.dl_m);
+            if (res_on && !pv.zero_req)  // PodFitsResources (predicates.go:127-145)
+              drop = !((S.cap_c == 0 || S.cap_c - now_c >= pv.req_c) && (S.cap_m == 0 || S.cap_m - now_m >= pv.req_m));
+            if (d.w_lr) {  // LeastRequested (priorities.go:43-76) can only fall as requested grows
+              const int32_t lr_now = lr_win(now_c + pv.req_c, S.cap_c, S.inv_c) + lr_win(now_m + pv.req_m, S.cap_m, S.inv_m);
+              const int32_t lr_snap =
+                  lr_win(S.snp_c + pv.req_c, S.cap_c, S.inv_c) + lr_win(S.snp_m + pv.req_m, S.cap_m, S.inv_m);
+              drop |= (lr_now >> 1) != (lr_snap >> 1);
+            }
+            if (!drop && pv.nk && S.nk) {  // PodFitsPorts / NoDiskConflict vs the window's keys
+              for (uint32_t a = 0; a < S.nk; ++a) {
+                const uint32_t key = my_cl[KSG_CL_KEY + a];
+                for (uint32_t b = 0; b < pv.nk; ++b) {
+                  const bool on = b < pv.n_ports ? ports_on : disk_on;
+                  drop |= on && (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b)) == key;
+                }
+              }
+            }
+            if (!drop && spread_on && pv.s >= 0 && ((S.smask >> (pv.s & 31)) & 1u)) {
+              // ServiceSpreading (spreading.go:72-86) under an unchanged maxCount
+              int32_t delta = 0, snapc = 0;
+              for (uint32_t a = 0; a < S.ns; ++a)
+                if (my_cl[KSG_CL_SV + a] == (uint32_t)pv.s) {
+                  snapc = (int32_t)my_cl[KSG_CL_SC + a];
+                  ++delta;
+                }
+              if (delta)
+                drop = frac10_f32((int64_t)pv.smax - snapc - delta, pv.smax) !=
+                       frac10_f32((int64_t)pv.smax - snapc, pv.smax);
+            }
+            if (drop)
+              atomicOr(reinterpret_cast<unsigned long long*>(L_drop + (size_t)par * P * 64 + (S.node >> 6)),
+                       1ULL << (S.node & 63));
+          }
+        }
+        cntd = __popcll(__ballot(drop));
+      }
+      if (lane == 0) {
+        ctl->chk_cnt[c][par] = cntd;
+        st_rel(&ctl->chk_seq[c], i + 1);
+      }
+      cstamp(c == 0 ? 18 : 21);
+    }
+    // write the window's deltas of this checker's slots back to HBM (the next snapshot)
+    if (S.node != ~0u) {
+      const uint32_t n = d.lo + S.node;
+      d.used_cpu[n] = (int64_t)((uint64_t)S.snp_c + (uint64_t)S.dl_c);
+      d.used_mem[n] = (int64_t)((uint64_t)S.snp_m + (uint64_t)S.dl_m);
+      for (uint32_t a = 0; a < S.nk; ++a)
+        __hip_atomic_fetch_or(d.keymap + (size_t)my_cl[KSG_CL_KEY + a] * d.nw + (n >> 6), 1ULL << (n & 63),
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (uint32_t a = 0; a < S.ns; ++a) {
+        const uint32_t sa = my_cl[KSG_CL_SV + a];
+        bool first = true;
+        int32_t count = 0;
+        for (uint32_t b = 0; b < S.ns; ++b) {
+          if (my_cl[KSG_CL_SV + b] == sa) {
+            if (b < a) first = false;
+            ++count;
+          }
+        }
+        __hip_atomic_fetch_add(d.svc_total + sa, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (first) {
+          const int32_t fin = (int32_t)my_cl[KSG_CL_SC + a] + count;
+          d.svc_cnt[(size_t)sa * d.n_nodes + n] = fin;
+          __hip_atomic_fetch_max(d.svc_max + sa, fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    if constexpr (STAMP) {
+      if (lane >= 16 && lane < 22) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
+    }
+    drain_stores();
+    if (lane == 0) st_rel(&ctl->fin[c], 1u);
+    return;
+  }
+  if (wave != 0) return;
+
+  // =========================================================================
+  // committer (wave 0)
+  // =========================================================================
+  __builtin_amdgcn_s_setprio(3);
+  uint32_t resolved = n_pods, reason = 0, n_slots = 0, n_draws = 0;
+  uint32_t cn0 = ~0u, cn1 = ~0u;  // nodes of slots lane and 64 + lane
+  uint32_t sk0 = 0, sk1 = 0;      // their key counts
+  uint32_t ss0 = 0, ss1 = 0;      // their service entry counts
+  int64_t dc0 = 0, dm0 = 0, dc1 = 0, dm1 = 0;  // their window deltas (current through the last commit)
+  uint32_t xs = KSG_NO_SLOT, xnode = 0;  // slot and node of the last commit (pod i-1)
+  uint32_t prev_nsv = 0, prev_sv = 0;    // pod i-1's services (lane t < prev_nsv)
+  // lanes 0..5 of the snapshot loads of that node: cap_c, cap_m, used_c, used_m, 10/cap_c, 10/cap_m
+  const uint64_t* const xsrc = lane == 0   ? reinterpret_cast<const uint64_t*>(d.cap_cpu)
+                               : lane == 1 ? reinterpret_cast<const uint64_t*>(d.cap_mem)
+                               : lane == 2 ? reinterpret_cast<const uint64_t*>(d.used_cpu)
+                               : lane == 3 ? reinterpret_cast<const uint64_t*>(d.used_mem)
+                               : lane == 4 ? reinterpret_cast<const uint64_t*>(d.inv10_cpu)
+                                           : reinterpret_cast<const uint64_t*>(d.inv10_mem);
+  uint64_t t_last = 0, t_acc = 0;
+#define KSG_STAMP2(k)                                        \
+  if constexpr (STAMP) {                                     \
+    const uint64_t t_now = __builtin_amdgcn_s_memtime();     \
+    t_acc += lane == (uint32_t)(k) ? t_now - t_last : 0ULL;  \
+    t_last = t_now;                                          \
+  }
+#define KSG_COUNT2(k, v)                                   \
+  if constexpr (STAMP) {                                   \
+    t_acc += lane == (uint32_t)(k) ? (uint64_t)(v) : 0ULL; \
+  }
+  if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
+  for (uint32_t i = 0; i < n_pods; ++i) {
+    const uint32_t e = i % RING, par = i & 1;
+    const bool have_x = xs != KSG_NO_SLOT;
+    const uint32_t xw = d.lo + (have_x ? xnode : 0u);
+    // the node and lists of commit i-1: the snapshot loaded here, unconditionally and
+    // lane by lane so it stays in a VGPR, and the slot's table row (lane t: entry t);
+    // both are first read by the re-check below (the ring, the checkers and the
+    // flags come in between)
+    const uint64_t xv = gld(xsrc + xw);
+    const uint32_t xcl = lane < KSG_CL_SC ? L_cl[(size_t)(have_x ? xs : 0u) * KSG_CL_W + lane] : 0u;
+    if (ld_acq(&r_hdr[e].ready) != i + 1) {
+      __builtin_amdgcn_s_setprio(0);  // a producer shares this SIMD: do not starve it
+      bool hung = false;
+      for (uint32_t spin = 0; ld_acq(&r_hdr[e].ready) != i + 1; ++spin)
+        if (spin > 16 * KSG_SPIN_LIMIT || ld_acq(&ctl->hang)) {
+          hung = true;
+          break;
+        }
+      __builtin_amdgcn_s_setprio(3);
+      if (hung) {
+        resolved = i;
+        reason = KSG_STOP_HANG;
+        break;
+      }
+    }
+    KSG_STAMP2(0)
+    const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
+    const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
+    const uint32_t k0 = __builtin_amdgcn_readfirstlane(r_hdr[e].k0);
+    const int32_t pred = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].pred);
+    const int32_t s = (int32_t)__builtin_amdgcn_readlane(rec, WS_SVC);
+    // svc_cnt[s][x] at the snapshot (any valid address when there is no x / s)
+    const int32_t xcv = gld(d.svc_cnt + (size_t)(s >= 0 ? s : 0) * d.n_nodes + xw);
+    if (__builtin_amdgcn_readlane(rec, WS_ERR) || m0 == KSG_S32_NONE) {
+      // ServiceAffinity peer error / nothing fit at the snapshot (commits only
+      // remove fits): no draw, no commit
+      if (lane == 0) {
+        L_cm[i].kind = 0;
+        L_out[i] = __builtin_amdgcn_readlane(rec, WS_ERR) ? KSG_OUT_ERROR : KSG_OUT_NOFIT;
+        st_rel(&ctl->sel_seq, i + 1);
+      }
+      xs = KSG_NO_SLOT;  // pod i+1's checkers see every commit up to i-1
+      prev_nsv = 0;
+      continue;
+    }
+    const PodView pv = pod_view(rec);
+    const uint32_t nss = __builtin_amdgcn_readlane(rec, WS_NSS);
+    const uint32_t n_sel = nss & 0xffff, n_svcs = nss >> 16, nk = pv.nk;
+    if (__builtin_amdgcn_readlane(rec, WS_NINL) > KSG_WIN_INLINE || nk > KSG_SLOT_KEYS || n_svcs > KSG_SLOT_SVCS) {
+      resolved = i;  // lists longer than the record / a slot: the exact per-pod kernel takes it
+      reason = i == 0 ? KSG_STOP_OVERSIZE : KSG_STOP_SLOT;
+      break;
+    }
+    KSG_STAMP2(1)
+    // ---- the checkers' drops for this pod (slots as of commits <= i-2)
+    bool hung = false;
+    for (uint32_t spin = 0;; ++spin) {
+      bool done = true;
+#pragma unroll
+      for (int c = 0; c < KSG_RES_NCHK; ++c) done = done && ld_acq(&ctl->chk_seq[c]) >= i + 1;
+      if (done) break;
+      if (spin > 16 * KSG_SPIN_LIMIT || ld_acq(&ctl->hang)) {
+        hung = true;
+        break;
+      }
+    }
+    if (hung) {
+      resolved = i;
+      reason = KSG_STOP_HANG;
+      break;
+    }
+    KSG_STAMP2(2)
+    // ---- x's slot as of commit i-1 (this wave's deltas and counts, the table row)
+    const uint32_t xl = xs & 63;
+    const bool x_hi = xs >= 64;
+    const uint32_t xnk = have_x ? (uint32_t)__builtin_amdgcn_readlane((int)(x_hi ? sk1 : sk0), (int)xl) : 0u;
+    const uint32_t xns = have_x ? (uint32_t)__builtin_amdgcn_readlane((int)(x_hi ? ss1 : ss0), (int)xl) : 0u;
+    // window entries of service s on x (commit i-1 included)
+    const uint32_t x_cnt_s =
+        s >= 0 ? (uint32_t)__popcll(__ballot(lane - KSG_CL_SV < xns && xcl == (uint32_t)s)) : 0u;
+    if (s >= 0 && (spread_on || aff_on)) {
+      // a service scalar this pod reads changed in the window: by commits <= i-2
+      // (the checkers' flags) or by commit i-1 (here)
+      bool flagged = (L_flag[s >> 5] >> (s & 31)) & 1u;
+      const bool prev_has = __ballot(lane < prev_nsv && prev_sv == (uint32_t)s) != 0;
+      if (!flagged && have_x && prev_has) {
+        const int32_t x_snapc = __builtin_amdgcn_readfirstlane(xcv);
+        if (spread_on && x_snapc + (int32_t)x_cnt_s > pv.smax) flagged = true;  // maxCount rises
+        if (aff_on && (int32_t)__builtin_amdgcn_readfirstlane(r_svc[e].peer[0]) == -1 &&
+            !((L_peerset[s >> 5] >> (s & 31)) & 1u))
+          flagged = true;  // commit i-1 gave the service its first peer
+      }
+      if (flagged) {
+        resolved = i;
+        reason = KSG_STOP_SERVICE;
+        break;
+      }
+    }
+    uint32_t dropped = 0;
+#pragma unroll
+    for (int c = 0; c < KSG_RES_NCHK; ++c) dropped += __builtin_amdgcn_readfirstlane(ctl->chk_cnt[c][par]);
+    const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
+    uint64_t* dw = L_drop + (size_t)par * P * 64;
+    // ---- re-check x for this pod: a tie at the snapshot the checkers did not drop
+    bool x_drop = false;
+    if (have_x) {
+      const uint64_t xb = 1ULL << (xnode & 63);
+      const uint64_t t0x = t0e[xnode >> 6], dwx = dw[xnode >> 6];
+      if ((t0x & xb) && !(dwx & xb)) {
+        const int64_t x_cc = (int64_t)readlane64(xv, 0), x_cm = (int64_t)readlane64(xv, 1);
+        const int64_t x_sc = (int64_t)readlane64(xv, 2), x_sm = (int64_t)readlane64(xv, 3);
+        const double x_ic = __longlong_as_double((long long)readlane64(xv, 4));
+        const double x_im = __longlong_as_double((long long)readlane64(xv, 5));
+        const int64_t dlc = (int64_t)readlane64((uint64_t)(x_hi ? dc1 : dc0), (int)xl);
+        const int64_t dlm = (int64_t)readlane64((uint64_t)(x_hi ? dm1 : dm0), (int)xl);
+        const int64_t now_c = (int64_t)((uint64_t)x_sc + (uint64_t)dlc);
+        const int64_t now_m = (int64_t)((uint64_t)x_sm + (uint64_t)dlm);
+        bool xd = false;
+        if (res_on && !pv.zero_req)  // PodFitsResources
+          xd = !((x_cc == 0 || x_cc - now_c >= pv.req_c) && (x_cm == 0 || x_cm - now_m >= pv.req_m));
+        if (d.w_lr) {  // LeastRequested
+          const int32_t lr_now = lr_win(now_c + pv.req_c, x_cc, x_ic) + lr_win(now_m + pv.req_m, x_cm, x_im);
+          const int32_t lr_snap = lr_win(x_sc + pv.req_c, x_cc, x_ic) + lr_win(x_sm + pv.req_m, x_cm, x_im);
+          xd |= (lr_now >> 1) != (lr_snap >> 1);
+        }
+        if (spread_on && x_cnt_s) {  // ServiceSpreading under an unchanged maxCount
+          const int32_t x_snapc = __builtin_amdgcn_readfirstlane(xcv);
+          xd |= frac10_f32((int64_t)pv.smax - x_snapc - (int32_t)x_cnt_s, pv.smax) !=
+                frac10_f32((int64_t)pv.smax - x_snapc, pv.smax);
+        }
+        if (nk && xnk) {  // PodFitsPorts / NoDiskConflict: table lane t holds key t
+          bool hit = false;
+          for (uint32_t b = 0; b < nk; ++b) {
+            const bool on = b < pv.n_ports ? ports_on : disk_on;
+            hit |= on && lane < xnk && xcl == (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b));
+          }
+          xd |= __ballot(hit) != 0;
+        }
+        x_drop = __builtin_amdgcn_readfirstlane((int)xd) != 0;
+      }
+    }
+    dropped += x_drop ? 1u : 0u;
+    KSG_STAMP2(3)
+    if (dropped >= k0) {
+      resolved = i;  // every snapshot tie got worse: needs a fresh snapshot
+      reason = KSG_STOP_EXHAUSTED;
+      break;
+    }
+    // ---- selection: k live ties, ix-th in descending rank = (k-1-ix)-th ascending
+    const uint32_t k = k0 - dropped;
+    uint32_t woff;
+    if (dropped == 0) {
+      woff = (uint32_t)pred;  // staged by the producer
+    } else {
+      KSG_COUNT2(7, 64)
+      uint32_t ix;
+      if (dropped < 64) {
+        ix = __builtin_amdgcn_readfirstlane(r_mod[e * 64 + dropped]);
+      } else {
+        const uint64_t r = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(r_hdr[e].r >> 32)) << 32) |
+                           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r_hdr[e].r);
+        ix = umod64_32(r, k);
+      }
+      uint64_t live[P];
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        live[q] = t0e[lane * P + q] & ~dw[lane * P + q];
+        dw[lane * P + q] = 0;  // (cleared for the pod two ahead)
+        if (x_drop && lane * P + q == (xnode >> 6)) live[q] &= ~(1ULL << (xnode & 63));
+      }
+      uint32_t cl = 0;
+#pragma unroll
+      for (int q = 0; q < P; ++q) cl += __popcll(live[q]);
+      const uint32_t incl = dpp_scan_add(cl);
+      woff = select_in_lanes<P>(live, cl, incl, k - 1 - ix, lane);
+    }
+    KSG_STAMP2(4)
+    // ---- AssumePod's slot
+    const uint64_t hit0 = __ballot(cn0 == woff);
+    const uint64_t hit1 = __ballot(cn1 == woff);
+    const bool in_c = (hit0 | hit1) != 0;
+    uint32_t slot, base_nk = 0, base_ns = 0;
+    if (in_c) {
+      slot = hit0 ? (uint32_t)__builtin_ctzll(hit0) : 64u + (uint32_t)__builtin_ctzll(hit1);
+      const uint32_t sl = slot & 63;
+      base_nk = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? sk0 : sk1), (int)sl);
+      base_ns = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? ss0 : ss1), (int)sl);
+      if (base_nk + nk > KSG_SLOT_KEYS || base_ns + n_svcs > KSG_SLOT_SVCS) {
+        resolved = i;  // this pod is redone (with the same draw) in the next window
+        reason = KSG_STOP_SLOT;
+        break;
+      }
+    } else {
+      if (n_slots == KSG_MAX_SLOTS) {
+        resolved = i;
+        reason = KSG_STOP_SLOT;
+        break;
+      }
+      slot = n_slots++;
+    }
+    // the pod's keys and service ids into the slot's table row: record lane L
+    // holds dword L, so each list entry is stored by the lane that holds it
+    {
+      uint32_t* row = L_cl + (size_t)slot * KSG_CL_W;
+      const uint32_t kt = lane - WS_IDS, st = lane - (WS_IDS + nk + n_sel);
+      if (kt < nk) row[KSG_CL_KEY + base_nk + kt] = rec;
+      if (st < n_svcs) row[KSG_CL_SV + base_ns + st] = rec;
+    }
+    if (lane == 0) {
+      L_cm[i] = WinCommit{1u, slot, woff, (in_c ? 0u : 1u) | ((int32_t)woff == pred ? 2u : 0u)};
+      L_out[i] = (int32_t)(d.lo + woff);
+      st_rel(&ctl->sel_seq, i + 1);  // the checkers apply it and move on
+    }
+    if ((int32_t)woff != pred) KSG_COUNT2(8, 64)
+    if (lane == (slot & 63)) {  // this wave's counts and deltas of the slot
+      if (slot >= 64) {
+        if (!in_c) {
+          cn1 = woff;
+          dc1 = dm1 = 0;
+        }
+        dc1 = (int64_t)((uint64_t)dc1 + (uint64_t)pv.req_c);
+        dm1 = (int64_t)((uint64_t)dm1 + (uint64_t)pv.req_m);
+        sk1 = base_nk + nk;
+        ss1 = base_ns + n_svcs;
+      } else {
+        if (!in_c) {
+          cn0 = woff;
+          dc0 = dm0 = 0;
+        }
+        dc0 = (int64_t)((uint64_t)dc0 + (uint64_t)pv.req_c);
+        dm0 = (int64_t)((uint64_t)dm0 + (uint64_t)pv.req_m);
+        sk0 = base_nk + nk;
+        ss0 = base_ns + n_svcs;
+      }
+    }
+    xs = slot;
+    xnode = woff;
+    prev_nsv = n_svcs;
+    prev_sv = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + (lane < n_svcs ? lane : 0u), 63u), 64);
+    ++n_draws;
+    KSG_STAMP2(5)
+  }
+  if (lane == 0) {
+    ctl->resolved = resolved;
+    st_rel(&ctl->stop, 1u);
+  }
+  // the checkers apply the last commits and write their slots back
+  bool drained = false;
+  for (uint32_t spin = 0; spin <= 16 * KSG_SPIN_LIMIT; ++spin) {
+    bool done = true;
+#pragma unroll
+    for (int c = 0; c < KSG_RES_NCHK; ++c) done = done && ld_acq(&ctl->fin[c]) != 0;
+    if (done) {
+      drained = true;
+      break;
+    }
+  }
+  if (!drained || ld_acq(&ctl->hang)) reason = KSG_STOP_HANG;
+  if constexpr (STAMP) {
+    if (lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
+  }
+#undef KSG_STAMP2
+#undef KSG_COUNT2
+  const uint32_t n_peer = __builtin_amdgcn_readfirstlane(ctl->n_peer);
+  for (uint32_t t = lane; t < n_peer; t += 64) {
+    const uint32_t sv = L_peer[2 * t];
+    int32_t expect = -1;
+    __hip_atomic_compare_exchange_strong(d.svc_peer + sv, &expect, (int32_t)L_peer[2 * t + 1], __ATOMIC_RELAXED,
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (uint32_t t = lane; t < resolved; t += 64) out[t] = L_out[t];
+  if (lane == 0) {
+    *rng_io = rng0 + (uint64_t)n_draws * 0x9E3779B97F4A7C15ULL;
+    if (reason == KSG_STOP_HANG) {
+      run->halt = KSG_HALT_HANG;
+    } else if (reason == KSG_STOP_OVERSIZE) {
+      run->halt = KSG_HALT_OVERSIZE;  // pod pos: the host runs the exact per-pod path, then resumes
+    } else if (resolved == 0 || resolved > n_pods) {
+      run->halt = KSG_HALT_BADCOUNT;
+    } else {
+      run->pos = pos + resolved;
+      run->windows += 1;
+      if (reason >= 1 && reason <= 3) run->stops[reason] += 1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
 static uint32_t win_P(const KsgDev& d) {
@@ -1489,10 +2329,13 @@ uint32_t ksg_win_max_window(const KsgDev& d) {
   if (P == 0) return 0;
   if (d.n_anti > 0 && d.n_domains_total > 0 && P > 8) return 0;  // anti-affinity: up to 32k nodes
   const uint32_t nflag = (d.n_services + 31) / 32;
+  // (KSG_DEBUG & 128 runs the LDS-slot resolver for every configuration)
+  const bool anti = (d.n_anti > 0 && d.n_domains_total > 0) || (d.dbg & 128);
   uint32_t lo = 0, hi = 4096;
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1) / 2;
-    if (win_lds_offsets(P, nflag, mid, d.n_anti > 0).total <= kWinLdsBudget) lo = mid;
+    const uint32_t need = anti ? win_lds_offsets(P, nflag, mid, d.n_anti > 0).total : win2_lds_offsets(P, nflag, mid).total;
+    if (need <= kWinLdsBudget) lo = mid;
     else hi = mid - 1;
   }
   return lo;
@@ -1514,9 +2357,41 @@ static hipError_t win_resolve_launch(const KsgDev& d, uint32_t wcap, size_t lds,
   return hipGetLastError();
 }
 
+template <int PP, bool ST>
+static hipError_t win_resolve2_launch(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run,
+                                      const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
+                                      hipStream_t st) {
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_resolve2_kernel<PP, ST>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipGetLastError();
+    once = true;
+  }
+  hipLaunchKernelGGL((ksg_win_resolve2_kernel<PP, ST>), dim3(1), dim3(512), lds, st, d, wcap, run, sums, x, rng, out);
+  return hipGetLastError();
+}
+
 hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
                                   const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
   const uint32_t P = win_P(d);
+  if (x.fit_off == 0 && !(d.dbg & 128)) {  // no ServiceAntiAffinity: the register-slot resolver
+    // (KSG_DEBUG & 128: the LDS-slot resolver instead, for comparison)
+    const size_t lds2 = win2_lds_offsets(P, (d.n_services + 31) / 32, wcap).total;
+    const bool stamp2 = (d.dbg & 8) != 0;
+#define KSG_RES2_CASE(PP)                                                                         \
+  if (P == PP)                                                                                    \
+    return stamp2 ? win_resolve2_launch<PP, true>(d, wcap, lds2, run, sums, x, rng, out, st)      \
+                  : win_resolve2_launch<PP, false>(d, wcap, lds2, run, sums, x, rng, out, st);
+    KSG_RES2_CASE(1)
+    KSG_RES2_CASE(2)
+    KSG_RES2_CASE(4)
+    KSG_RES2_CASE(8)
+    KSG_RES2_CASE(16)
+    KSG_RES2_CASE(32)
+#undef KSG_RES2_CASE
+    return hipErrorInvalidValue;
+  }
   const size_t lds = win_lds_offsets(P, (d.n_services + 31) / 32, wcap, x.fit_off != 0).total;
   const bool stamp = (d.dbg & 8) != 0;  // KSG_DEBUG & 8: per-section s_memtime stamps
   const bool anti = x.fit_off != 0;

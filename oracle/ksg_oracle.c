@@ -866,3 +866,188 @@ void orc_admit_pods(const ksg_admission_set *sets, uint32_t n_sets, const ksg_po
     }
   }
 }
+
+/* ====================================== incremental mode, node-sharded threads */
+/* The strong CPU design point (SURVEY.md 8(d) "CPU timing" ii): the incremental
+ * restatement with every pod's node loop split over `nthreads` threads (contiguous
+ * node-rank shards, like the GPU shards); per pod, thread 0 resolves the pod's
+ * context, every thread filters/scores its shard and reports its max and tie count,
+ * thread 0 merges (selectHost: global max, ties in descending rank, one Int63 draw per
+ * success) and commits. Two spin barriers per pod. Configurations with
+ * ServiceAntiAffinity (a cross-shard domain-count reduction) run single-threaded. */
+#include <pthread.h>
+#include <stdatomic.h>
+
+typedef struct {
+  orc *o;
+  const ksg_pod *pods;
+  const uint32_t *ids;
+  uint32_t n;
+  uint64_t *rng;
+  int32_t *out;
+  int T;
+  int any;        /* some priority has a weight (else the HostPriorityList is empty) */
+  pctx c;         /* the current pod (thread 0 writes it before barrier A) */
+  int skip;
+  int32_t maxc;
+  int64_t *tmax;  /* per thread: local max score (NONE_SCORE: nothing fits) */
+  uint64_t *tcnt; /* per thread: nodes at it */
+  atomic_int bar_count, bar_sense;
+} mt_job;
+
+typedef struct {
+  mt_job *j;
+  int t;
+} mt_arg;
+
+static void mt_barrier(mt_job *j, int *sense) {
+  *sense = !*sense;
+  if (atomic_fetch_add_explicit(&j->bar_count, 1, memory_order_acq_rel) == j->T - 1) {
+    atomic_store_explicit(&j->bar_count, 0, memory_order_relaxed);
+    atomic_store_explicit(&j->bar_sense, *sense, memory_order_release);
+  } else {
+    while (atomic_load_explicit(&j->bar_sense, memory_order_acquire) != *sense) {
+#if defined(__x86_64__)
+      __builtin_ia32_pause();
+#endif
+    }
+  }
+}
+
+/* incr_prioritize's per-node score without ServiceAntiAffinity */
+static int64_t mt_score(const orc *o, const pctx *c, int32_t maxc, uint32_t n) {
+  const ksg_config *cf = &o->cfg;
+  if (cf->n_priority_configs == 0) return 1; /* EqualPriority fallback */
+  int64_t sc = 0;
+  if (cf->w_least_requested) {
+    int64_t tc = (int64_t)((uint64_t)o->used_c[n] + (uint64_t)c->p->milli_cpu);
+    int64_t tm = (int64_t)((uint64_t)o->used_m[n] + (uint64_t)c->p->memory);
+    sc += (int64_t)cf->w_least_requested * ((calculate_score(tc, o->cap_c[n]) + calculate_score(tm, o->cap_m[n])) / 2);
+  }
+  if (cf->w_service_spreading) {
+    int32_t s = c->p->service;
+    int32_t cnt = s >= 0 ? o->svc_cnt[(size_t)s * o->N + n] : 0;
+    sc += (int64_t)cf->w_service_spreading * (maxc > 0 ? frac10_f32((int64_t)maxc - cnt, maxc) : 10);
+  }
+  for (uint32_t q = 0; q < cf->n_label_pref; ++q) {
+    if (!cf->w_pref[q]) continue;
+    int exists = node_has_key(o, n, cf->pref_key[q]);
+    int ok = (exists && cf->pref_presence[q]) || (!exists && !cf->pref_presence[q]);
+    sc += (int64_t)cf->w_pref[q] * (ok ? 10 : 0);
+  }
+  return sc + (int64_t)cf->w_equal;
+}
+
+static void *mt_worker(void *argp) {
+  mt_arg *a = (mt_arg *)argp;
+  mt_job *j = a->j;
+  orc *o = j->o;
+  const int t = a->t;
+  const uint32_t lo = (uint32_t)(((uint64_t)o->N * t) / j->T), hi = (uint32_t)(((uint64_t)o->N * (t + 1)) / j->T);
+  int sense = 0;
+  for (uint32_t i = 0; i < j->n; ++i) {
+    if (t == 0) {
+      j->skip = 0;
+      j->c.p = j->pods + i;
+      j->c.ids = j->ids;
+      resolve_affinity(o, &j->c);
+      if (j->c.error) {
+        j->out[i] = KSG_OUT_ERROR;
+        j->skip = 1;
+      }
+      const int32_t s = j->pods[i].service;
+      j->maxc = s >= 0 ? o->svc_max[s] : 0;
+    }
+    mt_barrier(j, &sense); /* A: the pod's context is ready */
+    if (!j->skip) {
+      int64_t best = NONE_SCORE;
+      uint64_t k = 0;
+      for (uint32_t n = lo; n < hi; ++n) {
+        const int f = incr_fail_code(o, &j->c, n);
+        o->fails[n] = (uint8_t)f;
+        if (f) continue;
+        const int64_t sc = mt_score(o, &j->c, j->maxc, n);
+        o->scores[n] = sc;
+        if (sc > best) {
+          best = sc;
+          k = 1;
+        } else if (sc == best) {
+          ++k;
+        }
+      }
+      j->tmax[t] = best;
+      j->tcnt[t] = k;
+    }
+    mt_barrier(j, &sense); /* B: every shard reported */
+    if (t == 0 && !j->skip) {
+      int64_t M = NONE_SCORE;
+      uint64_t k = 0;
+      for (int g = 0; g < j->T; ++g)
+        if (j->tcnt[g] && j->tmax[g] > M) M = j->tmax[g];
+      for (int g = 0; g < j->T; ++g)
+        if (j->tcnt[g] && j->tmax[g] == M) k += j->tcnt[g];
+      if (!j->any) k = 0; /* every weight 0: empty HostPriorityList (generic_scheduler.go:149-151) */
+      if (k == 0) {
+        j->out[i] = KSG_OUT_NOFIT;
+      } else {
+        uint64_t ix = (splitmix_next(j->rng) >> 1) % k; /* rand.Int() % len(ties) */
+        int32_t node = -1;
+        for (int g = j->T - 1; g >= 0 && node < 0; --g) { /* ties in descending rank */
+          if (!j->tcnt[g] || j->tmax[g] != M) continue;
+          if (ix >= j->tcnt[g]) {
+            ix -= j->tcnt[g];
+            continue;
+          }
+          const uint32_t glo = (uint32_t)(((uint64_t)o->N * g) / j->T), ghi = (uint32_t)(((uint64_t)o->N * (g + 1)) / j->T);
+          for (int64_t n = (int64_t)ghi - 1; n >= (int64_t)glo; --n)
+            if (!o->fails[n] && o->scores[n] == M) {
+              if (ix == 0) {
+                node = (int32_t)n;
+                break;
+              }
+              --ix;
+            }
+        }
+        commit(o, j->pods + i, j->ids, (uint32_t)node);
+        j->out[i] = node;
+      }
+    }
+  }
+  return NULL;
+}
+
+int orc_schedule_batch_mt(orc *o, const ksg_pod *pods, uint32_t n, const uint32_t *ids, uint32_t n_ids,
+                          uint64_t *rng_state, int32_t *out_nodes, int nthreads) {
+  if (nthreads <= 1 || o->faithful || o->cfg.n_anti > 0 || o->N == 0 || (uint32_t)nthreads > o->N)
+    return orc_schedule_batch(o, pods, n, ids, n_ids, rng_state, out_nodes);
+  mt_job j;
+  memset(&j, 0, sizeof j);
+  j.o = o;
+  j.pods = pods;
+  j.ids = ids;
+  j.n = n;
+  j.rng = rng_state;
+  j.out = out_nodes;
+  j.T = nthreads;
+  const ksg_config *cf = &o->cfg;
+  j.any = cf->n_priority_configs == 0 || cf->w_least_requested || cf->w_service_spreading || cf->w_equal;
+  for (uint32_t q = 0; q < cf->n_label_pref; ++q) j.any |= cf->w_pref[q] != 0;
+  j.tmax = (int64_t *)calloc((size_t)nthreads, 8);
+  j.tcnt = (uint64_t *)calloc((size_t)nthreads, 8);
+  atomic_init(&j.bar_count, 0);
+  atomic_init(&j.bar_sense, 0);
+  pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+  mt_arg *args = (mt_arg *)calloc((size_t)nthreads, sizeof(mt_arg));
+  for (int t = 0; t < nthreads; ++t) {
+    args[t].j = &j;
+    args[t].t = t;
+    if (t) pthread_create(&th[t], NULL, mt_worker, &args[t]);
+  }
+  mt_worker(&args[0]);
+  for (int t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
+  free(th);
+  free(args);
+  free(j.tmax);
+  free(j.tcnt);
+  return KSG_OK;
+}

@@ -46,6 +46,7 @@ def load():
         "orc_schedule_batch": (C.c_int, [vp, vp, C.c_uint32, vp, C.c_uint32, P(C.c_uint64), vp]),
         "orc_read_requested": (None, [vp, vp, vp]),
         "orc_admit_pods": (None, [vp, C.c_uint32, vp, C.c_uint32, vp, vp, C.c_int, vp]),
+        "orc_schedule_batch_mt": (C.c_int, [vp, vp, C.c_uint32, vp, C.c_uint32, P(C.c_uint64), vp, C.c_int]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -123,6 +124,17 @@ class OracleScheduler:
         st = C.c_uint64(rng_state)
         self._lib.orc_schedule_batch(self._o, abi.ptr(pods), n, abi.ptr(_u32(batch.ids)), len(batch.ids),
                                      C.byref(st), abi.ptr(out))
+        return out[:n], st.value
+
+    def batch_mt(self, batch: PodBatch, rng_state: int, nthreads: int):
+        """Incremental mode with each pod's node loop split over `nthreads` threads
+        (node-rank shards); same decisions as batch()."""
+        n = len(batch)
+        pods = np.ascontiguousarray(batch.pods, dtype=abi.POD_DTYPE)
+        out = np.empty(max(n, 1), np.int32)
+        st = C.c_uint64(rng_state)
+        self._lib.orc_schedule_batch_mt(self._o, abi.ptr(pods), n, abi.ptr(_u32(batch.ids)), len(batch.ids),
+                                        C.byref(st), abi.ptr(out), int(nthreads))
         return out[:n], st.value
 
     def evaluate(self, batch: PodBatch, i: int = 0):

@@ -160,3 +160,19 @@ def test_families_ref_model_vs_c_oracle(family):
         assert not bad, f"faithful={faithful} first mismatches {[(i, want[i], got[i]) for i in bad[:5]]}"
         assert st_g == st_w
     assert sum(k == "ok" for k, _ in want) > len(want) // 2
+
+
+@pytest.mark.parametrize("name,nn,npods,threads", [("config2", 700, 1500, 4), ("config1", 500, 1000, 8),
+                                                     ("config2", 130, 600, 3)])
+def test_incremental_node_sharded_threads(name, nn, npods, threads):
+    """The nproc-thread CPU baseline (orc_schedule_batch_mt, node-rank shards per pod)
+    makes the single-threaded incremental restatement's decisions."""
+    c = Case(name, nn, npods)
+    a = OracleScheduler(c.cfg)
+    b = OracleScheduler(c.cfg)
+    for o in (a, b):
+        o.set_cluster(c.view.arrays)
+    oa, sa = a.batch(c.batch, 11)
+    ob, sb = b.batch_mt(c.batch, 11, threads)
+    assert np.array_equal(oa, ob) and sa == sb
+    assert all(np.array_equal(x, y) for x, y in zip(a.read_requested(), b.read_requested()))
