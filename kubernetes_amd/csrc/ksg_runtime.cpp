@@ -689,7 +689,7 @@ int ksg_destroy(ksg_ctx* c) {
     fprintf(stderr, "ksg producers (sum over waves): slot-wait %d loads %d draw-wait %d stage %d\n", h[12], h[13],
             h[14], h[15]);
     fprintf(stderr, "ksg stamps raw:");
-    for (int q = 0; q < 24; ++q) fprintf(stderr, " %d", h[q]);
+    for (int q = 0; q < 32; ++q) fprintf(stderr, " %d", h[q]);
     fprintf(stderr, "\n");
   }
   {

@@ -1485,7 +1485,8 @@ struct alignas(16) WinCommit {
   uint32_t kind;   // 0: no commit (error / no fit), 1: commit
   uint32_t slot;
   uint32_t node;   // shard offset of the node
-  uint32_t flags;  // bit 0: a new slot, bit 1: the node is the producer's predicted node
+  uint32_t flags;  // bit 0: a new slot, bit 1: the node is the producer's predicted node,
+                   // bits 8..15: the pod's service count
 };
 struct alignas(16) WinCtl2 {
   uint32_t stop;      // the committer is done: pods [0, resolved) are decided
@@ -1496,10 +1497,19 @@ struct alignas(16) WinCtl2 {
   uint32_t chk_cnt[KSG_RES_NCHK][2];  // checker c's drops for the pod of parity p
   uint32_t fin[KSG_RES_NCHK];         // checker c applied every commit and wrote its slots back
   uint32_t hang;                      // a wait exceeded its spin limit (a bug)
-  uint32_t pad[1];
+  uint32_t xseq;                      // pods the x-checker is done with
+  uint32_t xres[2];                   // its verdict for the pod of parity p: bit 0 x drops, bit 1 flag
+  // mailbox: the committer's decision for pod xm_seq - 1, posted as soon as the
+  // slot is known (before the table row and the commit record are written), so
+  // the x-checker's snapshot loads overlap the rest of the commit
+  uint32_t xm_seq;
+  uint32_t xm_kind, xm_slot, xm_node, xm_bnk, xm_bns;  // commit?, slot, node, list lengths before it
+  uint32_t xm_dl[4];                  // the slot's delta after it (cpu lo/hi, memory lo/hi)
+  uint32_t xn_seq, xn_node;           // earlier still: the node alone (~0u: no commit), right after the draw
+  uint32_t pad[2];
 };
 // per-slot list table: [0, 8) conflict keys, [8, 20) service ids, [20, 32) the
-// services' counts on the node at the snapshot
+// services' counts on the node at the snapshot (written by the owner checker)
 #define KSG_CL_KEY 0
 #define KSG_CL_SV 8
 #define KSG_CL_SC 20
@@ -1632,6 +1642,15 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       wm_at[q] = ok ? base + x.wcap * x.ostride * 8 + i * 4 : ~0u;
     }
     const uint32_t row_b = x.ostride * 8, row_m = x.ostride * 4;
+    uint64_t p_last = 0, p_acc = 0;  // KSG_DEBUG & 8: lanes 24..27 ring wait, loads, draw wait, the rest
+    auto pstamp = [&](uint32_t k) {
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        p_acc += lane == k ? t_now - p_last : 0ULL;
+        p_last = t_now;
+      }
+    };
+    if constexpr (STAMP) p_last = __builtin_amdgcn_s_memtime();
     for (uint32_t j = wave - KSG_RES_P0; j < n_pods; j += NPW) {
       const uint32_t e = j % RING;
       // ring entry free: the checkers applied the commit of pod j - RING (while
@@ -1648,6 +1667,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         if (j < RING || done + RING >= j + 3) break;
         __builtin_amdgcn_s_sleep(1);
       }
+      pstamp(24);
       const uint32_t rec = lane < DW ? recs[(size_t)j * DW + lane] : 0u;
       uint64_t t0[P];
       int32_t mw[P];
@@ -1673,6 +1693,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       }
       const uint32_t incl = dpp_scan_add(cnt);
       const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      pstamp(25);
       // draw index = drawable pods before j (every one of them known)
       uint32_t idx = 0;
       for (uint32_t spin = 0;; ++spin) {
@@ -1692,6 +1713,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         if (all) break;
         __builtin_amdgcn_s_sleep(1);
       }
+      pstamp(26);
       uint64_t sm = rng0 + (uint64_t)idx * 0x9E3779B97F4A7C15ULL;
       const uint64_t r = ksg_splitmix_next(&sm) >> 1;  // rand.Int() (generic_scheduler.go:94)
       uint32_t mv = 0;
@@ -1741,6 +1763,10 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         r_hdr[e].pred = pred;
         st_rel(&r_hdr[e].ready, j + 1);
       }
+      pstamp(27);
+    }
+    if constexpr (STAMP) {
+      if (lane >= 24 && lane < 28) atomicAdd(d.dbgbuf + lane, (int32_t)(p_acc / 64));
     }
     return;
   }
@@ -1977,6 +2003,150 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     if (lane == 0) st_rel(&ctl->fin[c], 1u);
     return;
   }
+  // =========================================================================
+  // x-checker (wave 1): pod i against the slot commit i-1 went into, as of that
+  // commit (the checkers' view lags a pod), while the committer finishes commit
+  // i-1 and reads pod i; also whether commit i-1 raised the pod's service's
+  // maxCount or gave it its first peer. Commit i-1 comes from the mailbox, its
+  // lists from pod i-1's ring record, earlier commits' lists from the table row.
+  // =========================================================================
+  if (wave == 1) {
+    __builtin_amdgcn_s_setprio(2);
+    // lane L < 4 evaluates one LeastRequested term: resource L & 1 (cpu, memory),
+    // at the slot's requested total now (L < 2) or at the snapshot (L >= 2)
+    const uint32_t rl = lane & 1;
+    const int64_t* const cap_src = rl ? d.cap_mem : d.cap_cpu;
+    const int64_t* const use_src = rl ? d.used_mem : d.used_cpu;
+    const double* const inv_src = rl ? d.inv10_mem : d.inv10_cpu;
+    uint64_t x_last = 0, x_acc = 0;  // KSG_DEBUG & 8: lanes 28..30 wait, check, loads
+    if constexpr (STAMP) x_last = __builtin_amdgcn_s_memtime();
+    for (uint32_t i = 0; i < n_pods; ++i) {
+      const uint32_t e = i % RING, par = i & 1;
+      bool stopped = false;
+      for (uint32_t spin = 0;; ++spin) {  // pod i-1's node drawn and pod i staged, or the end
+        if (ld_acq(&ctl->xn_seq) >= i && ld_acq(&r_hdr[e].ready) == i + 1) break;
+        if (ld_acq(&ctl->stop)) {
+          stopped = true;
+          break;
+        }
+        if (spin > 16 * KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          stopped = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (stopped) break;
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        x_acc += lane == 28 ? t_now - x_last : 0ULL;
+        x_last = t_now;
+      }
+      uint32_t res = 0;
+      const uint32_t xnode = i ? __builtin_amdgcn_readfirstlane(ctl->xn_node) : ~0u;
+      const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
+      const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
+      if (xnode != ~0u && !__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE) {
+        // the node's snapshot (in flight while the committer finishes commit i-1)
+        const uint32_t xw = d.lo + xnode;
+        const int64_t capv = gld(cap_src + xw), usev = gld(use_src + xw);
+        const double invv = gld(inv_src + xw);
+        const PodView pv = pod_view(rec);
+        const int32_t s = pv.s;
+        const int32_t xcv = gld(d.svc_cnt + (size_t)(s >= 0 ? s : 0) * d.n_nodes + xw);
+        for (uint32_t spin = 0; ld_acq(&ctl->xm_seq) < i; ++spin) {  // the rest of commit i-1
+          if (ld_acq(&ctl->stop)) {  // (the committer stopped between the draw and the mailbox)
+            stopped = true;
+            break;
+          }
+          if (spin > 16 * KSG_SPIN_LIMIT) {
+            ctl->hang = 1;
+            stopped = true;
+            break;
+          }
+        }
+        if (stopped) break;
+        const uint32_t xslot = __builtin_amdgcn_readfirstlane(ctl->xm_slot);
+        const uint32_t bnk = __builtin_amdgcn_readfirstlane(ctl->xm_bnk);
+        const uint32_t bns = __builtin_amdgcn_readfirstlane(ctl->xm_bns);
+        // the slot's delta after commit i-1, resource L & 1 ((readfirstlane returns
+        // int: widen through uint32_t, no sign extension)
+        const uint64_t dlc = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(ctl->xm_dl[1]) << 32) |
+                             (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(ctl->xm_dl[0]);
+        const uint64_t dlm = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(ctl->xm_dl[3]) << 32) |
+                             (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(ctl->xm_dl[2]);
+        // pod i-1's record: its keys and service ids follow the earlier commits' in the slot's lists
+        const uint32_t ep = (i - 1) % RING;
+        const uint32_t prec = lane < DW ? r_rec[ep * DW + lane] : 0u;
+        const uint32_t pnpp = __builtin_amdgcn_readlane(prec, WS_NPP), pnss = __builtin_amdgcn_readlane(prec, WS_NSS);
+        const uint32_t pnk = (pnpp & 0xffff) + (pnpp >> 16), pnsel = pnss & 0xffff, pns = pnss >> 16;
+        const uint32_t xnk = bnk + pnk, xns = bns + pns;
+        // lane t < 8: key t of the slot; lane 8 + u (u < 12): its service u
+        const uint32_t kt = lane - KSG_CL_KEY, ut = lane - KSG_CL_SV;
+        const bool from_row = (kt < KSG_SLOT_KEYS && kt < bnk) || (ut < KSG_SLOT_SVCS && ut < bns);
+        const uint32_t src = kt < KSG_SLOT_KEYS ? WS_IDS + (kt - bnk) : WS_IDS + pnk + pnsel + (ut - bns);
+        const uint32_t from_rec = (uint32_t)__shfl((int)prec, (int)min(src, 63u), 64);
+        const uint32_t rowv = from_row ? L_cl[(size_t)xslot * KSG_CL_W + lane] : 0u;
+        const uint32_t xcl = from_row ? rowv : from_rec;
+        const uint32_t nk = pv.nk;
+        const bool s_ent = s >= 0 && ut < xns && xcl == (uint32_t)s;
+        const uint32_t x_cnt_s = (uint32_t)__popcll(__ballot(s_ent));
+        const bool prev_has = __ballot(s_ent && ut >= bns) != 0;  // pod i-1 is a pod of service s
+        if constexpr (STAMP) {
+          const uint64_t t_now = __builtin_amdgcn_s_memtime();
+          x_acc += lane == 30 ? t_now - x_last : 0ULL;
+          x_last = t_now;
+        }
+        const int64_t reqv = rl ? pv.req_m : pv.req_c;
+        const int64_t nowv = (int64_t)((uint64_t)usev + (rl ? dlm : dlc));  // requested total now
+        bool xd = false, flag_x = false;
+        if (res_on && !pv.zero_req)  // PodFitsResources: lanes 0 and 1
+          xd = (__ballot(lane < 2 && !(capv == 0 || capv - nowv >= reqv)) & 3ULL) != 0;
+        if (d.w_lr) {  // LeastRequested: one term per lane
+          const int32_t lrv = lr_win((lane < 2 ? nowv : usev) + reqv, capv, invv);
+          const int32_t lr_now = __builtin_amdgcn_readlane(lrv, 0) + __builtin_amdgcn_readlane(lrv, 1);
+          const int32_t lr_snap = __builtin_amdgcn_readlane(lrv, 2) + __builtin_amdgcn_readlane(lrv, 3);
+          xd |= (lr_now >> 1) != (lr_snap >> 1);
+        }
+        if (x_cnt_s) {
+          const int32_t x_snapc = __builtin_amdgcn_readfirstlane(xcv);
+          if (spread_on) {  // ServiceSpreading under an unchanged maxCount: lane 0 now, lane 1 the snapshot
+            const int32_t fr = (int32_t)frac10_f32((int64_t)pv.smax - x_snapc - (lane == 0 ? (int32_t)x_cnt_s : 0),
+                                                   pv.smax);
+            xd |= __builtin_amdgcn_readlane(fr, 0) != __builtin_amdgcn_readlane(fr, 1);
+          }
+          if (prev_has) {  // commit i-1, a pod of service s: maxCount rises / first peer
+            flag_x = spread_on && x_snapc + (int32_t)x_cnt_s > pv.smax;
+            if (aff_on && (int32_t)__builtin_amdgcn_readfirstlane(r_svc[e].peer[0]) == -1 &&
+                !((L_peerset[s >> 5] >> (s & 31)) & 1u))
+              flag_x = true;
+          }
+        }
+        if (nk && xnk) {  // PodFitsPorts / NoDiskConflict: lane t holds key t
+          bool hit = false;
+          for (uint32_t b = 0; b < nk; ++b) {
+            const bool on = b < pv.n_ports ? ports_on : disk_on;
+            hit |= on && kt < xnk && xcl == (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b));
+          }
+          xd |= __ballot(hit) != 0;
+        }
+        res = (xd ? 1u : 0u) | (flag_x ? 2u : 0u);
+      }
+      if (lane == 0) {
+        ctl->xres[par] = res;
+        st_rel(&ctl->xseq, i + 1);
+      }
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        x_acc += lane == 29 ? t_now - x_last : 0ULL;
+        x_last = t_now;
+      }
+    }
+    if constexpr (STAMP) {
+      if (lane >= 28 && lane < 31) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
+    }
+    return;
+  }
   if (wave != 0) return;
 
   // =========================================================================
@@ -1988,15 +2158,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   uint32_t sk0 = 0, sk1 = 0;      // their key counts
   uint32_t ss0 = 0, ss1 = 0;      // their service entry counts
   int64_t dc0 = 0, dm0 = 0, dc1 = 0, dm1 = 0;  // their window deltas (current through the last commit)
-  uint32_t xs = KSG_NO_SLOT, xnode = 0;  // slot and node of the last commit (pod i-1)
-  uint32_t prev_nsv = 0, prev_sv = 0;    // pod i-1's services (lane t < prev_nsv)
-  // lanes 0..5 of the snapshot loads of that node: cap_c, cap_m, used_c, used_m, 10/cap_c, 10/cap_m
-  const uint64_t* const xsrc = lane == 0   ? reinterpret_cast<const uint64_t*>(d.cap_cpu)
-                               : lane == 1 ? reinterpret_cast<const uint64_t*>(d.cap_mem)
-                               : lane == 2 ? reinterpret_cast<const uint64_t*>(d.used_cpu)
-                               : lane == 3 ? reinterpret_cast<const uint64_t*>(d.used_mem)
-                               : lane == 4 ? reinterpret_cast<const uint64_t*>(d.inv10_cpu)
-                                           : reinterpret_cast<const uint64_t*>(d.inv10_mem);
+  uint32_t xnode = 0;                    // node of the last commit (pod i-1)
+  bool have_x = false;
   uint64_t t_last = 0, t_acc = 0;
 #define KSG_STAMP2(k)                                        \
   if constexpr (STAMP) {                                     \
@@ -2011,14 +2174,6 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
   for (uint32_t i = 0; i < n_pods; ++i) {
     const uint32_t e = i % RING, par = i & 1;
-    const bool have_x = xs != KSG_NO_SLOT;
-    const uint32_t xw = d.lo + (have_x ? xnode : 0u);
-    // the node and lists of commit i-1: the snapshot loaded here, unconditionally and
-    // lane by lane so it stays in a VGPR, and the slot's table row (lane t: entry t);
-    // both are first read by the re-check below (the ring, the checkers and the
-    // flags come in between)
-    const uint64_t xv = gld(xsrc + xw);
-    const uint32_t xcl = lane < KSG_CL_SC ? L_cl[(size_t)(have_x ? xs : 0u) * KSG_CL_W + lane] : 0u;
     if (ld_acq(&r_hdr[e].ready) != i + 1) {
       __builtin_amdgcn_s_setprio(0);  // a producer shares this SIMD: do not starve it
       bool hung = false;
@@ -2035,26 +2190,33 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       }
     }
     KSG_STAMP2(0)
+    // ---- the staged pod: record, header, T0 words, r mod (k0 - d) (one round of LDS reads)
     const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
+    const uint32_t rmod = r_mod[e * 64 + lane];
+    const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
+    uint64_t t0w[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) t0w[q] = t0e[lane * P + q];
     const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
     const uint32_t k0 = __builtin_amdgcn_readfirstlane(r_hdr[e].k0);
     const int32_t pred = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].pred);
-    const int32_t s = (int32_t)__builtin_amdgcn_readlane(rec, WS_SVC);
-    // svc_cnt[s][x] at the snapshot (any valid address when there is no x / s)
-    const int32_t xcv = gld(d.svc_cnt + (size_t)(s >= 0 ? s : 0) * d.n_nodes + xw);
     if (__builtin_amdgcn_readlane(rec, WS_ERR) || m0 == KSG_S32_NONE) {
       // ServiceAffinity peer error / nothing fit at the snapshot (commits only
       // remove fits): no draw, no commit
       if (lane == 0) {
         L_cm[i].kind = 0;
         L_out[i] = __builtin_amdgcn_readlane(rec, WS_ERR) ? KSG_OUT_ERROR : KSG_OUT_NOFIT;
+        ctl->xm_kind = 0;
+        ctl->xn_node = ~0u;
+        st_rel(&ctl->xm_seq, i + 1);
+        st_rel(&ctl->xn_seq, i + 1);
         st_rel(&ctl->sel_seq, i + 1);
       }
-      xs = KSG_NO_SLOT;  // pod i+1's checkers see every commit up to i-1
-      prev_nsv = 0;
+      have_x = false;  // pod i+1's checkers see every commit up to i-1
       continue;
     }
     const PodView pv = pod_view(rec);
+    const int32_t s = pv.s;
     const uint32_t nss = __builtin_amdgcn_readlane(rec, WS_NSS);
     const uint32_t n_sel = nss & 0xffff, n_svcs = nss >> 16, nk = pv.nk;
     if (__builtin_amdgcn_readlane(rec, WS_NINL) > KSG_WIN_INLINE || nk > KSG_SLOT_KEYS || n_svcs > KSG_SLOT_SVCS) {
@@ -2063,10 +2225,11 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       break;
     }
     KSG_STAMP2(1)
-    // ---- the checkers' drops for this pod (slots as of commits <= i-2)
+    // ---- the checkers' drops (slots as of commits <= i-2) and the x-checker's
+    // verdict on the slot of commit i-1
     bool hung = false;
     for (uint32_t spin = 0;; ++spin) {
-      bool done = true;
+      bool done = ld_acq(&ctl->xseq) >= i + 1;
 #pragma unroll
       for (int c = 0; c < KSG_RES_NCHK; ++c) done = done && ld_acq(&ctl->chk_seq[c]) >= i + 1;
       if (done) break;
@@ -2081,77 +2244,35 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       break;
     }
     KSG_STAMP2(2)
-    // ---- x's slot as of commit i-1 (this wave's deltas and counts, the table row)
-    const uint32_t xl = xs & 63;
-    const bool x_hi = xs >= 64;
-    const uint32_t xnk = have_x ? (uint32_t)__builtin_amdgcn_readlane((int)(x_hi ? sk1 : sk0), (int)xl) : 0u;
-    const uint32_t xns = have_x ? (uint32_t)__builtin_amdgcn_readlane((int)(x_hi ? ss1 : ss0), (int)xl) : 0u;
-    // window entries of service s on x (commit i-1 included)
-    const uint32_t x_cnt_s =
-        s >= 0 ? (uint32_t)__popcll(__ballot(lane - KSG_CL_SV < xns && xcl == (uint32_t)s)) : 0u;
-    if (s >= 0 && (spread_on || aff_on)) {
-      // a service scalar this pod reads changed in the window: by commits <= i-2
-      // (the checkers' flags) or by commit i-1 (here)
-      bool flagged = (L_flag[s >> 5] >> (s & 31)) & 1u;
-      const bool prev_has = __ballot(lane < prev_nsv && prev_sv == (uint32_t)s) != 0;
-      if (!flagged && have_x && prev_has) {
-        const int32_t x_snapc = __builtin_amdgcn_readfirstlane(xcv);
-        if (spread_on && x_snapc + (int32_t)x_cnt_s > pv.smax) flagged = true;  // maxCount rises
-        if (aff_on && (int32_t)__builtin_amdgcn_readfirstlane(r_svc[e].peer[0]) == -1 &&
-            !((L_peerset[s >> 5] >> (s & 31)) & 1u))
-          flagged = true;  // commit i-1 gave the service its first peer
-      }
-      if (flagged) {
-        resolved = i;
-        reason = KSG_STOP_SERVICE;
-        break;
-      }
-    }
-    uint32_t dropped = 0;
-#pragma unroll
-    for (int c = 0; c < KSG_RES_NCHK; ++c) dropped += __builtin_amdgcn_readfirstlane(ctl->chk_cnt[c][par]);
-    const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
+    // one round of LDS reads: drop counts, verdict, the service flag word, the drop bitmap
     uint64_t* dw = L_drop + (size_t)par * P * 64;
-    // ---- re-check x for this pod: a tie at the snapshot the checkers did not drop
+    const uint32_t cc0 = ctl->chk_cnt[0][par], cc1 = ctl->chk_cnt[1][par];
+    const uint32_t xr = ctl->xres[par];
+    const uint32_t fw = s >= 0 ? L_flag[s >> 5] : 0u;
+    uint64_t dww[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) dww[q] = dw[lane * P + q];
+    const uint32_t xres = __builtin_amdgcn_readfirstlane(xr);
+    if (s >= 0 && (spread_on || aff_on) && ((xres & 2u) || ((__builtin_amdgcn_readfirstlane(fw) >> (s & 31)) & 1u))) {
+      resolved = i;  // a service scalar this pod reads changed in the window
+      reason = KSG_STOP_SERVICE;
+      break;
+    }
+    uint32_t dropped = __builtin_amdgcn_readfirstlane(cc0) + __builtin_amdgcn_readfirstlane(cc1);
     bool x_drop = false;
-    if (have_x) {
+    if (have_x && (xres & 1u)) {  // x counts as a new drop iff it was a snapshot tie the checkers kept
+      const uint32_t xwd = xnode >> 6, xo = xwd / P, xq = xwd % P;
+      uint64_t t0x = 0, dwx = 0;
+#pragma unroll
+      for (int q = 0; q < P; ++q)
+        if ((uint32_t)q == xq) {
+          t0x = readlane64(t0w[q], (int)xo);
+          dwx = readlane64(dww[q], (int)xo);
+        }
       const uint64_t xb = 1ULL << (xnode & 63);
-      const uint64_t t0x = t0e[xnode >> 6], dwx = dw[xnode >> 6];
-      if ((t0x & xb) && !(dwx & xb)) {
-        const int64_t x_cc = (int64_t)readlane64(xv, 0), x_cm = (int64_t)readlane64(xv, 1);
-        const int64_t x_sc = (int64_t)readlane64(xv, 2), x_sm = (int64_t)readlane64(xv, 3);
-        const double x_ic = __longlong_as_double((long long)readlane64(xv, 4));
-        const double x_im = __longlong_as_double((long long)readlane64(xv, 5));
-        const int64_t dlc = (int64_t)readlane64((uint64_t)(x_hi ? dc1 : dc0), (int)xl);
-        const int64_t dlm = (int64_t)readlane64((uint64_t)(x_hi ? dm1 : dm0), (int)xl);
-        const int64_t now_c = (int64_t)((uint64_t)x_sc + (uint64_t)dlc);
-        const int64_t now_m = (int64_t)((uint64_t)x_sm + (uint64_t)dlm);
-        bool xd = false;
-        if (res_on && !pv.zero_req)  // PodFitsResources
-          xd = !((x_cc == 0 || x_cc - now_c >= pv.req_c) && (x_cm == 0 || x_cm - now_m >= pv.req_m));
-        if (d.w_lr) {  // LeastRequested
-          const int32_t lr_now = lr_win(now_c + pv.req_c, x_cc, x_ic) + lr_win(now_m + pv.req_m, x_cm, x_im);
-          const int32_t lr_snap = lr_win(x_sc + pv.req_c, x_cc, x_ic) + lr_win(x_sm + pv.req_m, x_cm, x_im);
-          xd |= (lr_now >> 1) != (lr_snap >> 1);
-        }
-        if (spread_on && x_cnt_s) {  // ServiceSpreading under an unchanged maxCount
-          const int32_t x_snapc = __builtin_amdgcn_readfirstlane(xcv);
-          xd |= frac10_f32((int64_t)pv.smax - x_snapc - (int32_t)x_cnt_s, pv.smax) !=
-                frac10_f32((int64_t)pv.smax - x_snapc, pv.smax);
-        }
-        if (nk && xnk) {  // PodFitsPorts / NoDiskConflict: table lane t holds key t
-          bool hit = false;
-          for (uint32_t b = 0; b < nk; ++b) {
-            const bool on = b < pv.n_ports ? ports_on : disk_on;
-            hit |= on && lane < xnk && xcl == (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b));
-          }
-          xd |= __ballot(hit) != 0;
-        }
-        x_drop = __builtin_amdgcn_readfirstlane((int)xd) != 0;
-      }
+      x_drop = (t0x & xb) && !(dwx & xb);
     }
     dropped += x_drop ? 1u : 0u;
-    KSG_STAMP2(3)
     if (dropped >= k0) {
       resolved = i;  // every snapshot tie got worse: needs a fresh snapshot
       reason = KSG_STOP_EXHAUSTED;
@@ -2166,7 +2287,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       KSG_COUNT2(7, 64)
       uint32_t ix;
       if (dropped < 64) {
-        ix = __builtin_amdgcn_readfirstlane(r_mod[e * 64 + dropped]);
+        ix = (uint32_t)__builtin_amdgcn_readlane((int)rmod, (int)dropped);
       } else {
         const uint64_t r = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(r_hdr[e].r >> 32)) << 32) |
                            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r_hdr[e].r);
@@ -2175,8 +2296,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       uint64_t live[P];
 #pragma unroll
       for (int q = 0; q < P; ++q) {
-        live[q] = t0e[lane * P + q] & ~dw[lane * P + q];
-        dw[lane * P + q] = 0;  // (cleared for the pod two ahead)
+        live[q] = t0w[q] & ~dww[q];
+        if (dww[q]) dw[lane * P + q] = 0;  // (cleared for the pod two ahead)
         if (x_drop && lane * P + q == (xnode >> 6)) live[q] &= ~(1ULL << (xnode & 63));
       }
       uint32_t cl = 0;
@@ -2185,12 +2306,17 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       const uint32_t incl = dpp_scan_add(cl);
       woff = select_in_lanes<P>(live, cl, incl, k - 1 - ix, lane);
     }
-    KSG_STAMP2(4)
+    if (lane == 0) {  // the x-checker loads the node's snapshot meanwhile
+      ctl->xn_node = woff;
+      st_rel(&ctl->xn_seq, i + 1);
+    }
+    KSG_STAMP2(3)
     // ---- AssumePod's slot
     const uint64_t hit0 = __ballot(cn0 == woff);
     const uint64_t hit1 = __ballot(cn1 == woff);
     const bool in_c = (hit0 | hit1) != 0;
     uint32_t slot, base_nk = 0, base_ns = 0;
+    int64_t base_dc = 0, base_dm = 0;
     if (in_c) {
       slot = hit0 ? (uint32_t)__builtin_ctzll(hit0) : 64u + (uint32_t)__builtin_ctzll(hit1);
       const uint32_t sl = slot & 63;
@@ -2201,6 +2327,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         reason = KSG_STOP_SLOT;
         break;
       }
+      base_dc = (int64_t)readlane64((uint64_t)(slot < 64 ? dc0 : dc1), (int)sl);
+      base_dm = (int64_t)readlane64((uint64_t)(slot < 64 ? dm0 : dm1), (int)sl);
     } else {
       if (n_slots == KSG_MAX_SLOTS) {
         resolved = i;
@@ -2209,8 +2337,24 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       }
       slot = n_slots++;
     }
-    // the pod's keys and service ids into the slot's table row: record lane L
-    // holds dword L, so each list entry is stored by the lane that holds it
+    const int64_t new_dc = (int64_t)((uint64_t)base_dc + (uint64_t)pv.req_c);
+    const int64_t new_dm = (int64_t)((uint64_t)base_dm + (uint64_t)pv.req_m);
+    {  // the mailbox first: the x-checker starts on pod i+1
+      const uint32_t mv = lane == 0   ? 1u
+                          : lane == 1 ? slot
+                          : lane == 2 ? woff
+                          : lane == 3 ? base_nk
+                          : lane == 4 ? base_ns
+                          : lane == 5 ? (uint32_t)new_dc
+                          : lane == 6 ? (uint32_t)((uint64_t)new_dc >> 32)
+                          : lane == 7 ? (uint32_t)new_dm
+                                      : (uint32_t)((uint64_t)new_dm >> 32);
+      if (lane < 9) (&ctl->xm_kind)[lane] = mv;
+      if (lane == 0) st_rel(&ctl->xm_seq, i + 1);
+    }
+    KSG_STAMP2(4)
+    // the slot's table row: the pod's keys and service ids (record lane L holds
+    // dword L, so each list entry is stored by the lane that holds it)
     {
       uint32_t* row = L_cl + (size_t)slot * KSG_CL_W;
       const uint32_t kt = lane - WS_IDS, st = lane - (WS_IDS + nk + n_sel);
@@ -2218,36 +2362,28 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       if (st < n_svcs) row[KSG_CL_SV + base_ns + st] = rec;
     }
     if (lane == 0) {
-      L_cm[i] = WinCommit{1u, slot, woff, (in_c ? 0u : 1u) | ((int32_t)woff == pred ? 2u : 0u)};
+      L_cm[i] = WinCommit{1u, slot, woff, (in_c ? 0u : 1u) | ((int32_t)woff == pred ? 2u : 0u) | (n_svcs << 8)};
       L_out[i] = (int32_t)(d.lo + woff);
-      st_rel(&ctl->sel_seq, i + 1);  // the checkers apply it and move on
+      st_rel(&ctl->sel_seq, i + 1);  // the checkers and the x-checker move on
     }
     if ((int32_t)woff != pred) KSG_COUNT2(8, 64)
     if (lane == (slot & 63)) {  // this wave's counts and deltas of the slot
       if (slot >= 64) {
-        if (!in_c) {
-          cn1 = woff;
-          dc1 = dm1 = 0;
-        }
-        dc1 = (int64_t)((uint64_t)dc1 + (uint64_t)pv.req_c);
-        dm1 = (int64_t)((uint64_t)dm1 + (uint64_t)pv.req_m);
+        if (!in_c) cn1 = woff;
+        dc1 = new_dc;
+        dm1 = new_dm;
         sk1 = base_nk + nk;
         ss1 = base_ns + n_svcs;
       } else {
-        if (!in_c) {
-          cn0 = woff;
-          dc0 = dm0 = 0;
-        }
-        dc0 = (int64_t)((uint64_t)dc0 + (uint64_t)pv.req_c);
-        dm0 = (int64_t)((uint64_t)dm0 + (uint64_t)pv.req_m);
+        if (!in_c) cn0 = woff;
+        dc0 = new_dc;
+        dm0 = new_dm;
         sk0 = base_nk + nk;
         ss0 = base_ns + n_svcs;
       }
     }
-    xs = slot;
+    have_x = true;
     xnode = woff;
-    prev_nsv = n_svcs;
-    prev_sv = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + (lane < n_svcs ? lane : 0u), 63u), 64);
     ++n_draws;
     KSG_STAMP2(5)
   }
