@@ -457,6 +457,18 @@ __device__ __forceinline__ uint32_t ld_acq(uint32_t* p) {
 __device__ __forceinline__ void st_rel(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// polling: relaxed LDS loads issue back to back under one lgkmcnt wait (an
+// acquire load waits for each), then one LDS-only acquire once the wait is over
+// (no vmcnt wait on the poller's loads in flight)
+__device__ __forceinline__ uint32_t ld_rlx(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void acq_lds() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }
+// a polled word as a wave-uniform (scalar) value: the wait loops branch on
+// SCC instead of juggling the exec mask
+__device__ __forceinline__ uint32_t ld_u(uint32_t* p) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)ld_rlx(p));
+}
 
 // The target-th set bit (ascending, 0-based) of the P-word-per-lane bitmap
 // `bits` (lane l owns words l*P + q), given each lane's popcount `cl` and its
@@ -1499,14 +1511,11 @@ struct alignas(16) WinCtl2 {
   uint32_t hang;                      // a wait exceeded its spin limit (a bug)
   uint32_t xseq;                      // pods the x-checker is done with
   uint32_t xres[2];                   // its verdict for the pod of parity p: bit 0 x drops, bit 1 flag
-  // mailbox: the committer's decision for pod xm_seq - 1, posted as soon as the
-  // slot is known (before the table row and the commit record are written), so
-  // the x-checker's snapshot loads overlap the rest of the commit
-  uint32_t xm_seq;
-  uint32_t xm_kind, xm_slot, xm_node, xm_bnk, xm_bns;  // commit?, slot, node, list lengths before it
-  uint32_t xm_dl[4];                  // the slot's delta after it (cpu lo/hi, memory lo/hi)
-  uint32_t xn_seq, xn_node;           // earlier still: the node alone (~0u: no commit), right after the draw
-  uint32_t pad[2];
+  // the node pod xn_seq - 1 drew (~0u: no commit), posted right after the draw
+  // so the x-checker's work overlaps the rest of the commit
+  uint32_t xn_seq, xn_node;
+  uint32_t pad[1];
+  uint32_t t_x, t_n;                  // KSG_DEBUG & 8: clock at the xres / xn posts
 };
 // per-slot list table: [0, 8) conflict keys, [8, 20) service ids, [20, 32) the
 // services' counts on the node at the snapshot (written by the owner checker)
@@ -1661,9 +1670,9 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
           ctl->hang = 1;
           return;
         }
-        uint32_t done = ld_acq(&ctl->chk_seq[0]);
+        uint32_t done = ld_acq(&ctl->xseq) + 1;  // (the x-checker of pod i reads pod i-1's entry)
 #pragma unroll
-        for (int c = 1; c < KSG_RES_NCHK; ++c) done = min(done, ld_acq(&ctl->chk_seq[c]));
+        for (int c = 0; c < KSG_RES_NCHK; ++c) done = min(done, ld_acq(&ctl->chk_seq[c]));
         if (j < RING || done + RING >= j + 3) break;
         __builtin_amdgcn_s_sleep(1);
       }
@@ -1894,8 +1903,9 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       // re-checks the slot of commit i-1 itself): it starts once commit i-2 is
       // published, a whole pod before the committer needs its drops
       for (uint32_t spin = 0;; ++spin) {
-        if (i < n_pods && ld_acq(&ctl->sel_seq) + 1 >= i && ld_acq(&r_hdr[e].ready) == i + 1) break;
-        if (ld_acq(&ctl->stop)) {
+        const uint32_t ss = ld_rlx(&ctl->sel_seq), rd = ld_rlx(&r_hdr[e].ready), st = ld_rlx(&ctl->stop);
+        if (i < n_pods && ss + 1 >= i && rd == i + 1) break;
+        if (st) {
           stopped = true;
           break;
         }
@@ -1904,8 +1914,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
           stopped = true;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
       }
+      acq_lds();
       cstamp(c == 0 ? 16 : 19);
       if (stopped) {
         // pods [0, resolved) are decided: apply the commits this checker has not
@@ -2007,8 +2017,11 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   // x-checker (wave 1): pod i against the slot commit i-1 went into, as of that
   // commit (the checkers' view lags a pod), while the committer finishes commit
   // i-1 and reads pod i; also whether commit i-1 raised the pod's service's
-  // maxCount or gave it its first peer. Commit i-1 comes from the mailbox, its
-  // lists from pod i-1's ring record, earlier commits' lists from the table row.
+  // maxCount or gave it its first peer. The x-checker follows the slots itself
+  // (the same in-order bookkeeping as the committer's: node, list lengths and
+  // delta per slot in registers), so it needs only the drawn node from the
+  // committer; commit i-1's lists come from pod i-1's ring record, earlier
+  // commits' from the table row.
   // =========================================================================
   if (wave == 1) {
     __builtin_amdgcn_s_setprio(2);
@@ -2018,14 +2031,17 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     const int64_t* const cap_src = rl ? d.cap_mem : d.cap_cpu;
     const int64_t* const use_src = rl ? d.used_mem : d.used_cpu;
     const double* const inv_src = rl ? d.inv10_mem : d.inv10_cpu;
+    uint32_t xcn0 = ~0u, xcn1 = ~0u, xsk0 = 0, xsk1 = 0, xss0 = 0, xss1 = 0, xn_slots = 0;
+    int64_t xdc0 = 0, xdm0 = 0, xdc1 = 0, xdm1 = 0;
     uint64_t x_last = 0, x_acc = 0;  // KSG_DEBUG & 8: lanes 28..30 wait, check, loads
     if constexpr (STAMP) x_last = __builtin_amdgcn_s_memtime();
     for (uint32_t i = 0; i < n_pods; ++i) {
       const uint32_t e = i % RING, par = i & 1;
       bool stopped = false;
       for (uint32_t spin = 0;; ++spin) {  // pod i-1's node drawn and pod i staged, or the end
-        if (ld_acq(&ctl->xn_seq) >= i && ld_acq(&r_hdr[e].ready) == i + 1) break;
-        if (ld_acq(&ctl->stop)) {
+        const uint32_t xn = ld_rlx(&ctl->xn_seq), rd = ld_rlx(&r_hdr[e].ready), st = ld_rlx(&ctl->stop);
+        if (xn >= i && rd == i + 1) break;
+        if (st) {
           stopped = true;
           break;
         }
@@ -2034,50 +2050,74 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
           stopped = true;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
       }
+      acq_lds();
       if (stopped) break;
       if constexpr (STAMP) {
         const uint64_t t_now = __builtin_amdgcn_s_memtime();
         x_acc += lane == 28 ? t_now - x_last : 0ULL;
         x_last = t_now;
+        if (i) x_acc += lane == 31 ? (uint64_t)(uint32_t)((uint32_t)t_now - ctl->t_n) : 0ULL;
       }
       uint32_t res = 0;
       const uint32_t xnode = i ? __builtin_amdgcn_readfirstlane(ctl->xn_node) : ~0u;
       const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
       const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
-      if (xnode != ~0u && !__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE) {
-        // the node's snapshot (in flight while the committer finishes commit i-1)
-        const uint32_t xw = d.lo + xnode;
-        const int64_t capv = gld(cap_src + xw), usev = gld(use_src + xw);
-        const double invv = gld(inv_src + xw);
-        const PodView pv = pod_view(rec);
-        const int32_t s = pv.s;
-        const int32_t xcv = gld(d.svc_cnt + (size_t)(s >= 0 ? s : 0) * d.n_nodes + xw);
-        for (uint32_t spin = 0; ld_acq(&ctl->xm_seq) < i; ++spin) {  // the rest of commit i-1
-          if (ld_acq(&ctl->stop)) {  // (the committer stopped between the draw and the mailbox)
-            stopped = true;
-            break;
-          }
-          if (spin > 16 * KSG_SPIN_LIMIT) {
-            ctl->hang = 1;
-            stopped = true;
-            break;
+      // the node's snapshot first (in flight over the bookkeeping below)
+      const bool do_check = xnode != ~0u && !__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE;
+      const PodView pv = pod_view(rec);
+      const int32_t s = pv.s;
+      const uint32_t xw = d.lo + (do_check ? xnode : 0u);
+      int64_t capv = 0, usev = 0;
+      double invv = 0.0;
+      int32_t xcv = 0;
+      if (do_check) {
+        capv = gld(cap_src + xw);
+        usev = gld(use_src + xw);
+        invv = gld(inv_src + xw);
+        xcv = gld(d.svc_cnt + (size_t)(s >= 0 ? s : 0) * d.n_nodes + xw);
+      }
+      // commit i-1 into its slot (the committer's bookkeeping, replayed)
+      uint32_t xslot = 0, bnk = 0, bns = 0;
+      uint64_t dlc = 0, dlm = 0;
+      uint32_t prec = 0;
+      if (xnode != ~0u) {
+        const uint32_t ep = (i - 1) % RING;
+        prec = lane < DW ? r_rec[ep * DW + lane] : 0u;
+        const PodView ppv = pod_view(prec);
+        const uint32_t p_svcs = (uint32_t)__builtin_amdgcn_readlane(prec, WS_NSS) >> 16;
+        const uint64_t hit0 = __ballot(xcn0 == xnode), hit1 = __ballot(xcn1 == xnode);
+        const bool in_c = (hit0 | hit1) != 0;
+        if (in_c) {
+          xslot = hit0 ? (uint32_t)__builtin_ctzll(hit0) : 64u + (uint32_t)__builtin_ctzll(hit1);
+          const uint32_t sl = xslot & 63;
+          bnk = (uint32_t)__builtin_amdgcn_readlane((int)(xslot < 64 ? xsk0 : xsk1), (int)sl);
+          bns = (uint32_t)__builtin_amdgcn_readlane((int)(xslot < 64 ? xss0 : xss1), (int)sl);
+          dlc = readlane64((uint64_t)(xslot < 64 ? xdc0 : xdc1), (int)sl);
+          dlm = readlane64((uint64_t)(xslot < 64 ? xdm0 : xdm1), (int)sl);
+        } else {
+          xslot = xn_slots < KSG_MAX_SLOTS ? xn_slots++ : 0u;  // (a full table stops the committer)
+        }
+        dlc += (uint64_t)ppv.req_c;
+        dlm += (uint64_t)ppv.req_m;
+        if (lane == (xslot & 63)) {
+          if (xslot >= 64) {
+            if (!in_c) xcn1 = xnode;
+            xsk1 = bnk + ppv.nk;
+            xss1 = bns + p_svcs;
+            xdc1 = (int64_t)dlc;
+            xdm1 = (int64_t)dlm;
+          } else {
+            if (!in_c) xcn0 = xnode;
+            xsk0 = bnk + ppv.nk;
+            xss0 = bns + p_svcs;
+            xdc0 = (int64_t)dlc;
+            xdm0 = (int64_t)dlm;
           }
         }
-        if (stopped) break;
-        const uint32_t xslot = __builtin_amdgcn_readfirstlane(ctl->xm_slot);
-        const uint32_t bnk = __builtin_amdgcn_readfirstlane(ctl->xm_bnk);
-        const uint32_t bns = __builtin_amdgcn_readfirstlane(ctl->xm_bns);
-        // the slot's delta after commit i-1, resource L & 1 ((readfirstlane returns
-        // int: widen through uint32_t, no sign extension)
-        const uint64_t dlc = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(ctl->xm_dl[1]) << 32) |
-                             (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(ctl->xm_dl[0]);
-        const uint64_t dlm = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(ctl->xm_dl[3]) << 32) |
-                             (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(ctl->xm_dl[2]);
+      }
+      if (do_check) {
         // pod i-1's record: its keys and service ids follow the earlier commits' in the slot's lists
-        const uint32_t ep = (i - 1) % RING;
-        const uint32_t prec = lane < DW ? r_rec[ep * DW + lane] : 0u;
         const uint32_t pnpp = __builtin_amdgcn_readlane(prec, WS_NPP), pnss = __builtin_amdgcn_readlane(prec, WS_NSS);
         const uint32_t pnk = (pnpp & 0xffff) + (pnpp >> 16), pnsel = pnss & 0xffff, pns = pnss >> 16;
         const uint32_t xnk = bnk + pnk, xns = bns + pns;
@@ -2134,6 +2174,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       }
       if (lane == 0) {
         ctl->xres[par] = res;
+        if constexpr (STAMP) ctl->t_x = (uint32_t)__builtin_amdgcn_s_memtime();
         st_rel(&ctl->xseq, i + 1);
       }
       if constexpr (STAMP) {
@@ -2143,7 +2184,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       }
     }
     if constexpr (STAMP) {
-      if (lane >= 28 && lane < 31) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
+      if (lane >= 28 && lane < 32) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
     }
     return;
   }
@@ -2206,9 +2247,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       if (lane == 0) {
         L_cm[i].kind = 0;
         L_out[i] = __builtin_amdgcn_readlane(rec, WS_ERR) ? KSG_OUT_ERROR : KSG_OUT_NOFIT;
-        ctl->xm_kind = 0;
         ctl->xn_node = ~0u;
-        st_rel(&ctl->xm_seq, i + 1);
         st_rel(&ctl->xn_seq, i + 1);
         st_rel(&ctl->sel_seq, i + 1);
       }
@@ -2229,21 +2268,24 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     // verdict on the slot of commit i-1
     bool hung = false;
     for (uint32_t spin = 0;; ++spin) {
-      bool done = ld_acq(&ctl->xseq) >= i + 1;
+      const uint32_t xs = ld_rlx(&ctl->xseq), hg = ld_rlx(&ctl->hang);
+      uint32_t cs = ld_rlx(&ctl->chk_seq[0]);
 #pragma unroll
-      for (int c = 0; c < KSG_RES_NCHK; ++c) done = done && ld_acq(&ctl->chk_seq[c]) >= i + 1;
-      if (done) break;
-      if (spin > 16 * KSG_SPIN_LIMIT || ld_acq(&ctl->hang)) {
+      for (int c = 1; c < KSG_RES_NCHK; ++c) cs = min(cs, ld_rlx(&ctl->chk_seq[c]));
+      if (xs >= i + 1 && cs >= i + 1) break;
+      if (spin > 16 * KSG_SPIN_LIMIT || hg) {
         hung = true;
         break;
       }
     }
+    acq_lds();
     if (hung) {
       resolved = i;
       reason = KSG_STOP_HANG;
       break;
     }
     KSG_STAMP2(2)
+    if constexpr (STAMP) t_acc += lane == 6 ? (uint64_t)(uint32_t)((uint32_t)t_last - ctl->t_x) : 0ULL;
     // one round of LDS reads: drop counts, verdict, the service flag word, the drop bitmap
     uint64_t* dw = L_drop + (size_t)par * P * 64;
     const uint32_t cc0 = ctl->chk_cnt[0][par], cc1 = ctl->chk_cnt[1][par];
@@ -2308,6 +2350,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     }
     if (lane == 0) {  // the x-checker loads the node's snapshot meanwhile
       ctl->xn_node = woff;
+      if constexpr (STAMP) ctl->t_n = (uint32_t)__builtin_amdgcn_s_memtime();
       st_rel(&ctl->xn_seq, i + 1);
     }
     KSG_STAMP2(3)
@@ -2339,19 +2382,6 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     }
     const int64_t new_dc = (int64_t)((uint64_t)base_dc + (uint64_t)pv.req_c);
     const int64_t new_dm = (int64_t)((uint64_t)base_dm + (uint64_t)pv.req_m);
-    {  // the mailbox first: the x-checker starts on pod i+1
-      const uint32_t mv = lane == 0   ? 1u
-                          : lane == 1 ? slot
-                          : lane == 2 ? woff
-                          : lane == 3 ? base_nk
-                          : lane == 4 ? base_ns
-                          : lane == 5 ? (uint32_t)new_dc
-                          : lane == 6 ? (uint32_t)((uint64_t)new_dc >> 32)
-                          : lane == 7 ? (uint32_t)new_dm
-                                      : (uint32_t)((uint64_t)new_dm >> 32);
-      if (lane < 9) (&ctl->xm_kind)[lane] = mv;
-      if (lane == 0) st_rel(&ctl->xm_seq, i + 1);
-    }
     KSG_STAMP2(4)
     // the slot's table row: the pod's keys and service ids (record lane L holds
     // dword L, so each list entry is stored by the lane that holds it)
@@ -2433,6 +2463,1031 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
 }
 
 // ---------------------------------------------------------------------------
+// phase B, pre-selecting resolver (every configuration without
+// ServiceAntiAffinity)
+// ---------------------------------------------------------------------------
+// The sequential chain per pod is cut to the committer's own work: a re-check
+// of one node, a choice between three staged candidates, and the commit.
+//  CHECKERS (waves 4, 5; lane l of checker c watches slot 64c + l) test pod i
+//    as soon as commit i-2 is published, against the slot state in LDS — which
+//    the committer keeps current, so there is nothing to apply. A slot read
+//    while commit i-1 is being written into it may show part of that commit:
+//    every test is monotone in each part (a commit only adds requested totals,
+//    keys and service entries), so the drops found lie between the exact drops
+//    as of commit i-2 and as of commit i-1, and the committer's re-check of
+//    commit i-1's node completes them.
+//  PRE-SELECTORS (waves 1, 2: even and odd pods), once the checkers are done
+//    with pod i: the live ties L0 = T0 minus their d drops, k' = k0 - d, and the
+//    three nodes the draw can land on: A = the (r mod k')-th of L0 from the top
+//    (nothing more drops) and B0, B1 = the (r mod (k'-1))-th from the top and
+//    the one after it (commit i-1's node x drops too: the answer is B0 when x
+//    ranks above it, else B1); which of pod i-1's candidates are in L0; then
+//    the three nodes' snapshots and the pod's service counts on them.
+//  FLAGGER (wave 3) applies each commit's service flags (maxCount rises, first
+//    peers) in commit order, a pod before any later pod reads them.
+//  COMMITTER (wave 0) re-checks x for pod i (x's snapshot came with the
+//    candidate it was drawn from; its window delta and lists are the
+//    committer's own), picks A, B0 or B1, and writes the commit into the slot
+//    state.
+//  PRODUCERS (the other waves) stage pods ahead into the ring, as above.
+// threads: 16 waves (10 producers) while the registers allow, else 8 (2 producers)
+__host__ __device__ constexpr uint32_t win3_nt(uint32_t P) { return P <= 8 ? 1024u : 512u; }
+#define KSG_R3_FL 3  // flagger wave
+#define KSG_R3_C0 4  // first checker wave
+#define KSG_R3_P0 (KSG_R3_C0 + KSG_RES_NCHK)  // first producer wave
+#define KSG_CS_OK 0
+#define KSG_CS_NOFIT 1
+#define KSG_CS_ERROR 2
+#define KSG_CS_OVERSIZE 3
+#define KSG_NO_NODE 0xffffffffu
+
+struct alignas(16) RingHdr3 {
+  int32_t m0;
+  uint32_t k0;
+  uint64_t r;  // Int63 draw of the pod
+  uint32_t ready;
+  uint32_t drawable;
+  uint32_t pad[2];
+};
+struct alignas(16) RingSvc3 {  // per service entry t of the pod (t < n_svcs)
+  int32_t max[KSG_SLOT_SVCS];   // svc_max[sv] at the snapshot
+  int32_t peer[KSG_SLOT_SVCS];  // svc_peer[sv] at the snapshot
+};
+struct alignas(16) WinCommit3 {
+  uint32_t kind;  // 0: no commit (error / no fit), 1: commit
+  uint32_t slot, node;
+  uint32_t svc;   // service entries of the slot before the commit | the pod's service count << 16
+};
+struct alignas(16) WinCtl3 {
+  uint32_t stop;      // the committer is done: pods [0, resolved) are decided
+  uint32_t resolved;
+  uint32_t sel_seq;   // commits published for pods [0, sel_seq)
+  uint32_t psel_seq;  // pods the pre-selector is done with
+  uint32_t chk_seq[KSG_RES_NCHK];     // pods checker c is done with
+  uint32_t chk_cnt[KSG_RES_NCHK][2];  // checker c's drops for the pod of parity p
+  uint32_t fin[KSG_RES_NCHK];         // checker c wrote its slots back
+  uint32_t fin_p;                     // the flagger applied every commit's first peers
+  uint32_t hang;                      // a wait exceeded its spin limit (a bug)
+  uint32_t n_peer;                    // first service peers recorded (L_peer entries)
+  uint32_t flag_seq;                  // commits [0, flag_seq) have had their flags applied
+  uint32_t csnap_seq[2];              // pod + 1 whose candidates' snapshots are staged, by parity
+  uint32_t pad0[2];
+  // the pre-selector's verdict for the pod of parity p
+  uint32_t c_status[2], c_kp[2], c_a[2], c_b0[2], c_b1[2];
+  uint32_t c_xlive[2];  // bit j: pod i-1's candidate j is a live tie of pod i (in T0, not dropped)
+};
+
+struct WinLdsOff3 {
+  uint32_t ctl, r_hdr, r_t0, r_rec, r_mod, r_svc;
+  uint32_t cm, out, peer, flag, peerset, drop, pub, drw;
+  uint32_t s_meta, s_dl, s_cap, s_snp, s_inv, s_keys, s_svcs, s_sc, csnap, csc;
+  uint32_t total;
+};
+
+__host__ __device__ inline WinLdsOff3 win3_lds_offsets(uint32_t P, uint32_t nflag, uint32_t W) {
+  WinLdsOff3 o;
+  const uint32_t R = win_ring(P);
+  uint32_t at = 0;
+  o.ctl = at;     at += win_al16(sizeof(WinCtl3));
+  o.r_hdr = at;   at += win_al16((size_t)R * sizeof(RingHdr3));
+  o.r_t0 = at;    at += win_al16((size_t)R * P * 64 * 8);
+  o.r_rec = at;   at += win_al16((size_t)R * KSG_WIN_SUM_DWORDS * 4);
+  o.r_mod = at;   at += win_al16((size_t)R * 64 * 4);
+  o.r_svc = at;   at += win_al16((size_t)R * sizeof(RingSvc3));
+  o.cm = at;      at += win_al16((size_t)W * sizeof(WinCommit3));
+  o.out = at;     at += win_al16((size_t)W * 4);
+  o.peer = at;    at += win_al16((size_t)W * 2 * 4);
+  o.flag = at;    at += win_al16((size_t)nflag * 4);
+  o.peerset = at; at += win_al16((size_t)nflag * 4);
+  o.drop = at;    at += win_al16((size_t)2 * P * 64 * 8);
+  o.pub = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
+  o.drw = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
+  o.s_meta = at;  at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(SlotMeta));
+  o.s_dl = at;    at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(I64x2));
+  o.s_cap = at;   at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(I64x2));
+  o.s_snp = at;   at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(I64x2));
+  o.s_inv = at;   at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(F64x2));
+  o.s_keys = at;  at += win_al16((size_t)KSG_MAX_SLOTS * KSG_SLOT_KEYS * 4);
+  o.s_svcs = at;  at += win_al16((size_t)KSG_MAX_SLOTS * KSG_SLOT_SVCS * 4);
+  o.s_sc = at;    at += win_al16((size_t)KSG_MAX_SLOTS * KSG_SLOT_SVCS * 4);
+  o.csnap = at;   at += win_al16((size_t)2 * 18 * 8);   // [parity][candidate][cap c/m, used c/m, 10/cap c/m]
+  o.csc = at;     at += win_al16((size_t)2 * 36 * 4);   // [parity][candidate][service t]: svc_cnt on the node
+  o.total = at;
+  return o;
+}
+
+template <int P, bool STAMP>
+__global__ __launch_bounds__(win3_nt(P)) void ksg_win_resolve3_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
+                                                               const KsgWinSum* __restrict__ sums,
+                                                               const KsgWinXchg x, uint64_t* rng_io,
+                                                               int32_t* __restrict__ out_batch) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t pos = run->pos, n_batch = run->n;
+  if (run->halt || pos >= n_batch) return;  // the chain is done (uniform, before any barrier)
+  const uint32_t n_pods = min(wcap, n_batch - pos);
+  int32_t* __restrict__ out = out_batch + pos;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t nflag = (d.n_services + 31) / 32;
+  const uint32_t nwords = d.nwords;
+  constexpr uint32_t RING = win_ring(P);
+  constexpr uint32_t NT = win3_nt(P);
+  constexpr uint32_t NPW = NT / 64 - KSG_R3_P0;  // producer waves
+  constexpr uint32_t DW = KSG_WIN_SUM_DWORDS;
+  constexpr uint32_t PW = P * 64;                 // bitmap words per pod
+  const WinLdsOff3 o = win3_lds_offsets(P, nflag, wcap);
+  WinCtl3* ctl = reinterpret_cast<WinCtl3*>(smem + o.ctl);
+  RingHdr3* r_hdr = reinterpret_cast<RingHdr3*>(smem + o.r_hdr);
+  uint64_t* r_t0 = reinterpret_cast<uint64_t*>(smem + o.r_t0);
+  uint32_t* r_rec = reinterpret_cast<uint32_t*>(smem + o.r_rec);
+  uint32_t* r_mod = reinterpret_cast<uint32_t*>(smem + o.r_mod);
+  RingSvc3* r_svc = reinterpret_cast<RingSvc3*>(smem + o.r_svc);
+  WinCommit3* L_cm = reinterpret_cast<WinCommit3*>(smem + o.cm);
+  int32_t* L_out = reinterpret_cast<int32_t*>(smem + o.out);
+  uint32_t* L_peer = reinterpret_cast<uint32_t*>(smem + o.peer);
+  uint32_t* L_flag = reinterpret_cast<uint32_t*>(smem + o.flag);
+  uint32_t* L_peerset = reinterpret_cast<uint32_t*>(smem + o.peerset);
+  uint64_t* L_drop = reinterpret_cast<uint64_t*>(smem + o.drop);  // [2][PW] by pod parity
+  uint32_t* L_pub = reinterpret_cast<uint32_t*>(smem + o.pub);
+  uint32_t* L_drw = reinterpret_cast<uint32_t*>(smem + o.drw);
+  SlotMeta* s_meta = reinterpret_cast<SlotMeta*>(smem + o.s_meta);
+  I64x2* s_dl = reinterpret_cast<I64x2*>(smem + o.s_dl);
+  I64x2* s_cap = reinterpret_cast<I64x2*>(smem + o.s_cap);
+  I64x2* s_snp = reinterpret_cast<I64x2*>(smem + o.s_snp);
+  F64x2* s_inv = reinterpret_cast<F64x2*>(smem + o.s_inv);
+  uint32_t* s_keys = reinterpret_cast<uint32_t*>(smem + o.s_keys);
+  uint32_t* s_svcs = reinterpret_cast<uint32_t*>(smem + o.s_svcs);
+  int32_t* s_sc = reinterpret_cast<int32_t*>(smem + o.s_sc);
+  int64_t* L_csnap = reinterpret_cast<int64_t*>(smem + o.csnap);
+  int32_t* L_csc = reinterpret_cast<int32_t*>(smem + o.csc);
+  const bool spread_on = d.w_spread != 0;
+  const bool aff_on = (d.preds & KSG_PRED_SERVICEAFFINITY) && d.n_aff > 0;
+  const bool res_on = (d.preds & KSG_PRED_PODFITSRESOURCES) != 0;
+  const bool ports_on = (d.preds & KSG_PRED_PODFITSPORTS) != 0;
+  const bool disk_on = (d.preds & KSG_PRED_NODISKCONFLICT) != 0;
+  const uint32_t nbits = (wcap + 31) / 32;
+
+  for (uint32_t t = tid; t < RING; t += NT) r_hdr[t].ready = 0;
+  if (tid == 0) *ctl = WinCtl3{};
+  for (uint32_t w = tid; w < nflag; w += NT) {
+    L_flag[w] = 0;
+    L_peerset[w] = 0;
+  }
+  for (uint32_t w = tid; w < nbits; w += NT) {
+    L_pub[w] = 0;
+    L_drw[w] = 0;
+  }
+  for (uint32_t w = tid; w < 2 * PW; w += NT) L_drop[w] = 0;
+  for (uint32_t t = tid; t < KSG_MAX_SLOTS; t += NT) s_meta[t] = SlotMeta{KSG_NO_NODE, 0u, 0u, 0u};
+  __syncthreads();
+  const uint64_t rng0 = *rng_io;
+
+  // =========================================================================
+  // producers
+  // =========================================================================
+  if (wave >= KSG_R3_P0) {
+    const uint32_t* recs = reinterpret_cast<const uint32_t*>(sums);
+    uint32_t wb_at[P], wm_at[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      const uint32_t wq = lane * P + q;
+      uint32_t g = 0;
+      for (uint32_t r = 1; r < x.world; ++r)
+        if (wq >= x.wlo[r] && x.nw[r] > 0) g = r;
+      const uint32_t i = wq - x.wlo[g];
+      const bool ok = wq < nwords && i < x.nw[g];
+      const uint32_t base = (uint32_t)(g * x.blk);
+      wb_at[q] = ok ? base + i * 8 : ~0u;
+      wm_at[q] = ok ? base + x.wcap * x.ostride * 8 + i * 4 : ~0u;
+    }
+    const uint32_t row_b = x.ostride * 8, row_m = x.ostride * 4;
+    uint64_t p_last = 0, p_acc = 0;  // KSG_DEBUG & 8: lanes 24..27 ring wait, loads, draw wait, the rest
+    auto pstamp = [&](uint32_t k) {
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        p_acc += lane == k ? t_now - p_last : 0ULL;
+        p_last = t_now;
+      }
+    };
+    if constexpr (STAMP) p_last = __builtin_amdgcn_s_memtime();
+    for (uint32_t j = wave - KSG_R3_P0; j < n_pods; j += NPW) {
+      const uint32_t e = j % RING;
+      // ring entry free: pod j - RING is done with (the checkers of pod j - RING + 2
+      // imply the committer is past it; the pre-selectors and the flagger are past it)
+      for (uint32_t spin = 0;; ++spin) {
+        const uint32_t st = ld_u(&ctl->stop);
+        uint32_t done = min(ld_u(&ctl->psel_seq), ld_u(&ctl->flag_seq) + 2);
+#pragma unroll
+        for (int c = 0; c < KSG_RES_NCHK; ++c) done = min(done, ld_u(&ctl->chk_seq[c]));
+        if (st) return;
+        if (j < RING || done + RING >= j + 3) break;
+        if (spin > KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      acq_lds();
+      pstamp(24);
+      const uint32_t rec = lane < DW ? recs[(size_t)j * DW + lane] : 0u;
+      uint64_t t0[P];
+      int32_t mw[P];
+      int32_t lm = KSG_S32_NONE;
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        t0[q] = wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + j * row_b) : 0ULL;
+        mw[q] = wm_at[q] != ~0u ? *reinterpret_cast<const int32_t*>(x.buf + wm_at[q] + j * row_m) : KSG_S32_NONE;
+        lm = mw[q] > lm ? mw[q] : lm;
+      }
+      const int32_t m0 = wave_total_max(lm);
+      const bool drawable = __builtin_amdgcn_readlane(rec, WS_ERR) == 0 && m0 != KSG_S32_NONE;
+      const uint32_t wj = j >> 5, bj = 1u << (j & 31);
+      if (lane == 0) {  // the drawable bit first, then "known" (readers read them in that order)
+        if (drawable) atomicOr(&L_drw[wj], bj);
+        atomicOr(&L_pub[wj], bj);
+      }
+      uint32_t cnt = 0;
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        t0[q] = (m0 != KSG_S32_NONE && mw[q] == m0) ? t0[q] : 0ULL;
+        cnt += __popcll(t0[q]);
+      }
+      const uint32_t k0 = wave_total_add(cnt);
+      const uint32_t n_svcs = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NSS) >> 16;
+      const uint32_t nk = ((uint32_t)__builtin_amdgcn_readlane(rec, WS_NPP) & 0xffff) +
+                          ((uint32_t)__builtin_amdgcn_readlane(rec, WS_NPP) >> 16);
+      const uint32_t n_sel = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NSS) & 0xffff;
+      const bool inl = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NINL) <= KSG_WIN_INLINE && n_svcs <= KSG_SLOT_SVCS;
+      const uint32_t t_sv = lane < n_svcs ? lane : 0u;
+      const uint32_t my_sv = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + t_sv, 63u), 64);
+      int32_t s_max = 0, s_peer = 0;
+      if (drawable && inl && lane < n_svcs) {  // the pod's services' scalars (in flight over the draw wait)
+        s_max = d.svc_max[my_sv];
+        s_peer = d.svc_peer[my_sv];
+      }
+      pstamp(25);
+      // draw index = drawable pods before j (every one of them known)
+      uint32_t idx = 0;
+      for (uint32_t spin = 0;; ++spin) {
+        if (ld_acq(&ctl->stop)) return;
+        if (spin > KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          return;
+        }
+        bool all = true;
+        idx = 0;
+        for (uint32_t w = 0; w <= wj; ++w) {
+          const uint32_t mask = w < wj ? ~0u : bj - 1u;
+          const uint32_t pub = __builtin_amdgcn_readfirstlane(ld_acq(&L_pub[w]));
+          all = all && (pub & mask) == mask;
+          idx += __popc(__builtin_amdgcn_readfirstlane(L_drw[w]) & mask);
+        }
+        if (all) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      pstamp(26);
+      uint64_t sm = rng0 + (uint64_t)idx * 0x9E3779B97F4A7C15ULL;
+      const uint64_t r = ksg_splitmix_next(&sm) >> 1;  // rand.Int() (generic_scheduler.go:94)
+      uint32_t mv = 0;
+      if (drawable && lane < k0) mv = umod64_32(r, k0 - lane);
+      r_mod[e * 64 + lane] = mv;
+      if (lane < DW) r_rec[e * DW + lane] = rec;
+#pragma unroll
+      for (int q = 0; q < P; ++q) r_t0[(size_t)e * PW + lane * P + q] = t0[q];
+      if (inl && lane < n_svcs) {
+        r_svc[e].max[lane] = s_max;
+        r_svc[e].peer[lane] = s_peer;
+      }
+      if (lane == 0) {
+        r_hdr[e].m0 = m0;
+        r_hdr[e].k0 = k0;
+        r_hdr[e].r = r;
+        r_hdr[e].drawable = drawable;
+        st_rel(&r_hdr[e].ready, j + 1);
+      }
+      pstamp(27);
+    }
+    if constexpr (STAMP) {
+      if (lane >= 24 && lane < 28) atomicAdd(d.dbgbuf + lane, (int32_t)(p_acc / 64));
+    }
+    return;
+  }
+
+  // =========================================================================
+  // checkers (waves KSG_RES_C0 ..): lane l of checker c watches slot 64c + l
+  // =========================================================================
+  if (wave >= KSG_R3_C0) {
+    __builtin_amdgcn_s_setprio(2);
+    const uint32_t c = wave - KSG_R3_C0;
+    const uint32_t my_slot = c * 64 + lane;
+    const uint32_t* my_keys = s_keys + (size_t)my_slot * KSG_SLOT_KEYS;
+    const uint32_t* my_svcs = s_svcs + (size_t)my_slot * KSG_SLOT_SVCS;
+    const int32_t* my_sc = s_sc + (size_t)my_slot * KSG_SLOT_SVCS;
+    // the slot's node and snapshot, cached once the committer has created it
+    uint32_t node = KSG_NO_NODE;
+    int64_t cap_c = 0, cap_m = 0, snp_c = 0, snp_m = 0;
+    double inv_c = 0.0, inv_m = 0.0;
+    uint64_t t_last = 0, t_acc = 0;
+    auto cstamp = [&](uint32_t k) {
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        t_acc += lane == k ? t_now - t_last : 0ULL;
+        t_last = t_now;
+      }
+    };
+    if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
+    for (uint32_t i = 0;; ++i) {
+      const uint32_t e = i % RING, par = i & 1;
+      bool stopped = false;
+      // pod i is checked once commit i-2 is published
+      for (uint32_t spin = 0;; ++spin) {
+        const uint32_t ss = ld_u(&ctl->sel_seq), rd = ld_u(&r_hdr[e].ready), st = ld_u(&ctl->stop);
+        if (i < n_pods && ss + 1 >= i && rd == i + 1) break;
+        if (st) {
+          stopped = true;
+          break;
+        }
+        if (spin > 16 * KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          stopped = true;
+          break;
+        }
+      }
+      acq_lds();
+      if (stopped) break;
+      cstamp(c == 0 ? 16 : 19);
+      if (node == KSG_NO_NODE) {
+        const uint32_t nd = __hip_atomic_load(&s_meta[my_slot].node, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (nd != KSG_NO_NODE) {  // created (its snapshot was written before the node)
+          cap_c = s_cap[my_slot].c;
+          cap_m = s_cap[my_slot].m;
+          snp_c = s_snp[my_slot].c;
+          snp_m = s_snp[my_slot].m;
+          inv_c = s_inv[my_slot].c;
+          inv_m = s_inv[my_slot].m;
+          node = nd;
+        }
+      }
+      cstamp(c == 0 ? 17 : 20);
+      const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
+      const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
+      uint32_t cntd = 0;
+      if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE) {
+        const PodView pv = pod_view(rec);
+        bool drop = false;
+        if (node != KSG_NO_NODE) {
+          const uint64_t* t0e = r_t0 + (size_t)e * PW;
+          if ((t0e[node >> 6] >> (node & 63)) & 1ULL) {
+            // does the slot (a snapshot tie of the pod) score below M0 now?
+            const int64_t dl_c = s_dl[my_slot].c, dl_m = s_dl[my_slot].m;
+            const uint32_t m_nk = __hip_atomic_load(&s_meta[my_slot].nk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t m_ns = __hip_atomic_load(&s_meta[my_slot].ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t m_smask = s_meta[my_slot].smask;
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            const int64_t now_c = (int64_t)((uint64_t)snp_c + (uint64_t)dl_c);
+            const int64_t now_m = (int64_t)((uint64_t)snp_m + (uint64_t)dl_m);
+            if (res_on && !pv.zero_req)  // PodFitsResources (predicates.go:127-145)
+              drop = !((cap_c == 0 || cap_c - now_c >= pv.req_c) && (cap_m == 0 || cap_m - now_m >= pv.req_m));
+            if (d.w_lr) {  // LeastRequested (priorities.go:43-76) can only fall as requested grows
+              const int32_t lr_now = lr_win(now_c + pv.req_c, cap_c, inv_c) + lr_win(now_m + pv.req_m, cap_m, inv_m);
+              const int32_t lr_snap = lr_win(snp_c + pv.req_c, cap_c, inv_c) + lr_win(snp_m + pv.req_m, cap_m, inv_m);
+              drop |= (lr_now >> 1) != (lr_snap >> 1);
+            }
+            if (!drop && pv.nk && m_nk) {  // PodFitsPorts / NoDiskConflict vs the window's keys
+              for (uint32_t a = 0; a < m_nk; ++a) {
+                const uint32_t key = my_keys[a];
+                for (uint32_t b = 0; b < pv.nk; ++b) {
+                  const bool on = b < pv.n_ports ? ports_on : disk_on;
+                  drop |= on && (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b)) == key;
+                }
+              }
+            }
+            if (!drop && spread_on && pv.s >= 0 && ((m_smask >> (pv.s & 31)) & 1u)) {
+              // ServiceSpreading (spreading.go:72-86) under an unchanged maxCount
+              int32_t delta = 0, snapc = 0;
+              for (uint32_t a = 0; a < m_ns; ++a)
+                if (my_svcs[a] == (uint32_t)pv.s) {
+                  snapc = my_sc[a];
+                  ++delta;
+                }
+              if (delta)
+                drop = frac10_f32((int64_t)pv.smax - snapc - delta, pv.smax) !=
+                       frac10_f32((int64_t)pv.smax - snapc, pv.smax);
+            }
+            if (drop)
+              atomicOr(reinterpret_cast<unsigned long long*>(L_drop + (size_t)par * PW + (node >> 6)),
+                       1ULL << (node & 63));
+          }
+        }
+        cntd = __popcll(__ballot(drop));
+      }
+      if (lane == 0) {
+        ctl->chk_cnt[c][par] = cntd;
+        st_rel(&ctl->chk_seq[c], i + 1);
+      }
+      cstamp(c == 0 ? 18 : 21);
+    }
+    // the committer is done (it wrote every commit before it set stop): write
+    // the window's deltas of this checker's slots back to HBM (the next snapshot)
+    const uint32_t nd = s_meta[my_slot].node;
+    if (nd != KSG_NO_NODE) {
+      const uint32_t n = d.lo + nd;
+      const uint32_t m_nk = s_meta[my_slot].nk, m_ns = s_meta[my_slot].ns;
+      d.used_cpu[n] = (int64_t)((uint64_t)s_snp[my_slot].c + (uint64_t)s_dl[my_slot].c);
+      d.used_mem[n] = (int64_t)((uint64_t)s_snp[my_slot].m + (uint64_t)s_dl[my_slot].m);
+      for (uint32_t a = 0; a < m_nk; ++a)
+        __hip_atomic_fetch_or(d.keymap + (size_t)my_keys[a] * d.nw + (n >> 6), 1ULL << (n & 63), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+      for (uint32_t a = 0; a < m_ns; ++a) {
+        const uint32_t sa = my_svcs[a];
+        bool first = true;
+        int32_t count = 0;
+        for (uint32_t b = 0; b < m_ns; ++b) {
+          if (my_svcs[b] == sa) {
+            if (b < a) first = false;
+            ++count;
+          }
+        }
+        __hip_atomic_fetch_add(d.svc_total + sa, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (first) {
+          const int32_t fin = my_sc[a] + count;
+          d.svc_cnt[(size_t)sa * d.n_nodes + n] = fin;
+          __hip_atomic_fetch_max(d.svc_max + sa, fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    if constexpr (STAMP) {
+      if (lane >= 16 && lane < 22) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
+    }
+    drain_stores();
+    if (lane == 0) st_rel(&ctl->fin[c], 1u);
+    return;
+  }
+
+  // =========================================================================
+  // flagger (wave 3): the service flags later pods stop on (maxCount rises,
+  // first peer) and the first peers, of each commit in commit order
+  // =========================================================================
+  if (wave == KSG_R3_FL) {
+    __builtin_amdgcn_s_setprio(2);
+    auto apply_flags = [&](uint32_t q) {
+      const uint32_t kind = __builtin_amdgcn_readfirstlane(L_cm[q].kind);
+      const uint32_t svw = __builtin_amdgcn_readfirstlane(L_cm[q].svc);
+      const uint32_t n_svcs = svw >> 16, bns = svw & 0xffff;
+      if (kind != 1 || n_svcs == 0) return;
+      const uint32_t slot = __builtin_amdgcn_readfirstlane(L_cm[q].slot);
+      const uint32_t wn = d.lo + __builtin_amdgcn_readfirstlane(L_cm[q].node);
+      const uint32_t eq = q % RING;
+      const uint32_t prec = lane < DW ? r_rec[eq * DW + lane] : 0u;
+      const uint32_t npp = __builtin_amdgcn_readlane(prec, WS_NPP), nss = __builtin_amdgcn_readlane(prec, WS_NSS);
+      const uint32_t nk = (npp & 0xffff) + (npp >> 16), n_sel = nss & 0xffff;
+      const bool sv_lane = lane < n_svcs;
+      const uint32_t my_sv =
+          (uint32_t)__shfl((int)prec, (int)min(WS_IDS + nk + n_sel + (sv_lane ? lane : 0u), 63u), 64);
+      int32_t mx = 0, peer = 0, sc = 0;
+      if (sv_lane) {
+        mx = r_svc[eq].max[lane];
+        peer = r_svc[eq].peer[lane];
+        sc = s_sc[(size_t)slot * KSG_SLOT_SVCS + bns + lane];
+      }
+      // entries of each service on the node through this commit (the list may
+      // have grown since: only the first bns + n_svcs count)
+      const uint32_t ent = lane < bns + n_svcs ? s_svcs[(size_t)slot * KSG_SLOT_SVCS + lane] : ~0u;
+      uint32_t through = 0;
+      for (uint32_t t = 0; t < n_svcs; ++t) {
+        const uint32_t sv_t = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)t);
+        const uint32_t b_t = (uint32_t)__popcll(__ballot(ent == sv_t));
+        if (lane == t) through = b_t;
+      }
+      bool changed = sv_lane && aff_on && peer == -1 && !((L_peerset[my_sv >> 5] >> (my_sv & 31)) & 1u);
+      uint64_t pm = __ballot(sv_lane && peer == -1);
+      if (pm) {  // first commit of a service with no peer yet: its first peer, in commit order
+        uint32_t n_peer = __builtin_amdgcn_readfirstlane(ctl->n_peer);
+        while (pm) {
+          const uint32_t b = __builtin_ctzll(pm);
+          pm &= pm - 1;
+          const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)b);
+          if (!((L_peerset[fsv >> 5] >> (fsv & 31)) & 1u)) {
+            if (lane == 0) {
+              L_peerset[fsv >> 5] |= 1u << (fsv & 31);
+              L_peer[2 * n_peer] = fsv;
+              L_peer[2 * n_peer + 1] = wn;
+            }
+            ++n_peer;
+            lds_fence();
+          }
+        }
+        if (lane == 0) ctl->n_peer = n_peer;
+      }
+      if (sv_lane && spread_on && sc + (int32_t)through > mx) changed = true;  // maxCount rises
+      if (changed) atomicOr(&L_flag[my_sv >> 5], 1u << (my_sv & 31));
+    };
+    uint64_t f_last = 0, f_acc = 0;  // KSG_DEBUG & 8: lanes 22, 23 wait, apply
+    if constexpr (STAMP) f_last = __builtin_amdgcn_s_memtime();
+    for (uint32_t q = 0;; ++q) {
+      bool done = false;
+      for (uint32_t spin = 0;; ++spin) {  // commit q published, or the committer done before it
+        const uint32_t ss = ld_u(&ctl->sel_seq), st = ld_u(&ctl->stop);
+        if (ss >= q + 1) break;
+        if (st) {
+          acq_lds();
+          done = ld_u(&ctl->sel_seq) < q + 1;
+          if (done) break;
+        }
+        if (spin > 16 * KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          done = true;
+          break;
+        }
+      }
+      acq_lds();
+      if (done) break;
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        f_acc += lane == 22 ? t_now - f_last : 0ULL;
+        f_last = t_now;
+      }
+      apply_flags(q);
+      if (lane == 0) st_rel(&ctl->flag_seq, q + 1);
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        f_acc += lane == 23 ? t_now - f_last : 0ULL;
+        f_last = t_now;
+      }
+    }
+    if constexpr (STAMP) {
+      if (lane >= 22 && lane < 24) atomicAdd(d.dbgbuf + lane, (int32_t)(f_acc / 64));
+    }
+    if (lane == 0) st_rel(&ctl->fin_p, 1u);
+    return;
+  }
+
+  // =========================================================================
+  // pre-selectors (wave 1: even pods, wave 2: odd pods)
+  // =========================================================================
+  if (wave == 1 || wave == 2) {
+    __builtin_amdgcn_s_setprio(2);
+    const uint32_t par = wave - 1;
+    // lanes 0..17 load candidate j = lane / 6's field f = lane % 6; lanes 18..53
+    // candidate j = (lane - 18) / 12's count of the pod's service (lane - 18) % 12
+    const uint32_t cj_s = lane < 18 ? lane / 6 : 0u, cf = lane % 6;
+    const uint64_t* const fsrc = cf == 0   ? reinterpret_cast<const uint64_t*>(d.cap_cpu)
+                                 : cf == 1 ? reinterpret_cast<const uint64_t*>(d.cap_mem)
+                                 : cf == 2 ? reinterpret_cast<const uint64_t*>(d.used_cpu)
+                                 : cf == 3 ? reinterpret_cast<const uint64_t*>(d.used_mem)
+                                 : cf == 4 ? reinterpret_cast<const uint64_t*>(d.inv10_cpu)
+                                           : reinterpret_cast<const uint64_t*>(d.inv10_mem);
+    const uint32_t cj_c = lane >= 18 && lane < 54 ? (lane - 18) / 12 : 3u, ct = (lane - 18) % 12;
+    uint64_t x_last = 0, x_acc = 0;  // KSG_DEBUG & 8: lanes 28..31 wait, select, order, prefetch
+    auto xstamp = [&](uint32_t k) {
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        x_acc += lane == k ? t_now - x_last : 0ULL;
+        x_last = t_now;
+      }
+    };
+    if constexpr (STAMP) x_last = __builtin_amdgcn_s_memtime();
+    bool stopped = false;
+    for (uint32_t i = par; i < n_pods && !stopped; i += 2) {
+      const uint32_t e = i % RING;
+      for (uint32_t spin = 0;; ++spin) {  // the checkers are done with pod i
+        uint32_t cs = ld_u(&ctl->chk_seq[0]);
+#pragma unroll
+        for (int c = 1; c < KSG_RES_NCHK; ++c) cs = min(cs, ld_u(&ctl->chk_seq[c]));
+        const uint32_t rd = ld_u(&r_hdr[e].ready), st = ld_u(&ctl->stop);
+        if (cs >= i + 1 && rd == i + 1) break;
+        if (st) {
+          stopped = true;
+          break;
+        }
+        if (spin > 16 * KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          stopped = true;
+          break;
+        }
+      }
+      acq_lds();
+      if (stopped) break;
+      xstamp(28);
+      const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
+      const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
+      const uint32_t err = __builtin_amdgcn_readlane(rec, WS_ERR);
+      const uint32_t npp = __builtin_amdgcn_readlane(rec, WS_NPP), nss = __builtin_amdgcn_readlane(rec, WS_NSS);
+      const uint32_t nk = (npp & 0xffff) + (npp >> 16), n_sel = nss & 0xffff, n_svcs = nss >> 16;
+      uint32_t status = KSG_CS_OK, kp = 0;
+      uint32_t ca = KSG_NO_NODE, cb0 = KSG_NO_NODE, cb1 = KSG_NO_NODE;
+      uint64_t live[P];
+#pragma unroll
+      for (int q = 0; q < P; ++q) live[q] = 0;
+      if (err || m0 == KSG_S32_NONE) {
+        status = err ? KSG_CS_ERROR : KSG_CS_NOFIT;
+      } else if (__builtin_amdgcn_readlane(rec, WS_NINL) > KSG_WIN_INLINE || nk > KSG_SLOT_KEYS ||
+                 n_svcs > KSG_SLOT_SVCS) {
+        status = KSG_CS_OVERSIZE;  // lists longer than the record / a slot
+      } else {
+        const uint32_t k0 = __builtin_amdgcn_readfirstlane(r_hdr[e].k0);
+        uint32_t cc = 0;
+#pragma unroll
+        for (int c = 0; c < KSG_RES_NCHK; ++c) cc += __builtin_amdgcn_readfirstlane(ctl->chk_cnt[c][par]);
+        kp = k0 - cc;
+        const uint64_t* t0e = r_t0 + (size_t)e * PW;
+        uint64_t* dw = L_drop + (size_t)par * PW;
+        uint32_t cl = 0;
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+          const uint64_t dq = dw[lane * P + q];
+          live[q] = t0e[lane * P + q] & ~dq;
+          if (dq) dw[lane * P + q] = 0;  // (cleared for the pod two ahead)
+          cl += __popcll(live[q]);
+        }
+        const uint32_t incl = dpp_scan_add(cl);
+        const uint32_t rmod = r_mod[e * 64 + lane];
+        const uint64_t r = r_hdr[e].r;
+        const uint64_t ru = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(r >> 32)) << 32) |
+                            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r);
+        if (kp >= 1) {  // nothing more drops: the (r mod k')-th live tie from the top
+          const uint32_t ix = cc < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)rmod, (int)cc) : umod64_32(ru, kp);
+          ca = select_in_lanes<P>(live, cl, incl, kp - 1 - ix, lane);
+        }
+        if (kp >= 2) {  // x drops too: the (r mod (k'-1))-th from the top of L0 minus x
+          const uint32_t ix =
+              cc + 1 < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)rmod, (int)(cc + 1)) : umod64_32(ru, kp - 1);
+          cb0 = select_in_lanes<P>(live, cl, incl, kp - 2 - ix, lane);
+          cb1 = select_in_lanes<P>(live, cl, incl, kp - 1 - ix, lane);
+        }
+      }
+      xstamp(29);
+      // pod i-1's candidates (the other pre-selector's), then this pod's verdict
+      // (pod i+1's pre-selector waits for it before it overwrites pod i-1's)
+      for (uint32_t spin = 0;; ++spin) {
+        const uint32_t ps = ld_u(&ctl->psel_seq), st = ld_u(&ctl->stop);
+        if (ps >= i) break;
+        if (st) {
+          stopped = true;
+          break;
+        }
+        if (spin > 16 * KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          stopped = true;
+          break;
+        }
+      }
+      acq_lds();
+      if (stopped) break;
+      uint32_t xlive = 0;
+      if (status == KSG_CS_OK && i > 0 && __builtin_amdgcn_readfirstlane(ctl->c_status[par ^ 1]) == KSG_CS_OK) {
+        const uint32_t pa = __builtin_amdgcn_readfirstlane(ctl->c_a[par ^ 1]);
+        const uint32_t pb0 = __builtin_amdgcn_readfirstlane(ctl->c_b0[par ^ 1]);
+        const uint32_t pb1 = __builtin_amdgcn_readfirstlane(ctl->c_b1[par ^ 1]);
+        uint32_t xl = 0;
+#pragma unroll
+        for (int q = 0; q < P; ++q) {  // is pod i-1's candidate j (commit i-1's node, if drawn from it) live?
+          const uint32_t wq = lane * P + q;
+          xl |= ((pa >> 6) == wq && ((live[q] >> (pa & 63)) & 1ULL)) ? 1u : 0u;
+          xl |= ((pb0 >> 6) == wq && ((live[q] >> (pb0 & 63)) & 1ULL)) ? 2u : 0u;
+          xl |= ((pb1 >> 6) == wq && ((live[q] >> (pb1 & 63)) & 1ULL)) ? 4u : 0u;
+        }
+        xlive = wave_or_u32(xl);
+      }
+      if (lane == 0) {
+        ctl->c_status[par] = status;
+        ctl->c_kp[par] = kp;
+        ctl->c_a[par] = ca;
+        ctl->c_b0[par] = cb0;
+        ctl->c_b1[par] = cb1;
+        ctl->c_xlive[par] = xlive;
+        st_rel(&ctl->psel_seq, i + 1);
+      }
+      xstamp(30);
+      // the candidates' snapshots and the pod's service counts on them (the
+      // committer waits for these only when it writes the commit)
+      if (status == KSG_CS_OK) {
+        const uint32_t cjs = cj_s == 0 ? ca : cj_s == 1 ? cb0 : cb1;
+        const uint32_t cjc = cj_c == 0 ? ca : cj_c == 1 ? cb0 : cj_c == 2 ? cb1 : KSG_NO_NODE;
+        const uint32_t my_sv = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + ct, 63u), 64);
+        uint64_t fv = 0;
+        int32_t scv = 0;
+        if (lane < 18 && cjs != KSG_NO_NODE) fv = gld(fsrc + d.lo + cjs);
+        if (cjc != KSG_NO_NODE && ct < n_svcs) scv = gld(d.svc_cnt + (size_t)my_sv * d.n_nodes + d.lo + cjc);
+        if (lane < 18) L_csnap[par * 18 + lane] = (int64_t)fv;
+        if (lane >= 18 && lane < 54) L_csc[par * 36 + (lane - 18)] = scv;
+      }
+      if (lane == 0) st_rel(&ctl->csnap_seq[par], i + 1);
+      xstamp(31);
+    }
+    if constexpr (STAMP) {
+      if (lane >= 28 && lane < 32) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
+    }
+    return;
+  }
+  if (wave != 0) return;
+
+  // =========================================================================
+  // committer (wave 0)
+  // =========================================================================
+  __builtin_amdgcn_s_setprio(3);
+  uint32_t resolved = n_pods, reason = 0, n_slots = 0, n_draws = 0;
+  uint32_t cn0 = ~0u, cn1 = ~0u;  // nodes of slots lane and 64 + lane
+  uint32_t sk0 = 0, sk1 = 0;      // their key counts
+  uint32_t ss0 = 0, ss1 = 0;      // their service entry counts
+  uint32_t sm0 = 0, sm1 = 0;      // their service masks
+  int64_t dc0 = 0, dm0 = 0, dc1 = 0, dm1 = 0;  // their window deltas
+  // commit i-1 (pod i's re-check): node, slot, list lengths; lane L < 4 holds
+  // resource L & 1's snapshot (capacity, requested, 10/capacity) and delta
+  const uint32_t rl = lane & 1;
+  bool have_x = false;
+  uint32_t x_node = 0, x_cj = 0, x_slot = 0, x_bns = 0, x_nk = 0, x_ns = 0;
+  int64_t xs_cap = 0, xs_snp = 0, x_dl = 0;
+  double xs_inv = 0.0;
+  uint64_t t_last = 0, t_acc = 0;
+#define KSG_STAMP3(k)                                        \
+  if constexpr (STAMP) {                                     \
+    const uint64_t t_now = __builtin_amdgcn_s_memtime();     \
+    t_acc += lane == (uint32_t)(k) ? t_now - t_last : 0ULL;  \
+    t_last = t_now;                                          \
+  }
+  if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
+  for (uint32_t i = 0; i < n_pods; ++i) {
+    const uint32_t e = i % RING, par = i & 1;
+    bool hung = false;
+    for (uint32_t spin = 0;; ++spin) {  // pod i staged
+      const uint32_t rd = ld_u(&r_hdr[e].ready), hg = ld_u(&ctl->hang);
+      if (rd == i + 1) break;
+      if (spin > 16 * KSG_SPIN_LIMIT || hg) {
+        hung = true;
+        break;
+      }
+    }
+    acq_lds();
+    if (hung) {
+      resolved = i;
+      reason = KSG_STOP_HANG;
+      break;
+    }
+    KSG_STAMP3(0)
+    const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
+    const PodView pv = pod_view(rec);
+    const int32_t s = pv.s;
+    const uint32_t nss = __builtin_amdgcn_readlane(rec, WS_NSS);
+    const uint32_t n_sel = nss & 0xffff, n_svcs = nss >> 16, nk = pv.nk;
+    KSG_STAMP3(1)
+    // ---- pod i against commit i-1's node x, as of that commit
+    bool xd = false, flag_x = false;
+    if (have_x) {
+      const int64_t reqv = rl ? pv.req_m : pv.req_c;
+      const int64_t nowv = (int64_t)((uint64_t)xs_snp + (uint64_t)x_dl);  // requested total now
+      if (res_on && !pv.zero_req)  // PodFitsResources: lanes 0 and 1
+        xd = (__ballot(lane < 2 && !(xs_cap == 0 || xs_cap - nowv >= reqv)) & 3ULL) != 0;
+      if (d.w_lr) {  // LeastRequested: lanes 0, 1 now, lanes 2, 3 at the snapshot
+        const int32_t lrv = lr_win((lane < 2 ? nowv : xs_snp) + reqv, xs_cap, xs_inv);
+        const int32_t lr_now = __builtin_amdgcn_readlane(lrv, 0) + __builtin_amdgcn_readlane(lrv, 1);
+        const int32_t lr_snap = __builtin_amdgcn_readlane(lrv, 2) + __builtin_amdgcn_readlane(lrv, 3);
+        xd |= (lr_now >> 1) != (lr_snap >> 1);
+      }
+      // x's lists: lane t < 8 key t; lane 8 + u service entry u and its snapshot count
+      const uint32_t ut = lane - KSG_SLOT_KEYS;
+      const uint32_t xcl = lane < x_nk                  ? s_keys[(size_t)x_slot * KSG_SLOT_KEYS + lane]
+                           : (lane >= KSG_SLOT_KEYS && ut < x_ns) ? s_svcs[(size_t)x_slot * KSG_SLOT_SVCS + ut]
+                                                        : ~0u;
+      if (s >= 0) {
+        const uint64_t smk = __ballot(lane >= KSG_SLOT_KEYS && ut < x_ns && xcl == (uint32_t)s);
+        if (smk) {
+          const uint32_t x_cnt_s = (uint32_t)__popcll(smk);
+          const uint32_t fl = (uint32_t)__builtin_ctzll(smk);
+          const int32_t x_snapc = __builtin_amdgcn_readfirstlane(s_sc[(size_t)x_slot * KSG_SLOT_SVCS + (fl - KSG_SLOT_KEYS)]);
+          if (spread_on) {  // ServiceSpreading under an unchanged maxCount: lane 0 now, lane 1 the snapshot
+            const int32_t fr = (int32_t)frac10_f32(
+                (int64_t)pv.smax - x_snapc - (lane == 0 ? (int32_t)x_cnt_s : 0), pv.smax);
+            xd |= __builtin_amdgcn_readlane(fr, 0) != __builtin_amdgcn_readlane(fr, 1);
+          }
+          if ((smk >> (KSG_SLOT_KEYS + x_bns)) != 0) {  // commit i-1, a pod of service s: maxCount rises / first peer
+            flag_x = spread_on && x_snapc + (int32_t)x_cnt_s > pv.smax;
+            if (aff_on && (int32_t)__builtin_amdgcn_readfirstlane(r_svc[e].peer[0]) == -1 &&
+                !((__builtin_amdgcn_readfirstlane(L_peerset[s >> 5]) >> (s & 31)) & 1u))
+              flag_x = true;
+          }
+        }
+      }
+      if (nk && x_nk) {  // PodFitsPorts / NoDiskConflict
+        bool hit = false;
+        for (uint32_t b = 0; b < nk; ++b) {
+          const bool on = b < pv.n_ports ? ports_on : disk_on;
+          hit |= on && lane < x_nk && xcl == (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b));
+        }
+        xd |= __ballot(hit) != 0;
+      }
+    }
+    KSG_STAMP3(2)
+    // ---- the pre-selector's verdict (the re-check above overlapped its wait)
+    for (uint32_t spin = 0;; ++spin) {
+      const uint32_t ps = ld_u(&ctl->psel_seq), hg = ld_u(&ctl->hang);
+      if (ps >= i + 1) break;
+      if (spin > 16 * KSG_SPIN_LIMIT || hg) {
+        hung = true;
+        break;
+      }
+    }
+    acq_lds();
+    if (hung) {
+      resolved = i;
+      reason = KSG_STOP_HANG;
+      break;
+    }
+    const uint32_t status = __builtin_amdgcn_readfirstlane(ctl->c_status[par]);
+    if (status == KSG_CS_NOFIT || status == KSG_CS_ERROR) {
+      // ServiceAffinity peer error / nothing fit at the snapshot (commits only
+      // remove fits): no draw, no commit
+      if (lane == 0) {
+        L_cm[i].kind = 0;
+        L_out[i] = status == KSG_CS_ERROR ? KSG_OUT_ERROR : KSG_OUT_NOFIT;
+        st_rel(&ctl->sel_seq, i + 1);
+      }
+      have_x = false;  // pod i+1's checkers see every commit up to i-1
+      continue;
+    }
+    if (status == KSG_CS_OVERSIZE) {
+      resolved = i;  // the exact per-pod kernel takes it
+      reason = i == 0 ? KSG_STOP_OVERSIZE : KSG_STOP_SLOT;
+      break;
+    }
+    const uint32_t kp = __builtin_amdgcn_readfirstlane(ctl->c_kp[par]);
+    const uint32_t ca = __builtin_amdgcn_readfirstlane(ctl->c_a[par]);
+    const uint32_t cb0 = __builtin_amdgcn_readfirstlane(ctl->c_b0[par]);
+    const uint32_t cb1 = __builtin_amdgcn_readfirstlane(ctl->c_b1[par]);
+    const uint32_t xlv = __builtin_amdgcn_readfirstlane(ctl->c_xlive[par]);
+    KSG_STAMP3(6)
+    // the flags of commits <= i-2, and the candidates' snapshots
+    for (uint32_t spin = 0;; ++spin) {
+      const uint32_t fs = ld_u(&ctl->flag_seq), cs = ld_u(&ctl->csnap_seq[par]), hg = ld_u(&ctl->hang);
+      if (fs + 1 >= i && cs == i + 1) break;
+      if (spin > 16 * KSG_SPIN_LIMIT || hg) {
+        hung = true;
+        break;
+      }
+    }
+    acq_lds();
+    if (hung) {
+      resolved = i;
+      reason = KSG_STOP_HANG;
+      break;
+    }
+    const uint32_t fw = s >= 0 ? L_flag[s >> 5] : 0u;
+    KSG_STAMP3(5)
+    if (s >= 0 && (spread_on || aff_on) && (flag_x || ((__builtin_amdgcn_readfirstlane(fw) >> (s & 31)) & 1u))) {
+      resolved = i;  // a service scalar this pod reads changed in the window
+      reason = KSG_STOP_SERVICE;
+      break;
+    }
+    // ---- the draw: A, or with x dropping too (x a live tie), B0 / B1
+    const bool x_drop = xd && ((xlv >> x_cj) & 1u) != 0;
+    if (kp - (x_drop ? 1u : 0u) == 0) {
+      resolved = i;  // every snapshot tie got worse: needs a fresh snapshot
+      reason = KSG_STOP_EXHAUSTED;
+      break;
+    }
+    const uint32_t cj = !x_drop ? 0u : x_node > cb0 ? 1u : 2u;
+    const uint32_t woff = cj == 0 ? ca : cj == 1 ? cb0 : cb1;
+    // ---- AssumePod's slot
+    const uint64_t hit0 = __ballot(cn0 == woff);
+    const uint64_t hit1 = __ballot(cn1 == woff);
+    const bool in_c = (hit0 | hit1) != 0;
+    uint32_t slot, base_nk = 0, base_ns = 0, base_sm = 0;
+    int64_t base_dc = 0, base_dm = 0;
+    if (in_c) {
+      slot = hit0 ? (uint32_t)__builtin_ctzll(hit0) : 64u + (uint32_t)__builtin_ctzll(hit1);
+      const uint32_t sl = slot & 63;
+      base_nk = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? sk0 : sk1), (int)sl);
+      base_ns = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? ss0 : ss1), (int)sl);
+      if (base_nk + nk > KSG_SLOT_KEYS || base_ns + n_svcs > KSG_SLOT_SVCS) {
+        resolved = i;  // this pod is redone (with the same draw) in the next window
+        reason = KSG_STOP_SLOT;
+        break;
+      }
+      base_sm = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? sm0 : sm1), (int)sl);
+      base_dc = (int64_t)readlane64((uint64_t)(slot < 64 ? dc0 : dc1), (int)sl);
+      base_dm = (int64_t)readlane64((uint64_t)(slot < 64 ? dm0 : dm1), (int)sl);
+    } else {
+      if (n_slots == KSG_MAX_SLOTS) {
+        resolved = i;
+        reason = KSG_STOP_SLOT;
+        break;
+      }
+      slot = n_slots++;
+    }
+    KSG_STAMP3(3)
+    const int64_t new_dc = (int64_t)((uint64_t)base_dc + (uint64_t)pv.req_c);
+    const int64_t new_dm = (int64_t)((uint64_t)base_dm + (uint64_t)pv.req_m);
+    // the chosen candidate's snapshot, resource rl (the slot's, and the next re-check's)
+    const int64_t* cs = L_csnap + par * 18 + cj * 6;
+    const int64_t cs_cap = cs[rl], cs_snp = cs[2 + rl];
+    const double cs_inv = __longlong_as_double((long long)cs[4 + rl]);
+    const uint32_t kt = lane - WS_IDS, st = lane - (WS_IDS + nk + n_sel);
+    const uint32_t new_sm = base_sm | wave_or_u32(st < n_svcs ? (1u << (rec & 31)) : 0u);
+    if (!in_c && lane < 2) {  // the new slot's snapshot, before its node
+      (&s_cap[slot].c)[rl] = cs_cap;
+      (&s_snp[slot].c)[rl] = cs_snp;
+      (&s_inv[slot].c)[rl] = cs_inv;
+    }
+    // the pod's keys and service ids (record lane L holds dword L, so each list
+    // entry is stored by the lane that holds it) and the services' counts on the node
+    if (kt < nk) s_keys[(size_t)slot * KSG_SLOT_KEYS + base_nk + kt] = rec;
+    if (st < n_svcs) {
+      s_sc[(size_t)slot * KSG_SLOT_SVCS + base_ns + st] = L_csc[par * 36 + cj * 12 + st];
+      s_svcs[(size_t)slot * KSG_SLOT_SVCS + base_ns + st] = rec;
+    }
+    // (the checkers read a slot's lengths before its lists and its node before its
+    // snapshot; one wave's LDS stores land in program order, so only the compiler
+    // must keep them in order)
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (lane == 0) {
+      s_dl[slot].c = new_dc;
+      s_dl[slot].m = new_dm;
+      s_meta[slot].nk = base_nk + nk;
+      s_meta[slot].ns = base_ns + n_svcs;
+      s_meta[slot].smask = new_sm;
+      if (!in_c) s_meta[slot].node = woff;
+      L_cm[i] = WinCommit3{1u, slot, woff, base_ns | (n_svcs << 16)};
+      L_out[i] = (int32_t)(d.lo + woff);
+      st_rel(&ctl->sel_seq, i + 1);  // the checkers move on
+    }
+    if (lane == (slot & 63)) {  // this wave's view of the slot
+      if (slot >= 64) {
+        if (!in_c) cn1 = woff;
+        dc1 = new_dc;
+        dm1 = new_dm;
+        sk1 = base_nk + nk;
+        ss1 = base_ns + n_svcs;
+        sm1 = new_sm;
+      } else {
+        if (!in_c) cn0 = woff;
+        dc0 = new_dc;
+        dm0 = new_dm;
+        sk0 = base_nk + nk;
+        ss0 = base_ns + n_svcs;
+        sm0 = new_sm;
+      }
+    }
+    have_x = true;
+    x_node = woff;
+    x_cj = cj;
+    x_slot = slot;
+    x_bns = base_ns;
+    x_nk = base_nk + nk;
+    x_ns = base_ns + n_svcs;
+    x_dl = rl ? new_dm : new_dc;
+    xs_cap = cs_cap;
+    xs_snp = cs_snp;
+    xs_inv = cs_inv;
+    ++n_draws;
+    KSG_STAMP3(4)
+  }
+  if (lane == 0) {
+    ctl->resolved = resolved;
+    st_rel(&ctl->stop, 1u);
+  }
+  // the checkers write their slots back, the pre-selector records the last first peers
+  bool drained = false;
+  for (uint32_t spin = 0; spin <= 16 * KSG_SPIN_LIMIT; ++spin) {
+    bool done = ld_acq(&ctl->fin_p) != 0;
+#pragma unroll
+    for (int c = 0; c < KSG_RES_NCHK; ++c) done = done && ld_acq(&ctl->fin[c]) != 0;
+    if (done) {
+      drained = true;
+      break;
+    }
+  }
+  if (!drained || ld_acq(&ctl->hang)) reason = KSG_STOP_HANG;
+  if constexpr (STAMP) {
+    if (lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
+  }
+#undef KSG_STAMP3
+  const uint32_t n_peer = __builtin_amdgcn_readfirstlane(ctl->n_peer);
+  for (uint32_t t = lane; t < n_peer; t += 64) {
+    const uint32_t sv = L_peer[2 * t];
+    int32_t expect = -1;
+    __hip_atomic_compare_exchange_strong(d.svc_peer + sv, &expect, (int32_t)L_peer[2 * t + 1], __ATOMIC_RELAXED,
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (uint32_t t = lane; t < resolved; t += 64) out[t] = L_out[t];
+  if (lane == 0) {
+    *rng_io = rng0 + (uint64_t)n_draws * 0x9E3779B97F4A7C15ULL;
+    if (reason == KSG_STOP_HANG) {
+      run->halt = KSG_HALT_HANG;
+    } else if (reason == KSG_STOP_OVERSIZE) {
+      run->halt = KSG_HALT_OVERSIZE;  // pod pos: the host runs the exact per-pod path, then resumes
+    } else if (resolved == 0 || resolved > n_pods) {
+      run->halt = KSG_HALT_BADCOUNT;
+    } else {
+      run->pos = pos + resolved;
+      run->windows += 1;
+      if (reason >= 1 && reason <= 3) run->stops[reason] += 1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
 static uint32_t win_P(const KsgDev& d) {
@@ -2470,7 +3525,9 @@ uint32_t ksg_win_max_window(const KsgDev& d) {
   uint32_t lo = 0, hi = 4096;
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1) / 2;
-    const uint32_t need = anti ? win_lds_offsets(P, nflag, mid, d.n_anti > 0).total : win2_lds_offsets(P, nflag, mid).total;
+    const uint32_t need = anti             ? win_lds_offsets(P, nflag, mid, d.n_anti > 0).total
+                          : (d.dbg & 512) ? win3_lds_offsets(P, nflag, mid).total
+                                          : win2_lds_offsets(P, nflag, mid).total;
     if (need <= kWinLdsBudget) lo = mid;
     else hi = mid - 1;
   }
@@ -2494,6 +3551,22 @@ static hipError_t win_resolve_launch(const KsgDev& d, uint32_t wcap, size_t lds,
 }
 
 template <int PP, bool ST>
+static hipError_t win_resolve3_launch(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run,
+                                      const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
+                                      hipStream_t st) {
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_resolve3_kernel<PP, ST>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipGetLastError();
+    once = true;
+  }
+  hipLaunchKernelGGL((ksg_win_resolve3_kernel<PP, ST>), dim3(1), dim3(win3_nt(PP)), lds, st, d, wcap, run, sums, x, rng,
+                     out);
+  return hipGetLastError();
+}
+
+template <int PP, bool ST>
 static hipError_t win_resolve2_launch(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run,
                                       const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
                                       hipStream_t st) {
@@ -2511,6 +3584,24 @@ static hipError_t win_resolve2_launch(const KsgDev& d, uint32_t wcap, size_t lds
 hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
                                   const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
   const uint32_t P = win_P(d);
+  if (x.fit_off == 0 && (d.dbg & 512) && !(d.dbg & 128)) {
+    // KSG_DEBUG & 512: the pre-selecting resolver (measured slower than the
+    // register-slot resolver on config 2: DESIGN.md section 4), for comparison
+    const size_t lds3 = win3_lds_offsets(P, (d.n_services + 31) / 32, wcap).total;
+    const bool stamp3 = (d.dbg & 8) != 0;
+#define KSG_RES3_CASE(PP)                                                                         \
+  if (P == PP)                                                                                    \
+    return stamp3 ? win_resolve3_launch<PP, true>(d, wcap, lds3, run, sums, x, rng, out, st)      \
+                  : win_resolve3_launch<PP, false>(d, wcap, lds3, run, sums, x, rng, out, st);
+    KSG_RES3_CASE(1)
+    KSG_RES3_CASE(2)
+    KSG_RES3_CASE(4)
+    KSG_RES3_CASE(8)
+    KSG_RES3_CASE(16)
+    KSG_RES3_CASE(32)
+#undef KSG_RES3_CASE
+    return hipErrorInvalidValue;
+  }
   if (x.fit_off == 0 && !(d.dbg & 128)) {  // no ServiceAntiAffinity: the register-slot resolver
     // (KSG_DEBUG & 128: the LDS-slot resolver instead, for comparison)
     const size_t lds2 = win2_lds_offsets(P, (d.n_services + 31) / 32, wcap).total;

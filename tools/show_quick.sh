@@ -5,5 +5,5 @@ for f in gpurun_out/dbg_c*.err; do echo $f; grep "stamps raw" $f | python -c "
 import sys
 for l in sys.stdin:
     v=[int(x) for x in l.split(':')[1].split()]
-    print(' committer', [round(x*64/6000) for x in v[0:6]], 'checker0', [round(x*64/6000) for x in v[16:19]], 'checker1', [round(x*64/6000) for x in v[19:22]], 'drops', v[7], 'unpred', v[8]);
-    print(' producers(sum over waves)', [round(x*64/6000) for x in v[24:28]], 'xchk wait,rest,loads', [round(x*64/6000) for x in v[28:31]])"; done
+    print(' committer', [round(x*64/6000) for x in v[0:7]], 'checker0', [round(x*64/6000) for x in v[16:19]], 'checker1', [round(x*64/6000) for x in v[19:22]], 'drops', v[7], 'unpred', v[8]);
+    print(' producers(sum over waves)', [round(x*64/6000) for x in v[24:28]], 'flagger', [round(x*64/6000) for x in v[22:24]], 'presel', [round(x*64/6000) for x in v[28:32]])"; done
