@@ -4,7 +4,8 @@
 A "step" is one batch of `--batch` pods scheduled in order through the hot path
 (filter every node, score, argmax + reference tie-break, commit) by
 ksg_schedule_batch: windows of pods are scored against a snapshot on all CUs
-(ksg_win_score_kernel) and resolved in order, exactly, by ksg_win_resolve_kernel;
+(ksg_win_score_kernel) and resolved in order, exactly, by one workgroup
+(ksg_win_resolve2_kernel; ksg_win_resolve_kernel with ServiceAntiAffinity);
 node state is resident in HBM before the timed region (the C ABI copies the
 batch descriptors in, ~B*88 bytes, inside the step).
 
@@ -20,7 +21,10 @@ batch descriptors in, ~B*88 bytes, inside the step).
 Roofline: bound "hbm"; achieved = algorithmic bytes per launch / kernel time,
 with SURVEY.md 8(d)'s 60 B/node/pod for this predicate+priority set
 (resources 32 + ports 8 + PD 8 + labels 8 + spread count 4) x nodes x pods per
-launch; kernel time from HIP events on the library's stream. cpu_baseline: the
+launch; kernel time from HIP events on the library's stream. The resolver is a
+latency-bound dependency chain, so the line also carries `latency`: resolver
+cycles per pod at the 2.4 GHz engine clock and, from an untimed KSG_DEBUG=8
+rerun, the chain's per-stage cycles. cpu_baseline: the
 C restatement in faithful mode (the reference's per-pod MapPodsToMachines
 regroup + per-node rescans + sort; single thread like the reference's one
 scheduling goroutine) timed on this host over a bounded prefix of the same
@@ -40,6 +44,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip-level parameters
+CLOCK_MHZ = 2400.0  # MI355X max engine clock (MI355X_MICROARCH.md); the resolver's stamps count it
 BYTES_PER_NODE = {"config1": 32, "config2": 60, "config3": 60, "config4": 64, "config5": 84}
 
 
@@ -56,6 +61,58 @@ def _torch_sync():
             torch.cuda.synchronize()
     except Exception:
         pass
+
+
+# KSG_DEBUG=8 counter layout of the register-slot resolver (ksg_window.hip):
+# lane -> (role, stage); counters are cycles / 64 summed over windows
+_STAGES2 = {
+    0: ("committer", "ring_wait"), 1: ("committer", "head"), 2: ("committer", "wait_checkers_and_xcheck"),
+    3: ("committer", "select"), 4: ("committer", "slot_and_node_post"), 5: ("committer", "commit"),
+    6: ("handoff", "xcheck_to_committer"), 31: ("handoff", "node_to_xchecker"),
+    16: ("checker0", "wait"), 17: ("checker0", "apply"), 18: ("checker0", "check"),
+    19: ("checker1", "wait"), 20: ("checker1", "apply"), 21: ("checker1", "check"),
+    24: ("producers_sum_over_waves", "ring_wait"), 25: ("producers_sum_over_waves", "loads"),
+    26: ("producers_sum_over_waves", "draw_wait"), 27: ("producers_sum_over_waves", "stage"),
+    28: ("xchecker", "wait_node"), 29: ("xchecker", "check"), 30: ("xchecker", "bookkeeping_and_lists"),
+}
+
+
+def _stage_breakdown(cfg, view, args, step_batch, anti):
+    """Per-stage resolver cycles per pod from a KSG_DEBUG=8 context over the
+    bench's first steps (untimed; the stamps cost a few percent)."""
+    from kubernetes_amd import workload
+    from kubernetes_amd.engine import DeviceScheduler
+
+    old = os.environ.get("KSG_DEBUG")
+    os.environ["KSG_DEBUG"] = str(int(old or "0") | 8)  # read when the context builds its device state
+    s2 = None
+    try:
+        s2 = DeviceScheduler(cfg, device=0)
+        if args.window is not None:
+            s2.set_window(args.window)
+        s2.set_cluster(view.arrays)
+        rng = workload.TIEBREAK_SEED
+        pods = 0
+        for s in range(min(3, args.warmup + args.steps)):
+            b = step_batch(s)
+            _, rng = s2.batch(b, rng)
+            pods += len(b.pods)
+        c = s2.debug_counters().astype(np.int64) * 64
+    finally:
+        if s2 is not None:
+            s2.close()
+        if old is None:
+            del os.environ["KSG_DEBUG"]
+        else:
+            os.environ["KSG_DEBUG"] = old
+    if anti:
+        return {"pods": pods, "raw_cycles_per_pod": [round(float(v) / pods, 1) for v in c],
+                "note": "LDS-slot resolver (ServiceAntiAffinity): raw counters, layout in ksg_window.hip"}
+    out = {"pods": pods, "unit": "cycles/pod",
+           "drops_per_pod": float(c[7]) / 64 / pods, "unpredicted_per_pod": float(c[8]) / 64 / pods}
+    for lane, (role, st) in _STAGES2.items():
+        out.setdefault(role, {})[st] = round(float(c[lane]) / pods, 1)
+    return out
 
 
 def main():
@@ -75,6 +132,8 @@ def main():
                          "(rehearsal of the sharded path with several ranks on one GPU)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (profiles/), keyed by workload")
+    ap.add_argument("--no-stages", action="store_true",
+                    help="skip the resolver's per-stage cycle breakdown (a second, untimed run with KSG_DEBUG=8)")
     args = ap.parse_args()
 
     world, rank, local_rank = _dist_env()
@@ -179,16 +238,28 @@ def main():
     # from the HIP events the library records around each resolver launch.
     # exact path (--window 0) / sharded: the one batch kernel per step.
     bpn = BYTES_PER_NODE.get(wl, 60)
+    anti = any(int(cfg.w_anti[a]) != 0 for a in range(int(cfg.n_anti)))
+    wcap = args.window if args.window else int(os.environ.get("KSG_WINDOW", "128"))
+    nwords = (n_nodes + 63) // 64
     if kk["launches"] > 0:
         launches = kk["launches"]
         pods_per_launch = pods_timed / launches
         kavg_s = kk["resolve_ms"] / launches / 1e3
-        kname = "ksg_win_resolve_kernel"
-        # phase A scores this rank's shard (N/world nodes); with world > 1 its
-        # event window also holds the per-window all-gather
+        # the in-order resolver: the LDS-slot one with ServiceAntiAffinity, else the
+        # register-slot one (ksg_window.hip)
+        kname = "ksg_win_resolve_kernel" if anti else "ksg_win_resolve2_kernel"
+        # phase A scores this rank's shard (N/world nodes) for the window's wcap pods;
+        # with world > 1 its event window also holds the per-window all-gather. Its
+        # bytes: the node state once per launch + the per-word bitmaps and maxima it
+        # writes + the pod records (its node loads are shared by a wave's 8 pods and
+        # stay in L2 across pod groups, so per-(node, pod) bytes overstate it)
+        ev_s = kk["eval_ms"] / launches / 1e3
+        ev_bytes = bpn * (n_nodes / world) + wcap * (nwords / world) * 12 + wcap * 192
         extra = {"launches": launches, "pods_per_launch": pods_per_launch,
                  "win_eval_ms_avg": kk["eval_ms"] / launches,
-                 "win_eval_GBps": bpn * (n_nodes / world) * pods_per_launch / (kk["eval_ms"] / launches / 1e3) / 1e9}
+                 "win_eval_model_bytes_per_launch": ev_bytes,
+                 "win_eval_model_GBps": ev_bytes / ev_s / 1e9,
+                 "win_eval_node_pod_evals_per_s": (n_nodes / world) * wcap / ev_s}
     else:
         pods_per_launch = args.batch
         kavg_s = float(np.mean(kern_ms)) / 1e3 if kern_ms else float("nan")
@@ -197,6 +268,7 @@ def main():
     alg_bytes = bpn * n_nodes * pods_per_launch
     achieved = alg_bytes / kavg_s
     traffic = None
+    tj = {}
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
@@ -209,6 +281,24 @@ def main():
                 "frac": achieved / HBM_PEAK, "traffic": traffic, "kernel": kname,
                 "kernel_ms_avg": kavg_s * 1e3, "bytes_per_node_pod": bpn, "alg_bytes_per_launch": alg_bytes}
     roofline.update(extra)
+    if kk["launches"] > 0:
+        ent = tj.get(f"{wl}:{n_nodes}:ksg_win_score_kernel")  # phase A's counter-measured bytes (profiles/)
+        if ent:
+            roofline["win_eval_traffic"] = ent["hbm_bytes_per_launch"]
+            roofline["win_eval_traffic_GBps"] = ent["hbm_bytes_per_launch"] / (kk["eval_ms"] / launches / 1e3) / 1e9
+
+    # ---- latency view: the resolver is one in-order dependency chain per window
+    # (one workgroup), so its bound is the chain's cycles per pod,
+    # not bytes. Stage breakdown: a second, untimed run of the first steps on a
+    # context with the resolver's s_memtime stamps on (KSG_DEBUG=8).
+    latency = None
+    if kk["launches"] > 0:
+        us_pod = kk["resolve_ms"] * 1e3 / pods_timed
+        latency = {"bound": "latency", "resolver_us_per_pod": us_pod, "clock_mhz": CLOCK_MHZ,
+                   "resolver_cycles_per_pod": us_pod * CLOCK_MHZ,
+                   "window_eval_us_per_pod": kk["eval_ms"] * 1e3 / pods_timed}
+        if world == 1 and not args.no_stages:
+            latency["stages"] = _stage_breakdown(cfg, view, args, step_batch, anti)
 
     # ---- CPU baseline: faithful restatement, single thread, bounded prefix ------
     cpu = None
@@ -298,6 +388,7 @@ def main():
                    else (f"node-sharded x{world}: shard scoring, {xname} all-gather per window, replicated resolver"
                          if kk["launches"] else f"node-sharded x{world}, {xname} all-gather per pod")},
         "roofline": roofline,
+        "latency": latency,
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

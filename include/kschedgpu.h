@@ -261,6 +261,12 @@ int ksg_last_batch_ms(ksg_ctx* ctx, double* ms);
  * context's stream. */
 int ksg_last_batch_kernel_ms(ksg_ctx* ctx, double* out3);
 
+/* Diagnostics: the window resolver's per-stage clock counters (s_memtime
+ * cycles / 64, summed over every window since the context was created) for a
+ * context created with KSG_DEBUG=8 in the environment; out32[32] (layout:
+ * DESIGN.md section 4, "resolver stages"). KSG_ERR_STATE when not enabled. */
+int ksg_debug_counters(ksg_ctx* ctx, int32_t* out32);
+
 /* ---- node sharding (multi-GPU) ------------------------------
  * Nodes are split into contiguous runs of 64-node words in name-rank order.
  * Per pod every shard produces one record: this header followed by the shard's

@@ -177,6 +177,7 @@ EXPORTS = [
     "ksg_last_batch_stats",
     "ksg_last_batch_ms",
     "ksg_last_batch_kernel_ms",
+    "ksg_debug_counters",
     "ksg_shard",
     "ksg_read_requested",
     "ksg_shard_range",
@@ -232,6 +233,7 @@ def load_library() -> C.CDLL:
         "ksg_last_batch_stats": (C.c_int, [vp, vp]),
         "ksg_last_batch_ms": (C.c_int, [vp, P(C.c_double)]),
         "ksg_last_batch_kernel_ms": (C.c_int, [vp, vp]),
+        "ksg_debug_counters": (C.c_int, [vp, vp]),
         "ksg_shard": (C.c_int, [vp, P(U32), P(U32)]),
         "ksg_read_requested": (C.c_int, [vp, vp, vp]),
         "ksg_shard_range": (C.c_int, [U32, C.c_int, C.c_int, P(U32), P(U32)]),

@@ -121,6 +121,15 @@ struct ksg_ctx {
   size_t out_cap = 0;
   uint64_t* d_rng = nullptr;
   int64_t* d_summary = nullptr;
+  // the per-pod path (begin / commit / evaluate): the pod and its id list in
+  // one device buffer (one copy in), and the decide kernel's summary and chosen
+  // node written straight into pinned host memory (no copy out)
+  uint8_t* d_one = nullptr;
+  size_t one_cap = 0;
+  const ksg_pod* one_pod = nullptr;
+  const uint32_t* one_ids = nullptr;
+  uint8_t* h_map = nullptr;  // pinned, coherent: [0, 32) summary int64[3], [32, 36) node
+  uint8_t* d_map = nullptr;  // its device address
   KsgPatch* d_patch = nullptr;
   size_t patch_cap = 0;
   uint8_t* d_admit = nullptr;  // kubelet admission: sets, pods, ids, pairs, codes (one buffer)
@@ -400,6 +409,31 @@ int upload_pods(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32_t* ids
   return KSG_OK;
 }
 
+// the single-pod APIs: pod + ids staged contiguously, one copy into d_one;
+// one_pod / one_ids point into it until the next single-pod upload
+int upload_one(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, size_t n_ids) {
+  const size_t pb = (sizeof(ksg_pod) + 15) & ~(size_t)15, ib = std::max<size_t>(n_ids, 1) * sizeof(uint32_t);
+  int rc = grow(c, (void**)&c->d_one, &c->one_cap, pb + ib, 1);
+  if (rc) return rc;
+  if ((rc = grow_host(c, &c->h_up, &c->h_up_cap, pb + ib))) return rc;
+  memcpy(c->h_up, pod, sizeof(ksg_pod));
+  if (n_ids) memcpy(c->h_up + pb, ids, n_ids * sizeof(uint32_t));
+  HIPCHK(c, hipMemcpyAsync(c->d_one, c->h_up, pb + (n_ids ? n_ids * sizeof(uint32_t) : 0), hipMemcpyHostToDevice,
+                           c->st));
+  c->one_pod = reinterpret_cast<const ksg_pod*>(c->d_one);
+  c->one_ids = reinterpret_cast<const uint32_t*>(c->d_one + pb);
+  return KSG_OK;
+}
+
+int ensure_map(ksg_ctx* c) {
+  if (c->h_map) return KSG_OK;
+  HIPCHK(c, hipHostMalloc((void**)&c->h_map, 64, hipHostMallocCoherent));
+  void* dp = nullptr;
+  HIPCHK(c, hipHostGetDevicePointer(&dp, c->h_map, 0));
+  c->d_map = static_cast<uint8_t*>(dp);
+  return KSG_OK;
+}
+
 size_t pod_ids_extent(const ksg_pod* p) {
   size_t e = 0;
   e = std::max<size_t>(e, (size_t)p->ports_off + p->n_ports);
@@ -417,11 +451,13 @@ bool anti_on(const ksg_ctx* c) { return c->cfg.n_anti > 0 && c->dev.n_domains_to
 // ---- cross-rank exchange: RCCL over xGMI, or the caller's host transport ----
 int grow_host(ksg_ctx* c, uint8_t** p, size_t* cap, size_t need) {
   if (*cap >= need) return KSG_OK;
+  // geometric: a pinned (re)allocation costs ~0.2 ms (hipHostFree synchronises)
+  const size_t nc = std::max<size_t>(need, std::max<size_t>(*cap * 2, 4096));
   if (*p) (void)hipHostFree(*p);
   *p = nullptr;
   *cap = 0;
-  HIPCHK(c, hipHostMalloc((void**)p, need, hipHostMallocDefault));
-  *cap = need;
+  HIPCHK(c, hipHostMalloc((void**)p, nc, hipHostMallocDefault));
+  *cap = nc;
   return KSG_OK;
 }
 
@@ -700,7 +736,7 @@ int ksg_destroy(ksg_ctx* c) {
   free_cluster(c);
   void* scratch[] = {c->d_pods, c->d_ids, c->d_fail, c->d_score, c->d_rec_send, c->d_rec_recv, c->d_dpart,
                      c->d_dglobal, c->d_out, c->d_rng, c->d_summary, c->d_patch, c->d_shard_wlo,
-                     c->d_winsum, c->d_xsend, c->d_xrecv, c->d_run, c->d_dcnt, c->d_admit};
+                     c->d_winsum, c->d_xsend, c->d_xrecv, c->d_run, c->d_dcnt, c->d_admit, c->d_one};
   for (void* p : scratch)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -708,6 +744,7 @@ int ksg_destroy(ksg_ctx* c) {
   if (c->h_run) (void)hipHostFree(c->h_run);
   if (c->h_up) (void)hipHostFree(c->h_up);
   if (c->h_dn) (void)hipHostFree(c->h_dn);
+  if (c->h_map) (void)hipHostFree(c->h_map);
   if (c->h_xrecv) (void)hipHostFree(c->h_xrecv);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -1060,19 +1097,21 @@ int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int6
   int rc = check_pod(c, pod, ids, ext);
   if (rc) return rc;
   if ((rc = flush_patches(c))) return rc;
-  if ((rc = upload_pods(c, pod, 1, ids, ext))) return rc;
-  if ((rc = scan_exchange(c, c->d_pods, c->d_ids, KSG_MODE_BEGIN, fail_codes ? c->d_fail : nullptr, nullptr)))
+  if ((rc = ensure_map(c)) || (rc = upload_one(c, pod, ids, ext))) return rc;
+  if ((rc = scan_exchange(c, c->one_pod, c->one_ids, KSG_MODE_BEGIN, fail_codes ? c->d_fail : nullptr, nullptr)))
     return rc;
-  HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods, c->d_ids, rec_buf(c), c->rec_bytes, c->world,
-                              c->d_shard_wlo, 0, 0, c->d_rng, nullptr, 0, c->d_summary, c->st));
+  HIPCHK(c, ksg_launch_decide(c->dev, c->one_pod, c->one_ids, rec_buf(c), c->rec_bytes, c->world,
+                              c->d_shard_wlo, 0, 0, c->d_rng, nullptr, 0, reinterpret_cast<int64_t*>(c->d_map),
+                              c->st));
   int64_t summ[3];
   const size_t nf = fail_codes ? (size_t)(c->hi - c->lo) : 0;
-  if ((rc = grow_host(c, &c->h_dn, &c->h_dn_cap, sizeof summ + nf))) return rc;
-  HIPCHK(c, hipMemcpyAsync(c->h_dn, c->d_summary, sizeof summ, hipMemcpyDeviceToHost, c->st));
-  if (nf) HIPCHK(c, hipMemcpyAsync(c->h_dn + sizeof summ, c->d_fail, nf, hipMemcpyDeviceToHost, c->st));
+  if (nf) {
+    if ((rc = grow_host(c, &c->h_dn, &c->h_dn_cap, nf))) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->h_dn, c->d_fail, nf, hipMemcpyDeviceToHost, c->st));
+  }
   HIPCHK(c, hipStreamSynchronize(c->st));
-  memcpy(summ, c->h_dn, sizeof summ);
-  if (nf) memcpy(fail_codes, c->h_dn + sizeof summ, nf);
+  memcpy(summ, c->h_map, sizeof summ);
+  if (nf) memcpy(fail_codes, c->h_dn, nf);
   if (summ[2]) return fail(c, KSG_ERR_NOPEER, "service affinity peer is not on a known node");
   if (max_score) *max_score = summ[1] > 0 ? summ[0] : 0;
   if (tie_count) *tie_count = (uint32_t)summ[1];
@@ -1087,14 +1126,14 @@ int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int6
 // the device half of a commit: decide the tie_index-th tie and apply AssumePod's delta
 static int commit_on_device(ksg_ctx* c, uint32_t tie_index, int32_t* node) {
   HIPCHK(c, hipSetDevice(c->device));
-  int rc = ensure_out(c, 1);
+  int rc = ensure_map(c);
   if (rc) return rc;
-  HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods, c->d_ids, rec_buf(c), c->rec_bytes, c->world,
-                              c->d_shard_wlo, 2, tie_index, c->d_rng, c->d_out, 0, c->d_summary, c->st));
-  if ((rc = grow_host(c, &c->h_dn, &c->h_dn_cap, 4))) return rc;
-  HIPCHK(c, hipMemcpyAsync(c->h_dn, c->d_out, 4, hipMemcpyDeviceToHost, c->st));
+  // the pending pod is still in d_one (begin's upload; nothing re-uploads before the commit)
+  HIPCHK(c, ksg_launch_decide(c->dev, c->one_pod, c->one_ids, rec_buf(c), c->rec_bytes, c->world,
+                              c->d_shard_wlo, 2, tie_index, c->d_rng, reinterpret_cast<int32_t*>(c->d_map + 32), 0,
+                              c->d_summary, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
-  memcpy(node, c->h_dn, 4);
+  memcpy(node, c->h_map + 32, 4);
   if (*node < 0) return fail(c, KSG_ERR_STATE, "commit selected no node (%d)", *node);
   return KSG_OK;
 }
@@ -1305,12 +1344,12 @@ int ksg_evaluate(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, uint8_t* f
   int rc = check_pod(c, pod, ids, ext);
   if (rc) return rc;
   if ((rc = flush_patches(c))) return rc;
-  if ((rc = upload_pods(c, pod, 1, ids, ext))) return rc;
+  if ((rc = upload_one(c, pod, ids, ext))) return rc;
   // errors surface through the BEGIN record, so run BEGIN first for the flag
-  if ((rc = scan_exchange(c, c->d_pods, c->d_ids, KSG_MODE_BEGIN, nullptr, nullptr))) return rc;
-  HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods, c->d_ids, rec_buf(c), c->rec_bytes, c->world,
+  if ((rc = scan_exchange(c, c->one_pod, c->one_ids, KSG_MODE_BEGIN, nullptr, nullptr))) return rc;
+  HIPCHK(c, ksg_launch_decide(c->dev, c->one_pod, c->one_ids, rec_buf(c), c->rec_bytes, c->world,
                               c->d_shard_wlo, 0, 0, c->d_rng, nullptr, 0, c->d_summary, c->st));
-  if ((rc = scan_exchange(c, c->d_pods, c->d_ids, KSG_MODE_EVAL, c->d_fail, c->d_score))) return rc;
+  if ((rc = scan_exchange(c, c->one_pod, c->one_ids, KSG_MODE_EVAL, c->d_fail, c->d_score))) return rc;
   int64_t summ[3];
   HIPCHK(c, hipMemcpyAsync(summ, c->d_summary, sizeof summ, hipMemcpyDeviceToHost, c->st));
   const size_t ns = c->hi - c->lo;
@@ -1349,6 +1388,16 @@ int ksg_last_batch_kernel_ms(ksg_ctx* c, double* out3) {
   if (!c || !out3) return KSG_ERR_ARG;
   KSG_LOCK(c);
   for (int i = 0; i < 3; ++i) out3[i] = c->last_kms[i];
+  return KSG_OK;
+}
+
+int ksg_debug_counters(ksg_ctx* c, int32_t* out32) {
+  if (!c || !out32) return KSG_ERR_ARG;
+  KSG_LOCK(c);
+  if (!c->dev.dbgbuf) return fail(c, KSG_ERR_STATE, "debug counters need KSG_DEBUG=8 at ksg_create");
+  (void)hipSetDevice(c->device);
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  HIPCHK(c, hipMemcpy(out32, c->dev.dbgbuf, 32 * sizeof(int32_t), hipMemcpyDeviceToHost));
   return KSG_OK;
 }
 

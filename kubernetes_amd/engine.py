@@ -220,6 +220,15 @@ class DeviceScheduler:
         self._lib.ksg_last_batch_kernel_ms(self._ctx, abi.ptr(o))
         return {"eval_ms": float(o[0]), "resolve_ms": float(o[1]), "launches": int(o[2])}
 
+    def debug_counters(self) -> np.ndarray:
+        """KSG_DEBUG=8 contexts: the window resolver's per-stage cycle counters
+        (cycles / 64, summed over every window so far)."""
+        o = np.zeros(32, np.int32)
+        rc = self._lib.ksg_debug_counters(self._ctx, abi.ptr(o))
+        if rc != abi.KSG_OK:
+            self._err(rc)
+        return o
+
     def last_batch_ms(self) -> float:
         ms = C.c_double(0)
         self._lib.ksg_last_batch_ms(self._ctx, C.byref(ms))

@@ -624,7 +624,10 @@ static int incr_fail_code(const orc *o, const pctx *c, uint32_t n) {
   return KSG_FAIL_NONE;
 }
 
-static int incr_prioritize(orc *o, const pctx *c, const uint8_t *fails, int64_t *score) {
+/* ext_dcount (n_anti x n_pairs, or NULL): ServiceAntiAffinity's domain counts
+ * supplied by the caller (the sum of the node shards' partial counts, as a
+ * sharded scan receives them from its all-reduce) instead of computed here */
+static int incr_prioritize(orc *o, const pctx *c, const uint8_t *fails, int64_t *score, const int32_t *ext_dcount) {
   const ksg_config *cf = &o->cfg;
   uint32_t nfilt = 0;
   for (uint32_t n = 0; n < o->N; ++n) nfilt += fails[n] == 0;
@@ -642,6 +645,10 @@ static int incr_prioritize(orc *o, const pctx *c, const uint8_t *fails, int64_t 
   int32_t *dcount[KSG_MAX_ANTI] = {0};
   for (uint32_t a = 0; a < cf->n_anti; ++a) {
     if (!cf->w_anti[a]) continue;
+    if (ext_dcount) {
+      dcount[a] = (int32_t *)ext_dcount + (size_t)a * o->n_pairs;
+      continue;
+    }
     dcount[a] = (int32_t *)calloc(o->n_pairs, 4);
     if (s >= 0)
       for (uint32_t n = 0; n < o->N; ++n) {
@@ -678,7 +685,8 @@ static int incr_prioritize(orc *o, const pctx *c, const uint8_t *fails, int64_t 
     sc += (int64_t)cf->w_equal;
     score[n] = sc;
   }
-  for (uint32_t a = 0; a < cf->n_anti; ++a) free(dcount[a]);
+  if (!ext_dcount)
+    for (uint32_t a = 0; a < cf->n_anti; ++a) free(dcount[a]);
   return any && nfilt > 0;
 }
 
@@ -699,7 +707,7 @@ static int evaluate(orc *o, const ksg_pod *p, const uint32_t *ids) {
     return faithful_prioritize(o, &c, o->fails, o->scores);
   }
   for (uint32_t n = 0; n < o->N; ++n) o->fails[n] = (uint8_t)incr_fail_code(o, &c, n);
-  return incr_prioritize(o, &c, o->fails, o->scores);
+  return incr_prioritize(o, &c, o->fails, o->scores, NULL);
 }
 
 typedef struct {
@@ -754,6 +762,54 @@ int orc_evaluate(orc *o, const ksg_pod *p, const uint32_t *ids, uint8_t *fail_ou
   if (o->N == 0) return KSG_NONODES;
   int r = evaluate(o, p, ids);
   if (r < 0) return r;
+  if (fail_out) memcpy(fail_out, o->fails, o->N);
+  if (score_out)
+    for (uint32_t n = 0; n < o->N; ++n) score_out[n] = o->fails[n] ? 0 : o->scores[n];
+  return KSG_OK;
+}
+
+/* The node-sharded ServiceAntiAffinity step, restated (ksg_runtime.cpp
+ * scan_exchange): a shard [lo, hi) sums, per anti priority a and label pair pr,
+ * the pod's service count over its FILTERED nodes labelled pr
+ * (spreading.go:118-139, over the shard's nodes only) into
+ * out[a * n_pairs + pr] (int32, wrapping as ncclSum); the shards' partials are
+ * all-reduced and every shard scores with the sum (orc_evaluate_counts). */
+int orc_domain_counts(orc *o, const ksg_pod *p, const uint32_t *ids, uint32_t lo, uint32_t hi, int32_t *out) {
+  const ksg_config *cf = &o->cfg;
+  memset(out, 0, (size_t)(cf->n_anti ? cf->n_anti : 1) * o->n_pairs * 4);
+  pctx c;
+  c.p = p;
+  c.ids = ids;
+  resolve_affinity(o, &c);
+  if (c.error) return KSG_ERR_NOPEER;
+  const int32_t s = p->service;
+  if (s < 0) return KSG_OK;
+  if (hi > o->N) hi = o->N;
+  for (uint32_t n = lo; n < hi; ++n) {
+    if (incr_fail_code(o, &c, n)) continue;
+    for (uint32_t a = 0; a < cf->n_anti; ++a) {
+      if (!cf->w_anti[a]) continue;
+      const int32_t pr = node_pair_for_key(o, n, cf->anti_key[a]);
+      if (pr >= 0) {
+        uint32_t *slot = (uint32_t *)&out[(size_t)a * o->n_pairs + pr];
+        *slot += (uint32_t)o->svc_cnt[(size_t)s * o->N + n];
+      }
+    }
+  }
+  return KSG_OK;
+}
+
+/* orc_evaluate (incremental mode) with the domain counts supplied */
+int orc_evaluate_counts(orc *o, const ksg_pod *p, const uint32_t *ids, const int32_t *dcount, uint8_t *fail_out,
+                        int64_t *score_out) {
+  if (o->N == 0) return KSG_NONODES;
+  pctx c;
+  c.p = p;
+  c.ids = ids;
+  resolve_affinity(o, &c);
+  if (c.error) return KSG_ERR_NOPEER;
+  for (uint32_t n = 0; n < o->N; ++n) o->fails[n] = (uint8_t)incr_fail_code(o, &c, n);
+  (void)incr_prioritize(o, &c, o->fails, o->scores, dcount);
   if (fail_out) memcpy(fail_out, o->fails, o->N);
   if (score_out)
     for (uint32_t n = 0; n < o->N; ++n) score_out[n] = o->fails[n] ? 0 : o->scores[n];

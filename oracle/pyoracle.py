@@ -41,6 +41,8 @@ def load():
         "orc_add_pod": (C.c_int, [vp, C.c_uint32, vp, vp]),
         "orc_remove_pod": (C.c_int, [vp, C.c_uint64]),
         "orc_evaluate": (C.c_int, [vp, vp, vp, vp, vp]),
+        "orc_domain_counts": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, vp]),
+        "orc_evaluate_counts": (C.c_int, [vp, vp, vp, vp, vp, vp]),
         "orc_schedule_begin": (C.c_int, [vp, vp, vp, C.c_size_t, P(C.c_int64), P(C.c_uint32), vp]),
         "orc_schedule_commit": (C.c_int, [vp, C.c_uint32, P(C.c_int32)]),
         "orc_schedule_batch": (C.c_int, [vp, vp, C.c_uint32, vp, C.c_uint32, P(C.c_uint64), vp]),
@@ -143,6 +145,24 @@ class OracleScheduler:
         scores = np.zeros(max(self.n_nodes, 1), np.int64)
         rc = self._lib.orc_evaluate(self._o, abi.ptr(pod), abi.ptr(_u32(batch.ids)), abi.ptr(fails),
                                     abi.ptr(scores))
+        return rc, fails[: self.n_nodes], scores[: self.n_nodes]
+
+    def domain_counts(self, batch: PodBatch, i: int, lo: int, hi: int, n_anti: int, n_pairs: int):
+        """ServiceAntiAffinity partial domain counts of pod i over the filtered
+        nodes of shard [lo, hi) (orc_domain_counts): int32[n_anti, n_pairs]."""
+        pod = np.ascontiguousarray(batch.pods[i : i + 1])
+        out = np.zeros((max(n_anti, 1), max(n_pairs, 1)), np.int32)
+        rc = self._lib.orc_domain_counts(self._o, abi.ptr(pod), abi.ptr(_u32(batch.ids)), lo, hi, abi.ptr(out))
+        return rc, out
+
+    def evaluate_counts(self, batch: PodBatch, i: int, dcount: np.ndarray):
+        """evaluate() scoring ServiceAntiAffinity with the supplied domain counts."""
+        pod = np.ascontiguousarray(batch.pods[i : i + 1])
+        fails = np.zeros(max(self.n_nodes, 1), np.uint8)
+        scores = np.zeros(max(self.n_nodes, 1), np.int64)
+        dc = np.ascontiguousarray(dcount, np.int32)
+        rc = self._lib.orc_evaluate_counts(self._o, abi.ptr(pod), abi.ptr(_u32(batch.ids)), abi.ptr(dc),
+                                           abi.ptr(fails), abi.ptr(scores))
         return rc, fails[: self.n_nodes], scores[: self.n_nodes]
 
     def shard(self):

@@ -120,3 +120,76 @@ def test_merge_rule_tie_order_and_errors():
     none = np.stack([make_shard_record(np.array([1]), np.array([0]), 0, 0, 2)] * 2)
     rc, node, _, _, st = merge_records(none, n, rng_state=9)
     assert rc == abi.KSG_NOFIT and st == 9  # no draw on FitError (generic_scheduler.go:72-77)
+
+
+def _anti_worker(rank, world, port, nn, npods, seed, q):
+    """ServiceAntiAffinity's sharded step (ksg_runtime.cpp scan_exchange): each
+    rank sums the pod's service counts over the filtered nodes of its own shard
+    per label domain, the partials are all-reduced (SUM, int32), every rank
+    scores its shard with the global counts, and the shard records go through
+    the product's winner rule."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        case = Case("config4", nn, npods)
+        n = case.view.arrays.n_nodes
+        n_pairs = len(case.view.arrays.pair_keys)
+        n_anti = int(case.cfg.n_anti)
+        lo, hi = shard_range(n, rank, world)
+        spans = [shard_range(n, g, world) for g in range(world)]
+        nwords_max = max((b + 63) // 64 - a // 64 for a, b in spans)
+        orc = OracleScheduler(case.cfg)
+        orc.set_cluster(case.view.arrays)
+        rng = seed
+        out, reduced_equal, split = [], True, 0
+        for i in range(len(case.batch)):
+            rc, part = orc.domain_counts(case.batch, i, lo, hi, n_anti, n_pairs)
+            t = torch.from_numpy(part.copy())
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            glob = t.numpy()
+            _, whole = orc.domain_counts(case.batch, i, 0, n, n_anti, n_pairs)
+            reduced_equal &= bool(np.array_equal(glob, whole))
+            split += int(0 < part.sum() < glob.sum())  # both shards hold counted pods
+            rc2, fails, scores = orc.evaluate_counts(case.batch, i, glob)
+            rec = make_shard_record(fails[lo:hi], scores[lo:hi], lo, lo // 64, nwords_max,
+                                    error=rc < 0 or rc2 < 0)
+            gathered = [torch.zeros(len(rec), dtype=torch.uint8) for _ in range(world)]
+            dist.all_gather(gathered, torch.from_numpy(rec))
+            recs = np.stack([g.numpy() for g in gathered])
+            mrc, node, _, _, rng = merge_records(recs, n, rng_state=rng)
+            if mrc == abi.KSG_OK:
+                orc.add_pod(node, case.batch, i)
+                out.append(node)
+            else:
+                out.append(abi.KSG_OUT_NOFIT if mrc == abi.KSG_NOFIT else abi.KSG_OUT_ERROR)
+        q.put((rank, out, rng, reduced_equal, split))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_anti_affinity_domain_allreduce():
+    """World-2 gloo rehearsal of the ServiceAntiAffinity all-reduce path: the
+    summed shard partials equal the whole cluster's domain counts for every pod,
+    and scoring each shard with them reproduces the single-process schedule."""
+    nn, npods, seed = 450, 400, 4321
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_anti_worker, args=(r, WORLD, port, nn, npods, seed, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(WORLD)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    case = Case("config4", nn, npods)
+    assert int(case.cfg.n_anti) > 0
+    orc = OracleScheduler(case.cfg)
+    orc.set_cluster(case.view.arrays)
+    want, st = orc.batch(case.batch, seed)
+    for rank, out, rng, reduced_equal, split in res:
+        assert reduced_equal, rank
+        assert split >= 20, split  # the reduction actually combines two shards
+        assert np.array_equal(np.asarray(out), want), rank
+        assert rng == st

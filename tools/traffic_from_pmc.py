@@ -14,7 +14,8 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = {"ksg_win_resolve_kernel": "ksg_win_resolve_kernel", "ksg_win_score_kernel": "ksg_win_score_kernel",
+KERNELS = {"ksg_win_resolve_kernel": "ksg_win_resolve_kernel", "ksg_win_resolve2_kernel": "ksg_win_resolve2_kernel",
+           "ksg_win_resolve3_kernel": "ksg_win_resolve3_kernel", "ksg_win_score_kernel": "ksg_win_score_kernel",
            "ksg_batch_kernel": "ksg_batch_kernel"}
 
 
