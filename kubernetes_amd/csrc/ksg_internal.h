@@ -142,6 +142,11 @@ struct KsgWinXchg {
   uint32_t fit_off;   // ServiceAntiAffinity: byte offset in a block of the fit bitmaps
                       // uint64[wcap][ostride] (nodes the pod fits at the snapshot), else 0
   uint32_t wlo[KSG_MAX_WORLD], nw[KSG_MAX_WORLD];
+  // ServiceAntiAffinity: the window's per-(pod, domain) counts the count pass
+  // accumulates; the resolver zeroes them for the next window's count pass (its
+  // score pass has read them), so no per-window fill is enqueued
+  int32_t* dcnt;
+  uint32_t dcnt_n;
 };
 
 // Device-side progress of a chain of windows (ksg_window.hip): the host enqueues

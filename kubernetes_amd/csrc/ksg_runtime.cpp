@@ -1190,7 +1190,16 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     // every rank runs the same resolver over the whole replicated node state, so
     // every rank commits the same pods to the same nodes.
     const KsgDev full = full_geometry(c);
-    const uint32_t W = std::min(c->window, ksg_win_max_window(full));
+    uint32_t W = std::min(c->window, ksg_win_max_window(full));
+    // Phase A scores all W pods of a window whatever the resolver gets through.
+    // Where windows stop early (ServiceAntiAffinity: every ~13 pods on config 4)
+    // the capacity follows the pods per window measured on earlier batches: 3x
+    // that, in pod groups of 8, at least 16. (A sharded context keeps W: every
+    // rank must size its launches alike, and its estimate restarts each batch.)
+    if (!c->xchg && c->ppw_est > 0.0) {
+      const uint32_t want = ((uint32_t)std::ceil(3.0 * c->ppw_est) + 7u) & ~7u;
+      W = std::min(W, std::max<uint32_t>(want, 16u));
+    }
     KsgWinXchg x{};
     x.ostride = std::max<uint32_t>(c->nwords_max, 1);
     x.wcap = W;
@@ -1203,10 +1212,16 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     }
     const bool anti = anti_on(c);
     const size_t fit_off = ((size_t)W * x.ostride * 12 + 7) & ~(size_t)7;
+    // (the domain counts are zeroed once here, then by each resolver for the next window)
     x.fit_off = anti ? (uint32_t)fit_off : 0u;
     x.blk = ((anti ? fit_off + (size_t)W * x.ostride * 8 : (size_t)W * x.ostride * 12) + 255) & ~(size_t)255;
     const size_t dcnt_n = (size_t)W * std::max<uint32_t>(c->D, 1);
-    if (anti && (rc = grow(c, (void**)&c->d_dcnt, &c->dcnt_cap, dcnt_n, sizeof(int32_t)))) return rc;
+    if (anti) {
+      if ((rc = grow(c, (void**)&c->d_dcnt, &c->dcnt_cap, dcnt_n, sizeof(int32_t)))) return rc;
+      HIPCHK(c, hipMemsetAsync(c->d_dcnt, 0, dcnt_n * sizeof(int32_t), c->st));
+      x.dcnt = c->d_dcnt;
+      x.dcnt_n = (uint32_t)dcnt_n;
+    }
     if ((rc = grow(c, (void**)&c->d_winsum, &c->win_cap, W, sizeof(KsgWinSum)))) return rc;
     if ((rc = grow(c, (void**)&c->d_xsend, &c->xsend_cap, x.blk, 1))) return rc;
     if (c->xchg && (rc = grow(c, (void**)&c->d_xrecv, &c->xrecv_cap, x.blk * c->world, 1))) return rc;
@@ -1244,7 +1259,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
         // HIP events on this stream around each kernel (per-kernel device time)
         if (anti) {
           // ServiceAntiAffinity: the pods' per-domain counts over their filtered nodes first
-          HIPCHK(c, hipMemsetAsync(c->d_dcnt, 0, dcnt_n * sizeof(int32_t), c->st));
+          // (into d_dcnt, zero: the previous resolver cleared it)
           HIPCHK(c, ksg_launch_win_eval(c->dev, 1, c->d_pods, c->d_ids, c->d_run, W, c->d_winsum, wbits, wmax,
                                         x.ostride, c->d_dcnt, nullptr, c->st));
           if (c->xchg && (rc = allreduce_sum_i32(c, c->d_dcnt, c->d_dcnt, (uint32_t)dcnt_n))) return rc;

@@ -645,6 +645,9 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
   const uint32_t nwords = d.nwords;
   constexpr uint32_t KSG_RING = win_ring(P);
   constexpr uint32_t KSG_RES_NT = win_res_nt(P);
+  if constexpr (ANTI) {  // this window's score pass has read the domain counts: zero them for the next
+    for (uint32_t t = tid; t < x.dcnt_n; t += KSG_RES_NT) x.dcnt[t] = 0;
+  }
   constexpr bool anti_on = ANTI;  // (the host passes fit bitmaps, x.fit_off != 0, exactly then)
   const WinLdsOff o = win_lds_offsets(P, nflag, wcap, anti_on);
   WinCtl* ctl = reinterpret_cast<WinCtl*>(smem + o.ctl);
