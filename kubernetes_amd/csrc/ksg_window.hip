@@ -1517,6 +1517,7 @@ struct alignas(16) WinCtl2 {
   // the node pod xn_seq - 1 drew (~0u: no commit), posted right after the draw
   // so the x-checker's work overlaps the rest of the commit
   uint32_t xn_seq, xn_node;
+  uint32_t fin_x;                     // the x-checker applied every commit's flags and first peers
   uint32_t pad[1];
   uint32_t t_x, t_n;                  // KSG_DEBUG & 8: clock at the xres / xn posts
 };
@@ -1673,7 +1674,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
           ctl->hang = 1;
           return;
         }
-        uint32_t done = ld_acq(&ctl->xseq) + 1;  // (the x-checker of pod i reads pod i-1's entry)
+        uint32_t done = ld_acq(&ctl->xseq);  // (the x-checker of pod i reads pod i-1's entry until it is done)
 #pragma unroll
         for (int c = 0; c < KSG_RES_NCHK; ++c) done = min(done, ld_acq(&ctl->chk_seq[c]));
         if (j < RING || done + RING >= j + 3) break;
@@ -1798,8 +1799,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     S.nk = S.ns = S.smask = 0;
     // AssumePod of pod p (plugin/pkg/scheduler/scheduler.go:115-118) into the
     // owner lane's slot: requested totals, list lengths; the services' snapshot
-    // counts into the table; the service flags (maxCount rises, first peer)
-    // later pods of the window stop on
+    // counts into the table (the x-checker applies the service flags, in commit
+    // order)
     auto apply = [&](uint32_t p) {
       const uint32_t kind = __builtin_amdgcn_readfirstlane(L_cm[p].kind);
       const uint32_t slot = __builtin_amdgcn_readfirstlane(L_cm[p].slot);
@@ -1841,43 +1842,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         const bool sv_lane = lane < n_svcs;
         const uint32_t my_sv =
             (uint32_t)__shfl((int)prec, (int)min(WS_IDS + nk + n_sel + (sv_lane ? lane : 0u), 63u), 64);
-        int32_t cnt = 0, mx = 0, peer = 0;
-        if (sv_lane) {
-          cnt = is_pred ? r_svc[ep].cnt[lane] : gld(d.svc_cnt + (size_t)my_sv * d.n_nodes + wn);
-          mx = r_svc[ep].max[lane];
-          peer = r_svc[ep].peer[lane];
-        }
-        // earlier window commits of each service on this node (table lanes KSG_CL_SV..)
-        const uint32_t ent = lane - KSG_CL_SV < base_ns ? L_cl[(size_t)slot * KSG_CL_W + lane] : ~0u;
-        uint32_t before = 0;
-        for (uint32_t t = 0; t < n_svcs; ++t) {
-          const uint32_t sv_t = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)t);
-          const uint32_t b_t = (uint32_t)__popcll(__ballot(ent == sv_t));
-          if (lane == t) before = b_t;
-        }
-        bool changed = sv_lane && aff_on && peer == -1 && !((L_peerset[my_sv >> 5] >> (my_sv & 31)) & 1u);
-        // first commit of a service with no peer yet: its first peer, in commit order
-        uint64_t pm = __ballot(sv_lane && peer == -1);
-        if (pm) {
-          uint32_t n_peer = __builtin_amdgcn_readfirstlane(ctl->n_peer);
-          while (pm) {
-            const uint32_t b = __builtin_ctzll(pm);
-            pm &= pm - 1;
-            const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)b);
-            if (!((L_peerset[fsv >> 5] >> (fsv & 31)) & 1u)) {
-              if (lane == 0) {
-                L_peerset[fsv >> 5] |= 1u << (fsv & 31);
-                L_peer[2 * n_peer] = fsv;
-                L_peer[2 * n_peer + 1] = wn;
-              }
-              ++n_peer;
-              lds_fence();
-            }
-          }
-          if (lane == 0) ctl->n_peer = n_peer;
-        }
-        if (sv_lane && spread_on && cnt + (int32_t)before + 1 > mx) changed = true;  // maxCount rises
-        if (changed) atomicOr(&L_flag[my_sv >> 5], 1u << (my_sv & 31));
+        int32_t cnt = 0;
+        if (sv_lane) cnt = is_pred ? r_svc[ep].cnt[lane] : gld(d.svc_cnt + (size_t)my_sv * d.n_nodes + wn);
         if (sv_lane) L_cl[(size_t)slot * KSG_CL_W + KSG_CL_SC + base_ns + lane] = (uint32_t)cnt;
         new_mask = wave_or_u32(sv_lane ? (1u << (my_sv & 31)) : 0u);
       }
@@ -1917,6 +1883,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
           stopped = true;
           break;
         }
+        __builtin_amdgcn_s_sleep(2);  // (off the chain: leave the LDS to the committer and the x-checker)
       }
       acq_lds();
       cstamp(c == 0 ? 16 : 19);
@@ -2036,9 +2003,98 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     const double* const inv_src = rl ? d.inv10_mem : d.inv10_cpu;
     uint32_t xcn0 = ~0u, xcn1 = ~0u, xsk0 = 0, xsk1 = 0, xss0 = 0, xss1 = 0, xn_slots = 0;
     int64_t xdc0 = 0, xdm0 = 0, xdc1 = 0, xdm1 = 0;
+    // commit q (node) into its slot, the committer's bookkeeping replayed: the
+    // slot, its list lengths before q, its delta after q, pod q's record
+    auto replay = [&](uint32_t q, uint32_t node, uint32_t& slot, uint32_t& bnk, uint32_t& bns, uint64_t& dlc,
+                      uint64_t& dlm, uint32_t& prec) {
+      const uint32_t eq = q % RING;
+      prec = lane < DW ? r_rec[eq * DW + lane] : 0u;
+      const PodView ppv = pod_view(prec);
+      const uint32_t p_svcs = (uint32_t)__builtin_amdgcn_readlane(prec, WS_NSS) >> 16;
+      const uint64_t hit0 = __ballot(xcn0 == node), hit1 = __ballot(xcn1 == node);
+      const bool in_c = (hit0 | hit1) != 0;
+      bnk = bns = 0;
+      dlc = dlm = 0;
+      if (in_c) {
+        slot = hit0 ? (uint32_t)__builtin_ctzll(hit0) : 64u + (uint32_t)__builtin_ctzll(hit1);
+        const uint32_t sl = slot & 63;
+        bnk = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? xsk0 : xsk1), (int)sl);
+        bns = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? xss0 : xss1), (int)sl);
+        dlc = readlane64((uint64_t)(slot < 64 ? xdc0 : xdc1), (int)sl);
+        dlm = readlane64((uint64_t)(slot < 64 ? xdm0 : xdm1), (int)sl);
+      } else {
+        slot = xn_slots < KSG_MAX_SLOTS ? xn_slots++ : 0u;  // (a full table stops the committer)
+      }
+      dlc += (uint64_t)ppv.req_c;
+      dlm += (uint64_t)ppv.req_m;
+      if (lane == (slot & 63)) {
+        if (slot >= 64) {
+          if (!in_c) xcn1 = node;
+          xsk1 = bnk + ppv.nk;
+          xss1 = bns + p_svcs;
+          xdc1 = (int64_t)dlc;
+          xdm1 = (int64_t)dlm;
+        } else {
+          if (!in_c) xcn0 = node;
+          xsk0 = bnk + ppv.nk;
+          xss0 = bns + p_svcs;
+          xdc0 = (int64_t)dlc;
+          xdm0 = (int64_t)dlm;
+        }
+      }
+    };
+    // the service flags later pods stop on (maxCount rises, first peer) and the
+    // first peers of commit q, in commit order (one wave: L_peer, n_peer and
+    // L_peerset have a single writer)
+    auto flags = [&](uint32_t q, uint32_t node, uint32_t slot, uint32_t bns, uint32_t prec) {
+      const uint32_t nss = __builtin_amdgcn_readlane(prec, WS_NSS), npp = __builtin_amdgcn_readlane(prec, WS_NPP);
+      const uint32_t n_svcs = nss >> 16, n_sel = nss & 0xffff, pnk = (npp & 0xffff) + (npp >> 16);
+      if (!n_svcs) return;
+      const uint32_t wn = d.lo + node, eq = q % RING;
+      const bool sv_lane = lane < n_svcs;
+      const uint32_t my_sv =
+          (uint32_t)__shfl((int)prec, (int)min(WS_IDS + pnk + n_sel + (sv_lane ? lane : 0u), 63u), 64);
+      int32_t mx = 0, peer = 0, cnt = 0;
+      if (sv_lane) {
+        cnt = gld(d.svc_cnt + (size_t)my_sv * d.n_nodes + wn);
+        mx = r_svc[eq].max[lane];
+        peer = r_svc[eq].peer[lane];
+      }
+      // earlier window commits of each service on this node (table lanes KSG_CL_SV..)
+      const uint32_t ent = lane - KSG_CL_SV < bns ? L_cl[(size_t)slot * KSG_CL_W + lane] : ~0u;
+      uint32_t before = 0;
+      for (uint32_t t = 0; t < n_svcs; ++t) {
+        const uint32_t sv_t = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)t);
+        const uint32_t b_t = (uint32_t)__popcll(__ballot(ent == sv_t));
+        if (lane == t) before = b_t;
+      }
+      bool changed = sv_lane && aff_on && peer == -1 && !((L_peerset[my_sv >> 5] >> (my_sv & 31)) & 1u);
+      uint64_t pm = __ballot(sv_lane && peer == -1);
+      if (pm) {  // first commit of a service with no peer yet: its first peer
+        uint32_t n_peer = __builtin_amdgcn_readfirstlane(ctl->n_peer);
+        while (pm) {
+          const uint32_t b = __builtin_ctzll(pm);
+          pm &= pm - 1;
+          const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)b);
+          if (!((L_peerset[fsv >> 5] >> (fsv & 31)) & 1u)) {
+            if (lane == 0) {
+              L_peerset[fsv >> 5] |= 1u << (fsv & 31);
+              L_peer[2 * n_peer] = fsv;
+              L_peer[2 * n_peer + 1] = wn;
+            }
+            ++n_peer;
+            lds_fence();
+          }
+        }
+        if (lane == 0) ctl->n_peer = n_peer;
+      }
+      if (sv_lane && spread_on && cnt + (int32_t)before + 1 > mx) changed = true;  // maxCount rises
+      if (changed) atomicOr(&L_flag[my_sv >> 5], 1u << (my_sv & 31));
+    };
     uint64_t x_last = 0, x_acc = 0;  // KSG_DEBUG & 8: lanes 28..30 wait, check, loads
     if constexpr (STAMP) x_last = __builtin_amdgcn_s_memtime();
-    for (uint32_t i = 0; i < n_pods; ++i) {
+    uint32_t i = 0;
+    for (; i < n_pods; ++i) {
       const uint32_t e = i % RING, par = i & 1;
       bool stopped = false;
       for (uint32_t spin = 0;; ++spin) {  // pod i-1's node drawn and pod i staged, or the end
@@ -2084,41 +2140,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       uint32_t xslot = 0, bnk = 0, bns = 0;
       uint64_t dlc = 0, dlm = 0;
       uint32_t prec = 0;
-      if (xnode != ~0u) {
-        const uint32_t ep = (i - 1) % RING;
-        prec = lane < DW ? r_rec[ep * DW + lane] : 0u;
-        const PodView ppv = pod_view(prec);
-        const uint32_t p_svcs = (uint32_t)__builtin_amdgcn_readlane(prec, WS_NSS) >> 16;
-        const uint64_t hit0 = __ballot(xcn0 == xnode), hit1 = __ballot(xcn1 == xnode);
-        const bool in_c = (hit0 | hit1) != 0;
-        if (in_c) {
-          xslot = hit0 ? (uint32_t)__builtin_ctzll(hit0) : 64u + (uint32_t)__builtin_ctzll(hit1);
-          const uint32_t sl = xslot & 63;
-          bnk = (uint32_t)__builtin_amdgcn_readlane((int)(xslot < 64 ? xsk0 : xsk1), (int)sl);
-          bns = (uint32_t)__builtin_amdgcn_readlane((int)(xslot < 64 ? xss0 : xss1), (int)sl);
-          dlc = readlane64((uint64_t)(xslot < 64 ? xdc0 : xdc1), (int)sl);
-          dlm = readlane64((uint64_t)(xslot < 64 ? xdm0 : xdm1), (int)sl);
-        } else {
-          xslot = xn_slots < KSG_MAX_SLOTS ? xn_slots++ : 0u;  // (a full table stops the committer)
-        }
-        dlc += (uint64_t)ppv.req_c;
-        dlm += (uint64_t)ppv.req_m;
-        if (lane == (xslot & 63)) {
-          if (xslot >= 64) {
-            if (!in_c) xcn1 = xnode;
-            xsk1 = bnk + ppv.nk;
-            xss1 = bns + p_svcs;
-            xdc1 = (int64_t)dlc;
-            xdm1 = (int64_t)dlm;
-          } else {
-            if (!in_c) xcn0 = xnode;
-            xsk0 = bnk + ppv.nk;
-            xss0 = bns + p_svcs;
-            xdc0 = (int64_t)dlc;
-            xdm0 = (int64_t)dlm;
-          }
-        }
-      }
+      if (xnode != ~0u) replay(i - 1, xnode, xslot, bnk, bns, dlc, dlm, prec);
       if (do_check) {
         // pod i-1's record: its keys and service ids follow the earlier commits' in the slot's lists
         const uint32_t pnpp = __builtin_amdgcn_readlane(prec, WS_NPP), pnss = __builtin_amdgcn_readlane(prec, WS_NSS);
@@ -2180,15 +2202,37 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         if constexpr (STAMP) ctl->t_x = (uint32_t)__builtin_amdgcn_s_memtime();
         st_rel(&ctl->xseq, i + 1);
       }
+      // off the chain now: commit i-1's service flags and first peers (the
+      // committer reads them for pod i+1 once this iteration is done)
+      if (xnode != ~0u) flags(i - 1, xnode, xslot, bns, prec);
       if constexpr (STAMP) {
         const uint64_t t_now = __builtin_amdgcn_s_memtime();
         x_acc += lane == 29 ? t_now - x_last : 0ULL;
         x_last = t_now;
       }
     }
+    // the committer is done: the commits from i-1 on were not replayed yet; their
+    // first peers still count (the window's end writes them)
+    for (uint32_t spin = 0; !ld_acq(&ctl->stop); ++spin) {
+      if (spin > 16 * KSG_SPIN_LIMIT) {
+        ctl->hang = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const uint32_t R = __builtin_amdgcn_readfirstlane(ctl->resolved);
+    for (uint32_t q = i >= 1 ? i - 1 : 0; q < R; ++q) {
+      if (__builtin_amdgcn_readfirstlane(L_cm[q].kind) != 1) continue;
+      const uint32_t node = __builtin_amdgcn_readfirstlane(L_cm[q].node);
+      uint32_t slot, bnk, bns, prec;
+      uint64_t dlc, dlm;
+      replay(q, node, slot, bnk, bns, dlc, dlm, prec);
+      flags(q, node, slot, bns, prec);
+    }
     if constexpr (STAMP) {
       if (lane >= 28 && lane < 32) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
     }
+    if (lane == 0) st_rel(&ctl->fin_x, 1u);
     return;
   }
   if (wave != 0) return;
@@ -2424,10 +2468,11 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     ctl->resolved = resolved;
     st_rel(&ctl->stop, 1u);
   }
-  // the checkers apply the last commits and write their slots back
+  // the checkers apply the last commits and write their slots back; the
+  // x-checker records the last first peers
   bool drained = false;
   for (uint32_t spin = 0; spin <= 16 * KSG_SPIN_LIMIT; ++spin) {
-    bool done = true;
+    bool done = ld_acq(&ctl->fin_x) != 0;
 #pragma unroll
     for (int c = 0; c < KSG_RES_NCHK; ++c) done = done && ld_acq(&ctl->fin[c]) != 0;
     if (done) {
@@ -3491,6 +3536,1165 @@ __global__ __launch_bounds__(win3_nt(P)) void ksg_win_resolve3_kernel(KsgDev d, 
 }
 
 // ---------------------------------------------------------------------------
+// phase B, lag-3 resolver (every configuration without ServiceAntiAffinity)
+// ---------------------------------------------------------------------------
+// The register-slot resolver above spends its chain per pod on a select (a
+// scan over T0 minus the drops) and a hand-off to and from the x-checker. Here
+// the checkers run two pods ahead instead of one, which leaves them and a
+// pre-selector time to stage everything the draw can land on:
+//  CHECKERS (waves 3, 4; lane l of checker c owns slot 64c + l, register
+//    state as above) apply commit i-3 and test pod i against their slots, as
+//    soon as commit i-3 is published.
+//  PRE-SELECTOR (wave 2), once the checkers are done with pod i: the live ties
+//    L0 = T0 minus their d drops, k' = k0 - d, and for e = 0, 1, 2 further
+//    drops (the nodes of commits i-2 and i-1, which the checkers did not see)
+//    the e+1 nodes of L0 from the (r mod (k'-e))-th from the top down: A; B0,
+//    B1; C0, C1, C2 (the e-th answer is the first of them whose rank in L0
+//    minus the dropped nodes is right). Also: which of pods i-1's and i-2's
+//    candidates lie in L0, and the six candidates' snapshots plus pod i+1's
+//    service count on each (prefetched for the committer's next re-check).
+//  X2-CHECKER (wave 1) follows the commits in order: it applies each commit's
+//    service flags (maxCount rises, first peers), and re-checks pod i against
+//    the node of commit i-2 as of that commit.
+//  COMMITTER (wave 0) re-checks pod i against commit i-1's node itself (the
+//    node's snapshot came with its candidate; its delta and lists are the
+//    committer's own), counts the two late drops, picks among the six staged
+//    candidates with a few scalar compares, and commits.
+//  PRODUCERS stage pods into the ring as above.
+__host__ __device__ constexpr uint32_t win4_nt(uint32_t P) { return P <= 8 ? 1024u : 512u; }
+#define KSG_R4_X2 1  // x2-checker wave
+#define KSG_R4_PS 2  // pre-selector wave
+#define KSG_R4_C0 3  // first checker wave
+#define KSG_R4_P0 (KSG_R4_C0 + KSG_RES_NCHK)
+#define KSG_R4_NCAND 6
+#define KSG_R4_NB 4  // per-pod buffers (drops, candidates) by pod index mod 4
+
+struct alignas(16) WinCommit4 {
+  uint32_t kind;   // 0: no commit (error / no fit), 1: commit
+  uint32_t slot;
+  uint32_t node;   // shard offset of the node
+  uint32_t flags;  // bit 0: a new slot, bits 2..4: the candidate it was drawn as, bits 8..15: n_svcs
+};
+struct alignas(16) WinCand4 {  // the pre-selector's verdict for one pod
+  uint32_t status;  // KSG_CS_*
+  uint32_t kp;      // k' = k0 - the checkers' drops
+  uint32_t xlive;   // bits 0..5: pod i-1's candidate j is in L0; bits 6..11: pod i-2's
+  uint32_t pad;
+  uint32_t c[8];    // A, B0, B1, C0, C1, C2 (KSG_NO_NODE where k' is too small)
+};
+struct alignas(16) WinCtl4 {
+  uint32_t stop;      // the committer is done: pods [0, resolved) are decided
+  uint32_t resolved;
+  uint32_t sel_seq;   // commits published for pods [0, sel_seq)
+  uint32_t psel_seq;  // pods the pre-selector is done with
+  uint32_t chk_seq[KSG_RES_NCHK];
+  uint32_t chk_cnt[KSG_RES_NCHK][KSG_R4_NB];
+  uint32_t fin[KSG_RES_NCHK];
+  uint32_t fin_x;     // the x2-checker applied every commit's flags and first peers
+  uint32_t hang;
+  uint32_t n_peer;
+  uint32_t x2_seq;    // pods the x2-checker is done with
+  uint32_t x2_res[KSG_R4_NB];      // bit 0: pod i's node of commit i-2 drops
+  uint32_t csnap_seq[KSG_R4_NB];   // pod + 1 whose candidates' snapshots are staged
+  uint32_t pad[2];
+};
+
+struct WinLdsOff4 {
+  uint32_t ctl, r_hdr, r_t0, r_rec, r_mod, r_svc;
+  uint32_t cm, out, peer, flag, peerset, drop, pub, drw, clist, cand, csnap, csc;
+  uint32_t total;
+};
+
+__host__ __device__ inline WinLdsOff4 win4_lds_offsets(uint32_t P, uint32_t nflag, uint32_t W) {
+  WinLdsOff4 o;
+  const uint32_t R = win_ring(P);
+  uint32_t at = 0;
+  o.ctl = at;     at += win_al16(sizeof(WinCtl4));
+  o.r_hdr = at;   at += win_al16((size_t)R * sizeof(RingHdr3));
+  o.r_t0 = at;    at += win_al16((size_t)R * P * 64 * 8);
+  o.r_rec = at;   at += win_al16((size_t)R * KSG_WIN_SUM_DWORDS * 4);
+  o.r_mod = at;   at += win_al16((size_t)R * 64 * 4);
+  o.r_svc = at;   at += win_al16((size_t)R * sizeof(RingSvc3));
+  o.cm = at;      at += win_al16((size_t)W * sizeof(WinCommit4));
+  o.out = at;     at += win_al16((size_t)W * 4);
+  o.peer = at;    at += win_al16((size_t)W * 2 * 4);
+  o.flag = at;    at += win_al16((size_t)nflag * 4);
+  o.peerset = at; at += win_al16((size_t)nflag * 4);
+  o.drop = at;    at += win_al16((size_t)KSG_R4_NB * P * 64 * 8);
+  o.pub = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
+  o.drw = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
+  o.clist = at;   at += win_al16((size_t)KSG_MAX_SLOTS * KSG_CL_W * 4);
+  o.cand = at;    at += win_al16((size_t)KSG_R4_NB * sizeof(WinCand4));
+  o.csnap = at;   at += win_al16((size_t)KSG_R4_NB * KSG_R4_NCAND * 6 * 8);  // cap c/m, used c/m, 10/cap c/m
+  o.csc = at;     at += win_al16((size_t)KSG_R4_NB * 8 * 4);  // the next pod's service count on each candidate
+  o.total = at;
+  return o;
+}
+
+// lane-parallel re-check of pod `rec` against one node x as of its latest
+// commit: lanes 0..3 hold resource L & 1's capacity, snapshot requested total,
+// 10/capacity and window delta; lane t < 8 x's key t, lane 8 + u its service
+// entry u (xcl); x_snapc: the pod's service's count on x at the snapshot.
+// Returns bit 0: x scores below M0 now, bit 1: the pod's service scalars moved
+// (commit `prev_lo`.. of x was a pod of its service: maxCount rises / first peer).
+struct XState {
+  int64_t cap, snp, dl;  // resource lane & 1
+  double inv;
+  uint32_t nk, ns;       // x's list lengths
+};
+__device__ __forceinline__ uint32_t recheck_x(const KsgDev& d, const PodView& pv, uint32_t rec, const XState& xs,
+                                              uint32_t xcl, uint32_t new_from, int32_t x_snapc, bool res_on,
+                                              bool ports_on, bool disk_on, bool spread_on, bool aff_on,
+                                              int32_t peer0, bool peerset_s, uint32_t lane) {
+  const uint32_t rl = lane & 1;
+  const int64_t reqv = rl ? pv.req_m : pv.req_c;
+  const int64_t nowv = (int64_t)((uint64_t)xs.snp + (uint64_t)xs.dl);
+  bool xd = false, flag = false;
+  if (res_on && !pv.zero_req)  // PodFitsResources: lanes 0 and 1
+    xd = (__ballot(lane < 2 && !(xs.cap == 0 || xs.cap - nowv >= reqv)) & 3ULL) != 0;
+  if (d.w_lr) {  // LeastRequested: lanes 0, 1 now, lanes 2, 3 at the snapshot
+    const int32_t lrv = lr_win((lane < 2 ? nowv : xs.snp) + reqv, xs.cap, xs.inv);
+    const int32_t lr_now = __builtin_amdgcn_readlane(lrv, 0) + __builtin_amdgcn_readlane(lrv, 1);
+    const int32_t lr_snap = __builtin_amdgcn_readlane(lrv, 2) + __builtin_amdgcn_readlane(lrv, 3);
+    xd |= (lr_now >> 1) != (lr_snap >> 1);
+  }
+  const uint32_t ut = lane - KSG_CL_SV;
+  const int32_t s = pv.s;
+  if (s >= 0) {
+    const uint64_t smk = __ballot(ut < xs.ns && xcl == (uint32_t)s);
+    if (smk) {
+      const int32_t cnt = (int32_t)__popcll(smk);
+      if (spread_on) {  // ServiceSpreading under an unchanged maxCount: lane 0 now, lane 1 the snapshot
+        const int32_t fr = (int32_t)frac10_f32((int64_t)pv.smax - x_snapc - (lane == 0 ? cnt : 0), pv.smax);
+        xd |= __builtin_amdgcn_readlane(fr, 0) != __builtin_amdgcn_readlane(fr, 1);
+      }
+      if ((smk >> (KSG_CL_SV + new_from)) != 0) {  // the latest commit was a pod of service s
+        flag = spread_on && x_snapc + cnt > pv.smax;
+        if (aff_on && peer0 == -1 && !peerset_s) flag = true;
+      }
+    }
+  }
+  if (pv.nk && xs.nk) {  // PodFitsPorts / NoDiskConflict
+    bool hit = false;
+    for (uint32_t b = 0; b < pv.nk; ++b) {
+      const bool on = b < pv.n_ports ? ports_on : disk_on;
+      hit |= on && lane < xs.nk && xcl == (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b));
+    }
+    xd |= __ballot(hit) != 0;
+  }
+  return (xd ? 1u : 0u) | (flag ? 2u : 0u);
+}
+
+template <int P, bool STAMP>
+__global__ __launch_bounds__(win4_nt(P)) void ksg_win_resolve4_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
+                                                                    const KsgWinSum* __restrict__ sums,
+                                                                    const KsgWinXchg x, uint64_t* rng_io,
+                                                                    int32_t* __restrict__ out_batch) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t pos = run->pos, n_batch = run->n;
+  if (run->halt || pos >= n_batch) return;  // the chain is done (uniform, before any barrier)
+  const uint32_t n_pods = min(wcap, n_batch - pos);
+  int32_t* __restrict__ out = out_batch + pos;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t nflag = (d.n_services + 31) / 32;
+  const uint32_t nwords = d.nwords;
+  constexpr uint32_t RING = win_ring(P);
+  constexpr uint32_t NT = win4_nt(P);
+  constexpr uint32_t NPW = NT / 64 - KSG_R4_P0;  // producer waves
+  constexpr uint32_t DW = KSG_WIN_SUM_DWORDS;
+  constexpr uint32_t PW = P * 64;
+  const WinLdsOff4 o = win4_lds_offsets(P, nflag, wcap);
+  WinCtl4* ctl = reinterpret_cast<WinCtl4*>(smem + o.ctl);
+  RingHdr3* r_hdr = reinterpret_cast<RingHdr3*>(smem + o.r_hdr);
+  uint64_t* r_t0 = reinterpret_cast<uint64_t*>(smem + o.r_t0);
+  uint32_t* r_rec = reinterpret_cast<uint32_t*>(smem + o.r_rec);
+  uint32_t* r_mod = reinterpret_cast<uint32_t*>(smem + o.r_mod);
+  RingSvc3* r_svc = reinterpret_cast<RingSvc3*>(smem + o.r_svc);
+  WinCommit4* L_cm = reinterpret_cast<WinCommit4*>(smem + o.cm);
+  int32_t* L_out = reinterpret_cast<int32_t*>(smem + o.out);
+  uint32_t* L_peer = reinterpret_cast<uint32_t*>(smem + o.peer);
+  uint32_t* L_flag = reinterpret_cast<uint32_t*>(smem + o.flag);
+  uint32_t* L_peerset = reinterpret_cast<uint32_t*>(smem + o.peerset);
+  uint64_t* L_drop = reinterpret_cast<uint64_t*>(smem + o.drop);  // [NB][PW] by pod index mod NB
+  uint32_t* L_pub = reinterpret_cast<uint32_t*>(smem + o.pub);
+  uint32_t* L_drw = reinterpret_cast<uint32_t*>(smem + o.drw);
+  uint32_t* L_cl = reinterpret_cast<uint32_t*>(smem + o.clist);   // [slot][KSG_CL_W]
+  WinCand4* L_cand = reinterpret_cast<WinCand4*>(smem + o.cand);  // [NB]
+  int64_t* L_csnap = reinterpret_cast<int64_t*>(smem + o.csnap);  // [NB][6 candidates][6 fields]
+  int32_t* L_csc = reinterpret_cast<int32_t*>(smem + o.csc);      // [NB][8]
+  const bool spread_on = d.w_spread != 0;
+  const bool aff_on = (d.preds & KSG_PRED_SERVICEAFFINITY) && d.n_aff > 0;
+  const bool res_on = (d.preds & KSG_PRED_PODFITSRESOURCES) != 0;
+  const bool ports_on = (d.preds & KSG_PRED_PODFITSPORTS) != 0;
+  const bool disk_on = (d.preds & KSG_PRED_NODISKCONFLICT) != 0;
+  const uint32_t nbits = (wcap + 31) / 32;
+
+  for (uint32_t t = tid; t < RING; t += NT) r_hdr[t].ready = 0;
+  if (tid == 0) *ctl = WinCtl4{};
+  for (uint32_t w = tid; w < nflag; w += NT) {
+    L_flag[w] = 0;
+    L_peerset[w] = 0;
+  }
+  for (uint32_t w = tid; w < nbits; w += NT) {
+    L_pub[w] = 0;
+    L_drw[w] = 0;
+  }
+  for (uint32_t w = tid; w < KSG_R4_NB * PW; w += NT) L_drop[w] = 0;
+  __syncthreads();
+  const uint64_t rng0 = *rng_io;
+
+  // =========================================================================
+  // producers
+  // =========================================================================
+  if (wave >= KSG_R4_P0) {
+    const uint32_t* recs = reinterpret_cast<const uint32_t*>(sums);
+    uint32_t wb_at[P], wm_at[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      const uint32_t wq = lane * P + q;
+      uint32_t g = 0;
+      for (uint32_t r = 1; r < x.world; ++r)
+        if (wq >= x.wlo[r] && x.nw[r] > 0) g = r;
+      const uint32_t i = wq - x.wlo[g];
+      const bool ok = wq < nwords && i < x.nw[g];
+      const uint32_t base = (uint32_t)(g * x.blk);
+      wb_at[q] = ok ? base + i * 8 : ~0u;
+      wm_at[q] = ok ? base + x.wcap * x.ostride * 8 + i * 4 : ~0u;
+    }
+    const uint32_t row_b = x.ostride * 8, row_m = x.ostride * 4;
+    uint64_t p_last = 0, p_acc = 0;  // KSG_DEBUG & 8: lanes 24..27 ring wait, loads, draw wait, the rest
+    auto pstamp = [&](uint32_t k) {
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        p_acc += lane == k ? t_now - p_last : 0ULL;
+        p_last = t_now;
+      }
+    };
+    if constexpr (STAMP) p_last = __builtin_amdgcn_s_memtime();
+    for (uint32_t j = wave - KSG_R4_P0; j < n_pods; j += NPW) {
+      const uint32_t e = j % RING;
+      // ring entry free: every role is past pod j - RING (the checkers read a pod's
+      // entry again three pods later, the x2-checker two pods later, the
+      // pre-selector reads the next pod's entry)
+      for (uint32_t spin = 0;; ++spin) {
+        const uint32_t st = ld_u(&ctl->stop);
+        uint32_t done = min(min(ld_u(&ctl->psel_seq), ld_u(&ctl->x2_seq)), ld_u(&ctl->sel_seq));
+#pragma unroll
+        for (int c = 0; c < KSG_RES_NCHK; ++c) done = min(done, ld_u(&ctl->chk_seq[c]));
+        if (st) return;
+        if (j < RING || done + RING >= j + 5) break;
+        if (spin > KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      acq_lds();
+      pstamp(24);
+      const uint32_t rec = lane < DW ? recs[(size_t)j * DW + lane] : 0u;
+      uint64_t t0[P];
+      int32_t mw[P];
+      int32_t lm = KSG_S32_NONE;
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        t0[q] = wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + j * row_b) : 0ULL;
+        mw[q] = wm_at[q] != ~0u ? *reinterpret_cast<const int32_t*>(x.buf + wm_at[q] + j * row_m) : KSG_S32_NONE;
+        lm = mw[q] > lm ? mw[q] : lm;
+      }
+      const int32_t m0 = wave_total_max(lm);
+      const bool drawable = __builtin_amdgcn_readlane(rec, WS_ERR) == 0 && m0 != KSG_S32_NONE;
+      const uint32_t wj = j >> 5, bj = 1u << (j & 31);
+      if (lane == 0) {  // the drawable bit first, then "known" (readers read them in that order)
+        if (drawable) atomicOr(&L_drw[wj], bj);
+        atomicOr(&L_pub[wj], bj);
+      }
+      uint32_t cnt = 0;
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        t0[q] = (m0 != KSG_S32_NONE && mw[q] == m0) ? t0[q] : 0ULL;
+        cnt += __popcll(t0[q]);
+      }
+      const uint32_t k0 = wave_total_add(cnt);
+      const uint32_t n_svcs = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NSS) >> 16;
+      const uint32_t nk = ((uint32_t)__builtin_amdgcn_readlane(rec, WS_NPP) & 0xffff) +
+                          ((uint32_t)__builtin_amdgcn_readlane(rec, WS_NPP) >> 16);
+      const uint32_t n_sel = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NSS) & 0xffff;
+      const bool inl = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NINL) <= KSG_WIN_INLINE && n_svcs <= KSG_SLOT_SVCS;
+      const uint32_t t_sv = lane < n_svcs ? lane : 0u;
+      const uint32_t my_sv = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + t_sv, 63u), 64);
+      int32_t s_max = 0, s_peer = 0;
+      if (drawable && inl && lane < n_svcs) {  // the pod's services' scalars (in flight over the draw wait)
+        s_max = d.svc_max[my_sv];
+        s_peer = d.svc_peer[my_sv];
+      }
+      pstamp(25);
+      // draw index = drawable pods before j (every one of them known)
+      uint32_t idx = 0;
+      for (uint32_t spin = 0;; ++spin) {
+        if (ld_acq(&ctl->stop)) return;
+        if (spin > KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          return;
+        }
+        bool all = true;
+        idx = 0;
+        for (uint32_t w = 0; w <= wj; ++w) {
+          const uint32_t mask = w < wj ? ~0u : bj - 1u;
+          const uint32_t pub = __builtin_amdgcn_readfirstlane(ld_acq(&L_pub[w]));
+          all = all && (pub & mask) == mask;
+          idx += __popc(__builtin_amdgcn_readfirstlane(L_drw[w]) & mask);
+        }
+        if (all) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      pstamp(26);
+      uint64_t sm = rng0 + (uint64_t)idx * 0x9E3779B97F4A7C15ULL;
+      const uint64_t r = ksg_splitmix_next(&sm) >> 1;  // rand.Int() (generic_scheduler.go:94)
+      uint32_t mv = 0;
+      if (drawable && lane < k0) mv = umod64_32(r, k0 - lane);
+      r_mod[e * 64 + lane] = mv;
+      if (lane < DW) r_rec[e * DW + lane] = rec;
+#pragma unroll
+      for (int q = 0; q < P; ++q) r_t0[(size_t)e * PW + lane * P + q] = t0[q];
+      if (inl && lane < n_svcs) {
+        r_svc[e].max[lane] = s_max;
+        r_svc[e].peer[lane] = s_peer;
+      }
+      if (lane == 0) {
+        r_hdr[e].m0 = m0;
+        r_hdr[e].k0 = k0;
+        r_hdr[e].r = r;
+        r_hdr[e].drawable = drawable;
+        st_rel(&r_hdr[e].ready, j + 1);
+      }
+      pstamp(27);
+    }
+    if constexpr (STAMP) {
+      if (lane >= 24 && lane < 28) atomicAdd(d.dbgbuf + lane, (int32_t)(p_acc / 64));
+    }
+    return;
+  }
+
+  // =========================================================================
+  // checkers: lane l of checker c owns slot 64c + l
+  // =========================================================================
+  if (wave >= KSG_R4_C0) {
+    __builtin_amdgcn_s_setprio(2);
+    const uint32_t c = wave - KSG_R4_C0;
+    const uint32_t my_slot = c * 64 + lane;
+    const uint32_t* my_cl = L_cl + (size_t)my_slot * KSG_CL_W;
+    RegSlot S;
+    S.node = ~0u;
+    S.cap_c = S.cap_m = S.snp_c = S.snp_m = S.dl_c = S.dl_m = 0;
+    S.inv_c = S.inv_m = 0.0;
+    S.nk = S.ns = S.smask = 0;
+    // AssumePod of pod p (plugin/pkg/scheduler/scheduler.go:115-118) into the
+    // owner lane's slot: requested totals, list lengths, the services' snapshot
+    // counts into the table (the x2-checker applies the service flags)
+    auto apply = [&](uint32_t p) {
+      const uint32_t kind = __builtin_amdgcn_readfirstlane(L_cm[p].kind);
+      const uint32_t slot = __builtin_amdgcn_readfirstlane(L_cm[p].slot);
+      if (kind != 1 || (slot >> 6) != c) return;
+      const uint32_t woff = __builtin_amdgcn_readfirstlane(L_cm[p].node);
+      const uint32_t fl = __builtin_amdgcn_readfirstlane(L_cm[p].flags);
+      const bool fresh = (fl & 1u) != 0;
+      const uint32_t cj = (fl >> 2) & 7u;
+      const uint32_t ol = slot & 63, ep = p % RING, wn = d.lo + woff;
+      const uint32_t prec = lane < DW ? r_rec[ep * DW + lane] : 0u;
+      const PodView ppv = pod_view(prec);
+      const uint32_t nss = __builtin_amdgcn_readlane(prec, WS_NSS);
+      const uint32_t n_sel = nss & 0xffff, n_svcs = nss >> 16, nk = ppv.nk;
+      const uint32_t base_nk = fresh ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)S.nk, (int)ol);
+      const uint32_t base_ns = fresh ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)S.ns, (int)ol);
+      if (fresh) {  // its candidate's snapshot is staged (the pre-selector stages it after the verdict)
+        for (uint32_t spin = 0; ld_u(&ctl->csnap_seq[p % KSG_R4_NB]) != p + 1; ++spin)
+          if (spin > 16 * KSG_SPIN_LIMIT || ld_u(&ctl->hang)) {
+            ctl->hang = 1;
+            break;
+          }
+        acq_lds();
+      }
+      if (fresh && lane == ol) {  // the new slot's snapshot: staged with its candidate
+        const int64_t* cs = L_csnap + ((size_t)(p % KSG_R4_NB) * KSG_R4_NCAND + cj) * 6;
+        S.cap_c = cs[0];
+        S.cap_m = cs[1];
+        S.snp_c = cs[2];
+        S.snp_m = cs[3];
+        S.inv_c = __longlong_as_double((long long)cs[4]);
+        S.inv_m = __longlong_as_double((long long)cs[5]);
+        S.node = woff;
+        S.dl_c = S.dl_m = 0;
+        S.smask = 0;
+      }
+      uint32_t new_mask = 0;
+      if (n_svcs) {  // the pod's services' snapshot counts on the node, into the table
+        const bool sv_lane = lane < n_svcs;
+        const uint32_t my_sv =
+            (uint32_t)__shfl((int)prec, (int)min(WS_IDS + nk + n_sel + (sv_lane ? lane : 0u), 63u), 64);
+        if (sv_lane)
+          L_cl[(size_t)slot * KSG_CL_W + KSG_CL_SC + base_ns + lane] =
+              (uint32_t)gld(d.svc_cnt + (size_t)my_sv * d.n_nodes + wn);
+        new_mask = wave_or_u32(sv_lane ? (1u << (my_sv & 31)) : 0u);
+      }
+      if (lane == ol) {
+        S.dl_c = (int64_t)((uint64_t)S.dl_c + (uint64_t)ppv.req_c);
+        S.dl_m = (int64_t)((uint64_t)S.dl_m + (uint64_t)ppv.req_m);
+        S.nk = base_nk + nk;
+        S.ns = base_ns + n_svcs;
+        S.smask |= new_mask;
+      }
+    };
+
+    uint64_t t_last = 0, t_acc = 0;
+    auto cstamp = [&](uint32_t k) {
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        t_acc += lane == k ? t_now - t_last : 0ULL;
+        t_last = t_now;
+      }
+    };
+    if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
+    for (uint32_t i = 0;; ++i) {
+      const uint32_t e = i % RING, nb = i % KSG_R4_NB;
+      bool stopped = false;
+      // pod i is checked against the slots as of commits <= i-3: it starts once
+      // commit i-3 is published
+      for (uint32_t spin = 0;; ++spin) {
+        const uint32_t ss = ld_u(&ctl->sel_seq), rd = ld_u(&r_hdr[e].ready), st = ld_u(&ctl->stop);
+        if (i < n_pods && ss + 2 >= i && rd == i + 1) break;
+        if (st) {
+          stopped = true;
+          break;
+        }
+        if (spin > 16 * KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          stopped = true;
+          break;
+        }
+      }
+      acq_lds();
+      cstamp(c == 0 ? 16 : 19);
+      if (stopped) {
+        // pods [0, resolved) are decided: apply the commits this checker has not
+        const uint32_t R = __builtin_amdgcn_readfirstlane(ctl->resolved);
+        for (uint32_t q = i >= 3 ? i - 3 : 0; q < R; ++q) apply(q);
+        break;
+      }
+      if (i >= 3) apply(i - 3);
+      cstamp(c == 0 ? 17 : 20);
+      const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
+      const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
+      uint32_t cntd = 0;
+      if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE) {
+        const PodView pv = pod_view(rec);
+        bool drop = false;
+        if (S.node != ~0u) {
+          const uint64_t* t0e = r_t0 + (size_t)e * PW;
+          if ((t0e[S.node >> 6] >> (S.node & 63)) & 1ULL) {
+            // does the slot (a snapshot tie of the pod) score below M0 now?
+            const int64_t now_c = (int64_t)((uint64_t)S.snp_c + (uint64_t)S.dl_c);
+            const int64_t now_m = (int64_t)((uint64_t)S.snp_m + (uint64_t)S.dl_m);
+            if (res_on && !pv.zero_req)  // PodFitsResources (predicates.go:127-145)
+              drop = !((S.cap_c == 0 || S.cap_c - now_c >= pv.req_c) && (S.cap_m == 0 || S.cap_m - now_m >= pv.req_m));
+            if (d.w_lr) {  // LeastRequested (priorities.go:43-76) can only fall as requested grows
+              const int32_t lr_now = lr_win(now_c + pv.req_c, S.cap_c, S.inv_c) + lr_win(now_m + pv.req_m, S.cap_m, S.inv_m);
+              const int32_t lr_snap =
+                  lr_win(S.snp_c + pv.req_c, S.cap_c, S.inv_c) + lr_win(S.snp_m + pv.req_m, S.cap_m, S.inv_m);
+              drop |= (lr_now >> 1) != (lr_snap >> 1);
+            }
+            if (!drop && pv.nk && S.nk) {  // PodFitsPorts / NoDiskConflict vs the window's keys
+              for (uint32_t a = 0; a < S.nk; ++a) {
+                const uint32_t key = my_cl[KSG_CL_KEY + a];
+                for (uint32_t b = 0; b < pv.nk; ++b) {
+                  const bool on = b < pv.n_ports ? ports_on : disk_on;
+                  drop |= on && (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b)) == key;
+                }
+              }
+            }
+            if (!drop && spread_on && pv.s >= 0 && ((S.smask >> (pv.s & 31)) & 1u)) {
+              // ServiceSpreading (spreading.go:72-86) under an unchanged maxCount
+              int32_t delta = 0, snapc = 0;
+              for (uint32_t a = 0; a < S.ns; ++a)
+                if (my_cl[KSG_CL_SV + a] == (uint32_t)pv.s) {
+                  snapc = (int32_t)my_cl[KSG_CL_SC + a];
+                  ++delta;
+                }
+              if (delta)
+                drop = frac10_f32((int64_t)pv.smax - snapc - delta, pv.smax) !=
+                       frac10_f32((int64_t)pv.smax - snapc, pv.smax);
+            }
+            if (drop)
+              atomicOr(reinterpret_cast<unsigned long long*>(L_drop + (size_t)nb * PW + (S.node >> 6)),
+                       1ULL << (S.node & 63));
+          }
+        }
+        cntd = __popcll(__ballot(drop));
+      }
+      if (lane == 0) {
+        ctl->chk_cnt[c][nb] = cntd;
+        st_rel(&ctl->chk_seq[c], i + 1);
+      }
+      cstamp(c == 0 ? 18 : 21);
+    }
+    // write the window's deltas of this checker's slots back to HBM (the next snapshot)
+    if (S.node != ~0u) {
+      const uint32_t n = d.lo + S.node;
+      d.used_cpu[n] = (int64_t)((uint64_t)S.snp_c + (uint64_t)S.dl_c);
+      d.used_mem[n] = (int64_t)((uint64_t)S.snp_m + (uint64_t)S.dl_m);
+      for (uint32_t a = 0; a < S.nk; ++a)
+        __hip_atomic_fetch_or(d.keymap + (size_t)my_cl[KSG_CL_KEY + a] * d.nw + (n >> 6), 1ULL << (n & 63),
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (uint32_t a = 0; a < S.ns; ++a) {
+        const uint32_t sa = my_cl[KSG_CL_SV + a];
+        bool first = true;
+        int32_t count = 0;
+        for (uint32_t b = 0; b < S.ns; ++b) {
+          if (my_cl[KSG_CL_SV + b] == sa) {
+            if (b < a) first = false;
+            ++count;
+          }
+        }
+        __hip_atomic_fetch_add(d.svc_total + sa, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (first) {
+          const int32_t fin = (int32_t)my_cl[KSG_CL_SC + a] + count;
+          d.svc_cnt[(size_t)sa * d.n_nodes + n] = fin;
+          __hip_atomic_fetch_max(d.svc_max + sa, fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    if constexpr (STAMP) {
+      if (lane >= 16 && lane < 22) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
+    }
+    drain_stores();
+    if (lane == 0) st_rel(&ctl->fin[c], 1u);
+    return;
+  }
+
+  // =========================================================================
+  // pre-selector (wave 2)
+  // =========================================================================
+  if (wave == KSG_R4_PS) {
+    __builtin_amdgcn_s_setprio(2);
+    // prefetch lanes: 0..35 candidate j = lane / 6, field f = lane % 6; 36..41 the
+    // next pod's service count on candidate lane - 36
+    const uint32_t fj = lane < 36 ? lane / 6 : 0u, ff = lane % 6;
+    const uint64_t* const fsrc = ff == 0   ? reinterpret_cast<const uint64_t*>(d.cap_cpu)
+                                 : ff == 1 ? reinterpret_cast<const uint64_t*>(d.cap_mem)
+                                 : ff == 2 ? reinterpret_cast<const uint64_t*>(d.used_cpu)
+                                 : ff == 3 ? reinterpret_cast<const uint64_t*>(d.used_mem)
+                                 : ff == 4 ? reinterpret_cast<const uint64_t*>(d.inv10_cpu)
+                                           : reinterpret_cast<const uint64_t*>(d.inv10_mem);
+    // the candidates of pods i-1 and i-2 (lane j < 6 holds candidate j), for L0 membership
+    uint32_t pc1 = KSG_NO_NODE, pc2 = KSG_NO_NODE;
+    uint64_t x_last = 0, x_acc = 0;  // KSG_DEBUG & 8: lanes 28..30 wait, select, prefetch
+    auto xstamp = [&](uint32_t k) {
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        x_acc += lane == k ? t_now - x_last : 0ULL;
+        x_last = t_now;
+      }
+    };
+    if constexpr (STAMP) x_last = __builtin_amdgcn_s_memtime();
+    bool stopped = false;
+    for (uint32_t i = 0; i < n_pods && !stopped; ++i) {
+      const uint32_t e = i % RING, nb = i % KSG_R4_NB;
+      const bool has_next = i + 1 < n_pods;
+      const uint32_t en = (i + 1) % RING;
+      for (uint32_t spin = 0;; ++spin) {  // the checkers are done with pod i; pod i+1 staged
+        uint32_t cs = ld_u(&ctl->chk_seq[0]);
+#pragma unroll
+        for (int c = 1; c < KSG_RES_NCHK; ++c) cs = min(cs, ld_u(&ctl->chk_seq[c]));
+        const uint32_t rn = ld_u(&r_hdr[en].ready), st = ld_u(&ctl->stop);
+        if (cs >= i + 1 && (!has_next || rn == i + 2)) break;
+        if (st) {
+          stopped = true;
+          break;
+        }
+        if (spin > 16 * KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          stopped = true;
+          break;
+        }
+      }
+      acq_lds();
+      if (stopped) break;
+      xstamp(28);
+      const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
+      const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
+      const uint32_t err = __builtin_amdgcn_readlane(rec, WS_ERR);
+      const uint32_t npp = __builtin_amdgcn_readlane(rec, WS_NPP), nss = __builtin_amdgcn_readlane(rec, WS_NSS);
+      const uint32_t nk = (npp & 0xffff) + (npp >> 16), n_svcs = nss >> 16;
+      uint32_t status = KSG_CS_OK, kp = 0, xlive = 0;
+      uint32_t cand = KSG_NO_NODE;  // lane j < 6: candidate j
+      if (err || m0 == KSG_S32_NONE) {
+        status = err ? KSG_CS_ERROR : KSG_CS_NOFIT;
+      } else if (__builtin_amdgcn_readlane(rec, WS_NINL) > KSG_WIN_INLINE || nk > KSG_SLOT_KEYS ||
+                 n_svcs > KSG_SLOT_SVCS) {
+        status = KSG_CS_OVERSIZE;  // lists longer than the record / a slot
+      } else {
+        const uint32_t k0 = __builtin_amdgcn_readfirstlane(r_hdr[e].k0);
+        uint32_t cc = 0;
+#pragma unroll
+        for (int c = 0; c < KSG_RES_NCHK; ++c) cc += __builtin_amdgcn_readfirstlane(ctl->chk_cnt[c][nb]);
+        kp = k0 - cc;
+        const uint64_t* t0e = r_t0 + (size_t)e * PW;
+        uint64_t* dw = L_drop + (size_t)nb * PW;
+        // which of pods i-1's (lanes 0..5) and i-2's (lanes 6..11) candidates are
+        // live ties of this pod: in T0 and not dropped (before the drops are cleared)
+        const uint32_t pc2s = (uint32_t)__shfl((int)pc2, (int)((lane - 6) & 63), 64);
+        const uint32_t pcx = lane < 6 ? pc1 : lane < 12 ? pc2s : KSG_NO_NODE;
+        bool lv = false;
+        if (pcx != KSG_NO_NODE) lv = (((t0e[pcx >> 6] & ~dw[pcx >> 6]) >> (pcx & 63)) & 1ULL) != 0;
+        xlive = (uint32_t)__ballot(lv);
+        uint64_t live[P];
+        uint32_t cl = 0;
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+          const uint64_t dq = dw[lane * P + q];
+          live[q] = t0e[lane * P + q] & ~dq;
+          if (dq) dw[lane * P + q] = 0;  // (cleared for the pod four ahead)
+          cl += __popcll(live[q]);
+        }
+        const uint32_t incl = dpp_scan_add(cl);
+        const uint32_t rmod = r_mod[e * 64 + lane];
+        const uint64_t r = r_hdr[e].r;
+        const uint64_t ru = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(r >> 32)) << 32) |
+                            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r);
+        // e further drops: the (r mod (k'-e))-th live tie from the top and the e after it
+        uint32_t cv[KSG_R4_NCAND];
+#pragma unroll
+        for (int j = 0; j < KSG_R4_NCAND; ++j) cv[j] = KSG_NO_NODE;
+#pragma unroll
+        for (uint32_t ex = 0; ex < 3; ++ex) {
+          if (kp < ex + 1) break;
+          const uint32_t dd = cc + ex;
+          const uint32_t ix = dd < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)rmod, (int)dd) : umod64_32(ru, kp - ex);
+          const uint32_t t = kp - 1 - ex - ix;  // ascending rank in L0 minus the e dropped nodes
+          const uint32_t base = ex == 0 ? 0u : ex == 1 ? 1u : 3u;
+#pragma unroll
+          for (uint32_t m = 0; m <= ex; ++m)
+            if (t + m < kp) cv[base + m] = select_in_lanes<P>(live, cl, incl, t + m, lane);
+        }
+#pragma unroll
+        for (int j = 0; j < KSG_R4_NCAND; ++j) cand = lane == (uint32_t)j ? cv[j] : cand;
+      }
+      xstamp(29);
+      if (lane == 0) {
+        L_cand[nb].status = status;
+        L_cand[nb].kp = kp;
+        L_cand[nb].xlive = xlive;
+      }
+      if (lane < KSG_R4_NCAND) L_cand[nb].c[lane] = cand;
+      if (lane == 0) st_rel(&ctl->psel_seq, i + 1);
+      // the candidates' snapshots and the next pod's primary service count on them
+      // (the committer reads these when it re-checks pod i+1)
+      if (status == KSG_CS_OK) {
+        const uint32_t cfs = (uint32_t)__shfl((int)cand, (int)fj, 64);
+        const uint32_t csv = (uint32_t)__shfl((int)cand, (int)min(lane - 36, 7u), 64);
+        int32_t s_next = -1;
+        if (has_next) s_next = (int32_t)__builtin_amdgcn_readfirstlane(r_rec[en * DW + WS_SVC]);
+        uint64_t fv = 0;
+        int32_t scv = 0;
+        if (lane < 36 && cfs != KSG_NO_NODE) fv = gld(fsrc + d.lo + cfs);
+        if (lane >= 36 && lane < 42 && csv != KSG_NO_NODE && s_next >= 0)
+          scv = gld(d.svc_cnt + (size_t)s_next * d.n_nodes + d.lo + csv);
+        if (lane < 36) L_csnap[(size_t)nb * KSG_R4_NCAND * 6 + lane] = (int64_t)fv;
+        if (lane >= 36 && lane < 42) L_csc[nb * 8 + (lane - 36)] = scv;
+      }
+      if (lane == 0) st_rel(&ctl->csnap_seq[nb], i + 1);
+      pc2 = pc1;
+      pc1 = status == KSG_CS_OK ? cand : KSG_NO_NODE;
+      xstamp(30);
+    }
+    if constexpr (STAMP) {
+      if (lane >= 28 && lane < 31) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
+    }
+    return;
+  }
+
+  // =========================================================================
+  // x2-checker (wave 1): follows the commits in order
+  // =========================================================================
+  if (wave == KSG_R4_X2) {
+    __builtin_amdgcn_s_setprio(2);
+    const uint32_t rl = lane & 1;
+    // the committer's slot bookkeeping, replayed: node, list lengths, delta per slot
+    uint32_t xcn0 = ~0u, xcn1 = ~0u, xsk0 = 0, xsk1 = 0, xss0 = 0, xss1 = 0, xn_slots = 0;
+    int64_t xdc0 = 0, xdm0 = 0, xdc1 = 0, xdm1 = 0;
+    // commit q into its slot: returns the slot, its list lengths before q and its delta after q
+    auto replay = [&](uint32_t q, uint32_t& slot, uint32_t& bnk, uint32_t& bns, uint64_t& dlc, uint64_t& dlm,
+                      uint32_t& prec) {
+      const uint32_t node = __builtin_amdgcn_readfirstlane(L_cm[q].node);
+      const uint32_t eq = q % RING;
+      prec = lane < DW ? r_rec[eq * DW + lane] : 0u;
+      const PodView ppv = pod_view(prec);
+      const uint32_t p_svcs = (uint32_t)__builtin_amdgcn_readlane(prec, WS_NSS) >> 16;
+      const uint64_t hit0 = __ballot(xcn0 == node), hit1 = __ballot(xcn1 == node);
+      const bool in_c = (hit0 | hit1) != 0;
+      bnk = bns = 0;
+      dlc = dlm = 0;
+      if (in_c) {
+        slot = hit0 ? (uint32_t)__builtin_ctzll(hit0) : 64u + (uint32_t)__builtin_ctzll(hit1);
+        const uint32_t sl = slot & 63;
+        bnk = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? xsk0 : xsk1), (int)sl);
+        bns = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? xss0 : xss1), (int)sl);
+        dlc = readlane64((uint64_t)(slot < 64 ? xdc0 : xdc1), (int)sl);
+        dlm = readlane64((uint64_t)(slot < 64 ? xdm0 : xdm1), (int)sl);
+      } else {
+        slot = xn_slots < KSG_MAX_SLOTS ? xn_slots++ : 0u;
+      }
+      dlc += (uint64_t)ppv.req_c;
+      dlm += (uint64_t)ppv.req_m;
+      if (lane == (slot & 63)) {
+        if (slot >= 64) {
+          if (!in_c) xcn1 = node;
+          xsk1 = bnk + ppv.nk;
+          xss1 = bns + p_svcs;
+          xdc1 = (int64_t)dlc;
+          xdm1 = (int64_t)dlm;
+        } else {
+          if (!in_c) xcn0 = node;
+          xsk0 = bnk + ppv.nk;
+          xss0 = bns + p_svcs;
+          xdc0 = (int64_t)dlc;
+          xdm0 = (int64_t)dlm;
+        }
+      }
+    };
+    // the service flags later pods stop on (maxCount rises, first peer) and the
+    // first peers, of commit q (its slot's entries through q are `ent` lanes)
+    auto flags = [&](uint32_t q, uint32_t slot, uint32_t bns, uint32_t prec) {
+      const uint32_t nss = __builtin_amdgcn_readlane(prec, WS_NSS), npp = __builtin_amdgcn_readlane(prec, WS_NPP);
+      const uint32_t n_svcs = nss >> 16, n_sel = nss & 0xffff, nk = (npp & 0xffff) + (npp >> 16);
+      if (!n_svcs) return;
+      const uint32_t wn = d.lo + __builtin_amdgcn_readfirstlane(L_cm[q].node);
+      const uint32_t eq = q % RING;
+      const bool sv_lane = lane < n_svcs;
+      const uint32_t my_sv =
+          (uint32_t)__shfl((int)prec, (int)min(WS_IDS + nk + n_sel + (sv_lane ? lane : 0u), 63u), 64);
+      int32_t mx = 0, peer = 0, cnt = 0;
+      if (sv_lane) {
+        cnt = gld(d.svc_cnt + (size_t)my_sv * d.n_nodes + wn);
+        mx = r_svc[eq].max[lane];
+        peer = r_svc[eq].peer[lane];
+      }
+      const uint32_t ent = lane - KSG_CL_SV < bns ? L_cl[(size_t)slot * KSG_CL_W + lane] : ~0u;
+      uint32_t before = 0;  // earlier window commits of each service on this node
+      for (uint32_t t = 0; t < n_svcs; ++t) {
+        const uint32_t sv_t = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)t);
+        const uint32_t b_t = (uint32_t)__popcll(__ballot(ent == sv_t));
+        if (lane == t) before = b_t;
+      }
+      bool changed = sv_lane && aff_on && peer == -1 && !((L_peerset[my_sv >> 5] >> (my_sv & 31)) & 1u);
+      uint64_t pm = __ballot(sv_lane && peer == -1);
+      if (pm) {  // first commit of a service with no peer yet: its first peer, in commit order
+        uint32_t n_peer = __builtin_amdgcn_readfirstlane(ctl->n_peer);
+        while (pm) {
+          const uint32_t b = __builtin_ctzll(pm);
+          pm &= pm - 1;
+          const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)b);
+          if (!((L_peerset[fsv >> 5] >> (fsv & 31)) & 1u)) {
+            if (lane == 0) {
+              L_peerset[fsv >> 5] |= 1u << (fsv & 31);
+              L_peer[2 * n_peer] = fsv;
+              L_peer[2 * n_peer + 1] = wn;
+            }
+            ++n_peer;
+            lds_fence();
+          }
+        }
+        if (lane == 0) ctl->n_peer = n_peer;
+      }
+      if (sv_lane && spread_on && cnt + (int32_t)before + 1 > mx) changed = true;  // maxCount rises
+      if (changed) atomicOr(&L_flag[my_sv >> 5], 1u << (my_sv & 31));
+    };
+    uint64_t x_last = 0, x_acc = 0;  // KSG_DEBUG & 8: lanes 22, 23 wait, work
+    if constexpr (STAMP) x_last = __builtin_amdgcn_s_memtime();
+    uint32_t i = 0;
+    bool stopped = false;
+    for (; i < n_pods; ++i) {
+      const uint32_t e = i % RING, nb = i % KSG_R4_NB;
+      for (uint32_t spin = 0;; ++spin) {  // commit i-2 published, pod i staged
+        const uint32_t ss = ld_u(&ctl->sel_seq), rd = ld_u(&r_hdr[e].ready), st = ld_u(&ctl->stop);
+        if (ss + 1 >= i && rd == i + 1) break;
+        if (st) {
+          stopped = true;
+          break;
+        }
+        if (spin > 16 * KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          stopped = true;
+          break;
+        }
+      }
+      acq_lds();
+      if (stopped) break;
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        x_acc += lane == 22 ? t_now - x_last : 0ULL;
+        x_last = t_now;
+      }
+      uint32_t res = 0;
+      const uint32_t kind = i >= 2 ? __builtin_amdgcn_readfirstlane(L_cm[i - 2].kind) : 0u;
+      if (kind == 1) {
+        uint32_t slot, bnk, bns, prec;
+        uint64_t dlc, dlm;
+        replay(i - 2, slot, bnk, bns, dlc, dlm, prec);
+        flags(i - 2, slot, bns, prec);
+        const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
+        const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
+        if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE) {
+          // pod i against commit i-2's node as of that commit
+          const uint32_t node = __builtin_amdgcn_readfirstlane(L_cm[i - 2].node);
+          const uint32_t cj = (__builtin_amdgcn_readfirstlane(L_cm[i - 2].flags) >> 2) & 7u;
+          for (uint32_t spin = 0; ld_u(&ctl->csnap_seq[(i - 2) % KSG_R4_NB]) != i - 1; ++spin)
+            if (spin > 16 * KSG_SPIN_LIMIT || ld_u(&ctl->hang)) {
+              ctl->hang = 1;
+              break;
+            }
+          acq_lds();
+          const PodView pv = pod_view(rec);
+          const int32_t x_snapc =
+              pv.s >= 0 ? __builtin_amdgcn_readfirstlane(gld(d.svc_cnt + (size_t)pv.s * d.n_nodes + d.lo + node)) : 0;
+          const int64_t* cs = L_csnap + ((size_t)((i - 2) % KSG_R4_NB) * KSG_R4_NCAND + cj) * 6;
+          XState xs;
+          xs.cap = cs[rl];
+          xs.snp = cs[2 + rl];
+          xs.inv = __longlong_as_double((long long)cs[4 + rl]);
+          xs.dl = (int64_t)(rl ? dlm : dlc);
+          const uint32_t pnpp = __builtin_amdgcn_readlane(prec, WS_NPP), pnss = __builtin_amdgcn_readlane(prec, WS_NSS);
+          const uint32_t pnk = (pnpp & 0xffff) + (pnpp >> 16), pnsel = pnss & 0xffff, pns = pnss >> 16;
+          xs.nk = bnk + pnk;
+          xs.ns = bns + pns;
+          // lane t < 8: key t; lane 8 + u (u < 12): service entry u (the table row, then pod i-2's record)
+          const uint32_t kt = lane - KSG_CL_KEY, ut = lane - KSG_CL_SV;
+          const bool from_row = (kt < KSG_SLOT_KEYS && kt < bnk) || (ut < KSG_SLOT_SVCS && ut < bns);
+          const uint32_t src = kt < KSG_SLOT_KEYS ? WS_IDS + (kt - bnk) : WS_IDS + pnk + pnsel + (ut - bns);
+          const uint32_t from_rec = (uint32_t)__shfl((int)prec, (int)min(src, 63u), 64);
+          const uint32_t rowv = from_row ? L_cl[(size_t)slot * KSG_CL_W + lane] : 0u;
+          const uint32_t xcl = from_row ? rowv : from_rec;
+          res = recheck_x(d, pv, rec, xs, xcl, 0u, x_snapc, res_on, ports_on, disk_on, spread_on, aff_on, 0, true,
+                          lane) & 1u;
+        }
+      }
+      if (lane == 0) {
+        ctl->x2_res[nb] = res;
+        st_rel(&ctl->x2_seq, i + 1);
+      }
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        x_acc += lane == 23 ? t_now - x_last : 0ULL;
+        x_last = t_now;
+      }
+    }
+    // the committer is done: the flags / first peers of the commits not applied yet
+    for (uint32_t spin = 0; !ld_u(&ctl->stop); ++spin) {
+      if (spin > 16 * KSG_SPIN_LIMIT) {
+        ctl->hang = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    acq_lds();
+    const uint32_t R = __builtin_amdgcn_readfirstlane(ctl->resolved);
+    for (uint32_t q = i >= 2 ? i - 2 : 0; q < R; ++q) {
+      if (__builtin_amdgcn_readfirstlane(L_cm[q].kind) != 1) continue;
+      uint32_t slot, bnk, bns, prec;
+      uint64_t dlc, dlm;
+      replay(q, slot, bnk, bns, dlc, dlm, prec);
+      flags(q, slot, bns, prec);
+    }
+    if constexpr (STAMP) {
+      if (lane >= 22 && lane < 24) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
+    }
+    drain_stores();
+    if (lane == 0) st_rel(&ctl->fin_x, 1u);
+    return;
+  }
+  if (wave != 0) return;
+
+  // =========================================================================
+  // committer (wave 0)
+  // =========================================================================
+  __builtin_amdgcn_s_setprio(3);
+  uint32_t resolved = n_pods, reason = 0, n_slots = 0, n_draws = 0;
+  uint32_t cn0 = ~0u, cn1 = ~0u;  // nodes of slots lane and 64 + lane
+  uint32_t sk0 = 0, sk1 = 0;      // their key counts
+  uint32_t ss0 = 0, ss1 = 0;      // their service entry counts
+  int64_t dc0 = 0, dm0 = 0, dc1 = 0, dm1 = 0;  // their window deltas
+  const uint32_t rl = lane & 1;
+  // commit i-1 (x1) and commit i-2 (x2): valid, node, the candidate index it was drawn as
+  bool h1 = false, h2 = false;
+  uint32_t x1 = 0, x2 = 0, x1cj = 0, x2cj = 0, x1slot = 0, x1bns = 0;
+  XState xs1;
+  xs1.cap = xs1.snp = xs1.dl = 0;
+  xs1.inv = 0.0;
+  xs1.nk = xs1.ns = 0;
+  int32_t x1_snapc = 0;  // pod i's service count on x1 at the snapshot (staged with x1's candidate)
+  uint64_t t_last = 0, t_acc = 0;
+#define KSG_STAMP4(k)                                        \
+  if constexpr (STAMP) {                                     \
+    const uint64_t t_now = __builtin_amdgcn_s_memtime();     \
+    t_acc += lane == (uint32_t)(k) ? t_now - t_last : 0ULL;  \
+    t_last = t_now;                                          \
+  }
+#define KSG_COUNT4(k, v)                                   \
+  if constexpr (STAMP) {                                   \
+    t_acc += lane == (uint32_t)(k) ? (uint64_t)(v) : 0ULL; \
+  }
+  if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
+  for (uint32_t i = 0; i < n_pods; ++i) {
+    const uint32_t e = i % RING, nb = i % KSG_R4_NB;
+    bool hung = false;
+    for (uint32_t spin = 0;; ++spin) {  // pod i staged (the re-check needs only the pod)
+      const uint32_t rd = ld_u(&r_hdr[e].ready), hg = ld_u(&ctl->hang);
+      if (rd == i + 1) break;
+      if (spin > 16 * KSG_SPIN_LIMIT || hg) {
+        hung = true;
+        break;
+      }
+    }
+    acq_lds();
+    if (hung) {
+      resolved = i;
+      reason = KSG_STOP_HANG;
+      break;
+    }
+    KSG_STAMP4(0)
+    const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
+    const PodView pv = pod_view(rec);
+    const int32_t s = pv.s;
+    const uint32_t nss = __builtin_amdgcn_readlane(rec, WS_NSS);
+    const uint32_t n_sel = nss & 0xffff, n_svcs = nss >> 16, nk = pv.nk;
+    // ---- pod i against commit i-1's node, as of that commit
+    uint32_t r1 = 0;
+    if (h1) {
+      const uint32_t xcl = lane < xs1.nk ? L_cl[(size_t)x1slot * KSG_CL_W + lane]
+                           : (lane >= KSG_CL_SV && lane - KSG_CL_SV < xs1.ns) ? L_cl[(size_t)x1slot * KSG_CL_W + lane]
+                                                                             : ~0u;
+      const int32_t peer0 = (int32_t)__builtin_amdgcn_readfirstlane(r_svc[e].peer[0]);
+      const bool pset = s >= 0 && ((__builtin_amdgcn_readfirstlane(L_peerset[s >> 5]) >> (s & 31)) & 1u) != 0;
+      r1 = recheck_x(d, pv, rec, xs1, xcl, x1bns, x1_snapc, res_on, ports_on, disk_on, spread_on, aff_on, peer0,
+                     pset, lane);
+    }
+    KSG_STAMP4(1)
+    // ---- the pre-selector's candidates, the x2-checker's verdict, the flags of commits <= i-2
+    for (uint32_t spin = 0;; ++spin) {
+      const uint32_t ps = ld_u(&ctl->psel_seq), xq = ld_u(&ctl->x2_seq), hg = ld_u(&ctl->hang);
+      if (ps >= i + 1 && xq >= i + 1) break;
+      if (spin > 16 * KSG_SPIN_LIMIT || hg) {
+        hung = true;
+        break;
+      }
+    }
+    acq_lds();
+    if (hung) {
+      resolved = i;
+      reason = KSG_STOP_HANG;
+      break;
+    }
+    KSG_STAMP4(2)
+    const uint32_t status = __builtin_amdgcn_readfirstlane(L_cand[nb].status);
+    if (status == KSG_CS_NOFIT || status == KSG_CS_ERROR) {
+      // ServiceAffinity peer error / nothing fit at the snapshot: no draw, no commit
+      if (lane == 0) {
+        L_cm[i].kind = 0;
+        L_out[i] = status == KSG_CS_ERROR ? KSG_OUT_ERROR : KSG_OUT_NOFIT;
+        st_rel(&ctl->sel_seq, i + 1);
+      }
+      h2 = h1;
+      x2 = x1;
+      x2cj = x1cj;
+      h1 = false;
+      continue;
+    }
+    if (status == KSG_CS_OVERSIZE) {
+      resolved = i;  // the exact per-pod kernel takes it
+      reason = i == 0 ? KSG_STOP_OVERSIZE : KSG_STOP_SLOT;
+      break;
+    }
+    const uint32_t kp = __builtin_amdgcn_readfirstlane(L_cand[nb].kp);
+    const uint32_t xlv = __builtin_amdgcn_readfirstlane(L_cand[nb].xlive);
+    const uint32_t cl6 = lane < KSG_R4_NCAND ? L_cand[nb].c[lane] : KSG_NO_NODE;
+    const uint32_t xr2 = __builtin_amdgcn_readfirstlane(ctl->x2_res[nb]);
+    const uint32_t fw = s >= 0 ? __builtin_amdgcn_readfirstlane(L_flag[s >> 5]) : 0u;
+    if (s >= 0 && (spread_on || aff_on) && ((r1 & 2u) || ((fw >> (s & 31)) & 1u))) {
+      resolved = i;  // a service scalar this pod reads changed in the window
+      reason = KSG_STOP_SERVICE;
+      break;
+    }
+    // ---- the two late drops: x1 (commit i-1), x2 (commit i-2, unless it is x1's node)
+    const bool d1 = h1 && (r1 & 1u) && ((xlv >> x1cj) & 1u);
+    const bool d2 = h2 && (xr2 & 1u) && ((xlv >> (6 + x2cj)) & 1u) && !(h1 && x1 == x2);
+    const uint32_t ex = (d1 ? 1u : 0u) + (d2 ? 1u : 0u);
+    if (kp <= ex) {
+      resolved = i;  // every snapshot tie got worse: needs a fresh snapshot
+      reason = KSG_STOP_EXHAUSTED;
+      break;
+    }
+    // the answer: among the ex+1 staged nodes, the first whose rank in L0 minus
+    // the dropped nodes is the draw's
+    uint32_t cj;
+    if (ex == 0) {
+      cj = 0;
+    } else if (ex == 1) {
+      const uint32_t xd = d1 ? x1 : x2;
+      const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)cl6, 1);
+      cj = xd > b0 ? 1u : 2u;
+    } else {
+      cj = 5;
+#pragma unroll
+      for (uint32_t m = 0; m < 3; ++m) {
+        const uint32_t cm = (uint32_t)__builtin_amdgcn_readlane((int)cl6, (int)(3 + m));
+        const uint32_t below = (x1 < cm ? 1u : 0u) + (x2 < cm ? 1u : 0u);
+        if (cj == 5 && cm != x1 && cm != x2 && below == m) cj = 3 + m;
+      }
+    }
+    const uint32_t woff = (uint32_t)__builtin_amdgcn_readlane((int)cl6, (int)cj);
+    if (ex) KSG_COUNT4(7, 64)
+    if (cj) KSG_COUNT4(8, 64)
+    KSG_STAMP4(3)
+    // ---- AssumePod's slot
+    const uint64_t hit0 = __ballot(cn0 == woff);
+    const uint64_t hit1 = __ballot(cn1 == woff);
+    const bool in_c = (hit0 | hit1) != 0;
+    uint32_t slot, base_nk = 0, base_ns = 0;
+    int64_t base_dc = 0, base_dm = 0;
+    if (in_c) {
+      slot = hit0 ? (uint32_t)__builtin_ctzll(hit0) : 64u + (uint32_t)__builtin_ctzll(hit1);
+      const uint32_t sl = slot & 63;
+      base_nk = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? sk0 : sk1), (int)sl);
+      base_ns = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? ss0 : ss1), (int)sl);
+      if (base_nk + nk > KSG_SLOT_KEYS || base_ns + n_svcs > KSG_SLOT_SVCS) {
+        resolved = i;  // this pod is redone (with the same draw) in the next window
+        reason = KSG_STOP_SLOT;
+        break;
+      }
+      base_dc = (int64_t)readlane64((uint64_t)(slot < 64 ? dc0 : dc1), (int)sl);
+      base_dm = (int64_t)readlane64((uint64_t)(slot < 64 ? dm0 : dm1), (int)sl);
+    } else {
+      if (n_slots == KSG_MAX_SLOTS) {
+        resolved = i;
+        reason = KSG_STOP_SLOT;
+        break;
+      }
+      slot = n_slots++;
+    }
+    const int64_t new_dc = (int64_t)((uint64_t)base_dc + (uint64_t)pv.req_c);
+    const int64_t new_dm = (int64_t)((uint64_t)base_dm + (uint64_t)pv.req_m);
+    {  // the slot's table row: the pod's keys and service ids (record lane L holds dword L)
+      uint32_t* row = L_cl + (size_t)slot * KSG_CL_W;
+      const uint32_t kt = lane - WS_IDS, st = lane - (WS_IDS + nk + n_sel);
+      if (kt < nk) row[KSG_CL_KEY + base_nk + kt] = rec;
+      if (st < n_svcs) row[KSG_CL_SV + base_ns + st] = rec;
+    }
+    if (lane == 0) {
+      L_cm[i] = WinCommit4{1u, slot, woff, (in_c ? 0u : 1u) | (cj << 2) | (n_svcs << 8)};
+      L_out[i] = (int32_t)(d.lo + woff);
+      st_rel(&ctl->sel_seq, i + 1);  // the checkers and the x2-checker move on
+    }
+    if (lane == (slot & 63)) {  // this wave's counts and deltas of the slot
+      if (slot >= 64) {
+        if (!in_c) cn1 = woff;
+        dc1 = new_dc;
+        dm1 = new_dm;
+        sk1 = base_nk + nk;
+        ss1 = base_ns + n_svcs;
+      } else {
+        if (!in_c) cn0 = woff;
+        dc0 = new_dc;
+        dm0 = new_dm;
+        sk0 = base_nk + nk;
+        ss0 = base_ns + n_svcs;
+      }
+    }
+    KSG_STAMP4(4)
+    // ---- x1 for pod i+1: this commit's node, its snapshot staged with its candidate
+    for (uint32_t spin = 0;; ++spin) {
+      const uint32_t cs = ld_u(&ctl->csnap_seq[nb]), hg = ld_u(&ctl->hang);
+      if (cs == i + 1) break;
+      if (spin > 16 * KSG_SPIN_LIMIT || hg) {
+        hung = true;
+        break;
+      }
+    }
+    acq_lds();
+    if (hung) {
+      resolved = i + 1;  // (pod i is committed)
+      reason = KSG_STOP_HANG;
+      ++n_draws;
+      break;
+    }
+    {
+      const int64_t* cs = L_csnap + ((size_t)nb * KSG_R4_NCAND + cj) * 6;
+      xs1.cap = cs[rl];
+      xs1.snp = cs[2 + rl];
+      xs1.inv = __longlong_as_double((long long)cs[4 + rl]);
+      x1_snapc = __builtin_amdgcn_readfirstlane(L_csc[nb * 8 + cj]);
+    }
+    h2 = h1;
+    x2 = x1;
+    x2cj = x1cj;
+    h1 = true;
+    x1 = woff;
+    x1cj = cj;
+    x1slot = slot;
+    x1bns = base_ns;
+    xs1.dl = rl ? new_dm : new_dc;
+    xs1.nk = base_nk + nk;
+    xs1.ns = base_ns + n_svcs;
+    ++n_draws;
+    KSG_STAMP4(5)
+  }
+  if (lane == 0) {
+    ctl->resolved = resolved;
+    st_rel(&ctl->stop, 1u);
+  }
+  // the checkers apply the last commits and write their slots back; the
+  // x2-checker records the last first peers
+  bool drained = false;
+  for (uint32_t spin = 0; spin <= 16 * KSG_SPIN_LIMIT; ++spin) {
+    bool done = ld_acq(&ctl->fin_x) != 0;
+#pragma unroll
+    for (int c = 0; c < KSG_RES_NCHK; ++c) done = done && ld_acq(&ctl->fin[c]) != 0;
+    if (done) {
+      drained = true;
+      break;
+    }
+  }
+  if (!drained || ld_acq(&ctl->hang)) reason = KSG_STOP_HANG;
+  if constexpr (STAMP) {
+    if (lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
+  }
+#undef KSG_STAMP4
+#undef KSG_COUNT4
+  const uint32_t n_peer = __builtin_amdgcn_readfirstlane(ctl->n_peer);
+  for (uint32_t t = lane; t < n_peer; t += 64) {
+    const uint32_t sv = L_peer[2 * t];
+    int32_t expect = -1;
+    __hip_atomic_compare_exchange_strong(d.svc_peer + sv, &expect, (int32_t)L_peer[2 * t + 1], __ATOMIC_RELAXED,
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (uint32_t t = lane; t < resolved; t += 64) out[t] = L_out[t];
+  if (lane == 0) {
+    *rng_io = rng0 + (uint64_t)n_draws * 0x9E3779B97F4A7C15ULL;
+    if (reason == KSG_STOP_HANG) {
+      run->halt = KSG_HALT_HANG;
+    } else if (reason == KSG_STOP_OVERSIZE) {
+      run->halt = KSG_HALT_OVERSIZE;  // pod pos: the host runs the exact per-pod path, then resumes
+    } else if (resolved == 0 || resolved > n_pods) {
+      run->halt = KSG_HALT_BADCOUNT;
+    } else {
+      run->pos = pos + resolved;
+      run->windows += 1;
+      if (reason >= 1 && reason <= 3) run->stops[reason] += 1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
 static uint32_t win_P(const KsgDev& d) {
@@ -3528,9 +4732,10 @@ uint32_t ksg_win_max_window(const KsgDev& d) {
   uint32_t lo = 0, hi = 4096;
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1) / 2;
-    const uint32_t need = anti             ? win_lds_offsets(P, nflag, mid, d.n_anti > 0).total
-                          : (d.dbg & 512) ? win3_lds_offsets(P, nflag, mid).total
-                                          : win2_lds_offsets(P, nflag, mid).total;
+    const uint32_t need = anti              ? win_lds_offsets(P, nflag, mid, d.n_anti > 0).total
+                          : (d.dbg & 512)  ? win3_lds_offsets(P, nflag, mid).total
+                          : (d.dbg & 1024) ? win4_lds_offsets(P, nflag, mid).total
+                                           : win2_lds_offsets(P, nflag, mid).total;
     if (need <= kWinLdsBudget) lo = mid;
     else hi = mid - 1;
   }
@@ -3570,6 +4775,22 @@ static hipError_t win_resolve3_launch(const KsgDev& d, uint32_t wcap, size_t lds
 }
 
 template <int PP, bool ST>
+static hipError_t win_resolve4_launch(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run,
+                                      const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
+                                      hipStream_t st) {
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_resolve4_kernel<PP, ST>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipGetLastError();
+    once = true;
+  }
+  hipLaunchKernelGGL((ksg_win_resolve4_kernel<PP, ST>), dim3(1), dim3(win4_nt(PP)), lds, st, d, wcap, run, sums, x, rng,
+                     out);
+  return hipGetLastError();
+}
+
+template <int PP, bool ST>
 static hipError_t win_resolve2_launch(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run,
                                       const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
                                       hipStream_t st) {
@@ -3587,6 +4808,22 @@ static hipError_t win_resolve2_launch(const KsgDev& d, uint32_t wcap, size_t lds
 hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
                                   const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
   const uint32_t P = win_P(d);
+  if (x.fit_off == 0 && (d.dbg & 1024) && !(d.dbg & (128 | 512))) {  // KSG_DEBUG & 1024: the lag-3 resolver
+    const size_t lds4 = win4_lds_offsets(P, (d.n_services + 31) / 32, wcap).total;
+    const bool stamp4 = (d.dbg & 8) != 0;
+#define KSG_RES4_CASE(PP)                                                                         \
+  if (P == PP)                                                                                    \
+    return stamp4 ? win_resolve4_launch<PP, true>(d, wcap, lds4, run, sums, x, rng, out, st)      \
+                  : win_resolve4_launch<PP, false>(d, wcap, lds4, run, sums, x, rng, out, st);
+    KSG_RES4_CASE(1)
+    KSG_RES4_CASE(2)
+    KSG_RES4_CASE(4)
+    KSG_RES4_CASE(8)
+    KSG_RES4_CASE(16)
+    KSG_RES4_CASE(32)
+#undef KSG_RES4_CASE
+    return hipErrorInvalidValue;
+  }
   if (x.fit_off == 0 && (d.dbg & 512) && !(d.dbg & 128)) {
     // KSG_DEBUG & 512: the pre-selecting resolver (measured slower than the
     // register-slot resolver on config 2: DESIGN.md section 4), for comparison

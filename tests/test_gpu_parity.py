@@ -48,7 +48,7 @@ def test_batch_matches_oracle(name, nn, npods, window):
     dev.close()
 
 
-@pytest.mark.parametrize("resolver", [128, 512])
+@pytest.mark.parametrize("resolver", [128, 512, 1024])
 @pytest.mark.parametrize("name,nn,npods", [
     ("config1", 500, 1000),
     ("config2", 2000, 3000),
@@ -56,9 +56,9 @@ def test_batch_matches_oracle(name, nn, npods, window):
     ("config2", 9000, 800),
 ])
 def test_alternative_resolvers_match_oracle(name, nn, npods, resolver, monkeypatch):
-    """The window path's two alternative in-order resolvers (KSG_DEBUG & 128: the
-    LDS-slot resolver, & 512: the pre-selecting resolver), kept for comparison,
-    give the oracle's placements too."""
+    """The window path's alternative in-order resolvers (KSG_DEBUG & 128: the
+    LDS-slot resolver, & 512: the pre-selecting resolver, & 1024: the lag-3
+    resolver) give the oracle's placements too."""
     monkeypatch.setenv("KSG_DEBUG", str(resolver))
     case = Case(name, nn, npods)
     dev, orc = _pair(case, 1024)
