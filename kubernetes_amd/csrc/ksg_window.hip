@@ -339,6 +339,7 @@ __host__ __device__ constexpr uint32_t win_ring(uint32_t P) { return P <= 8 ? 16
 #define KSG_SLOT_SVCS 12
 #define KSG_MAX_SLOTS (64 * KSG_RES_NCHK)
 #define KSG_NO_SLOT 0xffffu
+#define KSG_NO_NODE 0xffffffffu
 
 struct alignas(16) I64x2 {
   int64_t c, m;
@@ -2005,10 +2006,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     int64_t xdc0 = 0, xdm0 = 0, xdc1 = 0, xdm1 = 0;
     // commit q (node) into its slot, the committer's bookkeeping replayed: the
     // slot, its list lengths before q, its delta after q, pod q's record
-    auto replay = [&](uint32_t q, uint32_t node, uint32_t& slot, uint32_t& bnk, uint32_t& bns, uint64_t& dlc,
-                      uint64_t& dlm, uint32_t& prec) {
-      const uint32_t eq = q % RING;
-      prec = lane < DW ? r_rec[eq * DW + lane] : 0u;
+    auto replay = [&](uint32_t node, uint32_t prec, uint32_t& slot, uint32_t& bnk, uint32_t& bns, uint64_t& dlc,
+                      uint64_t& dlm) {
       const PodView ppv = pod_view(prec);
       const uint32_t p_svcs = (uint32_t)__builtin_amdgcn_readlane(prec, WS_NSS) >> 16;
       const uint64_t hit0 = __ballot(xcn0 == node), hit1 = __ballot(xcn1 == node);
@@ -2097,9 +2096,30 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     for (; i < n_pods; ++i) {
       const uint32_t e = i % RING, par = i & 1;
       bool stopped = false;
-      for (uint32_t spin = 0;; ++spin) {  // pod i-1's node drawn and pod i staged, or the end
-        const uint32_t xn = ld_rlx(&ctl->xn_seq), rd = ld_rlx(&r_hdr[e].ready), st = ld_rlx(&ctl->stop);
-        if (xn >= i && rd == i + 1) break;
+      for (uint32_t spin = 0;; ++spin) {  // pod i staged (long before pod i-1's node is drawn), or the end
+        const uint32_t rd = ld_u(&r_hdr[e].ready), st = ld_u(&ctl->stop);
+        if (rd == i + 1) break;
+        if (st) {
+          stopped = true;
+          break;
+        }
+        if (spin > 16 * KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          stopped = true;
+          break;
+        }
+      }
+      acq_lds();
+      if (stopped) break;
+      // pods i's and i-1's records ahead of the node
+      const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
+      const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
+      const uint32_t prec = (i && lane < DW) ? r_rec[((i - 1) % RING) * DW + lane] : 0u;
+      const PodView pv = pod_view(rec);
+      const int32_t s = pv.s;
+      for (uint32_t spin = 0;; ++spin) {  // pod i-1's node drawn, or the end
+        const uint32_t xn = ld_u(&ctl->xn_seq), st = ld_u(&ctl->stop);
+        if (xn >= i) break;
         if (st) {
           stopped = true;
           break;
@@ -2120,12 +2140,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       }
       uint32_t res = 0;
       const uint32_t xnode = i ? __builtin_amdgcn_readfirstlane(ctl->xn_node) : ~0u;
-      const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
-      const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
       // the node's snapshot first (in flight over the bookkeeping below)
       const bool do_check = xnode != ~0u && !__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE;
-      const PodView pv = pod_view(rec);
-      const int32_t s = pv.s;
       const uint32_t xw = d.lo + (do_check ? xnode : 0u);
       int64_t capv = 0, usev = 0;
       double invv = 0.0;
@@ -2139,8 +2155,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       // commit i-1 into its slot (the committer's bookkeeping, replayed)
       uint32_t xslot = 0, bnk = 0, bns = 0;
       uint64_t dlc = 0, dlm = 0;
-      uint32_t prec = 0;
-      if (xnode != ~0u) replay(i - 1, xnode, xslot, bnk, bns, dlc, dlm, prec);
+      if (xnode != ~0u) replay(xnode, prec, xslot, bnk, bns, dlc, dlm);
       if (do_check) {
         // pod i-1's record: its keys and service ids follow the earlier commits' in the slot's lists
         const uint32_t pnpp = __builtin_amdgcn_readlane(prec, WS_NPP), pnss = __builtin_amdgcn_readlane(prec, WS_NSS);
@@ -2224,9 +2239,10 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     for (uint32_t q = i >= 1 ? i - 1 : 0; q < R; ++q) {
       if (__builtin_amdgcn_readfirstlane(L_cm[q].kind) != 1) continue;
       const uint32_t node = __builtin_amdgcn_readfirstlane(L_cm[q].node);
-      uint32_t slot, bnk, bns, prec;
+      const uint32_t prec = lane < DW ? r_rec[(q % RING) * DW + lane] : 0u;
+      uint32_t slot, bnk, bns;
       uint64_t dlc, dlm;
-      replay(q, node, slot, bnk, bns, dlc, dlm, prec);
+      replay(node, prec, slot, bnk, bns, dlc, dlm);
       flags(q, node, slot, bns, prec);
     }
     if constexpr (STAMP) {
@@ -2547,7 +2563,6 @@ __host__ __device__ constexpr uint32_t win3_nt(uint32_t P) { return P <= 8 ? 102
 #define KSG_CS_NOFIT 1
 #define KSG_CS_ERROR 2
 #define KSG_CS_OVERSIZE 3
-#define KSG_NO_NODE 0xffffffffu
 
 struct alignas(16) RingHdr3 {
   int32_t m0;
