@@ -170,6 +170,30 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
                  : -1;
   int32_t tot = 0;  // svc_total of each pod's service (lane j)
   if (MODE == KSG_WIN_ANTI && lane < np) tot = c.svc_total;
+  // ServiceAntiAffinity term of every pod of the group on this lane's node
+  // (CalculateAntiAffinityPriority, spreading.go:152-166): the count loads are
+  // all issued before the first use, not one L2 round trip per pod
+  int64_t aterm[KSG_PG];
+  if constexpr (MODE == KSG_WIN_ANTI) {
+    int32_t pcs[KSG_PG][KSG_MAX_ANTI];
+#pragma unroll
+    for (int j = 0; j < KSG_PG; ++j)
+#pragma unroll
+      for (int a = 0; a < KSG_MAX_ANTI; ++a)
+        pcs[j][a] = ((uint32_t)j < np && dom[a] >= 0)
+                        ? dcnt[(size_t)(p0 + j) * d.n_domains_total + d.anti_dom_off[a] + dom[a]]
+                        : 0;
+#pragma unroll
+    for (int j = 0; j < KSG_PG; ++j) {
+      const int32_t tj = __builtin_amdgcn_readlane(tot, j);
+      int64_t s = 0;
+#pragma unroll
+      for (int a = 0; a < KSG_MAX_ANTI; ++a)
+        if (dom[a] >= 0)  // unlabelled nodes score 0
+          s += (int64_t)d.w_anti[a] * (tj > 0 ? frac10_f32((int64_t)tj - pcs[j][a], tj) : 10);
+      aterm[j] = s;
+    }
+  }
 
   // ---- score every pod of the group on this word
   int32_t my_max = KSG_S32_NONE;
@@ -226,17 +250,7 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
             const int64_t ss = mx > 0 ? frac10_f32((int64_t)mx - cnt[j], mx) : 10;
             s += (int64_t)d.w_spread * ss;
           }
-          if constexpr (MODE == KSG_WIN_ANTI) {  // CalculateAntiAffinityPriority (spreading.go:152-166)
-            const int32_t tj = __builtin_amdgcn_readlane(tot, j);
-#pragma unroll
-            for (int a = 0; a < KSG_MAX_ANTI; ++a) {
-              if (dom[a] >= 0) {  // unlabelled nodes score 0
-                const int32_t pc = dcnt[(size_t)(p0 + j) * d.n_domains_total + d.anti_dom_off[a] + dom[a]];
-                const int64_t sa = tj > 0 ? frac10_f32((int64_t)tj - pc, tj) : 10;
-                s += (int64_t)d.w_anti[a] * sa;
-              }
-            }
-          }
+          if constexpr (MODE == KSG_WIN_ANTI) s += aterm[j];  // (computed above)
           sc = (int32_t)s;
         }
       }
@@ -1515,9 +1529,9 @@ struct alignas(16) WinCtl2 {
   uint32_t hang;                      // a wait exceeded its spin limit (a bug)
   uint32_t xseq;                      // pods the x-checker is done with
   uint32_t xres[2];                   // its verdict for the pod of parity p: bit 0 x drops, bit 1 flag
-  // the node pod xn_seq - 1 drew (~0u: no commit), posted right after the draw
-  // so the x-checker's work overlaps the rest of the commit
-  uint32_t xn_seq, xn_node;
+  // pods whose drawn node is posted in L_xn (~0u: no commit), posted right after
+  // the draw so the x-checker's work overlaps the rest of the commit
+  uint32_t xn_seq, xn_pad;
   uint32_t fin_x;                     // the x-checker applied every commit's flags and first peers
   uint32_t pad[1];
   uint32_t t_x, t_n;                  // KSG_DEBUG & 8: clock at the xres / xn posts
@@ -1531,7 +1545,7 @@ struct alignas(16) WinCtl2 {
 
 struct WinLdsOff2 {
   uint32_t ctl, r_hdr, r_t0, r_rec, r_mod, r_svc;
-  uint32_t cm, out, peer, flag, peerset, drop, pub, drw, clist;
+  uint32_t cm, out, xn, peer, flag, peerset, drop, pub, drw, clist;
   uint32_t total;
 };
 
@@ -1547,6 +1561,7 @@ __host__ __device__ inline WinLdsOff2 win2_lds_offsets(uint32_t P, uint32_t nfla
   o.r_svc = at;   at += win_al16((size_t)R * sizeof(RingSvc));
   o.cm = at;      at += win_al16((size_t)W * sizeof(WinCommit));
   o.out = at;     at += win_al16((size_t)W * 4);
+  o.xn = at;      at += win_al16((size_t)W * 4);
   o.peer = at;    at += win_al16((size_t)W * 2 * 4);
   o.flag = at;    at += win_al16((size_t)nflag * 4);
   o.peerset = at; at += win_al16((size_t)nflag * 4);
@@ -1595,6 +1610,10 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   RingSvc* r_svc = reinterpret_cast<RingSvc*>(smem + o.r_svc);
   WinCommit* L_cm = reinterpret_cast<WinCommit*>(smem + o.cm);
   int32_t* L_out = reinterpret_cast<int32_t*>(smem + o.out);
+  // node drawn by pod p (~0u: no commit), one entry per pod: the committer runs
+  // ahead of the x-checker through pods that make no commit, so a single
+  // mailbox would be overwritten before the x-checker reads commit p's node
+  uint32_t* L_xn = reinterpret_cast<uint32_t*>(smem + o.xn);
   uint32_t* L_peer = reinterpret_cast<uint32_t*>(smem + o.peer);
   uint32_t* L_flag = reinterpret_cast<uint32_t*>(smem + o.flag);
   uint32_t* L_peerset = reinterpret_cast<uint32_t*>(smem + o.peerset);
@@ -2139,7 +2158,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         if (i) x_acc += lane == 31 ? (uint64_t)(uint32_t)((uint32_t)t_now - ctl->t_n) : 0ULL;
       }
       uint32_t res = 0;
-      const uint32_t xnode = i ? __builtin_amdgcn_readfirstlane(ctl->xn_node) : ~0u;
+      const uint32_t xnode = i ? __builtin_amdgcn_readfirstlane(L_xn[i - 1]) : ~0u;
       // the node's snapshot first (in flight over the bookkeeping below)
       const bool do_check = xnode != ~0u && !__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE;
       const uint32_t xw = d.lo + (do_check ? xnode : 0u);
@@ -2310,7 +2329,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       if (lane == 0) {
         L_cm[i].kind = 0;
         L_out[i] = __builtin_amdgcn_readlane(rec, WS_ERR) ? KSG_OUT_ERROR : KSG_OUT_NOFIT;
-        ctl->xn_node = ~0u;
+        L_xn[i] = ~0u;
         st_rel(&ctl->xn_seq, i + 1);
         st_rel(&ctl->sel_seq, i + 1);
       }
@@ -2412,7 +2431,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       woff = select_in_lanes<P>(live, cl, incl, k - 1 - ix, lane);
     }
     if (lane == 0) {  // the x-checker loads the node's snapshot meanwhile
-      ctl->xn_node = woff;
+      L_xn[i] = woff;
       if constexpr (STAMP) ctl->t_n = (uint32_t)__builtin_amdgcn_s_memtime();
       st_rel(&ctl->xn_seq, i + 1);
     }
