@@ -62,6 +62,7 @@ struct KsgDev {
   int32_t has_static_score;
   int32_t has_static_fit;
   int32_t dbg;                // debug switches (KSG_DEBUG env), 0 in production
+  uint32_t rr_dz;             // ServiceAntiAffinity re-rank: domain rows (0: off; ksg_window.hip)
   int32_t* dbgbuf;            // KSG_DEBUG & 4: per-pod resolver trace
   // arrays
   const int64_t* cap_cpu;
@@ -147,7 +148,22 @@ struct KsgWinXchg {
   // score pass has read them), so no per-window fill is enqueued
   int32_t* dcnt;
   uint32_t dcnt_n;
+  // ServiceAntiAffinity re-rank (one anti priority, one rank): a pod whose
+  // service had commits earlier in the window is re-ranked per label domain
+  // instead of ending the window. Phase A's count pass also writes, per (pod,
+  // domain row), the best score without the anti term over the pod's filtered
+  // nodes (dmb, int32[wcap][dz]; row dz-1 = unlabelled nodes), and the score pass
+  // the bitmap of filtered nodes at their row's best (uint64[wcap][ostride] at
+  // b_off); zmap = uint64[dz][nw], the nodes of each domain row. The resolver
+  // resets dmb to KSG_S32_NONE for the next window.
+  uint32_t rr;        // re-rank on (else a service's commit ends the window)
+  uint32_t dz;        // domain rows: anti domains + 1 (<= KSG_RR_MAXZ)
+  uint32_t b_off;     // byte offset in a block of the best-per-domain bitmaps
+  int32_t* dmb;
+  const uint64_t* zmap;
 };
+#define KSG_RR_MAXZ 32     // domain rows the re-rank handles (one lane each)
+#define KSG_RR_MAXSVC 4096 // services (an LDS count per service)
 
 // Device-side progress of a chain of windows (ksg_window.hip): the host enqueues
 // several windows back to back and each kernel reads where the previous one

@@ -450,6 +450,17 @@ __global__ void ksg_pairmap_kernel(uint32_t n_nodes, const ksg_node* __restrict_
     atomicOr(pairmap + (size_t)pairs[i] * nw + (n >> 6), 1ULL << (n & 63));
 }
 
+// ServiceAntiAffinity re-rank (ksg_window.hip): zmap[row][n/64] |= bit, row =
+// the node's domain of the first anti priority, d0 for unlabelled nodes
+__global__ void ksg_zonemap_kernel(uint32_t n_nodes, const int32_t* __restrict__ anti_domain, uint32_t d0,
+                                   uint32_t nw, unsigned long long* zmap) {
+  const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= n_nodes) return;
+  const int32_t z = anti_domain[n];
+  const uint32_t row = z >= 0 ? (uint32_t)z : d0;
+  atomicOr(zmap + (size_t)row * nw + (n >> 6), 1ULL << (n & 63));
+}
+
 // host-mirror deltas (add/remove pod outside a batch)
 // op: 0 store32, 1 store64, 2 or64, 3 andnot64. Patches are applied in order
 // by one thread so that several patches to one word compose.
@@ -568,6 +579,15 @@ hipError_t ksg_launch_static(const KsgStaticCfg& sc, uint32_t n_nodes, const ksg
   hipLaunchKernelGGL(ksg_static_kernel, dim3(blocks), dim3(256), 0, st, sc, n_nodes, nodes, node_pairs,
                      pair_keys, dom_of_pair, n_pairs, nw, static_fit, static_score, anti_domain,
                      aff_pair);
+  return hipGetLastError();
+}
+
+hipError_t ksg_launch_zonemap(uint32_t n_nodes, const int32_t* anti_domain, uint32_t d0, uint32_t nw,
+                              uint64_t* zmap, hipStream_t st) {
+  const uint32_t blocks = (n_nodes + 255) / 256;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(ksg_zonemap_kernel, dim3(blocks), dim3(256), 0, st, n_nodes, anti_domain, d0, nw,
+                     reinterpret_cast<unsigned long long*>(zmap));
   return hipGetLastError();
 }
 

@@ -40,7 +40,10 @@ hipError_t ksg_launch_scan(int R, bool anti, const KsgDev& d, const ksg_pod* pod
                            const int32_t* dglobal, hipStream_t st);
 hipError_t ksg_launch_win_eval(const KsgDev& d, int mode, const ksg_pod* batch, const uint32_t* ids,
                                const KsgWinRun* run, uint32_t wcap, KsgWinSum* sums, uint64_t* wbits, int32_t* wmax,
-                               uint32_t ostride, int32_t* dcnt, uint64_t* wfit, hipStream_t st);
+                               uint32_t ostride, int32_t* dcnt, uint64_t* wfit, int32_t* dmb, uint64_t* wbz,
+                               uint32_t dz, hipStream_t st);
+hipError_t ksg_launch_zonemap(uint32_t n_nodes, const int32_t* anti_domain, uint32_t d0, uint32_t nw,
+                              uint64_t* zmap, hipStream_t st);
 hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
                                   const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st);
 uint32_t ksg_win_max_window(const KsgDev& d);
@@ -152,7 +155,9 @@ struct ksg_ctx {
   uint8_t* d_xsend = nullptr;   // phase A block of this shard (KsgWinXchg layout)
   uint8_t* d_xrecv = nullptr;   // all-gathered blocks of every shard (world > 1)
   int32_t* d_dcnt = nullptr;     // [W][D] per-pod anti-affinity domain counts (phase A pre-pass)
-  size_t win_cap = 0, xsend_cap = 0, xrecv_cap = 0, dcnt_cap = 0;
+  int32_t* d_dmb = nullptr;      // [W][D+1] re-rank: best score without the anti term per domain row
+  uint64_t* d_zmap = nullptr;    // [D+1][nw] re-rank: nodes of each domain row (cluster allocation)
+  size_t win_cap = 0, xsend_cap = 0, xrecv_cap = 0, dcnt_cap = 0, dmb_cap = 0;
   KsgWinRun* d_run = nullptr;      // progress of the window chain (device)
   KsgWinRun* h_run = nullptr;      // pinned host copy
   uint32_t last_stats[4] = {0, 0, 0, 0};  // windows, stops (service scalar), stops (ties exhausted)
@@ -892,6 +897,16 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   memcpy(sc.aff_key, c->cfg.aff_key, sizeof sc.aff_key);
   HIPCHK(c, ksg_launch_static(sc, n_nodes, dn, dnp, dpk, ddom, n_pairs, c->nw, sfit, sscore, anti_dom, aff_pair,
                               (unsigned long long*)pairmap, c->st));
+  // ServiceAntiAffinity re-rank (one anti priority, one rank, few domains, an
+  // LDS count per service): the nodes of each domain row, row D = unlabelled
+  c->d_zmap = nullptr;
+  uint32_t rr_dz = 0;
+  if (c->cfg.n_anti == 1 && c->cfg.w_anti[0] != 0 && c->D > 0 && c->D + 1 <= KSG_RR_MAXZ && c->world == 1 &&
+      n_services <= KSG_RR_MAXSVC && !(getenv("KSG_DEBUG") && (atoi(getenv("KSG_DEBUG")) & 2048))) {
+    rr_dz = c->D + 1;
+    if ((rc = dalloc(c, &c->d_zmap, (size_t)rr_dz * std::max<uint32_t>(c->nw, 1), owner))) return rc;
+    HIPCHK(c, ksg_launch_zonemap(n_nodes, anti_dom, c->D, c->nw, c->d_zmap, c->st));
+  }
   HIPCHK(c, hipStreamSynchronize(c->st));
   for (void* p : tmp) (void)hipFree(p);
 
@@ -905,6 +920,7 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   d.n_services = n_services;
   d.max_keys = c->cfg.max_conflict_keys;
   d.n_domains_total = c->D;
+  d.rr_dz = rr_dz;
   d.preds = c->cfg.predicates;
   d.n_aff = (c->cfg.predicates & KSG_PRED_SERVICEAFFINITY) ? c->cfg.n_aff_labels : 0;
   // ServiceAffinity predicates (label groups); none given: one over every label
@@ -1211,16 +1227,30 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       x.nw[g] = b - a;
     }
     const bool anti = anti_on(c);
+    const bool rr = anti && c->dev.rr_dz != 0 && c->d_zmap;  // ServiceAntiAffinity re-rank
     const size_t fit_off = ((size_t)W * x.ostride * 12 + 7) & ~(size_t)7;
     // (the domain counts are zeroed once here, then by each resolver for the next window)
     x.fit_off = anti ? (uint32_t)fit_off : 0u;
-    x.blk = ((anti ? fit_off + (size_t)W * x.ostride * 8 : (size_t)W * x.ostride * 12) + 255) & ~(size_t)255;
+    x.b_off = rr ? (uint32_t)(fit_off + (size_t)W * x.ostride * 8) : 0u;
+    x.blk = ((rr     ? fit_off + (size_t)W * x.ostride * 16
+              : anti ? fit_off + (size_t)W * x.ostride * 8
+                     : (size_t)W * x.ostride * 12) +
+             255) & ~(size_t)255;
     const size_t dcnt_n = (size_t)W * std::max<uint32_t>(c->D, 1);
     if (anti) {
       if ((rc = grow(c, (void**)&c->d_dcnt, &c->dcnt_cap, dcnt_n, sizeof(int32_t)))) return rc;
       HIPCHK(c, hipMemsetAsync(c->d_dcnt, 0, dcnt_n * sizeof(int32_t), c->st));
       x.dcnt = c->d_dcnt;
       x.dcnt_n = (uint32_t)dcnt_n;
+    }
+    if (rr) {  // (the resolver resets the row bests to KSG_S32_NONE for the next window)
+      const size_t dmb_n = (size_t)W * c->dev.rr_dz;
+      if ((rc = grow(c, (void**)&c->d_dmb, &c->dmb_cap, dmb_n, sizeof(int32_t)))) return rc;
+      HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)c->d_dmb, (int)0x80000000, dmb_n, c->st));
+      x.rr = 1;
+      x.dz = c->dev.rr_dz;
+      x.dmb = c->d_dmb;
+      x.zmap = c->d_zmap;
     }
     if ((rc = grow(c, (void**)&c->d_winsum, &c->win_cap, W, sizeof(KsgWinSum)))) return rc;
     if ((rc = grow(c, (void**)&c->d_xsend, &c->xsend_cap, x.blk, 1))) return rc;
@@ -1261,12 +1291,14 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
           // ServiceAntiAffinity: the pods' per-domain counts over their filtered nodes first
           // (into d_dcnt, zero: the previous resolver cleared it)
           HIPCHK(c, ksg_launch_win_eval(c->dev, 1, c->d_pods, c->d_ids, c->d_run, W, c->d_winsum, wbits, wmax,
-                                        x.ostride, c->d_dcnt, nullptr, c->st));
+                                        x.ostride, c->d_dcnt, nullptr, x.dmb, nullptr, x.dz, c->st));
           if (c->xchg && (rc = allreduce_sum_i32(c, c->d_dcnt, c->d_dcnt, (uint32_t)dcnt_n))) return rc;
         }
         HIPCHK(c, ksg_launch_win_eval(c->dev, anti ? 2 : 0, c->d_pods, c->d_ids, c->d_run, W, c->d_winsum, wbits,
                                       wmax, x.ostride, c->d_dcnt,
-                                      anti ? reinterpret_cast<uint64_t*>(c->d_xsend + fit_off) : nullptr, c->st));
+                                      anti ? reinterpret_cast<uint64_t*>(c->d_xsend + fit_off) : nullptr, x.dmb,
+                                      rr ? reinterpret_cast<uint64_t*>(c->d_xsend + x.b_off) : nullptr, x.dz,
+                                      c->st));
         if (c->xchg && (rc = allgather(c, c->d_xsend, c->d_xrecv, x.blk))) return rc;
         HIPCHK(c, hipEventRecord(c->wev[2 * k + 1], c->st));
         HIPCHK(c, ksg_launch_win_resolve(full, W, c->d_run, c->d_winsum, x, c->d_rng, c->d_out, c->st));

@@ -85,7 +85,9 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
                                                                  uint64_t* __restrict__ wbits,
                                                                  int32_t* __restrict__ wmax, uint32_t ostride,
                                                                  int32_t* __restrict__ dcnt,
-                                                                 uint64_t* __restrict__ wfit) {
+                                                                 uint64_t* __restrict__ wfit,
+                                                                 int32_t* __restrict__ dmb,
+                                                                 uint64_t* __restrict__ wbz, uint32_t dz) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (KSG_SC_NT / 64) + (threadIdx.x >> 6));
   const uint32_t p0 = blockIdx.y * KSG_PG;
@@ -122,9 +124,15 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
   int64_t rc = 0, rm = 0;
   int32_t svc = -1, smax = 0, zr = 0;
   PodCtx c;
+  // lane j < np: pod j's list lengths (ports, pds, sel, svcs) and offsets, for its record
+  uint32_t q_n[4] = {0, 0, 0, 0}, q_off[4] = {0, 0, 0, 0};
   if (lane < np) {
     const ksg_pod& p = pods[p0 + lane];
     pod_resolve<false>(d, p, ids, c);
+    if (w == 0) {
+      q_n[0] = p.n_ports; q_n[1] = p.n_pds; q_n[2] = p.n_sel; q_n[3] = p.n_svcs;
+      q_off[0] = p.ports_off; q_off[1] = p.pds_off; q_off[2] = p.sel_off; q_off[3] = p.svcs_off;
+    }
     uint64_t m = shard_m;
     if (!has_word) m = 0;  // (no bitmap word to read)
     else if (d.has_static_fit) m &= d.static_fit[gw];  // LabelsPresence (predicates.go:215-229)
@@ -194,10 +202,20 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
       aterm[j] = s;
     }
   }
+  // re-rank (dmb != nullptr): this node's domain row for the first anti priority
+  // (dz - 1: unlabelled), and in the score pass each pod's best score without
+  // the anti term over its filtered nodes of that row (the count pass's max)
+  const int32_t zrow = (dmb && valid) ? (dom[0] >= 0 ? dom[0] : (int32_t)dz - 1) : -1;
+  int32_t mbz[KSG_PG];
+  if constexpr (MODE == KSG_WIN_ANTI) {
+#pragma unroll
+    for (int j = 0; j < KSG_PG; ++j)
+      mbz[j] = ((uint32_t)j < np && zrow >= 0) ? dmb[(size_t)(p0 + j) * dz + zrow] : KSG_S32_NONE;
+  }
 
   // ---- score every pod of the group on this word
   int32_t my_max = KSG_S32_NONE;
-  uint64_t my_bits = 0, my_fit = 0;
+  uint64_t my_bits = 0, my_fit = 0, my_bz = 0;
   const bool res_on = (P & KSG_PRED_PODFITSRESOURCES) != 0;
 #pragma unroll
   for (int j = 0; j < KSG_PG; ++j) {
@@ -213,6 +231,32 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
         fit = fit && fc && fmm;
       }
       if constexpr (MODE == KSG_WIN_COUNT) {
+        if (dmb) {
+          // re-rank: the best score without the anti term per domain row (the
+          // same sum the score pass forms), one atomic max per (wave, row)
+          int32_t bs = KSG_S32_NONE;
+          if (fit) {
+            int64_t s = sst;
+            if (d.w_lr) {
+              const int64_t tc = (int64_t)((uint64_t)usedc + (uint64_t)rcj);
+              const int64_t tm = (int64_t)((uint64_t)usedm + (uint64_t)rmj);
+              s += (int64_t)d.w_lr * ((lr_win(tc, capc, inv_c) + lr_win(tm, capm, inv_m)) >> 1);
+            }
+            if (d.w_spread) {
+              const int32_t mx = __builtin_amdgcn_readlane(smax, j);
+              s += (int64_t)d.w_spread * (mx > 0 ? frac10_f32((int64_t)mx - cnt[j], mx) : 10);
+            }
+            bs = (int32_t)s;
+          }
+          uint64_t zp = __ballot(fit && zrow >= 0);
+          while (zp) {
+            const int32_t zz = __builtin_amdgcn_readlane(zrow, (int)__builtin_ctzll(zp));
+            const bool mine = ((zp >> lane) & 1ULL) && zrow == zz;
+            const int32_t mx = wave_total_max(mine ? bs : KSG_S32_NONE);
+            if (lane == 0) atomicMax(dmb + (size_t)(p0 + j) * dz + zz, mx);
+            zp &= ~__ballot(mine);
+          }
+        }
         // the pod's service pods on filtered labelled nodes, per domain
         // (calculateAntiAffinityPriority, spreading.go:130-151): summed over the
         // wave one domain at a time, one atomic per (wave, domain)
@@ -234,6 +278,7 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
         const uint64_t fb = __ballot(fit);
         if (lane == (uint32_t)j) my_fit = fb;
       }
+      int32_t base = KSG_S32_NONE;  // (re-rank) the score without the anti term
       int32_t sc = KSG_S32_NONE;
       if (fit) {
         if (d.equal_fallback) {
@@ -250,6 +295,7 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
             const int64_t ss = mx > 0 ? frac10_f32((int64_t)mx - cnt[j], mx) : 10;
             s += (int64_t)d.w_spread * ss;
           }
+          base = (int32_t)s;
           if constexpr (MODE == KSG_WIN_ANTI) s += aterm[j];  // (computed above)
           sc = (int32_t)s;
         }
@@ -261,13 +307,22 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
         my_max = m;
         my_bits = b;
       }
+      if constexpr (MODE == KSG_WIN_ANTI) {
+        if (dmb) {  // filtered nodes at their domain row's best score without the anti term
+          const uint64_t bz = __ballot(fit && zrow >= 0 && base == mbz[j]);
+          if (lane == (uint32_t)j) my_bz = bz;
+        }
+      }
     }
   }
   if constexpr (MODE == KSG_WIN_COUNT) return;
   if (lane < np && has_word) {
     wmax[(size_t)(p0 + lane) * ostride + w] = my_max;
     wbits[(size_t)(p0 + lane) * ostride + w] = my_bits;
-    if constexpr (MODE == KSG_WIN_ANTI) wfit[(size_t)(p0 + lane) * ostride + w] = my_fit;
+    if constexpr (MODE == KSG_WIN_ANTI) {
+      wfit[(size_t)(p0 + lane) * ostride + w] = my_fit;
+      if (dmb) wbz[(size_t)(p0 + lane) * ostride + w] = my_bz;
+    }
   }
 
   // ---- the resolver's record of each pod (one wave per pod group)
@@ -292,18 +347,25 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
       S->n_sel = (uint16_t)p.n_sel;
       S->n_svcs = (uint16_t)p.n_svcs;
     }
-    for (uint32_t j = 0; j < np; ++j) {
-      const ksg_pod& p = pods[p0 + j];
-      const uint32_t ninl = p.n_ports + p.n_pds + p.n_sel + p.n_svcs;
-      if (lane < KSG_WIN_INLINE && lane < ninl) {
-        uint32_t t = lane, v;
-        if (t < p.n_ports) v = ids[p.ports_off + t];
-        else if ((t -= p.n_ports) < p.n_pds) v = ids[p.pds_off + t];
-        else if ((t -= p.n_pds) < p.n_sel) v = ids[p.sel_off + t];
-        else v = ids[p.svcs_off + (t - p.n_sel)];
-        sums[p0 + j].ids[lane] = v;
-      }
+    // the pods' inline id lists: lane t takes entry t of every pod of the group,
+    // all loads issued before the first store (not one pod's round trip after
+    // another's)
+    uint32_t v[KSG_PG], ninl[KSG_PG];
+#pragma unroll
+    for (int j = 0; j < KSG_PG; ++j) {
+      const uint32_t a = __builtin_amdgcn_readlane(q_n[0], j), b = __builtin_amdgcn_readlane(q_n[1], j);
+      const uint32_t e = __builtin_amdgcn_readlane(q_n[2], j), f = __builtin_amdgcn_readlane(q_n[3], j);
+      ninl[j] = (uint32_t)j < np ? a + b + e + f : 0u;
+      uint32_t t = lane, idx;
+      if (t < a) idx = __builtin_amdgcn_readlane(q_off[0], j) + t;
+      else if ((t -= a) < b) idx = __builtin_amdgcn_readlane(q_off[1], j) + t;
+      else if ((t -= b) < e) idx = __builtin_amdgcn_readlane(q_off[2], j) + t;
+      else idx = __builtin_amdgcn_readlane(q_off[3], j) + (t - e);
+      v[j] = (lane < KSG_WIN_INLINE && lane < ninl[j]) ? ids[idx] : 0u;
     }
+#pragma unroll
+    for (int j = 0; j < KSG_PG; ++j)
+      if (lane < KSG_WIN_INLINE && lane < ninl[j]) sums[p0 + j].ids[lane] = v[j];
   }
 }
 
@@ -418,12 +480,17 @@ struct WinLdsOff {
   uint32_t s_meta, s_cap, s_snp, s_dl, s_inv;          // slots
   uint32_t keys, svcs, scnt;
   uint32_t peer, out, flag, peerset, drop, ord;
+  // re-rank (dz > 0): ring B words, per-row best scores and domain counts;
+  // the domain rows' node words; window commits per service; the checkers'
+  // per-row count additions by pod parity
+  uint32_t r_b, r_mb, r_dc, zm, nsv, dca;
   uint32_t total;
 };
 
 __host__ __device__ constexpr uint32_t win_al16(size_t x) { return (uint32_t)((x + 15) & ~(size_t)15); }
 
-__host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag, uint32_t W, bool anti) {
+__host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag, uint32_t W, bool anti,
+                                                     uint32_t dz = 0, uint32_t nsvc = 0) {
   WinLdsOff o;
   const uint32_t KSG_RING = win_ring(P);
   uint32_t at = 0;
@@ -448,6 +515,12 @@ __host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag,
   o.peerset = at; at += win_al16((size_t)nflag * 4);
   o.drop = at;    at += win_al16((size_t)2 * P * 64 * 8);
   o.ord = at;     at += win_al16((size_t)2 * sizeof(WinOrder));
+  o.r_b = at;     at += dz ? win_al16((size_t)KSG_RING * P * 64 * 8) : 0u;
+  o.r_mb = at;    at += dz ? win_al16((size_t)KSG_RING * KSG_RR_MAXZ * 4) : 0u;
+  o.r_dc = at;    at += dz ? win_al16((size_t)KSG_RING * KSG_RR_MAXZ * 4) : 0u;
+  o.zm = at;      at += win_al16((size_t)dz * P * 64 * 8);
+  o.nsv = at;     at += dz ? win_al16((size_t)nsvc * 4) : 0u;
+  o.dca = at;     at += dz ? win_al16((size_t)KSG_RES_NCHK * 2 * KSG_RR_MAXZ * 4) : 0u;
   o.total = at;
   return o;
 }
@@ -660,11 +733,23 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
   const uint32_t nwords = d.nwords;
   constexpr uint32_t KSG_RING = win_ring(P);
   constexpr uint32_t KSG_RES_NT = win_res_nt(P);
+  // re-rank: a pod whose service had commits earlier in the window is ranked
+  // again per domain row (committer) instead of ending the window
+  const bool rr = ANTI && x.rr != 0;
+  const uint32_t dz = rr ? x.dz : 0u;
   if constexpr (ANTI) {  // this window's score pass has read the domain counts: zero them for the next
-    for (uint32_t t = tid; t < x.dcnt_n; t += KSG_RES_NT) x.dcnt[t] = 0;
+    // (with the re-rank the producers stage them: the committer zeroes them at the end)
+    if (!rr)
+      for (uint32_t t = tid; t < x.dcnt_n; t += KSG_RES_NT) x.dcnt[t] = 0;
   }
   constexpr bool anti_on = ANTI;  // (the host passes fit bitmaps, x.fit_off != 0, exactly then)
-  const WinLdsOff o = win_lds_offsets(P, nflag, wcap, anti_on);
+  const WinLdsOff o = win_lds_offsets(P, nflag, wcap, anti_on, dz, d.n_services);
+  uint64_t* const r_b = reinterpret_cast<uint64_t*>(smem + o.r_b);   // [ring][P*64] best-per-row words
+  int32_t* const r_mb = reinterpret_cast<int32_t*>(smem + o.r_mb);   // [ring][KSG_RR_MAXZ] best per row
+  int32_t* const r_dc = reinterpret_cast<int32_t*>(smem + o.r_dc);   // [ring][KSG_RR_MAXZ] domain counts
+  uint64_t* const L_zm = reinterpret_cast<uint64_t*>(smem + o.zm);   // [dz][P*64] nodes of each row
+  uint32_t* const L_nsv = reinterpret_cast<uint32_t*>(smem + o.nsv); // window commits per service
+  int32_t* const L_dca = reinterpret_cast<int32_t*>(smem + o.dca);   // [chk][parity][KSG_RR_MAXZ]
   WinCtl* ctl = reinterpret_cast<WinCtl*>(smem + o.ctl);
   RingHdr* r_hdr = reinterpret_cast<RingHdr*>(smem + o.r_hdr);
   uint64_t* r_t0 = reinterpret_cast<uint64_t*>(smem + o.r_t0);
@@ -697,6 +782,13 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
     }
   }
   for (uint32_t w = tid; w < 2 * P * 64u; w += KSG_RES_NT) L_drop[w] = 0;
+  if (rr) {
+    for (uint32_t t = tid; t < dz * P * 64; t += KSG_RES_NT) {
+      const uint32_t row = t / (P * 64), w = t % (P * 64);
+      L_zm[t] = w < nwords ? x.zmap[(size_t)row * d.nw + d.wlo + w] : 0ULL;
+    }
+    for (uint32_t t = tid; t < d.n_services; t += KSG_RES_NT) L_nsv[t] = 0;
+  }
   __syncthreads();
   const uint64_t rng0 = *rng_io;
 
@@ -847,6 +939,17 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
         for (int q = 0; q < P; ++q)
           r_fit[(size_t)e * P * 64 + lane * P + q] =
               wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + x.fit_off + j * row_b) : 0ULL;
+        if (rr) {  // the re-rank's inputs: best-per-row words, best per row, domain counts
+#pragma unroll
+          for (int q = 0; q < P; ++q)
+            r_b[(size_t)e * P * 64 + lane * P + q] =
+                wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + x.b_off + j * row_b) : 0ULL;
+          if (lane < dz) {
+            r_mb[e * KSG_RR_MAXZ + lane] = x.dmb[(size_t)j * dz + lane];
+            r_dc[e * KSG_RR_MAXZ + lane] =
+                lane + 1 < dz ? x.dcnt[(size_t)j * d.n_domains_total + d.anti_dom_off[0] + lane] : 0;
+          }
+        }
       }
       if (inl && lane < n_svcs) {
         r_svc[e].cnt[lane] = s_cnt;
@@ -892,25 +995,52 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
       const uint32_t rec = lane < KSG_WIN_SUM_DWORDS ? r_rec[e * KSG_WIN_SUM_DWORDS + lane] : 0u;
       const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
       uint32_t cnt = 0, astop = 0;
+      int32_t dadd = 0;  // (re-rank) this lane's domain row: window commits of the pod's service it counts
       if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE && c * 64 < ns) {
         const PodView pv = pod_view(rec);
         const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
-        bool drop = false, moved = false;
+        bool drop = false, moved = false, t0_drop = false;
+        uint32_t ks = 0, zr = ~0u;
         if (sl < ns && sl != xs) {
           const uint32_t nd = S.meta[sl].node;
-          if ((t0e[nd >> 6] >> (nd & 63)) & 1ULL) {
+          const bool in_t0 = (t0e[nd >> 6] >> (nd & 63)) & 1ULL;
+          // (re-rank: every node at its domain row's best is a candidate, T0 among them)
+          const bool in_b = rr ? ((r_b[(size_t)e * P * 64 + (nd >> 6)] >> (nd & 63)) & 1ULL) != 0 : in_t0;
+          if (in_b) {
             drop = slot_drops(d, S, sl, pv, rec, res_on, ports_on, disk_on, spread_on);
             if (drop)
               atomicOr(reinterpret_cast<unsigned long long*>(L_drop + (size_t)par * P * 64 + (nd >> 6)),
                        1ULL << (nd & 63));
+            t0_drop = drop && in_t0;
           }
-          if (anti_on && pv.s >= 0 && ((r_fit[(size_t)e * P * 64 + (nd >> 6)] >> (nd & 63)) & 1ULL) &&
-              !slot_fits_now(S, sl, pv, rec, res_on, ports_on, disk_on))
-            moved = anti_counts_move(d, nd, pv.s);
+          const bool fit_snap = anti_on && pv.s >= 0 && ((r_fit[(size_t)e * P * 64 + (nd >> 6)] >> (nd & 63)) & 1ULL);
+          bool fits_now = false;
+          if (fit_snap) {
+            fits_now = slot_fits_now(S, sl, pv, rec, res_on, ports_on, disk_on);
+            if (!fits_now) moved = anti_counts_move(d, nd, pv.s);
+          }
+          if (rr && fits_now && ((S.meta[sl].smask >> (pv.s & 31)) & 1u)) {
+            // the window's commits of the pod's service on this node count in its domain
+            const uint32_t* sv = S.svcs + (size_t)sl * KSG_SLOT_SVCS;
+            for (uint32_t a = 0; a < S.meta[sl].ns; ++a) ks += sv[a] == (uint32_t)pv.s;
+            for (uint32_t r = 0; r + 1 < dz; ++r)
+              if ((L_zm[(size_t)r * P * 64 + (nd >> 6)] >> (nd & 63)) & 1ULL) zr = r;
+          }
         }
-        cnt = __popcll(__ballot(drop));
+        cnt = __popcll(__ballot(t0_drop));
         astop = __ballot(moved) != 0;
+        if (rr) {
+          uint64_t pm = __ballot(ks != 0 && zr != ~0u);
+          while (pm) {
+            const int b = (int)__builtin_ctzll(pm);
+            pm &= pm - 1;
+            const uint32_t zz = (uint32_t)__builtin_amdgcn_readlane((int)zr, b);
+            const int32_t kk = __builtin_amdgcn_readlane((int)ks, b);
+            if (lane == zz) dadd += kk;
+          }
+        }
       }
+      if (rr && lane < dz) L_dca[(c * 2 + par) * KSG_RR_MAXZ + lane] = dadd;
       if (lane == 0) {
         ctl->chk_cnt[c][par] = cnt;
         ctl->chk_stop[c][par] = astop;
@@ -1004,7 +1134,9 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
             for (uint32_t b = 0; b < base_ns; ++b) before += sl[b] == my_sv;
             changed = aff_on && peer == -1 && !((L_peerset[my_sv >> 5] >> (my_sv & 31)) & 1u);
             // ServiceAntiAffinity divides by the service's pod count: any commit changes it
-            changed |= anti_on;
+            // (the re-rank takes that: later pods of the service are ranked again)
+            changed |= anti_on && !rr;
+            if (rr) atomicAdd(&L_nsv[my_sv], 1u);
           }
           // first commit of a service with no peer yet: record the peer (in order)
           uint64_t pm = __ballot(sv_lane && peer == -1);
@@ -1128,6 +1260,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
     const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
     const uint32_t k0 = __builtin_amdgcn_readfirstlane(r_hdr[e].k0);
     const int32_t s = (int32_t)__builtin_amdgcn_readlane(rec, WS_SVC);
+    uint32_t mv_n = 0;  // (re-rank) earlier window commits of the pod's service
     if (s >= 0 && (spread_on || aff_on || anti_on)) {
       // the flags of every earlier commit that may concern this pod's service
       const bool prev_has = __ballot(lane < prev_nsv && prev_sv == (uint32_t)s) != 0;
@@ -1141,7 +1274,9 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
         reason = KSG_STOP_SERVICE;
         break;
       }
+      if (rr) mv_n = __builtin_amdgcn_readfirstlane(L_nsv[s]);
     }
+    const bool moved = mv_n != 0;
     // (the order buffer of parity i was last used by order i-2)
     if (!wait_scribe(i >= 1 ? i - 1 : 0)) {
       resolved = i;
@@ -1178,7 +1313,10 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
     // ---- the slot the previous pod just committed into: re-check it here
     const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
     bool a_drop = false;
-    if (ls_valid && ((t0e[ls_node >> 6] >> (ls_node & 63)) & 1ULL)) {
+    const bool a_in_t0 = ls_valid && ((t0e[ls_node >> 6] >> (ls_node & 63)) & 1ULL);
+    // (re-rank: a node at its domain row's best may be a tie once the pod is ranked again)
+    const bool a_in_b = ls_valid && rr && ((r_b[(size_t)e * P * 64 + (ls_node >> 6)] >> (ls_node & 63)) & 1ULL);
+    if (a_in_t0 || a_in_b) {
       const int64_t now_c = (int64_t)((uint64_t)ls_snp_c + (uint64_t)ls_dl_c);
       const int64_t now_m = (int64_t)((uint64_t)ls_snp_m + (uint64_t)ls_dl_m);
       if (res_on && !pv.zero_req) {  // PodFitsResources
@@ -1246,6 +1384,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
       chk_drops += __builtin_amdgcn_readfirstlane(ctl->chk_cnt[c][par]);
       chk_stop |= __builtin_amdgcn_readfirstlane(ctl->chk_stop[c][par]);
     }
+    bool ls_counts = false;  // (re-rank) the last slot's node is still among the pod's filtered nodes
     if (anti_on && pv.s >= 0 && !chk_stop && ls_valid &&
         ((r_fit[(size_t)e * P * 64 + (ls_node >> 6)] >> (ls_node & 63)) & 1ULL)) {
       // the last slot, from the register copy: does the pod still fit it?
@@ -1266,6 +1405,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
         fit = __ballot(hit) == 0;
       }
       if (!fit && anti_counts_move(d, ls_node, pv.s)) chk_stop = 1;
+      ls_counts = fit;
     }
     if (chk_stop) {
       resolved = i;  // the pod's anti-affinity domain counts changed in the window
@@ -1274,15 +1414,88 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
     }
     KSG_STAMP(3)
     // ---- selection: k live ties, ix-th in descending rank = (k-1-ix)-th ascending
-    const uint32_t dropped = chk_drops + (a_drop ? 1u : 0u);
-    if (dropped >= k0) {
+    const uint32_t dropped = chk_drops + ((a_drop && a_in_t0) ? 1u : 0u);
+    if (!moved && dropped >= k0) {
       resolved = i;  // every snapshot tie got worse: needs a fresh snapshot
       reason = KSG_STOP_EXHAUSTED;
       break;
     }
     const uint32_t k = k0 - dropped;
     uint32_t woff;
-    if (dropped == 0) {
+    if (moved) {
+      // ---- re-rank (calculateAntiAffinityPriority, spreading.go:104-168): the
+      // service's pod count n and the pod's per-domain counts over its filtered
+      // nodes moved with the window's commits of the service. A node's score is
+      // its score without the anti term (unchanged unless the node was committed
+      // in the window: those are the checkers' drops) plus its domain row's
+      // term, so the best is among each row's best nodes at the snapshot (B) and
+      // the sequential tie set is B minus drops, in the rows whose best + term
+      // is the maximum. A row whose every B node dropped ends the window if its
+      // snapshot best + term could still reach that maximum.
+      KSG_COUNT(9, 64)
+      uint64_t* dw = L_drop + (size_t)par * P * 64;
+      const int32_t nn = (int32_t)__builtin_amdgcn_readlane(rec, WS_STOT) + (int32_t)mv_n;
+      int32_t ls_add = 0;
+      uint32_t ls_row = ~0u;
+      if (ls_counts) {  // the last slot's commits of the service (the checkers skip that slot)
+        const uint32_t kls = (uint32_t)__popcll(__ballot(lane < ls_ns && ls_sv == (uint32_t)s));
+        if (kls) {
+          const uint64_t zb = __ballot(lane + 1 < dz &&
+                                       ((L_zm[(size_t)lane * P * 64 + (ls_node >> 6)] >> (ls_node & 63)) & 1ULL));
+          if (zb) {
+            ls_row = (uint32_t)__builtin_ctzll(zb);
+            ls_add = (int32_t)kls;
+          }
+        }
+      }
+      int32_t cz = 0, mbz = KSG_S32_NONE;
+      if (lane < dz) {
+        cz = r_dc[e * KSG_RR_MAXZ + lane] + L_dca[par * KSG_RR_MAXZ + lane] +
+             L_dca[(2 + par) * KSG_RR_MAXZ + lane] + (lane == ls_row ? ls_add : 0);
+        mbz = r_mb[e * KSG_RR_MAXZ + lane];
+      }
+      // unlabelled nodes (row dz-1) score 0 (spreading.go:164-166)
+      const int64_t aa = lane + 1 < dz ? (int64_t)d.w_anti[0] * frac10_f32((int64_t)nn - cz, nn) : 0;
+      uint64_t lw[P];
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        lw[q] = r_b[(size_t)e * P * 64 + lane * P + q] & ~dw[lane * P + q];
+        if (a_drop && lane * P + q == (a_node >> 6)) lw[q] &= ~(1ULL << (a_node & 63));
+      }
+      uint32_t livez = 0;
+      for (uint32_t r = 0; r < dz; ++r) {
+        uint32_t c1 = 0;
+#pragma unroll
+        for (int q = 0; q < P; ++q) c1 += __popcll(lw[q] & L_zm[(size_t)r * P * 64 + lane * P + q]);
+        const uint32_t tr = wave_total_add(c1);
+        if (lane == r) livez = tr;
+      }
+      const int32_t val = (lane < dz && mbz != KSG_S32_NONE) ? (int32_t)((int64_t)mbz + aa) : KSG_S32_NONE;
+      const int32_t mlive = wave_total_max(livez > 0 ? val : KSG_S32_NONE);
+      if (mlive == KSG_S32_NONE || __ballot(lane < dz && livez == 0 && mbz != KSG_S32_NONE && val > mlive)) {
+        resolved = i;  // the best row's best nodes all got worse: needs a fresh snapshot
+        reason = KSG_STOP_EXHAUSTED;
+        break;
+      }
+      const bool zs = lane < dz && livez > 0 && val == mlive;
+      const uint64_t zsel = __ballot(zs);
+      const uint32_t k2 = wave_total_add(zs ? livez : 0u);
+      const uint64_t r = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(r_hdr[e].r >> 32)) << 32) |
+                         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r_hdr[e].r);
+      const uint32_t ix = umod64_32(r, k2);
+      uint64_t sw[P];
+      uint32_t cl = 0;
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        uint64_t m = 0;
+        for (uint64_t zz = zsel; zz; zz &= zz - 1)
+          m |= L_zm[(size_t)__builtin_ctzll(zz) * P * 64 + lane * P + q];
+        sw[q] = lw[q] & m;
+        cl += __popcll(sw[q]);
+      }
+      const uint32_t incl = dpp_scan_add(cl);
+      woff = select_in_lanes<P>(sw, cl, incl, k2 - 1 - ix, lane);
+    } else if (dropped == 0) {
       woff = (uint32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].pred);  // staged by the producer
     } else {
       KSG_COUNT(7, 64)
@@ -1313,6 +1526,10 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
       for (int q = 0; q < P; ++q) cl += __popcll(live[q]);
       const uint32_t incl = dpp_scan_add(cl);
       woff = select_in_lanes<P>(live, cl, incl, k - 1 - ix, lane);
+    }
+    if (rr) {  // (re-rank: drops outside T0 are scattered too) clear them for the pod two ahead
+#pragma unroll
+      for (int q = 0; q < P; ++q) L_drop[(size_t)par * P * 64 + lane * P + q] = 0;
     }
     const uint32_t wn = d.lo + woff;
     KSG_STAMP(4)
@@ -1425,6 +1642,10 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
   if (lane == 0) st_rel(&ctl->stop, 1u);
   const bool drained = wait_scribe(resolved);
   if (!drained) reason = KSG_STOP_HANG;
+  if (rr) {  // the producers staged this window's domain counts and row bests: reset them for the next
+    for (uint32_t t = lane; t < x.dcnt_n; t += 64) x.dcnt[t] = 0;
+    for (uint32_t t = lane; t < wcap * dz; t += 64) x.dmb[t] = KSG_S32_NONE;
+  }
   if constexpr (STAMP) {
     if (lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
   }
@@ -4740,18 +4961,19 @@ static const size_t kWinLdsBudget = 156 * 1024;
 
 hipError_t ksg_launch_win_eval(const KsgDev& d, int mode, const ksg_pod* batch, const uint32_t* ids,
                                const KsgWinRun* run, uint32_t wcap, KsgWinSum* sums, uint64_t* wbits, int32_t* wmax,
-                               uint32_t ostride, int32_t* dcnt, uint64_t* wfit, hipStream_t st) {
+                               uint32_t ostride, int32_t* dcnt, uint64_t* wfit, int32_t* dmb, uint64_t* wbz,
+                               uint32_t dz, hipStream_t st) {
   const uint32_t gx = std::max<uint32_t>(1, (d.nwords + KSG_SC_NT / 64 - 1) / (KSG_SC_NT / 64));
   const dim3 grid(gx, (wcap + KSG_PG - 1) / KSG_PG);
   if (mode == KSG_WIN_COUNT)
     hipLaunchKernelGGL(ksg_win_score_kernel<KSG_WIN_COUNT>, grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, run, wcap,
-                       sums, wbits, wmax, ostride, dcnt, wfit);
+                       sums, wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz);
   else if (mode == KSG_WIN_ANTI)
     hipLaunchKernelGGL(ksg_win_score_kernel<KSG_WIN_ANTI>, grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, run, wcap,
-                       sums, wbits, wmax, ostride, dcnt, wfit);
+                       sums, wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz);
   else
     hipLaunchKernelGGL(ksg_win_score_kernel<KSG_WIN_PLAIN>, grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, run, wcap,
-                       sums, wbits, wmax, ostride, dcnt, wfit);
+                       sums, wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz);
   return hipGetLastError();
 }
 
@@ -4766,7 +4988,7 @@ uint32_t ksg_win_max_window(const KsgDev& d) {
   uint32_t lo = 0, hi = 4096;
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1) / 2;
-    const uint32_t need = anti              ? win_lds_offsets(P, nflag, mid, d.n_anti > 0).total
+    const uint32_t need = anti              ? win_lds_offsets(P, nflag, mid, d.n_anti > 0, d.rr_dz, d.n_services).total
                           : (d.dbg & 512)  ? win3_lds_offsets(P, nflag, mid).total
                           : (d.dbg & 1024) ? win4_lds_offsets(P, nflag, mid).total
                                            : win2_lds_offsets(P, nflag, mid).total;
@@ -4893,7 +5115,8 @@ hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run
 #undef KSG_RES2_CASE
     return hipErrorInvalidValue;
   }
-  const size_t lds = win_lds_offsets(P, (d.n_services + 31) / 32, wcap, x.fit_off != 0).total;
+  const size_t lds =
+      win_lds_offsets(P, (d.n_services + 31) / 32, wcap, x.fit_off != 0, x.rr ? x.dz : 0u, d.n_services).total;
   const bool stamp = (d.dbg & 8) != 0;  // KSG_DEBUG & 8: per-section s_memtime stamps
   const bool anti = x.fit_off != 0;
 #define KSG_RES_CASE(PP, AN)                                                                          \
