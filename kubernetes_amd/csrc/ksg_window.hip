@@ -1756,6 +1756,16 @@ struct alignas(16) WinCtl2 {
   uint32_t fin_x;                     // the x-checker applied every commit's flags and first peers
   uint32_t pad[1];
   uint32_t t_x, t_n;                  // KSG_DEBUG & 8: clock at the xres / xn posts
+  // ServiceAntiAffinity (re-rank): checker c found a slot the pod fitted at the
+  // snapshot, no longer fits, labelled and holding pods of its service (the
+  // domain counts moved: the window ends); the x-checker's correction of the
+  // domain count of commit i-1's node's row (row ~0u: none), by pod parity
+  uint32_t chk_stop[KSG_RES_NCHK][2];
+  uint32_t xdz[2];
+  int32_t xdc[2];
+  // window commits of the pod's service up to commit i-2, read by the x-checker
+  // before it applies commit i-1's (the committer adds commit i-1 itself)
+  uint32_t xnsv[2];
 };
 // per-slot list table: [0, 8) conflict keys, [8, 20) service ids, [20, 32) the
 // services' counts on the node at the snapshot (written by the owner checker)
@@ -1767,10 +1777,13 @@ struct alignas(16) WinCtl2 {
 struct WinLdsOff2 {
   uint32_t ctl, r_hdr, r_t0, r_rec, r_mod, r_svc;
   uint32_t cm, out, xn, peer, flag, peerset, drop, pub, drw, clist;
+  // ServiceAntiAffinity re-rank (dz > 0; see the LDS-slot resolver's WinLdsOff)
+  uint32_t r_fit, r_b, r_mb, r_dc, zm, nsv, dca;
   uint32_t total;
 };
 
-__host__ __device__ inline WinLdsOff2 win2_lds_offsets(uint32_t P, uint32_t nflag, uint32_t W) {
+__host__ __device__ inline WinLdsOff2 win2_lds_offsets(uint32_t P, uint32_t nflag, uint32_t W, uint32_t dz = 0,
+                                                       uint32_t nsvc = 0) {
   WinLdsOff2 o;
   const uint32_t R = win_ring(P);
   uint32_t at = 0;
@@ -1790,6 +1803,13 @@ __host__ __device__ inline WinLdsOff2 win2_lds_offsets(uint32_t P, uint32_t nfla
   o.pub = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
   o.drw = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
   o.clist = at;   at += win_al16((size_t)KSG_MAX_SLOTS * KSG_CL_W * 4);
+  o.r_fit = at;   at += dz ? win_al16((size_t)R * P * 64 * 8) : 0u;
+  o.r_b = at;     at += dz ? win_al16((size_t)R * P * 64 * 8) : 0u;
+  o.r_mb = at;    at += dz ? win_al16((size_t)R * KSG_RR_MAXZ * 4) : 0u;
+  o.r_dc = at;    at += dz ? win_al16((size_t)R * KSG_RR_MAXZ * 4) : 0u;
+  o.zm = at;      at += win_al16((size_t)dz * P * 64 * 8);
+  o.nsv = at;     at += dz ? win_al16((size_t)nsvc * 4) : 0u;
+  o.dca = at;     at += dz ? win_al16((size_t)KSG_RES_NCHK * 2 * KSG_RR_MAXZ * 4) : 0u;
   o.total = at;
   return o;
 }
@@ -1800,9 +1820,12 @@ struct RegSlot {
   int64_t cap_c, cap_m, snp_c, snp_m, dl_c, dl_m;
   double inv_c, inv_m;
   uint32_t nk, ns, smask;  // list lengths as of the commits this checker applied
+  uint32_t row;            // (ServiceAntiAffinity re-rank) the node's domain row, ~0u unlabelled
 };
 
-template <int P, bool STAMP>
+// ANTI: ServiceAntiAffinity with the re-rank (x.rr; the LDS-slot resolver above
+// takes every other anti-affinity configuration)
+template <int P, bool STAMP, bool ANTI>
 __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
                                                                const KsgWinSum* __restrict__ sums,
                                                                const KsgWinXchg x, uint64_t* rng_io,
@@ -1822,7 +1845,15 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   constexpr uint32_t NT = 512;
   constexpr uint32_t NPW = NT / 64 - KSG_RES_P0;  // producer waves
   constexpr uint32_t DW = KSG_WIN_SUM_DWORDS;
-  const WinLdsOff2 o = win2_lds_offsets(P, nflag, wcap);
+  const uint32_t dz = ANTI ? x.dz : 0u;
+  const WinLdsOff2 o = win2_lds_offsets(P, nflag, wcap, dz, d.n_services);
+  uint64_t* const r_fit = reinterpret_cast<uint64_t*>(smem + o.r_fit);  // [ring][P*64] fit at the snapshot
+  uint64_t* const r_b = reinterpret_cast<uint64_t*>(smem + o.r_b);      // [ring][P*64] best-per-row nodes
+  int32_t* const r_mb = reinterpret_cast<int32_t*>(smem + o.r_mb);      // [ring][KSG_RR_MAXZ] best per row
+  int32_t* const r_dc = reinterpret_cast<int32_t*>(smem + o.r_dc);      // [ring][KSG_RR_MAXZ] domain counts
+  uint64_t* const L_zm = reinterpret_cast<uint64_t*>(smem + o.zm);      // [dz][P*64] nodes of each row
+  uint32_t* const L_nsv = reinterpret_cast<uint32_t*>(smem + o.nsv);    // window commits per service
+  int32_t* const L_dca = reinterpret_cast<int32_t*>(smem + o.dca);      // [chk][parity][KSG_RR_MAXZ]
   WinCtl2* ctl = reinterpret_cast<WinCtl2*>(smem + o.ctl);
   RingHdr* r_hdr = reinterpret_cast<RingHdr*>(smem + o.r_hdr);
   uint64_t* r_t0 = reinterpret_cast<uint64_t*>(smem + o.r_t0);
@@ -1860,6 +1891,13 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     L_drw[w] = 0;
   }
   for (uint32_t w = tid; w < 2 * P * 64u; w += NT) L_drop[w] = 0;
+  if constexpr (ANTI) {
+    for (uint32_t t = tid; t < dz * P * 64; t += NT) {
+      const uint32_t row = t / (P * 64), w = t % (P * 64);
+      L_zm[t] = w < nwords ? x.zmap[(size_t)row * d.nw + d.wlo + w] : 0ULL;
+    }
+    for (uint32_t t = tid; t < d.n_services; t += NT) L_nsv[t] = 0;
+  }
   __syncthreads();
   const uint64_t rng0 = *rng_io;
 
@@ -2002,6 +2040,20 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       if (lane < DW) r_rec[e * DW + lane] = rec;
 #pragma unroll
       for (int q = 0; q < P; ++q) r_t0[(size_t)e * P * 64 + lane * P + q] = t0[q];
+      if constexpr (ANTI) {  // fit at the snapshot, best-per-row nodes, row bests, domain counts
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+          r_fit[(size_t)e * P * 64 + lane * P + q] =
+              wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + x.fit_off + j * row_b) : 0ULL;
+          r_b[(size_t)e * P * 64 + lane * P + q] =
+              wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + x.b_off + j * row_b) : 0ULL;
+        }
+        if (lane < dz) {
+          r_mb[e * KSG_RR_MAXZ + lane] = x.dmb[(size_t)j * dz + lane];
+          r_dc[e * KSG_RR_MAXZ + lane] =
+              lane + 1 < dz ? x.dcnt[(size_t)j * d.n_domains_total + d.anti_dom_off[0] + lane] : 0;
+        }
+      }
       if (inl && lane < n_svcs) {
         r_svc[e].cnt[lane] = s_cnt;
         r_svc[e].max[lane] = s_max;
@@ -2038,6 +2090,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     S.cap_c = S.cap_m = S.snp_c = S.snp_m = S.dl_c = S.dl_m = 0;
     S.inv_c = S.inv_m = 0.0;
     S.nk = S.ns = S.smask = 0;
+    S.row = ~0u;
     // AssumePod of pod p (plugin/pkg/scheduler/scheduler.go:115-118) into the
     // owner lane's slot: requested totals, list lengths; the services' snapshot
     // counts into the table (the x-checker applies the service flags, in commit
@@ -2076,6 +2129,10 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         S.node = woff;
         S.dl_c = S.dl_m = 0;
         S.smask = 0;
+        if constexpr (ANTI) {
+          const int32_t dm = gld(d.anti_domain + wn);  // (first anti priority: the re-rank's domain rows)
+          S.row = dm >= 0 ? (uint32_t)dm : ~0u;
+        }
       }
       uint32_t new_mask = 0;
       if (n_svcs) {
@@ -2140,7 +2197,81 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
       const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
       uint32_t cntd = 0;
-      if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE) {
+      if constexpr (ANTI) {
+        // the pod against this lane's slot as of commits <= i-2: a drop among the
+        // nodes at their domain row's best (B; T0 drops counted for the fast
+        // path), the domain-count stop, and the window's commits of the pod's
+        // service the slot adds to its row's count while the pod still fits it
+        bool drop = false, t0d = false, astop = false;
+        uint32_t ks = 0;
+        if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE && S.node != ~0u) {
+          const PodView pv = pod_view(rec);
+          const uint32_t wd = S.node >> 6;
+          const uint64_t nb = 1ULL << (S.node & 63);
+          const bool in_t0 = (r_t0[(size_t)e * P * 64 + wd] & nb) != 0;
+          const bool in_b = (r_b[(size_t)e * P * 64 + wd] & nb) != 0;
+          const bool fsnap = pv.s >= 0 && (r_fit[(size_t)e * P * 64 + wd] & nb) != 0;
+          if (in_b || fsnap) {
+            const int64_t now_c = (int64_t)((uint64_t)S.snp_c + (uint64_t)S.dl_c);
+            const int64_t now_m = (int64_t)((uint64_t)S.snp_m + (uint64_t)S.dl_m);
+            bool nofit = false;
+            if (res_on && !pv.zero_req)  // PodFitsResources (predicates.go:127-145)
+              nofit = !((S.cap_c == 0 || S.cap_c - now_c >= pv.req_c) && (S.cap_m == 0 || S.cap_m - now_m >= pv.req_m));
+            if (!nofit && pv.nk && S.nk) {  // PodFitsPorts / NoDiskConflict vs the window's keys
+              for (uint32_t a = 0; a < S.nk; ++a) {
+                const uint32_t key = my_cl[KSG_CL_KEY + a];
+                for (uint32_t b = 0; b < pv.nk; ++b) {
+                  const bool on = b < pv.n_ports ? ports_on : disk_on;
+                  nofit |= on && (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b)) == key;
+                }
+              }
+            }
+            if (in_b) {
+              drop = nofit;
+              if (!drop && d.w_lr) {  // LeastRequested (priorities.go:43-76)
+                const int32_t lr_now = lr_win(now_c + pv.req_c, S.cap_c, S.inv_c) + lr_win(now_m + pv.req_m, S.cap_m, S.inv_m);
+                const int32_t lr_snap =
+                    lr_win(S.snp_c + pv.req_c, S.cap_c, S.inv_c) + lr_win(S.snp_m + pv.req_m, S.cap_m, S.inv_m);
+                drop = (lr_now >> 1) != (lr_snap >> 1);
+              }
+              if (!drop && spread_on && pv.s >= 0 && ((S.smask >> (pv.s & 31)) & 1u)) {
+                int32_t delta = 0, snapc = 0;  // ServiceSpreading (spreading.go:72-86) under an unchanged maxCount
+                for (uint32_t a = 0; a < S.ns; ++a)
+                  if (my_cl[KSG_CL_SV + a] == (uint32_t)pv.s) {
+                    snapc = (int32_t)my_cl[KSG_CL_SC + a];
+                    ++delta;
+                  }
+                if (delta)
+                  drop = frac10_f32((int64_t)pv.smax - snapc - delta, pv.smax) !=
+                         frac10_f32((int64_t)pv.smax - snapc, pv.smax);
+              }
+              if (drop)
+                atomicOr(reinterpret_cast<unsigned long long*>(L_drop + (size_t)par * P * 64 + wd), nb);
+              t0d = drop && in_t0;
+            }
+            if (fsnap) {
+              if (nofit) {
+                astop = anti_counts_move(d, S.node, pv.s);
+              } else if ((S.smask >> (pv.s & 31)) & 1u) {
+                for (uint32_t a = 0; a < S.ns; ++a) ks += my_cl[KSG_CL_SV + a] == (uint32_t)pv.s;
+              }
+            }
+          }
+        }
+        cntd = __popcll(__ballot(t0d));
+        int32_t dadd = 0;
+        uint64_t pm = __ballot(ks != 0 && S.row != ~0u);
+        while (pm) {
+          const int b = (int)__builtin_ctzll(pm);
+          pm &= pm - 1;
+          const uint32_t zz = (uint32_t)__builtin_amdgcn_readlane((int)S.row, b);
+          const int32_t kk = __builtin_amdgcn_readlane((int)ks, b);
+          if (lane == zz) dadd += kk;
+        }
+        if (lane < dz) L_dca[(c * 2 + par) * KSG_RR_MAXZ + lane] = dadd;
+        const uint32_t ast = __ballot(astop) != 0;
+        if (lane == 0) ctl->chk_stop[c][par] = ast;
+      } else if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE) {
         const PodView pv = pod_view(rec);
         bool drop = false;
         if (S.node != ~0u) {
@@ -2246,12 +2377,14 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     int64_t xdc0 = 0, xdm0 = 0, xdc1 = 0, xdm1 = 0;
     // commit q (node) into its slot, the committer's bookkeeping replayed: the
     // slot, its list lengths before q, its delta after q, pod q's record
+    bool x_in_c = false;  // the last replayed commit went into an existing slot
     auto replay = [&](uint32_t node, uint32_t prec, uint32_t& slot, uint32_t& bnk, uint32_t& bns, uint64_t& dlc,
                       uint64_t& dlm) {
       const PodView ppv = pod_view(prec);
       const uint32_t p_svcs = (uint32_t)__builtin_amdgcn_readlane(prec, WS_NSS) >> 16;
       const uint64_t hit0 = __ballot(xcn0 == node), hit1 = __ballot(xcn1 == node);
       const bool in_c = (hit0 | hit1) != 0;
+      x_in_c = in_c;
       bnk = bns = 0;
       dlc = dlm = 0;
       if (in_c) {
@@ -2293,6 +2426,9 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       const bool sv_lane = lane < n_svcs;
       const uint32_t my_sv =
           (uint32_t)__shfl((int)prec, (int)min(WS_IDS + pnk + n_sel + (sv_lane ? lane : 0u), 63u), 64);
+      if constexpr (ANTI) {  // (re-rank) the service's window commits: its pod count n moved
+        if (sv_lane) atomicAdd(&L_nsv[my_sv], 1u);
+      }
       int32_t mx = 0, peer = 0, cnt = 0;
       if (sv_lane) {
         cnt = gld(d.svc_cnt + (size_t)my_sv * d.n_nodes + wn);
@@ -2385,13 +2521,16 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       const uint32_t xw = d.lo + (do_check ? xnode : 0u);
       int64_t capv = 0, usev = 0;
       double invv = 0.0;
-      int32_t xcv = 0;
+      int32_t xcv = 0, xdm = -1;
       if (do_check) {
         capv = gld(cap_src + xw);
         usev = gld(use_src + xw);
         invv = gld(inv_src + xw);
         xcv = gld(d.svc_cnt + (size_t)(s >= 0 ? s : 0) * d.n_nodes + xw);
+        if constexpr (ANTI) xdm = gld(d.anti_domain + xw);
       }
+      uint32_t xst = 0, xrow = ~0u;  // (re-rank) domain-count stop; row of x and its count correction
+      int32_t xcorr = 0;
       // commit i-1 into its slot (the committer's bookkeeping, replayed)
       uint32_t xslot = 0, bnk = 0, bns = 0;
       uint64_t dlc = 0, dlm = 0;
@@ -2450,9 +2589,47 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
           }
           xd |= __ballot(hit) != 0;
         }
-        res = (xd ? 1u : 0u) | (flag_x ? 2u : 0u);
+        if constexpr (ANTI) {
+          // x as of commit i-1 and as of i-2 (the checkers' view of it): does the
+          // pod still fit it (PodFitsResources, host ports, PDs), and its
+          // service's window commits there; the domain count of x's row moves by
+          // the difference, or the window ends if the pod no longer fits a
+          // labelled x that held pods of its service at the snapshot
+          if (s >= 0 && ((r_fit[(size_t)e * P * 64 + (xnode >> 6)] >> (xnode & 63)) & 1ULL)) {
+            const PodView qv = pod_view(prec);
+            const int64_t befv = (int64_t)((uint64_t)nowv - (uint64_t)(rl ? qv.req_m : qv.req_c));
+            bool fa = true, fb = true;
+            if (res_on && !pv.zero_req) {
+              fa = (__ballot(lane < 2 && !(capv == 0 || capv - nowv >= reqv)) & 3ULL) == 0;
+              fb = (__ballot(lane < 2 && !(capv == 0 || capv - befv >= reqv)) & 3ULL) == 0;
+            }
+            if (nk && xnk) {
+              bool ha = false, hb = false;
+              for (uint32_t b = 0; b < nk; ++b) {
+                const bool on = b < pv.n_ports ? ports_on : disk_on;
+                const bool eq = on && xcl == (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b));
+                ha |= eq && kt < xnk;
+                hb |= eq && kt < bnk;
+              }
+              fa = fa && __ballot(ha) == 0;
+              fb = fb && __ballot(hb) == 0;
+            }
+            const uint32_t kb = (uint32_t)__popcll(__ballot(s_ent && ut < bns));
+            if (!fa && xdm >= 0 && xcv > 0) xst = 1;
+            if (xdm >= 0) {
+              xrow = (uint32_t)xdm;
+              xcorr = (fa ? (int32_t)x_cnt_s : 0) - ((x_in_c && fb) ? (int32_t)kb : 0);
+            }
+          }
+        }
+        res = (xd ? 1u : 0u) | (flag_x ? 2u : 0u) | (xst ? 4u : 0u);
       }
       if (lane == 0) {
+        if constexpr (ANTI) {
+          ctl->xdz[par] = xrow;
+          ctl->xdc[par] = xcorr;
+          ctl->xnsv[par] = s >= 0 ? L_nsv[s] : 0u;
+        }
         ctl->xres[par] = res;
         if constexpr (STAMP) ctl->t_x = (uint32_t)__builtin_amdgcn_s_memtime();
         st_rel(&ctl->xseq, i + 1);
@@ -2504,6 +2681,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   int64_t dc0 = 0, dm0 = 0, dc1 = 0, dm1 = 0;  // their window deltas (current through the last commit)
   uint32_t xnode = 0;                    // node of the last commit (pod i-1)
   bool have_x = false;
+  uint32_t prev_sv = ~0u;                // (ServiceAntiAffinity) services of commit i-1, lane t < count
   uint64_t t_last = 0, t_acc = 0;
 #define KSG_STAMP2(k)                                        \
   if constexpr (STAMP) {                                     \
@@ -2555,6 +2733,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         st_rel(&ctl->sel_seq, i + 1);
       }
       have_x = false;  // pod i+1's checkers see every commit up to i-1
+      prev_sv = ~0u;
       continue;
     }
     const PodView pv = pod_view(rec);
@@ -2603,6 +2782,17 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       reason = KSG_STOP_SERVICE;
       break;
     }
+    uint32_t mv_n = 0;  // (ServiceAntiAffinity) window commits of the pod's service before it
+    if constexpr (ANTI) {
+      if ((xres & 4u) || __builtin_amdgcn_readfirstlane(ctl->chk_stop[0][par] | ctl->chk_stop[1][par])) {
+        resolved = i;  // the pod's domain counts moved: a fitted node holding its service's pods left its filter
+        reason = KSG_STOP_SERVICE;
+        break;
+      }
+      if (s >= 0)
+        mv_n = __builtin_amdgcn_readfirstlane(ctl->xnsv[par]) + (__ballot(prev_sv == (uint32_t)s) != 0 ? 1u : 0u);
+    }
+    const bool moved = mv_n != 0;
     uint32_t dropped = __builtin_amdgcn_readfirstlane(cc0) + __builtin_amdgcn_readfirstlane(cc1);
     bool x_drop = false;
     if (have_x && (xres & 1u)) {  // x counts as a new drop iff it was a snapshot tie the checkers kept
@@ -2618,7 +2808,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       x_drop = (t0x & xb) && !(dwx & xb);
     }
     dropped += x_drop ? 1u : 0u;
-    if (dropped >= k0) {
+    if (!moved && dropped >= k0) {
       resolved = i;  // every snapshot tie got worse: needs a fresh snapshot
       reason = KSG_STOP_EXHAUSTED;
       break;
@@ -2626,7 +2816,63 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     // ---- selection: k live ties, ix-th in descending rank = (k-1-ix)-th ascending
     const uint32_t k = k0 - dropped;
     uint32_t woff;
-    if (dropped == 0) {
+    if (moved) {
+      // ---- ServiceAntiAffinity re-rank (calculateAntiAffinityPriority,
+      // spreading.go:104-168; the LDS-slot resolver has the same step): the
+      // service's pod count and the pod's domain counts moved, so every domain
+      // row's term is recomputed and the tie set is the live best-per-row nodes
+      // of the rows whose best + term is the maximum
+      KSG_COUNT2(9, 64)
+      const int32_t nn = (int32_t)__builtin_amdgcn_readlane(rec, WS_STOT) + (int32_t)mv_n;
+      const uint32_t xz = __builtin_amdgcn_readfirstlane(ctl->xdz[par]);
+      const int32_t xc = (int32_t)__builtin_amdgcn_readfirstlane(ctl->xdc[par]);
+      int32_t cz = 0, mbz = KSG_S32_NONE;
+      if (lane < dz) {
+        cz = r_dc[e * KSG_RR_MAXZ + lane] + L_dca[par * KSG_RR_MAXZ + lane] + L_dca[(2 + par) * KSG_RR_MAXZ + lane] +
+             (lane == xz ? xc : 0);
+        mbz = r_mb[e * KSG_RR_MAXZ + lane];
+      }
+      // unlabelled nodes (row dz-1) score 0 (spreading.go:164-166)
+      const int64_t aa = lane + 1 < dz ? (int64_t)d.w_anti[0] * frac10_f32((int64_t)nn - cz, nn) : 0;
+      uint64_t lw[P];
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        lw[q] = r_b[(size_t)e * P * 64 + lane * P + q] & ~dww[q];
+        if (have_x && (xres & 1u) && lane * P + q == (xnode >> 6)) lw[q] &= ~(1ULL << (xnode & 63));
+      }
+      uint32_t livez = 0;
+      for (uint32_t r = 0; r < dz; ++r) {
+        uint32_t c1 = 0;
+#pragma unroll
+        for (int q = 0; q < P; ++q) c1 += __popcll(lw[q] & L_zm[(size_t)r * P * 64 + lane * P + q]);
+        const uint32_t tr = wave_total_add(c1);
+        if (lane == r) livez = tr;
+      }
+      const int32_t val = (lane < dz && mbz != KSG_S32_NONE) ? (int32_t)((int64_t)mbz + aa) : KSG_S32_NONE;
+      const int32_t mlive = wave_total_max(livez > 0 ? val : KSG_S32_NONE);
+      if (mlive == KSG_S32_NONE || __ballot(lane < dz && livez == 0 && mbz != KSG_S32_NONE && val > mlive)) {
+        resolved = i;  // the best row's best nodes all got worse: needs a fresh snapshot
+        reason = KSG_STOP_EXHAUSTED;
+        break;
+      }
+      const bool zs = lane < dz && livez > 0 && val == mlive;
+      const uint64_t zsel = __ballot(zs);
+      const uint32_t k2 = wave_total_add(zs ? livez : 0u);
+      const uint64_t r = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(r_hdr[e].r >> 32)) << 32) |
+                         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r_hdr[e].r);
+      const uint32_t ix = umod64_32(r, k2);
+      uint64_t sw[P];
+      uint32_t cl = 0;
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        uint64_t m = 0;
+        for (uint64_t zz = zsel; zz; zz &= zz - 1) m |= L_zm[(size_t)__builtin_ctzll(zz) * P * 64 + lane * P + q];
+        sw[q] = lw[q] & m;
+        cl += __popcll(sw[q]);
+      }
+      const uint32_t incl = dpp_scan_add(cl);
+      woff = select_in_lanes<P>(sw, cl, incl, k2 - 1 - ix, lane);
+    } else if (dropped == 0) {
       woff = (uint32_t)pred;  // staged by the producer
     } else {
       KSG_COUNT2(7, 64)
@@ -2650,6 +2896,11 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       for (int q = 0; q < P; ++q) cl += __popcll(live[q]);
       const uint32_t incl = dpp_scan_add(cl);
       woff = select_in_lanes<P>(live, cl, incl, k - 1 - ix, lane);
+    }
+    if constexpr (ANTI) {  // (drops outside T0 are scattered too) clear them for the pod two ahead
+#pragma unroll
+      for (int q = 0; q < P; ++q)
+        if (dww[q]) dw[lane * P + q] = 0;
     }
     if (lane == 0) {  // the x-checker loads the node's snapshot meanwhile
       L_xn[i] = woff;
@@ -2717,6 +2968,10 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     }
     have_x = true;
     xnode = woff;
+    if constexpr (ANTI) {
+      const uint32_t sv_t = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + (lane < n_svcs ? lane : 0u), 63u), 64);
+      prev_sv = lane < n_svcs ? sv_t : ~0u;
+    }
     ++n_draws;
     KSG_STAMP2(5)
   }
@@ -2737,6 +2992,10 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     }
   }
   if (!drained || ld_acq(&ctl->hang)) reason = KSG_STOP_HANG;
+  if constexpr (ANTI) {  // the producers staged this window's domain counts and row bests: reset them for the next
+    for (uint32_t t = lane; t < x.dcnt_n; t += 64) x.dcnt[t] = 0;
+    for (uint32_t t = lane; t < wcap * dz; t += 64) x.dmb[t] = KSG_S32_NONE;
+  }
   if constexpr (STAMP) {
     if (lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
   }
@@ -4988,7 +5247,9 @@ uint32_t ksg_win_max_window(const KsgDev& d) {
   uint32_t lo = 0, hi = 4096;
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1) / 2;
-    const uint32_t need = anti              ? win_lds_offsets(P, nflag, mid, d.n_anti > 0, d.rr_dz, d.n_services).total
+    const uint32_t need = (anti && d.rr_dz && !(d.dbg & 4096))
+                              ? win2_lds_offsets(P, nflag, mid, d.rr_dz, d.n_services).total
+                          : anti            ? win_lds_offsets(P, nflag, mid, d.n_anti > 0, d.rr_dz, d.n_services).total
                           : (d.dbg & 512)  ? win3_lds_offsets(P, nflag, mid).total
                           : (d.dbg & 1024) ? win4_lds_offsets(P, nflag, mid).total
                                            : win2_lds_offsets(P, nflag, mid).total;
@@ -5046,18 +5307,19 @@ static hipError_t win_resolve4_launch(const KsgDev& d, uint32_t wcap, size_t lds
   return hipGetLastError();
 }
 
-template <int PP, bool ST>
+template <int PP, bool ST, bool AN>
 static hipError_t win_resolve2_launch(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run,
                                       const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
                                       hipStream_t st) {
   static bool once = false;
   if (!once) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_resolve2_kernel<PP, ST>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_resolve2_kernel<PP, ST, AN>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipGetLastError();
     once = true;
   }
-  hipLaunchKernelGGL((ksg_win_resolve2_kernel<PP, ST>), dim3(1), dim3(512), lds, st, d, wcap, run, sums, x, rng, out);
+  hipLaunchKernelGGL((ksg_win_resolve2_kernel<PP, ST, AN>), dim3(1), dim3(512), lds, st, d, wcap, run, sums, x, rng,
+                     out);
   return hipGetLastError();
 }
 
@@ -5104,8 +5366,8 @@ hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run
     const bool stamp2 = (d.dbg & 8) != 0;
 #define KSG_RES2_CASE(PP)                                                                         \
   if (P == PP)                                                                                    \
-    return stamp2 ? win_resolve2_launch<PP, true>(d, wcap, lds2, run, sums, x, rng, out, st)      \
-                  : win_resolve2_launch<PP, false>(d, wcap, lds2, run, sums, x, rng, out, st);
+    return stamp2 ? win_resolve2_launch<PP, true, false>(d, wcap, lds2, run, sums, x, rng, out, st) \
+                  : win_resolve2_launch<PP, false, false>(d, wcap, lds2, run, sums, x, rng, out, st);
     KSG_RES2_CASE(1)
     KSG_RES2_CASE(2)
     KSG_RES2_CASE(4)
@@ -5113,6 +5375,22 @@ hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run
     KSG_RES2_CASE(16)
     KSG_RES2_CASE(32)
 #undef KSG_RES2_CASE
+    return hipErrorInvalidValue;
+  }
+  if (x.fit_off != 0 && x.rr && !(d.dbg & 4096)) {
+    // ServiceAntiAffinity with the re-rank: the register-slot resolver
+    // (KSG_DEBUG & 4096: the LDS-slot resolver instead, for comparison)
+    const size_t lds2 = win2_lds_offsets(P, (d.n_services + 31) / 32, wcap, x.dz, d.n_services).total;
+    const bool stamp2 = (d.dbg & 8) != 0;
+#define KSG_RES2A_CASE(PP)                                                                        \
+  if (P == PP)                                                                                    \
+    return stamp2 ? win_resolve2_launch<PP, true, true>(d, wcap, lds2, run, sums, x, rng, out, st) \
+                  : win_resolve2_launch<PP, false, true>(d, wcap, lds2, run, sums, x, rng, out, st);
+    KSG_RES2A_CASE(1)
+    KSG_RES2A_CASE(2)
+    KSG_RES2A_CASE(4)
+    KSG_RES2A_CASE(8)
+#undef KSG_RES2A_CASE
     return hipErrorInvalidValue;
   }
   const size_t lds =

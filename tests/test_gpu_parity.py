@@ -71,6 +71,30 @@ def test_alternative_resolvers_match_oracle(name, nn, npods, resolver, monkeypat
     dev.close()
 
 
+@pytest.mark.parametrize("resolver", [2048, 4096])
+@pytest.mark.parametrize("name,nn,npods", [("config4", 900, 1500), ("config4", 5000, 3000)])
+def test_anti_affinity_alternatives_match_oracle(name, nn, npods, resolver, monkeypatch):
+    """ServiceAntiAffinity windows without the re-rank (KSG_DEBUG & 2048: a
+    service's commit ends the window) and the re-rank in the LDS-slot resolver
+    (& 4096) give the oracle's placements too (the default is the re-rank in
+    the register-slot resolver)."""
+    monkeypatch.setenv("KSG_DEBUG", str(resolver))
+    case = Case(name, nn, npods)
+    dev, orc = _pair(case, 1024)
+    got, sg = run_batch(dev, case)
+    want, sw = run_batch(orc, case)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"first mismatches at {bad[:8]}: gpu {got[bad[:8]]} oracle {want[bad[:8]]}"
+    assert sg == sw
+    st = dev.last_batch_stats()
+    assert st["windows"] > 0
+    if resolver == 2048:  # every window ends at a pod whose service had a commit in it
+        assert st["stops_service"] >= st["windows"] // 2
+    else:
+        assert st["stops_service"] < st["windows"] // 2
+    dev.close()
+
+
 @pytest.mark.parametrize("window", [0, 256])
 def test_batch_chunks_equal_one_batch(window):
     """Batch boundaries must not change outcomes (state persists across launches)."""
