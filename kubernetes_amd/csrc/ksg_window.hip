@@ -1763,6 +1763,7 @@ struct alignas(16) WinCtl2 {
   uint32_t chk_stop[KSG_RES_NCHK][2];
   uint32_t xdz[2];
   int32_t xdc[2];
+  uint32_t xrw[2];  // domain row of commit i-1's node (its drop's row)
   // window commits of the pod's service up to commit i-2, read by the x-checker
   // before it applies commit i-1's (the committer adds commit i-1 itself)
   uint32_t xnsv[2];
@@ -1778,7 +1779,7 @@ struct WinLdsOff2 {
   uint32_t ctl, r_hdr, r_t0, r_rec, r_mod, r_svc;
   uint32_t cm, out, xn, peer, flag, peerset, drop, pub, drw, clist;
   // ServiceAntiAffinity re-rank (dz > 0; see the LDS-slot resolver's WinLdsOff)
-  uint32_t r_fit, r_b, r_mb, r_dc, zm, nsv, dca;
+  uint32_t r_fit, r_b, r_mb, r_dc, zm, nsv, dca, r_kz, ddr;
   uint32_t total;
 };
 
@@ -1810,6 +1811,8 @@ __host__ __device__ inline WinLdsOff2 win2_lds_offsets(uint32_t P, uint32_t nfla
   o.zm = at;      at += win_al16((size_t)dz * P * 64 * 8);
   o.nsv = at;     at += dz ? win_al16((size_t)nsvc * 4) : 0u;
   o.dca = at;     at += dz ? win_al16((size_t)KSG_RES_NCHK * 2 * KSG_RR_MAXZ * 4) : 0u;
+  o.r_kz = at;    at += dz ? win_al16((size_t)R * KSG_RR_MAXZ * 4) : 0u;
+  o.ddr = at;     at += dz ? win_al16((size_t)KSG_RES_NCHK * 2 * KSG_RR_MAXZ * 4) : 0u;
   o.total = at;
   return o;
 }
@@ -1854,6 +1857,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   uint64_t* const L_zm = reinterpret_cast<uint64_t*>(smem + o.zm);      // [dz][P*64] nodes of each row
   uint32_t* const L_nsv = reinterpret_cast<uint32_t*>(smem + o.nsv);    // window commits per service
   int32_t* const L_dca = reinterpret_cast<int32_t*>(smem + o.dca);      // [chk][parity][KSG_RR_MAXZ]
+  int32_t* const r_kz = reinterpret_cast<int32_t*>(smem + o.r_kz);      // [ring][KSG_RR_MAXZ] B nodes per row
+  int32_t* const L_ddr = reinterpret_cast<int32_t*>(smem + o.ddr);      // [chk][parity][KSG_RR_MAXZ] B drops per row
   WinCtl2* ctl = reinterpret_cast<WinCtl2*>(smem + o.ctl);
   RingHdr* r_hdr = reinterpret_cast<RingHdr*>(smem + o.r_hdr);
   uint64_t* r_t0 = reinterpret_cast<uint64_t*>(smem + o.r_t0);
@@ -2041,13 +2046,24 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
 #pragma unroll
       for (int q = 0; q < P; ++q) r_t0[(size_t)e * P * 64 + lane * P + q] = t0[q];
       if constexpr (ANTI) {  // fit at the snapshot, best-per-row nodes, row bests, domain counts
+        uint64_t bw[P];
 #pragma unroll
         for (int q = 0; q < P; ++q) {
           r_fit[(size_t)e * P * 64 + lane * P + q] =
               wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + x.fit_off + j * row_b) : 0ULL;
-          r_b[(size_t)e * P * 64 + lane * P + q] =
-              wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + x.b_off + j * row_b) : 0ULL;
+          bw[q] = wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + x.b_off + j * row_b) : 0ULL;
+          r_b[(size_t)e * P * 64 + lane * P + q] = bw[q];
         }
+        // B nodes per domain row (the committer's re-rank subtracts the drops)
+        int32_t kz = 0;
+        for (uint32_t rw = 0; rw < dz; ++rw) {
+          uint32_t c1 = 0;
+#pragma unroll
+          for (int q = 0; q < P; ++q) c1 += __popcll(bw[q] & L_zm[(size_t)rw * P * 64 + lane * P + q]);
+          const uint32_t tr = wave_total_add(c1);
+          if (lane == rw) kz = (int32_t)tr;
+        }
+        if (lane < dz) r_kz[e * KSG_RR_MAXZ + lane] = kz;
         if (lane < dz) {
           r_mb[e * KSG_RR_MAXZ + lane] = x.dmb[(size_t)j * dz + lane];
           r_dc[e * KSG_RR_MAXZ + lane] =
@@ -2259,6 +2275,12 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
           }
         }
         cntd = __popcll(__ballot(t0d));
+        int32_t ddrop = 0;  // B drops of this lane's row (unlabelled nodes: row dz-1)
+        for (uint64_t dm = __ballot(drop); dm; dm &= dm - 1) {
+          const uint32_t rw = (uint32_t)__builtin_amdgcn_readlane((int)S.row, (int)__builtin_ctzll(dm));
+          if (lane == (rw != ~0u ? rw : dz - 1)) ++ddrop;
+        }
+        if (lane < dz) L_ddr[(c * 2 + par) * KSG_RR_MAXZ + lane] = ddrop;
         int32_t dadd = 0;
         uint64_t pm = __ballot(ks != 0 && S.row != ~0u);
         while (pm) {
@@ -2531,6 +2553,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       }
       uint32_t xst = 0, xrow = ~0u;  // (re-rank) domain-count stop; row of x and its count correction
       int32_t xcorr = 0;
+      uint32_t xrw = 0;              // (re-rank) x's domain row (dz-1: unlabelled)
       // commit i-1 into its slot (the committer's bookkeeping, replayed)
       uint32_t xslot = 0, bnk = 0, bns = 0;
       uint64_t dlc = 0, dlm = 0;
@@ -2590,6 +2613,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
           xd |= __ballot(hit) != 0;
         }
         if constexpr (ANTI) {
+          xrw = xdm >= 0 ? (uint32_t)xdm : dz - 1;
           // x as of commit i-1 and as of i-2 (the checkers' view of it): does the
           // pod still fit it (PodFitsResources, host ports, PDs), and its
           // service's window commits there; the domain count of x's row moves by
@@ -2628,6 +2652,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         if constexpr (ANTI) {
           ctl->xdz[par] = xrow;
           ctl->xdc[par] = xcorr;
+          ctl->xrw[par] = xrw;
           ctl->xnsv[par] = s >= 0 ? L_nsv[s] : 0u;
         }
         ctl->xres[par] = res;
@@ -2836,18 +2861,28 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       const int64_t aa = lane + 1 < dz ? (int64_t)d.w_anti[0] * frac10_f32((int64_t)nn - cz, nn) : 0;
       uint64_t lw[P];
 #pragma unroll
-      for (int q = 0; q < P; ++q) {
-        lw[q] = r_b[(size_t)e * P * 64 + lane * P + q] & ~dww[q];
-        if (have_x && (xres & 1u) && lane * P + q == (xnode >> 6)) lw[q] &= ~(1ULL << (xnode & 63));
-      }
-      uint32_t livez = 0;
-      for (uint32_t r = 0; r < dz; ++r) {
-        uint32_t c1 = 0;
+      for (int q = 0; q < P; ++q) lw[q] = r_b[(size_t)e * P * 64 + lane * P + q] & ~dww[q];
+      // live B nodes per row: the producer's count minus the checkers' drops
+      // minus x if it is a B node the checkers kept and the x-checker dropped
+      bool x_new = false;
+      if (have_x && (xres & 1u)) {
+        const uint32_t xwd = xnode >> 6, xo = xwd / P, xq = xwd % P;
+        uint64_t lx = 0;
 #pragma unroll
-        for (int q = 0; q < P; ++q) c1 += __popcll(lw[q] & L_zm[(size_t)r * P * 64 + lane * P + q]);
-        const uint32_t tr = wave_total_add(c1);
-        if (lane == r) livez = tr;
+        for (int q = 0; q < P; ++q)
+          if ((uint32_t)q == xq) lx = readlane64(lw[q], (int)xo);
+        x_new = (lx >> (xnode & 63)) & 1ULL;
+        if (lane == xo) {
+#pragma unroll
+          for (int q = 0; q < P; ++q)
+            if ((uint32_t)q == xq) lw[q] &= ~(1ULL << (xnode & 63));
+        }
       }
+      const uint32_t xrwv = __builtin_amdgcn_readfirstlane(ctl->xrw[par]);
+      uint32_t livez = 0;
+      if (lane < dz)
+        livez = (uint32_t)(r_kz[e * KSG_RR_MAXZ + lane] - L_ddr[par * KSG_RR_MAXZ + lane] -
+                           L_ddr[(2 + par) * KSG_RR_MAXZ + lane] - ((x_new && lane == xrwv) ? 1 : 0));
       const int32_t val = (lane < dz && mbz != KSG_S32_NONE) ? (int32_t)((int64_t)mbz + aa) : KSG_S32_NONE;
       const int32_t mlive = wave_total_max(livez > 0 ? val : KSG_S32_NONE);
       if (mlive == KSG_S32_NONE || __ballot(lane < dz && livez == 0 && mbz != KSG_S32_NONE && val > mlive)) {
