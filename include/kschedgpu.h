@@ -342,6 +342,62 @@ int ksg_admit_pods(ksg_ctx* ctx, const ksg_admission_set* sets, uint32_t n_sets,
                    uint32_t n_pods, const uint32_t* ids, uint32_t n_ids, const uint32_t* pairs, uint32_t n_pairs,
                    uint8_t* codes);
 
+/* ---- extensions beyond this reference vintage ----
+ * BASELINE.json's configs name node taints / pod tolerations, extended (scalar)
+ * resources and BalancedResourceAllocation. smarterclayton/kubernetes v0.13 has
+ * none of them, so their semantics follow the published later kube-scheduler
+ * (v1.10: algorithm/predicates PodToleratesNodeTaints and PodFitsResources'
+ * ScalarResources, priorities TaintTolerationPriority + NormalizeReduce and
+ * BalancedResourceAllocation) and PARITY IS UNPINNED (no reference to run or
+ * table to check against; the C restatement oracle/ksg_oracle.c is the checker).
+ * Off unless ksg_set_extensions enables them; a context with any extension on
+ * schedules on the exact one-pod-at-a-time kernels (no speculative windows) and
+ * on one rank. The reference's own predicates and priorities are unchanged. */
+#define KSG_EXT_TAINTS (1u << 0) /* PodToleratesNodeTaints: NoSchedule / NoExecute taints */
+#define KSG_EXT_SCALAR (1u << 1) /* extended resources: allocatable >= used + request    */
+#define KSG_FAIL_TAINTS 8        /* fail codes after the reference's seven             */
+#define KSG_FAIL_SCALAR 9
+#define KSG_MAX_SCALAR 4         /* extended resource kinds (e.g. GPU counts)          */
+
+typedef struct ksg_ext_config {
+  uint32_t filters;            /* KSG_EXT_* bitmask                                     */
+  int32_t w_taint_toleration;  /* TaintTolerationPriority weight (0 = off)              */
+  int32_t w_balanced;          /* BalancedResourceAllocation weight (0 = off)           */
+  uint32_t n_scalar;           /* extended resource kinds in use (<= KSG_MAX_SCALAR)    */
+  uint32_t max_taints;         /* interned taint ids are < max_taints                   */
+} ksg_ext_config;
+
+/* Per pod, alongside its ksg_pod. The caller interns each distinct node taint
+ * (key, value, effect) and lists the ones the pod's tolerations do NOT tolerate
+ * (Toleration.ToleratesTaint: effect empty or equal, key empty or equal,
+ * operator Exists or value equal): hard = effect NoSchedule or NoExecute,
+ * soft = effect PreferNoSchedule against the tolerations whose effect is empty
+ * or PreferNoSchedule. Lists are (offset, count) into the call's id array. */
+typedef struct ksg_pod_ext {
+  int64_t scalar[KSG_MAX_SCALAR]; /* extended resource requests (0: not requested)   */
+  uint32_t hard_off, n_hard;
+  uint32_t soft_off, n_soft;
+} ksg_pod_ext;
+
+/* Enable extensions; call before ksg_set_cluster (KSG_ERR_ARG for a sharded
+ * context, weights outside the int32 score bound, n_scalar > KSG_MAX_SCALAR). */
+int ksg_set_extensions(ksg_ctx* ctx, const ksg_ext_config* ext);
+/* Per node, after ksg_set_cluster: scalar_cap[r * n_nodes + n] = allocatable of
+ * resource r (0: none), node n's taint ids taint_ids[taint_off[n], + taint_n[n]).
+ * Resets the extended-resource usage (re-add pods with ksg_add_pod_ext). */
+int ksg_set_node_ext(ksg_ctx* ctx, uint32_t n_nodes, const int64_t* scalar_cap, const uint32_t* taint_off,
+                     const uint32_t* taint_n, const uint32_t* taint_ids, uint32_t n_taint_ids);
+/* The pod-taking entry points with each pod's extension record (ext[i] goes
+ * with pods[i]); the plain forms use an all-zero record. */
+int ksg_add_pod_ext(ksg_ctx* ctx, uint32_t host_id, const ksg_pod* pod, const ksg_pod_ext* ext,
+                    const uint32_t* ids);
+int ksg_schedule_batch_ext(ksg_ctx* ctx, const ksg_pod* pods, const ksg_pod_ext* ext, uint32_t n,
+                           const uint32_t* ids, uint32_t n_ids, uint64_t* rng_state, int32_t* out_nodes);
+int ksg_schedule_begin_ext(ksg_ctx* ctx, const ksg_pod* pod, const ksg_pod_ext* ext, const uint32_t* ids,
+                           int64_t* max_score, uint32_t* tie_count, uint8_t* fail_codes);
+int ksg_evaluate_ext(ksg_ctx* ctx, const ksg_pod* pod, const ksg_pod_ext* ext, const uint32_t* ids,
+                     uint8_t* fail_out, int64_t* score_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -43,6 +43,12 @@ FAIL_NODISKCONFLICT = 4
 FAIL_PODFITSPORTS = 5
 FAIL_PODFITSRESOURCES = 6
 FAIL_SERVICEAFFINITY = 7
+# extensions beyond this reference vintage (include/kschedgpu.h; parity unpinned)
+EXT_TAINTS = 1 << 0
+EXT_SCALAR = 1 << 1
+FAIL_TAINTS = 8
+FAIL_SCALAR = 9
+MAX_SCALAR = 4
 
 MAX_ANTI = 4
 MAX_LABEL_PREF = 8
@@ -114,6 +120,11 @@ class KsgPod(C.Structure):
     ]
 
 
+class KsgExtConfig(C.Structure):
+    _fields_ = [("filters", U32), ("w_taint_toleration", I32), ("w_balanced", I32), ("n_scalar", U32),
+                ("max_taints", U32)]
+
+
 class KsgAdmissionSet(C.Structure):
     _fields_ = [("cap_milli_cpu", I64), ("cap_memory", I64), ("pod_off", U32), ("n_pods", U32),
                 ("label_off", U32), ("n_labels", U32)]
@@ -155,6 +166,10 @@ POD_DTYPE = np.dtype(
 ADMISSION_SET_DTYPE = np.dtype(
     [("cap_milli_cpu", "<i8"), ("cap_memory", "<i8"), ("pod_off", "<u4"), ("n_pods", "<u4"),
      ("label_off", "<u4"), ("n_labels", "<u4")], align=True)
+POD_EXT_DTYPE = np.dtype(
+    [("scalar", "<i8", (MAX_SCALAR,)), ("hard_off", "<u4"), ("n_hard", "<u4"), ("soft_off", "<u4"),
+     ("n_soft", "<u4")], align=True)
+assert POD_EXT_DTYPE.itemsize == 48
 assert ADMISSION_SET_DTYPE.itemsize == C.sizeof(KsgAdmissionSet)
 assert NODE_DTYPE.itemsize == C.sizeof(KsgNode)
 assert POD_DTYPE.itemsize == C.sizeof(KsgPod)
@@ -186,6 +201,12 @@ EXPORTS = [
     "ksg_check_pods_exceeding_capacity",
     "ksg_pod_matches_node_labels",
     "ksg_admit_pods",
+    "ksg_set_extensions",
+    "ksg_set_node_ext",
+    "ksg_add_pod_ext",
+    "ksg_schedule_batch_ext",
+    "ksg_schedule_begin_ext",
+    "ksg_evaluate_ext",
 ]
 
 # int (*ksg_allgather_fn)(void* user, const void* send, void* recv, uint64_t bytes)
@@ -242,6 +263,12 @@ def load_library() -> C.CDLL:
         "ksg_check_pods_exceeding_capacity": (C.c_int, [vp, vp, U32, vp, U32, vp]),
         "ksg_pod_matches_node_labels": (C.c_int, [vp, vp, U32, vp, U32, vp, U32, vp, U32, vp]),
         "ksg_admit_pods": (C.c_int, [vp, vp, U32, vp, U32, vp, U32, vp, U32, vp]),
+        "ksg_set_extensions": (C.c_int, [vp, P(KsgExtConfig)]),
+        "ksg_set_node_ext": (C.c_int, [vp, U32, vp, vp, vp, vp, U32]),
+        "ksg_add_pod_ext": (C.c_int, [vp, U32, vp, vp, vp]),
+        "ksg_schedule_batch_ext": (C.c_int, [vp, vp, vp, U32, vp, U32, P(U64), vp]),
+        "ksg_schedule_begin_ext": (C.c_int, [vp, vp, vp, vp, P(I64), P(U32), vp]),
+        "ksg_evaluate_ext": (C.c_int, [vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)

@@ -228,6 +228,8 @@ struct PodCtx {
   const uint32_t* pds;
   const uint32_t* sel;
   int32_t req_aff[KSG_MAX_AFF];
+  const ksg_pod_ext* ext;  // extensions (nullptr: none); its taint lists index ids
+  const uint32_t* ids;
 };
 
 // SelectorFromSet's trap per ServiceAffinity predicate (predicates.go:311-315,
@@ -266,6 +268,8 @@ __device__ __forceinline__ void pod_resolve(const KsgDev& d, const ksg_pod& p, c
   c.error = 0;
   c.spread_max = 0;
   c.svc_total = 0;
+  c.ext = nullptr;
+  c.ids = ids;
   int32_t peer = -1;
   if (c.svc >= 0) {
     c.spread_max = ld_st<COH>(d.svc_max + c.svc);
@@ -334,7 +338,45 @@ __device__ __forceinline__ int node_fail_l(const KsgDev& d, const PodCtx& c, con
       if (j < d.n_aff && c.req_aff[j] >= 0 && !(d.pairmap[(size_t)c.req_aff[j] * d.nw + wi] & bit))
         return KSG_FAIL_SERVICEAFFINITY;
   }
+  if (d.ext_filters && c.ext) {  // extensions (include/kschedgpu.h; parity unpinned)
+    if (d.ext_filters & KSG_EXT_TAINTS)  // PodToleratesNodeTaints: an untolerated NoSchedule/NoExecute taint
+      for (uint32_t i = 0; i < c.ext->n_hard; ++i)
+        if (d.taintmap[(size_t)c.ids[c.ext->hard_off + i] * d.nw + wi] & bit) return KSG_FAIL_TAINTS;
+    if (d.ext_filters & KSG_EXT_SCALAR)  // PodFitsResources' ScalarResources: allocatable < used + request
+      for (uint32_t r = 0; r < d.n_scalar; ++r) {
+        const int64_t req = c.ext->scalar[r];
+        if (req > 0) {
+          const int64_t cap = d.scalar_cap[(size_t)r * d.n_nodes + n];
+          const int64_t used = ld_st<COH>(d.scalar_used + (size_t)r * d.n_nodes + n);
+          if (cap < (int64_t)((uint64_t)used + (uint64_t)req)) return KSG_FAIL_SCALAR;
+        }
+      }
+  }
   return KSG_FAIL_NONE;
+}
+
+// BalancedResourceAllocation (kube-scheduler v1.10 balanced_resource_allocation.go,
+// not in this reference; parity unpinned) over the same requested totals as
+// LeastRequested, float64 op for op: fraction = requested / capacity (1 when
+// capacity is 0); 0 if either fraction >= 1, else int((1 - |fc - fm|) * 10).
+__device__ __forceinline__ int64_t balanced_score(int64_t tc, int64_t capc, int64_t tm, int64_t capm) {
+  const double fc = capc == 0 ? 1.0 : __ddiv_rn((double)tc, (double)capc);
+  const double fm = capm == 0 ? 1.0 : __ddiv_rn((double)tm, (double)capm);
+  if (fc >= 1.0 || fm >= 1.0) return 0;
+  return (int64_t)__dmul_rn(__dsub_rn(1.0, fabs(__dsub_rn(fc, fm))), 10.0);
+}
+
+// TaintTolerationPriority's map (v1.10 taint_toleration.go): the node's
+// PreferNoSchedule taints the pod does not tolerate
+__device__ __forceinline__ int32_t soft_taints(const KsgDev& d, const PodCtx& c, uint32_t wi, uint64_t bit) {
+  int32_t k = 0;
+  for (uint32_t i = 0; i < c.ext->n_soft; ++i) k += (d.taintmap[(size_t)c.ids[c.ext->soft_off + i] * d.nw + wi] & bit) != 0;
+  return k;
+}
+// ... and its reduce, NormalizeReduce(10, reverse=true): 10 - 10 * count / max
+// over the filtered nodes (every node 10 when the max is 0)
+__device__ __forceinline__ int64_t taint_score(int32_t cnt, int32_t mx) {
+  return mx == 0 ? 10 : 10 - (10 * (int64_t)cnt) / mx;
 }
 
 struct PtrLists {
@@ -370,6 +412,11 @@ __device__ __forceinline__ int64_t node_score(const KsgDev& d, const PodCtx& c, 
     const int64_t sc = c.spread_max > 0 ? frac10_f32((int64_t)c.spread_max - cnt, c.spread_max) : 10;
     s += (int64_t)d.w_spread * sc;
   }
+  if (d.w_bal) {  // extension: BalancedResourceAllocation
+    const int64_t tc = (int64_t)((uint64_t)usedc + (uint64_t)c.req_cpu);
+    const int64_t tm = (int64_t)((uint64_t)usedm + (uint64_t)c.req_mem);
+    s += (int64_t)d.w_bal * balanced_score(tc, capc, tm, capm);
+  }
   return s;
 }
 
@@ -394,7 +441,7 @@ __device__ __forceinline__ int64_t anti_term(const KsgDev& d, const PodCtx& c, u
 // atomic (no return except the per-service count), so the commit costs one
 // memory round trip instead of a serial chain. Caller drains with vmcnt(0).
 __device__ __forceinline__ void commit_pod_wave(const KsgDev& d, const ksg_pod& p, const uint32_t* ids,
-                                                uint32_t w, uint32_t lane) {
+                                                uint32_t w, uint32_t lane, const ksg_pod_ext* ext = nullptr) {
   const uint32_t nk = p.n_ports + p.n_pds;
   if (lane == 0) {
     __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(d.used_cpu + w), (uint64_t)p.milli_cpu,
@@ -402,6 +449,9 @@ __device__ __forceinline__ void commit_pod_wave(const KsgDev& d, const ksg_pod& 
   } else if (lane == 1) {
     __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(d.used_mem + w), (uint64_t)p.memory,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (ext && lane - 2 < d.n_scalar && ext->scalar[lane - 2]) {  // extended resources
+    __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(d.scalar_used + (size_t)(lane - 2) * d.n_nodes + w),
+                           (uint64_t)ext->scalar[lane - 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const uint64_t bit = 1ULL << (w & 63);
   const size_t wi = w >> 6;

@@ -82,6 +82,13 @@ struct KsgDev {
   const int32_t* anti_domain;
   const int32_t* aff_pair;
   int32_t* score_scratch;     // exact kernels with R > KSG_R_LDS: per-node scores in HBM, not LDS
+  // extensions beyond the reference (ksg_set_extensions; exact kernels only, parity unpinned)
+  uint32_t ext_filters;       // KSG_EXT_*
+  int32_t w_taint, w_bal;     // TaintTolerationPriority, BalancedResourceAllocation weights
+  uint32_t n_scalar;          // extended resource kinds
+  const int64_t* scalar_cap;  // [n_scalar][N] allocatable
+  int64_t* scalar_used;       // [n_scalar][N] requested by the pods on the node (mutable)
+  const uint64_t* taintmap;   // [max_taints][nw] nodes carrying taint t
 };
 
 // static-table configuration (LabelsPresence, EqualPriority, LabelPreference,

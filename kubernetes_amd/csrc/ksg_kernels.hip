@@ -40,8 +40,13 @@ __device__ __forceinline__ int32_t scan_pod(const KsgDev& d, const PodCtx& c, ui
                                             uint64_t bit, int32_t* s_score, int32_t* s_dcount,
                                             const int32_t* dglobal, const int64_t* rcapc, const int64_t* rcapm,
                                             const int64_t* rusedc, const int64_t* rusedm,
-                                            uint8_t* fail_out) {
+                                            uint8_t* fail_out, int32_t* s_tmax = nullptr) {
   const bool need_cnt = (d.w_spread != 0 || ANTI) && c.svc >= 0;
+  // extension TaintTolerationPriority: normalised by the max over the filtered
+  // nodes, so it is added in a second pass like the anti-affinity term
+  // (s_tmax: zeroed by the caller before the barrier that precedes this scan)
+  const bool tt = d.w_taint != 0 && c.ext != nullptr && s_tmax != nullptr && !d.equal_fallback;
+  int32_t tmax = 0;
   int32_t m = KSG_S32_NONE;
   // register-cached node state needs compile-time j; otherwise keep the loop rolled
 #pragma unroll REG ? R : 1
@@ -62,6 +67,7 @@ __device__ __forceinline__ int32_t scan_pod(const KsgDev& d, const PodCtx& c, ui
       if (fail_out) fail_out[n - d.lo] = (uint8_t)f;
       if (f == KSG_FAIL_NONE) {
         sc = (int32_t)node_score(d, c, n, capc, capm, usedc, usedm, cnt);
+        if (tt) tmax = max(tmax, soft_taints(d, c, wi, bit));
         if (ANTI && s_dcount && cnt != 0) {
           for (uint32_t a = 0; a < d.n_anti; ++a) {
             const int32_t dom = d.anti_domain[(size_t)a * d.n_nodes + n];
@@ -71,16 +77,25 @@ __device__ __forceinline__ int32_t scan_pod(const KsgDev& d, const PodCtx& c, ui
       }
     }
     s_score[j * KSG_NT + tid] = sc;
-    if (!ANTI) m = sc > m ? sc : m;
+    if (!ANTI && !tt) m = sc > m ? sc : m;
   }
-  if (ANTI) {
+  if (ANTI || tt) {
+    if (tt) {
+      tmax = wave_max_i32(tmax);
+      if ((tid & 63) == 0) atomicMax(s_tmax, tmax);
+    }
     __syncthreads();
     const int32_t* dc = dglobal ? dglobal : s_dcount;
+    const int32_t tm = tt ? *s_tmax : 0;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       int32_t v = s_score[j * KSG_NT + tid];
       if (v != KSG_S32_NONE && !d.equal_fallback) {
-        v += (int32_t)anti_term(d, c, d.lo + j * KSG_NT + tid, dc);
+        if (ANTI) v += (int32_t)anti_term(d, c, d.lo + j * KSG_NT + tid, dc);
+        if (tt) {
+          const uint32_t wi = (d.lo >> 6) + j * KSG_NWAVE + wave;
+          v += (int32_t)((int64_t)d.w_taint * taint_score(soft_taints(d, c, wi, bit), tm));
+        }
         s_score[j * KSG_NT + tid] = v;
       }
       m = v > m ? v : m;
@@ -142,12 +157,14 @@ template <int R, bool ANTI, bool REG>
 __global__ __launch_bounds__(KSG_NT) void ksg_batch_kernel(KsgDev d, const ksg_pod* __restrict__ pods,
                                                           const uint32_t* __restrict__ ids,
                                                           uint32_t n_pods, uint64_t* rng_io,
-                                                          int32_t* __restrict__ out) {
+                                                          int32_t* __restrict__ out,
+                                                          const ksg_pod_ext* __restrict__ exts) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // per-node scores: LDS up to KSG_R_LDS nodes per thread, else HBM scratch
   // (each thread only ever reads back its own entries)
   int32_t* s_score = R > KSG_R_LDS ? d.score_scratch : reinterpret_cast<int32_t*>(smem);
   int32_t* s_dcount = R > KSG_R_LDS ? reinterpret_cast<int32_t*>(smem) : s_score + R * KSG_NT;
+  int32_t* s_tmax = s_dcount + d.n_domains_total;  // (extension TaintTolerationPriority's max)
   __shared__ uint64_t s_tie[R * KSG_NWAVE];
   __shared__ int32_t s_wmax[KSG_NWAVE];
   __shared__ uint32_t s_wcnt[KSG_NWAVE];
@@ -176,16 +193,18 @@ __global__ __launch_bounds__(KSG_NT) void ksg_batch_kernel(KsgDev d, const ksg_p
     const ksg_pod& p = pods[i];
     PodCtx c;
     pod_resolve(d, p, ids, c);
+    if (exts) c.ext = exts + i;
     if (c.error) {
       if (tid == 0) out[i] = KSG_OUT_ERROR;
       continue;  // uniform; no LDS touched for this pod
     }
-    if (ANTI) {
+    if (ANTI || exts) {
       for (uint32_t k = tid; k < d.n_domains_total; k += KSG_NT) s_dcount[k] = 0;
+      if (tid == 0) *s_tmax = 0;
       __syncthreads();
     }
     const int32_t m = scan_pod<R, ANTI, REG>(d, c, tid, wave, bit, s_score, s_dcount, nullptr, rcapc, rcapm,
-                                             rusedc, rusedm, nullptr);
+                                             rusedc, rusedm, nullptr, exts ? s_tmax : nullptr);
     int32_t M;
     uint64_t k;
     reduce_ties<R>(d, m, tid, lane, wave, s_score, s_wmax, s_wcnt, s_tie, M, k);
@@ -198,7 +217,7 @@ __global__ __launch_bounds__(KSG_NT) void ksg_batch_kernel(KsgDev d, const ksg_p
     const uint64_t target = k - 1 - (r % k);           // ix-th host in descending name order
     if (wave == 0) {
       const int32_t win = select_tie(s_tie, R * KSG_NWAVE, target, lane, d.lo);
-      commit_pod_wave(d, p, ids, (uint32_t)win, lane);
+      commit_pod_wave(d, p, ids, (uint32_t)win, lane, exts ? exts + i : nullptr);
       if (lane == 0) {
         s_winner = win;
         out[i] = win;
@@ -235,12 +254,14 @@ __global__ __launch_bounds__(KSG_NT) void ksg_scan_kernel(KsgDev d, const ksg_po
                                                          int64_t* __restrict__ score_out,
                                                          uint8_t* __restrict__ record,
                                                          int32_t* __restrict__ dpart,
-                                                         const int32_t* __restrict__ dglobal) {
+                                                         const int32_t* __restrict__ dglobal,
+                                                         const ksg_pod_ext* __restrict__ ext) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // per-node scores: LDS up to KSG_R_LDS nodes per thread, else HBM scratch
   // (each thread only ever reads back its own entries)
   int32_t* s_score = R > KSG_R_LDS ? d.score_scratch : reinterpret_cast<int32_t*>(smem);
   int32_t* s_dcount = R > KSG_R_LDS ? reinterpret_cast<int32_t*>(smem) : s_score + R * KSG_NT;
+  int32_t* s_tmax = s_dcount + d.n_domains_total;  // (extension TaintTolerationPriority's max)
   __shared__ uint64_t s_tie[R * KSG_NWAVE];
   __shared__ int32_t s_wmax[KSG_NWAVE];
   __shared__ uint32_t s_wcnt[KSG_NWAVE];
@@ -252,6 +273,7 @@ __global__ __launch_bounds__(KSG_NT) void ksg_scan_kernel(KsgDev d, const ksg_po
   const ksg_pod& p = pods[0];
   PodCtx c;
   pod_resolve(d, p, ids, c);
+  c.ext = ext;
   KsgRecordHdr* hdr = reinterpret_cast<KsgRecordHdr*>(record);
   uint64_t* words = reinterpret_cast<uint64_t*>(record + sizeof(KsgRecordHdr));
   if (c.error) {
@@ -265,8 +287,10 @@ __global__ __launch_bounds__(KSG_NT) void ksg_scan_kernel(KsgDev d, const ksg_po
     return;
   }
   const bool lds_dcount = ANTI && phase != 2;
-  if (lds_dcount) {
-    for (uint32_t k = tid; k < d.n_domains_total; k += KSG_NT) s_dcount[k] = 0;
+  if (lds_dcount || ext) {
+    if (lds_dcount)
+      for (uint32_t k = tid; k < d.n_domains_total; k += KSG_NT) s_dcount[k] = 0;
+    if (tid == 0) *s_tmax = 0;
     __syncthreads();
   }
   if (ANTI && phase == 1) {
@@ -292,7 +316,7 @@ __global__ __launch_bounds__(KSG_NT) void ksg_scan_kernel(KsgDev d, const ksg_po
   }
   const int32_t m = scan_pod<R, ANTI, false>(d, c, tid, wave, bit, s_score, lds_dcount ? s_dcount : nullptr,
                                              phase == 2 ? dglobal : nullptr, nullptr, nullptr, nullptr, nullptr,
-                                             fail_out);
+                                             fail_out, ext ? s_tmax : nullptr);
   if (mode == KSG_MODE_EVAL) {
 #pragma unroll
     for (int j = 0; j < R; ++j) {
@@ -327,7 +351,8 @@ __global__ __launch_bounds__(64) void ksg_decide_kernel(KsgDev d, const ksg_pod*
                                                        const uint32_t* __restrict__ shard_wlo,
                                                        int mode, uint64_t tie_index,
                                                        uint64_t* rng_io, int32_t* out,
-                                                       uint32_t out_idx, int64_t* summary) {
+                                                       uint32_t out_idx, int64_t* summary,
+                                                       const ksg_pod_ext* ext) {
   const uint32_t lane = threadIdx.x;
   const KsgMerged mg = ksg_merge_summary(records, rec_bytes, world, d.empty_priorities);
   const int64_t M = mg.max_score;
@@ -371,7 +396,7 @@ __global__ __launch_bounds__(64) void ksg_decide_kernel(KsgDev d, const ksg_pod*
     if (lane == 0) out[out_idx] = KSG_OUT_ERROR;
     return;
   }
-  commit_pod_wave(d, pods[0], ids, (uint32_t)win, lane);
+  commit_pod_wave(d, pods[0], ids, (uint32_t)win, lane, ext);
   if (lane == 0) out[out_idx] = win;
 }
 
@@ -480,7 +505,8 @@ __global__ void ksg_patch_kernel(const KsgPatch* __restrict__ patches, uint32_t 
 // ---- launch wrappers (called from ksg_runtime.cpp) ------------------------
 // dynamic LDS = R*1024 int32 scores + the anti-affinity domain counts
 static size_t lds_bytes(int R, const KsgDev& d) {
-  return (R > KSG_R_LDS ? 0 : (size_t)R * KSG_NT * sizeof(int32_t)) + (size_t)d.n_domains_total * sizeof(int32_t);
+  return (R > KSG_R_LDS ? 0 : (size_t)R * KSG_NT * sizeof(int32_t)) + (size_t)d.n_domains_total * sizeof(int32_t) +
+         16;  // + TaintTolerationPriority's max (extension)
 }
 
 template <typename K>
@@ -492,26 +518,26 @@ static void allow_big_lds(K kernel) {
 
 template <int R, bool ANTI, bool REG>
 static hipError_t launch_batch_t(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids, uint32_t n,
-                                 uint64_t* rng, int32_t* out, hipStream_t st) {
+                                 uint64_t* rng, int32_t* out, const ksg_pod_ext* ext, hipStream_t st) {
   static bool once = (allow_big_lds(ksg_batch_kernel<R, ANTI, REG>), true);
   (void)once;
   hipLaunchKernelGGL((ksg_batch_kernel<R, ANTI, REG>), dim3(1), dim3(KSG_NT), lds_bytes(R, d), st, d, pods, ids,
-                     n, rng, out);
+                     n, rng, out, ext);
   return hipGetLastError();
 }
 
 template <bool ANTI>
 static hipError_t launch_batch_a(int R, const KsgDev& d, const ksg_pod* pods, const uint32_t* ids, uint32_t n,
-                                 uint64_t* rng, int32_t* out, hipStream_t st) {
+                                 uint64_t* rng, int32_t* out, const ksg_pod_ext* ext, hipStream_t st) {
   switch (R) {
-    case 1: return launch_batch_t<1, ANTI, true>(d, pods, ids, n, rng, out, st);
-    case 2: return launch_batch_t<2, ANTI, true>(d, pods, ids, n, rng, out, st);
-    case 4: return launch_batch_t<4, ANTI, true>(d, pods, ids, n, rng, out, st);
-    case 8: return launch_batch_t<8, ANTI, false>(d, pods, ids, n, rng, out, st);
-    case 16: return launch_batch_t<16, ANTI, false>(d, pods, ids, n, rng, out, st);
-    case 32: return launch_batch_t<32, ANTI, false>(d, pods, ids, n, rng, out, st);
-    case 64: return launch_batch_t<64, ANTI, false>(d, pods, ids, n, rng, out, st);
-    case 128: return launch_batch_t<128, ANTI, false>(d, pods, ids, n, rng, out, st);
+    case 1: return launch_batch_t<1, ANTI, true>(d, pods, ids, n, rng, out, ext, st);
+    case 2: return launch_batch_t<2, ANTI, true>(d, pods, ids, n, rng, out, ext, st);
+    case 4: return launch_batch_t<4, ANTI, true>(d, pods, ids, n, rng, out, ext, st);
+    case 8: return launch_batch_t<8, ANTI, false>(d, pods, ids, n, rng, out, ext, st);
+    case 16: return launch_batch_t<16, ANTI, false>(d, pods, ids, n, rng, out, ext, st);
+    case 32: return launch_batch_t<32, ANTI, false>(d, pods, ids, n, rng, out, ext, st);
+    case 64: return launch_batch_t<64, ANTI, false>(d, pods, ids, n, rng, out, ext, st);
+    case 128: return launch_batch_t<128, ANTI, false>(d, pods, ids, n, rng, out, ext, st);
   }
   return hipErrorInvalidValue;
 }
@@ -519,51 +545,52 @@ static hipError_t launch_batch_a(int R, const KsgDev& d, const ksg_pod* pods, co
 template <int R, bool ANTI>
 static hipError_t launch_scan_t(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids, int mode, int phase,
                                 uint8_t* fail_out, int64_t* score_out, uint8_t* record, int32_t* dpart,
-                                const int32_t* dglobal, hipStream_t st) {
+                                const int32_t* dglobal, const ksg_pod_ext* ext, hipStream_t st) {
   static bool once = (allow_big_lds(ksg_scan_kernel<R, ANTI>), true);
   (void)once;
   hipLaunchKernelGGL((ksg_scan_kernel<R, ANTI>), dim3(1), dim3(KSG_NT), lds_bytes(R, d), st, d, pods, ids, mode,
-                     phase, fail_out, score_out, record, dpart, dglobal);
+                     phase, fail_out, score_out, record, dpart, dglobal, ext);
   return hipGetLastError();
 }
 
 template <bool ANTI>
 static hipError_t launch_scan_a(int R, const KsgDev& d, const ksg_pod* pods, const uint32_t* ids, int mode,
                                 int phase, uint8_t* fail_out, int64_t* score_out, uint8_t* record, int32_t* dpart,
-                                const int32_t* dglobal, hipStream_t st) {
+                                const int32_t* dglobal, const ksg_pod_ext* ext, hipStream_t st) {
   switch (R) {
-    case 1: return launch_scan_t<1, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, st);
-    case 2: return launch_scan_t<2, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, st);
-    case 4: return launch_scan_t<4, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, st);
-    case 8: return launch_scan_t<8, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, st);
-    case 16: return launch_scan_t<16, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, st);
-    case 32: return launch_scan_t<32, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, st);
-    case 64: return launch_scan_t<64, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, st);
-    case 128: return launch_scan_t<128, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, st);
+    case 1: return launch_scan_t<1, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, ext, st);
+    case 2: return launch_scan_t<2, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, ext, st);
+    case 4: return launch_scan_t<4, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, ext, st);
+    case 8: return launch_scan_t<8, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, ext, st);
+    case 16: return launch_scan_t<16, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, ext, st);
+    case 32: return launch_scan_t<32, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, ext, st);
+    case 64: return launch_scan_t<64, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, ext, st);
+    case 128: return launch_scan_t<128, ANTI>(d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, ext, st);
   }
   return hipErrorInvalidValue;
 }
 
 hipError_t ksg_launch_batch(int R, bool anti, const KsgDev& d, const ksg_pod* pods, const uint32_t* ids,
-                            uint32_t n, uint64_t* rng, int32_t* out, hipStream_t st) {
-  return anti ? launch_batch_a<true>(R, d, pods, ids, n, rng, out, st)
-              : launch_batch_a<false>(R, d, pods, ids, n, rng, out, st);
+                            uint32_t n, uint64_t* rng, int32_t* out, hipStream_t st, const ksg_pod_ext* ext) {
+  return anti ? launch_batch_a<true>(R, d, pods, ids, n, rng, out, ext, st)
+              : launch_batch_a<false>(R, d, pods, ids, n, rng, out, ext, st);
 }
 
 hipError_t ksg_launch_scan(int R, bool anti, const KsgDev& d, const ksg_pod* pods, const uint32_t* ids, int mode,
                            int phase, uint8_t* fail_out, int64_t* score_out, uint8_t* record, int32_t* dpart,
-                           const int32_t* dglobal, hipStream_t st) {
-  return anti ? launch_scan_a<true>(R, d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, st)
-              : launch_scan_a<false>(R, d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, st);
+                           const int32_t* dglobal, hipStream_t st, const ksg_pod_ext* ext) {
+  return anti ? launch_scan_a<true>(R, d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, ext, st)
+              : launch_scan_a<false>(R, d, pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, ext,
+                                     st);
 }
 
 hipError_t ksg_launch_decide(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids,
                              const uint8_t* records, uint32_t rec_bytes, uint32_t world,
                              const uint32_t* shard_wlo, int mode, uint64_t tie_index,
                              uint64_t* rng, int32_t* out, uint32_t out_idx, int64_t* summary,
-                             hipStream_t st) {
+                             hipStream_t st, const ksg_pod_ext* ext) {
   hipLaunchKernelGGL(ksg_decide_kernel, dim3(1), dim3(64), 0, st, d, pods, ids, records, rec_bytes,
-                     world, shard_wlo, mode, tie_index, rng, out, out_idx, summary);
+                     world, shard_wlo, mode, tie_index, rng, out, out_idx, summary, ext);
   return hipGetLastError();
 }
 

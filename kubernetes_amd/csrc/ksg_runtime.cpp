@@ -16,6 +16,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -33,11 +34,11 @@
 
 hipError_t ksg_launch_batch(int R, bool anti, const KsgDev& d, const ksg_pod* pods,
                             const uint32_t* ids, uint32_t n, uint64_t* rng, int32_t* out,
-                            hipStream_t st);
+                            hipStream_t st, const ksg_pod_ext* ext = nullptr);
 hipError_t ksg_launch_scan(int R, bool anti, const KsgDev& d, const ksg_pod* pods,
                            const uint32_t* ids, int mode, int phase, uint8_t* fail_out,
                            int64_t* score_out, uint8_t* record, int32_t* dpart,
-                           const int32_t* dglobal, hipStream_t st);
+                           const int32_t* dglobal, hipStream_t st, const ksg_pod_ext* ext = nullptr);
 hipError_t ksg_launch_win_eval(const KsgDev& d, int mode, const ksg_pod* batch, const uint32_t* ids,
                                const KsgWinRun* run, uint32_t wcap, KsgWinSum* sums, uint64_t* wbits, int32_t* wmax,
                                uint32_t ostride, int32_t* dcnt, uint64_t* wfit, int32_t* dmb, uint64_t* wbz,
@@ -51,7 +52,7 @@ hipError_t ksg_launch_decide(const KsgDev& d, const ksg_pod* pods, const uint32_
                              const uint8_t* records, uint32_t rec_bytes, uint32_t world,
                              const uint32_t* shard_wlo, int mode, uint64_t tie_index,
                              uint64_t* rng, int32_t* out, uint32_t out_idx, int64_t* summary,
-                             hipStream_t st);
+                             hipStream_t st, const ksg_pod_ext* ext = nullptr);
 hipError_t ksg_launch_static(const KsgStaticCfg& sc, uint32_t n_nodes, const ksg_node* nodes,
                              const uint32_t* node_pairs, const uint32_t* pair_keys,
                              const int32_t* dom_of_pair, uint32_t n_pairs, uint32_t nw,
@@ -66,6 +67,7 @@ namespace {
 struct PodRec {
   uint32_t host;
   int64_t cpu, mem;
+  int64_t scalar[KSG_MAX_SCALAR];  // extension: extended resource requests
   std::vector<uint32_t> keys;  // ports + PDs
   std::vector<uint32_t> svcs;
   uint64_t seq;
@@ -174,6 +176,16 @@ struct ksg_ctx {
   std::unordered_set<uint64_t> dfr_uids;
   int64_t dfr_sum = 0;   // sum of the deferred pods' requests (cpu + memory), capped
   bool dfr_neg = false;  // a deferred pod has a negative request
+
+  // extensions (ksg_set_extensions; exact kernels, one rank, parity unpinned)
+  bool ext_on = false;
+  ksg_ext_config ext{};
+  std::vector<int64_t> sc_used;  // [n_scalar][N] host mirror of scalar_used
+  std::unordered_map<uint64_t, std::array<int64_t, KSG_MAX_SCALAR>> ext_scalar;  // uid -> requests
+  const ksg_pod_ext* cur_ext = nullptr;  // the _ext entry point's records for this call
+  ksg_pod_ext* d_pext = nullptr;         // device copy (batch) / the single pod's (d_one_ext)
+  size_t pext_cap = 0;
+  ksg_pod_ext* d_one_ext = nullptr;
 
   // begin/commit
   bool pending = false;
@@ -318,6 +330,19 @@ int mirror_add(ksg_ctx* c, uint32_t h, const ksg_pod* p, const uint32_t* ids, bo
       return fail(c, KSG_ERR_CAPACITY, "conflict key %u >= max_conflict_keys %u", k, c->cfg.max_conflict_keys);
   for (uint32_t s : r.svcs)
     if (s >= c->S) return fail(c, KSG_ERR_ARG, "service %u >= n_services %u", s, c->S);
+  for (uint32_t q = 0; q < KSG_MAX_SCALAR; ++q) r.scalar[q] = 0;
+  if (c->ext_on && c->ext.n_scalar) {  // extension: the pod's extended resource requests
+    auto it = c->ext_scalar.find(p->uid);
+    if (it != c->ext_scalar.end())
+      for (uint32_t q = 0; q < c->ext.n_scalar; ++q) r.scalar[q] = it->second[q];
+    if (h < c->N)
+      for (uint32_t q = 0; q < c->ext.n_scalar; ++q) {
+        if (!r.scalar[q]) continue;
+        int64_t& u = c->sc_used[(size_t)q * c->N + h];
+        u = (int64_t)((uint64_t)u + (uint64_t)r.scalar[q]);
+        if (emit) patch64(c, c->dev.scalar_used + (size_t)q * c->N + h, u);
+      }
+  }
   if (h < c->N) {
     c->used_c[h] = (int64_t)((uint64_t)c->used_c[h] + (uint64_t)r.cpu);
     c->used_m[h] = (int64_t)((uint64_t)c->used_m[h] + (uint64_t)r.mem);
@@ -358,6 +383,8 @@ int mirror_add(ksg_ctx* c, uint32_t h, const ksg_pod* p, const uint32_t* ids, bo
 void reset_mirror(ksg_ctx* c) {
   c->used_c.assign(c->N, 0);
   c->used_m.assign(c->N, 0);
+  c->sc_used.assign((size_t)c->ext.n_scalar * c->N, 0);
+  c->ext_scalar.clear();
   c->key_ref.clear();
   c->svc_cnt.assign((size_t)c->S * c->N, 0);
   c->svc_ext.assign(c->S, {});
@@ -418,15 +445,22 @@ int upload_pods(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32_t* ids
 // one_pod / one_ids point into it until the next single-pod upload
 int upload_one(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, size_t n_ids) {
   const size_t pb = (sizeof(ksg_pod) + 15) & ~(size_t)15, ib = std::max<size_t>(n_ids, 1) * sizeof(uint32_t);
-  int rc = grow(c, (void**)&c->d_one, &c->one_cap, pb + ib, 1);
+  // (extensions: the pod's ksg_pod_ext after the ids, all-zero for the plain entry points)
+  const size_t eo = (pb + ib + 15) & ~(size_t)15, eb = c->ext_on ? sizeof(ksg_pod_ext) : 0;
+  int rc = grow(c, (void**)&c->d_one, &c->one_cap, eo + eb, 1);
   if (rc) return rc;
-  if ((rc = grow_host(c, &c->h_up, &c->h_up_cap, pb + ib))) return rc;
+  if ((rc = grow_host(c, &c->h_up, &c->h_up_cap, eo + eb))) return rc;
   memcpy(c->h_up, pod, sizeof(ksg_pod));
   if (n_ids) memcpy(c->h_up + pb, ids, n_ids * sizeof(uint32_t));
-  HIPCHK(c, hipMemcpyAsync(c->d_one, c->h_up, pb + (n_ids ? n_ids * sizeof(uint32_t) : 0), hipMemcpyHostToDevice,
-                           c->st));
+  if (eb) {
+    if (c->cur_ext) memcpy(c->h_up + eo, c->cur_ext, eb);
+    else memset(c->h_up + eo, 0, eb);
+  }
+  HIPCHK(c, hipMemcpyAsync(c->d_one, c->h_up, eb ? eo + eb : pb + (n_ids ? n_ids * sizeof(uint32_t) : 0),
+                           hipMemcpyHostToDevice, c->st));
   c->one_pod = reinterpret_cast<const ksg_pod*>(c->d_one);
   c->one_ids = reinterpret_cast<const uint32_t*>(c->d_one + pb);
+  c->d_one_ext = eb ? reinterpret_cast<ksg_pod_ext*>(c->d_one + eo) : nullptr;
   return KSG_OK;
 }
 
@@ -445,6 +479,15 @@ size_t pod_ids_extent(const ksg_pod* p) {
   e = std::max<size_t>(e, (size_t)p->pds_off + p->n_pds);
   e = std::max<size_t>(e, (size_t)p->sel_off + p->n_sel);
   e = std::max<size_t>(e, (size_t)p->svcs_off + p->n_svcs);
+  return e;
+}
+// ... and the extension record's taint lists (the single-pod _ext entry points)
+size_t call_ids_extent(const ksg_ctx* c, const ksg_pod* p) {
+  size_t e = pod_ids_extent(p);
+  if (c->cur_ext) {
+    e = std::max<size_t>(e, (size_t)c->cur_ext->hard_off + c->cur_ext->n_hard);
+    e = std::max<size_t>(e, (size_t)c->cur_ext->soft_off + c->cur_ext->n_soft);
+  }
   return e;
 }
 
@@ -524,7 +567,8 @@ int scan_exchange(ksg_ctx* c, const ksg_pod* dpod, const uint32_t* dids, int mod
                               nullptr, c->d_dglobal, c->st));
   } else {
     HIPCHK(c, ksg_launch_scan(c->R, anti, c->dev, dpod, dids, mode, 0, fail_out, score_out, c->d_rec_send,
-                              nullptr, nullptr, c->st));
+                              nullptr, nullptr, c->st,
+                              (c->ext_on && dpod == c->one_pod) ? c->d_one_ext : nullptr));
   }
   if (mode == KSG_MODE_BEGIN) {
     if (c->xchg) {
@@ -550,6 +594,7 @@ KsgDev full_geometry(const ksg_ctx* c) {
 
 bool use_window(ksg_ctx* c, const ksg_pod* pods, uint32_t n) {
   if (c->window == 0 || c->nw > 32 * 64 || ksg_win_max_window(full_geometry(c)) < 8) return false;
+  if (c->ext_on) return false;  // extensions run on the exact kernels only
   // monotonicity under commits needs non-negative pod-dependent weights
   if (c->cfg.w_least_requested < 0 || c->cfg.w_service_spreading < 0) return false;
   // lr_win (ksg_device.h) is exact for 0 <= capacity, requested totals <= 2^49
@@ -930,10 +975,12 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
     d.n_aff_groups = 1;
     d.aff_group_mask[0] = (1u << d.n_aff) - 1u;
   }
-  d.equal_fallback = c->cfg.n_priority_configs == 0;
+  // (extension priorities count as priority configs)
+  const bool ext_prio = c->ext_on && (c->ext.w_taint_toleration || c->ext.w_balanced);
+  d.equal_fallback = c->cfg.n_priority_configs == 0 && !ext_prio;
   // prioritizeNodes skips weight-0 configs; if every config has weight 0 the
   // HostPriorityList is empty and Schedule returns *FitError.
-  bool any_weight = c->cfg.w_least_requested || c->cfg.w_service_spreading || c->cfg.w_equal;
+  bool any_weight = c->cfg.w_least_requested || c->cfg.w_service_spreading || c->cfg.w_equal || ext_prio;
   for (uint32_t a = 0; a < c->cfg.n_anti; ++a) any_weight |= c->cfg.w_anti[a] != 0;
   for (uint32_t q = 0; q < c->cfg.n_label_pref; ++q) any_weight |= c->cfg.w_pref[q] != 0;
   d.empty_priorities = (!d.equal_fallback && !any_weight) ? 1 : 0;
@@ -965,6 +1012,21 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   d.anti_domain = anti_dom;
   d.aff_pair = aff_pair;
   d.score_scratch = gscore;
+  if (c->ext_on) {  // extensions: extended resources (allocatable, requested) and taint bitmaps
+    int64_t *scap = nullptr, *sused = nullptr;
+    uint64_t* tmap = nullptr;
+    const size_t nsr = std::max<uint32_t>(c->ext.n_scalar, 1);
+    if ((rc = dalloc(c, &scap, nsr * NN, owner)) || (rc = dalloc(c, &sused, nsr * NN, owner)) ||
+        (rc = dalloc(c, &tmap, (size_t)std::max<uint32_t>(c->ext.max_taints, 1) * std::max<uint32_t>(c->nw, 1), owner)))
+      return rc;
+    d.ext_filters = c->ext.filters;
+    d.w_taint = c->ext.w_taint_toleration;
+    d.w_bal = c->ext.w_balanced;
+    d.n_scalar = c->ext.n_scalar;
+    d.scalar_cap = scap;
+    d.scalar_used = sused;
+    d.taintmap = tmap;
+  }
   c->lds = (size_t)d.n_domains_total * sizeof(int32_t);
 
   // scratch sized for the shard
@@ -1012,11 +1074,19 @@ static int remove_pod_impl(ksg_ctx* c, uint64_t uid) {
   PodRec r = std::move(it->second);
   c->pods.erase(it);
   const uint32_t h = r.host;
+  if (c->ext_on) c->ext_scalar.erase(uid);
   if (h < c->N) {
     c->used_c[h] = (int64_t)((uint64_t)c->used_c[h] - (uint64_t)r.cpu);
     c->used_m[h] = (int64_t)((uint64_t)c->used_m[h] - (uint64_t)r.mem);
     patch64(c, c->dev.used_cpu + h, c->used_c[h]);
     patch64(c, c->dev.used_mem + h, c->used_m[h]);
+    if (c->ext_on)
+      for (uint32_t q = 0; q < c->ext.n_scalar; ++q) {
+        if (!r.scalar[q]) continue;
+        int64_t& u = c->sc_used[(size_t)q * c->N + h];
+        u = (int64_t)((uint64_t)u - (uint64_t)r.scalar[q]);
+        patch64(c, c->dev.scalar_used + (size_t)q * c->N + h, u);
+      }
     for (uint32_t k : r.keys) {
       auto kit = c->key_ref.find(((uint64_t)k << 32) | h);
       if (kit != c->key_ref.end() && --kit->second == 0) {
@@ -1069,6 +1139,7 @@ static int apply_queued(ksg_ctx* c) {
 int ksg_add_pod(ksg_ctx* c, uint32_t host_id, const ksg_pod* pod, const uint32_t* ids) {
   if (!c || !pod) return KSG_ERR_ARG;
   KSG_LOCK(c);
+  if (c->ext_on && !c->cur_ext) c->ext_scalar.erase(pod->uid);  // (plain entry point: no extension requests)
   HIPCHK(c, hipSetDevice(c->device));  // reflector threads: patches flush on this context's device
   if (!c->pending) return add_pod_impl(c, host_id, pod, ids);
   if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
@@ -1109,7 +1180,8 @@ int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int6
     if (int rq = apply_queued(c)) return rq;
   }
   if (c->N == 0) return KSG_NONODES;
-  const size_t ext = pod_ids_extent(pod);
+  if (c->ext_on && !c->cur_ext) c->ext_scalar.erase(pod->uid);  // (plain entry point: no extension requests)
+  const size_t ext = call_ids_extent(c, pod);
   int rc = check_pod(c, pod, ids, ext);
   if (rc) return rc;
   if ((rc = flush_patches(c))) return rc;
@@ -1147,7 +1219,7 @@ static int commit_on_device(ksg_ctx* c, uint32_t tie_index, int32_t* node) {
   // the pending pod is still in d_one (begin's upload; nothing re-uploads before the commit)
   HIPCHK(c, ksg_launch_decide(c->dev, c->one_pod, c->one_ids, rec_buf(c), c->rec_bytes, c->world,
                               c->d_shard_wlo, 2, tie_index, c->d_rng, reinterpret_cast<int32_t*>(c->d_map + 32), 0,
-                              c->d_summary, c->st));
+                              c->d_summary, c->st, c->ext_on ? c->d_one_ext : nullptr));
   HIPCHK(c, hipStreamSynchronize(c->st));
   memcpy(node, c->h_map + 32, 4);
   if (*node < 0) return fail(c, KSG_ERR_STATE, "commit selected no node (%d)", *node);
@@ -1186,6 +1258,8 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     for (uint32_t i = 0; i < n; ++i) out_nodes[i] = KSG_OUT_NONODES;
     return KSG_OK;
   }
+  if (c->ext_on && !c->cur_ext)  // (plain entry point: the pods carry no extension requests)
+    for (uint32_t i = 0; i < n; ++i) c->ext_scalar.erase(pods[i].uid);
   for (uint32_t i = 0; i < n; ++i) {
     int rc = check_pod(c, pods + i, ids, n_ids);
     if (rc) return rc;
@@ -1346,7 +1420,17 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       K = round_k(n - std::min(pos, n));
     }
   } else if (!c->xchg) {
-    HIPCHK(c, ksg_launch_batch(c->R, anti_on(c), c->dev, c->d_pods, c->d_ids, n, c->d_rng, c->d_out, c->st));
+    const ksg_pod_ext* dext = nullptr;
+    if (c->ext_on) {  // extensions: each pod's record (all-zero for the plain entry point)
+      if ((rc = grow(c, (void**)&c->d_pext, &c->pext_cap, n, sizeof(ksg_pod_ext)))) return rc;
+      if (c->cur_ext) {
+        HIPCHK(c, hipMemcpyAsync(c->d_pext, c->cur_ext, (size_t)n * sizeof(ksg_pod_ext), hipMemcpyHostToDevice, c->st));
+      } else {
+        HIPCHK(c, hipMemsetAsync(c->d_pext, 0, (size_t)n * sizeof(ksg_pod_ext), c->st));
+      }
+      dext = c->d_pext;
+    }
+    HIPCHK(c, ksg_launch_batch(c->R, anti_on(c), c->dev, c->d_pods, c->d_ids, n, c->d_rng, c->d_out, c->st, dext));
   } else {
     for (uint32_t i = 0; i < n; ++i) {
       if ((rc = scan_exchange(c, c->d_pods + i, c->d_ids, KSG_MODE_BEGIN, nullptr, nullptr))) return rc;
@@ -1387,7 +1471,7 @@ int ksg_evaluate(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, uint8_t* f
   if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
   HIPCHK(c, hipSetDevice(c->device));
   if (c->N == 0) return KSG_NONODES;
-  const size_t ext = pod_ids_extent(pod);
+  const size_t ext = call_ids_extent(c, pod);
   int rc = check_pod(c, pod, ids, ext);
   if (rc) return rc;
   if ((rc = flush_patches(c))) return rc;
@@ -1523,6 +1607,141 @@ static int admit_impl(ksg_ctx* c, int mode, const ksg_admission_set* sets, uint3
   for (uint32_t i = 0; i < n_pods; ++i)
     if (in_set[i]) out[i] = c->h_dn[i];
   return KSG_OK;
+}
+
+// ---- extensions (include/kschedgpu.h; parity unpinned) ----------------------
+int ksg_set_extensions(ksg_ctx* c, const ksg_ext_config* e) {
+  if (!c || !e) return KSG_ERR_ARG;
+  KSG_LOCK(c);
+  if (c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_extensions: call before ksg_set_cluster");
+  if (c->world > 1 || c->xchg) return fail(c, KSG_ERR_ARG, "extensions: one rank only");
+  if ((e->filters & ~(KSG_EXT_TAINTS | KSG_EXT_SCALAR)) || e->n_scalar > KSG_MAX_SCALAR)
+    return fail(c, KSG_ERR_ARG, "extensions: bad filters / n_scalar");
+  int64_t bound = 10LL * (std::llabs((int64_t)c->cfg.w_least_requested) + std::llabs((int64_t)c->cfg.w_service_spreading) +
+                          std::llabs((int64_t)e->w_taint_toleration) + std::llabs((int64_t)e->w_balanced)) +
+                  std::llabs((int64_t)c->cfg.w_equal);
+  for (uint32_t a = 0; a < c->cfg.n_anti; ++a) bound += 10LL * std::llabs((int64_t)c->cfg.w_anti[a]);
+  for (uint32_t q = 0; q < c->cfg.n_label_pref; ++q) bound += 10LL * std::llabs((int64_t)c->cfg.w_pref[q]);
+  if (bound >= KSG_SCORE_BOUND) return fail(c, KSG_ERR_ARG, "extensions: priority weights too large");
+  c->ext = *e;
+  c->ext_on = e->filters || e->w_taint_toleration || e->w_balanced || e->n_scalar;
+  return KSG_OK;
+}
+
+int ksg_set_node_ext(ksg_ctx* c, uint32_t n_nodes, const int64_t* scalar_cap, const uint32_t* taint_off,
+                     const uint32_t* taint_n, const uint32_t* taint_ids, uint32_t n_taint_ids) {
+  if (!c) return KSG_ERR_ARG;
+  KSG_LOCK(c);
+  if (!c->ext_on) return fail(c, KSG_ERR_STATE, "ksg_set_node_ext: extensions are off");
+  if (!c->have_cluster || n_nodes != c->N) return fail(c, KSG_ERR_ARG, "ksg_set_node_ext: node count != cluster");
+  if (int rc0 = flush_deferred(c)) return rc0;
+  if (!c->pods.empty()) return fail(c, KSG_ERR_STATE, "ksg_set_node_ext: call before adding pods");
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t NN = std::max<uint32_t>(c->N, 1);
+  if (c->ext.n_scalar && n_nodes) {
+    if (!scalar_cap) return fail(c, KSG_ERR_ARG, "ksg_set_node_ext: scalar_cap missing");
+    HIPCHK(c, hipMemcpyAsync(const_cast<int64_t*>(c->dev.scalar_cap), scalar_cap, (size_t)c->ext.n_scalar * n_nodes * 8,
+                             hipMemcpyHostToDevice, c->st));
+  }
+  std::vector<uint64_t> tm((size_t)std::max<uint32_t>(c->ext.max_taints, 1) * std::max<uint32_t>(c->nw, 1), 0);
+  if (taint_off && taint_n)
+    for (uint32_t n = 0; n < n_nodes; ++n)
+      for (uint32_t i = 0; i < taint_n[n]; ++i) {
+        if ((size_t)taint_off[n] + i >= n_taint_ids || !taint_ids) return fail(c, KSG_ERR_ARG, "taint list out of range");
+        const uint32_t t = taint_ids[taint_off[n] + i];
+        if (t >= c->ext.max_taints) return fail(c, KSG_ERR_CAPACITY, "taint id %u >= max_taints", t);
+        tm[(size_t)t * c->nw + (n >> 6)] |= 1ULL << (n & 63);
+      }
+  HIPCHK(c, hipMemcpyAsync(const_cast<uint64_t*>(c->dev.taintmap), tm.data(), tm.size() * 8, hipMemcpyHostToDevice,
+                           c->st));
+  HIPCHK(c, hipMemsetAsync(c->dev.scalar_used, 0, (size_t)std::max<uint32_t>(c->ext.n_scalar, 1) * NN * 8, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  c->sc_used.assign((size_t)c->ext.n_scalar * c->N, 0);
+  return KSG_OK;
+}
+
+// validate a pod's extension record against the call's id array and record its
+// extended-resource requests by uid (the host mirror's AssumePod/remove)
+static int note_ext(ksg_ctx* c, const ksg_pod* p, const ksg_pod_ext* e, size_t n_ids) {
+  if ((size_t)e->hard_off + e->n_hard > n_ids || (size_t)e->soft_off + e->n_soft > n_ids)
+    return fail(c, KSG_ERR_ARG, "extension taint list out of range");
+  std::array<int64_t, KSG_MAX_SCALAR> sc{};
+  bool any = false;
+  for (uint32_t q = 0; q < c->ext.n_scalar; ++q) {
+    sc[q] = e->scalar[q];
+    any |= sc[q] != 0;
+  }
+  if (any) c->ext_scalar[p->uid] = sc;
+  else c->ext_scalar.erase(p->uid);
+  return KSG_OK;
+}
+static int check_taint_ids(ksg_ctx* c, const ksg_pod_ext* e, const uint32_t* ids) {
+  for (uint32_t i = 0; i < e->n_hard; ++i)
+    if (ids[e->hard_off + i] >= c->ext.max_taints) return fail(c, KSG_ERR_CAPACITY, "taint id out of range");
+  for (uint32_t i = 0; i < e->n_soft; ++i)
+    if (ids[e->soft_off + i] >= c->ext.max_taints) return fail(c, KSG_ERR_CAPACITY, "taint id out of range");
+  return KSG_OK;
+}
+
+int ksg_add_pod_ext(ksg_ctx* c, uint32_t host_id, const ksg_pod* pod, const ksg_pod_ext* ext, const uint32_t* ids) {
+  if (!c || !pod) return KSG_ERR_ARG;
+  KSG_LOCK(c);
+  if (ext && !c->ext_on) return fail(c, KSG_ERR_STATE, "extensions are off");
+  if (c->ext_on) {
+    const ksg_pod_ext z{};
+    const ksg_pod_ext* e = ext ? ext : &z;
+    const size_t n_ids = std::max(pod_ids_extent(pod), std::max<size_t>((size_t)e->hard_off + e->n_hard,
+                                                                         (size_t)e->soft_off + e->n_soft));
+    if (int rc = note_ext(c, pod, e, n_ids)) return rc;
+  }
+  c->cur_ext = ext;
+  const int rc = ksg_add_pod(c, host_id, pod, ids);
+  c->cur_ext = nullptr;
+  return rc;
+}
+
+int ksg_schedule_batch_ext(ksg_ctx* c, const ksg_pod* pods, const ksg_pod_ext* ext, uint32_t n, const uint32_t* ids,
+                           uint32_t n_ids, uint64_t* rng_state, int32_t* out_nodes) {
+  if (!c || (n && (!pods || !out_nodes)) || !rng_state) return KSG_ERR_ARG;
+  KSG_LOCK(c);
+  if (ext && !c->ext_on) return fail(c, KSG_ERR_STATE, "extensions are off");
+  if (c->ext_on && ext)
+    for (uint32_t i = 0; i < n; ++i) {
+      if (int rc = note_ext(c, pods + i, ext + i, n_ids)) return rc;
+      if (int rc = check_taint_ids(c, ext + i, ids)) return rc;
+    }
+  c->cur_ext = ext;
+  const int rc = ksg_schedule_batch(c, pods, n, ids, n_ids, rng_state, out_nodes);
+  c->cur_ext = nullptr;
+  return rc;
+}
+
+int ksg_schedule_begin_ext(ksg_ctx* c, const ksg_pod* pod, const ksg_pod_ext* ext, const uint32_t* ids,
+                           int64_t* max_score, uint32_t* tie_count, uint8_t* fail_codes) {
+  if (!c || !pod) return KSG_ERR_ARG;
+  KSG_LOCK(c);
+  if (ext && !c->ext_on) return fail(c, KSG_ERR_STATE, "extensions are off");
+  c->cur_ext = ext;
+  int rc = KSG_OK;
+  if (ext) {
+    const size_t n_ids = call_ids_extent(c, pod);
+    if (!(rc = note_ext(c, pod, ext, n_ids))) rc = check_taint_ids(c, ext, ids);
+  }
+  if (!rc) rc = ksg_schedule_begin(c, pod, ids, max_score, tie_count, fail_codes);
+  c->cur_ext = nullptr;
+  return rc;
+}
+
+int ksg_evaluate_ext(ksg_ctx* c, const ksg_pod* pod, const ksg_pod_ext* ext, const uint32_t* ids, uint8_t* fail_out,
+                     int64_t* score_out) {
+  if (!c || !pod) return KSG_ERR_ARG;
+  KSG_LOCK(c);
+  if (ext && !c->ext_on) return fail(c, KSG_ERR_STATE, "extensions are off");
+  c->cur_ext = ext;
+  int rc = ext ? check_taint_ids(c, ext, ids) : KSG_OK;
+  if (!rc) rc = ksg_evaluate(c, pod, ids, fail_out, score_out);
+  c->cur_ext = nullptr;
+  return rc;
 }
 
 int ksg_check_pods_exceeding_capacity(ksg_ctx* c, const ksg_admission_set* sets, uint32_t n_sets,

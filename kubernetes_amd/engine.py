@@ -11,6 +11,8 @@ from __future__ import annotations
 import ctypes as C
 from dataclasses import dataclass, field
 
+from typing import Optional
+
 import numpy as np
 
 from . import abi
@@ -43,12 +45,16 @@ class PodBatch:
 
     pods: np.ndarray
     ids: np.ndarray  # uint32
+    # extensions (include/kschedgpu.h ksg_pod_ext, POD_EXT_DTYPE[n]; None: none)
+    ext: Optional[np.ndarray] = None
 
     def __len__(self):
         return int(self.pods.shape[0])
 
     def one(self, i: int) -> "PodBatch":
-        return PodBatch(self.pods[i : i + 1].copy(), self.ids)
+        return PodBatch(self.pods[i : i + 1].copy(), self.ids,
+                        None if self.ext is None else self.ext[i : i + 1].copy())
+
 
 
 def _u32(a) -> np.ndarray:
@@ -140,10 +146,31 @@ class DeviceScheduler:
             self._err(rc)
         self.n_nodes = len(nodes)
 
+    # ---- extensions (include/kschedgpu.h; parity unpinned) ---------------------
+    def set_extensions(self, ext: abi.KsgExtConfig):
+        rc = self._lib.ksg_set_extensions(self._ctx, C.byref(ext))
+        if rc != abi.KSG_OK:
+            self._err(rc)
+
+    def set_node_ext(self, scalar_cap: np.ndarray, taint_off: np.ndarray, taint_n: np.ndarray,
+                     taint_ids: np.ndarray):
+        """scalar_cap int64[n_scalar, N]; node n's taints taint_ids[taint_off[n]:+taint_n[n]]."""
+        cap = np.ascontiguousarray(scalar_cap, np.int64).reshape(-1)
+        cap = cap if len(cap) else np.zeros(1, np.int64)
+        ti = _u32(taint_ids if len(taint_ids) else np.zeros(1, np.uint32))
+        rc = self._lib.ksg_set_node_ext(self._ctx, self.n_nodes, abi.ptr(cap), abi.ptr(_u32(taint_off)),
+                                        abi.ptr(_u32(taint_n)), abi.ptr(ti), len(taint_ids))
+        if rc != abi.KSG_OK:
+            self._err(rc)
+
     def add_pod(self, host_id: int, batch: PodBatch, i: int = 0):
         pod = np.ascontiguousarray(batch.pods[i : i + 1])
         ids = _u32(batch.ids if len(batch.ids) else np.zeros(1, np.uint32))
-        rc = self._lib.ksg_add_pod(self._ctx, int(host_id), abi.ptr(pod), abi.ptr(ids))
+        if batch.ext is not None:
+            ext = np.ascontiguousarray(batch.ext[i : i + 1], dtype=abi.POD_EXT_DTYPE)
+            rc = self._lib.ksg_add_pod_ext(self._ctx, int(host_id), abi.ptr(pod), abi.ptr(ext), abi.ptr(ids))
+        else:
+            rc = self._lib.ksg_add_pod(self._ctx, int(host_id), abi.ptr(pod), abi.ptr(ids))
         if rc != abi.KSG_OK:
             self._err(rc)
 
@@ -161,8 +188,13 @@ class DeviceScheduler:
         k = C.c_uint32(0)
         lo, hi = self.shard()
         fails = np.zeros(max(hi - lo, 1), np.uint8) if want_fail else None
-        rc = self._lib.ksg_schedule_begin(self._ctx, abi.ptr(pod), abi.ptr(ids), C.byref(m), C.byref(k),
-                                          abi.ptr(fails))
+        if batch.ext is not None:
+            ext = np.ascontiguousarray(batch.ext[i : i + 1], dtype=abi.POD_EXT_DTYPE)
+            rc = self._lib.ksg_schedule_begin_ext(self._ctx, abi.ptr(pod), abi.ptr(ext), abi.ptr(ids), C.byref(m),
+                                                  C.byref(k), abi.ptr(fails))
+        else:
+            rc = self._lib.ksg_schedule_begin(self._ctx, abi.ptr(pod), abi.ptr(ids), C.byref(m), C.byref(k),
+                                              abi.ptr(fails))
         if rc not in (abi.KSG_OK, abi.KSG_NOFIT, abi.KSG_NONODES):
             self._err(rc)
         return rc, m.value, k.value, (fails[: hi - lo] if fails is not None else None)
@@ -181,8 +213,13 @@ class DeviceScheduler:
         ids = _u32(batch.ids if len(batch.ids) else np.zeros(1, np.uint32))
         out = np.empty(max(n, 1), np.int32)
         st = C.c_uint64(rng_state)
-        rc = self._lib.ksg_schedule_batch(self._ctx, abi.ptr(pods), n, abi.ptr(ids), len(batch.ids), C.byref(st),
-                                          abi.ptr(out))
+        if batch.ext is not None:
+            ext = np.ascontiguousarray(batch.ext, dtype=abi.POD_EXT_DTYPE)
+            rc = self._lib.ksg_schedule_batch_ext(self._ctx, abi.ptr(pods), abi.ptr(ext), n, abi.ptr(ids),
+                                                  len(batch.ids), C.byref(st), abi.ptr(out))
+        else:
+            rc = self._lib.ksg_schedule_batch(self._ctx, abi.ptr(pods), n, abi.ptr(ids), len(batch.ids),
+                                              C.byref(st), abi.ptr(out))
         if rc != abi.KSG_OK:
             self._err(rc)
         return out[:n], st.value
@@ -194,7 +231,12 @@ class DeviceScheduler:
         lo, hi = self.shard()
         fails = np.zeros(max(hi - lo, 1), np.uint8)
         scores = np.zeros(max(hi - lo, 1), np.int64)
-        rc = self._lib.ksg_evaluate(self._ctx, abi.ptr(pod), abi.ptr(ids), abi.ptr(fails), abi.ptr(scores))
+        if batch.ext is not None:
+            ext = np.ascontiguousarray(batch.ext[i : i + 1], dtype=abi.POD_EXT_DTYPE)
+            rc = self._lib.ksg_evaluate_ext(self._ctx, abi.ptr(pod), abi.ptr(ext), abi.ptr(ids), abi.ptr(fails),
+                                            abi.ptr(scores))
+        else:
+            rc = self._lib.ksg_evaluate(self._ctx, abi.ptr(pod), abi.ptr(ids), abi.ptr(fails), abi.ptr(scores))
         if rc not in (abi.KSG_OK, abi.KSG_NONODES):
             self._err(rc)
         return rc, fails[: hi - lo], scores[: hi - lo]

@@ -23,6 +23,7 @@
  *                 HostPriorityList and sorts it (generic_scheduler.go:84-96).
  *   incremental — per-node totals/bitsets updated on commit, closed forms.
  */
+#include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -38,6 +39,7 @@ typedef struct {
   uint32_t *svcs, n_svcs;
   uint64_t seq;
   int alive;
+  int64_t scalar[KSG_MAX_SCALAR]; /* extension: extended resource requests */
 } opod;
 
 typedef struct orc {
@@ -68,6 +70,12 @@ typedef struct orc {
   int64_t pend_M;
   int64_t *scores; /* N */
   uint8_t *fails;  /* N */
+  /* extensions (include/kschedgpu.h; later kube-scheduler semantics, parity unpinned) */
+  int ext_on;
+  ksg_ext_config ext;
+  int64_t *scap, *sused;  /* [n_scalar][N] */
+  uint32_t **ntaint, *nnt; /* per node taint ids */
+  ksg_pod_ext pend_ext;
 } orc;
 
 #define NONE_SCORE (-0x7fffffffffffffffLL - 1)
@@ -150,7 +158,20 @@ static void free_pods(orc *o) {
   o->n_pods = o->cap_pods = 0;
 }
 
+static void free_ext(orc *o) {
+  if (o->ntaint)
+    for (uint32_t n = 0; n < o->N; ++n) free(o->ntaint[n]);
+  free(o->ntaint);
+  free(o->nnt);
+  free(o->scap);
+  free(o->sused);
+  o->ntaint = NULL;
+  o->nnt = NULL;
+  o->scap = o->sused = NULL;
+}
+
 static void free_cluster(orc *o) {
+  free_ext(o);
   for (uint32_t n = 0; n < o->N; ++n) free(o->node_pairs[n]);
   free(o->node_pairs);
   free(o->node_np);
@@ -256,7 +277,12 @@ static void recompute_svc_max(orc *o, uint32_t s) {
   o->svc_max[s] = m;
 }
 
+int orc_add_pod_ext(orc *o, uint32_t host_id, const ksg_pod *p, const ksg_pod_ext *e, const uint32_t *ids);
 int orc_add_pod(orc *o, uint32_t host_id, const ksg_pod *p, const uint32_t *ids) {
+  return orc_add_pod_ext(o, host_id, p, NULL, ids);
+}
+
+int orc_add_pod_ext(orc *o, uint32_t host_id, const ksg_pod *p, const ksg_pod_ext *e, const uint32_t *ids) {
   if (o->n_pods == o->cap_pods) {
     o->cap_pods = o->cap_pods ? o->cap_pods * 2 : 256;
     o->pods = (opod *)realloc(o->pods, (size_t)o->cap_pods * sizeof(opod));
@@ -274,6 +300,10 @@ int orc_add_pod(orc *o, uint32_t host_id, const ksg_pod *p, const uint32_t *ids)
   q->n_svcs = p->n_svcs;
   q->seq = ++o->seq;
   q->alive = 1;
+  for (int r = 0; r < KSG_MAX_SCALAR; ++r) q->scalar[r] = (e && o->ext_on && (uint32_t)r < o->ext.n_scalar) ? e->scalar[r] : 0;
+  if (host_id < o->N && o->sused)
+    for (uint32_t r = 0; r < o->ext.n_scalar; ++r)
+      o->sused[(size_t)r * o->N + host_id] = (int64_t)((uint64_t)o->sused[(size_t)r * o->N + host_id] + (uint64_t)q->scalar[r]);
   if (host_id < o->N) {
     o->used_c[host_id] = (int64_t)((uint64_t)o->used_c[host_id] + (uint64_t)q->cpu);
     o->used_m[host_id] = (int64_t)((uint64_t)o->used_m[host_id] + (uint64_t)q->mem);
@@ -299,6 +329,9 @@ int orc_remove_pod(orc *o, uint64_t uid) {
     if (!q->alive || q->uid != uid) continue;
     q->alive = 0;
     uint32_t h = q->host;
+    if (h < o->N && o->sused)
+      for (uint32_t r = 0; r < o->ext.n_scalar; ++r)
+        o->sused[(size_t)r * o->N + h] = (int64_t)((uint64_t)o->sused[(size_t)r * o->N + h] - (uint64_t)q->scalar[r]);
     if (h < o->N) {
       o->used_c[h] = (int64_t)((uint64_t)o->used_c[h] - (uint64_t)q->cpu);
       o->used_m[h] = (int64_t)((uint64_t)o->used_m[h] - (uint64_t)q->mem);
@@ -333,7 +366,79 @@ typedef struct {
   const uint32_t *ids;
   int32_t req_aff[KSG_MAX_AFF];
   int error;
+  const ksg_pod_ext *ext; /* extensions (NULL: none) */
 } pctx;
+
+/* ---------------------------------------------------------- extensions
+ * Not in the reference; the published kube-scheduler v1.10 algorithms,
+ * restated (parity unpinned): PodToleratesNodeTaints (an untolerated
+ * NoSchedule / NoExecute taint fails the node), PodFitsResources'
+ * ScalarResources (allocatable < requested + request fails), TaintToleration
+ * priority (untolerated PreferNoSchedule taints, NormalizeReduce(10, reverse))
+ * and BalancedResourceAllocation (float64, over the same requested totals as
+ * LeastRequested here). */
+static int node_has_taint(const orc *o, uint32_t n, uint32_t t) {
+  for (uint32_t i = 0; i < o->nnt[n]; ++i)
+    if (o->ntaint[n][i] == t) return 1;
+  return 0;
+}
+
+/* used: the node's extended-resource requests (per resource) */
+static int ext_fail_code(const orc *o, const pctx *c, uint32_t n, const int64_t *used) {
+  if (!o->ext_on || !c->ext) return KSG_FAIL_NONE;
+  if (o->ext.filters & KSG_EXT_TAINTS)
+    for (uint32_t i = 0; i < c->ext->n_hard; ++i)
+      if (node_has_taint(o, n, c->ids[c->ext->hard_off + i])) return KSG_FAIL_TAINTS;
+  if (o->ext.filters & KSG_EXT_SCALAR)
+    for (uint32_t r = 0; r < o->ext.n_scalar; ++r) {
+      int64_t req = c->ext->scalar[r];
+      if (req > 0 && o->scap[(size_t)r * o->N + n] < (int64_t)((uint64_t)used[r] + (uint64_t)req)) return KSG_FAIL_SCALAR;
+    }
+  return KSG_FAIL_NONE;
+}
+
+static int64_t balanced_score(int64_t tc, int64_t cc, int64_t tm, int64_t cm) {
+  volatile double fc = cc == 0 ? 1.0 : (double)tc / (double)cc;
+  volatile double fm = cm == 0 ? 1.0 : (double)tm / (double)cm;
+  if (fc >= 1.0 || fm >= 1.0) return 0;
+  volatile double diff = fabs(fc - fm);
+  volatile double one_minus = 1.0 - diff;
+  volatile double v = one_minus * 10.0;
+  return (int64_t)v;
+}
+
+static int32_t soft_taints(const orc *o, const pctx *c, uint32_t n) {
+  int32_t k = 0;
+  for (uint32_t i = 0; i < c->ext->n_soft; ++i) k += node_has_taint(o, n, c->ids[c->ext->soft_off + i]);
+  return k;
+}
+
+/* the extension priorities over the filtered nodes; tc/tm: requested totals incl. the pod */
+static void ext_prioritize(const orc *o, const pctx *c, const uint8_t *fails, int64_t *score, const int64_t *tc,
+                           const int64_t *tm) {
+  if (!o->ext_on) return;
+  if (o->ext.w_balanced)
+    for (uint32_t n = 0; n < o->N; ++n)
+      if (!fails[n]) score[n] += (int64_t)o->ext.w_balanced * balanced_score(tc[n], o->cap_c[n], tm[n], o->cap_m[n]);
+  if (o->ext.w_taint_toleration && c->ext) {
+    int32_t mx = 0;
+    for (uint32_t n = 0; n < o->N; ++n)
+      if (!fails[n]) {
+        int32_t k = soft_taints(o, c, n);
+        if (k > mx) mx = k;
+      }
+    for (uint32_t n = 0; n < o->N; ++n)
+      if (!fails[n]) {
+        int64_t v = mx == 0 ? 10 : 10 - (10 * (int64_t)soft_taints(o, c, n)) / mx;
+        score[n] += (int64_t)o->ext.w_taint_toleration * v;
+      }
+  } else if (o->ext.w_taint_toleration) {
+    for (uint32_t n = 0; n < o->N; ++n)
+      if (!fails[n]) score[n] += (int64_t)o->ext.w_taint_toleration * 10;
+  }
+}
+
+static int ext_prio_on(const orc *o) { return o->ext_on && (o->ext.w_taint_toleration || o->ext.w_balanced); }
 
 /* CheckServiceAffinity (predicates.go:257-324) for every ServiceAffinity
  * predicate at once: req_aff[j] = the value label j must have (pair id), the
@@ -495,6 +600,13 @@ static int faithful_fail_code(const orc *o, const pctx *c, const machine_map *m,
   if ((P & KSG_PRED_PODFITSPORTS) && !f_fits_ports(o, c, m, n)) return KSG_FAIL_PODFITSPORTS;
   if ((P & KSG_PRED_PODFITSRESOURCES) && !f_fits_resources(o, c, m, n)) return KSG_FAIL_PODFITSRESOURCES;
   if ((P & KSG_PRED_SERVICEAFFINITY) && !f_service_affinity(o, c, n)) return KSG_FAIL_SERVICEAFFINITY;
+  if (o->ext_on && c->ext) {
+    int64_t used[KSG_MAX_SCALAR] = {0};
+    for (uint32_t e = 0; e < m->len[n]; ++e)
+      for (uint32_t r = 0; r < o->ext.n_scalar; ++r)
+        used[r] = (int64_t)((uint64_t)used[r] + (uint64_t)o->pods[m->lists[n][e]].scalar[r]);
+    return ext_fail_code(o, c, n, used);
+  }
   return KSG_FAIL_NONE;
 }
 
@@ -504,12 +616,29 @@ static int faithful_prioritize(orc *o, const pctx *c, const uint8_t *fails, int6
   const ksg_config *cf = &o->cfg;
   uint32_t nfilt = 0;
   for (uint32_t n = 0; n < o->N; ++n) nfilt += fails[n] == 0;
-  if (cf->n_priority_configs == 0) { /* EqualPriority */
+  if (cf->n_priority_configs == 0 && !ext_prio_on(o)) { /* EqualPriority */
     for (uint32_t n = 0; n < o->N; ++n) score[n] = 1;
     return nfilt > 0;
   }
-  int any = 0;
+  int any = ext_prio_on(o);
   for (uint32_t n = 0; n < o->N; ++n) score[n] = 0;
+  if (ext_prio_on(o)) { /* extensions: requested totals by regrouping, as LeastRequested does */
+    machine_map m;
+    map_pods_to_machines(o, &m);
+    int64_t *tc = (int64_t *)calloc(o->N ? o->N : 1, 8), *tm = (int64_t *)calloc(o->N ? o->N : 1, 8);
+    for (uint32_t n = 0; n < o->N; ++n) {
+      for (uint32_t e = 0; e < m.len[n]; ++e) {
+        tc[n] = (int64_t)((uint64_t)tc[n] + (uint64_t)o->pods[m.lists[n][e]].cpu);
+        tm[n] = (int64_t)((uint64_t)tm[n] + (uint64_t)o->pods[m.lists[n][e]].mem);
+      }
+      tc[n] = (int64_t)((uint64_t)tc[n] + (uint64_t)c->p->milli_cpu);
+      tm[n] = (int64_t)((uint64_t)tm[n] + (uint64_t)c->p->memory);
+    }
+    free_machine_map(o, &m);
+    ext_prioritize(o, c, fails, score, tc, tm);
+    free(tc);
+    free(tm);
+  }
   if (cf->w_least_requested) { /* LeastRequestedPriority, priorities.go:43-91 */
     any = 1;
     machine_map m;
@@ -621,6 +750,11 @@ static int incr_fail_code(const orc *o, const pctx *c, uint32_t n) {
     if (!(fc && fm)) return KSG_FAIL_PODFITSRESOURCES;
   }
   if ((P & KSG_PRED_SERVICEAFFINITY) && !f_service_affinity(o, c, n)) return KSG_FAIL_SERVICEAFFINITY;
+  if (o->ext_on && c->ext) {
+    int64_t used[KSG_MAX_SCALAR] = {0};
+    for (uint32_t r = 0; r < o->ext.n_scalar; ++r) used[r] = o->sused[(size_t)r * o->N + n];
+    return ext_fail_code(o, c, n, used);
+  }
   return KSG_FAIL_NONE;
 }
 
@@ -631,11 +765,11 @@ static int incr_prioritize(orc *o, const pctx *c, const uint8_t *fails, int64_t 
   const ksg_config *cf = &o->cfg;
   uint32_t nfilt = 0;
   for (uint32_t n = 0; n < o->N; ++n) nfilt += fails[n] == 0;
-  if (cf->n_priority_configs == 0) {
+  if (cf->n_priority_configs == 0 && !ext_prio_on(o)) {
     for (uint32_t n = 0; n < o->N; ++n) score[n] = 1;
     return nfilt > 0;
   }
-  int any = cf->w_least_requested || cf->w_service_spreading || cf->w_equal;
+  int any = cf->w_least_requested || cf->w_service_spreading || cf->w_equal || ext_prio_on(o);
   for (uint32_t q = 0; q < cf->n_label_pref; ++q) any |= cf->w_pref[q] != 0;
   for (uint32_t a = 0; a < cf->n_anti; ++a) any |= cf->w_anti[a] != 0;
   int32_t s = c->p->service;
@@ -685,6 +819,16 @@ static int incr_prioritize(orc *o, const pctx *c, const uint8_t *fails, int64_t 
     sc += (int64_t)cf->w_equal;
     score[n] = sc;
   }
+  if (ext_prio_on(o)) {
+    int64_t *tc = (int64_t *)calloc(o->N ? o->N : 1, 8), *tm = (int64_t *)calloc(o->N ? o->N : 1, 8);
+    for (uint32_t n = 0; n < o->N; ++n) {
+      tc[n] = (int64_t)((uint64_t)o->used_c[n] + (uint64_t)c->p->milli_cpu);
+      tm[n] = (int64_t)((uint64_t)o->used_m[n] + (uint64_t)c->p->memory);
+    }
+    ext_prioritize(o, c, fails, score, tc, tm);
+    free(tc);
+    free(tm);
+  }
   if (!ext_dcount)
     for (uint32_t a = 0; a < cf->n_anti; ++a) free(dcount[a]);
   return any && nfilt > 0;
@@ -693,10 +837,11 @@ static int incr_prioritize(orc *o, const pctx *c, const uint8_t *fails, int64_t 
 /* ============================================================== Schedule */
 /* evaluate: fills o->fails / o->scores; returns 1 if the priority list is
  * non-empty, 0 if empty, <0 on error */
-static int evaluate(orc *o, const ksg_pod *p, const uint32_t *ids) {
+static int evaluate_ext(orc *o, const ksg_pod *p, const ksg_pod_ext *e, const uint32_t *ids) {
   pctx c;
   c.p = p;
   c.ids = ids;
+  c.ext = e;
   resolve_affinity(o, &c);
   if (c.error) return KSG_ERR_NOPEER;
   if (o->faithful) {
@@ -709,6 +854,7 @@ static int evaluate(orc *o, const ksg_pod *p, const uint32_t *ids) {
   for (uint32_t n = 0; n < o->N; ++n) o->fails[n] = (uint8_t)incr_fail_code(o, &c, n);
   return incr_prioritize(o, &c, o->fails, o->scores, NULL);
 }
+static int evaluate(orc *o, const ksg_pod *p, const uint32_t *ids) { return evaluate_ext(o, p, NULL, ids); }
 
 typedef struct {
   int64_t score;
@@ -756,7 +902,9 @@ static int32_t pick(orc *o, uint64_t ix) {
   return -1;
 }
 
-static void commit(orc *o, const ksg_pod *p, const uint32_t *ids, uint32_t node) { orc_add_pod(o, node, p, ids); }
+static void commit(orc *o, const ksg_pod *p, const ksg_pod_ext *e, const uint32_t *ids, uint32_t node) {
+  orc_add_pod_ext(o, node, p, e, ids);
+}
 
 int orc_evaluate(orc *o, const ksg_pod *p, const uint32_t *ids, uint8_t *fail_out, int64_t *score_out) {
   if (o->N == 0) return KSG_NONODES;
@@ -780,6 +928,7 @@ int orc_domain_counts(orc *o, const ksg_pod *p, const uint32_t *ids, uint32_t lo
   pctx c;
   c.p = p;
   c.ids = ids;
+  c.ext = NULL;
   resolve_affinity(o, &c);
   if (c.error) return KSG_ERR_NOPEER;
   const int32_t s = p->service;
@@ -806,6 +955,7 @@ int orc_evaluate_counts(orc *o, const ksg_pod *p, const uint32_t *ids, const int
   pctx c;
   c.p = p;
   c.ids = ids;
+  c.ext = NULL;
   resolve_affinity(o, &c);
   if (c.error) return KSG_ERR_NOPEER;
   for (uint32_t n = 0; n < o->N; ++n) o->fails[n] = (uint8_t)incr_fail_code(o, &c, n);
@@ -816,11 +966,18 @@ int orc_evaluate_counts(orc *o, const ksg_pod *p, const uint32_t *ids, const int
   return KSG_OK;
 }
 
+int orc_schedule_begin_ext(orc *o, const ksg_pod *p, const ksg_pod_ext *e, const uint32_t *ids, size_t n_ids,
+                           int64_t *max_score, uint32_t *tie_count, uint8_t *fail_codes);
 int orc_schedule_begin(orc *o, const ksg_pod *p, const uint32_t *ids, size_t n_ids, int64_t *max_score,
                        uint32_t *tie_count, uint8_t *fail_codes) {
+  return orc_schedule_begin_ext(o, p, NULL, ids, n_ids, max_score, tie_count, fail_codes);
+}
+
+int orc_schedule_begin_ext(orc *o, const ksg_pod *p, const ksg_pod_ext *e, const uint32_t *ids, size_t n_ids,
+                           int64_t *max_score, uint32_t *tie_count, uint8_t *fail_codes) {
   o->pending = 0;
   if (o->N == 0) return KSG_NONODES;
-  int r = evaluate(o, p, ids);
+  int r = evaluate_ext(o, p, e, ids);
   if (r < 0) return r;
   if (fail_codes) memcpy(fail_codes, o->fails, o->N);
   int64_t M = 0;
@@ -836,6 +993,8 @@ int orc_schedule_begin(orc *o, const ksg_pod *p, const uint32_t *ids, size_t n_i
   o->pend_n_ids = n_ids;
   o->pend_k = k;
   o->pend_M = M;
+  memset(&o->pend_ext, 0, sizeof o->pend_ext);
+  if (e) o->pend_ext = *e;
   return KSG_OK;
 }
 
@@ -844,21 +1003,29 @@ int orc_schedule_commit(orc *o, uint32_t tie_index, int32_t *out_node) {
   int32_t node = pick(o, tie_index);
   o->pending = 0;
   if (node < 0) return KSG_ERR_STATE;
-  commit(o, &o->pend, o->pend_ids, (uint32_t)node);
+  commit(o, &o->pend, &o->pend_ext, o->pend_ids, (uint32_t)node);
   if (out_node) *out_node = node;
   return KSG_OK;
 }
 
 /* the same loop the device runs: begin, draw Int63 iff something fits, commit */
+int orc_schedule_batch_ext(orc *o, const ksg_pod *pods, const ksg_pod_ext *exts, uint32_t n, const uint32_t *ids,
+                           uint32_t n_ids, uint64_t *rng_state, int32_t *out_nodes);
 int orc_schedule_batch(orc *o, const ksg_pod *pods, uint32_t n, const uint32_t *ids, uint32_t n_ids,
                        uint64_t *rng_state, int32_t *out_nodes) {
+  return orc_schedule_batch_ext(o, pods, NULL, n, ids, n_ids, rng_state, out_nodes);
+}
+
+int orc_schedule_batch_ext(orc *o, const ksg_pod *pods, const ksg_pod_ext *exts, uint32_t n, const uint32_t *ids,
+                           uint32_t n_ids, uint64_t *rng_state, int32_t *out_nodes) {
   (void)n_ids;
   for (uint32_t i = 0; i < n; ++i) {
     if (o->N == 0) {
       out_nodes[i] = KSG_OUT_NONODES;
       continue;
     }
-    int r = evaluate(o, pods + i, ids);
+    const ksg_pod_ext *e = exts ? exts + i : NULL;
+    int r = evaluate_ext(o, pods + i, e, ids);
     if (r < 0) {
       out_nodes[i] = KSG_OUT_ERROR;
       continue;
@@ -871,10 +1038,43 @@ int orc_schedule_batch(orc *o, const ksg_pod *pods, uint32_t n, const uint32_t *
     }
     uint64_t rr = splitmix_next(rng_state) >> 1;
     int32_t node = pick(o, rr % k);
-    commit(o, pods + i, ids, (uint32_t)node);
+    commit(o, pods + i, e, ids, (uint32_t)node);
     out_nodes[i] = node;
   }
   return KSG_OK;
+}
+
+int orc_evaluate_ext(orc *o, const ksg_pod *p, const ksg_pod_ext *e, const uint32_t *ids, uint8_t *fail_out,
+                     int64_t *score_out) {
+  if (o->N == 0) return KSG_NONODES;
+  int r = evaluate_ext(o, p, e, ids);
+  if (r < 0) return r;
+  if (fail_out) memcpy(fail_out, o->fails, o->N);
+  if (score_out)
+    for (uint32_t n = 0; n < o->N; ++n) score_out[n] = o->fails[n] ? 0 : o->scores[n];
+  return KSG_OK;
+}
+
+void orc_set_extensions(orc *o, const ksg_ext_config *e) {
+  o->ext = *e;
+  o->ext_on = e->filters || e->w_taint_toleration || e->w_balanced || e->n_scalar;
+}
+
+/* after orc_set_cluster: allocatable of each extended resource, taints per node */
+void orc_set_node_ext(orc *o, const int64_t *scalar_cap, const uint32_t *taint_off, const uint32_t *taint_n,
+                      const uint32_t *taint_ids) {
+  free_ext(o);
+  const size_t NN = o->N ? o->N : 1, ns = o->ext.n_scalar ? o->ext.n_scalar : 1;
+  o->scap = (int64_t *)calloc(ns * NN, 8);
+  o->sused = (int64_t *)calloc(ns * NN, 8);
+  if (scalar_cap) memcpy(o->scap, scalar_cap, (size_t)o->ext.n_scalar * o->N * 8);
+  o->ntaint = (uint32_t **)calloc(NN, sizeof(uint32_t *));
+  o->nnt = (uint32_t *)calloc(NN, 4);
+  for (uint32_t n = 0; n < o->N; ++n) {
+    o->nnt[n] = taint_n ? taint_n[n] : 0;
+    o->ntaint[n] = (uint32_t *)malloc((o->nnt[n] ? o->nnt[n] : 1) * 4);
+    for (uint32_t i = 0; i < o->nnt[n]; ++i) o->ntaint[n][i] = taint_ids[taint_off[n] + i];
+  }
 }
 
 void orc_read_requested(orc *o, int64_t *c, int64_t *m) {
@@ -1006,6 +1206,7 @@ static void *mt_worker(void *argp) {
       j->skip = 0;
       j->c.p = j->pods + i;
       j->c.ids = j->ids;
+      j->c.ext = NULL;
       resolve_affinity(o, &j->c);
       if (j->c.error) {
         j->out[i] = KSG_OUT_ERROR;
@@ -1064,7 +1265,7 @@ static void *mt_worker(void *argp) {
               --ix;
             }
         }
-        commit(o, j->pods + i, j->ids, (uint32_t)node);
+        commit(o, j->pods + i, NULL, j->ids, (uint32_t)node);
         j->out[i] = node;
       }
     }

@@ -49,6 +49,12 @@ def load():
         "orc_read_requested": (None, [vp, vp, vp]),
         "orc_admit_pods": (None, [vp, C.c_uint32, vp, C.c_uint32, vp, vp, C.c_int, vp]),
         "orc_schedule_batch_mt": (C.c_int, [vp, vp, C.c_uint32, vp, C.c_uint32, P(C.c_uint64), vp, C.c_int]),
+        "orc_set_extensions": (None, [vp, P(abi.KsgExtConfig)]),
+        "orc_set_node_ext": (None, [vp, vp, vp, vp, vp]),
+        "orc_add_pod_ext": (C.c_int, [vp, C.c_uint32, vp, vp, vp]),
+        "orc_schedule_batch_ext": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.c_uint32, P(C.c_uint64), vp]),
+        "orc_schedule_begin_ext": (C.c_int, [vp, vp, vp, vp, C.c_size_t, P(C.c_int64), P(C.c_uint32), vp]),
+        "orc_evaluate_ext": (C.c_int, [vp, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -91,9 +97,22 @@ class OracleScheduler:
                                   abi.ptr(pk), len(pk), int(cl.n_services))
         self.n_nodes = len(nodes)
 
+    def set_extensions(self, ext: abi.KsgExtConfig):
+        self._lib.orc_set_extensions(self._o, C.byref(ext))
+
+    def set_node_ext(self, scalar_cap, taint_off, taint_n, taint_ids):
+        cap = np.ascontiguousarray(scalar_cap, np.int64).reshape(-1)
+        cap = cap if len(cap) else np.zeros(1, np.int64)
+        self._lib.orc_set_node_ext(self._o, abi.ptr(cap), abi.ptr(_u32(taint_off)), abi.ptr(_u32(taint_n)),
+                                   abi.ptr(_u32(taint_ids)))
+
+    def _ext(self, batch: PodBatch, i: int):
+        return None if batch.ext is None else np.ascontiguousarray(batch.ext[i : i + 1], dtype=abi.POD_EXT_DTYPE)
+
     def add_pod(self, host_id: int, batch: PodBatch, i: int = 0):
         pod = np.ascontiguousarray(batch.pods[i : i + 1])
-        self._lib.orc_add_pod(self._o, int(host_id), abi.ptr(pod), abi.ptr(_u32(batch.ids)))
+        self._lib.orc_add_pod_ext(self._o, int(host_id), abi.ptr(pod), abi.ptr(self._ext(batch, i)),
+                                  abi.ptr(_u32(batch.ids)))
 
     def remove_pod(self, uid: int):
         rc = self._lib.orc_remove_pod(self._o, int(uid))
@@ -106,8 +125,8 @@ class OracleScheduler:
         m = C.c_int64(0)
         k = C.c_uint32(0)
         fails = np.zeros(max(self.n_nodes, 1), np.uint8) if want_fail else None
-        rc = self._lib.orc_schedule_begin(self._o, abi.ptr(pod), abi.ptr(ids), len(batch.ids), C.byref(m),
-                                          C.byref(k), abi.ptr(fails))
+        rc = self._lib.orc_schedule_begin_ext(self._o, abi.ptr(pod), abi.ptr(self._ext(batch, i)), abi.ptr(ids),
+                                              len(batch.ids), C.byref(m), C.byref(k), abi.ptr(fails))
         if rc not in (abi.KSG_OK, abi.KSG_NOFIT, abi.KSG_NONODES):
             raise RuntimeError(f"oracle begin rc={rc}")
         return rc, m.value, k.value, (fails[: self.n_nodes] if fails is not None else None)
@@ -124,8 +143,9 @@ class OracleScheduler:
         pods = np.ascontiguousarray(batch.pods, dtype=abi.POD_DTYPE)
         out = np.empty(max(n, 1), np.int32)
         st = C.c_uint64(rng_state)
-        self._lib.orc_schedule_batch(self._o, abi.ptr(pods), n, abi.ptr(_u32(batch.ids)), len(batch.ids),
-                                     C.byref(st), abi.ptr(out))
+        ext = None if batch.ext is None else np.ascontiguousarray(batch.ext, dtype=abi.POD_EXT_DTYPE)
+        self._lib.orc_schedule_batch_ext(self._o, abi.ptr(pods), abi.ptr(ext), n, abi.ptr(_u32(batch.ids)),
+                                         len(batch.ids), C.byref(st), abi.ptr(out))
         return out[:n], st.value
 
     def batch_mt(self, batch: PodBatch, rng_state: int, nthreads: int):
@@ -143,8 +163,8 @@ class OracleScheduler:
         pod = np.ascontiguousarray(batch.pods[i : i + 1])
         fails = np.zeros(max(self.n_nodes, 1), np.uint8)
         scores = np.zeros(max(self.n_nodes, 1), np.int64)
-        rc = self._lib.orc_evaluate(self._o, abi.ptr(pod), abi.ptr(_u32(batch.ids)), abi.ptr(fails),
-                                    abi.ptr(scores))
+        rc = self._lib.orc_evaluate_ext(self._o, abi.ptr(pod), abi.ptr(self._ext(batch, i)),
+                                        abi.ptr(_u32(batch.ids)), abi.ptr(fails), abi.ptr(scores))
         return rc, fails[: self.n_nodes], scores[: self.n_nodes]
 
     def domain_counts(self, batch: PodBatch, i: int, lo: int, hi: int, n_anti: int, n_pairs: int):

@@ -1,0 +1,73 @@
+"""Extensions beyond the reference vintage on the device (exact kernels) against
+the C restatement, bit-exact. PARITY UNPINNED with respect to any reference
+(none exists for these): the oracle restates the
+published v1.10 algorithms (kubernetes_amd/extensions.py)."""
+import numpy as np
+import pytest
+
+from kubernetes_amd import abi
+from kubernetes_amd.engine import DeviceScheduler, PodBatch
+from oracle.pyoracle import OracleScheduler
+from tests.ext_cases import ExtCase
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name,nn,npods,kw", [
+    ("config2", 700, 900, dict()),
+    ("config2", 40, 400, dict()),                 # GPUs and capacity run out: FitErrors
+    ("config4", 900, 600, dict()),                # with ServiceAffinity + ServiceAntiAffinity
+    ("config2", 5000, 600, dict(w_taint=2, w_bal=3)),
+    ("config2", 300, 500, dict(taints=False)),
+    ("config1", 2000, 500, dict(gpus=False)),
+])
+def test_batch_with_extensions_matches_oracle(name, nn, npods, kw):
+    c = ExtCase(name, nn, npods, **kw)
+    dev = c.load(DeviceScheduler(c.cfg, device=0))
+    orc = c.load(OracleScheduler(c.cfg))
+    for i in range(0, 60, 3):  # placed pods with extended resource requests
+        dev.add_pod(i % nn, c.batch, i)
+        orc.add_pod(i % nn, c.batch, i)
+    rest = PodBatch(c.batch.pods[60:], c.batch.ids, c.batch.ext[60:])
+    got, sg = dev.batch(rest, 77)
+    want, sw = orc.batch(rest, 77)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"first mismatches at {bad[:8]}: gpu {got[bad[:8]]} oracle {want[bad[:8]]}"
+    assert sg == sw
+    assert dev.last_batch_stats()["windows"] == 0  # extensions run on the exact kernels
+    gc, gm = dev.read_requested()
+    wc, wm = orc.read_requested()
+    assert np.array_equal(gc, wc) and np.array_equal(gm, wm)
+    dev.close()
+
+
+def test_begin_commit_evaluate_remove_with_extensions():
+    c = ExtCase("config2", 300, 250)
+    dev = c.load(DeviceScheduler(c.cfg, device=0))
+    orc = c.load(OracleScheduler(c.cfg))
+    rng = np.random.default_rng(5)
+    placed = []
+    for i in range(len(c.batch)):
+        if i % 10 == 0:
+            rg, fg, sg = dev.evaluate(c.batch, i)
+            ro, fo, so = orc.evaluate(c.batch, i)
+            assert rg == ro and np.array_equal(fg, fo)
+            fit = fg == 0
+            assert np.array_equal(sg[fit], so[fit])
+            assert set(np.unique(fg)) <= {0, abi.FAIL_HOSTNAME, abi.FAIL_MATCHNODESELECTOR, abi.FAIL_NODISKCONFLICT,
+                                          abi.FAIL_PODFITSPORTS, abi.FAIL_PODFITSRESOURCES, abi.FAIL_TAINTS,
+                                          abi.FAIL_SCALAR}
+        rg, mg, kg, failg = dev.begin(c.batch, i, want_fail=True)
+        ro, mo, ko, failo = orc.begin(c.batch, i, want_fail=True)
+        assert (rg, kg) == (ro, ko), i
+        assert np.array_equal(failg, failo)
+        if rg == abi.KSG_OK:
+            assert mg == mo
+            ix = int(rng.integers(0, kg))
+            assert dev.commit(ix) == orc.commit(ix)
+            placed.append(i)
+        if i % 7 == 6 and placed:  # remove a placed pod (its GPUs come back)
+            uid = int(c.batch.pods[placed.pop(0)]["uid"])
+            dev.remove_pod(uid)
+            orc.remove_pod(uid)
+    dev.close()
