@@ -132,6 +132,10 @@ def main():
                          "(rehearsal of the sharded path with several ranks on one GPU)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per launch (profiles/), keyed by workload")
+    ap.add_argument("--extensions", action="store_true",
+                    help="add the extensions beyond this reference vintage (taints / tolerations, GPU and FPGA "
+                         "counts, TaintToleration + BalancedResourceAllocation; parity unpinned, exact kernels), "
+                         "reported as a separate workload (SURVEY.md section 0, item 2)")
     ap.add_argument("--no-stages", action="store_true",
                     help="skip the resolver's per-stage cycle breakdown (a second, untimed run with KSG_DEBUG=8)")
     args = ap.parse_args()
@@ -154,6 +158,27 @@ def main():
     batch = ingest.ingest_pods(view, w.pods, aff_labels=w.config.affinity_labels())
     cfg = w.config.compile(it.key_id)
     n_nodes = view.arrays.n_nodes
+    ext = None  # (--extensions) the context's ExtConfig and node arrays
+    if args.extensions:
+        from kubernetes_amd.extensions import ExtInterner
+
+        ecfg, node_taints, node_scalar, tols, scal = workload.extension_data(n_nodes, n_pods)
+        inter = ExtInterner(ecfg)
+        node_arrays = inter.node_arrays(node_taints, node_scalar)
+        rec, ids_x = inter.pod_records(batch.ids, tols, scal)
+        batch = PodBatch(batch.pods, ids_x, rec)
+        ext = (ecfg.compile(max(len(inter.taints), 1)), node_arrays)
+        if world > 1:
+            raise SystemExit("--extensions runs on one rank (the exact kernels)")
+
+    def load_cluster(s):
+        """set_cluster (+ the extensions, which must be enabled before it)."""
+        if ext is not None:
+            s.set_extensions(ext[0])
+        s.set_cluster(view.arrays)
+        if ext is not None:
+            s.set_node_ext(*ext[1])
+        return s
     if rank == 0:
         print(f"[bench] {wl}: {n_nodes} nodes, {n_pods} pods, ingest {time.time() - t0:.1f}s", file=sys.stderr,
               flush=True)
@@ -182,11 +207,11 @@ def main():
         sched = DeviceScheduler(cfg, device=0)
     if args.window is not None:
         sched.set_window(args.window)
-    sched.set_cluster(view.arrays)
+    load_cluster(sched)
 
     def step_batch(s):
         sl = slice(s * args.batch, (s + 1) * args.batch)
-        return PodBatch(batch.pods[sl], batch.ids)
+        return PodBatch(batch.pods[sl], batch.ids, None if batch.ext is None else batch.ext[sl])
 
     rng = workload.TIEBREAK_SEED
     outs = []
@@ -297,7 +322,7 @@ def main():
         latency = {"bound": "latency", "resolver_us_per_pod": us_pod, "clock_mhz": CLOCK_MHZ,
                    "resolver_cycles_per_pod": us_pod * CLOCK_MHZ,
                    "window_eval_us_per_pod": kk["eval_ms"] * 1e3 / pods_timed}
-        if world == 1 and not args.no_stages:
+        if world == 1 and not args.no_stages and ext is None:
             latency["stages"] = _stage_breakdown(cfg, view, args, step_batch, anti)
 
     # ---- CPU baseline: faithful restatement, single thread, bounded prefix ------
@@ -305,15 +330,15 @@ def main():
     if not args.no_cpu_baseline and world == 1:
         from oracle.pyoracle import OracleScheduler
 
-        orc = OracleScheduler(cfg, faithful=True)
-        orc.set_cluster(view.arrays)
+        orc = load_cluster(OracleScheduler(cfg, faithful=True))
         r = workload.TIEBREAK_SEED
         done = 0
         t_c = time.perf_counter()
         chunk = 50
         cpu_out = []
         while done < n_pods and time.perf_counter() - t_c < args.cpu_seconds:
-            sub = PodBatch(batch.pods[done:done + chunk], batch.ids)
+            sub = PodBatch(batch.pods[done:done + chunk], batch.ids,
+                           None if batch.ext is None else batch.ext[done:done + chunk])
             o, r = orc.batch(sub, r)
             cpu_out.append(o)
             done += len(sub)
@@ -322,13 +347,13 @@ def main():
         agree = bool(np.array_equal(cpu_out, out[:done]))
         # the stronger CPU design point beside it: the same restatement in incremental
         # mode (closed forms over SoA, no per-pod re-list), one thread, a bounded prefix
-        inc = OracleScheduler(cfg, faithful=False)
-        inc.set_cluster(view.arrays)
+        inc = load_cluster(OracleScheduler(cfg, faithful=False))
         r = workload.TIEBREAK_SEED
         done_i = 0
         t_i = time.perf_counter()
         while done_i < n_pods and time.perf_counter() - t_i < min(args.cpu_seconds, 5.0):
-            o, r = inc.batch(PodBatch(batch.pods[done_i:done_i + 200], batch.ids), r)
+            o, r = inc.batch(PodBatch(batch.pods[done_i:done_i + 200], batch.ids,
+                                      None if batch.ext is None else batch.ext[done_i:done_i + 200]), r)
             done_i += len(o)
         inc_s = time.perf_counter() - t_i
         inc.close()
@@ -339,13 +364,14 @@ def main():
         mt.set_cluster(view.arrays)
         r = workload.TIEBREAK_SEED
         done_m = 0
-        mt_out = []
+        mt_out = [np.zeros(0, np.int32)]
         t_m = time.perf_counter()
-        while done_m < n_pods and time.perf_counter() - t_m < min(args.cpu_seconds, 5.0):
+        # (the threaded restatement has no extensions: --extensions skips it)
+        while ext is None and done_m < n_pods and time.perf_counter() - t_m < min(args.cpu_seconds, 5.0):
             o, r = mt.batch_mt(PodBatch(batch.pods[done_m:done_m + 500], batch.ids), r, nthr)
             mt_out.append(o)
             done_m += len(o)
-        mt_s = time.perf_counter() - t_m
+        mt_s = max(time.perf_counter() - t_m, 1e-9)
         mt.close()
         mt_agree = bool(np.array_equal(np.concatenate(mt_out), out[:done_m]))
         cpu = {"value": done / cpu_s, "unit": "pods/s", "cores": 1, "kind": "port",
@@ -356,7 +382,7 @@ def main():
                "incremental": {"value": done_i / inc_s, "unit": "pods/s", "cores": 1,
                                "sample": f"first {done_i} pods, incremental mode (SoA closed forms, "
                                          f"no per-pod re-list), {inc_s:.1f}s"},
-               "incremental_nproc": {"value": done_m / mt_s, "unit": "pods/s", "cores": nthr,
+               "incremental_nproc": None if ext is not None else {"value": done_m / mt_s, "unit": "pods/s", "cores": nthr,
                                      "sample": f"first {done_m} pods, incremental mode, each pod's node loop "
                                                f"split over {nthr} threads (node-rank shards, two spin barriers "
                                                f"per pod; ServiceAntiAffinity configs run 1 thread), "
@@ -378,7 +404,9 @@ def main():
         "dtype": "int64",
         "data": "synthetic (seeded splitmix64 scheduler_perf-style cluster; SURVEY.md 8(d))",
         "config": {"workload": f"{wl}: {n_nodes} nodes, {n_pods} pods, "
-                               + ("DefaultProvider" if wl in ("config2", "config3", "config5") else wl),
+                               + ("DefaultProvider" if wl in ("config2", "config3", "config5") else wl)
+                               + (" + extensions (taints/tolerations, GPU/FPGA counts, TaintToleration, "
+                                  "BalancedResourceAllocation; parity unpinned, exact kernels)" if ext else ""),
                    "nodes": n_nodes, "pods_per_step": args.batch,
                    "placed_in_timed": int((timed >= 0).sum()), "fit_errors_in_timed": int((timed == -1).sum()),
                    "snapshots_in_timed": wstats,

@@ -152,3 +152,39 @@ def build(name: str, n_nodes: Optional[int] = None, n_pods: Optional[int] = None
                 for p in pods]
     cfg.max_conflict_keys = 4096
     return Workload(name, nodes, pods, make_services(), cfg, [])
+
+
+def extension_data(n_nodes: int, n_pods: int, seed: int = 11, taints: bool = True, gpus: bool = True,
+                   w_taint: int = 1, w_bal: int = 1):
+    """Seeded taints / tolerations / extended resources for a workload of n_nodes x
+    n_pods (the extensions beyond this reference vintage, kubernetes_amd/extensions.py;
+    parity unpinned): per node 0-3 taints from a pool of six (NoSchedule, NoExecute,
+    PreferNoSchedule), 0/0/4/8 GPUs and 0-2 FPGAs; per pod 0-2 tolerations (10%),
+    0-2 GPUs and an FPGA for one pod in ten.
+    -> (ExtConfig, node_taints, node_scalar, pod_tolerations, pod_scalar)."""
+    from .extensions import NO_EXECUTE, NO_SCHEDULE, PREFER_NO_SCHEDULE, ExtConfig, Taint, Toleration
+
+    rng = _SM(seed)
+    gpu, fpga = "nvidia.com/gpu", "example.com/fpga"
+    cfg = ExtConfig(taints=taints, scalar_resources=(gpu, fpga) if gpus else (), w_taint_toleration=w_taint,
+                    w_balanced=w_bal)
+    pool = [Taint("dedicated", "db", NO_SCHEDULE), Taint("dedicated", "ml", NO_SCHEDULE),
+            Taint("maint", "", NO_EXECUTE), Taint("spot", "true", PREFER_NO_SCHEDULE),
+            Taint("slow-disk", "", PREFER_NO_SCHEDULE), Taint("zone-drain", "z1", PREFER_NO_SCHEDULE)]
+    node_taints = []
+    for _ in range(n_nodes):
+        k = rng.below(4)
+        node_taints.append(sorted({pool[rng.below(len(pool))] for _ in range(k)}, key=pool.index))
+    node_scalar = {gpu: [[0, 0, 4, 8][rng.below(4)] for _ in range(n_nodes)],
+                   fpga: [rng.below(3) for _ in range(n_nodes)]}
+    tol_pool = [Toleration("dedicated", "Equal", "db", NO_SCHEDULE), Toleration("dedicated", "Exists"),
+                Toleration("maint", "Exists", "", NO_EXECUTE), Toleration("spot", "Equal", "true"),
+                Toleration("", "Exists"), Toleration("slow-disk", "Exists", "", PREFER_NO_SCHEDULE),
+                Toleration("zone-drain", "Equal", "z2")]
+    tols, scal = [], []
+    for _ in range(n_pods):
+        k = rng.below(3) if rng.below(10) else 0
+        tols.append([tol_pool[rng.below(len(tol_pool) - 1) if rng.below(20) else len(tol_pool) - 2]
+                     for _ in range(k)])
+        scal.append({gpu: [0, 0, 0, 1, 2][rng.below(5)], fpga: 1 if rng.below(10) == 0 else 0})
+    return cfg, node_taints, node_scalar if gpus else None, tols, scal
