@@ -263,13 +263,25 @@ def main():
     # from the HIP events the library records around each resolver launch.
     # exact path (--window 0) / sharded: the one batch kernel per step.
     bpn = BYTES_PER_NODE.get(wl, 60)
+    # the in-order resolver this config runs: the LDS-slot one for ServiceAntiAffinity
+    # without the re-rank (several anti priorities, > 31 label values, sharded,
+    # KSG_DEBUG & 2048 / 4096), else the register-slot one (ksg_window.hip,
+    # ksg_set_cluster's rr_dz)
+    dbg = int(os.environ.get("KSG_DEBUG", "0") or 0)
     anti = any(int(cfg.w_anti[a]) != 0 for a in range(int(cfg.n_anti)))
+    if anti:
+        pk = np.asarray(view.arrays.pair_keys, np.uint32) & np.uint32(0x7FFFFFFF)
+        n_dom = int((pk[1:] == np.uint32(cfg.anti_key[0])).sum()) if len(pk) > 1 else 0
+        rerank = (int(cfg.n_anti) == 1 and world == 1 and n_dom + 1 <= 32 and view.arrays.n_services <= 4096
+                  and not (dbg & 2048))
+        anti = not (rerank and not (dbg & 4096))  # True: the LDS-slot resolver runs
     wcap = args.window if args.window else int(os.environ.get("KSG_WINDOW", "128"))
     nwords = (n_nodes + 63) // 64
     if kk["launches"] > 0:
         launches = kk["launches"]
         pods_per_launch = pods_timed / launches
-        kavg_s = kk["resolve_ms"] / launches / 1e3
+        # (KSG_KERNEL_EVENTS=0 drops the per-kernel events: no kernel times, an A/B switch)
+        kavg_s = kk["resolve_ms"] / launches / 1e3 or float("nan")
         # the in-order resolver: the LDS-slot one with ServiceAntiAffinity, else the
         # register-slot one (ksg_window.hip)
         kname = "ksg_win_resolve_kernel" if anti else "ksg_win_resolve2_kernel"
@@ -278,7 +290,7 @@ def main():
         # bytes: the node state once per launch + the per-word bitmaps and maxima it
         # writes + the pod records (its node loads are shared by a wave's 8 pods and
         # stay in L2 across pod groups, so per-(node, pod) bytes overstate it)
-        ev_s = kk["eval_ms"] / launches / 1e3
+        ev_s = kk["eval_ms"] / launches / 1e3 or float("nan")
         ev_bytes = bpn * (n_nodes / world) + wcap * (nwords / world) * 12 + wcap * 192
         extra = {"launches": launches, "pods_per_launch": pods_per_launch,
                  "win_eval_ms_avg": kk["eval_ms"] / launches,
@@ -310,7 +322,7 @@ def main():
         ent = tj.get(f"{wl}:{n_nodes}:ksg_win_score_kernel")  # phase A's counter-measured bytes (profiles/)
         if ent:
             roofline["win_eval_traffic"] = ent["hbm_bytes_per_launch"]
-            roofline["win_eval_traffic_GBps"] = ent["hbm_bytes_per_launch"] / (kk["eval_ms"] / launches / 1e3) / 1e9
+            roofline["win_eval_traffic_GBps"] = ent["hbm_bytes_per_launch"] / ev_s / 1e9
 
     # ---- latency view: the resolver is one in-order dependency chain per window
     # (one workgroup), so its bound is the chain's cycles per pod,

@@ -153,6 +153,7 @@ struct ksg_ctx {
 
   // window (speculative) path
   uint32_t window = 128;        // 0 = exact one-pod-at-a-time kernel
+  bool kernel_events = true;    // HIP events around each window kernel (KSG_KERNEL_EVENTS=0: off)
   KsgWinSum* d_winsum = nullptr;
   uint8_t* d_xsend = nullptr;   // phase A block of this shard (KsgWinXchg layout)
   uint8_t* d_xrecv = nullptr;   // all-gathered blocks of every shard (world > 1)
@@ -745,6 +746,7 @@ static int create_impl(const ksg_config* cfg, int device, int rank, int world, c
   }
   int rc;
   if (const char* wenv = getenv("KSG_WINDOW")) c->window = (uint32_t)atoi(wenv);
+  if (const char* kev = getenv("KSG_KERNEL_EVENTS")) c->kernel_events = atoi(kev) != 0;
   if ((rc = dalloc(c, &c->d_rng, 1, nullptr)) || (rc = dalloc(c, &c->d_summary, 4, nullptr)) ||
       (rc = dalloc(c, &c->d_run, 1, nullptr)))
     return bail(rc);
@@ -1374,9 +1376,9 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
                                       rr ? reinterpret_cast<uint64_t*>(c->d_xsend + x.b_off) : nullptr, x.dz,
                                       c->st));
         if (c->xchg && (rc = allgather(c, c->d_xsend, c->d_xrecv, x.blk))) return rc;
-        HIPCHK(c, hipEventRecord(c->wev[2 * k + 1], c->st));
+        if (c->kernel_events) HIPCHK(c, hipEventRecord(c->wev[2 * k + 1], c->st));
         HIPCHK(c, ksg_launch_win_resolve(full, W, c->d_run, c->d_winsum, x, c->d_rng, c->d_out, c->st));
-        HIPCHK(c, hipEventRecord(c->wev[2 * k + 2], c->st));
+        if (c->kernel_events) HIPCHK(c, hipEventRecord(c->wev[2 * k + 2], c->st));
       }
       HIPCHK(c, hipMemcpyAsync(c->h_run, c->d_run, sizeof(KsgWinRun), hipMemcpyDeviceToHost, c->st));
       if ((rc = flush_deferred(c))) return rc;  // the host mirror catches up while the device works
@@ -1389,7 +1391,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       }
       // every launch of the round, including the ones after the batch was done
       // (they return at once), so the mean matches a kernel trace of the run
-      for (uint32_t k = 0; k < K; ++k) {
+      for (uint32_t k = 0; k < K && c->kernel_events; ++k) {
         float a = 0.f, b = 0.f;
         HIPCHK(c, hipEventElapsedTime(&a, c->wev[2 * k], c->wev[2 * k + 1]));
         HIPCHK(c, hipEventElapsedTime(&b, c->wev[2 * k + 1], c->wev[2 * k + 2]));
