@@ -75,6 +75,13 @@ struct PodRec {
 
 constexpr uint32_t kMaxNodesPerShard = KSG_R_MAX * KSG_NT;
 
+// Timing-only events: no system-scope fence when they complete. A default
+// hipEventRecord writes back and invalidates the caches, which costs the
+// stream time between the window kernels and evicts the node state the next
+// kernel reads from L2 (KSG_EVENT_FENCE=1 restores the default for A/B).
+const unsigned kTimingEvent =
+    (getenv("KSG_EVENT_FENCE") && atoi(getenv("KSG_EVENT_FENCE"))) ? hipEventDefault : hipEventDisableSystemFence;
+
 }  // namespace
 
 struct ksg_ctx {
@@ -729,7 +736,8 @@ static int create_impl(const ksg_config* cfg, int device, int rank, int world, c
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) return bail(fail(c, KSG_ERR_HIP, "hipSetDevice(%d): %s", device, hipGetErrorString(e)));
   if ((e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking)) != hipSuccess ||
-      (e = hipEventCreate(&c->ev0)) != hipSuccess || (e = hipEventCreate(&c->ev1)) != hipSuccess)
+      (e = hipEventCreateWithFlags(&c->ev0, kTimingEvent)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&c->ev1, kTimingEvent)) != hipSuccess)
     return bail(fail(c, KSG_ERR_HIP, "stream/event: %s", hipGetErrorString(e)));
   // The exchange path (shard scan, all-gather of per-shard records, replicated
   // resolve) runs for world > 1, and for a 1-rank RCCL communicator when the caller
@@ -1356,7 +1364,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       if (c->wev.size() < 2 * (size_t)K + 1) {
         const size_t old = c->wev.size();
         c->wev.resize(2 * (size_t)K + 1, nullptr);
-        for (size_t i = old; i < c->wev.size(); ++i) HIPCHK(c, hipEventCreate(&c->wev[i]));
+        for (size_t i = old; i < c->wev.size(); ++i) HIPCHK(c, hipEventCreateWithFlags(&c->wev[i], kTimingEvent));
       }
       *c->h_run = KsgWinRun{pos, n, 0, 0, {0, 0, 0, 0}};
       HIPCHK(c, hipMemcpyAsync(c->d_run, c->h_run, sizeof(KsgWinRun), hipMemcpyHostToDevice, c->st));
