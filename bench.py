@@ -69,6 +69,7 @@ _STAGES2 = {
     0: ("committer", "ring_wait"), 1: ("committer", "head"), 2: ("committer", "wait_checkers_and_xcheck"),
     3: ("committer", "select"), 4: ("committer", "slot_and_node_post"), 5: ("committer", "commit"),
     6: ("handoff", "xcheck_to_committer"), 31: ("handoff", "node_to_xchecker"),
+    10: ("committer", "ring_wait_first4"), 11: ("committer", "ring_wait_rest"),
     16: ("checker0", "wait"), 17: ("checker0", "apply"), 18: ("checker0", "check"),
     19: ("checker1", "wait"), 20: ("checker1", "apply"), 21: ("checker1", "check"),
     24: ("producers_sum_over_waves", "ring_wait"), 25: ("producers_sum_over_waves", "loads"),
@@ -227,11 +228,14 @@ def main():
     barrier()
     t_start = time.perf_counter()
     kern_ms = []
+    host_us = {}
     kk = {"eval_ms": 0.0, "resolve_ms": 0.0, "launches": 0}
     wstats = {"windows": 0, "stops_service": 0, "stops_exhausted": 0, "stops_cache": 0}
     for s in range(args.warmup, args.warmup + args.steps):
         o, rng = sched.batch(step_batch(s), rng)
         kern_ms.append(sched.last_batch_ms())
+        for k_, v_ in sched.last_batch_host_us().items():
+            host_us[k_] = host_us.get(k_, 0.0) + v_
         for k_, v_ in sched.last_batch_kernel_ms().items():
             kk[k_] += v_
         for k_, v_ in sched.last_batch_stats().items():
@@ -410,6 +414,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "device_ms_per_step": float(np.mean(kern_ms)) if kern_ms else None,
+        "host_us_per_step": {k_: round(v_ / args.steps, 1) for k_, v_ in host_us.items()},
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,

@@ -261,6 +261,16 @@ int ksg_last_batch_ms(ksg_ctx* ctx, double* ms);
  * context's stream. */
 int ksg_last_batch_kernel_ms(ksg_ctx* ctx, double* out3);
 
+/* Host time (microseconds, steady clock) of the last ksg_schedule_batch by
+ * phase: out8[0] validation (pod checks, duplicate uids), [1] upload (pending
+ * patches, pod copy-in), [2] window setup and round sizing, [3] enqueueing the
+ * launches and copies, [4] the host-mirror replay of the previous batch
+ * (overlapped with the device), [5] waiting for the device at the end of each
+ * window round (the placements' copy-out rides with it), [6] waiting for a
+ * separate copy-out (exact path, or a round that did not finish the batch),
+ * [7] the deferred-replay bookkeeping. No reference counterpart (diagnostics). */
+int ksg_last_batch_host_us(ksg_ctx* ctx, double* out8);
+
 /* Diagnostics: the window resolver's per-stage clock counters (s_memtime
  * cycles / 64, summed over every window since the context was created) for a
  * context created with KSG_DEBUG=8 in the environment; out32[32] (layout:

@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -173,6 +174,7 @@ struct ksg_ctx {
   uint32_t last_stats[4] = {0, 0, 0, 0};  // windows, stops (service scalar), stops (ties exhausted)
   std::vector<hipEvent_t> wev;     // event pairs around the chained window kernels
   double last_kms[3] = {0, 0, 0};  // phase A ms, phase B ms, launches (window path)
+  double last_hus[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // host us per phase of the last batch (ksg_last_batch_host_us)
   int64_t max_cap = 0, min_cap = 0;
 
   // Commits of the last ksg_schedule_batch not yet replayed into the host
@@ -1268,6 +1270,14 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     for (uint32_t i = 0; i < n; ++i) out_nodes[i] = KSG_OUT_NONODES;
     return KSG_OK;
   }
+  // host time per phase (ksg_last_batch_host_us)
+  for (double& v : c->last_hus) v = 0.0;
+  auto t_last = std::chrono::steady_clock::now();
+  auto hphase = [&](int k) {
+    const auto t = std::chrono::steady_clock::now();
+    c->last_hus[k] += std::chrono::duration<double, std::micro>(t - t_last).count();
+    t_last = t;
+  };
   if (c->ext_on && !c->cur_ext)  // (plain entry point: the pods carry no extension requests)
     for (uint32_t i = 0; i < n; ++i) c->ext_scalar.erase(pods[i].uid);
   for (uint32_t i = 0; i < n; ++i) {
@@ -1276,14 +1286,46 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     if (c->pods.count(pods[i].uid) || c->dfr_uids.count(pods[i].uid))
       return fail(c, KSG_ERR_ARG, "pod %u: duplicate uid", i);
   }
+  hphase(0);
   int rc;
   if (c->dfr_neg && (rc = flush_deferred(c))) return rc;
   if ((rc = flush_patches(c))) return rc;
   if ((rc = upload_pods(c, pods, n, ids, n_ids))) return rc;
   if ((rc = ensure_out(c, n))) return rc;
+  // the placements and the generator state come back through pinned staging
+  // (a pageable copy-out blocks the host until the stream drains); the window
+  // path enqueues them with each round, which usually ends the batch, so the
+  // host waits for the device once per batch
+  const size_t dn_rng = ((size_t)n * 4 + 7) & ~(size_t)7;
+  if ((rc = grow_host(c, &c->h_dn, &c->h_dn_cap, dn_rng + 8))) return rc;
+  bool tail_queued = false;
+  auto enqueue_tail = [&]() -> int {
+    HIPCHK(c, hipEventRecord(c->ev1, c->st));
+    HIPCHK(c, hipMemcpyAsync(c->h_dn, c->d_out, (size_t)n * 4, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipMemcpyAsync(c->h_dn + dn_rng, c->d_rng, 8, hipMemcpyDeviceToHost, c->st));
+    return KSG_OK;
+  };
+  // Host work that overlaps the device: the previous batch's mirror replay, then
+  // this batch's deferred-replay inputs (pods, ids, every uid: the few pods that
+  // find no node are taken out again after the wait)
+  bool stashed = false, dup_any = false;
+  auto overlap_work = [&]() -> int {
+    if (stashed) return KSG_OK;
+    int rc2 = flush_deferred(c);
+    if (rc2) return rc2;
+    hphase(4);
+    c->dfr_pods.assign(pods, pods + n);
+    c->dfr_ids.assign(ids, ids + n_ids);
+    c->dfr_uids.reserve(2 * (size_t)n);
+    for (uint32_t i = 0; i < n; ++i) dup_any |= !c->dfr_uids.insert(pods[i].uid).second;
+    stashed = true;
+    hphase(7);
+    return KSG_OK;
+  };
   HIPCHK(c, hipMemcpyAsync(c->d_rng, rng_state, 8, hipMemcpyHostToDevice, c->st));
   HIPCHK(c, hipEventRecord(c->ev0, c->st));
   c->last_stats[0] = c->last_stats[1] = c->last_stats[2] = c->last_stats[3] = 0;
+  hphase(1);
   if (use_window(c, pods, n)) {
     // Window path. Phase A scores the window on this rank's shard; with world > 1
     // the per-word results are all-gathered once per window (not per pod) and
@@ -1360,6 +1402,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     };
     uint32_t pos = 0, K = round_k(n);
     c->last_kms[0] = c->last_kms[1] = c->last_kms[2] = 0;
+    hphase(2);
     while (pos < n) {
       if (c->wev.size() < 2 * (size_t)K + 1) {
         const size_t old = c->wev.size();
@@ -1389,8 +1432,11 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
         if (c->kernel_events) HIPCHK(c, hipEventRecord(c->wev[2 * k + 2], c->st));
       }
       HIPCHK(c, hipMemcpyAsync(c->h_run, c->d_run, sizeof(KsgWinRun), hipMemcpyDeviceToHost, c->st));
-      if ((rc = flush_deferred(c))) return rc;  // the host mirror catches up while the device works
+      if ((rc = enqueue_tail())) return rc;
+      hphase(3);
+      if ((rc = overlap_work())) return rc;  // the host mirror catches up while the device works
       HIPCHK(c, hipStreamSynchronize(c->st));
+      hphase(5);
       const KsgWinRun r = *c->h_run;
       if (r.windows > 0 && r.pos > pos) {  // pods per window, smoothed over rounds and batches
         const double ppw = (double)(r.pos - pos) / (double)r.windows;
@@ -1413,6 +1459,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       if (r.halt == KSG_HALT_BADCOUNT || r.pos < pos || r.pos > n)
         return fail(c, KSG_ERR_STATE, "window resolver: bad progress (halt %u, pos %u -> %u)", r.halt, pos, r.pos);
       pos = r.pos;
+      tail_queued = pos >= n && r.halt != KSG_HALT_OVERSIZE;  // (the copies saw the finished batch)
       if (r.halt == KSG_HALT_OVERSIZE) {
         // a pod whose id lists exceed the window record: the exact per-pod path
         if (!c->xchg) {
@@ -1428,6 +1475,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       }
       // next round (rare: stops shortened this round's windows): the rest at W/2 pods per window
       K = round_k(n - std::min(pos, n));
+      hphase(2);
     }
   } else if (!c->xchg) {
     const ksg_pod_ext* dext = nullptr;
@@ -1448,28 +1496,36 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
                                   c->d_shard_wlo, 1, 0, c->d_rng, c->d_out, i, c->d_summary, c->st));
     }
   }
-  HIPCHK(c, hipEventRecord(c->ev1, c->st));
-  HIPCHK(c, hipMemcpyAsync(out_nodes, c->d_out, (size_t)n * 4, hipMemcpyDeviceToHost, c->st));
-  HIPCHK(c, hipMemcpyAsync(rng_state, c->d_rng, 8, hipMemcpyDeviceToHost, c->st));
-  if ((rc = flush_deferred(c))) return rc;
-  HIPCHK(c, hipStreamSynchronize(c->st));
+  if (!tail_queued) {
+    if ((rc = enqueue_tail())) return rc;
+    hphase(3);
+    if ((rc = overlap_work())) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    hphase(6);
+  }
+  memcpy(out_nodes, c->h_dn, (size_t)n * 4);
+  memcpy(rng_state, c->h_dn + dn_rng, 8);
   float ms = 0.f;
   HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
   c->last_ms = ms;
   // the device applied every commit; the host mirror replays them later
   // (flush_deferred), overlapped with the next batch's device work
-  c->dfr_pods.assign(pods, pods + n);
-  c->dfr_ids.assign(ids, ids + n_ids);
   c->dfr_out.assign(out_nodes, out_nodes + n);
-  c->dfr_uids.reserve(2 * (size_t)n);
+  for (uint32_t i = 0; i < n; ++i)  // the uids of the pods that found no node are free again
+    if (out_nodes[i] < 0 && !dup_any) c->dfr_uids.erase(pods[i].uid);
+  if (dup_any) {  // a uid repeats within the batch: an error iff two placed pods share it
+    for (uint32_t i = 0; i < n; ++i) c->dfr_uids.erase(pods[i].uid);
+    for (uint32_t i = 0; i < n; ++i)
+      if (out_nodes[i] >= 0 && !c->dfr_uids.insert(pods[i].uid).second)  // (mirror_add reports it at the replay)
+        return fail(c, KSG_ERR_ARG, "pod %u: duplicate uid within the batch", i);
+  }
   for (uint32_t i = 0; i < n; ++i) {
     if (out_nodes[i] < 0) continue;
-    if (!c->dfr_uids.insert(pods[i].uid).second)  // (mirror_add reports it as before, at the replay)
-      return fail(c, KSG_ERR_ARG, "pod %u: duplicate uid within the batch", i);
     if (pods[i].milli_cpu < 0 || pods[i].memory < 0) c->dfr_neg = true;
     else c->dfr_sum = std::min<int64_t>(c->dfr_sum + std::min<int64_t>(pods[i].milli_cpu + pods[i].memory,
                                                                         KSG_WIN_LR_BOUND), KSG_WIN_LR_BOUND + 1);
   }
+  hphase(7);
   return KSG_OK;
 }
 
@@ -1529,6 +1585,13 @@ int ksg_last_batch_kernel_ms(ksg_ctx* c, double* out3) {
   if (!c || !out3) return KSG_ERR_ARG;
   KSG_LOCK(c);
   for (int i = 0; i < 3; ++i) out3[i] = c->last_kms[i];
+  return KSG_OK;
+}
+
+int ksg_last_batch_host_us(ksg_ctx* c, double* out8) {
+  if (!c || !out8) return KSG_ERR_ARG;
+  KSG_LOCK(c);
+  for (int k = 0; k < 8; ++k) out8[k] = c->last_hus[k];
   return KSG_OK;
 }
 

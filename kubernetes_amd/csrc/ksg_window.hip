@@ -2721,11 +2721,13 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
   for (uint32_t i = 0; i < n_pods; ++i) {
     const uint32_t e = i % RING, par = i & 1;
-    if (ld_acq(&r_hdr[e].ready) != i + 1) {
+    // (relaxed polls, then one LDS-only acquire: an acquire load also waits for
+    // the previous pod's stores in flight)
+    if (ld_u(&r_hdr[e].ready) != i + 1) {
       __builtin_amdgcn_s_setprio(0);  // a producer shares this SIMD: do not starve it
       bool hung = false;
-      for (uint32_t spin = 0; ld_acq(&r_hdr[e].ready) != i + 1; ++spin)
-        if (spin > 16 * KSG_SPIN_LIMIT || ld_acq(&ctl->hang)) {
+      for (uint32_t spin = 0; ld_u(&r_hdr[e].ready) != i + 1; ++spin)
+        if (spin > 16 * KSG_SPIN_LIMIT || ld_u(&ctl->hang)) {
           hung = true;
           break;
         }
@@ -2735,6 +2737,11 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         reason = KSG_STOP_HANG;
         break;
       }
+    }
+    acq_lds();
+    if constexpr (STAMP) {  // ring wait of the window's first 4 pods (lane 10) vs the rest (lane 11)
+      const uint64_t t_now = __builtin_amdgcn_s_memtime();
+      t_acc += lane == (i < 4 ? 10u : 11u) ? t_now - t_last : 0ULL;
     }
     KSG_STAMP2(0)
     // ---- the staged pod: record, header, T0 words, r mod (k0 - d) (one round of LDS reads)

@@ -262,6 +262,15 @@ class DeviceScheduler:
         self._lib.ksg_last_batch_kernel_ms(self._ctx, abi.ptr(o))
         return {"eval_ms": float(o[0]), "resolve_ms": float(o[1]), "launches": int(o[2])}
 
+    HOST_PHASES = ("validate", "upload", "setup", "enqueue", "mirror_replay", "round_wait", "final_wait",
+                   "bookkeeping")
+
+    def last_batch_host_us(self) -> dict:
+        """Host microseconds of the last batch by phase (ksg_last_batch_host_us)."""
+        o = np.zeros(8, np.float64)
+        self._lib.ksg_last_batch_host_us(self._ctx, abi.ptr(o))
+        return {k: float(v) for k, v in zip(self.HOST_PHASES, o)}
+
     def debug_counters(self) -> np.ndarray:
         """KSG_DEBUG=8 contexts: the window resolver's per-stage cycle counters
         (cycles / 64, summed over every window so far)."""

@@ -200,6 +200,35 @@ def test_batch_rejects_duplicate_uids_and_keeps_mirror():
     dev.close()
 
 
+def test_batch_uid_reuse_after_no_fit_and_in_batch_duplicates():
+    """The deferred-replay uid set: a pod that found no node leaves its uid free
+    for a later batch (an unschedulable pod's retry); two placed pods of one batch
+    with the same uid fail the call."""
+    from kubernetes_amd.engine import KsgError
+
+    case = Case("config2", 300, 200)
+    for window in (0, 128):
+        dev, orc = _pair(case, window)
+        dev.set_cluster(case.view.arrays)
+        orc.set_cluster(case.view.arrays)
+        first = case.batch.pods[:40].copy()
+        first[7]["milli_cpu"] = 10**13  # fits no node
+        got, st = dev.batch(PodBatch(first, case.batch.ids), 11)
+        want, sw = orc.batch(PodBatch(first, case.batch.ids), 11)
+        assert np.array_equal(got, want) and st == sw
+        assert got[7] == abi.KSG_OUT_NOFIT
+        retry = case.batch.pods[40:80].copy()
+        retry[0] = case.batch.pods[7]  # the same uid, now with a request that fits
+        g2, st = dev.batch(PodBatch(retry, case.batch.ids), st)
+        w2, sw = orc.batch(PodBatch(retry, case.batch.ids), sw)
+        assert np.array_equal(g2, w2) and st == sw and g2[0] >= 0
+        dup = case.batch.pods[80:90].copy()
+        dup[5] = dup[2]
+        with pytest.raises(KsgError):
+            dev.batch(PodBatch(dup, case.batch.ids), st)
+        dev.close()
+
+
 _BIG = {}
 
 
