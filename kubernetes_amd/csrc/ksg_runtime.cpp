@@ -151,6 +151,10 @@ struct ksg_ctx {
 
   // host mirror
   std::vector<int64_t> used_c, used_m;
+  // max over nodes of used_c / used_m for use_window: raised by each mirror add,
+  // recomputed after anything else changes them (a removal, a negative total)
+  int64_t mu_max = 0;
+  bool mu_neg = false, mu_dirty = true;
   std::unordered_map<uint64_t, uint32_t> key_ref;  // (key << 32) | node
   std::vector<int32_t> svc_cnt;                    // S*N
   std::vector<std::unordered_map<uint32_t, int32_t>> svc_ext;
@@ -356,6 +360,8 @@ int mirror_add(ksg_ctx* c, uint32_t h, const ksg_pod* p, const uint32_t* ids, bo
   if (h < c->N) {
     c->used_c[h] = (int64_t)((uint64_t)c->used_c[h] + (uint64_t)r.cpu);
     c->used_m[h] = (int64_t)((uint64_t)c->used_m[h] + (uint64_t)r.mem);
+    if (c->mu_neg || c->used_c[h] < 0 || c->used_m[h] < 0) c->mu_dirty = true;
+    else c->mu_max = std::max(c->mu_max, std::max(c->used_c[h], c->used_m[h]));
     if (emit) {
       patch64(c, c->dev.used_cpu + h, c->used_c[h]);
       patch64(c, c->dev.used_mem + h, c->used_m[h]);
@@ -392,6 +398,7 @@ int mirror_add(ksg_ctx* c, uint32_t h, const ksg_pod* p, const uint32_t* ids, bo
 
 void reset_mirror(ksg_ctx* c) {
   c->used_c.assign(c->N, 0);
+  c->mu_dirty = true;
   c->used_m.assign(c->N, 0);
   c->sc_used.assign((size_t)c->ext.n_scalar * c->N, 0);
   c->ext_scalar.clear();
@@ -610,11 +617,17 @@ bool use_window(ksg_ctx* c, const ksg_pod* pods, uint32_t n) {
   // lr_win (ksg_device.h) is exact for 0 <= capacity, requested totals <= 2^49
   const int64_t lim = KSG_WIN_LR_BOUND;
   if (c->max_cap > lim || c->min_cap < 0) return false;
-  int64_t mu = 0;
-  for (uint32_t i = 0; i < c->N; ++i) {
-    if (c->used_c[i] < 0 || c->used_m[i] < 0) return false;
-    mu = std::max<int64_t>(mu, std::max<int64_t>(c->used_c[i], c->used_m[i]));
+  if (c->mu_dirty) {
+    c->mu_max = 0;
+    c->mu_neg = false;
+    for (uint32_t i = 0; i < c->N; ++i) {
+      c->mu_neg |= c->used_c[i] < 0 || c->used_m[i] < 0;
+      c->mu_max = std::max<int64_t>(c->mu_max, std::max<int64_t>(c->used_c[i], c->used_m[i]));
+    }
+    c->mu_dirty = false;
   }
+  if (c->mu_neg) return false;
+  const int64_t mu = c->mu_max;
   // commits not yet in the mirror (non-negative: checked by the caller) only add
   int64_t sum = c->dfr_sum;
   for (uint32_t i = 0; i < n; ++i) {
@@ -1090,6 +1103,7 @@ static int remove_pod_impl(ksg_ctx* c, uint64_t uid) {
   if (h < c->N) {
     c->used_c[h] = (int64_t)((uint64_t)c->used_c[h] - (uint64_t)r.cpu);
     c->used_m[h] = (int64_t)((uint64_t)c->used_m[h] - (uint64_t)r.mem);
+    c->mu_dirty = true;
     patch64(c, c->dev.used_cpu + h, c->used_c[h]);
     patch64(c, c->dev.used_mem + h, c->used_m[h]);
     if (c->ext_on)
