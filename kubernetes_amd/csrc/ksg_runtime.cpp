@@ -104,6 +104,9 @@ struct ksg_ctx {
   uint8_t *h_xsend = nullptr, *h_xrecv = nullptr;
   size_t h_xsend_cap = 0, h_xrecv_cap = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // the batch path's waits spin on this event (KSG_SPIN_WAIT=0: hipStreamSynchronize)
+  hipEvent_t ev_wait = nullptr;
+  bool spin_wait = true;
   double last_ms = 0.0;
   std::string err;
 
@@ -657,6 +660,22 @@ int flush_deferred(ksg_ctx* c) {
 
 int ensure_out(ksg_ctx* c, size_t n) { return grow(c, (void**)&c->d_out, &c->out_cap, n, sizeof(int32_t)); }
 
+// Waits for the stream's work so far. The batch path's host thread has nothing
+// left to do at this point, so it polls an event instead of sleeping in
+// hipStreamSynchronize, whose wake-up lands on the per-batch critical path.
+int wait_device(ksg_ctx* c) {
+  if (!c->spin_wait || !c->ev_wait) {
+    HIPCHK(c, hipStreamSynchronize(c->st));
+    return KSG_OK;
+  }
+  HIPCHK(c, hipEventRecord(c->ev_wait, c->st));
+  hipError_t e;
+  while ((e = hipEventQuery(c->ev_wait)) == hipErrorNotReady) {
+  }
+  if (e != hipSuccess) return fail(c, KSG_ERR_HIP, "hipEventQuery: %s", hipGetErrorString(e));
+  return KSG_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -752,8 +771,10 @@ static int create_impl(const ksg_config* cfg, int device, int rank, int world, c
   if (e != hipSuccess) return bail(fail(c, KSG_ERR_HIP, "hipSetDevice(%d): %s", device, hipGetErrorString(e)));
   if ((e = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&c->ev0, kTimingEvent)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&c->ev1, kTimingEvent)) != hipSuccess)
+      (e = hipEventCreateWithFlags(&c->ev1, kTimingEvent)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&c->ev_wait, hipEventDisableTiming)) != hipSuccess)
     return bail(fail(c, KSG_ERR_HIP, "stream/event: %s", hipGetErrorString(e)));
+  c->spin_wait = !(getenv("KSG_SPIN_WAIT") && atoi(getenv("KSG_SPIN_WAIT")) == 0);
   // The exchange path (shard scan, all-gather of per-shard records, replicated
   // resolve) runs for world > 1, and for a 1-rank RCCL communicator when the caller
   // passes an nccl_id with world == 1 (RCCL itself exercised on a single GPU).
@@ -823,6 +844,7 @@ int ksg_destroy(ksg_ctx* c) {
   if (c->h_xrecv) (void)hipHostFree(c->h_xrecv);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->ev_wait) (void)hipEventDestroy(c->ev_wait);
   for (auto& e : c->wev)
     if (e) (void)hipEventDestroy(e);
   if (c->st) (void)hipStreamDestroy(c->st);
@@ -1449,7 +1471,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       if ((rc = enqueue_tail())) return rc;
       hphase(3);
       if ((rc = overlap_work())) return rc;  // the host mirror catches up while the device works
-      HIPCHK(c, hipStreamSynchronize(c->st));
+      if ((rc = wait_device(c))) return rc;
       hphase(5);
       const KsgWinRun r = *c->h_run;
       if (r.windows > 0 && r.pos > pos) {  // pods per window, smoothed over rounds and batches
@@ -1514,7 +1536,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     if ((rc = enqueue_tail())) return rc;
     hphase(3);
     if ((rc = overlap_work())) return rc;
-    HIPCHK(c, hipStreamSynchronize(c->st));
+    if ((rc = wait_device(c))) return rc;
     hphase(6);
   }
   memcpy(out_nodes, c->h_dn, (size_t)n * 4);
