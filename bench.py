@@ -296,7 +296,10 @@ def main():
         # stay in L2 across pod groups, so per-(node, pod) bytes overstate it)
         ev_s = kk["eval_ms"] / launches / 1e3 or float("nan")
         ev_bytes = bpn * (n_nodes / world) + wcap * (nwords / world) * 12 + wcap * 192
+        # (HIP events around every timed_launch_stride-th launch of a round, the
+        # sampled mean scaled to all launches; KSG_KERNEL_EVENTS=N sets the stride)
         extra = {"launches": launches, "pods_per_launch": pods_per_launch,
+                 "timed_launch_stride": int(os.environ.get("KSG_KERNEL_EVENTS", "4") or 0),
                  "win_eval_ms_avg": kk["eval_ms"] / launches,
                  "win_eval_model_bytes_per_launch": ev_bytes,
                  "win_eval_model_GBps": ev_bytes / ev_s / 1e9,

@@ -168,7 +168,11 @@ struct ksg_ctx {
 
   // window (speculative) path
   uint32_t window = 128;        // 0 = exact one-pod-at-a-time kernel
-  bool kernel_events = true;    // HIP events around each window kernel (KSG_KERNEL_EVENTS=0: off)
+  // HIP events around every ev_stride-th window launch (phase A and resolver;
+  // KSG_KERNEL_EVENTS=N: every N-th, 0: none). An event between two dependent
+  // launches lengthens the gap between them, so a sample of the windows is timed
+  // and the per-launch mean scaled to all launches (ksg_last_batch_kernel_ms).
+  uint32_t ev_stride = 4;
   KsgWinSum* d_winsum = nullptr;
   uint8_t* d_xsend = nullptr;   // phase A block of this shard (KsgWinXchg layout)
   uint8_t* d_xrecv = nullptr;   // all-gathered blocks of every shard (world > 1)
@@ -790,7 +794,7 @@ static int create_impl(const ksg_config* cfg, int device, int rank, int world, c
   }
   int rc;
   if (const char* wenv = getenv("KSG_WINDOW")) c->window = (uint32_t)atoi(wenv);
-  if (const char* kev = getenv("KSG_KERNEL_EVENTS")) c->kernel_events = atoi(kev) != 0;
+  if (const char* kev = getenv("KSG_KERNEL_EVENTS")) c->ev_stride = (uint32_t)std::max(atoi(kev), 0);
   if ((rc = dalloc(c, &c->d_rng, 1, nullptr)) || (rc = dalloc(c, &c->d_summary, 4, nullptr)) ||
       (rc = dalloc(c, &c->d_run, 1, nullptr)))
     return bail(rc);
@@ -1449,7 +1453,9 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       HIPCHK(c, hipMemcpyAsync(c->d_run, c->h_run, sizeof(KsgWinRun), hipMemcpyHostToDevice, c->st));
       HIPCHK(c, hipEventRecord(c->wev[0], c->st));
       for (uint32_t k = 0; k < K; ++k) {
-        // HIP events on this stream around each kernel (per-kernel device time)
+        // HIP events on this stream around the sampled launches (per-kernel device time)
+        const bool evk = c->ev_stride && k % c->ev_stride == 0;
+        if (evk && k > 0) HIPCHK(c, hipEventRecord(c->wev[2 * k], c->st));
         if (anti) {
           // ServiceAntiAffinity: the pods' per-domain counts over their filtered nodes first
           // (into d_dcnt, zero: the previous resolver cleared it)
@@ -1463,9 +1469,9 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
                                       rr ? reinterpret_cast<uint64_t*>(c->d_xsend + x.b_off) : nullptr, x.dz,
                                       c->st));
         if (c->xchg && (rc = allgather(c, c->d_xsend, c->d_xrecv, x.blk))) return rc;
-        if (c->kernel_events) HIPCHK(c, hipEventRecord(c->wev[2 * k + 1], c->st));
+        if (evk) HIPCHK(c, hipEventRecord(c->wev[2 * k + 1], c->st));
         HIPCHK(c, ksg_launch_win_resolve(full, W, c->d_run, c->d_winsum, x, c->d_rng, c->d_out, c->st));
-        if (c->kernel_events) HIPCHK(c, hipEventRecord(c->wev[2 * k + 2], c->st));
+        if (evk) HIPCHK(c, hipEventRecord(c->wev[2 * k + 2], c->st));
       }
       HIPCHK(c, hipMemcpyAsync(c->h_run, c->d_run, sizeof(KsgWinRun), hipMemcpyDeviceToHost, c->st));
       if ((rc = enqueue_tail())) return rc;
@@ -1479,14 +1485,22 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
         ppw_est = ppw_est > 0.0 ? 0.5 * ppw_est + 0.5 * ppw : ppw;
         if (!c->xchg) c->ppw_est = ppw_est;
       }
-      // every launch of the round, including the ones after the batch was done
-      // (they return at once), so the mean matches a kernel trace of the run
-      for (uint32_t k = 0; k < K && c->kernel_events; ++k) {
+      // the sampled launches (every one of the round's launches is a sampling
+      // candidate, including the ones after the batch was done, which return at
+      // once, so the mean matches a kernel trace of the run), scaled to all K
+      double ea = 0.0, eb = 0.0;
+      uint32_t nt = 0;
+      for (uint32_t k = 0; c->ev_stride && k < K; k += c->ev_stride) {
         float a = 0.f, b = 0.f;
         HIPCHK(c, hipEventElapsedTime(&a, c->wev[2 * k], c->wev[2 * k + 1]));
         HIPCHK(c, hipEventElapsedTime(&b, c->wev[2 * k + 1], c->wev[2 * k + 2]));
-        c->last_kms[0] += a;
-        c->last_kms[1] += b;
+        ea += a;
+        eb += b;
+        ++nt;
+      }
+      if (nt) {
+        c->last_kms[0] += ea * K / nt;
+        c->last_kms[1] += eb * K / nt;
       }
       c->last_kms[2] += K;
       c->last_stats[0] += r.windows;

@@ -229,6 +229,25 @@ def test_batch_uid_reuse_after_no_fit_and_in_batch_duplicates():
         dev.close()
 
 
+def test_kernel_time_sampling_strides(monkeypatch):
+    """ksg_last_batch_kernel_ms: HIP events around every N-th window launch
+    (KSG_KERNEL_EVENTS=N at context creation), scaled to all launches; 0 times
+    nothing. The decisions never depend on it."""
+    case = Case("config2", 600, 400)
+    res = {}
+    for stride in ("1", "4", "0"):
+        monkeypatch.setenv("KSG_KERNEL_EVENTS", stride)
+        dev, orc = _pair(case, 128)
+        got, sg = run_batch(dev, case)
+        res[stride] = (got, sg, dev.last_batch_kernel_ms())
+        dev.close()
+    assert all(np.array_equal(res["1"][0], r[0]) and res["1"][1] == r[1] for r in res.values())
+    for stride in ("1", "4"):
+        k = res[stride][2]
+        assert k["launches"] > 0 and k["resolve_ms"] > 0 and k["eval_ms"] > 0
+    assert res["0"][2]["resolve_ms"] == 0 and res["0"][2]["launches"] > 0
+
+
 _BIG = {}
 
 
