@@ -225,24 +225,23 @@ def main():
             dist.barrier()
         _torch_sync()
 
+    # the library's per-batch diagnostics (device ms, kernel ms from the HIP
+    # events, window stats, host phases) accumulate in the context: read once
+    # on each side of the timed steps (ksg_batch_totals), not after every step
+    tot0 = sched.batch_totals()
     barrier()
     t_start = time.perf_counter()
-    kern_ms = []
-    host_us = {}
-    kk = {"eval_ms": 0.0, "resolve_ms": 0.0, "launches": 0}
-    wstats = {"windows": 0, "stops_service": 0, "stops_exhausted": 0, "stops_cache": 0}
     for s in range(args.warmup, args.warmup + args.steps):
         o, rng = sched.batch(step_batch(s), rng)
-        kern_ms.append(sched.last_batch_ms())
-        for k_, v_ in sched.last_batch_host_us().items():
-            host_us[k_] = host_us.get(k_, 0.0) + v_
-        for k_, v_ in sched.last_batch_kernel_ms().items():
-            kk[k_] += v_
-        for k_, v_ in sched.last_batch_stats().items():
-            wstats[k_] += v_
         outs.append(o)
     barrier()
     elapsed = time.perf_counter() - t_start
+    tot1 = sched.batch_totals()
+    assert tot1["batches"] - tot0["batches"] == args.steps
+    kern_ms = [(tot1["device_ms"] - tot0["device_ms"]) / args.steps]
+    host_us = {k_: tot1["host_us"][k_] - tot0["host_us"][k_] for k_ in tot1["host_us"]}
+    kk = {k_: tot1[k_] - tot0[k_] for k_ in ("eval_ms", "resolve_ms", "launches")}
+    wstats = {k_: tot1[k_] - tot0[k_] for k_ in ("windows", "stops_service", "stops_exhausted", "stops_cache")}
     if dist is not None:
         import torch
 

@@ -274,6 +274,13 @@ int ksg_last_batch_kernel_ms(ksg_ctx* ctx, double* out3);
  * [7] the deferred-replay bookkeeping. No reference counterpart (diagnostics). */
 int ksg_last_batch_host_us(ksg_ctx* ctx, double* out8);
 
+/* The per-batch diagnostics above summed over every successful
+ * ksg_schedule_batch since the context was created, so a caller can read them
+ * once around a run instead of after each batch: out24[0] batches, [1] device
+ * ms (ksg_last_batch_ms), [2..4] ksg_last_batch_kernel_ms, [5..8]
+ * ksg_last_batch_stats, [9..16] ksg_last_batch_host_us, [17..23] zero. */
+int ksg_batch_totals(ksg_ctx* ctx, double* out24);
+
 /* Diagnostics: the window resolver's per-stage clock counters (s_memtime
  * cycles / 64, summed over every window since the context was created) for a
  * context created with KSG_DEBUG=8 in the environment; out32[32] (layout:

@@ -193,6 +193,7 @@ EXPORTS = [
     "ksg_last_batch_ms",
     "ksg_last_batch_kernel_ms",
     "ksg_last_batch_host_us",
+    "ksg_batch_totals",
     "ksg_debug_counters",
     "ksg_shard",
     "ksg_read_requested",
@@ -256,6 +257,7 @@ def load_library() -> C.CDLL:
         "ksg_last_batch_ms": (C.c_int, [vp, P(C.c_double)]),
         "ksg_last_batch_kernel_ms": (C.c_int, [vp, vp]),
         "ksg_last_batch_host_us": (C.c_int, [vp, vp]),
+        "ksg_batch_totals": (C.c_int, [vp, vp]),
         "ksg_debug_counters": (C.c_int, [vp, vp]),
         "ksg_shard": (C.c_int, [vp, P(U32), P(U32)]),
         "ksg_read_requested": (C.c_int, [vp, vp, vp]),

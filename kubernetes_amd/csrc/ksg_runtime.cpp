@@ -186,6 +186,7 @@ struct ksg_ctx {
   std::vector<hipEvent_t> wev;     // event pairs around the chained window kernels
   double last_kms[3] = {0, 0, 0};  // phase A ms, phase B ms, launches (window path)
   double last_hus[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // host us per phase of the last batch (ksg_last_batch_host_us)
+  double totals[24] = {};  // ksg_batch_totals: the per-batch diagnostics summed over batches
   int64_t max_cap = 0, min_cap = 0;
 
   // Commits of the last ksg_schedule_batch not yet replayed into the host
@@ -1576,6 +1577,12 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
                                                                         KSG_WIN_LR_BOUND), KSG_WIN_LR_BOUND + 1);
   }
   hphase(7);
+  double* t = c->totals;  // (layout: ksg_batch_totals in kschedgpu.h)
+  t[0] += 1;
+  t[1] += c->last_ms;
+  for (int q = 0; q < 3; ++q) t[2 + q] += c->last_kms[q];
+  for (int q = 0; q < 4; ++q) t[5 + q] += c->last_stats[q];
+  for (int q = 0; q < 8; ++q) t[9 + q] += c->last_hus[q];
   return KSG_OK;
 }
 
@@ -1635,6 +1642,13 @@ int ksg_last_batch_kernel_ms(ksg_ctx* c, double* out3) {
   if (!c || !out3) return KSG_ERR_ARG;
   KSG_LOCK(c);
   for (int i = 0; i < 3; ++i) out3[i] = c->last_kms[i];
+  return KSG_OK;
+}
+
+int ksg_batch_totals(ksg_ctx* c, double* out24) {
+  if (!c || !out24) return KSG_ERR_ARG;
+  KSG_LOCK(c);
+  for (int k = 0; k < 24; ++k) out24[k] = c->totals[k];
   return KSG_OK;
 }
 

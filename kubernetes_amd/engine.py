@@ -271,6 +271,15 @@ class DeviceScheduler:
         self._lib.ksg_last_batch_host_us(self._ctx, abi.ptr(o))
         return {k: float(v) for k, v in zip(self.HOST_PHASES, o)}
 
+    def batch_totals(self) -> dict:
+        """The per-batch diagnostics summed over every batch so far (ksg_batch_totals)."""
+        o = np.zeros(24, np.float64)
+        self._lib.ksg_batch_totals(self._ctx, abi.ptr(o))
+        return {"batches": int(o[0]), "device_ms": float(o[1]), "eval_ms": float(o[2]),
+                "resolve_ms": float(o[3]), "launches": int(o[4]), "windows": int(o[5]),
+                "stops_service": int(o[6]), "stops_exhausted": int(o[7]), "stops_cache": int(o[8]),
+                "host_us": {k: float(v) for k, v in zip(self.HOST_PHASES, o[9:17])}}
+
     def debug_counters(self) -> np.ndarray:
         """KSG_DEBUG=8 contexts: the window resolver's per-stage cycle counters
         (cycles / 64, summed over every window so far)."""

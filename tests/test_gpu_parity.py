@@ -248,6 +248,26 @@ def test_kernel_time_sampling_strides(monkeypatch):
     assert res["0"][2]["resolve_ms"] == 0 and res["0"][2]["launches"] > 0
 
 
+def test_batch_totals_sum_the_per_batch_diagnostics():
+    """ksg_batch_totals = the per-batch diagnostics summed over batches."""
+    case = Case("config2", 500, 300)
+    dev, _ = _pair(case, 128)
+    dev.set_cluster(case.view.arrays)
+    t0 = dev.batch_totals()
+    assert t0["batches"] == 0 and t0["device_ms"] == 0.0
+    rng, dms, res, win = 3, 0.0, 0.0, 0
+    for s in (0, 150):
+        _, rng = dev.batch(PodBatch(case.batch.pods[s:s + 150], case.batch.ids), rng)
+        dms += dev.last_batch_ms()
+        res += dev.last_batch_kernel_ms()["resolve_ms"]
+        win += dev.last_batch_stats()["windows"]
+    t1 = dev.batch_totals()
+    assert t1["batches"] == 2 and win == t1["windows"] > 0
+    assert abs(t1["device_ms"] - dms) < 1e-9 and abs(t1["resolve_ms"] - res) < 1e-9
+    assert t1["host_us"]["validate"] > 0
+    dev.close()
+
+
 _BIG = {}
 
 
