@@ -258,10 +258,10 @@ int ksg_last_batch_ms(ksg_ctx* ctx, double* ms);
  * resolver (ksg_win_resolve_kernel), out3[2] = resolver launches (windows are
  * chained on the device, so a round may end with launches that find the batch
  * done and return at once); from HIP events recorded on the context's stream
- * around every 4th launch of a round (KSG_KERNEL_EVENTS=N in the environment at
- * context creation: every N-th, 0: none), the sampled launches' mean scaled to
- * all launches: an event between two dependent launches lengthens the gap
- * between them. */
+ * around every 4th launch of a round, the sampled positions rotating from round
+ * to round (KSG_KERNEL_EVENTS=N in the environment at context creation: every
+ * N-th, 0: none), the sampled launches' mean scaled to all launches: an event
+ * between two dependent launches lengthens the gap between them. */
 int ksg_last_batch_kernel_ms(ksg_ctx* ctx, double* out3);
 
 /* Host time (microseconds, steady clock) of the last ksg_schedule_batch by

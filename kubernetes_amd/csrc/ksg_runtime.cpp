@@ -173,6 +173,7 @@ struct ksg_ctx {
   // launches lengthens the gap between them, so a sample of the windows is timed
   // and the per-launch mean scaled to all launches (ksg_last_batch_kernel_ms).
   uint32_t ev_stride = 4;
+  uint32_t ev_phase = 0;  // which launches of a round are timed; advances every round
   KsgWinSum* d_winsum = nullptr;
   uint8_t* d_xsend = nullptr;   // phase A block of this shard (KsgWinXchg layout)
   uint8_t* d_xrecv = nullptr;   // all-gathered blocks of every shard (world > 1)
@@ -1450,12 +1451,17 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
         c->wev.resize(2 * (size_t)K + 1, nullptr);
         for (size_t i = old; i < c->wev.size(); ++i) HIPCHK(c, hipEventCreateWithFlags(&c->wev[i], kTimingEvent));
       }
+      // the sampled launches rotate from round to round (launches k with
+      // (k + ev_off) % es == 0), so every position in a round, the no-op
+      // launches after the batch's end included, is timed equally often
+      const uint32_t es = std::min(c->ev_stride, K);  // (a short round still times one launch)
+      const uint32_t ev_off = es ? c->ev_phase++ % es : 0u;
       *c->h_run = KsgWinRun{pos, n, 0, 0, {0, 0, 0, 0}};
       HIPCHK(c, hipMemcpyAsync(c->d_run, c->h_run, sizeof(KsgWinRun), hipMemcpyHostToDevice, c->st));
       HIPCHK(c, hipEventRecord(c->wev[0], c->st));
       for (uint32_t k = 0; k < K; ++k) {
         // HIP events on this stream around the sampled launches (per-kernel device time)
-        const bool evk = c->ev_stride && k % c->ev_stride == 0;
+        const bool evk = es && (k + ev_off) % es == 0;
         if (evk && k > 0) HIPCHK(c, hipEventRecord(c->wev[2 * k], c->st));
         if (anti) {
           // ServiceAntiAffinity: the pods' per-domain counts over their filtered nodes first
@@ -1491,7 +1497,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       // once, so the mean matches a kernel trace of the run), scaled to all K
       double ea = 0.0, eb = 0.0;
       uint32_t nt = 0;
-      for (uint32_t k = 0; c->ev_stride && k < K; k += c->ev_stride) {
+      for (uint32_t k = es ? (es - ev_off) % es : 0u; es && k < K; k += es) {
         float a = 0.f, b = 0.f;
         HIPCHK(c, hipEventElapsedTime(&a, c->wev[2 * k], c->wev[2 * k + 1]));
         HIPCHK(c, hipEventElapsedTime(&b, c->wev[2 * k + 1], c->wev[2 * k + 2]));
