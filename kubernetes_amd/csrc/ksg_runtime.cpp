@@ -92,6 +92,9 @@ struct ksg_ctx {
   ncclComm_t comm = nullptr;
   bool xchg = false;
   double ppw_est = 0.0;  // pods resolved per window (window path round sizing)
+  // windows per round = margin x (pods left) / ppw_est + 1 (KSG_ROUND_MARGIN): the
+  // launches past the batch's end cost ~8 us each, a second round a host round trip
+  double round_margin = 1.0;
   // pinned staging for the per-call uploads / small read-backs (a pageable
   // hipMemcpyAsync is a staged, effectively synchronous copy)
   uint8_t* h_up = nullptr;
@@ -781,6 +784,7 @@ static int create_impl(const ksg_config* cfg, int device, int rank, int world, c
       (e = hipEventCreateWithFlags(&c->ev_wait, hipEventDisableTiming)) != hipSuccess)
     return bail(fail(c, KSG_ERR_HIP, "stream/event: %s", hipGetErrorString(e)));
   c->spin_wait = !(getenv("KSG_SPIN_WAIT") && atoi(getenv("KSG_SPIN_WAIT")) == 0);
+  if (const char* rm = getenv("KSG_ROUND_MARGIN")) c->round_margin = std::min(std::max(atof(rm), 0.5), 4.0);
   // The exchange path (shard scan, all-gather of per-shard records, replicated
   // resolve) runs for world > 1, and for a 1-rank RCCL communicator when the caller
   // passes an nccl_id with world == 1 (RCCL itself exercised on a single GPU).
@@ -1439,7 +1443,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     double ppw_est = c->xchg ? 0.0 : c->ppw_est;
     auto round_k = [&](uint32_t left) -> uint32_t {
       const double ppw = ppw_est > 0.0 ? std::min<double>(std::max(ppw_est, 1.0), (double)W) : 0.8 * W;
-      const double k = std::ceil((double)left / ppw * 1.1) + 1.0;
+      const double k = std::ceil((double)left / ppw * c->round_margin) + 1.0;
       return (uint32_t)std::min(k, 8192.0);
     };
     uint32_t pos = 0, K = round_k(n);
