@@ -48,7 +48,13 @@
 #include <algorithm>
 
 #define KSG_SC_NT 256  // phase A: 4 waves, one 64-node word each
-#define KSG_PG 8       // phase A: pods per wave
+// phase A: pods per wave. 4 below 512 words per shard (32k nodes): the grid has
+// (words / 4) x (W / PG) workgroups, too few to cover the latency at 8 pods per
+// wave (config 2: 320 workgroups on 256 CUs); 8 above, where the grid is large
+// and the node state each wave loads is shared by more pods
+#define KSG_PG_SMALL 4
+#define KSG_PG_LARGE 8
+#define KSG_PG_WORDS 512
 
 // dword offsets inside KsgWinSum (lane j of the resolver holds dword j)
 #define WS_ERR 2
@@ -77,7 +83,7 @@
 #define KSG_WIN_PLAIN 0
 #define KSG_WIN_COUNT 1
 #define KSG_WIN_ANTI 2
-template <int MODE>
+template <int MODE, int KSG_PG>
 __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, const ksg_pod* __restrict__ batch,
                                                                  const uint32_t* __restrict__ ids,
                                                                  const KsgWinRun* __restrict__ run, uint32_t wcap,
@@ -5265,16 +5271,23 @@ hipError_t ksg_launch_win_eval(const KsgDev& d, int mode, const ksg_pod* batch, 
                                uint32_t ostride, int32_t* dcnt, uint64_t* wfit, int32_t* dmb, uint64_t* wbz,
                                uint32_t dz, hipStream_t st) {
   const uint32_t gx = std::max<uint32_t>(1, (d.nwords + KSG_SC_NT / 64 - 1) / (KSG_SC_NT / 64));
-  const dim3 grid(gx, (wcap + KSG_PG - 1) / KSG_PG);
-  if (mode == KSG_WIN_COUNT)
-    hipLaunchKernelGGL(ksg_win_score_kernel<KSG_WIN_COUNT>, grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, run, wcap,
-                       sums, wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz);
-  else if (mode == KSG_WIN_ANTI)
-    hipLaunchKernelGGL(ksg_win_score_kernel<KSG_WIN_ANTI>, grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, run, wcap,
-                       sums, wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz);
-  else
-    hipLaunchKernelGGL(ksg_win_score_kernel<KSG_WIN_PLAIN>, grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, run, wcap,
-                       sums, wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz);
+  const bool small = d.nwords < KSG_PG_WORDS;
+  const uint32_t pg = small ? KSG_PG_SMALL : KSG_PG_LARGE;
+  const dim3 grid(gx, (wcap + pg - 1) / pg);
+#define KSG_EVAL_LAUNCH(M, G)                                                                                    \
+  hipLaunchKernelGGL((ksg_win_score_kernel<M, G>), grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, run, wcap, sums, \
+                     wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz)
+  if (mode == KSG_WIN_COUNT) {
+    if (small) KSG_EVAL_LAUNCH(KSG_WIN_COUNT, KSG_PG_SMALL);
+    else KSG_EVAL_LAUNCH(KSG_WIN_COUNT, KSG_PG_LARGE);
+  } else if (mode == KSG_WIN_ANTI) {
+    if (small) KSG_EVAL_LAUNCH(KSG_WIN_ANTI, KSG_PG_SMALL);
+    else KSG_EVAL_LAUNCH(KSG_WIN_ANTI, KSG_PG_LARGE);
+  } else {
+    if (small) KSG_EVAL_LAUNCH(KSG_WIN_PLAIN, KSG_PG_SMALL);
+    else KSG_EVAL_LAUNCH(KSG_WIN_PLAIN, KSG_PG_LARGE);
+  }
+#undef KSG_EVAL_LAUNCH
   return hipGetLastError();
 }
 
