@@ -78,6 +78,40 @@ _STAGES2 = {
 }
 
 
+# the plain resolver (every configuration without ServiceAntiAffinity, ksg_plain.hip)
+_STAGES_PLAIN = {
+    0: ("committer", "ring_wait"), 1: ("committer", "head"),
+    2: ("committer", "wait_checkers_and_xcheck"), 3: ("committer", "select_and_node_post"),
+    4: ("committer", "slot"), 5: ("committer", "commit"),
+    6: ("handoff", "xcheck_to_committer"), 31: ("handoff", "node_to_xchecker"),
+    10: ("committer", "ring_wait_first4"), 11: ("committer", "ring_wait_rest"),
+    16: ("checker0", "wait"), 17: ("checker0", "apply"), 18: ("checker0", "check"),
+    19: ("checker1", "wait"), 20: ("checker1", "apply"), 21: ("checker1", "check"),
+    24: ("producers_sum_over_waves", "ring_wait"), 25: ("producers_sum_over_waves", "loads"),
+    26: ("producers_sum_over_waves", "draw_wait"), 27: ("producers_sum_over_waves", "stage"),
+    28: ("xchecker", "wait_node"), 29: ("xchecker", "flags"), 30: ("xchecker", "bookkeeping_and_lists"),
+}
+
+
+def _phase_a_bytes(cfg, pods, ns, nw, w):
+    """Algorithmic bytes of one phase-A launch (ksg_win_score_kernel) scoring w
+    pods on a shard of ns nodes / nw words: the node state once per wave (cap and
+    requested totals 32 B, the static score 4 B), per (pod, word) one 8-byte
+    predicate word per list entry of the pod (nodeSelector pairs, PDs, host
+    ports, ServiceAffinity pairs; the LabelsPresence word once per word), per
+    (pod, node) the pod's service count (4 B, when ServiceSpreading or
+    ServiceAntiAffinity is on), the per-(pod, word) best score + tie bitmap
+    written (12 B) and the pods' 192-byte records. The pods' list lengths are
+    the workload's means."""
+    n_list = float(np.mean(pods["n_sel"] + pods["n_pds"] + pods["n_ports"])) if len(pods) else 0.0
+    na = int(cfg.n_aff_labels)
+    n_list += float(np.mean((pods["aff_pair"][:, :na] >= 0).sum(axis=1))) if na and len(pods) else 0.0
+    frac_svc = float(np.mean(pods["service"] >= 0)) if len(pods) else 0.0
+    cnt_on = int(cfg.w_service_spreading) != 0 or any(int(cfg.w_anti[a]) != 0 for a in range(int(cfg.n_anti)))
+    return (36.0 * ns + 8.0 * nw + w * nw * 8.0 * n_list + (w * ns * 4.0 * frac_svc if cnt_on else 0.0)
+            + w * nw * 12.0 + w * 192.0)
+
+
 def _stage_breakdown(cfg, view, args, step_batch, anti):
     """Per-stage resolver cycles per pod from a KSG_DEBUG=8 context over the
     bench's first steps (untimed; the stamps cost a few percent)."""
@@ -111,7 +145,8 @@ def _stage_breakdown(cfg, view, args, step_batch, anti):
                 "note": "LDS-slot resolver (ServiceAntiAffinity): raw counters, layout in ksg_window.hip"}
     out = {"pods": pods, "unit": "cycles/pod",
            "drops_per_pod": float(c[7]) / 64 / pods, "unpredicted_per_pod": float(c[8]) / 64 / pods}
-    for lane, (role, st) in _STAGES2.items():
+    plain = not any(int(cfg.w_anti[a]) != 0 for a in range(int(cfg.n_anti)))
+    for lane, (role, st) in (_STAGES_PLAIN if plain else _STAGES2).items():
         out.setdefault(role, {})[st] = round(float(c[lane]) / pods, 1)
     return out
 
@@ -288,19 +323,20 @@ def main():
         # the in-order resolver: the LDS-slot one with ServiceAntiAffinity, else the
         # register-slot one (ksg_window.hip)
         kname = "ksg_win_resolve_kernel" if anti else "ksg_win_resolve2_kernel"
-        # phase A scores this rank's shard (N/world nodes) for the window's wcap pods;
-        # with world > 1 its event window also holds the per-window all-gather. Its
-        # bytes: the node state once per launch + the per-word bitmaps and maxima it
-        # writes + the pod records (its node loads are shared by a wave's 8 pods and
-        # stay in L2 across pod groups, so per-(node, pod) bytes overstate it)
+        # phase A scores this rank's shard (N/world nodes) for the window's W pods
+        # (the capacity the library used: it shrinks W where windows stop early);
+        # with world > 1 its event window also holds the per-window all-gather.
         ev_s = kk["eval_ms"] / launches / 1e3 or float("nan")
-        ev_bytes = bpn * (n_nodes / world) + wcap * (nwords / world) * 12 + wcap * 192
+        w_used = tot1["wcap_sum"] - tot0["wcap_sum"]
+        w_mean = w_used / launches if w_used > 0 else float(wcap)
+        ev_bytes = _phase_a_bytes(cfg, batch.pods, n_nodes / world, nwords / world, w_mean)
         # (HIP events around every timed_launch_stride-th launch of a round, the
         # sampled mean scaled to all launches; KSG_KERNEL_EVENTS=N sets the stride)
         extra = {"launches": launches, "pods_per_launch": pods_per_launch,
                  "timed_launch_stride": int(os.environ.get("KSG_KERNEL_EVENTS", "4") or 0),
                  "win_eval_ms_avg": kk["eval_ms"] / launches,
                  "win_eval_model_bytes_per_launch": ev_bytes,
+                 "win_eval_pods_per_launch": w_mean,
                  "win_eval_model_GBps": ev_bytes / ev_s / 1e9,
                  "win_eval_node_pod_evals_per_s": (n_nodes / world) * wcap / ev_s}
     else:

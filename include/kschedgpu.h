@@ -278,7 +278,9 @@ int ksg_last_batch_host_us(ksg_ctx* ctx, double* out8);
  * ksg_schedule_batch since the context was created, so a caller can read them
  * once around a run instead of after each batch: out24[0] batches, [1] device
  * ms (ksg_last_batch_ms), [2..4] ksg_last_batch_kernel_ms, [5..8]
- * ksg_last_batch_stats, [9..16] ksg_last_batch_host_us, [17..23] zero. */
+ * ksg_last_batch_stats, [9..16] ksg_last_batch_host_us, [17] the window
+ * capacity (pods phase A scores per launch) summed over the window-path
+ * launches, [18..23] zero. */
 int ksg_batch_totals(ksg_ctx* ctx, double* out24);
 
 /* Diagnostics: the window resolver's per-stage clock counters (s_memtime

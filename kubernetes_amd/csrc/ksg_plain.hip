@@ -1,0 +1,1224 @@
+// ksg_plain.hip — phase B of the window path (the in-order resolver) for every
+// configuration without ServiceAntiAffinity; ksg_window.hip has phase A and the
+// anti-affinity resolvers.
+//
+// Phase A scored the window's W pods against one snapshot: per (pod, 64-node
+// word) the word's best score and the bitmap of nodes at it. For pod i, M0 is
+// its best score and T0 the nodes at M0 (k0 of them). A commit can only make
+// its node worse for a later pod of the window whose service scalars it did not
+// change (requested totals grow, keys and service entries are only added), so
+// the reference's sequential answer (generic_scheduler.go:54-96) is the
+// ix-th node, from the top, of T0 minus the committed nodes ("slots") whose
+// score for pod i fell below M0 ("drops"), ix = Int63() mod (k0 - drops).
+//
+// One workgroup of 8 waves, pipelined over the window's pods:
+//  PRODUCERS (waves 4..7) stage pod j into ring entry j mod RING: its record,
+//    T0 by word with its prefix counts (T0 bits below each 64-word row and
+//    below each word inside its row: the ascending position of any node in T0
+//    is two LDS reads away), its draw r (splitmix64 at the pod's draw index =
+//    the drawable pods before it) and r mod (k0 - d) for d < 64, and six
+//    CANDIDATES: the nodes the draw lands on when 0, 1 or 2 ties drop (the
+//    (k0-1-r mod k0)-th tie ascending; the (k0-2-r mod (k0-1))-th and the next;
+//    the (k0-3-r mod (k0-2))-th and the two next), with their snapshots
+//    (capacity, requested totals, 10 / capacity) and the pod's service counts
+//    on them.
+//  CHECKERS (waves 2, 3; lane l of checker c owns slot 64c + l, its state in
+//    registers) check pod i once commit i-2 is published: apply commit i-2 to
+//    its slot (a new slot's snapshot from the candidate staging, else from L2),
+//    then test pod i against every slot in T0 as of commits <= i-2, and post
+//    the dropping slots (a 64-bit mask per checker) and each drop's position in
+//    T0.
+//  X-CHECKER (wave 1) re-checks pod i against the node x of commit i-1 as of
+//    that commit (the checkers' view lags a commit): x's snapshot from the
+//    candidate staging when x is a candidate (LDS; else from L2), x's window
+//    delta and lists from its own replay of the committer's slot bookkeeping
+//    (node -> slot, list lengths, delta) and the table row / pod i-1's record.
+//    It posts "x drops" and "commit i-1 raised a service scalar of the pod",
+//    then applies commit i-1's service flags in commit order (a ServiceSpreading
+//    maxCount rise or a ServiceAffinity first peer ends the window at the next
+//    pod of that service; the window's first peers are recorded for the
+//    write-back).
+//  COMMITTER (wave 0) walks the window in order. Per pod i: the ring entry; the
+//    checkers' drops and the x-checker's verdict; the select: the staged
+//    prediction when nothing dropped, else T0's tp-th node ascending, tp the
+//    least fixed point of tp = (k-1-ix) + #(drop positions <= tp), found
+//    through the row and word prefixes (no walk over the node words: the chain
+//    does not grow with the node count); the drawn node and its candidate
+//    index to the x-checker; the slot; the pod's keys and service ids into the
+//    slot's table row; the commit record.
+//
+// Hand-offs (LDS; every poll is relaxed loads then one LDS-only acquire
+// fence, every post a workgroup-scope release store after the data it covers):
+//
+//   flag / data            writer      reader              pod index        ordered by
+//   r_hdr[e].ready         producer j  all but producers   j                ready = j+1 release after the entry
+//   L_pub / L_drw bits     producer j  producers > j       j                L_drw before L_pub (atomicOr, in order)
+//   L_xn[i]                committer   x-checker           i (checks i+1)   xn_seq = i+1 release after L_xn[i]
+//   L_cm[i], L_out[i],     committer   checkers (apply i   i                sel_seq = i+1 release after them
+//    slot row keys / ids               at pod i+2)
+//   slot row counts        checker     checkers, x-checker commits <= i-2   chk_seq release (x-checker reads
+//                          (apply)                                          rows of commits it replayed: lists
+//                                                                           only; counts from the staging / L2)
+//   chk_seq[c], chk_msk,   checker c   committer, producers i               chk_seq[c] = i+1 release after
+//    chk_cnt, L_dpos                                                        the mask, count, positions
+//   xres[i & 1]            x-checker   committer           i                xseq = i+1 release after xres
+//   L_flag, L_peer,        x-checker   committer           commits <= i-2   program order in the x-checker,
+//    L_peerset, n_peer                 (reads at pod i)                     xseq >= i+1 acquired by the committer
+//   stop, resolved         committer   all                 —                stop = 1 release after resolved
+//   fin[c], fin_x          checkers,   committer           —                release after the write-back /
+//                          x-checker                                        the last first peers
+//
+// Ring entry e = j mod RING is rewritten for pod j once the checkers are done
+// with pod j-RING+2 (they apply commit j-RING while checking it) and the
+// x-checker with pod j-RING+1 (it reads pod j-RING's record, candidates and
+// staged counts). The committer reads an entry only for its own pod. Every
+// wait has a spin limit; a timed-out wait sets ctl->hang and the host fails
+// the batch.
+#include "ksg_resolver.h"
+
+#define KSG_NCAND 6     // candidate nodes staged per pod (0, 1 or 2 drops)
+#define KSG_CSV_MAX 10  // services of a pod whose counts on the candidates are staged (6 x 10 lanes)
+#define KSG_NO_CAND 7u  // commit flags: the drawn node is no candidate
+
+struct alignas(16) PlCommit {
+  uint32_t kind;   // 0: no commit (error / no fit), 1: commit
+  uint32_t slot;
+  uint32_t node;   // shard offset of the node
+  uint32_t flags;  // bit 0: a new slot; bits 1..3: candidate index (KSG_NO_CAND: none);
+                   // bits 8..15: the pod's service count; 16..23: the slot's service
+                   // entries before the commit; 24..31: its conflict keys before it
+};
+struct alignas(16) PlCtl {
+  uint32_t stop;      // the committer is done: pods [0, resolved) are decided
+  uint32_t resolved;
+  uint32_t sel_seq;   // commit records published for pods [0, sel_seq)
+  uint32_t n_peer;    // first service peers recorded in the window (L_peer entries)
+  uint32_t chk_seq[KSG_RES_NCHK];        // pods checker c is done with
+  uint32_t chk_cnt[KSG_RES_NCHK][2];     // checker c's drops for the pod of parity p
+  uint32_t chk_msk[KSG_RES_NCHK][2][2];  // ... and its dropping slots (lane l: slot 64c + l)
+  uint32_t fin[KSG_RES_NCHK];            // checker c applied every commit and wrote its slots back
+  uint32_t hang;                         // a wait exceeded its spin limit (a bug)
+  uint32_t xseq;                         // pods the x-checker is done with
+  uint32_t xres[2];                      // its verdict for the pod of parity p: bit 0 x drops, bit 1 flag
+  uint32_t xn_seq;                       // pods whose drawn node is posted in L_xn
+  uint32_t fin_x;                        // the x-checker applied every commit's flags and first peers
+  uint32_t t_x, t_n;                     // KSG_DEBUG & 8: clock at the xres / xn posts
+};
+struct PlLdsOff {
+  uint32_t ctl, r_hdr, r_t0, r_wp, r_lp, r_rec, r_mod, r_svc, r_cand, r_csnap, r_csv;  // ring
+  uint32_t cm, out, xn, peer, flag, peerset, pub, drw, clist, dpos;                   // window
+  uint32_t total;
+};
+
+__host__ __device__ inline PlLdsOff plain_lds_offsets(uint32_t P, uint32_t nflag, uint32_t W) {
+  PlLdsOff o;
+  const uint32_t R = win2_ring(P, false);
+  uint32_t at = 0;
+  o.ctl = at;     at += win_al16(sizeof(PlCtl));
+  o.r_hdr = at;   at += win_al16((size_t)R * sizeof(RingHdr));
+  o.r_t0 = at;    at += win_al16((size_t)R * P * 64 * 8);       // T0 by word
+  o.r_wp = at;    at += win_al16((size_t)R * P * 64 * 2);       // T0 bits below the word in its row (u16)
+  o.r_lp = at;    at += win_al16((size_t)R * 32 * 8);           // per row: T0 bits below it, up to its end
+  o.r_rec = at;   at += win_al16((size_t)R * KSG_WIN_SUM_DWORDS * 4);
+  o.r_mod = at;   at += win_al16((size_t)R * 64 * 4);           // r mod (k0 - d)
+  o.r_svc = at;   at += win_al16((size_t)R * sizeof(RingSvc));  // the pod's services' max / peer
+  o.r_cand = at;  at += win_al16((size_t)R * 8 * 4);            // candidate nodes (~0u: none)
+  o.r_csnap = at; at += win_al16((size_t)R * KSG_NCAND * 6 * 8);  // [cand][cap c, m, used c, m, inv c, m]
+  o.r_csv = at;   at += win_al16((size_t)R * KSG_NCAND * KSG_SLOT_SVCS * 4);  // [cand][service t] counts
+  o.cm = at;      at += win_al16((size_t)W * sizeof(PlCommit));
+  o.out = at;     at += win_al16((size_t)W * 4);
+  o.xn = at;      at += win_al16((size_t)W * 4);
+  o.peer = at;    at += win_al16((size_t)W * 2 * 4);
+  o.flag = at;    at += win_al16((size_t)nflag * 4);
+  o.peerset = at; at += win_al16((size_t)nflag * 4);
+  o.pub = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
+  o.drw = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
+  o.clist = at;   at += win_al16((size_t)KSG_MAX_SLOTS * KSG_CL_W * 4);
+  o.dpos = at;    at += win_al16((size_t)2 * KSG_MAX_SLOTS * 4);
+  o.total = at;
+  return o;
+}
+
+template <int P, bool STAMP>
+__global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
+                                                            const KsgWinSum* __restrict__ sums, const KsgWinXchg x,
+                                                            uint64_t* rng_io, int32_t* __restrict__ out_batch) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t pos = run->pos, n_batch = run->n;
+  if (run->halt || pos >= n_batch) return;  // the chain is done (uniform, before any barrier)
+  const uint32_t n_pods = min(wcap, n_batch - pos);
+  int32_t* __restrict__ out = out_batch + pos;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t nflag = (d.n_services + 31) / 32;
+  const uint32_t nwords = d.nwords;
+  constexpr uint32_t RING = win2_ring(P, false);
+  constexpr uint32_t NT = 512;
+  constexpr uint32_t NPW = NT / 64 - KSG_RES_P0;  // producer waves
+  constexpr uint32_t DW = KSG_WIN_SUM_DWORDS;
+  const PlLdsOff o = plain_lds_offsets(P, nflag, wcap);
+  PlCtl* ctl = reinterpret_cast<PlCtl*>(smem + o.ctl);
+  RingHdr* r_hdr = reinterpret_cast<RingHdr*>(smem + o.r_hdr);
+  uint64_t* r_t0 = reinterpret_cast<uint64_t*>(smem + o.r_t0);
+  uint16_t* r_wp = reinterpret_cast<uint16_t*>(smem + o.r_wp);
+  uint32_t* r_lp = reinterpret_cast<uint32_t*>(smem + o.r_lp);
+  uint32_t* r_rec = reinterpret_cast<uint32_t*>(smem + o.r_rec);
+  uint32_t* r_mod = reinterpret_cast<uint32_t*>(smem + o.r_mod);
+  RingSvc* r_svc = reinterpret_cast<RingSvc*>(smem + o.r_svc);
+  uint32_t* r_cand = reinterpret_cast<uint32_t*>(smem + o.r_cand);
+  uint64_t* r_csnap = reinterpret_cast<uint64_t*>(smem + o.r_csnap);
+  int32_t* r_csv = reinterpret_cast<int32_t*>(smem + o.r_csv);
+  PlCommit* L_cm = reinterpret_cast<PlCommit*>(smem + o.cm);
+  int32_t* L_out = reinterpret_cast<int32_t*>(smem + o.out);
+  // node drawn by pod p | its candidate index << 28 (~0u: no commit), one entry
+  // per pod: the committer runs ahead of the x-checker through pods that make
+  // no commit, so a single mailbox would be overwritten before it is read
+  uint32_t* L_xn = reinterpret_cast<uint32_t*>(smem + o.xn);
+  uint32_t* L_peer = reinterpret_cast<uint32_t*>(smem + o.peer);
+  uint32_t* L_flag = reinterpret_cast<uint32_t*>(smem + o.flag);
+  uint32_t* L_peerset = reinterpret_cast<uint32_t*>(smem + o.peerset);
+  uint32_t* L_pub = reinterpret_cast<uint32_t*>(smem + o.pub);  // pods whose drawable bit is known
+  uint32_t* L_drw = reinterpret_cast<uint32_t*>(smem + o.drw);  // drawable pods
+  uint32_t* L_cl = reinterpret_cast<uint32_t*>(smem + o.clist);  // [slot][KSG_CL_W]
+  uint32_t* L_dpos = reinterpret_cast<uint32_t*>(smem + o.dpos);  // [parity][slot] drop positions in T0
+  const bool spread_on = d.w_spread != 0;
+  const bool aff_on = (d.preds & KSG_PRED_SERVICEAFFINITY) && d.n_aff > 0;
+  const bool res_on = (d.preds & KSG_PRED_PODFITSRESOURCES) != 0;
+  const bool ports_on = (d.preds & KSG_PRED_PODFITSPORTS) != 0;
+  const bool disk_on = (d.preds & KSG_PRED_NODISKCONFLICT) != 0;
+  const uint32_t nbits = (wcap + 31) / 32;
+  // KSG_DEBUG bits 16..19: a fixed delay per pod in one wave role (committer,
+  // x-checker, checkers, producers) to test the hand-offs under another
+  // interleaving than the natural one (tests/test_gpu_fuzz.py)
+  const uint32_t skew = ((uint32_t)d.dbg >> 16) & 15u;
+
+  for (uint32_t t = tid; t < RING; t += NT) r_hdr[t].ready = 0;
+  if (tid == 0) *ctl = PlCtl{};
+  for (uint32_t w = tid; w < nflag; w += NT) {
+    L_flag[w] = 0;
+    L_peerset[w] = 0;
+  }
+  for (uint32_t w = tid; w < nbits; w += NT) {
+    L_pub[w] = 0;
+    L_drw[w] = 0;
+  }
+  __syncthreads();
+  const uint64_t rng0 = *rng_io;
+
+  // =========================================================================
+  // producers
+  // =========================================================================
+  if (wave >= KSG_RES_P0) {
+    const uint32_t* recs = reinterpret_cast<const uint32_t*>(sums);
+    // lane l holds words q*64 + l: byte offsets of the rank block and row phase
+    // A wrote them at (~0u = no such word); coalesced loads, conflict-free LDS
+    uint32_t wb_at[P], wm_at[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      const uint32_t wq = q * 64 + lane;
+      uint32_t g = 0;
+      for (uint32_t r = 1; r < x.world; ++r)
+        if (wq >= x.wlo[r] && x.nw[r] > 0) g = r;
+      const uint32_t i = wq - x.wlo[g];
+      const bool ok = wq < nwords && i < x.nw[g];
+      const uint32_t base = (uint32_t)(g * x.blk);
+      wb_at[q] = ok ? base + i * 8 : ~0u;
+      wm_at[q] = ok ? base + x.wcap * x.ostride * 8 + i * 4 : ~0u;
+    }
+    const uint32_t row_b = x.ostride * 8, row_m = x.ostride * 4;
+    uint64_t p_last = 0, p_acc = 0;  // KSG_DEBUG & 8: lanes 24..27 ring wait, loads, draw wait, the rest
+    auto pstamp = [&](uint32_t k) {
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        p_acc += lane == k ? t_now - p_last : 0ULL;
+        p_last = t_now;
+      }
+    };
+    if constexpr (STAMP) p_last = __builtin_amdgcn_s_memtime();
+    for (uint32_t j = wave - KSG_RES_P0; j < n_pods; j += NPW) {
+      const uint32_t e = j % RING;
+      // ring entry free: the checkers applied commit j - RING (while checking
+      // pod j - RING + 2); the x-checker of pod j - RING + 1 read its record
+      for (uint32_t spin = 0;; ++spin) {
+        if (ld_acq(&ctl->stop)) return;
+        if (spin > KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          return;
+        }
+        uint32_t done = ld_acq(&ctl->xseq);
+#pragma unroll
+        for (int c = 0; c < KSG_RES_NCHK; ++c) done = min(done, ld_acq(&ctl->chk_seq[c]));
+        if (j < RING || done + RING >= j + 3) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      pstamp(24);
+      if (skew & 8u) __builtin_amdgcn_s_sleep(8);
+      const uint32_t rec = lane < DW ? recs[(size_t)j * DW + lane] : 0u;
+      uint64_t t0[P];
+      int32_t mw[P];
+      int32_t lm = KSG_S32_NONE;
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        t0[q] = wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + j * row_b) : 0ULL;
+        mw[q] = wm_at[q] != ~0u ? *reinterpret_cast<const int32_t*>(x.buf + wm_at[q] + j * row_m) : KSG_S32_NONE;
+        lm = mw[q] > lm ? mw[q] : lm;
+      }
+      const int32_t m0 = wave_total_max(lm);
+      const bool drawable = __builtin_amdgcn_readlane(rec, WS_ERR) == 0 && m0 != KSG_S32_NONE;
+      const uint32_t wj = j >> 5, bj = 1u << (j & 31);
+      if (lane == 0) {  // the drawable bit first, then "known" (readers read them in that order)
+        if (drawable) atomicOr(&L_drw[wj], bj);
+        atomicOr(&L_pub[wj], bj);
+      }
+      // T0 and its prefixes: per row q, the bits below each lane's word (ex_q)
+      // and below the row (rowex[q], wave-uniform)
+      uint32_t ex_q[P], rowex[P];
+      uint32_t k0 = 0;
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        t0[q] = (m0 != KSG_S32_NONE && mw[q] == m0) ? t0[q] : 0ULL;
+        const uint32_t c1 = (uint32_t)__popcll(t0[q]);
+        const uint32_t in1 = dpp_scan_add(c1);
+        ex_q[q] = in1 - c1;
+        rowex[q] = k0;
+        k0 += (uint32_t)__builtin_amdgcn_readlane((int)in1, 63);
+      }
+      pstamp(25);
+      // draw index = drawable pods before j (every one of them known)
+      uint32_t idx = 0;
+      for (uint32_t spin = 0;; ++spin) {
+        if (ld_acq(&ctl->stop)) return;
+        if (spin > KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          return;
+        }
+        bool all = true;
+        idx = 0;
+        for (uint32_t w = 0; w <= wj; ++w) {
+          const uint32_t mask = w < wj ? ~0u : bj - 1u;
+          const uint32_t pub = __builtin_amdgcn_readfirstlane(ld_acq(&L_pub[w]));
+          all = all && (pub & mask) == mask;
+          idx += __popc(__builtin_amdgcn_readfirstlane(L_drw[w]) & mask);
+        }
+        if (all) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      pstamp(26);
+      uint64_t sm = rng0 + (uint64_t)idx * 0x9E3779B97F4A7C15ULL;
+      const uint64_t r = ksg_splitmix_next(&sm) >> 1;  // rand.Int() (generic_scheduler.go:94)
+      uint32_t mv = 0;
+      if (drawable && lane < k0) mv = umod64_32(r, k0 - lane);
+      const uint32_t n_svcs = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NSS) >> 16;
+      const uint32_t nk = ((uint32_t)__builtin_amdgcn_readlane(rec, WS_NPP) & 0xffff) +
+                          ((uint32_t)__builtin_amdgcn_readlane(rec, WS_NPP) >> 16);
+      const uint32_t n_sel = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NSS) & 0xffff;
+      const bool inl = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NINL) <= KSG_WIN_INLINE && n_svcs <= KSG_SLOT_SVCS;
+      // the candidates: ascending T0 positions k0-1-ix0; k0-2-ix1 (+1); k0-3-ix2 (+1, +2)
+      // (lane c < 6 holds candidate c; a lane-indexed array would go to scratch)
+      uint32_t cand_l = ~0u, cand0 = ~0u;
+      if (drawable) {
+#pragma unroll
+        for (int c = 0; c < KSG_NCAND; ++c) {
+          const uint32_t dd = c == 0 ? 0u : c < 3 ? 1u : 2u;
+          const uint32_t off = c == 0 ? 0u : c < 3 ? (uint32_t)c - 1 : (uint32_t)c - 3;
+          if (k0 > dd) {
+            const uint32_t ixd = (uint32_t)__builtin_amdgcn_readlane((int)mv, (int)dd);
+            const uint32_t node = select_qmajor<P>(t0, ex_q, rowex, k0 - 1 - dd - ixd + off, lane);
+            if (lane == (uint32_t)c) cand_l = node;
+            if (c == 0) cand0 = node;
+          }
+        }
+      }
+      // their snapshots (lane L < 36: candidate L / 6, field L % 6) and the pod's
+      // service counts on them (lane L < 6 n_svcs: candidate L / n_svcs, service
+      // L % n_svcs), all loads in flight together
+      const bool csv_on = inl && n_svcs > 0 && n_svcs <= KSG_CSV_MAX;
+      const uint32_t cL = lane / 6, fL = lane % 6;
+      const uint32_t cn_ = (uint32_t)__shfl((int)cand_l, (int)(cL < KSG_NCAND ? cL : 0u), 64);
+      const uint32_t cn = lane < 6 * KSG_NCAND ? cn_ : ~0u;
+      uint64_t snap = 0;
+      if (cn != ~0u) {
+        const uint32_t pn = d.lo + cn;
+        const int64_t* src = fL == 0 ? d.cap_cpu : fL == 1 ? d.cap_mem : fL == 2 ? d.used_cpu : d.used_mem;
+        snap = fL < 4 ? (uint64_t)gld(src + pn)
+                      : (uint64_t)gld(reinterpret_cast<const int64_t*>(fL == 4 ? d.inv10_cpu : d.inv10_mem) + pn);
+      }
+      const uint32_t cS = csv_on ? lane / n_svcs : KSG_NCAND, tS = csv_on ? lane % n_svcs : 0u;
+      const uint32_t sv_s = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + tS, 63u), 64);
+      const uint32_t cns_ = (uint32_t)__shfl((int)cand_l, (int)(cS < KSG_NCAND ? cS : 0u), 64);
+      const uint32_t cns = cS < KSG_NCAND ? cns_ : ~0u;
+      int32_t scv = 0;
+      if (cns != ~0u) scv = gld(d.svc_cnt + (size_t)sv_s * d.n_nodes + d.lo + cns);
+      // the pod's services' max and first peer (the flagger's service flags)
+      const uint32_t t_sv = lane < n_svcs ? lane : 0u;
+      const uint32_t my_sv = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + t_sv, 63u), 64);
+      int32_t s_max = 0, s_peer = 0;
+      if (drawable && inl && lane < n_svcs) {
+        s_max = gld(d.svc_max + my_sv);
+        s_peer = gld(d.svc_peer + my_sv);
+      }
+      r_mod[e * 64 + lane] = mv;
+      if (lane < DW) r_rec[e * DW + lane] = rec;
+      uint32_t lpe = 0, lpi = 0;
+#pragma unroll
+      for (int q = 0; q < P; ++q) {
+        r_t0[(size_t)e * P * 64 + q * 64 + lane] = t0[q];
+        r_wp[(size_t)e * P * 64 + q * 64 + lane] = (uint16_t)ex_q[q];
+        if (lane == (uint32_t)q) {
+          lpe = rowex[q];
+          lpi = q + 1 < P ? rowex[q + 1 < P ? q + 1 : q] : k0;
+        }
+      }
+      if (lane < P) {
+        r_lp[(e * 32 + lane) * 2] = lpe;
+        r_lp[(e * 32 + lane) * 2 + 1] = lpi;
+      }
+      if (lane < KSG_NCAND) r_cand[e * 8 + lane] = cand_l;
+      if (lane < 6 * KSG_NCAND) r_csnap[(e * KSG_NCAND + cL) * 6 + fL] = snap;
+      if (cS < KSG_NCAND) r_csv[(e * KSG_NCAND + cS) * KSG_SLOT_SVCS + tS] = scv;
+      if (inl && lane < n_svcs) {
+        r_svc[e].max[lane] = s_max;
+        r_svc[e].peer[lane] = s_peer;
+      }
+      if (lane == 0) {
+        r_hdr[e].m0 = m0;
+        r_hdr[e].k0 = k0;
+        r_hdr[e].r = r;
+        r_hdr[e].drawable = drawable;
+        r_hdr[e].pred = (int32_t)cand0;
+        r_hdr[e].pad = csv_on ? 1u : 0u;  // the candidates' service counts are staged
+        st_rel(&r_hdr[e].ready, j + 1);
+      }
+      pstamp(27);
+    }
+    if constexpr (STAMP) {
+      if (lane >= 24 && lane < 28) atomicAdd(d.dbgbuf + lane, (int32_t)(p_acc / 64));
+    }
+    return;
+  }
+
+  // =========================================================================
+  // checkers (waves KSG_RES_C0 ..): lane l of checker c owns slot 64c + l
+  // =========================================================================
+  if (wave >= KSG_RES_C0) {
+    __builtin_amdgcn_s_setprio(2);
+    const uint32_t c = wave - KSG_RES_C0;
+    const uint32_t my_slot = c * 64 + lane;
+    const uint32_t* my_cl = L_cl + (size_t)my_slot * KSG_CL_W;
+    RegSlot S;
+    S.node = ~0u;
+    S.cap_c = S.cap_m = S.snp_c = S.snp_m = S.dl_c = S.dl_m = 0;
+    S.inv_c = S.inv_m = 0.0;
+    S.nk = S.ns = S.smask = 0;
+    S.row = ~0u;
+    // AssumePod of pod p (plugin/pkg/scheduler/scheduler.go:115-118) into the
+    // owner lane's slot: requested totals, list lengths (the committer wrote the
+    // lists into the table row) and the services' snapshot counts
+    auto apply = [&](uint32_t p) {
+      const uint32_t kind = __builtin_amdgcn_readfirstlane(L_cm[p].kind);
+      const uint32_t slot = __builtin_amdgcn_readfirstlane(L_cm[p].slot);
+      if (kind != 1 || (slot >> 6) != c) return;
+      const uint32_t woff = __builtin_amdgcn_readfirstlane(L_cm[p].node);
+      const uint32_t fl = __builtin_amdgcn_readfirstlane(L_cm[p].flags);
+      const bool fresh = (fl & 1u) != 0;
+      const uint32_t cidx = (fl >> 1) & 7u, n_svcs = (fl >> 8) & 0xffu, bns = (fl >> 16) & 0xffu, bnk = fl >> 24;
+      const uint32_t ol = slot & 63, ep = p % RING, wn = d.lo + woff;
+      const uint32_t prec = lane < DW ? r_rec[ep * DW + lane] : 0u;
+      const PodView ppv = pod_view(prec);
+      if (fresh && lane == ol) {  // the new slot's snapshot: staged for a candidate, else from L2
+        if (cidx < KSG_NCAND) {
+          const uint64_t* cs = r_csnap + (ep * KSG_NCAND + cidx) * 6;
+          S.cap_c = (int64_t)cs[0];
+          S.cap_m = (int64_t)cs[1];
+          S.snp_c = (int64_t)cs[2];
+          S.snp_m = (int64_t)cs[3];
+          S.inv_c = __longlong_as_double((long long)cs[4]);
+          S.inv_m = __longlong_as_double((long long)cs[5]);
+        } else {
+          S.cap_c = gld(d.cap_cpu + wn);
+          S.cap_m = gld(d.cap_mem + wn);
+          S.snp_c = gld(d.used_cpu + wn);
+          S.snp_m = gld(d.used_mem + wn);
+          S.inv_c = gld(d.inv10_cpu + wn);
+          S.inv_m = gld(d.inv10_mem + wn);
+        }
+        S.node = woff;
+        S.dl_c = S.dl_m = 0;
+        S.smask = 0;
+      }
+      uint32_t new_mask = 0;
+      if (n_svcs) {
+        // the pod's services' snapshot counts on the node into the table row:
+        // staged for a candidate, else from L2
+        const bool sv_lane = lane < n_svcs;
+        const uint32_t sv = sv_lane ? L_cl[(size_t)slot * KSG_CL_W + KSG_CL_SV + bns + lane] : 0u;
+        const bool staged = cidx < KSG_NCAND && r_hdr[ep].pad != 0;
+        int32_t cnt = 0;
+        if (sv_lane)
+          cnt = staged ? r_csv[(ep * KSG_NCAND + cidx) * KSG_SLOT_SVCS + lane] : gld(d.svc_cnt + (size_t)sv * d.n_nodes + wn);
+        if (sv_lane) L_cl[(size_t)slot * KSG_CL_W + KSG_CL_SC + bns + lane] = (uint32_t)cnt;
+        new_mask = wave_or_u32(sv_lane ? (1u << (sv & 31)) : 0u);
+      }
+      if (lane == ol) {
+        S.dl_c = (int64_t)((uint64_t)S.dl_c + (uint64_t)ppv.req_c);
+        S.dl_m = (int64_t)((uint64_t)S.dl_m + (uint64_t)ppv.req_m);
+        S.nk = bnk + ppv.nk;
+        S.ns = bns + n_svcs;
+        S.smask |= new_mask;
+      }
+    };
+
+    uint64_t t_last = 0, t_acc = 0;
+    auto cstamp = [&](uint32_t k) {
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        t_acc += lane == k ? t_now - t_last : 0ULL;
+        t_last = t_now;
+      }
+    };
+    if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
+    for (uint32_t i = 0;; ++i) {
+      const uint32_t e = i % RING, par = i & 1;
+      bool stopped = false;
+      // pod i is checked against the slots as of commits <= i-2 (the committer
+      // re-checks the node of commit i-1 itself): it starts once commit i-2 is
+      // published, a whole pod before the committer needs its drops
+      for (uint32_t spin = 0;; ++spin) {
+        const uint32_t ss = ld_rlx(&ctl->sel_seq), rd = ld_rlx(&r_hdr[e].ready), st = ld_rlx(&ctl->stop);
+        if (i < n_pods && ss + 1 >= i && rd == i + 1) break;
+        if (st) {
+          stopped = true;
+          break;
+        }
+        if (spin > 16 * KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          stopped = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);  // (off the chain: leave the LDS to the committer)
+      }
+      acq_lds();
+      cstamp(c == 0 ? 16 : 19);
+      if (stopped) {
+        // pods [0, resolved) are decided: apply the commits this checker has not
+        // (the committer runs ahead of the checkers over pods that do not commit)
+        const uint32_t R = __builtin_amdgcn_readfirstlane(ctl->resolved);
+        for (uint32_t q = i >= 2 ? i - 2 : 0; q < R; ++q) apply(q);
+        break;
+      }
+      if (skew & 4u) __builtin_amdgcn_s_sleep(8);
+      if (i >= 2) apply(i - 2);
+      cstamp(c == 0 ? 17 : 20);
+      const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
+      const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
+      bool drop = false;
+      uint32_t dpos = 0;
+      if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE && S.node != ~0u) {
+        const PodView pv = pod_view(rec);
+        const uint32_t wd = S.node >> 6;
+        const uint64_t tw = r_t0[(size_t)e * P * 64 + wd];
+        // the node's ascending position in T0 (used only if it drops)
+        dpos = r_lp[(e * 32 + (wd >> 6)) * 2] + r_wp[(size_t)e * P * 64 + wd] +
+               (uint32_t)__popcll(tw & ((1ULL << (S.node & 63)) - 1ULL));
+        if ((tw >> (S.node & 63)) & 1ULL) {
+          // does the slot (a snapshot tie of the pod) score below M0 now?
+          const int64_t now_c = (int64_t)((uint64_t)S.snp_c + (uint64_t)S.dl_c);
+          const int64_t now_m = (int64_t)((uint64_t)S.snp_m + (uint64_t)S.dl_m);
+          if (res_on && !pv.zero_req)  // PodFitsResources (predicates.go:127-145)
+            drop = !((S.cap_c == 0 || S.cap_c - now_c >= pv.req_c) && (S.cap_m == 0 || S.cap_m - now_m >= pv.req_m));
+          if (d.w_lr) {  // LeastRequested (priorities.go:43-76) can only fall as requested grows
+            const int32_t lr_now = lr_win(now_c + pv.req_c, S.cap_c, S.inv_c) + lr_win(now_m + pv.req_m, S.cap_m, S.inv_m);
+            const int32_t lr_snap =
+                lr_win(S.snp_c + pv.req_c, S.cap_c, S.inv_c) + lr_win(S.snp_m + pv.req_m, S.cap_m, S.inv_m);
+            drop |= (lr_now >> 1) != (lr_snap >> 1);
+          }
+          if (!drop && pv.nk && S.nk) {  // PodFitsPorts / NoDiskConflict vs the window's keys
+            for (uint32_t a = 0; a < S.nk; ++a) {
+              const uint32_t key = my_cl[KSG_CL_KEY + a];
+              for (uint32_t b = 0; b < pv.nk; ++b) {
+                const bool on = b < pv.n_ports ? ports_on : disk_on;
+                drop |= on && (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b)) == key;
+              }
+            }
+          }
+          if (!drop && spread_on && pv.s >= 0 && ((S.smask >> (pv.s & 31)) & 1u)) {
+            // ServiceSpreading (spreading.go:72-86) under an unchanged maxCount
+            int32_t delta = 0, snapc = 0;
+            for (uint32_t a = 0; a < S.ns; ++a)
+              if (my_cl[KSG_CL_SV + a] == (uint32_t)pv.s) {
+                snapc = (int32_t)my_cl[KSG_CL_SC + a];
+                ++delta;
+              }
+            if (delta)
+              drop = frac10_f32((int64_t)pv.smax - snapc - delta, pv.smax) != frac10_f32((int64_t)pv.smax - snapc, pv.smax);
+          }
+        }
+      }
+      if (drop) L_dpos[par * KSG_MAX_SLOTS + my_slot] = dpos;
+      const uint64_t dmsk = __ballot(drop);
+      if (lane == 0) {
+        ctl->chk_cnt[c][par] = (uint32_t)__popcll(dmsk);
+        ctl->chk_msk[c][par][0] = (uint32_t)dmsk;
+        ctl->chk_msk[c][par][1] = (uint32_t)(dmsk >> 32);
+        st_rel(&ctl->chk_seq[c], i + 1);
+      }
+      cstamp(c == 0 ? 18 : 21);
+    }
+    // write the window's deltas of this checker's slots back to HBM (the next snapshot)
+    if (S.node != ~0u) {
+      const uint32_t n = d.lo + S.node;
+      d.used_cpu[n] = (int64_t)((uint64_t)S.snp_c + (uint64_t)S.dl_c);
+      d.used_mem[n] = (int64_t)((uint64_t)S.snp_m + (uint64_t)S.dl_m);
+      for (uint32_t a = 0; a < S.nk; ++a)
+        __hip_atomic_fetch_or(d.keymap + (size_t)my_cl[KSG_CL_KEY + a] * d.nw + (n >> 6), 1ULL << (n & 63),
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (uint32_t a = 0; a < S.ns; ++a) {
+        const uint32_t sa = my_cl[KSG_CL_SV + a];
+        bool first = true;
+        int32_t count = 0;
+        for (uint32_t b = 0; b < S.ns; ++b) {
+          if (my_cl[KSG_CL_SV + b] == sa) {
+            if (b < a) first = false;
+            ++count;
+          }
+        }
+        __hip_atomic_fetch_add(d.svc_total + sa, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (first) {
+          const int32_t fin = (int32_t)my_cl[KSG_CL_SC + a] + count;
+          d.svc_cnt[(size_t)sa * d.n_nodes + n] = fin;
+          __hip_atomic_fetch_max(d.svc_max + sa, fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    if constexpr (STAMP) {
+      if (lane >= 16 && lane < 22) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
+    }
+    drain_stores();
+    if (lane == 0) st_rel(&ctl->fin[c], 1u);
+    return;
+  }
+
+  // =========================================================================
+  // x-checker (wave 1): pod i against commit i-1's node x as of that commit
+  // (the checkers' view lags a commit), while the committer finishes commit
+  // i-1 and reads pod i; then commit i-1's service flags, in commit order
+  // =========================================================================
+  if (wave == 1) {
+    __builtin_amdgcn_s_setprio(2);
+    // lane L < 4 evaluates one LeastRequested term: resource L & 1 (cpu, memory),
+    // at the node's requested total now (L < 2) or at the snapshot (L >= 2)
+    const uint32_t rl = lane & 1;
+    // the committer's slot bookkeeping, replayed: lane l holds slots l and 64 + l
+    // (node, list lengths, window delta after the commits replayed so far)
+    uint32_t xcn0 = ~0u, xcn1 = ~0u, xsk0 = 0, xsk1 = 0, xss0 = 0, xss1 = 0, xn_slots = 0;
+    int64_t xdc0 = 0, xdm0 = 0, xdc1 = 0, xdm1 = 0;
+    auto replay = [&](uint32_t node, uint32_t prec, uint32_t& slot, uint32_t& bnk, uint32_t& bns, uint64_t& dlc,
+                      uint64_t& dlm) {
+      const PodView ppv = pod_view(prec);
+      const uint32_t p_svcs = (uint32_t)__builtin_amdgcn_readlane(prec, WS_NSS) >> 16;
+      const uint64_t hit0 = __ballot(xcn0 == node), hit1 = __ballot(xcn1 == node);
+      const bool in_c = (hit0 | hit1) != 0;
+      bnk = bns = 0;
+      dlc = dlm = 0;
+      if (in_c) {
+        slot = hit0 ? (uint32_t)__builtin_ctzll(hit0) : 64u + (uint32_t)__builtin_ctzll(hit1);
+        const uint32_t sl = slot & 63;
+        bnk = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? xsk0 : xsk1), (int)sl);
+        bns = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? xss0 : xss1), (int)sl);
+        dlc = readlane64((uint64_t)(slot < 64 ? xdc0 : xdc1), (int)sl);
+        dlm = readlane64((uint64_t)(slot < 64 ? xdm0 : xdm1), (int)sl);
+      } else {
+        slot = xn_slots < KSG_MAX_SLOTS ? xn_slots++ : 0u;  // (a full table stops the committer)
+      }
+      dlc += (uint64_t)ppv.req_c;
+      dlm += (uint64_t)ppv.req_m;
+      if (lane == (slot & 63)) {
+        if (slot >= 64) {
+          if (!in_c) xcn1 = node;
+          xsk1 = bnk + ppv.nk;
+          xss1 = bns + p_svcs;
+          xdc1 = (int64_t)dlc;
+          xdm1 = (int64_t)dlm;
+        } else {
+          if (!in_c) xcn0 = node;
+          xsk0 = bnk + ppv.nk;
+          xss0 = bns + p_svcs;
+          xdc0 = (int64_t)dlc;
+          xdm0 = (int64_t)dlm;
+        }
+      }
+    };
+    // commit q of a pod of services sv_t on node x (slot, bns entries before it):
+    // a maxCount rise (its snapshot count on x plus the window's entries there
+    // above the snapshot max) or the service's first peer in the window ends the
+    // window at the next pod of that service; the window's first peer of a
+    // service is the earliest commit's node (one wave, commit order)
+    auto flags = [&](uint32_t q, uint32_t node, uint32_t cidx, uint32_t slot, uint32_t bns, uint32_t prec) {
+      const uint32_t nss = __builtin_amdgcn_readlane(prec, WS_NSS), npp = __builtin_amdgcn_readlane(prec, WS_NPP);
+      const uint32_t n_svcs = nss >> 16, n_sel = nss & 0xffff, pnk = (npp & 0xffff) + (npp >> 16);
+      if (!n_svcs) return;
+      const uint32_t wn = d.lo + node, eq = q % RING;
+      const bool sv_lane = lane < n_svcs;
+      const uint32_t my_sv =
+          (uint32_t)__shfl((int)prec, (int)min(WS_IDS + pnk + n_sel + (sv_lane ? lane : 0u), 63u), 64);
+      const bool staged = cidx < KSG_NCAND && r_hdr[eq].pad != 0;
+      int32_t mx = 0, peer = 0, cnt = 0;
+      if (sv_lane) {
+        cnt = staged ? r_csv[(eq * KSG_NCAND + cidx) * KSG_SLOT_SVCS + lane] : gld(d.svc_cnt + (size_t)my_sv * d.n_nodes + wn);
+        mx = r_svc[eq].max[lane];
+        peer = r_svc[eq].peer[lane];
+      }
+      // earlier window commits of each service on this node (table lanes KSG_CL_SV..)
+      const uint32_t ent = lane - KSG_CL_SV < bns ? L_cl[(size_t)slot * KSG_CL_W + lane] : ~0u;
+      uint32_t before = 0;
+      for (uint32_t t = 0; t < n_svcs; ++t) {
+        const uint32_t sv_t = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)t);
+        const uint32_t b_t = (uint32_t)__popcll(__ballot(ent == sv_t));
+        if (lane == t) before = b_t;
+      }
+      bool changed = sv_lane && aff_on && peer == -1 && !((L_peerset[my_sv >> 5] >> (my_sv & 31)) & 1u);
+      uint64_t pm = __ballot(sv_lane && peer == -1);
+      if (pm) {  // first commit of a service with no peer yet: its first peer
+        uint32_t n_peer = __builtin_amdgcn_readfirstlane(ctl->n_peer);
+        while (pm) {
+          const uint32_t b = __builtin_ctzll(pm);
+          pm &= pm - 1;
+          const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)b);
+          if (!((L_peerset[fsv >> 5] >> (fsv & 31)) & 1u)) {
+            if (lane == 0) {
+              L_peerset[fsv >> 5] |= 1u << (fsv & 31);
+              L_peer[2 * n_peer] = fsv;
+              L_peer[2 * n_peer + 1] = wn;
+            }
+            ++n_peer;
+            lds_fence();
+          }
+        }
+        if (lane == 0) ctl->n_peer = n_peer;
+      }
+      if (sv_lane && spread_on && cnt + (int32_t)before + 1 > mx) changed = true;  // maxCount rises
+      if (changed) atomicOr(&L_flag[my_sv >> 5], 1u << (my_sv & 31));
+    };
+    uint64_t x_last = 0, x_acc = 0;  // KSG_DEBUG & 8: lanes 28..30 wait, check, flags; 31 node hand-off
+    if constexpr (STAMP) x_last = __builtin_amdgcn_s_memtime();
+    uint32_t i = 0;
+    for (; i < n_pods; ++i) {
+      const uint32_t e = i % RING, par = i & 1, ep = (i + RING - 1) % RING;
+      bool stopped = false;
+      for (uint32_t spin = 0;; ++spin) {  // pod i staged (long before pod i-1's node is drawn), or the end
+        const uint32_t rd = ld_u(&r_hdr[e].ready), st = ld_u(&ctl->stop);
+        if (rd == i + 1) break;
+        if (st) {
+          stopped = true;
+          break;
+        }
+        if (spin > 16 * KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          stopped = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      acq_lds();
+      if (stopped) break;
+      // pods i's and i-1's records ahead of the node
+      const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
+      const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
+      const int32_t peer0 = __builtin_amdgcn_readfirstlane(r_svc[e].peer[0]);
+      const uint32_t prec = (i && lane < DW) ? r_rec[ep * DW + lane] : 0u;
+      const bool p_staged = i && r_hdr[ep].pad != 0;
+      const PodView pv = pod_view(rec);
+      const int32_t s = pv.s;
+      for (uint32_t spin = 0;; ++spin) {  // pod i-1's node drawn, or the end
+        const uint32_t xn = ld_u(&ctl->xn_seq), st = ld_u(&ctl->stop);
+        if (xn >= i) break;
+        if (st) {
+          stopped = true;
+          break;
+        }
+        if (spin > 16 * KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          stopped = true;
+          break;
+        }
+      }
+      acq_lds();
+      if (stopped) break;
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        x_acc += lane == 28 ? t_now - x_last : 0ULL;
+        x_last = t_now;
+        if (i) x_acc += lane == 31 ? (uint64_t)(uint32_t)((uint32_t)t_now - ctl->t_n) : 0ULL;
+      }
+      if (skew & 2u) __builtin_amdgcn_s_sleep(8);
+      uint32_t res = 0;
+      const uint32_t xv = i ? __builtin_amdgcn_readfirstlane(L_xn[i - 1]) : ~0u;
+      const uint32_t xnode = xv == ~0u ? ~0u : xv & 0x0fffffffu, xcid = xv == ~0u ? KSG_NO_CAND : xv >> 28;
+      const bool do_check = xnode != ~0u && !__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE;
+      const uint32_t xw = d.lo + (do_check ? xnode : 0u);
+      // x's snapshot: staged for a candidate (LDS), else from L2 (in flight over
+      // the bookkeeping below)
+      int64_t capv = 0, usev = 0;
+      double invv = 0.0;
+      if (do_check) {
+        if (xcid < KSG_NCAND) {
+          const uint64_t* cs = r_csnap + (ep * KSG_NCAND + xcid) * 6;
+          capv = (int64_t)cs[rl];
+          usev = (int64_t)cs[2 + rl];
+          invv = __longlong_as_double((long long)cs[4 + rl]);
+        } else {
+          capv = gld((rl ? d.cap_mem : d.cap_cpu) + xw);
+          usev = gld((rl ? d.used_mem : d.used_cpu) + xw);
+          invv = gld((rl ? d.inv10_mem : d.inv10_cpu) + xw);
+        }
+      }
+      // commit i-1 into its slot (the committer's bookkeeping, replayed)
+      uint32_t xslot = 0, bnk = 0, bns = 0;
+      uint64_t dlc = 0, dlm = 0;
+      if (xnode != ~0u) replay(xnode, prec, xslot, bnk, bns, dlc, dlm);
+      if (do_check) {
+        // pod i-1's record: its keys and service ids follow the earlier commits' in the slot's lists
+        const uint32_t pnpp = __builtin_amdgcn_readlane(prec, WS_NPP), pnss = __builtin_amdgcn_readlane(prec, WS_NSS);
+        const uint32_t pnk = (pnpp & 0xffff) + (pnpp >> 16), pnsel = pnss & 0xffff, pns = pnss >> 16;
+        const uint32_t xnk = bnk + pnk, xns = bns + pns;
+        // lane t < 8: key t of the slot; lane 8 + u (u < 12): its service u
+        const uint32_t kt = lane - KSG_CL_KEY, ut = lane - KSG_CL_SV;
+        const bool from_row = (kt < KSG_SLOT_KEYS && kt < bnk) || (ut < KSG_SLOT_SVCS && ut < bns);
+        const uint32_t src = kt < KSG_SLOT_KEYS ? WS_IDS + (kt - bnk) : WS_IDS + pnk + pnsel + (ut - bns);
+        const uint32_t from_rec = (uint32_t)__shfl((int)prec, (int)min(src, 63u), 64);
+        const uint32_t rowv = from_row ? L_cl[(size_t)xslot * KSG_CL_W + lane] : 0u;
+        const uint32_t xcl = from_row ? rowv : from_rec;
+        const uint32_t nk = pv.nk;
+        const bool s_ent = s >= 0 && ut < xns && xcl == (uint32_t)s;
+        const uint64_t ents = __ballot(s_ent);
+        const uint32_t x_cnt_s = (uint32_t)__popcll(ents);
+        const uint64_t prev_ents = __ballot(s_ent && ut >= bns);  // commit i-1's entries of service s
+        if constexpr (STAMP) {
+          const uint64_t t_now = __builtin_amdgcn_s_memtime();
+          x_acc += lane == 30 ? t_now - x_last : 0ULL;
+          x_last = t_now;
+        }
+        const int64_t reqv = rl ? pv.req_m : pv.req_c;
+        const int64_t nowv = (int64_t)((uint64_t)usev + (rl ? dlm : dlc));  // requested total now
+        bool xd = false, flag_x = false;
+        if (res_on && !pv.zero_req)  // PodFitsResources: lanes 0 and 1
+          xd = (__ballot(lane < 2 && !(capv == 0 || capv - nowv >= reqv)) & 3ULL) != 0;
+        if (d.w_lr) {  // LeastRequested: one term per lane
+          const int32_t lrv = lr_win((lane < 2 ? nowv : usev) + reqv, capv, invv);
+          const int32_t lr_now = __builtin_amdgcn_readlane(lrv, 0) + __builtin_amdgcn_readlane(lrv, 1);
+          const int32_t lr_snap = __builtin_amdgcn_readlane(lrv, 2) + __builtin_amdgcn_readlane(lrv, 3);
+          xd |= (lr_now >> 1) != (lr_snap >> 1);
+        }
+        if (x_cnt_s) {
+          // s's snapshot count on x: staged with pod i-1's services when pod i-1 is
+          // a pod of s, else from L2 (the checkers may not have written it yet)
+          int32_t x_snapc;
+          if (prev_ents && p_staged && xcid < KSG_NCAND)
+            x_snapc = r_csv[(ep * KSG_NCAND + xcid) * KSG_SLOT_SVCS + (uint32_t)__builtin_ctzll(prev_ents) - KSG_CL_SV - bns];
+          else
+            x_snapc = gld(d.svc_cnt + (size_t)s * d.n_nodes + xw);
+          x_snapc = __builtin_amdgcn_readfirstlane(x_snapc);
+          if (spread_on) {  // ServiceSpreading under an unchanged maxCount: lane 0 now, lane 1 the snapshot
+            const int32_t fr = (int32_t)frac10_f32((int64_t)pv.smax - x_snapc - (lane == 0 ? (int32_t)x_cnt_s : 0),
+                                                   pv.smax);
+            xd |= __builtin_amdgcn_readlane(fr, 0) != __builtin_amdgcn_readlane(fr, 1);
+          }
+          if (prev_ents) {  // commit i-1, a pod of service s: maxCount rises / first peer
+            flag_x = spread_on && x_snapc + (int32_t)x_cnt_s > pv.smax;
+            if (aff_on && peer0 == -1 && !((L_peerset[s >> 5] >> (s & 31)) & 1u)) flag_x = true;
+          }
+        }
+        if (nk && xnk) {  // PodFitsPorts / NoDiskConflict: lane t holds key t
+          bool hit = false;
+          for (uint32_t b = 0; b < nk; ++b) {
+            const bool on = b < pv.n_ports ? ports_on : disk_on;
+            hit |= on && kt < xnk && xcl == (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b));
+          }
+          xd |= __ballot(hit) != 0;
+        }
+        res = (xd ? 1u : 0u) | (flag_x ? 2u : 0u);
+      }
+      if (lane == 0) {
+        ctl->xres[par] = res;
+        if constexpr (STAMP) ctl->t_x = (uint32_t)__builtin_amdgcn_s_memtime();
+        st_rel(&ctl->xseq, i + 1);
+      }
+      // off the chain now: commit i-1's service flags and first peers (the
+      // committer reads them for pod i+1 once this iteration is done)
+      if (xnode != ~0u) flags(i - 1, xnode, xcid, xslot, bns, prec);
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        x_acc += lane == 29 ? t_now - x_last : 0ULL;
+        x_last = t_now;
+      }
+    }
+    // the committer is done: the commits from i-1 on were not replayed yet; their
+    // first peers still count (the window's end writes them)
+    for (uint32_t spin = 0; !ld_acq(&ctl->stop); ++spin) {
+      if (spin > 16 * KSG_SPIN_LIMIT) {
+        ctl->hang = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const uint32_t R = __builtin_amdgcn_readfirstlane(ctl->resolved);
+    for (uint32_t q = i >= 1 ? i - 1 : 0; q < R; ++q) {
+      if (__builtin_amdgcn_readfirstlane(L_cm[q].kind) != 1) continue;
+      const uint32_t node = __builtin_amdgcn_readfirstlane(L_cm[q].node);
+      const uint32_t cid = (__builtin_amdgcn_readfirstlane(L_cm[q].flags) >> 1) & 7u;
+      const uint32_t prec = lane < DW ? r_rec[(q % RING) * DW + lane] : 0u;
+      uint32_t slot, bnk, bns;
+      uint64_t dlc, dlm;
+      replay(node, prec, slot, bnk, bns, dlc, dlm);
+      flags(q, node, cid, slot, bns, prec);
+    }
+    if constexpr (STAMP) {
+      if (lane >= 28 && lane < 32) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
+    }
+    if (lane == 0) st_rel(&ctl->fin_x, 1u);
+    return;
+  }
+  if (wave != 0) return;
+
+  // =========================================================================
+  // committer (wave 0)
+  // =========================================================================
+  __builtin_amdgcn_s_setprio(3);
+  uint32_t resolved = n_pods, reason = 0, n_slots = 0, n_draws = 0;
+  uint32_t cn0 = ~0u, cn1 = ~0u;  // nodes of slots lane and 64 + lane
+  uint32_t sk0 = 0, sk1 = 0;      // their key counts
+  uint32_t ss0 = 0, ss1 = 0;      // their service entry counts
+  int64_t dc0 = 0, dm0 = 0, dc1 = 0, dm1 = 0;  // their window deltas (current through the last commit)
+  bool have_x = false;                   // commit i-1's node x (and its slot)
+  uint32_t xnode = 0, xslot = 0;
+  uint64_t t_last = 0, t_acc = 0;
+#define KSG_STAMPP(k)                                        \
+  if constexpr (STAMP) {                                     \
+    const uint64_t t_now = __builtin_amdgcn_s_memtime();     \
+    t_acc += lane == (uint32_t)(k) ? t_now - t_last : 0ULL;  \
+    t_last = t_now;                                          \
+  }
+#define KSG_COUNTP(k, v)                                   \
+  if constexpr (STAMP) {                                   \
+    t_acc += lane == (uint32_t)(k) ? (uint64_t)(v) : 0ULL; \
+  }
+  if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
+  for (uint32_t i = 0; i < n_pods; ++i) {
+    const uint32_t e = i % RING, par = i & 1;
+    if (ld_u(&r_hdr[e].ready) != i + 1) {
+      __builtin_amdgcn_s_setprio(0);  // a producer shares this SIMD: do not starve it
+      bool hung = false;
+      for (uint32_t spin = 0; ld_u(&r_hdr[e].ready) != i + 1; ++spin)
+        if (spin > 16 * KSG_SPIN_LIMIT || ld_u(&ctl->hang)) {
+          hung = true;
+          break;
+        }
+      __builtin_amdgcn_s_setprio(3);
+      if (hung) {
+        resolved = i;
+        reason = KSG_STOP_HANG;
+        break;
+      }
+    }
+    acq_lds();
+    if constexpr (STAMP) {  // ring wait of the window's first 4 pods (lane 10) vs the rest (lane 11)
+      const uint64_t t_now = __builtin_amdgcn_s_memtime();
+      t_acc += lane == (i < 4 ? 10u : 11u) ? t_now - t_last : 0ULL;
+    }
+    KSG_STAMPP(0)
+    if (skew & 1u) __builtin_amdgcn_s_sleep(8);
+    // ---- the staged pod (one round of LDS reads): record, header, r mod
+    // (k0 - d), the row prefixes (lane q < P), the candidates (lane c < 6),
+    // where x sits in T0
+    const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
+    const uint32_t rmod = r_mod[e * 64 + lane];
+    const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
+    uint32_t lp_ex = 0, lp_in = 0;
+    if (lane < P) {
+      lp_ex = r_lp[(e * 32 + lane) * 2];
+      lp_in = r_lp[(e * 32 + lane) * 2 + 1];
+    }
+    const uint32_t cand = lane < KSG_NCAND ? r_cand[e * 8 + lane] : ~0u;
+    uint64_t t0x = 0;
+    uint32_t xpos0 = 0;
+    if (have_x) {
+      const uint32_t xw = xnode >> 6;
+      t0x = t0e[xw];
+      xpos0 = r_lp[(e * 32 + (xw >> 6)) * 2] + r_wp[(size_t)e * P * 64 + xw];
+    }
+    const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
+    const uint32_t k0 = __builtin_amdgcn_readfirstlane(r_hdr[e].k0);
+    const int32_t pred = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].pred);
+    if (__builtin_amdgcn_readlane(rec, WS_ERR) || m0 == KSG_S32_NONE) {
+      // ServiceAffinity peer error / nothing fit at the snapshot (commits only
+      // remove fits): no draw, no commit
+      if (lane == 0) {
+        L_cm[i].kind = 0;
+        L_out[i] = __builtin_amdgcn_readlane(rec, WS_ERR) ? KSG_OUT_ERROR : KSG_OUT_NOFIT;
+        L_xn[i] = ~0u;
+        st_rel(&ctl->xn_seq, i + 1);
+        st_rel(&ctl->sel_seq, i + 1);
+      }
+      have_x = false;  // pod i+1's checkers see every commit up to i-1
+      continue;
+    }
+    const PodView pv = pod_view(rec);
+    const int32_t s = pv.s;
+    const uint32_t nss = __builtin_amdgcn_readlane(rec, WS_NSS);
+    const uint32_t n_sel = nss & 0xffff, n_svcs = nss >> 16, nk = pv.nk;
+    if (__builtin_amdgcn_readlane(rec, WS_NINL) > KSG_WIN_INLINE || nk > KSG_SLOT_KEYS || n_svcs > KSG_SLOT_SVCS) {
+      resolved = i;  // lists longer than the record / a slot: the exact per-pod kernel takes it
+      reason = i == 0 ? KSG_STOP_OVERSIZE : KSG_STOP_SLOT;
+      break;
+    }
+    KSG_STAMPP(1)
+    // ---- the checkers' drops (slots as of commits <= i-2) and the x-checker's
+    // verdict on commit i-1's node
+    bool hung = false;
+    for (uint32_t spin = 0;; ++spin) {
+      const uint32_t xs = ld_rlx(&ctl->xseq), hg = ld_rlx(&ctl->hang);
+      uint32_t cs = ld_rlx(&ctl->chk_seq[0]);
+#pragma unroll
+      for (int c = 1; c < KSG_RES_NCHK; ++c) cs = min(cs, ld_rlx(&ctl->chk_seq[c]));
+      if (cs >= i + 1 && xs >= i + 1) break;
+      if (spin > 16 * KSG_SPIN_LIMIT || hg) {
+        hung = true;
+        break;
+      }
+    }
+    acq_lds();
+    if (hung) {
+      resolved = i;
+      reason = KSG_STOP_HANG;
+      break;
+    }
+    KSG_STAMPP(2)
+    if constexpr (STAMP) t_acc += lane == 6 ? (uint64_t)(uint32_t)((uint32_t)t_last - ctl->t_x) : 0ULL;
+    // one round of LDS reads: drop counts and masks, the drops' positions, the
+    // verdict, the service flag word
+    const uint32_t cc0 = ctl->chk_cnt[0][par], cc1 = ctl->chk_cnt[1][par];
+    const uint32_t xres = __builtin_amdgcn_readfirstlane(ctl->xres[par]);
+    const uint32_t fw = s >= 0 ? L_flag[s >> 5] : 0u;
+    const uint64_t msk0 = ((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[0][par][1]) << 32) |
+                          (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[0][par][0]);
+    const uint64_t msk1 = ((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[1][par][1]) << 32) |
+                          (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[1][par][0]);
+    const uint32_t dp0 = L_dpos[par * KSG_MAX_SLOTS + lane];
+    const uint32_t dp1 = L_dpos[par * KSG_MAX_SLOTS + 64 + lane];
+    if (s >= 0 && (spread_on || aff_on) && ((xres & 2u) || ((__builtin_amdgcn_readfirstlane(fw) >> (s & 31)) & 1u))) {
+      resolved = i;  // a service scalar this pod reads changed in the window
+      reason = KSG_STOP_SERVICE;
+      break;
+    }
+    // x counts as a new drop iff it is a snapshot tie whose slot the checkers
+    // kept (a new slot: they have not seen it)
+    const bool x_kept = !(((xslot < 64 ? msk0 : msk1) >> (xslot & 63)) & 1ULL);
+    const bool x_drop = have_x && (xres & 1u) && ((t0x >> (xnode & 63)) & 1ULL) && x_kept;
+    const uint32_t dropped = __builtin_amdgcn_readfirstlane(cc0) + __builtin_amdgcn_readfirstlane(cc1) + (x_drop ? 1u : 0u);
+    if (dropped >= k0) {
+      resolved = i;  // every snapshot tie got worse: needs a fresh snapshot
+      reason = KSG_STOP_EXHAUSTED;
+      break;
+    }
+    // ---- selection: k live ties, the ix-th in descending rank = the (k-1-ix)-th ascending
+    const uint32_t k = k0 - dropped;
+    uint32_t woff;
+    if (dropped == 0) {
+      woff = (uint32_t)pred;  // staged by the producer
+    } else {
+      // T0's tp-th node ascending, tp the least fixed point of
+      // tp = t + #(drop positions <= tp): its row (row prefixes, lane q < P),
+      // its word (the row's word prefixes) and its bit (mbcnt rank)
+      KSG_COUNTP(7, 64)
+      uint32_t ix;
+      if (dropped < 64) {
+        ix = (uint32_t)__builtin_amdgcn_readlane((int)rmod, (int)dropped);
+      } else {
+        const uint64_t r = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(r_hdr[e].r >> 32)) << 32) |
+                           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r_hdr[e].r);
+        ix = umod64_32(r, k);
+      }
+      const uint32_t t = k - 1 - ix;
+      const uint32_t d0 = ((msk0 >> lane) & 1ULL) ? dp0 : ~0u;
+      const uint32_t d1 = ((msk1 >> lane) & 1ULL) ? dp1 : ~0u;
+      const uint32_t xpos = x_drop ? xpos0 + (uint32_t)__popcll(t0x & ((1ULL << (xnode & 63)) - 1ULL)) : ~0u;
+      uint32_t tp = t;
+      for (;;) {
+        const uint32_t cnt = (uint32_t)__popcll(__ballot(d0 <= tp)) + (uint32_t)__popcll(__ballot(d1 <= tp)) +
+                             (xpos <= tp ? 1u : 0u);
+        if (t + cnt == tp) break;
+        tp = t + cnt;
+      }
+      const uint32_t qs = (uint32_t)__builtin_ctzll(__ballot(lane < P && lp_ex <= tp && tp < lp_in));
+      const uint32_t loc = tp - (uint32_t)__builtin_amdgcn_readlane((int)lp_ex, (int)qs);
+      const uint64_t w = t0e[qs * 64 + lane];
+      const uint32_t wpq = r_wp[(size_t)e * P * 64 + qs * 64 + lane];
+      const uint32_t ls = (uint32_t)__builtin_ctzll(__ballot(wpq <= loc && loc < wpq + (uint32_t)__popcll(w)));
+      const uint64_t ws = readlane64(w, (int)ls);
+      const uint32_t lw = loc - (uint32_t)__builtin_amdgcn_readlane((int)wpq, (int)ls);
+      const uint32_t rank =
+          __builtin_amdgcn_mbcnt_hi((uint32_t)(ws >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ws, 0u));
+      const uint32_t bsel = (uint32_t)__builtin_ctzll(__ballot(((ws >> lane) & 1ULL) && rank == lw));
+      woff = (qs * 64 + ls) * 64 + bsel;
+    }
+    const uint64_t cm = __ballot(cand == woff);
+    const uint32_t cidx = cm ? (uint32_t)__builtin_ctzll(cm) : KSG_NO_CAND;
+    if (lane == 0) {  // the x-checker takes the node's snapshot meanwhile
+      L_xn[i] = woff | (cidx << 28);
+      if constexpr (STAMP) ctl->t_n = (uint32_t)__builtin_amdgcn_s_memtime();
+      st_rel(&ctl->xn_seq, i + 1);
+    }
+    KSG_STAMPP(3)
+    // ---- AssumePod's slot
+    const uint64_t hit0 = __ballot(cn0 == woff);
+    const uint64_t hit1 = __ballot(cn1 == woff);
+    const bool in_c = (hit0 | hit1) != 0;
+    uint32_t slot, base_nk = 0, base_ns = 0;
+    int64_t base_dc = 0, base_dm = 0;
+    if (in_c) {
+      slot = hit0 ? (uint32_t)__builtin_ctzll(hit0) : 64u + (uint32_t)__builtin_ctzll(hit1);
+      const uint32_t sl = slot & 63;
+      base_nk = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? sk0 : sk1), (int)sl);
+      base_ns = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? ss0 : ss1), (int)sl);
+      if (base_nk + nk > KSG_SLOT_KEYS || base_ns + n_svcs > KSG_SLOT_SVCS) {
+        resolved = i;  // this pod is redone (with the same draw) in the next window
+        reason = KSG_STOP_SLOT;
+        break;
+      }
+      base_dc = (int64_t)readlane64((uint64_t)(slot < 64 ? dc0 : dc1), (int)sl);
+      base_dm = (int64_t)readlane64((uint64_t)(slot < 64 ? dm0 : dm1), (int)sl);
+    } else {
+      if (n_slots == KSG_MAX_SLOTS) {
+        resolved = i;
+        reason = KSG_STOP_SLOT;
+        break;
+      }
+      slot = n_slots++;
+    }
+    const int64_t new_dc = (int64_t)((uint64_t)base_dc + (uint64_t)pv.req_c);
+    const int64_t new_dm = (int64_t)((uint64_t)base_dm + (uint64_t)pv.req_m);
+    const uint32_t wn = d.lo + woff;
+    KSG_STAMPP(4)
+    // the slot's table row: the pod's keys and service ids (record lane L holds
+    // dword L, so each list entry is stored by the lane that holds it)
+    {
+      uint32_t* row = L_cl + (size_t)slot * KSG_CL_W;
+      const uint32_t kt = lane - WS_IDS, st_ = lane - (WS_IDS + nk + n_sel);
+      if (kt < nk) row[KSG_CL_KEY + base_nk + kt] = rec;
+      if (st_ < n_svcs) row[KSG_CL_SV + base_ns + st_] = rec;
+    }
+    if (lane == 0) {
+      L_cm[i] = PlCommit{1u, slot, woff,
+                         (in_c ? 0u : 1u) | (cidx << 1) | (n_svcs << 8) | (base_ns << 16) | (base_nk << 24)};
+      L_out[i] = (int32_t)wn;
+      st_rel(&ctl->sel_seq, i + 1);  // the checkers move on
+    }
+    if ((int32_t)woff != pred) KSG_COUNTP(8, 64)
+    if (lane == (slot & 63)) {  // this wave's counts and deltas of the slot
+      if (slot >= 64) {
+        if (!in_c) cn1 = woff;
+        dc1 = new_dc;
+        dm1 = new_dm;
+        sk1 = base_nk + nk;
+        ss1 = base_ns + n_svcs;
+      } else {
+        if (!in_c) cn0 = woff;
+        dc0 = new_dc;
+        dm0 = new_dm;
+        sk0 = base_nk + nk;
+        ss0 = base_ns + n_svcs;
+      }
+    }
+    have_x = true;
+    xnode = woff;
+    xslot = slot;
+    ++n_draws;
+    KSG_STAMPP(5)
+  }
+  if (lane == 0) {
+    ctl->resolved = resolved;
+    st_rel(&ctl->stop, 1u);
+  }
+  // the checkers apply the last commits and write their slots back; the
+  // x-checker records the last first peers
+  bool drained = false;
+  for (uint32_t spin = 0; spin <= 16 * KSG_SPIN_LIMIT; ++spin) {
+    bool done = ld_acq(&ctl->fin_x) != 0;
+#pragma unroll
+    for (int c = 0; c < KSG_RES_NCHK; ++c) done = done && ld_acq(&ctl->fin[c]) != 0;
+    if (done) {
+      drained = true;
+      break;
+    }
+  }
+  if (!drained || ld_acq(&ctl->hang)) reason = KSG_STOP_HANG;
+  if constexpr (STAMP) {
+    if (lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
+  }
+#undef KSG_STAMPP
+#undef KSG_COUNTP
+  const uint32_t n_peer = __builtin_amdgcn_readfirstlane(ctl->n_peer);
+  for (uint32_t t = lane; t < n_peer; t += 64) {
+    const uint32_t sv = L_peer[2 * t];
+    int32_t expect = -1;
+    __hip_atomic_compare_exchange_strong(d.svc_peer + sv, &expect, (int32_t)L_peer[2 * t + 1], __ATOMIC_RELAXED,
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (uint32_t t = lane; t < resolved; t += 64) out[t] = L_out[t];
+  if (lane == 0) {
+    *rng_io = rng0 + (uint64_t)n_draws * 0x9E3779B97F4A7C15ULL;
+    if (reason == KSG_STOP_HANG) {
+      run->halt = KSG_HALT_HANG;
+    } else if (reason == KSG_STOP_OVERSIZE) {
+      run->halt = KSG_HALT_OVERSIZE;  // pod pos: the host runs the exact per-pod path, then resumes
+    } else if (resolved == 0 || resolved > n_pods) {
+      run->halt = KSG_HALT_BADCOUNT;
+    } else {
+      run->pos = pos + resolved;
+      run->windows += 1;
+      if (reason >= 1 && reason <= 3) run->stops[reason] += 1;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host launcher
+// ---------------------------------------------------------------------------
+uint32_t ksg_win_plain_lds(const KsgDev& d, uint32_t wcap) {
+  const uint32_t P = (d.nwords + 63) / 64;
+  const uint32_t PP = P <= 1 ? 1 : P <= 2 ? 2 : P <= 4 ? 4 : P <= 8 ? 8 : P <= 16 ? 16 : 32;
+  return plain_lds_offsets(PP, (d.n_services + 31) / 32, wcap).total;
+}
+
+template <int PP, bool ST>
+static hipError_t win_plain_launch(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run, const KsgWinSum* sums,
+                                   const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_plain_kernel<PP, ST>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipGetLastError();  // do not leave a sticky error behind
+    once = true;
+  }
+  hipLaunchKernelGGL((ksg_win_plain_kernel<PP, ST>), dim3(1), dim3(512), lds, st, d, wcap, run, sums, x, rng, out);
+  return hipGetLastError();
+}
+
+hipError_t ksg_launch_win_plain(const KsgDev& d, uint32_t P, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
+                                const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
+  const size_t lds = plain_lds_offsets(P, (d.n_services + 31) / 32, wcap).total;
+  const bool stamp = (d.dbg & 8) != 0;  // KSG_DEBUG & 8: per-section s_memtime stamps
+#define KSG_PLAIN_CASE(PP)                                                                  \
+  if (P == PP)                                                                              \
+    return stamp ? win_plain_launch<PP, true>(d, wcap, lds, run, sums, x, rng, out, st)    \
+                 : win_plain_launch<PP, false>(d, wcap, lds, run, sums, x, rng, out, st);
+  KSG_PLAIN_CASE(1)
+  KSG_PLAIN_CASE(2)
+  KSG_PLAIN_CASE(4)
+  KSG_PLAIN_CASE(8)
+  KSG_PLAIN_CASE(16)
+  KSG_PLAIN_CASE(32)
+#undef KSG_PLAIN_CASE
+  return hipErrorInvalidValue;
+}

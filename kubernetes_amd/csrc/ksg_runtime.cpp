@@ -115,6 +115,10 @@ struct ksg_ctx {
 
   // cluster
   bool have_cluster = false;
+  // a batch failed after its device work was enqueued: the device may hold some
+  // of its commits and the host mirror none, so every call fails until
+  // ksg_set_cluster uploads the cluster again
+  bool diverged = false;
   uint32_t N = 0, nw = 0, n_pairs = 0, S = 0, D = 0;
   uint32_t lo = 0, hi = 0, wlo = 0, nwords = 0, nwords_max = 0;
   std::vector<uint32_t> shard_wlo_h;
@@ -189,6 +193,8 @@ struct ksg_ctx {
   uint32_t last_stats[4] = {0, 0, 0, 0};  // windows, stops (service scalar), stops (ties exhausted)
   std::vector<hipEvent_t> wev;     // event pairs around the chained window kernels
   double last_kms[3] = {0, 0, 0};  // phase A ms, phase B ms, launches (window path)
+  double last_wsum = 0;            // window capacity W summed over the launches
+  bool dbg_fail_next = false;      // KSG_DEBUG & 16384: the next window batch fails after its device work
   double last_hus[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // host us per phase of the last batch (ksg_last_batch_host_us)
   double totals[24] = {};  // ksg_batch_totals: the per-batch diagnostics summed over batches
   int64_t max_cap = 0, min_cap = 0;
@@ -650,6 +656,13 @@ bool use_window(ksg_ctx* c, const ksg_pod* pods, uint32_t n) {
   return mu + sum <= lim;
 }
 
+int cluster_ok(ksg_ctx* c) {
+  if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
+  if (c->diverged)
+    return fail(c, KSG_ERR_STATE, "an earlier batch failed after its device work started: call ksg_set_cluster");
+  return KSG_OK;
+}
+
 void drop_deferred(ksg_ctx* c) {
   c->dfr_pods.clear();
   c->dfr_ids.clear();
@@ -881,6 +894,7 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   }
   free_cluster(c);
   drop_deferred(c);
+  c->diverged = false;
   c->ppw_est = 0.0;
   c->N = n_nodes;
   c->nw = (n_nodes + 63) / 64;
@@ -1115,7 +1129,7 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
 
 static int add_pod_impl(ksg_ctx* c, uint32_t host_id, const ksg_pod* pod, const uint32_t* ids) {
   if (int rc0 = flush_deferred(c)) return rc0;
-  if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
+  if (int rs = cluster_ok(c)) return rs;
   int rc = check_pod(c, pod, ids, pod_ids_extent(pod));
   if (rc) return rc;
   rc = mirror_add(c, host_id, pod, ids, true);
@@ -1125,6 +1139,7 @@ static int add_pod_impl(ksg_ctx* c, uint32_t host_id, const ksg_pod* pod, const 
 }
 
 static int remove_pod_impl(ksg_ctx* c, uint64_t uid) {
+  if (c->diverged) return cluster_ok(c);
   if (int rc0 = flush_deferred(c)) return rc0;
   auto it = c->pods.find(uid);
   if (it == c->pods.end()) return fail(c, KSG_ERR_ARG, "unknown pod uid %llu", (unsigned long long)uid);
@@ -1200,7 +1215,7 @@ int ksg_add_pod(ksg_ctx* c, uint32_t host_id, const ksg_pod* pod, const uint32_t
   if (c->ext_on && !c->cur_ext) c->ext_scalar.erase(pod->uid);  // (plain entry point: no extension requests)
   HIPCHK(c, hipSetDevice(c->device));  // reflector threads: patches flush on this context's device
   if (!c->pending) return add_pod_impl(c, host_id, pod, ids);
-  if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
+  if (int rs = cluster_ok(c)) return rs;
   const size_t ext = pod_ids_extent(pod);
   int rc = check_pod(c, pod, ids, ext);
   if (rc) return rc;
@@ -1231,7 +1246,7 @@ int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int6
   if (!c || !pod) return KSG_ERR_ARG;
   KSG_LOCK(c);
   if (int rc0 = flush_deferred(c)) return rc0;
-  if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
+  if (int rs = cluster_ok(c)) return rs;
   HIPCHK(c, hipSetDevice(c->device));
   if (c->pending) {  // the previous begin was abandoned: its queued updates apply now
     c->pending = false;
@@ -1307,7 +1322,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
                        uint64_t* rng_state, int32_t* out_nodes) {
   if (!c || (n && (!pods || !out_nodes)) || !rng_state) return KSG_ERR_ARG;
   KSG_LOCK(c);
-  if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
+  if (int rs = cluster_ok(c)) return rs;
   if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
   HIPCHK(c, hipSetDevice(c->device));
   c->last_ms = 0.0;
@@ -1324,8 +1339,6 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     c->last_hus[k] += std::chrono::duration<double, std::micro>(t - t_last).count();
     t_last = t;
   };
-  if (c->ext_on && !c->cur_ext)  // (plain entry point: the pods carry no extension requests)
-    for (uint32_t i = 0; i < n; ++i) c->ext_scalar.erase(pods[i].uid);
   for (uint32_t i = 0; i < n; ++i) {
     int rc = check_pod(c, pods + i, ids, n_ids);
     if (rc) return rc;
@@ -1354,23 +1367,44 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
   // Host work that overlaps the device: the previous batch's mirror replay, then
   // this batch's deferred-replay inputs (pods, ids, every uid: the few pods that
   // find no node are taken out again after the wait)
+  // (stashed into locals: they become the context's deferred replay only when
+  // the batch succeeds; a failure after the device work started leaves the
+  // context diverged until ksg_set_cluster)
   bool stashed = false, dup_any = false;
+  std::vector<ksg_pod> st_pods;
+  std::vector<uint32_t> st_ids;
+  std::unordered_set<uint64_t> st_uids;
   auto overlap_work = [&]() -> int {
     if (stashed) return KSG_OK;
     int rc2 = flush_deferred(c);
     if (rc2) return rc2;
     hphase(4);
-    c->dfr_pods.assign(pods, pods + n);
-    c->dfr_ids.assign(ids, ids + n_ids);
-    c->dfr_uids.reserve(2 * (size_t)n);
-    for (uint32_t i = 0; i < n; ++i) dup_any |= !c->dfr_uids.insert(pods[i].uid).second;
+    st_pods.assign(pods, pods + n);
+    st_ids.assign(ids, ids + n_ids);
+    st_uids.swap(c->dfr_uids);  // (empty after the flush: keeps its buckets)
+    st_uids.reserve(2 * (size_t)n);
+    for (uint32_t i = 0; i < n; ++i) dup_any |= !st_uids.insert(pods[i].uid).second;
     stashed = true;
     hphase(7);
     return KSG_OK;
   };
+  struct DivergeGuard {
+    ksg_ctx* c;
+    bool armed = false;
+    ~DivergeGuard() {
+      if (armed) {
+        drop_deferred(c);
+        c->diverged = true;
+      }
+    }
+  } guard{c};
+  if (c->dev.dbg & 16384) c->dbg_fail_next = true;  // KSG_DEBUG & 16384: fail the batch after its device work
+  guard.armed = true;  // device work from here on
   HIPCHK(c, hipMemcpyAsync(c->d_rng, rng_state, 8, hipMemcpyHostToDevice, c->st));
   HIPCHK(c, hipEventRecord(c->ev0, c->st));
   c->last_stats[0] = c->last_stats[1] = c->last_stats[2] = c->last_stats[3] = 0;
+  c->last_kms[0] = c->last_kms[1] = c->last_kms[2] = 0;
+  c->last_wsum = 0;
   hphase(1);
   if (use_window(c, pods, n)) {
     // Window path. Phase A scores the window on this rank's shard; with world > 1
@@ -1448,6 +1482,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     };
     uint32_t pos = 0, K = round_k(n);
     c->last_kms[0] = c->last_kms[1] = c->last_kms[2] = 0;
+    c->last_wsum = 0;
     hphase(2);
     while (pos < n) {
       if (c->wev.size() < 2 * (size_t)K + 1) {
@@ -1514,8 +1549,13 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
         c->last_kms[1] += eb * K / nt;
       }
       c->last_kms[2] += K;
+      c->last_wsum += (double)W * K;
       c->last_stats[0] += r.windows;
       for (int q = 1; q <= 3; ++q) c->last_stats[q] += r.stops[q];
+      if (c->dbg_fail_next) {
+        c->dbg_fail_next = false;
+        return fail(c, KSG_ERR_STATE, "window resolver: injected failure (KSG_DEBUG & 16384) at pod %u", r.pos);
+      }
       if (r.halt == KSG_HALT_HANG) return fail(c, KSG_ERR_STATE, "window resolver: ring wait timed out at pod %u", r.pos);
       if (r.halt == KSG_HALT_BADCOUNT || r.pos < pos || r.pos > n)
         return fail(c, KSG_ERR_STATE, "window resolver: bad progress (halt %u, pos %u -> %u)", r.halt, pos, r.pos);
@@ -1571,6 +1611,15 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
   c->last_ms = ms;
   // the device applied every commit; the host mirror replays them later
   // (flush_deferred), overlapped with the next batch's device work
+  if (!stashed) {  // (overlap_work ran on every path that reaches here)
+    return fail(c, KSG_ERR_STATE, "internal: batch replay inputs missing");
+  }
+  guard.armed = false;
+  if (c->ext_on && !c->cur_ext)  // (plain entry point: the pods carry no extension requests)
+    for (uint32_t i = 0; i < n; ++i) c->ext_scalar.erase(pods[i].uid);
+  c->dfr_pods.swap(st_pods);
+  c->dfr_ids.swap(st_ids);
+  c->dfr_uids.swap(st_uids);
   c->dfr_out.assign(out_nodes, out_nodes + n);
   for (uint32_t i = 0; i < n; ++i)  // the uids of the pods that found no node are free again
     if (out_nodes[i] < 0 && !dup_any) c->dfr_uids.erase(pods[i].uid);
@@ -1591,6 +1640,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
   t[0] += 1;
   t[1] += c->last_ms;
   for (int q = 0; q < 3; ++q) t[2 + q] += c->last_kms[q];
+  t[17] += c->last_wsum;
   for (int q = 0; q < 4; ++q) t[5 + q] += c->last_stats[q];
   for (int q = 0; q < 8; ++q) t[9 + q] += c->last_hus[q];
   return KSG_OK;
@@ -1600,7 +1650,7 @@ int ksg_evaluate(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, uint8_t* f
   if (!c || !pod) return KSG_ERR_ARG;
   KSG_LOCK(c);
   if (int rc0 = flush_deferred(c)) return rc0;
-  if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
+  if (int rs = cluster_ok(c)) return rs;
   if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
   HIPCHK(c, hipSetDevice(c->device));
   if (c->N == 0) return KSG_NONODES;
@@ -1720,10 +1770,18 @@ static int admit_impl(ksg_ctx* c, int mode, const ksg_admission_set* sets, uint3
     if ((mode & KSG_ADMIT_MODE_SELECTOR) && (uint64_t)sets[s].label_off + sets[s].n_labels > n_pairs)
       return fail(c, KSG_ERR_ARG, "admission set %u: labels out of range", s);
   }
-  if (mode & KSG_ADMIT_MODE_SELECTOR)
+  if (mode & KSG_ADMIT_MODE_SELECTOR) {
+    if ((n_ids && !ids) || (n_pairs && !pairs)) return fail(c, KSG_ERR_ARG, "admission: ids / pairs == NULL");
     for (uint32_t i = 0; i < n_pods; ++i)
       if ((uint64_t)pods[i].sel_off + pods[i].n_sel > n_ids)
         return fail(c, KSG_ERR_ARG, "pod %u: nodeSelector ids out of range", i);
+  }
+  // each pod in at most one set (one kernel lane per set writes its pods' results)
+  std::vector<uint8_t> in_set(n_pods, 0);
+  for (uint32_t s = 0; s < n_sets; ++s)
+    for (uint32_t k = 0; k < sets[s].n_pods; ++k)
+      if (in_set[sets[s].pod_off + k]++)
+        return fail(c, KSG_ERR_ARG, "admission sets %u and an earlier one share pod %u", s, sets[s].pod_off + k);
   for (uint32_t i = 0; i < n_pods; ++i) out[i] = KSG_ADMIT_OK;  // pods in no set
   if (n_sets == 0 || n_pods == 0) return KSG_OK;
   HIPCHK(c, hipSetDevice(c->device));
@@ -1749,8 +1807,6 @@ static int admit_impl(ksg_ctx* c, int mode, const ksg_admission_set* sets, uint3
   HIPCHK(c, hipMemcpyAsync(c->h_dn, c->d_admit + o_out, n_pods, hipMemcpyDeviceToHost, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
   // pods outside every set keep KSG_ADMIT_OK; the kernel wrote the others
-  std::vector<uint8_t> in_set(n_pods, 0);
-  for (uint32_t s = 0; s < n_sets; ++s) memset(in_set.data() + sets[s].pod_off, 1, sets[s].n_pods);
   for (uint32_t i = 0; i < n_pods; ++i)
     if (in_set[i]) out[i] = c->h_dn[i];
   return KSG_OK;
@@ -1809,9 +1865,13 @@ int ksg_set_node_ext(ksg_ctx* c, uint32_t n_nodes, const int64_t* scalar_cap, co
 
 // validate a pod's extension record against the call's id array and record its
 // extended-resource requests by uid (the host mirror's AssumePod/remove)
-static int note_ext(ksg_ctx* c, const ksg_pod* p, const ksg_pod_ext* e, size_t n_ids) {
+static int check_ext_range(ksg_ctx* c, const ksg_pod_ext* e, size_t n_ids) {
   if ((size_t)e->hard_off + e->n_hard > n_ids || (size_t)e->soft_off + e->n_soft > n_ids)
     return fail(c, KSG_ERR_ARG, "extension taint list out of range");
+  return KSG_OK;
+}
+static int note_ext(ksg_ctx* c, const ksg_pod* p, const ksg_pod_ext* e, size_t n_ids) {
+  if (int rc = check_ext_range(c, e, n_ids)) return rc;
   std::array<int64_t, KSG_MAX_SCALAR> sc{};
   bool any = false;
   for (uint32_t q = 0; q < c->ext.n_scalar; ++q) {
@@ -1852,14 +1912,22 @@ int ksg_schedule_batch_ext(ksg_ctx* c, const ksg_pod* pods, const ksg_pod_ext* e
   if (!c || (n && (!pods || !out_nodes)) || !rng_state) return KSG_ERR_ARG;
   KSG_LOCK(c);
   if (ext && !c->ext_on) return fail(c, KSG_ERR_STATE, "extensions are off");
+  // validate the whole batch first; each placed pod's extended-resource requests
+  // are recorded (for the host mirror's deferred replay) only once the batch
+  // succeeded, and the pods that found no node leave no entry
   if (c->ext_on && ext)
     for (uint32_t i = 0; i < n; ++i) {
-      if (int rc = note_ext(c, pods + i, ext + i, n_ids)) return rc;
+      if (int rc = check_ext_range(c, ext + i, n_ids)) return rc;
       if (int rc = check_taint_ids(c, ext + i, ids)) return rc;
     }
   c->cur_ext = ext;
   const int rc = ksg_schedule_batch(c, pods, n, ids, n_ids, rng_state, out_nodes);
   c->cur_ext = nullptr;
+  if (rc == KSG_OK && c->ext_on && ext)
+    for (uint32_t i = 0; i < n; ++i) {
+      if (out_nodes[i] >= 0) (void)note_ext(c, pods + i, ext + i, n_ids);
+      else c->ext_scalar.erase(pods[i].uid);
+    }
   return rc;
 }
 

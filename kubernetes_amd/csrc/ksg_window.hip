@@ -44,6 +44,7 @@
 // pods over the pod's FILTERED nodes: phase A runs a count pass first, and a
 // window stops at a pod whose service count or domain counts moved.
 #include "ksg_device.h"
+#include "ksg_resolver.h"
 
 #include <algorithm>
 
@@ -56,19 +57,6 @@
 #define KSG_PG_LARGE 8
 #define KSG_PG_WORDS 512
 
-// dword offsets inside KsgWinSum (lane j of the resolver holds dword j)
-#define WS_ERR 2
-#define WS_SVC 3
-#define WS_HOST 4
-#define WS_SMAX 5
-#define WS_STOT 6
-#define WS_NINL 7
-#define WS_CPU 8
-#define WS_MEM 10
-#define WS_AFF 12
-#define WS_NPP 16
-#define WS_NSS 17
-#define WS_IDS 19
 
 // ---------------------------------------------------------------------------
 // phase A
@@ -408,317 +396,6 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
 // state lives in LDS (structure of arrays by slot, at most KSG_MAX_SLOTS).
 // The node state in HBM stays the pristine snapshot while the window
 // resolves; the window's deltas are written back once, at the end.
-// threads of the resolver workgroup: 8 waves
-// (16 waves for P <= 8 measured no faster than 8: the chain, not the producers, limits)
-__host__ __device__ constexpr uint32_t win_res_nt(uint32_t P) { return P <= 8 ? 512u : 512u; }
-#define KSG_RES_C0 2                                  // first checker wave (0: committer, 1: scribe)
-#define KSG_RES_NCHK 2                                // checker waves
-#define KSG_RES_P0 (KSG_RES_C0 + KSG_RES_NCHK)        // first producer wave
-#define KSG_RES_NPW (KSG_RES_NT / 64 - KSG_RES_P0)    // producer waves (KSG_RES_NT: in the kernel)
-// ring entries: 16, or 4 when the T0 words of an entry are large (P > 8: more than 32k nodes)
-__host__ __device__ constexpr uint32_t win_ring(uint32_t P) { return P <= 8 ? 16u : 4u; }
-#define KSG_SLOT_KEYS 8
-#define KSG_SLOT_SVCS 12
-#define KSG_MAX_SLOTS (64 * KSG_RES_NCHK)
-#define KSG_NO_SLOT 0xffffu
-#define KSG_NO_NODE 0xffffffffu
-
-struct alignas(16) I64x2 {
-  int64_t c, m;
-};
-struct alignas(16) F64x2 {
-  double c, m;
-};
-struct alignas(16) SlotMeta {
-  uint32_t node;    // shard offset of the node
-  uint32_t nk, ns;  // conflict keys / service entries added by the window
-  uint32_t smask;   // OR of 1 << (service & 31) over the service entries
-};
-struct alignas(16) RingHdr {
-  int32_t m0;
-  uint32_t k0;
-  uint64_t r;          // Int63 draw of the pod
-  uint32_t ready;      // pod index + 1 once the entry is complete
-  uint32_t drawable;
-  int32_t pred;        // (r mod k0)-th tie of T0 from the top (shard offset), -1: none
-  uint32_t pad;
-  int64_t cap_c, cap_m, used_c, used_m;  // snapshot of pred
-  double inv_c, inv_m;                   // 10 / capacity of pred
-};
-struct alignas(16) RingSvc {  // per service entry t of the pod (t < n_svcs)
-  int32_t cnt[KSG_SLOT_SVCS];   // svc_cnt[sv][pred] at the snapshot
-  int32_t max[KSG_SLOT_SVCS];   // svc_max[sv]
-  int32_t peer[KSG_SLOT_SVCS];  // svc_peer[sv]
-  int32_t pad[4];
-};
-struct alignas(16) WinCtl {
-  uint32_t consumed;    // pods the committer is done with (ring entries free)
-  uint32_t stop;        // the window ended early: every other wave exits
-  uint32_t draw_next;   // next pod allowed to take a draw index
-  uint32_t draw_count;  // draws of pods [0, draw_next)
-  uint32_t sel_seq;     // pods the committer has selected a node for
-  uint32_t xs_slot;     // slot the last selected pod commits into (KSG_NO_SLOT: none)
-  uint32_t xs_nslots;   // slots in use once that pod is committed
-  uint32_t pad0;
-  uint32_t chk_seq[KSG_RES_NCHK];     // pods checker c is done with
-  uint32_t chk_cnt[KSG_RES_NCHK][2];  // checker c's drops for the pod of parity p
-  uint32_t chk_stop[KSG_RES_NCHK][2]; // checker c: the pod's anti-affinity domain counts changed
-  uint32_t order_seq;                 // orders the committer has issued (one per pod)
-  uint32_t scribe_done;               // orders the scribe has written into the slots
-  uint32_t n_peer;                    // services given their first peer in the window
-  uint32_t pad[1];
-};
-// One pod's outcome, handed from the committer to the scribe (two buffers, by
-// pod parity). The scribe reads the pod itself from its ring entry.
-struct alignas(16) WinOrder {
-  uint32_t kind;     // 0: no commit (error / no fit), 1: commit
-  uint32_t slot, node;
-  int32_t out;       // placement (node rank or KSG_OUT_*)
-  uint32_t e;        // ring entry of the pod
-  uint32_t in_c;     // the slot existed before this commit
-  uint32_t is_pred;  // the node is the producer's predicted node (its snapshot is staged)
-  uint32_t pad;
-};
-
-// byte offsets of the resolver's dynamic LDS arrays (host and device agree)
-struct WinLdsOff {
-  uint32_t ctl, r_hdr, r_t0, r_rec, r_mod, r_svc, r_fit;  // ring
-  uint32_t s_meta, s_cap, s_snp, s_dl, s_inv;          // slots
-  uint32_t keys, svcs, scnt;
-  uint32_t peer, out, flag, peerset, drop, ord;
-  // re-rank (dz > 0): ring B words, per-row best scores and domain counts;
-  // the domain rows' node words; window commits per service; the checkers'
-  // per-row count additions by pod parity
-  uint32_t r_b, r_mb, r_dc, zm, nsv, dca;
-  uint32_t total;
-};
-
-__host__ __device__ constexpr uint32_t win_al16(size_t x) { return (uint32_t)((x + 15) & ~(size_t)15); }
-
-__host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag, uint32_t W, bool anti,
-                                                     uint32_t dz = 0, uint32_t nsvc = 0) {
-  WinLdsOff o;
-  const uint32_t KSG_RING = win_ring(P);
-  uint32_t at = 0;
-  o.ctl = at;     at += win_al16(sizeof(WinCtl));
-  o.r_hdr = at;   at += win_al16((size_t)KSG_RING * sizeof(RingHdr));
-  o.r_t0 = at;    at += win_al16((size_t)KSG_RING * P * 64 * 8);
-  o.r_rec = at;   at += win_al16((size_t)KSG_RING * KSG_WIN_SUM_DWORDS * 4);
-  o.r_mod = at;   at += win_al16((size_t)KSG_RING * 64 * 4);
-  o.r_svc = at;   at += win_al16((size_t)KSG_RING * sizeof(RingSvc));
-  o.r_fit = at;   at += anti ? win_al16((size_t)KSG_RING * P * 64 * 8) : 0u;  // fit bitmaps (anti-affinity)
-  o.s_meta = at;  at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(SlotMeta));
-  o.s_cap = at;   at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(I64x2));
-  o.s_snp = at;   at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(I64x2));
-  o.s_dl = at;    at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(I64x2));
-  o.s_inv = at;   at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(F64x2));
-  o.keys = at;    at += win_al16((size_t)KSG_MAX_SLOTS * KSG_SLOT_KEYS * 4);
-  o.svcs = at;    at += win_al16((size_t)KSG_MAX_SLOTS * KSG_SLOT_SVCS * 4);
-  o.scnt = at;    at += win_al16((size_t)KSG_MAX_SLOTS * KSG_SLOT_SVCS * 4);
-  o.peer = at;    at += win_al16((size_t)W * 2 * 4);
-  o.out = at;     at += win_al16((size_t)W * 4);
-  o.flag = at;    at += win_al16((size_t)nflag * 4);
-  o.peerset = at; at += win_al16((size_t)nflag * 4);
-  o.drop = at;    at += win_al16((size_t)2 * P * 64 * 8);
-  o.ord = at;     at += win_al16((size_t)2 * sizeof(WinOrder));
-  o.r_b = at;     at += dz ? win_al16((size_t)KSG_RING * P * 64 * 8) : 0u;
-  o.r_mb = at;    at += dz ? win_al16((size_t)KSG_RING * KSG_RR_MAXZ * 4) : 0u;
-  o.r_dc = at;    at += dz ? win_al16((size_t)KSG_RING * KSG_RR_MAXZ * 4) : 0u;
-  o.zm = at;      at += win_al16((size_t)dz * P * 64 * 8);
-  o.nsv = at;     at += dz ? win_al16((size_t)nsvc * 4) : 0u;
-  o.dca = at;     at += dz ? win_al16((size_t)KSG_RES_NCHK * 2 * KSG_RR_MAXZ * 4) : 0u;
-  o.total = at;
-  return o;
-}
-
-#define KSG_STOP_SERVICE 1
-#define KSG_STOP_EXHAUSTED 2
-#define KSG_STOP_SLOT 3
-#define KSG_STOP_OVERSIZE 4
-#define KSG_STOP_HANG 9        // a ring/draw wait exceeded KSG_SPIN_LIMIT polls (a bug): the host fails
-#define KSG_SPIN_LIMIT (1u << 22)
-
-// a global-address-space load: global_load (vmcnt only), not flat_load, whose
-// lgkmcnt share would make every later LDS wait also wait for it
-template <typename T>
-__device__ __forceinline__ T gld(const T* p) {
-  return *(const __attribute__((address_space(1))) T*)p;
-}
-__device__ __forceinline__ void lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
-__device__ __forceinline__ uint32_t ld_acq(uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void st_rel(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// polling: relaxed LDS loads issue back to back under one lgkmcnt wait (an
-// acquire load waits for each), then one LDS-only acquire once the wait is over
-// (no vmcnt wait on the poller's loads in flight)
-__device__ __forceinline__ uint32_t ld_rlx(uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void acq_lds() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local"); }
-// a polled word as a wave-uniform (scalar) value: the wait loops branch on
-// SCC instead of juggling the exec mask
-__device__ __forceinline__ uint32_t ld_u(uint32_t* p) {
-  return (uint32_t)__builtin_amdgcn_readfirstlane((int)ld_rlx(p));
-}
-
-// The target-th set bit (ascending, 0-based) of the P-word-per-lane bitmap
-// `bits` (lane l owns words l*P + q), given each lane's popcount `cl` and its
-// inclusive prefix `incl`. Wave-uniform result: the word-major bit offset.
-template <int P>
-__device__ __forceinline__ uint32_t select_in_lanes(const uint64_t (&bits)[P], uint32_t cl, uint32_t incl,
-                                                    uint32_t target, uint32_t lane) {
-  const uint32_t excl = incl - cl;
-  const int ol = (int)__builtin_ctzll(__ballot(excl <= target && target < incl));
-  // the owner lane's words, in scalar registers; then the bit by mbcnt rank
-  uint32_t local = target - (uint32_t)__builtin_amdgcn_readlane((int)excl, ol);
-  uint64_t wsel = 0;
-  uint32_t qsel = 0;
-#pragma unroll
-  for (int q = 0; q < P; ++q) {
-    const uint64_t wq = readlane64(bits[q], ol);
-    const uint32_t pc = __popcll(wq);
-    if (qsel == (uint32_t)q) {
-      if (local < pc) {
-        wsel = wq;
-      } else {
-        local -= pc;
-        qsel = q + 1;
-      }
-    }
-  }
-  const uint32_t rank =
-      __builtin_amdgcn_mbcnt_hi((uint32_t)(wsel >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)wsel, 0u));
-  const uint32_t bsel = (uint32_t)__builtin_ctzll(__ballot(((wsel >> lane) & 1ULL) && rank == local));
-  return ((uint32_t)ol * P + qsel) * 64 + bsel;
-}
-
-// LDS views of the slots (structure of arrays by slot index)
-struct WinSlots {
-  SlotMeta* meta;
-  I64x2 *cap, *snp, *dl;
-  F64x2* inv;
-  uint32_t* keys;
-  uint32_t* svcs;
-  int32_t* scnt;
-};
-
-// The pod-side inputs of a re-check (wave-uniform, read from the pod's record).
-struct PodView {
-  int64_t req_c, req_m;
-  bool zero_req;
-  uint32_t n_ports, n_pds, nk;
-  int32_t s, smax;
-};
-
-// Does slot `sl` (a snapshot tie of the pod) score below M0 once the window's
-// deltas are applied? The node fit the pod at the snapshot; only those deltas
-// (requested totals, keys, service counts) can change that. `rec` is this
-// lane's dword of the pod's record (the pod's key ids are read from it).
-__device__ __forceinline__ bool slot_drops(const KsgDev& d, const WinSlots& S, uint32_t sl, const PodView& pv,
-                                           uint32_t rec, bool res_on, bool ports_on, bool disk_on,
-                                           bool spread_on) {
-  const I64x2 cap = S.cap[sl], snp = S.snp[sl], dl = S.dl[sl];
-  const SlotMeta me = S.meta[sl];
-  const int64_t now_c = (int64_t)((uint64_t)snp.c + (uint64_t)dl.c);
-  const int64_t now_m = (int64_t)((uint64_t)snp.m + (uint64_t)dl.m);
-  bool drop = false;
-  if (res_on && !pv.zero_req) {  // PodFitsResources (predicates.go:127-145)
-    const bool fc = cap.c == 0 || cap.c - now_c >= pv.req_c;
-    const bool fm = cap.m == 0 || cap.m - now_m >= pv.req_m;
-    drop = !(fc && fm);
-  }
-  if (pv.nk && !drop && me.nk) {  // PodFitsPorts / NoDiskConflict against the window's keys
-    const uint32_t* ks = S.keys + (size_t)sl * KSG_SLOT_KEYS;
-    for (uint32_t a = 0; a < me.nk; ++a) {
-      const uint32_t key = ks[a];
-      if (ports_on)
-        for (uint32_t b = 0; b < pv.n_ports; ++b)
-          drop |= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + b) == key;
-      if (disk_on)
-        for (uint32_t b = 0; b < pv.n_pds; ++b)
-          drop |= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + pv.n_ports + b) == key;
-    }
-  }
-  if (!drop && d.w_lr) {  // LeastRequested (priorities.go:43-76) can only fall as requested grows
-    const F64x2 iv = S.inv[sl];
-    const int32_t lr_now = lr_win(now_c + pv.req_c, cap.c, iv.c) + lr_win(now_m + pv.req_m, cap.m, iv.m);
-    const int32_t lr_snap = lr_win(snp.c + pv.req_c, cap.c, iv.c) + lr_win(snp.m + pv.req_m, cap.m, iv.m);
-    drop = (lr_now >> 1) != (lr_snap >> 1);
-  }
-  if (!drop && spread_on && pv.s >= 0 && ((me.smask >> (pv.s & 31)) & 1u)) {
-    // ServiceSpreading (spreading.go:72-86) under an unchanged maxCount
-    const uint32_t* sv = S.svcs + (size_t)sl * KSG_SLOT_SVCS;
-    const int32_t* sc = S.scnt + (size_t)sl * KSG_SLOT_SVCS;
-    int32_t delta = 0, snapc = 0;
-    for (uint32_t a = 0; a < me.ns; ++a)
-      if (sv[a] == (uint32_t)pv.s) {
-        snapc = sc[a];
-        ++delta;
-      }
-    if (delta)
-      drop = frac10_f32((int64_t)pv.smax - snapc - delta, pv.smax) != frac10_f32((int64_t)pv.smax - snapc, pv.smax);
-  }
-  return drop;
-}
-
-// ServiceAntiAffinity: a node the pod fitted at the snapshot that it no longer
-// fits (the window's commits took its resources or a key) leaves the pod's
-// filtered set; if the node is labelled and holds pods of the pod's service,
-// the pod's per-domain counts and so the scores of a whole domain change
-// (spreading.go:130-151): not a monotone change, the window must end there.
-__device__ __forceinline__ bool anti_counts_move(const KsgDev& d, uint32_t node, int32_t s) {
-  bool labelled = false;
-#pragma unroll
-  for (int a = 0; a < KSG_MAX_ANTI; ++a)
-    if ((uint32_t)a < d.n_anti && d.w_anti[a] != 0 && d.anti_domain[(size_t)a * d.n_nodes + d.lo + node] >= 0)
-      labelled = true;
-  return labelled && d.svc_cnt[(size_t)s * d.n_nodes + d.lo + node] > 0;
-}
-
-// The resource and key parts of the filter against slot sl's current state
-// (the static parts cannot change in a window).
-__device__ __forceinline__ bool slot_fits_now(const WinSlots& S, uint32_t sl, const PodView& pv, uint32_t rec,
-                                              bool res_on, bool ports_on, bool disk_on) {
-  const I64x2 cap = S.cap[sl], snp = S.snp[sl], dl = S.dl[sl];
-  const int64_t now_c = (int64_t)((uint64_t)snp.c + (uint64_t)dl.c);
-  const int64_t now_m = (int64_t)((uint64_t)snp.m + (uint64_t)dl.m);
-  bool fit = true;
-  if (res_on && !pv.zero_req)
-    fit = (cap.c == 0 || cap.c - now_c >= pv.req_c) && (cap.m == 0 || cap.m - now_m >= pv.req_m);
-  const uint32_t nk = S.meta[sl].nk;
-  if (fit && pv.nk && nk) {
-    const uint32_t* ks = S.keys + (size_t)sl * KSG_SLOT_KEYS;
-    for (uint32_t a = 0; a < nk; ++a) {
-      const uint32_t key = ks[a];
-      if (ports_on)
-        for (uint32_t b = 0; b < pv.n_ports; ++b) fit &= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + b) != key;
-      if (disk_on)
-        for (uint32_t b = 0; b < pv.n_pds; ++b)
-          fit &= (uint32_t)__builtin_amdgcn_readlane(rec, WS_IDS + pv.n_ports + b) != key;
-    }
-  }
-  return fit;
-}
-
-__device__ __forceinline__ PodView pod_view(uint32_t rec) {
-  PodView pv;
-  const uint32_t npp = __builtin_amdgcn_readlane(rec, WS_NPP);
-  pv.req_c = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_CPU) |
-                       ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_CPU + 1) << 32));
-  pv.req_m = (int64_t)((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_MEM) |
-                       ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rec, WS_MEM + 1) << 32));
-  pv.zero_req = pv.req_c == 0 && pv.req_m == 0;
-  pv.n_ports = npp & 0xffff;
-  pv.n_pds = npp >> 16;
-  pv.nk = pv.n_ports + pv.n_pds;
-  pv.s = (int32_t)__builtin_amdgcn_readlane(rec, WS_SVC);
-  pv.smax = (int32_t)__builtin_amdgcn_readlane(rec, WS_SMAX);
-  return pv;
-}
-
 // ANTI: ServiceAntiAffinity is on (its checks are compiled only into these
 // instantiations: they cost the others scalar registers on the chain)
 template <int P, bool STAMP, bool ANTI>
@@ -735,7 +412,6 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
   const uint32_t lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t nflag = (d.n_services + 31) / 32;
-  const uint32_t nshard = d.hi - d.lo;
   const uint32_t nwords = d.nwords;
   constexpr uint32_t KSG_RING = win_ring(P);
   constexpr uint32_t KSG_RES_NT = win_res_nt(P);
@@ -802,23 +478,6 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
   // producers
   // =========================================================================
   if (wave >= KSG_RES_P0) {
-    // warm this XCD's L2 with the node state: the producers' loads of each
-    // pod's predicted node (and the committer's loads of other nodes) then hit L2
-    // (KSG_DEBUG & 64: skip, to measure what it buys)
-    if (!(d.dbg & 64)) {
-      const uint32_t pw = wave - KSG_RES_P0, nt = KSG_RES_NPW * 64;
-      const uint32_t n16 = (nshard + 1) / 2;  // 16-byte chunks of one int64 array
-      uint64_t acc = 0;
-      const int64_t* arr[6] = {d.cap_cpu + d.lo, d.cap_mem + d.lo, d.used_cpu + d.lo, d.used_mem + d.lo,
-                               reinterpret_cast<const int64_t*>(d.inv10_cpu) + d.lo,
-                               reinterpret_cast<const int64_t*>(d.inv10_mem) + d.lo};
-      for (uint32_t t = pw * 64 + lane; t < n16; t += nt) {
-        const uint32_t idx = 2 * t + 1 < nshard ? 2 * t + 1 : 2 * t;
-#pragma unroll
-        for (int a = 0; a < 6; ++a) acc ^= (uint64_t)arr[a][idx];  // six loads in flight
-      }
-      if (acc == 0x5bd1e995a5a5a5a5ULL) ctl->pad[0] = 1;  // keeps the loads
-    }
     const uint32_t* recs = reinterpret_cast<const uint32_t*>(sums);
     // this lane's words lane*P + q: byte offsets of the rank block and row phase
     // A wrote them at (~0u = no such word)
@@ -1752,6 +1411,9 @@ struct alignas(16) WinCtl2 {
   uint32_t n_peer;    // first service peers recorded in the window (L_peer entries)
   uint32_t chk_seq[KSG_RES_NCHK];     // pods checker c is done with
   uint32_t chk_cnt[KSG_RES_NCHK][2];  // checker c's drops for the pod of parity p
+  // (no ServiceAntiAffinity) checker c's dropping slots for the pod of parity p
+  // (lane l: slot 64c + l; its drop's ascending T0 position is in L_dpos)
+  uint32_t chk_msk[KSG_RES_NCHK][2][2];
   uint32_t fin[KSG_RES_NCHK];         // checker c applied every commit and wrote its slots back
   uint32_t hang;                      // a wait exceeded its spin limit (a bug)
   uint32_t xseq;                      // pods the x-checker is done with
@@ -1774,14 +1436,13 @@ struct alignas(16) WinCtl2 {
   // before it applies commit i-1's (the committer adds commit i-1 itself)
   uint32_t xnsv[2];
 };
-// per-slot list table: [0, 8) conflict keys, [8, 20) service ids, [20, 32) the
-// services' counts on the node at the snapshot (written by the owner checker)
-#define KSG_CL_KEY 0
-#define KSG_CL_SV 8
-#define KSG_CL_SC 20
-#define KSG_CL_W 32
 
 struct WinLdsOff2 {
+  // r_lp: per ring entry and lane, the T0 bits in lanes below / up to it
+  // (exclusive, inclusive prefix); r_wp: per ring entry and word, the T0 bits
+  // in the lane's words below it (u16); dpos: the checkers' drop positions in
+  // T0 by pod parity and slot (no ServiceAntiAffinity: the sparse select)
+  uint32_t r_lp, r_wp, dpos;
   uint32_t ctl, r_hdr, r_t0, r_rec, r_mod, r_svc;
   uint32_t cm, out, xn, peer, flag, peerset, drop, pub, drw, clist;
   // ServiceAntiAffinity re-rank (dz > 0; see the LDS-slot resolver's WinLdsOff)
@@ -1792,7 +1453,7 @@ struct WinLdsOff2 {
 __host__ __device__ inline WinLdsOff2 win2_lds_offsets(uint32_t P, uint32_t nflag, uint32_t W, uint32_t dz = 0,
                                                        uint32_t nsvc = 0) {
   WinLdsOff2 o;
-  const uint32_t R = win_ring(P);
+  const uint32_t R = win2_ring(P, dz != 0);
   uint32_t at = 0;
   o.ctl = at;     at += win_al16(sizeof(WinCtl2));
   o.r_hdr = at;   at += win_al16((size_t)R * sizeof(RingHdr));
@@ -1806,7 +1467,7 @@ __host__ __device__ inline WinLdsOff2 win2_lds_offsets(uint32_t P, uint32_t nfla
   o.peer = at;    at += win_al16((size_t)W * 2 * 4);
   o.flag = at;    at += win_al16((size_t)nflag * 4);
   o.peerset = at; at += win_al16((size_t)nflag * 4);
-  o.drop = at;    at += win_al16((size_t)2 * P * 64 * 8);
+  o.drop = at;    at += dz ? win_al16((size_t)2 * P * 64 * 8) : 0u;  // (the re-rank's drop bitmap)
   o.pub = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
   o.drw = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
   o.clist = at;   at += win_al16((size_t)KSG_MAX_SLOTS * KSG_CL_W * 4);
@@ -1819,18 +1480,13 @@ __host__ __device__ inline WinLdsOff2 win2_lds_offsets(uint32_t P, uint32_t nfla
   o.dca = at;     at += dz ? win_al16((size_t)KSG_RES_NCHK * 2 * KSG_RR_MAXZ * 4) : 0u;
   o.r_kz = at;    at += dz ? win_al16((size_t)R * KSG_RR_MAXZ * 4) : 0u;
   o.ddr = at;     at += dz ? win_al16((size_t)KSG_RES_NCHK * 2 * KSG_RR_MAXZ * 4) : 0u;
+  o.r_lp = at;    at += dz ? 0u : win_al16((size_t)R * 64 * 8);
+  o.r_wp = at;    at += dz ? 0u : win_al16((size_t)R * P * 64 * 2);
+  o.dpos = at;    at += dz ? 0u : win_al16((size_t)2 * KSG_MAX_SLOTS * 4);
   o.total = at;
   return o;
 }
 
-// One slot in a checker lane's registers.
-struct RegSlot {
-  uint32_t node;  // shard offset; ~0u: the lane owns no slot yet
-  int64_t cap_c, cap_m, snp_c, snp_m, dl_c, dl_m;
-  double inv_c, inv_m;
-  uint32_t nk, ns, smask;  // list lengths as of the commits this checker applied
-  uint32_t row;            // (ServiceAntiAffinity re-rank) the node's domain row, ~0u unlabelled
-};
 
 // ANTI: ServiceAntiAffinity with the re-rank (x.rr; the LDS-slot resolver above
 // takes every other anti-affinity configuration)
@@ -1848,9 +1504,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   const uint32_t lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t nflag = (d.n_services + 31) / 32;
-  const uint32_t nshard = d.hi - d.lo;
   const uint32_t nwords = d.nwords;
-  constexpr uint32_t RING = win_ring(P);
+  constexpr uint32_t RING = win2_ring(P, ANTI);
   constexpr uint32_t NT = 512;
   constexpr uint32_t NPW = NT / 64 - KSG_RES_P0;  // producer waves
   constexpr uint32_t DW = KSG_WIN_SUM_DWORDS;
@@ -1884,6 +1539,9 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   uint32_t* L_pub = reinterpret_cast<uint32_t*>(smem + o.pub);    // pods whose drawable bit is known
   uint32_t* L_drw = reinterpret_cast<uint32_t*>(smem + o.drw);    // drawable pods
   uint32_t* L_cl = reinterpret_cast<uint32_t*>(smem + o.clist);   // [slot][KSG_CL_W]
+  uint32_t* r_lp = reinterpret_cast<uint32_t*>(smem + o.r_lp);    // [ring][64][2] lane prefix (excl, incl)
+  uint16_t* r_wp = reinterpret_cast<uint16_t*>(smem + o.r_wp);    // [ring][P*64] prefix within the lane
+  uint32_t* L_dpos = reinterpret_cast<uint32_t*>(smem + o.dpos);  // [2][KSG_MAX_SLOTS] drop positions
   const bool spread_on = d.w_spread != 0;
   const bool aff_on = (d.preds & KSG_PRED_SERVICEAFFINITY) && d.n_aff > 0;
   const bool res_on = (d.preds & KSG_PRED_PODFITSRESOURCES) != 0;
@@ -1901,7 +1559,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     L_pub[w] = 0;
     L_drw[w] = 0;
   }
-  for (uint32_t w = tid; w < 2 * P * 64u; w += NT) L_drop[w] = 0;
+  if constexpr (ANTI)
+    for (uint32_t w = tid; w < 2 * P * 64u; w += NT) L_drop[w] = 0;
   if constexpr (ANTI) {
     for (uint32_t t = tid; t < dz * P * 64; t += NT) {
       const uint32_t row = t / (P * 64), w = t % (P * 64);
@@ -1916,25 +1575,13 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   // producers
   // =========================================================================
   if (wave >= KSG_RES_P0) {
-    if (!(d.dbg & 64)) {  // warm this XCD's L2 with the node state (KSG_DEBUG & 64: skip)
-      const uint32_t pw = wave - KSG_RES_P0, nt = NPW * 64;
-      const uint32_t n16 = (nshard + 1) / 2;
-      uint64_t acc = 0;
-      const int64_t* arr[6] = {d.cap_cpu + d.lo, d.cap_mem + d.lo, d.used_cpu + d.lo, d.used_mem + d.lo,
-                               reinterpret_cast<const int64_t*>(d.inv10_cpu) + d.lo,
-                               reinterpret_cast<const int64_t*>(d.inv10_mem) + d.lo};
-      for (uint32_t t = pw * 64 + lane; t < n16; t += nt) {
-        const uint32_t idx = 2 * t + 1 < nshard ? 2 * t + 1 : 2 * t;
-#pragma unroll
-        for (int a = 0; a < 6; ++a) acc ^= (uint64_t)arr[a][idx];
-      }
-      if (acc == 0x5bd1e995a5a5a5a5ULL) ctl->pad[0] = 1;  // keeps the loads
-    }
     const uint32_t* recs = reinterpret_cast<const uint32_t*>(sums);
     uint32_t wb_at[P], wm_at[P];
 #pragma unroll
     for (int q = 0; q < P; ++q) {
-      const uint32_t wq = lane * P + q;
+      // lane l holds words l*P + q (ServiceAntiAffinity: the LDS-slot layout its
+      // re-rank walks), else q*64 + l (coalesced loads, bank-conflict-free LDS)
+      const uint32_t wq = ANTI ? lane * P + q : q * 64 + lane;
       uint32_t g = 0;
       for (uint32_t r = 1; r < x.world; ++r)
         if (wq >= x.wlo[r] && x.nw[r] > 0) g = r;
@@ -1994,8 +1641,23 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         t0[q] = (m0 != KSG_S32_NONE && mw[q] == m0) ? t0[q] : 0ULL;
         cnt += __popcll(t0[q]);
       }
-      const uint32_t incl = dpp_scan_add(cnt);
-      const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      uint32_t incl = 0, k0 = 0;
+      // (q-major) per row q = words [64q, 64q + 64): the T0 bits below each lane's
+      // word in the row (ex_q) and below the row (rowex[q], wave-uniform)
+      uint32_t ex_q[P], rowex[P];
+      if constexpr (ANTI) {
+        incl = dpp_scan_add(cnt);
+        k0 = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      } else {
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+          const uint32_t c1 = (uint32_t)__popcll(t0[q]);
+          const uint32_t in1 = dpp_scan_add(c1);
+          ex_q[q] = in1 - c1;
+          rowex[q] = k0;
+          k0 += (uint32_t)__builtin_amdgcn_readlane((int)in1, 63);
+        }
+      }
       pstamp(25);
       // draw index = drawable pods before j (every one of them known)
       uint32_t idx = 0;
@@ -2034,7 +1696,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       int32_t s_cnt = 0, s_max = 0, s_peer = 0;
       if (drawable) {
         const uint32_t ix0 = __builtin_amdgcn_readfirstlane(mv);  // lane 0: r mod k0
-        pred = (int32_t)select_in_lanes<P>(t0, cnt, incl, k0 - 1 - ix0, lane);
+        if constexpr (ANTI) pred = (int32_t)select_in_lanes<P>(t0, cnt, incl, k0 - 1 - ix0, lane);
+        else pred = (int32_t)select_qmajor<P>(t0, ex_q, rowex, k0 - 1 - ix0, lane);
         const uint32_t pn = d.lo + (uint32_t)pred;
         if (lane == 0) pv = d.cap_cpu[pn];
         else if (lane == 1) pv = d.cap_mem[pn];
@@ -2049,8 +1712,29 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       }
       r_mod[e * 64 + lane] = mv;
       if (lane < DW) r_rec[e * DW + lane] = rec;
+      if constexpr (ANTI) {
 #pragma unroll
-      for (int q = 0; q < P; ++q) r_t0[(size_t)e * P * 64 + lane * P + q] = t0[q];
+        for (int q = 0; q < P; ++q) r_t0[(size_t)e * P * 64 + lane * P + q] = t0[q];
+      } else {
+        // T0 by word, and the sparse select's prefix counts: T0 bits below each
+        // row (r_lp[q] = {below, up to the row's end}) and below each word within
+        // its row (r_wp, u16), so the ascending position of node n in T0 is
+        // r_lp[n >> 12] + r_wp[n >> 6] + the bits below n in its word
+        uint32_t lpe = 0, lpi = 0;
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+          r_t0[(size_t)e * P * 64 + q * 64 + lane] = t0[q];
+          r_wp[(size_t)e * P * 64 + q * 64 + lane] = (uint16_t)ex_q[q];
+          if (lane == (uint32_t)q) {
+            lpe = rowex[q];
+            lpi = q + 1 < P ? rowex[q + 1 < P ? q + 1 : q] : k0;
+          }
+        }
+        if (lane < P) {
+          r_lp[(e * 64 + lane) * 2] = lpe;
+          r_lp[(e * 64 + lane) * 2 + 1] = lpi;
+        }
+      }
       if constexpr (ANTI) {  // fit at the snapshot, best-per-row nodes, row bests, domain counts
         uint64_t bw[P];
 #pragma unroll
@@ -2219,6 +1903,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
       const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
       uint32_t cntd = 0;
+      uint64_t dmsk = 0;
       if constexpr (ANTI) {
         // the pod against this lane's slot as of commits <= i-2: a drop among the
         // nodes at their domain row's best (B; T0 drops counted for the fast
@@ -2302,9 +1987,15 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       } else if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE) {
         const PodView pv = pod_view(rec);
         bool drop = false;
+        uint32_t dpos = 0;
         if (S.node != ~0u) {
           const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
-          if ((t0e[S.node >> 6] >> (S.node & 63)) & 1ULL) {
+          const uint32_t wd = S.node >> 6;
+          const uint64_t tw = t0e[wd];
+          // the node's ascending position in T0 (used only if it drops)
+          dpos = r_lp[(e * 64 + (wd >> 6)) * 2] + r_wp[(size_t)e * P * 64 + wd] +
+                 (uint32_t)__popcll(tw & ((1ULL << (S.node & 63)) - 1ULL));
+          if ((tw >> (S.node & 63)) & 1ULL) {
             // does the slot (a snapshot tie of the pod) score below M0 now?
             const int64_t now_c = (int64_t)((uint64_t)S.snp_c + (uint64_t)S.dl_c);
             const int64_t now_m = (int64_t)((uint64_t)S.snp_m + (uint64_t)S.dl_m);
@@ -2337,15 +2028,18 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
                 drop = frac10_f32((int64_t)pv.smax - snapc - delta, pv.smax) !=
                        frac10_f32((int64_t)pv.smax - snapc, pv.smax);
             }
-            if (drop)
-              atomicOr(reinterpret_cast<unsigned long long*>(L_drop + (size_t)par * P * 64 + (S.node >> 6)),
-                       1ULL << (S.node & 63));
           }
         }
-        cntd = __popcll(__ballot(drop));
+        if (drop) L_dpos[par * KSG_MAX_SLOTS + my_slot] = dpos;
+        dmsk = __ballot(drop);
+        cntd = __popcll(dmsk);
       }
       if (lane == 0) {
         ctl->chk_cnt[c][par] = cntd;
+        if constexpr (!ANTI) {
+          ctl->chk_msk[c][par][0] = (uint32_t)dmsk;
+          ctl->chk_msk[c][par][1] = (uint32_t)(dmsk >> 32);
+        }
         st_rel(&ctl->chk_seq[c], i + 1);
       }
       cstamp(c == 0 ? 18 : 21);
@@ -2711,6 +2405,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   uint32_t ss0 = 0, ss1 = 0;      // their service entry counts
   int64_t dc0 = 0, dm0 = 0, dc1 = 0, dm1 = 0;  // their window deltas (current through the last commit)
   uint32_t xnode = 0;                    // node of the last commit (pod i-1)
+  uint32_t xslot = 0;                    // and its slot
   bool have_x = false;
   uint32_t prev_sv = ~0u;                // (ServiceAntiAffinity) services of commit i-1, lane t < count
   uint64_t t_last = 0, t_acc = 0;
@@ -2755,8 +2450,25 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     const uint32_t rmod = r_mod[e * 64 + lane];
     const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
     uint64_t t0w[P];
+    uint32_t lp_ex = 0, lp_in = 0, xlp = 0, xwp = 0;
+    uint64_t t0x = 0;
+    if constexpr (ANTI) {
 #pragma unroll
-    for (int q = 0; q < P; ++q) t0w[q] = t0e[lane * P + q];
+      for (int q = 0; q < P; ++q) t0w[q] = t0e[lane * P + q];
+    } else {
+      // the sparse select's row prefixes (lane q < P: row q), and where commit
+      // i-1's node sits in T0
+      if (lane < P) {
+        lp_ex = r_lp[(e * 64 + lane) * 2];
+        lp_in = r_lp[(e * 64 + lane) * 2 + 1];
+      }
+      if (have_x) {
+        const uint32_t xw = xnode >> 6;
+        t0x = t0e[xw];
+        xwp = r_wp[(size_t)e * P * 64 + xw];
+        xlp = r_lp[(e * 64 + (xw >> 6)) * 2];
+      }
+    }
     const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
     const uint32_t k0 = __builtin_amdgcn_readfirstlane(r_hdr[e].k0);
     const int32_t pred = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].pred);
@@ -2812,8 +2524,19 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     const uint32_t xr = ctl->xres[par];
     const uint32_t fw = s >= 0 ? L_flag[s >> 5] : 0u;
     uint64_t dww[P];
+    uint64_t msk0 = 0, msk1 = 0;
+    uint32_t dp0 = 0, dp1 = 0;
+    if constexpr (ANTI) {
 #pragma unroll
-    for (int q = 0; q < P; ++q) dww[q] = dw[lane * P + q];
+      for (int q = 0; q < P; ++q) dww[q] = dw[lane * P + q];
+    } else {  // the checkers' dropping slots and the drops' positions in T0
+      msk0 = ((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[0][par][1]) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[0][par][0]);
+      msk1 = ((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[1][par][1]) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[1][par][0]);
+      dp0 = L_dpos[par * KSG_MAX_SLOTS + lane];
+      dp1 = L_dpos[par * KSG_MAX_SLOTS + 64 + lane];
+    }
     const uint32_t xres = __builtin_amdgcn_readfirstlane(xr);
     if (s >= 0 && (spread_on || aff_on) && ((xres & 2u) || ((__builtin_amdgcn_readfirstlane(fw) >> (s & 31)) & 1u))) {
       resolved = i;  // a service scalar this pod reads changed in the window
@@ -2833,7 +2556,12 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     const bool moved = mv_n != 0;
     uint32_t dropped = __builtin_amdgcn_readfirstlane(cc0) + __builtin_amdgcn_readfirstlane(cc1);
     bool x_drop = false;
-    if (have_x && (xres & 1u)) {  // x counts as a new drop iff it was a snapshot tie the checkers kept
+    if constexpr (!ANTI) {
+      // x counts as a new drop iff it is a snapshot tie whose slot the checkers
+      // kept (a new slot: they have not seen it)
+      const bool x_kept = !(((xslot < 64 ? msk0 : msk1) >> (xslot & 63)) & 1ULL);
+      x_drop = have_x && (xres & 1u) && ((t0x >> (xnode & 63)) & 1ULL) && x_kept;
+    } else if (have_x && (xres & 1u)) {  // x counts as a new drop iff it was a snapshot tie the checkers kept
       const uint32_t xwd = xnode >> 6, xo = xwd / P, xq = xwd % P;
       uint64_t t0x = 0, dwx = 0;
 #pragma unroll
@@ -2922,6 +2650,43 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       woff = select_in_lanes<P>(sw, cl, incl, k2 - 1 - ix, lane);
     } else if (dropped == 0) {
       woff = (uint32_t)pred;  // staged by the producer
+    } else if constexpr (!ANTI) {
+      // ---- sparse select: the live ties are T0 minus the drops, whose
+      // ascending T0 positions are known (the checkers' and x's). The (k-1-ix)-th
+      // live tie ascending is T0's tp-th, tp the least fixed point of
+      // tp = t + #(drops at positions <= tp); then its lane (lane prefixes), its
+      // word (the owner lane's word prefixes) and its bit (mbcnt rank)
+      KSG_COUNT2(7, 64)
+      uint32_t ix;
+      if (dropped < 64) {
+        ix = (uint32_t)__builtin_amdgcn_readlane((int)rmod, (int)dropped);
+      } else {
+        const uint64_t r = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(r_hdr[e].r >> 32)) << 32) |
+                           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r_hdr[e].r);
+        ix = umod64_32(r, k);
+      }
+      const uint32_t t = k - 1 - ix;
+      const uint32_t d0 = ((msk0 >> lane) & 1ULL) ? dp0 : ~0u;
+      const uint32_t d1 = ((msk1 >> lane) & 1ULL) ? dp1 : ~0u;
+      const uint32_t xpos = x_drop ? xlp + xwp + (uint32_t)__popcll(t0x & ((1ULL << (xnode & 63)) - 1ULL)) : ~0u;
+      uint32_t tp = t;
+      for (;;) {
+        const uint32_t cnt = (uint32_t)__popcll(__ballot(d0 <= tp)) + (uint32_t)__popcll(__ballot(d1 <= tp)) +
+                             (xpos <= tp ? 1u : 0u);
+        if (t + cnt == tp) break;
+        tp = t + cnt;
+      }
+      const uint32_t qs = (uint32_t)__builtin_ctzll(__ballot(lane < P && lp_ex <= tp && tp < lp_in));
+      const uint32_t loc = tp - (uint32_t)__builtin_amdgcn_readlane((int)lp_ex, (int)qs);
+      const uint64_t w = t0e[qs * 64 + lane];
+      const uint32_t wpq = r_wp[(size_t)e * P * 64 + qs * 64 + lane];
+      const uint32_t ls = (uint32_t)__builtin_ctzll(__ballot(wpq <= loc && loc < wpq + (uint32_t)__popcll(w)));
+      const uint64_t ws = readlane64(w, (int)ls);
+      const uint32_t lw = loc - (uint32_t)__builtin_amdgcn_readlane((int)wpq, (int)ls);
+      const uint32_t rank =
+          __builtin_amdgcn_mbcnt_hi((uint32_t)(ws >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ws, 0u));
+      const uint32_t bsel = (uint32_t)__builtin_ctzll(__ballot(((ws >> lane) & 1ULL) && rank == lw));
+      woff = (qs * 64 + ls) * 64 + bsel;
     } else {
       KSG_COUNT2(7, 64)
       uint32_t ix;
@@ -3016,6 +2781,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     }
     have_x = true;
     xnode = woff;
+    xslot = slot;
     if constexpr (ANTI) {
       const uint32_t sv_t = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + (lane < n_svcs ? lane : 0u), 63u), 64);
       prev_sv = lane < n_svcs ? sv_t : ~0u;
@@ -3074,2191 +2840,13 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
 }
 
 // ---------------------------------------------------------------------------
-// phase B, pre-selecting resolver (every configuration without
-// ServiceAntiAffinity)
-// ---------------------------------------------------------------------------
-// The sequential chain per pod is cut to the committer's own work: a re-check
-// of one node, a choice between three staged candidates, and the commit.
-//  CHECKERS (waves 4, 5; lane l of checker c watches slot 64c + l) test pod i
-//    as soon as commit i-2 is published, against the slot state in LDS — which
-//    the committer keeps current, so there is nothing to apply. A slot read
-//    while commit i-1 is being written into it may show part of that commit:
-//    every test is monotone in each part (a commit only adds requested totals,
-//    keys and service entries), so the drops found lie between the exact drops
-//    as of commit i-2 and as of commit i-1, and the committer's re-check of
-//    commit i-1's node completes them.
-//  PRE-SELECTORS (waves 1, 2: even and odd pods), once the checkers are done
-//    with pod i: the live ties L0 = T0 minus their d drops, k' = k0 - d, and the
-//    three nodes the draw can land on: A = the (r mod k')-th of L0 from the top
-//    (nothing more drops) and B0, B1 = the (r mod (k'-1))-th from the top and
-//    the one after it (commit i-1's node x drops too: the answer is B0 when x
-//    ranks above it, else B1); which of pod i-1's candidates are in L0; then
-//    the three nodes' snapshots and the pod's service counts on them.
-//  FLAGGER (wave 3) applies each commit's service flags (maxCount rises, first
-//    peers) in commit order, a pod before any later pod reads them.
-//  COMMITTER (wave 0) re-checks x for pod i (x's snapshot came with the
-//    candidate it was drawn from; its window delta and lists are the
-//    committer's own), picks A, B0 or B1, and writes the commit into the slot
-//    state.
-//  PRODUCERS (the other waves) stage pods ahead into the ring, as above.
-// threads: 16 waves (10 producers) while the registers allow, else 8 (2 producers)
-__host__ __device__ constexpr uint32_t win3_nt(uint32_t P) { return P <= 8 ? 1024u : 512u; }
-#define KSG_R3_FL 3  // flagger wave
-#define KSG_R3_C0 4  // first checker wave
-#define KSG_R3_P0 (KSG_R3_C0 + KSG_RES_NCHK)  // first producer wave
-#define KSG_CS_OK 0
-#define KSG_CS_NOFIT 1
-#define KSG_CS_ERROR 2
-#define KSG_CS_OVERSIZE 3
-
-struct alignas(16) RingHdr3 {
-  int32_t m0;
-  uint32_t k0;
-  uint64_t r;  // Int63 draw of the pod
-  uint32_t ready;
-  uint32_t drawable;
-  uint32_t pad[2];
-};
-struct alignas(16) RingSvc3 {  // per service entry t of the pod (t < n_svcs)
-  int32_t max[KSG_SLOT_SVCS];   // svc_max[sv] at the snapshot
-  int32_t peer[KSG_SLOT_SVCS];  // svc_peer[sv] at the snapshot
-};
-struct alignas(16) WinCommit3 {
-  uint32_t kind;  // 0: no commit (error / no fit), 1: commit
-  uint32_t slot, node;
-  uint32_t svc;   // service entries of the slot before the commit | the pod's service count << 16
-};
-struct alignas(16) WinCtl3 {
-  uint32_t stop;      // the committer is done: pods [0, resolved) are decided
-  uint32_t resolved;
-  uint32_t sel_seq;   // commits published for pods [0, sel_seq)
-  uint32_t psel_seq;  // pods the pre-selector is done with
-  uint32_t chk_seq[KSG_RES_NCHK];     // pods checker c is done with
-  uint32_t chk_cnt[KSG_RES_NCHK][2];  // checker c's drops for the pod of parity p
-  uint32_t fin[KSG_RES_NCHK];         // checker c wrote its slots back
-  uint32_t fin_p;                     // the flagger applied every commit's first peers
-  uint32_t hang;                      // a wait exceeded its spin limit (a bug)
-  uint32_t n_peer;                    // first service peers recorded (L_peer entries)
-  uint32_t flag_seq;                  // commits [0, flag_seq) have had their flags applied
-  uint32_t csnap_seq[2];              // pod + 1 whose candidates' snapshots are staged, by parity
-  uint32_t pad0[2];
-  // the pre-selector's verdict for the pod of parity p
-  uint32_t c_status[2], c_kp[2], c_a[2], c_b0[2], c_b1[2];
-  uint32_t c_xlive[2];  // bit j: pod i-1's candidate j is a live tie of pod i (in T0, not dropped)
-};
-
-struct WinLdsOff3 {
-  uint32_t ctl, r_hdr, r_t0, r_rec, r_mod, r_svc;
-  uint32_t cm, out, peer, flag, peerset, drop, pub, drw;
-  uint32_t s_meta, s_dl, s_cap, s_snp, s_inv, s_keys, s_svcs, s_sc, csnap, csc;
-  uint32_t total;
-};
-
-__host__ __device__ inline WinLdsOff3 win3_lds_offsets(uint32_t P, uint32_t nflag, uint32_t W) {
-  WinLdsOff3 o;
-  const uint32_t R = win_ring(P);
-  uint32_t at = 0;
-  o.ctl = at;     at += win_al16(sizeof(WinCtl3));
-  o.r_hdr = at;   at += win_al16((size_t)R * sizeof(RingHdr3));
-  o.r_t0 = at;    at += win_al16((size_t)R * P * 64 * 8);
-  o.r_rec = at;   at += win_al16((size_t)R * KSG_WIN_SUM_DWORDS * 4);
-  o.r_mod = at;   at += win_al16((size_t)R * 64 * 4);
-  o.r_svc = at;   at += win_al16((size_t)R * sizeof(RingSvc3));
-  o.cm = at;      at += win_al16((size_t)W * sizeof(WinCommit3));
-  o.out = at;     at += win_al16((size_t)W * 4);
-  o.peer = at;    at += win_al16((size_t)W * 2 * 4);
-  o.flag = at;    at += win_al16((size_t)nflag * 4);
-  o.peerset = at; at += win_al16((size_t)nflag * 4);
-  o.drop = at;    at += win_al16((size_t)2 * P * 64 * 8);
-  o.pub = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
-  o.drw = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
-  o.s_meta = at;  at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(SlotMeta));
-  o.s_dl = at;    at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(I64x2));
-  o.s_cap = at;   at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(I64x2));
-  o.s_snp = at;   at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(I64x2));
-  o.s_inv = at;   at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(F64x2));
-  o.s_keys = at;  at += win_al16((size_t)KSG_MAX_SLOTS * KSG_SLOT_KEYS * 4);
-  o.s_svcs = at;  at += win_al16((size_t)KSG_MAX_SLOTS * KSG_SLOT_SVCS * 4);
-  o.s_sc = at;    at += win_al16((size_t)KSG_MAX_SLOTS * KSG_SLOT_SVCS * 4);
-  o.csnap = at;   at += win_al16((size_t)2 * 18 * 8);   // [parity][candidate][cap c/m, used c/m, 10/cap c/m]
-  o.csc = at;     at += win_al16((size_t)2 * 36 * 4);   // [parity][candidate][service t]: svc_cnt on the node
-  o.total = at;
-  return o;
-}
-
-template <int P, bool STAMP>
-__global__ __launch_bounds__(win3_nt(P)) void ksg_win_resolve3_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
-                                                               const KsgWinSum* __restrict__ sums,
-                                                               const KsgWinXchg x, uint64_t* rng_io,
-                                                               int32_t* __restrict__ out_batch) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const uint32_t pos = run->pos, n_batch = run->n;
-  if (run->halt || pos >= n_batch) return;  // the chain is done (uniform, before any barrier)
-  const uint32_t n_pods = min(wcap, n_batch - pos);
-  int32_t* __restrict__ out = out_batch + pos;
-  const uint32_t tid = threadIdx.x;
-  const uint32_t lane = tid & 63;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t nflag = (d.n_services + 31) / 32;
-  const uint32_t nwords = d.nwords;
-  constexpr uint32_t RING = win_ring(P);
-  constexpr uint32_t NT = win3_nt(P);
-  constexpr uint32_t NPW = NT / 64 - KSG_R3_P0;  // producer waves
-  constexpr uint32_t DW = KSG_WIN_SUM_DWORDS;
-  constexpr uint32_t PW = P * 64;                 // bitmap words per pod
-  const WinLdsOff3 o = win3_lds_offsets(P, nflag, wcap);
-  WinCtl3* ctl = reinterpret_cast<WinCtl3*>(smem + o.ctl);
-  RingHdr3* r_hdr = reinterpret_cast<RingHdr3*>(smem + o.r_hdr);
-  uint64_t* r_t0 = reinterpret_cast<uint64_t*>(smem + o.r_t0);
-  uint32_t* r_rec = reinterpret_cast<uint32_t*>(smem + o.r_rec);
-  uint32_t* r_mod = reinterpret_cast<uint32_t*>(smem + o.r_mod);
-  RingSvc3* r_svc = reinterpret_cast<RingSvc3*>(smem + o.r_svc);
-  WinCommit3* L_cm = reinterpret_cast<WinCommit3*>(smem + o.cm);
-  int32_t* L_out = reinterpret_cast<int32_t*>(smem + o.out);
-  uint32_t* L_peer = reinterpret_cast<uint32_t*>(smem + o.peer);
-  uint32_t* L_flag = reinterpret_cast<uint32_t*>(smem + o.flag);
-  uint32_t* L_peerset = reinterpret_cast<uint32_t*>(smem + o.peerset);
-  uint64_t* L_drop = reinterpret_cast<uint64_t*>(smem + o.drop);  // [2][PW] by pod parity
-  uint32_t* L_pub = reinterpret_cast<uint32_t*>(smem + o.pub);
-  uint32_t* L_drw = reinterpret_cast<uint32_t*>(smem + o.drw);
-  SlotMeta* s_meta = reinterpret_cast<SlotMeta*>(smem + o.s_meta);
-  I64x2* s_dl = reinterpret_cast<I64x2*>(smem + o.s_dl);
-  I64x2* s_cap = reinterpret_cast<I64x2*>(smem + o.s_cap);
-  I64x2* s_snp = reinterpret_cast<I64x2*>(smem + o.s_snp);
-  F64x2* s_inv = reinterpret_cast<F64x2*>(smem + o.s_inv);
-  uint32_t* s_keys = reinterpret_cast<uint32_t*>(smem + o.s_keys);
-  uint32_t* s_svcs = reinterpret_cast<uint32_t*>(smem + o.s_svcs);
-  int32_t* s_sc = reinterpret_cast<int32_t*>(smem + o.s_sc);
-  int64_t* L_csnap = reinterpret_cast<int64_t*>(smem + o.csnap);
-  int32_t* L_csc = reinterpret_cast<int32_t*>(smem + o.csc);
-  const bool spread_on = d.w_spread != 0;
-  const bool aff_on = (d.preds & KSG_PRED_SERVICEAFFINITY) && d.n_aff > 0;
-  const bool res_on = (d.preds & KSG_PRED_PODFITSRESOURCES) != 0;
-  const bool ports_on = (d.preds & KSG_PRED_PODFITSPORTS) != 0;
-  const bool disk_on = (d.preds & KSG_PRED_NODISKCONFLICT) != 0;
-  const uint32_t nbits = (wcap + 31) / 32;
-
-  for (uint32_t t = tid; t < RING; t += NT) r_hdr[t].ready = 0;
-  if (tid == 0) *ctl = WinCtl3{};
-  for (uint32_t w = tid; w < nflag; w += NT) {
-    L_flag[w] = 0;
-    L_peerset[w] = 0;
-  }
-  for (uint32_t w = tid; w < nbits; w += NT) {
-    L_pub[w] = 0;
-    L_drw[w] = 0;
-  }
-  for (uint32_t w = tid; w < 2 * PW; w += NT) L_drop[w] = 0;
-  for (uint32_t t = tid; t < KSG_MAX_SLOTS; t += NT) s_meta[t] = SlotMeta{KSG_NO_NODE, 0u, 0u, 0u};
-  __syncthreads();
-  const uint64_t rng0 = *rng_io;
-
-  // =========================================================================
-  // producers
-  // =========================================================================
-  if (wave >= KSG_R3_P0) {
-    const uint32_t* recs = reinterpret_cast<const uint32_t*>(sums);
-    uint32_t wb_at[P], wm_at[P];
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-      const uint32_t wq = lane * P + q;
-      uint32_t g = 0;
-      for (uint32_t r = 1; r < x.world; ++r)
-        if (wq >= x.wlo[r] && x.nw[r] > 0) g = r;
-      const uint32_t i = wq - x.wlo[g];
-      const bool ok = wq < nwords && i < x.nw[g];
-      const uint32_t base = (uint32_t)(g * x.blk);
-      wb_at[q] = ok ? base + i * 8 : ~0u;
-      wm_at[q] = ok ? base + x.wcap * x.ostride * 8 + i * 4 : ~0u;
-    }
-    const uint32_t row_b = x.ostride * 8, row_m = x.ostride * 4;
-    uint64_t p_last = 0, p_acc = 0;  // KSG_DEBUG & 8: lanes 24..27 ring wait, loads, draw wait, the rest
-    auto pstamp = [&](uint32_t k) {
-      if constexpr (STAMP) {
-        const uint64_t t_now = __builtin_amdgcn_s_memtime();
-        p_acc += lane == k ? t_now - p_last : 0ULL;
-        p_last = t_now;
-      }
-    };
-    if constexpr (STAMP) p_last = __builtin_amdgcn_s_memtime();
-    for (uint32_t j = wave - KSG_R3_P0; j < n_pods; j += NPW) {
-      const uint32_t e = j % RING;
-      // ring entry free: pod j - RING is done with (the checkers of pod j - RING + 2
-      // imply the committer is past it; the pre-selectors and the flagger are past it)
-      for (uint32_t spin = 0;; ++spin) {
-        const uint32_t st = ld_u(&ctl->stop);
-        uint32_t done = min(ld_u(&ctl->psel_seq), ld_u(&ctl->flag_seq) + 2);
-#pragma unroll
-        for (int c = 0; c < KSG_RES_NCHK; ++c) done = min(done, ld_u(&ctl->chk_seq[c]));
-        if (st) return;
-        if (j < RING || done + RING >= j + 3) break;
-        if (spin > KSG_SPIN_LIMIT) {
-          ctl->hang = 1;
-          return;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      acq_lds();
-      pstamp(24);
-      const uint32_t rec = lane < DW ? recs[(size_t)j * DW + lane] : 0u;
-      uint64_t t0[P];
-      int32_t mw[P];
-      int32_t lm = KSG_S32_NONE;
-#pragma unroll
-      for (int q = 0; q < P; ++q) {
-        t0[q] = wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + j * row_b) : 0ULL;
-        mw[q] = wm_at[q] != ~0u ? *reinterpret_cast<const int32_t*>(x.buf + wm_at[q] + j * row_m) : KSG_S32_NONE;
-        lm = mw[q] > lm ? mw[q] : lm;
-      }
-      const int32_t m0 = wave_total_max(lm);
-      const bool drawable = __builtin_amdgcn_readlane(rec, WS_ERR) == 0 && m0 != KSG_S32_NONE;
-      const uint32_t wj = j >> 5, bj = 1u << (j & 31);
-      if (lane == 0) {  // the drawable bit first, then "known" (readers read them in that order)
-        if (drawable) atomicOr(&L_drw[wj], bj);
-        atomicOr(&L_pub[wj], bj);
-      }
-      uint32_t cnt = 0;
-#pragma unroll
-      for (int q = 0; q < P; ++q) {
-        t0[q] = (m0 != KSG_S32_NONE && mw[q] == m0) ? t0[q] : 0ULL;
-        cnt += __popcll(t0[q]);
-      }
-      const uint32_t k0 = wave_total_add(cnt);
-      const uint32_t n_svcs = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NSS) >> 16;
-      const uint32_t nk = ((uint32_t)__builtin_amdgcn_readlane(rec, WS_NPP) & 0xffff) +
-                          ((uint32_t)__builtin_amdgcn_readlane(rec, WS_NPP) >> 16);
-      const uint32_t n_sel = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NSS) & 0xffff;
-      const bool inl = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NINL) <= KSG_WIN_INLINE && n_svcs <= KSG_SLOT_SVCS;
-      const uint32_t t_sv = lane < n_svcs ? lane : 0u;
-      const uint32_t my_sv = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + t_sv, 63u), 64);
-      int32_t s_max = 0, s_peer = 0;
-      if (drawable && inl && lane < n_svcs) {  // the pod's services' scalars (in flight over the draw wait)
-        s_max = d.svc_max[my_sv];
-        s_peer = d.svc_peer[my_sv];
-      }
-      pstamp(25);
-      // draw index = drawable pods before j (every one of them known)
-      uint32_t idx = 0;
-      for (uint32_t spin = 0;; ++spin) {
-        if (ld_acq(&ctl->stop)) return;
-        if (spin > KSG_SPIN_LIMIT) {
-          ctl->hang = 1;
-          return;
-        }
-        bool all = true;
-        idx = 0;
-        for (uint32_t w = 0; w <= wj; ++w) {
-          const uint32_t mask = w < wj ? ~0u : bj - 1u;
-          const uint32_t pub = __builtin_amdgcn_readfirstlane(ld_acq(&L_pub[w]));
-          all = all && (pub & mask) == mask;
-          idx += __popc(__builtin_amdgcn_readfirstlane(L_drw[w]) & mask);
-        }
-        if (all) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      pstamp(26);
-      uint64_t sm = rng0 + (uint64_t)idx * 0x9E3779B97F4A7C15ULL;
-      const uint64_t r = ksg_splitmix_next(&sm) >> 1;  // rand.Int() (generic_scheduler.go:94)
-      uint32_t mv = 0;
-      if (drawable && lane < k0) mv = umod64_32(r, k0 - lane);
-      r_mod[e * 64 + lane] = mv;
-      if (lane < DW) r_rec[e * DW + lane] = rec;
-#pragma unroll
-      for (int q = 0; q < P; ++q) r_t0[(size_t)e * PW + lane * P + q] = t0[q];
-      if (inl && lane < n_svcs) {
-        r_svc[e].max[lane] = s_max;
-        r_svc[e].peer[lane] = s_peer;
-      }
-      if (lane == 0) {
-        r_hdr[e].m0 = m0;
-        r_hdr[e].k0 = k0;
-        r_hdr[e].r = r;
-        r_hdr[e].drawable = drawable;
-        st_rel(&r_hdr[e].ready, j + 1);
-      }
-      pstamp(27);
-    }
-    if constexpr (STAMP) {
-      if (lane >= 24 && lane < 28) atomicAdd(d.dbgbuf + lane, (int32_t)(p_acc / 64));
-    }
-    return;
-  }
-
-  // =========================================================================
-  // checkers (waves KSG_RES_C0 ..): lane l of checker c watches slot 64c + l
-  // =========================================================================
-  if (wave >= KSG_R3_C0) {
-    __builtin_amdgcn_s_setprio(2);
-    const uint32_t c = wave - KSG_R3_C0;
-    const uint32_t my_slot = c * 64 + lane;
-    const uint32_t* my_keys = s_keys + (size_t)my_slot * KSG_SLOT_KEYS;
-    const uint32_t* my_svcs = s_svcs + (size_t)my_slot * KSG_SLOT_SVCS;
-    const int32_t* my_sc = s_sc + (size_t)my_slot * KSG_SLOT_SVCS;
-    // the slot's node and snapshot, cached once the committer has created it
-    uint32_t node = KSG_NO_NODE;
-    int64_t cap_c = 0, cap_m = 0, snp_c = 0, snp_m = 0;
-    double inv_c = 0.0, inv_m = 0.0;
-    uint64_t t_last = 0, t_acc = 0;
-    auto cstamp = [&](uint32_t k) {
-      if constexpr (STAMP) {
-        const uint64_t t_now = __builtin_amdgcn_s_memtime();
-        t_acc += lane == k ? t_now - t_last : 0ULL;
-        t_last = t_now;
-      }
-    };
-    if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
-    for (uint32_t i = 0;; ++i) {
-      const uint32_t e = i % RING, par = i & 1;
-      bool stopped = false;
-      // pod i is checked once commit i-2 is published
-      for (uint32_t spin = 0;; ++spin) {
-        const uint32_t ss = ld_u(&ctl->sel_seq), rd = ld_u(&r_hdr[e].ready), st = ld_u(&ctl->stop);
-        if (i < n_pods && ss + 1 >= i && rd == i + 1) break;
-        if (st) {
-          stopped = true;
-          break;
-        }
-        if (spin > 16 * KSG_SPIN_LIMIT) {
-          ctl->hang = 1;
-          stopped = true;
-          break;
-        }
-      }
-      acq_lds();
-      if (stopped) break;
-      cstamp(c == 0 ? 16 : 19);
-      if (node == KSG_NO_NODE) {
-        const uint32_t nd = __hip_atomic_load(&s_meta[my_slot].node, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (nd != KSG_NO_NODE) {  // created (its snapshot was written before the node)
-          cap_c = s_cap[my_slot].c;
-          cap_m = s_cap[my_slot].m;
-          snp_c = s_snp[my_slot].c;
-          snp_m = s_snp[my_slot].m;
-          inv_c = s_inv[my_slot].c;
-          inv_m = s_inv[my_slot].m;
-          node = nd;
-        }
-      }
-      cstamp(c == 0 ? 17 : 20);
-      const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
-      const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
-      uint32_t cntd = 0;
-      if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE) {
-        const PodView pv = pod_view(rec);
-        bool drop = false;
-        if (node != KSG_NO_NODE) {
-          const uint64_t* t0e = r_t0 + (size_t)e * PW;
-          if ((t0e[node >> 6] >> (node & 63)) & 1ULL) {
-            // does the slot (a snapshot tie of the pod) score below M0 now?
-            const int64_t dl_c = s_dl[my_slot].c, dl_m = s_dl[my_slot].m;
-            const uint32_t m_nk = __hip_atomic_load(&s_meta[my_slot].nk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const uint32_t m_ns = __hip_atomic_load(&s_meta[my_slot].ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const uint32_t m_smask = s_meta[my_slot].smask;
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);
-            const int64_t now_c = (int64_t)((uint64_t)snp_c + (uint64_t)dl_c);
-            const int64_t now_m = (int64_t)((uint64_t)snp_m + (uint64_t)dl_m);
-            if (res_on && !pv.zero_req)  // PodFitsResources (predicates.go:127-145)
-              drop = !((cap_c == 0 || cap_c - now_c >= pv.req_c) && (cap_m == 0 || cap_m - now_m >= pv.req_m));
-            if (d.w_lr) {  // LeastRequested (priorities.go:43-76) can only fall as requested grows
-              const int32_t lr_now = lr_win(now_c + pv.req_c, cap_c, inv_c) + lr_win(now_m + pv.req_m, cap_m, inv_m);
-              const int32_t lr_snap = lr_win(snp_c + pv.req_c, cap_c, inv_c) + lr_win(snp_m + pv.req_m, cap_m, inv_m);
-              drop |= (lr_now >> 1) != (lr_snap >> 1);
-            }
-            if (!drop && pv.nk && m_nk) {  // PodFitsPorts / NoDiskConflict vs the window's keys
-              for (uint32_t a = 0; a < m_nk; ++a) {
-                const uint32_t key = my_keys[a];
-                for (uint32_t b = 0; b < pv.nk; ++b) {
-                  const bool on = b < pv.n_ports ? ports_on : disk_on;
-                  drop |= on && (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b)) == key;
-                }
-              }
-            }
-            if (!drop && spread_on && pv.s >= 0 && ((m_smask >> (pv.s & 31)) & 1u)) {
-              // ServiceSpreading (spreading.go:72-86) under an unchanged maxCount
-              int32_t delta = 0, snapc = 0;
-              for (uint32_t a = 0; a < m_ns; ++a)
-                if (my_svcs[a] == (uint32_t)pv.s) {
-                  snapc = my_sc[a];
-                  ++delta;
-                }
-              if (delta)
-                drop = frac10_f32((int64_t)pv.smax - snapc - delta, pv.smax) !=
-                       frac10_f32((int64_t)pv.smax - snapc, pv.smax);
-            }
-            if (drop)
-              atomicOr(reinterpret_cast<unsigned long long*>(L_drop + (size_t)par * PW + (node >> 6)),
-                       1ULL << (node & 63));
-          }
-        }
-        cntd = __popcll(__ballot(drop));
-      }
-      if (lane == 0) {
-        ctl->chk_cnt[c][par] = cntd;
-        st_rel(&ctl->chk_seq[c], i + 1);
-      }
-      cstamp(c == 0 ? 18 : 21);
-    }
-    // the committer is done (it wrote every commit before it set stop): write
-    // the window's deltas of this checker's slots back to HBM (the next snapshot)
-    const uint32_t nd = s_meta[my_slot].node;
-    if (nd != KSG_NO_NODE) {
-      const uint32_t n = d.lo + nd;
-      const uint32_t m_nk = s_meta[my_slot].nk, m_ns = s_meta[my_slot].ns;
-      d.used_cpu[n] = (int64_t)((uint64_t)s_snp[my_slot].c + (uint64_t)s_dl[my_slot].c);
-      d.used_mem[n] = (int64_t)((uint64_t)s_snp[my_slot].m + (uint64_t)s_dl[my_slot].m);
-      for (uint32_t a = 0; a < m_nk; ++a)
-        __hip_atomic_fetch_or(d.keymap + (size_t)my_keys[a] * d.nw + (n >> 6), 1ULL << (n & 63), __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_AGENT);
-      for (uint32_t a = 0; a < m_ns; ++a) {
-        const uint32_t sa = my_svcs[a];
-        bool first = true;
-        int32_t count = 0;
-        for (uint32_t b = 0; b < m_ns; ++b) {
-          if (my_svcs[b] == sa) {
-            if (b < a) first = false;
-            ++count;
-          }
-        }
-        __hip_atomic_fetch_add(d.svc_total + sa, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (first) {
-          const int32_t fin = my_sc[a] + count;
-          d.svc_cnt[(size_t)sa * d.n_nodes + n] = fin;
-          __hip_atomic_fetch_max(d.svc_max + sa, fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-    }
-    if constexpr (STAMP) {
-      if (lane >= 16 && lane < 22) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
-    }
-    drain_stores();
-    if (lane == 0) st_rel(&ctl->fin[c], 1u);
-    return;
-  }
-
-  // =========================================================================
-  // flagger (wave 3): the service flags later pods stop on (maxCount rises,
-  // first peer) and the first peers, of each commit in commit order
-  // =========================================================================
-  if (wave == KSG_R3_FL) {
-    __builtin_amdgcn_s_setprio(2);
-    auto apply_flags = [&](uint32_t q) {
-      const uint32_t kind = __builtin_amdgcn_readfirstlane(L_cm[q].kind);
-      const uint32_t svw = __builtin_amdgcn_readfirstlane(L_cm[q].svc);
-      const uint32_t n_svcs = svw >> 16, bns = svw & 0xffff;
-      if (kind != 1 || n_svcs == 0) return;
-      const uint32_t slot = __builtin_amdgcn_readfirstlane(L_cm[q].slot);
-      const uint32_t wn = d.lo + __builtin_amdgcn_readfirstlane(L_cm[q].node);
-      const uint32_t eq = q % RING;
-      const uint32_t prec = lane < DW ? r_rec[eq * DW + lane] : 0u;
-      const uint32_t npp = __builtin_amdgcn_readlane(prec, WS_NPP), nss = __builtin_amdgcn_readlane(prec, WS_NSS);
-      const uint32_t nk = (npp & 0xffff) + (npp >> 16), n_sel = nss & 0xffff;
-      const bool sv_lane = lane < n_svcs;
-      const uint32_t my_sv =
-          (uint32_t)__shfl((int)prec, (int)min(WS_IDS + nk + n_sel + (sv_lane ? lane : 0u), 63u), 64);
-      int32_t mx = 0, peer = 0, sc = 0;
-      if (sv_lane) {
-        mx = r_svc[eq].max[lane];
-        peer = r_svc[eq].peer[lane];
-        sc = s_sc[(size_t)slot * KSG_SLOT_SVCS + bns + lane];
-      }
-      // entries of each service on the node through this commit (the list may
-      // have grown since: only the first bns + n_svcs count)
-      const uint32_t ent = lane < bns + n_svcs ? s_svcs[(size_t)slot * KSG_SLOT_SVCS + lane] : ~0u;
-      uint32_t through = 0;
-      for (uint32_t t = 0; t < n_svcs; ++t) {
-        const uint32_t sv_t = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)t);
-        const uint32_t b_t = (uint32_t)__popcll(__ballot(ent == sv_t));
-        if (lane == t) through = b_t;
-      }
-      bool changed = sv_lane && aff_on && peer == -1 && !((L_peerset[my_sv >> 5] >> (my_sv & 31)) & 1u);
-      uint64_t pm = __ballot(sv_lane && peer == -1);
-      if (pm) {  // first commit of a service with no peer yet: its first peer, in commit order
-        uint32_t n_peer = __builtin_amdgcn_readfirstlane(ctl->n_peer);
-        while (pm) {
-          const uint32_t b = __builtin_ctzll(pm);
-          pm &= pm - 1;
-          const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)b);
-          if (!((L_peerset[fsv >> 5] >> (fsv & 31)) & 1u)) {
-            if (lane == 0) {
-              L_peerset[fsv >> 5] |= 1u << (fsv & 31);
-              L_peer[2 * n_peer] = fsv;
-              L_peer[2 * n_peer + 1] = wn;
-            }
-            ++n_peer;
-            lds_fence();
-          }
-        }
-        if (lane == 0) ctl->n_peer = n_peer;
-      }
-      if (sv_lane && spread_on && sc + (int32_t)through > mx) changed = true;  // maxCount rises
-      if (changed) atomicOr(&L_flag[my_sv >> 5], 1u << (my_sv & 31));
-    };
-    uint64_t f_last = 0, f_acc = 0;  // KSG_DEBUG & 8: lanes 22, 23 wait, apply
-    if constexpr (STAMP) f_last = __builtin_amdgcn_s_memtime();
-    for (uint32_t q = 0;; ++q) {
-      bool done = false;
-      for (uint32_t spin = 0;; ++spin) {  // commit q published, or the committer done before it
-        const uint32_t ss = ld_u(&ctl->sel_seq), st = ld_u(&ctl->stop);
-        if (ss >= q + 1) break;
-        if (st) {
-          acq_lds();
-          done = ld_u(&ctl->sel_seq) < q + 1;
-          if (done) break;
-        }
-        if (spin > 16 * KSG_SPIN_LIMIT) {
-          ctl->hang = 1;
-          done = true;
-          break;
-        }
-      }
-      acq_lds();
-      if (done) break;
-      if constexpr (STAMP) {
-        const uint64_t t_now = __builtin_amdgcn_s_memtime();
-        f_acc += lane == 22 ? t_now - f_last : 0ULL;
-        f_last = t_now;
-      }
-      apply_flags(q);
-      if (lane == 0) st_rel(&ctl->flag_seq, q + 1);
-      if constexpr (STAMP) {
-        const uint64_t t_now = __builtin_amdgcn_s_memtime();
-        f_acc += lane == 23 ? t_now - f_last : 0ULL;
-        f_last = t_now;
-      }
-    }
-    if constexpr (STAMP) {
-      if (lane >= 22 && lane < 24) atomicAdd(d.dbgbuf + lane, (int32_t)(f_acc / 64));
-    }
-    if (lane == 0) st_rel(&ctl->fin_p, 1u);
-    return;
-  }
-
-  // =========================================================================
-  // pre-selectors (wave 1: even pods, wave 2: odd pods)
-  // =========================================================================
-  if (wave == 1 || wave == 2) {
-    __builtin_amdgcn_s_setprio(2);
-    const uint32_t par = wave - 1;
-    // lanes 0..17 load candidate j = lane / 6's field f = lane % 6; lanes 18..53
-    // candidate j = (lane - 18) / 12's count of the pod's service (lane - 18) % 12
-    const uint32_t cj_s = lane < 18 ? lane / 6 : 0u, cf = lane % 6;
-    const uint64_t* const fsrc = cf == 0   ? reinterpret_cast<const uint64_t*>(d.cap_cpu)
-                                 : cf == 1 ? reinterpret_cast<const uint64_t*>(d.cap_mem)
-                                 : cf == 2 ? reinterpret_cast<const uint64_t*>(d.used_cpu)
-                                 : cf == 3 ? reinterpret_cast<const uint64_t*>(d.used_mem)
-                                 : cf == 4 ? reinterpret_cast<const uint64_t*>(d.inv10_cpu)
-                                           : reinterpret_cast<const uint64_t*>(d.inv10_mem);
-    const uint32_t cj_c = lane >= 18 && lane < 54 ? (lane - 18) / 12 : 3u, ct = (lane - 18) % 12;
-    uint64_t x_last = 0, x_acc = 0;  // KSG_DEBUG & 8: lanes 28..31 wait, select, order, prefetch
-    auto xstamp = [&](uint32_t k) {
-      if constexpr (STAMP) {
-        const uint64_t t_now = __builtin_amdgcn_s_memtime();
-        x_acc += lane == k ? t_now - x_last : 0ULL;
-        x_last = t_now;
-      }
-    };
-    if constexpr (STAMP) x_last = __builtin_amdgcn_s_memtime();
-    bool stopped = false;
-    for (uint32_t i = par; i < n_pods && !stopped; i += 2) {
-      const uint32_t e = i % RING;
-      for (uint32_t spin = 0;; ++spin) {  // the checkers are done with pod i
-        uint32_t cs = ld_u(&ctl->chk_seq[0]);
-#pragma unroll
-        for (int c = 1; c < KSG_RES_NCHK; ++c) cs = min(cs, ld_u(&ctl->chk_seq[c]));
-        const uint32_t rd = ld_u(&r_hdr[e].ready), st = ld_u(&ctl->stop);
-        if (cs >= i + 1 && rd == i + 1) break;
-        if (st) {
-          stopped = true;
-          break;
-        }
-        if (spin > 16 * KSG_SPIN_LIMIT) {
-          ctl->hang = 1;
-          stopped = true;
-          break;
-        }
-      }
-      acq_lds();
-      if (stopped) break;
-      xstamp(28);
-      const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
-      const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
-      const uint32_t err = __builtin_amdgcn_readlane(rec, WS_ERR);
-      const uint32_t npp = __builtin_amdgcn_readlane(rec, WS_NPP), nss = __builtin_amdgcn_readlane(rec, WS_NSS);
-      const uint32_t nk = (npp & 0xffff) + (npp >> 16), n_sel = nss & 0xffff, n_svcs = nss >> 16;
-      uint32_t status = KSG_CS_OK, kp = 0;
-      uint32_t ca = KSG_NO_NODE, cb0 = KSG_NO_NODE, cb1 = KSG_NO_NODE;
-      uint64_t live[P];
-#pragma unroll
-      for (int q = 0; q < P; ++q) live[q] = 0;
-      if (err || m0 == KSG_S32_NONE) {
-        status = err ? KSG_CS_ERROR : KSG_CS_NOFIT;
-      } else if (__builtin_amdgcn_readlane(rec, WS_NINL) > KSG_WIN_INLINE || nk > KSG_SLOT_KEYS ||
-                 n_svcs > KSG_SLOT_SVCS) {
-        status = KSG_CS_OVERSIZE;  // lists longer than the record / a slot
-      } else {
-        const uint32_t k0 = __builtin_amdgcn_readfirstlane(r_hdr[e].k0);
-        uint32_t cc = 0;
-#pragma unroll
-        for (int c = 0; c < KSG_RES_NCHK; ++c) cc += __builtin_amdgcn_readfirstlane(ctl->chk_cnt[c][par]);
-        kp = k0 - cc;
-        const uint64_t* t0e = r_t0 + (size_t)e * PW;
-        uint64_t* dw = L_drop + (size_t)par * PW;
-        uint32_t cl = 0;
-#pragma unroll
-        for (int q = 0; q < P; ++q) {
-          const uint64_t dq = dw[lane * P + q];
-          live[q] = t0e[lane * P + q] & ~dq;
-          if (dq) dw[lane * P + q] = 0;  // (cleared for the pod two ahead)
-          cl += __popcll(live[q]);
-        }
-        const uint32_t incl = dpp_scan_add(cl);
-        const uint32_t rmod = r_mod[e * 64 + lane];
-        const uint64_t r = r_hdr[e].r;
-        const uint64_t ru = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(r >> 32)) << 32) |
-                            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r);
-        if (kp >= 1) {  // nothing more drops: the (r mod k')-th live tie from the top
-          const uint32_t ix = cc < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)rmod, (int)cc) : umod64_32(ru, kp);
-          ca = select_in_lanes<P>(live, cl, incl, kp - 1 - ix, lane);
-        }
-        if (kp >= 2) {  // x drops too: the (r mod (k'-1))-th from the top of L0 minus x
-          const uint32_t ix =
-              cc + 1 < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)rmod, (int)(cc + 1)) : umod64_32(ru, kp - 1);
-          cb0 = select_in_lanes<P>(live, cl, incl, kp - 2 - ix, lane);
-          cb1 = select_in_lanes<P>(live, cl, incl, kp - 1 - ix, lane);
-        }
-      }
-      xstamp(29);
-      // pod i-1's candidates (the other pre-selector's), then this pod's verdict
-      // (pod i+1's pre-selector waits for it before it overwrites pod i-1's)
-      for (uint32_t spin = 0;; ++spin) {
-        const uint32_t ps = ld_u(&ctl->psel_seq), st = ld_u(&ctl->stop);
-        if (ps >= i) break;
-        if (st) {
-          stopped = true;
-          break;
-        }
-        if (spin > 16 * KSG_SPIN_LIMIT) {
-          ctl->hang = 1;
-          stopped = true;
-          break;
-        }
-      }
-      acq_lds();
-      if (stopped) break;
-      uint32_t xlive = 0;
-      if (status == KSG_CS_OK && i > 0 && __builtin_amdgcn_readfirstlane(ctl->c_status[par ^ 1]) == KSG_CS_OK) {
-        const uint32_t pa = __builtin_amdgcn_readfirstlane(ctl->c_a[par ^ 1]);
-        const uint32_t pb0 = __builtin_amdgcn_readfirstlane(ctl->c_b0[par ^ 1]);
-        const uint32_t pb1 = __builtin_amdgcn_readfirstlane(ctl->c_b1[par ^ 1]);
-        uint32_t xl = 0;
-#pragma unroll
-        for (int q = 0; q < P; ++q) {  // is pod i-1's candidate j (commit i-1's node, if drawn from it) live?
-          const uint32_t wq = lane * P + q;
-          xl |= ((pa >> 6) == wq && ((live[q] >> (pa & 63)) & 1ULL)) ? 1u : 0u;
-          xl |= ((pb0 >> 6) == wq && ((live[q] >> (pb0 & 63)) & 1ULL)) ? 2u : 0u;
-          xl |= ((pb1 >> 6) == wq && ((live[q] >> (pb1 & 63)) & 1ULL)) ? 4u : 0u;
-        }
-        xlive = wave_or_u32(xl);
-      }
-      if (lane == 0) {
-        ctl->c_status[par] = status;
-        ctl->c_kp[par] = kp;
-        ctl->c_a[par] = ca;
-        ctl->c_b0[par] = cb0;
-        ctl->c_b1[par] = cb1;
-        ctl->c_xlive[par] = xlive;
-        st_rel(&ctl->psel_seq, i + 1);
-      }
-      xstamp(30);
-      // the candidates' snapshots and the pod's service counts on them (the
-      // committer waits for these only when it writes the commit)
-      if (status == KSG_CS_OK) {
-        const uint32_t cjs = cj_s == 0 ? ca : cj_s == 1 ? cb0 : cb1;
-        const uint32_t cjc = cj_c == 0 ? ca : cj_c == 1 ? cb0 : cj_c == 2 ? cb1 : KSG_NO_NODE;
-        const uint32_t my_sv = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + ct, 63u), 64);
-        uint64_t fv = 0;
-        int32_t scv = 0;
-        if (lane < 18 && cjs != KSG_NO_NODE) fv = gld(fsrc + d.lo + cjs);
-        if (cjc != KSG_NO_NODE && ct < n_svcs) scv = gld(d.svc_cnt + (size_t)my_sv * d.n_nodes + d.lo + cjc);
-        if (lane < 18) L_csnap[par * 18 + lane] = (int64_t)fv;
-        if (lane >= 18 && lane < 54) L_csc[par * 36 + (lane - 18)] = scv;
-      }
-      if (lane == 0) st_rel(&ctl->csnap_seq[par], i + 1);
-      xstamp(31);
-    }
-    if constexpr (STAMP) {
-      if (lane >= 28 && lane < 32) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
-    }
-    return;
-  }
-  if (wave != 0) return;
-
-  // =========================================================================
-  // committer (wave 0)
-  // =========================================================================
-  __builtin_amdgcn_s_setprio(3);
-  uint32_t resolved = n_pods, reason = 0, n_slots = 0, n_draws = 0;
-  uint32_t cn0 = ~0u, cn1 = ~0u;  // nodes of slots lane and 64 + lane
-  uint32_t sk0 = 0, sk1 = 0;      // their key counts
-  uint32_t ss0 = 0, ss1 = 0;      // their service entry counts
-  uint32_t sm0 = 0, sm1 = 0;      // their service masks
-  int64_t dc0 = 0, dm0 = 0, dc1 = 0, dm1 = 0;  // their window deltas
-  // commit i-1 (pod i's re-check): node, slot, list lengths; lane L < 4 holds
-  // resource L & 1's snapshot (capacity, requested, 10/capacity) and delta
-  const uint32_t rl = lane & 1;
-  bool have_x = false;
-  uint32_t x_node = 0, x_cj = 0, x_slot = 0, x_bns = 0, x_nk = 0, x_ns = 0;
-  int64_t xs_cap = 0, xs_snp = 0, x_dl = 0;
-  double xs_inv = 0.0;
-  uint64_t t_last = 0, t_acc = 0;
-#define KSG_STAMP3(k)                                        \
-  if constexpr (STAMP) {                                     \
-    const uint64_t t_now = __builtin_amdgcn_s_memtime();     \
-    t_acc += lane == (uint32_t)(k) ? t_now - t_last : 0ULL;  \
-    t_last = t_now;                                          \
-  }
-  if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
-  for (uint32_t i = 0; i < n_pods; ++i) {
-    const uint32_t e = i % RING, par = i & 1;
-    bool hung = false;
-    for (uint32_t spin = 0;; ++spin) {  // pod i staged
-      const uint32_t rd = ld_u(&r_hdr[e].ready), hg = ld_u(&ctl->hang);
-      if (rd == i + 1) break;
-      if (spin > 16 * KSG_SPIN_LIMIT || hg) {
-        hung = true;
-        break;
-      }
-    }
-    acq_lds();
-    if (hung) {
-      resolved = i;
-      reason = KSG_STOP_HANG;
-      break;
-    }
-    KSG_STAMP3(0)
-    const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
-    const PodView pv = pod_view(rec);
-    const int32_t s = pv.s;
-    const uint32_t nss = __builtin_amdgcn_readlane(rec, WS_NSS);
-    const uint32_t n_sel = nss & 0xffff, n_svcs = nss >> 16, nk = pv.nk;
-    KSG_STAMP3(1)
-    // ---- pod i against commit i-1's node x, as of that commit
-    bool xd = false, flag_x = false;
-    if (have_x) {
-      const int64_t reqv = rl ? pv.req_m : pv.req_c;
-      const int64_t nowv = (int64_t)((uint64_t)xs_snp + (uint64_t)x_dl);  // requested total now
-      if (res_on && !pv.zero_req)  // PodFitsResources: lanes 0 and 1
-        xd = (__ballot(lane < 2 && !(xs_cap == 0 || xs_cap - nowv >= reqv)) & 3ULL) != 0;
-      if (d.w_lr) {  // LeastRequested: lanes 0, 1 now, lanes 2, 3 at the snapshot
-        const int32_t lrv = lr_win((lane < 2 ? nowv : xs_snp) + reqv, xs_cap, xs_inv);
-        const int32_t lr_now = __builtin_amdgcn_readlane(lrv, 0) + __builtin_amdgcn_readlane(lrv, 1);
-        const int32_t lr_snap = __builtin_amdgcn_readlane(lrv, 2) + __builtin_amdgcn_readlane(lrv, 3);
-        xd |= (lr_now >> 1) != (lr_snap >> 1);
-      }
-      // x's lists: lane t < 8 key t; lane 8 + u service entry u and its snapshot count
-      const uint32_t ut = lane - KSG_SLOT_KEYS;
-      const uint32_t xcl = lane < x_nk                  ? s_keys[(size_t)x_slot * KSG_SLOT_KEYS + lane]
-                           : (lane >= KSG_SLOT_KEYS && ut < x_ns) ? s_svcs[(size_t)x_slot * KSG_SLOT_SVCS + ut]
-                                                        : ~0u;
-      if (s >= 0) {
-        const uint64_t smk = __ballot(lane >= KSG_SLOT_KEYS && ut < x_ns && xcl == (uint32_t)s);
-        if (smk) {
-          const uint32_t x_cnt_s = (uint32_t)__popcll(smk);
-          const uint32_t fl = (uint32_t)__builtin_ctzll(smk);
-          const int32_t x_snapc = __builtin_amdgcn_readfirstlane(s_sc[(size_t)x_slot * KSG_SLOT_SVCS + (fl - KSG_SLOT_KEYS)]);
-          if (spread_on) {  // ServiceSpreading under an unchanged maxCount: lane 0 now, lane 1 the snapshot
-            const int32_t fr = (int32_t)frac10_f32(
-                (int64_t)pv.smax - x_snapc - (lane == 0 ? (int32_t)x_cnt_s : 0), pv.smax);
-            xd |= __builtin_amdgcn_readlane(fr, 0) != __builtin_amdgcn_readlane(fr, 1);
-          }
-          if ((smk >> (KSG_SLOT_KEYS + x_bns)) != 0) {  // commit i-1, a pod of service s: maxCount rises / first peer
-            flag_x = spread_on && x_snapc + (int32_t)x_cnt_s > pv.smax;
-            if (aff_on && (int32_t)__builtin_amdgcn_readfirstlane(r_svc[e].peer[0]) == -1 &&
-                !((__builtin_amdgcn_readfirstlane(L_peerset[s >> 5]) >> (s & 31)) & 1u))
-              flag_x = true;
-          }
-        }
-      }
-      if (nk && x_nk) {  // PodFitsPorts / NoDiskConflict
-        bool hit = false;
-        for (uint32_t b = 0; b < nk; ++b) {
-          const bool on = b < pv.n_ports ? ports_on : disk_on;
-          hit |= on && lane < x_nk && xcl == (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b));
-        }
-        xd |= __ballot(hit) != 0;
-      }
-    }
-    KSG_STAMP3(2)
-    // ---- the pre-selector's verdict (the re-check above overlapped its wait)
-    for (uint32_t spin = 0;; ++spin) {
-      const uint32_t ps = ld_u(&ctl->psel_seq), hg = ld_u(&ctl->hang);
-      if (ps >= i + 1) break;
-      if (spin > 16 * KSG_SPIN_LIMIT || hg) {
-        hung = true;
-        break;
-      }
-    }
-    acq_lds();
-    if (hung) {
-      resolved = i;
-      reason = KSG_STOP_HANG;
-      break;
-    }
-    const uint32_t status = __builtin_amdgcn_readfirstlane(ctl->c_status[par]);
-    if (status == KSG_CS_NOFIT || status == KSG_CS_ERROR) {
-      // ServiceAffinity peer error / nothing fit at the snapshot (commits only
-      // remove fits): no draw, no commit
-      if (lane == 0) {
-        L_cm[i].kind = 0;
-        L_out[i] = status == KSG_CS_ERROR ? KSG_OUT_ERROR : KSG_OUT_NOFIT;
-        st_rel(&ctl->sel_seq, i + 1);
-      }
-      have_x = false;  // pod i+1's checkers see every commit up to i-1
-      continue;
-    }
-    if (status == KSG_CS_OVERSIZE) {
-      resolved = i;  // the exact per-pod kernel takes it
-      reason = i == 0 ? KSG_STOP_OVERSIZE : KSG_STOP_SLOT;
-      break;
-    }
-    const uint32_t kp = __builtin_amdgcn_readfirstlane(ctl->c_kp[par]);
-    const uint32_t ca = __builtin_amdgcn_readfirstlane(ctl->c_a[par]);
-    const uint32_t cb0 = __builtin_amdgcn_readfirstlane(ctl->c_b0[par]);
-    const uint32_t cb1 = __builtin_amdgcn_readfirstlane(ctl->c_b1[par]);
-    const uint32_t xlv = __builtin_amdgcn_readfirstlane(ctl->c_xlive[par]);
-    KSG_STAMP3(6)
-    // the flags of commits <= i-2, and the candidates' snapshots
-    for (uint32_t spin = 0;; ++spin) {
-      const uint32_t fs = ld_u(&ctl->flag_seq), cs = ld_u(&ctl->csnap_seq[par]), hg = ld_u(&ctl->hang);
-      if (fs + 1 >= i && cs == i + 1) break;
-      if (spin > 16 * KSG_SPIN_LIMIT || hg) {
-        hung = true;
-        break;
-      }
-    }
-    acq_lds();
-    if (hung) {
-      resolved = i;
-      reason = KSG_STOP_HANG;
-      break;
-    }
-    const uint32_t fw = s >= 0 ? L_flag[s >> 5] : 0u;
-    KSG_STAMP3(5)
-    if (s >= 0 && (spread_on || aff_on) && (flag_x || ((__builtin_amdgcn_readfirstlane(fw) >> (s & 31)) & 1u))) {
-      resolved = i;  // a service scalar this pod reads changed in the window
-      reason = KSG_STOP_SERVICE;
-      break;
-    }
-    // ---- the draw: A, or with x dropping too (x a live tie), B0 / B1
-    const bool x_drop = xd && ((xlv >> x_cj) & 1u) != 0;
-    if (kp - (x_drop ? 1u : 0u) == 0) {
-      resolved = i;  // every snapshot tie got worse: needs a fresh snapshot
-      reason = KSG_STOP_EXHAUSTED;
-      break;
-    }
-    const uint32_t cj = !x_drop ? 0u : x_node > cb0 ? 1u : 2u;
-    const uint32_t woff = cj == 0 ? ca : cj == 1 ? cb0 : cb1;
-    // ---- AssumePod's slot
-    const uint64_t hit0 = __ballot(cn0 == woff);
-    const uint64_t hit1 = __ballot(cn1 == woff);
-    const bool in_c = (hit0 | hit1) != 0;
-    uint32_t slot, base_nk = 0, base_ns = 0, base_sm = 0;
-    int64_t base_dc = 0, base_dm = 0;
-    if (in_c) {
-      slot = hit0 ? (uint32_t)__builtin_ctzll(hit0) : 64u + (uint32_t)__builtin_ctzll(hit1);
-      const uint32_t sl = slot & 63;
-      base_nk = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? sk0 : sk1), (int)sl);
-      base_ns = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? ss0 : ss1), (int)sl);
-      if (base_nk + nk > KSG_SLOT_KEYS || base_ns + n_svcs > KSG_SLOT_SVCS) {
-        resolved = i;  // this pod is redone (with the same draw) in the next window
-        reason = KSG_STOP_SLOT;
-        break;
-      }
-      base_sm = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? sm0 : sm1), (int)sl);
-      base_dc = (int64_t)readlane64((uint64_t)(slot < 64 ? dc0 : dc1), (int)sl);
-      base_dm = (int64_t)readlane64((uint64_t)(slot < 64 ? dm0 : dm1), (int)sl);
-    } else {
-      if (n_slots == KSG_MAX_SLOTS) {
-        resolved = i;
-        reason = KSG_STOP_SLOT;
-        break;
-      }
-      slot = n_slots++;
-    }
-    KSG_STAMP3(3)
-    const int64_t new_dc = (int64_t)((uint64_t)base_dc + (uint64_t)pv.req_c);
-    const int64_t new_dm = (int64_t)((uint64_t)base_dm + (uint64_t)pv.req_m);
-    // the chosen candidate's snapshot, resource rl (the slot's, and the next re-check's)
-    const int64_t* cs = L_csnap + par * 18 + cj * 6;
-    const int64_t cs_cap = cs[rl], cs_snp = cs[2 + rl];
-    const double cs_inv = __longlong_as_double((long long)cs[4 + rl]);
-    const uint32_t kt = lane - WS_IDS, st = lane - (WS_IDS + nk + n_sel);
-    const uint32_t new_sm = base_sm | wave_or_u32(st < n_svcs ? (1u << (rec & 31)) : 0u);
-    if (!in_c && lane < 2) {  // the new slot's snapshot, before its node
-      (&s_cap[slot].c)[rl] = cs_cap;
-      (&s_snp[slot].c)[rl] = cs_snp;
-      (&s_inv[slot].c)[rl] = cs_inv;
-    }
-    // the pod's keys and service ids (record lane L holds dword L, so each list
-    // entry is stored by the lane that holds it) and the services' counts on the node
-    if (kt < nk) s_keys[(size_t)slot * KSG_SLOT_KEYS + base_nk + kt] = rec;
-    if (st < n_svcs) {
-      s_sc[(size_t)slot * KSG_SLOT_SVCS + base_ns + st] = L_csc[par * 36 + cj * 12 + st];
-      s_svcs[(size_t)slot * KSG_SLOT_SVCS + base_ns + st] = rec;
-    }
-    // (the checkers read a slot's lengths before its lists and its node before its
-    // snapshot; one wave's LDS stores land in program order, so only the compiler
-    // must keep them in order)
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (lane == 0) {
-      s_dl[slot].c = new_dc;
-      s_dl[slot].m = new_dm;
-      s_meta[slot].nk = base_nk + nk;
-      s_meta[slot].ns = base_ns + n_svcs;
-      s_meta[slot].smask = new_sm;
-      if (!in_c) s_meta[slot].node = woff;
-      L_cm[i] = WinCommit3{1u, slot, woff, base_ns | (n_svcs << 16)};
-      L_out[i] = (int32_t)(d.lo + woff);
-      st_rel(&ctl->sel_seq, i + 1);  // the checkers move on
-    }
-    if (lane == (slot & 63)) {  // this wave's view of the slot
-      if (slot >= 64) {
-        if (!in_c) cn1 = woff;
-        dc1 = new_dc;
-        dm1 = new_dm;
-        sk1 = base_nk + nk;
-        ss1 = base_ns + n_svcs;
-        sm1 = new_sm;
-      } else {
-        if (!in_c) cn0 = woff;
-        dc0 = new_dc;
-        dm0 = new_dm;
-        sk0 = base_nk + nk;
-        ss0 = base_ns + n_svcs;
-        sm0 = new_sm;
-      }
-    }
-    have_x = true;
-    x_node = woff;
-    x_cj = cj;
-    x_slot = slot;
-    x_bns = base_ns;
-    x_nk = base_nk + nk;
-    x_ns = base_ns + n_svcs;
-    x_dl = rl ? new_dm : new_dc;
-    xs_cap = cs_cap;
-    xs_snp = cs_snp;
-    xs_inv = cs_inv;
-    ++n_draws;
-    KSG_STAMP3(4)
-  }
-  if (lane == 0) {
-    ctl->resolved = resolved;
-    st_rel(&ctl->stop, 1u);
-  }
-  // the checkers write their slots back, the pre-selector records the last first peers
-  bool drained = false;
-  for (uint32_t spin = 0; spin <= 16 * KSG_SPIN_LIMIT; ++spin) {
-    bool done = ld_acq(&ctl->fin_p) != 0;
-#pragma unroll
-    for (int c = 0; c < KSG_RES_NCHK; ++c) done = done && ld_acq(&ctl->fin[c]) != 0;
-    if (done) {
-      drained = true;
-      break;
-    }
-  }
-  if (!drained || ld_acq(&ctl->hang)) reason = KSG_STOP_HANG;
-  if constexpr (STAMP) {
-    if (lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
-  }
-#undef KSG_STAMP3
-  const uint32_t n_peer = __builtin_amdgcn_readfirstlane(ctl->n_peer);
-  for (uint32_t t = lane; t < n_peer; t += 64) {
-    const uint32_t sv = L_peer[2 * t];
-    int32_t expect = -1;
-    __hip_atomic_compare_exchange_strong(d.svc_peer + sv, &expect, (int32_t)L_peer[2 * t + 1], __ATOMIC_RELAXED,
-                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  for (uint32_t t = lane; t < resolved; t += 64) out[t] = L_out[t];
-  if (lane == 0) {
-    *rng_io = rng0 + (uint64_t)n_draws * 0x9E3779B97F4A7C15ULL;
-    if (reason == KSG_STOP_HANG) {
-      run->halt = KSG_HALT_HANG;
-    } else if (reason == KSG_STOP_OVERSIZE) {
-      run->halt = KSG_HALT_OVERSIZE;  // pod pos: the host runs the exact per-pod path, then resumes
-    } else if (resolved == 0 || resolved > n_pods) {
-      run->halt = KSG_HALT_BADCOUNT;
-    } else {
-      run->pos = pos + resolved;
-      run->windows += 1;
-      if (reason >= 1 && reason <= 3) run->stops[reason] += 1;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// phase B, lag-3 resolver (every configuration without ServiceAntiAffinity)
-// ---------------------------------------------------------------------------
-// The register-slot resolver above spends its chain per pod on a select (a
-// scan over T0 minus the drops) and a hand-off to and from the x-checker. Here
-// the checkers run two pods ahead instead of one, which leaves them and a
-// pre-selector time to stage everything the draw can land on:
-//  CHECKERS (waves 3, 4; lane l of checker c owns slot 64c + l, register
-//    state as above) apply commit i-3 and test pod i against their slots, as
-//    soon as commit i-3 is published.
-//  PRE-SELECTOR (wave 2), once the checkers are done with pod i: the live ties
-//    L0 = T0 minus their d drops, k' = k0 - d, and for e = 0, 1, 2 further
-//    drops (the nodes of commits i-2 and i-1, which the checkers did not see)
-//    the e+1 nodes of L0 from the (r mod (k'-e))-th from the top down: A; B0,
-//    B1; C0, C1, C2 (the e-th answer is the first of them whose rank in L0
-//    minus the dropped nodes is right). Also: which of pods i-1's and i-2's
-//    candidates lie in L0, and the six candidates' snapshots plus pod i+1's
-//    service count on each (prefetched for the committer's next re-check).
-//  X2-CHECKER (wave 1) follows the commits in order: it applies each commit's
-//    service flags (maxCount rises, first peers), and re-checks pod i against
-//    the node of commit i-2 as of that commit.
-//  COMMITTER (wave 0) re-checks pod i against commit i-1's node itself (the
-//    node's snapshot came with its candidate; its delta and lists are the
-//    committer's own), counts the two late drops, picks among the six staged
-//    candidates with a few scalar compares, and commits.
-//  PRODUCERS stage pods into the ring as above.
-__host__ __device__ constexpr uint32_t win4_nt(uint32_t P) { return P <= 8 ? 1024u : 512u; }
-#define KSG_R4_X2 1  // x2-checker wave
-#define KSG_R4_PS 2  // pre-selector wave
-#define KSG_R4_C0 3  // first checker wave
-#define KSG_R4_P0 (KSG_R4_C0 + KSG_RES_NCHK)
-#define KSG_R4_NCAND 6
-#define KSG_R4_NB 4  // per-pod buffers (drops, candidates) by pod index mod 4
-
-struct alignas(16) WinCommit4 {
-  uint32_t kind;   // 0: no commit (error / no fit), 1: commit
-  uint32_t slot;
-  uint32_t node;   // shard offset of the node
-  uint32_t flags;  // bit 0: a new slot, bits 2..4: the candidate it was drawn as, bits 8..15: n_svcs
-};
-struct alignas(16) WinCand4 {  // the pre-selector's verdict for one pod
-  uint32_t status;  // KSG_CS_*
-  uint32_t kp;      // k' = k0 - the checkers' drops
-  uint32_t xlive;   // bits 0..5: pod i-1's candidate j is in L0; bits 6..11: pod i-2's
-  uint32_t pad;
-  uint32_t c[8];    // A, B0, B1, C0, C1, C2 (KSG_NO_NODE where k' is too small)
-};
-struct alignas(16) WinCtl4 {
-  uint32_t stop;      // the committer is done: pods [0, resolved) are decided
-  uint32_t resolved;
-  uint32_t sel_seq;   // commits published for pods [0, sel_seq)
-  uint32_t psel_seq;  // pods the pre-selector is done with
-  uint32_t chk_seq[KSG_RES_NCHK];
-  uint32_t chk_cnt[KSG_RES_NCHK][KSG_R4_NB];
-  uint32_t fin[KSG_RES_NCHK];
-  uint32_t fin_x;     // the x2-checker applied every commit's flags and first peers
-  uint32_t hang;
-  uint32_t n_peer;
-  uint32_t x2_seq;    // pods the x2-checker is done with
-  uint32_t x2_res[KSG_R4_NB];      // bit 0: pod i's node of commit i-2 drops
-  uint32_t csnap_seq[KSG_R4_NB];   // pod + 1 whose candidates' snapshots are staged
-  uint32_t pad[2];
-};
-
-struct WinLdsOff4 {
-  uint32_t ctl, r_hdr, r_t0, r_rec, r_mod, r_svc;
-  uint32_t cm, out, peer, flag, peerset, drop, pub, drw, clist, cand, csnap, csc;
-  uint32_t total;
-};
-
-__host__ __device__ inline WinLdsOff4 win4_lds_offsets(uint32_t P, uint32_t nflag, uint32_t W) {
-  WinLdsOff4 o;
-  const uint32_t R = win_ring(P);
-  uint32_t at = 0;
-  o.ctl = at;     at += win_al16(sizeof(WinCtl4));
-  o.r_hdr = at;   at += win_al16((size_t)R * sizeof(RingHdr3));
-  o.r_t0 = at;    at += win_al16((size_t)R * P * 64 * 8);
-  o.r_rec = at;   at += win_al16((size_t)R * KSG_WIN_SUM_DWORDS * 4);
-  o.r_mod = at;   at += win_al16((size_t)R * 64 * 4);
-  o.r_svc = at;   at += win_al16((size_t)R * sizeof(RingSvc3));
-  o.cm = at;      at += win_al16((size_t)W * sizeof(WinCommit4));
-  o.out = at;     at += win_al16((size_t)W * 4);
-  o.peer = at;    at += win_al16((size_t)W * 2 * 4);
-  o.flag = at;    at += win_al16((size_t)nflag * 4);
-  o.peerset = at; at += win_al16((size_t)nflag * 4);
-  o.drop = at;    at += win_al16((size_t)KSG_R4_NB * P * 64 * 8);
-  o.pub = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
-  o.drw = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
-  o.clist = at;   at += win_al16((size_t)KSG_MAX_SLOTS * KSG_CL_W * 4);
-  o.cand = at;    at += win_al16((size_t)KSG_R4_NB * sizeof(WinCand4));
-  o.csnap = at;   at += win_al16((size_t)KSG_R4_NB * KSG_R4_NCAND * 6 * 8);  // cap c/m, used c/m, 10/cap c/m
-  o.csc = at;     at += win_al16((size_t)KSG_R4_NB * 8 * 4);  // the next pod's service count on each candidate
-  o.total = at;
-  return o;
-}
-
-// lane-parallel re-check of pod `rec` against one node x as of its latest
-// commit: lanes 0..3 hold resource L & 1's capacity, snapshot requested total,
-// 10/capacity and window delta; lane t < 8 x's key t, lane 8 + u its service
-// entry u (xcl); x_snapc: the pod's service's count on x at the snapshot.
-// Returns bit 0: x scores below M0 now, bit 1: the pod's service scalars moved
-// (commit `prev_lo`.. of x was a pod of its service: maxCount rises / first peer).
-struct XState {
-  int64_t cap, snp, dl;  // resource lane & 1
-  double inv;
-  uint32_t nk, ns;       // x's list lengths
-};
-__device__ __forceinline__ uint32_t recheck_x(const KsgDev& d, const PodView& pv, uint32_t rec, const XState& xs,
-                                              uint32_t xcl, uint32_t new_from, int32_t x_snapc, bool res_on,
-                                              bool ports_on, bool disk_on, bool spread_on, bool aff_on,
-                                              int32_t peer0, bool peerset_s, uint32_t lane) {
-  const uint32_t rl = lane & 1;
-  const int64_t reqv = rl ? pv.req_m : pv.req_c;
-  const int64_t nowv = (int64_t)((uint64_t)xs.snp + (uint64_t)xs.dl);
-  bool xd = false, flag = false;
-  if (res_on && !pv.zero_req)  // PodFitsResources: lanes 0 and 1
-    xd = (__ballot(lane < 2 && !(xs.cap == 0 || xs.cap - nowv >= reqv)) & 3ULL) != 0;
-  if (d.w_lr) {  // LeastRequested: lanes 0, 1 now, lanes 2, 3 at the snapshot
-    const int32_t lrv = lr_win((lane < 2 ? nowv : xs.snp) + reqv, xs.cap, xs.inv);
-    const int32_t lr_now = __builtin_amdgcn_readlane(lrv, 0) + __builtin_amdgcn_readlane(lrv, 1);
-    const int32_t lr_snap = __builtin_amdgcn_readlane(lrv, 2) + __builtin_amdgcn_readlane(lrv, 3);
-    xd |= (lr_now >> 1) != (lr_snap >> 1);
-  }
-  const uint32_t ut = lane - KSG_CL_SV;
-  const int32_t s = pv.s;
-  if (s >= 0) {
-    const uint64_t smk = __ballot(ut < xs.ns && xcl == (uint32_t)s);
-    if (smk) {
-      const int32_t cnt = (int32_t)__popcll(smk);
-      if (spread_on) {  // ServiceSpreading under an unchanged maxCount: lane 0 now, lane 1 the snapshot
-        const int32_t fr = (int32_t)frac10_f32((int64_t)pv.smax - x_snapc - (lane == 0 ? cnt : 0), pv.smax);
-        xd |= __builtin_amdgcn_readlane(fr, 0) != __builtin_amdgcn_readlane(fr, 1);
-      }
-      if ((smk >> (KSG_CL_SV + new_from)) != 0) {  // the latest commit was a pod of service s
-        flag = spread_on && x_snapc + cnt > pv.smax;
-        if (aff_on && peer0 == -1 && !peerset_s) flag = true;
-      }
-    }
-  }
-  if (pv.nk && xs.nk) {  // PodFitsPorts / NoDiskConflict
-    bool hit = false;
-    for (uint32_t b = 0; b < pv.nk; ++b) {
-      const bool on = b < pv.n_ports ? ports_on : disk_on;
-      hit |= on && lane < xs.nk && xcl == (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b));
-    }
-    xd |= __ballot(hit) != 0;
-  }
-  return (xd ? 1u : 0u) | (flag ? 2u : 0u);
-}
-
-template <int P, bool STAMP>
-__global__ __launch_bounds__(win4_nt(P)) void ksg_win_resolve4_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
-                                                                    const KsgWinSum* __restrict__ sums,
-                                                                    const KsgWinXchg x, uint64_t* rng_io,
-                                                                    int32_t* __restrict__ out_batch) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const uint32_t pos = run->pos, n_batch = run->n;
-  if (run->halt || pos >= n_batch) return;  // the chain is done (uniform, before any barrier)
-  const uint32_t n_pods = min(wcap, n_batch - pos);
-  int32_t* __restrict__ out = out_batch + pos;
-  const uint32_t tid = threadIdx.x;
-  const uint32_t lane = tid & 63;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t nflag = (d.n_services + 31) / 32;
-  const uint32_t nwords = d.nwords;
-  constexpr uint32_t RING = win_ring(P);
-  constexpr uint32_t NT = win4_nt(P);
-  constexpr uint32_t NPW = NT / 64 - KSG_R4_P0;  // producer waves
-  constexpr uint32_t DW = KSG_WIN_SUM_DWORDS;
-  constexpr uint32_t PW = P * 64;
-  const WinLdsOff4 o = win4_lds_offsets(P, nflag, wcap);
-  WinCtl4* ctl = reinterpret_cast<WinCtl4*>(smem + o.ctl);
-  RingHdr3* r_hdr = reinterpret_cast<RingHdr3*>(smem + o.r_hdr);
-  uint64_t* r_t0 = reinterpret_cast<uint64_t*>(smem + o.r_t0);
-  uint32_t* r_rec = reinterpret_cast<uint32_t*>(smem + o.r_rec);
-  uint32_t* r_mod = reinterpret_cast<uint32_t*>(smem + o.r_mod);
-  RingSvc3* r_svc = reinterpret_cast<RingSvc3*>(smem + o.r_svc);
-  WinCommit4* L_cm = reinterpret_cast<WinCommit4*>(smem + o.cm);
-  int32_t* L_out = reinterpret_cast<int32_t*>(smem + o.out);
-  uint32_t* L_peer = reinterpret_cast<uint32_t*>(smem + o.peer);
-  uint32_t* L_flag = reinterpret_cast<uint32_t*>(smem + o.flag);
-  uint32_t* L_peerset = reinterpret_cast<uint32_t*>(smem + o.peerset);
-  uint64_t* L_drop = reinterpret_cast<uint64_t*>(smem + o.drop);  // [NB][PW] by pod index mod NB
-  uint32_t* L_pub = reinterpret_cast<uint32_t*>(smem + o.pub);
-  uint32_t* L_drw = reinterpret_cast<uint32_t*>(smem + o.drw);
-  uint32_t* L_cl = reinterpret_cast<uint32_t*>(smem + o.clist);   // [slot][KSG_CL_W]
-  WinCand4* L_cand = reinterpret_cast<WinCand4*>(smem + o.cand);  // [NB]
-  int64_t* L_csnap = reinterpret_cast<int64_t*>(smem + o.csnap);  // [NB][6 candidates][6 fields]
-  int32_t* L_csc = reinterpret_cast<int32_t*>(smem + o.csc);      // [NB][8]
-  const bool spread_on = d.w_spread != 0;
-  const bool aff_on = (d.preds & KSG_PRED_SERVICEAFFINITY) && d.n_aff > 0;
-  const bool res_on = (d.preds & KSG_PRED_PODFITSRESOURCES) != 0;
-  const bool ports_on = (d.preds & KSG_PRED_PODFITSPORTS) != 0;
-  const bool disk_on = (d.preds & KSG_PRED_NODISKCONFLICT) != 0;
-  const uint32_t nbits = (wcap + 31) / 32;
-
-  for (uint32_t t = tid; t < RING; t += NT) r_hdr[t].ready = 0;
-  if (tid == 0) *ctl = WinCtl4{};
-  for (uint32_t w = tid; w < nflag; w += NT) {
-    L_flag[w] = 0;
-    L_peerset[w] = 0;
-  }
-  for (uint32_t w = tid; w < nbits; w += NT) {
-    L_pub[w] = 0;
-    L_drw[w] = 0;
-  }
-  for (uint32_t w = tid; w < KSG_R4_NB * PW; w += NT) L_drop[w] = 0;
-  __syncthreads();
-  const uint64_t rng0 = *rng_io;
-
-  // =========================================================================
-  // producers
-  // =========================================================================
-  if (wave >= KSG_R4_P0) {
-    const uint32_t* recs = reinterpret_cast<const uint32_t*>(sums);
-    uint32_t wb_at[P], wm_at[P];
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-      const uint32_t wq = lane * P + q;
-      uint32_t g = 0;
-      for (uint32_t r = 1; r < x.world; ++r)
-        if (wq >= x.wlo[r] && x.nw[r] > 0) g = r;
-      const uint32_t i = wq - x.wlo[g];
-      const bool ok = wq < nwords && i < x.nw[g];
-      const uint32_t base = (uint32_t)(g * x.blk);
-      wb_at[q] = ok ? base + i * 8 : ~0u;
-      wm_at[q] = ok ? base + x.wcap * x.ostride * 8 + i * 4 : ~0u;
-    }
-    const uint32_t row_b = x.ostride * 8, row_m = x.ostride * 4;
-    uint64_t p_last = 0, p_acc = 0;  // KSG_DEBUG & 8: lanes 24..27 ring wait, loads, draw wait, the rest
-    auto pstamp = [&](uint32_t k) {
-      if constexpr (STAMP) {
-        const uint64_t t_now = __builtin_amdgcn_s_memtime();
-        p_acc += lane == k ? t_now - p_last : 0ULL;
-        p_last = t_now;
-      }
-    };
-    if constexpr (STAMP) p_last = __builtin_amdgcn_s_memtime();
-    for (uint32_t j = wave - KSG_R4_P0; j < n_pods; j += NPW) {
-      const uint32_t e = j % RING;
-      // ring entry free: every role is past pod j - RING (the checkers read a pod's
-      // entry again three pods later, the x2-checker two pods later, the
-      // pre-selector reads the next pod's entry)
-      for (uint32_t spin = 0;; ++spin) {
-        const uint32_t st = ld_u(&ctl->stop);
-        uint32_t done = min(min(ld_u(&ctl->psel_seq), ld_u(&ctl->x2_seq)), ld_u(&ctl->sel_seq));
-#pragma unroll
-        for (int c = 0; c < KSG_RES_NCHK; ++c) done = min(done, ld_u(&ctl->chk_seq[c]));
-        if (st) return;
-        if (j < RING || done + RING >= j + 5) break;
-        if (spin > KSG_SPIN_LIMIT) {
-          ctl->hang = 1;
-          return;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      acq_lds();
-      pstamp(24);
-      const uint32_t rec = lane < DW ? recs[(size_t)j * DW + lane] : 0u;
-      uint64_t t0[P];
-      int32_t mw[P];
-      int32_t lm = KSG_S32_NONE;
-#pragma unroll
-      for (int q = 0; q < P; ++q) {
-        t0[q] = wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + j * row_b) : 0ULL;
-        mw[q] = wm_at[q] != ~0u ? *reinterpret_cast<const int32_t*>(x.buf + wm_at[q] + j * row_m) : KSG_S32_NONE;
-        lm = mw[q] > lm ? mw[q] : lm;
-      }
-      const int32_t m0 = wave_total_max(lm);
-      const bool drawable = __builtin_amdgcn_readlane(rec, WS_ERR) == 0 && m0 != KSG_S32_NONE;
-      const uint32_t wj = j >> 5, bj = 1u << (j & 31);
-      if (lane == 0) {  // the drawable bit first, then "known" (readers read them in that order)
-        if (drawable) atomicOr(&L_drw[wj], bj);
-        atomicOr(&L_pub[wj], bj);
-      }
-      uint32_t cnt = 0;
-#pragma unroll
-      for (int q = 0; q < P; ++q) {
-        t0[q] = (m0 != KSG_S32_NONE && mw[q] == m0) ? t0[q] : 0ULL;
-        cnt += __popcll(t0[q]);
-      }
-      const uint32_t k0 = wave_total_add(cnt);
-      const uint32_t n_svcs = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NSS) >> 16;
-      const uint32_t nk = ((uint32_t)__builtin_amdgcn_readlane(rec, WS_NPP) & 0xffff) +
-                          ((uint32_t)__builtin_amdgcn_readlane(rec, WS_NPP) >> 16);
-      const uint32_t n_sel = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NSS) & 0xffff;
-      const bool inl = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NINL) <= KSG_WIN_INLINE && n_svcs <= KSG_SLOT_SVCS;
-      const uint32_t t_sv = lane < n_svcs ? lane : 0u;
-      const uint32_t my_sv = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + t_sv, 63u), 64);
-      int32_t s_max = 0, s_peer = 0;
-      if (drawable && inl && lane < n_svcs) {  // the pod's services' scalars (in flight over the draw wait)
-        s_max = d.svc_max[my_sv];
-        s_peer = d.svc_peer[my_sv];
-      }
-      pstamp(25);
-      // draw index = drawable pods before j (every one of them known)
-      uint32_t idx = 0;
-      for (uint32_t spin = 0;; ++spin) {
-        if (ld_acq(&ctl->stop)) return;
-        if (spin > KSG_SPIN_LIMIT) {
-          ctl->hang = 1;
-          return;
-        }
-        bool all = true;
-        idx = 0;
-        for (uint32_t w = 0; w <= wj; ++w) {
-          const uint32_t mask = w < wj ? ~0u : bj - 1u;
-          const uint32_t pub = __builtin_amdgcn_readfirstlane(ld_acq(&L_pub[w]));
-          all = all && (pub & mask) == mask;
-          idx += __popc(__builtin_amdgcn_readfirstlane(L_drw[w]) & mask);
-        }
-        if (all) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      pstamp(26);
-      uint64_t sm = rng0 + (uint64_t)idx * 0x9E3779B97F4A7C15ULL;
-      const uint64_t r = ksg_splitmix_next(&sm) >> 1;  // rand.Int() (generic_scheduler.go:94)
-      uint32_t mv = 0;
-      if (drawable && lane < k0) mv = umod64_32(r, k0 - lane);
-      r_mod[e * 64 + lane] = mv;
-      if (lane < DW) r_rec[e * DW + lane] = rec;
-#pragma unroll
-      for (int q = 0; q < P; ++q) r_t0[(size_t)e * PW + lane * P + q] = t0[q];
-      if (inl && lane < n_svcs) {
-        r_svc[e].max[lane] = s_max;
-        r_svc[e].peer[lane] = s_peer;
-      }
-      if (lane == 0) {
-        r_hdr[e].m0 = m0;
-        r_hdr[e].k0 = k0;
-        r_hdr[e].r = r;
-        r_hdr[e].drawable = drawable;
-        st_rel(&r_hdr[e].ready, j + 1);
-      }
-      pstamp(27);
-    }
-    if constexpr (STAMP) {
-      if (lane >= 24 && lane < 28) atomicAdd(d.dbgbuf + lane, (int32_t)(p_acc / 64));
-    }
-    return;
-  }
-
-  // =========================================================================
-  // checkers: lane l of checker c owns slot 64c + l
-  // =========================================================================
-  if (wave >= KSG_R4_C0) {
-    __builtin_amdgcn_s_setprio(2);
-    const uint32_t c = wave - KSG_R4_C0;
-    const uint32_t my_slot = c * 64 + lane;
-    const uint32_t* my_cl = L_cl + (size_t)my_slot * KSG_CL_W;
-    RegSlot S;
-    S.node = ~0u;
-    S.cap_c = S.cap_m = S.snp_c = S.snp_m = S.dl_c = S.dl_m = 0;
-    S.inv_c = S.inv_m = 0.0;
-    S.nk = S.ns = S.smask = 0;
-    // AssumePod of pod p (plugin/pkg/scheduler/scheduler.go:115-118) into the
-    // owner lane's slot: requested totals, list lengths, the services' snapshot
-    // counts into the table (the x2-checker applies the service flags)
-    auto apply = [&](uint32_t p) {
-      const uint32_t kind = __builtin_amdgcn_readfirstlane(L_cm[p].kind);
-      const uint32_t slot = __builtin_amdgcn_readfirstlane(L_cm[p].slot);
-      if (kind != 1 || (slot >> 6) != c) return;
-      const uint32_t woff = __builtin_amdgcn_readfirstlane(L_cm[p].node);
-      const uint32_t fl = __builtin_amdgcn_readfirstlane(L_cm[p].flags);
-      const bool fresh = (fl & 1u) != 0;
-      const uint32_t cj = (fl >> 2) & 7u;
-      const uint32_t ol = slot & 63, ep = p % RING, wn = d.lo + woff;
-      const uint32_t prec = lane < DW ? r_rec[ep * DW + lane] : 0u;
-      const PodView ppv = pod_view(prec);
-      const uint32_t nss = __builtin_amdgcn_readlane(prec, WS_NSS);
-      const uint32_t n_sel = nss & 0xffff, n_svcs = nss >> 16, nk = ppv.nk;
-      const uint32_t base_nk = fresh ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)S.nk, (int)ol);
-      const uint32_t base_ns = fresh ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)S.ns, (int)ol);
-      if (fresh) {  // its candidate's snapshot is staged (the pre-selector stages it after the verdict)
-        for (uint32_t spin = 0; ld_u(&ctl->csnap_seq[p % KSG_R4_NB]) != p + 1; ++spin)
-          if (spin > 16 * KSG_SPIN_LIMIT || ld_u(&ctl->hang)) {
-            ctl->hang = 1;
-            break;
-          }
-        acq_lds();
-      }
-      if (fresh && lane == ol) {  // the new slot's snapshot: staged with its candidate
-        const int64_t* cs = L_csnap + ((size_t)(p % KSG_R4_NB) * KSG_R4_NCAND + cj) * 6;
-        S.cap_c = cs[0];
-        S.cap_m = cs[1];
-        S.snp_c = cs[2];
-        S.snp_m = cs[3];
-        S.inv_c = __longlong_as_double((long long)cs[4]);
-        S.inv_m = __longlong_as_double((long long)cs[5]);
-        S.node = woff;
-        S.dl_c = S.dl_m = 0;
-        S.smask = 0;
-      }
-      uint32_t new_mask = 0;
-      if (n_svcs) {  // the pod's services' snapshot counts on the node, into the table
-        const bool sv_lane = lane < n_svcs;
-        const uint32_t my_sv =
-            (uint32_t)__shfl((int)prec, (int)min(WS_IDS + nk + n_sel + (sv_lane ? lane : 0u), 63u), 64);
-        if (sv_lane)
-          L_cl[(size_t)slot * KSG_CL_W + KSG_CL_SC + base_ns + lane] =
-              (uint32_t)gld(d.svc_cnt + (size_t)my_sv * d.n_nodes + wn);
-        new_mask = wave_or_u32(sv_lane ? (1u << (my_sv & 31)) : 0u);
-      }
-      if (lane == ol) {
-        S.dl_c = (int64_t)((uint64_t)S.dl_c + (uint64_t)ppv.req_c);
-        S.dl_m = (int64_t)((uint64_t)S.dl_m + (uint64_t)ppv.req_m);
-        S.nk = base_nk + nk;
-        S.ns = base_ns + n_svcs;
-        S.smask |= new_mask;
-      }
-    };
-
-    uint64_t t_last = 0, t_acc = 0;
-    auto cstamp = [&](uint32_t k) {
-      if constexpr (STAMP) {
-        const uint64_t t_now = __builtin_amdgcn_s_memtime();
-        t_acc += lane == k ? t_now - t_last : 0ULL;
-        t_last = t_now;
-      }
-    };
-    if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
-    for (uint32_t i = 0;; ++i) {
-      const uint32_t e = i % RING, nb = i % KSG_R4_NB;
-      bool stopped = false;
-      // pod i is checked against the slots as of commits <= i-3: it starts once
-      // commit i-3 is published
-      for (uint32_t spin = 0;; ++spin) {
-        const uint32_t ss = ld_u(&ctl->sel_seq), rd = ld_u(&r_hdr[e].ready), st = ld_u(&ctl->stop);
-        if (i < n_pods && ss + 2 >= i && rd == i + 1) break;
-        if (st) {
-          stopped = true;
-          break;
-        }
-        if (spin > 16 * KSG_SPIN_LIMIT) {
-          ctl->hang = 1;
-          stopped = true;
-          break;
-        }
-      }
-      acq_lds();
-      cstamp(c == 0 ? 16 : 19);
-      if (stopped) {
-        // pods [0, resolved) are decided: apply the commits this checker has not
-        const uint32_t R = __builtin_amdgcn_readfirstlane(ctl->resolved);
-        for (uint32_t q = i >= 3 ? i - 3 : 0; q < R; ++q) apply(q);
-        break;
-      }
-      if (i >= 3) apply(i - 3);
-      cstamp(c == 0 ? 17 : 20);
-      const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
-      const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
-      uint32_t cntd = 0;
-      if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE) {
-        const PodView pv = pod_view(rec);
-        bool drop = false;
-        if (S.node != ~0u) {
-          const uint64_t* t0e = r_t0 + (size_t)e * PW;
-          if ((t0e[S.node >> 6] >> (S.node & 63)) & 1ULL) {
-            // does the slot (a snapshot tie of the pod) score below M0 now?
-            const int64_t now_c = (int64_t)((uint64_t)S.snp_c + (uint64_t)S.dl_c);
-            const int64_t now_m = (int64_t)((uint64_t)S.snp_m + (uint64_t)S.dl_m);
-            if (res_on && !pv.zero_req)  // PodFitsResources (predicates.go:127-145)
-              drop = !((S.cap_c == 0 || S.cap_c - now_c >= pv.req_c) && (S.cap_m == 0 || S.cap_m - now_m >= pv.req_m));
-            if (d.w_lr) {  // LeastRequested (priorities.go:43-76) can only fall as requested grows
-              const int32_t lr_now = lr_win(now_c + pv.req_c, S.cap_c, S.inv_c) + lr_win(now_m + pv.req_m, S.cap_m, S.inv_m);
-              const int32_t lr_snap =
-                  lr_win(S.snp_c + pv.req_c, S.cap_c, S.inv_c) + lr_win(S.snp_m + pv.req_m, S.cap_m, S.inv_m);
-              drop |= (lr_now >> 1) != (lr_snap >> 1);
-            }
-            if (!drop && pv.nk && S.nk) {  // PodFitsPorts / NoDiskConflict vs the window's keys
-              for (uint32_t a = 0; a < S.nk; ++a) {
-                const uint32_t key = my_cl[KSG_CL_KEY + a];
-                for (uint32_t b = 0; b < pv.nk; ++b) {
-                  const bool on = b < pv.n_ports ? ports_on : disk_on;
-                  drop |= on && (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b)) == key;
-                }
-              }
-            }
-            if (!drop && spread_on && pv.s >= 0 && ((S.smask >> (pv.s & 31)) & 1u)) {
-              // ServiceSpreading (spreading.go:72-86) under an unchanged maxCount
-              int32_t delta = 0, snapc = 0;
-              for (uint32_t a = 0; a < S.ns; ++a)
-                if (my_cl[KSG_CL_SV + a] == (uint32_t)pv.s) {
-                  snapc = (int32_t)my_cl[KSG_CL_SC + a];
-                  ++delta;
-                }
-              if (delta)
-                drop = frac10_f32((int64_t)pv.smax - snapc - delta, pv.smax) !=
-                       frac10_f32((int64_t)pv.smax - snapc, pv.smax);
-            }
-            if (drop)
-              atomicOr(reinterpret_cast<unsigned long long*>(L_drop + (size_t)nb * PW + (S.node >> 6)),
-                       1ULL << (S.node & 63));
-          }
-        }
-        cntd = __popcll(__ballot(drop));
-      }
-      if (lane == 0) {
-        ctl->chk_cnt[c][nb] = cntd;
-        st_rel(&ctl->chk_seq[c], i + 1);
-      }
-      cstamp(c == 0 ? 18 : 21);
-    }
-    // write the window's deltas of this checker's slots back to HBM (the next snapshot)
-    if (S.node != ~0u) {
-      const uint32_t n = d.lo + S.node;
-      d.used_cpu[n] = (int64_t)((uint64_t)S.snp_c + (uint64_t)S.dl_c);
-      d.used_mem[n] = (int64_t)((uint64_t)S.snp_m + (uint64_t)S.dl_m);
-      for (uint32_t a = 0; a < S.nk; ++a)
-        __hip_atomic_fetch_or(d.keymap + (size_t)my_cl[KSG_CL_KEY + a] * d.nw + (n >> 6), 1ULL << (n & 63),
-                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (uint32_t a = 0; a < S.ns; ++a) {
-        const uint32_t sa = my_cl[KSG_CL_SV + a];
-        bool first = true;
-        int32_t count = 0;
-        for (uint32_t b = 0; b < S.ns; ++b) {
-          if (my_cl[KSG_CL_SV + b] == sa) {
-            if (b < a) first = false;
-            ++count;
-          }
-        }
-        __hip_atomic_fetch_add(d.svc_total + sa, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (first) {
-          const int32_t fin = (int32_t)my_cl[KSG_CL_SC + a] + count;
-          d.svc_cnt[(size_t)sa * d.n_nodes + n] = fin;
-          __hip_atomic_fetch_max(d.svc_max + sa, fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-    }
-    if constexpr (STAMP) {
-      if (lane >= 16 && lane < 22) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
-    }
-    drain_stores();
-    if (lane == 0) st_rel(&ctl->fin[c], 1u);
-    return;
-  }
-
-  // =========================================================================
-  // pre-selector (wave 2)
-  // =========================================================================
-  if (wave == KSG_R4_PS) {
-    __builtin_amdgcn_s_setprio(2);
-    // prefetch lanes: 0..35 candidate j = lane / 6, field f = lane % 6; 36..41 the
-    // next pod's service count on candidate lane - 36
-    const uint32_t fj = lane < 36 ? lane / 6 : 0u, ff = lane % 6;
-    const uint64_t* const fsrc = ff == 0   ? reinterpret_cast<const uint64_t*>(d.cap_cpu)
-                                 : ff == 1 ? reinterpret_cast<const uint64_t*>(d.cap_mem)
-                                 : ff == 2 ? reinterpret_cast<const uint64_t*>(d.used_cpu)
-                                 : ff == 3 ? reinterpret_cast<const uint64_t*>(d.used_mem)
-                                 : ff == 4 ? reinterpret_cast<const uint64_t*>(d.inv10_cpu)
-                                           : reinterpret_cast<const uint64_t*>(d.inv10_mem);
-    // the candidates of pods i-1 and i-2 (lane j < 6 holds candidate j), for L0 membership
-    uint32_t pc1 = KSG_NO_NODE, pc2 = KSG_NO_NODE;
-    uint64_t x_last = 0, x_acc = 0;  // KSG_DEBUG & 8: lanes 28..30 wait, select, prefetch
-    auto xstamp = [&](uint32_t k) {
-      if constexpr (STAMP) {
-        const uint64_t t_now = __builtin_amdgcn_s_memtime();
-        x_acc += lane == k ? t_now - x_last : 0ULL;
-        x_last = t_now;
-      }
-    };
-    if constexpr (STAMP) x_last = __builtin_amdgcn_s_memtime();
-    bool stopped = false;
-    for (uint32_t i = 0; i < n_pods && !stopped; ++i) {
-      const uint32_t e = i % RING, nb = i % KSG_R4_NB;
-      const bool has_next = i + 1 < n_pods;
-      const uint32_t en = (i + 1) % RING;
-      for (uint32_t spin = 0;; ++spin) {  // the checkers are done with pod i; pod i+1 staged
-        uint32_t cs = ld_u(&ctl->chk_seq[0]);
-#pragma unroll
-        for (int c = 1; c < KSG_RES_NCHK; ++c) cs = min(cs, ld_u(&ctl->chk_seq[c]));
-        const uint32_t rn = ld_u(&r_hdr[en].ready), st = ld_u(&ctl->stop);
-        if (cs >= i + 1 && (!has_next || rn == i + 2)) break;
-        if (st) {
-          stopped = true;
-          break;
-        }
-        if (spin > 16 * KSG_SPIN_LIMIT) {
-          ctl->hang = 1;
-          stopped = true;
-          break;
-        }
-      }
-      acq_lds();
-      if (stopped) break;
-      xstamp(28);
-      const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
-      const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
-      const uint32_t err = __builtin_amdgcn_readlane(rec, WS_ERR);
-      const uint32_t npp = __builtin_amdgcn_readlane(rec, WS_NPP), nss = __builtin_amdgcn_readlane(rec, WS_NSS);
-      const uint32_t nk = (npp & 0xffff) + (npp >> 16), n_svcs = nss >> 16;
-      uint32_t status = KSG_CS_OK, kp = 0, xlive = 0;
-      uint32_t cand = KSG_NO_NODE;  // lane j < 6: candidate j
-      if (err || m0 == KSG_S32_NONE) {
-        status = err ? KSG_CS_ERROR : KSG_CS_NOFIT;
-      } else if (__builtin_amdgcn_readlane(rec, WS_NINL) > KSG_WIN_INLINE || nk > KSG_SLOT_KEYS ||
-                 n_svcs > KSG_SLOT_SVCS) {
-        status = KSG_CS_OVERSIZE;  // lists longer than the record / a slot
-      } else {
-        const uint32_t k0 = __builtin_amdgcn_readfirstlane(r_hdr[e].k0);
-        uint32_t cc = 0;
-#pragma unroll
-        for (int c = 0; c < KSG_RES_NCHK; ++c) cc += __builtin_amdgcn_readfirstlane(ctl->chk_cnt[c][nb]);
-        kp = k0 - cc;
-        const uint64_t* t0e = r_t0 + (size_t)e * PW;
-        uint64_t* dw = L_drop + (size_t)nb * PW;
-        // which of pods i-1's (lanes 0..5) and i-2's (lanes 6..11) candidates are
-        // live ties of this pod: in T0 and not dropped (before the drops are cleared)
-        const uint32_t pc2s = (uint32_t)__shfl((int)pc2, (int)((lane - 6) & 63), 64);
-        const uint32_t pcx = lane < 6 ? pc1 : lane < 12 ? pc2s : KSG_NO_NODE;
-        bool lv = false;
-        if (pcx != KSG_NO_NODE) lv = (((t0e[pcx >> 6] & ~dw[pcx >> 6]) >> (pcx & 63)) & 1ULL) != 0;
-        xlive = (uint32_t)__ballot(lv);
-        uint64_t live[P];
-        uint32_t cl = 0;
-#pragma unroll
-        for (int q = 0; q < P; ++q) {
-          const uint64_t dq = dw[lane * P + q];
-          live[q] = t0e[lane * P + q] & ~dq;
-          if (dq) dw[lane * P + q] = 0;  // (cleared for the pod four ahead)
-          cl += __popcll(live[q]);
-        }
-        const uint32_t incl = dpp_scan_add(cl);
-        const uint32_t rmod = r_mod[e * 64 + lane];
-        const uint64_t r = r_hdr[e].r;
-        const uint64_t ru = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(r >> 32)) << 32) |
-                            (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r);
-        // e further drops: the (r mod (k'-e))-th live tie from the top and the e after it
-        uint32_t cv[KSG_R4_NCAND];
-#pragma unroll
-        for (int j = 0; j < KSG_R4_NCAND; ++j) cv[j] = KSG_NO_NODE;
-#pragma unroll
-        for (uint32_t ex = 0; ex < 3; ++ex) {
-          if (kp < ex + 1) break;
-          const uint32_t dd = cc + ex;
-          const uint32_t ix = dd < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)rmod, (int)dd) : umod64_32(ru, kp - ex);
-          const uint32_t t = kp - 1 - ex - ix;  // ascending rank in L0 minus the e dropped nodes
-          const uint32_t base = ex == 0 ? 0u : ex == 1 ? 1u : 3u;
-#pragma unroll
-          for (uint32_t m = 0; m <= ex; ++m)
-            if (t + m < kp) cv[base + m] = select_in_lanes<P>(live, cl, incl, t + m, lane);
-        }
-#pragma unroll
-        for (int j = 0; j < KSG_R4_NCAND; ++j) cand = lane == (uint32_t)j ? cv[j] : cand;
-      }
-      xstamp(29);
-      if (lane == 0) {
-        L_cand[nb].status = status;
-        L_cand[nb].kp = kp;
-        L_cand[nb].xlive = xlive;
-      }
-      if (lane < KSG_R4_NCAND) L_cand[nb].c[lane] = cand;
-      if (lane == 0) st_rel(&ctl->psel_seq, i + 1);
-      // the candidates' snapshots and the next pod's primary service count on them
-      // (the committer reads these when it re-checks pod i+1)
-      if (status == KSG_CS_OK) {
-        const uint32_t cfs = (uint32_t)__shfl((int)cand, (int)fj, 64);
-        const uint32_t csv = (uint32_t)__shfl((int)cand, (int)min(lane - 36, 7u), 64);
-        int32_t s_next = -1;
-        if (has_next) s_next = (int32_t)__builtin_amdgcn_readfirstlane(r_rec[en * DW + WS_SVC]);
-        uint64_t fv = 0;
-        int32_t scv = 0;
-        if (lane < 36 && cfs != KSG_NO_NODE) fv = gld(fsrc + d.lo + cfs);
-        if (lane >= 36 && lane < 42 && csv != KSG_NO_NODE && s_next >= 0)
-          scv = gld(d.svc_cnt + (size_t)s_next * d.n_nodes + d.lo + csv);
-        if (lane < 36) L_csnap[(size_t)nb * KSG_R4_NCAND * 6 + lane] = (int64_t)fv;
-        if (lane >= 36 && lane < 42) L_csc[nb * 8 + (lane - 36)] = scv;
-      }
-      if (lane == 0) st_rel(&ctl->csnap_seq[nb], i + 1);
-      pc2 = pc1;
-      pc1 = status == KSG_CS_OK ? cand : KSG_NO_NODE;
-      xstamp(30);
-    }
-    if constexpr (STAMP) {
-      if (lane >= 28 && lane < 31) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
-    }
-    return;
-  }
-
-  // =========================================================================
-  // x2-checker (wave 1): follows the commits in order
-  // =========================================================================
-  if (wave == KSG_R4_X2) {
-    __builtin_amdgcn_s_setprio(2);
-    const uint32_t rl = lane & 1;
-    // the committer's slot bookkeeping, replayed: node, list lengths, delta per slot
-    uint32_t xcn0 = ~0u, xcn1 = ~0u, xsk0 = 0, xsk1 = 0, xss0 = 0, xss1 = 0, xn_slots = 0;
-    int64_t xdc0 = 0, xdm0 = 0, xdc1 = 0, xdm1 = 0;
-    // commit q into its slot: returns the slot, its list lengths before q and its delta after q
-    auto replay = [&](uint32_t q, uint32_t& slot, uint32_t& bnk, uint32_t& bns, uint64_t& dlc, uint64_t& dlm,
-                      uint32_t& prec) {
-      const uint32_t node = __builtin_amdgcn_readfirstlane(L_cm[q].node);
-      const uint32_t eq = q % RING;
-      prec = lane < DW ? r_rec[eq * DW + lane] : 0u;
-      const PodView ppv = pod_view(prec);
-      const uint32_t p_svcs = (uint32_t)__builtin_amdgcn_readlane(prec, WS_NSS) >> 16;
-      const uint64_t hit0 = __ballot(xcn0 == node), hit1 = __ballot(xcn1 == node);
-      const bool in_c = (hit0 | hit1) != 0;
-      bnk = bns = 0;
-      dlc = dlm = 0;
-      if (in_c) {
-        slot = hit0 ? (uint32_t)__builtin_ctzll(hit0) : 64u + (uint32_t)__builtin_ctzll(hit1);
-        const uint32_t sl = slot & 63;
-        bnk = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? xsk0 : xsk1), (int)sl);
-        bns = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? xss0 : xss1), (int)sl);
-        dlc = readlane64((uint64_t)(slot < 64 ? xdc0 : xdc1), (int)sl);
-        dlm = readlane64((uint64_t)(slot < 64 ? xdm0 : xdm1), (int)sl);
-      } else {
-        slot = xn_slots < KSG_MAX_SLOTS ? xn_slots++ : 0u;
-      }
-      dlc += (uint64_t)ppv.req_c;
-      dlm += (uint64_t)ppv.req_m;
-      if (lane == (slot & 63)) {
-        if (slot >= 64) {
-          if (!in_c) xcn1 = node;
-          xsk1 = bnk + ppv.nk;
-          xss1 = bns + p_svcs;
-          xdc1 = (int64_t)dlc;
-          xdm1 = (int64_t)dlm;
-        } else {
-          if (!in_c) xcn0 = node;
-          xsk0 = bnk + ppv.nk;
-          xss0 = bns + p_svcs;
-          xdc0 = (int64_t)dlc;
-          xdm0 = (int64_t)dlm;
-        }
-      }
-    };
-    // the service flags later pods stop on (maxCount rises, first peer) and the
-    // first peers, of commit q (its slot's entries through q are `ent` lanes)
-    auto flags = [&](uint32_t q, uint32_t slot, uint32_t bns, uint32_t prec) {
-      const uint32_t nss = __builtin_amdgcn_readlane(prec, WS_NSS), npp = __builtin_amdgcn_readlane(prec, WS_NPP);
-      const uint32_t n_svcs = nss >> 16, n_sel = nss & 0xffff, nk = (npp & 0xffff) + (npp >> 16);
-      if (!n_svcs) return;
-      const uint32_t wn = d.lo + __builtin_amdgcn_readfirstlane(L_cm[q].node);
-      const uint32_t eq = q % RING;
-      const bool sv_lane = lane < n_svcs;
-      const uint32_t my_sv =
-          (uint32_t)__shfl((int)prec, (int)min(WS_IDS + nk + n_sel + (sv_lane ? lane : 0u), 63u), 64);
-      int32_t mx = 0, peer = 0, cnt = 0;
-      if (sv_lane) {
-        cnt = gld(d.svc_cnt + (size_t)my_sv * d.n_nodes + wn);
-        mx = r_svc[eq].max[lane];
-        peer = r_svc[eq].peer[lane];
-      }
-      const uint32_t ent = lane - KSG_CL_SV < bns ? L_cl[(size_t)slot * KSG_CL_W + lane] : ~0u;
-      uint32_t before = 0;  // earlier window commits of each service on this node
-      for (uint32_t t = 0; t < n_svcs; ++t) {
-        const uint32_t sv_t = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)t);
-        const uint32_t b_t = (uint32_t)__popcll(__ballot(ent == sv_t));
-        if (lane == t) before = b_t;
-      }
-      bool changed = sv_lane && aff_on && peer == -1 && !((L_peerset[my_sv >> 5] >> (my_sv & 31)) & 1u);
-      uint64_t pm = __ballot(sv_lane && peer == -1);
-      if (pm) {  // first commit of a service with no peer yet: its first peer, in commit order
-        uint32_t n_peer = __builtin_amdgcn_readfirstlane(ctl->n_peer);
-        while (pm) {
-          const uint32_t b = __builtin_ctzll(pm);
-          pm &= pm - 1;
-          const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)b);
-          if (!((L_peerset[fsv >> 5] >> (fsv & 31)) & 1u)) {
-            if (lane == 0) {
-              L_peerset[fsv >> 5] |= 1u << (fsv & 31);
-              L_peer[2 * n_peer] = fsv;
-              L_peer[2 * n_peer + 1] = wn;
-            }
-            ++n_peer;
-            lds_fence();
-          }
-        }
-        if (lane == 0) ctl->n_peer = n_peer;
-      }
-      if (sv_lane && spread_on && cnt + (int32_t)before + 1 > mx) changed = true;  // maxCount rises
-      if (changed) atomicOr(&L_flag[my_sv >> 5], 1u << (my_sv & 31));
-    };
-    uint64_t x_last = 0, x_acc = 0;  // KSG_DEBUG & 8: lanes 22, 23 wait, work
-    if constexpr (STAMP) x_last = __builtin_amdgcn_s_memtime();
-    uint32_t i = 0;
-    bool stopped = false;
-    for (; i < n_pods; ++i) {
-      const uint32_t e = i % RING, nb = i % KSG_R4_NB;
-      for (uint32_t spin = 0;; ++spin) {  // commit i-2 published, pod i staged
-        const uint32_t ss = ld_u(&ctl->sel_seq), rd = ld_u(&r_hdr[e].ready), st = ld_u(&ctl->stop);
-        if (ss + 1 >= i && rd == i + 1) break;
-        if (st) {
-          stopped = true;
-          break;
-        }
-        if (spin > 16 * KSG_SPIN_LIMIT) {
-          ctl->hang = 1;
-          stopped = true;
-          break;
-        }
-      }
-      acq_lds();
-      if (stopped) break;
-      if constexpr (STAMP) {
-        const uint64_t t_now = __builtin_amdgcn_s_memtime();
-        x_acc += lane == 22 ? t_now - x_last : 0ULL;
-        x_last = t_now;
-      }
-      uint32_t res = 0;
-      const uint32_t kind = i >= 2 ? __builtin_amdgcn_readfirstlane(L_cm[i - 2].kind) : 0u;
-      if (kind == 1) {
-        uint32_t slot, bnk, bns, prec;
-        uint64_t dlc, dlm;
-        replay(i - 2, slot, bnk, bns, dlc, dlm, prec);
-        flags(i - 2, slot, bns, prec);
-        const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
-        const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
-        if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE) {
-          // pod i against commit i-2's node as of that commit
-          const uint32_t node = __builtin_amdgcn_readfirstlane(L_cm[i - 2].node);
-          const uint32_t cj = (__builtin_amdgcn_readfirstlane(L_cm[i - 2].flags) >> 2) & 7u;
-          for (uint32_t spin = 0; ld_u(&ctl->csnap_seq[(i - 2) % KSG_R4_NB]) != i - 1; ++spin)
-            if (spin > 16 * KSG_SPIN_LIMIT || ld_u(&ctl->hang)) {
-              ctl->hang = 1;
-              break;
-            }
-          acq_lds();
-          const PodView pv = pod_view(rec);
-          const int32_t x_snapc =
-              pv.s >= 0 ? __builtin_amdgcn_readfirstlane(gld(d.svc_cnt + (size_t)pv.s * d.n_nodes + d.lo + node)) : 0;
-          const int64_t* cs = L_csnap + ((size_t)((i - 2) % KSG_R4_NB) * KSG_R4_NCAND + cj) * 6;
-          XState xs;
-          xs.cap = cs[rl];
-          xs.snp = cs[2 + rl];
-          xs.inv = __longlong_as_double((long long)cs[4 + rl]);
-          xs.dl = (int64_t)(rl ? dlm : dlc);
-          const uint32_t pnpp = __builtin_amdgcn_readlane(prec, WS_NPP), pnss = __builtin_amdgcn_readlane(prec, WS_NSS);
-          const uint32_t pnk = (pnpp & 0xffff) + (pnpp >> 16), pnsel = pnss & 0xffff, pns = pnss >> 16;
-          xs.nk = bnk + pnk;
-          xs.ns = bns + pns;
-          // lane t < 8: key t; lane 8 + u (u < 12): service entry u (the table row, then pod i-2's record)
-          const uint32_t kt = lane - KSG_CL_KEY, ut = lane - KSG_CL_SV;
-          const bool from_row = (kt < KSG_SLOT_KEYS && kt < bnk) || (ut < KSG_SLOT_SVCS && ut < bns);
-          const uint32_t src = kt < KSG_SLOT_KEYS ? WS_IDS + (kt - bnk) : WS_IDS + pnk + pnsel + (ut - bns);
-          const uint32_t from_rec = (uint32_t)__shfl((int)prec, (int)min(src, 63u), 64);
-          const uint32_t rowv = from_row ? L_cl[(size_t)slot * KSG_CL_W + lane] : 0u;
-          const uint32_t xcl = from_row ? rowv : from_rec;
-          res = recheck_x(d, pv, rec, xs, xcl, 0u, x_snapc, res_on, ports_on, disk_on, spread_on, aff_on, 0, true,
-                          lane) & 1u;
-        }
-      }
-      if (lane == 0) {
-        ctl->x2_res[nb] = res;
-        st_rel(&ctl->x2_seq, i + 1);
-      }
-      if constexpr (STAMP) {
-        const uint64_t t_now = __builtin_amdgcn_s_memtime();
-        x_acc += lane == 23 ? t_now - x_last : 0ULL;
-        x_last = t_now;
-      }
-    }
-    // the committer is done: the flags / first peers of the commits not applied yet
-    for (uint32_t spin = 0; !ld_u(&ctl->stop); ++spin) {
-      if (spin > 16 * KSG_SPIN_LIMIT) {
-        ctl->hang = 1;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    acq_lds();
-    const uint32_t R = __builtin_amdgcn_readfirstlane(ctl->resolved);
-    for (uint32_t q = i >= 2 ? i - 2 : 0; q < R; ++q) {
-      if (__builtin_amdgcn_readfirstlane(L_cm[q].kind) != 1) continue;
-      uint32_t slot, bnk, bns, prec;
-      uint64_t dlc, dlm;
-      replay(q, slot, bnk, bns, dlc, dlm, prec);
-      flags(q, slot, bns, prec);
-    }
-    if constexpr (STAMP) {
-      if (lane >= 22 && lane < 24) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
-    }
-    drain_stores();
-    if (lane == 0) st_rel(&ctl->fin_x, 1u);
-    return;
-  }
-  if (wave != 0) return;
-
-  // =========================================================================
-  // committer (wave 0)
-  // =========================================================================
-  __builtin_amdgcn_s_setprio(3);
-  uint32_t resolved = n_pods, reason = 0, n_slots = 0, n_draws = 0;
-  uint32_t cn0 = ~0u, cn1 = ~0u;  // nodes of slots lane and 64 + lane
-  uint32_t sk0 = 0, sk1 = 0;      // their key counts
-  uint32_t ss0 = 0, ss1 = 0;      // their service entry counts
-  int64_t dc0 = 0, dm0 = 0, dc1 = 0, dm1 = 0;  // their window deltas
-  const uint32_t rl = lane & 1;
-  // commit i-1 (x1) and commit i-2 (x2): valid, node, the candidate index it was drawn as
-  bool h1 = false, h2 = false;
-  uint32_t x1 = 0, x2 = 0, x1cj = 0, x2cj = 0, x1slot = 0, x1bns = 0;
-  XState xs1;
-  xs1.cap = xs1.snp = xs1.dl = 0;
-  xs1.inv = 0.0;
-  xs1.nk = xs1.ns = 0;
-  int32_t x1_snapc = 0;  // pod i's service count on x1 at the snapshot (staged with x1's candidate)
-  uint64_t t_last = 0, t_acc = 0;
-#define KSG_STAMP4(k)                                        \
-  if constexpr (STAMP) {                                     \
-    const uint64_t t_now = __builtin_amdgcn_s_memtime();     \
-    t_acc += lane == (uint32_t)(k) ? t_now - t_last : 0ULL;  \
-    t_last = t_now;                                          \
-  }
-#define KSG_COUNT4(k, v)                                   \
-  if constexpr (STAMP) {                                   \
-    t_acc += lane == (uint32_t)(k) ? (uint64_t)(v) : 0ULL; \
-  }
-  if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
-  for (uint32_t i = 0; i < n_pods; ++i) {
-    const uint32_t e = i % RING, nb = i % KSG_R4_NB;
-    bool hung = false;
-    for (uint32_t spin = 0;; ++spin) {  // pod i staged (the re-check needs only the pod)
-      const uint32_t rd = ld_u(&r_hdr[e].ready), hg = ld_u(&ctl->hang);
-      if (rd == i + 1) break;
-      if (spin > 16 * KSG_SPIN_LIMIT || hg) {
-        hung = true;
-        break;
-      }
-    }
-    acq_lds();
-    if (hung) {
-      resolved = i;
-      reason = KSG_STOP_HANG;
-      break;
-    }
-    KSG_STAMP4(0)
-    const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
-    const PodView pv = pod_view(rec);
-    const int32_t s = pv.s;
-    const uint32_t nss = __builtin_amdgcn_readlane(rec, WS_NSS);
-    const uint32_t n_sel = nss & 0xffff, n_svcs = nss >> 16, nk = pv.nk;
-    // ---- pod i against commit i-1's node, as of that commit
-    uint32_t r1 = 0;
-    if (h1) {
-      const uint32_t xcl = lane < xs1.nk ? L_cl[(size_t)x1slot * KSG_CL_W + lane]
-                           : (lane >= KSG_CL_SV && lane - KSG_CL_SV < xs1.ns) ? L_cl[(size_t)x1slot * KSG_CL_W + lane]
-                                                                             : ~0u;
-      const int32_t peer0 = (int32_t)__builtin_amdgcn_readfirstlane(r_svc[e].peer[0]);
-      const bool pset = s >= 0 && ((__builtin_amdgcn_readfirstlane(L_peerset[s >> 5]) >> (s & 31)) & 1u) != 0;
-      r1 = recheck_x(d, pv, rec, xs1, xcl, x1bns, x1_snapc, res_on, ports_on, disk_on, spread_on, aff_on, peer0,
-                     pset, lane);
-    }
-    KSG_STAMP4(1)
-    // ---- the pre-selector's candidates, the x2-checker's verdict, the flags of commits <= i-2
-    for (uint32_t spin = 0;; ++spin) {
-      const uint32_t ps = ld_u(&ctl->psel_seq), xq = ld_u(&ctl->x2_seq), hg = ld_u(&ctl->hang);
-      if (ps >= i + 1 && xq >= i + 1) break;
-      if (spin > 16 * KSG_SPIN_LIMIT || hg) {
-        hung = true;
-        break;
-      }
-    }
-    acq_lds();
-    if (hung) {
-      resolved = i;
-      reason = KSG_STOP_HANG;
-      break;
-    }
-    KSG_STAMP4(2)
-    const uint32_t status = __builtin_amdgcn_readfirstlane(L_cand[nb].status);
-    if (status == KSG_CS_NOFIT || status == KSG_CS_ERROR) {
-      // ServiceAffinity peer error / nothing fit at the snapshot: no draw, no commit
-      if (lane == 0) {
-        L_cm[i].kind = 0;
-        L_out[i] = status == KSG_CS_ERROR ? KSG_OUT_ERROR : KSG_OUT_NOFIT;
-        st_rel(&ctl->sel_seq, i + 1);
-      }
-      h2 = h1;
-      x2 = x1;
-      x2cj = x1cj;
-      h1 = false;
-      continue;
-    }
-    if (status == KSG_CS_OVERSIZE) {
-      resolved = i;  // the exact per-pod kernel takes it
-      reason = i == 0 ? KSG_STOP_OVERSIZE : KSG_STOP_SLOT;
-      break;
-    }
-    const uint32_t kp = __builtin_amdgcn_readfirstlane(L_cand[nb].kp);
-    const uint32_t xlv = __builtin_amdgcn_readfirstlane(L_cand[nb].xlive);
-    const uint32_t cl6 = lane < KSG_R4_NCAND ? L_cand[nb].c[lane] : KSG_NO_NODE;
-    const uint32_t xr2 = __builtin_amdgcn_readfirstlane(ctl->x2_res[nb]);
-    const uint32_t fw = s >= 0 ? __builtin_amdgcn_readfirstlane(L_flag[s >> 5]) : 0u;
-    if (s >= 0 && (spread_on || aff_on) && ((r1 & 2u) || ((fw >> (s & 31)) & 1u))) {
-      resolved = i;  // a service scalar this pod reads changed in the window
-      reason = KSG_STOP_SERVICE;
-      break;
-    }
-    // ---- the two late drops: x1 (commit i-1), x2 (commit i-2, unless it is x1's node)
-    const bool d1 = h1 && (r1 & 1u) && ((xlv >> x1cj) & 1u);
-    const bool d2 = h2 && (xr2 & 1u) && ((xlv >> (6 + x2cj)) & 1u) && !(h1 && x1 == x2);
-    const uint32_t ex = (d1 ? 1u : 0u) + (d2 ? 1u : 0u);
-    if (kp <= ex) {
-      resolved = i;  // every snapshot tie got worse: needs a fresh snapshot
-      reason = KSG_STOP_EXHAUSTED;
-      break;
-    }
-    // the answer: among the ex+1 staged nodes, the first whose rank in L0 minus
-    // the dropped nodes is the draw's
-    uint32_t cj;
-    if (ex == 0) {
-      cj = 0;
-    } else if (ex == 1) {
-      const uint32_t xd = d1 ? x1 : x2;
-      const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)cl6, 1);
-      cj = xd > b0 ? 1u : 2u;
-    } else {
-      cj = 5;
-#pragma unroll
-      for (uint32_t m = 0; m < 3; ++m) {
-        const uint32_t cm = (uint32_t)__builtin_amdgcn_readlane((int)cl6, (int)(3 + m));
-        const uint32_t below = (x1 < cm ? 1u : 0u) + (x2 < cm ? 1u : 0u);
-        if (cj == 5 && cm != x1 && cm != x2 && below == m) cj = 3 + m;
-      }
-    }
-    const uint32_t woff = (uint32_t)__builtin_amdgcn_readlane((int)cl6, (int)cj);
-    if (ex) KSG_COUNT4(7, 64)
-    if (cj) KSG_COUNT4(8, 64)
-    KSG_STAMP4(3)
-    // ---- AssumePod's slot
-    const uint64_t hit0 = __ballot(cn0 == woff);
-    const uint64_t hit1 = __ballot(cn1 == woff);
-    const bool in_c = (hit0 | hit1) != 0;
-    uint32_t slot, base_nk = 0, base_ns = 0;
-    int64_t base_dc = 0, base_dm = 0;
-    if (in_c) {
-      slot = hit0 ? (uint32_t)__builtin_ctzll(hit0) : 64u + (uint32_t)__builtin_ctzll(hit1);
-      const uint32_t sl = slot & 63;
-      base_nk = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? sk0 : sk1), (int)sl);
-      base_ns = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? ss0 : ss1), (int)sl);
-      if (base_nk + nk > KSG_SLOT_KEYS || base_ns + n_svcs > KSG_SLOT_SVCS) {
-        resolved = i;  // this pod is redone (with the same draw) in the next window
-        reason = KSG_STOP_SLOT;
-        break;
-      }
-      base_dc = (int64_t)readlane64((uint64_t)(slot < 64 ? dc0 : dc1), (int)sl);
-      base_dm = (int64_t)readlane64((uint64_t)(slot < 64 ? dm0 : dm1), (int)sl);
-    } else {
-      if (n_slots == KSG_MAX_SLOTS) {
-        resolved = i;
-        reason = KSG_STOP_SLOT;
-        break;
-      }
-      slot = n_slots++;
-    }
-    const int64_t new_dc = (int64_t)((uint64_t)base_dc + (uint64_t)pv.req_c);
-    const int64_t new_dm = (int64_t)((uint64_t)base_dm + (uint64_t)pv.req_m);
-    {  // the slot's table row: the pod's keys and service ids (record lane L holds dword L)
-      uint32_t* row = L_cl + (size_t)slot * KSG_CL_W;
-      const uint32_t kt = lane - WS_IDS, st = lane - (WS_IDS + nk + n_sel);
-      if (kt < nk) row[KSG_CL_KEY + base_nk + kt] = rec;
-      if (st < n_svcs) row[KSG_CL_SV + base_ns + st] = rec;
-    }
-    if (lane == 0) {
-      L_cm[i] = WinCommit4{1u, slot, woff, (in_c ? 0u : 1u) | (cj << 2) | (n_svcs << 8)};
-      L_out[i] = (int32_t)(d.lo + woff);
-      st_rel(&ctl->sel_seq, i + 1);  // the checkers and the x2-checker move on
-    }
-    if (lane == (slot & 63)) {  // this wave's counts and deltas of the slot
-      if (slot >= 64) {
-        if (!in_c) cn1 = woff;
-        dc1 = new_dc;
-        dm1 = new_dm;
-        sk1 = base_nk + nk;
-        ss1 = base_ns + n_svcs;
-      } else {
-        if (!in_c) cn0 = woff;
-        dc0 = new_dc;
-        dm0 = new_dm;
-        sk0 = base_nk + nk;
-        ss0 = base_ns + n_svcs;
-      }
-    }
-    KSG_STAMP4(4)
-    // ---- x1 for pod i+1: this commit's node, its snapshot staged with its candidate
-    for (uint32_t spin = 0;; ++spin) {
-      const uint32_t cs = ld_u(&ctl->csnap_seq[nb]), hg = ld_u(&ctl->hang);
-      if (cs == i + 1) break;
-      if (spin > 16 * KSG_SPIN_LIMIT || hg) {
-        hung = true;
-        break;
-      }
-    }
-    acq_lds();
-    if (hung) {
-      resolved = i + 1;  // (pod i is committed)
-      reason = KSG_STOP_HANG;
-      ++n_draws;
-      break;
-    }
-    {
-      const int64_t* cs = L_csnap + ((size_t)nb * KSG_R4_NCAND + cj) * 6;
-      xs1.cap = cs[rl];
-      xs1.snp = cs[2 + rl];
-      xs1.inv = __longlong_as_double((long long)cs[4 + rl]);
-      x1_snapc = __builtin_amdgcn_readfirstlane(L_csc[nb * 8 + cj]);
-    }
-    h2 = h1;
-    x2 = x1;
-    x2cj = x1cj;
-    h1 = true;
-    x1 = woff;
-    x1cj = cj;
-    x1slot = slot;
-    x1bns = base_ns;
-    xs1.dl = rl ? new_dm : new_dc;
-    xs1.nk = base_nk + nk;
-    xs1.ns = base_ns + n_svcs;
-    ++n_draws;
-    KSG_STAMP4(5)
-  }
-  if (lane == 0) {
-    ctl->resolved = resolved;
-    st_rel(&ctl->stop, 1u);
-  }
-  // the checkers apply the last commits and write their slots back; the
-  // x2-checker records the last first peers
-  bool drained = false;
-  for (uint32_t spin = 0; spin <= 16 * KSG_SPIN_LIMIT; ++spin) {
-    bool done = ld_acq(&ctl->fin_x) != 0;
-#pragma unroll
-    for (int c = 0; c < KSG_RES_NCHK; ++c) done = done && ld_acq(&ctl->fin[c]) != 0;
-    if (done) {
-      drained = true;
-      break;
-    }
-  }
-  if (!drained || ld_acq(&ctl->hang)) reason = KSG_STOP_HANG;
-  if constexpr (STAMP) {
-    if (lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
-  }
-#undef KSG_STAMP4
-#undef KSG_COUNT4
-  const uint32_t n_peer = __builtin_amdgcn_readfirstlane(ctl->n_peer);
-  for (uint32_t t = lane; t < n_peer; t += 64) {
-    const uint32_t sv = L_peer[2 * t];
-    int32_t expect = -1;
-    __hip_atomic_compare_exchange_strong(d.svc_peer + sv, &expect, (int32_t)L_peer[2 * t + 1], __ATOMIC_RELAXED,
-                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  for (uint32_t t = lane; t < resolved; t += 64) out[t] = L_out[t];
-  if (lane == 0) {
-    *rng_io = rng0 + (uint64_t)n_draws * 0x9E3779B97F4A7C15ULL;
-    if (reason == KSG_STOP_HANG) {
-      run->halt = KSG_HALT_HANG;
-    } else if (reason == KSG_STOP_OVERSIZE) {
-      run->halt = KSG_HALT_OVERSIZE;  // pod pos: the host runs the exact per-pod path, then resumes
-    } else if (resolved == 0 || resolved > n_pods) {
-      run->halt = KSG_HALT_BADCOUNT;
-    } else {
-      run->pos = pos + resolved;
-      run->windows += 1;
-      if (reason >= 1 && reason <= 3) run->stops[reason] += 1;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
+// the plain resolver (every configuration without ServiceAntiAffinity, ksg_plain.hip)
+uint32_t ksg_win_plain_lds(const KsgDev& d, uint32_t wcap);
+hipError_t ksg_launch_win_plain(const KsgDev& d, uint32_t P, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
+                                const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st);
+
 static uint32_t win_P(const KsgDev& d) {
   const uint32_t P = (d.nwords + 63) / 64;
   return P <= 1 ? 1 : P <= 2 ? 2 : P <= 4 ? 4 : P <= 8 ? 8 : P <= 16 ? 16 : P <= 32 ? 32 : 0;
@@ -5304,10 +2892,9 @@ uint32_t ksg_win_max_window(const KsgDev& d) {
     const uint32_t mid = (lo + hi + 1) / 2;
     const uint32_t need = (anti && d.rr_dz && !(d.dbg & 4096))
                               ? win2_lds_offsets(P, nflag, mid, d.rr_dz, d.n_services).total
-                          : anti            ? win_lds_offsets(P, nflag, mid, d.n_anti > 0, d.rr_dz, d.n_services).total
-                          : (d.dbg & 512)  ? win3_lds_offsets(P, nflag, mid).total
-                          : (d.dbg & 1024) ? win4_lds_offsets(P, nflag, mid).total
-                                           : win2_lds_offsets(P, nflag, mid).total;
+                          : anti   ? win_lds_offsets(P, nflag, mid, d.n_anti > 0, d.rr_dz, d.n_services).total
+                          : P <= 8 ? ksg_win_plain_lds(d, mid)
+                                   : win2_lds_offsets(P, nflag, mid).total;
     if (need <= kWinLdsBudget) lo = mid;
     else hi = mid - 1;
   }
@@ -5330,38 +2917,6 @@ static hipError_t win_resolve_launch(const KsgDev& d, uint32_t wcap, size_t lds,
   return hipGetLastError();
 }
 
-template <int PP, bool ST>
-static hipError_t win_resolve3_launch(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run,
-                                      const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
-                                      hipStream_t st) {
-  static bool once = false;
-  if (!once) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_resolve3_kernel<PP, ST>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipGetLastError();
-    once = true;
-  }
-  hipLaunchKernelGGL((ksg_win_resolve3_kernel<PP, ST>), dim3(1), dim3(win3_nt(PP)), lds, st, d, wcap, run, sums, x, rng,
-                     out);
-  return hipGetLastError();
-}
-
-template <int PP, bool ST>
-static hipError_t win_resolve4_launch(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run,
-                                      const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
-                                      hipStream_t st) {
-  static bool once = false;
-  if (!once) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_resolve4_kernel<PP, ST>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipGetLastError();
-    once = true;
-  }
-  hipLaunchKernelGGL((ksg_win_resolve4_kernel<PP, ST>), dim3(1), dim3(win4_nt(PP)), lds, st, d, wcap, run, sums, x, rng,
-                     out);
-  return hipGetLastError();
-}
-
 template <int PP, bool ST, bool AN>
 static hipError_t win_resolve2_launch(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run,
                                       const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
@@ -5381,55 +2936,17 @@ static hipError_t win_resolve2_launch(const KsgDev& d, uint32_t wcap, size_t lds
 hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
                                   const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
   const uint32_t P = win_P(d);
-  if (x.fit_off == 0 && (d.dbg & 1024) && !(d.dbg & (128 | 512))) {  // KSG_DEBUG & 1024: the lag-3 resolver
-    const size_t lds4 = win4_lds_offsets(P, (d.n_services + 31) / 32, wcap).total;
-    const bool stamp4 = (d.dbg & 8) != 0;
-#define KSG_RES4_CASE(PP)                                                                         \
-  if (P == PP)                                                                                    \
-    return stamp4 ? win_resolve4_launch<PP, true>(d, wcap, lds4, run, sums, x, rng, out, st)      \
-                  : win_resolve4_launch<PP, false>(d, wcap, lds4, run, sums, x, rng, out, st);
-    KSG_RES4_CASE(1)
-    KSG_RES4_CASE(2)
-    KSG_RES4_CASE(4)
-    KSG_RES4_CASE(8)
-    KSG_RES4_CASE(16)
-    KSG_RES4_CASE(32)
-#undef KSG_RES4_CASE
-    return hipErrorInvalidValue;
-  }
-  if (x.fit_off == 0 && (d.dbg & 512) && !(d.dbg & 128)) {
-    // KSG_DEBUG & 512: the pre-selecting resolver (measured slower than the
-    // register-slot resolver on config 2: DESIGN.md section 4), for comparison
-    const size_t lds3 = win3_lds_offsets(P, (d.n_services + 31) / 32, wcap).total;
-    const bool stamp3 = (d.dbg & 8) != 0;
-#define KSG_RES3_CASE(PP)                                                                         \
-  if (P == PP)                                                                                    \
-    return stamp3 ? win_resolve3_launch<PP, true>(d, wcap, lds3, run, sums, x, rng, out, st)      \
-                  : win_resolve3_launch<PP, false>(d, wcap, lds3, run, sums, x, rng, out, st);
-    KSG_RES3_CASE(1)
-    KSG_RES3_CASE(2)
-    KSG_RES3_CASE(4)
-    KSG_RES3_CASE(8)
-    KSG_RES3_CASE(16)
-    KSG_RES3_CASE(32)
-#undef KSG_RES3_CASE
-    return hipErrorInvalidValue;
-  }
-  if (x.fit_off == 0 && !(d.dbg & 128)) {  // no ServiceAntiAffinity: the register-slot resolver
-    // (KSG_DEBUG & 128: the LDS-slot resolver instead, for comparison)
+  if (x.fit_off == 0 && !(d.dbg & 128) && P <= 8)  // no ServiceAntiAffinity: the plain resolver (ksg_plain.hip)
+    return ksg_launch_win_plain(d, P, wcap, run, sums, x, rng, out, st);  // (KSG_DEBUG & 128: the LDS-slot one)
+  if (x.fit_off == 0 && !(d.dbg & 128)) {  // (more than 32k nodes per shard: the register-slot resolver, for now)
     const size_t lds2 = win2_lds_offsets(P, (d.n_services + 31) / 32, wcap).total;
     const bool stamp2 = (d.dbg & 8) != 0;
-#define KSG_RES2_CASE(PP)                                                                         \
-  if (P == PP)                                                                                    \
-    return stamp2 ? win_resolve2_launch<PP, true, false>(d, wcap, lds2, run, sums, x, rng, out, st) \
-                  : win_resolve2_launch<PP, false, false>(d, wcap, lds2, run, sums, x, rng, out, st);
-    KSG_RES2_CASE(1)
-    KSG_RES2_CASE(2)
-    KSG_RES2_CASE(4)
-    KSG_RES2_CASE(8)
-    KSG_RES2_CASE(16)
-    KSG_RES2_CASE(32)
-#undef KSG_RES2_CASE
+    if (P == 16)
+      return stamp2 ? win_resolve2_launch<16, true, false>(d, wcap, lds2, run, sums, x, rng, out, st)
+                    : win_resolve2_launch<16, false, false>(d, wcap, lds2, run, sums, x, rng, out, st);
+    if (P == 32)
+      return stamp2 ? win_resolve2_launch<32, true, false>(d, wcap, lds2, run, sums, x, rng, out, st)
+                    : win_resolve2_launch<32, false, false>(d, wcap, lds2, run, sums, x, rng, out, st);
     return hipErrorInvalidValue;
   }
   if (x.fit_off != 0 && x.rr && !(d.dbg & 4096)) {

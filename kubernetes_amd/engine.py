@@ -278,7 +278,8 @@ class DeviceScheduler:
         return {"batches": int(o[0]), "device_ms": float(o[1]), "eval_ms": float(o[2]),
                 "resolve_ms": float(o[3]), "launches": int(o[4]), "windows": int(o[5]),
                 "stops_service": int(o[6]), "stops_exhausted": int(o[7]), "stops_cache": int(o[8]),
-                "host_us": {k: float(v) for k, v in zip(self.HOST_PHASES, o[9:17])}}
+                "host_us": {k: float(v) for k, v in zip(self.HOST_PHASES, o[9:17])},
+                "wcap_sum": float(o[17])}
 
     def debug_counters(self) -> np.ndarray:
         """KSG_DEBUG=8 contexts: the window resolver's per-stage cycle counters

@@ -118,37 +118,46 @@ def test_family_windows_match_oracle(family):
         dev.close()
 
 
-# ---- repeated runs: the resolver's waves hand off through LDS flags, so a
-# missing wait shows up as an occasional divergence, not a deterministic one
-# (a single drawn-node mailbox the committer could overwrite while running
-# ahead through no-commit pods differed in ~1 of 5 runs of `namespaces`)
+# ---- interleavings: the resolver's waves hand off through LDS flags, so a
+# missing wait would show up only under some interleaving (a single drawn-node
+# mailbox the committer could overwrite while running ahead through no-commit
+# pods differed in ~1 of 5 runs of `namespaces` in round 2). Instead of
+# repeating runs, each case runs once per fixed delay pattern: KSG_DEBUG bits
+# 16..19 make one wave role (committer, x-checker, checkers, producers) sleep
+# ~512 cycles per pod (ksg_plain.hip), which pushes every hand-off onto its
+# other side (the role that is usually ahead falls behind, and vice versa)
+_SKEWS = (0, 1, 2, 4, 8, 1 | 4, 2 | 8, 2 | 4)
+
+
 @pytest.mark.parametrize("family", FAMILIES)
-def test_family_repeated_runs_match_oracle(family):
+def test_family_interleavings_match_oracle(family, monkeypatch):
     case = FamilyCase(family, 700, 500)
     orc = case.load(OracleScheduler(case.cfg))
     want, _ = orc.batch(case.batch, 777)
     for window in (5, 64):
-        for rep in range(12):
+        for skew in _SKEWS:
+            monkeypatch.setenv("KSG_DEBUG", str(skew << 16))  # (read by ksg_set_cluster)
             dev = case.load(DeviceScheduler(case.cfg, device=0))
             dev.set_window(window)
             got, _ = dev.batch(case.batch, 777)
             dev.close()
             bad = np.nonzero(got != want)[0]
-            assert bad.size == 0, f"{family} window {window} run {rep}: first mismatches at {bad[:6]}"
+            assert bad.size == 0, f"{family} window {window} skew {skew}: first mismatches at {bad[:6]}"
 
 
 @pytest.mark.parametrize("seed", range(0, 64, 4))
-def test_fuzz_repeated_runs_match_oracle(seed):
+def test_fuzz_interleavings_match_oracle(seed, monkeypatch):
     cfg, arrays, batch, desc = _case(seed)
     orc = OracleScheduler(cfg)
     orc.set_cluster(arrays)
     want, _ = orc.batch(batch, 4242 + seed)
     for window in (5, 64):
-        for rep in range(6):
+        for skew in _SKEWS[::2] if seed % 8 else _SKEWS:
+            monkeypatch.setenv("KSG_DEBUG", str(skew << 16))
             dev = DeviceScheduler(cfg, device=0)
             dev.set_window(window)
             dev.set_cluster(arrays)
             got, _ = dev.batch(batch, 4242 + seed)
             dev.close()
             bad = np.nonzero(got != want)[0]
-            assert bad.size == 0, f"{desc} window {window} run {rep}: first mismatches at {bad[:6]}"
+            assert bad.size == 0, f"{desc} window {window} skew {skew}: first mismatches at {bad[:6]}"

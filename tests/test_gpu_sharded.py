@@ -215,3 +215,93 @@ def test_rccl_one_rank_begin_commit_matches_oracle():
     finally:
         dev.close()
         orc.close()
+
+
+# ---- ranks with different histories before a shared batch -------------------------
+def _history_worker(rank, world, port, q):
+    """Both ranks run the same (collective) batches; between them rank 0 alone
+    adds and removes extra pods (its host mirror, patch queue and deferred replay
+    differ from rank 1's) and arrives late. Both ranks must enqueue the same
+    launches and collectives in every batch (a rank that sized its window rounds
+    from its own history would hang the all-gather) and end with the oracle's
+    placements."""
+    import time
+
+    import torch.distributed as dist
+
+    from kubernetes_amd.engine import DeviceScheduler, PodBatch, gloo_allgather
+    from tests.helpers import Case
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        case = Case("config2", 1500, 1600)
+        dev = DeviceScheduler(case.cfg, device=0, rank=rank, world=world, allgather=gloo_allgather())
+        dev.set_window(128)
+        dev.set_cluster(case.view.arrays)
+        pods = case.batch.pods
+        rng = 1234
+        outs = []
+        # (the batches themselves are collective: every rank makes the same calls)
+        for a, b in ((0, 150), (150, 400), (400, 600)):
+            o, rng = dev.batch(PodBatch(pods[a:b], case.batch.ids), rng)
+            outs.append(o)
+            if rank == 0:  # rank-local history between the batches
+                ep = pods[1500 + a // 6:1500 + b // 6].copy()
+                ep["service"], ep["n_svcs"] = -1, 0  # (a removed pod leaves no service peer behind)
+                extra = PodBatch(ep, case.batch.ids)
+                for i in range(len(extra)):
+                    dev.add_pod((7 * i + a) % 1500, extra, i)
+                for i in range(len(extra)):
+                    dev.remove_pod(int(extra.pods[i]["uid"]))
+                time.sleep(0.3)
+        o, rng = dev.batch(PodBatch(pods[600:1500], case.batch.ids), rng)
+        outs.append(o)
+        used_c, used_m = dev.read_requested()
+        dev.close()
+        q.put((rank, np.concatenate(outs).tolist(), rng, used_c.tolist(), used_m.tolist(), None))
+    except Exception as e:
+        import traceback
+
+        q.put((rank, None, None, None, None, traceback.format_exc() + repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_ranks_with_different_histories():
+    """(Round-1 advisor: per-rank round sizing could hang the exchange.) Every
+    collective of a window round is sized from this batch's progress only."""
+    import torch.multiprocessing as mp
+
+    from kubernetes_amd.engine import PodBatch
+    from oracle.pyoracle import OracleScheduler
+    from tests.helpers import Case
+
+    case = Case("config2", 1500, 1600)
+    orc = OracleScheduler(case.cfg)
+    orc.set_cluster(case.view.arrays)
+    want, st = orc.batch(PodBatch(case.batch.pods[:1500], case.batch.ids), 1234)
+    wc, wm = orc.read_requested()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_history_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = []
+    try:
+        for _ in range(2):
+            res.append(q.get(timeout=110))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for rank, out, rng, uc, um, err in sorted(res, key=lambda r: r[0]):
+        assert err is None, err
+        got = np.asarray(out)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, f"rank {rank}: first mismatches at {bad[:8]}"
+        assert rng == st
+        assert np.array_equal(np.asarray(uc), wc) and np.array_equal(np.asarray(um), wm)

@@ -142,3 +142,27 @@ def test_random_sets_hip_vs_c_oracle(seed):
         assert (got == abi.ADMIT_CAPACITY).any() and (got == abi.ADMIT_NODESELECTOR).any()
     finally:
         ka.close()
+
+
+@pytest.mark.gpu
+def test_overlapping_admission_sets_are_refused():
+    """Two admission sets sharing a pod would have two kernel lanes write its
+    result: the call fails with KSG_ERR_ARG before any device work."""
+    from kubernetes_amd.engine import KsgError
+
+    sets = _random_sets(4)
+    ka = KubeletAdmission()
+    try:
+        arr, batch, pairs = ka.build(sets)
+        bad = arr.copy()
+        j = next(k for k in range(1, len(bad)) if bad[k]["n_pods"] > 0)
+        bad[j]["pod_off"] = bad[0]["pod_off"]  # set j now covers set 0's first pods
+        bad[j]["n_pods"] = max(1, min(int(bad[j]["n_pods"]), int(bad[0]["n_pods"])))
+        if int(bad[0]["n_pods"]) == 0:
+            bad[0]["n_pods"] = 1
+        with pytest.raises(KsgError, match="share pod"):
+            ka.engine.admit(bad, batch, pairs, 3)
+        got = ka.engine.admit(arr, batch, pairs, 3)  # the context is still usable
+        assert np.array_equal(got, pyoracle.admit_pods(arr, batch, pairs, 3))
+    finally:
+        ka.close()
