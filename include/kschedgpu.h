@@ -81,10 +81,10 @@ extern "C" {
 #define KSG_FAIL_PODFITSRESOURCES 6
 #define KSG_FAIL_SERVICEAFFINITY 7
 
-#define KSG_MAX_ANTI 4          /* ServiceAntiAffinity priorities (policy)      */
-#define KSG_MAX_LABEL_PREF 8    /* LabelPreference priorities (policy)          */
-#define KSG_MAX_PRESENCE 8      /* LabelsPresence predicates (policy)           */
-#define KSG_MAX_PRESENCE_KEYS 8 /* labels per LabelsPresence predicate          */
+#define KSG_MAX_ANTI 16          /* ServiceAntiAffinity priorities (policy)      */
+#define KSG_MAX_LABEL_PREF 32    /* LabelPreference priorities (policy)          */
+#define KSG_MAX_PRESENCE 16      /* LabelsPresence predicates (policy)           */
+#define KSG_MAX_PRESENCE_KEYS 16 /* labels per LabelsPresence predicate          */
 #define KSG_MAX_AFF 4           /* ServiceAffinity labels (union of predicates) */
 #define KSG_MAX_AFF_GROUPS 8    /* ServiceAffinity predicates (label groups)    */
 
@@ -100,25 +100,29 @@ extern "C" {
 
 /* Scheduler configuration: the compiled form of map[string]FitPredicate +
  * []PriorityConfig that NewGenericScheduler receives (factory.go:149).
- *
- * Weights are int32 (factory.compile refuses anything outside int32), and
- * ksg_create returns KSG_ERR_ARG when a combined score could reach 2^30 in
- * magnitude: 10 * (sum of |w| over score-10 priorities) + |w_equal| >= 2^30
- * (scores are kept in int32 on the device). */
+ * Any Policy the reference accepts fits: weights are int64 and the list caps
+ * above are well past what a Policy names in practice (the reference registers
+ * any number, plugins.go:81-183); factory.compile reports a Policy beyond them. */
 typedef struct ksg_config {
   uint32_t predicates;          /* KSG_PRED_* bitmask                                   */
   uint32_t n_priority_configs;  /* len(priorityConfigs); 0 => EqualPriority fallback
                                    (generic_scheduler.go:141-143)                       */
-  int32_t w_least_requested;    /* LeastRequestedPriority weight, 0 = absent/skipped    */
-  int32_t w_service_spreading;  /* ServiceSpreadingPriority weight                       */
-  int32_t w_equal;              /* EqualPriority weight (DefaultProvider: 0, skipped)    */
+  /* Priority weights are Go ints (plugin/pkg/scheduler/api/types.go:46: int64 on
+   * the reference's platform) and combined scores wrap like Go's int
+   * (generic_scheduler.go:145-159). While 10 * sum|w| + |w_equal| < 2^30 and at
+   * most 4 ServiceAntiAffinity priorities carry a weight, the window path runs
+   * with int32 scores; otherwise every batch takes the exact kernels with int64
+   * (wrapping) combined scores. */
+  int64_t w_least_requested;    /* LeastRequestedPriority weight, 0 = absent/skipped    */
+  int64_t w_service_spreading;  /* ServiceSpreadingPriority weight                       */
+  int64_t w_equal;              /* EqualPriority weight (DefaultProvider: 0, skipped)    */
   uint32_t n_anti;              /* ServiceAntiAffinity priorities                        */
   uint32_t anti_key[KSG_MAX_ANTI];   /* label-key id of each                           */
-  int32_t w_anti[KSG_MAX_ANTI];
+  int64_t w_anti[KSG_MAX_ANTI];
   uint32_t n_label_pref;        /* LabelPreference priorities                            */
   uint32_t pref_key[KSG_MAX_LABEL_PREF];
   uint32_t pref_presence[KSG_MAX_LABEL_PREF];
-  int32_t w_pref[KSG_MAX_LABEL_PREF];
+  int64_t w_pref[KSG_MAX_LABEL_PREF];
   uint32_t n_presence;          /* LabelsPresence predicates                             */
   uint32_t presence_n_keys[KSG_MAX_PRESENCE];
   uint32_t presence_keys[KSG_MAX_PRESENCE][KSG_MAX_PRESENCE_KEYS];
@@ -402,7 +406,7 @@ typedef struct ksg_pod_ext {
 } ksg_pod_ext;
 
 /* Enable extensions; call before ksg_set_cluster (KSG_ERR_ARG for a sharded
- * context, weights outside the int32 score bound, n_scalar > KSG_MAX_SCALAR). */
+ * context, n_scalar > KSG_MAX_SCALAR). */
 int ksg_set_extensions(ksg_ctx* ctx, const ksg_ext_config* ext);
 /* Per node, after ksg_set_cluster: scalar_cap[r * n_nodes + n] = allocatable of
  * resource r (0: none), node n's taint ids taint_ids[taint_off[n], + taint_n[n]).

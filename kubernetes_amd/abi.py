@@ -50,10 +50,10 @@ FAIL_TAINTS = 8
 FAIL_SCALAR = 9
 MAX_SCALAR = 4
 
-MAX_ANTI = 4
-MAX_LABEL_PREF = 8
-MAX_PRESENCE = 8
-MAX_PRESENCE_KEYS = 8
+MAX_ANTI = 16
+MAX_LABEL_PREF = 32
+MAX_PRESENCE = 16
+MAX_PRESENCE_KEYS = 16
 MAX_AFF = 4
 MAX_AFF_GROUPS = 8
 PAIR_INVALID = 0x80000000  # pair_keys flag: SelectorFromSet rejects the (key, value)
@@ -69,16 +69,16 @@ class KsgConfig(C.Structure):
     _fields_ = [
         ("predicates", U32),
         ("n_priority_configs", U32),
-        ("w_least_requested", I32),
-        ("w_service_spreading", I32),
-        ("w_equal", I32),
+        ("w_least_requested", I64),
+        ("w_service_spreading", I64),
+        ("w_equal", I64),
         ("n_anti", U32),
         ("anti_key", U32 * MAX_ANTI),
-        ("w_anti", I32 * MAX_ANTI),
+        ("w_anti", I64 * MAX_ANTI),
         ("n_label_pref", U32),
         ("pref_key", U32 * MAX_LABEL_PREF),
         ("pref_presence", U32 * MAX_LABEL_PREF),
-        ("w_pref", I32 * MAX_LABEL_PREF),
+        ("w_pref", I64 * MAX_LABEL_PREF),
         ("n_presence", U32),
         ("presence_n_keys", U32 * MAX_PRESENCE),
         ("presence_keys", (U32 * MAX_PRESENCE_KEYS) * MAX_PRESENCE),

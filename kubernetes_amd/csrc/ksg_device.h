@@ -85,6 +85,10 @@ __device__ __forceinline__ int64_t frac10_f32(int64_t num, int64_t den) {
   return (int64_t)s;
 }
 
+// Go's int arithmetic wraps (two's complement); so do these
+__host__ __device__ __forceinline__ int64_t wsum(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+__host__ __device__ __forceinline__ int64_t wmul(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
+
 __device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
@@ -401,21 +405,22 @@ __device__ __forceinline__ int64_t node_score(const KsgDev& d, const PodCtx& c, 
                                               int64_t capc, int64_t capm, int64_t usedc,
                                               int64_t usedm, int32_t cnt) {
   if (d.equal_fallback) return 1;  // EqualPriority (generic_scheduler.go:141-143,180-195)
+  // combinedScores[host] += score * weight (generic_scheduler.go:145-159), Go int: wrapping
   int64_t s = 0;
-  if (d.has_static_score) s += d.static_score[n];
+  if (d.has_static_score) s = d.static_score[n];
   if (d.w_lr) {  // calculateOccupancy (priorities.go:43-76): all pods on node + this pod
     const int64_t tc = (int64_t)((uint64_t)usedc + (uint64_t)c.req_cpu);
     const int64_t tm = (int64_t)((uint64_t)usedm + (uint64_t)c.req_mem);
-    s += (int64_t)d.w_lr * ((lr_calc(tc, capc) + lr_calc(tm, capm)) / 2);
+    s = wsum(s, wmul(d.w_lr, (lr_calc(tc, capc) + lr_calc(tm, capm)) / 2));
   }
   if (d.w_spread) {  // CalculateSpreadPriority (spreading.go:72-86)
     const int64_t sc = c.spread_max > 0 ? frac10_f32((int64_t)c.spread_max - cnt, c.spread_max) : 10;
-    s += (int64_t)d.w_spread * sc;
+    s = wsum(s, wmul(d.w_spread, sc));
   }
   if (d.w_bal) {  // extension: BalancedResourceAllocation
     const int64_t tc = (int64_t)((uint64_t)usedc + (uint64_t)c.req_cpu);
     const int64_t tm = (int64_t)((uint64_t)usedm + (uint64_t)c.req_mem);
-    s += (int64_t)d.w_bal * balanced_score(tc, capc, tm, capm);
+    s = wsum(s, wmul(d.w_bal, balanced_score(tc, capc, tm, capm)));
   }
   return s;
 }
@@ -430,7 +435,7 @@ __device__ __forceinline__ int64_t anti_term(const KsgDev& d, const PodCtx& c, u
       const int64_t tot = c.svc_total;
       sc = tot > 0 ? frac10_f32(tot - dcount[d.anti_dom_off[a] + dom], tot) : 10;
     }
-    s += (int64_t)d.w_anti[a] * sc;
+    s = wsum(s, wmul(d.w_anti[a], sc));
   }
   return s;
 }
@@ -464,6 +469,7 @@ __device__ __forceinline__ void commit_pod_wave(const KsgDev& d, const ksg_pod& 
     const uint32_t s = ids[p.svcs_off + i];
     const int32_t old = __hip_atomic_fetch_add(d.svc_cnt + (size_t)s * d.n_nodes + w, 1, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_or(d.svc_bits + (size_t)s * d.nw + wi, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_fetch_max(d.svc_max + s, old + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_fetch_add(d.svc_total + s, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int32_t expect = -1;

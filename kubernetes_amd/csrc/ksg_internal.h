@@ -8,11 +8,12 @@
 //   inv10_cpu[N], inv10_mem[N]    f64     static   10.0 / capacity (window path's LeastRequested)
 //   used_cpu[N], used_mem[N]      int64   mutable  sum of limits of ALL pods on node
 //   static_fit[nw]                uint64  static   AND of LabelsPresence predicates
-//   static_score[N]               int32   static   sum of w * score of pod-independent
+//   static_score[N]               int64   static   sum of w * score of pod-independent
 //                                                  priorities (EqualPriority, LabelPreference)
 //   keymap[K][nw]                 uint64  mutable  conflict key (host port / GCE PD) in use
 //   pairmap[P][nw]                uint64  static   node carries label pair p (p=0: empty)
 //   svc_cnt[S][N]                 int32   mutable  pods matching service s on node
+//   svc_bits[S][nw]               uint64  mutable  svc_cnt[s][n] > 0
 //   svc_max[S], svc_total[S]      int32   mutable  ServiceSpreading maxCount / #pods
 //   svc_peer[S]                   int32   mutable  first service peer's node (-1 none,
 //                                                  -2 not a known node)
@@ -35,9 +36,12 @@
 // score sentinels for nodes that do not fit (int64 records / int32 LDS scores)
 #define KSG_SCORE_NONE (-0x7fffffffffffffffLL - 1)
 #define KSG_S32_NONE ((int32_t)0x80000000)
-// combined scores are kept in int32 on the device; the host rejects weight
-// sets whose |score| could reach this bound
+// combined scores: int32 on the window path, which the host takes only while no
+// |score| can reach this bound (and at most KSG_WIN_MAX_ANTI anti-affinity
+// priorities carry a weight); int64 and wrapping like Go's int on the exact
+// kernels otherwise (KsgDev.wide)
 #define KSG_SCORE_BOUND (1LL << 30)
+#define KSG_WIN_MAX_ANTI 4
 // largest capacity / requested total the window path accepts (lr_win's bound,
 // ksg_device.h)
 #define KSG_WIN_LR_BOUND (1LL << 49)
@@ -50,9 +54,9 @@ struct KsgDev {
   uint32_t n_pairs, n_services, max_keys, n_domains_total;
   // config (compiled)
   uint32_t preds;
-  int32_t w_lr, w_spread;
+  int64_t w_lr, w_spread;
   uint32_t n_anti;
-  int32_t w_anti[KSG_MAX_ANTI];
+  int64_t w_anti[KSG_MAX_ANTI];
   uint32_t anti_dom_off[KSG_MAX_ANTI];
   uint32_t n_aff;
   uint32_t n_aff_groups;      // ServiceAffinity predicates (>= 1 when n_aff > 0)
@@ -62,6 +66,7 @@ struct KsgDev {
   int32_t has_static_score;
   int32_t has_static_fit;
   int32_t dbg;                // debug switches (KSG_DEBUG env), 0 in production
+  int32_t wide;               // int64 combined scores (exact kernels only)
   uint32_t rr_dz;             // ServiceAntiAffinity re-rank: domain rows (0: off; ksg_window.hip)
   int32_t* dbgbuf;            // KSG_DEBUG & 4: per-pod resolver trace
   // arrays
@@ -72,16 +77,18 @@ struct KsgDev {
   int64_t* used_cpu;
   int64_t* used_mem;
   const uint64_t* static_fit;
-  const int32_t* static_score;
+  const int64_t* static_score;
   uint64_t* keymap;
   const uint64_t* pairmap;
   int32_t* svc_cnt;
+  uint64_t* svc_bits;         // [S][nw] node holds pods of service s (svc_cnt > 0): phase A
+                              // loads a count only where its bit is set
   int32_t* svc_max;
   int32_t* svc_total;
   int32_t* svc_peer;
   const int32_t* anti_domain;
   const int32_t* aff_pair;
-  int32_t* score_scratch;     // exact kernels with R > KSG_R_LDS: per-node scores in HBM, not LDS
+  void* score_scratch;        // exact kernels with R > the LDS bound: per-node scores in HBM, not LDS
   // extensions beyond the reference (ksg_set_extensions; exact kernels only, parity unpinned)
   uint32_t ext_filters;       // KSG_EXT_*
   int32_t w_taint, w_bal;     // TaintTolerationPriority, BalancedResourceAllocation weights
@@ -101,8 +108,8 @@ struct KsgStaticCfg {
   uint32_t n_pref;
   uint32_t pref_key[KSG_MAX_LABEL_PREF];
   uint32_t pref_presence[KSG_MAX_LABEL_PREF];
-  int32_t w_pref[KSG_MAX_LABEL_PREF];
-  int32_t w_equal;
+  int64_t w_pref[KSG_MAX_LABEL_PREF];
+  int64_t w_equal;
   uint32_t n_anti;
   uint32_t anti_key[KSG_MAX_ANTI];
   uint32_t n_aff;
@@ -163,6 +170,10 @@ struct KsgWinXchg {
   // the bitmap of filtered nodes at their row's best (uint64[wcap][ostride] at
   // b_off); zmap = uint64[dz][nw], the nodes of each domain row. The resolver
   // resets dmb to KSG_S32_NONE for the next window.
+  // the plain resolver (no ServiceAntiAffinity): per window pod, its T0 image
+  // (ksg_plain.hip, ksg_win_t0_kernel) at img + pod * img_stride
+  uint8_t* img;
+  uint32_t img_stride;
   uint32_t rr;        // re-rank on (else a service's commit ends the window)
   uint32_t dz;        // domain rows: anti domains + 1 (<= KSG_RR_MAXZ)
   uint32_t b_off;     // byte offset in a block of the best-per-domain bitmaps

@@ -32,28 +32,49 @@
 // totals (REG, R <= 4). The filter+score of node n is evaluated once per pod.
 // ============================================================================
 
+// Combined-score type SC: int32 while every |score| stays below
+// KSG_SCORE_BOUND; int64 wrapping like Go's int otherwise (KsgDev.wide: weights
+// the reference accepts up to int64, generic_scheduler.go:145-159).
+template <typename SC>
+struct ScoreT;
+template <>
+struct ScoreT<int32_t> {
+  static constexpr int32_t none = KSG_S32_NONE;
+  static constexpr int r_lds = KSG_R_LDS;  // nodes per thread whose scores fit the LDS
+  static __device__ __forceinline__ int32_t wave_max(int32_t v) { return wave_max_i32(v); }
+  static __device__ __forceinline__ int32_t add(int32_t a, int64_t b) { return a + (int32_t)b; }
+};
+template <>
+struct ScoreT<int64_t> {
+  static constexpr int64_t none = KSG_SCORE_NONE;
+  static constexpr int r_lds = KSG_R_LDS / 2;
+  static __device__ __forceinline__ int64_t wave_max(int64_t v) { return wave_max_i64(v); }
+  static __device__ __forceinline__ int64_t add(int64_t a, int64_t b) { return wsum(a, b); }
+};
+
 // Filter + score every node of the shard into s_score; returns this thread's max.
 // With ANTI the ServiceAntiAffinity term is added after the domain counts are
 // complete (one extra barrier).
-template <int R, bool ANTI, bool REG>
-__device__ __forceinline__ int32_t scan_pod(const KsgDev& d, const PodCtx& c, uint32_t tid, uint32_t wave,
-                                            uint64_t bit, int32_t* s_score, int32_t* s_dcount,
-                                            const int32_t* dglobal, const int64_t* rcapc, const int64_t* rcapm,
-                                            const int64_t* rusedc, const int64_t* rusedm,
-                                            uint8_t* fail_out, int32_t* s_tmax = nullptr) {
+template <int R, bool ANTI, bool REG, typename SC>
+__device__ __forceinline__ SC scan_pod(const KsgDev& d, const PodCtx& c, uint32_t tid, uint32_t wave,
+                                       uint64_t bit, SC* s_score, int32_t* s_dcount,
+                                       const int32_t* dglobal, const int64_t* rcapc, const int64_t* rcapm,
+                                       const int64_t* rusedc, const int64_t* rusedm,
+                                       uint8_t* fail_out, int32_t* s_tmax = nullptr) {
+  using T = ScoreT<SC>;
   const bool need_cnt = (d.w_spread != 0 || ANTI) && c.svc >= 0;
   // extension TaintTolerationPriority: normalised by the max over the filtered
   // nodes, so it is added in a second pass like the anti-affinity term
   // (s_tmax: zeroed by the caller before the barrier that precedes this scan)
   const bool tt = d.w_taint != 0 && c.ext != nullptr && s_tmax != nullptr && !d.equal_fallback;
   int32_t tmax = 0;
-  int32_t m = KSG_S32_NONE;
+  SC m = T::none;
   // register-cached node state needs compile-time j; otherwise keep the loop rolled
 #pragma unroll REG ? R : 1
   for (int j = 0; j < R; ++j) {
     const uint32_t n = d.lo + j * KSG_NT + tid;
     const uint32_t wi = (d.lo >> 6) + j * KSG_NWAVE + wave;
-    int32_t sc = KSG_S32_NONE;
+    SC sc = T::none;
     if (n < d.hi) {
       int64_t capc, capm, usedc, usedm;
       if constexpr (REG) {
@@ -66,7 +87,7 @@ __device__ __forceinline__ int32_t scan_pod(const KsgDev& d, const PodCtx& c, ui
       const int f = node_fail(d, c, n, wi, bit, capc, capm, usedc, usedm);
       if (fail_out) fail_out[n - d.lo] = (uint8_t)f;
       if (f == KSG_FAIL_NONE) {
-        sc = (int32_t)node_score(d, c, n, capc, capm, usedc, usedm, cnt);
+        sc = (SC)node_score(d, c, n, capc, capm, usedc, usedm, cnt);
         if (tt) tmax = max(tmax, soft_taints(d, c, wi, bit));
         if (ANTI && s_dcount && cnt != 0) {
           for (uint32_t a = 0; a < d.n_anti; ++a) {
@@ -89,12 +110,12 @@ __device__ __forceinline__ int32_t scan_pod(const KsgDev& d, const PodCtx& c, ui
     const int32_t tm = tt ? *s_tmax : 0;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-      int32_t v = s_score[j * KSG_NT + tid];
-      if (v != KSG_S32_NONE && !d.equal_fallback) {
-        if (ANTI) v += (int32_t)anti_term(d, c, d.lo + j * KSG_NT + tid, dc);
+      SC v = s_score[j * KSG_NT + tid];
+      if (v != T::none && !d.equal_fallback) {
+        if (ANTI) v = T::add(v, anti_term(d, c, d.lo + j * KSG_NT + tid, dc));
         if (tt) {
           const uint32_t wi = (d.lo >> 6) + j * KSG_NWAVE + wave;
-          v += (int32_t)((int64_t)d.w_taint * taint_score(soft_taints(d, c, wi, bit), tm));
+          v = T::add(v, (int64_t)d.w_taint * taint_score(soft_taints(d, c, wi, bit), tm));
         }
         s_score[j * KSG_NT + tid] = v;
       }
@@ -105,21 +126,22 @@ __device__ __forceinline__ int32_t scan_pod(const KsgDev& d, const PodCtx& c, ui
 }
 
 // Block max of the per-thread maxima, then tie ballots into s_tie and the tie count.
-template <int R>
-__device__ __forceinline__ void reduce_ties(const KsgDev& d, int32_t m, uint32_t tid, uint32_t lane, uint32_t wave,
-                                            const int32_t* s_score, int32_t* s_wmax, uint32_t* s_wcnt,
-                                            uint64_t* s_tie, int32_t& M, uint64_t& k) {
-  m = wave_max_i32(m);
+template <int R, typename SC>
+__device__ __forceinline__ void reduce_ties(const KsgDev& d, SC m, uint32_t tid, uint32_t lane, uint32_t wave,
+                                            const SC* s_score, SC* s_wmax, uint32_t* s_wcnt,
+                                            uint64_t* s_tie, SC& M, uint64_t& k) {
+  using T = ScoreT<SC>;
+  m = T::wave_max(m);
   if (lane == 0) s_wmax[wave] = m;
   __syncthreads();
   M = s_wmax[0];
 #pragma unroll
   for (int w = 1; w < KSG_NWAVE; ++w) M = s_wmax[w] > M ? s_wmax[w] : M;
-  if (d.empty_priorities) M = KSG_S32_NONE;  // all weights 0: empty HostPriorityList
+  if (d.empty_priorities) M = T::none;  // all weights 0: empty HostPriorityList
   uint32_t wc = 0;
 #pragma unroll
   for (int j = 0; j < R; ++j) {
-    const uint64_t b = __ballot(M != KSG_S32_NONE && s_score[j * KSG_NT + tid] == M);
+    const uint64_t b = __ballot(M != T::none && s_score[j * KSG_NT + tid] == M);
     if (lane == 0) s_tie[j * KSG_NWAVE + wave] = b;
     wc += __popcll(b);
   }
@@ -153,7 +175,7 @@ __device__ __forceinline__ int32_t select_tie(const uint64_t* words, uint32_t nw
   return -1;
 }
 
-template <int R, bool ANTI, bool REG>
+template <int R, bool ANTI, bool REG, typename SC>
 __global__ __launch_bounds__(KSG_NT) void ksg_batch_kernel(KsgDev d, const ksg_pod* __restrict__ pods,
                                                           const uint32_t* __restrict__ ids,
                                                           uint32_t n_pods, uint64_t* rng_io,
@@ -162,11 +184,12 @@ __global__ __launch_bounds__(KSG_NT) void ksg_batch_kernel(KsgDev d, const ksg_p
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // per-node scores: LDS up to KSG_R_LDS nodes per thread, else HBM scratch
   // (each thread only ever reads back its own entries)
-  int32_t* s_score = R > KSG_R_LDS ? d.score_scratch : reinterpret_cast<int32_t*>(smem);
-  int32_t* s_dcount = R > KSG_R_LDS ? reinterpret_cast<int32_t*>(smem) : s_score + R * KSG_NT;
+  using T = ScoreT<SC>;
+  SC* s_score = R > T::r_lds ? reinterpret_cast<SC*>(d.score_scratch) : reinterpret_cast<SC*>(smem);
+  int32_t* s_dcount = R > T::r_lds ? reinterpret_cast<int32_t*>(smem) : reinterpret_cast<int32_t*>(s_score + R * KSG_NT);
   int32_t* s_tmax = s_dcount + d.n_domains_total;  // (extension TaintTolerationPriority's max)
   __shared__ uint64_t s_tie[R * KSG_NWAVE];
-  __shared__ int32_t s_wmax[KSG_NWAVE];
+  __shared__ SC s_wmax[KSG_NWAVE];
   __shared__ uint32_t s_wcnt[KSG_NWAVE];
   __shared__ int32_t s_winner;
 
@@ -203,12 +226,12 @@ __global__ __launch_bounds__(KSG_NT) void ksg_batch_kernel(KsgDev d, const ksg_p
       if (tid == 0) *s_tmax = 0;
       __syncthreads();
     }
-    const int32_t m = scan_pod<R, ANTI, REG>(d, c, tid, wave, bit, s_score, s_dcount, nullptr, rcapc, rcapm,
-                                             rusedc, rusedm, nullptr, exts ? s_tmax : nullptr);
-    int32_t M;
+    const SC m = scan_pod<R, ANTI, REG, SC>(d, c, tid, wave, bit, s_score, s_dcount, nullptr, rcapc, rcapm,
+                                            rusedc, rusedm, nullptr, exts ? s_tmax : nullptr);
+    SC M;
     uint64_t k;
-    reduce_ties<R>(d, m, tid, lane, wave, s_score, s_wmax, s_wcnt, s_tie, M, k);
-    if (M == KSG_S32_NONE || k == 0) {
+    reduce_ties<R, SC>(d, m, tid, lane, wave, s_score, s_wmax, s_wcnt, s_tie, M, k);
+    if (M == T::none || k == 0) {
       if (tid == 0) out[i] = KSG_OUT_NOFIT;  // *FitError: no rand draw
       __syncthreads();
       continue;
@@ -247,7 +270,7 @@ __global__ __launch_bounds__(KSG_NT) void ksg_batch_kernel(KsgDev d, const ksg_p
 // (partial over this shard, written to dpart); phase 2: complete pass with
 // all-reduced domain counts read from dglobal.
 // ============================================================================
-template <int R, bool ANTI>
+template <int R, bool ANTI, typename SC>
 __global__ __launch_bounds__(KSG_NT) void ksg_scan_kernel(KsgDev d, const ksg_pod* __restrict__ pods,
                                                          const uint32_t* __restrict__ ids, int mode,
                                                          int phase, uint8_t* __restrict__ fail_out,
@@ -259,11 +282,12 @@ __global__ __launch_bounds__(KSG_NT) void ksg_scan_kernel(KsgDev d, const ksg_po
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // per-node scores: LDS up to KSG_R_LDS nodes per thread, else HBM scratch
   // (each thread only ever reads back its own entries)
-  int32_t* s_score = R > KSG_R_LDS ? d.score_scratch : reinterpret_cast<int32_t*>(smem);
-  int32_t* s_dcount = R > KSG_R_LDS ? reinterpret_cast<int32_t*>(smem) : s_score + R * KSG_NT;
+  using T = ScoreT<SC>;
+  SC* s_score = R > T::r_lds ? reinterpret_cast<SC*>(d.score_scratch) : reinterpret_cast<SC*>(smem);
+  int32_t* s_dcount = R > T::r_lds ? reinterpret_cast<int32_t*>(smem) : reinterpret_cast<int32_t*>(s_score + R * KSG_NT);
   int32_t* s_tmax = s_dcount + d.n_domains_total;  // (extension TaintTolerationPriority's max)
   __shared__ uint64_t s_tie[R * KSG_NWAVE];
-  __shared__ int32_t s_wmax[KSG_NWAVE];
+  __shared__ SC s_wmax[KSG_NWAVE];
   __shared__ uint32_t s_wcnt[KSG_NWAVE];
 
   const uint32_t tid = threadIdx.x;
@@ -295,13 +319,13 @@ __global__ __launch_bounds__(KSG_NT) void ksg_scan_kernel(KsgDev d, const ksg_po
   }
   if (ANTI && phase == 1) {
     // domain counts only (the sharded all-reduce needs them before any score)
-    scan_pod<R, false, false>(d, c, tid, wave, bit, s_score, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                              nullptr);
+    scan_pod<R, false, false, SC>(d, c, tid, wave, bit, s_score, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                  nullptr);
     const bool need = c.svc >= 0;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const uint32_t n = d.lo + j * KSG_NT + tid;
-      if (need && n < d.hi && s_score[j * KSG_NT + tid] != KSG_S32_NONE) {
+      if (need && n < d.hi && s_score[j * KSG_NT + tid] != T::none) {
         const int32_t cnt = ld_mut(d.svc_cnt + (size_t)c.svc * d.n_nodes + n);
         if (cnt)
           for (uint32_t a = 0; a < d.n_anti; ++a) {
@@ -314,24 +338,27 @@ __global__ __launch_bounds__(KSG_NT) void ksg_scan_kernel(KsgDev d, const ksg_po
     for (uint32_t k = tid; k < d.n_domains_total; k += KSG_NT) dpart[k] = s_dcount[k];
     return;
   }
-  const int32_t m = scan_pod<R, ANTI, false>(d, c, tid, wave, bit, s_score, lds_dcount ? s_dcount : nullptr,
-                                             phase == 2 ? dglobal : nullptr, nullptr, nullptr, nullptr, nullptr,
-                                             fail_out, ext ? s_tmax : nullptr);
+  const SC m = scan_pod<R, ANTI, false, SC>(d, c, tid, wave, bit, s_score, lds_dcount ? s_dcount : nullptr,
+                                            phase == 2 ? dglobal : nullptr, nullptr, nullptr, nullptr, nullptr,
+                                            fail_out, ext ? s_tmax : nullptr);
   if (mode == KSG_MODE_EVAL) {
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const uint32_t n = d.lo + j * KSG_NT + tid;
-      if (n < d.hi) score_out[n - d.lo] = s_score[j * KSG_NT + tid];
+      if (n < d.hi) {
+        const SC v = s_score[j * KSG_NT + tid];
+        score_out[n - d.lo] = v == T::none ? KSG_SCORE_NONE : (int64_t)v;
+      }
     }
     return;
   }
-  int32_t M;
+  SC M;
   uint64_t k;
-  reduce_ties<R>(d, m, tid, lane, wave, s_score, s_wmax, s_wcnt, s_tie, M, k);
+  reduce_ties<R, SC>(d, m, tid, lane, wave, s_score, s_wmax, s_wcnt, s_tie, M, k);
   for (uint32_t w = tid; w < d.nwords; w += KSG_NT) words[w] = s_tie[w];
   if (tid == 0) {
-    hdr->max_score = M == KSG_S32_NONE ? KSG_SCORE_NONE : (int64_t)M;
-    hdr->tie_count = M == KSG_S32_NONE ? 0 : k;
+    hdr->max_score = M == T::none ? KSG_SCORE_NONE : (int64_t)M;
+    hdr->tie_count = M == T::none ? 0 : k;
     hdr->error = 0;
   }
 }
@@ -424,10 +451,10 @@ __global__ void ksg_static_kernel(KsgStaticCfg sc, uint32_t n_nodes, const ksg_n
                                   const uint32_t* __restrict__ pair_keys,
                                   const int32_t* __restrict__ dom_of_pair,  // [n_anti][n_pairs]
                                   uint32_t n_pairs, uint32_t nw, uint64_t* static_fit,
-                                  int32_t* static_score, int32_t* anti_domain, int32_t* aff_pair) {
+                                  int64_t* static_score, int32_t* anti_domain, int32_t* aff_pair) {
   const uint32_t n = blockIdx.x * blockDim.x + threadIdx.x;
   bool fits = true;
-  int32_t score = 0;
+  int64_t score = 0;
   if (n < n_nodes) {
     const uint32_t* pairs = node_pairs + nodes[n].label_off;
     const uint32_t np = nodes[n].n_labels;
@@ -441,7 +468,7 @@ __global__ void ksg_static_kernel(KsgStaticCfg sc, uint32_t n_nodes, const ksg_n
     for (uint32_t q = 0; q < sc.n_pref; ++q) {
       const bool exists = node_has_key(pairs, np, pair_keys, sc.pref_key[q]);
       const bool ok = (exists && sc.pref_presence[q]) || (!exists && !sc.pref_presence[q]);
-      score += sc.w_pref[q] * (ok ? 10 : 0);
+      score = wsum(score, wmul(sc.w_pref[q], ok ? 10 : 0));
     }
     static_score[n] = score;
     for (uint32_t a = 0; a < sc.n_anti; ++a) {
@@ -503,9 +530,10 @@ __global__ void ksg_patch_kernel(const KsgPatch* __restrict__ patches, uint32_t 
 }
 
 // ---- launch wrappers (called from ksg_runtime.cpp) ------------------------
-// dynamic LDS = R*1024 int32 scores + the anti-affinity domain counts
+// dynamic LDS = R*1024 scores + the anti-affinity domain counts
+template <typename SC>
 static size_t lds_bytes(int R, const KsgDev& d) {
-  return (R > KSG_R_LDS ? 0 : (size_t)R * KSG_NT * sizeof(int32_t)) + (size_t)d.n_domains_total * sizeof(int32_t) +
+  return (R > ScoreT<SC>::r_lds ? 0 : (size_t)R * KSG_NT * sizeof(SC)) + (size_t)d.n_domains_total * sizeof(int32_t) +
          16;  // + TaintTolerationPriority's max (extension)
 }
 
@@ -519,10 +547,17 @@ static void allow_big_lds(K kernel) {
 template <int R, bool ANTI, bool REG>
 static hipError_t launch_batch_t(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids, uint32_t n,
                                  uint64_t* rng, int32_t* out, const ksg_pod_ext* ext, hipStream_t st) {
-  static bool once = (allow_big_lds(ksg_batch_kernel<R, ANTI, REG>), true);
+  if (d.wide) {
+    static bool once64 = (allow_big_lds(ksg_batch_kernel<R, ANTI, REG, int64_t>), true);
+    (void)once64;
+    hipLaunchKernelGGL((ksg_batch_kernel<R, ANTI, REG, int64_t>), dim3(1), dim3(KSG_NT), lds_bytes<int64_t>(R, d), st,
+                       d, pods, ids, n, rng, out, ext);
+    return hipGetLastError();
+  }
+  static bool once = (allow_big_lds(ksg_batch_kernel<R, ANTI, REG, int32_t>), true);
   (void)once;
-  hipLaunchKernelGGL((ksg_batch_kernel<R, ANTI, REG>), dim3(1), dim3(KSG_NT), lds_bytes(R, d), st, d, pods, ids,
-                     n, rng, out, ext);
+  hipLaunchKernelGGL((ksg_batch_kernel<R, ANTI, REG, int32_t>), dim3(1), dim3(KSG_NT), lds_bytes<int32_t>(R, d), st, d,
+                     pods, ids, n, rng, out, ext);
   return hipGetLastError();
 }
 
@@ -546,10 +581,17 @@ template <int R, bool ANTI>
 static hipError_t launch_scan_t(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids, int mode, int phase,
                                 uint8_t* fail_out, int64_t* score_out, uint8_t* record, int32_t* dpart,
                                 const int32_t* dglobal, const ksg_pod_ext* ext, hipStream_t st) {
-  static bool once = (allow_big_lds(ksg_scan_kernel<R, ANTI>), true);
+  if (d.wide) {
+    static bool once64 = (allow_big_lds(ksg_scan_kernel<R, ANTI, int64_t>), true);
+    (void)once64;
+    hipLaunchKernelGGL((ksg_scan_kernel<R, ANTI, int64_t>), dim3(1), dim3(KSG_NT), lds_bytes<int64_t>(R, d), st, d,
+                       pods, ids, mode, phase, fail_out, score_out, record, dpart, dglobal, ext);
+    return hipGetLastError();
+  }
+  static bool once = (allow_big_lds(ksg_scan_kernel<R, ANTI, int32_t>), true);
   (void)once;
-  hipLaunchKernelGGL((ksg_scan_kernel<R, ANTI>), dim3(1), dim3(KSG_NT), lds_bytes(R, d), st, d, pods, ids, mode,
-                     phase, fail_out, score_out, record, dpart, dglobal, ext);
+  hipLaunchKernelGGL((ksg_scan_kernel<R, ANTI, int32_t>), dim3(1), dim3(KSG_NT), lds_bytes<int32_t>(R, d), st, d, pods,
+                     ids, mode, phase, fail_out, score_out, record, dpart, dglobal, ext);
   return hipGetLastError();
 }
 
@@ -597,7 +639,7 @@ hipError_t ksg_launch_decide(const KsgDev& d, const ksg_pod* pods, const uint32_
 hipError_t ksg_launch_static(const KsgStaticCfg& sc, uint32_t n_nodes, const ksg_node* nodes,
                              const uint32_t* node_pairs, const uint32_t* pair_keys,
                              const int32_t* dom_of_pair, uint32_t n_pairs, uint32_t nw,
-                             uint64_t* static_fit, int32_t* static_score, int32_t* anti_domain,
+                             uint64_t* static_fit, int64_t* static_score, int32_t* anti_domain,
                              int32_t* aff_pair, unsigned long long* pairmap, hipStream_t st) {
   const uint32_t blocks = (n_nodes + 255) / 256;
   if (blocks == 0) return hipSuccess;

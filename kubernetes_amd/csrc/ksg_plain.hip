@@ -139,6 +139,94 @@ __host__ __device__ inline PlLdsOff plain_lds_offsets(uint32_t P, uint32_t nflag
   return o;
 }
 
+// ---------------------------------------------------------------------------
+// T0 images: per window pod, T0 by word and its prefix counts, built in parallel
+// (one workgroup per pod) between phase A and the resolver, so a producer only
+// copies the image into its ring entry
+// ---------------------------------------------------------------------------
+// image of one pod at img + pod * stride: t0 uint64[P*64] (word q*64 + l), wp
+// uint16[P*64] (T0 bits below the word in its row), lp uint32[32][2] (per row:
+// T0 bits below it, up to its end), hdr int32 {m0, k0}
+__host__ __device__ constexpr uint32_t t0img_wp(uint32_t P) { return P * 64 * 8; }
+__host__ __device__ constexpr uint32_t t0img_lp(uint32_t P) { return P * 64 * 10; }
+__host__ __device__ constexpr uint32_t t0img_hdr(uint32_t P) { return P * 64 * 10 + 256; }
+__host__ __device__ constexpr uint32_t t0img_stride(uint32_t P) { return (P * 64 * 10 + 256 + 16 + 255) & ~255u; }
+
+// byte offsets of word w's best-score bitmap and best score in the (gathered)
+// phase-A blocks (KsgWinXchg), ~0u: no such word
+__device__ __forceinline__ void xchg_word_at(const KsgWinXchg& x, uint32_t nwords, uint32_t w, uint32_t& b_at,
+                                             uint32_t& m_at) {
+  uint32_t g = 0;
+  for (uint32_t r = 1; r < x.world; ++r)
+    if (w >= x.wlo[r] && x.nw[r] > 0) g = r;
+  const uint32_t i = w - x.wlo[g];
+  const bool ok = w < nwords && i < x.nw[g];
+  const uint32_t base = (uint32_t)(g * x.blk);
+  b_at = ok ? base + i * 8 : ~0u;
+  m_at = ok ? base + x.wcap * x.ostride * 8 + i * 4 : ~0u;
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void ksg_win_t0_kernel(uint32_t nwords, uint32_t wcap, const KsgWinRun* run,
+                                                         const KsgWinXchg x) {
+  __shared__ int32_t s_max[4];
+  __shared__ uint32_t s_tot[32];
+  const uint32_t pos = run->pos, n_batch = run->n;
+  if (run->halt || pos >= n_batch) return;
+  const uint32_t j = blockIdx.x;
+  if (j >= min(wcap, n_batch - pos)) return;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr uint32_t RPW = (P + 3) / 4;  // rows per wave
+  uint64_t t0[RPW];
+  int32_t mw[RPW];
+  int32_t lm = KSG_S32_NONE;
+#pragma unroll
+  for (uint32_t k = 0; k < RPW; ++k) {
+    const uint32_t q = wave + 4 * k;
+    uint32_t b_at = ~0u, m_at = ~0u;
+    if (q < P) xchg_word_at(x, nwords, q * 64 + lane, b_at, m_at);
+    t0[k] = b_at != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + b_at + (size_t)j * x.ostride * 8) : 0ULL;
+    mw[k] = m_at != ~0u ? *reinterpret_cast<const int32_t*>(x.buf + m_at + (size_t)j * x.ostride * 4) : KSG_S32_NONE;
+    lm = mw[k] > lm ? mw[k] : lm;
+  }
+  lm = wave_total_max(lm);
+  if (lane == 0) s_max[wave] = lm;
+  __syncthreads();
+  const int32_t m0 = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
+  uint8_t* im = x.img + (size_t)j * x.img_stride;
+  uint64_t* it0 = reinterpret_cast<uint64_t*>(im);
+  uint16_t* iwp = reinterpret_cast<uint16_t*>(im + t0img_wp(P));
+#pragma unroll
+  for (uint32_t k = 0; k < RPW; ++k) {
+    const uint32_t q = wave + 4 * k;
+    if (q >= P) break;  // (wave-uniform)
+    const uint64_t w = (m0 != KSG_S32_NONE && mw[k] == m0) ? t0[k] : 0ULL;
+    const uint32_t c1 = (uint32_t)__popcll(w);
+    const uint32_t in1 = dpp_scan_add(c1);
+    it0[q * 64 + lane] = w;
+    iwp[q * 64 + lane] = (uint16_t)(in1 - c1);
+    if (lane == 63) s_tot[q] = in1;
+  }
+  __syncthreads();
+  if (wave == 0) {  // row prefixes, k0, m0
+    const uint32_t tot = lane < P ? s_tot[lane] : 0u;
+    const uint32_t in1 = dpp_scan_add(tot);
+    // (the cross-lane read stays outside the lane-0 branch: inside it, only
+    // lane 0 would be active for the scan the compiler may sink there)
+    const int32_t k0 = __builtin_amdgcn_readlane((int)in1, 63);
+    uint32_t* ilp = reinterpret_cast<uint32_t*>(im + t0img_lp(P));
+    if (lane < P) {
+      ilp[lane * 2] = in1 - tot;
+      ilp[lane * 2 + 1] = in1;
+    }
+    if (lane == 0) {
+      int32_t* ih = reinterpret_cast<int32_t*>(im + t0img_hdr(P));
+      ih[0] = m0;
+      ih[1] = k0;
+    }
+  }
+}
+
 template <int P, bool STAMP>
 __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
                                                             const KsgWinSum* __restrict__ sums, const KsgWinXchg x,
@@ -152,7 +240,6 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   const uint32_t lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t nflag = (d.n_services + 31) / 32;
-  const uint32_t nwords = d.nwords;
   constexpr uint32_t RING = win2_ring(P, false);
   constexpr uint32_t NT = 512;
   constexpr uint32_t NPW = NT / 64 - KSG_RES_P0;  // producer waves
@@ -211,22 +298,6 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   // =========================================================================
   if (wave >= KSG_RES_P0) {
     const uint32_t* recs = reinterpret_cast<const uint32_t*>(sums);
-    // lane l holds words q*64 + l: byte offsets of the rank block and row phase
-    // A wrote them at (~0u = no such word); coalesced loads, conflict-free LDS
-    uint32_t wb_at[P], wm_at[P];
-#pragma unroll
-    for (int q = 0; q < P; ++q) {
-      const uint32_t wq = q * 64 + lane;
-      uint32_t g = 0;
-      for (uint32_t r = 1; r < x.world; ++r)
-        if (wq >= x.wlo[r] && x.nw[r] > 0) g = r;
-      const uint32_t i = wq - x.wlo[g];
-      const bool ok = wq < nwords && i < x.nw[g];
-      const uint32_t base = (uint32_t)(g * x.blk);
-      wb_at[q] = ok ? base + i * 8 : ~0u;
-      wm_at[q] = ok ? base + x.wcap * x.ostride * 8 + i * 4 : ~0u;
-    }
-    const uint32_t row_b = x.ostride * 8, row_m = x.ostride * 4;
     uint64_t p_last = 0, p_acc = 0;  // KSG_DEBUG & 8: lanes 24..27 ring wait, loads, draw wait, the rest
     auto pstamp = [&](uint32_t k) {
       if constexpr (STAMP) {
@@ -255,35 +326,38 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       pstamp(24);
       if (skew & 8u) __builtin_amdgcn_s_sleep(8);
       const uint32_t rec = lane < DW ? recs[(size_t)j * DW + lane] : 0u;
-      uint64_t t0[P];
-      int32_t mw[P];
-      int32_t lm = KSG_S32_NONE;
+      // the pod's T0 image into the ring entry: 16-byte loads, all in flight,
+      // then the LDS stores (T0 words, in-row prefixes, row prefixes, m0 / k0)
+      const uint8_t* im = x.img + (size_t)j * x.img_stride;
+      constexpr uint32_t NT0 = P * 64 * 8 / 16, NWP = P * 64 * 2 / 16;  // 16-byte chunks
+      constexpr uint32_t NC = (NT0 + NWP + 63) / 64;
+      uint4 ch[NC];
 #pragma unroll
-      for (int q = 0; q < P; ++q) {
-        t0[q] = wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + j * row_b) : 0ULL;
-        mw[q] = wm_at[q] != ~0u ? *reinterpret_cast<const int32_t*>(x.buf + wm_at[q] + j * row_m) : KSG_S32_NONE;
-        lm = mw[q] > lm ? mw[q] : lm;
+      for (uint32_t k = 0; k < NC; ++k) {
+        const uint32_t t = k * 64 + lane;
+        ch[k] = t < NT0 + NWP ? *reinterpret_cast<const uint4*>(im + (size_t)t * 16) : uint4{0, 0, 0, 0};
       }
-      const int32_t m0 = wave_total_max(lm);
+      const uint32_t lpv = lane < 2 * P ? *reinterpret_cast<const uint32_t*>(im + t0img_lp(P) + lane * 4) : 0u;
+      const int32_t m0 = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int32_t*>(im + t0img_hdr(P)));
+      const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane(*reinterpret_cast<const int32_t*>(im + t0img_hdr(P) + 4));
       const bool drawable = __builtin_amdgcn_readlane(rec, WS_ERR) == 0 && m0 != KSG_S32_NONE;
       const uint32_t wj = j >> 5, bj = 1u << (j & 31);
       if (lane == 0) {  // the drawable bit first, then "known" (readers read them in that order)
         if (drawable) atomicOr(&L_drw[wj], bj);
         atomicOr(&L_pub[wj], bj);
       }
-      // T0 and its prefixes: per row q, the bits below each lane's word (ex_q)
-      // and below the row (rowex[q], wave-uniform)
-      uint32_t ex_q[P], rowex[P];
-      uint32_t k0 = 0;
+      uint4* e_t0 = reinterpret_cast<uint4*>(r_t0 + (size_t)e * P * 64);
+      uint4* e_wp = reinterpret_cast<uint4*>(r_wp + (size_t)e * P * 64);
 #pragma unroll
-      for (int q = 0; q < P; ++q) {
-        t0[q] = (m0 != KSG_S32_NONE && mw[q] == m0) ? t0[q] : 0ULL;
-        const uint32_t c1 = (uint32_t)__popcll(t0[q]);
-        const uint32_t in1 = dpp_scan_add(c1);
-        ex_q[q] = in1 - c1;
-        rowex[q] = k0;
-        k0 += (uint32_t)__builtin_amdgcn_readlane((int)in1, 63);
+      for (uint32_t k = 0; k < NC; ++k) {
+        const uint32_t t = k * 64 + lane;
+        if (t < NT0) e_t0[t] = ch[k];
+        else if (t < NT0 + NWP) e_wp[t - NT0] = ch[k];
       }
+      if (lane < 2 * P) r_lp[e * 64 + lane] = lpv;
+      // (the entry is read back below through other pointer types: no
+      // reordering of those loads above these stores)
+      asm volatile("" ::: "memory");
       pstamp(25);
       // draw index = drawable pods before j (every one of them known)
       uint32_t idx = 0;
@@ -314,8 +388,14 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
                           ((uint32_t)__builtin_amdgcn_readlane(rec, WS_NPP) >> 16);
       const uint32_t n_sel = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NSS) & 0xffff;
       const bool inl = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NINL) <= KSG_WIN_INLINE && n_svcs <= KSG_SLOT_SVCS;
-      // the candidates: ascending T0 positions k0-1-ix0; k0-2-ix1 (+1); k0-3-ix2 (+1, +2)
-      // (lane c < 6 holds candidate c; a lane-indexed array would go to scratch)
+      // the candidates: ascending T0 positions k0-1-ix0; k0-2-ix1 (+1); k0-3-ix2
+      // (+1, +2), found like the committer's select (row prefixes, then the row's
+      // word prefixes, then the bit); lane c < 6 holds candidate c
+      // (shuffles with every lane active: a disabled source lane reads as 0)
+      const uint32_t lpe_ = (uint32_t)__shfl((int)lpv, (int)((2 * lane) & 63), 64);
+      const uint32_t lpi_ = (uint32_t)__shfl((int)lpv, (int)((2 * lane + 1) & 63), 64);
+      const uint32_t lp_ex = lane < P ? lpe_ : 0u, lp_in = lane < P ? lpi_ : 0u;
+      const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
       uint32_t cand_l = ~0u, cand0 = ~0u;
       if (drawable) {
 #pragma unroll
@@ -324,7 +404,33 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           const uint32_t off = c == 0 ? 0u : c < 3 ? (uint32_t)c - 1 : (uint32_t)c - 3;
           if (k0 > dd) {
             const uint32_t ixd = (uint32_t)__builtin_amdgcn_readlane((int)mv, (int)dd);
-            const uint32_t node = select_qmajor<P>(t0, ex_q, rowex, k0 - 1 - dd - ixd + off, lane);
+            const uint32_t tp = k0 - 1 - dd - ixd + off;
+            const uint32_t qs = (uint32_t)__builtin_ctzll(__ballot(lane < P && lp_ex <= tp && tp < lp_in));
+            const uint32_t loc = tp - (uint32_t)__builtin_amdgcn_readlane((int)lp_ex, (int)qs);
+            const uint64_t w = t0e[qs * 64 + lane];
+            const uint32_t wpq = r_wp[(size_t)e * P * 64 + qs * 64 + lane];
+            const uint32_t ls = (uint32_t)__builtin_ctzll(__ballot(wpq <= loc && loc < wpq + (uint32_t)__popcll(w)));
+            const uint64_t ws = readlane64(w, (int)ls);
+            const uint32_t lw = loc - (uint32_t)__builtin_amdgcn_readlane((int)wpq, (int)ls);
+            const uint32_t rank =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(ws >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ws, 0u));
+            uint32_t node = (qs * 64 + ls) * 64 + (uint32_t)__builtin_ctzll(__ballot(((ws >> lane) & 1ULL) && rank == lw));
+            if (qs >= P || ls >= 64 || node >= d.hi - d.lo) {  // (inconsistent prefixes: a bug; the host fails the batch)
+              if ((d.dbg & 32) && lane == 0) {  // what the producer saw (ksg_debug_counters)
+                int32_t* g = d.dbgbuf;
+                g[0] = (int32_t)j; g[1] = (int32_t)c; g[2] = (int32_t)k0; g[3] = (int32_t)tp; g[4] = (int32_t)qs;
+                g[5] = (int32_t)ls; g[6] = (int32_t)loc; g[7] = (int32_t)__builtin_amdgcn_readlane((int)lp_ex, 0);
+                g[8] = (int32_t)__builtin_amdgcn_readlane((int)lp_in, 0); g[9] = m0; g[10] = (int32_t)ixd;
+                g[11] = (int32_t)__builtin_amdgcn_readlane((int)wpq, 0);
+                g[12] = (int32_t)__builtin_amdgcn_readlane((int)__popcll(w), 0);
+                g[13] = (int32_t)__builtin_amdgcn_readlane((int)wpq, 7);
+                g[14] = (int32_t)__builtin_amdgcn_readlane((int)__popcll(w), 7);
+                g[15] = (int32_t)lpv; g[16] = (int32_t)__builtin_amdgcn_readlane((int)lpv, 1);
+                g[17] = (int32_t)e; g[18] = (int32_t)node;
+              }
+              node = ~0u;
+              ctl->hang = 1;
+            }
             if (lane == (uint32_t)c) cand_l = node;
             if (c == 0) cand0 = node;
           }
@@ -360,20 +466,6 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       }
       r_mod[e * 64 + lane] = mv;
       if (lane < DW) r_rec[e * DW + lane] = rec;
-      uint32_t lpe = 0, lpi = 0;
-#pragma unroll
-      for (int q = 0; q < P; ++q) {
-        r_t0[(size_t)e * P * 64 + q * 64 + lane] = t0[q];
-        r_wp[(size_t)e * P * 64 + q * 64 + lane] = (uint16_t)ex_q[q];
-        if (lane == (uint32_t)q) {
-          lpe = rowex[q];
-          lpi = q + 1 < P ? rowex[q + 1 < P ? q + 1 : q] : k0;
-        }
-      }
-      if (lane < P) {
-        r_lp[(e * 32 + lane) * 2] = lpe;
-        r_lp[(e * 32 + lane) * 2 + 1] = lpi;
-      }
       if (lane < KSG_NCAND) r_cand[e * 8 + lane] = cand_l;
       if (lane < 6 * KSG_NCAND) r_csnap[(e * KSG_NCAND + cL) * 6 + fL] = snap;
       if (cS < KSG_NCAND) r_csv[(e * KSG_NCAND + cS) * KSG_SLOT_SVCS + tS] = scv;
@@ -519,7 +611,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         const uint32_t wd = S.node >> 6;
         const uint64_t tw = r_t0[(size_t)e * P * 64 + wd];
         // the node's ascending position in T0 (used only if it drops)
-        dpos = r_lp[(e * 32 + (wd >> 6)) * 2] + r_wp[(size_t)e * P * 64 + wd] +
+        dpos = r_lp[e * 64 + (wd >> 6) * 2] + r_wp[(size_t)e * P * 64 + wd] +
                (uint32_t)__popcll(tw & ((1ULL << (S.node & 63)) - 1ULL));
         if ((tw >> (S.node & 63)) & 1ULL) {
           // does the slot (a snapshot tie of the pod) score below M0 now?
@@ -587,6 +679,9 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         if (first) {
           const int32_t fin = (int32_t)my_cl[KSG_CL_SC + a] + count;
           d.svc_cnt[(size_t)sa * d.n_nodes + n] = fin;
+          if (fin > 0)
+            __hip_atomic_fetch_or(d.svc_bits + (size_t)sa * d.nw + (n >> 6), 1ULL << (n & 63), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_fetch_max(d.svc_max + sa, fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
@@ -936,8 +1031,8 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
     uint32_t lp_ex = 0, lp_in = 0;
     if (lane < P) {
-      lp_ex = r_lp[(e * 32 + lane) * 2];
-      lp_in = r_lp[(e * 32 + lane) * 2 + 1];
+      lp_ex = r_lp[e * 64 + lane * 2];
+      lp_in = r_lp[e * 64 + lane * 2 + 1];
     }
     const uint32_t cand = lane < KSG_NCAND ? r_cand[e * 8 + lane] : ~0u;
     uint64_t t0x = 0;
@@ -945,7 +1040,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     if (have_x) {
       const uint32_t xw = xnode >> 6;
       t0x = t0e[xw];
-      xpos0 = r_lp[(e * 32 + (xw >> 6)) * 2] + r_wp[(size_t)e * P * 64 + xw];
+      xpos0 = r_lp[e * 64 + (xw >> 6) * 2] + r_wp[(size_t)e * P * 64 + xw];
     }
     const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
     const uint32_t k0 = __builtin_amdgcn_readfirstlane(r_hdr[e].k0);
@@ -1061,6 +1156,11 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           __builtin_amdgcn_mbcnt_hi((uint32_t)(ws >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ws, 0u));
       const uint32_t bsel = (uint32_t)__builtin_ctzll(__ballot(((ws >> lane) & 1ULL) && rank == lw));
       woff = (qs * 64 + ls) * 64 + bsel;
+    }
+    if (woff >= d.hi - d.lo) {  // (never: inconsistent prefixes or drop positions; the host fails the batch)
+      resolved = i;
+      reason = KSG_STOP_HANG;
+      break;
     }
     const uint64_t cm = __ballot(cand == woff);
     const uint32_t cidx = cm ? (uint32_t)__builtin_ctzll(cm) : KSG_NO_CAND;
@@ -1185,10 +1285,32 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
 // ---------------------------------------------------------------------------
 // host launcher
 // ---------------------------------------------------------------------------
+static uint32_t plain_P(const KsgDev& d);
 uint32_t ksg_win_plain_lds(const KsgDev& d, uint32_t wcap) {
+  return plain_lds_offsets(plain_P(d), (d.n_services + 31) / 32, wcap).total;
+}
+
+static uint32_t plain_P(const KsgDev& d) {
   const uint32_t P = (d.nwords + 63) / 64;
-  const uint32_t PP = P <= 1 ? 1 : P <= 2 ? 2 : P <= 4 ? 4 : P <= 8 ? 8 : P <= 16 ? 16 : 32;
-  return plain_lds_offsets(PP, (d.n_services + 31) / 32, wcap).total;
+  return P <= 1 ? 1 : P <= 2 ? 2 : P <= 4 ? 4 : P <= 8 ? 8 : P <= 16 ? 16 : 32;
+}
+
+uint32_t ksg_win_t0_stride(const KsgDev& d) { return t0img_stride(plain_P(d)); }
+
+// the window's T0 images (x.img), after phase A (and its all-gather)
+hipError_t ksg_launch_win_t0(const KsgDev& d, uint32_t wcap, const KsgWinRun* run, const KsgWinXchg& x,
+                             hipStream_t st) {
+  const uint32_t P = plain_P(d);
+#define KSG_T0_CASE(PP) \
+  if (P == PP) hipLaunchKernelGGL((ksg_win_t0_kernel<PP>), dim3(wcap), dim3(256), 0, st, d.nwords, wcap, run, x);
+  KSG_T0_CASE(1)
+  KSG_T0_CASE(2)
+  KSG_T0_CASE(4)
+  KSG_T0_CASE(8)
+  KSG_T0_CASE(16)
+  KSG_T0_CASE(32)
+#undef KSG_T0_CASE
+  return hipGetLastError();
 }
 
 template <int PP, bool ST>

@@ -319,7 +319,7 @@ __device__ __forceinline__ bool slot_drops(const KsgDev& d, const WinSlots& S, u
 __device__ __forceinline__ bool anti_counts_move(const KsgDev& d, uint32_t node, int32_t s) {
   bool labelled = false;
 #pragma unroll
-  for (int a = 0; a < KSG_MAX_ANTI; ++a)
+  for (int a = 0; a < KSG_WIN_MAX_ANTI; ++a)
     if ((uint32_t)a < d.n_anti && d.w_anti[a] != 0 && d.anti_domain[(size_t)a * d.n_nodes + d.lo + node] >= 0)
       labelled = true;
   return labelled && d.svc_cnt[(size_t)s * d.n_nodes + d.lo + node] > 0;

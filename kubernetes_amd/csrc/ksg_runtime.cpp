@@ -46,6 +46,9 @@ hipError_t ksg_launch_win_eval(const KsgDev& d, int mode, const ksg_pod* batch, 
                                uint32_t dz, hipStream_t st);
 hipError_t ksg_launch_zonemap(uint32_t n_nodes, const int32_t* anti_domain, uint32_t d0, uint32_t nw,
                               uint64_t* zmap, hipStream_t st);
+hipError_t ksg_launch_win_t0(const KsgDev& d, uint32_t wcap, const KsgWinRun* run, const KsgWinXchg& x,
+                             hipStream_t st);
+uint32_t ksg_win_t0_stride(const KsgDev& d);
 hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
                                   const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st);
 uint32_t ksg_win_max_window(const KsgDev& d);
@@ -57,7 +60,7 @@ hipError_t ksg_launch_decide(const KsgDev& d, const ksg_pod* pods, const uint32_
 hipError_t ksg_launch_static(const KsgStaticCfg& sc, uint32_t n_nodes, const ksg_node* nodes,
                              const uint32_t* node_pairs, const uint32_t* pair_keys,
                              const int32_t* dom_of_pair, uint32_t n_pairs, uint32_t nw,
-                             uint64_t* static_fit, int32_t* static_score, int32_t* anti_domain,
+                             uint64_t* static_fit, int64_t* static_score, int32_t* anti_domain,
                              int32_t* aff_pair, unsigned long long* pairmap, hipStream_t st);
 hipError_t ksg_launch_patch(const KsgPatch* patches, uint32_t n, hipStream_t st);
 hipError_t ksg_launch_admit(const ksg_admission_set* sets, uint32_t n_sets, const ksg_pod* pods,
@@ -184,6 +187,8 @@ struct ksg_ctx {
   KsgWinSum* d_winsum = nullptr;
   uint8_t* d_xsend = nullptr;   // phase A block of this shard (KsgWinXchg layout)
   uint8_t* d_xrecv = nullptr;   // all-gathered blocks of every shard (world > 1)
+  uint8_t* d_t0img = nullptr;   // the plain resolver's T0 images, one per window pod
+  size_t t0img_cap = 0;
   int32_t* d_dcnt = nullptr;     // [W][D] per-pod anti-affinity domain counts (phase A pre-pass)
   int32_t* d_dmb = nullptr;      // [W][D+1] re-rank: best score without the anti term per domain row
   uint64_t* d_zmap = nullptr;    // [D+1][nw] re-rank: nodes of each domain row (cluster allocation)
@@ -394,6 +399,7 @@ int mirror_add(ksg_ctx* c, uint32_t h, const ksg_pod* p, const uint32_t* ids, bo
     if (h < c->N) {
       v = ++c->svc_cnt[(size_t)s * c->N + h];
       if (emit) patch32(c, c->dev.svc_cnt + (size_t)s * c->N + h, v);
+      if (emit && v == 1) patch_or(c, c->dev.svc_bits + (size_t)s * c->nw + (h >> 6), 1ULL << (h & 63));
     } else {
       v = ++c->svc_ext[s][h];
     }
@@ -630,6 +636,8 @@ KsgDev full_geometry(const ksg_ctx* c) {
 bool use_window(ksg_ctx* c, const ksg_pod* pods, uint32_t n) {
   if (c->window == 0 || c->nw > 32 * 64 || ksg_win_max_window(full_geometry(c)) < 8) return false;
   if (c->ext_on) return false;  // extensions run on the exact kernels only
+  // int64 combined scores / more anti-affinity priorities than phase A keeps in registers
+  if (c->dev.wide || c->dev.n_anti > KSG_WIN_MAX_ANTI) return false;
   // monotonicity under commits needs non-negative pod-dependent weights
   if (c->cfg.w_least_requested < 0 || c->cfg.w_service_spreading < 0) return false;
   // lr_win (ksg_device.h) is exact for 0 <= capacity, requested totals <= 2^49
@@ -654,6 +662,17 @@ bool use_window(ksg_ctx* c, const ksg_pod* pods, uint32_t n) {
     if (sum > lim) return false;
   }
   return mu + sum <= lim;
+}
+
+// |combined score| bound of a weight set: 10 * sum |w| over the score-10
+// priorities + |w_equal| (+ the extensions'), exact in 128 bits
+unsigned __int128 score_bound(const ksg_config& cf, int64_t w_taint, int64_t w_bal) {
+  auto mag = [](int64_t w) -> unsigned __int128 { return w < 0 ? (unsigned __int128)(0 - (uint64_t)w) : (unsigned __int128)w; };
+  unsigned __int128 b = 10 * (mag(cf.w_least_requested) + mag(cf.w_service_spreading) + mag(w_taint) + mag(w_bal)) +
+                        mag(cf.w_equal);
+  for (uint32_t a = 0; a < cf.n_anti; ++a) b += 10 * mag(cf.w_anti[a]);
+  for (uint32_t q = 0; q < cf.n_label_pref; ++q) b += 10 * mag(cf.w_pref[q]);
+  return b;
 }
 
 int cluster_ok(ksg_ctx* c) {
@@ -765,16 +784,6 @@ static int create_impl(const ksg_config* cfg, int device, int rank, int world, c
     if (cfg->aff_group_mask[g] >> cfg->n_aff_labels) return KSG_ERR_ARG;  // a label the config lacks
   for (uint32_t q = 0; q < cfg->n_presence; ++q)
     if (cfg->presence_n_keys[q] > KSG_MAX_PRESENCE_KEYS) return KSG_ERR_ARG;
-  {  // combined scores are int32 on the device
-    int64_t bound = 10LL * (std::llabs((int64_t)cfg->w_least_requested) + std::llabs((int64_t)cfg->w_service_spreading)) +
-                    std::llabs((int64_t)cfg->w_equal);
-    for (uint32_t a = 0; a < cfg->n_anti; ++a) bound += 10LL * std::llabs((int64_t)cfg->w_anti[a]);
-    for (uint32_t q = 0; q < cfg->n_label_pref; ++q) bound += 10LL * std::llabs((int64_t)cfg->w_pref[q]);
-    if (bound >= KSG_SCORE_BOUND) {
-      fprintf(stderr, "ksg_create: priority weights too large (|score| bound %lld)\n", (long long)bound);
-      return KSG_ERR_ARG;
-    }
-  }
   ksg_ctx* c = new ksg_ctx();
   c->cfg = *cfg;
   if (c->cfg.max_conflict_keys == 0) c->cfg.max_conflict_keys = 1024;
@@ -855,7 +864,8 @@ int ksg_destroy(ksg_ctx* c) {
   free_cluster(c);
   void* scratch[] = {c->d_pods, c->d_ids, c->d_fail, c->d_score, c->d_rec_send, c->d_rec_recv, c->d_dpart,
                      c->d_dglobal, c->d_out, c->d_rng, c->d_summary, c->d_patch, c->d_shard_wlo,
-                     c->d_winsum, c->d_xsend, c->d_xrecv, c->d_run, c->d_dcnt, c->d_admit, c->d_one};
+                     c->d_winsum, c->d_xsend, c->d_xrecv, c->d_run, c->d_dcnt, c->d_admit, c->d_one,
+                     c->d_t0img};
   for (void* p : scratch)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -943,7 +953,9 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   int64_t *cap_c, *cap_m;
   double *inv_c, *inv_m;
   uint64_t *sfit, *keymap, *pairmap;
-  int32_t *sscore, *anti_dom, *aff_pair, *gscore = nullptr;
+  int64_t* sscore;
+  int32_t *anti_dom, *aff_pair;
+  int64_t* gscore = nullptr;  // (int32 or int64 scores: sized for int64)
   const size_t NN = std::max<uint32_t>(n_nodes, 1);
   if ((rc = dalloc(c, &cap_c, NN, owner)) || (rc = dalloc(c, &cap_m, NN, owner)) ||
       (rc = dalloc(c, &inv_c, NN, owner)) || (rc = dalloc(c, &inv_m, NN, owner)) ||
@@ -953,12 +965,13 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
       (rc = dalloc(c, &keymap, (size_t)c->cfg.max_conflict_keys * std::max<uint32_t>(c->nw, 1), owner)) ||
       (rc = dalloc(c, &pairmap, (size_t)n_pairs * std::max<uint32_t>(c->nw, 1), owner)) ||
       (rc = dalloc(c, &d.svc_cnt, (size_t)std::max<uint32_t>(n_services, 1) * NN, owner)) ||
+      (rc = dalloc(c, &d.svc_bits, (size_t)std::max<uint32_t>(n_services, 1) * std::max<uint32_t>(c->nw, 1), owner)) ||
       (rc = dalloc(c, &d.svc_max, std::max<uint32_t>(n_services, 1), owner)) ||
       (rc = dalloc(c, &d.svc_total, std::max<uint32_t>(n_services, 1), owner)) ||
       (rc = dalloc(c, &d.svc_peer, std::max<uint32_t>(n_services, 1), owner)) ||
       (rc = dalloc(c, &anti_dom, (size_t)std::max<uint32_t>(c->cfg.n_anti, 1) * NN, owner)) ||
       (rc = dalloc(c, &aff_pair, (size_t)std::max<uint32_t>(c->cfg.n_aff_labels, 1) * NN, owner)) ||
-      (c->R > KSG_R_LDS && (rc = dalloc(c, &gscore, (size_t)c->R * KSG_NT, owner))))
+      (c->R > KSG_R_LDS / 2 && (rc = dalloc(c, &gscore, (size_t)c->R * KSG_NT, owner))))
     return rc;
   if (n_services) HIPCHK(c, hipMemsetAsync(d.svc_peer, 0xff, n_services * sizeof(int32_t), c->st));
 
@@ -1055,6 +1068,8 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   for (uint32_t a = 0; a < c->cfg.n_anti; ++a) any_weight |= c->cfg.w_anti[a] != 0;
   for (uint32_t q = 0; q < c->cfg.n_label_pref; ++q) any_weight |= c->cfg.w_pref[q] != 0;
   d.empty_priorities = (!d.equal_fallback && !any_weight) ? 1 : 0;
+  // int64 combined scores (exact kernels) once a |score| could reach KSG_SCORE_BOUND
+  d.wide = score_bound(c->cfg, c->ext.w_taint_toleration, c->ext.w_balanced) >= (unsigned __int128)KSG_SCORE_BOUND;
   d.w_lr = c->cfg.w_least_requested;
   d.w_spread = c->cfg.w_service_spreading;
   d.n_anti = 0;
@@ -1067,7 +1082,7 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   for (uint32_t q = 0; q < c->cfg.n_label_pref; ++q) any_pref |= c->cfg.w_pref[q] != 0;
   d.has_static_score = (c->cfg.w_equal != 0 || any_pref) ? 1 : 0;
   d.dbg = getenv("KSG_DEBUG") ? atoi(getenv("KSG_DEBUG")) : 0;
-  if (d.dbg & 8) {
+  if (d.dbg & (8 | 32)) {  // (32: the plain resolver's inconsistency record, ksg_plain.hip)
     (void)hipMalloc(&d.dbgbuf, 128);
     (void)hipMemset(d.dbgbuf, 0, 128);
   }
@@ -1174,6 +1189,7 @@ static int remove_pod_impl(ksg_ctx* c, uint64_t uid) {
       int32_t& v = c->svc_cnt[(size_t)s * c->N + h];
       before = v--;
       patch32(c, c->dev.svc_cnt + (size_t)s * c->N + h, v);
+      if (v == 0) patch_andnot(c, c->dev.svc_bits + (size_t)s * c->nw + (h >> 6), 1ULL << (h & 63));
     } else {
       auto& m = c->svc_ext[s];
       before = m[h]--;
@@ -1462,6 +1478,12 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     if ((rc = grow(c, (void**)&c->d_xsend, &c->xsend_cap, x.blk, 1))) return rc;
     if (c->xchg && (rc = grow(c, (void**)&c->d_xrecv, &c->xrecv_cap, x.blk * c->world, 1))) return rc;
     x.buf = c->xchg ? c->d_xrecv : c->d_xsend;
+    const bool plain = !anti && !(c->dev.dbg & 128);  // the plain resolver reads T0 images
+    if (plain) {
+      x.img_stride = ksg_win_t0_stride(full);
+      if ((rc = grow(c, (void**)&c->d_t0img, &c->t0img_cap, (size_t)W * x.img_stride, 1))) return rc;
+      x.img = c->d_t0img;
+    }
     uint64_t* wbits = reinterpret_cast<uint64_t*>(c->d_xsend);
     int32_t* wmax = reinterpret_cast<int32_t*>(c->d_xsend + (size_t)W * x.ostride * 8);
     // Windows are chained on the device: each kernel reads the window's start
@@ -1515,6 +1537,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
                                       rr ? reinterpret_cast<uint64_t*>(c->d_xsend + x.b_off) : nullptr, x.dz,
                                       c->st));
         if (c->xchg && (rc = allgather(c, c->d_xsend, c->d_xrecv, x.blk))) return rc;
+        if (plain) HIPCHK(c, ksg_launch_win_t0(full, W, c->d_run, x, c->st));
         if (evk) HIPCHK(c, hipEventRecord(c->wev[2 * k + 1], c->st));
         HIPCHK(c, ksg_launch_win_resolve(full, W, c->d_run, c->d_winsum, x, c->d_rng, c->d_out, c->st));
         if (evk) HIPCHK(c, hipEventRecord(c->wev[2 * k + 2], c->st));
@@ -1820,12 +1843,6 @@ int ksg_set_extensions(ksg_ctx* c, const ksg_ext_config* e) {
   if (c->world > 1 || c->xchg) return fail(c, KSG_ERR_ARG, "extensions: one rank only");
   if ((e->filters & ~(KSG_EXT_TAINTS | KSG_EXT_SCALAR)) || e->n_scalar > KSG_MAX_SCALAR)
     return fail(c, KSG_ERR_ARG, "extensions: bad filters / n_scalar");
-  int64_t bound = 10LL * (std::llabs((int64_t)c->cfg.w_least_requested) + std::llabs((int64_t)c->cfg.w_service_spreading) +
-                          std::llabs((int64_t)e->w_taint_toleration) + std::llabs((int64_t)e->w_balanced)) +
-                  std::llabs((int64_t)c->cfg.w_equal);
-  for (uint32_t a = 0; a < c->cfg.n_anti; ++a) bound += 10LL * std::llabs((int64_t)c->cfg.w_anti[a]);
-  for (uint32_t q = 0; q < c->cfg.n_label_pref; ++q) bound += 10LL * std::llabs((int64_t)c->cfg.w_pref[q]);
-  if (bound >= KSG_SCORE_BOUND) return fail(c, KSG_ERR_ARG, "extensions: priority weights too large");
   c->ext = *e;
   c->ext_on = e->filters || e->w_taint_toleration || e->w_balanced || e->n_scalar;
   return KSG_OK;

@@ -109,7 +109,7 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
     capm = d.cap_mem[n];
     usedc = d.used_cpu[n];
     usedm = d.used_mem[n];
-    if (d.has_static_score) sst = d.static_score[n];
+    if (d.has_static_score) sst = (int32_t)d.static_score[n];  // (window path: |score| < KSG_SCORE_BOUND)
   }
   const double inv_c = lr_inv10(capc), inv_m = lr_inv10(capm);
 
@@ -154,19 +154,27 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
     smax = c.spread_max;
   }
 
-  // ---- per-pod service counts of this lane's node, all issued up front
+  // ---- per-pod service counts of this lane's node, all issued up front: the
+  // service's node word first (svc_bits, one 8-byte load per wave), then a count
+  // only where the node holds pods of the service (most counts are 0)
   const bool need_cnt = d.w_spread != 0 || MODE != KSG_WIN_PLAIN;
+  uint64_t sbw[KSG_PG];
+#pragma unroll
+  for (int j = 0; j < KSG_PG; ++j) {
+    const int32_t s = __builtin_amdgcn_readlane(svc, j);
+    sbw[j] = (need_cnt && has_word && (uint32_t)j < np && s >= 0) ? d.svc_bits[(size_t)s * d.nw + gw] : 0ULL;
+  }
   int32_t cnt[KSG_PG];
 #pragma unroll
   for (int j = 0; j < KSG_PG; ++j) {
     const int32_t s = __builtin_amdgcn_readlane(svc, j);
-    cnt[j] = (need_cnt && valid && (uint32_t)j < np && s >= 0) ? d.svc_cnt[(size_t)s * d.n_nodes + n] : 0;
+    cnt[j] = (valid && ((sbw[j] >> lane) & 1ULL)) ? d.svc_cnt[(size_t)s * d.n_nodes + n] : 0;
   }
 
   // anti-affinity label domains of this lane's node (dense per priority, -1 unlabelled)
-  int32_t dom[KSG_MAX_ANTI];
+  int32_t dom[KSG_WIN_MAX_ANTI];
 #pragma unroll
-  for (int a = 0; a < KSG_MAX_ANTI; ++a)
+  for (int a = 0; a < KSG_WIN_MAX_ANTI; ++a)
     dom[a] = (MODE != KSG_WIN_PLAIN && valid && (uint32_t)a < d.n_anti && d.w_anti[a] != 0)
                  ? d.anti_domain[(size_t)a * d.n_nodes + n]
                  : -1;
@@ -177,11 +185,11 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
   // all issued before the first use, not one L2 round trip per pod
   int64_t aterm[KSG_PG];
   if constexpr (MODE == KSG_WIN_ANTI) {
-    int32_t pcs[KSG_PG][KSG_MAX_ANTI];
+    int32_t pcs[KSG_PG][KSG_WIN_MAX_ANTI];
 #pragma unroll
     for (int j = 0; j < KSG_PG; ++j)
 #pragma unroll
-      for (int a = 0; a < KSG_MAX_ANTI; ++a)
+      for (int a = 0; a < KSG_WIN_MAX_ANTI; ++a)
         pcs[j][a] = ((uint32_t)j < np && dom[a] >= 0)
                         ? dcnt[(size_t)(p0 + j) * d.n_domains_total + d.anti_dom_off[a] + dom[a]]
                         : 0;
@@ -190,7 +198,7 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
       const int32_t tj = __builtin_amdgcn_readlane(tot, j);
       int64_t s = 0;
 #pragma unroll
-      for (int a = 0; a < KSG_MAX_ANTI; ++a)
+      for (int a = 0; a < KSG_WIN_MAX_ANTI; ++a)
         if (dom[a] >= 0)  // unlabelled nodes score 0
           s += (int64_t)d.w_anti[a] * (tj > 0 ? frac10_f32((int64_t)tj - pcs[j][a], tj) : 10);
       aterm[j] = s;
@@ -256,7 +264,7 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
         // wave one domain at a time, one atomic per (wave, domain)
         const int32_t cj = fit ? cnt[j] : 0;
 #pragma unroll
-        for (int a = 0; a < KSG_MAX_ANTI; ++a) {
+        for (int a = 0; a < KSG_WIN_MAX_ANTI; ++a) {
           uint64_t pend = __ballot(cj != 0 && dom[a] >= 0);
           while (pend) {
             const int32_t dd = __builtin_amdgcn_readlane(dom[a], (int)__builtin_ctzll(pend));
@@ -1345,6 +1353,9 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
       if (first) {
         const int32_t fin = sc[a] + count;
         d.svc_cnt[(size_t)sa * d.n_nodes + n] = fin;
+        if (fin > 0)
+          __hip_atomic_fetch_or(d.svc_bits + (size_t)sa * d.nw + (n >> 6), 1ULL << (n & 63), __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_max(d.svc_max + sa, fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -2066,6 +2077,9 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         if (first) {
           const int32_t fin = (int32_t)my_cl[KSG_CL_SC + a] + count;
           d.svc_cnt[(size_t)sa * d.n_nodes + n] = fin;
+          if (fin > 0)
+            __hip_atomic_fetch_or(d.svc_bits + (size_t)sa * d.nw + (n >> 6), 1ULL << (n & 63), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_fetch_max(d.svc_max + sa, fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
@@ -2892,9 +2906,8 @@ uint32_t ksg_win_max_window(const KsgDev& d) {
     const uint32_t mid = (lo + hi + 1) / 2;
     const uint32_t need = (anti && d.rr_dz && !(d.dbg & 4096))
                               ? win2_lds_offsets(P, nflag, mid, d.rr_dz, d.n_services).total
-                          : anti   ? win_lds_offsets(P, nflag, mid, d.n_anti > 0, d.rr_dz, d.n_services).total
-                          : P <= 8 ? ksg_win_plain_lds(d, mid)
-                                   : win2_lds_offsets(P, nflag, mid).total;
+                          : anti ? win_lds_offsets(P, nflag, mid, d.n_anti > 0, d.rr_dz, d.n_services).total
+                                 : ksg_win_plain_lds(d, mid);
     if (need <= kWinLdsBudget) lo = mid;
     else hi = mid - 1;
   }
@@ -2936,19 +2949,8 @@ static hipError_t win_resolve2_launch(const KsgDev& d, uint32_t wcap, size_t lds
 hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
                                   const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
   const uint32_t P = win_P(d);
-  if (x.fit_off == 0 && !(d.dbg & 128) && P <= 8)  // no ServiceAntiAffinity: the plain resolver (ksg_plain.hip)
+  if (x.fit_off == 0 && !(d.dbg & 128))  // no ServiceAntiAffinity: the plain resolver (ksg_plain.hip)
     return ksg_launch_win_plain(d, P, wcap, run, sums, x, rng, out, st);  // (KSG_DEBUG & 128: the LDS-slot one)
-  if (x.fit_off == 0 && !(d.dbg & 128)) {  // (more than 32k nodes per shard: the register-slot resolver, for now)
-    const size_t lds2 = win2_lds_offsets(P, (d.n_services + 31) / 32, wcap).total;
-    const bool stamp2 = (d.dbg & 8) != 0;
-    if (P == 16)
-      return stamp2 ? win_resolve2_launch<16, true, false>(d, wcap, lds2, run, sums, x, rng, out, st)
-                    : win_resolve2_launch<16, false, false>(d, wcap, lds2, run, sums, x, rng, out, st);
-    if (P == 32)
-      return stamp2 ? win_resolve2_launch<32, true, false>(d, wcap, lds2, run, sums, x, rng, out, st)
-                    : win_resolve2_launch<32, false, false>(d, wcap, lds2, run, sums, x, rng, out, st);
-    return hipErrorInvalidValue;
-  }
   if (x.fit_off != 0 && x.rr && !(d.dbg & 4096)) {
     // ServiceAntiAffinity with the re-rank: the register-slot resolver
     // (KSG_DEBUG & 4096: the LDS-slot resolver instead, for comparison)

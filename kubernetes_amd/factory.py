@@ -27,7 +27,12 @@ from . import abi
 
 DefaultProvider = "DefaultProvider"
 
-_I32_MIN, _I32_MAX = -(1 << 31), (1 << 31) - 1
+_I64_MIN, _I64_MAX = -(1 << 63), (1 << 63) - 1
+
+
+def _go_int(x: int) -> int:
+    """x wrapped to Go's int (int64, two's complement)."""
+    return ((int(x) + (1 << 63)) % (1 << 64)) - (1 << 63)
 _VALID_NAME = re.compile(r"[a-zA-Z0-9]([-a-zA-Z0-9]*[a-zA-Z0-9])")
 
 
@@ -271,23 +276,19 @@ class SchedulerConfig:
             cfg.aff_group_mask[g] = m
         cfg.n_priority_configs = len(self.priorities)
         n_anti = n_pref = 0
-        tot = {"LeastRequestedPriority": 0, "ServiceSpreadingPriority": 0, "EqualPriority": 0}
         for p in self.priorities:
-            # Policy weights are Go ints (plugin/pkg/scheduler/api/types.go:46); the
-            # device keeps them (and their sums) as int32: refuse, never wrap
-            if not (_I32_MIN <= int(p.weight) <= _I32_MAX):
-                raise ConfigError(f"priority weight {p.weight} of {p.kind} is outside int32")
-            if p.kind in tot:
-                tot[p.kind] += int(p.weight)
-                if not (_I32_MIN <= tot[p.kind] <= _I32_MAX):
-                    raise ConfigError(f"summed {p.kind} weight {tot[p.kind]} is outside int32")
+            # Policy weights are Go ints (plugin/pkg/scheduler/api/types.go:46: int64),
+            # and combined scores wrap like them (generic_scheduler.go:145-159): two
+            # configs of one kind add up to their summed weight, mod 2^64
+            if not (_I64_MIN <= int(p.weight) <= _I64_MAX):
+                raise ConfigError(f"priority weight {p.weight} of {p.kind} is outside Go's int")
         for p in self.priorities:
             if p.kind == "LeastRequestedPriority":
-                cfg.w_least_requested += p.weight
+                cfg.w_least_requested = _go_int(cfg.w_least_requested + p.weight)
             elif p.kind == "ServiceSpreadingPriority":
-                cfg.w_service_spreading += p.weight
+                cfg.w_service_spreading = _go_int(cfg.w_service_spreading + p.weight)
             elif p.kind == "EqualPriority":
-                cfg.w_equal += p.weight
+                cfg.w_equal = _go_int(cfg.w_equal + p.weight)
             elif p.kind == "ServiceAntiAffinity":
                 if n_anti == abi.MAX_ANTI:
                     raise ConfigError("too many ServiceAntiAffinity priorities")

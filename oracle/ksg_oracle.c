@@ -88,6 +88,11 @@ static uint64_t splitmix_next(uint64_t *s) {
   return z ^ (z >> 31);
 }
 
+/* Go int arithmetic wraps (two's complement): combinedScores[host] +=
+ * score * weight (generic_scheduler.go:145-159) with weight a Go int */
+static int64_t go_add(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+static int64_t go_mul(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
+
 static int64_t go_div(int64_t a, int64_t b) {
   if (b == -1) return (int64_t)(0ULL - (uint64_t)a);
   return a / b;
@@ -419,7 +424,7 @@ static void ext_prioritize(const orc *o, const pctx *c, const uint8_t *fails, in
   if (!o->ext_on) return;
   if (o->ext.w_balanced)
     for (uint32_t n = 0; n < o->N; ++n)
-      if (!fails[n]) score[n] += (int64_t)o->ext.w_balanced * balanced_score(tc[n], o->cap_c[n], tm[n], o->cap_m[n]);
+      if (!fails[n]) score[n] = go_add(score[n], go_mul(o->ext.w_balanced, balanced_score(tc[n], o->cap_c[n], tm[n], o->cap_m[n])));
   if (o->ext.w_taint_toleration && c->ext) {
     int32_t mx = 0;
     for (uint32_t n = 0; n < o->N; ++n)
@@ -430,11 +435,11 @@ static void ext_prioritize(const orc *o, const pctx *c, const uint8_t *fails, in
     for (uint32_t n = 0; n < o->N; ++n)
       if (!fails[n]) {
         int64_t v = mx == 0 ? 10 : 10 - (10 * (int64_t)soft_taints(o, c, n)) / mx;
-        score[n] += (int64_t)o->ext.w_taint_toleration * v;
+        score[n] = go_add(score[n], go_mul(o->ext.w_taint_toleration, v));
       }
   } else if (o->ext.w_taint_toleration) {
     for (uint32_t n = 0; n < o->N; ++n)
-      if (!fails[n]) score[n] += (int64_t)o->ext.w_taint_toleration * 10;
+      if (!fails[n]) score[n] = go_add(score[n], go_mul(o->ext.w_taint_toleration, 10));
   }
 }
 
@@ -655,7 +660,7 @@ static int faithful_prioritize(orc *o, const pctx *c, const uint8_t *fails, int6
       tm = (int64_t)((uint64_t)tm + (uint64_t)c->p->memory);
       int64_t cs = calculate_score(tc, o->cap_c[n]);
       int64_t ms = calculate_score(tm, o->cap_m[n]);
-      score[n] += (int64_t)cf->w_least_requested * ((cs + ms) / 2);
+      score[n] = go_add(score[n], go_mul(cf->w_least_requested, ((cs + ms) / 2)));
     }
     free_machine_map(o, &m);
   }
@@ -683,7 +688,7 @@ static int faithful_prioritize(orc *o, const pctx *c, const uint8_t *fails, int6
     for (uint32_t n = 0; n < o->N; ++n) {
       if (fails[n]) continue;
       int64_t sc = maxCount > 0 ? frac10_f32((int64_t)maxCount - counts[n], maxCount) : 10;
-      score[n] += (int64_t)cf->w_service_spreading * sc;
+      score[n] = go_add(score[n], go_mul(cf->w_service_spreading, sc));
     }
     free(counts);
   }
@@ -709,7 +714,7 @@ static int faithful_prioritize(orc *o, const pctx *c, const uint8_t *fails, int6
       int32_t pr = node_pair_for_key(o, n, cf->anti_key[a]);
       int64_t sc = 0;
       if (pr >= 0) sc = nsp > 0 ? frac10_f32(nsp - podCounts[pr], nsp) : 10;
-      score[n] += (int64_t)cf->w_anti[a] * sc;
+      score[n] = go_add(score[n], go_mul(cf->w_anti[a], sc));
     }
     free(podCounts);
   }
@@ -720,13 +725,13 @@ static int faithful_prioritize(orc *o, const pctx *c, const uint8_t *fails, int6
       if (fails[n]) continue;
       int exists = node_has_key(o, n, cf->pref_key[q]);
       int ok = (exists && cf->pref_presence[q]) || (!exists && !cf->pref_presence[q]);
-      score[n] += (int64_t)cf->w_pref[q] * (ok ? 10 : 0);
+      score[n] = go_add(score[n], go_mul(cf->w_pref[q], (ok ? 10 : 0)));
     }
   }
   if (cf->w_equal) {
     any = 1;
     for (uint32_t n = 0; n < o->N; ++n)
-      if (!fails[n]) score[n] += (int64_t)cf->w_equal;
+      if (!fails[n]) score[n] = go_add(score[n], cf->w_equal);
   }
   return any && nfilt > 0;
 }
@@ -797,26 +802,26 @@ static int incr_prioritize(orc *o, const pctx *c, const uint8_t *fails, int64_t 
     if (cf->w_least_requested) {
       int64_t tc = (int64_t)((uint64_t)o->used_c[n] + (uint64_t)c->p->milli_cpu);
       int64_t tm = (int64_t)((uint64_t)o->used_m[n] + (uint64_t)c->p->memory);
-      sc += (int64_t)cf->w_least_requested * ((calculate_score(tc, o->cap_c[n]) + calculate_score(tm, o->cap_m[n])) / 2);
+      sc = go_add(sc, go_mul(cf->w_least_requested, ((calculate_score(tc, o->cap_c[n]) + calculate_score(tm, o->cap_m[n])) / 2)));
     }
     if (cf->w_service_spreading) {
       int32_t cnt = s >= 0 ? o->svc_cnt[(size_t)s * o->N + n] : 0;
-      sc += (int64_t)cf->w_service_spreading * (maxc > 0 ? frac10_f32((int64_t)maxc - cnt, maxc) : 10);
+      sc = go_add(sc, go_mul(cf->w_service_spreading, (maxc > 0 ? frac10_f32((int64_t)maxc - cnt, maxc) : 10)));
     }
     for (uint32_t a = 0; a < cf->n_anti; ++a) {
       if (!cf->w_anti[a]) continue;
       int32_t pr = node_pair_for_key(o, n, cf->anti_key[a]);
       int64_t v = 0;
       if (pr >= 0) v = tot > 0 ? frac10_f32(tot - dcount[a][pr], tot) : 10;
-      sc += (int64_t)cf->w_anti[a] * v;
+      sc = go_add(sc, go_mul(cf->w_anti[a], v));
     }
     for (uint32_t q = 0; q < cf->n_label_pref; ++q) {
       if (!cf->w_pref[q]) continue;
       int exists = node_has_key(o, n, cf->pref_key[q]);
       int ok = (exists && cf->pref_presence[q]) || (!exists && !cf->pref_presence[q]);
-      sc += (int64_t)cf->w_pref[q] * (ok ? 10 : 0);
+      sc = go_add(sc, go_mul(cf->w_pref[q], (ok ? 10 : 0)));
     }
-    sc += (int64_t)cf->w_equal;
+    sc = go_add(sc, cf->w_equal);
     score[n] = sc;
   }
   if (ext_prio_on(o)) {
@@ -1178,20 +1183,20 @@ static int64_t mt_score(const orc *o, const pctx *c, int32_t maxc, uint32_t n) {
   if (cf->w_least_requested) {
     int64_t tc = (int64_t)((uint64_t)o->used_c[n] + (uint64_t)c->p->milli_cpu);
     int64_t tm = (int64_t)((uint64_t)o->used_m[n] + (uint64_t)c->p->memory);
-    sc += (int64_t)cf->w_least_requested * ((calculate_score(tc, o->cap_c[n]) + calculate_score(tm, o->cap_m[n])) / 2);
+    sc = go_add(sc, go_mul(cf->w_least_requested, ((calculate_score(tc, o->cap_c[n]) + calculate_score(tm, o->cap_m[n])) / 2)));
   }
   if (cf->w_service_spreading) {
     int32_t s = c->p->service;
     int32_t cnt = s >= 0 ? o->svc_cnt[(size_t)s * o->N + n] : 0;
-    sc += (int64_t)cf->w_service_spreading * (maxc > 0 ? frac10_f32((int64_t)maxc - cnt, maxc) : 10);
+    sc = go_add(sc, go_mul(cf->w_service_spreading, (maxc > 0 ? frac10_f32((int64_t)maxc - cnt, maxc) : 10)));
   }
   for (uint32_t q = 0; q < cf->n_label_pref; ++q) {
     if (!cf->w_pref[q]) continue;
     int exists = node_has_key(o, n, cf->pref_key[q]);
     int ok = (exists && cf->pref_presence[q]) || (!exists && !cf->pref_presence[q]);
-    sc += (int64_t)cf->w_pref[q] * (ok ? 10 : 0);
+    sc = go_add(sc, go_mul(cf->w_pref[q], (ok ? 10 : 0)));
   }
-  return sc + (int64_t)cf->w_equal;
+  return go_add(sc, cf->w_equal);
 }
 
 static void *mt_worker(void *argp) {

@@ -354,7 +354,9 @@ def prioritize_nodes(pod: Pod, pod_lister: PodLister, configs: List[Tuple[Priori
         if weight == 0:
             continue
         for host, score in fn(pod, pod_lister, nodes):
-            combined[host] = combined.get(host, 0) + score * weight
+            # Go int (int64) arithmetic wraps
+            v = combined.get(host, 0) + score * weight
+            combined[host] = ((v + (1 << 63)) % (1 << 64)) - (1 << 63)
     return list(combined.items())
 
 

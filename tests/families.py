@@ -13,7 +13,12 @@ library and compare every decision.
                   stay per namespace (spreading.go:61-70, predicates.go:284-290)
   negative        negative weights on every priority kind (Policy weights are not
                   validated, plugins.go:159,169): the batch takes the exact path
-  big_weights     weights just under the device's int32 score bound
+  big_weights     weights just under the window path's int32 score bound
+  huge_weights    Go int weights around 2^40 and 2^62 (combined scores wrap like
+                  Go's int64, generic_scheduler.go:145-159): the exact kernels
+                  with int64 scores
+  many_anti       six ServiceAntiAffinity priorities (two per label: the reference
+                  registers any number, plugins.go:145-183): the exact kernels
   existing_hosts  pre-existing pods with Status.Host == "" and on hosts outside the
                   node list (MapPodsToMachines keys on Status.Host, predicates.go:354-375)
   invalid_selectors  ServiceAffinity over two predicates with invalid nodeSelector
@@ -24,9 +29,10 @@ from __future__ import annotations
 from kubernetes_amd import factory, workload
 from kubernetes_amd.api import ObjectMeta, PodStatus, Quantity, Service, ServiceSpec
 
-FAMILIES = ("multi_service", "namespaces", "negative", "big_weights", "existing_hosts", "invalid_selectors")
+FAMILIES = ("multi_service", "namespaces", "negative", "big_weights", "huge_weights", "many_anti", "existing_hosts",
+            "invalid_selectors")
 
-# 10 * sum|w| + |w_equal| must stay below 2^30 (KSG_SCORE_BOUND, ksg_internal.h)
+# the window path keeps 10 * sum|w| + |w_equal| below 2^30 (KSG_SCORE_BOUND, ksg_internal.h)
 BIG_W = (1 << 30) // 10 // 4 - 1
 
 
@@ -105,6 +111,29 @@ def build(family: str, nn: int, npods: int, seed: int = 7) -> workload.Workload:
         cfg.priorities = [factory.PriorityDesc(p.kind, BIG_W if p.kind in (
             "LeastRequestedPriority", "ServiceSpreadingPriority") else p.weight, p.label, p.presence)
             for p in cfg.priorities]
+    elif family == "huge_weights":
+        pods = workload.make_pods(npods, rng, n_apps=8)
+        services = workload.make_services(8)
+        _tighten(nodes, rng)
+        cfg = _policy(_DEFAULT_PREDS,
+                      [{"name": "LeastRequestedPriority", "weight": 1}, {"name": "ServiceSpreadingPriority", "weight": 1},
+                       {"name": "HugeRack", "weight": (1 << 62) + 12345,  # 10 * w wraps past 2^63
+                        "argument": {"labelPreference": {"label": "rack", "presence": True}}},
+                       {"name": "HugeZone", "weight": -(3 << 40),
+                        "argument": {"serviceAntiAffinity": {"label": "zone"}}}],
+                      "huge")
+        cfg.priorities = [factory.PriorityDesc(p.kind, (3 << 40) + 7 if p.kind == "LeastRequestedPriority" else
+                                               (5 << 39) if p.kind == "ServiceSpreadingPriority" else p.weight,
+                                               p.label, p.presence)
+                          for p in cfg.priorities]
+    elif family == "many_anti":
+        pods = workload.make_pods(npods, rng, n_apps=6)
+        services = workload.make_services(6)
+        anti = [{"name": f"Anti{i}-{lab}", "weight": w, "argument": {"serviceAntiAffinity": {"label": lab}}}
+                for i, (lab, w) in enumerate((("zone", 1), ("rack", 2), ("region", 1), ("zone", 3), ("rack", 1),
+                                              ("region", 2)))]
+        cfg = _policy(_DEFAULT_PREDS, [{"name": "LeastRequestedPriority", "weight": 1},
+                                       {"name": "ServiceSpreadingPriority", "weight": 1}] + anti, "ma")
     elif family == "existing_hosts":
         pods = workload.make_pods(npods + npods // 3, rng, n_apps=4)
         services = workload.make_services(4)

@@ -136,33 +136,33 @@ def test_pod_services_index_matches_scan(seed):
         assert view.pod_services(pod) == want
 
 
-def test_weights_outside_int32_are_refused():
-    """Policy weights are Go ints (plugin/pkg/scheduler/api/types.go:46); the device keeps
-    them as int32, so compile() refuses (never wraps) a weight or a summed builtin weight
-    outside int32."""
-    for w in (1 << 31, -(1 << 31) - 1, 1 << 40):
+def test_weights_are_go_ints_and_wrap():
+    """Policy weights are Go ints (plugin/pkg/scheduler/api/types.go:46: int64): compile()
+    keeps any weight in int64 (the library runs weights past the window path's int32
+    score bound on the exact kernels with int64 scores), refuses one outside it, and
+    two builtin configs of one kind add up mod 2^64 like Go's combinedScores."""
+    for w in (1 << 63, -(1 << 63) - 1):
         cfg = factory.create_from_config({"priorities": [
             {"name": f"HugePref{abs(w)}", "weight": w, "argument": {"labelPreference": {"label": "rack"}}}]})
-        with pytest.raises(factory.ConfigError, match="outside int32"):
+        with pytest.raises(factory.ConfigError, match="outside Go's int"):
             cfg.compile(lambda k: 0)
-    ok = factory.create_from_config({"priorities": [
-        {"name": "MaxPref", "weight": (1 << 31) - 1, "argument": {"labelPreference": {"label": "rack"}}}]})
-    assert ok.compile(lambda k: 0).w_pref[0] == (1 << 31) - 1
+    for w in ((1 << 63) - 1, -(1 << 63), 1 << 40, (1 << 31) - 1):
+        ok = factory.create_from_config({"priorities": [
+            {"name": f"Pref{w}", "weight": w, "argument": {"labelPreference": {"label": "rack"}}}]})
+        assert ok.compile(lambda k: 0).w_pref[0] == w
+    two = factory.SchedulerConfig({}, [factory.PriorityDesc("LeastRequestedPriority", (1 << 62) + 5),
+                                       factory.PriorityDesc("LeastRequestedPriority", 3 << 61)])
+    assert two.compile(lambda k: 0).w_least_requested == ((1 << 62) + 5 + (3 << 61)) - (1 << 64)
 
 
-def test_library_refuses_weights_over_the_score_bound():
-    """ksg_create returns KSG_ERR_ARG (before any HIP call) when a combined score could
-    reach 2^30: 10 * sum|w| + |w_equal| >= KSG_SCORE_BOUND (include/kschedgpu.h)."""
-    import ctypes as C
-
-    lib = abi.load_library()
-    for w_pref, ok in (((1 << 30) // 10 - 30, True), ((1 << 30) // 10, False), ((1 << 31) - 1, False)):
-        cfg = factory.create_from_config({"priorities": [
-            {"name": f"BoundPref{w_pref}", "weight": w_pref, "argument": {"labelPreference": {"label": "rack"}}},
-            {"name": "LeastRequestedPriority", "weight": 1}, {"name": "ServiceSpreadingPriority", "weight": 1}]}
-        ).compile(lambda k: 0)
-        if ok:
-            continue  # a valid config goes on to create a HIP stream: GPU tests cover it
-        ctx = C.c_void_p()
-        assert lib.ksg_create(C.byref(cfg), 0, C.byref(ctx)) == abi.KSG_ERR_ARG
-        assert not ctx.value
+def test_policy_lists_past_the_window_caps_compile():
+    """Six ServiceAntiAffinity priorities and twenty LabelPreference ones: the
+    reference registers any number (plugins.go:81-183); the library takes them on
+    the exact kernels (the window path keeps four anti-affinity terms in registers)."""
+    prios = [{"name": f"Anti{i}", "weight": 1 + i, "argument": {"serviceAntiAffinity": {"label": "zone"}}}
+             for i in range(6)]
+    prios += [{"name": f"Pref{i}", "weight": 1, "argument": {"labelPreference": {"label": "rack"}}}
+              for i in range(20)]
+    cfg = factory.create_from_config({"priorities": prios}).compile(lambda k: 0)
+    assert cfg.n_anti == 6 and cfg.n_label_pref == 20
+    assert [cfg.w_anti[a] for a in range(6)] == [1, 2, 3, 4, 5, 6]
