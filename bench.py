@@ -5,7 +5,8 @@ A "step" is one batch of `--batch` pods scheduled in order through the hot path
 (filter every node, score, argmax + reference tie-break, commit) by
 ksg_schedule_batch: windows of pods are scored against a snapshot on all CUs
 (ksg_win_score_kernel) and resolved in order, exactly, by one workgroup
-(ksg_win_resolve2_kernel; ksg_win_resolve_kernel with ServiceAntiAffinity);
+(ksg_win_plain_kernel, fed by ksg_win_t0_kernel's per-pod T0 images;
+ksg_win_resolve2_kernel / ksg_win_resolve_kernel with ServiceAntiAffinity);
 node state is resident in HBM before the timed region (the C ABI copies the
 batch descriptors in, ~B*88 bytes, inside the step).
 
@@ -307,6 +308,7 @@ def main():
     # ksg_set_cluster's rr_dz)
     dbg = int(os.environ.get("KSG_DEBUG", "0") or 0)
     anti = any(int(cfg.w_anti[a]) != 0 for a in range(int(cfg.n_anti)))
+    plain = not anti and not (dbg & 128)  # no ServiceAntiAffinity: the plain resolver (ksg_plain.hip)
     if anti:
         pk = np.asarray(view.arrays.pair_keys, np.uint32) & np.uint32(0x7FFFFFFF)
         n_dom = int((pk[1:] == np.uint32(cfg.anti_key[0])).sum()) if len(pk) > 1 else 0
@@ -320,9 +322,10 @@ def main():
         pods_per_launch = pods_timed / launches
         # (KSG_KERNEL_EVENTS=0 drops the per-kernel events: no kernel times, an A/B switch)
         kavg_s = kk["resolve_ms"] / launches / 1e3 or float("nan")
-        # the in-order resolver: the LDS-slot one with ServiceAntiAffinity, else the
-        # register-slot one (ksg_window.hip)
-        kname = "ksg_win_resolve_kernel" if anti else "ksg_win_resolve2_kernel"
+        # the in-order resolver: the plain one without ServiceAntiAffinity (ksg_plain.hip),
+        # else the LDS-slot one or the register-slot re-rank (ksg_window.hip)
+        kname = ("ksg_win_plain_kernel" if plain else
+                 "ksg_win_resolve_kernel" if anti else "ksg_win_resolve2_kernel")
         # phase A scores this rank's shard (N/world nodes) for the window's W pods
         # (the capacity the library used: it shrinks W where windows stop early);
         # with world > 1 its event window also holds the per-window all-gather.
