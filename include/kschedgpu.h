@@ -220,7 +220,13 @@ int ksg_remove_pod(ksg_ctx* ctx, uint64_t uid);
  * r = rand.Int() iff tie_count > 0 and calls commit(r % tie_count), which picks
  * the tie_index-th tie in descending name order (generic_scheduler.go:88-95)
  * and applies AssumePod's delta. fail_codes (optional, n_nodes bytes) gets the
- * per-node KSG_FAIL_* code to rebuild FailedPredicateMap. */
+ * per-node KSG_FAIL_* code to rebuild FailedPredicateMap.
+ * On one rank (shards up to 16,384 nodes, int32 scores) both calls are served
+ * by a resident workgroup polling mapped host memory (ksg_serve.hip): no
+ * kernel launch, copy or stream synchronisation per call. It returns after
+ * KSG_SERVE_IDLE_US (default 20,000) without a request and is relaunched by
+ * the next one; any other entry point that needs the device stops it first.
+ * KSG_SERVE=0 in the environment at ksg_create: kernels launched per call. */
 int ksg_schedule_begin(ksg_ctx* ctx, const ksg_pod* pod, const uint32_t* ids,
                        int64_t* max_score, uint32_t* tie_count, uint8_t* fail_codes);
 int ksg_schedule_commit(ksg_ctx* ctx, uint32_t tie_index, int32_t* out_node);
@@ -292,6 +298,11 @@ int ksg_batch_totals(ksg_ctx* ctx, double* out24);
  * context created with KSG_DEBUG=8 in the environment; out32[32] (layout:
  * DESIGN.md section 4, "resolver stages"). KSG_ERR_STATE when not enabled. */
 int ksg_debug_counters(ksg_ctx* ctx, int32_t* out32);
+
+/* Diagnostics of the resident begin/commit server: out4[0] kernel launches,
+ * [1] requests served (begin, commit, patch, exit), [2] 1 while resident,
+ * [3] 1 when this context can use it. No reference counterpart. */
+int ksg_serve_stats(ksg_ctx* ctx, uint64_t* out4);
 
 /* ---- node sharding (multi-GPU) ------------------------------
  * Nodes are split into contiguous runs of 64-node words in name-rank order.

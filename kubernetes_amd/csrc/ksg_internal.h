@@ -212,6 +212,54 @@ struct KsgPatch {
   uint32_t pad;
 };
 
+// ---- the resident drop-in server (ksg_serve.hip) ---------------------------
+// ksg_schedule_begin / ksg_schedule_commit talk to one resident workgroup
+// through pinned, host-coherent memory mapped into the device (KsgSrvBox): no
+// kernel launch, copy or stream synchronisation per call.
+//
+// Request block: KSG_SRV_CHUNKS chunks of 16 B that the server reads with ONE
+// 16-B-per-lane wave load per poll. Dwords 0..2 of a chunk carry data, dword 3
+// the request's sequence number (its tag). The host writes every data dword,
+// then every tag; x86 stores become visible in program order and a 16-B read
+// is one PCIe read, so a chunk whose tag matches was read after its data (and
+// after the `ext` payload) landed. Data dwords, in order: the header
+// (KSG_SRV_HDR_DW), then the payload's first KSG_SRV_INLINE_DW dwords; the
+// rest of the payload is at `ext`, read once the block matched. Payload: the
+// ksg_pod, its id list, its ksg_pod_ext (extensions).
+#define KSG_SRV_CHUNKS 64
+#define KSG_SRV_CHUNK_DW 3
+#define KSG_SRV_HDR_DW 8
+#define KSG_SRV_INLINE_DW (KSG_SRV_CHUNKS * KSG_SRV_CHUNK_DW - KSG_SRV_HDR_DW)
+#define KSG_SRV_EXT_DW 4096
+#define KSG_SRV_PAY_DW (KSG_SRV_INLINE_DW + KSG_SRV_EXT_DW)
+#define KSG_SRV_PATCHES 4096
+#define KSG_SRV_MAX_R 16  // nodes per thread the server takes (shards up to 16384 nodes)
+enum {
+  KSG_SRV_BEGIN = 1,   // scan the payload's pod: respond {seq, k | ~0u on error, max lo, max hi}
+  KSG_SRV_COMMIT = 2,  // commit tie `tie` of begin `bseq` (rescanned if not the one in LDS): {seq, node}
+  KSG_SRV_PATCH = 3,   // apply `n_patch` patches from `patch` in order, reload cached totals: {seq}
+  KSG_SRV_EXIT = 4,    // respond {seq} and return
+};
+// header dwords
+enum { KSG_SRVH_KIND = 0, KSG_SRVH_BSEQ, KSG_SRVH_TIE, KSG_SRVH_FLAGS, KSG_SRVH_PAYDW, KSG_SRVH_IDS_AT,
+       KSG_SRVH_EXT_AT, KSG_SRVH_NPATCH };
+#define KSG_SRV_BADREQ 0xFFFFFFFEu  // response: the payload's layout or ids are out of range
+#define KSG_SRVF_WANT_FAIL 1u  // BEGIN: write the fail code of every node to `fail`
+#define KSG_SRVF_EXT 2u        // the payload carries a ksg_pod_ext at EXT_AT
+struct KsgSrvBox {
+  uint32_t req[KSG_SRV_CHUNKS * 4];
+  uint32_t resp[16];  // {seq, a, b, c}: one 16-B store
+  uint32_t ext[KSG_SRV_EXT_DW];
+  KsgPatch patch[KSG_SRV_PATCHES];
+};
+struct KsgSrvArgs {
+  KsgSrvBox* box;        // device address of the mapped box
+  uint8_t* fail;         // device address of the mapped fail-code area (shard nodes)
+  uint32_t start_seq;    // the server serves start_seq + 1, + 2, ...
+  uint64_t idle_ticks;   // returns after this long without a request (wall_clock64: 100 MHz)
+  uint32_t stamps;       // KSG_SERVE_STAMPS: per-stage s_memtime cycles of each BEGIN in resp[4..9]
+};
+
 #ifdef __HIP__
 #define KSG_HD __host__ __device__
 #else

@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -63,6 +64,7 @@ hipError_t ksg_launch_static(const KsgStaticCfg& sc, uint32_t n_nodes, const ksg
                              uint64_t* static_fit, int64_t* static_score, int32_t* anti_domain,
                              int32_t* aff_pair, unsigned long long* pairmap, hipStream_t st);
 hipError_t ksg_launch_patch(const KsgPatch* patches, uint32_t n, hipStream_t st);
+hipError_t ksg_launch_serve(int R, bool anti, bool ext, const KsgDev& d, const KsgSrvArgs& a, hipStream_t st);
 hipError_t ksg_launch_admit(const ksg_admission_set* sets, uint32_t n_sets, const ksg_pod* pods,
                             const uint32_t* ids, const uint32_t* pairs, int mode, uint8_t* out, hipStream_t st);
 
@@ -224,6 +226,25 @@ struct ksg_ctx {
   size_t pext_cap = 0;
   ksg_pod_ext* d_one_ext = nullptr;
 
+  // the resident drop-in server (ksg_serve.hip): begin / commit as requests in
+  // mapped host memory instead of launches, copies and stream syncs
+  bool srv_enabled = true;      // KSG_SERVE=0: the launch-per-call path
+  bool srv_running = false;     // a server kernel may be resident on `st`
+  KsgSrvBox* srv_box = nullptr;   // pinned, coherent, mapped
+  KsgSrvBox* srv_dbox = nullptr;  // its device address
+  uint8_t* srv_fail = nullptr;    // fail codes of the shard's nodes (mapped)
+  uint8_t* srv_dfail = nullptr;
+  size_t srv_fail_cap = 0;
+  uint32_t srv_seq = 0;         // last request posted
+  uint64_t srv_idle_us = 20000; // the server returns after this long without a request
+  bool pend_srv = false;        // the pending begin was served by the server (its seq: srv_bseq)
+  uint32_t srv_bseq = 0;
+  uint32_t srv_bhdr[KSG_SRV_HDR_DW] = {};  // that begin's header (its payload layout)
+  uint64_t srv_launches = 0;
+  bool srv_stamps = false;      // KSG_SERVE_STAMPS=1: sum the server's per-stage cycles of each begin
+  double srv_stage[6] = {};     // (printed by ksg_destroy)
+  uint64_t srv_stamped = 0;
+
   // begin/commit
   bool pending = false;
   uint64_t pending_k = 0;
@@ -324,8 +345,11 @@ void patch_andnot(ksg_ctx* c, const void* addr, uint64_t v) {
   c->patches.push_back(KsgPatch{(uint64_t)(uintptr_t)addr, v, 3, 0});
 }
 
+int srv_flush_patches(ksg_ctx* c);
+
 int flush_patches(ksg_ctx* c) {
   if (c->patches.empty()) return KSG_OK;
+  if (c->srv_running) return srv_flush_patches(c);
   int rc = grow(c, (void**)&c->d_patch, &c->patch_cap, c->patches.size(), sizeof(KsgPatch));
   if (rc) return rc;
   HIPCHK(c, hipMemcpyAsync(c->d_patch, c->patches.data(), c->patches.size() * sizeof(KsgPatch),
@@ -717,6 +741,148 @@ int wait_device(ksg_ctx* c) {
   return KSG_OK;
 }
 
+// ---- the resident drop-in server (ksg_serve.hip) ------------------------------
+bool srv_eligible(const ksg_ctx* c) {
+  return c->srv_enabled && c->world == 1 && !c->xchg && c->R <= KSG_SRV_MAX_R && !c->dev.wide && c->N > 0;
+}
+
+int srv_alloc(ksg_ctx* c) {
+  if (!c->srv_box) {
+    HIPCHK(c, hipHostMalloc((void**)&c->srv_box, sizeof(KsgSrvBox), hipHostMallocCoherent | hipHostMallocMapped));
+    memset(c->srv_box, 0, sizeof(KsgSrvBox));
+    void* dp = nullptr;
+    HIPCHK(c, hipHostGetDevicePointer(&dp, c->srv_box, 0));
+    c->srv_dbox = static_cast<KsgSrvBox*>(dp);
+  }
+  return KSG_OK;
+}
+
+int srv_launch(ksg_ctx* c, uint32_t start_seq) {
+  if (int rc = srv_alloc(c)) return rc;
+  const size_t nf = std::max<size_t>(c->hi - c->lo, 1);
+  if (c->srv_fail_cap < nf) {
+    if (c->srv_fail) (void)hipHostFree(c->srv_fail);
+    c->srv_fail = nullptr;
+    c->srv_fail_cap = 0;
+    HIPCHK(c, hipHostMalloc((void**)&c->srv_fail, nf, hipHostMallocCoherent | hipHostMallocMapped));
+    void* dp = nullptr;
+    HIPCHK(c, hipHostGetDevicePointer(&dp, c->srv_fail, 0));
+    c->srv_dfail = static_cast<uint8_t*>(dp);
+    c->srv_fail_cap = nf;
+  }
+  KsgSrvArgs a{c->srv_dbox, c->srv_dfail, start_seq, (uint64_t)c->srv_idle_us * 100, c->srv_stamps ? 1u : 0u};
+  HIPCHK(c, ksg_launch_serve(c->R, anti_on(c), c->ext_on, c->dev, a, c->st));
+  c->srv_running = true;
+  ++c->srv_launches;
+  return KSG_OK;
+}
+
+// Posts request ++srv_seq (header dwords hdr[0..KSG_SRV_HDR_DW); the payload
+// chunks were written by the caller or are left from the pending begin) and
+// waits for its response. A server that returned (idle) before it saw the
+// request is relaunched to serve it.
+int srv_call(ksg_ctx* c, const uint32_t* hdr, uint32_t* resp4) {
+  if (!c->srv_running) {
+    if (int rc = srv_launch(c, c->srv_seq)) return rc;
+  }
+  const uint32_t seq = ++c->srv_seq;
+  uint32_t* req = c->srv_box->req;
+  for (uint32_t i = 0; i < KSG_SRV_HDR_DW; ++i) req[4 * (i / KSG_SRV_CHUNK_DW) + i % KSG_SRV_CHUNK_DW] = hdr[i];
+  std::atomic_thread_fence(std::memory_order_release);  // data, then tags (x86: stores stay in order)
+  for (uint32_t q = 0; q < KSG_SRV_CHUNKS; ++q) __atomic_store_n(&req[4 * q + 3], seq, __ATOMIC_RELEASE);
+  const uint32_t* rs = c->srv_box->resp;
+  auto t0 = std::chrono::steady_clock::now();
+  uint32_t spins = 0, relaunches = 0;
+  while (__atomic_load_n(&rs[0], __ATOMIC_ACQUIRE) != seq) {
+    if ((++spins & 255) != 0) continue;
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    if (us < 20.0) continue;
+    const hipError_t q = hipStreamQuery(c->st);
+    if (q == hipSuccess) {  // the server returned without serving `seq`
+      if (__atomic_load_n(&rs[0], __ATOMIC_ACQUIRE) == seq) break;
+      if (++relaunches > 3) return fail(c, KSG_ERR_HIP, "drop-in server exits without serving request %u", seq);
+      c->srv_running = false;
+      if (int rc = srv_launch(c, seq - 1)) return rc;
+      t0 = std::chrono::steady_clock::now();
+    } else if (q != hipErrorNotReady) {
+      c->srv_running = false;
+      return fail(c, KSG_ERR_HIP, "drop-in server: %s", hipGetErrorString(q));
+    } else if (us > 5e6) {
+      return fail(c, KSG_ERR_HIP, "drop-in server did not answer request %u in 5 s", seq);
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  for (int i = 0; i < 4; ++i) resp4[i] = __atomic_load_n(&rs[i], __ATOMIC_RELAXED);
+  if (c->srv_stamps && hdr[KSG_SRVH_KIND] == KSG_SRV_BEGIN && __atomic_load_n(&rs[10], __ATOMIC_RELAXED) == seq) {
+    for (int i = 0; i < 6; ++i) c->srv_stage[i] += __atomic_load_n(&rs[4 + i], __ATOMIC_RELAXED);
+    ++c->srv_stamped;
+  }
+  return KSG_OK;
+}
+
+// Ends the resident server so other work can use the stream.
+int srv_stop(ksg_ctx* c) {
+  if (!c->srv_running) return KSG_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (hipStreamQuery(c->st) != hipSuccess) {
+    uint32_t hdr[KSG_SRV_HDR_DW] = {KSG_SRV_EXIT};
+    uint32_t r[4];
+    if (int rc = srv_call(c, hdr, r)) return rc;
+  }
+  c->srv_running = false;
+  c->pend_srv = false;  // (a pending begin is re-run by the launch-per-call commit)
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  return KSG_OK;
+}
+
+int srv_flush_patches(ksg_ctx* c) {
+  if (int rc = srv_alloc(c)) return rc;
+  size_t at = 0;
+  while (at < c->patches.size()) {
+    const uint32_t n = (uint32_t)std::min<size_t>(c->patches.size() - at, KSG_SRV_PATCHES);
+    memcpy(c->srv_box->patch, c->patches.data() + at, (size_t)n * sizeof(KsgPatch));
+    uint32_t hdr[KSG_SRV_HDR_DW] = {KSG_SRV_PATCH};
+    hdr[KSG_SRVH_NPATCH] = n;
+    uint32_t r[4];
+    if (int rc = srv_call(c, hdr, r)) return rc;
+    at += n;
+  }
+  c->patches.clear();
+  return KSG_OK;
+}
+
+// The pod, its ids [0, n_ids) and (extensions) its record as the request
+// payload; false if it does not fit the block + ext area.
+bool srv_put_pod(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, size_t n_ids, const ksg_pod_ext* ext,
+                 uint32_t* hdr) {
+  const uint32_t pod_dw = (uint32_t)(sizeof(ksg_pod) / 4), ext_dw = (uint32_t)(sizeof(ksg_pod_ext) / 4);
+  const uint32_t ids_at = pod_dw;
+  const uint32_t ext_at = (ids_at + (uint32_t)n_ids + 1) & ~1u;  // 8-byte aligned
+  const uint64_t paydw = ext ? (uint64_t)ext_at + ext_dw : (uint64_t)ids_at + n_ids;
+  if (paydw > KSG_SRV_PAY_DW) return false;
+  uint32_t* req = c->srv_box->req;
+  auto put = [&](uint32_t i, uint32_t v) {  // payload dword i
+    if (i < KSG_SRV_INLINE_DW) {
+      const uint32_t j = KSG_SRV_HDR_DW + i;
+      req[4 * (j / KSG_SRV_CHUNK_DW) + j % KSG_SRV_CHUNK_DW] = v;
+    } else {
+      c->srv_box->ext[i - KSG_SRV_INLINE_DW] = v;
+    }
+  };
+  const uint32_t* pw = reinterpret_cast<const uint32_t*>(pod);
+  for (uint32_t i = 0; i < pod_dw; ++i) put(i, pw[i]);
+  for (uint32_t i = 0; i < n_ids; ++i) put(ids_at + i, ids[i]);
+  if (ext) {
+    const uint32_t* ew = reinterpret_cast<const uint32_t*>(ext);
+    for (uint32_t i = 0; i < ext_dw; ++i) put(ext_at + i, ew[i]);
+  }
+  hdr[KSG_SRVH_PAYDW] = (uint32_t)paydw;
+  hdr[KSG_SRVH_IDS_AT] = ids_at;
+  hdr[KSG_SRVH_EXT_AT] = ext_at;
+  if (ext) hdr[KSG_SRVH_FLAGS] |= KSG_SRVF_EXT;
+  return true;
+}
+
 }  // namespace
 
 extern "C" {
@@ -806,6 +972,9 @@ static int create_impl(const ksg_config* cfg, int device, int rank, int world, c
       (e = hipEventCreateWithFlags(&c->ev_wait, hipEventDisableTiming)) != hipSuccess)
     return bail(fail(c, KSG_ERR_HIP, "stream/event: %s", hipGetErrorString(e)));
   c->spin_wait = !(getenv("KSG_SPIN_WAIT") && atoi(getenv("KSG_SPIN_WAIT")) == 0);
+  c->srv_enabled = !(getenv("KSG_SERVE") && atoi(getenv("KSG_SERVE")) == 0);
+  c->srv_stamps = getenv("KSG_SERVE_STAMPS") && atoi(getenv("KSG_SERVE_STAMPS")) != 0;
+  if (const char* iu = getenv("KSG_SERVE_IDLE_US")) c->srv_idle_us = (uint64_t)std::max(atoll(iu), 1LL);
   if (const char* rm = getenv("KSG_ROUND_MARGIN")) c->round_margin = std::min(std::max(atof(rm), 0.5), 4.0);
   // The exchange path (shard scan, all-gather of per-shard records, replicated
   // resolve) runs for world > 1, and for a 1-rank RCCL communicator when the caller
@@ -858,6 +1027,14 @@ int ksg_destroy(ksg_ctx* c) {
   }
   {
     KSG_LOCK(c);  // waits for a call in flight on another thread
+    (void)hipSetDevice(c->device);
+    (void)srv_stop(c);
+  }
+  if (c->srv_stamped) {
+    const double n = (double)c->srv_stamped;
+    fprintf(stderr, "ksg serve stamps (s_memtime cycles per begin, %llu begins): to-LDS %.0f check %.0f resolve %.0f "
+            "scan %.0f reduce %.0f fail-codes %.0f\n", (unsigned long long)c->srv_stamped, c->srv_stage[0] / n,
+            c->srv_stage[1] / n, c->srv_stage[2] / n, c->srv_stage[3] / n, c->srv_stage[4] / n, c->srv_stage[5] / n);
   }
   (void)hipSetDevice(c->device);
   if (c->st) (void)hipStreamSynchronize(c->st);
@@ -874,6 +1051,8 @@ int ksg_destroy(ksg_ctx* c) {
   if (c->h_up) (void)hipHostFree(c->h_up);
   if (c->h_dn) (void)hipHostFree(c->h_dn);
   if (c->h_map) (void)hipHostFree(c->h_map);
+  if (c->srv_box) (void)hipHostFree(c->srv_box);
+  if (c->srv_fail) (void)hipHostFree(c->srv_fail);
   if (c->h_xrecv) (void)hipHostFree(c->h_xrecv);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -891,6 +1070,7 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
                     uint32_t n_node_pairs, const uint32_t* pair_keys, uint32_t n_pairs, uint32_t n_services) {
   if (!c) return KSG_ERR_ARG;
   KSG_LOCK(c);
+  if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->st));
   if (n_nodes && !nodes) return fail(c, KSG_ERR_ARG, "nodes == NULL");
@@ -1266,6 +1446,7 @@ int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int6
   HIPCHK(c, hipSetDevice(c->device));
   if (c->pending) {  // the previous begin was abandoned: its queued updates apply now
     c->pending = false;
+    c->pend_srv = false;
     if (int rq = apply_queued(c)) return rq;
   }
   if (c->N == 0) return KSG_NONODES;
@@ -1273,6 +1454,35 @@ int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int6
   const size_t ext = call_ids_extent(c, pod);
   int rc = check_pod(c, pod, ids, ext);
   if (rc) return rc;
+  if (srv_eligible(c)) {  // the resident server: one request, no launch / copy / stream sync
+    uint32_t hdr[KSG_SRV_HDR_DW] = {KSG_SRV_BEGIN};
+    if ((rc = srv_alloc(c))) return rc;
+    // (an all-zero record for the plain entry point of an extensions context)
+    static const ksg_pod_ext zero_ext{};
+    const ksg_pod_ext* xr = c->ext_on ? (c->cur_ext ? c->cur_ext : &zero_ext) : nullptr;
+    if (srv_put_pod(c, pod, ids, ext, xr, hdr)) {
+      if ((rc = flush_patches(c)) || (!c->srv_running && (rc = srv_flush_patches(c)))) return rc;
+      if (fail_codes) hdr[KSG_SRVH_FLAGS] |= KSG_SRVF_WANT_FAIL;
+      uint32_t r[4];
+      if ((rc = srv_call(c, hdr, r))) return rc;
+      if (r[1] == KSG_SRV_BADREQ) return fail(c, KSG_ERR_STATE, "drop-in server rejected begin request");
+      if (r[1] == ~0u) return fail(c, KSG_ERR_NOPEER, "service affinity peer is not on a known node");
+      if (fail_codes) memcpy(fail_codes, c->srv_fail, (size_t)(c->hi - c->lo));
+      const int64_t m = (int64_t)((uint64_t)r[2] | ((uint64_t)r[3] << 32));
+      if (max_score) *max_score = r[1] > 0 ? m : 0;
+      if (tie_count) *tie_count = r[1];
+      if (r[1] == 0) return KSG_NOFIT;
+      c->pending = true;
+      c->pending_k = r[1];
+      c->pend = *pod;
+      c->pend_ids.assign(ids, ids + ext);
+      c->pend_srv = true;
+      c->srv_bseq = c->srv_seq;
+      memcpy(c->srv_bhdr, hdr, sizeof hdr);
+      return KSG_OK;
+    }
+  }
+  if ((rc = srv_stop(c))) return rc;
   if ((rc = flush_patches(c))) return rc;
   if ((rc = ensure_map(c)) || (rc = upload_one(c, pod, ids, ext))) return rc;
   if ((rc = scan_exchange(c, c->one_pod, c->one_ids, KSG_MODE_BEGIN, fail_codes ? c->d_fail : nullptr, nullptr)))
@@ -1303,8 +1513,25 @@ int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int6
 // the device half of a commit: decide the tie_index-th tie and apply AssumePod's delta
 static int commit_on_device(ksg_ctx* c, uint32_t tie_index, int32_t* node) {
   HIPCHK(c, hipSetDevice(c->device));
+  if (c->pend_srv) {  // served by the resident server: one request
+    c->pend_srv = false;
+    // the begin's payload layout (the payload itself is still in the block / ext area)
+    uint32_t hdr[KSG_SRV_HDR_DW];
+    memcpy(hdr, c->srv_bhdr, sizeof hdr);
+    hdr[KSG_SRVH_KIND] = KSG_SRV_COMMIT;
+    hdr[KSG_SRVH_BSEQ] = c->srv_bseq;
+    hdr[KSG_SRVH_TIE] = tie_index;
+    hdr[KSG_SRVH_FLAGS] &= ~KSG_SRVF_WANT_FAIL;
+    uint32_t r[4];
+    if (int rc = srv_call(c, hdr, r)) return rc;
+    if (r[1] == KSG_SRV_BADREQ) return fail(c, KSG_ERR_STATE, "drop-in server rejected commit request");
+    *node = (int32_t)r[1];
+    if (*node < 0) return fail(c, KSG_ERR_STATE, "commit selected no node (%d)", *node);
+    return KSG_OK;
+  }
   int rc = ensure_map(c);
   if (rc) return rc;
+  if ((rc = srv_stop(c))) return rc;
   // the pending pod is still in d_one (begin's upload; nothing re-uploads before the commit)
   HIPCHK(c, ksg_launch_decide(c->dev, c->one_pod, c->one_ids, rec_buf(c), c->rec_bytes, c->world,
                               c->d_shard_wlo, 2, tie_index, c->d_rng, reinterpret_cast<int32_t*>(c->d_map + 32), 0,
@@ -1338,6 +1565,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
                        uint64_t* rng_state, int32_t* out_nodes) {
   if (!c || (n && (!pods || !out_nodes)) || !rng_state) return KSG_ERR_ARG;
   KSG_LOCK(c);
+  if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
   if (int rs = cluster_ok(c)) return rs;
   if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
   HIPCHK(c, hipSetDevice(c->device));
@@ -1672,6 +1900,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
 int ksg_evaluate(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, uint8_t* fail_out, int64_t* score_out) {
   if (!c || !pod) return KSG_ERR_ARG;
   KSG_LOCK(c);
+  if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
   if (int rc0 = flush_deferred(c)) return rc0;
   if (int rs = cluster_ok(c)) return rs;
   if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
@@ -1742,9 +1971,20 @@ int ksg_last_batch_host_us(ksg_ctx* c, double* out8) {
   return KSG_OK;
 }
 
+int ksg_serve_stats(ksg_ctx* c, uint64_t* out4) {
+  if (!c || !out4) return KSG_ERR_ARG;
+  KSG_LOCK(c);
+  out4[0] = c->srv_launches;
+  out4[1] = c->srv_seq;
+  out4[2] = c->srv_running ? 1 : 0;
+  out4[3] = srv_eligible(c) ? 1 : 0;
+  return KSG_OK;
+}
+
 int ksg_debug_counters(ksg_ctx* c, int32_t* out32) {
   if (!c || !out32) return KSG_ERR_ARG;
   KSG_LOCK(c);
+  if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
   if (!c->dev.dbgbuf) return fail(c, KSG_ERR_STATE, "debug counters need KSG_DEBUG=8 at ksg_create");
   (void)hipSetDevice(c->device);
   HIPCHK(c, hipStreamSynchronize(c->st));
@@ -1770,6 +2010,7 @@ int ksg_shard(ksg_ctx* c, uint32_t* lo, uint32_t* hi) {
 int ksg_read_requested(ksg_ctx* c, int64_t* milli_cpu, int64_t* memory) {
   if (!c || !c->have_cluster) return KSG_ERR_ARG;
   KSG_LOCK(c);
+  if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
   HIPCHK(c, hipSetDevice(c->device));
   int rc = flush_patches(c);
   if (rc) return rc;
@@ -1787,6 +2028,7 @@ static int admit_impl(ksg_ctx* c, int mode, const ksg_admission_set* sets, uint3
                       uint8_t* out) {
   if (!c || (n_sets && !sets) || (n_pods && (!pods || !out))) return KSG_ERR_ARG;
   KSG_LOCK(c);
+  if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
   for (uint32_t s = 0; s < n_sets; ++s) {
     if ((uint64_t)sets[s].pod_off + sets[s].n_pods > n_pods)
       return fail(c, KSG_ERR_ARG, "admission set %u: pods out of range", s);
@@ -1839,6 +2081,7 @@ static int admit_impl(ksg_ctx* c, int mode, const ksg_admission_set* sets, uint3
 int ksg_set_extensions(ksg_ctx* c, const ksg_ext_config* e) {
   if (!c || !e) return KSG_ERR_ARG;
   KSG_LOCK(c);
+  if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
   if (c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_extensions: call before ksg_set_cluster");
   if (c->world > 1 || c->xchg) return fail(c, KSG_ERR_ARG, "extensions: one rank only");
   if ((e->filters & ~(KSG_EXT_TAINTS | KSG_EXT_SCALAR)) || e->n_scalar > KSG_MAX_SCALAR)
@@ -1852,6 +2095,7 @@ int ksg_set_node_ext(ksg_ctx* c, uint32_t n_nodes, const int64_t* scalar_cap, co
                      const uint32_t* taint_n, const uint32_t* taint_ids, uint32_t n_taint_ids) {
   if (!c) return KSG_ERR_ARG;
   KSG_LOCK(c);
+  if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
   if (!c->ext_on) return fail(c, KSG_ERR_STATE, "ksg_set_node_ext: extensions are off");
   if (!c->have_cluster || n_nodes != c->N) return fail(c, KSG_ERR_ARG, "ksg_set_node_ext: node count != cluster");
   if (int rc0 = flush_deferred(c)) return rc0;

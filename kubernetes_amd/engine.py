@@ -281,6 +281,12 @@ class DeviceScheduler:
                 "host_us": {k: float(v) for k, v in zip(self.HOST_PHASES, o[9:17])},
                 "wcap_sum": float(o[17])}
 
+    def serve_stats(self) -> dict:
+        """The resident begin/commit server (ksg_serve_stats)."""
+        o = np.zeros(4, np.uint64)
+        self._lib.ksg_serve_stats(self._ctx, abi.ptr(o))
+        return {"launches": int(o[0]), "requests": int(o[1]), "running": bool(o[2]), "eligible": bool(o[3])}
+
     def debug_counters(self) -> np.ndarray:
         """KSG_DEBUG=8 contexts: the window resolver's per-stage cycle counters
         (cycles / 64, summed over every window so far)."""

@@ -1,0 +1,144 @@
+"""The resident begin/commit server (ksg_serve.hip) against the C oracle.
+
+ksg_schedule_begin / ksg_schedule_commit on one rank are served by a resident
+workgroup polling mapped host memory. These sequences drive it through every
+request kind and hand-over: begin + commit with fail codes, abandoned begins,
+FitErrors, ksg_add_pod / ksg_remove_pod between pods (queued mirror patches
+applied by the server), ksg_evaluate and ksg_schedule_batch in the middle (the
+server leaves the stream and is relaunched), and an idle timeout short enough
+that the server returns between requests, including between a begin and its
+commit (the commit rescans the pod the host left in the request block). Every
+result is compared with the oracle: return code, max score, tie count, fail
+codes, chosen node, committed totals.
+"""
+import numpy as np
+import pytest
+
+from kubernetes_amd import abi
+from kubernetes_amd.engine import DeviceScheduler, PodBatch
+from oracle.pyoracle import OracleScheduler
+from tests.helpers import Case
+
+pytestmark = pytest.mark.gpu
+
+
+def _drive(case, dev, orc, seed, n_pods, *, evaluate_every=0, batch_at=(), churn=0.0, abandon=0.1):
+    rng = np.random.default_rng(seed)
+    n = case.view.arrays.n_nodes
+    live = []  # uids placed by commit / add_pod, removable
+    i = 0
+    while i < n_pods:
+        if i in batch_at:  # a short batch through the window path in between
+            sub = PodBatch(case.batch.pods[i:i + 40], case.batch.ids)
+            g, sg = dev.batch(sub, 1234 + i)
+            w, sw = orc.batch(sub, 1234 + i)
+            assert np.array_equal(g, w) and sg == sw, f"batch at {i}"
+            live.extend(int(case.batch.pods[i + q]["uid"]) for q in range(len(g)) if g[q] >= 0)
+            i += 40
+            continue
+        if evaluate_every and i % evaluate_every == 0:
+            rcg, fg, sg = dev.evaluate(case.batch, i)
+            rco, fo, so = orc.evaluate(case.batch, i)
+            assert rcg == rco and np.array_equal(fg, fo)
+            assert np.array_equal(sg[fg == 0], so[fo == 0])
+        if churn and rng.random() < churn:
+            if live and rng.random() < 0.5:
+                uid = live.pop(int(rng.integers(0, len(live))))
+                dev.remove_pod(uid)
+                orc.remove_pod(uid)
+            else:  # an existing pod reported by the store (some hosts are not nodes)
+                host = int(rng.integers(0, n + 3))
+                dev.add_pod(host, case.batch, i)
+                orc.add_pod(host, case.batch, i)
+                live.append(int(case.batch.pods[i]["uid"]))
+                i += 1
+                continue
+        want_fail = bool(rng.random() < 0.7)
+        rg, mg, kg, fg = dev.begin(case.batch, i, want_fail=want_fail)
+        ro, mo, ko, fo = orc.begin(case.batch, i, want_fail=want_fail)
+        assert (rg, kg) == (ro, ko), f"pod {i}: gpu {(rg, kg)} oracle {(ro, ko)}"
+        if want_fail:
+            assert np.array_equal(fg, fo), f"pod {i}: fail codes"
+        if rg == abi.KSG_OK:
+            assert mg == mo, f"pod {i}: max score"
+            if rng.random() < abandon:  # the next begin abandons this one
+                i += 1
+                continue
+            ix = int(rng.integers(0, kg))
+            ng, no = dev.commit(ix), orc.commit(ix)
+            assert ng == no, f"pod {i}: node gpu {ng} oracle {no}"
+            live.append(int(case.batch.pods[i]["uid"]))
+        i += 1
+    gc, gm = dev.read_requested()
+    wc, wm = orc.read_requested()
+    assert np.array_equal(gc, wc) and np.array_equal(gm, wm)
+
+
+@pytest.mark.parametrize("name,nn,npods", [
+    ("config1", 500, 500),     # R = 1, register-cached totals
+    ("config2", 2000, 500),    # R = 2
+    ("config2", 5000, 500),    # R = 8 (config 2's node count)
+    ("config4", 900, 400),     # ServiceAffinity + ServiceAntiAffinity
+    ("config3", 15000, 200),   # R = 16
+])
+def test_serve_begin_commit_matches_oracle(name, nn, npods):
+    case = Case(name, nn, npods)
+    dev = DeviceScheduler(case.cfg, device=0)
+    orc = OracleScheduler(case.cfg)
+    dev.set_cluster(case.view.arrays)
+    orc.set_cluster(case.view.arrays)
+    _drive(case, dev, orc, seed=nn + npods, n_pods=npods)
+    st = dev.serve_stats()
+    assert st["eligible"] and st["launches"] >= 1 and st["requests"] >= npods, st
+    dev.close()
+
+
+@pytest.mark.parametrize("name,nn,npods", [("config2", 1500, 400), ("config4", 700, 300)])
+def test_serve_interleaved_with_add_remove_evaluate_batch(name, nn, npods):
+    """Mirror patches through the server, and evaluate / batch taking the stream."""
+    case = Case(name, nn, npods)
+    dev = DeviceScheduler(case.cfg, device=0)
+    orc = OracleScheduler(case.cfg)
+    dev.set_cluster(case.view.arrays)
+    orc.set_cluster(case.view.arrays)
+    _drive(case, dev, orc, seed=5, n_pods=npods, evaluate_every=37, batch_at=(100, 250), churn=0.2)
+    st = dev.serve_stats()
+    assert st["launches"] >= 3, st  # relaunched after each evaluate / batch
+    dev.close()
+
+
+def test_serve_idle_timeout_relaunch(monkeypatch):
+    """A 1-us idle limit: the server returns between nearly every pair of
+    requests, between a begin and its commit too (the commit rescans)."""
+    monkeypatch.setenv("KSG_SERVE_IDLE_US", "1")
+    case = Case("config2", 1200, 300)
+    dev = DeviceScheduler(case.cfg, device=0)
+    orc = OracleScheduler(case.cfg)
+    dev.set_cluster(case.view.arrays)
+    orc.set_cluster(case.view.arrays)
+    _drive(case, dev, orc, seed=11, n_pods=300, churn=0.1)
+    st = dev.serve_stats()
+    assert st["launches"] > 100, st
+    dev.close()
+
+
+def test_serve_matches_launch_per_call_path(monkeypatch):
+    """KSG_SERVE=0 (round-2 path: scan + decide launches) and the server agree."""
+    case = Case("config2", 3000, 300)
+    devs = []
+    for serve in ("1", "0"):
+        monkeypatch.setenv("KSG_SERVE", serve)
+        d = DeviceScheduler(case.cfg, device=0)
+        d.set_cluster(case.view.arrays)
+        devs.append(d)
+    assert devs[0].serve_stats()["eligible"] and not devs[1].serve_stats()["eligible"]
+    rng = np.random.default_rng(2)
+    for i in range(300):
+        a = devs[0].begin(case.batch, i, want_fail=True)
+        b = devs[1].begin(case.batch, i, want_fail=True)
+        assert a[:3] == b[:3] and np.array_equal(a[3], b[3])
+        if a[0] == abi.KSG_OK:
+            ix = int(rng.integers(0, a[2]))
+            assert devs[0].commit(ix) == devs[1].commit(ix)
+    for d in devs:
+        d.close()

@@ -9,8 +9,10 @@
  * 100-500 milli-cpu / 128-640 MiB in 8 services, one host port on every 16th
  * pod; splitmix64 draws as in ksg_schedule_batch.
  *
- * Prints one JSON line: per-call latency percentiles (us) and pods/s.
- * usage: dropin_latency [n_nodes=5000] [n_pods=4000] [warmup=200] */
+ * Prints one JSON line: per-pod latency percentiles (us), pods/s, the begin
+ * and commit calls' own medians, and whether the resident server
+ * (ksg_serve.hip) served them (KSG_SERVE=0: kernels launched per call).
+ * usage: dropin_latency [n_nodes=5000] [n_pods=4000] [warmup=200] [want_fail=0] */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -50,6 +52,7 @@ int main(int argc, char** argv) {
   const uint32_t n_nodes = argc > 1 ? (uint32_t)atoi(argv[1]) : 5000;
   const uint32_t n_pods = argc > 2 ? (uint32_t)atoi(argv[2]) : 4000;
   const uint32_t warmup = argc > 3 ? (uint32_t)atoi(argv[3]) : 200;
+  const int want_fail = argc > 4 ? atoi(argv[4]) : 0;
   const uint32_t n_svc = 8;
   ksg_ctx* ctx = NULL;
 
@@ -92,6 +95,9 @@ int main(int argc, char** argv) {
   }
 
   double* lat = calloc(n_pods, sizeof *lat);
+  double* lat_b = calloc(n_pods, sizeof *lat_b);
+  double* lat_c = calloc(n_pods, sizeof *lat_c);
+  uint8_t* fails = calloc(n_nodes, 1);
   uint64_t rng = 0x5eed;
   uint32_t placed = 0, nofit = 0;
   double t_all = 0.0;
@@ -100,7 +106,9 @@ int main(int argc, char** argv) {
     uint32_t ties = 0;
     int32_t node = KSG_OUT_NOFIT;
     const double t0 = now_us();
-    CHECK(ksg_schedule_begin(ctx, &pods[i], ids + 2 * (size_t)i, &best, &ties, NULL));
+    const int rb = ksg_schedule_begin(ctx, &pods[i], ids + 2 * (size_t)i, &best, &ties, want_fail ? fails : NULL);
+    if (rb != KSG_OK && rb != KSG_NOFIT) CHECK(rb);
+    const double tb = now_us();
     if (ties > 0) {
       const uint64_t r = sm_next(&rng) >> 1;  /* rand.Int() */
       CHECK(ksg_schedule_commit(ctx, (uint32_t)(r % ties), &node));
@@ -108,19 +116,27 @@ int main(int argc, char** argv) {
     const double t1 = now_us();
     if (i >= warmup) {
       lat[i - warmup] = t1 - t0;
+      lat_b[i - warmup] = tb - t0;
+      lat_c[i - warmup] = t1 - tb;
       t_all += t1 - t0;
       if (node >= 0) ++placed;
       else ++nofit;
     }
   }
   qsort(lat, n_pods, sizeof *lat, cmp_d);
+  qsort(lat_b, n_pods, sizeof *lat_b, cmp_d);
+  qsort(lat_c, n_pods, sizeof *lat_c, cmp_d);
+  uint64_t sv[4] = {0, 0, 0, 0};
+  ksg_serve_stats(ctx, sv);
 #define PCT(q) lat[(size_t)((q) * (n_pods - 1))]
   printf("{\"metric\": \"drop-in per-pod latency (ksg_schedule_begin + ksg_schedule_commit, C caller)\", "
          "\"nodes\": %u, \"pods\": %u, \"warmup\": %u, \"placed\": %u, \"nofit\": %u, "
          "\"us_p50\": %.2f, \"us_p90\": %.2f, \"us_p99\": %.2f, \"us_max\": %.2f, \"us_mean\": %.2f, "
-         "\"pods_per_s\": %.1f, \"histogram_us\": {\"edges\": [5, 10, 20, 40, 80, 160, 320], \"counts\": [",
+         "\"pods_per_s\": %.1f, \"want_fail\": %d, \"begin_us_p50\": %.2f, \"commit_us_p50\": %.2f, "
+         "\"served\": {\"eligible\": %d, \"launches\": %llu, \"requests\": %llu}, \"histogram_us\": {\"edges\": [5, 10, 20, 40, 80, 160, 320], \"counts\": [",
          n_nodes, n_pods, warmup, placed, nofit, PCT(0.5), PCT(0.9), PCT(0.99), lat[n_pods - 1],
-         t_all / n_pods, n_pods / (t_all * 1e-6));
+         t_all / n_pods, n_pods / (t_all * 1e-6), want_fail, lat_b[n_pods / 2], lat_c[n_pods / 2], (int)sv[3],
+         (unsigned long long)sv[0], (unsigned long long)sv[1]);
   const double edges[] = {5, 10, 20, 40, 80, 160, 320, 1e30};
   size_t k = 0;
   for (int b = 0; b < 8; ++b) {
@@ -131,6 +147,9 @@ int main(int argc, char** argv) {
   printf("]}}\n");
   ksg_destroy(ctx);
   free(lat);
+  free(lat_b);
+  free(lat_c);
+  free(fails);
   free(ids);
   free(pods);
   free(nodes);
