@@ -173,6 +173,9 @@ def main():
                     help="add the extensions beyond this reference vintage (taints / tolerations, GPU and FPGA "
                          "counts, TaintToleration + BalancedResourceAllocation; parity unpinned, exact kernels), "
                          "reported as a separate workload (SURVEY.md section 0, item 2)")
+    ap.add_argument("--ext-filters-only", action="store_true",
+                    help="with --extensions: the filters only (taints, extended resources), TaintToleration and "
+                         "BalancedResourceAllocation weights 0, so batches take the window path")
     ap.add_argument("--no-stages", action="store_true",
                     help="skip the resolver's per-stage cycle breakdown (a second, untimed run with KSG_DEBUG=8)")
     args = ap.parse_args()
@@ -199,7 +202,9 @@ def main():
     if args.extensions:
         from kubernetes_amd.extensions import ExtInterner
 
-        ecfg, node_taints, node_scalar, tols, scal = workload.extension_data(n_nodes, n_pods)
+        fo = args.ext_filters_only
+        ecfg, node_taints, node_scalar, tols, scal = workload.extension_data(n_nodes, n_pods, w_taint=0 if fo else 1,
+                                                                             w_bal=0 if fo else 1)
         inter = ExtInterner(ecfg)
         node_arrays = inter.node_arrays(node_taints, node_scalar)
         rec, ids_x = inter.pod_records(batch.ids, tols, scal)
@@ -463,8 +468,10 @@ def main():
         "data": "synthetic (seeded splitmix64 scheduler_perf-style cluster; SURVEY.md 8(d))",
         "config": {"workload": f"{wl}: {n_nodes} nodes, {n_pods} pods, "
                                + ("DefaultProvider" if wl in ("config2", "config3", "config5") else wl)
-                               + (" + extensions (taints/tolerations, GPU/FPGA counts, TaintToleration, "
-                                  "BalancedResourceAllocation; parity unpinned, exact kernels)" if ext else ""),
+                               + ((" + extension filters (taints/tolerations, GPU/FPGA counts; scoring "
+                                   "extensions off; parity unpinned, window path)" if args.ext_filters_only else
+                                   " + extensions (taints/tolerations, GPU/FPGA counts, TaintToleration, "
+                                   "BalancedResourceAllocation; parity unpinned, exact kernels)") if ext else ""),
                    "nodes": n_nodes, "pods_per_step": args.batch,
                    "placed_in_timed": int((timed >= 0).sum()), "fit_errors_in_timed": int((timed == -1).sum()),
                    "snapshots_in_timed": wstats,

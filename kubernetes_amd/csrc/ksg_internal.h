@@ -45,6 +45,9 @@
 // largest capacity / requested total the window path accepts (lr_win's bound,
 // ksg_device.h)
 #define KSG_WIN_LR_BOUND (1LL << 49)
+// largest extended resource request the window path takes (a window's deltas
+// then fit int32: <= 4096 x 2^16)
+#define KSG_WIN_XREQ_BOUND (1LL << 16)
 
 struct KsgDev {
   // cluster geometry
@@ -133,9 +136,10 @@ struct KsgWinSum {
   int64_t memory;
   int32_t req_aff[KSG_MAX_AFF];  // resolved ServiceAffinity pairs
   uint16_t n_ports, n_pds, n_sel, n_svcs;
-  uint32_t pad;
+  uint32_t xmask;      // extensions: the extended resource kinds the pod requests (bit r: scalar[r] > 0)
   uint32_t ids[KSG_WIN_INLINE];  // ports, pds, sel, svcs (in that order)
-  uint32_t pad2[5];
+  int32_t xreq[4];     // extensions: the extended resource requests (the window path takes <= 2^16)
+  uint32_t pad2;
 };
 static_assert(sizeof(KsgWinSum) == 192, "KsgWinSum layout");
 #define KSG_WIN_SUM_DWORDS (sizeof(KsgWinSum) / 4)
@@ -173,6 +177,9 @@ struct KsgWinXchg {
   // the plain resolver (no ServiceAntiAffinity): per window pod, its T0 image
   // (ksg_plain.hip, ksg_win_t0_kernel) at img + pod * img_stride
   uint8_t* img;
+  // extensions (taints, extended resources; scoring extensions off): the batch's
+  // ksg_pod_ext records (pod pos + i of the window at exts[pos + i]), else nullptr
+  const ksg_pod_ext* exts;
   uint32_t img_stride;
   uint32_t rr;        // re-rank on (else a service's commit ends the window)
   uint32_t dz;        // domain rows: anti domains + 1 (<= KSG_RR_MAXZ)

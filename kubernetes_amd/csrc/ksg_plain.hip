@@ -274,6 +274,8 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   const bool res_on = (d.preds & KSG_PRED_PODFITSRESOURCES) != 0;
   const bool ports_on = (d.preds & KSG_PRED_PODFITSPORTS) != 0;
   const bool disk_on = (d.preds & KSG_PRED_NODISKCONFLICT) != 0;
+  // (extensions) extended resources: re-checked on the slots like cpu / memory
+  const bool xs_on = x.exts != nullptr && (d.ext_filters & KSG_EXT_SCALAR) && d.n_scalar > 0;
   const uint32_t nbits = (wcap + 31) / 32;
   // KSG_DEBUG bits 16..19: a fixed delay per pod in one wave role (committer,
   // x-checker, checkers, producers) to test the hand-offs under another
@@ -504,6 +506,9 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     S.inv_c = S.inv_m = 0.0;
     S.nk = S.ns = S.smask = 0;
     S.row = ~0u;
+    S.xk = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) S.xh[r] = S.xdl[r] = 0;
     // AssumePod of pod p (plugin/pkg/scheduler/scheduler.go:115-118) into the
     // owner lane's slot: requested totals, list lengths (the committer wrote the
     // lists into the table row) and the services' snapshot counts
@@ -538,6 +543,15 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         S.node = woff;
         S.dl_c = S.dl_m = 0;
         S.smask = 0;
+        S.xk = 0;
+        if (xs_on)  // (extensions) the node's extended resource headroom at the snapshot
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            S.xdl[r] = 0;
+            S.xh[r] = (uint32_t)r < d.n_scalar ? xhead(gld(d.scalar_cap + (size_t)r * d.n_nodes + wn),
+                                                       gld(d.scalar_used + (size_t)r * d.n_nodes + wn))
+                                               : 0;
+          }
       }
       uint32_t new_mask = 0;
       if (n_svcs) {
@@ -558,6 +572,10 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         S.nk = bnk + ppv.nk;
         S.ns = bns + n_svcs;
         S.smask |= new_mask;
+        S.xk |= ppv.xm;
+        if (xs_on)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) S.xdl[r] += (int32_t)__builtin_amdgcn_readlane(prec, WS_XREQ + r);
       }
     };
 
@@ -619,6 +637,12 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           const int64_t now_m = (int64_t)((uint64_t)S.snp_m + (uint64_t)S.dl_m);
           if (res_on && !pv.zero_req)  // PodFitsResources (predicates.go:127-145)
             drop = !((S.cap_c == 0 || S.cap_c - now_c >= pv.req_c) && (S.cap_m == 0 || S.cap_m - now_m >= pv.req_m));
+          if (S.xk & pv.xm)  // (extensions) extended resources: allocatable >= used + request
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int32_t q = (int32_t)__builtin_amdgcn_readlane(rec, WS_XREQ + r);
+              drop |= q > 0 && S.xh[r] - S.xdl[r] < q;
+            }
           if (d.w_lr) {  // LeastRequested (priorities.go:43-76) can only fall as requested grows
             const int32_t lr_now = lr_win(now_c + pv.req_c, S.cap_c, S.inv_c) + lr_win(now_m + pv.req_m, S.cap_m, S.inv_m);
             const int32_t lr_snap =
@@ -707,20 +731,29 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     // the committer's slot bookkeeping, replayed: lane l holds slots l and 64 + l
     // (node, list lengths, window delta after the commits replayed so far)
     uint32_t xcn0 = ~0u, xcn1 = ~0u, xsk0 = 0, xsk1 = 0, xss0 = 0, xss1 = 0, xn_slots = 0;
+    uint32_t xsx0 = 0, xsx1 = 0;  // (extensions) extended resource kinds the window took on the slot
+    int32_t xsd0[4] = {0, 0, 0, 0}, xsd1[4] = {0, 0, 0, 0};  // ... and its requests of each kind
     int64_t xdc0 = 0, xdm0 = 0, xdc1 = 0, xdm1 = 0;
     auto replay = [&](uint32_t node, uint32_t prec, uint32_t& slot, uint32_t& bnk, uint32_t& bns, uint64_t& dlc,
-                      uint64_t& dlm) {
+                      uint64_t& dlm, uint32_t& xk, int32_t (&xd)[4]) {
       const PodView ppv = pod_view(prec);
       const uint32_t p_svcs = (uint32_t)__builtin_amdgcn_readlane(prec, WS_NSS) >> 16;
       const uint64_t hit0 = __ballot(xcn0 == node), hit1 = __ballot(xcn1 == node);
       const bool in_c = (hit0 | hit1) != 0;
       bnk = bns = 0;
       dlc = dlm = 0;
+      xk = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xd[r] = 0;
       if (in_c) {
         slot = hit0 ? (uint32_t)__builtin_ctzll(hit0) : 64u + (uint32_t)__builtin_ctzll(hit1);
         const uint32_t sl = slot & 63;
         bnk = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? xsk0 : xsk1), (int)sl);
         bns = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? xss0 : xss1), (int)sl);
+        xk = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? xsx0 : xsx1), (int)sl);
+        if (xs_on)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xd[r] = __builtin_amdgcn_readlane(slot < 64 ? xsd0[r] : xsd1[r], (int)sl);
         dlc = readlane64((uint64_t)(slot < 64 ? xdc0 : xdc1), (int)sl);
         dlm = readlane64((uint64_t)(slot < 64 ? xdm0 : xdm1), (int)sl);
       } else {
@@ -728,17 +761,27 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       }
       dlc += (uint64_t)ppv.req_c;
       dlm += (uint64_t)ppv.req_m;
+      xk |= ppv.xm;
+      if (xs_on)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xd[r] += (int32_t)__builtin_amdgcn_readlane(prec, WS_XREQ + r);
       if (lane == (slot & 63)) {
         if (slot >= 64) {
           if (!in_c) xcn1 = node;
           xsk1 = bnk + ppv.nk;
           xss1 = bns + p_svcs;
+          xsx1 = xk;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xsd1[r] = xd[r];
           xdc1 = (int64_t)dlc;
           xdm1 = (int64_t)dlm;
         } else {
           if (!in_c) xcn0 = node;
           xsk0 = bnk + ppv.nk;
           xss0 = bns + p_svcs;
+          xsx0 = xk;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xsd0[r] = xd[r];
           xdc0 = (int64_t)dlc;
           xdm0 = (int64_t)dlm;
         }
@@ -856,6 +899,11 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       // the bookkeeping below)
       int64_t capv = 0, usev = 0;
       double invv = 0.0;
+      // (extensions) lane r < 4: x's headroom of extended resource r at the snapshot
+      const bool xk_chk = do_check && xs_on && pv.xm != 0;
+      int32_t xhv = 0;
+      if (xk_chk && lane < d.n_scalar)
+        xhv = xhead(gld(d.scalar_cap + (size_t)lane * d.n_nodes + xw), gld(d.scalar_used + (size_t)lane * d.n_nodes + xw));
       if (do_check) {
         if (xcid < KSG_NCAND) {
           const uint64_t* cs = r_csnap + (ep * KSG_NCAND + xcid) * 6;
@@ -869,9 +917,10 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         }
       }
       // commit i-1 into its slot (the committer's bookkeeping, replayed)
-      uint32_t xslot = 0, bnk = 0, bns = 0;
+      uint32_t xslot = 0, bnk = 0, bns = 0, xkinds = 0;
+      int32_t xdl[4];
       uint64_t dlc = 0, dlm = 0;
-      if (xnode != ~0u) replay(xnode, prec, xslot, bnk, bns, dlc, dlm);
+      if (xnode != ~0u) replay(xnode, prec, xslot, bnk, bns, dlc, dlm, xkinds, xdl);
       if (do_check) {
         // pod i-1's record: its keys and service ids follow the earlier commits' in the slot's lists
         const uint32_t pnpp = __builtin_amdgcn_readlane(prec, WS_NPP), pnss = __builtin_amdgcn_readlane(prec, WS_NSS);
@@ -932,6 +981,11 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           }
           xd |= __ballot(hit) != 0;
         }
+        if (xk_chk && (xkinds & pv.xm)) {  // (extensions) extended resources, lane r: kind r
+          const int32_t q = __shfl((int)rec, (int)(WS_XREQ + (lane & 3)), 64);  // (a per-lane source: not readlane)
+          const int32_t dl = (lane & 3) == 0 ? xdl[0] : (lane & 3) == 1 ? xdl[1] : (lane & 3) == 2 ? xdl[2] : xdl[3];
+          xd |= (__ballot(lane < 4 && q > 0 && xhv - dl < q) & 15ULL) != 0;
+        }
         res = (xd ? 1u : 0u) | (flag_x ? 2u : 0u);
       }
       if (lane == 0) {
@@ -963,9 +1017,10 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       const uint32_t node = __builtin_amdgcn_readfirstlane(L_cm[q].node);
       const uint32_t cid = (__builtin_amdgcn_readfirstlane(L_cm[q].flags) >> 1) & 7u;
       const uint32_t prec = lane < DW ? r_rec[(q % RING) * DW + lane] : 0u;
-      uint32_t slot, bnk, bns;
+      uint32_t slot, bnk, bns, xk;
+      int32_t xd[4];
       uint64_t dlc, dlm;
-      replay(node, prec, slot, bnk, bns, dlc, dlm);
+      replay(node, prec, slot, bnk, bns, dlc, dlm, xk, xd);
       flags(q, node, cid, slot, bns, prec);
     }
     if constexpr (STAMP) {
@@ -1106,6 +1161,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       reason = KSG_STOP_SERVICE;
       break;
     }
+
     // x counts as a new drop iff it is a snapshot tie whose slot the checkers
     // kept (a new slot: they have not seen it)
     const bool x_kept = !(((xslot < 64 ? msk0 : msk1) >> (xslot & 63)) & 1ULL);
@@ -1266,6 +1322,20 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   for (uint32_t t = lane; t < resolved; t += 64) out[t] = L_out[t];
+  if (x.exts && (d.ext_filters & KSG_EXT_SCALAR)) {
+    // (extensions) the window's extended resource requests into the node state
+    // (the checkers wrote cpu / memory back; these live in no slot)
+    for (uint32_t t = lane; t < resolved; t += 64) {
+      if (L_cm[t].kind != 1) continue;
+      const ksg_pod_ext& pe = x.exts[pos + t];
+      const uint32_t wn = d.lo + L_cm[t].node;
+      for (uint32_t r = 0; r < d.n_scalar; ++r)
+        if (pe.scalar[r] != 0)
+          __hip_atomic_fetch_add(reinterpret_cast<uint64_t*>(d.scalar_used + (size_t)r * d.n_nodes + wn),
+                                 (uint64_t)pe.scalar[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    drain_stores();
+  }
   if (lane == 0) {
     *rng_io = rng0 + (uint64_t)n_draws * 0x9E3779B97F4A7C15ULL;
     if (reason == KSG_STOP_HANG) {

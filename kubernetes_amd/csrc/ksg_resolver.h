@@ -20,7 +20,9 @@
 #define WS_AFF 12
 #define WS_NPP 16
 #define WS_NSS 17
+#define WS_XM 18   // extended resource kinds the pod requests (extensions)
 #define WS_IDS 19
+#define WS_XREQ 43 // its extended resource requests (4 dwords)
 
 // threads of the resolver workgroup: 8 waves
 // (16 waves for P <= 8 measured no faster than 8: the chain, not the producers, limits)
@@ -258,6 +260,7 @@ struct PodView {
   bool zero_req;
   uint32_t n_ports, n_pds, nk;
   int32_t s, smax;
+  uint32_t xm;  // extended resource kinds requested (extensions; 0 otherwise)
 };
 
 // Does slot `sl` (a snapshot tie of the pod) score below M0 once the window's
@@ -363,6 +366,7 @@ __device__ __forceinline__ PodView pod_view(uint32_t rec) {
   pv.nk = pv.n_ports + pv.n_pds;
   pv.s = (int32_t)__builtin_amdgcn_readlane(rec, WS_SVC);
   pv.smax = (int32_t)__builtin_amdgcn_readlane(rec, WS_SMAX);
+  pv.xm = (uint32_t)__builtin_amdgcn_readlane(rec, WS_XM);
   return pv;
 }
 
@@ -380,4 +384,14 @@ struct RegSlot {
   double inv_c, inv_m;
   uint32_t nk, ns, smask;  // list lengths as of the commits this checker applied
   uint32_t row;            // (ServiceAntiAffinity re-rank) the node's domain row, ~0u unlabelled
+  uint32_t xk;             // (extensions) extended resource kinds the window's commits requested here
+  int32_t xh[4];           // (extensions) allocatable - requested at the snapshot, clamped to int32
+  int32_t xdl[4];          // (extensions) the window's requests here (<= 4096 x 2^16)
 };
+// allocatable - requested of an extended resource at the snapshot, clamped to
+// int32: with a window's deltas <= 2^28 and requests <= 2^16 every fit test
+// h - delta >= request decides as the unclamped one does
+__device__ __forceinline__ int32_t xhead(int64_t cap, int64_t used) {
+  const int64_t h = (int64_t)((uint64_t)cap - (uint64_t)used);
+  return h > 0x7fffffffLL ? 0x7fffffff : h < -0x80000000LL ? (int32_t)0x80000000 : (int32_t)h;
+}

@@ -44,7 +44,7 @@ hipError_t ksg_launch_scan(int R, bool anti, const KsgDev& d, const ksg_pod* pod
 hipError_t ksg_launch_win_eval(const KsgDev& d, int mode, const ksg_pod* batch, const uint32_t* ids,
                                const KsgWinRun* run, uint32_t wcap, KsgWinSum* sums, uint64_t* wbits, int32_t* wmax,
                                uint32_t ostride, int32_t* dcnt, uint64_t* wfit, int32_t* dmb, uint64_t* wbz,
-                               uint32_t dz, hipStream_t st);
+                               uint32_t dz, hipStream_t st, const ksg_pod_ext* exts = nullptr);
 hipError_t ksg_launch_zonemap(uint32_t n_nodes, const int32_t* anti_domain, uint32_t d0, uint32_t nw,
                               uint64_t* zmap, hipStream_t st);
 hipError_t ksg_launch_win_t0(const KsgDev& d, uint32_t wcap, const KsgWinRun* run, const KsgWinXchg& x,
@@ -659,7 +659,19 @@ KsgDev full_geometry(const ksg_ctx* c) {
 
 bool use_window(ksg_ctx* c, const ksg_pod* pods, uint32_t n) {
   if (c->window == 0 || c->nw > 32 * 64 || ksg_win_max_window(full_geometry(c)) < 8) return false;
-  if (c->ext_on) return false;  // extensions run on the exact kernels only
+  // extensions: the filters only (PodToleratesNodeTaints is static per (pod,
+  // node); extended resources only shrink under commits and the resolver
+  // re-checks them on the window's committed nodes like cpu / memory).
+  // TaintToleration and BalancedAllocation scores (the latter can rise on a
+  // committed node), negative requests and requests past 2^16 take the exact
+  // kernels.
+  if (c->ext_on) {
+    if (c->ext.w_taint_toleration != 0 || c->ext.w_balanced != 0 || anti_on(c) || (c->dev.dbg & 128)) return false;
+    if (c->cur_ext)
+      for (uint32_t i = 0; i < n; ++i)
+        for (uint32_t r = 0; r < c->ext.n_scalar; ++r)
+          if (c->cur_ext[i].scalar[r] < 0 || c->cur_ext[i].scalar[r] > KSG_WIN_XREQ_BOUND) return false;
+  }
   // int64 combined scores / more anti-affinity priorities than phase A keeps in registers
   if (c->dev.wide || c->dev.n_anti > KSG_WIN_MAX_ANTI) return false;
   // monotonicity under commits needs non-negative pod-dependent weights
@@ -1650,6 +1662,16 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
   c->last_kms[0] = c->last_kms[1] = c->last_kms[2] = 0;
   c->last_wsum = 0;
   hphase(1);
+  const ksg_pod_ext* dext = nullptr;
+  if (c->ext_on) {  // extensions: each pod's record (all-zero for the plain entry point)
+    if ((rc = grow(c, (void**)&c->d_pext, &c->pext_cap, n, sizeof(ksg_pod_ext)))) return rc;
+    if (c->cur_ext) {
+      HIPCHK(c, hipMemcpyAsync(c->d_pext, c->cur_ext, (size_t)n * sizeof(ksg_pod_ext), hipMemcpyHostToDevice, c->st));
+    } else {
+      HIPCHK(c, hipMemsetAsync(c->d_pext, 0, (size_t)n * sizeof(ksg_pod_ext), c->st));
+    }
+    dext = c->d_pext;
+  }
   if (use_window(c, pods, n)) {
     // Window path. Phase A scores the window on this rank's shard; with world > 1
     // the per-word results are all-gathered once per window (not per pod) and
@@ -1667,6 +1689,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       W = std::min(W, std::max<uint32_t>(want, 16u));
     }
     KsgWinXchg x{};
+    x.exts = dext;  // (extensions: the filters; use_window keeps the scores off this path)
     x.ostride = std::max<uint32_t>(c->nwords_max, 1);
     x.wcap = W;
     x.world = (uint32_t)c->world;
@@ -1763,7 +1786,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
                                       wmax, x.ostride, c->d_dcnt,
                                       anti ? reinterpret_cast<uint64_t*>(c->d_xsend + fit_off) : nullptr, x.dmb,
                                       rr ? reinterpret_cast<uint64_t*>(c->d_xsend + x.b_off) : nullptr, x.dz,
-                                      c->st));
+                                      c->st, dext));
         if (c->xchg && (rc = allgather(c, c->d_xsend, c->d_xrecv, x.blk))) return rc;
         if (plain) HIPCHK(c, ksg_launch_win_t0(full, W, c->d_run, x, c->st));
         if (evk) HIPCHK(c, hipEventRecord(c->wev[2 * k + 1], c->st));
@@ -1816,7 +1839,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
         // a pod whose id lists exceed the window record: the exact per-pod path
         if (!c->xchg) {
           HIPCHK(c, ksg_launch_batch(c->R, anti, c->dev, c->d_pods + pos, c->d_ids, 1, c->d_rng,
-                                     c->d_out + pos, c->st));
+                                     c->d_out + pos, c->st, dext ? dext + pos : nullptr));
         } else {
           if ((rc = scan_exchange(c, c->d_pods + pos, c->d_ids, KSG_MODE_BEGIN, nullptr, nullptr))) return rc;
           HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods + pos, c->d_ids, rec_buf(c), c->rec_bytes, c->world,
@@ -1830,16 +1853,6 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       hphase(2);
     }
   } else if (!c->xchg) {
-    const ksg_pod_ext* dext = nullptr;
-    if (c->ext_on) {  // extensions: each pod's record (all-zero for the plain entry point)
-      if ((rc = grow(c, (void**)&c->d_pext, &c->pext_cap, n, sizeof(ksg_pod_ext)))) return rc;
-      if (c->cur_ext) {
-        HIPCHK(c, hipMemcpyAsync(c->d_pext, c->cur_ext, (size_t)n * sizeof(ksg_pod_ext), hipMemcpyHostToDevice, c->st));
-      } else {
-        HIPCHK(c, hipMemsetAsync(c->d_pext, 0, (size_t)n * sizeof(ksg_pod_ext), c->st));
-      }
-      dext = c->d_pext;
-    }
     HIPCHK(c, ksg_launch_batch(c->R, anti_on(c), c->dev, c->d_pods, c->d_ids, n, c->d_rng, c->d_out, c->st, dext));
   } else {
     for (uint32_t i = 0; i < n; ++i) {

@@ -71,7 +71,10 @@
 #define KSG_WIN_PLAIN 0
 #define KSG_WIN_COUNT 1
 #define KSG_WIN_ANTI 2
-template <int MODE, int KSG_PG>
+// EXT: the extensions' filters (PodToleratesNodeTaints: static per (pod, node);
+// extended resources: allocatable >= used + request, monotone under commits
+// like cpu / memory), MODE PLAIN only
+template <int MODE, int KSG_PG, bool EXT = false>
 __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, const ksg_pod* __restrict__ batch,
                                                                  const uint32_t* __restrict__ ids,
                                                                  const KsgWinRun* __restrict__ run, uint32_t wcap,
@@ -81,7 +84,8 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
                                                                  int32_t* __restrict__ dcnt,
                                                                  uint64_t* __restrict__ wfit,
                                                                  int32_t* __restrict__ dmb,
-                                                                 uint64_t* __restrict__ wbz, uint32_t dz) {
+                                                                 uint64_t* __restrict__ wbz, uint32_t dz,
+                                                                 const ksg_pod_ext* __restrict__ exts) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (KSG_SC_NT / 64) + (threadIdx.x >> 6));
   const uint32_t p0 = blockIdx.y * KSG_PG;
@@ -112,6 +116,15 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
     if (d.has_static_score) sst = (int32_t)d.static_score[n];  // (window path: |score| < KSG_SCORE_BOUND)
   }
   const double inv_c = lr_inv10(capc), inv_m = lr_inv10(capm);
+  // extended resources of this lane's node
+  const bool xs_on = EXT && (d.ext_filters & KSG_EXT_SCALAR) && d.n_scalar > 0;
+  int64_t xcap[KSG_MAX_SCALAR], xuse[KSG_MAX_SCALAR];
+#pragma unroll
+  for (int r = 0; r < KSG_MAX_SCALAR; ++r) {
+    const bool on = xs_on && valid && (uint32_t)r < d.n_scalar;
+    xcap[r] = on ? d.scalar_cap[(size_t)r * d.n_nodes + n] : 0;
+    xuse[r] = on ? d.scalar_used[(size_t)r * d.n_nodes + n] : 0;
+  }
 
   // ---- lane j < np: pod p0+j's context and its fit word for this node word
   uint64_t fm = 0;
@@ -120,9 +133,21 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
   PodCtx c;
   // lane j < np: pod j's list lengths (ports, pds, sel, svcs) and offsets, for its record
   uint32_t q_n[4] = {0, 0, 0, 0}, q_off[4] = {0, 0, 0, 0};
+  int64_t xreq[KSG_MAX_SCALAR] = {0, 0, 0, 0};  // lane j: pod j's extended resource requests
+  uint32_t xmask = 0;
   if (lane < np) {
     const ksg_pod& p = pods[p0 + lane];
     pod_resolve<false>(d, p, ids, c);
+    if constexpr (EXT) {
+      const ksg_pod_ext& pe = exts[pos + p0 + lane];
+      if (xs_on)
+#pragma unroll
+        for (int r = 0; r < KSG_MAX_SCALAR; ++r)
+          if ((uint32_t)r < d.n_scalar) {
+            xreq[r] = pe.scalar[r];
+            xmask |= xreq[r] > 0 ? 1u << r : 0u;
+          }
+    }
     if (w == 0) {
       q_n[0] = p.n_ports; q_n[1] = p.n_pds; q_n[2] = p.n_sel; q_n[3] = p.n_svcs;
       q_off[0] = p.ports_off; q_off[1] = p.pds_off; q_off[2] = p.sel_off; q_off[3] = p.svcs_off;
@@ -144,6 +169,11 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
 #pragma unroll
       for (uint32_t j = 0; j < KSG_MAX_AFF; ++j)
         if (j < d.n_aff && c.req_aff[j] >= 0) m &= d.pairmap[(size_t)c.req_aff[j] * d.nw + gw];
+    }
+    if constexpr (EXT) {  // PodToleratesNodeTaints: an untolerated NoSchedule / NoExecute taint
+      const ksg_pod_ext& pe = exts[pos + p0 + lane];
+      if (d.ext_filters & KSG_EXT_TAINTS)
+        for (uint32_t t = 0; t < pe.n_hard; ++t) m &= ~d.taintmap[(size_t)ids[pe.hard_off + t] * d.nw + gw];
     }
     }
     fm = m;
@@ -231,6 +261,14 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
         const bool fc = capc == 0 || (int64_t)((uint64_t)capc - (uint64_t)usedc) >= rcj;
         const bool fmm = capm == 0 || (int64_t)((uint64_t)capm - (uint64_t)usedm) >= rmj;
         fit = fit && fc && fmm;
+      }
+      if constexpr (EXT) {  // PodFitsResources' extended resources: allocatable >= used + request
+        if (xs_on)
+#pragma unroll
+          for (int r = 0; r < KSG_MAX_SCALAR; ++r) {
+            const int64_t q = (int64_t)readlane64((uint64_t)xreq[r], j);
+            if ((uint32_t)r < d.n_scalar && q > 0 && xcap[r] < (int64_t)((uint64_t)xuse[r] + (uint64_t)q)) fit = false;
+          }
       }
       if constexpr (MODE == KSG_WIN_COUNT) {
         if (dmb) {
@@ -348,6 +386,9 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
       S->n_pds = (uint16_t)p.n_pds;
       S->n_sel = (uint16_t)p.n_sel;
       S->n_svcs = (uint16_t)p.n_svcs;
+      S->xmask = xmask;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) S->xreq[r] = r < KSG_MAX_SCALAR ? (int32_t)xreq[r] : 0;
     }
     // the pods' inline id lists: lane t takes entry t of every pod of the group,
     // all loads issued before the first store (not one pod's round trip after
@@ -2871,15 +2912,21 @@ static const size_t kWinLdsBudget = 156 * 1024;
 hipError_t ksg_launch_win_eval(const KsgDev& d, int mode, const ksg_pod* batch, const uint32_t* ids,
                                const KsgWinRun* run, uint32_t wcap, KsgWinSum* sums, uint64_t* wbits, int32_t* wmax,
                                uint32_t ostride, int32_t* dcnt, uint64_t* wfit, int32_t* dmb, uint64_t* wbz,
-                               uint32_t dz, hipStream_t st) {
+                               uint32_t dz, hipStream_t st, const ksg_pod_ext* exts) {
   const uint32_t gx = std::max<uint32_t>(1, (d.nwords + KSG_SC_NT / 64 - 1) / (KSG_SC_NT / 64));
   const bool small = d.nwords < KSG_PG_WORDS;
   const uint32_t pg = small ? KSG_PG_SMALL : KSG_PG_LARGE;
   const dim3 grid(gx, (wcap + pg - 1) / pg);
 #define KSG_EVAL_LAUNCH(M, G)                                                                                    \
   hipLaunchKernelGGL((ksg_win_score_kernel<M, G>), grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, run, wcap, sums, \
-                     wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz)
-  if (mode == KSG_WIN_COUNT) {
+                     wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz, nullptr)
+#define KSG_EVAL_LAUNCH_X(G)                                                                              \
+  hipLaunchKernelGGL((ksg_win_score_kernel<KSG_WIN_PLAIN, G, true>), grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, \
+                     run, wcap, sums, wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz, exts)
+  if (exts) {  // extensions (plain mode only: the host keeps ServiceAntiAffinity off this path)
+    if (small) KSG_EVAL_LAUNCH_X(KSG_PG_SMALL);
+    else KSG_EVAL_LAUNCH_X(KSG_PG_LARGE);
+  } else if (mode == KSG_WIN_COUNT) {
     if (small) KSG_EVAL_LAUNCH(KSG_WIN_COUNT, KSG_PG_SMALL);
     else KSG_EVAL_LAUNCH(KSG_WIN_COUNT, KSG_PG_LARGE);
   } else if (mode == KSG_WIN_ANTI) {
@@ -2890,6 +2937,7 @@ hipError_t ksg_launch_win_eval(const KsgDev& d, int mode, const ksg_pod* batch, 
     else KSG_EVAL_LAUNCH(KSG_WIN_PLAIN, KSG_PG_LARGE);
   }
 #undef KSG_EVAL_LAUNCH
+#undef KSG_EVAL_LAUNCH_X
   return hipGetLastError();
 }
 

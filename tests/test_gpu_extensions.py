@@ -1,7 +1,12 @@
-"""Extensions beyond the reference vintage on the device (exact kernels) against
-the C restatement, bit-exact. PARITY UNPINNED with respect to any reference
-(none exists for these): the oracle restates the
-published v1.10 algorithms (kubernetes_amd/extensions.py)."""
+"""Extensions beyond the reference vintage on the device against the C
+restatement, bit-exact. PARITY UNPINNED with respect to any reference (none
+exists for these): the oracle restates the
+published v1.10 algorithms (kubernetes_amd/extensions.py).
+
+With TaintToleration and BalancedAllocation scoring on, batches run on the exact
+kernels; with them off (the filters only: PodToleratesNodeTaints, extended
+resources) on the window path, whose resolver ends a window at a pod one of
+whose snapshot ties took an extended resource it requests."""
 import numpy as np
 import pytest
 
@@ -34,7 +39,54 @@ def test_batch_with_extensions_matches_oracle(name, nn, npods, kw):
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, f"first mismatches at {bad[:8]}: gpu {got[bad[:8]]} oracle {want[bad[:8]]}"
     assert sg == sw
-    assert dev.last_batch_stats()["windows"] == 0  # extensions run on the exact kernels
+    # TaintToleration / BalancedAllocation scores: the exact kernels
+    assert dev.last_batch_stats()["windows"] == 0
+    gc, gm = dev.read_requested()
+    wc, wm = orc.read_requested()
+    assert np.array_equal(gc, wc) and np.array_equal(gm, wm)
+    dev.close()
+
+
+@pytest.mark.parametrize("window", [5, 64, 128])
+@pytest.mark.parametrize("name,nn,npods,kw", [
+    ("config2", 700, 1500, dict()),
+    ("config2", 60, 600, dict()),                  # GPUs run out: contention stops and FitErrors
+    ("config2", 5000, 1200, dict()),
+    ("config2", 300, 500, dict(taints=False)),
+    ("config1", 2000, 800, dict(gpus=False)),      # taints only
+])
+def test_window_path_with_extension_filters_matches_oracle(name, nn, npods, kw, window):
+    """Scoring extensions off: the window path, in two batches (the second one
+    sees the first one's extended resources written back), then removals."""
+    c = ExtCase(name, nn, npods, w_taint=0, w_bal=0, **kw)
+    dev = c.load(DeviceScheduler(c.cfg, device=0))
+    dev.set_window(window)
+    orc = c.load(OracleScheduler(c.cfg))
+    for i in range(0, 60, 3):  # placed pods with extended resource requests
+        dev.add_pod(i % nn, c.batch, i)
+        orc.add_pod(i % nn, c.batch, i)
+    half = 60 + (npods - 60) // 2
+    rng = 77
+    for lo, hi in ((60, half), (half, npods)):
+        sub = PodBatch(c.batch.pods[lo:hi], c.batch.ids, c.batch.ext[lo:hi])
+        got, sg = dev.batch(sub, rng)
+        want, sw = orc.batch(sub, rng)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, f"[{lo}:{hi}] first mismatches at {bad[:8]}: gpu {got[bad[:8]]} oracle {want[bad[:8]]}"
+        assert sg == sw
+        assert dev.last_batch_stats()["windows"] > 0  # the window path took it
+        rng = sg
+    for q in range(0, len(want), 9):  # removals give the pods' GPUs back (host mirror replay)
+        if want[q] >= 0:
+            uid = int(c.batch.pods[half + q]["uid"])
+            dev.remove_pod(uid)
+            orc.remove_pod(uid)
+    tail = PodBatch(c.batch.pods[:60], c.batch.ids, c.batch.ext[:60])  # uids 0..59 are placed: new uids
+    tail.pods = tail.pods.copy()
+    tail.pods["uid"] += 10_000_000
+    got, sg = dev.batch(tail, rng)
+    want, sw = orc.batch(tail, rng)
+    assert np.array_equal(got, want) and sg == sw
     gc, gm = dev.read_requested()
     wc, wm = orc.read_requested()
     assert np.array_equal(gc, wc) and np.array_equal(gm, wm)
