@@ -265,7 +265,8 @@ int ksg_last_batch_ms(ksg_ctx* ctx, double* ms);
 
 /* Window path of the last ksg_schedule_batch: out3[0] = device ms in the
  * snapshot-scoring kernel(s) (ksg_win_score_kernel), out3[1] = device ms in the
- * resolver (ksg_win_resolve_kernel), out3[2] = resolver launches (windows are
+ * resolver (ksg_win_plain_kernel, or with ServiceAntiAffinity
+ * ksg_win_resolve2_kernel / ksg_win_resolve_kernel), out3[2] = resolver launches (windows are
  * chained on the device, so a round may end with launches that find the batch
  * done and return at once); from HIP events recorded on the context's stream
  * around every 4th launch of a round, the sampled positions rotating from round

@@ -227,7 +227,10 @@ __global__ __launch_bounds__(256) void ksg_win_t0_kernel(uint32_t nwords, uint32
   }
 }
 
-template <int P, bool STAMP>
+// XS: extended resources re-checked on the slots (extensions; a separate
+// instantiation: their per-slot state would cost every other configuration
+// registers on the chain)
+template <int P, bool STAMP, bool XS>
 __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
                                                             const KsgWinSum* __restrict__ sums, const KsgWinXchg x,
                                                             uint64_t* rng_io, int32_t* __restrict__ out_batch) {
@@ -275,7 +278,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   const bool ports_on = (d.preds & KSG_PRED_PODFITSPORTS) != 0;
   const bool disk_on = (d.preds & KSG_PRED_NODISKCONFLICT) != 0;
   // (extensions) extended resources: re-checked on the slots like cpu / memory
-  const bool xs_on = x.exts != nullptr && (d.ext_filters & KSG_EXT_SCALAR) && d.n_scalar > 0;
+  constexpr bool xs_on = XS;
   const uint32_t nbits = (wcap + 31) / 32;
   // KSG_DEBUG bits 16..19: a fixed delay per pod in one wave role (committer,
   // x-checker, checkers, producers) to test the hand-offs under another
@@ -572,10 +575,11 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         S.nk = bnk + ppv.nk;
         S.ns = bns + n_svcs;
         S.smask |= new_mask;
-        S.xk |= ppv.xm;
-        if (xs_on)
+        if (XS) {
+          S.xk |= ppv.xm;
 #pragma unroll
           for (int r = 0; r < 4; ++r) S.xdl[r] += (int32_t)__builtin_amdgcn_readlane(prec, WS_XREQ + r);
+        }
       }
     };
 
@@ -637,7 +641,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           const int64_t now_m = (int64_t)((uint64_t)S.snp_m + (uint64_t)S.dl_m);
           if (res_on && !pv.zero_req)  // PodFitsResources (predicates.go:127-145)
             drop = !((S.cap_c == 0 || S.cap_c - now_c >= pv.req_c) && (S.cap_m == 0 || S.cap_m - now_m >= pv.req_m));
-          if (S.xk & pv.xm)  // (extensions) extended resources: allocatable >= used + request
+          if (XS && (S.xk & pv.xm))  // (extensions) extended resources: allocatable >= used + request
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int32_t q = (int32_t)__builtin_amdgcn_readlane(rec, WS_XREQ + r);
@@ -750,7 +754,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         const uint32_t sl = slot & 63;
         bnk = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? xsk0 : xsk1), (int)sl);
         bns = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? xss0 : xss1), (int)sl);
-        xk = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? xsx0 : xsx1), (int)sl);
+        if (XS) xk = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? xsx0 : xsx1), (int)sl);
         if (xs_on)
 #pragma unroll
           for (int r = 0; r < 4; ++r) xd[r] = __builtin_amdgcn_readlane(slot < 64 ? xsd0[r] : xsd1[r], (int)sl);
@@ -761,10 +765,11 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       }
       dlc += (uint64_t)ppv.req_c;
       dlm += (uint64_t)ppv.req_m;
-      xk |= ppv.xm;
-      if (xs_on)
+      if (XS) {
+        xk |= ppv.xm;
 #pragma unroll
         for (int r = 0; r < 4; ++r) xd[r] += (int32_t)__builtin_amdgcn_readlane(prec, WS_XREQ + r);
+      }
       if (lane == (slot & 63)) {
         if (slot >= 64) {
           if (!in_c) xcn1 = node;
@@ -1177,6 +1182,31 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     uint32_t woff;
     if (dropped == 0) {
       woff = (uint32_t)pred;  // staged by the producer
+    } else if (dropped <= 2) {
+      // one or two drops: the node is one of the producer's candidates for that
+      // count (positions t, t+1 [, t+2] ascending, t = k - 1 - ix); which one
+      // follows from the drop positions, no walk over T0
+      KSG_COUNTP(7, 64)
+      uint32_t pa = ~0u, pb = ~0u;  // the drop positions, ascending
+      for (uint64_t mm = msk0; mm; mm &= mm - 1) {
+        const uint32_t p = (uint32_t)__builtin_amdgcn_readlane((int)dp0, (int)__builtin_ctzll(mm));
+        if (p < pa) { pb = pa; pa = p; } else if (p < pb) { pb = p; }
+      }
+      for (uint64_t mm = msk1; mm; mm &= mm - 1) {
+        const uint32_t p = (uint32_t)__builtin_amdgcn_readlane((int)dp1, (int)__builtin_ctzll(mm));
+        if (p < pa) { pb = pa; pa = p; } else if (p < pb) { pb = p; }
+      }
+      if (x_drop) {
+        const uint32_t p = xpos0 + (uint32_t)__popcll(t0x & ((1ULL << (xnode & 63)) - 1ULL));
+        if (p < pa) { pb = pa; pa = p; } else if (p < pb) { pb = p; }
+      }
+      const uint32_t ix = (uint32_t)__builtin_amdgcn_readlane((int)rmod, (int)dropped);
+      const uint32_t t = k - 1 - ix;
+      uint32_t tp = t;
+      if (pa <= tp) ++tp;
+      if (pb <= tp) ++tp;  // (pb > pa: the least fixed point of tp = t + #(drops <= tp))
+      // candidates: 1 + (tp - t) for one drop, 3 + (tp - t) for two
+      woff = (uint32_t)__builtin_amdgcn_readlane((int)cand, (int)((dropped == 1 ? 1u : 3u) + (tp - t)));
     } else {
       // T0's tp-th node ascending, tp the least fixed point of
       // tp = t + #(drop positions <= tp): its row (row prefixes, lane q < P),
@@ -1322,7 +1352,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   for (uint32_t t = lane; t < resolved; t += 64) out[t] = L_out[t];
-  if (x.exts && (d.ext_filters & KSG_EXT_SCALAR)) {
+  if (XS) {
     // (extensions) the window's extended resource requests into the node state
     // (the checkers wrote cpu / memory back; these live in no slot)
     for (uint32_t t = lane; t < resolved; t += 64) {
@@ -1383,18 +1413,29 @@ hipError_t ksg_launch_win_t0(const KsgDev& d, uint32_t wcap, const KsgWinRun* ru
   return hipGetLastError();
 }
 
-template <int PP, bool ST>
-static hipError_t win_plain_launch(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run, const KsgWinSum* sums,
-                                   const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
+template <int PP, bool ST, bool XS>
+static hipError_t win_plain_launch_x(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run,
+                                     const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
+                                     hipStream_t st) {
   static bool once = false;
   if (!once) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_plain_kernel<PP, ST>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_plain_kernel<PP, ST, XS>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipGetLastError();  // do not leave a sticky error behind
     once = true;
   }
-  hipLaunchKernelGGL((ksg_win_plain_kernel<PP, ST>), dim3(1), dim3(512), lds, st, d, wcap, run, sums, x, rng, out);
+  hipLaunchKernelGGL((ksg_win_plain_kernel<PP, ST, XS>), dim3(1), dim3(512), lds, st, d, wcap, run, sums, x, rng,
+                     out);
   return hipGetLastError();
+}
+
+template <int PP, bool ST>
+static hipError_t win_plain_launch(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run, const KsgWinSum* sums,
+                                   const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
+  // (extensions) extended resources on the slots
+  if (x.exts != nullptr && (d.ext_filters & KSG_EXT_SCALAR) && d.n_scalar > 0)
+    return win_plain_launch_x<PP, ST, true>(d, wcap, lds, run, sums, x, rng, out, st);
+  return win_plain_launch_x<PP, ST, false>(d, wcap, lds, run, sums, x, rng, out, st);
 }
 
 hipError_t ksg_launch_win_plain(const KsgDev& d, uint32_t P, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,

@@ -15,34 +15,37 @@
 //    Per (pod, word) it stores the word's best score and the bitmap of nodes at
 //    that score; the wave that owns word 0 also writes each pod's 192-byte
 //    resolver record (KsgWinSum).
-//  phase B (ksg_win_resolve_kernel, one wave): walks the window in order and
-//    reproduces the sequential result. M0 = max over the words of the best
-//    scores, T0 = nodes at M0. For a "clean" pod — one whose service scalars
-//    (ServiceSpreading maxCount, ServiceAffinity peer) no earlier pod of the
-//    window changed — a commit can only make the committed node WORSE
-//    (requested totals grow: LeastRequested falls and PodFitsResources can flip
-//    to false; host ports / PDs only get added; service counts grow under a
-//    fixed maxCount), and every other node is untouched. So the sequential max
-//    is still M0 unless all of T0 was made worse, and the sequential tie set is
-//    T0 minus the nodes committed earlier in the window (set C) whose
-//    re-evaluated score dropped. Phase B re-scores only T0 ∩ C from LDS copies
-//    of the committed nodes ("slots"), draws the Int63 the reference draws
-//    (generic_scheduler.go:94), selects the ix-th tie in descending name order,
-//    commits into the slot, and continues. A pod that is not clean, or whose
-//    whole T0 dropped, ends the window; the host starts the next window (new
-//    snapshot) at that pod. Results are bit-identical to the one-pod-at-a-time
-//    path (tests/test_gpu_parity.py compares both with the oracle).
-//
-// Latency is everything in phase B (one wave, one pod after another): the
-// committed-node mask C and the pod's T0 live in registers (lane l owns words
-// [l*P, l*P+P)), prefix counts are DPP row scans, candidates are compacted
-// through LDS so one pass of 64 lanes re-checks them, and the snapshot loads
-// of a newly committed node are retired lazily (only when a later pod needs
-// that node, else at the next commit).
+//  phase B: walks the window in order and reproduces the sequential result.
+//    M0 = max over the words of the best scores, T0 = nodes at M0. For a
+//    "clean" pod — one whose service scalars (ServiceSpreading maxCount,
+//    ServiceAffinity peer) no earlier pod of the window changed — a commit can
+//    only make the committed node WORSE (requested totals grow: LeastRequested
+//    falls and PodFitsResources can flip to false; host ports / PDs only get
+//    added; service counts grow under a fixed maxCount; extensions: extended
+//    resources only get taken), and every other node is untouched. So the
+//    sequential max is still M0 unless all of T0 was made worse, and the
+//    sequential tie set is T0 minus the nodes committed earlier in the window
+//    (set C, "slots") whose re-evaluated score dropped. Phase B re-checks only
+//    T0 ∩ C, draws the Int63 the reference draws (generic_scheduler.go:94),
+//    selects the ix-th tie in descending name order, commits into the slot,
+//    and continues. A pod that is not clean, or whose whole T0 dropped, ends
+//    the window; the next window (a new snapshot) starts at that pod. Results
+//    are bit-identical to the one-pod-at-a-time path (tests/test_gpu_parity.py
+//    compares both with the oracle).
+//    Resolvers, each one workgroup of 512 threads (committer, checkers,
+//    x-checker, producers pipelined over the window's pods):
+//      ksg_win_plain_kernel (ksg_plain.hip) — every configuration without
+//        ServiceAntiAffinity; reads the per-pod T0 images ksg_win_t0_kernel
+//        builds between the two phases;
+//      ksg_win_resolve2_kernel (this file) — ServiceAntiAffinity with the
+//        per-domain re-rank (one anti priority, one rank, <= 31 label values);
+//      ksg_win_resolve_kernel (this file, LDS slots) — the other
+//        ServiceAntiAffinity configurations.
 //
 // ServiceAntiAffinity scores a node by its domain's count of the pod's service
-// pods over the pod's FILTERED nodes: phase A runs a count pass first, and a
-// window stops at a pod whose service count or domain counts moved.
+// pods over the pod's FILTERED nodes: phase A runs a count pass first; a pod
+// whose service had commits earlier in the window is re-ranked per domain
+// (resolve2), or (LDS-slot resolver) ends the window.
 #include "ksg_device.h"
 #include "ksg_resolver.h"
 
