@@ -242,30 +242,70 @@ struct KsgPatch {
 #define KSG_SRV_PATCHES 4096
 #define KSG_SRV_MAX_R 16  // nodes per thread the server takes (shards up to 16384 nodes)
 enum {
-  KSG_SRV_BEGIN = 1,   // scan the payload's pod: respond {seq, k | ~0u on error, max lo, max hi}
-  KSG_SRV_COMMIT = 2,  // commit tie `tie` of begin `bseq` (rescanned if not the one in LDS): {seq, node}
+  KSG_SRV_BEGIN = 1,   // scan the payload's pod: its tie words into `ties`, then respond
+                       // {seq, k | ~0u on error, max lo, max hi} (the grid server: `part`, below)
+  KSG_SRV_COMMIT = 2,  // AssumePod of the payload's pod on node `arg` (the host picked it from the
+                       // begin's tie words): {seq, node}; not waited for by the host
   KSG_SRV_PATCH = 3,   // apply `n_patch` patches from `patch` in order, reload cached totals: {seq}
   KSG_SRV_EXIT = 4,    // respond {seq} and return
 };
 // header dwords
-enum { KSG_SRVH_KIND = 0, KSG_SRVH_BSEQ, KSG_SRVH_TIE, KSG_SRVH_FLAGS, KSG_SRVH_PAYDW, KSG_SRVH_IDS_AT,
+// ARG: COMMIT the node; BEGIN the last control request posted before it (its scan waits until
+// that one is applied: the grid server's scan workgroups)
+enum { KSG_SRVH_KIND = 0, KSG_SRVH_ARG, KSG_SRVH_RSV, KSG_SRVH_FLAGS, KSG_SRVH_PAYDW, KSG_SRVH_IDS_AT,
        KSG_SRVH_EXT_AT, KSG_SRVH_NPATCH };
-#define KSG_SRV_BADREQ 0xFFFFFFFEu  // response: the payload's layout or ids are out of range
+#define KSG_SRV_BADREQ 0xFFFFFFFEu  // response: the payload's layout, ids or node are out of range
 #define KSG_SRVF_WANT_FAIL 1u  // BEGIN: write the fail code of every node to `fail`
 #define KSG_SRVF_EXT 2u        // the payload carries a ksg_pod_ext at EXT_AT
+// The grid server (ksg_serve_grid_kernel): a leader workgroup plus one scan
+// workgroup per 256 nodes. Each scan workgroup reads a BEGIN from the host
+// block itself, scans its nodes and writes its part (best score, count, tie
+// words; fail codes into `fail`) straight into host memory, the sequence number
+// last; the host merges the parts. The leader serves COMMIT / PATCH / EXIT and
+// answers each once it is applied, so a BEGIN posted after that answer scans
+// the state it left.
+#define KSG_GSRV_NT 256
+#define KSG_GSRV_MAXW 255  // scan workgroups: shards up to 65,280 nodes
+struct alignas(64) KsgSrvPart {
+  uint32_t seq;     // the BEGIN this part answers (its 16-B store comes last)
+  int32_t max;      // best score over the workgroup's nodes (KSG_S32_NONE: none fits)
+  uint32_t cnt;     // its nodes at max
+  uint32_t err;     // 1: the pod's ServiceAffinity peer is on an unknown node; 2: a bad request
+  uint64_t tie[4];  // its nodes at max, one word per 64
+  uint32_t stamp[4];  // KSG_SERVE_STAMPS wall-clock ticks: request seen, masks + loads done, stored; then seq again
+};
+// Two request blocks: `req` (+ `ext`) carries BEGIN, `creq` (+ `cext`) the control
+// requests COMMIT / PATCH / EXIT, so the host posts the next BEGIN while the server
+// may still be reading a COMMIT. Sequence numbers count both.
 struct KsgSrvBox {
   uint32_t req[KSG_SRV_CHUNKS * 4];
+  uint32_t creq[KSG_SRV_CHUNKS * 4];
+  uint32_t cext[KSG_SRV_EXT_DW];
   uint32_t resp[16];  // {seq, a, b, c}: one 16-B store
   uint32_t ext[KSG_SRV_EXT_DW];
   KsgPatch patch[KSG_SRV_PATCHES];
+  uint32_t dbg[256];  // KSG_SERVE_DEBUG: the last stage each workgroup of the server reached (seq << 8 | stage)
+  uint64_t ties[KSG_SRV_MAX_R * 16];  // the one-workgroup server's tie words of the last BEGIN
+  KsgSrvPart part[KSG_GSRV_MAXW];     // the grid server's parts of the last BEGIN
+};
+struct KsgSrvGrid {
+  uint32_t quit;     // == the launch's epoch: the scan workgroups return
+  uint32_t applied;  // the last control request the leader applied (a BEGIN waits for its ARG)
+  uint32_t pad[14];
 };
 struct KsgSrvArgs {
   KsgSrvBox* box;        // device address of the mapped box
   uint8_t* fail;         // device address of the mapped fail-code area (shard nodes)
   uint32_t start_seq;    // the server serves start_seq + 1, + 2, ...
   uint64_t idle_ticks;   // returns after this long without a request (wall_clock64: 100 MHz)
-  uint32_t stamps;       // KSG_SERVE_STAMPS: per-stage s_memtime cycles of each BEGIN in resp[4..9]
+  uint32_t stamps;       // bit 0, KSG_SERVE_STAMPS: per-stage s_memtime cycles of each BEGIN in resp[4..9];
+                         // bit 1, KSG_SERVE_DEBUG: stage markers in box->dbg
+  KsgSrvGrid* grid;      // the grid server's device state (nullptr: the one-workgroup server)
+  uint32_t n_workers;    // its scan workgroups
+  uint32_t epoch;        // its launch number
+  uint32_t grid_opts;    // scan workgroups' polling: bits 0-7 extra sleeps, KSG_GSRV_POLL1
 };
+#define KSG_GSRV_POLL1 256u  // poll chunk 0 alone until its tag moves
 
 #ifdef __HIP__
 #define KSG_HD __host__ __device__

@@ -65,6 +65,7 @@ hipError_t ksg_launch_static(const KsgStaticCfg& sc, uint32_t n_nodes, const ksg
                              int32_t* aff_pair, unsigned long long* pairmap, hipStream_t st);
 hipError_t ksg_launch_patch(const KsgPatch* patches, uint32_t n, hipStream_t st);
 hipError_t ksg_launch_serve(int R, bool anti, bool ext, const KsgDev& d, const KsgSrvArgs& a, hipStream_t st);
+hipError_t ksg_launch_serve_grid(const KsgDev& d, const KsgSrvArgs& a, hipStream_t st);
 hipError_t ksg_launch_admit(const ksg_admission_set* sets, uint32_t n_sets, const ksg_pod* pods,
                             const uint32_t* ids, const uint32_t* pairs, int mode, uint8_t* out, hipStream_t st);
 
@@ -237,11 +238,24 @@ struct ksg_ctx {
   size_t srv_fail_cap = 0;
   uint32_t srv_seq = 0;         // last request posted
   uint64_t srv_idle_us = 20000; // the server returns after this long without a request
-  bool pend_srv = false;        // the pending begin was served by the server (its seq: srv_bseq)
-  uint32_t srv_bseq = 0;
+  bool pend_srv = false;        // the pending begin was served by the server
   uint32_t srv_bhdr[KSG_SRV_HDR_DW] = {};  // that begin's header (its payload layout)
+  std::vector<uint64_t> srv_tw;  // its tie words (node lo + 64 i + b), the commit picks from them
+  uint32_t srv_unacked = 0;      // a COMMIT posted without waiting for its answer (0: none)
+  uint32_t srv_served = 0;       // every request up to this one was served
+  uint32_t srv_last_ctl = 0;     // the last control request posted
+  bool srv_pext_on = false;      // the pending begin's extension record (its commit carries it)
+  ksg_pod_ext srv_pext{};
   uint64_t srv_launches = 0;
+  bool srv_grid_on = true;       // KSG_SERVE_GRID=0: the one-workgroup server at every size
+  uint32_t srv_grid_min = 1024;  // KSG_SERVE_GRID_MIN: shards above this many nodes take the grid server
+  KsgSrvGrid* srv_grid = nullptr;  // its device state (+ the fail codes)
+  size_t srv_grid_cap = 0;
+  uint32_t srv_epoch = 0;
   bool srv_stamps = false;      // KSG_SERVE_STAMPS=1: sum the server's per-stage cycles of each begin
+  int64_t srv_grid_opts = -1;   // KSG_SERVE_GRID_OPTS (KsgSrvArgs.grid_opts; -1: by size)
+  bool srv_debug = false;
+  bool srv_trace = false;       // KSG_SERVE_TRACE=1: every post, wait and relaunch to stderr       // KSG_SERVE_DEBUG=1: the grid server's stage markers, reported on a fault
   double srv_stage[6] = {};     // (printed by ksg_destroy)
   uint64_t srv_stamped = 0;
 
@@ -754,8 +768,17 @@ int wait_device(ksg_ctx* c) {
 }
 
 // ---- the resident drop-in server (ksg_serve.hip) ------------------------------
+// the grid server: plain configurations (no ServiceAntiAffinity, no extensions)
+// past srv_grid_min nodes, one scan workgroup per 256 nodes (<= 255)
+bool srv_grid(const ksg_ctx* c) {
+  const uint32_t n = c->hi - c->lo;
+  return c->srv_grid_on && !anti_on(c) && !c->ext_on && n > c->srv_grid_min &&
+         (n + KSG_GSRV_NT - 1) / KSG_GSRV_NT <= KSG_GSRV_MAXW;
+}
+
 bool srv_eligible(const ksg_ctx* c) {
-  return c->srv_enabled && c->world == 1 && !c->xchg && c->R <= KSG_SRV_MAX_R && !c->dev.wide && c->N > 0;
+  return c->srv_enabled && c->world == 1 && !c->xchg && (c->R <= KSG_SRV_MAX_R || srv_grid(c)) && !c->dev.wide &&
+         c->N > 0;
 }
 
 int srv_alloc(ksg_ctx* c) {
@@ -771,7 +794,7 @@ int srv_alloc(ksg_ctx* c) {
 
 int srv_launch(ksg_ctx* c, uint32_t start_seq) {
   if (int rc = srv_alloc(c)) return rc;
-  const size_t nf = std::max<size_t>(c->hi - c->lo, 1);
+  const size_t nf = ((size_t)(c->hi - c->lo) + 3 & ~(size_t)3) + 64;  // (the grid server stores 4 codes at a time)
   if (c->srv_fail_cap < nf) {
     if (c->srv_fail) (void)hipHostFree(c->srv_fail);
     c->srv_fail = nullptr;
@@ -782,60 +805,198 @@ int srv_launch(ksg_ctx* c, uint32_t start_seq) {
     c->srv_dfail = static_cast<uint8_t*>(dp);
     c->srv_fail_cap = nf;
   }
-  KsgSrvArgs a{c->srv_dbox, c->srv_dfail, start_seq, (uint64_t)c->srv_idle_us * 100, c->srv_stamps ? 1u : 0u};
-  HIPCHK(c, ksg_launch_serve(c->R, anti_on(c), c->ext_on, c->dev, a, c->st));
+  KsgSrvArgs a{c->srv_dbox, c->srv_dfail, start_seq, (uint64_t)c->srv_idle_us * 100,
+               (c->srv_stamps ? 1u : 0u) | (c->srv_debug ? 2u : 0u),
+               nullptr, 0, ++c->srv_epoch, 0};
+  if (srv_grid(c)) {
+    const uint32_t n = c->hi - c->lo;
+    const size_t need = sizeof(KsgSrvGrid);
+    if (c->srv_grid_cap < need) {
+      if (c->srv_grid) (void)hipFree(c->srv_grid);
+      c->srv_grid = nullptr;
+      c->srv_grid_cap = 0;
+      HIPCHK(c, hipMalloc((void**)&c->srv_grid, need));
+      HIPCHK(c, hipMemsetAsync(c->srv_grid, 0, need, c->st));
+      c->srv_grid_cap = need;
+    }
+    a.grid = c->srv_grid;
+    a.n_workers = (n + KSG_GSRV_NT - 1) / KSG_GSRV_NT;
+    // past 64 scan workgroups their polls of the host block crowd the link: each sleeps ~0.2 us
+    // more between polls (measured: 50,000 nodes 73 -> 38 us per pod; no gain at 15,000)
+    a.grid_opts = c->srv_grid_opts >= 0 ? (uint32_t)c->srv_grid_opts : a.n_workers > 64 ? 0x10u : 0u;
+    HIPCHK(c, ksg_launch_serve_grid(c->dev, a, c->st));
+  } else {
+    HIPCHK(c, ksg_launch_serve(c->R, anti_on(c), c->ext_on, c->dev, a, c->st));
+  }
   c->srv_running = true;
   ++c->srv_launches;
   return KSG_OK;
 }
 
-// Posts request ++srv_seq (header dwords hdr[0..KSG_SRV_HDR_DW); the payload
-// chunks were written by the caller or are left from the pending begin) and
-// waits for its response. A server that returned (idle) before it saw the
-// request is relaunched to serve it.
-int srv_call(ksg_ctx* c, const uint32_t* hdr, uint32_t* resp4) {
-  if (!c->srv_running) {
-    if (int rc = srv_launch(c, c->srv_seq)) return rc;
-  }
-  const uint32_t seq = ++c->srv_seq;
-  uint32_t* req = c->srv_box->req;
-  for (uint32_t i = 0; i < KSG_SRV_HDR_DW; ++i) req[4 * (i / KSG_SRV_CHUNK_DW) + i % KSG_SRV_CHUNK_DW] = hdr[i];
-  std::atomic_thread_fence(std::memory_order_release);  // data, then tags (x86: stores stay in order)
-  for (uint32_t q = 0; q < KSG_SRV_CHUNKS; ++q) __atomic_store_n(&req[4 * q + 3], seq, __ATOMIC_RELEASE);
+// Waits until request `seq` is answered: its response, or (a grid server's
+// BEGIN, parts > 0) that many parts. A server that returned (idle) before it saw
+// the request is relaunched to serve it.
+int srv_wait(ksg_ctx* c, uint32_t seq, uint32_t parts) {
   const uint32_t* rs = c->srv_box->resp;
+  auto done = [&]() {
+    if (!parts) return (int32_t)(__atomic_load_n(&rs[0], __ATOMIC_ACQUIRE) - seq) >= 0;  // (answered in order)
+    for (uint32_t q = 0; q < parts; ++q)
+      if (__atomic_load_n(&c->srv_box->part[q].seq, __ATOMIC_ACQUIRE) != seq ||
+          __atomic_load_n(&c->srv_box->part[q].stamp[3], __ATOMIC_ACQUIRE) != seq)  // (both ends of the store)
+        return false;
+    return true;
+  };
   auto t0 = std::chrono::steady_clock::now();
   uint32_t spins = 0, relaunches = 0;
-  while (__atomic_load_n(&rs[0], __ATOMIC_ACQUIRE) != seq) {
+  while (!done()) {
     if ((++spins & 255) != 0) continue;
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     if (us < 20.0) continue;
     const hipError_t q = hipStreamQuery(c->st);
     if (q == hipSuccess) {  // the server returned without serving `seq`
-      if (__atomic_load_n(&rs[0], __ATOMIC_ACQUIRE) == seq) break;
+      if (done()) break;
       if (++relaunches > 3) return fail(c, KSG_ERR_HIP, "drop-in server exits without serving request %u", seq);
       c->srv_running = false;
-      if (int rc = srv_launch(c, seq - 1)) return rc;
+      if (c->srv_trace) fprintf(stderr, "srv relaunch start %u (waiting %u)\n", c->srv_served, seq);
+      if (int rc = srv_launch(c, c->srv_served)) return rc;  // (every request after it is offered again)
       t0 = std::chrono::steady_clock::now();
     } else if (q != hipErrorNotReady) {
       c->srv_running = false;
-      return fail(c, KSG_ERR_HIP, "drop-in server: %s", hipGetErrorString(q));
+      std::string marks;
+      if (c->srv_debug)  // where each workgroup was (seq:stage), leader first
+        for (int i = 0; i < 12; ++i) {
+          const uint32_t m = __atomic_load_n(&c->srv_box->dbg[i], __ATOMIC_RELAXED);
+          marks += " " + std::to_string(m >> 8) + ":" + std::to_string(m & 255);
+        }
+      return fail(c, KSG_ERR_HIP, "drop-in server: %s (request %u%s)", hipGetErrorString(q), seq, marks.c_str());
     } else if (us > 5e6) {
       return fail(c, KSG_ERR_HIP, "drop-in server did not answer request %u in 5 s", seq);
     }
   }
   std::atomic_thread_fence(std::memory_order_acquire);
+  if ((int32_t)(seq - c->srv_served) > 0) c->srv_served = seq;  // (and every request before it)
+  return KSG_OK;
+}
+
+// The control block is free once the server has read the last COMMIT (posted
+// without waiting for its answer): before the host writes a control request.
+int srv_settle(ksg_ctx* c) {
+  if (!c->srv_unacked) return KSG_OK;
+  const uint32_t u = c->srv_unacked;
+  c->srv_unacked = 0;
+  if ((int32_t)(c->srv_served - u) >= 0) return KSG_OK;
+  if (int rc = srv_wait(c, u, 0)) return rc;
+  const uint32_t* rs = c->srv_box->resp;
+  if (__atomic_load_n(&rs[0], __ATOMIC_ACQUIRE) == u && __atomic_load_n(&rs[1], __ATOMIC_RELAXED) == KSG_SRV_BADREQ)
+    return fail(c, KSG_ERR_STATE, "drop-in server rejected commit request %u", u);
+  return KSG_OK;
+}
+
+// Posts request ++srv_seq (header dwords hdr[0..KSG_SRV_HDR_DW); the payload
+// chunks were written by the caller): a BEGIN into `req`, a control request into
+// `creq` once the last COMMIT there was read. A BEGIN carries the last control
+// request before it (ARG).
+int srv_post(ksg_ctx* c, const uint32_t* hdr_in, uint32_t* seq_out) {
+  if (!c->srv_running) {
+    if (int rc = srv_launch(c, c->srv_served)) return rc;
+  }
+  const bool ctl = hdr_in[KSG_SRVH_KIND] != KSG_SRV_BEGIN;
+  if (ctl) {
+    if (int rc = srv_settle(c)) return rc;
+  }
+  uint32_t hdr[KSG_SRV_HDR_DW];
+  memcpy(hdr, hdr_in, sizeof hdr);
+  if (!ctl) hdr[KSG_SRVH_ARG] = c->srv_last_ctl;
+  const uint32_t seq = ++c->srv_seq;
+  if (ctl) c->srv_last_ctl = seq;
+  if (c->srv_trace)
+    fprintf(stderr, "srv post %u kind %u arg %u served %u\n", seq, hdr[KSG_SRVH_KIND], hdr[KSG_SRVH_ARG], c->srv_served);
+  uint32_t* req = ctl ? c->srv_box->creq : c->srv_box->req;
+  for (uint32_t i = 0; i < KSG_SRV_HDR_DW; ++i) req[4 * (i / KSG_SRV_CHUNK_DW) + i % KSG_SRV_CHUNK_DW] = hdr[i];
+  std::atomic_thread_fence(std::memory_order_release);  // data, then tags (x86: stores stay in order)
+  for (uint32_t q = 0; q < KSG_SRV_CHUNKS; ++q) __atomic_store_n(&req[4 * q + 3], seq, __ATOMIC_RELEASE);
+  *seq_out = seq;
+  return KSG_OK;
+}
+
+// Posts a request and waits for its response {seq, a, b, c}.
+int srv_call(ksg_ctx* c, const uint32_t* hdr, uint32_t* resp4) {
+  uint32_t seq = 0;
+  if (int rc = srv_post(c, hdr, &seq)) return rc;
+  if (int rc = srv_wait(c, seq, 0)) return rc;
+  const uint32_t* rs = c->srv_box->resp;
   for (int i = 0; i < 4; ++i) resp4[i] = __atomic_load_n(&rs[i], __ATOMIC_RELAXED);
   if (c->srv_stamps && hdr[KSG_SRVH_KIND] == KSG_SRV_BEGIN && __atomic_load_n(&rs[10], __ATOMIC_RELAXED) == seq) {
-    for (int i = 0; i < 6; ++i) c->srv_stage[i] += __atomic_load_n(&rs[4 + i], __ATOMIC_RELAXED);
+    for (int i = 0; i < 6; ++i) c->srv_stage[i] += (int32_t)__atomic_load_n(&rs[4 + i], __ATOMIC_RELAXED);
     ++c->srv_stamped;
   }
   return KSG_OK;
+}
+
+// A BEGIN on either server: {k | ~0u (no peer) | KSG_SRV_BADREQ, max} and the
+// tie words into srv_tw. The grid server's parts are merged here.
+int srv_begin(ksg_ctx* c, const uint32_t* hdr, uint32_t* resp4) {
+  const uint32_t n = c->hi - c->lo, nwd = (n + 63) / 64;
+  if (!srv_grid(c)) {
+    if (int rc = srv_call(c, hdr, resp4)) return rc;
+    if (resp4[1] != KSG_SRV_BADREQ && resp4[1] != ~0u && resp4[1] > 0)
+      c->srv_tw.assign(c->srv_box->ties, c->srv_box->ties + nwd);
+    return KSG_OK;
+  }
+  const uint32_t G = (n + KSG_GSRV_NT - 1) / KSG_GSRV_NT;
+  uint32_t seq = 0;
+  if (int rc = srv_post(c, hdr, &seq)) return rc;
+  if (int rc = srv_wait(c, seq, G)) return rc;
+  const KsgSrvPart* pt = c->srv_box->part;
+  int32_t M = KSG_S32_NONE;
+  uint32_t err = 0;
+  for (uint32_t q = 0; q < G; ++q) {
+    M = std::max(M, pt[q].max);
+    err |= pt[q].err;
+  }
+  uint32_t k = 0;
+  c->srv_tw.assign((size_t)G * 4, 0);
+  if (M != KSG_S32_NONE)
+    for (uint32_t q = 0; q < G; ++q)
+      if (pt[q].max == M) {
+        k += pt[q].cnt;
+        for (int r = 0; r < 4; ++r) c->srv_tw[(size_t)q * 4 + r] = pt[q].tie[r];
+      }
+  c->srv_tw.resize(nwd);
+  if (c->srv_stamps) {  // worker 0: masks + loads, eval + publish (100-MHz ticks)
+    c->srv_stage[0] += (int32_t)(pt[0].stamp[1] - pt[0].stamp[0]);
+    c->srv_stage[1] += (int32_t)(pt[0].stamp[2] - pt[0].stamp[1]);  // (stamp[3]: the sequence number)
+    ++c->srv_stamped;
+  }
+  resp4[0] = seq;
+  resp4[1] = (err & 2) ? KSG_SRV_BADREQ : err ? ~0u : k;
+  if (c->srv_trace) fprintf(stderr, "srv begin %u max %d k %u err %u\n", seq, M, k, err);
+  const int64_t m64 = M;
+  resp4[2] = (uint32_t)(uint64_t)m64;
+  resp4[3] = (uint32_t)((uint64_t)m64 >> 32);
+  return KSG_OK;
+}
+
+// the t-th set bit (ascending) of the tie words -> node offset, -1 if none
+int64_t srv_pick(const std::vector<uint64_t>& tw, uint64_t t) {
+  uint64_t acc = 0;
+  for (size_t i = 0; i < tw.size(); ++i) {
+    const uint64_t pc = (uint64_t)__builtin_popcountll(tw[i]);
+    if (t < acc + pc) {
+      uint64_t w = tw[i];
+      for (uint64_t j = acc; j < t; ++j) w &= w - 1;  // drop the lower set bits
+      return (int64_t)(i * 64 + (uint64_t)__builtin_ctzll(w));
+    }
+    acc += pc;
+  }
+  return -1;
 }
 
 // Ends the resident server so other work can use the stream.
 int srv_stop(ksg_ctx* c) {
   if (!c->srv_running) return KSG_OK;
   HIPCHK(c, hipSetDevice(c->device));
+  if (int rc = srv_settle(c)) return rc;  // (the last commit is applied first)
   if (hipStreamQuery(c->st) != hipSuccess) {
     uint32_t hdr[KSG_SRV_HDR_DW] = {KSG_SRV_EXIT};
     uint32_t r[4];
@@ -866,19 +1027,20 @@ int srv_flush_patches(ksg_ctx* c) {
 // The pod, its ids [0, n_ids) and (extensions) its record as the request
 // payload; false if it does not fit the block + ext area.
 bool srv_put_pod(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, size_t n_ids, const ksg_pod_ext* ext,
-                 uint32_t* hdr) {
+                 uint32_t* hdr, bool ctl = false) {
   const uint32_t pod_dw = (uint32_t)(sizeof(ksg_pod) / 4), ext_dw = (uint32_t)(sizeof(ksg_pod_ext) / 4);
   const uint32_t ids_at = pod_dw;
   const uint32_t ext_at = (ids_at + (uint32_t)n_ids + 1) & ~1u;  // 8-byte aligned
   const uint64_t paydw = ext ? (uint64_t)ext_at + ext_dw : (uint64_t)ids_at + n_ids;
   if (paydw > KSG_SRV_PAY_DW) return false;
-  uint32_t* req = c->srv_box->req;
+  uint32_t* req = ctl ? c->srv_box->creq : c->srv_box->req;
+  uint32_t* xa = ctl ? c->srv_box->cext : c->srv_box->ext;
   auto put = [&](uint32_t i, uint32_t v) {  // payload dword i
     if (i < KSG_SRV_INLINE_DW) {
       const uint32_t j = KSG_SRV_HDR_DW + i;
       req[4 * (j / KSG_SRV_CHUNK_DW) + j % KSG_SRV_CHUNK_DW] = v;
     } else {
-      c->srv_box->ext[i - KSG_SRV_INLINE_DW] = v;
+      xa[i - KSG_SRV_INLINE_DW] = v;
     }
   };
   const uint32_t* pw = reinterpret_cast<const uint32_t*>(pod);
@@ -986,7 +1148,12 @@ static int create_impl(const ksg_config* cfg, int device, int rank, int world, c
   c->spin_wait = !(getenv("KSG_SPIN_WAIT") && atoi(getenv("KSG_SPIN_WAIT")) == 0);
   c->srv_enabled = !(getenv("KSG_SERVE") && atoi(getenv("KSG_SERVE")) == 0);
   c->srv_stamps = getenv("KSG_SERVE_STAMPS") && atoi(getenv("KSG_SERVE_STAMPS")) != 0;
+  c->srv_debug = getenv("KSG_SERVE_DEBUG") && atoi(getenv("KSG_SERVE_DEBUG")) != 0;
+  c->srv_trace = getenv("KSG_SERVE_TRACE") && atoi(getenv("KSG_SERVE_TRACE")) != 0;
+  if (const char* go = getenv("KSG_SERVE_GRID_OPTS")) c->srv_grid_opts = (int64_t)strtoul(go, nullptr, 0);
   if (const char* iu = getenv("KSG_SERVE_IDLE_US")) c->srv_idle_us = (uint64_t)std::max(atoll(iu), 1LL);
+  c->srv_grid_on = !(getenv("KSG_SERVE_GRID") && atoi(getenv("KSG_SERVE_GRID")) == 0);
+  if (const char* gm = getenv("KSG_SERVE_GRID_MIN")) c->srv_grid_min = (uint32_t)std::max(atoi(gm), 0);
   if (const char* rm = getenv("KSG_ROUND_MARGIN")) c->round_margin = std::min(std::max(atof(rm), 0.5), 4.0);
   // The exchange path (shard scan, all-gather of per-shard records, replicated
   // resolve) runs for world > 1, and for a 1-rank RCCL communicator when the caller
@@ -1042,7 +1209,12 @@ int ksg_destroy(ksg_ctx* c) {
     (void)hipSetDevice(c->device);
     (void)srv_stop(c);
   }
-  if (c->srv_stamped) {
+  if (c->srv_stamped && srv_grid(c)) {
+    const double n = (double)c->srv_stamped;
+    fprintf(stderr, "ksg grid serve stamps (10-ns ticks per begin, %llu begins, scan workgroup 0): request seen -> "
+            "masks + loads done %.1f, -> eval + part stored %.1f\n",
+            (unsigned long long)c->srv_stamped, c->srv_stage[0] / n, c->srv_stage[1] / n);
+  } else if (c->srv_stamped) {
     const double n = (double)c->srv_stamped;
     fprintf(stderr, "ksg serve stamps (s_memtime cycles per begin, %llu begins): to-LDS %.0f check %.0f resolve %.0f "
             "scan %.0f reduce %.0f fail-codes %.0f\n", (unsigned long long)c->srv_stamped, c->srv_stage[0] / n,
@@ -1064,6 +1236,7 @@ int ksg_destroy(ksg_ctx* c) {
   if (c->h_dn) (void)hipHostFree(c->h_dn);
   if (c->h_map) (void)hipHostFree(c->h_map);
   if (c->srv_box) (void)hipHostFree(c->srv_box);
+  if (c->srv_grid) (void)hipFree(c->srv_grid);
   if (c->srv_fail) (void)hipHostFree(c->srv_fail);
   if (c->h_xrecv) (void)hipHostFree(c->h_xrecv);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1476,7 +1649,7 @@ int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int6
       if ((rc = flush_patches(c)) || (!c->srv_running && (rc = srv_flush_patches(c)))) return rc;
       if (fail_codes) hdr[KSG_SRVH_FLAGS] |= KSG_SRVF_WANT_FAIL;
       uint32_t r[4];
-      if ((rc = srv_call(c, hdr, r))) return rc;
+      if ((rc = srv_begin(c, hdr, r))) return rc;
       if (r[1] == KSG_SRV_BADREQ) return fail(c, KSG_ERR_STATE, "drop-in server rejected begin request");
       if (r[1] == ~0u) return fail(c, KSG_ERR_NOPEER, "service affinity peer is not on a known node");
       if (fail_codes) memcpy(fail_codes, c->srv_fail, (size_t)(c->hi - c->lo));
@@ -1489,8 +1662,9 @@ int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int6
       c->pend = *pod;
       c->pend_ids.assign(ids, ids + ext);
       c->pend_srv = true;
-      c->srv_bseq = c->srv_seq;
       memcpy(c->srv_bhdr, hdr, sizeof hdr);
+      c->srv_pext_on = xr != nullptr;
+      if (xr) c->srv_pext = *xr;
       return KSG_OK;
     }
   }
@@ -1525,20 +1699,24 @@ int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int6
 // the device half of a commit: decide the tie_index-th tie and apply AssumePod's delta
 static int commit_on_device(ksg_ctx* c, uint32_t tie_index, int32_t* node) {
   HIPCHK(c, hipSetDevice(c->device));
-  if (c->pend_srv) {  // served by the resident server: one request
+  if (c->pend_srv) {  // served by the resident server
     c->pend_srv = false;
-    // the begin's payload layout (the payload itself is still in the block / ext area)
-    uint32_t hdr[KSG_SRV_HDR_DW];
-    memcpy(hdr, c->srv_bhdr, sizeof hdr);
-    hdr[KSG_SRVH_KIND] = KSG_SRV_COMMIT;
-    hdr[KSG_SRVH_BSEQ] = c->srv_bseq;
-    hdr[KSG_SRVH_TIE] = tie_index;
-    hdr[KSG_SRVH_FLAGS] &= ~KSG_SRVF_WANT_FAIL;
-    uint32_t r[4];
-    if (int rc = srv_call(c, hdr, r)) return rc;
-    if (r[1] == KSG_SRV_BADREQ) return fail(c, KSG_ERR_STATE, "drop-in server rejected commit request");
-    *node = (int32_t)r[1];
-    if (*node < 0) return fail(c, KSG_ERR_STATE, "commit selected no node (%d)", *node);
+    // the tie_index-th tie from the top (generic_scheduler.go:88-95) from the begin's tie words
+    const int64_t off = srv_pick(c->srv_tw, c->pending_k - 1 - tie_index);
+    if (off < 0 || off >= (int64_t)(c->hi - c->lo)) return fail(c, KSG_ERR_STATE, "commit selected no node");
+    *node = (int32_t)(c->lo + (uint32_t)off);
+    // AssumePod's delta: one control request carrying the pod, not waited for (the next
+    // BEGIN's scan waits on the device until it is applied)
+    uint32_t hdr[KSG_SRV_HDR_DW] = {KSG_SRV_COMMIT};
+    if (int rc = srv_settle(c)) return rc;  // (the control block is free)
+    if (!srv_put_pod(c, &c->pend, c->pend_ids.data(), c->pend_ids.size(), c->srv_pext_on ? &c->srv_pext : nullptr,
+                     hdr, true))
+      return fail(c, KSG_ERR_STATE, "pending pod does not fit the request block");
+    hdr[KSG_SRVH_ARG] = (uint32_t)*node;
+    if (c->srv_trace) fprintf(stderr, "srv commit node %d\n", *node);
+    uint32_t seq = 0;
+    if (int rc = srv_post(c, hdr, &seq)) return rc;
+    c->srv_unacked = seq;
     return KSG_OK;
   }
   int rc = ensure_map(c);
@@ -1990,7 +2168,7 @@ int ksg_serve_stats(ksg_ctx* c, uint64_t* out4) {
   out4[0] = c->srv_launches;
   out4[1] = c->srv_seq;
   out4[2] = c->srv_running ? 1 : 0;
-  out4[3] = srv_eligible(c) ? 1 : 0;
+  out4[3] = srv_eligible(c) ? (srv_grid(c) ? 2 : 1) : 0;
   return KSG_OK;
 }
 

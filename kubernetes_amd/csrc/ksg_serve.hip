@@ -49,6 +49,11 @@ __device__ __forceinline__ u32x4 sys_ld16(const uint32_t* p) {
   asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
   return v;
 }
+// two 16-B loads in flight together (the one-workgroup server polls both request blocks)
+__device__ __forceinline__ void sys_ld16x2(const uint32_t* p, const uint32_t* q, u32x4& v, u32x4& u) {
+  asm volatile("global_load_dwordx4 %0, %2, off sc0 sc1\n\tglobal_load_dwordx4 %1, %3, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+               : "=&v"(v), "=&v"(u) : "v"(p), "v"(q) : "memory");
+}
 __device__ __forceinline__ void sys_st16(uint32_t* p, u32x4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" ::"v"(p), "v"(v) : "memory");
 }
@@ -175,6 +180,47 @@ __device__ __forceinline__ void word_masks(const KsgDev& d, const PodCtx& c, uin
   s_wm[WM_AFF * nwq + q] = m_aff;
 }
 
+// One node of the plain scan, branch-free: every predicate's verdict from the
+// word masks and the resource totals, the first failing one by selects
+// (node_fail_l's order), the score computed regardless (node_score; int32, the
+// server's contexts keep |score| < 2^30) and kept by the caller where f == 0.
+__device__ __forceinline__ int32_t eval_node(const KsgDev& d, const PodCtx& c, uint32_t n, uint64_t bit,
+                                             const uint64_t* s_wm, uint32_t nwq, uint32_t q, bool res_on,
+                                             int64_t capc, int64_t capm, int64_t usedc, int64_t usedm, double invc,
+                                             double invm, int32_t ss, int32_t cnt, const int32_t* s_tab,
+                                             int32_t n_tab, int& f) {
+  const uint32_t P = d.preds;
+  const uint64_t w_lp = s_wm[WM_LP * nwq + q], w_sel = s_wm[WM_SEL * nwq + q], w_pd = s_wm[WM_PD * nwq + q],
+                 w_port = s_wm[WM_PORT * nwq + q], w_aff = s_wm[WM_AFF * nwq + q];
+  const bool host_bad = (P & KSG_PRED_HOSTNAME) && c.host != -1 && (int32_t)n != c.host;
+  const bool res_bad = res_on && !((capc == 0 || (int64_t)((uint64_t)capc - (uint64_t)usedc) >= c.req_cpu) &&
+                                   (capm == 0 || (int64_t)((uint64_t)capm - (uint64_t)usedm) >= c.req_mem));
+  f = (w_aff & bit) ? KSG_FAIL_NONE : KSG_FAIL_SERVICEAFFINITY;
+  f = res_bad ? KSG_FAIL_PODFITSRESOURCES : f;
+  f = (w_port & bit) ? KSG_FAIL_PODFITSPORTS : f;
+  f = (w_pd & bit) ? KSG_FAIL_NODISKCONFLICT : f;
+  f = (w_sel & bit) ? f : KSG_FAIL_MATCHNODESELECTOR;
+  f = (w_lp & bit) ? f : KSG_FAIL_LABELSPRESENCE;
+  f = host_bad ? KSG_FAIL_HOSTNAME : f;
+  int32_t s = ss;
+  if (d.w_lr) {
+    const int64_t tc = (int64_t)((uint64_t)usedc + (uint64_t)c.req_cpu);
+    const int64_t tm = (int64_t)((uint64_t)usedm + (uint64_t)c.req_mem);
+    s += (int32_t)d.w_lr * ((lr_fast(tc, capc, invc) + lr_fast(tm, capm, invm)) / 2);
+  }
+  if (d.w_spread) {
+    int32_t sp = 10;
+    if (c.spread_max > 0) {
+      const uint32_t ct = (uint32_t)cnt < (uint32_t)n_tab ? (uint32_t)cnt : 0u;
+      sp = s_tab[ct];
+      if ((uint32_t)cnt >= (uint32_t)n_tab)  // (past the table: rare)
+        sp = (int32_t)frac10_f32((int64_t)c.spread_max - cnt, c.spread_max);
+    }
+    s += (int32_t)d.w_spread * sp;
+  }
+  return d.equal_fallback ? 1 : s;  // EqualPriority (generic_scheduler.go:141-143,180-195)
+}
+
 template <int R, bool REG, int G>
 __device__ __forceinline__ int32_t serve_scan_plain(const KsgDev& d, const PodCtx& c, uint32_t tid, uint32_t wave,
                                                     uint64_t bit, int32_t* s_score, uint8_t* fail_out,
@@ -224,35 +270,9 @@ __device__ __forceinline__ int32_t serve_scan_plain(const KsgDev& d, const PodCt
       const uint32_t j = j0 + g;
       const uint32_t n = d.lo + j * KSG_NT + tid;
       const uint32_t q = j * KSG_NWAVE + wave;
-      const uint64_t w_lp = s_wm[WM_LP * NWQ + q], w_sel = s_wm[WM_SEL * NWQ + q], w_pd = s_wm[WM_PD * NWQ + q],
-                     w_port = s_wm[WM_PORT * NWQ + q], w_aff = s_wm[WM_AFF * NWQ + q];
-      const bool host_bad = (P & KSG_PRED_HOSTNAME) && c.host != -1 && (int32_t)n != c.host;
-      const bool res_bad = res_on && !((capc[g] == 0 || (int64_t)((uint64_t)capc[g] - (uint64_t)usedc[g]) >= c.req_cpu) &&
-                                       (capm[g] == 0 || (int64_t)((uint64_t)capm[g] - (uint64_t)usedm[g]) >= c.req_mem));
-      int f = (w_aff & bit) ? KSG_FAIL_NONE : KSG_FAIL_SERVICEAFFINITY;
-      f = res_bad ? KSG_FAIL_PODFITSRESOURCES : f;
-      f = (w_port & bit) ? KSG_FAIL_PODFITSPORTS : f;
-      f = (w_pd & bit) ? KSG_FAIL_NODISKCONFLICT : f;
-      f = (w_sel & bit) ? f : KSG_FAIL_MATCHNODESELECTOR;
-      f = (w_lp & bit) ? f : KSG_FAIL_LABELSPRESENCE;
-      f = host_bad ? KSG_FAIL_HOSTNAME : f;
-      int32_t s = ss[g];
-      if (d.w_lr) {
-        const int64_t tc = (int64_t)((uint64_t)usedc[g] + (uint64_t)c.req_cpu);
-        const int64_t tm = (int64_t)((uint64_t)usedm[g] + (uint64_t)c.req_mem);
-        s += (int32_t)d.w_lr * ((lr_fast(tc, capc[g], invc[g]) + lr_fast(tm, capm[g], invm[g])) / 2);
-      }
-      if (d.w_spread) {
-        int32_t sp = 10;
-        if (c.spread_max > 0) {
-          const uint32_t ct = (uint32_t)cnt[g] < (uint32_t)n_tab ? (uint32_t)cnt[g] : 0u;
-          sp = s_tab[ct];
-          if ((uint32_t)cnt[g] >= (uint32_t)n_tab)  // (past the table: rare)
-            sp = (int32_t)frac10_f32((int64_t)c.spread_max - cnt[g], c.spread_max);
-        }
-        s += (int32_t)d.w_spread * sp;
-      }
-      s = d.equal_fallback ? 1 : s;  // EqualPriority (generic_scheduler.go:141-143,180-195)
+      int f;
+      const int32_t s = eval_node(d, c, n, bit, s_wm, NWQ, q, res_on, capc[g], capm[g], usedc[g], usedm[g], invc[g],
+                                  invm[g], ss[g], cnt[g], s_tab, n_tab, f);
       const bool valid = n < d.hi;
       if (fail_out && valid) fail_out[n - d.lo] = (uint8_t)f;
       const int32_t sc = (valid && f == KSG_FAIL_NONE) ? s : KSG_S32_NONE;
@@ -287,7 +307,6 @@ __global__ __launch_bounds__(KSG_NT) void ksg_serve_kernel(KsgDev d, KsgSrvArgs 
   __shared__ SC s_wmax[KSG_NWAVE];
   __shared__ uint32_t s_wcnt[KSG_NWAVE];
   __shared__ uint32_t s_kind;
-  __shared__ int32_t s_winner;
   __shared__ KsgPatch s_pt[64];
 
   const uint32_t tid = threadIdx.x;
@@ -315,10 +334,9 @@ __global__ __launch_bounds__(KSG_NT) void ksg_serve_kernel(KsgDev d, KsgSrvArgs 
   // to resp[4..11] before the response (ksg_runtime.cpp sums them)
   uint64_t st_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   auto stamp = [&](int i) {
-    if (a.stamps && tid == 0) st_[i] = __builtin_amdgcn_s_memtime();
+    if ((a.stamps & 1u) && tid == 0) st_[i] = __builtin_amdgcn_s_memtime();
   };
   uint32_t seq = a.start_seq + 1;
-  uint32_t pend = 0;    // the begin whose scan (M, k, s_tie) is in LDS; 0: none
   SC M = T::none;
   uint32_t k = 0;
   bool err = false;
@@ -371,25 +389,30 @@ __global__ __launch_bounds__(KSG_NT) void ksg_serve_kernel(KsgDev d, KsgSrvArgs 
 
   for (;;) {
     __syncthreads();  // every wave is done with the previous request's LDS
-    // ---- wave 0 waits for request `seq`: every chunk's tag equal to it ----
+    // ---- wave 0 waits for request `seq` in either block: every chunk's tag equal to it ----
     if (wave == 0) {
       const uint64_t t0 = wall_clock64();
-      u32x4 v;
-      bool ok = false;
+      u32x4 v, u;
+      uint32_t got = 0;  // 1: the BEGIN block, 2: the control block
       for (;;) {
-        v = sys_ld16(a.box->req + lane * 4);
+        sys_ld16x2(a.box->req + lane * 4, a.box->creq + lane * 4, v, u);
         if (__ballot(v.w != seq) == 0) {
-          ok = true;
+          got = 1;
+          break;
+        }
+        if (__ballot(u.w != seq) == 0) {
+          got = 2;
+          v = u;
           break;
         }
         if (wall_clock64() - t0 > a.idle_ticks) break;
       }
-      if (ok) {
+      if (got) {
         s_req[lane * KSG_SRV_CHUNK_DW + 0] = v.x;
         s_req[lane * KSG_SRV_CHUNK_DW + 1] = v.y;
         s_req[lane * KSG_SRV_CHUNK_DW + 2] = v.z;
       }
-      if (lane == 0) s_kind = ok ? v.x : 0u;  // chunk 0's first dword is the header's kind
+      if (lane == 0) s_kind = got ? v.x : 0u;  // chunk 0's first dword is the header's kind
       stamp(0);
     }
     __syncthreads();
@@ -433,107 +456,413 @@ __global__ __launch_bounds__(KSG_NT) void ksg_serve_kernel(KsgDev d, KsgSrvArgs 
       }
       __syncthreads();
       load_totals();  // (agent-scope loads: L2 holds the patched values)
-      pend = 0;
       if (tid == 0) respond(a, seq, 0, 0, 0);
       ++seq;
       continue;
     }
-    // ---- BEGIN / COMMIT: the pod's payload beyond the block ----
+    // ---- BEGIN / COMMIT: the pod's payload beyond the block (read before any answer: the host
+    // writes the next request's once it has one) ----
     const bool begin = kind == KSG_SRV_BEGIN;
-    const bool rescan = begin || pend != s_req[KSG_SRVH_BSEQ];
-    if (rescan) {
+    {
       const uint32_t paydw = min(s_req[KSG_SRVH_PAYDW], (uint32_t)KSG_SRV_PAY_DW);
+      const uint32_t* xa = begin ? a.box->ext : a.box->cext;
       if (paydw > KSG_SRV_INLINE_DW) {
         for (uint32_t t = tid; t < paydw - KSG_SRV_INLINE_DW; t += KSG_NT)
-          s_req[KSG_SRV_HDR_DW + KSG_SRV_INLINE_DW + t] = sys_ld32(a.box->ext + t);
+          s_req[KSG_SRV_HDR_DW + KSG_SRV_INLINE_DW + t] = sys_ld32(xa + t);
         __syncthreads();
       }
     }
-    const bool bad = req_bad(d, s_req);
+    const uint32_t node = s_req[KSG_SRVH_ARG];
+    const bool bad = req_bad(d, s_req) || (!begin && (node < d.lo || node >= d.hi));
     stamp(2);
     if (bad) {  // (never, unless the host side has a bug)
       if (tid == 0) respond(a, seq, KSG_SRV_BADREQ, 0, 0);
-      pend = 0;
       ++seq;
       continue;
     }
-    if (rescan) {
-      const bool want_fail = begin && (s_req[KSG_SRVH_FLAGS] & KSG_SRVF_WANT_FAIL);
+    if (begin) {
+      const bool want_fail = (s_req[KSG_SRVH_FLAGS] & KSG_SRVF_WANT_FAIL) != 0;
       scan(want_fail);
-      pend = begin ? seq : s_req[KSG_SRVH_BSEQ];
-      if (begin) {
-        if (want_fail && !err) {  // the shard's fail codes into host memory, then the response
-          const uint32_t nb = d.hi - d.lo;
-          for (uint32_t t = tid * 4; t < nb; t += KSG_NT * 4) {
-            if (t + 4 <= nb) {
-              *reinterpret_cast<volatile uint32_t*>(a.fail + t) = *reinterpret_cast<const uint32_t*>(s_fail + t);
-            } else {
-              for (uint32_t u = t; u < nb; ++u) reinterpret_cast<volatile uint8_t*>(a.fail)[u] = s_fail[u];
-            }
+      const bool put_fail = want_fail && !err, put_ties = !err && k > 0;
+      if (put_fail) {  // the shard's fail codes into host memory
+        const uint32_t nb = d.hi - d.lo;
+        for (uint32_t t = tid * 4; t < nb; t += KSG_NT * 4) {
+          if (t + 4 <= nb) {
+            *reinterpret_cast<volatile uint32_t*>(a.fail + t) = *reinterpret_cast<const uint32_t*>(s_fail + t);
+          } else {
+            for (uint32_t u = t; u < nb; ++u) reinterpret_cast<volatile uint8_t*>(a.fail)[u] = s_fail[u];
           }
-          drain_stores();
-          __syncthreads();
         }
-        if (tid == 0) {
-          if (a.stamps) {  // stage cycles: request seen->LDS, check, resolve, scan, reduce, fail codes
-            stamp(6);
-            u32x4 x0, x1;
-            x0.x = (uint32_t)(st_[1] - st_[0]);
-            x0.y = (uint32_t)(st_[2] - st_[1]);
-            x0.z = (uint32_t)(st_[3] - st_[2]);
-            x0.w = (uint32_t)(st_[4] - st_[3]);
-            x1.x = (uint32_t)(st_[5] - st_[4]);
-            x1.y = (uint32_t)(st_[6] - st_[5]);
-            x1.z = seq;
-            x1.w = 0;
-            sys_st16(a.box->resp + 4, x0);
-            sys_st16(a.box->resp + 8, x1);
-          }
-          const int64_t m64 = (int64_t)M;
-          respond(a, seq, err ? ~0u : k, (uint32_t)(uint64_t)m64, (uint32_t)((uint64_t)m64 >> 32));
+      }
+      if (put_ties) {  // the tie words (the host picks the commit's node from them)
+        const uint32_t nwd = min((uint32_t)(R * KSG_NWAVE), (d.hi - d.lo + 63) >> 6);
+        for (uint32_t i = tid * 2; i < nwd; i += KSG_NT * 2) {
+          u32x4 v;
+          v.x = (uint32_t)s_tie[i];
+          v.y = (uint32_t)(s_tie[i] >> 32);
+          v.z = (uint32_t)s_tie[i + 1];
+          v.w = (uint32_t)(s_tie[i + 1] >> 32);
+          sys_st16(reinterpret_cast<uint32_t*>(a.box->ties + i), v);
         }
-        ++seq;
+      }
+      if (put_fail || put_ties) {  // ... before the response
+        drain_stores();
+        __syncthreads();
+      }
+      if (tid == 0) {
+        if (a.stamps & 1u) {  // stage cycles: request seen->LDS, check, resolve, scan, reduce, fail codes
+          stamp(6);
+          u32x4 x0, x1;
+          x0.x = (uint32_t)(st_[1] - st_[0]);
+          x0.y = (uint32_t)(st_[2] - st_[1]);
+          x0.z = (uint32_t)(st_[3] - st_[2]);
+          x0.w = (uint32_t)(st_[4] - st_[3]);
+          x1.x = (uint32_t)(st_[5] - st_[4]);
+          x1.y = (uint32_t)(st_[6] - st_[5]);
+          x1.z = seq;
+          x1.w = 0;
+          sys_st16(a.box->resp + 4, x0);
+          sys_st16(a.box->resp + 8, x1);
+        }
+        const int64_t m64 = (int64_t)M;
+        respond(a, seq, err ? ~0u : k, (uint32_t)(uint64_t)m64, (uint32_t)((uint64_t)m64 >> 32));
+      }
+      ++seq;
+      continue;
+    }
+    // ---- COMMIT: AssumePod's delta on the host's node (answered first: requests are served in order) ----
+    if (wave == 0) {
+      if (lane == 0) respond(a, seq, node, 0, 0);
+      const uint32_t* pay = s_req + KSG_SRV_HDR_DW;
+      const ksg_pod& p = *reinterpret_cast<const ksg_pod*>(pay);
+      const uint32_t* ids = pay + s_req[KSG_SRVH_IDS_AT];
+      const ksg_pod_ext* ext = (EXT && (s_req[KSG_SRVH_FLAGS] & KSG_SRVF_EXT))
+                                   ? reinterpret_cast<const ksg_pod_ext*>(pay + s_req[KSG_SRVH_EXT_AT])
+                                   : nullptr;
+      commit_pod_wave(d, p, ids, node, lane, ext);
+      drain_stores();
+    }
+    if constexpr (REG) {
+      const ksg_pod& p = *reinterpret_cast<const ksg_pod*>(s_req + KSG_SRV_HDR_DW);
+      const uint32_t off = node - d.lo;
+      const uint32_t jw = off / KSG_NT, tw = off % KSG_NT;
+#pragma unroll
+      for (int j = 0; j < R; ++j)
+        if ((uint32_t)j == jw && tid == tw) {
+          rusedc[j] = (int64_t)((uint64_t)rusedc[j] + (uint64_t)p.milli_cpu);
+          rusedm[j] = (int64_t)((uint64_t)rusedm[j] + (uint64_t)p.memory);
+        }
+    }
+    ++seq;
+  }
+}
+
+// ============================================================================
+// The grid server: the scan spread over one workgroup per 256 nodes.
+//
+// The one-workgroup server is VALU-bound on its CU (16 waves x R nodes of
+// ~250 instructions each: ~11 us of begin at 5,000 nodes). Here workgroups
+// 1..G each own 256 nodes (one per thread) and serve BEGIN: each reads the
+// request from the host block itself, so the pod reaches all of them in the
+// same round trip, filters and scores its nodes, and writes its part {max,
+// count, 4 tie words} and its nodes' fail codes straight into host memory,
+// the part's sequence number last. The host merges the parts (the max, the
+// count at it) and picks a commit's node from their tie words
+// (generic_scheduler.go:88-95): the begin path has no device-side hand-off.
+// Workgroup 0 (the leader) serves COMMIT (AssumePod's delta), PATCH and EXIT
+// and answers each once it is applied and drained, so a BEGIN the host posts
+// after that answer scans the state it left (every scan load of mutable state
+// is an sc1 load). Both kinds of workgroup take any request newer than the
+// last one they saw and skip the kinds they do not serve.
+// ============================================================================
+__device__ __forceinline__ void agent_st32(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void agent_st64(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// scan workgroups' backstop beyond the leader's idle limit (wall_clock64 ticks, 100 MHz: 10 ms)
+#define KSG_GSRV_WAIT 1000000ull
+// KSG_SERVE_DEBUG: workgroup `slot` reached `stage` of request `seq` (host memory, read after a fault)
+__device__ __forceinline__ void grid_mark(const KsgSrvArgs& a, uint32_t slot, uint32_t seq, uint32_t stage) {
+  if (a.stamps & 2u)
+    __hip_atomic_store(a.box->dbg + slot, (seq << 8) | stage, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// wave 0: the next request in the host block (every tag equal to one sequence
+// number > last) into s_req. -> its kind (0: none before the limit / told to quit)
+__device__ __forceinline__ uint32_t grid_poll(const KsgSrvArgs& a, const uint32_t* blk, uint32_t lane, uint32_t last,
+                                              bool worker, uint64_t limit, uint32_t* s_req, uint32_t& seq_out) {
+  const uint64_t t0 = wall_clock64();
+  bool armed = !worker || !(a.grid_opts & KSG_GSRV_POLL1);
+  for (uint32_t it = 0;; ++it) {
+    // (KSG_GSRV_POLL1: a scan workgroup reads chunk 0 alone until its tag moves, then the block)
+    const u32x4 v = sys_ld16(blk + (armed ? lane * 4 : 0));
+    const uint32_t t = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.w);
+    if (!armed) {
+      if ((int32_t)(t - last) > 0) {
+        armed = true;
         continue;
       }
+    } else if (__ballot(v.w != t) == 0 && (int32_t)(t - last) > 0) {
+      s_req[lane * KSG_SRV_CHUNK_DW + 0] = v.x;
+      s_req[lane * KSG_SRV_CHUNK_DW + 1] = v.y;
+      s_req[lane * KSG_SRV_CHUNK_DW + 2] = v.z;
+      seq_out = t;
+      return (uint32_t)__builtin_amdgcn_readfirstlane((int)v.x);
     }
-    // ---- COMMIT: the tie_index-th tie from the top, then AssumePod's delta ----
-    const uint32_t tie = s_req[KSG_SRVH_TIE];
-    if (wave == 0) {
-      int32_t win = -1;
-      if (!err && k > 0 && tie < k) win = select_tie(s_tie, R * KSG_NWAVE, (uint64_t)(k - 1 - tie), lane, d.lo);
-      if (lane == 0) {
-        respond(a, seq, (uint32_t)win, 0, 0);
-        s_winner = win;
+    if (worker) {  // (every 8th poll looks at `quit`; a short sleep spares the link)
+      if ((it & 7) == 7 && ld_mut(&a.grid->quit) == a.epoch) return 0;
+      __builtin_amdgcn_s_sleep(2);
+      for (uint32_t z = 0; z < (a.grid_opts & 255u); ++z) __builtin_amdgcn_s_sleep(8);
+    }
+    if (wall_clock64() - t0 > limit) return 0;
+  }
+}
+
+// the payload beyond the block (every thread; the caller synchronises)
+__device__ __forceinline__ void grid_load_ext(const uint32_t* xa, uint32_t* s_req, uint32_t tid) {
+  const uint32_t paydw = min(s_req[KSG_SRVH_PAYDW], (uint32_t)KSG_SRV_PAY_DW);
+  if (paydw > KSG_SRV_INLINE_DW)
+    for (uint32_t t = tid; t < paydw - KSG_SRV_INLINE_DW; t += KSG_GSRV_NT)
+      s_req[KSG_SRV_HDR_DW + KSG_SRV_INLINE_DW + t] = sys_ld32(xa + t);
+}
+
+__global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, KsgSrvArgs a) {
+  constexpr uint32_t NW = KSG_GSRV_NT / 64;
+  __shared__ __attribute__((aligned(16))) uint32_t s_req[KSG_SRV_HDR_DW + KSG_SRV_PAY_DW];
+  __shared__ int32_t s_tab[KSG_NT];
+  __shared__ uint64_t s_wm[WM_N * NW];
+  __shared__ int32_t s_wmax[NW];
+  __shared__ uint32_t s_wcnt[NW];
+  __shared__ uint64_t s_tw[NW];
+  __shared__ uint32_t s_kind, s_seq, s_ready;
+  __shared__ KsgPatch s_pt[64];
+
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint64_t bit = 1ULL << lane;
+  uint32_t last = a.start_seq;
+
+  if (blockIdx.x > 0) {
+    // ======================= scan workgroup w: BEGIN =======================
+    const uint32_t w = blockIdx.x - 1;
+    KsgDev dw = d;  // this workgroup's nodes: [lo, hi) of the shard
+    dw.lo = d.lo + w * KSG_GSRV_NT;
+    dw.hi = min(d.hi, dw.lo + KSG_GSRV_NT);
+    const uint32_t n = dw.lo + tid;
+    const bool valid = n < dw.hi;
+    const uint32_t nn = valid ? n : dw.lo;
+    KsgSrvPart* hp = a.box->part + w;
+    for (;;) {
+      __syncthreads();
+      if (wave == 0) {
+        uint32_t t = 0;
+        // (the leader returns first and raises `quit`; the limit is a backstop)
+        const uint32_t kind = grid_poll(a, a.box->req, lane, last, true, 4 * a.idle_ticks + KSG_GSRV_WAIT, s_req, t);
+        if (lane == 0) {
+          s_kind = kind;
+          s_seq = t;
+        }
       }
-      if (win >= 0) {
+      __syncthreads();
+      const uint32_t kind = s_kind, T = s_seq;
+      if (kind == 0 || kind >= KSG_SRV_EXIT) return;
+      last = T;
+      if (kind != KSG_SRV_BEGIN) continue;
+      const uint64_t ts_seen = wall_clock64();
+      if (tid == 0) grid_mark(a, 1 + w, T, 1);
+      // this thread's node: the loads of its static data in flight with the payload's
+      const int64_t capc = d.cap_cpu[nn], capm = d.cap_mem[nn];
+      const double invc = d.w_lr ? d.inv10_cpu[nn] : 0.0, invm = d.w_lr ? d.inv10_mem[nn] : 0.0;
+      const int32_t ss = d.has_static_score ? (int32_t)d.static_score[nn] : 0;
+      grid_load_ext(a.box->ext, s_req, tid);
+      if (wave == 0) {  // the control requests posted before this BEGIN are applied (commits it must see)
+        const uint32_t after = s_req[KSG_SRVH_ARG];
+        const uint64_t t0 = wall_clock64();
+        while ((int32_t)(ld_mut(&a.grid->applied) - after) < 0) {
+          if (wall_clock64() - t0 > KSG_GSRV_WAIT || ld_mut(&a.grid->quit) == a.epoch) {
+            if (lane == 0) s_kind = 0;  // (the leader left: this launch cannot serve it)
+            break;
+          }
+        }
+      }
+      __syncthreads();
+      if (s_kind == 0) return;
+      // mutable state only from here on (issued after `applied` covers the BEGIN's ARG)
+      const int64_t usedc = ld_mut(d.used_cpu + nn), usedm = ld_mut(d.used_mem + nn);
+      const bool want_fail = (s_req[KSG_SRVH_FLAGS] & KSG_SRVF_WANT_FAIL) != 0;
+      int32_t sc = KSG_S32_NONE;
+      uint32_t err = 0;
+      if (req_bad(d, s_req)) {
+        err = 2;
+      } else {
         const uint32_t* pay = s_req + KSG_SRV_HDR_DW;
         const ksg_pod& p = *reinterpret_cast<const ksg_pod*>(pay);
         const uint32_t* ids = pay + s_req[KSG_SRVH_IDS_AT];
-        const ksg_pod_ext* ext = (EXT && (s_req[KSG_SRVH_FLAGS] & KSG_SRVF_EXT))
-                                     ? reinterpret_cast<const ksg_pod_ext*>(pay + s_req[KSG_SRVH_EXT_AT])
-                                     : nullptr;
-        commit_pod_wave(d, p, ids, (uint32_t)win, lane, ext);
+        const bool need_cnt = d.w_spread && p.service >= 0 && !d.equal_fallback;
+        const int32_t cnt = need_cnt ? ld_mut(d.svc_cnt + (size_t)p.service * d.n_nodes + nn) : 0;
+        PodCtx c;
+        pod_resolve(d, p, ids, c);
+        c.ext = nullptr;
+        if (tid == 0) grid_mark(a, 1 + w, T, 3);
+        if (c.error) {
+          err = 1;
+        } else {
+          int32_t n_tab = 0;
+          if (need_cnt && c.spread_max > 0) {
+            n_tab = c.spread_max >= KSG_NT ? KSG_NT : c.spread_max + 1;
+            for (int32_t t = (int32_t)tid; t < n_tab; t += KSG_GSRV_NT)
+              s_tab[t] = (int32_t)frac10_f32((int64_t)c.spread_max - t, c.spread_max);
+          }
+          const uint32_t nwq = (dw.hi - dw.lo + 63) >> 6;
+          if (tid < nwq) word_masks(dw, c, tid, s_wm, NW);
+          __syncthreads();  // (the word masks and the table)
+          if (tid == 0) grid_mark(a, 1 + w, T, 4);
+          if ((a.stamps & 1u) && tid == 0) s_ready = (uint32_t)wall_clock64();
+          int f;
+          const bool res_on = (d.preds & KSG_PRED_PODFITSRESOURCES) && !c.zero_req;
+          const int32_t s = eval_node(d, c, n, bit, s_wm, NW, wave, res_on, capc, capm, usedc, usedm, invc, invm, ss,
+                                      cnt, s_tab, n_tab, f);
+          sc = (valid && f == KSG_FAIL_NONE) ? s : KSG_S32_NONE;
+          if (want_fail) {  // four nodes' codes per dword, straight into host memory
+            const uint32_t fb = valid ? (uint32_t)f : 0u;
+            const uint32_t b0 = __shfl(fb, (int)((lane * 4 + 0) & 63), 64), b1 = __shfl(fb, (int)((lane * 4 + 1) & 63), 64);
+            const uint32_t b2 = __shfl(fb, (int)((lane * 4 + 2) & 63), 64), b3 = __shfl(fb, (int)((lane * 4 + 3) & 63), 64);
+            const uint32_t at = w * KSG_GSRV_NT + wave * 64 + lane * 4;  // (shard-relative; the area is 4-padded)
+            if (lane < 16 && dw.lo + wave * 64 + lane * 4 < dw.hi)
+              *reinterpret_cast<volatile uint32_t*>(a.fail + at) = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+          }
+        }
       }
-      drain_stores();
+      // the part: best score, count and tie words of these nodes
+      const int32_t wm = wave_total_max(sc);
+      if (lane == 0) s_wmax[wave] = wm;
+      __syncthreads();
+      int32_t M = s_wmax[0];
+#pragma unroll
+      for (uint32_t q = 1; q < NW; ++q) M = max(M, s_wmax[q]);
+      if (d.empty_priorities) M = KSG_S32_NONE;  // all weights 0: an empty HostPriorityList
+      const uint64_t tb = __ballot(M != KSG_S32_NONE && sc == M);
+      if (lane == 0) {
+        s_tw[wave] = tb;
+        s_wcnt[wave] = (uint32_t)__popcll(tb);
+      }
+      drain_stores();  // (this wave's fail-code stores)
+      __syncthreads();
+      if (tid < 4) {  // the part: one 64-B store of 4 lanes, the sequence number at both ends
+        uint32_t k = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < NW; ++q) k += s_wcnt[q];
+        const uint32_t r = (tid == 1 || tid == 2) ? tid - 1 : 0u;  // (lanes 1, 2: the tie words)
+        const uint64_t t0 = s_tw[2 * r], t1 = s_tw[2 * r + 1];
+        u32x4 v;
+        v.x = tid == 0 ? T : tid == 3 ? (uint32_t)ts_seen : (uint32_t)t0;
+        v.y = tid == 0 ? (uint32_t)M : tid == 3 ? s_ready : (uint32_t)(t0 >> 32);
+        v.z = tid == 0 ? k : tid == 3 ? (uint32_t)wall_clock64() : (uint32_t)t1;
+        v.w = tid == 0 ? err : tid == 3 ? T : (uint32_t)(t1 >> 32);
+        sys_st16(reinterpret_cast<uint32_t*>(hp) + 4 * tid, v);
+        if (tid == 0) grid_mark(a, 1 + w, T, 6);
+      }
+    }
+  }
+
+  // ======================= the leader: COMMIT, PATCH, EXIT =======================
+  last = ld_mut(&a.grid->applied);  // (a control request newer than that one is still to apply)
+  for (;;) {
+    __syncthreads();
+    if (wave == 0) {
+      uint32_t t = 0;
+      const uint32_t kind = grid_poll(a, a.box->creq, lane, last, false, a.idle_ticks, s_req, t);
+      if (lane == 0) {
+        s_kind = kind;
+        s_seq = t;
+      }
     }
     __syncthreads();
-    if constexpr (REG) {
-      const int32_t w = s_winner;
-      if (w >= 0) {
-        const ksg_pod& p = *reinterpret_cast<const ksg_pod*>(s_req + KSG_SRV_HDR_DW);
-        const uint32_t off = (uint32_t)w - d.lo;
-        const uint32_t jw = off / KSG_NT, tw = off % KSG_NT;
-#pragma unroll
-        for (int j = 0; j < R; ++j)
-          if ((uint32_t)j == jw && tid == tw) {
-            rusedc[j] = (int64_t)((uint64_t)rusedc[j] + (uint64_t)p.milli_cpu);
-            rusedm[j] = (int64_t)((uint64_t)rusedm[j] + (uint64_t)p.memory);
+    const uint32_t kind = s_kind, T = s_seq;
+    if (kind == 0 || kind > KSG_SRV_EXIT) {  // idle: the scan workgroups return too
+      if (tid == 0) agent_st32(&a.grid->quit, a.epoch);
+      return;
+    }
+    last = T;
+    if (tid == 0) grid_mark(a, 0, T, 0x10 + kind);
+    if (kind == KSG_SRV_EXIT) {  // (applied too: the next launch's leader skips it)
+      if (tid == 0) {
+        agent_st32(&a.grid->applied, T);
+        agent_st32(&a.grid->quit, a.epoch);
+        drain_stores();
+        respond(a, T, 0, 0, 0);
+      }
+      return;
+    }
+    if (kind != KSG_SRV_PATCH && kind != KSG_SRV_COMMIT) continue;  // (never: BEGINs use the other block)
+    if (kind == KSG_SRV_PATCH) {  // in order by one lane, agent scope (the scan workgroups read them)
+      const uint32_t np = s_req[KSG_SRVH_NPATCH];
+      if (wave == 0) {
+        for (uint32_t base = 0; base < np; base += 64) {
+          if (base + lane < np) {
+            const KsgPatch* src = a.box->patch + base + lane;
+            KsgPatch pt;
+            pt.addr = sys_ld64(&src->addr);
+            pt.value = sys_ld64(&src->value);
+            pt.width = sys_ld32(&src->width);
+            s_pt[lane] = pt;
           }
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+          if (lane == 0) {
+            const uint32_t m = min(64u, np - base);
+            for (uint32_t q = 0; q < m; ++q) {
+              const KsgPatch pt = s_pt[q];
+              switch (pt.width) {
+                case 0: agent_st32(reinterpret_cast<uint32_t*>(pt.addr), (uint32_t)pt.value); break;
+                case 1: agent_st64(reinterpret_cast<uint64_t*>(pt.addr), pt.value); break;
+                case 2:
+                  __hip_atomic_fetch_or(reinterpret_cast<uint64_t*>(pt.addr), pt.value, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+                  break;
+                case 3:
+                  __hip_atomic_fetch_and(reinterpret_cast<uint64_t*>(pt.addr), ~pt.value, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+                  break;
+              }
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
+        drain_stores();
+        if (lane == 0) {
+          agent_st32(&a.grid->applied, T);
+          respond(a, T, 0, 0, 0);
+        }
+      }
+      continue;
+    }
+    // ---- COMMIT: AssumePod's delta on the host's node, then `applied` ----
+    grid_load_ext(a.box->cext, s_req, tid);
+    __syncthreads();
+    const uint32_t node = s_req[KSG_SRVH_ARG];
+    const bool bad = req_bad(d, s_req) || node < d.lo || node >= d.hi;
+    if (wave == 0) {
+      if (!bad) {
+        const uint32_t* pay = s_req + KSG_SRV_HDR_DW;
+        const ksg_pod& p = *reinterpret_cast<const ksg_pod*>(pay);
+        const uint32_t* ids = pay + s_req[KSG_SRVH_IDS_AT];
+        commit_pod_wave(d, p, ids, node, lane, nullptr);
+        drain_stores();
+      }
+      if (lane == 0) {
+        agent_st32(&a.grid->applied, T);  // (a bad one too: the BEGINs after it must not wait forever)
+        respond(a, T, bad ? KSG_SRV_BADREQ : node, 0, 0);
       }
     }
-    pend = 0;
-    ++seq;
   }
+}
+
+hipError_t ksg_launch_serve_grid(const KsgDev& d, const KsgSrvArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(ksg_serve_grid_kernel, dim3(a.n_workers + 1), dim3(KSG_GSRV_NT), 0, st, d, a);
+  return hipGetLastError();
 }
 
 // ---- launch wrapper --------------------------------------------------------

@@ -285,7 +285,8 @@ class DeviceScheduler:
         """The resident begin/commit server (ksg_serve_stats)."""
         o = np.zeros(4, np.uint64)
         self._lib.ksg_serve_stats(self._ctx, abi.ptr(o))
-        return {"launches": int(o[0]), "requests": int(o[1]), "running": bool(o[2]), "eligible": bool(o[3])}
+        return {"launches": int(o[0]), "requests": int(o[1]), "running": bool(o[2]), "eligible": bool(o[3]),
+                "grid": int(o[3]) == 2}
 
     def debug_counters(self) -> np.ndarray:
         """KSG_DEBUG=8 contexts: the window resolver's per-stage cycle counters

@@ -74,14 +74,19 @@ def _drive(case, dev, orc, seed, n_pods, *, evaluate_every=0, batch_at=(), churn
     assert np.array_equal(gc, wc) and np.array_equal(gm, wm)
 
 
-@pytest.mark.parametrize("name,nn,npods", [
-    ("config1", 500, 500),     # R = 1, register-cached totals
-    ("config2", 2000, 500),    # R = 2
-    ("config2", 5000, 500),    # R = 8 (config 2's node count)
-    ("config4", 900, 400),     # ServiceAffinity + ServiceAntiAffinity
-    ("config3", 15000, 200),   # R = 16
+@pytest.mark.parametrize("name,nn,npods,grid", [
+    ("config1", 500, 500, False),     # one workgroup, R = 1, register-cached totals
+    ("config2", 2000, 500, False),    # R = 2
+    ("config2", 2000, 500, True),     # the grid server: 8 scan workgroups
+    ("config2", 5000, 500, False),    # R = 8 (config 2's node count)
+    ("config2", 5000, 500, True),
+    ("config4", 900, 400, False),     # ServiceAffinity + ServiceAntiAffinity
+    ("config3", 15000, 200, False),   # R = 16
+    ("config3", 15000, 200, True),
+    ("config2", 30000, 120, True),    # past the one-workgroup server's 16,384 nodes
 ])
-def test_serve_begin_commit_matches_oracle(name, nn, npods):
+def test_serve_begin_commit_matches_oracle(name, nn, npods, grid, monkeypatch):
+    monkeypatch.setenv("KSG_SERVE_GRID", "1" if grid else "0")
     case = Case(name, nn, npods)
     dev = DeviceScheduler(case.cfg, device=0)
     orc = OracleScheduler(case.cfg)
@@ -90,10 +95,11 @@ def test_serve_begin_commit_matches_oracle(name, nn, npods):
     _drive(case, dev, orc, seed=nn + npods, n_pods=npods)
     st = dev.serve_stats()
     assert st["eligible"] and st["launches"] >= 1 and st["requests"] >= npods, st
+    assert st["grid"] == grid, st
     dev.close()
 
 
-@pytest.mark.parametrize("name,nn,npods", [("config2", 1500, 400), ("config4", 700, 300)])
+@pytest.mark.parametrize("name,nn,npods", [("config2", 1500, 400), ("config4", 700, 300), ("config2", 3000, 300)])
 def test_serve_interleaved_with_add_remove_evaluate_batch(name, nn, npods):
     """Mirror patches through the server, and evaluate / batch taking the stream."""
     case = Case(name, nn, npods)
@@ -107,11 +113,12 @@ def test_serve_interleaved_with_add_remove_evaluate_batch(name, nn, npods):
     dev.close()
 
 
-def test_serve_idle_timeout_relaunch(monkeypatch):
+@pytest.mark.parametrize("nn", [900, 2500])  # the one-workgroup server, the grid server
+def test_serve_idle_timeout_relaunch(nn, monkeypatch):
     """A 1-us idle limit: the server returns between nearly every pair of
     requests, between a begin and its commit too (the commit rescans)."""
     monkeypatch.setenv("KSG_SERVE_IDLE_US", "1")
-    case = Case("config2", 1200, 300)
+    case = Case("config2", nn, 300)
     dev = DeviceScheduler(case.cfg, device=0)
     orc = OracleScheduler(case.cfg)
     dev.set_cluster(case.view.arrays)
