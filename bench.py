@@ -94,22 +94,38 @@ _STAGES_PLAIN = {
 }
 
 
-def _phase_a_bytes(cfg, pods, ns, nw, w):
+def _phase_a_bytes(cfg, pods, ids, ns, nw, w):
     """Algorithmic bytes of one phase-A launch (ksg_win_score_kernel) scoring w
-    pods on a shard of ns nodes / nw words: the node state once per wave (cap and
-    requested totals 32 B, the static score 4 B), per (pod, word) one 8-byte
-    predicate word per list entry of the pod (nodeSelector pairs, PDs, host
-    ports, ServiceAffinity pairs; the LabelsPresence word once per word), per
-    (pod, node) the pod's service count (4 B, when ServiceSpreading or
-    ServiceAntiAffinity is on), the per-(pod, word) best score + tie bitmap
-    written (12 B) and the pods' 192-byte records. The pods' list lengths are
-    the workload's means."""
-    n_list = float(np.mean(pods["n_sel"] + pods["n_pds"] + pods["n_ports"])) if len(pods) else 0.0
+    pods on a shard of ns nodes / nw words, counting each distinct row once per
+    launch (the window's pods share rows in L2; FETCH_SIZE sees a row once): the
+    node state (cap and requested totals 32 B, the static score 4 B) and the
+    LabelsPresence word once; one 8-byte word per word of every DISTINCT
+    predicate row the window's pods name (nodeSelector pairs, PD and host-port
+    keys, ServiceAffinity pairs); the service-count row (4 B per node) of every
+    distinct service among them (when ServiceSpreading or ServiceAntiAffinity is
+    on); the per-(pod, word) best score + tie bitmap written (12 B) and the pods'
+    192-byte records. Averaged over the batch's consecutive windows of w pods."""
+    w = max(1, int(round(w)))
     na = int(cfg.n_aff_labels)
-    n_list += float(np.mean((pods["aff_pair"][:, :na] >= 0).sum(axis=1))) if na and len(pods) else 0.0
-    frac_svc = float(np.mean(pods["service"] >= 0)) if len(pods) else 0.0
     cnt_on = int(cfg.w_service_spreading) != 0 or any(int(cfg.w_anti[a]) != 0 for a in range(int(cfg.n_anti)))
-    return (36.0 * ns + 8.0 * nw + w * nw * 8.0 * n_list + (w * ns * 4.0 * frac_svc if cnt_on else 0.0)
+    n = len(pods)
+    rows, svcs = [], []
+    for w0 in range(0, max(n - w + 1, 1), w):
+        sel, keys, aff, sv = set(), set(), set(), set()
+        for p in pods[w0:w0 + w]:
+            sel.update(ids[int(p["sel_off"]):int(p["sel_off"]) + int(p["n_sel"])].tolist())
+            keys.update(ids[int(p["pds_off"]):int(p["pds_off"]) + int(p["n_pds"])].tolist())
+            keys.update(ids[int(p["ports_off"]):int(p["ports_off"]) + int(p["n_ports"])].tolist())
+            for j in range(na):
+                if int(p["aff_pair"][j]) >= 0:
+                    aff.add(int(p["aff_pair"][j]))
+            if int(p["service"]) >= 0:
+                sv.add(int(p["service"]))
+        rows.append(len(sel | aff) + len(keys))  # (pairmap rows: selector and affinity pairs; keymap rows)
+        svcs.append(len(sv))
+    u_rows = float(np.mean(rows)) if rows else 0.0
+    u_svc = float(np.mean(svcs)) if svcs else 0.0
+    return (36.0 * ns + 8.0 * nw + u_rows * nw * 8.0 + (u_svc * ns * 4.0 if cnt_on else 0.0)
             + w * nw * 12.0 + w * 192.0)
 
 
@@ -337,7 +353,8 @@ def main():
         ev_s = kk["eval_ms"] / launches / 1e3 or float("nan")
         w_used = tot1["wcap_sum"] - tot0["wcap_sum"]
         w_mean = w_used / launches if w_used > 0 else float(wcap)
-        ev_bytes = _phase_a_bytes(cfg, batch.pods, n_nodes / world, nwords / world, w_mean)
+        ev_bytes = _phase_a_bytes(cfg, batch.pods[:4096], np.asarray(batch.ids), n_nodes / world, nwords / world,
+                                   w_mean)
         # (HIP events around every timed_launch_stride-th launch of a round, the
         # sampled mean scaled to all launches; KSG_KERNEL_EVENTS=N sets the stride)
         extra = {"launches": launches, "pods_per_launch": pods_per_launch,

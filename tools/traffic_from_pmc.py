@@ -4,7 +4,12 @@ profiles/traffic.json: HBM-side bytes per launch of each window-path kernel.
 
 Units and corrections follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section):
 FETCH_SIZE and WRITE_SIZE are reported in KiB; on gfx950 FETCH_SIZE counts half
-the bytes of a wide read (128-B requests tallied at 64 B), so it is doubled.
+the bytes of a wide read (128-B requests tallied at 64 B), so it is doubled. The
+doubling is calibrated here for every access width the kernels use
+(tools/fetch_calib.hip, profiles/r3_fetch_calib.json): contiguous 4-, 8- and
+16-B-per-lane reads, 8-B gathers one per 64-B or 128-B line, agent-scope (sc1)
+8-B loads -- FETCH_SIZE x 1024 is exactly half the bytes of the 128-B lines
+touched in each case.
 
 usage: tools/traffic_from_pmc.py <prof_dir> <workload> <n_nodes> [profiles/traffic.json]
 """
@@ -14,7 +19,8 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = {"ksg_win_resolve_kernel": "ksg_win_resolve_kernel", "ksg_win_resolve2_kernel": "ksg_win_resolve2_kernel",
+KERNELS = {"ksg_win_plain_kernel": "ksg_win_plain_kernel", "ksg_win_t0_kernel": "ksg_win_t0_kernel",
+           "ksg_win_resolve_kernel": "ksg_win_resolve_kernel", "ksg_win_resolve2_kernel": "ksg_win_resolve2_kernel",
            "ksg_win_resolve3_kernel": "ksg_win_resolve3_kernel", "ksg_win_score_kernel": "ksg_win_score_kernel",
            "ksg_batch_kernel": "ksg_batch_kernel"}
 
@@ -47,7 +53,7 @@ def main():
         wb = write.get(k, 0.0)
         tj[f"{wl}:{n_nodes}:{k}"] = {"hbm_bytes_per_launch": fb + wb, "fetch_bytes_per_launch": fb,
                                      "write_bytes_per_launch": wb, "source": os.path.basename(prof.rstrip("/")),
-                                     "note": "FETCH_SIZE KiB x1024 x2 (gfx950) + WRITE_SIZE KiB x1024, mean per launch"}
+                                     "note": "FETCH_SIZE KiB x1024 x2 (gfx950, calibrated: profiles/r3_fetch_calib.json) + WRITE_SIZE KiB x1024, mean per launch"}
         print(k, tj[f"{wl}:{n_nodes}:{k}"])
     with open(out, "w") as f:
         json.dump(tj, f, indent=1, sort_keys=True)
