@@ -221,12 +221,16 @@ int ksg_remove_pod(ksg_ctx* ctx, uint64_t uid);
  * the tie_index-th tie in descending name order (generic_scheduler.go:88-95)
  * and applies AssumePod's delta. fail_codes (optional, n_nodes bytes) gets the
  * per-node KSG_FAIL_* code to rebuild FailedPredicateMap.
- * On one rank (shards up to 16,384 nodes, int32 scores) both calls are served
- * by a resident workgroup polling mapped host memory (ksg_serve.hip): no
- * kernel launch, copy or stream synchronisation per call. It returns after
- * KSG_SERVE_IDLE_US (default 20,000) without a request and is relaunched by
- * the next one; any other entry point that needs the device stops it first.
- * KSG_SERVE=0 in the environment at ksg_create: kernels launched per call. */
+ * On one rank (int32 scores; plain shards up to 65,280 nodes, others up to
+ * 16,384) both calls are served by a resident kernel polling mapped host memory
+ * (ksg_serve.hip): no kernel launch, copy or stream synchronisation per call.
+ * begin returns the pod's tie words with its answer, and commit picks the node
+ * from them on the host and returns at once: AssumePod's delta is applied on
+ * the device before any later call reads device state (a rejected commit is
+ * reported by the next call). The server returns after KSG_SERVE_IDLE_US
+ * (default 20,000) without a request and is relaunched by the next one; any
+ * other entry point that needs the device stops it first. KSG_SERVE=0 in the
+ * environment at ksg_create: kernels launched per call. */
 int ksg_schedule_begin(ksg_ctx* ctx, const ksg_pod* pod, const uint32_t* ids,
                        int64_t* max_score, uint32_t* tie_count, uint8_t* fail_codes);
 int ksg_schedule_commit(ksg_ctx* ctx, uint32_t tie_index, int32_t* out_node);
