@@ -709,14 +709,15 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
         if (c.error) {
           err = 1;
         } else {
+          // the word masks' row loads in flight with pod_resolve's service loads, then the table
+          const uint32_t nwq = (dw.hi - dw.lo + 63) >> 6;
+          if (tid < nwq) word_masks(dw, c, tid, s_wm, NW);
           int32_t n_tab = 0;
           if (need_cnt && c.spread_max > 0) {
             n_tab = c.spread_max >= KSG_NT ? KSG_NT : c.spread_max + 1;
             for (int32_t t = (int32_t)tid; t < n_tab; t += KSG_GSRV_NT)
               s_tab[t] = (int32_t)frac10_f32((int64_t)c.spread_max - t, c.spread_max);
           }
-          const uint32_t nwq = (dw.hi - dw.lo + 63) >> 6;
-          if (tid < nwq) word_masks(dw, c, tid, s_wm, NW);
           __syncthreads();  // (the word masks and the table)
           if (tid == 0) grid_mark(a, 1 + w, T, 4);
           if ((a.stamps & 1u) && tid == 0) s_ready = (uint32_t)wall_clock64();
