@@ -307,7 +307,7 @@ int ksg_debug_counters(ksg_ctx* ctx, int32_t* out32);
 /* Diagnostics of the resident begin/commit server: out4[0] kernel launches,
  * [1] requests served (begin, commit, patch, exit), [2] 1 while resident,
  * [3] 1 when this context uses the one-workgroup server, 2 the grid server
- * (one scan workgroup per 256 nodes; plain configurations past 1,024 nodes,
+ * (one scan workgroup per 256 nodes; every plain shard by default,
  * KSG_SERVE_GRID=0 / KSG_SERVE_GRID_MIN), 0 none. No reference counterpart. */
 int ksg_serve_stats(ksg_ctx* ctx, uint64_t* out4);
 

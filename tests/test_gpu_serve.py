@@ -113,11 +113,13 @@ def test_serve_interleaved_with_add_remove_evaluate_batch(name, nn, npods):
     dev.close()
 
 
-@pytest.mark.parametrize("nn", [900, 2500])  # the one-workgroup server, the grid server
-def test_serve_idle_timeout_relaunch(nn, monkeypatch):
+@pytest.mark.parametrize("nn,grid", [(900, False), (900, True), (2500, True)])
+def test_serve_idle_timeout_relaunch(nn, grid, monkeypatch):
     """A 1-us idle limit: the server returns between nearly every pair of
-    requests, between a begin and its commit too (the commit rescans)."""
+    requests, between a begin and its commit too (the relaunched server is
+    offered every request after the last one the host saw served)."""
     monkeypatch.setenv("KSG_SERVE_IDLE_US", "1")
+    monkeypatch.setenv("KSG_SERVE_GRID", "1" if grid else "0")
     case = Case("config2", nn, 300)
     dev = DeviceScheduler(case.cfg, device=0)
     orc = OracleScheduler(case.cfg)
