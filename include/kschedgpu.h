@@ -215,6 +215,23 @@ int ksg_set_cluster(ksg_ctx* ctx, const ksg_node* nodes, uint32_t n_nodes,
 int ksg_add_pod(ksg_ctx* ctx, uint32_t host_id, const ksg_pod* pod, const uint32_t* ids);
 int ksg_remove_pod(ksg_ctx* ctx, uint64_t uid);
 
+/* Static node terms beyond the config's fixed slots (more LabelsPresence
+ * predicates or keys than KSG_MAX_PRESENCE x KSG_MAX_PRESENCE_KEYS, more
+ * LabelPreference priorities than KSG_MAX_LABEL_PREF): the caller evaluates
+ * them per node from the node labels and folds them in after ksg_set_cluster
+ * (they end with that node list: call again after the next one).
+ * fit_words (optional): ceil(n_nodes / 64) words in node-rank order, bit n%64
+ * of word n/64 set iff node n passes every extra LabelsPresence predicate
+ * (CheckNodeLabelPresence, predicates.go:194-229); a node that fails gets
+ * KSG_FAIL_LABELSPRESENCE. score (optional): n_nodes Go-int sums of weight x
+ * CalculateNodeLabelPriority (priorities.go:98-134) over the extra priorities,
+ * added to every node's combined score with Go's wrap; score_weighted != 0
+ * when any of them has a nonzero weight (the HostPriorityList is then not
+ * empty). The config's predicates must include KSG_PRED_LABELSPRESENCE and its
+ * n_priority_configs count the extra priorities. No reference counterpart (the
+ * reference's registry takes any number of them: plugins.go:81-117, 145-183). */
+int ksg_set_static_terms(ksg_ctx* ctx, const uint64_t* fit_words, const int64_t* score, int score_weighted);
+
 /* Split Schedule: begin evaluates every node and reports the best combined
  * score and the number of nodes tied at it (0 => KSG_NOFIT). The caller draws
  * r = rand.Int() iff tie_count > 0 and calls commit(r % tie_count), which picks

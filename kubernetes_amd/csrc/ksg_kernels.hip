@@ -509,6 +509,28 @@ hipError_t ksg_launch_static(const KsgStaticCfg& sc, uint32_t n_nodes, const ksg
   return hipGetLastError();
 }
 
+// ksg_set_static_terms: the caller's static node terms folded into the
+// config's (LabelsPresence predicates: AND of the fit words; LabelPreference
+// priorities: Go-int sum of the scores). own_fit / own_score: 0 when the config
+// set none (the arrays hold no terms yet: assign instead).
+__global__ void ksg_static_fold_kernel(uint64_t* static_fit, int64_t* static_score, const uint64_t* xfit,
+                                       const int64_t* xscore, uint32_t nw, uint32_t n, int own_fit, int own_score) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (xfit && t < nw) static_fit[t] = own_fit ? (static_fit[t] & xfit[t]) : xfit[t];
+  if (xscore && t < n)
+    static_score[t] = own_score ? (int64_t)((uint64_t)static_score[t] + (uint64_t)xscore[t]) : xscore[t];
+}
+
+hipError_t ksg_launch_static_fold(uint64_t* static_fit, int64_t* static_score, const uint64_t* xfit,
+                                  const int64_t* xscore, uint32_t nw, uint32_t n, int own_fit, int own_score,
+                                  hipStream_t st) {
+  const uint32_t blocks = ((nw > n ? nw : n) + 255) / 256;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(ksg_static_fold_kernel, dim3(blocks), dim3(256), 0, st, static_fit, static_score, xfit, xscore,
+                     nw, n, own_fit, own_score);
+  return hipGetLastError();
+}
+
 hipError_t ksg_launch_zonemap(uint32_t n_nodes, const int32_t* anti_domain, uint32_t d0, uint32_t nw,
                               uint64_t* zmap, hipStream_t st) {
   const uint32_t blocks = (n_nodes + 255) / 256;

@@ -64,6 +64,9 @@ hipError_t ksg_launch_static(const KsgStaticCfg& sc, uint32_t n_nodes, const ksg
                              uint64_t* static_fit, int64_t* static_score, int32_t* anti_domain,
                              int32_t* aff_pair, unsigned long long* pairmap, hipStream_t st);
 hipError_t ksg_launch_patch(const KsgPatch* patches, uint32_t n, hipStream_t st);
+hipError_t ksg_launch_static_fold(uint64_t* static_fit, int64_t* static_score, const uint64_t* xfit,
+                                  const int64_t* xscore, uint32_t nw, uint32_t n, int own_fit, int own_score,
+                                  hipStream_t st);
 hipError_t ksg_launch_serve(int R, bool anti, bool ext, const KsgDev& d, const KsgSrvArgs& a, hipStream_t st);
 hipError_t ksg_launch_serve_grid(const KsgDev& d, const KsgSrvArgs& a, hipStream_t st);
 hipError_t ksg_launch_admit(const ksg_admission_set* sets, uint32_t n_sets, const ksg_pod* pods,
@@ -256,6 +259,7 @@ struct ksg_ctx {
   bool srv_stamps = false;      // KSG_SERVE_STAMPS=1: sum the server's per-stage cycles of each begin
   int64_t srv_grid_opts = -1;   // KSG_SERVE_GRID_OPTS (KsgSrvArgs.grid_opts; -1: by size)
   bool srv_debug = false;
+  unsigned __int128 static_mag = 0;  // max |score| of the terms ksg_set_static_terms added
   bool srv_trace = false;       // KSG_SERVE_TRACE=1: every post, wait and relaunch to stderr       // KSG_SERVE_DEBUG=1: the grid server's stage markers, reported on a fault
   double srv_stage[6] = {};     // (printed by ksg_destroy)
   uint64_t srv_stamped = 0;
@@ -1436,6 +1440,7 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   d.empty_priorities = (!d.equal_fallback && !any_weight) ? 1 : 0;
   // int64 combined scores (exact kernels) once a |score| could reach KSG_SCORE_BOUND
   d.wide = score_bound(c->cfg, c->ext.w_taint_toleration, c->ext.w_balanced) >= (unsigned __int128)KSG_SCORE_BOUND;
+  c->static_mag = 0;  // (ksg_set_static_terms' terms end with the node list they were built for)
   d.w_lr = c->cfg.w_least_requested;
   d.w_spread = c->cfg.w_service_spreading;
   d.n_anti = 0;
@@ -1505,6 +1510,45 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   HIPCHK(c, hipStreamSynchronize(c->st));
   reset_mirror(c);
   c->have_cluster = true;
+  return KSG_OK;
+}
+
+int ksg_set_static_terms(ksg_ctx* c, const uint64_t* fit_words, const int64_t* score, int score_weighted) {
+  if (!c || (!fit_words && !score)) return KSG_ERR_ARG;
+  KSG_LOCK(c);
+  if (int rs = cluster_ok(c)) return rs;
+  if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
+  if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint32_t N = c->N, nw = (N + 63) / 64;
+  if (N == 0) return KSG_OK;
+  // a combined score stays int32 on the fast paths only while every |score| < 2^30
+  unsigned __int128 mag = 0;
+  if (score)
+    for (uint32_t n = 0; n < N; ++n) {
+      const unsigned __int128 m = score[n] < 0 ? (unsigned __int128)(0 - (uint64_t)score[n]) : (unsigned __int128)score[n];
+      mag = std::max(mag, m);
+    }
+  uint8_t* tmp = nullptr;
+  const size_t fb = fit_words ? (size_t)nw * 8 : 0, sb = score ? (size_t)N * 8 : 0;
+  HIPCHK(c, hipMalloc((void**)&tmp, fb + sb));
+  if (fit_words) HIPCHK(c, hipMemcpyAsync(tmp, fit_words, fb, hipMemcpyHostToDevice, c->st));
+  if (score) HIPCHK(c, hipMemcpyAsync(tmp + fb, score, sb, hipMemcpyHostToDevice, c->st));
+  KsgDev& d = c->dev;
+  HIPCHK(c, ksg_launch_static_fold(const_cast<uint64_t*>(d.static_fit), const_cast<int64_t*>(d.static_score),
+                                   fit_words ? reinterpret_cast<const uint64_t*>(tmp) : nullptr,
+                                   score ? reinterpret_cast<const int64_t*>(tmp + fb) : nullptr, nw, N,
+                                   d.has_static_fit, d.has_static_score, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  (void)hipFree(tmp);
+  if (fit_words) d.has_static_fit = 1;
+  if (score) {
+    d.has_static_score = 1;
+    c->static_mag += mag;
+    if (score_weighted) d.empty_priorities = 0;
+  }
+  d.wide = score_bound(c->cfg, c->ext.w_taint_toleration, c->ext.w_balanced) + c->static_mag >=
+           (unsigned __int128)KSG_SCORE_BOUND;
   return KSG_OK;
 }
 

@@ -281,6 +281,16 @@ class DeviceScheduler:
                 "host_us": {k: float(v) for k, v in zip(self.HOST_PHASES, o[9:17])},
                 "wcap_sum": float(o[17])}
 
+    def set_static_terms(self, fit_words, score, weighted: bool):
+        """ksg_set_static_terms: static node terms past the config's slots (after
+        set_cluster; fit_words uint64[ceil(N/64)] or None, score int64[N] or None)."""
+        fw = None if fit_words is None else np.ascontiguousarray(fit_words, np.uint64)
+        sc = None if score is None else np.ascontiguousarray(score, np.int64)
+        rc = self._lib.ksg_set_static_terms(self._ctx, None if fw is None else abi.ptr(fw),
+                                            None if sc is None else abi.ptr(sc), 1 if weighted else 0)
+        if rc != abi.KSG_OK:
+            self._err(rc)
+
     def serve_stats(self) -> dict:
         """The resident begin/commit server (ksg_serve_stats)."""
         o = np.zeros(4, np.uint64)

@@ -231,23 +231,70 @@ class SchedulerConfig:
         }
         return {c: by_kind.get(kind, kind) for c, kind in codes.items()}
 
-    def compile(self, key_id) -> abi.KsgConfig:
-        """-> ksg_config. key_id(label_key) interns a label key to its id."""
-        cfg = abi.KsgConfig()
-        bits = 0
-        presence = []
+    def split_static(self):
+        """The static node terms that fit ksg_config's slots and the ones past them:
+        (slotted LabelsPresence, extra LabelsPresence, slotted LabelPreference, extra
+        LabelPreference). Extras are evaluated on the host per node (static_terms)
+        and folded in with ksg_set_static_terms: the reference registers any number
+        of them (plugins.go:81-117, 145-183)."""
+        p_slot, p_extra = [], []
         for name in sorted(self.predicates):
             d = self.predicates[name]
-            bits |= _BUILTIN_PRED_BITS[d.kind]
             if d.kind == "LabelsPresence":
-                presence.append(d)
+                fits = len(p_slot) < abi.MAX_PRESENCE and len(d.labels) <= abi.MAX_PRESENCE_KEYS
+                (p_slot if fits else p_extra).append(d)
+        l_slot, l_extra = [], []
+        for p in self.priorities:
+            if p.kind == "LabelPreference":
+                (l_slot if len(l_slot) < abi.MAX_LABEL_PREF else l_extra).append(p)
+        return p_slot, p_extra, l_slot, l_extra
+
+    def static_terms(self, nodes):
+        """The extra static terms over `nodes` (node-rank order): (fit words | None,
+        scores | None, weighted). A node passes a LabelsPresence predicate iff every
+        label's presence matches (CheckNodeLabelPresence, predicates.go:194-229); a
+        LabelPreference priority scores 10 where the label's presence matches, else 0
+        (CalculateNodeLabelPriority, priorities.go:98-134), times its weight, summed as
+        Go ints (generic_scheduler.go:145-159)."""
+        import numpy as np
+
+        _, p_extra, _, l_extra = self.split_static()
+        n = len(nodes)
+        fit = score = None
+        if p_extra:
+            ok = np.ones(n, dtype=bool)
+            for i, node in enumerate(nodes):
+                labels = node.metadata.labels or {}
+                for d in p_extra:
+                    for l in d.labels:
+                        if (l in labels) != bool(d.presence):
+                            ok[i] = False
+            words = np.zeros((n + 63) // 64, dtype=np.uint64)
+            for i in np.nonzero(ok)[0]:
+                words[i >> 6] |= np.uint64(1) << np.uint64(i & 63)
+            fit = words
+        if l_extra:
+            s = [0] * n
+            for i, node in enumerate(nodes):
+                labels = node.metadata.labels or {}
+                for p in l_extra:
+                    if (p.label in labels) == bool(p.presence):
+                        s[i] = _go_int(s[i] + 10 * int(p.weight))
+            score = np.asarray(s, dtype=np.int64)
+        weighted = any(int(p.weight) != 0 for p in l_extra)
+        return fit, score, weighted
+
+    def compile(self, key_id) -> abi.KsgConfig:
+        """-> ksg_config. key_id(label_key) interns a label key to its id. Static
+        terms past the config's slots are left to static_terms / ksg_set_static_terms."""
+        cfg = abi.KsgConfig()
+        bits = 0
+        for name in sorted(self.predicates):
+            bits |= _BUILTIN_PRED_BITS[self.predicates[name].kind]
         cfg.predicates = bits
-        if len(presence) > abi.MAX_PRESENCE:
-            raise ConfigError("too many LabelsPresence predicates")
+        presence, _, prefs, _ = self.split_static()
         cfg.n_presence = len(presence)
         for q, d in enumerate(presence):
-            if len(d.labels) > abi.MAX_PRESENCE_KEYS:
-                raise ConfigError("too many labels in a LabelsPresence predicate")
             cfg.presence_n_keys[q] = len(d.labels)
             for i, l in enumerate(d.labels):
                 cfg.presence_keys[q][i] = key_id(l)
@@ -296,8 +343,8 @@ class SchedulerConfig:
                 cfg.w_anti[n_anti] = p.weight
                 n_anti += 1
             elif p.kind == "LabelPreference":
-                if n_pref == abi.MAX_LABEL_PREF:
-                    raise ConfigError("too many LabelPreference priorities")
+                if n_pref == len(prefs):
+                    continue  # (past the slots: a static term, static_terms)
                 cfg.pref_key[n_pref] = key_id(p.label)
                 cfg.pref_presence[n_pref] = 1 if p.presence else 0
                 cfg.w_pref[n_pref] = p.weight

@@ -160,6 +160,9 @@ class GPUScheduler:
         if nsig != self._node_sig or ssig != self._svc_sig or self.view is None:
             self.view = ClusterView(nodes, services, self.interner)
             self.engine.set_cluster(self.view.arrays)
+            fit, score, weighted = self.config.static_terms(self.view.nodes)
+            if fit is not None or score is not None:  # LabelsPresence / LabelPreference past the slots
+                self.engine.set_static_terms(fit, score, weighted)
             self._node_sig, self._svc_sig = nsig, ssig
             self._mirror = {}
             self._assumed = []

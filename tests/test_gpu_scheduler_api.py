@@ -21,6 +21,8 @@ pytestmark = pytest.mark.gpu
     ("config2", 20, 80, True, 0),
     ("config4", 48, 100, True, 12),
     ("policy_labels", 30, 80, False, 6),
+    ("policy_many_labels", 90, 120, False, 8),  # static terms past the config's slots (ksg_set_static_terms)
+    ("policy_many_labels", 500, 30, True, 0),
 ])
 def test_schedule_matches_ref_model(name, nn, npods, tight, existing):
     w = _workload(name, nn, npods, tight, existing)
@@ -103,3 +105,34 @@ def test_unnamed_pods_relist_keeps_device_equal_to_lister():
             assert np.array_equal(got_c, want), (step, got_c, want)
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("nn,npods", [(300, 120), (600, 30)])
+def test_batch_with_static_terms_matches_ref_model(nn, npods):
+    """ksg_schedule_batch (window path) under a Policy with more LabelsPresence /
+    LabelPreference terms than the config's slots: the host-folded static terms
+    (ksg_set_static_terms) against the object-level restatement, pod by pod."""
+    w = _workload("policy_many_labels", nn, npods, False, 0)
+    lister_ref = R.PodLister([])
+    preds, prios = R.from_config(w.config, w.nodes, lister_ref, R.ServiceLister(w.services))
+    rnd_ref = SplitMix64Rand(91)
+    ref = R.GenericScheduler(preds, prios, lister_ref, rnd_ref)
+    want = []
+    for p in w.pods:
+        try:
+            h = ref.schedule(p, w.nodes)
+        except (R.FitError, KeyError):
+            want.append(None)
+            continue
+        want.append(h)
+        q = copy.copy(p)
+        q.status = PodStatus(host=h)
+        lister_ref.pods.append(q)
+    gpu = GPUScheduler(w.config, FakePodLister([]), FakeServiceLister(w.services))
+    try:
+        got, state = gpu.schedule_batch(w.pods, FakeMinionLister(w.nodes), 91)
+        assert got == want
+        assert state == rnd_ref.state
+        assert gpu.engine.batch_totals()["windows"] > 0  # (the window path ran)
+    finally:
+        gpu.close()

@@ -38,8 +38,40 @@ def _policy_labels():
     })
 
 
+def _policy_many_labels():
+    """More LabelsPresence predicates / keys and LabelPreference priorities than
+    ksg_config's slots: the rest go through ksg_set_static_terms."""
+    preds = [{"name": "PodFitsResources"}, {"name": "MatchNodeSelector"},
+             {"name": "HasZone", "argument": {"labelsPresence": {"labels": ["zone"], "presence": True}}},
+             {"name": "HasRegionRack", "argument": {"labelsPresence": {"labels": ["region", "rack"], "presence": True}}},
+             # one key past a slot's keys in one predicate
+             {"name": "NoA", "argument": {"labelsPresence": {"labels": [f"a{j}" for j in range(abi.MAX_PRESENCE_KEYS + 1)],
+                                                            "presence": False}}}]
+    preds += [{"name": f"NoU{j:02d}", "argument": {"labelsPresence": {"labels": [f"u{j}"], "presence": False}}}
+              for j in range(abi.MAX_PRESENCE + 1)]
+    prios = [{"name": "LeastRequestedPriority", "weight": 1}]
+    prios += [{"name": f"Pref{j:02d}", "weight": 1 + j % 5,
+               "argument": {"labelPreference": {"label": f"t{j}", "presence": j % 3 != 0}}}
+              for j in range(abi.MAX_LABEL_PREF + 4)]
+    return factory.create_from_config({"predicates": preds, "priorities": prios})
+
+
 def _workload(name, nn, npods, tight=False, existing=0, seed=7):
-    if name == "policy_labels":
+    if name == "policy_many_labels":
+        rng = workload._SM(seed)
+        nodes = workload.make_nodes(nn, rng, dense_labels=2)
+        for i, n in enumerate(nodes):  # t_j on every (j + 2)-th node; u_j, a4 on a few
+            for j in range(abi.MAX_LABEL_PREF + 4):
+                if i % (j + 2) == 0:
+                    n.metadata.labels[f"t{j}"] = "x"
+            for j in range(abi.MAX_PRESENCE + 1):
+                if i % (j + 23) == 7:
+                    n.metadata.labels[f"u{j}"] = "x"
+            if i % 13 == 5:
+                n.metadata.labels["a4"] = "y"
+        pods = workload.make_pods(npods, rng, n_apps=10)
+        w = workload.Workload(name, nodes, pods, workload.make_services(10), _policy_many_labels(), [])
+    elif name == "policy_labels":
         rng = workload._SM(seed)
         nodes = workload.make_nodes(nn, rng, dense_labels=2)
         for i, n in enumerate(nodes):  # some nodes lack zone / carry k9
