@@ -265,7 +265,8 @@ enum { KSG_SRVH_KIND = 0, KSG_SRVH_ARG, KSG_SRVH_RSV, KSG_SRVH_FLAGS, KSG_SRVH_P
 // answers each once it is applied, so a BEGIN posted after that answer scans
 // the state it left.
 #define KSG_GSRV_NT 256
-#define KSG_GSRV_MAXW 255  // scan workgroups: shards up to 65,280 nodes
+#define KSG_GSRV_MAXW 255  // scan workgroups: shards up to 65,280 nodes (261,120 at 4 nodes per thread)
+#define KSG_GSRV_TIEW 16   // tie words of a scan workgroup at 4 nodes per thread
 struct alignas(64) KsgSrvPart {
   uint32_t seq;     // the BEGIN this part answers (its 16-B store comes last)
   int32_t max;      // best score over the workgroup's nodes (KSG_S32_NONE: none fits)
@@ -287,6 +288,7 @@ struct KsgSrvBox {
   uint32_t dbg[256];  // KSG_SERVE_DEBUG: the last stage each workgroup of the server reached (seq << 8 | stage)
   uint64_t ties[KSG_SRV_MAX_R * 16];  // the one-workgroup server's tie words of the last BEGIN
   KsgSrvPart part[KSG_GSRV_MAXW];     // the grid server's parts of the last BEGIN
+  uint64_t part_tie[KSG_GSRV_MAXW * KSG_GSRV_TIEW];  // ... their tie words at 4 nodes per thread
 };
 struct KsgSrvGrid {
   uint32_t quit;     // == the launch's epoch: the scan workgroups return

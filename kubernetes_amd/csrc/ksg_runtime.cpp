@@ -68,7 +68,7 @@ hipError_t ksg_launch_static_fold(uint64_t* static_fit, int64_t* static_score, c
                                   const int64_t* xscore, uint32_t nw, uint32_t n, int own_fit, int own_score,
                                   hipStream_t st);
 hipError_t ksg_launch_serve(int R, bool anti, bool ext, const KsgDev& d, const KsgSrvArgs& a, hipStream_t st);
-hipError_t ksg_launch_serve_grid(const KsgDev& d, const KsgSrvArgs& a, hipStream_t st);
+hipError_t ksg_launch_serve_grid(int npt, const KsgDev& d, const KsgSrvArgs& a, hipStream_t st);
 hipError_t ksg_launch_admit(const ksg_admission_set* sets, uint32_t n_sets, const ksg_pod* pods,
                             const uint32_t* ids, const uint32_t* pairs, int mode, uint8_t* out, hipStream_t st);
 
@@ -251,6 +251,7 @@ struct ksg_ctx {
   ksg_pod_ext srv_pext{};
   uint64_t srv_launches = 0;
   bool srv_grid_on = true;       // KSG_SERVE_GRID=0: the one-workgroup server at every size
+  uint32_t srv_npt4_min = 16384;  // KSG_SERVE_GRID_NPT4_MIN: past this many nodes 4 nodes per thread
   uint32_t srv_grid_min = 0;  // KSG_SERVE_GRID_MIN: shards above this many nodes take the grid server
                               // (it beats the one-workgroup server at 500 nodes already: 7.2 vs 10.9 us)
   KsgSrvGrid* srv_grid = nullptr;  // its device state (+ the fail codes)
@@ -775,10 +776,12 @@ int wait_device(ksg_ctx* c) {
 // ---- the resident drop-in server (ksg_serve.hip) ------------------------------
 // the grid server: plain configurations (no ServiceAntiAffinity, no extensions)
 // past srv_grid_min nodes, one scan workgroup per 256 nodes (<= 255)
+// nodes per thread of the grid server's scan workgroups
+uint32_t srv_npt(const ksg_ctx* c) { return c->hi - c->lo > c->srv_npt4_min ? 4u : 1u; }
+
 bool srv_grid(const ksg_ctx* c) {
-  const uint32_t n = c->hi - c->lo;
-  return c->srv_grid_on && !anti_on(c) && !c->ext_on && n > c->srv_grid_min &&
-         (n + KSG_GSRV_NT - 1) / KSG_GSRV_NT <= KSG_GSRV_MAXW;
+  const uint32_t n = c->hi - c->lo, per = KSG_GSRV_NT * srv_npt(c);
+  return c->srv_grid_on && !anti_on(c) && !c->ext_on && n > c->srv_grid_min && (n + per - 1) / per <= KSG_GSRV_MAXW;
 }
 
 bool srv_eligible(const ksg_ctx* c) {
@@ -825,11 +828,12 @@ int srv_launch(ksg_ctx* c, uint32_t start_seq) {
       c->srv_grid_cap = need;
     }
     a.grid = c->srv_grid;
-    a.n_workers = (n + KSG_GSRV_NT - 1) / KSG_GSRV_NT;
+    const uint32_t npt = srv_npt(c);
+    a.n_workers = (n + KSG_GSRV_NT * npt - 1) / (KSG_GSRV_NT * npt);
     // past 64 scan workgroups their polls of the host block crowd the link: each sleeps ~0.2 us
     // more between polls (measured: 50,000 nodes 73 -> 38 us per pod; no gain at 15,000)
     a.grid_opts = c->srv_grid_opts >= 0 ? (uint32_t)c->srv_grid_opts : a.n_workers > 64 ? 0x10u : 0u;
-    HIPCHK(c, ksg_launch_serve_grid(c->dev, a, c->st));
+    HIPCHK(c, ksg_launch_serve_grid((int)npt, c->dev, a, c->st));
   } else {
     HIPCHK(c, ksg_launch_serve(c->R, anti_on(c), c->ext_on, c->dev, a, c->st));
   }
@@ -948,7 +952,7 @@ int srv_begin(ksg_ctx* c, const uint32_t* hdr, uint32_t* resp4) {
       c->srv_tw.assign(c->srv_box->ties, c->srv_box->ties + nwd);
     return KSG_OK;
   }
-  const uint32_t G = (n + KSG_GSRV_NT - 1) / KSG_GSRV_NT;
+  const uint32_t npt = srv_npt(c), G = (n + KSG_GSRV_NT * npt - 1) / (KSG_GSRV_NT * npt), NWG = 4 * npt;
   uint32_t seq = 0;
   if (int rc = srv_post(c, hdr, &seq)) return rc;
   if (int rc = srv_wait(c, seq, G)) return rc;
@@ -960,12 +964,13 @@ int srv_begin(ksg_ctx* c, const uint32_t* hdr, uint32_t* resp4) {
     err |= pt[q].err;
   }
   uint32_t k = 0;
-  c->srv_tw.assign((size_t)G * 4, 0);
+  c->srv_tw.assign((size_t)G * NWG, 0);
   if (M != KSG_S32_NONE)
     for (uint32_t q = 0; q < G; ++q)
       if (pt[q].max == M) {
         k += pt[q].cnt;
-        for (int r = 0; r < 4; ++r) c->srv_tw[(size_t)q * 4 + r] = pt[q].tie[r];
+        const uint64_t* tw = npt == 1 ? pt[q].tie : c->srv_box->part_tie + (size_t)q * KSG_GSRV_TIEW;
+        for (uint32_t r = 0; r < NWG; ++r) c->srv_tw[(size_t)q * NWG + r] = tw[r];
       }
   c->srv_tw.resize(nwd);
   if (c->srv_stamps) {  // worker 0: masks + loads, eval + publish (100-MHz ticks)
@@ -1159,6 +1164,7 @@ static int create_impl(const ksg_config* cfg, int device, int rank, int world, c
   if (const char* iu = getenv("KSG_SERVE_IDLE_US")) c->srv_idle_us = (uint64_t)std::max(atoll(iu), 1LL);
   c->srv_grid_on = !(getenv("KSG_SERVE_GRID") && atoi(getenv("KSG_SERVE_GRID")) == 0);
   if (const char* gm = getenv("KSG_SERVE_GRID_MIN")) c->srv_grid_min = (uint32_t)std::max(atoi(gm), 0);
+  if (const char* g4 = getenv("KSG_SERVE_GRID_NPT4_MIN")) c->srv_npt4_min = (uint32_t)std::max(atoi(g4), 0);
   if (const char* rm = getenv("KSG_ROUND_MARGIN")) c->round_margin = std::min(std::max(atof(rm), 0.5), 4.0);
   // The exchange path (shard scan, all-gather of per-shard records, replicated
   // resolve) runs for world > 1, and for a 1-rank RCCL communicator when the caller

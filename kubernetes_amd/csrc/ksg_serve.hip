@@ -628,12 +628,15 @@ __device__ __forceinline__ void grid_load_ext(const uint32_t* xa, uint32_t* s_re
       s_req[KSG_SRV_HDR_DW + KSG_SRV_INLINE_DW + t] = sys_ld32(xa + t);
 }
 
+// NPT nodes per thread: 256 x NPT nodes per scan workgroup (NPT = 4 past
+// KSG_SERVE_GRID_NPT4_MIN nodes: a quarter of the pollers on the link)
+template <int NPT>
 __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, KsgSrvArgs a) {
-  constexpr uint32_t NW = KSG_GSRV_NT / 64;
+  constexpr uint32_t NODES = NPT * KSG_GSRV_NT, NW = NODES / 64, NWV = KSG_GSRV_NT / 64;
   __shared__ __attribute__((aligned(16))) uint32_t s_req[KSG_SRV_HDR_DW + KSG_SRV_PAY_DW];
   __shared__ int32_t s_tab[KSG_NT];
   __shared__ uint64_t s_wm[WM_N * NW];
-  __shared__ int32_t s_wmax[NW];
+  __shared__ int32_t s_wmax[NWV];
   __shared__ uint32_t s_wcnt[NW];
   __shared__ uint64_t s_tw[NW];
   __shared__ uint32_t s_kind, s_seq, s_ready;
@@ -648,11 +651,17 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
     // ======================= scan workgroup w: BEGIN =======================
     const uint32_t w = blockIdx.x - 1;
     KsgDev dw = d;  // this workgroup's nodes: [lo, hi) of the shard
-    dw.lo = d.lo + w * KSG_GSRV_NT;
-    dw.hi = min(d.hi, dw.lo + KSG_GSRV_NT);
-    const uint32_t n = dw.lo + tid;
-    const bool valid = n < dw.hi;
-    const uint32_t nn = valid ? n : dw.lo;
+    dw.lo = d.lo + w * NODES;
+    dw.hi = min(d.hi, dw.lo + NODES);
+    // this thread's nodes: dw.lo + j * 256 + tid (word j * 4 + wave, bit lane)
+    uint32_t nn[NPT];
+    bool valid[NPT];
+#pragma unroll
+    for (int j = 0; j < NPT; ++j) {
+      const uint32_t n = dw.lo + j * KSG_GSRV_NT + tid;
+      valid[j] = n < dw.hi;
+      nn[j] = valid[j] ? n : dw.lo;
+    }
     KsgSrvPart* hp = a.box->part + w;
     for (;;) {
       __syncthreads();
@@ -672,10 +681,18 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
       if (kind != KSG_SRV_BEGIN) continue;
       const uint64_t ts_seen = wall_clock64();
       if (tid == 0) grid_mark(a, 1 + w, T, 1);
-      // this thread's node: the loads of its static data in flight with the payload's
-      const int64_t capc = d.cap_cpu[nn], capm = d.cap_mem[nn];
-      const double invc = d.w_lr ? d.inv10_cpu[nn] : 0.0, invm = d.w_lr ? d.inv10_mem[nn] : 0.0;
-      const int32_t ss = d.has_static_score ? (int32_t)d.static_score[nn] : 0;
+      // the loads of the nodes' static data in flight with the payload's
+      int64_t capc[NPT], capm[NPT], usedc[NPT], usedm[NPT];
+      double invc[NPT], invm[NPT];
+      int32_t ss[NPT], cnt[NPT];
+#pragma unroll
+      for (int j = 0; j < NPT; ++j) {
+        capc[j] = d.cap_cpu[nn[j]];
+        capm[j] = d.cap_mem[nn[j]];
+        invc[j] = d.w_lr ? d.inv10_cpu[nn[j]] : 0.0;
+        invm[j] = d.w_lr ? d.inv10_mem[nn[j]] : 0.0;
+        ss[j] = d.has_static_score ? (int32_t)d.static_score[nn[j]] : 0;
+      }
       grid_load_ext(a.box->ext, s_req, tid);
       if (wave == 0) {  // the control requests posted before this BEGIN are applied (commits it must see)
         const uint32_t after = s_req[KSG_SRVH_ARG];
@@ -690,9 +707,15 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
       __syncthreads();
       if (s_kind == 0) return;
       // mutable state only from here on (issued after `applied` covers the BEGIN's ARG)
-      const int64_t usedc = ld_mut(d.used_cpu + nn), usedm = ld_mut(d.used_mem + nn);
+#pragma unroll
+      for (int j = 0; j < NPT; ++j) {
+        usedc[j] = ld_mut(d.used_cpu + nn[j]);
+        usedm[j] = ld_mut(d.used_mem + nn[j]);
+      }
       const bool want_fail = (s_req[KSG_SRVH_FLAGS] & KSG_SRVF_WANT_FAIL) != 0;
-      int32_t sc = KSG_S32_NONE;
+      int32_t sc[NPT];
+#pragma unroll
+      for (int j = 0; j < NPT; ++j) sc[j] = KSG_S32_NONE;
       uint32_t err = 0;
       if (req_bad(d, s_req)) {
         err = 2;
@@ -701,7 +724,9 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
         const ksg_pod& p = *reinterpret_cast<const ksg_pod*>(pay);
         const uint32_t* ids = pay + s_req[KSG_SRVH_IDS_AT];
         const bool need_cnt = d.w_spread && p.service >= 0 && !d.equal_fallback;
-        const int32_t cnt = need_cnt ? ld_mut(d.svc_cnt + (size_t)p.service * d.n_nodes + nn) : 0;
+#pragma unroll
+        for (int j = 0; j < NPT; ++j)
+          cnt[j] = need_cnt ? ld_mut(d.svc_cnt + (size_t)p.service * d.n_nodes + nn[j]) : 0;
         PodCtx c;
         pod_resolve(d, p, ids, c);
         c.ext = nullptr;
@@ -721,49 +746,82 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
           __syncthreads();  // (the word masks and the table)
           if (tid == 0) grid_mark(a, 1 + w, T, 4);
           if ((a.stamps & 1u) && tid == 0) s_ready = (uint32_t)wall_clock64();
-          int f;
           const bool res_on = (d.preds & KSG_PRED_PODFITSRESOURCES) && !c.zero_req;
-          const int32_t s = eval_node(d, c, n, bit, s_wm, NW, wave, res_on, capc, capm, usedc, usedm, invc, invm, ss,
-                                      cnt, s_tab, n_tab, f);
-          sc = (valid && f == KSG_FAIL_NONE) ? s : KSG_S32_NONE;
-          if (want_fail) {  // four nodes' codes per dword, straight into host memory
-            const uint32_t fb = valid ? (uint32_t)f : 0u;
-            const uint32_t b0 = __shfl(fb, (int)((lane * 4 + 0) & 63), 64), b1 = __shfl(fb, (int)((lane * 4 + 1) & 63), 64);
-            const uint32_t b2 = __shfl(fb, (int)((lane * 4 + 2) & 63), 64), b3 = __shfl(fb, (int)((lane * 4 + 3) & 63), 64);
-            const uint32_t at = w * KSG_GSRV_NT + wave * 64 + lane * 4;  // (shard-relative; the area is 4-padded)
-            if (lane < 16 && dw.lo + wave * 64 + lane * 4 < dw.hi)
-              *reinterpret_cast<volatile uint32_t*>(a.fail + at) = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+#pragma unroll
+          for (int j = 0; j < NPT; ++j) {
+            int f;
+            const uint32_t n = dw.lo + j * KSG_GSRV_NT + tid;
+            const int32_t s = eval_node(d, c, n, bit, s_wm, NW, j * NWV + wave, res_on, capc[j], capm[j], usedc[j],
+                                        usedm[j], invc[j], invm[j], ss[j], cnt[j], s_tab, n_tab, f);
+            sc[j] = (valid[j] && f == KSG_FAIL_NONE) ? s : KSG_S32_NONE;
+            if (want_fail) {  // four nodes' codes per dword, straight into host memory
+              const uint32_t fb = valid[j] ? (uint32_t)f : 0u;
+              const uint32_t b0 = __shfl(fb, (int)((lane * 4 + 0) & 63), 64), b1 = __shfl(fb, (int)((lane * 4 + 1) & 63), 64);
+              const uint32_t b2 = __shfl(fb, (int)((lane * 4 + 2) & 63), 64), b3 = __shfl(fb, (int)((lane * 4 + 3) & 63), 64);
+              const uint32_t off = j * KSG_GSRV_NT + wave * 64 + lane * 4;
+              if (lane < 16 && dw.lo + off < dw.hi)  // (shard-relative; the area is 4-padded)
+                *reinterpret_cast<volatile uint32_t*>(a.fail + w * NODES + off) = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+            }
           }
         }
       }
       // the part: best score, count and tie words of these nodes
-      const int32_t wm = wave_total_max(sc);
+      int32_t m = sc[0];
+#pragma unroll
+      for (int j = 1; j < NPT; ++j) m = max(m, sc[j]);
+      const int32_t wm = wave_total_max(m);
       if (lane == 0) s_wmax[wave] = wm;
       __syncthreads();
       int32_t M = s_wmax[0];
 #pragma unroll
-      for (uint32_t q = 1; q < NW; ++q) M = max(M, s_wmax[q]);
+      for (uint32_t q = 1; q < NWV; ++q) M = max(M, s_wmax[q]);
       if (d.empty_priorities) M = KSG_S32_NONE;  // all weights 0: an empty HostPriorityList
-      const uint64_t tb = __ballot(M != KSG_S32_NONE && sc == M);
-      if (lane == 0) {
-        s_tw[wave] = tb;
-        s_wcnt[wave] = (uint32_t)__popcll(tb);
+#pragma unroll
+      for (int j = 0; j < NPT; ++j) {
+        const uint64_t tb = __ballot(M != KSG_S32_NONE && sc[j] == M);
+        if (lane == 0) {
+          s_tw[j * NWV + wave] = tb;
+          s_wcnt[j * NWV + wave] = (uint32_t)__popcll(tb);
+        }
       }
       drain_stores();  // (this wave's fail-code stores)
       __syncthreads();
-      if (tid < 4) {  // the part: one 64-B store of 4 lanes, the sequence number at both ends
-        uint32_t k = 0;
+      if constexpr (NPT == 1) {
+        if (tid < 4) {  // the part: one 64-B store of 4 lanes, the sequence number at both ends
+          uint32_t k = 0;
 #pragma unroll
-        for (uint32_t q = 0; q < NW; ++q) k += s_wcnt[q];
-        const uint32_t r = (tid == 1 || tid == 2) ? tid - 1 : 0u;  // (lanes 1, 2: the tie words)
-        const uint64_t t0 = s_tw[2 * r], t1 = s_tw[2 * r + 1];
-        u32x4 v;
-        v.x = tid == 0 ? T : tid == 3 ? (uint32_t)ts_seen : (uint32_t)t0;
-        v.y = tid == 0 ? (uint32_t)M : tid == 3 ? s_ready : (uint32_t)(t0 >> 32);
-        v.z = tid == 0 ? k : tid == 3 ? (uint32_t)wall_clock64() : (uint32_t)t1;
-        v.w = tid == 0 ? err : tid == 3 ? T : (uint32_t)(t1 >> 32);
-        sys_st16(reinterpret_cast<uint32_t*>(hp) + 4 * tid, v);
-        if (tid == 0) grid_mark(a, 1 + w, T, 6);
+          for (uint32_t q = 0; q < NW; ++q) k += s_wcnt[q];
+          const uint32_t r = (tid == 1 || tid == 2) ? tid - 1 : 0u;  // (lanes 1, 2: the tie words)
+          const uint64_t t0 = s_tw[2 * r], t1 = s_tw[2 * r + 1];
+          u32x4 v;
+          v.x = tid == 0 ? T : tid == 3 ? (uint32_t)ts_seen : (uint32_t)t0;
+          v.y = tid == 0 ? (uint32_t)M : tid == 3 ? s_ready : (uint32_t)(t0 >> 32);
+          v.z = tid == 0 ? k : tid == 3 ? (uint32_t)wall_clock64() : (uint32_t)t1;
+          v.w = tid == 0 ? err : tid == 3 ? T : (uint32_t)(t1 >> 32);
+          sys_st16(reinterpret_cast<uint32_t*>(hp) + 4 * tid, v);
+          if (tid == 0) grid_mark(a, 1 + w, T, 6);
+        }
+      } else {
+        if (tid < NW / 2) {  // the tie words (acknowledged), then the header line
+          u32x4 v;
+          v.x = (uint32_t)s_tw[2 * tid];
+          v.y = (uint32_t)(s_tw[2 * tid] >> 32);
+          v.z = (uint32_t)s_tw[2 * tid + 1];
+          v.w = (uint32_t)(s_tw[2 * tid + 1] >> 32);
+          sys_st16(reinterpret_cast<uint32_t*>(a.box->part_tie + (size_t)w * KSG_GSRV_TIEW + 2 * tid), v);
+        }
+        if (tid < 4) {
+          uint32_t k = 0;
+#pragma unroll
+          for (uint32_t q = 0; q < NW; ++q) k += s_wcnt[q];
+          u32x4 v;
+          v.x = tid == 0 ? T : tid == 3 ? (uint32_t)ts_seen : 0u;
+          v.y = tid == 0 ? (uint32_t)M : tid == 3 ? s_ready : 0u;
+          v.z = tid == 0 ? k : tid == 3 ? (uint32_t)wall_clock64() : 0u;
+          v.w = tid == 0 ? err : tid == 3 ? T : 0u;
+          sys_st16(reinterpret_cast<uint32_t*>(hp) + 4 * tid, v);
+          if (tid == 0) grid_mark(a, 1 + w, T, 6);
+        }
       }
     }
   }
@@ -861,8 +919,11 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
   }
 }
 
-hipError_t ksg_launch_serve_grid(const KsgDev& d, const KsgSrvArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(ksg_serve_grid_kernel, dim3(a.n_workers + 1), dim3(KSG_GSRV_NT), 0, st, d, a);
+hipError_t ksg_launch_serve_grid(int npt, const KsgDev& d, const KsgSrvArgs& a, hipStream_t st) {
+  if (npt == 4)
+    hipLaunchKernelGGL(ksg_serve_grid_kernel<4>, dim3(a.n_workers + 1), dim3(KSG_GSRV_NT), 0, st, d, a);
+  else
+    hipLaunchKernelGGL(ksg_serve_grid_kernel<1>, dim3(a.n_workers + 1), dim3(KSG_GSRV_NT), 0, st, d, a);
   return hipGetLastError();
 }
 

@@ -83,7 +83,8 @@ def _drive(case, dev, orc, seed, n_pods, *, evaluate_every=0, batch_at=(), churn
     ("config4", 900, 400, False),     # ServiceAffinity + ServiceAntiAffinity
     ("config3", 15000, 200, False),   # R = 16
     ("config3", 15000, 200, True),
-    ("config2", 30000, 120, True),    # past the one-workgroup server's 16,384 nodes
+    ("config2", 30000, 120, True),    # past the one-workgroup server's 16,384 nodes (4 nodes per thread)
+    ("config5", 100000, 40, True),    # config 5's node count (98 scan workgroups of 1,024 nodes)
 ])
 def test_serve_begin_commit_matches_oracle(name, nn, npods, grid, monkeypatch):
     monkeypatch.setenv("KSG_SERVE_GRID", "1" if grid else "0")
@@ -151,3 +152,21 @@ def test_serve_matches_launch_per_call_path(monkeypatch):
             assert devs[0].commit(ix) == devs[1].commit(ix)
     for d in devs:
         d.close()
+
+
+@pytest.mark.parametrize("name,nn,npods,churn", [("config2", 2000, 300, 0.0), ("config1", 700, 300, 0.2),
+                                                 ("config2", 5000, 200, 0.1)])
+def test_serve_grid_four_nodes_per_thread(name, nn, npods, churn, monkeypatch):
+    """The grid server's 4-nodes-per-thread scan workgroups (the default past
+    16,384 nodes) forced at small sizes: partial last workgroups, fail codes,
+    tie words past the 64-B part, patches in between."""
+    monkeypatch.setenv("KSG_SERVE_GRID_NPT4_MIN", "0")
+    case = Case(name, nn, npods)
+    dev = DeviceScheduler(case.cfg, device=0)
+    orc = OracleScheduler(case.cfg)
+    dev.set_cluster(case.view.arrays)
+    orc.set_cluster(case.view.arrays)
+    _drive(case, dev, orc, seed=nn, n_pods=npods, churn=churn)
+    st = dev.serve_stats()
+    assert st["grid"] and st["requests"] >= npods, st
+    dev.close()
