@@ -238,7 +238,7 @@ int ksg_set_static_terms(ksg_ctx* ctx, const uint64_t* fit_words, const int64_t*
  * the tie_index-th tie in descending name order (generic_scheduler.go:88-95)
  * and applies AssumePod's delta. fail_codes (optional, n_nodes bytes) gets the
  * per-node KSG_FAIL_* code to rebuild FailedPredicateMap.
- * On one rank (int32 scores; plain shards up to 65,280 nodes, others up to
+ * On one rank (int32 scores; plain shards up to 261,120 nodes, others up to
  * 16,384) both calls are served by a resident kernel polling mapped host memory
  * (ksg_serve.hip): no kernel launch, copy or stream synchronisation per call.
  * begin returns the pod's tie words with its answer, and commit picks the node
