@@ -260,6 +260,17 @@ int ksg_schedule_batch(ksg_ctx* ctx, const ksg_pod* pods, uint32_t n,
                        const uint32_t* ids, uint32_t n_ids,
                        uint64_t* rng_state, int32_t* out_nodes);
 
+/* ksg_schedule_batch with the caller's own random source: draws[k] is the
+ * k-th rand.Int() value the caller's generator would return (e.g. a Go
+ * *rand.Rand's next n Int()s, n_draws >= n). Pod i that finds a node uses the
+ * next unused value, exactly as n sequential Schedule calls would
+ * (generic_scheduler.go:94); *draws_used = how many were used (the caller keeps
+ * the rest for its next call). The sequential path's stream is reproduced:
+ * no splitmix64. Every rank of a sharded context passes the same values. */
+int ksg_schedule_batch_draws(ksg_ctx* ctx, const ksg_pod* pods, uint32_t n, const uint32_t* ids,
+                             uint32_t n_ids, const uint64_t* draws, uint32_t n_draws, uint32_t* draws_used,
+                             int32_t* out_nodes);
+
 /* Introspection (HostPriorityList): per-node fail code and combined score for
  * a pod, without committing. score_out[i] is meaningful where fail_out[i]==0. */
 int ksg_evaluate(ksg_ctx* ctx, const ksg_pod* pod, const uint32_t* ids,

@@ -79,6 +79,7 @@ struct KsgDev {
   const double* inv10_mem;
   int64_t* used_cpu;
   int64_t* used_mem;
+  const uint64_t* draws;  // ksg_schedule_batch_draws: the caller's rand.Int() values (else splitmix64)
   const uint64_t* static_fit;
   const int64_t* static_score;
   uint64_t* keymap;
@@ -321,4 +322,12 @@ static inline KSG_HD uint64_t ksg_splitmix_next(uint64_t* s) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
   return z ^ (z >> 31);
+}
+// ... or the caller's own rand.Int() values, drawn ahead (ksg_schedule_batch_draws):
+// the state is then the index of the next value. state advance per draw:
+static inline KSG_HD uint64_t ksg_rng_step(const uint64_t* draws) { return draws ? 1ULL : 0x9E3779B97F4A7C15ULL; }
+// the draw at state s (the state before it): rand.Int() (generic_scheduler.go:94)
+static inline KSG_HD uint64_t ksg_rng_draw(const uint64_t* draws, uint64_t s) {
+  if (draws) return draws[s];
+  return ksg_splitmix_next(&s) >> 1;
 }

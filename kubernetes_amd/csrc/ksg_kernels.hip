@@ -94,7 +94,8 @@ __global__ __launch_bounds__(KSG_NT) void ksg_batch_kernel(KsgDev d, const ksg_p
       __syncthreads();
       continue;
     }
-    const uint64_t r = ksg_splitmix_next(&rng) >> 1;  // rand.Int() (generic_scheduler.go:94)
+    const uint64_t r = ksg_rng_draw(d.draws, rng);  // rand.Int() (generic_scheduler.go:94)
+    rng += ksg_rng_step(d.draws);
     const uint64_t target = k - 1 - (r % k);           // ix-th host in descending name order
     if (wave == 0) {
       const int32_t win = select_tie(s_tie, R * KSG_NWAVE, target, lane, d.lo);
@@ -261,7 +262,8 @@ __global__ __launch_bounds__(64) void ksg_decide_kernel(KsgDev d, const ksg_pod*
   uint64_t ix;
   if (mode == 1) {
     uint64_t rng = *rng_io;
-    ix = (ksg_splitmix_next(&rng) >> 1) % k;
+    ix = ksg_rng_draw(d.draws, rng) % k;
+    rng += ksg_rng_step(d.draws);
     if (lane == 0) *rng_io = rng;
   } else {
     ix = tie_index % k;

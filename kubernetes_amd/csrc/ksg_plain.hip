@@ -384,8 +384,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         __builtin_amdgcn_s_sleep(1);
       }
       pstamp(26);
-      uint64_t sm = rng0 + (uint64_t)idx * 0x9E3779B97F4A7C15ULL;
-      const uint64_t r = ksg_splitmix_next(&sm) >> 1;  // rand.Int() (generic_scheduler.go:94)
+      const uint64_t r = ksg_rng_draw(d.draws, rng0 + (uint64_t)idx * ksg_rng_step(d.draws));  // rand.Int() (generic_scheduler.go:94)
       uint32_t mv = 0;
       if (drawable && lane < k0) mv = umod64_32(r, k0 - lane);
       const uint32_t n_svcs = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NSS) >> 16;
@@ -1367,7 +1366,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     drain_stores();
   }
   if (lane == 0) {
-    *rng_io = rng0 + (uint64_t)n_draws * 0x9E3779B97F4A7C15ULL;
+    *rng_io = rng0 + (uint64_t)n_draws * ksg_rng_step(d.draws);
     if (reason == KSG_STOP_HANG) {
       run->halt = KSG_HALT_HANG;
     } else if (reason == KSG_STOP_OVERSIZE) {

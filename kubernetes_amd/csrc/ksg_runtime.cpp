@@ -164,6 +164,9 @@ struct ksg_ctx {
   uint8_t* d_map = nullptr;  // its device address
   KsgPatch* d_patch = nullptr;
   size_t patch_cap = 0;
+  uint64_t* d_draws = nullptr;  // ksg_schedule_batch_draws: the caller's rand.Int() values
+  size_t draws_cap = 0;
+  uint64_t draw_tmp = 0;
   uint8_t* d_admit = nullptr;  // kubelet admission: sets, pods, ids, pairs, codes (one buffer)
   size_t admit_cap = 0;
   std::vector<KsgPatch> patches;
@@ -1237,7 +1240,7 @@ int ksg_destroy(ksg_ctx* c) {
   void* scratch[] = {c->d_pods, c->d_ids, c->d_fail, c->d_score, c->d_rec_send, c->d_rec_recv, c->d_dpart,
                      c->d_dglobal, c->d_out, c->d_rng, c->d_summary, c->d_patch, c->d_shard_wlo,
                      c->d_winsum, c->d_xsend, c->d_xrecv, c->d_run, c->d_dcnt, c->d_admit, c->d_one,
-                     c->d_t0img};
+                     c->d_t0img, c->d_draws};
   for (void* p : scratch)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -2407,6 +2410,27 @@ int ksg_add_pod_ext(ksg_ctx* c, uint32_t host_id, const ksg_pod* pod, const ksg_
   c->cur_ext = ext;
   const int rc = ksg_add_pod(c, host_id, pod, ids);
   c->cur_ext = nullptr;
+  return rc;
+}
+
+int ksg_schedule_batch_draws(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32_t* ids, uint32_t n_ids,
+                             const uint64_t* draws, uint32_t n_draws, uint32_t* draws_used, int32_t* out_nodes) {
+  if (!c || (n && (!pods || !out_nodes || !draws)) || !draws_used) return KSG_ERR_ARG;
+  KSG_LOCK(c);
+  if (n_draws < n) return fail(c, KSG_ERR_ARG, "%u draws for %u pods: one per pod that may find a node", n_draws, n);
+  for (uint32_t k = 0; k < n; ++k)
+    if (draws[k] > (uint64_t)INT64_MAX) return fail(c, KSG_ERR_ARG, "draw %u is not a rand.Int() value", k);
+  *draws_used = 0;
+  if (n == 0) return ksg_schedule_batch(c, pods, 0, ids, n_ids, &c->draw_tmp, out_nodes);
+  HIPCHK(c, hipSetDevice(c->device));
+  if (int rs_ = srv_stop(c)) return rs_;
+  if (int rc = grow(c, (void**)&c->d_draws, &c->draws_cap, n, sizeof(uint64_t))) return rc;
+  HIPCHK(c, hipMemcpy(c->d_draws, draws, (size_t)n * sizeof(uint64_t), hipMemcpyHostToDevice));
+  c->dev.draws = c->d_draws;  // (the generator state is now the index of the next value)
+  uint64_t state = 0;
+  const int rc = ksg_schedule_batch(c, pods, n, ids, n_ids, &state, out_nodes);
+  c->dev.draws = nullptr;
+  if (rc == KSG_OK) *draws_used = (uint32_t)state;
   return rc;
 }
 

@@ -610,8 +610,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
         ctl->draw_count = idx + (drawable ? 1u : 0u);
         st_rel(&ctl->draw_next, j + 1);
       }
-      uint64_t sm = rng0 + (uint64_t)idx * 0x9E3779B97F4A7C15ULL;
-      const uint64_t r = ksg_splitmix_next(&sm) >> 1;  // rand.Int() (generic_scheduler.go:94)
+      const uint64_t r = ksg_rng_draw(d.draws, rng0 + (uint64_t)idx * ksg_rng_step(d.draws));  // rand.Int() (generic_scheduler.go:94)
 
       uint32_t mv = 0;
       if (drawable && lane < k0) mv = umod64_32(r, k0 - lane);
@@ -1412,7 +1411,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
   }
   for (uint32_t t = lane; t < resolved; t += 64) out[t] = L_out[t];
   if (lane == 0) {
-    *rng_io = rng0 + (uint64_t)n_draws * 0x9E3779B97F4A7C15ULL;
+    *rng_io = rng0 + (uint64_t)n_draws * ksg_rng_step(d.draws);
     if (reason == KSG_STOP_HANG) {
       run->halt = KSG_HALT_HANG;
     } else if (reason == KSG_STOP_OVERSIZE) {
@@ -1734,8 +1733,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         __builtin_amdgcn_s_sleep(1);
       }
       pstamp(26);
-      uint64_t sm = rng0 + (uint64_t)idx * 0x9E3779B97F4A7C15ULL;
-      const uint64_t r = ksg_splitmix_next(&sm) >> 1;  // rand.Int() (generic_scheduler.go:94)
+      const uint64_t r = ksg_rng_draw(d.draws, rng0 + (uint64_t)idx * ksg_rng_step(d.draws));  // rand.Int() (generic_scheduler.go:94)
       uint32_t mv = 0;
       if (drawable && lane < k0) mv = umod64_32(r, k0 - lane);
       int32_t pred = -1;
@@ -2882,7 +2880,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   }
   for (uint32_t t = lane; t < resolved; t += 64) out[t] = L_out[t];
   if (lane == 0) {
-    *rng_io = rng0 + (uint64_t)n_draws * 0x9E3779B97F4A7C15ULL;
+    *rng_io = rng0 + (uint64_t)n_draws * ksg_rng_step(d.draws);
     if (reason == KSG_STOP_HANG) {
       run->halt = KSG_HALT_HANG;
     } else if (reason == KSG_STOP_OVERSIZE) {

@@ -224,6 +224,21 @@ class DeviceScheduler:
             self._err(rc)
         return out[:n], st.value
 
+    def batch_draws(self, batch: PodBatch, draws):
+        """ksg_schedule_batch_draws: the batch with the caller's rand.Int() values
+        (draws[k] for the k-th pod that finds a node). -> (out, draws used)."""
+        n = len(batch)
+        pods = np.ascontiguousarray(batch.pods, dtype=abi.POD_DTYPE)
+        ids = _u32(batch.ids if len(batch.ids) else np.zeros(1, np.uint32))
+        out = np.empty(max(n, 1), np.int32)
+        dr = np.ascontiguousarray(draws if len(draws) else np.zeros(1), dtype=np.uint64)
+        used = C.c_uint32(0)
+        rc = self._lib.ksg_schedule_batch_draws(self._ctx, abi.ptr(pods), n, abi.ptr(ids), len(batch.ids), abi.ptr(dr),
+                                                len(draws), C.byref(used), abi.ptr(out))
+        if rc != abi.KSG_OK:
+            self._err(rc)
+        return out[:n], int(used.value)
+
     def evaluate(self, batch: PodBatch, i: int = 0):
         """Per-node (fail code, combined score) of the shard, no commit."""
         pod = np.ascontiguousarray(batch.pods[i : i + 1])
