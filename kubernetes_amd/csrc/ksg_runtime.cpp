@@ -68,7 +68,7 @@ hipError_t ksg_launch_static_fold(uint64_t* static_fit, int64_t* static_score, c
                                   const int64_t* xscore, uint32_t nw, uint32_t n, int own_fit, int own_score,
                                   hipStream_t st);
 hipError_t ksg_launch_serve(int R, bool anti, bool ext, const KsgDev& d, const KsgSrvArgs& a, hipStream_t st);
-hipError_t ksg_launch_serve_grid(int npt, const KsgDev& d, const KsgSrvArgs& a, hipStream_t st);
+hipError_t ksg_launch_serve_grid(int npt, bool ext, const KsgDev& d, const KsgSrvArgs& a, hipStream_t st);
 hipError_t ksg_launch_admit(const ksg_admission_set* sets, uint32_t n_sets, const ksg_pod* pods,
                             const uint32_t* ids, const uint32_t* pairs, int mode, uint8_t* out, hipStream_t st);
 
@@ -784,7 +784,10 @@ uint32_t srv_npt(const ksg_ctx* c) { return c->hi - c->lo > c->srv_npt4_min ? 4u
 
 bool srv_grid(const ksg_ctx* c) {
   const uint32_t n = c->hi - c->lo, per = KSG_GSRV_NT * srv_npt(c);
-  return c->srv_grid_on && !anti_on(c) && !c->ext_on && n > c->srv_grid_min && (n + per - 1) / per <= KSG_GSRV_MAXW;
+  // (extensions: the filters and BalancedAllocation are per node; TaintToleration normalises over
+  // the filtered set, a reduction across the scan workgroups: the one-workgroup server takes it)
+  return c->srv_grid_on && !anti_on(c) && !(c->ext_on && c->ext.w_taint_toleration) && n > c->srv_grid_min &&
+         (n + per - 1) / per <= KSG_GSRV_MAXW;
 }
 
 bool srv_eligible(const ksg_ctx* c) {
@@ -836,7 +839,7 @@ int srv_launch(ksg_ctx* c, uint32_t start_seq) {
     // past 64 scan workgroups their polls of the host block crowd the link: each sleeps ~0.2 us
     // more between polls (measured: 50,000 nodes 73 -> 38 us per pod; no gain at 15,000)
     a.grid_opts = c->srv_grid_opts >= 0 ? (uint32_t)c->srv_grid_opts : a.n_workers > 64 ? 0x10u : 0u;
-    HIPCHK(c, ksg_launch_serve_grid((int)npt, c->dev, a, c->st));
+    HIPCHK(c, ksg_launch_serve_grid((int)npt, c->ext_on, c->dev, a, c->st));
   } else {
     HIPCHK(c, ksg_launch_serve(c->R, anti_on(c), c->ext_on, c->dev, a, c->st));
   }

@@ -118,7 +118,7 @@ __device__ __forceinline__ int32_t lr_fast(int64_t req, int64_t cap, double inv1
 // 2^30, no wrap), so the sum is int32; LeastRequested goes through lr_fast and
 // ServiceSpreading's int(10 * float32(max - cnt) / float32(max)) through the
 // pod's table s_tab[cnt] (cnt < n_tab; the direct form past it).
-enum { WM_LP = 0, WM_SEL, WM_PD, WM_PORT, WM_AFF, WM_N };
+enum { WM_LP = 0, WM_SEL, WM_PD, WM_PORT, WM_AFF, WM_TAINT, WM_N };
 
 __device__ __forceinline__ void word_masks(const KsgDev& d, const PodCtx& c, uint32_t q, uint64_t* s_wm,
                                            uint32_t nwq) {
@@ -131,8 +131,11 @@ __device__ __forceinline__ void word_masks(const KsgDev& d, const PodCtx& c, uin
   if (P & KSG_PRED_SERVICEAFFINITY)
 #pragma unroll
     for (uint32_t j = 0; j < KSG_MAX_AFF; ++j) n_aff += (j < d.n_aff && c.req_aff[j] >= 0) ? 1u : 0u;
-  const uint32_t e1 = n_sel, e2 = e1 + n_pd, e3 = e2 + n_port, total = e3 + n_aff;
+  // (extensions: the pod's untolerated NoSchedule / NoExecute taints, taintmap rows)
+  const uint32_t n_taint = (c.ext && (d.ext_filters & KSG_EXT_TAINTS)) ? c.ext->n_hard : 0;
+  const uint32_t e1 = n_sel, e2 = e1 + n_pd, e3 = e2 + n_port, e4 = e3 + n_aff, total = e4 + n_taint;
   uint64_t m_lp = d.has_static_fit ? d.static_fit[wi] : ~0ULL, m_sel = ~0ULL, m_pd = 0, m_port = 0, m_aff = ~0ULL;
+  uint64_t m_taint = 0;
   for (uint32_t e0 = 0; e0 < total; e0 += 8) {
     uint64_t x[8];
 #pragma unroll
@@ -150,6 +153,9 @@ __device__ __forceinline__ void word_masks(const KsgDev& d, const PodCtx& c, uin
         } else if (e < e3) {
           id = c.ports[e - e2];
           base = d.keymap;
+        } else if (e >= e4) {
+          id = c.ids[c.ext->hard_off + (e - e4)];
+          base = d.taintmap;
         } else {  // the (e - e3)-th ServiceAffinity requirement
           const uint32_t k = e - e3;
           uint32_t seen = 0;
@@ -170,7 +176,8 @@ __device__ __forceinline__ void word_masks(const KsgDev& d, const PodCtx& c, uin
       if (e < e1) m_sel &= x[i];
       else if (e < e2) m_pd |= x[i];
       else if (e < e3) m_port |= x[i];
-      else if (e < total) m_aff &= x[i];
+      else if (e < e4) m_aff &= x[i];
+      else if (e < total) m_taint |= x[i];
     }
   }
   s_wm[WM_LP * nwq + q] = m_lp;
@@ -178,6 +185,7 @@ __device__ __forceinline__ void word_masks(const KsgDev& d, const PodCtx& c, uin
   s_wm[WM_PD * nwq + q] = m_pd;
   s_wm[WM_PORT * nwq + q] = m_port;
   s_wm[WM_AFF * nwq + q] = m_aff;
+  s_wm[WM_TAINT * nwq + q] = m_taint;
 }
 
 // One node of the plain scan, branch-free: every predicate's verdict from the
@@ -195,7 +203,20 @@ __device__ __forceinline__ int32_t eval_node(const KsgDev& d, const PodCtx& c, u
   const bool host_bad = (P & KSG_PRED_HOSTNAME) && c.host != -1 && (int32_t)n != c.host;
   const bool res_bad = res_on && !((capc == 0 || (int64_t)((uint64_t)capc - (uint64_t)usedc) >= c.req_cpu) &&
                                    (capm == 0 || (int64_t)((uint64_t)capm - (uint64_t)usedm) >= c.req_mem));
-  f = (w_aff & bit) ? KSG_FAIL_NONE : KSG_FAIL_SERVICEAFFINITY;
+  int fx = KSG_FAIL_NONE;  // extensions (node_fail_l's order: after the reference's predicates)
+  if (c.ext) {
+    if ((d.ext_filters & KSG_EXT_SCALAR) && n < d.hi)
+      for (uint32_t r = 0; r < d.n_scalar; ++r) {
+        const int64_t req = c.ext->scalar[r];
+        if (req > 0) {
+          const int64_t cap = d.scalar_cap[(size_t)r * d.n_nodes + n];
+          const int64_t used = ld_mut(d.scalar_used + (size_t)r * d.n_nodes + n);
+          if (cap < (int64_t)((uint64_t)used + (uint64_t)req)) fx = KSG_FAIL_SCALAR;
+        }
+      }
+    if (s_wm[WM_TAINT * nwq + q] & bit) fx = KSG_FAIL_TAINTS;
+  }
+  f = (w_aff & bit) ? fx : KSG_FAIL_SERVICEAFFINITY;
   f = res_bad ? KSG_FAIL_PODFITSRESOURCES : f;
   f = (w_port & bit) ? KSG_FAIL_PODFITSPORTS : f;
   f = (w_pd & bit) ? KSG_FAIL_NODISKCONFLICT : f;
@@ -217,6 +238,11 @@ __device__ __forceinline__ int32_t eval_node(const KsgDev& d, const PodCtx& c, u
         sp = (int32_t)frac10_f32((int64_t)c.spread_max - cnt, c.spread_max);
     }
     s += (int32_t)d.w_spread * sp;
+  }
+  if (c.ext && d.w_bal) {  // extension: BalancedResourceAllocation (int32: the score bound covers it)
+    const int64_t tc = (int64_t)((uint64_t)usedc + (uint64_t)c.req_cpu);
+    const int64_t tm = (int64_t)((uint64_t)usedm + (uint64_t)c.req_mem);
+    s += (int32_t)d.w_bal * (int32_t)balanced_score(tc, capc, tm, capm);
   }
   return d.equal_fallback ? 1 : s;  // EqualPriority (generic_scheduler.go:141-143,180-195)
 }
@@ -630,7 +656,7 @@ __device__ __forceinline__ void grid_load_ext(const uint32_t* xa, uint32_t* s_re
 
 // NPT nodes per thread: 256 x NPT nodes per scan workgroup (NPT = 4 past
 // KSG_SERVE_GRID_NPT4_MIN nodes: a quarter of the pollers on the link)
-template <int NPT>
+template <int NPT, bool EXT>
 __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, KsgSrvArgs a) {
   constexpr uint32_t NODES = NPT * KSG_GSRV_NT, NW = NODES / 64, NWV = KSG_GSRV_NT / 64;
   __shared__ __attribute__((aligned(16))) uint32_t s_req[KSG_SRV_HDR_DW + KSG_SRV_PAY_DW];
@@ -729,7 +755,10 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
           cnt[j] = need_cnt ? ld_mut(d.svc_cnt + (size_t)p.service * d.n_nodes + nn[j]) : 0;
         PodCtx c;
         pod_resolve(d, p, ids, c);
-        c.ext = nullptr;
+        // (extensions: the filters and BalancedAllocation; the host keeps TaintToleration off this server)
+        c.ext = (EXT && (s_req[KSG_SRVH_FLAGS] & KSG_SRVF_EXT))
+                    ? reinterpret_cast<const ksg_pod_ext*>(pay + s_req[KSG_SRVH_EXT_AT])
+                    : nullptr;
         if (tid == 0) grid_mark(a, 1 + w, T, 3);
         if (c.error) {
           err = 1;
@@ -908,7 +937,10 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
         const uint32_t* pay = s_req + KSG_SRV_HDR_DW;
         const ksg_pod& p = *reinterpret_cast<const ksg_pod*>(pay);
         const uint32_t* ids = pay + s_req[KSG_SRVH_IDS_AT];
-        commit_pod_wave(d, p, ids, node, lane, nullptr);
+        const ksg_pod_ext* ext = (EXT && (s_req[KSG_SRVH_FLAGS] & KSG_SRVF_EXT))
+                                     ? reinterpret_cast<const ksg_pod_ext*>(pay + s_req[KSG_SRVH_EXT_AT])
+                                     : nullptr;
+        commit_pod_wave(d, p, ids, node, lane, ext);
         drain_stores();
       }
       if (lane == 0) {
@@ -919,11 +951,12 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
   }
 }
 
-hipError_t ksg_launch_serve_grid(int npt, const KsgDev& d, const KsgSrvArgs& a, hipStream_t st) {
-  if (npt == 4)
-    hipLaunchKernelGGL(ksg_serve_grid_kernel<4>, dim3(a.n_workers + 1), dim3(KSG_GSRV_NT), 0, st, d, a);
-  else
-    hipLaunchKernelGGL(ksg_serve_grid_kernel<1>, dim3(a.n_workers + 1), dim3(KSG_GSRV_NT), 0, st, d, a);
+hipError_t ksg_launch_serve_grid(int npt, bool ext, const KsgDev& d, const KsgSrvArgs& a, hipStream_t st) {
+  const dim3 g(a.n_workers + 1), b(KSG_GSRV_NT);
+  if (npt == 4 && ext) hipLaunchKernelGGL((ksg_serve_grid_kernel<4, true>), g, b, 0, st, d, a);
+  else if (npt == 4) hipLaunchKernelGGL((ksg_serve_grid_kernel<4, false>), g, b, 0, st, d, a);
+  else if (ext) hipLaunchKernelGGL((ksg_serve_grid_kernel<1, true>), g, b, 0, st, d, a);
+  else hipLaunchKernelGGL((ksg_serve_grid_kernel<1, false>), g, b, 0, st, d, a);
   return hipGetLastError();
 }
 

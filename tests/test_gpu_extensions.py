@@ -93,8 +93,16 @@ def test_window_path_with_extension_filters_matches_oracle(name, nn, npods, kw, 
     dev.close()
 
 
-def test_begin_commit_evaluate_remove_with_extensions():
-    c = ExtCase("config2", 300, 250)
+@pytest.mark.parametrize("nn,kw,npt4", [
+    (300, dict(), False),                     # TaintToleration on: the one-workgroup server
+    (300, dict(w_taint=0, w_bal=3), False),   # filters + BalancedAllocation: the grid server
+    (3000, dict(w_taint=0, w_bal=0), False),
+    (2000, dict(w_taint=0, w_bal=2), True),   # ... at 4 nodes per thread
+])
+def test_begin_commit_evaluate_remove_with_extensions(nn, kw, npt4, monkeypatch):
+    if npt4:
+        monkeypatch.setenv("KSG_SERVE_GRID_NPT4_MIN", "0")
+    c = ExtCase("config2", nn, 250, **kw)
     dev = c.load(DeviceScheduler(c.cfg, device=0))
     orc = c.load(OracleScheduler(c.cfg))
     rng = np.random.default_rng(5)
@@ -122,4 +130,9 @@ def test_begin_commit_evaluate_remove_with_extensions():
             uid = int(c.batch.pods[placed.pop(0)]["uid"])
             dev.remove_pod(uid)
             orc.remove_pod(uid)
+    st = dev.serve_stats()
+    assert st["grid"] == (kw.get("w_taint", 1) == 0), st
+    gc, gm = dev.read_requested()
+    wc, wm = orc.read_requested()
+    assert np.array_equal(gc, wc) and np.array_equal(gm, wm)
     dev.close()
