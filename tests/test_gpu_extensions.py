@@ -100,6 +100,7 @@ def test_window_path_with_extension_filters_matches_oracle(name, nn, npods, kw, 
     (2000, dict(w_taint=0, w_bal=2), True),   # ... at 4 nodes per thread
 ])
 def test_begin_commit_evaluate_remove_with_extensions(nn, kw, npt4, monkeypatch):
+    monkeypatch.setenv("KSG_SERVE_GRID_EXT", "1")
     if npt4:
         monkeypatch.setenv("KSG_SERVE_GRID_NPT4_MIN", "0")
     c = ExtCase("config2", nn, 250, **kw)
