@@ -256,7 +256,7 @@ struct ksg_ctx {
   bool srv_grid_on = true;       // KSG_SERVE_GRID=0: the one-workgroup server at every size
   uint32_t srv_npt4_min = 16384;  // KSG_SERVE_GRID_NPT4_MIN: past this many nodes 4 nodes per thread
   uint32_t srv_grid_min = 0;
-  bool srv_grid_ext = false;  // KSG_SERVE_GRID_EXT=1: extension contexts (no TaintToleration) on the grid server  // KSG_SERVE_GRID_MIN: shards above this many nodes take the grid server
+  bool srv_grid_ext = true;  // KSG_SERVE_GRID_EXT=0: extension contexts on the one-workgroup server  // KSG_SERVE_GRID_MIN: shards above this many nodes take the grid server
                               // (it beats the one-workgroup server at 500 nodes already: 7.2 vs 10.9 us)
   KsgSrvGrid* srv_grid = nullptr;  // its device state (+ the fail codes)
   size_t srv_grid_cap = 0;
@@ -1173,7 +1173,7 @@ static int create_impl(const ksg_config* cfg, int device, int rank, int world, c
   c->srv_grid_on = !(getenv("KSG_SERVE_GRID") && atoi(getenv("KSG_SERVE_GRID")) == 0);
   if (const char* gm = getenv("KSG_SERVE_GRID_MIN")) c->srv_grid_min = (uint32_t)std::max(atoi(gm), 0);
   if (const char* g4 = getenv("KSG_SERVE_GRID_NPT4_MIN")) c->srv_npt4_min = (uint32_t)std::max(atoi(g4), 0);
-  c->srv_grid_ext = getenv("KSG_SERVE_GRID_EXT") && atoi(getenv("KSG_SERVE_GRID_EXT")) != 0;
+  c->srv_grid_ext = !(getenv("KSG_SERVE_GRID_EXT") && atoi(getenv("KSG_SERVE_GRID_EXT")) == 0);
   if (const char* rm = getenv("KSG_ROUND_MARGIN")) c->round_margin = std::min(std::max(atof(rm), 0.5), 4.0);
   // The exchange path (shard scan, all-gather of per-shard records, replicated
   // resolve) runs for world > 1, and for a 1-rank RCCL communicator when the caller
