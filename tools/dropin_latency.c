@@ -53,6 +53,8 @@ int main(int argc, char** argv) {
   const uint32_t n_pods = argc > 2 ? (uint32_t)atoi(argv[2]) : 4000;
   const uint32_t warmup = argc > 3 ? (uint32_t)atoi(argv[3]) : 200;
   const int want_fail = argc > 4 ? atoi(argv[4]) : 0;
+  /* 1: extensions (taints + one extended resource, the filters); 2: the same + TaintToleration */
+  const int ext_mode = argc > 5 ? atoi(argv[5]) : 0;
   const uint32_t n_svc = 8;
   ksg_ctx* ctx = NULL;
 
@@ -65,6 +67,15 @@ int main(int argc, char** argv) {
   cfg.w_service_spreading = 1;
   cfg.max_conflict_keys = 64;
   CHECK(ksg_create(&cfg, 0, &ctx));
+  if (ext_mode) {
+    ksg_ext_config e;
+    memset(&e, 0, sizeof e);
+    e.filters = KSG_EXT_TAINTS | KSG_EXT_SCALAR;
+    e.w_taint_toleration = ext_mode == 2 ? 1 : 0;
+    e.n_scalar = 1;
+    e.max_taints = 4;
+    CHECK(ksg_set_extensions(ctx, &e));
+  }
 
   ksg_node* nodes = calloc(n_nodes, sizeof *nodes);
   for (uint32_t i = 0; i < n_nodes; ++i) {
@@ -73,10 +84,24 @@ int main(int argc, char** argv) {
   }
   const uint32_t pair_keys[1] = {0};
   CHECK(ksg_set_cluster(ctx, nodes, n_nodes, NULL, 0, pair_keys, 1, n_svc));
+  if (ext_mode) {  /* 8 GPUs per node; every 5th node carries taint 1 (hard for the pods that do not tolerate it) */
+    int64_t* gcap = calloc(n_nodes, sizeof *gcap);
+    uint32_t* toff = calloc(n_nodes, sizeof *toff);
+    uint32_t* tn = calloc(n_nodes, sizeof *tn);
+    uint32_t* tid = calloc(n_nodes, sizeof *tid);
+    uint32_t nt = 0;
+    for (uint32_t i = 0; i < n_nodes; ++i) {
+      gcap[i] = 8;
+      toff[i] = nt;
+      if (i % 5 == 0) tid[nt++] = 1, tn[i] = 1;
+    }
+    CHECK(ksg_set_node_ext(ctx, n_nodes, gcap, toff, tn, tid, nt));
+  }
 
   const uint32_t total = warmup + n_pods;
   ksg_pod* pods = calloc(total, sizeof *pods);
-  uint32_t* ids = calloc(2 * (size_t)total, sizeof *ids);  /* pod i's list: ids + 2i, offsets 0 and 1 */
+  uint32_t* ids = calloc(3 * (size_t)total, sizeof *ids);  /* pod i's list: ids + 3i: port key, service, taint */
+  ksg_pod_ext* pext = calloc(total, sizeof *pext);
   uint64_t gen = 12345;
   for (uint32_t i = 0; i < total; ++i) {
     ksg_pod* p = &pods[i];
@@ -85,8 +110,12 @@ int main(int argc, char** argv) {
     p->memory = (128LL << 20) * (int64_t)(1 + sm_next(&gen) % 5);
     p->host = -1;
     p->service = (int32_t)(sm_next(&gen) % n_svc);
-    ids[2 * i] = (uint32_t)(i % 32);  /* host-port conflict key */
-    ids[2 * i + 1] = (uint32_t)p->service;
+    ids[3 * i] = (uint32_t)(i % 32);  /* host-port conflict key */
+    ids[3 * i + 1] = (uint32_t)p->service;
+    ids[3 * i + 2] = 1;  /* the taint it does not tolerate (every third pod) */
+    pext[i].scalar[0] = (i % 4 == 0) ? 1 : 0;
+    pext[i].hard_off = 2;
+    pext[i].n_hard = (i % 3 == 0) ? 1 : 0;
     p->ports_off = 0;
     p->n_ports = (i % 16 == 0) ? 1 : 0;
     p->svcs_off = 1;
@@ -106,7 +135,9 @@ int main(int argc, char** argv) {
     uint32_t ties = 0;
     int32_t node = KSG_OUT_NOFIT;
     const double t0 = now_us();
-    const int rb = ksg_schedule_begin(ctx, &pods[i], ids + 2 * (size_t)i, &best, &ties, want_fail ? fails : NULL);
+    const int rb = ext_mode ? ksg_schedule_begin_ext(ctx, &pods[i], &pext[i], ids + 3 * (size_t)i, &best, &ties,
+                                                     want_fail ? fails : NULL)
+                            : ksg_schedule_begin(ctx, &pods[i], ids + 3 * (size_t)i, &best, &ties, want_fail ? fails : NULL);
     if (rb != KSG_OK && rb != KSG_NOFIT) CHECK(rb);
     const double tb = now_us();
     if (ties > 0) {
@@ -132,10 +163,10 @@ int main(int argc, char** argv) {
   printf("{\"metric\": \"drop-in per-pod latency (ksg_schedule_begin + ksg_schedule_commit, C caller)\", "
          "\"nodes\": %u, \"pods\": %u, \"warmup\": %u, \"placed\": %u, \"nofit\": %u, "
          "\"us_p50\": %.2f, \"us_p90\": %.2f, \"us_p99\": %.2f, \"us_max\": %.2f, \"us_mean\": %.2f, "
-         "\"pods_per_s\": %.1f, \"want_fail\": %d, \"begin_us_p50\": %.2f, \"commit_us_p50\": %.2f, "
+         "\"pods_per_s\": %.1f, \"want_fail\": %d, \"ext\": %d, \"begin_us_p50\": %.2f, \"commit_us_p50\": %.2f, "
          "\"served\": {\"eligible\": %d, \"launches\": %llu, \"requests\": %llu}, \"histogram_us\": {\"edges\": [5, 10, 20, 40, 80, 160, 320], \"counts\": [",
          n_nodes, n_pods, warmup, placed, nofit, PCT(0.5), PCT(0.9), PCT(0.99), lat[n_pods - 1],
-         t_all / n_pods, n_pods / (t_all * 1e-6), want_fail, lat_b[n_pods / 2], lat_c[n_pods / 2], (int)sv[3],
+         t_all / n_pods, n_pods / (t_all * 1e-6), want_fail, ext_mode, lat_b[n_pods / 2], lat_c[n_pods / 2], (int)sv[3],
          (unsigned long long)sv[0], (unsigned long long)sv[1]);
   const double edges[] = {5, 10, 20, 40, 80, 160, 320, 1e30};
   size_t k = 0;
