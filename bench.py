@@ -439,18 +439,20 @@ def main():
         # ... and node-sharded over this process's CPU share (OMP_NUM_THREADS: 16 on the
         # GPU box, whose os.cpu_count() is the whole machine's), SURVEY.md 8(d) "CPU timing" ii
         nthr = max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
-        mt = OracleScheduler(cfg, faithful=False)
-        mt.set_cluster(view.arrays)
+        mt = load_cluster(OracleScheduler(cfg, faithful=False))
         r = workload.TIEBREAK_SEED
         done_m = 0
         mt_out = [np.zeros(0, np.int32)]
         t_m = time.perf_counter()
-        # (the threaded restatement has no extensions: --extensions skips it)
-        while ext is None and done_m < n_pods and time.perf_counter() - t_m < min(args.cpu_seconds, 5.0):
-            o, r = mt.batch_mt(PodBatch(batch.pods[done_m:done_m + 500], batch.ids), r, nthr)
+        # the whole run's pods (warm-up + timed) when they fit the budget: this leg is also the
+        # decision check of every pod the GPU placed, extension records included
+        while done_m < n_pods and time.perf_counter() - t_m < max(args.cpu_seconds, 30.0):
+            o, r = mt.batch_mt(PodBatch(batch.pods[done_m:done_m + 500], batch.ids,
+                                        None if batch.ext is None else batch.ext[done_m:done_m + 500]), r, nthr)
             mt_out.append(o)
             done_m += len(o)
         mt_s = max(time.perf_counter() - t_m, 1e-9)
+        mt_all = done_m == n_pods and r == rng  # (and the generator state after the last timed step)
         mt.close()
         mt_agree = bool(np.array_equal(np.concatenate(mt_out), out[:done_m]))
         cpu = {"value": done / cpu_s, "unit": "pods/s", "cores": 1, "kind": "port",
@@ -461,11 +463,14 @@ def main():
                "incremental": {"value": done_i / inc_s, "unit": "pods/s", "cores": 1,
                                "sample": f"first {done_i} pods, incremental mode (SoA closed forms, "
                                          f"no per-pod re-list), {inc_s:.1f}s"},
-               "incremental_nproc": None if ext is not None else {"value": done_m / mt_s, "unit": "pods/s", "cores": nthr,
-                                     "sample": f"first {done_m} pods, incremental mode, each pod's node loop "
-                                               f"split over {nthr} threads (node-rank shards, two spin barriers "
-                                               f"per pod; ServiceAntiAffinity configs run 1 thread), "
-                                               f"{mt_s:.1f}s; decisions identical to GPU: {mt_agree}"}}
+               "incremental_nproc": {"value": done_m / mt_s, "unit": "pods/s", "cores": nthr,
+                                     "sample": f"first {done_m} of the run's {n_pods} pods (warm-up + timed), "
+                                               f"incremental mode, each pod's node loop split over {nthr} threads "
+                                               f"(node-rank shards, two spin barriers per pod; ServiceAntiAffinity "
+                                               f"configs run 1 thread), {mt_s:.1f}s; decisions identical to GPU: "
+                                               f"{mt_agree}",
+                                     "decisions_identical": mt_agree, "pods_checked": done_m,
+                                     "whole_run_checked": bool(mt_all and mt_agree)}}
 
     xname = "RCCL" if args.transport == "rccl" else "host-staged gloo"
     line = {

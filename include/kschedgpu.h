@@ -422,9 +422,10 @@ int ksg_admit_pods(ksg_ctx* ctx, const ksg_admission_set* sets, uint32_t n_sets,
  * ScalarResources, priorities TaintTolerationPriority + NormalizeReduce and
  * BalancedResourceAllocation) and PARITY IS UNPINNED (no reference to run or
  * table to check against; the C restatement oracle/ksg_oracle.c is the checker).
- * Off unless ksg_set_extensions enables them; a context with any extension on
- * schedules on the exact one-pod-at-a-time kernels (no speculative windows) and
- * on one rank. The reference's own predicates and priorities are unchanged. */
+ * Off unless ksg_set_extensions enables them, on one rank. Batches take the
+ * speculative-window path unless a pod's extended-resource request is outside
+ * [0, 2^16] (the exact one-pod-at-a-time kernels then). The reference's own
+ * predicates and priorities are unchanged. */
 #define KSG_EXT_TAINTS (1u << 0) /* PodToleratesNodeTaints: NoSchedule / NoExecute taints */
 #define KSG_EXT_SCALAR (1u << 1) /* extended resources: allocatable >= used + request    */
 #define KSG_FAIL_TAINTS 8        /* fail codes after the reference's seven             */
@@ -469,6 +470,10 @@ int ksg_schedule_begin_ext(ksg_ctx* ctx, const ksg_pod* pod, const ksg_pod_ext* 
                            int64_t* max_score, uint32_t* tie_count, uint8_t* fail_codes);
 int ksg_evaluate_ext(ksg_ctx* ctx, const ksg_pod* pod, const ksg_pod_ext* ext, const uint32_t* ids,
                      uint8_t* fail_out, int64_t* score_out);
+/* Copy the committed extended-resource usage back to the host, for state checks:
+ * used[r * n_nodes + n] = the requests of resource r of every pod on node n
+ * (the extended-resource counterpart of ksg_read_requested). */
+int ksg_read_ext_used(ksg_ctx* ctx, int64_t* used);
 
 #ifdef __cplusplus
 }

@@ -256,6 +256,7 @@ enum {
 enum { KSG_SRVH_KIND = 0, KSG_SRVH_ARG, KSG_SRVH_RSV, KSG_SRVH_FLAGS, KSG_SRVH_PAYDW, KSG_SRVH_IDS_AT,
        KSG_SRVH_EXT_AT, KSG_SRVH_NPATCH };
 #define KSG_SRV_BADREQ 0xFFFFFFFEu  // response: the payload's layout, ids or node are out of range
+#define KSG_SRV_RESP_REJECTED 12  // resp[12]: the last request answered KSG_SRV_BADREQ (sticky; written first)
 #define KSG_SRVF_WANT_FAIL 1u  // BEGIN: write the fail code of every node to `fail`
 #define KSG_SRVF_EXT 2u        // the payload carries a ksg_pod_ext at EXT_AT
 // The grid server (ksg_serve_grid_kernel): a leader workgroup plus one scan

@@ -209,6 +209,7 @@ struct ksg_ctx {
   double last_kms[3] = {0, 0, 0};  // phase A ms, phase B ms, launches (window path)
   double last_wsum = 0;            // window capacity W summed over the launches
   bool dbg_fail_next = false;      // KSG_DEBUG & 16384: the next window batch fails after its device work
+  uint32_t dbg_corrupt = 0;        // KSG_DEBUG bits 22 / 23: corrupt the next COMMIT / BEGIN request's layout
   double last_hus[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // host us per phase of the last batch (ksg_last_batch_host_us)
   double totals[24] = {};  // ksg_batch_totals: the per-batch diagnostics summed over batches
   int64_t max_cap = 0, min_cap = 0;
@@ -485,6 +486,7 @@ void reset_mirror(ksg_ctx* c) {
   c->seq = 0;
   c->patches.clear();
   c->pending = false;
+  c->pend_srv = false;
   c->upd_q.clear();
   c->q_added.clear();
   c->q_removed.clear();
@@ -738,7 +740,8 @@ unsigned __int128 score_bound(const ksg_config& cf, int64_t w_taint, int64_t w_b
 int cluster_ok(ksg_ctx* c) {
   if (!c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_cluster not called");
   if (c->diverged)
-    return fail(c, KSG_ERR_STATE, "an earlier batch failed after its device work started: call ksg_set_cluster");
+    return fail(c, KSG_ERR_STATE, "device state diverged from the host mirror (a batch failed after its device work "
+                "started, or the drop-in server rejected a commit): call ksg_set_cluster");
   return KSG_OK;
 }
 
@@ -808,8 +811,18 @@ int srv_alloc(ksg_ctx* c) {
   return KSG_OK;
 }
 
-int srv_launch(ksg_ctx* c, uint32_t start_seq) {
+// (Re)launches the server on the stream, offering every request after the last
+// one answered. A COMMIT is posted without waiting for its answer, so the host's
+// srv_served may lag the server's: the response block names the last request the
+// server answered, and a server answers a request only once it will complete it
+// (the one-workgroup server applies a COMMIT's delta after answering it, before
+// it reads the next request or returns). Relaunching at srv_served alone would
+// offer an answered COMMIT again and apply its delta twice.
+int srv_launch(ksg_ctx* c) {
   if (int rc = srv_alloc(c)) return rc;
+  const uint32_t r0 = __atomic_load_n(&c->srv_box->resp[0], __ATOMIC_ACQUIRE);
+  if ((int32_t)(r0 - c->srv_served) > 0) c->srv_served = r0;
+  const uint32_t start_seq = c->srv_served;
   const size_t nf = ((size_t)(c->hi - c->lo) + 3 & ~(size_t)3) + 64;  // (the grid server stores 4 codes at a time)
   if (c->srv_fail_cap < nf) {
     if (c->srv_fail) (void)hipHostFree(c->srv_fail);
@@ -875,7 +888,7 @@ int srv_wait(ksg_ctx* c, uint32_t seq, uint32_t parts) {
       if (++relaunches > 3) return fail(c, KSG_ERR_HIP, "drop-in server exits without serving request %u", seq);
       c->srv_running = false;
       if (c->srv_trace) fprintf(stderr, "srv relaunch start %u (waiting %u)\n", c->srv_served, seq);
-      if (int rc = srv_launch(c, c->srv_served)) return rc;  // (every request after it is offered again)
+      if (int rc = srv_launch(c)) return rc;  // (every request after the last answered one is offered again)
       t0 = std::chrono::steady_clock::now();
     } else if (q != hipErrorNotReady) {
       c->srv_running = false;
@@ -901,11 +914,15 @@ int srv_settle(ksg_ctx* c) {
   if (!c->srv_unacked) return KSG_OK;
   const uint32_t u = c->srv_unacked;
   c->srv_unacked = 0;
-  if ((int32_t)(c->srv_served - u) >= 0) return KSG_OK;
-  if (int rc = srv_wait(c, u, 0)) return rc;
-  const uint32_t* rs = c->srv_box->resp;
-  if (__atomic_load_n(&rs[0], __ATOMIC_ACQUIRE) == u && __atomic_load_n(&rs[1], __ATOMIC_RELAXED) == KSG_SRV_BADREQ)
-    return fail(c, KSG_ERR_STATE, "drop-in server rejected commit request %u", u);
+  if ((int32_t)(c->srv_served - u) < 0)
+    if (int rc = srv_wait(c, u, 0)) return rc;
+  // resp[KSG_SRV_RESP_REJECTED]: the last request the server rejected, written before its
+  // response (later BEGIN answers overwrite resp[0..3], not this word). The host mirror
+  // already holds the commit's pod and the device does not: the context is diverged.
+  if (__atomic_load_n(&c->srv_box->resp[KSG_SRV_RESP_REJECTED], __ATOMIC_ACQUIRE) == u) {
+    c->diverged = true;
+    return fail(c, KSG_ERR_STATE, "drop-in server rejected commit request %u (ksg_set_cluster resyncs)", u);
+  }
   return KSG_OK;
 }
 
@@ -915,7 +932,7 @@ int srv_settle(ksg_ctx* c) {
 // request before it (ARG).
 int srv_post(ksg_ctx* c, const uint32_t* hdr_in, uint32_t* seq_out) {
   if (!c->srv_running) {
-    if (int rc = srv_launch(c, c->srv_served)) return rc;
+    if (int rc = srv_launch(c)) return rc;
   }
   const bool ctl = hdr_in[KSG_SRVH_KIND] != KSG_SRV_BEGIN;
   if (ctl) {
@@ -924,6 +941,13 @@ int srv_post(ksg_ctx* c, const uint32_t* hdr_in, uint32_t* seq_out) {
   uint32_t hdr[KSG_SRV_HDR_DW];
   memcpy(hdr, hdr_in, sizeof hdr);
   if (!ctl) hdr[KSG_SRVH_ARG] = c->srv_last_ctl;
+  if (c->dbg_corrupt) {
+    const uint32_t bit = hdr[KSG_SRVH_KIND] == KSG_SRV_COMMIT ? 1u : hdr[KSG_SRVH_KIND] == KSG_SRV_BEGIN ? 2u : 0u;
+    if (c->dbg_corrupt & bit) {
+      hdr[KSG_SRVH_IDS_AT] = KSG_SRV_PAY_DW + 1;  // (past the payload: req_bad)
+      c->dbg_corrupt &= ~bit;
+    }
+  }
   const uint32_t seq = ++c->srv_seq;
   if (ctl) c->srv_last_ctl = seq;
   if (c->srv_trace)
@@ -1021,7 +1045,8 @@ int srv_stop(ksg_ctx* c) {
     if (int rc = srv_call(c, hdr, r)) return rc;
   }
   c->srv_running = false;
-  c->pend_srv = false;  // (a pending begin is re-run by the launch-per-call commit)
+  // (a pending begin served by the server stays pending: its commit picks the node from
+  // srv_tw on the host and posts the COMMIT to a relaunched server)
   HIPCHK(c, hipStreamSynchronize(c->st));
   return KSG_OK;
 }
@@ -1468,6 +1493,9 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   for (uint32_t q = 0; q < c->cfg.n_label_pref; ++q) any_pref |= c->cfg.w_pref[q] != 0;
   d.has_static_score = (c->cfg.w_equal != 0 || any_pref) ? 1 : 0;
   d.dbg = getenv("KSG_DEBUG") ? atoi(getenv("KSG_DEBUG")) : 0;
+  // KSG_DEBUG bit 22 / 23: the next COMMIT / BEGIN posted to the resident server carries an
+  // out-of-range payload layout (tests/test_gpu_serve.py: the server must reject it, not fault)
+  c->dbg_corrupt = ((uint32_t)d.dbg >> 22) & 3u;
   if (d.dbg & (8 | 32)) {  // (32: the plain resolver's inconsistency record, ksg_plain.hip)
     (void)hipMalloc(&d.dbgbuf, 128);
     (void)hipMemset(d.dbgbuf, 0, 128);
@@ -1533,6 +1561,9 @@ int ksg_set_static_terms(ksg_ctx* c, const uint64_t* fit_words, const int64_t* s
   KSG_LOCK(c);
   if (int rs = cluster_ok(c)) return rs;
   if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
+  // (a node failing the extra fit words reports KSG_FAIL_LABELSPRESENCE: the config must name it)
+  if (fit_words && !(c->cfg.predicates & KSG_PRED_LABELSPRESENCE))
+    return fail(c, KSG_ERR_ARG, "ksg_set_static_terms: fit words need KSG_PRED_LABELSPRESENCE in the config");
   if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
   HIPCHK(c, hipSetDevice(c->device));
   const uint32_t N = c->N, nw = (N + 63) / 64;
@@ -1710,6 +1741,8 @@ int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int6
       if (fail_codes) hdr[KSG_SRVH_FLAGS] |= KSG_SRVF_WANT_FAIL;
       uint32_t r[4];
       if ((rc = srv_begin(c, hdr, r))) return rc;
+      // (the last COMMIT was served before this BEGIN: a rejected one diverged the context)
+      if ((rc = srv_settle(c))) return rc;
       if (r[1] == KSG_SRV_BADREQ) return fail(c, KSG_ERR_STATE, "drop-in server rejected begin request");
       if (r[1] == ~0u) return fail(c, KSG_ERR_NOPEER, "service affinity peer is not on a known node");
       if (fail_codes) memcpy(fail_codes, c->srv_fail, (size_t)(c->hi - c->lo));
@@ -1815,9 +1848,9 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
                        uint64_t* rng_state, int32_t* out_nodes) {
   if (!c || (n && (!pods || !out_nodes)) || !rng_state) return KSG_ERR_ARG;
   KSG_LOCK(c);
+  if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
   if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
   if (int rs = cluster_ok(c)) return rs;
-  if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
   HIPCHK(c, hipSetDevice(c->device));
   c->last_ms = 0.0;
   if (n == 0) return KSG_OK;
@@ -2151,10 +2184,10 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
 int ksg_evaluate(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, uint8_t* fail_out, int64_t* score_out) {
   if (!c || !pod) return KSG_ERR_ARG;
   KSG_LOCK(c);
+  if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
   if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
   if (int rc0 = flush_deferred(c)) return rc0;
   if (int rs = cluster_ok(c)) return rs;
-  if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
   HIPCHK(c, hipSetDevice(c->device));
   if (c->N == 0) return KSG_NONODES;
   const size_t ext = call_ids_extent(c, pod);
@@ -2332,8 +2365,8 @@ static int admit_impl(ksg_ctx* c, int mode, const ksg_admission_set* sets, uint3
 int ksg_set_extensions(ksg_ctx* c, const ksg_ext_config* e) {
   if (!c || !e) return KSG_ERR_ARG;
   KSG_LOCK(c);
-  if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
   if (c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_extensions: call before ksg_set_cluster");
+  if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
   if (c->world > 1 || c->xchg) return fail(c, KSG_ERR_ARG, "extensions: one rank only");
   if ((e->filters & ~(KSG_EXT_TAINTS | KSG_EXT_SCALAR)) || e->n_scalar > KSG_MAX_SCALAR)
     return fail(c, KSG_ERR_ARG, "extensions: bad filters / n_scalar");
@@ -2346,6 +2379,7 @@ int ksg_set_node_ext(ksg_ctx* c, uint32_t n_nodes, const int64_t* scalar_cap, co
                      const uint32_t* taint_n, const uint32_t* taint_ids, uint32_t n_taint_ids) {
   if (!c) return KSG_ERR_ARG;
   KSG_LOCK(c);
+  if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
   if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
   if (!c->ext_on) return fail(c, KSG_ERR_STATE, "ksg_set_node_ext: extensions are off");
   if (!c->have_cluster || n_nodes != c->N) return fail(c, KSG_ERR_ARG, "ksg_set_node_ext: node count != cluster");
@@ -2372,6 +2406,19 @@ int ksg_set_node_ext(ksg_ctx* c, uint32_t n_nodes, const int64_t* scalar_cap, co
   HIPCHK(c, hipMemsetAsync(c->dev.scalar_used, 0, (size_t)std::max<uint32_t>(c->ext.n_scalar, 1) * NN * 8, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
   c->sc_used.assign((size_t)c->ext.n_scalar * c->N, 0);
+  return KSG_OK;
+}
+
+int ksg_read_ext_used(ksg_ctx* c, int64_t* used) {
+  if (!c || !used || !c->have_cluster) return KSG_ERR_ARG;
+  KSG_LOCK(c);
+  if (!c->ext_on) return fail(c, KSG_ERR_STATE, "ksg_read_ext_used: extensions are off");
+  if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
+  HIPCHK(c, hipSetDevice(c->device));
+  if (int rc = flush_patches(c)) return rc;
+  const size_t nb = (size_t)c->ext.n_scalar * c->N * 8;
+  if (nb) HIPCHK(c, hipMemcpyAsync(used, c->dev.scalar_used, nb, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
   return KSG_OK;
 }
 
@@ -2427,6 +2474,7 @@ int ksg_schedule_batch_draws(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const 
   for (uint32_t k = 0; k < n; ++k)
     if (draws[k] > (uint64_t)INT64_MAX) return fail(c, KSG_ERR_ARG, "draw %u is not a rand.Int() value", k);
   *draws_used = 0;
+  if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
   if (n == 0) return ksg_schedule_batch(c, pods, 0, ids, n_ids, &c->draw_tmp, out_nodes);
   HIPCHK(c, hipSetDevice(c->device));
   if (int rs_ = srv_stop(c)) return rs_;

@@ -72,6 +72,16 @@ __device__ __forceinline__ void respond(const KsgSrvArgs& a, uint32_t seq, uint3
   v.w = z;
   sys_st16(a.box->resp, v);
 }
+// A rejected request: its sequence number into resp[KSG_SRV_RESP_REJECTED] before the
+// response (a COMMIT is not waited for, and later answers overwrite resp[0..3]; the host
+// checks this word when it settles the COMMIT)
+__device__ __forceinline__ void respond_rejected(const KsgSrvArgs& a, uint32_t seq) {
+  u32x4 r;
+  r.x = seq;
+  r.y = r.z = r.w = 0;
+  sys_st16(a.box->resp + KSG_SRV_RESP_REJECTED, r);
+  respond(a, seq, KSG_SRV_BADREQ, 0, 0);
+}
 
 // A BEGIN / COMMIT request's payload layout in range: no request can make the
 // server read outside its LDS copy of the request (the ids' values are checked
@@ -502,7 +512,7 @@ __global__ __launch_bounds__(KSG_NT) void ksg_serve_kernel(KsgDev d, KsgSrvArgs 
     const bool bad = req_bad(d, s_req) || (!begin && (node < d.lo || node >= d.hi));
     stamp(2);
     if (bad) {  // (never, unless the host side has a bug)
-      if (tid == 0) respond(a, seq, KSG_SRV_BADREQ, 0, 0);
+      if (tid == 0) respond_rejected(a, seq);
       ++seq;
       continue;
     }
@@ -945,7 +955,8 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
       }
       if (lane == 0) {
         agent_st32(&a.grid->applied, T);  // (a bad one too: the BEGINs after it must not wait forever)
-        respond(a, T, bad ? KSG_SRV_BADREQ : node, 0, 0);
+        if (bad) respond_rejected(a, T);
+        else respond(a, T, node, 0, 0);
       }
     }
   }

@@ -85,6 +85,7 @@ class DeviceScheduler:
             raise KsgError(rc, "ksg_create failed (see stderr)")
         self.cfg = cfg
         self.n_nodes = 0
+        self.n_scalar = 0
         self.world = world
         self.rank = rank
         if world > 1 and allgather is not None:
@@ -151,6 +152,7 @@ class DeviceScheduler:
         rc = self._lib.ksg_set_extensions(self._ctx, C.byref(ext))
         if rc != abi.KSG_OK:
             self._err(rc)
+        self.n_scalar = int(ext.n_scalar)
 
     def set_node_ext(self, scalar_cap: np.ndarray, taint_off: np.ndarray, taint_n: np.ndarray,
                      taint_ids: np.ndarray):
@@ -355,6 +357,14 @@ class DeviceScheduler:
         if rc != abi.KSG_OK:
             self._err(rc)
         return out[: len(pods)]
+
+    def read_ext_used(self) -> np.ndarray:
+        """Committed extended-resource usage, int64[n_scalar, n_nodes] (ksg_read_ext_used)."""
+        u = np.zeros(max(self.n_scalar * self.n_nodes, 1), np.int64)
+        rc = self._lib.ksg_read_ext_used(self._ctx, abi.ptr(u))
+        if rc != abi.KSG_OK:
+            self._err(rc)
+        return u[: self.n_scalar * self.n_nodes].reshape(self.n_scalar, self.n_nodes)
 
     def read_requested(self):
         c = np.zeros(max(self.n_nodes, 1), np.int64)

@@ -1087,6 +1087,11 @@ void orc_read_requested(orc *o, int64_t *c, int64_t *m) {
   if (m) memcpy(m, o->used_m, (size_t)o->N * 8);
 }
 
+/* the extended-resource usage [n_scalar][N] (ksg_read_ext_used) */
+void orc_read_ext_used(orc *o, int64_t *used) {
+  if (used && o->sused) memcpy(used, o->sused, (size_t)o->ext.n_scalar * o->N * 8);
+}
+
 /* ====================================================== kubelet admission */
 /* handleNotFittingPods' scheduler checks (pkg/kubelet/kubelet.go:1716-1771) over
  * the ksg_admission_set layout: PodMatchesNodeLabels (predicates.go:161-167),
@@ -1135,13 +1140,17 @@ void orc_admit_pods(const ksg_admission_set *sets, uint32_t n_sets, const ksg_po
  * context, every thread filters/scores its shard and reports its max and tie count,
  * thread 0 merges (selectHost: global max, ties in descending rank, one Int63 draw per
  * success) and commits. Two spin barriers per pod. Configurations with
- * ServiceAntiAffinity (a cross-shard domain-count reduction) run single-threaded. */
+ * ServiceAntiAffinity (a cross-shard domain-count reduction) run single-threaded.
+ * Extensions (parity unpinned): the filters and BalancedAllocation are per node;
+ * TaintToleration's NormalizeReduce max over the filtered nodes takes a third
+ * barrier (every shard's max untolerated soft-taint count) before the scores. */
 #include <pthread.h>
 #include <stdatomic.h>
 
 typedef struct {
   orc *o;
   const ksg_pod *pods;
+  const ksg_pod_ext *exts; /* extension records (NULL: none) */
   const uint32_t *ids;
   uint32_t n;
   uint64_t *rng;
@@ -1153,6 +1162,8 @@ typedef struct {
   int32_t maxc;
   int64_t *tmax;  /* per thread: local max score (NONE_SCORE: nothing fits) */
   uint64_t *tcnt; /* per thread: nodes at it */
+  int32_t *tsoft; /* per thread: max untolerated soft-taint count over its filtered nodes */
+  int32_t *soft;  /* per node: the pod's untolerated soft taints (TaintToleration) */
   atomic_int bar_count, bar_sense;
 } mt_job;
 
@@ -1178,7 +1189,7 @@ static void mt_barrier(mt_job *j, int *sense) {
 /* incr_prioritize's per-node score without ServiceAntiAffinity */
 static int64_t mt_score(const orc *o, const pctx *c, int32_t maxc, uint32_t n) {
   const ksg_config *cf = &o->cfg;
-  if (cf->n_priority_configs == 0) return 1; /* EqualPriority fallback */
+  if (cf->n_priority_configs == 0 && !ext_prio_on(o)) return 1; /* EqualPriority fallback */
   int64_t sc = 0;
   if (cf->w_least_requested) {
     int64_t tc = (int64_t)((uint64_t)o->used_c[n] + (uint64_t)c->p->milli_cpu);
@@ -1196,6 +1207,11 @@ static int64_t mt_score(const orc *o, const pctx *c, int32_t maxc, uint32_t n) {
     int ok = (exists && cf->pref_presence[q]) || (!exists && !cf->pref_presence[q]);
     sc = go_add(sc, go_mul(cf->w_pref[q], (ok ? 10 : 0)));
   }
+  if (o->ext_on && o->ext.w_balanced) { /* ext_prioritize's per-node term */
+    int64_t tc = (int64_t)((uint64_t)o->used_c[n] + (uint64_t)c->p->milli_cpu);
+    int64_t tm = (int64_t)((uint64_t)o->used_m[n] + (uint64_t)c->p->memory);
+    sc = go_add(sc, go_mul(o->ext.w_balanced, balanced_score(tc, o->cap_c[n], tm, o->cap_m[n])));
+  }
   return go_add(sc, cf->w_equal);
 }
 
@@ -1211,7 +1227,7 @@ static void *mt_worker(void *argp) {
       j->skip = 0;
       j->c.p = j->pods + i;
       j->c.ids = j->ids;
-      j->c.ext = NULL;
+      j->c.ext = j->exts ? j->exts + i : NULL;
       resolve_affinity(o, &j->c);
       if (j->c.error) {
         j->out[i] = KSG_OUT_ERROR;
@@ -1221,14 +1237,37 @@ static void *mt_worker(void *argp) {
       j->maxc = s >= 0 ? o->svc_max[s] : 0;
     }
     mt_barrier(j, &sense); /* A: the pod's context is ready */
-    if (!j->skip) {
-      int64_t best = NONE_SCORE;
-      uint64_t k = 0;
+    /* TaintToleration with a toleration record: the max over every shard's filtered nodes first */
+    const int taint_w = !j->skip && o->ext_on && o->ext.w_taint_toleration;
+    const int taint_norm = taint_w && j->c.ext;
+    if (taint_norm) {
+      int32_t mx = 0;
       for (uint32_t n = lo; n < hi; ++n) {
         const int f = incr_fail_code(o, &j->c, n);
         o->fails[n] = (uint8_t)f;
         if (f) continue;
-        const int64_t sc = mt_score(o, &j->c, j->maxc, n);
+        j->soft[n] = soft_taints(o, &j->c, n);
+        if (j->soft[n] > mx) mx = j->soft[n];
+      }
+      j->tsoft[t] = mx;
+      mt_barrier(j, &sense); /* C: every shard's max soft-taint count */
+    }
+    if (!j->skip) {
+      int64_t best = NONE_SCORE;
+      uint64_t k = 0;
+      int32_t mx = 0;
+      if (taint_norm)
+        for (int g = 0; g < j->T; ++g)
+          if (j->tsoft[g] > mx) mx = j->tsoft[g];
+      for (uint32_t n = lo; n < hi; ++n) {
+        const int f = taint_norm ? o->fails[n] : incr_fail_code(o, &j->c, n);
+        o->fails[n] = (uint8_t)f;
+        if (f) continue;
+        int64_t sc = mt_score(o, &j->c, j->maxc, n);
+        if (taint_w) { /* NormalizeReduce(10, reverse); no record: every node 10 */
+          const int64_t v = !taint_norm || mx == 0 ? 10 : 10 - (10 * (int64_t)j->soft[n]) / mx;
+          sc = go_add(sc, go_mul(o->ext.w_taint_toleration, v));
+        }
         o->scores[n] = sc;
         if (sc > best) {
           best = sc;
@@ -1270,7 +1309,7 @@ static void *mt_worker(void *argp) {
               --ix;
             }
         }
-        commit(o, j->pods + i, NULL, j->ids, (uint32_t)node);
+        commit(o, j->pods + i, j->exts ? j->exts + i : NULL, j->ids, (uint32_t)node);
         j->out[i] = node;
       }
     }
@@ -1278,13 +1317,21 @@ static void *mt_worker(void *argp) {
   return NULL;
 }
 
+int orc_schedule_batch_mt_ext(orc *o, const ksg_pod *pods, const ksg_pod_ext *exts, uint32_t n, const uint32_t *ids,
+                              uint32_t n_ids, uint64_t *rng_state, int32_t *out_nodes, int nthreads);
 int orc_schedule_batch_mt(orc *o, const ksg_pod *pods, uint32_t n, const uint32_t *ids, uint32_t n_ids,
                           uint64_t *rng_state, int32_t *out_nodes, int nthreads) {
+  return orc_schedule_batch_mt_ext(o, pods, NULL, n, ids, n_ids, rng_state, out_nodes, nthreads);
+}
+
+int orc_schedule_batch_mt_ext(orc *o, const ksg_pod *pods, const ksg_pod_ext *exts, uint32_t n, const uint32_t *ids,
+                              uint32_t n_ids, uint64_t *rng_state, int32_t *out_nodes, int nthreads) {
   if (nthreads <= 1 || o->faithful || o->cfg.n_anti > 0 || o->N == 0 || (uint32_t)nthreads > o->N)
-    return orc_schedule_batch(o, pods, n, ids, n_ids, rng_state, out_nodes);
+    return orc_schedule_batch_ext(o, pods, exts, n, ids, n_ids, rng_state, out_nodes);
   mt_job j;
   memset(&j, 0, sizeof j);
   j.o = o;
+  j.exts = o->ext_on ? exts : NULL;
   j.pods = pods;
   j.ids = ids;
   j.n = n;
@@ -1294,8 +1341,11 @@ int orc_schedule_batch_mt(orc *o, const ksg_pod *pods, uint32_t n, const uint32_
   const ksg_config *cf = &o->cfg;
   j.any = cf->n_priority_configs == 0 || cf->w_least_requested || cf->w_service_spreading || cf->w_equal;
   for (uint32_t q = 0; q < cf->n_label_pref; ++q) j.any |= cf->w_pref[q] != 0;
+  j.any |= ext_prio_on(o);
   j.tmax = (int64_t *)calloc((size_t)nthreads, 8);
   j.tcnt = (uint64_t *)calloc((size_t)nthreads, 8);
+  j.tsoft = (int32_t *)calloc((size_t)nthreads, 4);
+  j.soft = (int32_t *)calloc((size_t)o->N, 4);
   atomic_init(&j.bar_count, 0);
   atomic_init(&j.bar_sense, 0);
   pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
@@ -1311,5 +1361,7 @@ int orc_schedule_batch_mt(orc *o, const ksg_pod *pods, uint32_t n, const uint32_
   free(args);
   free(j.tmax);
   free(j.tcnt);
+  free(j.tsoft);
+  free(j.soft);
   return KSG_OK;
 }

@@ -47,8 +47,10 @@ def load():
         "orc_schedule_commit": (C.c_int, [vp, C.c_uint32, P(C.c_int32)]),
         "orc_schedule_batch": (C.c_int, [vp, vp, C.c_uint32, vp, C.c_uint32, P(C.c_uint64), vp]),
         "orc_read_requested": (None, [vp, vp, vp]),
+        "orc_read_ext_used": (None, [vp, vp]),
         "orc_admit_pods": (None, [vp, C.c_uint32, vp, C.c_uint32, vp, vp, C.c_int, vp]),
         "orc_schedule_batch_mt": (C.c_int, [vp, vp, C.c_uint32, vp, C.c_uint32, P(C.c_uint64), vp, C.c_int]),
+        "orc_schedule_batch_mt_ext": (C.c_int, [vp, vp, vp, C.c_uint32, vp, C.c_uint32, P(C.c_uint64), vp, C.c_int]),
         "orc_set_extensions": (None, [vp, P(abi.KsgExtConfig)]),
         "orc_set_node_ext": (None, [vp, vp, vp, vp, vp]),
         "orc_add_pod_ext": (C.c_int, [vp, C.c_uint32, vp, vp, vp]),
@@ -77,6 +79,7 @@ class OracleScheduler:
         self.cfg = cfg
         self._o = C.c_void_p(self._lib.orc_create(C.byref(cfg), 1 if faithful else 0))
         self.n_nodes = 0
+        self.n_scalar = 0
 
     def close(self):
         if self._o:
@@ -99,6 +102,12 @@ class OracleScheduler:
 
     def set_extensions(self, ext: abi.KsgExtConfig):
         self._lib.orc_set_extensions(self._o, C.byref(ext))
+        self.n_scalar = int(ext.n_scalar)
+
+    def read_ext_used(self):
+        u = np.zeros(max(self.n_scalar * self.n_nodes, 1), np.int64)
+        self._lib.orc_read_ext_used(self._o, abi.ptr(u))
+        return u[: self.n_scalar * self.n_nodes].reshape(self.n_scalar, self.n_nodes)
 
     def set_node_ext(self, scalar_cap, taint_off, taint_n, taint_ids):
         cap = np.ascontiguousarray(scalar_cap, np.int64).reshape(-1)
@@ -150,13 +159,14 @@ class OracleScheduler:
 
     def batch_mt(self, batch: PodBatch, rng_state: int, nthreads: int):
         """Incremental mode with each pod's node loop split over `nthreads` threads
-        (node-rank shards); same decisions as batch()."""
+        (node-rank shards); same decisions as batch(), extension records included."""
         n = len(batch)
         pods = np.ascontiguousarray(batch.pods, dtype=abi.POD_DTYPE)
         out = np.empty(max(n, 1), np.int32)
         st = C.c_uint64(rng_state)
-        self._lib.orc_schedule_batch_mt(self._o, abi.ptr(pods), n, abi.ptr(_u32(batch.ids)), len(batch.ids),
-                                        C.byref(st), abi.ptr(out), int(nthreads))
+        ext = None if batch.ext is None else np.ascontiguousarray(batch.ext, dtype=abi.POD_EXT_DTYPE)
+        self._lib.orc_schedule_batch_mt_ext(self._o, abi.ptr(pods), abi.ptr(ext), n, abi.ptr(_u32(batch.ids)),
+                                            len(batch.ids), C.byref(st), abi.ptr(out), int(nthreads))
         return out[:n], st.value
 
     def evaluate(self, batch: PodBatch, i: int = 0):

@@ -102,3 +102,29 @@ def test_oracle_modes_agree_with_extensions(kw):
     assert (outs[0][0] >= 0).sum() > 20
     if kw.get("gpus", True):  # GPUs run out: FitErrors on the extended resource
         assert (outs[0][0] == abi.KSG_OUT_NOFIT).sum() > 0
+
+
+@pytest.mark.parametrize("name,nn,w_taint,w_bal", [
+    ("config2", 700, 0, 0),    # filters only (the window path's extension set)
+    ("config2", 700, 1, 1),    # + TaintToleration (the cross-shard max) + BalancedAllocation
+    ("config1", 257, 3, 0),
+    ("config5", 1500, 0, 2),
+])
+def test_threaded_restatement_with_extensions_matches_single_thread(name, nn, w_taint, w_bal):
+    """orc_schedule_batch_mt_ext (the full-size checker for BASELINE config 5 with
+    extended resources) against the single-thread incremental restatement:
+    every decision, the generator state and the committed totals."""
+    e = ExtCase(name, nn, 600, seed=5, w_taint=w_taint, w_bal=w_bal)
+    a = e.load(OracleScheduler(e.cfg))
+    b = e.load(OracleScheduler(e.cfg))
+    placed = 0
+    for part in (slice(0, 250), slice(250, 600)):
+        sub = PodBatch(e.batch.pods[part], e.batch.ids, e.batch.ext[part])
+        ga, sa = a.batch(sub, 99 + part.start)
+        gb, sb = b.batch_mt(sub, 99 + part.start, 5)
+        assert np.array_equal(ga, gb) and sa == sb
+        placed += int((ga >= 0).sum())
+    assert placed > 0
+    for x, y in zip(a.read_requested(), b.read_requested()):
+        assert np.array_equal(x, y)
+    assert np.array_equal(a.read_ext_used(), b.read_ext_used())

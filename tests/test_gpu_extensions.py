@@ -137,3 +137,44 @@ def test_begin_commit_evaluate_remove_with_extensions(nn, kw, npt4, monkeypatch)
     wc, wm = orc.read_requested()
     assert np.array_equal(gc, wc) and np.array_equal(gm, wm)
     dev.close()
+
+
+def test_config5_extensions_full_size_matches_restatement():
+    """BASELINE config 5 as BASELINE.json states it: 100k heterogeneous nodes x
+    100k pods with extended resources (GPU / FPGA counts) and taints /
+    tolerations, in 1,000-pod batches on the window path, against the threaded
+    C restatement (orc_schedule_batch_mt_ext): every decision, the generator
+    state, the cpu / memory totals and the extended-resource usage; plus the
+    size-independent checks (usage == the placed pods' requests, no node above
+    its allocatable). Parity unpinned: nothing in this reference vintage reads
+    extended resources (pkg/api/resource_helpers.go:29-42)."""
+    import os
+
+    c = ExtCase("config5", 100000, 100000, w_taint=0, w_bal=0)
+    dev = c.load(DeviceScheduler(c.cfg, device=0))
+    got, rng, windows = [], 1234, 0
+    for s in range(0, len(c.batch), 1000):
+        g, rng = dev.batch(PodBatch(c.batch.pods[s:s + 1000], c.batch.ids, c.batch.ext[s:s + 1000]), rng)
+        got.append(g)
+        windows += dev.last_batch_stats()["windows"]
+    got = np.concatenate(got)
+    assert windows > 0
+    gc, gm = dev.read_requested()
+    gx = dev.read_ext_used()
+    dev.close()
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)))
+    orc = c.load(OracleScheduler(c.cfg))
+    want, sw = orc.batch_mt(c.batch, 1234, threads)
+    wc, wm = orc.read_requested()
+    wx = orc.read_ext_used()
+    orc.close()
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"first mismatches at {bad[:8]}: gpu {got[bad[:8]]} restatement {want[bad[:8]]}"
+    assert rng == sw and np.array_equal(gc, wc) and np.array_equal(gm, wm) and np.array_equal(gx, wx)
+    ok = got >= 0
+    assert ok.sum() > len(got) // 2 and (c.batch.ext["scalar"][ok] > 0).any()
+    cap = np.asarray(c.node_arrays[0], np.int64).reshape(gx.shape)
+    sx = np.zeros_like(gx)
+    for r in range(gx.shape[0]):
+        np.add.at(sx[r], got[ok], c.batch.ext["scalar"][ok, r])
+    assert np.array_equal(sx, gx) and (gx <= np.where(cap > 0, cap, 0)).all()

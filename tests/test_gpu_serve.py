@@ -170,3 +170,114 @@ def test_serve_grid_four_nodes_per_thread(name, nn, npods, churn, monkeypatch):
     st = dev.serve_stats()
     assert st["grid"] and st["requests"] >= npods, st
     dev.close()
+
+
+@pytest.mark.parametrize("name,nn,grid", [("config2", 900, False), ("config4", 700, False), ("config2", 2500, True)])
+def test_serve_pending_begin_survives_stream_users(name, nn, grid, monkeypatch):
+    """Calls that take the stream between a server-served begin and its commit
+    (read_requested, kubelet admission, a rejected evaluate / batch) stop the
+    server; the commit must still apply the pending pod on the node the begin's
+    tie words give (srv_stop dropped the pending begin and the
+    commit ran the launch-per-call decide on stale device records)."""
+    from kubernetes_amd.engine import KsgError
+
+    monkeypatch.setenv("KSG_SERVE_GRID", "1" if grid else "0")
+    case = Case(name, nn, 120)
+    dev = DeviceScheduler(case.cfg, device=0)
+    orc = OracleScheduler(case.cfg)
+    dev.set_cluster(case.view.arrays)
+    orc.set_cluster(case.view.arrays)
+    rng = np.random.default_rng(nn)
+    sets = np.zeros(1, abi.ADMISSION_SET_DTYPE)
+    sets[0]["n_pods"] = 1  # pod 0 against an unlimited capacity
+    one = PodBatch(case.batch.pods[:1], case.batch.ids)
+    for i in range(120):
+        rg, mg, kg, _ = dev.begin(case.batch, i)
+        ro, mo, ko, _ = orc.begin(case.batch, i)
+        assert (rg, kg) == (ro, ko), f"pod {i}"
+        if rg != abi.KSG_OK:
+            continue
+        assert mg == mo
+        kind = i % 4
+        if kind == 0:
+            dev.read_requested()
+        elif kind == 1:
+            assert dev.admit(sets, one, np.zeros(0, np.uint32), 1)[0] == 1
+        elif kind == 2:
+            with pytest.raises(KsgError, match="pending"):
+                dev.evaluate(case.batch, i)
+        else:
+            with pytest.raises(KsgError, match="pending"):
+                dev.batch(PodBatch(case.batch.pods[i + 1:i + 3], case.batch.ids), 7)
+        ix = int(rng.integers(0, kg))
+        assert dev.commit(ix) == orc.commit(ix), f"pod {i}"
+        gc, gm = dev.read_requested()
+        wc, wm = orc.read_requested()
+        assert np.array_equal(gc, wc) and np.array_equal(gm, wm), f"pod {i}: committed totals"
+    assert dev.serve_stats()["eligible"]
+    dev.close()
+
+
+@pytest.mark.parametrize("grid", [False, True])
+def test_serve_commit_then_idle_exit(grid, monkeypatch):
+    """A commit answered inside the idle window, then a pause longer than the idle
+    limit, then a begin: the relaunched server must not be offered the answered
+    COMMIT again (the one-workgroup server applied it twice)."""
+    import time
+
+    monkeypatch.setenv("KSG_SERVE_IDLE_US", "2000")
+    monkeypatch.setenv("KSG_SERVE_GRID", "1" if grid else "0")
+    case = Case("config2", 1200, 40)
+    dev = DeviceScheduler(case.cfg, device=0)
+    orc = OracleScheduler(case.cfg)
+    dev.set_cluster(case.view.arrays)
+    orc.set_cluster(case.view.arrays)
+    rng = np.random.default_rng(3)
+    for i in range(40):
+        rg, _, kg, _ = dev.begin(case.batch, i)
+        ro, _, ko, _ = orc.begin(case.batch, i)
+        assert (rg, kg) == (ro, ko), f"pod {i}"
+        if rg == abi.KSG_OK:
+            ix = int(rng.integers(0, kg))
+            assert dev.commit(ix) == orc.commit(ix), f"pod {i}"
+        time.sleep(0.01)  # > KSG_SERVE_IDLE_US: the server answers the commit, then returns
+    gc, gm = dev.read_requested()
+    wc, wm = orc.read_requested()
+    assert np.array_equal(gc, wc) and np.array_equal(gm, wm)
+    assert dev.serve_stats()["launches"] > 20
+    dev.close()
+
+
+@pytest.mark.parametrize("grid", [False, True])
+def test_serve_rejects_malformed_requests(grid, monkeypatch):
+    """A BEGIN and a COMMIT whose payload layout is out of range (KSG_DEBUG bits 23
+    / 22 corrupt the next one the host posts) are rejected by the server's layout
+    check (req_bad) instead of being read: the begin fails with KSG_ERR_STATE and
+    the context stays usable; the rejected commit (posted without waiting) is
+    reported by the next call and leaves the context diverged until
+    ksg_set_cluster, after which scheduling matches the oracle again (round 3's
+    illegal-address faults in both servers came from request payloads read
+    outside their layout; ADVICE r3: a rejected commit must diverge the context)."""
+    from kubernetes_amd.engine import KsgError
+
+    monkeypatch.setenv("KSG_SERVE_GRID", "1" if grid else "0")
+    case = Case("config2", 1500, 60)
+    dev = DeviceScheduler(case.cfg, device=0)
+    orc = OracleScheduler(case.cfg)
+    monkeypatch.setenv("KSG_DEBUG", str((1 << 22) | (1 << 23)))  # (read by ksg_set_cluster)
+    dev.set_cluster(case.view.arrays)
+    monkeypatch.delenv("KSG_DEBUG")
+    orc.set_cluster(case.view.arrays)
+    with pytest.raises(KsgError, match="rejected begin"):
+        dev.begin(case.batch, 0)
+    rg, _, kg, _ = dev.begin(case.batch, 0)  # the same pod again: served
+    ro, _, ko, _ = orc.begin(case.batch, 0)
+    assert (rg, kg) == (ro, ko) and rg == abi.KSG_OK
+    dev.commit(0)  # corrupted on the way: rejected by the server, reported by the next call
+    with pytest.raises(KsgError, match="rejected commit"):
+        dev.begin(case.batch, 1)
+    with pytest.raises(KsgError, match="ksg_set_cluster"):
+        dev.begin(case.batch, 1)
+    dev.set_cluster(case.view.arrays)
+    _drive(case, dev, orc, seed=1, n_pods=60, abandon=0.0)
+    dev.close()
