@@ -231,6 +231,15 @@ int ksg_remove_pod(ksg_ctx* ctx, uint64_t uid);
  * n_priority_configs count the extra priorities. No reference counterpart (the
  * reference's registry takes any number of them: plugins.go:81-117, 145-183). */
 int ksg_set_static_terms(ksg_ctx* ctx, const uint64_t* fit_words, const int64_t* score, int score_weighted);
+/* The same static terms evaluated on the device from the node labels of the last
+ * ksg_set_cluster, one slot pass per call: `extra`'s LabelsPresence slots
+ * (n_presence, presence_n_keys, presence_keys, presence_flag) and LabelPreference
+ * slots (n_label_pref, pref_key, pref_presence, w_pref) are evaluated per node
+ * (ksg_static_kernel) and folded in like ksg_set_static_terms' arrays; every other
+ * field of `extra` is ignored. Call it as often as the policy needs (each pass
+ * holds up to KSG_MAX_PRESENCE predicates of KSG_MAX_PRESENCE_KEYS keys and
+ * KSG_MAX_LABEL_PREF priorities); the terms end with the node list. */
+int ksg_add_static_config(ksg_ctx* ctx, const ksg_config* extra);
 
 /* Split Schedule: begin evaluates every node and reports the best combined
  * score and the number of nodes tied at it (0 => KSG_NOFIT). The caller draws

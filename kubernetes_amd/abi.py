@@ -209,6 +209,7 @@ EXPORTS = [
     "ksg_set_extensions",
     "ksg_set_node_ext",
     "ksg_read_ext_used",
+    "ksg_add_static_config",
     "ksg_add_pod_ext",
     "ksg_schedule_batch_ext",
     "ksg_schedule_begin_ext",
@@ -277,6 +278,7 @@ def load_library() -> C.CDLL:
         "ksg_set_extensions": (C.c_int, [vp, P(KsgExtConfig)]),
         "ksg_set_node_ext": (C.c_int, [vp, U32, vp, vp, vp, vp, U32]),
         "ksg_read_ext_used": (C.c_int, [vp, vp]),
+        "ksg_add_static_config": (C.c_int, [vp, C.POINTER(KsgConfig)]),
         "ksg_add_pod_ext": (C.c_int, [vp, U32, vp, vp, vp]),
         "ksg_schedule_batch_ext": (C.c_int, [vp, vp, vp, U32, vp, U32, P(U64), vp]),
         "ksg_schedule_begin_ext": (C.c_int, [vp, vp, vp, vp, P(I64), P(U32), vp]),

@@ -511,6 +511,18 @@ hipError_t ksg_launch_static(const KsgStaticCfg& sc, uint32_t n_nodes, const ksg
   return hipGetLastError();
 }
 
+// ksg_add_static_config: one slot pass of LabelsPresence / LabelPreference terms past the
+// config's slots, evaluated from the node labels into scratch (fit words, scores), then folded
+hipError_t ksg_launch_static_terms(const KsgStaticCfg& sc, uint32_t n_nodes, const ksg_node* nodes,
+                                   const uint32_t* node_pairs, const uint32_t* pair_keys, uint32_t n_pairs, uint32_t nw,
+                                   uint64_t* fit, int64_t* score, hipStream_t st) {
+  const uint32_t blocks = (n_nodes + 255) / 256;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(ksg_static_kernel, dim3(blocks), dim3(256), 0, st, sc, n_nodes, nodes, node_pairs, pair_keys,
+                     nullptr, n_pairs, nw, fit, score, nullptr, nullptr);
+  return hipGetLastError();
+}
+
 // ksg_set_static_terms: the caller's static node terms folded into the
 // config's (LabelsPresence predicates: AND of the fit words; LabelPreference
 // priorities: Go-int sum of the scores). own_fit / own_score: 0 when the config

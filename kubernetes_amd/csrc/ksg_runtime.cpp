@@ -64,6 +64,9 @@ hipError_t ksg_launch_static(const KsgStaticCfg& sc, uint32_t n_nodes, const ksg
                              uint64_t* static_fit, int64_t* static_score, int32_t* anti_domain,
                              int32_t* aff_pair, unsigned long long* pairmap, hipStream_t st);
 hipError_t ksg_launch_patch(const KsgPatch* patches, uint32_t n, hipStream_t st);
+hipError_t ksg_launch_static_terms(const KsgStaticCfg& sc, uint32_t n_nodes, const ksg_node* nodes,
+                                   const uint32_t* node_pairs, const uint32_t* pair_keys, uint32_t n_pairs, uint32_t nw,
+                                   uint64_t* fit, int64_t* score, hipStream_t st);
 hipError_t ksg_launch_static_fold(uint64_t* static_fit, int64_t* static_score, const uint64_t* xfit,
                                   const int64_t* xscore, uint32_t nw, uint32_t n, int own_fit, int own_score,
                                   hipStream_t st);
@@ -266,6 +269,10 @@ struct ksg_ctx {
   int64_t srv_grid_opts = -1;   // KSG_SERVE_GRID_OPTS (KsgSrvArgs.grid_opts; -1: by size)
   bool srv_debug = false;
   unsigned __int128 static_mag = 0;  // max |score| of the terms ksg_set_static_terms added
+  // the node labels on the device (ksg_add_static_config evaluates more static terms from them)
+  const ksg_node* d_lbl_nodes = nullptr;
+  const uint32_t* d_lbl_pairs = nullptr;
+  const uint32_t* d_lbl_keys = nullptr;
   bool srv_trace = false;       // KSG_SERVE_TRACE=1: every post, wait and relaunch to stderr       // KSG_SERVE_DEBUG=1: the grid server's stage markers, reported on a fault
   double srv_stage[6] = {};     // (printed by ksg_destroy)
   uint64_t srv_stamped = 0;
@@ -1409,9 +1416,13 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   uint32_t *dnp = nullptr, *dpk = nullptr;
   int32_t* ddom = nullptr;
   std::vector<void*> tmp;
-  if ((rc = dalloc(c, &dn, NN, &tmp)) || (rc = dalloc(c, &dnp, std::max<uint32_t>(n_node_pairs, 1), &tmp)) ||
-      (rc = dalloc(c, &dpk, n_pairs, &tmp)) || (rc = dalloc(c, &ddom, dom_of_pair.size(), &tmp)))
+  // (the node labels stay with the cluster: ksg_add_static_config reads them)
+  if ((rc = dalloc(c, &dn, NN, owner)) || (rc = dalloc(c, &dnp, std::max<uint32_t>(n_node_pairs, 1), owner)) ||
+      (rc = dalloc(c, &dpk, n_pairs, owner)) || (rc = dalloc(c, &ddom, dom_of_pair.size(), &tmp)))
     return rc;
+  c->d_lbl_nodes = dn;
+  c->d_lbl_pairs = dnp;
+  c->d_lbl_keys = dpk;
   if (n_nodes) HIPCHK(c, hipMemcpyAsync(dn, nodes, n_nodes * sizeof(ksg_node), hipMemcpyHostToDevice, c->st));
   if (n_node_pairs)
     HIPCHK(c, hipMemcpyAsync(dnp, node_pairs, n_node_pairs * 4, hipMemcpyHostToDevice, c->st));
@@ -1592,6 +1603,65 @@ int ksg_set_static_terms(ksg_ctx* c, const uint64_t* fit_words, const int64_t* s
     d.has_static_score = 1;
     c->static_mag += mag;
     if (score_weighted) d.empty_priorities = 0;
+  }
+  d.wide = score_bound(c->cfg, c->ext.w_taint_toleration, c->ext.w_balanced) + c->static_mag >=
+           (unsigned __int128)KSG_SCORE_BOUND;
+  return KSG_OK;
+}
+
+int ksg_add_static_config(ksg_ctx* c, const ksg_config* extra) {
+  if (!c || !extra) return KSG_ERR_ARG;
+  KSG_LOCK(c);
+  if (int rs = cluster_ok(c)) return rs;
+  if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
+  if (extra->n_presence > KSG_MAX_PRESENCE || extra->n_label_pref > KSG_MAX_LABEL_PREF)
+    return fail(c, KSG_ERR_ARG, "ksg_add_static_config: more terms than the config's slots");
+  for (uint32_t q = 0; q < extra->n_presence; ++q)
+    if (extra->presence_n_keys[q] > KSG_MAX_PRESENCE_KEYS)
+      return fail(c, KSG_ERR_ARG, "ksg_add_static_config: presence predicate %u has too many keys", q);
+  // (a node failing the extra predicates reports KSG_FAIL_LABELSPRESENCE: the config must name it)
+  if (extra->n_presence && !(c->cfg.predicates & KSG_PRED_LABELSPRESENCE))
+    return fail(c, KSG_ERR_ARG, "ksg_add_static_config: LabelsPresence terms need KSG_PRED_LABELSPRESENCE in the config");
+  if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint32_t N = c->N, nw = (N + 63) / 64;
+  if (N == 0 || (extra->n_presence == 0 && extra->n_label_pref == 0)) return KSG_OK;
+  KsgStaticCfg sc{};  // (the terms only: no EqualPriority, anti-affinity domains or affinity pairs)
+  sc.n_presence = extra->n_presence;
+  memcpy(sc.presence_n_keys, extra->presence_n_keys, sizeof sc.presence_n_keys);
+  memcpy(sc.presence_keys, extra->presence_keys, sizeof sc.presence_keys);
+  memcpy(sc.presence_flag, extra->presence_flag, sizeof sc.presence_flag);
+  sc.n_pref = extra->n_label_pref;
+  memcpy(sc.pref_key, extra->pref_key, sizeof sc.pref_key);
+  memcpy(sc.pref_presence, extra->pref_presence, sizeof sc.pref_presence);
+  memcpy(sc.w_pref, extra->w_pref, sizeof sc.w_pref);
+  // |the pass's score| <= 10 x sum |w| (Go-int weights: a wrapped sum is still bounded by it)
+  unsigned __int128 mag = 0;
+  bool weighted = false;
+  for (uint32_t q = 0; q < extra->n_label_pref; ++q) {
+    const int64_t w = extra->w_pref[q];
+    mag += (unsigned __int128)(w < 0 ? 0 - (uint64_t)w : (uint64_t)w) * 10u;
+    weighted |= w != 0;
+  }
+  const bool do_fit = extra->n_presence > 0, do_score = extra->n_label_pref > 0;
+  uint8_t* tmp = nullptr;
+  const size_t fb = (size_t)nw * 8;
+  HIPCHK(c, hipMalloc((void**)&tmp, fb + (size_t)N * 8));
+  uint64_t* xfit = reinterpret_cast<uint64_t*>(tmp);
+  int64_t* xscore = reinterpret_cast<int64_t*>(tmp + fb);
+  KsgDev& d = c->dev;
+  HIPCHK(c, ksg_launch_static_terms(sc, N, c->d_lbl_nodes, c->d_lbl_pairs, c->d_lbl_keys, c->n_pairs, nw, xfit, xscore,
+                                    c->st));
+  HIPCHK(c, ksg_launch_static_fold(const_cast<uint64_t*>(d.static_fit), const_cast<int64_t*>(d.static_score),
+                                   do_fit ? xfit : nullptr, do_score ? xscore : nullptr, nw, N, d.has_static_fit,
+                                   d.has_static_score, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  (void)hipFree(tmp);
+  if (do_fit) d.has_static_fit = 1;
+  if (do_score) {
+    d.has_static_score = 1;
+    c->static_mag += mag;
+    if (weighted) d.empty_priorities = 0;
   }
   d.wide = score_bound(c->cfg, c->ext.w_taint_toleration, c->ext.w_balanced) + c->static_mag >=
            (unsigned __int128)KSG_SCORE_BOUND;

@@ -308,6 +308,13 @@ class DeviceScheduler:
         if rc != abi.KSG_OK:
             self._err(rc)
 
+    def add_static_config(self, extra: abi.KsgConfig):
+        """ksg_add_static_config: one slot pass of LabelsPresence / LabelPreference terms
+        past the config's slots, evaluated on the device from the node labels."""
+        rc = self._lib.ksg_add_static_config(self._ctx, C.byref(extra))
+        if rc != abi.KSG_OK:
+            self._err(rc)
+
     def serve_stats(self) -> dict:
         """The resident begin/commit server (ksg_serve_stats)."""
         o = np.zeros(4, np.uint64)

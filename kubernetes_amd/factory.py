@@ -234,8 +234,8 @@ class SchedulerConfig:
     def split_static(self):
         """The static node terms that fit ksg_config's slots and the ones past them:
         (slotted LabelsPresence, extra LabelsPresence, slotted LabelPreference, extra
-        LabelPreference). Extras are evaluated on the host per node (static_terms)
-        and folded in with ksg_set_static_terms: the reference registers any number
+        LabelPreference). Extras are evaluated on the device per node in slot passes
+        (static_passes, ksg_add_static_config): the reference registers any number
         of them (plugins.go:81-117, 145-183)."""
         p_slot, p_extra = [], []
         for name in sorted(self.predicates):
@@ -249,44 +249,45 @@ class SchedulerConfig:
                 (l_slot if len(l_slot) < abi.MAX_LABEL_PREF else l_extra).append(p)
         return p_slot, p_extra, l_slot, l_extra
 
-    def static_terms(self, nodes):
-        """The extra static terms over `nodes` (node-rank order): (fit words | None,
-        scores | None, weighted). A node passes a LabelsPresence predicate iff every
-        label's presence matches (CheckNodeLabelPresence, predicates.go:194-229); a
-        LabelPreference priority scores 10 where the label's presence matches, else 0
-        (CalculateNodeLabelPriority, priorities.go:98-134), times its weight, summed as
-        Go ints (generic_scheduler.go:145-159)."""
-        import numpy as np
-
+    def static_passes(self, key_id) -> List[abi.KsgConfig]:
+        """The extra static terms as slot passes for ksg_add_static_config, evaluated
+        on the device per node: a LabelsPresence predicate passes a node iff every
+        label's presence matches (CheckNodeLabelPresence, predicates.go:194-229; a
+        predicate with more keys than a slot holds is split over slots, their AND is
+        the same); a LabelPreference priority scores 10 where the label's presence
+        matches, else 0 (CalculateNodeLabelPriority, priorities.go:98-134), times its
+        weight, summed as Go ints (generic_scheduler.go:145-159). key_id interns a
+        label key (the ids of the cluster's label pairs)."""
         _, p_extra, _, l_extra = self.split_static()
-        n = len(nodes)
-        fit = score = None
-        if p_extra:
-            ok = np.ones(n, dtype=bool)
-            for i, node in enumerate(nodes):
-                labels = node.metadata.labels or {}
-                for d in p_extra:
-                    for l in d.labels:
-                        if (l in labels) != bool(d.presence):
-                            ok[i] = False
-            words = np.zeros((n + 63) // 64, dtype=np.uint64)
-            for i in np.nonzero(ok)[0]:
-                words[i >> 6] |= np.uint64(1) << np.uint64(i & 63)
-            fit = words
-        if l_extra:
-            s = [0] * n
-            for i, node in enumerate(nodes):
-                labels = node.metadata.labels or {}
-                for p in l_extra:
-                    if (p.label in labels) == bool(p.presence):
-                        s[i] = _go_int(s[i] + 10 * int(p.weight))
-            score = np.asarray(s, dtype=np.int64)
-        weighted = any(int(p.weight) != 0 for p in l_extra)
-        return fit, score, weighted
+        pres = []  # (keys, presence) per slot
+        for d in p_extra:
+            keys = list(d.labels)
+            for at in range(0, max(len(keys), 1), abi.MAX_PRESENCE_KEYS):
+                pres.append((keys[at:at + abi.MAX_PRESENCE_KEYS], bool(d.presence)))
+        out = []
+        n_pass = max((len(pres) + abi.MAX_PRESENCE - 1) // abi.MAX_PRESENCE,
+                     (len(l_extra) + abi.MAX_LABEL_PREF - 1) // abi.MAX_LABEL_PREF)
+        for k in range(n_pass):
+            c = abi.KsgConfig()
+            ps = pres[k * abi.MAX_PRESENCE:(k + 1) * abi.MAX_PRESENCE]
+            c.n_presence = len(ps)
+            for q, (keys, presence) in enumerate(ps):
+                c.presence_n_keys[q] = len(keys)
+                for i, l in enumerate(keys):
+                    c.presence_keys[q][i] = key_id(l)
+                c.presence_flag[q] = 1 if presence else 0
+            ls = l_extra[k * abi.MAX_LABEL_PREF:(k + 1) * abi.MAX_LABEL_PREF]
+            c.n_label_pref = len(ls)
+            for q, p in enumerate(ls):
+                c.pref_key[q] = key_id(p.label)
+                c.pref_presence[q] = 1 if p.presence else 0
+                c.w_pref[q] = _go_int(int(p.weight))
+            out.append(c)
+        return out
 
     def compile(self, key_id) -> abi.KsgConfig:
         """-> ksg_config. key_id(label_key) interns a label key to its id. Static
-        terms past the config's slots are left to static_terms / ksg_set_static_terms."""
+        terms past the config's slots are left to static_passes / ksg_add_static_config."""
         cfg = abi.KsgConfig()
         bits = 0
         for name in sorted(self.predicates):

@@ -160,9 +160,9 @@ class GPUScheduler:
         if nsig != self._node_sig or ssig != self._svc_sig or self.view is None:
             self.view = ClusterView(nodes, services, self.interner)
             self.engine.set_cluster(self.view.arrays)
-            fit, score, weighted = self.config.static_terms(self.view.nodes)
-            if fit is not None or score is not None:  # LabelsPresence / LabelPreference past the slots
-                self.engine.set_static_terms(fit, score, weighted)
+            # LabelsPresence / LabelPreference past the config's slots: slot passes on the device
+            for extra in self.config.static_passes(self.interner.key_id):
+                self.engine.add_static_config(extra)
             self._node_sig, self._svc_sig = nsig, ssig
             self._mirror = {}
             self._assumed = []

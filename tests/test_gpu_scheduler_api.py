@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
     ("config2", 20, 80, True, 0),
     ("config4", 48, 100, True, 12),
     ("policy_labels", 30, 80, False, 6),
-    ("policy_many_labels", 90, 120, False, 8),  # static terms past the config's slots (ksg_set_static_terms)
+    ("policy_many_labels", 90, 120, False, 8),  # static terms past the config's slots (ksg_add_static_config)
     ("policy_many_labels", 500, 30, True, 0),
 ])
 def test_schedule_matches_ref_model(name, nn, npods, tight, existing):
@@ -110,8 +110,9 @@ def test_unnamed_pods_relist_keeps_device_equal_to_lister():
 @pytest.mark.parametrize("nn,npods", [(300, 120), (600, 30)])
 def test_batch_with_static_terms_matches_ref_model(nn, npods):
     """ksg_schedule_batch (window path) under a Policy with more LabelsPresence /
-    LabelPreference terms than the config's slots: the host-folded static terms
-    (ksg_set_static_terms) against the object-level restatement, pod by pod."""
+    LabelPreference terms than the config's slots: the static terms evaluated on the
+    device in two slot passes (ksg_add_static_config) against the object-level
+    restatement, pod by pod."""
     w = _workload("policy_many_labels", nn, npods, False, 0)
     lister_ref = R.PodLister([])
     preds, prios = R.from_config(w.config, w.nodes, lister_ref, R.ServiceLister(w.services))

@@ -38,9 +38,16 @@ def _policy_labels():
     })
 
 
+# LabelPreference priorities and single-key LabelsPresence predicates of _policy_many_labels:
+# past two slot passes' worth of the config's slots (ksg_add_static_config runs two passes)
+N_PREF = 2 * abi.MAX_LABEL_PREF + 4
+N_U = 2 * abi.MAX_PRESENCE + 1
+
+
 def _policy_many_labels():
     """More LabelsPresence predicates / keys and LabelPreference priorities than
-    ksg_config's slots: the rest go through ksg_set_static_terms."""
+    ksg_config's slots: the rest are evaluated on the device in slot passes
+    (ksg_add_static_config)."""
     preds = [{"name": "PodFitsResources"}, {"name": "MatchNodeSelector"},
              {"name": "HasZone", "argument": {"labelsPresence": {"labels": ["zone"], "presence": True}}},
              {"name": "HasRegionRack", "argument": {"labelsPresence": {"labels": ["region", "rack"], "presence": True}}},
@@ -48,11 +55,11 @@ def _policy_many_labels():
              {"name": "NoA", "argument": {"labelsPresence": {"labels": [f"a{j}" for j in range(abi.MAX_PRESENCE_KEYS + 1)],
                                                             "presence": False}}}]
     preds += [{"name": f"NoU{j:02d}", "argument": {"labelsPresence": {"labels": [f"u{j}"], "presence": False}}}
-              for j in range(abi.MAX_PRESENCE + 1)]
+              for j in range(N_U)]
     prios = [{"name": "LeastRequestedPriority", "weight": 1}]
     prios += [{"name": f"Pref{j:02d}", "weight": 1 + j % 5,
                "argument": {"labelPreference": {"label": f"t{j}", "presence": j % 3 != 0}}}
-              for j in range(abi.MAX_LABEL_PREF + 4)]
+              for j in range(N_PREF)]
     return factory.create_from_config({"predicates": preds, "priorities": prios})
 
 
@@ -61,10 +68,10 @@ def _workload(name, nn, npods, tight=False, existing=0, seed=7):
         rng = workload._SM(seed)
         nodes = workload.make_nodes(nn, rng, dense_labels=2)
         for i, n in enumerate(nodes):  # t_j on every (j + 2)-th node; u_j, a4 on a few
-            for j in range(abi.MAX_LABEL_PREF + 4):
+            for j in range(N_PREF):
                 if i % (j + 2) == 0:
                     n.metadata.labels[f"t{j}"] = "x"
-            for j in range(abi.MAX_PRESENCE + 1):
+            for j in range(N_U):
                 if i % (j + 23) == 7:
                     n.metadata.labels[f"u{j}"] = "x"
             if i % 13 == 5:
