@@ -284,6 +284,10 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   // x-checker, checkers, producers) to test the hand-offs under another
   // interleaving than the natural one (tests/test_gpu_fuzz.py)
   const uint32_t skew = ((uint32_t)d.dbg >> 16) & 15u;
+  // KSG_DEBUG bits 24..27: TIMING EXPERIMENTS ONLY (decisions are wrong): 1 the x-checker posts
+  // "no drop" as soon as the node arrives, 2 the checkers post "no drops" without checking, 4 the
+  // committer takes the staged prediction, 8 the committer does not wait for the verdicts
+  const uint32_t xpt = ((uint32_t)d.dbg >> 24) & 15u;
 
   for (uint32_t t = tid; t < RING; t += NT) r_hdr[t].ready = 0;
   if (tid == 0) *ctl = PlCtl{};
@@ -621,6 +625,14 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         break;
       }
       if (skew & 4u) __builtin_amdgcn_s_sleep(8);
+      if (xpt & 2u) {
+        if (lane == 0) {
+          ctl->chk_cnt[c][par] = 0;
+          ctl->chk_msk[c][par][0] = ctl->chk_msk[c][par][1] = 0;
+          st_rel(&ctl->chk_seq[c], i + 1);
+        }
+        continue;
+      }
       if (i >= 2) apply(i - 2);
       cstamp(c == 0 ? 17 : 20);
       const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
@@ -894,6 +906,10 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         if (i) x_acc += lane == 31 ? (uint64_t)(uint32_t)((uint32_t)t_now - ctl->t_n) : 0ULL;
       }
       if (skew & 2u) __builtin_amdgcn_s_sleep(8);
+      if ((xpt & 1u) && lane == 0) {
+        ctl->xres[par] = 0;
+        st_rel(&ctl->xseq, i + 1);
+      }
       uint32_t res = 0;
       const uint32_t xv = i ? __builtin_amdgcn_readfirstlane(L_xn[i - 1]) : ~0u;
       const uint32_t xnode = xv == ~0u ? ~0u : xv & 0x0fffffffu, xcid = xv == ~0u ? KSG_NO_CAND : xv >> 28;
@@ -992,7 +1008,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         }
         res = (xd ? 1u : 0u) | (flag_x ? 2u : 0u);
       }
-      if (lane == 0) {
+      if (lane == 0 && !(xpt & 1u)) {
         ctl->xres[par] = res;
         if constexpr (STAMP) ctl->t_x = (uint32_t)__builtin_amdgcn_s_memtime();
         st_rel(&ctl->xseq, i + 1);
@@ -1135,7 +1151,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       uint32_t cs = ld_rlx(&ctl->chk_seq[0]);
 #pragma unroll
       for (int c = 1; c < KSG_RES_NCHK; ++c) cs = min(cs, ld_rlx(&ctl->chk_seq[c]));
-      if (cs >= i + 1 && xs >= i + 1) break;
+      if ((cs >= i + 1 && xs >= i + 1) || (xpt & 8u)) break;
       if (spin > 16 * KSG_SPIN_LIMIT || hg) {
         hung = true;
         break;
@@ -1170,7 +1186,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     // kept (a new slot: they have not seen it)
     const bool x_kept = !(((xslot < 64 ? msk0 : msk1) >> (xslot & 63)) & 1ULL);
     const bool x_drop = have_x && (xres & 1u) && ((t0x >> (xnode & 63)) & 1ULL) && x_kept;
-    const uint32_t dropped = __builtin_amdgcn_readfirstlane(cc0) + __builtin_amdgcn_readfirstlane(cc1) + (x_drop ? 1u : 0u);
+    const uint32_t dropped = (xpt & 4u) ? 0u : __builtin_amdgcn_readfirstlane(cc0) + __builtin_amdgcn_readfirstlane(cc1) + (x_drop ? 1u : 0u);
     if (dropped >= k0) {
       resolved = i;  // every snapshot tie got worse: needs a fresh snapshot
       reason = KSG_STOP_EXHAUSTED;

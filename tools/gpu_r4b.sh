@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 TAG=${1:-r4b}
-timeout -k 10 600 python -u -m pytest tests/test_gpu_serve.py tests/test_gpu_extensions.py -x -v --timeout 300 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 || { tail -40 gpurun_out/${TAG}_tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_serve.py tests/test_gpu_extensions.py tests/test_gpu_scheduler_api.py -x -v --timeout 300 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 || { tail -40 gpurun_out/${TAG}_tests.log; exit 1; }
 tail -3 gpurun_out/${TAG}_tests.log
 timeout -k 10 300 python bench.py > gpurun_out/${TAG}_bench_default.json 2> gpurun_out/${TAG}_bench_default.err || { tail gpurun_out/${TAG}_bench_default.err; exit 1; }
 timeout -k 10 300 python bench.py --workload config5 --extensions --ext-filters-only --no-stages > gpurun_out/${TAG}_bench_c5_extf.json 2> gpurun_out/${TAG}_bench_c5_extf.err || { tail gpurun_out/${TAG}_bench_c5_extf.err; exit 1; }
