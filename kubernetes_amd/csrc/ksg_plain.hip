@@ -62,6 +62,8 @@
 //   chk_seq[c], chk_msk,   checker c   committer, producers i               chk_seq[c] = i+1 release after
 //    chk_cnt, L_dpos                                                        the mask, count, positions
 //   xres[i & 1]            x-checker   committer           i                xseq = i+1 release after xres
+//   xpre[i & 1]            x-checker   committer           i (vs pod i-1's  xpre_seq = i+1 release after xpre;
+//                                                          candidates)      posted after commit i-2's flags
 //   L_flag, L_peer,        x-checker   committer           commits <= i-2   program order in the x-checker,
 //    L_peerset, n_peer                 (reads at pod i)                     xseq >= i+1 acquired by the committer
 //   stop, resolved         committer   all                 —                stop = 1 release after resolved
@@ -103,6 +105,9 @@ struct alignas(16) PlCtl {
   uint32_t xn_seq;                       // pods whose drawn node is posted in L_xn
   uint32_t fin_x;                        // the x-checker applied every commit's flags and first peers
   uint32_t t_x, t_n;                     // KSG_DEBUG & 8: clock at the xres / xn posts
+  uint32_t xpre_seq;                     // pods whose pre-verdicts the x-checker posted
+  uint32_t xpre[2];                      // pod of parity p against each candidate c of the pod before it:
+                                         // bit c x drops, bit 8 + c flag (as xres, if commit i-1 lands on c)
 };
 struct PlLdsOff {
   uint32_t ctl, r_hdr, r_t0, r_wp, r_lp, r_rec, r_mod, r_svc, r_cand, r_csnap, r_csv;  // ring
@@ -884,6 +889,107 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       const bool p_staged = i && r_hdr[ep].pad != 0;
       const PodView pv = pod_view(rec);
       const int32_t s = pv.s;
+      // ---- pre-verdicts (off the chain: pod i-1's node is not drawn yet): pod i against each of
+      // pod i-1's staged candidates c as if commit i-1 lands on c, from the replay state of
+      // commits <= i-2 (lane c < 6); the committer uses bit c when the drawn node is candidate c,
+      // so this wave's check leaves the per-pod chain (VERDICT r3 "pre-compute pod i's verdict")
+      uint32_t pre = 0;
+      if (!XS && i > 0 && !__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE) {
+        const uint32_t candv = lane < KSG_NCAND ? r_cand[ep * 8 + lane] : ~0u;
+        // candidate c's slot (commits <= i-2) into lane c: list lengths and window deltas
+        uint32_t c_slot = 0, c_bnk = 0, c_bns = 0;
+        uint64_t c_dlc = 0, c_dlm = 0;
+#pragma unroll
+        for (int c = 0; c < KSG_NCAND; ++c) {
+          const uint32_t cn = (uint32_t)__builtin_amdgcn_readlane((int)candv, c);
+          if (cn == ~0u) continue;
+          const uint64_t h0 = __ballot(xcn0 == cn), h1 = __ballot(xcn1 == cn);
+          if ((h0 | h1) == 0) continue;
+          const uint32_t sl = h0 ? (uint32_t)__builtin_ctzll(h0) : 64u + (uint32_t)__builtin_ctzll(h1);
+          const uint32_t bk = (uint32_t)__builtin_amdgcn_readlane((int)(sl < 64 ? xsk0 : xsk1), (int)(sl & 63));
+          const uint32_t bs = (uint32_t)__builtin_amdgcn_readlane((int)(sl < 64 ? xss0 : xss1), (int)(sl & 63));
+          const uint64_t dc = readlane64((uint64_t)(sl < 64 ? xdc0 : xdc1), (int)(sl & 63));
+          const uint64_t dm = readlane64((uint64_t)(sl < 64 ? xdm0 : xdm1), (int)(sl & 63));
+          if (lane == (uint32_t)c) {
+            c_slot = sl;
+            c_bnk = bk;
+            c_bns = bs;
+            c_dlc = dc;
+            c_dlm = dm;
+          }
+        }
+        // pod i-1: its requests, keys and services (uniform)
+        const PodView ppv = pod_view(prec);
+        const uint32_t pnpp = __builtin_amdgcn_readlane(prec, WS_NPP), pnss = __builtin_amdgcn_readlane(prec, WS_NSS);
+        const uint32_t pnk = (pnpp & 0xffff) + (pnpp >> 16), pnsel = pnss & 0xffff, pns = pnss >> 16;
+        uint32_t p_s_cnt = 0, p_s_first = 0;  // pod i-1's entries of service s, the first one's index
+        if (s >= 0)
+          for (uint32_t t = 0; t < pns; ++t)
+            if ((uint32_t)__builtin_amdgcn_readlane((int)prec, (int)(WS_IDS + pnk + pnsel + t)) == (uint32_t)s) {
+              if (p_s_cnt == 0) p_s_first = t;
+              ++p_s_cnt;
+            }
+        const bool have = lane < KSG_NCAND && candv != ~0u;
+        bool xd = false, flag = false;
+        if (have) {
+          const uint64_t* cs = r_csnap + (ep * KSG_NCAND + lane) * 6;
+          const int64_t capc = (int64_t)cs[0], capm = (int64_t)cs[1], usec = (int64_t)cs[2], usem = (int64_t)cs[3];
+          const double invc = __longlong_as_double((long long)cs[4]), invm = __longlong_as_double((long long)cs[5]);
+          const int64_t nowc = (int64_t)((uint64_t)usec + c_dlc + (uint64_t)ppv.req_c);
+          const int64_t nowm = (int64_t)((uint64_t)usem + c_dlm + (uint64_t)ppv.req_m);
+          if (res_on && !pv.zero_req)  // PodFitsResources (predicates.go:127-145)
+            xd = !((capc == 0 || capc - nowc >= pv.req_c) && (capm == 0 || capm - nowm >= pv.req_m));
+          if (d.w_lr) {  // LeastRequested (priorities.go:43-76): now against the snapshot
+            const int32_t lr_now = lr_win(nowc + pv.req_c, capc, invc) + lr_win(nowm + pv.req_m, capm, invm);
+            const int32_t lr_snap = lr_win(usec + pv.req_c, capc, invc) + lr_win(usem + pv.req_m, capm, invm);
+            xd |= (lr_now >> 1) != (lr_snap >> 1);
+          }
+        }
+        // PodFitsPorts / NoDiskConflict: pod i's keys against the slot's keys and pod i-1's
+        if (pv.nk) {
+          uint32_t mbk = c_bnk;
+#pragma unroll
+          for (int sh = 1; sh < 8; sh <<= 1) mbk = max(mbk, (uint32_t)__shfl_xor((int)mbk, sh, 64));
+          mbk = (uint32_t)__builtin_amdgcn_readfirstlane((int)mbk);
+          for (uint32_t b = 0; b < pv.nk; ++b) {
+            const bool on = b < pv.n_ports ? ports_on : disk_on;
+            if (!on) continue;
+            const uint32_t kb = (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b));
+            for (uint32_t q = 0; q < pnk; ++q)
+              xd |= have && (uint32_t)__builtin_amdgcn_readlane((int)prec, (int)(WS_IDS + q)) == kb;
+            for (uint32_t a = 0; a < mbk; ++a)
+              xd |= have && a < c_bnk && L_cl[(size_t)c_slot * KSG_CL_W + KSG_CL_KEY + a] == kb;
+          }
+        }
+        // ServiceSpreading under an unchanged maxCount, and commit i-1's service flags
+        if (s >= 0) {
+          uint32_t mbs = c_bns;
+#pragma unroll
+          for (int sh = 1; sh < 8; sh <<= 1) mbs = max(mbs, (uint32_t)__shfl_xor((int)mbs, sh, 64));
+          mbs = (uint32_t)__builtin_amdgcn_readfirstlane((int)mbs);
+          uint32_t x_cnt_s = p_s_cnt;
+          for (uint32_t a = 0; a < mbs; ++a)
+            x_cnt_s += (have && a < c_bns && L_cl[(size_t)c_slot * KSG_CL_W + KSG_CL_SV + a] == (uint32_t)s) ? 1u : 0u;
+          if (have && x_cnt_s) {
+            // s's snapshot count on the candidate: staged with pod i-1's services, else from L2
+            const int32_t x_snapc = (p_s_cnt && p_staged)
+                                        ? r_csv[(ep * KSG_NCAND + lane) * KSG_SLOT_SVCS + p_s_first]
+                                        : gld(d.svc_cnt + (size_t)s * d.n_nodes + d.lo + candv);
+            if (spread_on)
+              xd |= frac10_f32((int64_t)pv.smax - x_snapc - (int32_t)x_cnt_s, pv.smax) !=
+                    frac10_f32((int64_t)pv.smax - x_snapc, pv.smax);
+            if (p_s_cnt) {  // commit i-1, a pod of service s: maxCount rises / first peer
+              flag = spread_on && x_snapc + (int32_t)x_cnt_s > pv.smax;
+              if (aff_on && peer0 == -1 && !((L_peerset[s >> 5] >> (s & 31)) & 1u)) flag = true;
+            }
+          }
+        }
+        pre = (uint32_t)(__ballot(have && xd) & 63ULL) | ((uint32_t)(__ballot(have && flag) & 63ULL) << 8);
+      }
+      if (lane == 0) {
+        ctl->xpre[par] = pre;
+        st_rel(&ctl->xpre_seq, i + 1);
+      }
       for (uint32_t spin = 0;; ++spin) {  // pod i-1's node drawn, or the end
         const uint32_t xn = ld_u(&ctl->xn_seq), st = ld_u(&ctl->stop);
         if (xn >= i) break;
@@ -913,7 +1019,10 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       uint32_t res = 0;
       const uint32_t xv = i ? __builtin_amdgcn_readfirstlane(L_xn[i - 1]) : ~0u;
       const uint32_t xnode = xv == ~0u ? ~0u : xv & 0x0fffffffu, xcid = xv == ~0u ? KSG_NO_CAND : xv >> 28;
-      const bool do_check = xnode != ~0u && !__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE;
+      // (a candidate's verdict was posted with the pre-verdicts: no check on the chain)
+      const bool pre_done = !XS && xcid < KSG_NCAND;
+      const bool do_check =
+          !pre_done && xnode != ~0u && !__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE;
       const uint32_t xw = d.lo + (do_check ? xnode : 0u);
       // x's snapshot: staged for a candidate (LDS), else from L2 (in flight over
       // the bookkeeping below)
@@ -1008,6 +1117,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         }
         res = (xd ? 1u : 0u) | (flag_x ? 2u : 0u);
       }
+      if (pre_done) res = ((pre >> xcid) & 1u) | (((pre >> (8 + xcid)) & 1u) << 1);
       if (lane == 0 && !(xpt & 1u)) {
         ctl->xres[par] = res;
         if constexpr (STAMP) ctl->t_x = (uint32_t)__builtin_amdgcn_s_memtime();
@@ -1062,6 +1172,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   int64_t dc0 = 0, dm0 = 0, dc1 = 0, dm1 = 0;  // their window deltas (current through the last commit)
   bool have_x = false;                   // commit i-1's node x (and its slot)
   uint32_t xnode = 0, xslot = 0;
+  uint32_t x_cidx = KSG_NO_CAND;         // x's candidate index (< 6: the x-checker pre-posted its verdict)
   uint64_t t_last = 0, t_acc = 0;
 #define KSG_STAMPP(k)                                        \
   if constexpr (STAMP) {                                     \
@@ -1147,11 +1258,13 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     // verdict on commit i-1's node
     bool hung = false;
     for (uint32_t spin = 0;; ++spin) {
-      const uint32_t xs = ld_rlx(&ctl->xseq), hg = ld_rlx(&ctl->hang);
+      const uint32_t xs = ld_rlx(&ctl->xseq), xp = ld_rlx(&ctl->xpre_seq), hg = ld_rlx(&ctl->hang);
       uint32_t cs = ld_rlx(&ctl->chk_seq[0]);
 #pragma unroll
       for (int c = 1; c < KSG_RES_NCHK; ++c) cs = min(cs, ld_rlx(&ctl->chk_seq[c]));
-      if ((cs >= i + 1 && xs >= i + 1) || (xpt & 8u)) break;
+      // x's verdict: pre-posted when x is a candidate (or there is no x), else the x-checker's
+      const bool x_ok = xs >= i + 1 || (xp >= i + 1 && (!have_x || (!XS && x_cidx < KSG_NCAND)));
+      if ((cs >= i + 1 && x_ok) || (xpt & 8u)) break;
       if (spin > 16 * KSG_SPIN_LIMIT || hg) {
         hung = true;
         break;
@@ -1168,7 +1281,10 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     // one round of LDS reads: drop counts and masks, the drops' positions, the
     // verdict, the service flag word
     const uint32_t cc0 = ctl->chk_cnt[0][par], cc1 = ctl->chk_cnt[1][par];
-    const uint32_t xres = __builtin_amdgcn_readfirstlane(ctl->xres[par]);
+    const uint32_t xpre = __builtin_amdgcn_readfirstlane(ctl->xpre[par]);
+    const uint32_t xres = (!XS && have_x && x_cidx < KSG_NCAND)
+                              ? ((xpre >> x_cidx) & 1u) | (((xpre >> (8 + x_cidx)) & 1u) << 1)
+                              : __builtin_amdgcn_readfirstlane(ctl->xres[par]);
     const uint32_t fw = s >= 0 ? L_flag[s >> 5] : 0u;
     const uint64_t msk0 = ((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[0][par][1]) << 32) |
                           (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[0][par][0]);
@@ -1334,6 +1450,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     have_x = true;
     xnode = woff;
     xslot = slot;
+    x_cidx = cidx;
     ++n_draws;
     KSG_STAMPP(5)
   }

@@ -617,6 +617,18 @@ __device__ __forceinline__ void agent_st32(uint32_t* p, uint32_t v) {
 __device__ __forceinline__ void agent_st64(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// The `applied` protocol between the leader and the scan workgroups (write the
+// invariant down, or use release / acquire). The leader applies a control request (COMMIT's
+// AssumePod delta, PATCH's mirror deltas) with agent-scope stores and atomics, drains them
+// (s_waitcnt vmcnt(0)) and then RELEASES `applied` = the request's sequence number at agent
+// scope. A scan workgroup polls `applied` with relaxed agent-scope loads until it covers the
+// BEGIN's ARG (the last control request the host posted before it), then every wave takes an
+// agent-scope ACQUIRE fence before its first load of mutable state (requested totals, keymap
+// rows, service counts, extended-resource usage). Those loads are agent-scope (ld_mut) as well,
+// so no stale vector-L1 copy from an earlier BEGIN is read either way.
+__device__ __forceinline__ void st_applied(const KsgSrvArgs& a, uint32_t seq) {
+  __hip_atomic_store(&a.grid->applied, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
 // scan workgroups' backstop beyond the leader's idle limit (wall_clock64 ticks, 100 MHz: 10 ms)
 #define KSG_GSRV_WAIT 1000000ull
 // KSG_SERVE_DEBUG: workgroup `slot` reached `stage` of request `seq` (host memory, read after a fault)
@@ -742,6 +754,7 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
       }
       __syncthreads();
       if (s_kind == 0) return;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (pairs with the leader's release of `applied`)
       // mutable state only from here on (issued after `applied` covers the BEGIN's ARG)
 #pragma unroll
       for (int j = 0; j < NPT; ++j) {
@@ -887,7 +900,7 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
     if (tid == 0) grid_mark(a, 0, T, 0x10 + kind);
     if (kind == KSG_SRV_EXIT) {  // (applied too: the next launch's leader skips it)
       if (tid == 0) {
-        agent_st32(&a.grid->applied, T);
+        st_applied(a, T);
         agent_st32(&a.grid->quit, a.epoch);
         drain_stores();
         respond(a, T, 0, 0, 0);
@@ -931,7 +944,7 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
         }
         drain_stores();
         if (lane == 0) {
-          agent_st32(&a.grid->applied, T);
+          st_applied(a, T);
           respond(a, T, 0, 0, 0);
         }
       }
@@ -954,7 +967,7 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
         drain_stores();
       }
       if (lane == 0) {
-        agent_st32(&a.grid->applied, T);  // (a bad one too: the BEGINs after it must not wait forever)
+        st_applied(a, T);  // (a bad one too: the BEGINs after it must not wait forever)
         if (bad) respond_rejected(a, T);
         else respond(a, T, node, 0, 0);
       }

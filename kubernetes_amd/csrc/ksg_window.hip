@@ -418,9 +418,10 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
 // ---------------------------------------------------------------------------
 // phase B
 // ---------------------------------------------------------------------------
-// One workgroup of 8 waves in three roles, pipelined over the window's pods:
+// One workgroup of 8 waves in four roles, pipelined over the window's pods
+// (wave 0 committer, wave 1 scribe, waves 2..3 checkers, waves 4..7 producers):
 //
-//  PRODUCERS (waves 3..7) stage pod j into ring entry j mod KSG_RING: its
+//  PRODUCERS stage pod j into ring entry j mod KSG_RING: its
 //    record, its T0 bitmap (nodes at the snapshot max M0, from phase A's
 //    per-word maxima), k0 = |T0|, its tie-break draw r (the splitmix64 output
 //    at the pod's draw index = the number of earlier window pods that draw:
@@ -429,7 +430,7 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
 //    the top, the answer whenever no tie dropped, with its snapshot state
 //    (capacity, requested totals, 10/capacity) and the pod's service counts
 //    on it and service scalars.
-//  CHECKERS (waves 1, 2) re-check pod i against the nodes committed earlier
+//  CHECKERS re-check pod i against the nodes committed earlier
 //    in the window ("slots", set C): checker c owns slots 64c..64c+63, one per
 //    lane. A slot is a candidate when its node is in T0 (one LDS read); a
 //    candidate drops when the window's deltas pushed its score below M0
@@ -443,9 +444,43 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
 //    prediction when nothing dropped), publishes the choice — which releases
 //    the checkers onto pod i+1 — and then commits into the slot.
 //
+//  SCRIBE (wave 1) writes each order the committer issues into the slot arrays
+//    (AssumePod's delta, the pod's keys and service entries, the services'
+//    snapshot counts), sets the service flags and first peers in commit order,
+//    counts each service's window commits (re-rank), and frees the pod's ring
+//    entry.
+//
 // So the checkers' scan of pod i+1 overlaps the commit of pod i, and the
 // sequential chain per pod is select + commit + one slot's re-check. Slot
 // state lives in LDS (structure of arrays by slot, at most KSG_MAX_SLOTS).
+//
+// Hand-offs (LDS; polls are acquire loads, posts release stores after the data
+// they cover; VERDICT r3 "bring the anti-affinity resolvers up to ksg_plain.hip's
+// standard"):
+//
+//   flag / data              writer      reader               pod index      ordered by
+//   r_hdr[e].ready + entry   producer j  checkers, committer, j              ready = j+1 release after the entry
+//    (record, T0, fit, r mod,            scribe
+//    services, B words)
+//   draw_count               producer j  producer j+1         j              draw_next = j+1 release after it
+//   consumed                 scribe      producers            i              consumed = i+1 release once order i
+//                                                                            is written (entry i mod KSG_RING free)
+//   xs_slot, xs_nslots       committer   checkers             i (pod i+1     sel_seq = i+1 release after them
+//                                                             skips xs_slot)
+//   L_drop[i & 1], chk_cnt,  checker c   committer            i              chk_seq[c] = i+1 release after the
+//    chk_stop, L_dca                                                         drop bits (atomicOr), counts, rows
+//   L_ord[i & 1] (WinOrder)  committer   scribe               i              order_seq = i+1 release after a
+//                                                                            wavefront fence (lds_fence)
+//   slot arrays, L_flag,     scribe      checkers, committer  orders <= i    scribe_done = i+1 release after the
+//    L_peer, n_peer, L_nsv                                                   writes; checkers of pod i+2 wait for
+//                                                                            scribe_done >= i+1, the committer
+//                                                                            (wait_scribe) before it reads a slot
+//   stop                     committer   all                  —              release; every other wave exits
+//
+// Every wait has a spin limit (the committer's and the checkers' end the
+// window with KSG_STOP_HANG; the host fails the batch). KSG_DEBUG bits 16..19
+// add a fixed delay per pod to the committer, scribe, checkers or producers
+// (tests/test_gpu_fuzz.py runs each skew once against the oracle).
 // The node state in HBM stays the pristine snapshot while the window
 // resolves; the window's deltas are written back once, at the end.
 // ANTI: ServiceAntiAffinity is on (its checks are compiled only into these
@@ -501,6 +536,9 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
   const bool res_on = (d.preds & KSG_PRED_PODFITSRESOURCES) != 0;
   const bool ports_on = (d.preds & KSG_PRED_PODFITSPORTS) != 0;
   const bool disk_on = (d.preds & KSG_PRED_NODISKCONFLICT) != 0;
+  // KSG_DEBUG bits 16..19: a fixed delay per pod in one role (committer, scribe, checkers,
+  // producers): another interleaving of the hand-offs than the natural one (tests/test_gpu_fuzz.py)
+  const uint32_t skew = ((uint32_t)d.dbg >> 16) & 15u;
 
   for (uint32_t t = tid; t < KSG_RING; t += KSG_RES_NT) r_hdr[t].ready = 0;
   if (tid == 0) {
@@ -573,6 +611,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
         __builtin_amdgcn_s_sleep(1);
       }
       pstamp(12);
+      if (skew & 8u) __builtin_amdgcn_s_sleep(8);
       const uint32_t rec = lane < KSG_WIN_SUM_DWORDS ? recs[(size_t)j * KSG_WIN_SUM_DWORDS + lane] : 0u;
       uint64_t t0[P];
       int32_t mw[P];
@@ -707,6 +746,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
           break;
         __builtin_amdgcn_s_sleep(1);
       }
+      if (skew & 4u) __builtin_amdgcn_s_sleep(8);
       const uint32_t xs = ctl->xs_slot, ns = ctl->xs_nslots;
       const uint32_t rec = lane < KSG_WIN_SUM_DWORDS ? r_rec[e * KSG_WIN_SUM_DWORDS + lane] : 0u;
       const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
@@ -791,6 +831,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
         __builtin_amdgcn_s_sleep(1);
       }
       if (!have) break;
+      if (skew & 2u) __builtin_amdgcn_s_sleep(8);
       const WinOrder& od = L_ord[i & 1];
       const uint32_t kind = __builtin_amdgcn_readfirstlane(od.kind);
       const int32_t outv = __builtin_amdgcn_readfirstlane(od.out);
@@ -971,6 +1012,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
       t_acc += lane == (i < 4 ? 10u : 11u) ? t_now - t_last : 0ULL;
     }
     KSG_STAMP(0)
+    if (skew & 1u) __builtin_amdgcn_s_sleep(8);
     // ---- head
     const uint32_t rec = lane < KSG_WIN_SUM_DWORDS ? r_rec[e * KSG_WIN_SUM_DWORDS + lane] : 0u;
     const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
@@ -1544,6 +1586,37 @@ __host__ __device__ inline WinLdsOff2 win2_lds_offsets(uint32_t P, uint32_t nfla
 
 // ANTI: ServiceAntiAffinity with the re-rank (x.rr; the LDS-slot resolver above
 // takes every other anti-affinity configuration)
+//
+// Hand-offs (LDS; every poll is relaxed loads then one LDS-only acquire fence,
+// every post a workgroup-scope release store after the data it covers):
+//
+//   flag / data              writer      reader              pod index        ordered by
+//   r_hdr[e].ready + entry   producer j  all but producers   j                ready = j+1 release after the entry
+//    (record, T0, fit, B,                                                     (lane prefixes r_lp / r_wp too)
+//    row bests / counts)
+//   L_pub / L_drw bits       producer j  producers > j       j                L_drw before L_pub (atomicOr, in order)
+//   L_xn[i]                  committer   x-checker           i (checks i+1)   xn_seq = i+1 release after L_xn[i]
+//   L_cm[i], L_out[i],       committer   checkers (apply i   i                sel_seq = i+1 release after them
+//    slot row keys / ids                 at pod i+2)
+//   slot row counts          checker     checkers,           commits <= i-2   chk_seq release (the x-checker
+//                            (apply)     x-checker                            reads rows of commits it replayed)
+//   chk_seq[c], chk_cnt,     checker c   committer,          i                chk_seq[c] = i+1 release after the
+//    chk_msk, L_dpos,                    producers                            masks, counts, positions and the
+//    chk_stop, L_dca, L_ddr                                                   anti-affinity row sums
+//   xres, xdz, xdc, xrw,     x-checker   committer           i                xseq = i+1 release after them
+//    xnsv [i & 1]
+//   L_flag, L_peer,          x-checker   committer           commits <= i-2   program order in the x-checker,
+//    L_peerset, n_peer,                  (reads at pod i)                     xseq >= i+1 acquired by the committer
+//    L_nsv
+//   stop, resolved           committer   all                 —                stop = 1 release after resolved
+//   fin[c], fin_x            checkers,   committer           —                release after the write-back /
+//                            x-checker                                        the last first peers
+//
+// Ring entry e = j mod RING is rewritten for pod j once the checkers are done
+// with pod j-RING+2 and the x-checker with pod j-RING+1. Every wait has a spin
+// limit; a timed-out wait sets ctl->hang and the host fails the batch. KSG_DEBUG
+// bits 16..19 add a fixed delay per pod to the committer, x-checker, checkers or
+// producers (tests/test_gpu_fuzz.py runs each skew once against the oracle).
 template <int P, bool STAMP, bool ANTI>
 __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
                                                                const KsgWinSum* __restrict__ sums,
@@ -1602,6 +1675,9 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   const bool ports_on = (d.preds & KSG_PRED_PODFITSPORTS) != 0;
   const bool disk_on = (d.preds & KSG_PRED_NODISKCONFLICT) != 0;
   const uint32_t nbits = (wcap + 31) / 32;
+  // KSG_DEBUG bits 16..19: a fixed delay per pod in one role (committer, x-checker, checkers,
+  // producers): another interleaving of the hand-offs than the natural one (tests/test_gpu_fuzz.py)
+  const uint32_t skew = ((uint32_t)d.dbg >> 16) & 15u;
 
   for (uint32_t t = tid; t < RING; t += NT) r_hdr[t].ready = 0;
   if (tid == 0) *ctl = WinCtl2{};
@@ -1672,6 +1748,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         __builtin_amdgcn_s_sleep(1);
       }
       pstamp(24);
+      if (skew & 8u) __builtin_amdgcn_s_sleep(8);
       const uint32_t rec = lane < DW ? recs[(size_t)j * DW + lane] : 0u;
       uint64_t t0[P];
       int32_t mw[P];
@@ -1944,6 +2021,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       }
       acq_lds();
       cstamp(c == 0 ? 16 : 19);
+      if (!stopped && (skew & 4u)) __builtin_amdgcn_s_sleep(8);
       if (stopped) {
         // pods [0, resolved) are decided: apply the commits this checker has not
         // (the committer runs ahead of the checkers over pods that do not commit)
@@ -2286,6 +2364,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       }
       acq_lds();
       if (stopped) break;
+      if (skew & 2u) __builtin_amdgcn_s_sleep(8);
       if constexpr (STAMP) {
         const uint64_t t_now = __builtin_amdgcn_s_memtime();
         x_acc += lane == 28 ? t_now - x_last : 0ULL;
@@ -2496,6 +2575,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       }
     }
     acq_lds();
+    if (skew & 1u) __builtin_amdgcn_s_sleep(8);
     if constexpr (STAMP) {  // ring wait of the window's first 4 pods (lane 10) vs the rest (lane 11)
       const uint64_t t_now = __builtin_amdgcn_s_memtime();
       t_acc += lane == (i < 4 ? 10u : 11u) ? t_now - t_last : 0ULL;

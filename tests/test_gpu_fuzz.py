@@ -124,8 +124,10 @@ def test_family_windows_match_oracle(family):
 # pods differed in ~1 of 5 runs of `namespaces` in round 2). Instead of
 # repeating runs, each case runs once per fixed delay pattern: KSG_DEBUG bits
 # 16..19 make one wave role (committer, x-checker, checkers, producers) sleep
-# ~512 cycles per pod (ksg_plain.hip), which pushes every hand-off onto its
-# other side (the role that is usually ahead falls behind, and vice versa)
+# ~512 cycles per pod (ksg_plain.hip; round 4: also the ServiceAntiAffinity
+# resolvers of ksg_window.hip, the register-slot re-rank and the LDS-slot one),
+# which pushes every hand-off onto its other side (the role that is usually
+# ahead falls behind, and vice versa)
 _SKEWS = (0, 1, 2, 4, 8, 1 | 4, 2 | 8, 2 | 4)
 
 
@@ -161,3 +163,29 @@ def test_fuzz_interleavings_match_oracle(seed, monkeypatch):
             dev.close()
             bad = np.nonzero(got != want)[0]
             assert bad.size == 0, f"{desc} window {window} skew {skew}: first mismatches at {bad[:6]}"
+
+
+@pytest.mark.parametrize("resolver", ["rerank", "ldsslot"])
+def test_anti_affinity_resolver_interleavings_match_oracle(resolver, monkeypatch):
+    """Config 4's ServiceAffinity + ServiceAntiAffinity at 900 nodes under every
+    skew: the register-slot re-rank resolver (ksg_win_resolve2_kernel<..., ANTI>)
+    and, with KSG_DEBUG & 4096, the LDS-slot one (ksg_win_resolve_kernel)."""
+    from tests.helpers import Case
+
+    case = Case("config4", 900, 600)
+    orc = OracleScheduler(case.cfg)
+    orc.set_cluster(case.view.arrays)
+    want, sw = orc.batch(case.batch, 31)
+    extra = 4096 if resolver == "ldsslot" else 0
+    for window in (5, 64, 128):
+        for skew in _SKEWS:
+            monkeypatch.setenv("KSG_DEBUG", str((skew << 16) | extra))
+            dev = DeviceScheduler(case.cfg, device=0)
+            dev.set_window(window)
+            dev.set_cluster(case.view.arrays)
+            got, sg = dev.batch(case.batch, 31)
+            windows = dev.last_batch_stats()["windows"]
+            dev.close()
+            bad = np.nonzero(got != want)[0]
+            assert bad.size == 0, f"{resolver} window {window} skew {skew}: first mismatches at {bad[:6]}"
+            assert sg == sw and windows > 0
