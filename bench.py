@@ -187,11 +187,12 @@ def main():
                     help="PMC-derived HBM bytes per launch (profiles/), keyed by workload")
     ap.add_argument("--extensions", action="store_true",
                     help="add the extensions beyond this reference vintage (taints / tolerations, GPU and FPGA "
-                         "counts, TaintToleration + BalancedResourceAllocation; parity unpinned, exact kernels), "
-                         "reported as a separate workload (SURVEY.md section 0, item 2)")
+                         "counts, TaintToleration + BalancedResourceAllocation; parity unpinned; the window path, "
+                         "--window 0 for the exact kernels), reported as a separate workload (SURVEY.md section 0, "
+                         "item 2)")
     ap.add_argument("--ext-filters-only", action="store_true",
                     help="with --extensions: the filters only (taints, extended resources), TaintToleration and "
-                         "BalancedResourceAllocation weights 0, so batches take the window path")
+                         "BalancedResourceAllocation weights 0")
     ap.add_argument("--no-stages", action="store_true",
                     help="skip the resolver's per-stage cycle breakdown (a second, untimed run with KSG_DEBUG=8)")
     args = ap.parse_args()
@@ -227,7 +228,7 @@ def main():
         batch = PodBatch(batch.pods, ids_x, rec)
         ext = (ecfg.compile(max(len(inter.taints), 1)), node_arrays)
         if world > 1:
-            raise SystemExit("--extensions runs on one rank (the exact kernels)")
+            raise SystemExit("--extensions runs on one rank")
 
     def load_cluster(s):
         """set_cluster (+ the extensions, which must be enabled before it)."""
@@ -385,11 +386,24 @@ def main():
                 "frac": achieved / HBM_PEAK, "traffic": traffic, "kernel": kname,
                 "kernel_ms_avg": kavg_s * 1e3, "bytes_per_node_pod": bpn, "alg_bytes_per_launch": alg_bytes}
     roofline.update(extra)
+    filter_score = None
     if kk["launches"] > 0:
         ent = tj.get(f"{wl}:{n_nodes}:ksg_win_score_kernel")  # phase A's counter-measured bytes (profiles/)
         if ent:
             roofline["win_eval_traffic"] = ent["hbm_bytes_per_launch"]
             roofline["win_eval_traffic_GBps"] = ent["hbm_bytes_per_launch"] / ev_s / 1e9
+        # the filter/score kernel itself (phase A: every node of the shard x the window's pods,
+        # findNodesThatFit + prioritizeNodes, generic_scheduler.go:100-165) against the HBM peak:
+        # its counter-measured bytes (FETCH x2 + WRITE, profiles/traffic.json) when this workload
+        # has a PMC pass, else its byte model, over its mean launch time from the HIP events
+        fs_bytes = ent["hbm_bytes_per_launch"] if ent else ev_bytes
+        filter_score = {"kernel": "ksg_win_score_kernel", "bound": "hbm", "unit": "GB/s",
+                        "basis": "pmc_traffic" if ent else "byte_model",
+                        "bytes_per_launch": fs_bytes, "ms_avg": ev_s * 1e3,
+                        "achieved": fs_bytes / ev_s / 1e9, "peak": HBM_PEAK / 1e9,
+                        "frac": fs_bytes / ev_s / HBM_PEAK,
+                        "pods_per_launch": w_mean, "nodes": n_nodes / world}
+        roofline["filter_score_frac"] = filter_score["frac"]
 
     # ---- latency view: the resolver is one in-order dependency chain per window
     # (one workgroup), so its bound is the chain's cycles per pod,
@@ -493,7 +507,7 @@ def main():
                                + ((" + extension filters (taints/tolerations, GPU/FPGA counts; scoring "
                                    "extensions off; parity unpinned, window path)" if args.ext_filters_only else
                                    " + extensions (taints/tolerations, GPU/FPGA counts, TaintToleration, "
-                                   "BalancedResourceAllocation; parity unpinned, exact kernels)") if ext else ""),
+                                   "BalancedResourceAllocation; parity unpinned)") if ext else ""),
                    "nodes": n_nodes, "pods_per_step": args.batch,
                    "placed_in_timed": int((timed >= 0).sum()), "fit_errors_in_timed": int((timed == -1).sum()),
                    "snapshots_in_timed": wstats,
@@ -503,6 +517,7 @@ def main():
                    else (f"node-sharded x{world}: shard scoring, {xname} all-gather per window, replicated resolver"
                          if kk["launches"] else f"node-sharded x{world}, {xname} all-gather per pod")},
         "roofline": roofline,
+        "filter_score": filter_score,
         "latency": latency,
         "cpu_baseline": cpu,
     }

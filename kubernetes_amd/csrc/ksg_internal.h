@@ -100,6 +100,9 @@ struct KsgDev {
   const int64_t* scalar_cap;  // [n_scalar][N] allocatable
   int64_t* scalar_used;       // [n_scalar][N] requested by the pods on the node (mutable)
   const uint64_t* taintmap;   // [max_taints][nw] nodes carrying taint t
+  // per node, its taint ids as a bitmask (max_taints <= 64; else nullptr): the window
+  // path's TaintToleration term counts a pod's untolerated soft taints as one popcount
+  const uint64_t* ntaint;
 };
 
 // static-table configuration (LabelsPresence, EqualPriority, LabelPreference,
@@ -182,6 +185,16 @@ struct KsgWinXchg {
   // ksg_pod_ext records (pod pos + i of the window at exts[pos + i]), else nullptr
   const ksg_pod_ext* exts;
   uint32_t img_stride;
+  // extensions with scores (TaintToleration / BalancedAllocation on the window path):
+  // esc != 0; phase A also writes each pod's fit bitmap (uint64[wcap][ostride] at efit_off
+  // in a block: non-T0 committed nodes whose score may rise need "fit at the snapshot"),
+  // its untolerated soft taints as a mask (psoft[pod]) and, in the count pass, the
+  // TaintToleration normalisation max over its filtered nodes (tmax[pod], zeroed by the
+  // resolver for the next window)
+  uint32_t esc;
+  uint32_t efit_off;
+  int32_t* tmax;
+  uint64_t* psoft;
   uint32_t rr;        // re-rank on (else a service's commit ends the window)
   uint32_t dz;        // domain rows: anti domains + 1 (<= KSG_RR_MAXZ)
   uint32_t b_off;     // byte offset in a block of the best-per-domain bitmaps

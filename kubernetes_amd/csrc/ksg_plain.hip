@@ -62,8 +62,6 @@
 //   chk_seq[c], chk_msk,   checker c   committer, producers i               chk_seq[c] = i+1 release after
 //    chk_cnt, L_dpos                                                        the mask, count, positions
 //   xres[i & 1]            x-checker   committer           i                xseq = i+1 release after xres
-//   xpre[i & 1]            x-checker   committer           i (vs pod i-1's  xpre_seq = i+1 release after xpre;
-//                                                          candidates)      posted after commit i-2's flags
 //   L_flag, L_peer,        x-checker   committer           commits <= i-2   program order in the x-checker,
 //    L_peerset, n_peer                 (reads at pod i)                     xseq >= i+1 acquired by the committer
 //   stop, resolved         committer   all                 —                stop = 1 release after resolved
@@ -105,13 +103,17 @@ struct alignas(16) PlCtl {
   uint32_t xn_seq;                       // pods whose drawn node is posted in L_xn
   uint32_t fin_x;                        // the x-checker applied every commit's flags and first peers
   uint32_t t_x, t_n;                     // KSG_DEBUG & 8: clock at the xres / xn posts
-  uint32_t xpre_seq;                     // pods whose pre-verdicts the x-checker posted
-  uint32_t xpre[2];                      // pod of parity p against each candidate c of the pod before it:
-                                         // bit c x drops, bit 8 + c flag (as xres, if commit i-1 lands on c)
+  // (extension scores) checker c's slots for the pod of parity p whose score ROSE above M0
+  // (L_sig: the score) and non-T0 slots that JOINED T0 (L_dpos: their T0 position), and a
+  // normalisation stop (a slot the pod fitted at its TaintToleration max no longer fits)
+  uint32_t chk_rmsk[KSG_RES_NCHK][2][2];
+  uint32_t chk_jmsk[KSG_RES_NCHK][2][2];
+  uint32_t chk_nstop[KSG_RES_NCHK][2];
+  int32_t xsig[2];                       // (extension scores) x's score when it rose (xres bit 2)
 };
 struct PlLdsOff {
   uint32_t ctl, r_hdr, r_t0, r_wp, r_lp, r_rec, r_mod, r_svc, r_cand, r_csnap, r_csv;  // ring
-  uint32_t cm, out, xn, peer, flag, peerset, pub, drw, clist, dpos;                   // window
+  uint32_t cm, out, xn, peer, flag, peerset, pub, drw, clist, dpos, sig;              // window
   uint32_t total;
 };
 
@@ -140,6 +142,7 @@ __host__ __device__ inline PlLdsOff plain_lds_offsets(uint32_t P, uint32_t nflag
   o.drw = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
   o.clist = at;   at += win_al16((size_t)KSG_MAX_SLOTS * KSG_CL_W * 4);
   o.dpos = at;    at += win_al16((size_t)2 * KSG_MAX_SLOTS * 4);
+  o.sig = at;     at += win_al16((size_t)2 * KSG_MAX_SLOTS * 4);    // (extension scores) risen slots' scores
   o.total = at;
   return o;
 }
@@ -277,13 +280,17 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   uint32_t* L_drw = reinterpret_cast<uint32_t*>(smem + o.drw);  // drawable pods
   uint32_t* L_cl = reinterpret_cast<uint32_t*>(smem + o.clist);  // [slot][KSG_CL_W]
   uint32_t* L_dpos = reinterpret_cast<uint32_t*>(smem + o.dpos);  // [parity][slot] drop positions in T0
+  int32_t* L_sig = reinterpret_cast<int32_t*>(smem + o.sig);       // [parity][slot] (extension scores) risen scores
   const bool spread_on = d.w_spread != 0;
   const bool aff_on = (d.preds & KSG_PRED_SERVICEAFFINITY) && d.n_aff > 0;
   const bool res_on = (d.preds & KSG_PRED_PODFITSRESOURCES) != 0;
   const bool ports_on = (d.preds & KSG_PRED_PODFITSPORTS) != 0;
   const bool disk_on = (d.preds & KSG_PRED_NODISKCONFLICT) != 0;
   // (extensions) extended resources: re-checked on the slots like cpu / memory
-  constexpr bool xs_on = XS;
+  const bool xs_on = XS && (d.ext_filters & KSG_EXT_SCALAR) && d.n_scalar > 0;
+  // (extensions) TaintToleration / BalancedAllocation: the slots are re-scored (risers and
+  // joiners, see the committer)
+  const bool esc = XS && x.esc != 0;
   const uint32_t nbits = (wcap + 31) / 32;
   // KSG_DEBUG bits 16..19: a fixed delay per pod in one wave role (committer,
   // x-checker, checkers, producers) to test the hand-offs under another
@@ -486,7 +493,15 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         r_svc[e].max[lane] = s_max;
         r_svc[e].peer[lane] = s_peer;
       }
+      uint64_t e_ps = 0;
+      int32_t e_tm = 0;
+      if (esc) {  // (extension scores) the pod's soft-taint mask and TaintToleration max
+        e_ps = x.psoft[j];
+        e_tm = x.tmax ? x.tmax[j] : 0;
+      }
       if (lane == 0) {
+        r_hdr[e].psoft = e_ps;
+        r_hdr[e].tmax = e_tm;
         r_hdr[e].m0 = m0;
         r_hdr[e].k0 = k0;
         r_hdr[e].r = r;
@@ -518,6 +533,8 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     S.nk = S.ns = S.smask = 0;
     S.row = ~0u;
     S.xk = 0;
+    S.sst = 0;
+    S.ntm = 0;
 #pragma unroll
     for (int r = 0; r < 4; ++r) S.xh[r] = S.xdl[r] = 0;
     // AssumePod of pod p (plugin/pkg/scheduler/scheduler.go:115-118) into the
@@ -555,6 +572,10 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         S.dl_c = S.dl_m = 0;
         S.smask = 0;
         S.xk = 0;
+        if (esc) {  // (extension scores) the node's static score and taints
+          S.sst = d.has_static_score ? (int32_t)gld(d.static_score + wn) : 0;
+          S.ntm = d.ntaint ? gld(d.ntaint + wn) : 0ULL;
+        }
         if (xs_on)  // (extensions) the node's extended resource headroom at the snapshot
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -644,14 +665,87 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
       bool drop = false;
       uint32_t dpos = 0;
+      uint32_t est = 0;  // (extension scores) 2: rose above M0 (esig), 4: joined T0, 8: normalisation stop
+      int32_t esig = 0;
       if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE && S.node != ~0u) {
         const PodView pv = pod_view(rec);
         const uint32_t wd = S.node >> 6;
         const uint64_t tw = r_t0[(size_t)e * P * 64 + wd];
-        // the node's ascending position in T0 (used only if it drops)
+        // the node's ascending position in T0 (used if it drops; for a node outside
+        // T0, the T0 nodes below it: where it joins)
         dpos = r_lp[e * 64 + (wd >> 6) * 2] + r_wp[(size_t)e * P * 64 + wd] +
                (uint32_t)__popcll(tw & ((1ULL << (S.node & 63)) - 1ULL));
-        if ((tw >> (S.node & 63)) & 1ULL) {
+        if (esc) {
+          // (extension scores) the slot's score for pod i now against the snapshot: T0 nodes
+          // drop (unfit / below M0) or rise above it; nodes outside T0 that the pod fitted at
+          // the snapshot can reach M0 (join T0) or pass it (BalancedAllocation rises)
+          const bool in_t0 = (tw >> (S.node & 63)) & 1ULL;
+          const int64_t now_c = (int64_t)((uint64_t)S.snp_c + (uint64_t)S.dl_c);
+          const int64_t now_m = (int64_t)((uint64_t)S.snp_m + (uint64_t)S.dl_m);
+          bool unfit = false;
+          if (res_on && !pv.zero_req)  // PodFitsResources (predicates.go:127-145)
+            unfit = !((S.cap_c == 0 || S.cap_c - now_c >= pv.req_c) && (S.cap_m == 0 || S.cap_m - now_m >= pv.req_m));
+          if (S.xk & pv.xm)  // extended resources
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int32_t q = (int32_t)__builtin_amdgcn_readlane(rec, WS_XREQ + r);
+              unfit |= q > 0 && S.xh[r] - S.xdl[r] < q;
+            }
+          if (!unfit && pv.nk && S.nk)  // PodFitsPorts / NoDiskConflict vs the window's keys
+            for (uint32_t a = 0; a < S.nk; ++a) {
+              const uint32_t key = my_cl[KSG_CL_KEY + a];
+              for (uint32_t b = 0; b < pv.nk; ++b) {
+                const bool on = b < pv.n_ports ? ports_on : disk_on;
+                unfit |= on && (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b)) == key;
+              }
+            }
+          // ServiceSpreading: the window's entries of the pod's service here (maxCount fixed)
+          int32_t snapc = 0, sdel = 0;
+          if (spread_on && pv.s >= 0 && ((S.smask >> (pv.s & 31)) & 1u))
+            for (uint32_t a = 0; a < S.ns; ++a)
+              if (my_cl[KSG_CL_SV + a] == (uint32_t)pv.s) {
+                snapc = (int32_t)my_cl[KSG_CL_SC + a];
+                ++sdel;
+              }
+          const bool sp = spread_on && pv.s >= 0 && pv.smax > 0;
+          const int64_t fr_snap = (sp && sdel) ? frac10_f32((int64_t)pv.smax - snapc, pv.smax) : 0;
+          const int64_t fr_now = (sp && sdel) ? frac10_f32((int64_t)pv.smax - snapc - sdel, pv.smax) : 0;
+          const int64_t dl = es_delta(d, pv.req_c, pv.req_m, S.cap_c, S.cap_m, S.inv_c, S.inv_m, S.snp_c, S.snp_m,
+                                      now_c, now_m, fr_snap, fr_now);
+          const uint64_t psoft = r_hdr[e].psoft;
+          const int32_t tmx = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].tmax);
+          const int32_t soft = __popcll(S.ntm & psoft);
+          const bool at_max = d.w_taint != 0 && tmx > 0 && soft == tmx;
+          if (in_t0) {
+            if (unfit) {
+              drop = true;
+              if (at_max) est |= 8u;  // (the normalisation max may fall: a fresh snapshot)
+            } else if (dl < 0) {
+              drop = true;
+            } else if (dl > 0) {
+              est |= 2u;
+              esig = (int32_t)(m0 + dl);
+            }
+          } else if (dl > 0 || (unfit && at_max)) {
+            const uint64_t fw = gld(reinterpret_cast<const uint64_t*>(x.buf + x.efit_off) + (size_t)i * x.ostride + wd);
+            if ((fw >> (S.node & 63)) & 1ULL) {  // fitted at the snapshot
+              if (unfit) {
+                est |= 8u;
+              } else {
+                const int32_t cs = sdel ? snapc : (sp ? gld(d.svc_cnt + (size_t)pv.s * d.n_nodes + d.lo + S.node) : 0);
+                const int64_t frs = sp ? frac10_f32((int64_t)pv.smax - cs, pv.smax) : 10;
+                const int64_t now = es_snap_score(d, pv.req_c, pv.req_m, S.cap_c, S.cap_m, S.inv_c, S.inv_m, S.snp_c,
+                                                  S.snp_m, frs, S.sst, soft, tmx) + dl;
+                if (now > m0) {
+                  est |= 2u;
+                  esig = (int32_t)now;
+                } else if (now == m0) {
+                  est |= 4u;
+                }
+              }
+            }
+          }
+        } else if ((tw >> (S.node & 63)) & 1ULL) {
           // does the slot (a snapshot tie of the pod) score below M0 now?
           const int64_t now_c = (int64_t)((uint64_t)S.snp_c + (uint64_t)S.dl_c);
           const int64_t now_m = (int64_t)((uint64_t)S.snp_m + (uint64_t)S.dl_m);
@@ -691,8 +785,19 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           }
         }
       }
-      if (drop) L_dpos[par * KSG_MAX_SLOTS + my_slot] = dpos;
+      if (drop || (est & 4u)) L_dpos[par * KSG_MAX_SLOTS + my_slot] = dpos;
+      if (est & 2u) L_sig[par * KSG_MAX_SLOTS + my_slot] = esig;
       const uint64_t dmsk = __ballot(drop);
+      if (esc) {
+        const uint64_t rm = __ballot((est & 2u) != 0), jm = __ballot((est & 4u) != 0), nm = __ballot((est & 8u) != 0);
+        if (lane == 0) {
+          ctl->chk_rmsk[c][par][0] = (uint32_t)rm;
+          ctl->chk_rmsk[c][par][1] = (uint32_t)(rm >> 32);
+          ctl->chk_jmsk[c][par][0] = (uint32_t)jm;
+          ctl->chk_jmsk[c][par][1] = (uint32_t)(jm >> 32);
+          ctl->chk_nstop[c][par] = nm != 0 ? 1u : 0u;
+        }
+      }
       if (lane == 0) {
         ctl->chk_cnt[c][par] = (uint32_t)__popcll(dmsk);
         ctl->chk_msk[c][par][0] = (uint32_t)dmsk;
@@ -889,107 +994,6 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       const bool p_staged = i && r_hdr[ep].pad != 0;
       const PodView pv = pod_view(rec);
       const int32_t s = pv.s;
-      // ---- pre-verdicts (off the chain: pod i-1's node is not drawn yet): pod i against each of
-      // pod i-1's staged candidates c as if commit i-1 lands on c, from the replay state of
-      // commits <= i-2 (lane c < 6); the committer uses bit c when the drawn node is candidate c,
-      // so this wave's check leaves the per-pod chain (VERDICT r3 "pre-compute pod i's verdict")
-      uint32_t pre = 0;
-      if (!XS && i > 0 && !__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE) {
-        const uint32_t candv = lane < KSG_NCAND ? r_cand[ep * 8 + lane] : ~0u;
-        // candidate c's slot (commits <= i-2) into lane c: list lengths and window deltas
-        uint32_t c_slot = 0, c_bnk = 0, c_bns = 0;
-        uint64_t c_dlc = 0, c_dlm = 0;
-#pragma unroll
-        for (int c = 0; c < KSG_NCAND; ++c) {
-          const uint32_t cn = (uint32_t)__builtin_amdgcn_readlane((int)candv, c);
-          if (cn == ~0u) continue;
-          const uint64_t h0 = __ballot(xcn0 == cn), h1 = __ballot(xcn1 == cn);
-          if ((h0 | h1) == 0) continue;
-          const uint32_t sl = h0 ? (uint32_t)__builtin_ctzll(h0) : 64u + (uint32_t)__builtin_ctzll(h1);
-          const uint32_t bk = (uint32_t)__builtin_amdgcn_readlane((int)(sl < 64 ? xsk0 : xsk1), (int)(sl & 63));
-          const uint32_t bs = (uint32_t)__builtin_amdgcn_readlane((int)(sl < 64 ? xss0 : xss1), (int)(sl & 63));
-          const uint64_t dc = readlane64((uint64_t)(sl < 64 ? xdc0 : xdc1), (int)(sl & 63));
-          const uint64_t dm = readlane64((uint64_t)(sl < 64 ? xdm0 : xdm1), (int)(sl & 63));
-          if (lane == (uint32_t)c) {
-            c_slot = sl;
-            c_bnk = bk;
-            c_bns = bs;
-            c_dlc = dc;
-            c_dlm = dm;
-          }
-        }
-        // pod i-1: its requests, keys and services (uniform)
-        const PodView ppv = pod_view(prec);
-        const uint32_t pnpp = __builtin_amdgcn_readlane(prec, WS_NPP), pnss = __builtin_amdgcn_readlane(prec, WS_NSS);
-        const uint32_t pnk = (pnpp & 0xffff) + (pnpp >> 16), pnsel = pnss & 0xffff, pns = pnss >> 16;
-        uint32_t p_s_cnt = 0, p_s_first = 0;  // pod i-1's entries of service s, the first one's index
-        if (s >= 0)
-          for (uint32_t t = 0; t < pns; ++t)
-            if ((uint32_t)__builtin_amdgcn_readlane((int)prec, (int)(WS_IDS + pnk + pnsel + t)) == (uint32_t)s) {
-              if (p_s_cnt == 0) p_s_first = t;
-              ++p_s_cnt;
-            }
-        const bool have = lane < KSG_NCAND && candv != ~0u;
-        bool xd = false, flag = false;
-        if (have) {
-          const uint64_t* cs = r_csnap + (ep * KSG_NCAND + lane) * 6;
-          const int64_t capc = (int64_t)cs[0], capm = (int64_t)cs[1], usec = (int64_t)cs[2], usem = (int64_t)cs[3];
-          const double invc = __longlong_as_double((long long)cs[4]), invm = __longlong_as_double((long long)cs[5]);
-          const int64_t nowc = (int64_t)((uint64_t)usec + c_dlc + (uint64_t)ppv.req_c);
-          const int64_t nowm = (int64_t)((uint64_t)usem + c_dlm + (uint64_t)ppv.req_m);
-          if (res_on && !pv.zero_req)  // PodFitsResources (predicates.go:127-145)
-            xd = !((capc == 0 || capc - nowc >= pv.req_c) && (capm == 0 || capm - nowm >= pv.req_m));
-          if (d.w_lr) {  // LeastRequested (priorities.go:43-76): now against the snapshot
-            const int32_t lr_now = lr_win(nowc + pv.req_c, capc, invc) + lr_win(nowm + pv.req_m, capm, invm);
-            const int32_t lr_snap = lr_win(usec + pv.req_c, capc, invc) + lr_win(usem + pv.req_m, capm, invm);
-            xd |= (lr_now >> 1) != (lr_snap >> 1);
-          }
-        }
-        // PodFitsPorts / NoDiskConflict: pod i's keys against the slot's keys and pod i-1's
-        if (pv.nk) {
-          uint32_t mbk = c_bnk;
-#pragma unroll
-          for (int sh = 1; sh < 8; sh <<= 1) mbk = max(mbk, (uint32_t)__shfl_xor((int)mbk, sh, 64));
-          mbk = (uint32_t)__builtin_amdgcn_readfirstlane((int)mbk);
-          for (uint32_t b = 0; b < pv.nk; ++b) {
-            const bool on = b < pv.n_ports ? ports_on : disk_on;
-            if (!on) continue;
-            const uint32_t kb = (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b));
-            for (uint32_t q = 0; q < pnk; ++q)
-              xd |= have && (uint32_t)__builtin_amdgcn_readlane((int)prec, (int)(WS_IDS + q)) == kb;
-            for (uint32_t a = 0; a < mbk; ++a)
-              xd |= have && a < c_bnk && L_cl[(size_t)c_slot * KSG_CL_W + KSG_CL_KEY + a] == kb;
-          }
-        }
-        // ServiceSpreading under an unchanged maxCount, and commit i-1's service flags
-        if (s >= 0) {
-          uint32_t mbs = c_bns;
-#pragma unroll
-          for (int sh = 1; sh < 8; sh <<= 1) mbs = max(mbs, (uint32_t)__shfl_xor((int)mbs, sh, 64));
-          mbs = (uint32_t)__builtin_amdgcn_readfirstlane((int)mbs);
-          uint32_t x_cnt_s = p_s_cnt;
-          for (uint32_t a = 0; a < mbs; ++a)
-            x_cnt_s += (have && a < c_bns && L_cl[(size_t)c_slot * KSG_CL_W + KSG_CL_SV + a] == (uint32_t)s) ? 1u : 0u;
-          if (have && x_cnt_s) {
-            // s's snapshot count on the candidate: staged with pod i-1's services, else from L2
-            const int32_t x_snapc = (p_s_cnt && p_staged)
-                                        ? r_csv[(ep * KSG_NCAND + lane) * KSG_SLOT_SVCS + p_s_first]
-                                        : gld(d.svc_cnt + (size_t)s * d.n_nodes + d.lo + candv);
-            if (spread_on)
-              xd |= frac10_f32((int64_t)pv.smax - x_snapc - (int32_t)x_cnt_s, pv.smax) !=
-                    frac10_f32((int64_t)pv.smax - x_snapc, pv.smax);
-            if (p_s_cnt) {  // commit i-1, a pod of service s: maxCount rises / first peer
-              flag = spread_on && x_snapc + (int32_t)x_cnt_s > pv.smax;
-              if (aff_on && peer0 == -1 && !((L_peerset[s >> 5] >> (s & 31)) & 1u)) flag = true;
-            }
-          }
-        }
-        pre = (uint32_t)(__ballot(have && xd) & 63ULL) | ((uint32_t)(__ballot(have && flag) & 63ULL) << 8);
-      }
-      if (lane == 0) {
-        ctl->xpre[par] = pre;
-        st_rel(&ctl->xpre_seq, i + 1);
-      }
       for (uint32_t spin = 0;; ++spin) {  // pod i-1's node drawn, or the end
         const uint32_t xn = ld_u(&ctl->xn_seq), st = ld_u(&ctl->stop);
         if (xn >= i) break;
@@ -1019,10 +1023,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       uint32_t res = 0;
       const uint32_t xv = i ? __builtin_amdgcn_readfirstlane(L_xn[i - 1]) : ~0u;
       const uint32_t xnode = xv == ~0u ? ~0u : xv & 0x0fffffffu, xcid = xv == ~0u ? KSG_NO_CAND : xv >> 28;
-      // (a candidate's verdict was posted with the pre-verdicts: no check on the chain)
-      const bool pre_done = !XS && xcid < KSG_NCAND;
-      const bool do_check =
-          !pre_done && xnode != ~0u && !__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE;
+      const bool do_check = xnode != ~0u && !__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE;
       const uint32_t xw = d.lo + (do_check ? xnode : 0u);
       // x's snapshot: staged for a candidate (LDS), else from L2 (in flight over
       // the bookkeeping below)
@@ -1075,8 +1076,10 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         const int64_t reqv = rl ? pv.req_m : pv.req_c;
         const int64_t nowv = (int64_t)((uint64_t)usev + (rl ? dlm : dlc));  // requested total now
         bool xd = false, flag_x = false;
+        bool xu = false;  // x no longer fits the pod (resources, keys, extended resources)
+        int32_t x_snapc = 0;
         if (res_on && !pv.zero_req)  // PodFitsResources: lanes 0 and 1
-          xd = (__ballot(lane < 2 && !(capv == 0 || capv - nowv >= reqv)) & 3ULL) != 0;
+          xu = xd = (__ballot(lane < 2 && !(capv == 0 || capv - nowv >= reqv)) & 3ULL) != 0;
         if (d.w_lr) {  // LeastRequested: one term per lane
           const int32_t lrv = lr_win((lane < 2 ? nowv : usev) + reqv, capv, invv);
           const int32_t lr_now = __builtin_amdgcn_readlane(lrv, 0) + __builtin_amdgcn_readlane(lrv, 1);
@@ -1086,7 +1089,6 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         if (x_cnt_s) {
           // s's snapshot count on x: staged with pod i-1's services when pod i-1 is
           // a pod of s, else from L2 (the checkers may not have written it yet)
-          int32_t x_snapc;
           if (prev_ents && p_staged && xcid < KSG_NCAND)
             x_snapc = r_csv[(ep * KSG_NCAND + xcid) * KSG_SLOT_SVCS + (uint32_t)__builtin_ctzll(prev_ents) - KSG_CL_SV - bns];
           else
@@ -1108,16 +1110,75 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
             const bool on = b < pv.n_ports ? ports_on : disk_on;
             hit |= on && kt < xnk && xcl == (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b));
           }
-          xd |= __ballot(hit) != 0;
+          const bool kh = __ballot(hit) != 0;
+          xd |= kh;
+          xu |= kh;
         }
         if (xk_chk && (xkinds & pv.xm)) {  // (extensions) extended resources, lane r: kind r
           const int32_t q = __shfl((int)rec, (int)(WS_XREQ + (lane & 3)), 64);  // (a per-lane source: not readlane)
           const int32_t dl = (lane & 3) == 0 ? xdl[0] : (lane & 3) == 1 ? xdl[1] : (lane & 3) == 2 ? xdl[2] : xdl[3];
-          xd |= (__ballot(lane < 4 && q > 0 && xhv - dl < q) & 15ULL) != 0;
+          const bool xh = (__ballot(lane < 4 && q > 0 && xhv - dl < q) & 15ULL) != 0;
+          xd |= xh;
+          xu |= xh;
         }
         res = (xd ? 1u : 0u) | (flag_x ? 2u : 0u);
+        if (esc) {
+          // (extension scores) x re-scored as the checkers do a slot: bit 0 drop (a T0 node unfit
+          // or below M0), 4 rose above M0 (xsig), 8 joined T0, 16 normalisation stop
+          const uint64_t t0w = r_t0[(size_t)e * P * 64 + (xnode >> 6)];
+          const bool in_t0 = (t0w >> (xnode & 63)) & 1ULL;
+          const int64_t capc = (int64_t)readlane64((uint64_t)capv, 0), capm = (int64_t)readlane64((uint64_t)capv, 1);
+          const int64_t usec = (int64_t)readlane64((uint64_t)usev, 0), usem = (int64_t)readlane64((uint64_t)usev, 1);
+          const double invc = __longlong_as_double((long long)readlane64((uint64_t)__double_as_longlong(invv), 0));
+          const double invm = __longlong_as_double((long long)readlane64((uint64_t)__double_as_longlong(invv), 1));
+          const int64_t nowc = (int64_t)((uint64_t)usec + dlc), nowm = (int64_t)((uint64_t)usem + dlm);
+          const bool sp = spread_on && s >= 0 && pv.smax > 0;
+          const int64_t fr_snap = (sp && x_cnt_s) ? frac10_f32((int64_t)pv.smax - x_snapc, pv.smax) : 0;
+          const int64_t fr_now = (sp && x_cnt_s) ? frac10_f32((int64_t)pv.smax - x_snapc - (int32_t)x_cnt_s, pv.smax) : 0;
+          const int64_t dl = es_delta(d, pv.req_c, pv.req_m, capc, capm, invc, invm, usec, usem, nowc, nowm, fr_snap,
+                                      fr_now);
+          const uint64_t psoft = r_hdr[e].psoft;
+          const int32_t tmx = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].tmax);
+          const uint64_t xntm = d.ntaint ? gld(d.ntaint + xw) : 0ULL;
+          const int32_t soft = __popcll(xntm & psoft);
+          const bool at_max = d.w_taint != 0 && tmx > 0 && soft == tmx;
+          uint32_t es = 0;
+          int32_t sig = 0;
+          bool edrop = false;
+          if (in_t0) {
+            if (xu) {
+              edrop = true;
+              if (at_max) es |= 16u;
+            } else if (dl < 0) {
+              edrop = true;
+            } else if (dl > 0) {
+              es |= 4u;
+              sig = (int32_t)(m0 + dl);
+            }
+          } else if (dl > 0 || (xu && at_max)) {
+            const uint64_t fw = gld(reinterpret_cast<const uint64_t*>(x.buf + x.efit_off) + (size_t)i * x.ostride + (xnode >> 6));
+            if ((fw >> (xnode & 63)) & 1ULL) {  // fitted at the snapshot
+              if (xu) {
+                es |= 16u;
+              } else {
+                const int32_t cs = x_cnt_s ? x_snapc : (sp ? gld(d.svc_cnt + (size_t)s * d.n_nodes + xw) : 0);
+                const int64_t frs = sp ? frac10_f32((int64_t)pv.smax - cs, pv.smax) : 10;
+                const int32_t xsst = d.has_static_score ? (int32_t)gld(d.static_score + xw) : 0;
+                const int64_t now =
+                    es_snap_score(d, pv.req_c, pv.req_m, capc, capm, invc, invm, usec, usem, frs, xsst, soft, tmx) + dl;
+                if (now > m0) {
+                  es |= 4u;
+                  sig = (int32_t)now;
+                } else if (now == m0) {
+                  es |= 8u;
+                }
+              }
+            }
+          }
+          res = (edrop ? 1u : 0u) | (flag_x ? 2u : 0u) | es;
+          if (lane == 0) ctl->xsig[par] = sig;
+        }
       }
-      if (pre_done) res = ((pre >> xcid) & 1u) | (((pre >> (8 + xcid)) & 1u) << 1);
       if (lane == 0 && !(xpt & 1u)) {
         ctl->xres[par] = res;
         if constexpr (STAMP) ctl->t_x = (uint32_t)__builtin_amdgcn_s_memtime();
@@ -1172,7 +1233,6 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   int64_t dc0 = 0, dm0 = 0, dc1 = 0, dm1 = 0;  // their window deltas (current through the last commit)
   bool have_x = false;                   // commit i-1's node x (and its slot)
   uint32_t xnode = 0, xslot = 0;
-  uint32_t x_cidx = KSG_NO_CAND;         // x's candidate index (< 6: the x-checker pre-posted its verdict)
   uint64_t t_last = 0, t_acc = 0;
 #define KSG_STAMPP(k)                                        \
   if constexpr (STAMP) {                                     \
@@ -1258,13 +1318,11 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     // verdict on commit i-1's node
     bool hung = false;
     for (uint32_t spin = 0;; ++spin) {
-      const uint32_t xs = ld_rlx(&ctl->xseq), xp = ld_rlx(&ctl->xpre_seq), hg = ld_rlx(&ctl->hang);
+      const uint32_t xs = ld_rlx(&ctl->xseq), hg = ld_rlx(&ctl->hang);
       uint32_t cs = ld_rlx(&ctl->chk_seq[0]);
 #pragma unroll
       for (int c = 1; c < KSG_RES_NCHK; ++c) cs = min(cs, ld_rlx(&ctl->chk_seq[c]));
-      // x's verdict: pre-posted when x is a candidate (or there is no x), else the x-checker's
-      const bool x_ok = xs >= i + 1 || (xp >= i + 1 && (!have_x || (!XS && x_cidx < KSG_NCAND)));
-      if ((cs >= i + 1 && x_ok) || (xpt & 8u)) break;
+      if ((cs >= i + 1 && xs >= i + 1) || (xpt & 8u)) break;
       if (spin > 16 * KSG_SPIN_LIMIT || hg) {
         hung = true;
         break;
@@ -1281,15 +1339,12 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     // one round of LDS reads: drop counts and masks, the drops' positions, the
     // verdict, the service flag word
     const uint32_t cc0 = ctl->chk_cnt[0][par], cc1 = ctl->chk_cnt[1][par];
-    const uint32_t xpre = __builtin_amdgcn_readfirstlane(ctl->xpre[par]);
-    const uint32_t xres = (!XS && have_x && x_cidx < KSG_NCAND)
-                              ? ((xpre >> x_cidx) & 1u) | (((xpre >> (8 + x_cidx)) & 1u) << 1)
-                              : __builtin_amdgcn_readfirstlane(ctl->xres[par]);
+    const uint32_t xres = __builtin_amdgcn_readfirstlane(ctl->xres[par]);
     const uint32_t fw = s >= 0 ? L_flag[s >> 5] : 0u;
-    const uint64_t msk0 = ((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[0][par][1]) << 32) |
-                          (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[0][par][0]);
-    const uint64_t msk1 = ((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[1][par][1]) << 32) |
-                          (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[1][par][0]);
+    uint64_t msk0 = ((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[0][par][1]) << 32) |
+                    (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[0][par][0]);
+    uint64_t msk1 = ((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[1][par][1]) << 32) |
+                    (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[1][par][0]);
     const uint32_t dp0 = L_dpos[par * KSG_MAX_SLOTS + lane];
     const uint32_t dp1 = L_dpos[par * KSG_MAX_SLOTS + 64 + lane];
     if (s >= 0 && (spread_on || aff_on) && ((xres & 2u) || ((__builtin_amdgcn_readfirstlane(fw) >> (s & 31)) & 1u))) {
@@ -1301,17 +1356,137 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     // x counts as a new drop iff it is a snapshot tie whose slot the checkers
     // kept (a new slot: they have not seen it)
     const bool x_kept = !(((xslot < 64 ? msk0 : msk1) >> (xslot & 63)) & 1ULL);
-    const bool x_drop = have_x && (xres & 1u) && ((t0x >> (xnode & 63)) & 1ULL) && x_kept;
-    const uint32_t dropped = (xpt & 4u) ? 0u : __builtin_amdgcn_readfirstlane(cc0) + __builtin_amdgcn_readfirstlane(cc1) + (x_drop ? 1u : 0u);
-    if (dropped >= k0) {
+    bool x_drop = have_x && (xres & 1u) && ((t0x >> (xnode & 63)) & 1ULL) && x_kept;
+    uint32_t dropped = (xpt & 4u) ? 0u : __builtin_amdgcn_readfirstlane(cc0) + __builtin_amdgcn_readfirstlane(cc1) + (x_drop ? 1u : 0u);
+    // (extension scores) risen slots (a score above M0: the ties are among them) and joined
+    // ones (non-T0 nodes now at M0: the ties are T0 minus the drops plus them); x's verdict
+    // replaces the checkers' for its slot (a BalancedAllocation score moves both ways)
+    uint64_t rm0 = 0, rm1 = 0, jm0 = 0, jm1 = 0;
+    uint32_t xpos = 0;
+    if (esc) {
+      const uint64_t xb0 = (have_x && xslot < 64) ? 1ULL << (xslot & 63) : 0ULL;
+      const uint64_t xb1 = (have_x && xslot >= 64) ? 1ULL << (xslot & 63) : 0ULL;
+      rm0 = (((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_rmsk[0][par][1]) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_rmsk[0][par][0])) & ~xb0;
+      rm1 = (((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_rmsk[1][par][1]) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_rmsk[1][par][0])) & ~xb1;
+      jm0 = (((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_jmsk[0][par][1]) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_jmsk[0][par][0])) & ~xb0;
+      jm1 = (((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_jmsk[1][par][1]) << 32) |
+             (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_jmsk[1][par][0])) & ~xb1;
+      msk0 &= ~xb0;
+      msk1 &= ~xb1;
+      const uint32_t nst = __builtin_amdgcn_readfirstlane(ctl->chk_nstop[0][par] | ctl->chk_nstop[1][par]);
+      if (nst || (have_x && (xres & 16u))) {
+        resolved = i;  // a committed node at the pod's TaintToleration max no longer fits
+        reason = KSG_STOP_SERVICE;
+        break;
+      }
+      x_drop = have_x && (xres & 1u);
+      if (have_x && (xres & 4u)) (xslot < 64 ? rm0 : rm1) |= 1ULL << (xslot & 63);
+      if (have_x && (xres & 8u)) (xslot < 64 ? jm0 : jm1) |= 1ULL << (xslot & 63);
+      xpos = xpos0 + (uint32_t)__popcll(t0x & ((1ULL << (xnode & 63)) - 1ULL));
+      dropped = (uint32_t)__popcll(msk0) + (uint32_t)__popcll(msk1) + (x_drop ? 1u : 0u);
+    }
+    const uint32_t n_add = (uint32_t)__popcll(jm0) + (uint32_t)__popcll(jm1);
+    if (dropped >= k0 && n_add == 0 && (rm0 | rm1) == 0) {
       resolved = i;  // every snapshot tie got worse: needs a fresh snapshot
       reason = KSG_STOP_EXHAUSTED;
       break;
     }
+    // T0's tp-th node ascending: its row (row prefixes, lane q < P), its word (the
+    // row's word prefixes) and its bit (mbcnt rank)
+    auto t0_node = [&](uint32_t tp) -> uint32_t {
+      const uint32_t qs = (uint32_t)__builtin_ctzll(__ballot(lane < P && lp_ex <= tp && tp < lp_in));
+      const uint32_t loc = tp - (uint32_t)__builtin_amdgcn_readlane((int)lp_ex, (int)qs);
+      const uint64_t w = t0e[qs * 64 + lane];
+      const uint32_t wpq = r_wp[(size_t)e * P * 64 + qs * 64 + lane];
+      const uint32_t ls = (uint32_t)__builtin_ctzll(__ballot(wpq <= loc && loc < wpq + (uint32_t)__popcll(w)));
+      const uint64_t ws = readlane64(w, (int)ls);
+      const uint32_t lw = loc - (uint32_t)__builtin_amdgcn_readlane((int)wpq, (int)ls);
+      const uint32_t rank =
+          __builtin_amdgcn_mbcnt_hi((uint32_t)(ws >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ws, 0u));
+      const uint32_t bsel = (uint32_t)__builtin_ctzll(__ballot(((ws >> lane) & 1ULL) && rank == lw));
+      return (qs * 64 + ls) * 64 + bsel;
+    };
+    // the least fixed point tp = t + #(drop positions <= tp): the t-th node of T0 minus the drops
+    auto t0_minus_drops = [&](uint32_t t) -> uint32_t {
+      const uint32_t d0 = ((msk0 >> lane) & 1ULL) ? dp0 : ~0u;
+      const uint32_t d1 = ((msk1 >> lane) & 1ULL) ? dp1 : ~0u;
+      const uint32_t xp = x_drop ? (esc ? xpos : xpos0 + (uint32_t)__popcll(t0x & ((1ULL << (xnode & 63)) - 1ULL))) : ~0u;
+      uint32_t tp = t;
+      for (;;) {
+        const uint32_t cnt = (uint32_t)__popcll(__ballot(d0 <= tp)) + (uint32_t)__popcll(__ballot(d1 <= tp)) +
+                             (xp <= tp ? 1u : 0u);
+        if (t + cnt == tp) break;
+        tp = t + cnt;
+      }
+      return tp;
+    };
+    auto r_draw = [&]() -> uint64_t {  // the pod's Int63 draw (staged)
+      return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(r_hdr[e].r >> 32)) << 32) |
+             (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r_hdr[e].r);
+    };
     // ---- selection: k live ties, the ix-th in descending rank = the (k-1-ix)-th ascending
     const uint32_t k = k0 - dropped;
     uint32_t woff;
-    if (dropped == 0) {
+    if (esc && (rm0 | rm1) != 0) {
+      // risers: M* = their best score, the ties the risers at it, ix-th from the top by rank
+      const int32_t sg0 = L_sig[par * KSG_MAX_SLOTS + lane], sg1 = L_sig[par * KSG_MAX_SLOTS + 64 + lane];
+      const int32_t xsg = (int32_t)__builtin_amdgcn_readfirstlane(ctl->xsig[par]);
+      const bool x_in0 = have_x && (xres & 4u) && xslot < 64 && lane == (xslot & 63);
+      const bool x_in1 = have_x && (xres & 4u) && xslot >= 64 && lane == (xslot & 63);
+      const int32_t v0 = ((rm0 >> lane) & 1ULL) ? (x_in0 ? xsg : sg0) : KSG_S32_NONE;
+      const int32_t v1 = ((rm1 >> lane) & 1ULL) ? (x_in1 ? xsg : sg1) : KSG_S32_NONE;
+      const int32_t ms = wave_total_max(max(v0, v1));
+      uint64_t tm0 = __ballot(((rm0 >> lane) & 1ULL) && v0 == ms), tm1 = __ballot(((rm1 >> lane) & 1ULL) && v1 == ms);
+      const uint32_t ks = (uint32_t)__popcll(tm0) + (uint32_t)__popcll(tm1);
+      uint32_t ix = umod64_32(r_draw(), ks);
+      int32_t top = -1;
+      for (;;) {  // the ix-th tie from the top (HostPriorityList: score desc, host desc)
+        const int32_t c0 = ((tm0 >> lane) & 1ULL) ? (int32_t)cn0 : -1, c1 = ((tm1 >> lane) & 1ULL) ? (int32_t)cn1 : -1;
+        top = wave_total_max(max(c0, c1));
+        if (ix == 0) break;
+        --ix;
+        tm0 &= ~__ballot(cn0 == (uint32_t)top);
+        tm1 &= ~__ballot(cn1 == (uint32_t)top);
+      }
+      woff = (uint32_t)top;
+    } else if (esc && n_add != 0) {
+      // joiners: the ties are T0 minus the drops plus the joined nodes (each between the
+      // T0 nodes around its rank: ap = the T0 nodes below it)
+      const bool x_j0 = have_x && (xres & 8u) && xslot < 64 && lane == (xslot & 63);
+      const bool x_j1 = have_x && (xres & 8u) && xslot >= 64 && lane == (xslot & 63);
+      const uint32_t ap0 = ((jm0 >> lane) & 1ULL) ? (x_j0 ? xpos : dp0) : ~0u;
+      const uint32_t ap1 = ((jm1 >> lane) & 1ULL) ? (x_j1 ? xpos : dp1) : ~0u;
+      const uint32_t d0 = ((msk0 >> lane) & 1ULL) ? dp0 : ~0u, d1 = ((msk1 >> lane) & 1ULL) ? dp1 : ~0u;
+      const uint32_t xdp = x_drop ? xpos : ~0u;
+      const uint32_t kk = k0 - dropped + n_add;
+      const uint32_t t = kk - 1 - umod64_32(r_draw(), kk);
+      woff = ~0u;
+      // a joined node with exactly t ties below it
+      for (uint64_t mm = jm0, mh = jm1; (mm | mh) && woff == ~0u;) {
+        const bool lo = mm != 0;
+        const uint32_t l = (uint32_t)__builtin_ctzll(lo ? mm : mh);
+        if (lo) mm &= mm - 1;
+        else mh &= mh - 1;
+        const uint32_t pa = (uint32_t)__builtin_amdgcn_readlane((int)(lo ? ap0 : ap1), (int)l);
+        const uint32_t na = (uint32_t)__builtin_amdgcn_readlane((int)(lo ? cn0 : cn1), (int)l);
+        const uint32_t bd = (uint32_t)__popcll(__ballot(d0 < pa)) + (uint32_t)__popcll(__ballot(d1 < pa)) +
+                            (xdp < pa ? 1u : 0u);
+        const uint32_t ba = (uint32_t)__popcll(__ballot(ap0 != ~0u && (ap0 < pa || (ap0 == pa && cn0 < na)))) +
+                            (uint32_t)__popcll(__ballot(ap1 != ~0u && (ap1 < pa || (ap1 == pa && cn1 < na))));
+        if (pa - bd + ba == t) woff = na;
+      }
+      // else a T0 node: with j joined nodes below it, the (t - j)-th of T0 minus the drops
+      for (uint32_t j = 0; woff == ~0u && j <= n_add && j <= t; ++j) {
+        const uint32_t tp = t0_minus_drops(t - j);
+        if (tp >= k0) continue;
+        const uint32_t ca = (uint32_t)__popcll(__ballot(ap0 != ~0u && ap0 <= tp)) +
+                            (uint32_t)__popcll(__ballot(ap1 != ~0u && ap1 <= tp));
+        if (ca == j) woff = t0_node(tp);
+      }
+    } else if (dropped == 0) {
       woff = (uint32_t)pred;  // staged by the producer
     } else if (dropped <= 2) {
       // one or two drops: the node is one of the producer's candidates for that
@@ -1347,32 +1522,9 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       if (dropped < 64) {
         ix = (uint32_t)__builtin_amdgcn_readlane((int)rmod, (int)dropped);
       } else {
-        const uint64_t r = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(r_hdr[e].r >> 32)) << 32) |
-                           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r_hdr[e].r);
-        ix = umod64_32(r, k);
+        ix = umod64_32(r_draw(), k);
       }
-      const uint32_t t = k - 1 - ix;
-      const uint32_t d0 = ((msk0 >> lane) & 1ULL) ? dp0 : ~0u;
-      const uint32_t d1 = ((msk1 >> lane) & 1ULL) ? dp1 : ~0u;
-      const uint32_t xpos = x_drop ? xpos0 + (uint32_t)__popcll(t0x & ((1ULL << (xnode & 63)) - 1ULL)) : ~0u;
-      uint32_t tp = t;
-      for (;;) {
-        const uint32_t cnt = (uint32_t)__popcll(__ballot(d0 <= tp)) + (uint32_t)__popcll(__ballot(d1 <= tp)) +
-                             (xpos <= tp ? 1u : 0u);
-        if (t + cnt == tp) break;
-        tp = t + cnt;
-      }
-      const uint32_t qs = (uint32_t)__builtin_ctzll(__ballot(lane < P && lp_ex <= tp && tp < lp_in));
-      const uint32_t loc = tp - (uint32_t)__builtin_amdgcn_readlane((int)lp_ex, (int)qs);
-      const uint64_t w = t0e[qs * 64 + lane];
-      const uint32_t wpq = r_wp[(size_t)e * P * 64 + qs * 64 + lane];
-      const uint32_t ls = (uint32_t)__builtin_ctzll(__ballot(wpq <= loc && loc < wpq + (uint32_t)__popcll(w)));
-      const uint64_t ws = readlane64(w, (int)ls);
-      const uint32_t lw = loc - (uint32_t)__builtin_amdgcn_readlane((int)wpq, (int)ls);
-      const uint32_t rank =
-          __builtin_amdgcn_mbcnt_hi((uint32_t)(ws >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ws, 0u));
-      const uint32_t bsel = (uint32_t)__builtin_ctzll(__ballot(((ws >> lane) & 1ULL) && rank == lw));
-      woff = (qs * 64 + ls) * 64 + bsel;
+      woff = t0_node(t0_minus_drops(k - 1 - ix));
     }
     if (woff >= d.hi - d.lo) {  // (never: inconsistent prefixes or drop positions; the host fails the batch)
       resolved = i;
@@ -1450,7 +1602,6 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     have_x = true;
     xnode = woff;
     xslot = slot;
-    x_cidx = cidx;
     ++n_draws;
     KSG_STAMPP(5)
   }
@@ -1484,6 +1635,8 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   for (uint32_t t = lane; t < resolved; t += 64) out[t] = L_out[t];
+  if (esc && x.tmax)  // (extension scores) the TaintToleration maxima start at 0 for the next window's count pass
+    for (uint32_t t = lane; t < wcap; t += 64) x.tmax[t] = 0;
   if (XS) {
     // (extensions) the window's extended resource requests into the node state
     // (the checkers wrote cpu / memory back; these live in no slot)
@@ -1565,7 +1718,7 @@ template <int PP, bool ST>
 static hipError_t win_plain_launch(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run, const KsgWinSum* sums,
                                    const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
   // (extensions) extended resources on the slots
-  if (x.exts != nullptr && (d.ext_filters & KSG_EXT_SCALAR) && d.n_scalar > 0)
+  if (x.exts != nullptr && (((d.ext_filters & KSG_EXT_SCALAR) && d.n_scalar > 0) || x.esc))
     return win_plain_launch_x<PP, ST, true>(d, wcap, lds, run, sums, x, rng, out, st);
   return win_plain_launch_x<PP, ST, false>(d, wcap, lds, run, sums, x, rng, out, st);
 }

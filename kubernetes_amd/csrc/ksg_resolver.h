@@ -65,6 +65,9 @@ struct alignas(16) RingHdr {
   uint32_t pad;
   int64_t cap_c, cap_m, used_c, used_m;  // snapshot of pred
   double inv_c, inv_m;                   // 10 / capacity of pred
+  uint64_t psoft;                        // (extension scores) the pod's untolerated soft taints (mask)
+  int32_t tmax;                          // ... its TaintToleration max over its filtered nodes
+  uint32_t pad3;
 };
 struct alignas(16) RingSvc {  // per service entry t of the pod (t < n_svcs)
   int32_t cnt[KSG_SLOT_SVCS];   // svc_cnt[sv][pred] at the snapshot
@@ -387,7 +390,42 @@ struct RegSlot {
   uint32_t xk;             // (extensions) extended resource kinds the window's commits requested here
   int32_t xh[4];           // (extensions) allocatable - requested at the snapshot, clamped to int32
   int32_t xdl[4];          // (extensions) the window's requests here (<= 4096 x 2^16)
+  int32_t sst;             // (extension scores) the node's static score
+  uint64_t ntm;            // (extension scores) the node's taints (mask)
 };
+
+// Extension scores on the window path (BalancedAllocation can RISE on a committed
+// node; TaintToleration's term is static per (pod, node) while its normalisation
+// max holds): the change of a committed node's score for a pod between the
+// snapshot and now. The static and TaintToleration terms cancel; LeastRequested,
+// ServiceSpreading (frac_* = the spreading scores) and BalancedAllocation move.
+__device__ __forceinline__ int64_t es_delta(const KsgDev& d, int64_t req_c, int64_t req_m, int64_t cap_c,
+                                            int64_t cap_m, double inv_c, double inv_m, int64_t snp_c, int64_t snp_m,
+                                            int64_t now_c, int64_t now_m, int64_t frac_snap, int64_t frac_now) {
+  int64_t dl = 0;
+  const int64_t tcn = (int64_t)((uint64_t)now_c + (uint64_t)req_c), tmn = (int64_t)((uint64_t)now_m + (uint64_t)req_m);
+  const int64_t tcs = (int64_t)((uint64_t)snp_c + (uint64_t)req_c), tms = (int64_t)((uint64_t)snp_m + (uint64_t)req_m);
+  if (d.w_lr)
+    dl += (int64_t)d.w_lr * ((int64_t)((lr_win(tcn, cap_c, inv_c) + lr_win(tmn, cap_m, inv_m)) >> 1) -
+                             (int64_t)((lr_win(tcs, cap_c, inv_c) + lr_win(tms, cap_m, inv_m)) >> 1));
+  if (d.w_spread) dl += (int64_t)d.w_spread * (frac_now - frac_snap);
+  if (d.w_bal) dl += (int64_t)d.w_bal * (balanced_score(tcn, cap_c, tmn, cap_m) - balanced_score(tcs, cap_c, tms, cap_m));
+  return dl;
+}
+// ... and a node's whole score for the pod at the snapshot (phase A's sum: static,
+// LeastRequested, ServiceSpreading, BalancedAllocation, TaintToleration)
+__device__ __forceinline__ int64_t es_snap_score(const KsgDev& d, int64_t req_c, int64_t req_m, int64_t cap_c,
+                                                 int64_t cap_m, double inv_c, double inv_m, int64_t snp_c,
+                                                 int64_t snp_m, int64_t frac_snap, int32_t sst, int32_t soft,
+                                                 int32_t tmax) {
+  int64_t s = sst;
+  const int64_t tcs = (int64_t)((uint64_t)snp_c + (uint64_t)req_c), tms = (int64_t)((uint64_t)snp_m + (uint64_t)req_m);
+  if (d.w_lr) s += (int64_t)d.w_lr * ((lr_win(tcs, cap_c, inv_c) + lr_win(tms, cap_m, inv_m)) >> 1);
+  if (d.w_spread) s += (int64_t)d.w_spread * frac_snap;
+  if (d.w_bal) s += (int64_t)d.w_bal * balanced_score(tcs, cap_c, tms, cap_m);
+  if (d.w_taint) s += (int64_t)d.w_taint * (d.ntaint ? taint_score(soft, tmax) : 10);
+  return s;
+}
 // allocatable - requested of an extended resource at the snapshot, clamped to
 // int32: with a window's deltas <= 2^28 and requests <= 2^16 every fit test
 // h - delta >= request decides as the unclamped one does

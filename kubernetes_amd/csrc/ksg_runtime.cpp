@@ -44,7 +44,8 @@ hipError_t ksg_launch_scan(int R, bool anti, const KsgDev& d, const ksg_pod* pod
 hipError_t ksg_launch_win_eval(const KsgDev& d, int mode, const ksg_pod* batch, const uint32_t* ids,
                                const KsgWinRun* run, uint32_t wcap, KsgWinSum* sums, uint64_t* wbits, int32_t* wmax,
                                uint32_t ostride, int32_t* dcnt, uint64_t* wfit, int32_t* dmb, uint64_t* wbz,
-                               uint32_t dz, hipStream_t st, const ksg_pod_ext* exts = nullptr);
+                               uint32_t dz, hipStream_t st, const ksg_pod_ext* exts = nullptr,
+                               int32_t* tmax = nullptr, uint64_t* psoft = nullptr);
 hipError_t ksg_launch_zonemap(uint32_t n_nodes, const int32_t* anti_domain, uint32_t d0, uint32_t nw,
                               uint64_t* zmap, hipStream_t st);
 hipError_t ksg_launch_win_t0(const KsgDev& d, uint32_t wcap, const KsgWinRun* run, const KsgWinXchg& x,
@@ -205,6 +206,9 @@ struct ksg_ctx {
   int32_t* d_dmb = nullptr;      // [W][D+1] re-rank: best score without the anti term per domain row
   uint64_t* d_zmap = nullptr;    // [D+1][nw] re-rank: nodes of each domain row (cluster allocation)
   size_t win_cap = 0, xsend_cap = 0, xrecv_cap = 0, dcnt_cap = 0, dmb_cap = 0;
+  int32_t* d_etmax = nullptr;    // [W] extension scores: TaintToleration max per window pod (count pass)
+  uint64_t* d_epsoft = nullptr;  // [W] ... the pods' untolerated soft taints as masks
+  size_t etmax_cap = 0, epsoft_cap = 0;
   KsgWinRun* d_run = nullptr;      // progress of the window chain (device)
   KsgWinRun* h_run = nullptr;      // pinned host copy
   uint32_t last_stats[4] = {0, 0, 0, 0};  // windows, stops (service scalar), stops (ties exhausted)
@@ -692,14 +696,17 @@ KsgDev full_geometry(const ksg_ctx* c) {
 
 bool use_window(ksg_ctx* c, const ksg_pod* pods, uint32_t n) {
   if (c->window == 0 || c->nw > 32 * 64 || ksg_win_max_window(full_geometry(c)) < 8) return false;
-  // extensions: the filters only (PodToleratesNodeTaints is static per (pod,
-  // node); extended resources only shrink under commits and the resolver
-  // re-checks them on the window's committed nodes like cpu / memory).
-  // TaintToleration and BalancedAllocation scores (the latter can rise on a
-  // committed node), negative requests and requests past 2^16 take the exact
+  // extensions: PodToleratesNodeTaints is static per (pod, node); extended
+  // resources only shrink under commits and the resolver re-checks them on the
+  // window's committed nodes like cpu / memory. With TaintToleration /
+  // BalancedAllocation scores the resolver re-scores the committed nodes (a
+  // BalancedAllocation score can RISE: ksg_plain.hip's risers and joiners); the
+  // TaintToleration term needs the node taints as one mask (max_taints <= 64).
+  // ServiceAntiAffinity, negative requests and requests past 2^16 take the exact
   // kernels.
   if (c->ext_on) {
-    if (c->ext.w_taint_toleration != 0 || c->ext.w_balanced != 0 || anti_on(c) || (c->dev.dbg & 128)) return false;
+    if (anti_on(c) || (c->dev.dbg & 128)) return false;
+    if (c->ext.w_taint_toleration != 0 && !c->dev.ntaint) return false;
     if (c->cur_ext)
       for (uint32_t i = 0; i < n; ++i)
         for (uint32_t r = 0; r < c->ext.n_scalar; ++r)
@@ -1278,7 +1285,7 @@ int ksg_destroy(ksg_ctx* c) {
   void* scratch[] = {c->d_pods, c->d_ids, c->d_fail, c->d_score, c->d_rec_send, c->d_rec_recv, c->d_dpart,
                      c->d_dglobal, c->d_out, c->d_rng, c->d_summary, c->d_patch, c->d_shard_wlo,
                      c->d_winsum, c->d_xsend, c->d_xrecv, c->d_run, c->d_dcnt, c->d_admit, c->d_one,
-                     c->d_t0img, c->d_draws};
+                     c->d_t0img, c->d_draws, c->d_etmax, c->d_epsoft};
   for (void* p : scratch)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -1537,6 +1544,12 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
     d.scalar_cap = scap;
     d.scalar_used = sused;
     d.taintmap = tmap;
+    d.ntaint = nullptr;
+    if (c->ext.max_taints <= 64) {  // (the window path's TaintToleration term: one mask per node)
+      uint64_t* ntm = nullptr;
+      if ((rc = dalloc(c, &ntm, NN, owner))) return rc;
+      d.ntaint = ntm;
+    }
   }
   c->lds = (size_t)d.n_domains_total * sizeof(int32_t);
 
@@ -2030,7 +2043,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       W = std::min(W, std::max<uint32_t>(want, 16u));
     }
     KsgWinXchg x{};
-    x.exts = dext;  // (extensions: the filters; use_window keeps the scores off this path)
+    x.exts = dext;  // (extensions: the filters, and the scores when esc)
     x.ostride = std::max<uint32_t>(c->nwords_max, 1);
     x.wcap = W;
     x.world = (uint32_t)c->world;
@@ -2046,10 +2059,24 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     // (the domain counts are zeroed once here, then by each resolver for the next window)
     x.fit_off = anti ? (uint32_t)fit_off : 0u;
     x.b_off = rr ? (uint32_t)(fit_off + (size_t)W * x.ostride * 8) : 0u;
-    x.blk = ((rr     ? fit_off + (size_t)W * x.ostride * 16
-              : anti ? fit_off + (size_t)W * x.ostride * 8
-                     : (size_t)W * x.ostride * 12) +
+    // extension scores on the plain resolver: the pods' fit bitmaps at the same offset
+    const bool esc = c->ext_on && (c->ext.w_taint_toleration != 0 || c->ext.w_balanced != 0);
+    const bool etm = esc && c->ext.w_taint_toleration != 0;  // (the TaintToleration count pass)
+    x.esc = esc ? 1u : 0u;
+    x.efit_off = esc ? (uint32_t)fit_off : 0u;
+    x.blk = ((rr            ? fit_off + (size_t)W * x.ostride * 16
+              : anti || esc ? fit_off + (size_t)W * x.ostride * 8
+                            : (size_t)W * x.ostride * 12) +
              255) & ~(size_t)255;
+    if (esc) {
+      if ((rc = grow(c, (void**)&c->d_etmax, &c->etmax_cap, W, sizeof(int32_t))) ||
+          (rc = grow(c, (void**)&c->d_epsoft, &c->epsoft_cap, W, sizeof(uint64_t))))
+        return rc;
+      // (zero once here; each resolver zeroes the maxima again for the next window's count pass)
+      HIPCHK(c, hipMemsetAsync(c->d_etmax, 0, (size_t)W * sizeof(int32_t), c->st));
+      x.tmax = c->d_etmax;
+      x.psoft = c->d_epsoft;
+    }
     const size_t dcnt_n = (size_t)W * std::max<uint32_t>(c->D, 1);
     if (anti) {
       if ((rc = grow(c, (void**)&c->d_dcnt, &c->dcnt_cap, dcnt_n, sizeof(int32_t)))) return rc;
@@ -2123,11 +2150,15 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
                                         x.ostride, c->d_dcnt, nullptr, x.dmb, nullptr, x.dz, c->st));
           if (c->xchg && (rc = allreduce_sum_i32(c, c->d_dcnt, c->d_dcnt, (uint32_t)dcnt_n))) return rc;
         }
+        if (etm)  // TaintToleration: each pod's max soft-taint count over its filtered nodes first
+          HIPCHK(c, ksg_launch_win_eval(c->dev, 3, c->d_pods, c->d_ids, c->d_run, W, c->d_winsum, wbits, wmax,
+                                        x.ostride, nullptr, nullptr, nullptr, nullptr, 0, c->st, dext, x.tmax,
+                                        x.psoft));
         HIPCHK(c, ksg_launch_win_eval(c->dev, anti ? 2 : 0, c->d_pods, c->d_ids, c->d_run, W, c->d_winsum, wbits,
                                       wmax, x.ostride, c->d_dcnt,
-                                      anti ? reinterpret_cast<uint64_t*>(c->d_xsend + fit_off) : nullptr, x.dmb,
-                                      rr ? reinterpret_cast<uint64_t*>(c->d_xsend + x.b_off) : nullptr, x.dz,
-                                      c->st, dext));
+                                      (anti || esc) ? reinterpret_cast<uint64_t*>(c->d_xsend + fit_off) : nullptr,
+                                      x.dmb, rr ? reinterpret_cast<uint64_t*>(c->d_xsend + x.b_off) : nullptr, x.dz,
+                                      c->st, dext, x.tmax, x.psoft));
         if (c->xchg && (rc = allgather(c, c->d_xsend, c->d_xrecv, x.blk))) return rc;
         if (plain) HIPCHK(c, ksg_launch_win_t0(full, W, c->d_run, x, c->st));
         if (evk) HIPCHK(c, hipEventRecord(c->wev[2 * k + 1], c->st));
@@ -2473,6 +2504,14 @@ int ksg_set_node_ext(ksg_ctx* c, uint32_t n_nodes, const int64_t* scalar_cap, co
       }
   HIPCHK(c, hipMemcpyAsync(const_cast<uint64_t*>(c->dev.taintmap), tm.data(), tm.size() * 8, hipMemcpyHostToDevice,
                            c->st));
+  if (c->dev.ntaint) {  // the same taints as one mask per node (taint ids < 64)
+    std::vector<uint64_t> ntm(std::max<uint32_t>(n_nodes, 1), 0);
+    if (taint_off && taint_n)
+      for (uint32_t n = 0; n < n_nodes; ++n)
+        for (uint32_t i = 0; i < taint_n[n]; ++i) ntm[n] |= 1ULL << (taint_ids[taint_off[n] + i] & 63);
+    HIPCHK(c, hipMemcpyAsync(const_cast<uint64_t*>(c->dev.ntaint), ntm.data(), ntm.size() * 8, hipMemcpyHostToDevice,
+                             c->st));
+  }
   HIPCHK(c, hipMemsetAsync(c->dev.scalar_used, 0, (size_t)std::max<uint32_t>(c->ext.n_scalar, 1) * NN * 8, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
   c->sc_used.assign((size_t)c->ext.n_scalar * c->N, 0);

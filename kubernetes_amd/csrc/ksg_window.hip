@@ -74,6 +74,9 @@
 #define KSG_WIN_PLAIN 0
 #define KSG_WIN_COUNT 1
 #define KSG_WIN_ANTI 2
+// extensions with TaintToleration scoring: a count pass first, the pod's max count of
+// untolerated PreferNoSchedule taints over its filtered nodes (NormalizeReduce's max)
+#define KSG_WIN_TMAX 3
 // EXT: the extensions' filters (PodToleratesNodeTaints: static per (pod, node);
 // extended resources: allocatable >= used + request, monotone under commits
 // like cpu / memory), MODE PLAIN only
@@ -88,7 +91,9 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
                                                                  uint64_t* __restrict__ wfit,
                                                                  int32_t* __restrict__ dmb,
                                                                  uint64_t* __restrict__ wbz, uint32_t dz,
-                                                                 const ksg_pod_ext* __restrict__ exts) {
+                                                                 const ksg_pod_ext* __restrict__ exts,
+                                                                 int32_t* __restrict__ tmax,
+                                                                 uint64_t* __restrict__ psoft) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (KSG_SC_NT / 64) + (threadIdx.x >> 6));
   const uint32_t p0 = blockIdx.y * KSG_PG;
@@ -129,8 +134,15 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
     xuse[r] = on ? d.scalar_used[(size_t)r * d.n_nodes + n] : 0;
   }
 
+  // extension scores: TaintToleration counts a pod's untolerated soft taints on this lane's
+  // node as popcount(node taint mask & pod soft mask) (taint ids < 64 on this path)
+  const bool tt = EXT && d.w_taint != 0 && d.ntaint != nullptr;
+  const uint64_t ntm = (tt && valid) ? d.ntaint[n] : 0ULL;
+
   // ---- lane j < np: pod p0+j's context and its fit word for this node word
   uint64_t fm = 0;
+  uint64_t ps = 0;   // lane j: pod j's untolerated soft taints (mask)
+  int32_t tmj = 0;   // lane j: its TaintToleration max (score pass)
   int64_t rc = 0, rm = 0;
   int32_t svc = -1, smax = 0, zr = 0;
   PodCtx c;
@@ -150,6 +162,10 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
             xreq[r] = pe.scalar[r];
             xmask |= xreq[r] > 0 ? 1u << r : 0u;
           }
+      if (tt) {
+        for (uint32_t t = 0; t < pe.n_soft; ++t) ps |= 1ULL << (ids[pe.soft_off + t] & 63);
+        if (MODE == KSG_WIN_PLAIN && tmax) tmj = tmax[p0 + lane];
+      }
     }
     if (w == 0) {
       q_n[0] = p.n_ports; q_n[1] = p.n_pds; q_n[2] = p.n_sel; q_n[3] = p.n_svcs;
@@ -273,6 +289,12 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
             if ((uint32_t)r < d.n_scalar && q > 0 && xcap[r] < (int64_t)((uint64_t)xuse[r] + (uint64_t)q)) fit = false;
           }
       }
+      if constexpr (MODE == KSG_WIN_TMAX) {  // the pod's max soft-taint count over its filtered nodes
+        const int32_t soft = fit ? __popcll(ntm & readlane64(ps, j)) : 0;
+        const int32_t mx = wave_total_max(soft);
+        if (lane == 0 && mx > 0) atomicMax(tmax + p0 + j, mx);
+        continue;
+      }
       if constexpr (MODE == KSG_WIN_COUNT) {
         if (dmb) {
           // re-rank: the best score without the anti term per domain row (the
@@ -317,7 +339,7 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
         }
         continue;
       }
-      if constexpr (MODE == KSG_WIN_ANTI) {
+      if (MODE == KSG_WIN_ANTI || (EXT && wfit != nullptr)) {  // (extension scores: non-T0 slots' fit)
         const uint64_t fb = __ballot(fit);
         if (lane == (uint32_t)j) my_fit = fb;
       }
@@ -337,6 +359,17 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
             const int32_t mx = __builtin_amdgcn_readlane(smax, j);
             const int64_t ss = mx > 0 ? frac10_f32((int64_t)mx - cnt[j], mx) : 10;
             s += (int64_t)d.w_spread * ss;
+          }
+          if constexpr (EXT) {  // extension scores (parity unpinned; the exact kernels' terms)
+            if (d.w_bal) {  // BalancedResourceAllocation, float64 op for op
+              const int64_t tc = (int64_t)((uint64_t)usedc + (uint64_t)rcj);
+              const int64_t tm = (int64_t)((uint64_t)usedm + (uint64_t)rmj);
+              s += (int64_t)d.w_bal * balanced_score(tc, capc, tm, capm);
+            }
+            if (tt)  // TaintToleration: NormalizeReduce(10, reverse) over the filtered nodes
+              s += (int64_t)d.w_taint * taint_score(__popcll(ntm & readlane64(ps, j)), __builtin_amdgcn_readlane(tmj, j));
+            else if (d.w_taint)
+              s += (int64_t)d.w_taint * 10;
           }
           base = (int32_t)s;
           if constexpr (MODE == KSG_WIN_ANTI) s += aterm[j];  // (computed above)
@@ -358,7 +391,7 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
       }
     }
   }
-  if constexpr (MODE == KSG_WIN_COUNT) return;
+  if constexpr (MODE == KSG_WIN_COUNT || MODE == KSG_WIN_TMAX) return;
   if (lane < np && has_word) {
     wmax[(size_t)(p0 + lane) * ostride + w] = my_max;
     wbits[(size_t)(p0 + lane) * ostride + w] = my_bits;
@@ -366,7 +399,11 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
       wfit[(size_t)(p0 + lane) * ostride + w] = my_fit;
       if (dmb) wbz[(size_t)(p0 + lane) * ostride + w] = my_bz;
     }
+    if constexpr (EXT)
+      if (wfit) wfit[(size_t)(p0 + lane) * ostride + w] = my_fit;
   }
+  if constexpr (EXT)
+    if (psoft && w == 0 && lane < np) psoft[p0 + lane] = ps;
 
   // ---- the resolver's record of each pod (one wave per pod group)
   if (w == 0) {
@@ -2993,20 +3030,24 @@ static const size_t kWinLdsBudget = 156 * 1024;
 hipError_t ksg_launch_win_eval(const KsgDev& d, int mode, const ksg_pod* batch, const uint32_t* ids,
                                const KsgWinRun* run, uint32_t wcap, KsgWinSum* sums, uint64_t* wbits, int32_t* wmax,
                                uint32_t ostride, int32_t* dcnt, uint64_t* wfit, int32_t* dmb, uint64_t* wbz,
-                               uint32_t dz, hipStream_t st, const ksg_pod_ext* exts) {
+                               uint32_t dz, hipStream_t st, const ksg_pod_ext* exts, int32_t* tmax,
+                               uint64_t* psoft) {
   const uint32_t gx = std::max<uint32_t>(1, (d.nwords + KSG_SC_NT / 64 - 1) / (KSG_SC_NT / 64));
   const bool small = d.nwords < KSG_PG_WORDS;
   const uint32_t pg = small ? KSG_PG_SMALL : KSG_PG_LARGE;
   const dim3 grid(gx, (wcap + pg - 1) / pg);
 #define KSG_EVAL_LAUNCH(M, G)                                                                                    \
   hipLaunchKernelGGL((ksg_win_score_kernel<M, G>), grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, run, wcap, sums, \
-                     wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz, nullptr)
-#define KSG_EVAL_LAUNCH_X(G)                                                                              \
-  hipLaunchKernelGGL((ksg_win_score_kernel<KSG_WIN_PLAIN, G, true>), grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, \
-                     run, wcap, sums, wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz, exts)
-  if (exts) {  // extensions (plain mode only: the host keeps ServiceAntiAffinity off this path)
-    if (small) KSG_EVAL_LAUNCH_X(KSG_PG_SMALL);
-    else KSG_EVAL_LAUNCH_X(KSG_PG_LARGE);
+                     wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz, nullptr, nullptr, nullptr)
+#define KSG_EVAL_LAUNCH_X(M, G)                                                                              \
+  hipLaunchKernelGGL((ksg_win_score_kernel<M, G, true>), grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, \
+                     run, wcap, sums, wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz, exts, tmax, psoft)
+  if (exts && mode == KSG_WIN_TMAX) {  // extensions: the TaintToleration count pass
+    if (small) KSG_EVAL_LAUNCH_X(KSG_WIN_TMAX, KSG_PG_SMALL);
+    else KSG_EVAL_LAUNCH_X(KSG_WIN_TMAX, KSG_PG_LARGE);
+  } else if (exts) {  // extensions (plain mode only: the host keeps ServiceAntiAffinity off this path)
+    if (small) KSG_EVAL_LAUNCH_X(KSG_WIN_PLAIN, KSG_PG_SMALL);
+    else KSG_EVAL_LAUNCH_X(KSG_WIN_PLAIN, KSG_PG_LARGE);
   } else if (mode == KSG_WIN_COUNT) {
     if (small) KSG_EVAL_LAUNCH(KSG_WIN_COUNT, KSG_PG_SMALL);
     else KSG_EVAL_LAUNCH(KSG_WIN_COUNT, KSG_PG_LARGE);
