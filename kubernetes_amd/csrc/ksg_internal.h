@@ -195,12 +195,17 @@ struct KsgWinXchg {
   uint32_t efit_off;
   int32_t* tmax;
   uint64_t* psoft;
+  // ... and the count pass's histogram of the pods' soft-taint counts over their filtered
+  // nodes (int32[wcap][KSG_TBINS]): thist[pod][tmax] nodes hold the max, so the max falls
+  // only once that many committed nodes at it stopped fitting (zeroed like tmax)
+  int32_t* thist;
   uint32_t rr;        // re-rank on (else a service's commit ends the window)
   uint32_t dz;        // domain rows: anti domains + 1 (<= KSG_RR_MAXZ)
   uint32_t b_off;     // byte offset in a block of the best-per-domain bitmaps
   int32_t* dmb;
   const uint64_t* zmap;
 };
+#define KSG_TBINS 65       // soft-taint counts 0..64 (taint ids < 64 on the window path)
 #define KSG_RR_MAXZ 32     // domain rows the re-rank handles (one lane each)
 #define KSG_RR_MAXSVC 4096 // services (an LDS count per service)
 

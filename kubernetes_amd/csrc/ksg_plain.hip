@@ -108,7 +108,7 @@ struct alignas(16) PlCtl {
   // normalisation stop (a slot the pod fitted at its TaintToleration max no longer fits)
   uint32_t chk_rmsk[KSG_RES_NCHK][2][2];
   uint32_t chk_jmsk[KSG_RES_NCHK][2][2];
-  uint32_t chk_nstop[KSG_RES_NCHK][2];
+  uint32_t chk_nmsk[KSG_RES_NCHK][2][2];  // slots the pod fitted at its TaintToleration max that stopped fitting
   int32_t xsig[2];                       // (extension scores) x's score when it rose (xres bit 2)
 };
 struct PlLdsOff {
@@ -494,14 +494,16 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         r_svc[e].peer[lane] = s_peer;
       }
       uint64_t e_ps = 0;
-      int32_t e_tm = 0;
-      if (esc) {  // (extension scores) the pod's soft-taint mask and TaintToleration max
+      int32_t e_tm = 0, e_tc = 0;
+      if (esc) {  // (extension scores) the pod's soft-taint mask, TaintToleration max and its node count
         e_ps = x.psoft[j];
         e_tm = x.tmax ? x.tmax[j] : 0;
+        e_tc = (x.thist && e_tm > 0) ? x.thist[(size_t)j * KSG_TBINS + e_tm] : 0;
       }
       if (lane == 0) {
         r_hdr[e].psoft = e_ps;
         r_hdr[e].tmax = e_tm;
+        r_hdr[e].tcnt = e_tc;
         r_hdr[e].m0 = m0;
         r_hdr[e].k0 = k0;
         r_hdr[e].r = r;
@@ -719,7 +721,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           if (in_t0) {
             if (unfit) {
               drop = true;
-              if (at_max) est |= 8u;  // (the normalisation max may fall: a fresh snapshot)
+              if (at_max) est |= 8u;  // (one fewer filtered node at the normalisation max)
             } else if (dl < 0) {
               drop = true;
             } else if (dl > 0) {
@@ -795,7 +797,8 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           ctl->chk_rmsk[c][par][1] = (uint32_t)(rm >> 32);
           ctl->chk_jmsk[c][par][0] = (uint32_t)jm;
           ctl->chk_jmsk[c][par][1] = (uint32_t)(jm >> 32);
-          ctl->chk_nstop[c][par] = nm != 0 ? 1u : 0u;
+          ctl->chk_nmsk[c][par][0] = (uint32_t)nm;
+          ctl->chk_nmsk[c][par][1] = (uint32_t)(nm >> 32);
         }
       }
       if (lane == 0) {
@@ -1376,9 +1379,16 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
              (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_jmsk[1][par][0])) & ~xb1;
       msk0 &= ~xb0;
       msk1 &= ~xb1;
-      const uint32_t nst = __builtin_amdgcn_readfirstlane(ctl->chk_nstop[0][par] | ctl->chk_nstop[1][par]);
-      if (nst || (have_x && (xres & 16u))) {
-        resolved = i;  // a committed node at the pod's TaintToleration max no longer fits
+      // the TaintToleration max falls once every filtered node at it stopped fitting: the
+      // checkers' such slots (x's by the x-checker) against the count pass's node count
+      const uint64_t nm0 = (((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_nmsk[0][par][1]) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_nmsk[0][par][0])) & ~xb0;
+      const uint64_t nm1 = (((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_nmsk[1][par][1]) << 32) |
+                            (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_nmsk[1][par][0])) & ~xb1;
+      const uint32_t gone = (uint32_t)__popcll(nm0) + (uint32_t)__popcll(nm1) + ((have_x && (xres & 16u)) ? 1u : 0u);
+      const int32_t tcnt = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].tcnt);
+      if (gone && (int32_t)gone >= tcnt) {
+        resolved = i;  // every filtered node at the pod's TaintToleration max stopped fitting
         reason = KSG_STOP_SERVICE;
         break;
       }
@@ -1635,8 +1645,10 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   for (uint32_t t = lane; t < resolved; t += 64) out[t] = L_out[t];
-  if (esc && x.tmax)  // (extension scores) the TaintToleration maxima start at 0 for the next window's count pass
+  if (esc && x.tmax) {  // (extension scores) the TaintToleration maxima and histograms start at 0 for the next window
     for (uint32_t t = lane; t < wcap; t += 64) x.tmax[t] = 0;
+    for (uint32_t t = lane; t < n_pods * KSG_TBINS; t += 64) x.thist[t] = 0;
+  }
   if (XS) {
     // (extensions) the window's extended resource requests into the node state
     // (the checkers wrote cpu / memory back; these live in no slot)

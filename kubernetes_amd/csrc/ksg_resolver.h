@@ -67,7 +67,7 @@ struct alignas(16) RingHdr {
   double inv_c, inv_m;                   // 10 / capacity of pred
   uint64_t psoft;                        // (extension scores) the pod's untolerated soft taints (mask)
   int32_t tmax;                          // ... its TaintToleration max over its filtered nodes
-  uint32_t pad3;
+  int32_t tcnt;                          // ... and how many of them hold it
 };
 struct alignas(16) RingSvc {  // per service entry t of the pod (t < n_svcs)
   int32_t cnt[KSG_SLOT_SVCS];   // svc_cnt[sv][pred] at the snapshot

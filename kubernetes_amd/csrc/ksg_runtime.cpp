@@ -45,7 +45,7 @@ hipError_t ksg_launch_win_eval(const KsgDev& d, int mode, const ksg_pod* batch, 
                                const KsgWinRun* run, uint32_t wcap, KsgWinSum* sums, uint64_t* wbits, int32_t* wmax,
                                uint32_t ostride, int32_t* dcnt, uint64_t* wfit, int32_t* dmb, uint64_t* wbz,
                                uint32_t dz, hipStream_t st, const ksg_pod_ext* exts = nullptr,
-                               int32_t* tmax = nullptr, uint64_t* psoft = nullptr);
+                               int32_t* tmax = nullptr, uint64_t* psoft = nullptr, int32_t* thist = nullptr);
 hipError_t ksg_launch_zonemap(uint32_t n_nodes, const int32_t* anti_domain, uint32_t d0, uint32_t nw,
                               uint64_t* zmap, hipStream_t st);
 hipError_t ksg_launch_win_t0(const KsgDev& d, uint32_t wcap, const KsgWinRun* run, const KsgWinXchg& x,
@@ -207,6 +207,8 @@ struct ksg_ctx {
   uint64_t* d_zmap = nullptr;    // [D+1][nw] re-rank: nodes of each domain row (cluster allocation)
   size_t win_cap = 0, xsend_cap = 0, xrecv_cap = 0, dcnt_cap = 0, dmb_cap = 0;
   int32_t* d_etmax = nullptr;    // [W] extension scores: TaintToleration max per window pod (count pass)
+  int32_t* d_ethist = nullptr;   // [W][KSG_TBINS] ... the histogram of its soft-taint counts
+  size_t ethist_cap = 0;
   uint64_t* d_epsoft = nullptr;  // [W] ... the pods' untolerated soft taints as masks
   size_t etmax_cap = 0, epsoft_cap = 0;
   KsgWinRun* d_run = nullptr;      // progress of the window chain (device)
@@ -1285,7 +1287,7 @@ int ksg_destroy(ksg_ctx* c) {
   void* scratch[] = {c->d_pods, c->d_ids, c->d_fail, c->d_score, c->d_rec_send, c->d_rec_recv, c->d_dpart,
                      c->d_dglobal, c->d_out, c->d_rng, c->d_summary, c->d_patch, c->d_shard_wlo,
                      c->d_winsum, c->d_xsend, c->d_xrecv, c->d_run, c->d_dcnt, c->d_admit, c->d_one,
-                     c->d_t0img, c->d_draws, c->d_etmax, c->d_epsoft};
+                     c->d_t0img, c->d_draws, c->d_etmax, c->d_epsoft, c->d_ethist};
   for (void* p : scratch)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -2070,11 +2072,14 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
              255) & ~(size_t)255;
     if (esc) {
       if ((rc = grow(c, (void**)&c->d_etmax, &c->etmax_cap, W, sizeof(int32_t))) ||
+          (rc = grow(c, (void**)&c->d_ethist, &c->ethist_cap, (size_t)W * KSG_TBINS, sizeof(int32_t))) ||
           (rc = grow(c, (void**)&c->d_epsoft, &c->epsoft_cap, W, sizeof(uint64_t))))
         return rc;
-      // (zero once here; each resolver zeroes the maxima again for the next window's count pass)
+      // (zero once here; each resolver zeroes them again for the next window's count pass)
       HIPCHK(c, hipMemsetAsync(c->d_etmax, 0, (size_t)W * sizeof(int32_t), c->st));
+      HIPCHK(c, hipMemsetAsync(c->d_ethist, 0, (size_t)W * KSG_TBINS * sizeof(int32_t), c->st));
       x.tmax = c->d_etmax;
+      x.thist = c->d_ethist;
       x.psoft = c->d_epsoft;
     }
     const size_t dcnt_n = (size_t)W * std::max<uint32_t>(c->D, 1);
@@ -2153,7 +2158,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
         if (etm)  // TaintToleration: each pod's max soft-taint count over its filtered nodes first
           HIPCHK(c, ksg_launch_win_eval(c->dev, 3, c->d_pods, c->d_ids, c->d_run, W, c->d_winsum, wbits, wmax,
                                         x.ostride, nullptr, nullptr, nullptr, nullptr, 0, c->st, dext, x.tmax,
-                                        x.psoft));
+                                        x.psoft, x.thist));
         HIPCHK(c, ksg_launch_win_eval(c->dev, anti ? 2 : 0, c->d_pods, c->d_ids, c->d_run, W, c->d_winsum, wbits,
                                       wmax, x.ostride, c->d_dcnt,
                                       (anti || esc) ? reinterpret_cast<uint64_t*>(c->d_xsend + fit_off) : nullptr,

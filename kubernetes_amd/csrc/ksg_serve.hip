@@ -618,16 +618,20 @@ __device__ __forceinline__ void agent_st64(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // The `applied` protocol between the leader and the scan workgroups (write the
-// invariant down, or use release / acquire). The leader applies a control request (COMMIT's
-// AssumePod delta, PATCH's mirror deltas) with agent-scope stores and atomics, drains them
-// (s_waitcnt vmcnt(0)) and then RELEASES `applied` = the request's sequence number at agent
-// scope. A scan workgroup polls `applied` with relaxed agent-scope loads until it covers the
-// BEGIN's ARG (the last control request the host posted before it), then every wave takes an
-// agent-scope ACQUIRE fence before its first load of mutable state (requested totals, keymap
-// rows, service counts, extended-resource usage). Those loads are agent-scope (ld_mut) as well,
-// so no stale vector-L1 copy from an earlier BEGIN is read either way.
+// invariant down, or use release / acquire). INVARIANT: every access to mutable node state
+// on either side is an agent-scope atomic (sc1: the leader's stores and read-modify-writes in
+// commit_pod_wave / the patch loop, the scan workgroups' ld_mut loads), so it is served at the
+// device's coherence point and no L1 / L2 copy can be stale. The leader drains its stores
+// (s_waitcnt vmcnt(0): each one acknowledged at that point) before it stores `applied` = the
+// request's sequence number; a scan workgroup polls `applied` (ld_mut) until it covers the
+// BEGIN's ARG (the last control request the host posted before it), and only after the
+// workgroup barrier that follows (a compiler barrier too) issues its loads of mutable state
+// (requested totals, keymap rows, service counts, extended-resource usage). A plain (non-sc1)
+// load of mutable state anywhere in the scan would break it. Agent-scope release / acquire
+// would not need the invariant, but on gfx950 they are an L2 write-back (buffer_wbl2 sc1) and
+// an L2 invalidate (buffer_inv sc1) per request: measured, 15,000 nodes 11.4 -> 22.1 us per pod.
 __device__ __forceinline__ void st_applied(const KsgSrvArgs& a, uint32_t seq) {
-  __hip_atomic_store(&a.grid->applied, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  agent_st32(&a.grid->applied, seq);
 }
 // scan workgroups' backstop beyond the leader's idle limit (wall_clock64 ticks, 100 MHz: 10 ms)
 #define KSG_GSRV_WAIT 1000000ull
@@ -754,7 +758,6 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
       }
       __syncthreads();
       if (s_kind == 0) return;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (pairs with the leader's release of `applied`)
       // mutable state only from here on (issued after `applied` covers the BEGIN's ARG)
 #pragma unroll
       for (int j = 0; j < NPT; ++j) {

@@ -93,7 +93,8 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
                                                                  uint64_t* __restrict__ wbz, uint32_t dz,
                                                                  const ksg_pod_ext* __restrict__ exts,
                                                                  int32_t* __restrict__ tmax,
-                                                                 uint64_t* __restrict__ psoft) {
+                                                                 uint64_t* __restrict__ psoft,
+                                                                 int32_t* __restrict__ thist) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (KSG_SC_NT / 64) + (threadIdx.x >> 6));
   const uint32_t p0 = blockIdx.y * KSG_PG;
@@ -293,6 +294,14 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
         const int32_t soft = fit ? __popcll(ntm & readlane64(ps, j)) : 0;
         const int32_t mx = wave_total_max(soft);
         if (lane == 0 && mx > 0) atomicMax(tmax + p0 + j, mx);
+        // ... and how many filtered nodes hold each count (one atomic per distinct count)
+        uint64_t pend = __ballot(fit);
+        while (pend) {
+          const int32_t v = __builtin_amdgcn_readlane(soft, (int)__builtin_ctzll(pend));
+          const uint64_t mine = __ballot(fit && soft == v);
+          if (lane == 0) atomicAdd(thist + (size_t)(p0 + j) * KSG_TBINS + v, (int32_t)__popcll(mine));
+          pend &= ~mine;
+        }
         continue;
       }
       if constexpr (MODE == KSG_WIN_COUNT) {
@@ -3031,17 +3040,17 @@ hipError_t ksg_launch_win_eval(const KsgDev& d, int mode, const ksg_pod* batch, 
                                const KsgWinRun* run, uint32_t wcap, KsgWinSum* sums, uint64_t* wbits, int32_t* wmax,
                                uint32_t ostride, int32_t* dcnt, uint64_t* wfit, int32_t* dmb, uint64_t* wbz,
                                uint32_t dz, hipStream_t st, const ksg_pod_ext* exts, int32_t* tmax,
-                               uint64_t* psoft) {
+                               uint64_t* psoft, int32_t* thist) {
   const uint32_t gx = std::max<uint32_t>(1, (d.nwords + KSG_SC_NT / 64 - 1) / (KSG_SC_NT / 64));
   const bool small = d.nwords < KSG_PG_WORDS;
   const uint32_t pg = small ? KSG_PG_SMALL : KSG_PG_LARGE;
   const dim3 grid(gx, (wcap + pg - 1) / pg);
 #define KSG_EVAL_LAUNCH(M, G)                                                                                    \
   hipLaunchKernelGGL((ksg_win_score_kernel<M, G>), grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, run, wcap, sums, \
-                     wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz, nullptr, nullptr, nullptr)
+                     wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz, nullptr, nullptr, nullptr, nullptr)
 #define KSG_EVAL_LAUNCH_X(M, G)                                                                              \
   hipLaunchKernelGGL((ksg_win_score_kernel<M, G, true>), grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, \
-                     run, wcap, sums, wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz, exts, tmax, psoft)
+                     run, wcap, sums, wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz, exts, tmax, psoft, thist)
   if (exts && mode == KSG_WIN_TMAX) {  // extensions: the TaintToleration count pass
     if (small) KSG_EVAL_LAUNCH_X(KSG_WIN_TMAX, KSG_PG_SMALL);
     else KSG_EVAL_LAUNCH_X(KSG_WIN_TMAX, KSG_PG_LARGE);

@@ -12,7 +12,9 @@
  * Prints one JSON line: per-pod latency percentiles (us), pods/s, the begin
  * and commit calls' own medians, and whether the resident server
  * (ksg_serve.hip) served them (KSG_SERVE=0: kernels launched per call).
- * usage: dropin_latency [n_nodes=5000] [n_pods=4000] [warmup=200] [want_fail=0] */
+ * usage: dropin_latency [n_nodes=5000] [n_pods=4000] [warmup=200] [want_fail=0] [ext=0] [policy=0]
+ * policy 1: config 4's shape (ServiceAffinity on region, ServiceAntiAffinity on zone with
+ * weight 1, plus the defaults; 4 regions x 2 zones, labels on every node). */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -55,6 +57,7 @@ int main(int argc, char** argv) {
   const int want_fail = argc > 4 ? atoi(argv[4]) : 0;
   /* 1: extensions (taints + one extended resource, the filters); 2: the same + TaintToleration */
   const int ext_mode = argc > 5 ? atoi(argv[5]) : 0;
+  const int policy = argc > 6 ? atoi(argv[6]) : 0;
   const uint32_t n_svc = 8;
   ksg_ctx* ctx = NULL;
 
@@ -66,6 +69,15 @@ int main(int argc, char** argv) {
   cfg.w_least_requested = 1;
   cfg.w_service_spreading = 1;
   cfg.max_conflict_keys = 64;
+  if (policy == 1) {  /* label key 0 = region (pairs 1..4), key 1 = zone (pairs 5..12) */
+    cfg.predicates |= KSG_PRED_SERVICEAFFINITY;
+    cfg.n_aff_labels = 1;
+    cfg.aff_key[0] = 0;
+    cfg.n_anti = 1;
+    cfg.anti_key[0] = 1;
+    cfg.w_anti[0] = 1;
+    cfg.n_priority_configs = 3;
+  }
   CHECK(ksg_create(&cfg, 0, &ctx));
   if (ext_mode) {
     ksg_ext_config e;
@@ -82,8 +94,23 @@ int main(int argc, char** argv) {
     nodes[i].cap_milli_cpu = 4000;
     nodes[i].cap_memory = 16LL << 30;
   }
-  const uint32_t pair_keys[1] = {0};
-  CHECK(ksg_set_cluster(ctx, nodes, n_nodes, NULL, 0, pair_keys, 1, n_svc));
+  uint32_t pair_keys[13] = {0};
+  uint32_t* npairs = NULL;
+  uint32_t n_np = 0, n_pk = 1;
+  if (policy == 1) {
+    for (uint32_t p = 1; p <= 4; ++p) pair_keys[p] = 0;
+    for (uint32_t p = 5; p <= 12; ++p) pair_keys[p] = 1;
+    n_pk = 13;
+    npairs = calloc(2 * (size_t)n_nodes, sizeof *npairs);
+    for (uint32_t i = 0; i < n_nodes; ++i) {
+      const uint32_t zone = i % 8;
+      nodes[i].label_off = n_np;
+      nodes[i].n_labels = 2;
+      npairs[n_np++] = 1 + zone / 2;
+      npairs[n_np++] = 5 + zone;
+    }
+  }
+  CHECK(ksg_set_cluster(ctx, nodes, n_nodes, npairs, n_np, pair_keys, n_pk, n_svc));
   if (ext_mode) {  /* 8 GPUs per node; every 5th node carries taint 1 (hard for the pods that do not tolerate it) */
     int64_t* gcap = calloc(n_nodes, sizeof *gcap);
     uint32_t* toff = calloc(n_nodes, sizeof *toff);
@@ -163,10 +190,10 @@ int main(int argc, char** argv) {
   printf("{\"metric\": \"drop-in per-pod latency (ksg_schedule_begin + ksg_schedule_commit, C caller)\", "
          "\"nodes\": %u, \"pods\": %u, \"warmup\": %u, \"placed\": %u, \"nofit\": %u, "
          "\"us_p50\": %.2f, \"us_p90\": %.2f, \"us_p99\": %.2f, \"us_max\": %.2f, \"us_mean\": %.2f, "
-         "\"pods_per_s\": %.1f, \"want_fail\": %d, \"ext\": %d, \"begin_us_p50\": %.2f, \"commit_us_p50\": %.2f, "
+         "\"pods_per_s\": %.1f, \"want_fail\": %d, \"ext\": %d, \"policy\": %d, \"begin_us_p50\": %.2f, \"commit_us_p50\": %.2f, "
          "\"served\": {\"eligible\": %d, \"launches\": %llu, \"requests\": %llu}, \"histogram_us\": {\"edges\": [5, 10, 20, 40, 80, 160, 320], \"counts\": [",
          n_nodes, n_pods, warmup, placed, nofit, PCT(0.5), PCT(0.9), PCT(0.99), lat[n_pods - 1],
-         t_all / n_pods, n_pods / (t_all * 1e-6), want_fail, ext_mode, lat_b[n_pods / 2], lat_c[n_pods / 2], (int)sv[3],
+         t_all / n_pods, n_pods / (t_all * 1e-6), want_fail, ext_mode, policy, lat_b[n_pods / 2], lat_c[n_pods / 2], (int)sv[3],
          (unsigned long long)sv[0], (unsigned long long)sv[1]);
   const double edges[] = {5, 10, 20, 40, 80, 160, 320, 1e30};
   size_t k = 0;
