@@ -53,8 +53,8 @@
 //   flag / data            writer      reader              pod index        ordered by
 //   r_hdr[e].ready         producer j  all but producers   j                ready = j+1 release after the entry
 //   L_pub / L_drw bits     producer j  producers > j       j                L_drw before L_pub (atomicOr, in order)
-//   L_xn[i]                committer   x-checker           i (checks i+1)   xn_seq = i+1 release after L_xn[i]
-//   L_cm[i], L_out[i],     committer   checkers (apply i   i                sel_seq = i+1 release after them
+//   L_cm[i].xn             committer   x-checker           i (checks i+1)   xn_seq = i+1 release after it
+//   L_cm[i] record, .out,  committer   checkers (apply i   i                sel_seq = i+1 release after them
 //    slot row keys / ids               at pod i+2)
 //   slot row counts        checker     checkers, x-checker commits <= i-2   chk_seq release (x-checker reads
 //                          (apply)                                          rows of commits it replayed: lists
@@ -80,6 +80,8 @@
 #define KSG_CSV_MAX 10  // services of a pod whose counts on the candidates are staged (6 x 10 lanes)
 #define KSG_NO_CAND 7u  // commit flags: the drawn node is no candidate
 
+// one per window pod; the first 16 bytes are the commit record (stored as one
+// 16-byte write), then the pod's answer and its drawn node (written apart)
 struct alignas(16) PlCommit {
   uint32_t kind;   // 0: no commit (error / no fit), 1: commit
   uint32_t slot;
@@ -87,6 +89,9 @@ struct alignas(16) PlCommit {
   uint32_t flags;  // bit 0: a new slot; bits 1..3: candidate index (KSG_NO_CAND: none);
                    // bits 8..15: the pod's service count; 16..23: the slot's service
                    // entries before the commit; 24..31: its conflict keys before it
+  int32_t out;     // the pod's answer (shard offset + lo, or KSG_OUT_*)
+  uint32_t xn;     // node drawn | its candidate index << 28 (~0u: no commit), for the x-checker
+  uint32_t pad[2];
 };
 struct alignas(16) PlCtl {
   uint32_t stop;      // the committer is done: pods [0, resolved) are decided
@@ -100,7 +105,7 @@ struct alignas(16) PlCtl {
   uint32_t hang;                         // a wait exceeded its spin limit (a bug)
   uint32_t xseq;                         // pods the x-checker is done with
   uint32_t xres[2];                      // its verdict for the pod of parity p: bit 0 x drops, bit 1 flag
-  uint32_t xn_seq;                       // pods whose drawn node is posted in L_xn
+  uint32_t xn_seq;                       // pods whose drawn node is posted in L_cm[].xn
   uint32_t fin_x;                        // the x-checker applied every commit's flags and first peers
   uint32_t t_x, t_n;                     // KSG_DEBUG & 8: clock at the xres / xn posts
   // (extension scores) checker c's slots for the pod of parity p whose score ROSE above M0
@@ -113,7 +118,7 @@ struct alignas(16) PlCtl {
 };
 struct PlLdsOff {
   uint32_t ctl, r_hdr, r_t0, r_wp, r_lp, r_rec, r_mod, r_svc, r_cand, r_csnap, r_csv;  // ring
-  uint32_t cm, out, xn, peer, flag, peerset, pub, drw, clist, dpos, sig;              // window
+  uint32_t clist, dpos, sig, cm, peer, pub, drw, flag, peerset;                        // window
   uint32_t total;
 };
 
@@ -132,17 +137,17 @@ __host__ __device__ inline PlLdsOff plain_lds_offsets(uint32_t P, uint32_t nflag
   o.r_cand = at;  at += win_al16((size_t)R * 8 * 4);            // candidate nodes (~0u: none)
   o.r_csnap = at; at += win_al16((size_t)R * KSG_NCAND * 6 * 8);  // [cand][cap c, m, used c, m, inv c, m]
   o.r_csv = at;   at += win_al16((size_t)R * KSG_NCAND * KSG_SLOT_SVCS * 4);  // [cand][service t] counts
-  o.cm = at;      at += win_al16((size_t)W * sizeof(PlCommit));
-  o.out = at;     at += win_al16((size_t)W * 4);
-  o.xn = at;      at += win_al16((size_t)W * 4);
-  o.peer = at;    at += win_al16((size_t)W * 2 * 4);
-  o.flag = at;    at += win_al16((size_t)nflag * 4);
-  o.peerset = at; at += win_al16((size_t)nflag * 4);
-  o.pub = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
-  o.drw = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
+  // fixed sizes first: every offset up to the commit records is a compile-time
+  // constant for a given P (an LDS immediate, not a register the roles' loops keep)
   o.clist = at;   at += win_al16((size_t)KSG_MAX_SLOTS * KSG_CL_W * 4);
   o.dpos = at;    at += win_al16((size_t)2 * KSG_MAX_SLOTS * 4);
   o.sig = at;     at += win_al16((size_t)2 * KSG_MAX_SLOTS * 4);    // (extension scores) risen slots' scores
+  o.cm = at;      at += win_al16((size_t)W * sizeof(PlCommit));
+  o.peer = at;    at += win_al16((size_t)W * 2 * 4);
+  o.pub = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
+  o.drw = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
+  o.flag = at;    at += win_al16((size_t)nflag * 4);
+  o.peerset = at; at += win_al16((size_t)nflag * 4);
   o.total = at;
   return o;
 }
@@ -267,12 +272,10 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   uint32_t* r_cand = reinterpret_cast<uint32_t*>(smem + o.r_cand);
   uint64_t* r_csnap = reinterpret_cast<uint64_t*>(smem + o.r_csnap);
   int32_t* r_csv = reinterpret_cast<int32_t*>(smem + o.r_csv);
+  // per window pod: commit record, answer and drawn node (the drawn node one entry per pod: the
+  // committer runs ahead of the x-checker through pods that make no commit, so a single mailbox
+  // would be overwritten before it is read)
   PlCommit* L_cm = reinterpret_cast<PlCommit*>(smem + o.cm);
-  int32_t* L_out = reinterpret_cast<int32_t*>(smem + o.out);
-  // node drawn by pod p | its candidate index << 28 (~0u: no commit), one entry
-  // per pod: the committer runs ahead of the x-checker through pods that make
-  // no commit, so a single mailbox would be overwritten before it is read
-  uint32_t* L_xn = reinterpret_cast<uint32_t*>(smem + o.xn);
   uint32_t* L_peer = reinterpret_cast<uint32_t*>(smem + o.peer);
   uint32_t* L_flag = reinterpret_cast<uint32_t*>(smem + o.flag);
   uint32_t* L_peerset = reinterpret_cast<uint32_t*>(smem + o.peerset);
@@ -295,11 +298,11 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   // KSG_DEBUG bits 16..19: a fixed delay per pod in one wave role (committer,
   // x-checker, checkers, producers) to test the hand-offs under another
   // interleaving than the natural one (tests/test_gpu_fuzz.py)
-  const uint32_t skew = ((uint32_t)d.dbg >> 16) & 15u;
+  const uint32_t skew = STAMP ? ((uint32_t)d.dbg >> 16) & 15u : 0u;  // (debug instantiation only)
   // KSG_DEBUG bits 24..27: TIMING EXPERIMENTS ONLY (decisions are wrong): 1 the x-checker posts
   // "no drop" as soon as the node arrives, 2 the checkers post "no drops" without checking, 4 the
   // committer takes the staged prediction, 8 the committer does not wait for the verdicts
-  const uint32_t xpt = ((uint32_t)d.dbg >> 24) & 15u;
+  const uint32_t xpt = STAMP ? ((uint32_t)d.dbg >> 24) & 15u : 0u;  // (debug instantiation only)
 
   for (uint32_t t = tid; t < RING; t += NT) r_hdr[t].ready = 0;
   if (tid == 0) *ctl = PlCtl{};
@@ -515,7 +518,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       pstamp(27);
     }
     if constexpr (STAMP) {
-      if (lane >= 24 && lane < 28) atomicAdd(d.dbgbuf + lane, (int32_t)(p_acc / 64));
+      if (d.dbgbuf && lane >= 24 && lane < 28) atomicAdd(d.dbgbuf + lane, (int32_t)(p_acc / 64));
     }
     return;
   }
@@ -673,6 +676,8 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         const PodView pv = pod_view(rec);
         const uint32_t wd = S.node >> 6;
         const uint64_t tw = r_t0[(size_t)e * P * 64 + wd];
+        SlotRow R;  // the slot's lists (as of the commits applied), in flight with the T0 word
+        R.load(my_cl);
         // the node's ascending position in T0 (used if it drops; for a node outside
         // T0, the T0 nodes below it: where it joins)
         dpos = r_lp[e * 64 + (wd >> 6) * 2] + r_wp[(size_t)e * P * 64 + wd] +
@@ -694,21 +699,10 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
               unfit |= q > 0 && S.xh[r] - S.xdl[r] < q;
             }
           if (!unfit && pv.nk && S.nk)  // PodFitsPorts / NoDiskConflict vs the window's keys
-            for (uint32_t a = 0; a < S.nk; ++a) {
-              const uint32_t key = my_cl[KSG_CL_KEY + a];
-              for (uint32_t b = 0; b < pv.nk; ++b) {
-                const bool on = b < pv.n_ports ? ports_on : disk_on;
-                unfit |= on && (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b)) == key;
-              }
-            }
+            unfit |= R.key_hit(S.nk, rec, pv.nk, pv.n_ports, ports_on, disk_on);
           // ServiceSpreading: the window's entries of the pod's service here (maxCount fixed)
           int32_t snapc = 0, sdel = 0;
-          if (spread_on && pv.s >= 0 && ((S.smask >> (pv.s & 31)) & 1u))
-            for (uint32_t a = 0; a < S.ns; ++a)
-              if (my_cl[KSG_CL_SV + a] == (uint32_t)pv.s) {
-                snapc = (int32_t)my_cl[KSG_CL_SC + a];
-                ++sdel;
-              }
+          if (spread_on && pv.s >= 0 && ((S.smask >> (pv.s & 31)) & 1u)) R.svc(S.ns, (uint32_t)pv.s, snapc, sdel);
           const bool sp = spread_on && pv.s >= 0 && pv.smax > 0;
           const int64_t fr_snap = (sp && sdel) ? frac10_f32((int64_t)pv.smax - snapc, pv.smax) : 0;
           const int64_t fr_now = (sp && sdel) ? frac10_f32((int64_t)pv.smax - snapc - sdel, pv.smax) : 0;
@@ -765,23 +759,12 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
                 lr_win(S.snp_c + pv.req_c, S.cap_c, S.inv_c) + lr_win(S.snp_m + pv.req_m, S.cap_m, S.inv_m);
             drop |= (lr_now >> 1) != (lr_snap >> 1);
           }
-          if (!drop && pv.nk && S.nk) {  // PodFitsPorts / NoDiskConflict vs the window's keys
-            for (uint32_t a = 0; a < S.nk; ++a) {
-              const uint32_t key = my_cl[KSG_CL_KEY + a];
-              for (uint32_t b = 0; b < pv.nk; ++b) {
-                const bool on = b < pv.n_ports ? ports_on : disk_on;
-                drop |= on && (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b)) == key;
-              }
-            }
-          }
+          if (!drop && pv.nk && S.nk)  // PodFitsPorts / NoDiskConflict vs the window's keys
+            drop |= R.key_hit(S.nk, rec, pv.nk, pv.n_ports, ports_on, disk_on);
           if (!drop && spread_on && pv.s >= 0 && ((S.smask >> (pv.s & 31)) & 1u)) {
             // ServiceSpreading (spreading.go:72-86) under an unchanged maxCount
             int32_t delta = 0, snapc = 0;
-            for (uint32_t a = 0; a < S.ns; ++a)
-              if (my_cl[KSG_CL_SV + a] == (uint32_t)pv.s) {
-                snapc = (int32_t)my_cl[KSG_CL_SC + a];
-                ++delta;
-              }
+            R.svc(S.ns, (uint32_t)pv.s, snapc, delta);
             if (delta)
               drop = frac10_f32((int64_t)pv.smax - snapc - delta, pv.smax) != frac10_f32((int64_t)pv.smax - snapc, pv.smax);
           }
@@ -839,7 +822,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       }
     }
     if constexpr (STAMP) {
-      if (lane >= 16 && lane < 22) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
+      if (d.dbgbuf && lane >= 16 && lane < 22) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
     }
     drain_stores();
     if (lane == 0) st_rel(&ctl->fin[c], 1u);
@@ -1024,7 +1007,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         st_rel(&ctl->xseq, i + 1);
       }
       uint32_t res = 0;
-      const uint32_t xv = i ? __builtin_amdgcn_readfirstlane(L_xn[i - 1]) : ~0u;
+      const uint32_t xv = i ? __builtin_amdgcn_readfirstlane(L_cm[i - 1].xn) : ~0u;
       const uint32_t xnode = xv == ~0u ? ~0u : xv & 0x0fffffffu, xcid = xv == ~0u ? KSG_NO_CAND : xv >> 28;
       const bool do_check = xnode != ~0u && !__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE;
       const uint32_t xw = d.lo + (do_check ? xnode : 0u);
@@ -1218,7 +1201,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       flags(q, node, cid, slot, bns, prec);
     }
     if constexpr (STAMP) {
-      if (lane >= 28 && lane < 32) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
+      if (d.dbgbuf && lane >= 28 && lane < 32) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
     }
     if (lane == 0) st_rel(&ctl->fin_x, 1u);
     return;
@@ -1299,8 +1282,8 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       // remove fits): no draw, no commit
       if (lane == 0) {
         L_cm[i].kind = 0;
-        L_out[i] = __builtin_amdgcn_readlane(rec, WS_ERR) ? KSG_OUT_ERROR : KSG_OUT_NOFIT;
-        L_xn[i] = ~0u;
+        L_cm[i].out = __builtin_amdgcn_readlane(rec, WS_ERR) ? KSG_OUT_ERROR : KSG_OUT_NOFIT;
+        L_cm[i].xn = ~0u;
         st_rel(&ctl->xn_seq, i + 1);
         st_rel(&ctl->sel_seq, i + 1);
       }
@@ -1544,7 +1527,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     const uint64_t cm = __ballot(cand == woff);
     const uint32_t cidx = cm ? (uint32_t)__builtin_ctzll(cm) : KSG_NO_CAND;
     if (lane == 0) {  // the x-checker takes the node's snapshot meanwhile
-      L_xn[i] = woff | (cidx << 28);
+      L_cm[i].xn = woff | (cidx << 28);
       if constexpr (STAMP) ctl->t_n = (uint32_t)__builtin_amdgcn_s_memtime();
       st_rel(&ctl->xn_seq, i + 1);
     }
@@ -1588,9 +1571,10 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       if (st_ < n_svcs) row[KSG_CL_SV + base_ns + st_] = rec;
     }
     if (lane == 0) {
-      L_cm[i] = PlCommit{1u, slot, woff,
-                         (in_c ? 0u : 1u) | (cidx << 1) | (n_svcs << 8) | (base_ns << 16) | (base_nk << 24)};
-      L_out[i] = (int32_t)wn;
+      // (the record's 16 bytes only: the drawn node next to it is the x-checker's)
+      *reinterpret_cast<uint4*>(&L_cm[i]) =
+          uint4{1u, slot, woff, (in_c ? 0u : 1u) | (cidx << 1) | (n_svcs << 8) | (base_ns << 16) | (base_nk << 24)};
+      L_cm[i].out = (int32_t)wn;
       st_rel(&ctl->sel_seq, i + 1);  // the checkers move on
     }
     if ((int32_t)woff != pred) KSG_COUNTP(8, 64)
@@ -1633,7 +1617,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   }
   if (!drained || ld_acq(&ctl->hang)) reason = KSG_STOP_HANG;
   if constexpr (STAMP) {
-    if (lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
+    if (d.dbgbuf && lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
   }
 #undef KSG_STAMPP
 #undef KSG_COUNTP
@@ -1644,7 +1628,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     __hip_atomic_compare_exchange_strong(d.svc_peer + sv, &expect, (int32_t)L_peer[2 * t + 1], __ATOMIC_RELAXED,
                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  for (uint32_t t = lane; t < resolved; t += 64) out[t] = L_out[t];
+  for (uint32_t t = lane; t < resolved; t += 64) out[t] = L_cm[t].out;
   if (esc && x.tmax) {  // (extension scores) the TaintToleration maxima and histograms start at 0 for the next window
     for (uint32_t t = lane; t < wcap; t += 64) x.tmax[t] = 0;
     for (uint32_t t = lane; t < n_pods * KSG_TBINS; t += 64) x.thist[t] = 0;
@@ -1738,7 +1722,9 @@ static hipError_t win_plain_launch(const KsgDev& d, uint32_t wcap, size_t lds, K
 hipError_t ksg_launch_win_plain(const KsgDev& d, uint32_t P, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
                                 const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
   const size_t lds = plain_lds_offsets(P, (d.n_services + 31) / 32, wcap).total;
-  const bool stamp = (d.dbg & 8) != 0;  // KSG_DEBUG & 8: per-section s_memtime stamps
+  // the debug instantiation: KSG_DEBUG & 8 (per-section s_memtime stamps), bits 16..19 (skews) or
+  // 24..27 (timing switches); the production one keeps no debug switch in a register
+  const bool stamp = (d.dbg & 8) != 0 || ((uint32_t)d.dbg & 0x0fff0000u) != 0;
 #define KSG_PLAIN_CASE(PP)                                                                  \
   if (P == PP)                                                                              \
     return stamp ? win_plain_launch<PP, true>(d, wcap, lds, run, sums, x, rng, out, st)    \

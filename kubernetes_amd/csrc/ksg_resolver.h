@@ -374,11 +374,57 @@ __device__ __forceinline__ PodView pod_view(uint32_t rec) {
 }
 
 // per-slot list table: [0, 8) conflict keys, [8, 20) service ids, [20, 32) the
-// services' counts on the node at the snapshot (written by the owner checker)
+// services' counts on the node at the snapshot (written by the owner checker).
+// Row stride 36 dwords (144 B, 16-byte aligned): a checker wave reads its 64
+// rows with ds_read_b128, whose 16-lane groups then start at 16 distinct
+// multiples of 4 banks mod 64 and cover every bank once (a 32-dword stride put
+// all 32 lanes of a ds_read_b32 group on one bank: a 32-way conflict per entry)
 #define KSG_CL_KEY 0
 #define KSG_CL_SV 8
 #define KSG_CL_SC 20
-#define KSG_CL_W 32
+#define KSG_CL_W 36
+
+// A checker lane's slot row in registers: eight 16-byte LDS reads issued
+// together, then the list scans run on registers (one dependent LDS read per
+// list entry before)
+struct SlotRow {
+  uint32_t w[32];
+  __device__ __forceinline__ void load(const uint32_t* row) {
+    const uint4* p = reinterpret_cast<const uint4*>(row);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint4 q = p[k];
+      w[4 * k] = q.x;
+      w[4 * k + 1] = q.y;
+      w[4 * k + 2] = q.z;
+      w[4 * k + 3] = q.w;
+    }
+  }
+  // the row's entries of service s among the first ns (cnt) and their snapshot count
+  __device__ __forceinline__ void svc(uint32_t ns, uint32_t s, int32_t& snapc, int32_t& cnt) const {
+    snapc = 0;
+    cnt = 0;
+#pragma unroll
+    for (int a = 0; a < KSG_SLOT_SVCS; ++a)
+      if ((uint32_t)a < ns && w[KSG_CL_SV + a] == s) {
+        snapc = (int32_t)w[KSG_CL_SC + a];
+        ++cnt;
+      }
+  }
+  // PodFitsPorts / NoDiskConflict: one of the pod's keys (record lanes WS_IDS..) among the
+  // row's first nk keys
+  __device__ __forceinline__ bool key_hit(uint32_t nk, uint32_t rec, uint32_t pod_nk, uint32_t n_ports, bool ports_on,
+                                          bool disk_on) const {
+    bool hit = false;
+    for (uint32_t b = 0; b < pod_nk; ++b) {
+      if (!(b < n_ports ? ports_on : disk_on)) continue;
+      const uint32_t kb = (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b));
+#pragma unroll
+      for (int a = 0; a < KSG_SLOT_KEYS; ++a) hit |= (uint32_t)a < nk && w[KSG_CL_KEY + a] == kb;
+    }
+    return hit;
+  }
+};
 
 // One slot in a checker lane's registers.
 struct RegSlot {

@@ -584,7 +584,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
   const bool disk_on = (d.preds & KSG_PRED_NODISKCONFLICT) != 0;
   // KSG_DEBUG bits 16..19: a fixed delay per pod in one role (committer, scribe, checkers,
   // producers): another interleaving of the hand-offs than the natural one (tests/test_gpu_fuzz.py)
-  const uint32_t skew = ((uint32_t)d.dbg >> 16) & 15u;
+  const uint32_t skew = STAMP ? ((uint32_t)d.dbg >> 16) & 15u : 0u;  // (debug instantiation only)
 
   for (uint32_t t = tid; t < KSG_RING; t += KSG_RES_NT) r_hdr[t].ready = 0;
   if (tid == 0) {
@@ -643,7 +643,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
     };
     auto pflush = [&]() {
       if constexpr (STAMP)
-        if (lane >= 12 && lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(pt_acc / 64));
+        if (d.dbgbuf && lane >= 12 && lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(pt_acc / 64));
     };
     if constexpr (STAMP) pt_last = __builtin_amdgcn_s_memtime();
     for (uint32_t j = wave - KSG_RES_P0; j < n_pods; j += KSG_RES_NPW) {
@@ -1451,7 +1451,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
     for (uint32_t t = lane; t < wcap * dz; t += 64) x.dmb[t] = KSG_S32_NONE;
   }
   if constexpr (STAMP) {
-    if (lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
+    if (d.dbgbuf && lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
   }
 #undef KSG_STAMP
 #undef KSG_COUNT
@@ -1539,12 +1539,17 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
 //    number of drawable pods before j, read from two LDS bitmaps every producer
 //    fills as soon as it knows its pod's max score (no producer-to-producer
 //    hand-off chain).
+// one per window pod; the first 16 bytes are the commit record (one 16-byte store),
+// then the pod's answer and its drawn node (written apart)
 struct alignas(16) WinCommit {
   uint32_t kind;   // 0: no commit (error / no fit), 1: commit
   uint32_t slot;
   uint32_t node;   // shard offset of the node
   uint32_t flags;  // bit 0: a new slot, bit 1: the node is the producer's predicted node,
                    // bits 8..15: the pod's service count
+  int32_t out;     // the pod's answer
+  uint32_t xn;     // node drawn (~0u: no commit), for the x-checker
+  uint32_t pad[2];
 };
 struct alignas(16) WinCtl2 {
   uint32_t stop;      // the committer is done: pods [0, resolved) are decided
@@ -1586,14 +1591,15 @@ struct WinLdsOff2 {
   // T0 by pod parity and slot (no ServiceAntiAffinity: the sparse select)
   uint32_t r_lp, r_wp, dpos;
   uint32_t ctl, r_hdr, r_t0, r_rec, r_mod, r_svc;
-  uint32_t cm, out, xn, peer, flag, peerset, drop, pub, drw, clist;
+  uint32_t cm, peer, flag, peerset, drop, pub, drw, clist;
   // ServiceAntiAffinity re-rank (dz > 0; see the LDS-slot resolver's WinLdsOff)
   uint32_t r_fit, r_b, r_mb, r_dc, zm, nsv, dca, r_kz, ddr;
   uint32_t total;
 };
 
+// (rr: the re-rank's arrays; -1: iff dz > 0; the kernel passes a constant)
 __host__ __device__ inline WinLdsOff2 win2_lds_offsets(uint32_t P, uint32_t nflag, uint32_t W, uint32_t dz = 0,
-                                                       uint32_t nsvc = 0) {
+                                                       uint32_t nsvc = 0, int rr_ = -1) {
   WinLdsOff2 o;
   const uint32_t R = win2_ring(P, dz != 0);
   uint32_t at = 0;
@@ -1603,28 +1609,29 @@ __host__ __device__ inline WinLdsOff2 win2_lds_offsets(uint32_t P, uint32_t nfla
   o.r_rec = at;   at += win_al16((size_t)R * KSG_WIN_SUM_DWORDS * 4);
   o.r_mod = at;   at += win_al16((size_t)R * 64 * 4);
   o.r_svc = at;   at += win_al16((size_t)R * sizeof(RingSvc));
+  // fixed sizes first (given P and whether the re-rank runs): their offsets are
+  // compile-time constants in the kernel, not registers the roles' loops keep
+  const bool rr = rr_ < 0 ? dz != 0 : rr_ != 0;
+  o.clist = at;   at += win_al16((size_t)KSG_MAX_SLOTS * KSG_CL_W * 4);
+  o.drop = at;    at += rr ? win_al16((size_t)2 * P * 64 * 8) : 0u;  // (the re-rank's drop bitmap)
+  o.r_fit = at;   at += rr ? win_al16((size_t)R * P * 64 * 8) : 0u;
+  o.r_b = at;     at += rr ? win_al16((size_t)R * P * 64 * 8) : 0u;
+  o.r_mb = at;    at += rr ? win_al16((size_t)R * KSG_RR_MAXZ * 4) : 0u;
+  o.r_dc = at;    at += rr ? win_al16((size_t)R * KSG_RR_MAXZ * 4) : 0u;
+  o.dca = at;     at += rr ? win_al16((size_t)KSG_RES_NCHK * 2 * KSG_RR_MAXZ * 4) : 0u;
+  o.r_kz = at;    at += rr ? win_al16((size_t)R * KSG_RR_MAXZ * 4) : 0u;
+  o.ddr = at;     at += rr ? win_al16((size_t)KSG_RES_NCHK * 2 * KSG_RR_MAXZ * 4) : 0u;
+  o.r_lp = at;    at += rr ? 0u : win_al16((size_t)R * 64 * 8);
+  o.r_wp = at;    at += rr ? 0u : win_al16((size_t)R * P * 64 * 2);
+  o.dpos = at;    at += rr ? 0u : win_al16((size_t)2 * KSG_MAX_SLOTS * 4);
   o.cm = at;      at += win_al16((size_t)W * sizeof(WinCommit));
-  o.out = at;     at += win_al16((size_t)W * 4);
-  o.xn = at;      at += win_al16((size_t)W * 4);
   o.peer = at;    at += win_al16((size_t)W * 2 * 4);
-  o.flag = at;    at += win_al16((size_t)nflag * 4);
-  o.peerset = at; at += win_al16((size_t)nflag * 4);
-  o.drop = at;    at += dz ? win_al16((size_t)2 * P * 64 * 8) : 0u;  // (the re-rank's drop bitmap)
   o.pub = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
   o.drw = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
-  o.clist = at;   at += win_al16((size_t)KSG_MAX_SLOTS * KSG_CL_W * 4);
-  o.r_fit = at;   at += dz ? win_al16((size_t)R * P * 64 * 8) : 0u;
-  o.r_b = at;     at += dz ? win_al16((size_t)R * P * 64 * 8) : 0u;
-  o.r_mb = at;    at += dz ? win_al16((size_t)R * KSG_RR_MAXZ * 4) : 0u;
-  o.r_dc = at;    at += dz ? win_al16((size_t)R * KSG_RR_MAXZ * 4) : 0u;
+  o.flag = at;    at += win_al16((size_t)nflag * 4);
+  o.peerset = at; at += win_al16((size_t)nflag * 4);
   o.zm = at;      at += win_al16((size_t)dz * P * 64 * 8);
-  o.nsv = at;     at += dz ? win_al16((size_t)nsvc * 4) : 0u;
-  o.dca = at;     at += dz ? win_al16((size_t)KSG_RES_NCHK * 2 * KSG_RR_MAXZ * 4) : 0u;
-  o.r_kz = at;    at += dz ? win_al16((size_t)R * KSG_RR_MAXZ * 4) : 0u;
-  o.ddr = at;     at += dz ? win_al16((size_t)KSG_RES_NCHK * 2 * KSG_RR_MAXZ * 4) : 0u;
-  o.r_lp = at;    at += dz ? 0u : win_al16((size_t)R * 64 * 8);
-  o.r_wp = at;    at += dz ? 0u : win_al16((size_t)R * P * 64 * 2);
-  o.dpos = at;    at += dz ? 0u : win_al16((size_t)2 * KSG_MAX_SLOTS * 4);
+  o.nsv = at;     at += rr ? win_al16((size_t)nsvc * 4) : 0u;
   o.total = at;
   return o;
 }
@@ -1641,8 +1648,8 @@ __host__ __device__ inline WinLdsOff2 win2_lds_offsets(uint32_t P, uint32_t nfla
 //    (record, T0, fit, B,                                                     (lane prefixes r_lp / r_wp too)
 //    row bests / counts)
 //   L_pub / L_drw bits       producer j  producers > j       j                L_drw before L_pub (atomicOr, in order)
-//   L_xn[i]                  committer   x-checker           i (checks i+1)   xn_seq = i+1 release after L_xn[i]
-//   L_cm[i], L_out[i],       committer   checkers (apply i   i                sel_seq = i+1 release after them
+//   L_cm[i].xn               committer   x-checker           i (checks i+1)   xn_seq = i+1 release after it
+//   L_cm[i] record, .out,    committer   checkers (apply i   i                sel_seq = i+1 release after them
 //    slot row keys / ids                 at pod i+2)
 //   slot row counts          checker     checkers,           commits <= i-2   chk_seq release (the x-checker
 //                            (apply)     x-checker                            reads rows of commits it replayed)
@@ -1683,7 +1690,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   constexpr uint32_t NPW = NT / 64 - KSG_RES_P0;  // producer waves
   constexpr uint32_t DW = KSG_WIN_SUM_DWORDS;
   const uint32_t dz = ANTI ? x.dz : 0u;
-  const WinLdsOff2 o = win2_lds_offsets(P, nflag, wcap, dz, d.n_services);
+  const WinLdsOff2 o = win2_lds_offsets(P, nflag, wcap, dz, d.n_services, ANTI ? 1 : 0);
   uint64_t* const r_fit = reinterpret_cast<uint64_t*>(smem + o.r_fit);  // [ring][P*64] fit at the snapshot
   uint64_t* const r_b = reinterpret_cast<uint64_t*>(smem + o.r_b);      // [ring][P*64] best-per-row nodes
   int32_t* const r_mb = reinterpret_cast<int32_t*>(smem + o.r_mb);      // [ring][KSG_RR_MAXZ] best per row
@@ -1699,12 +1706,10 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   uint32_t* r_rec = reinterpret_cast<uint32_t*>(smem + o.r_rec);
   uint32_t* r_mod = reinterpret_cast<uint32_t*>(smem + o.r_mod);
   RingSvc* r_svc = reinterpret_cast<RingSvc*>(smem + o.r_svc);
+  // per window pod: commit record, answer and drawn node (the drawn node one entry per pod: the
+  // committer runs ahead of the x-checker through pods that make no commit, so a single mailbox
+  // would be overwritten before the x-checker reads commit p's node)
   WinCommit* L_cm = reinterpret_cast<WinCommit*>(smem + o.cm);
-  int32_t* L_out = reinterpret_cast<int32_t*>(smem + o.out);
-  // node drawn by pod p (~0u: no commit), one entry per pod: the committer runs
-  // ahead of the x-checker through pods that make no commit, so a single
-  // mailbox would be overwritten before the x-checker reads commit p's node
-  uint32_t* L_xn = reinterpret_cast<uint32_t*>(smem + o.xn);
   uint32_t* L_peer = reinterpret_cast<uint32_t*>(smem + o.peer);
   uint32_t* L_flag = reinterpret_cast<uint32_t*>(smem + o.flag);
   uint32_t* L_peerset = reinterpret_cast<uint32_t*>(smem + o.peerset);
@@ -1723,7 +1728,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   const uint32_t nbits = (wcap + 31) / 32;
   // KSG_DEBUG bits 16..19: a fixed delay per pod in one role (committer, x-checker, checkers,
   // producers): another interleaving of the hand-offs than the natural one (tests/test_gpu_fuzz.py)
-  const uint32_t skew = ((uint32_t)d.dbg >> 16) & 15u;
+  // (the debug instantiation only: the production one keeps no debug switch in a register)
+  const uint32_t skew = STAMP ? ((uint32_t)d.dbg >> 16) & 15u : 0u;
 
   for (uint32_t t = tid; t < RING; t += NT) r_hdr[t].ready = 0;
   if (tid == 0) *ctl = WinCtl2{};
@@ -1954,7 +1960,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       pstamp(27);
     }
     if constexpr (STAMP) {
-      if (lane >= 24 && lane < 28) atomicAdd(d.dbgbuf + lane, (int32_t)(p_acc / 64));
+      if (d.dbgbuf && lane >= 24 && lane < 28) atomicAdd(d.dbgbuf + lane, (int32_t)(p_acc / 64));
     }
     return;
   }
@@ -2101,15 +2107,10 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
             bool nofit = false;
             if (res_on && !pv.zero_req)  // PodFitsResources (predicates.go:127-145)
               nofit = !((S.cap_c == 0 || S.cap_c - now_c >= pv.req_c) && (S.cap_m == 0 || S.cap_m - now_m >= pv.req_m));
-            if (!nofit && pv.nk && S.nk) {  // PodFitsPorts / NoDiskConflict vs the window's keys
-              for (uint32_t a = 0; a < S.nk; ++a) {
-                const uint32_t key = my_cl[KSG_CL_KEY + a];
-                for (uint32_t b = 0; b < pv.nk; ++b) {
-                  const bool on = b < pv.n_ports ? ports_on : disk_on;
-                  nofit |= on && (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b)) == key;
-                }
-              }
-            }
+            SlotRow R;  // the slot's lists, in registers
+            R.load(my_cl);
+            if (!nofit && pv.nk && S.nk)  // PodFitsPorts / NoDiskConflict vs the window's keys
+              nofit |= R.key_hit(S.nk, rec, pv.nk, pv.n_ports, ports_on, disk_on);
             if (in_b) {
               drop = nofit;
               if (!drop && d.w_lr) {  // LeastRequested (priorities.go:43-76)
@@ -2120,11 +2121,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
               }
               if (!drop && spread_on && pv.s >= 0 && ((S.smask >> (pv.s & 31)) & 1u)) {
                 int32_t delta = 0, snapc = 0;  // ServiceSpreading (spreading.go:72-86) under an unchanged maxCount
-                for (uint32_t a = 0; a < S.ns; ++a)
-                  if (my_cl[KSG_CL_SV + a] == (uint32_t)pv.s) {
-                    snapc = (int32_t)my_cl[KSG_CL_SC + a];
-                    ++delta;
-                  }
+                R.svc(S.ns, (uint32_t)pv.s, snapc, delta);
                 if (delta)
                   drop = frac10_f32((int64_t)pv.smax - snapc - delta, pv.smax) !=
                          frac10_f32((int64_t)pv.smax - snapc, pv.smax);
@@ -2137,7 +2134,9 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
               if (nofit) {
                 astop = anti_counts_move(d, S.node, pv.s);
               } else if ((S.smask >> (pv.s & 31)) & 1u) {
-                for (uint32_t a = 0; a < S.ns; ++a) ks += my_cl[KSG_CL_SV + a] == (uint32_t)pv.s;
+                int32_t sc_ = 0, kn_ = 0;
+                R.svc(S.ns, (uint32_t)pv.s, sc_, kn_);
+                ks = (uint32_t)kn_;
               }
             }
           }
@@ -2169,6 +2168,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
           const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
           const uint32_t wd = S.node >> 6;
           const uint64_t tw = t0e[wd];
+          SlotRow R;  // the slot's lists, in registers (in flight with the T0 word)
+          R.load(my_cl);
           // the node's ascending position in T0 (used only if it drops)
           dpos = r_lp[(e * 64 + (wd >> 6)) * 2] + r_wp[(size_t)e * P * 64 + wd] +
                  (uint32_t)__popcll(tw & ((1ULL << (S.node & 63)) - 1ULL));
@@ -2184,23 +2185,12 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
                   lr_win(S.snp_c + pv.req_c, S.cap_c, S.inv_c) + lr_win(S.snp_m + pv.req_m, S.cap_m, S.inv_m);
               drop |= (lr_now >> 1) != (lr_snap >> 1);
             }
-            if (!drop && pv.nk && S.nk) {  // PodFitsPorts / NoDiskConflict vs the window's keys
-              for (uint32_t a = 0; a < S.nk; ++a) {
-                const uint32_t key = my_cl[KSG_CL_KEY + a];
-                for (uint32_t b = 0; b < pv.nk; ++b) {
-                  const bool on = b < pv.n_ports ? ports_on : disk_on;
-                  drop |= on && (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b)) == key;
-                }
-              }
-            }
+            if (!drop && pv.nk && S.nk)  // PodFitsPorts / NoDiskConflict vs the window's keys
+              drop |= R.key_hit(S.nk, rec, pv.nk, pv.n_ports, ports_on, disk_on);
             if (!drop && spread_on && pv.s >= 0 && ((S.smask >> (pv.s & 31)) & 1u)) {
               // ServiceSpreading (spreading.go:72-86) under an unchanged maxCount
               int32_t delta = 0, snapc = 0;
-              for (uint32_t a = 0; a < S.ns; ++a)
-                if (my_cl[KSG_CL_SV + a] == (uint32_t)pv.s) {
-                  snapc = (int32_t)my_cl[KSG_CL_SC + a];
-                  ++delta;
-                }
+              R.svc(S.ns, (uint32_t)pv.s, snapc, delta);
               if (delta)
                 drop = frac10_f32((int64_t)pv.smax - snapc - delta, pv.smax) !=
                        frac10_f32((int64_t)pv.smax - snapc, pv.smax);
@@ -2251,7 +2241,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       }
     }
     if constexpr (STAMP) {
-      if (lane >= 16 && lane < 22) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
+      if (d.dbgbuf && lane >= 16 && lane < 22) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
     }
     drain_stores();
     if (lane == 0) st_rel(&ctl->fin[c], 1u);
@@ -2418,7 +2408,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         if (i) x_acc += lane == 31 ? (uint64_t)(uint32_t)((uint32_t)t_now - ctl->t_n) : 0ULL;
       }
       uint32_t res = 0;
-      const uint32_t xnode = i ? __builtin_amdgcn_readfirstlane(L_xn[i - 1]) : ~0u;
+      const uint32_t xnode = i ? __builtin_amdgcn_readfirstlane(L_cm[i - 1].xn) : ~0u;
       // the node's snapshot first (in flight over the bookkeeping below)
       const bool do_check = xnode != ~0u && !__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE;
       const uint32_t xw = d.lo + (do_check ? xnode : 0u);
@@ -2569,7 +2559,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       flags(q, node, slot, bns, prec);
     }
     if constexpr (STAMP) {
-      if (lane >= 28 && lane < 32) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
+      if (d.dbgbuf && lane >= 28 && lane < 32) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
     }
     if (lane == 0) st_rel(&ctl->fin_x, 1u);
     return;
@@ -2659,8 +2649,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       // remove fits): no draw, no commit
       if (lane == 0) {
         L_cm[i].kind = 0;
-        L_out[i] = __builtin_amdgcn_readlane(rec, WS_ERR) ? KSG_OUT_ERROR : KSG_OUT_NOFIT;
-        L_xn[i] = ~0u;
+        L_cm[i].out = __builtin_amdgcn_readlane(rec, WS_ERR) ? KSG_OUT_ERROR : KSG_OUT_NOFIT;
+        L_cm[i].xn = ~0u;
         st_rel(&ctl->xn_seq, i + 1);
         st_rel(&ctl->sel_seq, i + 1);
       }
@@ -2898,7 +2888,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         if (dww[q]) dw[lane * P + q] = 0;
     }
     if (lane == 0) {  // the x-checker loads the node's snapshot meanwhile
-      L_xn[i] = woff;
+      L_cm[i].xn = woff;
       if constexpr (STAMP) ctl->t_n = (uint32_t)__builtin_amdgcn_s_memtime();
       st_rel(&ctl->xn_seq, i + 1);
     }
@@ -2941,8 +2931,10 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       if (st < n_svcs) row[KSG_CL_SV + base_ns + st] = rec;
     }
     if (lane == 0) {
-      L_cm[i] = WinCommit{1u, slot, woff, (in_c ? 0u : 1u) | ((int32_t)woff == pred ? 2u : 0u) | (n_svcs << 8)};
-      L_out[i] = (int32_t)(d.lo + woff);
+      // (the record's 16 bytes only: the drawn node next to it is the x-checker's)
+      *reinterpret_cast<uint4*>(&L_cm[i]) =
+          uint4{1u, slot, woff, (in_c ? 0u : 1u) | ((int32_t)woff == pred ? 2u : 0u) | (n_svcs << 8)};
+      L_cm[i].out = (int32_t)(d.lo + woff);
       st_rel(&ctl->sel_seq, i + 1);  // the checkers and the x-checker move on
     }
     if ((int32_t)woff != pred) KSG_COUNT2(8, 64)
@@ -2993,7 +2985,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     for (uint32_t t = lane; t < wcap * dz; t += 64) x.dmb[t] = KSG_S32_NONE;
   }
   if constexpr (STAMP) {
-    if (lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
+    if (d.dbgbuf && lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
   }
 #undef KSG_STAMP2
 #undef KSG_COUNT2
@@ -3004,7 +2996,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     __hip_atomic_compare_exchange_strong(d.svc_peer + sv, &expect, (int32_t)L_peer[2 * t + 1], __ATOMIC_RELAXED,
                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  for (uint32_t t = lane; t < resolved; t += 64) out[t] = L_out[t];
+  for (uint32_t t = lane; t < resolved; t += 64) out[t] = L_cm[t].out;
   if (lane == 0) {
     *rng_io = rng0 + (uint64_t)n_draws * ksg_rng_step(d.draws);
     if (reason == KSG_STOP_HANG) {
@@ -3133,8 +3125,9 @@ hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run
   if (x.fit_off != 0 && x.rr && !(d.dbg & 4096)) {
     // ServiceAntiAffinity with the re-rank: the register-slot resolver
     // (KSG_DEBUG & 4096: the LDS-slot resolver instead, for comparison)
-    const size_t lds2 = win2_lds_offsets(P, (d.n_services + 31) / 32, wcap, x.dz, d.n_services).total;
-    const bool stamp2 = (d.dbg & 8) != 0;
+    const size_t lds2 = win2_lds_offsets(P, (d.n_services + 31) / 32, wcap, x.dz, d.n_services, 1).total;
+    // the debug instantiation: stamps (KSG_DEBUG & 8) or skews (bits 16..19)
+    const bool stamp2 = (d.dbg & 8) != 0 || ((uint32_t)d.dbg & 0x000f0000u) != 0;
 #define KSG_RES2A_CASE(PP)                                                                        \
   if (P == PP)                                                                                    \
     return stamp2 ? win_resolve2_launch<PP, true, true>(d, wcap, lds2, run, sums, x, rng, out, st) \
@@ -3148,7 +3141,8 @@ hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run
   }
   const size_t lds =
       win_lds_offsets(P, (d.n_services + 31) / 32, wcap, x.fit_off != 0, x.rr ? x.dz : 0u, d.n_services).total;
-  const bool stamp = (d.dbg & 8) != 0;  // KSG_DEBUG & 8: per-section s_memtime stamps
+  // the debug instantiation: stamps (KSG_DEBUG & 8) or skews (bits 16..19)
+  const bool stamp = (d.dbg & 8) != 0 || ((uint32_t)d.dbg & 0x000f0000u) != 0;
   const bool anti = x.fit_off != 0;
 #define KSG_RES_CASE(PP, AN)                                                                          \
   if (P == PP && anti == AN)                                                                          \
