@@ -81,12 +81,12 @@ extern "C" {
 #define KSG_FAIL_PODFITSRESOURCES 6
 #define KSG_FAIL_SERVICEAFFINITY 7
 
-#define KSG_MAX_ANTI 16          /* ServiceAntiAffinity priorities (policy)      */
+#define KSG_MAX_ANTI 64          /* ServiceAntiAffinity priorities (policy)      */
 #define KSG_MAX_LABEL_PREF 32    /* LabelPreference priorities (policy)          */
 #define KSG_MAX_PRESENCE 16      /* LabelsPresence predicates (policy)           */
 #define KSG_MAX_PRESENCE_KEYS 16 /* labels per LabelsPresence predicate          */
-#define KSG_MAX_AFF 4           /* ServiceAffinity labels (union of predicates) */
-#define KSG_MAX_AFF_GROUPS 8    /* ServiceAffinity predicates (label groups)    */
+#define KSG_MAX_AFF 16          /* ServiceAffinity labels (union of predicates) */
+#define KSG_MAX_AFF_GROUPS 32   /* ServiceAffinity predicates (label groups)    */
 
 /* Label pair flag in ksg_set_cluster's pair_keys[p]: the pair's key fails
  * IsQualifiedName or its value fails IsValidLabelValue (pkg/util/validation.go),

@@ -50,12 +50,12 @@ FAIL_TAINTS = 8
 FAIL_SCALAR = 9
 MAX_SCALAR = 4
 
-MAX_ANTI = 16
+MAX_ANTI = 64
 MAX_LABEL_PREF = 32
 MAX_PRESENCE = 16
 MAX_PRESENCE_KEYS = 16
-MAX_AFF = 4
-MAX_AFF_GROUPS = 8
+MAX_AFF = 16
+MAX_AFF_GROUPS = 32
 PAIR_INVALID = 0x80000000  # pair_keys flag: SelectorFromSet rejects the (key, value)
 AFF_INVALID = -2           # ksg_pod.aff_pair: the pod's own value for the label is invalid
 

@@ -127,6 +127,7 @@ struct KsgStaticCfg {
 // needs for one pod in one 192-byte record, so the sequential resolver streams
 // one record per pod instead of chasing the pod descriptor and id lists.
 #define KSG_WIN_INLINE 24
+#define KSG_WIN_SUM_AFF 4
 struct KsgWinSum {
   int32_t m0;          // best combined score at the snapshot (KSG_S32_NONE: nothing fits)
   uint32_t k0;         // nodes at m0 (bits of the pod's T0 bitmap)
@@ -138,7 +139,7 @@ struct KsgWinSum {
   uint32_t n_inline;   // total list entries; > KSG_WIN_INLINE: lists read from pods/ids
   int64_t milli_cpu;
   int64_t memory;
-  int32_t req_aff[KSG_MAX_AFF];  // resolved ServiceAffinity pairs
+  int32_t req_aff[KSG_WIN_SUM_AFF];  // resolved ServiceAffinity pairs (the first KSG_WIN_SUM_AFF; unread by the resolvers)
   uint16_t n_ports, n_pds, n_sel, n_svcs;
   uint32_t xmask;      // extensions: the extended resource kinds the pod requests (bit r: scalar[r] > 0)
   uint32_t ids[KSG_WIN_INLINE];  // ports, pds, sel, svcs (in that order)

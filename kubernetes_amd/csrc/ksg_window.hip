@@ -430,7 +430,7 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
       S->milli_cpu = c.req_cpu;
       S->memory = c.req_mem;
 #pragma unroll
-      for (int j = 0; j < KSG_MAX_AFF; ++j) S->req_aff[j] = c.req_aff[j];
+      for (int j = 0; j < KSG_WIN_SUM_AFF; ++j) S->req_aff[j] = c.req_aff[j];
       S->n_ports = (uint16_t)p.n_ports;
       S->n_pds = (uint16_t)p.n_pds;
       S->n_sel = (uint16_t)p.n_sel;

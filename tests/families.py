@@ -23,6 +23,10 @@ library and compare every decision.
                   node list (MapPodsToMachines keys on Status.Host, predicates.go:354-375)
   invalid_selectors  ServiceAffinity over two predicates with invalid nodeSelector
                   values and invalid node label values (SelectorFromSet's trap)
+  past_caps       a Policy past round 3's caps: six ServiceAffinity labels in ten
+                  predicates (label groups) and twenty ServiceAntiAffinity priorities
+                  (the reference registers any number of each, plugins.go:81-117,
+                  145-183): the exact kernels
 """
 from __future__ import annotations
 
@@ -30,7 +34,7 @@ from kubernetes_amd import factory, workload
 from kubernetes_amd.api import ObjectMeta, PodStatus, Quantity, Service, ServiceSpec
 
 FAMILIES = ("multi_service", "namespaces", "negative", "big_weights", "huge_weights", "many_anti", "existing_hosts",
-            "invalid_selectors")
+            "invalid_selectors", "past_caps")
 
 # the window path keeps 10 * sum|w| + |w_equal| below 2^30 (KSG_SCORE_BOUND, ksg_internal.h)
 BIG_W = (1 << 30) // 10 // 4 - 1
@@ -165,6 +169,29 @@ def build(family: str, nn: int, npods: int, seed: int = 7) -> workload.Workload:
                                          "argument": {"serviceAffinity": {"labels": ["rack", "zone"]}}}),
                       [{"name": "LeastRequestedPriority", "weight": 1}, {"name": "ServiceSpreadingPriority", "weight": 1}],
                       "inv")
+    elif family == "past_caps":
+        # labels derived from the zone (region, pool, tier pin it together), two
+        # single-valued ones and one on half the nodes (a peer node without the label
+        # constrains nothing for it, predicates.go:293-300)
+        for i, n in enumerate(nodes):
+            z = int(n.metadata.labels["zone"][1:])
+            n.metadata.labels.update({"pool": f"p{z % 2}", "tier": f"t{(z // 2) % 2}", "hw": "h0", "os": "linux"})
+            if i % 2:
+                n.metadata.labels["fabric"] = "f0"
+        pods = workload.make_pods(npods, rng, n_apps=6)
+        for i, p in enumerate(pods):
+            if i % 11 == 0:
+                p.spec.node_selector = dict(p.spec.node_selector or {}, pool=f"p{i % 2}")
+        services = workload.make_services(6)
+        groups = (["region"], ["pool"], ["tier"], ["hw"], ["os"], ["fabric"], ["region", "pool"], ["tier", "hw"],
+                  ["os", "fabric"], ["region", "tier", "fabric"])
+        aff = tuple({"name": f"Aff{g}", "argument": {"serviceAffinity": {"labels": labels}}}
+                    for g, labels in enumerate(groups))
+        anti = [{"name": f"Anti{i}", "weight": 1 + i % 3,
+                 "argument": {"serviceAntiAffinity": {"label": ("zone", "rack", "region", "pool")[i % 4]}}}
+                for i in range(20)]
+        cfg = _policy(_DEFAULT_PREDS + aff, [{"name": "LeastRequestedPriority", "weight": 1},
+                                             {"name": "ServiceSpreadingPriority", "weight": 1}] + anti, "pc")
     else:
         raise ValueError(family)
     cfg.max_conflict_keys = 4096

@@ -9,13 +9,14 @@ timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/${TAG}_bench_de
 for w in config3 config4 config5; do
   timeout -k 10 200 python bench.py --no-cpu-baseline --no-stages --workload $w > gpurun_out/${TAG}_bench_$w.json 2> gpurun_out/${TAG}_bench_$w.err || { tail gpurun_out/${TAG}_bench_$w.err; exit 1; }
 done
-timeout -k 10 300 python bench.py --no-cpu-baseline --extensions --no-stages > gpurun_out/${TAG}_bench_c2_ext.json 2> gpurun_out/${TAG}_bench_c2_ext.err || { tail gpurun_out/${TAG}_bench_c2_ext.err; exit 1; }
+timeout -k 10 300 python bench.py --no-cpu-baseline --extensions > gpurun_out/${TAG}_bench_c2_ext.json 2> gpurun_out/${TAG}_bench_c2_ext.err || { tail gpurun_out/${TAG}_bench_c2_ext.err; exit 1; }
 python - "$TAG" <<'PY'
 import json,sys
 t=sys.argv[1]
 for w in ("default","config3","config4","config5","c2_ext"):
     d=json.loads(open(f"gpurun_out/{t}_bench_{w}.json").read().strip().splitlines()[-1])
     print(w, round(d["value"]), round((d.get("latency") or {}).get("resolver_cycles_per_pod") or 0), round(d["ms_per_step"],3), d["config"]["snapshots_in_timed"])
-d=json.loads(open(f"gpurun_out/{t}_bench_default.json").read().strip().splitlines()[-1])
-print(json.dumps(d["latency"].get("stages")))
+for w in ("default","c2_ext"):
+    d=json.loads(open(f"gpurun_out/{t}_bench_{w}.json").read().strip().splitlines()[-1])
+    print(w, json.dumps(d["latency"].get("stages")))
 PY
