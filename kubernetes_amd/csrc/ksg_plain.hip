@@ -668,6 +668,15 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       cstamp(c == 0 ? 17 : 20);
       const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
       const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
+      // (extension scores) the slot's fit word and service count at the snapshot for this pod,
+      // in flight over the check (read only for a node outside T0 whose score may rise)
+      uint64_t e_fw = 0;
+      int32_t e_cs = 0;
+      if (esc && S.node != ~0u) {
+        e_fw = gld(reinterpret_cast<const uint64_t*>(x.buf + x.efit_off) + (size_t)i * x.ostride + (S.node >> 6));
+        const int32_t ps = (int32_t)__builtin_amdgcn_readfirstlane(r_rec[e * DW + WS_SVC]);
+        if (spread_on && ps >= 0) e_cs = gld(d.svc_cnt + (size_t)ps * d.n_nodes + d.lo + S.node);
+      }
       bool drop = false;
       uint32_t dpos = 0;
       uint32_t est = 0;  // (extension scores) 2: rose above M0 (esig), 4: joined T0, 8: normalisation stop
@@ -723,12 +732,11 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
               esig = (int32_t)(m0 + dl);
             }
           } else if (dl > 0 || (unfit && at_max)) {
-            const uint64_t fw = gld(reinterpret_cast<const uint64_t*>(x.buf + x.efit_off) + (size_t)i * x.ostride + wd);
-            if ((fw >> (S.node & 63)) & 1ULL) {  // fitted at the snapshot
+            if ((e_fw >> (S.node & 63)) & 1ULL) {  // fitted at the snapshot
               if (unfit) {
-                est |= 8u;
+                if (at_max) est |= 8u;  // (an unfit node off the max changes nothing)
               } else {
-                const int32_t cs = sdel ? snapc : (sp ? gld(d.svc_cnt + (size_t)pv.s * d.n_nodes + d.lo + S.node) : 0);
+                const int32_t cs = sdel ? snapc : e_cs;
                 const int64_t frs = sp ? frac10_f32((int64_t)pv.smax - cs, pv.smax) : 10;
                 const int64_t now = es_snap_score(d, pv.req_c, pv.req_m, S.cap_c, S.cap_m, S.inv_c, S.inv_m, S.snp_c,
                                                   S.snp_m, frs, S.sst, soft, tmx) + dl;
@@ -980,6 +988,18 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       const bool p_staged = i && r_hdr[ep].pad != 0;
       const PodView pv = pod_view(rec);
       const int32_t s = pv.s;
+      // (extension scores) pod i's fit word, the node taints, static score and service count of
+      // each of pod i-1's staged candidates (lane c), in flight while the node is drawn: the
+      // drawn node is usually one of them, and its re-score then reads no L2 on the chain
+      uint64_t c_fw = 0, c_ntm = 0;
+      int32_t c_sst = 0, c_cs = 0;
+      const uint32_t c_node = (esc && i > 0 && lane < KSG_NCAND) ? r_cand[ep * 8 + lane] : ~0u;
+      if (c_node != ~0u) {
+        c_fw = gld(reinterpret_cast<const uint64_t*>(x.buf + x.efit_off) + (size_t)i * x.ostride + (c_node >> 6));
+        c_ntm = d.ntaint ? gld(d.ntaint + d.lo + c_node) : 0ULL;
+        c_sst = d.has_static_score ? (int32_t)gld(d.static_score + d.lo + c_node) : 0;
+        c_cs = (spread_on && s >= 0) ? gld(d.svc_cnt + (size_t)s * d.n_nodes + d.lo + c_node) : 0;
+      }
       for (uint32_t spin = 0;; ++spin) {  // pod i-1's node drawn, or the end
         const uint32_t xn = ld_u(&ctl->xn_seq), st = ld_u(&ctl->stop);
         if (xn >= i) break;
@@ -1125,7 +1145,9 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
                                       fr_now);
           const uint64_t psoft = r_hdr[e].psoft;
           const int32_t tmx = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].tmax);
-          const uint64_t xntm = d.ntaint ? gld(d.ntaint + xw) : 0ULL;
+          // x's taints, static score, fit word and service count: prefetched for a candidate
+          const bool cand_x = xcid < KSG_NCAND;
+          const uint64_t xntm = cand_x ? readlane64(c_ntm, (int)xcid) : (d.ntaint ? gld(d.ntaint + xw) : 0ULL);
           const int32_t soft = __popcll(xntm & psoft);
           const bool at_max = d.w_taint != 0 && tmx > 0 && soft == tmx;
           uint32_t es = 0;
@@ -1142,14 +1164,20 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
               sig = (int32_t)(m0 + dl);
             }
           } else if (dl > 0 || (xu && at_max)) {
-            const uint64_t fw = gld(reinterpret_cast<const uint64_t*>(x.buf + x.efit_off) + (size_t)i * x.ostride + (xnode >> 6));
+            const uint64_t fw =
+                cand_x ? readlane64(c_fw, (int)xcid)
+                       : gld(reinterpret_cast<const uint64_t*>(x.buf + x.efit_off) + (size_t)i * x.ostride + (xnode >> 6));
             if ((fw >> (xnode & 63)) & 1ULL) {  // fitted at the snapshot
               if (xu) {
-                es |= 16u;
+                if (at_max) es |= 16u;  // (an unfit node off the max changes nothing)
               } else {
-                const int32_t cs = x_cnt_s ? x_snapc : (sp ? gld(d.svc_cnt + (size_t)s * d.n_nodes + xw) : 0);
+                const int32_t cs = x_cnt_s ? x_snapc
+                                           : !sp ? 0
+                                           : cand_x ? __builtin_amdgcn_readlane(c_cs, (int)xcid)
+                                                    : gld(d.svc_cnt + (size_t)s * d.n_nodes + xw);
                 const int64_t frs = sp ? frac10_f32((int64_t)pv.smax - cs, pv.smax) : 10;
-                const int32_t xsst = d.has_static_score ? (int32_t)gld(d.static_score + xw) : 0;
+                const int32_t xsst = cand_x ? __builtin_amdgcn_readlane(c_sst, (int)xcid)
+                                            : d.has_static_score ? (int32_t)gld(d.static_score + xw) : 0;
                 const int64_t now =
                     es_snap_score(d, pv.req_c, pv.req_m, capc, capm, invc, invm, usec, usem, frs, xsst, soft, tmx) + dl;
                 if (now > m0) {

@@ -96,8 +96,17 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
                                                                  uint64_t* __restrict__ psoft,
                                                                  int32_t* __restrict__ thist) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t w = __builtin_amdgcn_readfirstlane(blockIdx.x * (KSG_SC_NT / 64) + (threadIdx.x >> 6));
-  const uint32_t p0 = blockIdx.y * KSG_PG;
+  // XCD-aware order (a 1-D grid padded to a multiple of 8): the hardware deals
+  // workgroups round-robin to the 8 XCDs (linear id mod 8), so XCD k takes the
+  // k-th contiguous eighth of the (word group, pod group) pairs, pod group
+  // fastest: the node state of a word group is fetched into one XCD's L2 for all
+  // the window's pod groups instead of into every XCD's
+  const uint32_t gx = (d.nwords + KSG_SC_NT / 64 - 1) / (KSG_SC_NT / 64), gy = (wcap + KSG_PG - 1) / KSG_PG;
+  const uint32_t per = gridDim.x >> 3, lin = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+  if (lin >= max(gx, 1u) * gy) return;  // (padding; wave-uniform, no barrier in this kernel)
+  const uint32_t bx = lin / gy, by = lin - bx * gy;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(bx * (KSG_SC_NT / 64) + (threadIdx.x >> 6));
+  const uint32_t p0 = by * KSG_PG;
   // this window = pods [pos, pos + n_pods) of the batch (set by the previous resolver)
   const uint32_t pos = run->pos, n_batch = run->n;
   if (run->halt || pos >= n_batch) return;
@@ -3036,7 +3045,8 @@ hipError_t ksg_launch_win_eval(const KsgDev& d, int mode, const ksg_pod* batch, 
   const uint32_t gx = std::max<uint32_t>(1, (d.nwords + KSG_SC_NT / 64 - 1) / (KSG_SC_NT / 64));
   const bool small = d.nwords < KSG_PG_WORDS;
   const uint32_t pg = small ? KSG_PG_SMALL : KSG_PG_LARGE;
-  const dim3 grid(gx, (wcap + pg - 1) / pg);
+  // one dimension, a multiple of 8 workgroups (the kernel's XCD-aware order)
+  const dim3 grid((gx * ((wcap + pg - 1) / pg) + 7) & ~7u);
 #define KSG_EVAL_LAUNCH(M, G)                                                                                    \
   hipLaunchKernelGGL((ksg_win_score_kernel<M, G>), grid, dim3(KSG_SC_NT), 0, st, d, batch, ids, run, wcap, sums, \
                      wbits, wmax, ostride, dcnt, wfit, dmb, wbz, dz, nullptr, nullptr, nullptr, nullptr)
