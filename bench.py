@@ -86,8 +86,10 @@ _STAGES_PLAIN = {
     4: ("committer", "slot"), 5: ("committer", "commit"),
     6: ("handoff", "xcheck_to_committer"), 31: ("handoff", "node_to_xchecker"),
     10: ("committer", "ring_wait_first4"), 11: ("committer", "ring_wait_rest"),
+    12: ("committer", "verdict_reads"), 13: ("committer", "head_reads"),  # (select / head = the rest)
     16: ("checker0", "wait"), 17: ("checker0", "apply"), 18: ("checker0", "check"),
     19: ("checker1", "wait"), 20: ("checker1", "apply"), 21: ("checker1", "check"),
+    22: ("checker0", "check_loads"), 23: ("checker0", "check_resources_lr"),  # (check = the rest)
     24: ("producers_sum_over_waves", "ring_wait"), 25: ("producers_sum_over_waves", "loads"),
     26: ("producers_sum_over_waves", "draw_wait"), 27: ("producers_sum_over_waves", "stage"),
     28: ("xchecker", "wait_node"), 29: ("xchecker", "flags"), 30: ("xchecker", "bookkeeping_and_lists"),
@@ -129,7 +131,7 @@ def _phase_a_bytes(cfg, pods, ids, ns, nw, w):
             + w * nw * 12.0 + w * 192.0)
 
 
-def _stage_breakdown(cfg, view, args, step_batch, anti):
+def _stage_breakdown(cfg, view, args, step_batch, anti, ext=None):
     """Per-stage resolver cycles per pod from a KSG_DEBUG=8 context over the
     bench's first steps (untimed; the stamps cost a few percent)."""
     from kubernetes_amd import workload
@@ -142,7 +144,11 @@ def _stage_breakdown(cfg, view, args, step_batch, anti):
         s2 = DeviceScheduler(cfg, device=0)
         if args.window is not None:
             s2.set_window(args.window)
+        if ext is not None:
+            s2.set_extensions(ext[0])
         s2.set_cluster(view.arrays)
+        if ext is not None:
+            s2.set_node_ext(*ext[1])
         rng = workload.TIEBREAK_SEED
         pods = 0
         for s in range(min(3, args.warmup + args.steps)):
@@ -415,8 +421,8 @@ def main():
         latency = {"bound": "latency", "resolver_us_per_pod": us_pod, "clock_mhz": CLOCK_MHZ,
                    "resolver_cycles_per_pod": us_pod * CLOCK_MHZ,
                    "window_eval_us_per_pod": kk["eval_ms"] * 1e3 / pods_timed}
-        if world == 1 and not args.no_stages and ext is None:
-            latency["stages"] = _stage_breakdown(cfg, view, args, step_batch, anti)
+        if world == 1 and not args.no_stages:
+            latency["stages"] = _stage_breakdown(cfg, view, args, step_batch, anti, ext)
 
     # ---- CPU baseline: faithful restatement, single thread, bounded prefix ------
     cpu = None

@@ -85,6 +85,14 @@ __device__ __forceinline__ int64_t frac10_f32(int64_t num, int64_t den) {
   return (int64_t)s;
 }
 
+// the same for operands that fit int32 (counts and their maxima): (float)int32 rounds
+// the integer exactly as (float)int64 does, at a fraction of the conversion's cost
+__device__ __forceinline__ int32_t frac10_i32(int32_t num, int32_t den) {
+  const float q = __fdiv_rn((float)num, (float)den);
+  const float s = __fmul_rn(10.0f, q);
+  return (int32_t)s;
+}
+
 // Go's int arithmetic wraps (two's complement); so do these
 __host__ __device__ __forceinline__ int64_t wsum(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
 __host__ __device__ __forceinline__ int64_t wmul(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }

@@ -79,6 +79,10 @@
 #define KSG_NCAND 6     // candidate nodes staged per pod (0, 1 or 2 drops)
 #define KSG_CSV_MAX 10  // services of a pod whose counts on the candidates are staged (6 x 10 lanes)
 #define KSG_NO_CAND 7u  // commit flags: the drawn node is no candidate
+// staged snapshot fields per candidate: capacity, requested totals, 10 / capacity (cpu, memory),
+// (extension scores) the node's static score and taint mask, (extended resources) the
+// headroom of kinds 0, 1 and of kinds 2, 3 (two int32 each)
+#define KSG_CSNAP 10
 
 // one per window pod; the first 16 bytes are the commit record (stored as one
 // 16-byte write), then the pod's answer and its drawn node (written apart)
@@ -135,7 +139,7 @@ __host__ __device__ inline PlLdsOff plain_lds_offsets(uint32_t P, uint32_t nflag
   o.r_mod = at;   at += win_al16((size_t)R * 64 * 4);           // r mod (k0 - d)
   o.r_svc = at;   at += win_al16((size_t)R * sizeof(RingSvc));  // the pod's services' max / peer
   o.r_cand = at;  at += win_al16((size_t)R * 8 * 4);            // candidate nodes (~0u: none)
-  o.r_csnap = at; at += win_al16((size_t)R * KSG_NCAND * 6 * 8);  // [cand][cap c, m, used c, m, inv c, m]
+  o.r_csnap = at; at += win_al16((size_t)R * KSG_NCAND * KSG_CSNAP * 8);  // [cand][cap c, m, used c, m, inv c, m, sst, taints]
   o.r_csv = at;   at += win_al16((size_t)R * KSG_NCAND * KSG_SLOT_SVCS * 4);  // [cand][service t] counts
   // fixed sizes first: every offset up to the commit records is a compile-time
   // constant for a given P (an LDS immediate, not a register the roles' loops keep)
@@ -459,19 +463,35 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           }
         }
       }
-      // their snapshots (lane L < 36: candidate L / 6, field L % 6) and the pod's
-      // service counts on them (lane L < 6 n_svcs: candidate L / n_svcs, service
-      // L % n_svcs), all loads in flight together
+      // their snapshots (lane L < 60: candidate L / 10, field L % 10; the static score and the
+      // taints only with extension scores, the extended resources' headroom only with those) and the pod's service counts on them (lane
+      // L < 6 n_svcs: candidate L / n_svcs, service L % n_svcs), all loads in flight together
       const bool csv_on = inl && n_svcs > 0 && n_svcs <= KSG_CSV_MAX;
-      const uint32_t cL = lane / 6, fL = lane % 6;
+      const uint32_t cL = lane / KSG_CSNAP, fL = lane % KSG_CSNAP;
       const uint32_t cn_ = (uint32_t)__shfl((int)cand_l, (int)(cL < KSG_NCAND ? cL : 0u), 64);
-      const uint32_t cn = lane < 6 * KSG_NCAND ? cn_ : ~0u;
+      const uint32_t cn = lane < KSG_CSNAP * KSG_NCAND ? cn_ : ~0u;
       uint64_t snap = 0;
       if (cn != ~0u) {
         const uint32_t pn = d.lo + cn;
         const int64_t* src = fL == 0 ? d.cap_cpu : fL == 1 ? d.cap_mem : fL == 2 ? d.used_cpu : d.used_mem;
-        snap = fL < 4 ? (uint64_t)gld(src + pn)
-                      : (uint64_t)gld(reinterpret_cast<const int64_t*>(fL == 4 ? d.inv10_cpu : d.inv10_mem) + pn);
+        if (fL < 4)
+          snap = (uint64_t)gld(src + pn);
+        else if (fL < 6)
+          snap = (uint64_t)gld(reinterpret_cast<const int64_t*>(fL == 4 ? d.inv10_cpu : d.inv10_mem) + pn);
+        else if (esc && fL == 6)
+          snap = d.has_static_score ? (uint64_t)gld(d.static_score + pn) : 0ULL;
+        else if (esc && fL == 7)
+          snap = d.ntaint ? gld(d.ntaint + pn) : 0ULL;
+        else if (xs_on && fL >= 8) {
+          const uint32_t r0 = (fL - 8) * 2;
+          int32_t h0 = 0, h1 = 0;
+          if (r0 < d.n_scalar)
+            h0 = xhead(gld(d.scalar_cap + (size_t)r0 * d.n_nodes + pn), gld(d.scalar_used + (size_t)r0 * d.n_nodes + pn));
+          if (r0 + 1 < d.n_scalar)
+            h1 = xhead(gld(d.scalar_cap + (size_t)(r0 + 1) * d.n_nodes + pn),
+                       gld(d.scalar_used + (size_t)(r0 + 1) * d.n_nodes + pn));
+          snap = (uint64_t)(uint32_t)h0 | ((uint64_t)(uint32_t)h1 << 32);
+        }
       }
       const uint32_t cS = csv_on ? lane / n_svcs : KSG_NCAND, tS = csv_on ? lane % n_svcs : 0u;
       const uint32_t sv_s = (uint32_t)__shfl((int)rec, (int)min(WS_IDS + nk + n_sel + tS, 63u), 64);
@@ -490,7 +510,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       r_mod[e * 64 + lane] = mv;
       if (lane < DW) r_rec[e * DW + lane] = rec;
       if (lane < KSG_NCAND) r_cand[e * 8 + lane] = cand_l;
-      if (lane < 6 * KSG_NCAND) r_csnap[(e * KSG_NCAND + cL) * 6 + fL] = snap;
+      if (lane < KSG_CSNAP * KSG_NCAND) r_csnap[(e * KSG_NCAND + cL) * KSG_CSNAP + fL] = snap;
       if (cS < KSG_NCAND) r_csv[(e * KSG_NCAND + cS) * KSG_SLOT_SVCS + tS] = scv;
       if (inl && lane < n_svcs) {
         r_svc[e].max[lane] = s_max;
@@ -558,7 +578,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       const PodView ppv = pod_view(prec);
       if (fresh && lane == ol) {  // the new slot's snapshot: staged for a candidate, else from L2
         if (cidx < KSG_NCAND) {
-          const uint64_t* cs = r_csnap + (ep * KSG_NCAND + cidx) * 6;
+          const uint64_t* cs = r_csnap + (ep * KSG_NCAND + cidx) * KSG_CSNAP;
           S.cap_c = (int64_t)cs[0];
           S.cap_m = (int64_t)cs[1];
           S.snp_c = (int64_t)cs[2];
@@ -577,17 +597,19 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         S.dl_c = S.dl_m = 0;
         S.smask = 0;
         S.xk = 0;
-        if (esc) {  // (extension scores) the node's static score and taints
-          S.sst = d.has_static_score ? (int32_t)gld(d.static_score + wn) : 0;
-          S.ntm = d.ntaint ? gld(d.ntaint + wn) : 0ULL;
+        const uint64_t* cs = r_csnap + (ep * KSG_NCAND + (cidx < KSG_NCAND ? cidx : 0u)) * KSG_CSNAP;
+        if (esc) {  // (extension scores) the node's static score and taints: staged for a candidate
+          S.sst = cidx < KSG_NCAND ? (int32_t)cs[6] : d.has_static_score ? (int32_t)gld(d.static_score + wn) : 0;
+          S.ntm = cidx < KSG_NCAND ? cs[7] : d.ntaint ? gld(d.ntaint + wn) : 0ULL;
         }
-        if (xs_on)  // (extensions) the node's extended resource headroom at the snapshot
+        if (xs_on)  // (extensions) the node's extended resource headroom at the snapshot (staged likewise)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             S.xdl[r] = 0;
-            S.xh[r] = (uint32_t)r < d.n_scalar ? xhead(gld(d.scalar_cap + (size_t)r * d.n_nodes + wn),
-                                                       gld(d.scalar_used + (size_t)r * d.n_nodes + wn))
-                                               : 0;
+            S.xh[r] = cidx < KSG_NCAND ? (int32_t)(uint32_t)(cs[8 + (r >> 1)] >> (32 * (r & 1)))
+                      : (uint32_t)r < d.n_scalar ? xhead(gld(d.scalar_cap + (size_t)r * d.n_nodes + wn),
+                                                         gld(d.scalar_used + (size_t)r * d.n_nodes + wn))
+                                                 : 0;
           }
       }
       uint32_t new_mask = 0;
@@ -691,6 +713,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         // T0, the T0 nodes below it: where it joins)
         dpos = r_lp[e * 64 + (wd >> 6) * 2] + r_wp[(size_t)e * P * 64 + wd] +
                (uint32_t)__popcll(tw & ((1ULL << (S.node & 63)) - 1ULL));
+        cstamp(c == 0 ? 22 : 40);  // (KSG_DEBUG & 8, checker 0: the check's loads; lane 40 is dropped)
         if (esc) {
           // (extension scores) the slot's score for pod i now against the snapshot: T0 nodes
           // drop (unfit / below M0) or rise above it; nodes outside T0 that the pod fitted at
@@ -767,6 +790,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
                 lr_win(S.snp_c + pv.req_c, S.cap_c, S.inv_c) + lr_win(S.snp_m + pv.req_m, S.cap_m, S.inv_m);
             drop |= (lr_now >> 1) != (lr_snap >> 1);
           }
+          cstamp(c == 0 ? 23 : 40);  // (checker 0: resources and LeastRequested)
           if (!drop && pv.nk && S.nk)  // PodFitsPorts / NoDiskConflict vs the window's keys
             drop |= R.key_hit(S.nk, rec, pv.nk, pv.n_ports, ports_on, disk_on);
           if (!drop && spread_on && pv.s >= 0 && ((S.smask >> (pv.s & 31)) & 1u)) {
@@ -830,7 +854,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       }
     }
     if constexpr (STAMP) {
-      if (d.dbgbuf && lane >= 16 && lane < 22) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
+      if (d.dbgbuf && lane >= 16 && lane < 24) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
     }
     drain_stores();
     if (lane == 0) st_rel(&ctl->fin[c], 1u);
@@ -996,8 +1020,9 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       const uint32_t c_node = (esc && i > 0 && lane < KSG_NCAND) ? r_cand[ep * 8 + lane] : ~0u;
       if (c_node != ~0u) {
         c_fw = gld(reinterpret_cast<const uint64_t*>(x.buf + x.efit_off) + (size_t)i * x.ostride + (c_node >> 6));
-        c_ntm = d.ntaint ? gld(d.ntaint + d.lo + c_node) : 0ULL;
-        c_sst = d.has_static_score ? (int32_t)gld(d.static_score + d.lo + c_node) : 0;
+        const uint64_t* cs = r_csnap + (ep * KSG_NCAND + lane) * KSG_CSNAP;  // (staged by the producer)
+        c_ntm = cs[7];
+        c_sst = (int32_t)cs[6];
         c_cs = (spread_on && s >= 0) ? gld(d.svc_cnt + (size_t)s * d.n_nodes + d.lo + c_node) : 0;
       }
       for (uint32_t spin = 0;; ++spin) {  // pod i-1's node drawn, or the end
@@ -1038,11 +1063,13 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       // (extensions) lane r < 4: x's headroom of extended resource r at the snapshot
       const bool xk_chk = do_check && xs_on && pv.xm != 0;
       int32_t xhv = 0;
-      if (xk_chk && lane < d.n_scalar)
-        xhv = xhead(gld(d.scalar_cap + (size_t)lane * d.n_nodes + xw), gld(d.scalar_used + (size_t)lane * d.n_nodes + xw));
+      if (xk_chk && lane < d.n_scalar)  // (staged with a candidate's snapshot)
+        xhv = xcid < KSG_NCAND
+                  ? (int32_t)(uint32_t)(r_csnap[(ep * KSG_NCAND + xcid) * KSG_CSNAP + 8 + (lane >> 1)] >> (32 * (lane & 1)))
+                  : xhead(gld(d.scalar_cap + (size_t)lane * d.n_nodes + xw), gld(d.scalar_used + (size_t)lane * d.n_nodes + xw));
       if (do_check) {
         if (xcid < KSG_NCAND) {
-          const uint64_t* cs = r_csnap + (ep * KSG_NCAND + xcid) * 6;
+          const uint64_t* cs = r_csnap + (ep * KSG_NCAND + xcid) * KSG_CSNAP;
           capv = (int64_t)cs[rl];
           usev = (int64_t)cs[2 + rl];
           invv = __longlong_as_double((long long)cs[4 + rl]);
@@ -1305,6 +1332,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
     const uint32_t k0 = __builtin_amdgcn_readfirstlane(r_hdr[e].k0);
     const int32_t pred = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].pred);
+    KSG_STAMPP(13)  // (the head's LDS reads; lane 1: the rest of the head)
     if (__builtin_amdgcn_readlane(rec, WS_ERR) || m0 == KSG_S32_NONE) {
       // ServiceAffinity peer error / nothing fit at the snapshot (commits only
       // remove fits): no draw, no commit
@@ -1372,6 +1400,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     const bool x_kept = !(((xslot < 64 ? msk0 : msk1) >> (xslot & 63)) & 1ULL);
     bool x_drop = have_x && (xres & 1u) && ((t0x >> (xnode & 63)) & 1ULL) && x_kept;
     uint32_t dropped = (xpt & 4u) ? 0u : __builtin_amdgcn_readfirstlane(cc0) + __builtin_amdgcn_readfirstlane(cc1) + (x_drop ? 1u : 0u);
+    KSG_STAMPP(12)  // (the verdicts' LDS reads; lane 3: the select and the node post)
     // (extension scores) risen slots (a score above M0: the ties are among them) and joined
     // ones (non-T0 nodes now at M0: the ties are T0 minus the drops plus them); x's verdict
     // replaces the checkers' for its slot (a BalancedAllocation score moves both ways)

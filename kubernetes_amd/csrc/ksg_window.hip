@@ -125,7 +125,7 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
 
   // ---- node state, once per wave (read-only while phase A runs)
   int64_t capc = 0, capm = 0, usedc = 0, usedm = 0;
-  int32_t sst = 0;
+  int32_t sst = 0;  // (|static score| < 2^30 on this path)
   if (valid) {
     capc = d.cap_cpu[n];
     capm = d.cap_mem[n];
@@ -275,6 +275,7 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
   }
 
   // ---- score every pod of the group on this word
+  const int32_t w_lr = (int32_t)d.w_lr, w_spread = (int32_t)d.w_spread;  // (|w| < 2^30 / 10 on this path)
   int32_t my_max = KSG_S32_NONE;
   uint64_t my_bits = 0, my_fit = 0, my_bz = 0;
   const bool res_on = (P & KSG_PRED_PODFITSRESOURCES) != 0;
@@ -367,31 +368,37 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
         if (d.equal_fallback) {
           sc = 1;  // EqualPriority (generic_scheduler.go:141-143,180-195)
         } else {
-          int64_t s = sst;
+          // int32 arithmetic: the window path runs only while 10 x the summed |weights| plus the
+          // static score stay below KSG_SCORE_BOUND = 2^30 (KsgDev.wide: the exact kernels), so
+          // every term and partial sum here fits and the int64 sum would be the same
+          int32_t s = sst;
           if (d.w_lr) {  // calculateOccupancy (priorities.go:43-76)
             const int64_t tc = (int64_t)((uint64_t)usedc + (uint64_t)rcj);
             const int64_t tm = (int64_t)((uint64_t)usedm + (uint64_t)rmj);
-            s += (int64_t)d.w_lr * ((lr_win(tc, capc, inv_c) + lr_win(tm, capm, inv_m)) >> 1);
+            s += w_lr * ((lr_win(tc, capc, inv_c) + lr_win(tm, capm, inv_m)) >> 1);
           }
           if (d.w_spread) {  // CalculateSpreadPriority (spreading.go:72-86)
             const int32_t mx = __builtin_amdgcn_readlane(smax, j);
-            const int64_t ss = mx > 0 ? frac10_f32((int64_t)mx - cnt[j], mx) : 10;
-            s += (int64_t)d.w_spread * ss;
+            // (no count on this node: (mx - 0) / mx = 1 exactly, 10; the f32 divide only where
+            // a lane of the wave holds pods of the service)
+            int32_t ss = 10;
+            if (mx > 0 && cnt[j] != 0) ss = frac10_i32(mx - cnt[j], mx);
+            s += w_spread * ss;
           }
           if constexpr (EXT) {  // extension scores (parity unpinned; the exact kernels' terms)
             if (d.w_bal) {  // BalancedResourceAllocation, float64 op for op
               const int64_t tc = (int64_t)((uint64_t)usedc + (uint64_t)rcj);
               const int64_t tm = (int64_t)((uint64_t)usedm + (uint64_t)rmj);
-              s += (int64_t)d.w_bal * balanced_score(tc, capc, tm, capm);
+              s += d.w_bal * (int32_t)balanced_score(tc, capc, tm, capm);
             }
             if (tt)  // TaintToleration: NormalizeReduce(10, reverse) over the filtered nodes
-              s += (int64_t)d.w_taint * taint_score(__popcll(ntm & readlane64(ps, j)), __builtin_amdgcn_readlane(tmj, j));
+              s += d.w_taint * (int32_t)taint_score(__popcll(ntm & readlane64(ps, j)), __builtin_amdgcn_readlane(tmj, j));
             else if (d.w_taint)
-              s += (int64_t)d.w_taint * 10;
+              s += d.w_taint * 10;
           }
-          base = (int32_t)s;
-          if constexpr (MODE == KSG_WIN_ANTI) s += aterm[j];  // (computed above)
-          sc = (int32_t)s;
+          base = s;
+          if constexpr (MODE == KSG_WIN_ANTI) s += (int32_t)aterm[j];  // (computed above)
+          sc = s;
         }
       }
       int32_t m = wave_total_max(sc);
