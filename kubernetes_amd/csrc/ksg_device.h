@@ -76,6 +76,19 @@ __device__ __forceinline__ int32_t lr_win(int64_t requested, int64_t cap, double
   return qi;
 }
 __device__ __forceinline__ double lr_inv10(int64_t cap) { return cap > 0 ? 10.0 / (double)cap : 0.0; }
+// lr_win without the branch: the integer check runs every time (it changes nothing where q is
+// far from an integer, so the result is lr_win's), and independent calls interleave -- for the
+// latency-bound resolvers; phase A (VALU-bound, the check rarely needed) keeps the branch
+__device__ __forceinline__ int32_t lr_win_nb(int64_t requested, int64_t cap, double inv10) {
+  const bool zero = requested > cap || cap == 0;
+  const int64_t u = cap - requested;
+  int32_t qi = (int32_t)((double)u * inv10);
+  const uint64_t y = (uint64_t)u * 10ULL;
+  const bool up = (uint64_t)(qi + 1) * (uint64_t)cap <= y;
+  const bool dn = !up && (uint64_t)qi * (uint64_t)cap > y;
+  qi += up ? 1 : dn ? -1 : 0;
+  return zero ? 0 : qi;
+}
 
 // int(10 * (float32(num) / float32(den))) with IEEE f32 divide and multiply,
 // no contraction (spreading.go:79-83, 156-160).

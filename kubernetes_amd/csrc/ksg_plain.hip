@@ -738,8 +738,25 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           const bool sp = spread_on && pv.s >= 0 && pv.smax > 0;
           const int64_t fr_snap = (sp && sdel) ? frac10_f32((int64_t)pv.smax - snapc, pv.smax) : 0;
           const int64_t fr_now = (sp && sdel) ? frac10_f32((int64_t)pv.smax - snapc - sdel, pv.smax) : 0;
-          const int64_t dl = es_delta(d, pv.req_c, pv.req_m, S.cap_c, S.cap_m, S.inv_c, S.inv_m, S.snp_c, S.snp_m,
-                                      now_c, now_m, fr_snap, fr_now);
+          // es_delta's and es_snap_score's terms once (the snapshot terms serve both): four
+          // independent LeastRequested terms (branch-free, so they interleave) and two
+          // BalancedAllocation terms
+          const int64_t tcn = (int64_t)((uint64_t)now_c + (uint64_t)pv.req_c), tmn = (int64_t)((uint64_t)now_m + (uint64_t)pv.req_m);
+          const int64_t tcs = (int64_t)((uint64_t)S.snp_c + (uint64_t)pv.req_c), tms = (int64_t)((uint64_t)S.snp_m + (uint64_t)pv.req_m);
+          int32_t lr_n = 0, lr_s = 0;
+          int64_t ba_n = 0, ba_s = 0;
+          if (d.w_lr) {
+            lr_n = (lr_win_nb(tcn, S.cap_c, S.inv_c) + lr_win_nb(tmn, S.cap_m, S.inv_m)) >> 1;
+            lr_s = (lr_win_nb(tcs, S.cap_c, S.inv_c) + lr_win_nb(tms, S.cap_m, S.inv_m)) >> 1;
+          }
+          if (d.w_bal) {
+            ba_n = balanced_score(tcn, S.cap_c, tmn, S.cap_m);
+            ba_s = balanced_score(tcs, S.cap_c, tms, S.cap_m);
+          }
+          int64_t dl = 0;  // (es_delta's sum, term for term)
+          if (d.w_lr) dl += (int64_t)d.w_lr * ((int64_t)lr_n - (int64_t)lr_s);
+          if (d.w_spread) dl += (int64_t)d.w_spread * (fr_now - fr_snap);
+          if (d.w_bal) dl += (int64_t)d.w_bal * (ba_n - ba_s);
           const uint64_t psoft = r_hdr[e].psoft;
           const int32_t tmx = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].tmax);
           const int32_t soft = __popcll(S.ntm & psoft);
@@ -761,8 +778,12 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
               } else {
                 const int32_t cs = sdel ? snapc : e_cs;
                 const int64_t frs = sp ? frac10_f32((int64_t)pv.smax - cs, pv.smax) : 10;
-                const int64_t now = es_snap_score(d, pv.req_c, pv.req_m, S.cap_c, S.cap_m, S.inv_c, S.inv_m, S.snp_c,
-                                                  S.snp_m, frs, S.sst, soft, tmx) + dl;
+                int64_t now = S.sst;  // (es_snap_score's sum from the terms above, then the change)
+                if (d.w_lr) now += (int64_t)d.w_lr * lr_s;
+                if (d.w_spread) now += (int64_t)d.w_spread * frs;
+                if (d.w_bal) now += (int64_t)d.w_bal * ba_s;
+                if (d.w_taint) now += (int64_t)d.w_taint * (d.ntaint ? taint_score(soft, tmx) : 10);
+                now += dl;
                 if (now > m0) {
                   est |= 2u;
                   esig = (int32_t)now;
@@ -785,9 +806,10 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
               drop |= q > 0 && S.xh[r] - S.xdl[r] < q;
             }
           if (d.w_lr) {  // LeastRequested (priorities.go:43-76) can only fall as requested grows
-            const int32_t lr_now = lr_win(now_c + pv.req_c, S.cap_c, S.inv_c) + lr_win(now_m + pv.req_m, S.cap_m, S.inv_m);
+            const int32_t lr_now =
+                lr_win_nb(now_c + pv.req_c, S.cap_c, S.inv_c) + lr_win_nb(now_m + pv.req_m, S.cap_m, S.inv_m);
             const int32_t lr_snap =
-                lr_win(S.snp_c + pv.req_c, S.cap_c, S.inv_c) + lr_win(S.snp_m + pv.req_m, S.cap_m, S.inv_m);
+                lr_win_nb(S.snp_c + pv.req_c, S.cap_c, S.inv_c) + lr_win_nb(S.snp_m + pv.req_m, S.cap_m, S.inv_m);
             drop |= (lr_now >> 1) != (lr_snap >> 1);
           }
           cstamp(c == 0 ? 23 : 40);  // (checker 0: resources and LeastRequested)
@@ -1168,8 +1190,23 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           const bool sp = spread_on && s >= 0 && pv.smax > 0;
           const int64_t fr_snap = (sp && x_cnt_s) ? frac10_f32((int64_t)pv.smax - x_snapc, pv.smax) : 0;
           const int64_t fr_now = (sp && x_cnt_s) ? frac10_f32((int64_t)pv.smax - x_snapc - (int32_t)x_cnt_s, pv.smax) : 0;
-          const int64_t dl = es_delta(d, pv.req_c, pv.req_m, capc, capm, invc, invm, usec, usem, nowc, nowm, fr_snap,
-                                      fr_now);
+          // es_delta / es_snap_score lane-parallel (this wave's chain is the pod's): lanes 0..3 the
+          // LeastRequested terms (cpu / memory, now / at the snapshot), lanes 0 / 1 BalancedAllocation
+          // now / at the snapshot, one pass each instead of six calls one after another
+          const int64_t tcn = (int64_t)((uint64_t)nowc + (uint64_t)pv.req_c), tmn = (int64_t)((uint64_t)nowm + (uint64_t)pv.req_m);
+          const int64_t tcs = (int64_t)((uint64_t)usec + (uint64_t)pv.req_c), tms = (int64_t)((uint64_t)usem + (uint64_t)pv.req_m);
+          const bool l_cpu = (lane & 1) == 0, l_now = lane < 2;
+          const int32_t lrv = d.w_lr ? lr_win_nb(l_now ? (l_cpu ? tcn : tmn) : (l_cpu ? tcs : tms), l_cpu ? capc : capm,
+                                                 l_cpu ? invc : invm)
+                                     : 0;
+          const int32_t bav = d.w_bal ? (int32_t)balanced_score(lane == 0 ? tcn : tcs, capc, lane == 0 ? tmn : tms, capm) : 0;
+          const int32_t lr_n = (__builtin_amdgcn_readlane(lrv, 0) + __builtin_amdgcn_readlane(lrv, 1)) >> 1;
+          const int32_t lr_s = (__builtin_amdgcn_readlane(lrv, 2) + __builtin_amdgcn_readlane(lrv, 3)) >> 1;
+          const int32_t ba_n = __builtin_amdgcn_readlane(bav, 0), ba_s = __builtin_amdgcn_readlane(bav, 1);
+          int64_t dl = 0;  // (es_delta's sum, term for term)
+          if (d.w_lr) dl += (int64_t)d.w_lr * ((int64_t)lr_n - (int64_t)lr_s);
+          if (d.w_spread) dl += (int64_t)d.w_spread * (fr_now - fr_snap);
+          if (d.w_bal) dl += (int64_t)d.w_bal * ((int64_t)ba_n - (int64_t)ba_s);
           const uint64_t psoft = r_hdr[e].psoft;
           const int32_t tmx = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].tmax);
           // x's taints, static score, fit word and service count: prefetched for a candidate
@@ -1205,8 +1242,12 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
                 const int64_t frs = sp ? frac10_f32((int64_t)pv.smax - cs, pv.smax) : 10;
                 const int32_t xsst = cand_x ? __builtin_amdgcn_readlane(c_sst, (int)xcid)
                                             : d.has_static_score ? (int32_t)gld(d.static_score + xw) : 0;
-                const int64_t now =
-                    es_snap_score(d, pv.req_c, pv.req_m, capc, capm, invc, invm, usec, usem, frs, xsst, soft, tmx) + dl;
+                int64_t now = xsst;  // (es_snap_score's sum from the terms above, then the change)
+                if (d.w_lr) now += (int64_t)d.w_lr * lr_s;
+                if (d.w_spread) now += (int64_t)d.w_spread * frs;
+                if (d.w_bal) now += (int64_t)d.w_bal * ba_s;
+                if (d.w_taint) now += (int64_t)d.w_taint * (d.ntaint ? taint_score(soft, tmx) : 10);
+                now += dl;
                 if (now > m0) {
                   es |= 4u;
                   sig = (int32_t)now;

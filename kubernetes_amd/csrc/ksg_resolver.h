@@ -445,6 +445,8 @@ struct RegSlot {
 // max holds): the change of a committed node's score for a pod between the
 // snapshot and now. The static and TaintToleration terms cancel; LeastRequested,
 // ServiceSpreading (frac_* = the spreading scores) and BalancedAllocation move.
+// (The definitions: ksg_plain.hip's checkers and x-checker compute these sums inline from
+// terms they share, the x-checker lane-parallel; tests pin both against the restatement.)
 __device__ __forceinline__ int64_t es_delta(const KsgDev& d, int64_t req_c, int64_t req_m, int64_t cap_c,
                                             int64_t cap_m, double inv_c, double inv_m, int64_t snp_c, int64_t snp_m,
                                             int64_t now_c, int64_t now_m, int64_t frac_snap, int64_t frac_now) {
@@ -452,8 +454,8 @@ __device__ __forceinline__ int64_t es_delta(const KsgDev& d, int64_t req_c, int6
   const int64_t tcn = (int64_t)((uint64_t)now_c + (uint64_t)req_c), tmn = (int64_t)((uint64_t)now_m + (uint64_t)req_m);
   const int64_t tcs = (int64_t)((uint64_t)snp_c + (uint64_t)req_c), tms = (int64_t)((uint64_t)snp_m + (uint64_t)req_m);
   if (d.w_lr)
-    dl += (int64_t)d.w_lr * ((int64_t)((lr_win(tcn, cap_c, inv_c) + lr_win(tmn, cap_m, inv_m)) >> 1) -
-                             (int64_t)((lr_win(tcs, cap_c, inv_c) + lr_win(tms, cap_m, inv_m)) >> 1));
+    dl += (int64_t)d.w_lr * ((int64_t)((lr_win_nb(tcn, cap_c, inv_c) + lr_win_nb(tmn, cap_m, inv_m)) >> 1) -
+                             (int64_t)((lr_win_nb(tcs, cap_c, inv_c) + lr_win_nb(tms, cap_m, inv_m)) >> 1));
   if (d.w_spread) dl += (int64_t)d.w_spread * (frac_now - frac_snap);
   if (d.w_bal) dl += (int64_t)d.w_bal * (balanced_score(tcn, cap_c, tmn, cap_m) - balanced_score(tcs, cap_c, tms, cap_m));
   return dl;
@@ -466,7 +468,7 @@ __device__ __forceinline__ int64_t es_snap_score(const KsgDev& d, int64_t req_c,
                                                  int32_t tmax) {
   int64_t s = sst;
   const int64_t tcs = (int64_t)((uint64_t)snp_c + (uint64_t)req_c), tms = (int64_t)((uint64_t)snp_m + (uint64_t)req_m);
-  if (d.w_lr) s += (int64_t)d.w_lr * ((lr_win(tcs, cap_c, inv_c) + lr_win(tms, cap_m, inv_m)) >> 1);
+  if (d.w_lr) s += (int64_t)d.w_lr * ((lr_win_nb(tcs, cap_c, inv_c) + lr_win_nb(tms, cap_m, inv_m)) >> 1);
   if (d.w_spread) s += (int64_t)d.w_spread * frac_snap;
   if (d.w_bal) s += (int64_t)d.w_bal * balanced_score(tcs, cap_c, tms, cap_m);
   if (d.w_taint) s += (int64_t)d.w_taint * (d.ntaint ? taint_score(soft, tmax) : 10);
