@@ -336,7 +336,7 @@ def main():
     # ksg_set_cluster's rr_dz)
     dbg = int(os.environ.get("KSG_DEBUG", "0") or 0)
     anti = any(int(cfg.w_anti[a]) != 0 for a in range(int(cfg.n_anti)))
-    plain = not anti and not (dbg & 128)  # no ServiceAntiAffinity: the plain resolver (ksg_plain.hip)
+    plain = not anti  # no ServiceAntiAffinity: the plain resolver (ksg_plain.hip)
     if anti:
         pk = np.asarray(view.arrays.pair_keys, np.uint32) & np.uint32(0x7FFFFFFF)
         n_dom = int((pk[1:] == np.uint32(cfg.anti_key[0])).sum()) if len(pk) > 1 else 0

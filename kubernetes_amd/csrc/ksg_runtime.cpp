@@ -707,7 +707,7 @@ bool use_window(ksg_ctx* c, const ksg_pod* pods, uint32_t n) {
   // ServiceAntiAffinity, negative requests and requests past 2^16 take the exact
   // kernels.
   if (c->ext_on) {
-    if (anti_on(c) || (c->dev.dbg & 128)) return false;
+    if (anti_on(c)) return false;
     if (c->ext.w_taint_toleration != 0 && !c->dev.ntaint) return false;
     if (c->cur_ext)
       for (uint32_t i = 0; i < n; ++i)
@@ -2102,7 +2102,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     if ((rc = grow(c, (void**)&c->d_xsend, &c->xsend_cap, x.blk, 1))) return rc;
     if (c->xchg && (rc = grow(c, (void**)&c->d_xrecv, &c->xrecv_cap, x.blk * c->world, 1))) return rc;
     x.buf = c->xchg ? c->d_xrecv : c->d_xsend;
-    const bool plain = !anti && !(c->dev.dbg & 128);  // the plain resolver reads T0 images
+    const bool plain = !anti;  // the plain resolver reads T0 images
     if (plain) {
       x.img_stride = ksg_win_t0_stride(full);
       if ((rc = grow(c, (void**)&c->d_t0img, &c->t0img_cap, (size_t)W * x.img_stride, 1))) return rc;

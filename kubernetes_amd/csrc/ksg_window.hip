@@ -3087,8 +3087,7 @@ uint32_t ksg_win_max_window(const KsgDev& d) {
   if (P == 0) return 0;
   if (d.n_anti > 0 && d.n_domains_total > 0 && P > 8) return 0;  // anti-affinity: up to 32k nodes
   const uint32_t nflag = (d.n_services + 31) / 32;
-  // (KSG_DEBUG & 128 runs the LDS-slot resolver for every configuration)
-  const bool anti = (d.n_anti > 0 && d.n_domains_total > 0) || (d.dbg & 128);
+  const bool anti = d.n_anti > 0 && d.n_domains_total > 0;
   uint32_t lo = 0, hi = 4096;
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1) / 2;
@@ -3137,8 +3136,8 @@ static hipError_t win_resolve2_launch(const KsgDev& d, uint32_t wcap, size_t lds
 hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
                                   const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
   const uint32_t P = win_P(d);
-  if (x.fit_off == 0 && !(d.dbg & 128))  // no ServiceAntiAffinity: the plain resolver (ksg_plain.hip)
-    return ksg_launch_win_plain(d, P, wcap, run, sums, x, rng, out, st);  // (KSG_DEBUG & 128: the LDS-slot one)
+  if (x.fit_off == 0)  // no ServiceAntiAffinity: the plain resolver (ksg_plain.hip)
+    return ksg_launch_win_plain(d, P, wcap, run, sums, x, rng, out, st);
   if (x.fit_off != 0 && x.rr && !(d.dbg & 4096)) {
     // ServiceAntiAffinity with the re-rank: the register-slot resolver
     // (KSG_DEBUG & 4096: the LDS-slot resolver instead, for comparison)
@@ -3165,12 +3164,6 @@ hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run
   if (P == PP && anti == AN)                                                                          \
     return stamp ? win_resolve_launch<PP, true, AN>(d, wcap, lds, run, sums, x, rng, out, st)         \
                  : win_resolve_launch<PP, false, AN>(d, wcap, lds, run, sums, x, rng, out, st);
-  KSG_RES_CASE(1, false)
-  KSG_RES_CASE(2, false)
-  KSG_RES_CASE(4, false)
-  KSG_RES_CASE(8, false)
-  KSG_RES_CASE(16, false)
-  KSG_RES_CASE(32, false)
   KSG_RES_CASE(1, true)
   KSG_RES_CASE(2, true)
   KSG_RES_CASE(4, true)

@@ -49,29 +49,6 @@ def test_batch_matches_oracle(name, nn, npods, window):
     dev.close()
 
 
-@pytest.mark.parametrize("resolver", [128])
-@pytest.mark.parametrize("name,nn,npods", [
-    ("config1", 500, 1000),
-    ("config2", 2000, 3000),
-    ("config3", 1000, 2000),
-    ("config2", 9000, 800),
-])
-def test_alternative_resolvers_match_oracle(name, nn, npods, resolver, monkeypatch):
-    """The LDS-slot resolver (KSG_DEBUG & 128; the default for ServiceAntiAffinity
-    without the re-rank) on configurations the register-slot resolver takes by
-    default gives the oracle's placements too."""
-    monkeypatch.setenv("KSG_DEBUG", str(resolver))
-    case = Case(name, nn, npods)
-    dev, orc = _pair(case, 1024)
-    got, sg = run_batch(dev, case)
-    want, sw = run_batch(orc, case)
-    bad = np.nonzero(got != want)[0]
-    assert bad.size == 0, f"first mismatches at {bad[:8]}: gpu {got[bad[:8]]} oracle {want[bad[:8]]}"
-    assert sg == sw
-    assert dev.last_batch_stats()["windows"] > 0
-    dev.close()
-
-
 @pytest.mark.parametrize("resolver", [2048, 4096])
 @pytest.mark.parametrize("name,nn,npods", [("config4", 900, 1500), ("config4", 5000, 3000)])
 def test_anti_affinity_alternatives_match_oracle(name, nn, npods, resolver, monkeypatch):
