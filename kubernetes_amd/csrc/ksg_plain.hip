@@ -565,16 +565,17 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     // AssumePod of pod p (plugin/pkg/scheduler/scheduler.go:115-118) into the
     // owner lane's slot: requested totals, list lengths (the committer wrote the
     // lists into the table row) and the services' snapshot counts
-    auto apply = [&](uint32_t p) {
-      const uint32_t kind = __builtin_amdgcn_readfirstlane(L_cm[p].kind);
-      const uint32_t slot = __builtin_amdgcn_readfirstlane(L_cm[p].slot);
+    // (cmv: commit p's record, prec_v: pod p's record lane, both read by the caller)
+    auto apply_v = [&](uint32_t p, uint4 cmv, uint32_t prec_v) {
+      const uint32_t kind = __builtin_amdgcn_readfirstlane(cmv.x);
+      const uint32_t slot = __builtin_amdgcn_readfirstlane(cmv.y);
       if (kind != 1 || (slot >> 6) != c) return;
-      const uint32_t woff = __builtin_amdgcn_readfirstlane(L_cm[p].node);
-      const uint32_t fl = __builtin_amdgcn_readfirstlane(L_cm[p].flags);
+      const uint32_t woff = __builtin_amdgcn_readfirstlane(cmv.z);
+      const uint32_t fl = __builtin_amdgcn_readfirstlane(cmv.w);
       const bool fresh = (fl & 1u) != 0;
       const uint32_t cidx = (fl >> 1) & 7u, n_svcs = (fl >> 8) & 0xffu, bns = (fl >> 16) & 0xffu, bnk = fl >> 24;
       const uint32_t ol = slot & 63, ep = p % RING, wn = d.lo + woff;
-      const uint32_t prec = lane < DW ? r_rec[ep * DW + lane] : 0u;
+      const uint32_t prec = lane < DW ? prec_v : 0u;
       const PodView ppv = pod_view(prec);
       if (fresh && lane == ol) {  // the new slot's snapshot: staged for a candidate, else from L2
         if (cidx < KSG_NCAND) {
@@ -637,6 +638,9 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           for (int r = 0; r < 4; ++r) S.xdl[r] += (int32_t)__builtin_amdgcn_readlane(prec, WS_XREQ + r);
         }
       }
+    };
+    auto apply = [&](uint32_t p) {
+      apply_v(p, *reinterpret_cast<const uint4*>(&L_cm[p]), r_rec[(p % RING) * DW + min(lane, DW - 1)]);
     };
 
     uint64_t t_last = 0, t_acc = 0;
@@ -1047,8 +1051,28 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         c_sst = (int32_t)cs[6];
         c_cs = (spread_on && s >= 0) ? gld(d.svc_cnt + (size_t)s * d.n_nodes + d.lo + c_node) : 0;
       }
-      for (uint32_t spin = 0;; ++spin) {  // pod i-1's node drawn, or the end
+      // ahead of the node (pod i-1's candidates are staged): every candidate's snapshot fields
+      // (lane L < 60: candidate L / KSG_CSNAP, field L % KSG_CSNAP) and the snapshot count of
+      // pod i's service among pod i-1's staged service counts (lane c < 6: candidate c), so
+      // that a candidate's check after the node arrives reads them from registers
+      const uint64_t csall = i ? r_csnap[ep * KSG_NCAND * KSG_CSNAP + min(lane, (uint32_t)(KSG_NCAND * KSG_CSNAP - 1))] : 0ULL;
+      uint32_t p_s_first = 0;  // pod i-1's first entry of service s
+      if (i && s >= 0) {
+        const uint32_t pnpp = __builtin_amdgcn_readlane(prec, WS_NPP), pnss = __builtin_amdgcn_readlane(prec, WS_NSS);
+        const uint32_t pnk = (pnpp & 0xffff) + (pnpp >> 16), pnsel = pnss & 0xffff, pns = pnss >> 16;
+        const uint32_t sl = lane - (WS_IDS + pnk + pnsel);
+        const uint64_t hit = __ballot(sl < pns && sl < KSG_SLOT_SVCS && prec == (uint32_t)s);
+        p_s_first = hit ? (uint32_t)__builtin_ctzll(hit) - (WS_IDS + pnk + pnsel) : 0u;
+      }
+      const int32_t csv_c = (i && lane < KSG_NCAND) ? r_csv[(ep * KSG_NCAND + lane) * KSG_SLOT_SVCS + p_s_first] : 0;
+      // pod i-1's node drawn (its word read in the same round as the sequence word: LDS runs
+      // one wave's reads in issue order), or the end
+      uint32_t xv_poll = ~0u;
+      for (uint32_t spin = 0;; ++spin) {
         const uint32_t xn = ld_u(&ctl->xn_seq), st = ld_u(&ctl->stop);
+        asm volatile("" ::: "memory");
+        xv_poll = i ? L_cm[i - 1].xn : ~0u;
+        asm volatile("" ::"v"(xv_poll));  // (read in this round, not moved past the loop)
         if (xn >= i) break;
         if (st) {
           stopped = true;
@@ -1074,7 +1098,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         st_rel(&ctl->xseq, i + 1);
       }
       uint32_t res = 0;
-      const uint32_t xv = i ? __builtin_amdgcn_readfirstlane(L_cm[i - 1].xn) : ~0u;
+      const uint32_t xv = __builtin_amdgcn_readfirstlane(xv_poll);
       const uint32_t xnode = xv == ~0u ? ~0u : xv & 0x0fffffffu, xcid = xv == ~0u ? KSG_NO_CAND : xv >> 28;
       const bool do_check = xnode != ~0u && !__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE;
       const uint32_t xw = d.lo + (do_check ? xnode : 0u);
@@ -1090,11 +1114,14 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
                   ? (int32_t)(uint32_t)(r_csnap[(ep * KSG_NCAND + xcid) * KSG_CSNAP + 8 + (lane >> 1)] >> (32 * (lane & 1)))
                   : xhead(gld(d.scalar_cap + (size_t)lane * d.n_nodes + xw), gld(d.scalar_used + (size_t)lane * d.n_nodes + xw));
       if (do_check) {
-        if (xcid < KSG_NCAND) {
-          const uint64_t* cs = r_csnap + (ep * KSG_NCAND + xcid) * KSG_CSNAP;
-          capv = (int64_t)cs[rl];
-          usev = (int64_t)cs[2 + rl];
-          invv = __longlong_as_double((long long)cs[4 + rl]);
+        if (xcid < KSG_NCAND) {  // (from the registers read ahead of the node)
+          const int b = (int)(xcid * KSG_CSNAP);
+          const uint64_t cap_c = readlane64(csall, b), cap_m = readlane64(csall, b + 1);
+          const uint64_t use_c = readlane64(csall, b + 2), use_m = readlane64(csall, b + 3);
+          const uint64_t inv_c = readlane64(csall, b + 4), inv_m = readlane64(csall, b + 5);
+          capv = (int64_t)(rl ? cap_m : cap_c);
+          usev = (int64_t)(rl ? use_m : use_c);
+          invv = __longlong_as_double((long long)(rl ? inv_m : inv_c));
         } else {
           capv = gld((rl ? d.cap_mem : d.cap_cpu) + xw);
           usev = gld((rl ? d.used_mem : d.used_cpu) + xw);
@@ -1144,8 +1171,8 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         if (x_cnt_s) {
           // s's snapshot count on x: staged with pod i-1's services when pod i-1 is
           // a pod of s, else from L2 (the checkers may not have written it yet)
-          if (prev_ents && p_staged && xcid < KSG_NCAND)
-            x_snapc = r_csv[(ep * KSG_NCAND + xcid) * KSG_SLOT_SVCS + (uint32_t)__builtin_ctzll(prev_ents) - KSG_CL_SV - bns];
+          if (prev_ents && p_staged && xcid < KSG_NCAND)  // (read ahead of the node: p_s_first is that entry)
+            x_snapc = __builtin_amdgcn_readlane(csv_c, (int)xcid);
           else
             x_snapc = gld(d.svc_cnt + (size_t)s * d.n_nodes + xw);
           x_snapc = __builtin_amdgcn_readfirstlane(x_snapc);
@@ -1327,9 +1354,42 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     t_acc += lane == (uint32_t)(k) ? (uint64_t)(v) : 0ULL; \
   }
   if constexpr (STAMP) t_last = __builtin_amdgcn_s_memtime();
+  // the staged pod's entry: record, header, r mod (k0 - d), the row prefixes (lane
+  // q < P), the candidates (lane c < 6), where x sits in T0 -- one round of LDS reads,
+  // issued right behind the read of the entry's ready word (LDS runs one wave's reads in
+  // issue order, so what they return is the staged entry whenever that ready read says
+  // so; a compiler barrier keeps them behind it)
+  struct Head {
+    uint32_t rec, rmod, lp_ex, lp_in, cand, xlp, xwp, m0, k0, pred;
+    uint64_t t0x;
+  };
+  auto head_reads = [&](uint32_t e) -> Head {
+    // (every lane reads, at a clamped index: no exec-mask branch between the reads; the
+    // lanes past each array are masked once the reads are back)
+    Head h;
+    h.rec = r_rec[e * DW + min(lane, DW - 1)];
+    h.rmod = r_mod[e * 64 + lane];
+    h.lp_ex = r_lp[e * 64 + min(lane, (uint32_t)P - 1) * 2];
+    h.lp_in = r_lp[e * 64 + min(lane, (uint32_t)P - 1) * 2 + 1];
+    h.cand = r_cand[e * 8 + min(lane, (uint32_t)KSG_NCAND - 1)];
+    // (read whether or not there is an x: no branch between the reads, the word is
+    // masked once they are back)
+    const uint32_t xw = have_x ? xnode >> 6 : 0u;
+    h.t0x = r_t0[(size_t)e * P * 64 + xw];
+    h.xlp = r_lp[e * 64 + (xw >> 6) * 2];
+    h.xwp = r_wp[(size_t)e * P * 64 + xw];
+    h.m0 = (uint32_t)r_hdr[e].m0;
+    h.k0 = r_hdr[e].k0;
+    h.pred = (uint32_t)r_hdr[e].pred;
+    __builtin_amdgcn_sched_barrier(0);  // (every read issued before any of them is used)
+    return h;
+  };
   for (uint32_t i = 0; i < n_pods; ++i) {
     const uint32_t e = i % RING, par = i & 1;
-    if (ld_u(&r_hdr[e].ready) != i + 1) {
+    const uint32_t rd0 = ld_rlx(&r_hdr[e].ready);
+    asm volatile("" ::: "memory");  // (the entry's reads stay behind the ready read)
+    Head h = head_reads(e);
+    if (__builtin_amdgcn_readfirstlane(rd0) != i + 1) {
       __builtin_amdgcn_s_setprio(0);  // a producer shares this SIMD: do not starve it
       bool hung = false;
       for (uint32_t spin = 0; ld_u(&r_hdr[e].ready) != i + 1; ++spin)
@@ -1343,36 +1403,24 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         reason = KSG_STOP_HANG;
         break;
       }
+      acq_lds();
+      h = head_reads(e);  // (the staged entry, read after the wait)
     }
-    acq_lds();
     if constexpr (STAMP) {  // ring wait of the window's first 4 pods (lane 10) vs the rest (lane 11)
       const uint64_t t_now = __builtin_amdgcn_s_memtime();
       t_acc += lane == (i < 4 ? 10u : 11u) ? t_now - t_last : 0ULL;
     }
     KSG_STAMPP(0)
     if (skew & 1u) __builtin_amdgcn_s_sleep(8);
-    // ---- the staged pod (one round of LDS reads): record, header, r mod
-    // (k0 - d), the row prefixes (lane q < P), the candidates (lane c < 6),
-    // where x sits in T0
-    const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
-    const uint32_t rmod = r_mod[e * 64 + lane];
+    const uint32_t rec = lane < DW ? h.rec : 0u, rmod = h.rmod;
+    const uint32_t lp_ex = lane < P ? h.lp_ex : 0u, lp_in = lane < P ? h.lp_in : 0u;
+    const uint32_t cand = lane < KSG_NCAND ? h.cand : ~0u;
+    const uint32_t xpos0 = have_x ? h.xlp + h.xwp : 0u;
     const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
-    uint32_t lp_ex = 0, lp_in = 0;
-    if (lane < P) {
-      lp_ex = r_lp[e * 64 + lane * 2];
-      lp_in = r_lp[e * 64 + lane * 2 + 1];
-    }
-    const uint32_t cand = lane < KSG_NCAND ? r_cand[e * 8 + lane] : ~0u;
-    uint64_t t0x = 0;
-    uint32_t xpos0 = 0;
-    if (have_x) {
-      const uint32_t xw = xnode >> 6;
-      t0x = t0e[xw];
-      xpos0 = r_lp[e * 64 + (xw >> 6) * 2] + r_wp[(size_t)e * P * 64 + xw];
-    }
-    const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
-    const uint32_t k0 = __builtin_amdgcn_readfirstlane(r_hdr[e].k0);
-    const int32_t pred = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].pred);
+    const uint64_t t0x = have_x ? h.t0x : 0ULL;
+    const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(h.m0);
+    const uint32_t k0 = __builtin_amdgcn_readfirstlane(h.k0);
+    const int32_t pred = (int32_t)__builtin_amdgcn_readfirstlane(h.pred);
     KSG_STAMPP(13)  // (the head's LDS reads; lane 1: the rest of the head)
     if (__builtin_amdgcn_readlane(rec, WS_ERR) || m0 == KSG_S32_NONE) {
       // ServiceAffinity peer error / nothing fit at the snapshot (commits only
@@ -1399,19 +1447,45 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     KSG_STAMPP(1)
     // ---- the checkers' drops (slots as of commits <= i-2) and the x-checker's
     // verdict on commit i-1's node
+    // the verdicts (drop counts and masks, the drops' positions, the x-checker's verdict, the
+    // service flag word) are read in every poll round, right behind the sequence words
+    // (LDS runs one wave's reads in issue order, so the round that finds both sequence words
+    // posted has read the posted verdicts too: no second round of reads after the wait)
+    struct Verd {
+      uint32_t cc0, cc1, xres, fw, m0l, m0h, m1l, m1h, dp0, dp1;
+    };
+    auto verdict_reads = [&]() -> Verd {
+      Verd v;
+      v.cc0 = ctl->chk_cnt[0][par];
+      v.cc1 = ctl->chk_cnt[1][par];
+      v.xres = ctl->xres[par];
+      v.fw = L_flag[(s >= 0 ? (uint32_t)s : 0u) >> 5];
+      v.m0l = ctl->chk_msk[0][par][0];
+      v.m0h = ctl->chk_msk[0][par][1];
+      v.m1l = ctl->chk_msk[1][par][0];
+      v.m1h = ctl->chk_msk[1][par][1];
+      v.dp0 = L_dpos[par * KSG_MAX_SLOTS + lane];
+      v.dp1 = L_dpos[par * KSG_MAX_SLOTS + 64 + lane];
+      return v;
+    };
     bool hung = false;
+    Verd vd;
     for (uint32_t spin = 0;; ++spin) {
       const uint32_t xs = ld_rlx(&ctl->xseq), hg = ld_rlx(&ctl->hang);
       uint32_t cs = ld_rlx(&ctl->chk_seq[0]);
 #pragma unroll
       for (int c = 1; c < KSG_RES_NCHK; ++c) cs = min(cs, ld_rlx(&ctl->chk_seq[c]));
+      asm volatile("" ::: "memory");  // (the verdict reads stay behind the sequence reads)
+      vd = verdict_reads();
+      // (and in this round: the values are inputs here, so the reads are not moved past the loop)
+      asm volatile("" ::"v"(vd.cc0), "v"(vd.cc1), "v"(vd.xres), "v"(vd.fw), "v"(vd.m0l), "v"(vd.m0h), "v"(vd.m1l),
+                   "v"(vd.m1h), "v"(vd.dp0), "v"(vd.dp1));
       if ((cs >= i + 1 && xs >= i + 1) || (xpt & 8u)) break;
       if (spin > 16 * KSG_SPIN_LIMIT || hg) {
         hung = true;
         break;
       }
     }
-    acq_lds();
     if (hung) {
       resolved = i;
       reason = KSG_STOP_HANG;
@@ -1419,17 +1493,12 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     }
     KSG_STAMPP(2)
     if constexpr (STAMP) t_acc += lane == 6 ? (uint64_t)(uint32_t)((uint32_t)t_last - ctl->t_x) : 0ULL;
-    // one round of LDS reads: drop counts and masks, the drops' positions, the
-    // verdict, the service flag word
-    const uint32_t cc0 = ctl->chk_cnt[0][par], cc1 = ctl->chk_cnt[1][par];
-    const uint32_t xres = __builtin_amdgcn_readfirstlane(ctl->xres[par]);
-    const uint32_t fw = s >= 0 ? L_flag[s >> 5] : 0u;
-    uint64_t msk0 = ((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[0][par][1]) << 32) |
-                    (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[0][par][0]);
-    uint64_t msk1 = ((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[1][par][1]) << 32) |
-                    (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_msk[1][par][0]);
-    const uint32_t dp0 = L_dpos[par * KSG_MAX_SLOTS + lane];
-    const uint32_t dp1 = L_dpos[par * KSG_MAX_SLOTS + 64 + lane];
+    const uint32_t cc0 = vd.cc0, cc1 = vd.cc1, fw = vd.fw;
+    const uint32_t xres = __builtin_amdgcn_readfirstlane(vd.xres);
+    uint64_t msk0 = ((uint64_t)__builtin_amdgcn_readfirstlane(vd.m0h) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(vd.m0l);
+    uint64_t msk1 = ((uint64_t)__builtin_amdgcn_readfirstlane(vd.m1h) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(vd.m1l);
+    const uint32_t dp0 = vd.dp0, dp1 = vd.dp1;
+    acq_lds();  // (the ES masks, signs and the drop positions read below: after the wait)
     if (s >= 0 && (spread_on || aff_on) && ((xres & 2u) || ((__builtin_amdgcn_readfirstlane(fw) >> (s & 31)) & 1u))) {
       resolved = i;  // a service scalar this pod reads changed in the window
       reason = KSG_STOP_SERVICE;
