@@ -1051,28 +1051,8 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         c_sst = (int32_t)cs[6];
         c_cs = (spread_on && s >= 0) ? gld(d.svc_cnt + (size_t)s * d.n_nodes + d.lo + c_node) : 0;
       }
-      // ahead of the node (pod i-1's candidates are staged): every candidate's snapshot fields
-      // (lane L < 60: candidate L / KSG_CSNAP, field L % KSG_CSNAP) and the snapshot count of
-      // pod i's service among pod i-1's staged service counts (lane c < 6: candidate c), so
-      // that a candidate's check after the node arrives reads them from registers
-      const uint64_t csall = i ? r_csnap[ep * KSG_NCAND * KSG_CSNAP + min(lane, (uint32_t)(KSG_NCAND * KSG_CSNAP - 1))] : 0ULL;
-      uint32_t p_s_first = 0;  // pod i-1's first entry of service s
-      if (i && s >= 0) {
-        const uint32_t pnpp = __builtin_amdgcn_readlane(prec, WS_NPP), pnss = __builtin_amdgcn_readlane(prec, WS_NSS);
-        const uint32_t pnk = (pnpp & 0xffff) + (pnpp >> 16), pnsel = pnss & 0xffff, pns = pnss >> 16;
-        const uint32_t sl = lane - (WS_IDS + pnk + pnsel);
-        const uint64_t hit = __ballot(sl < pns && sl < KSG_SLOT_SVCS && prec == (uint32_t)s);
-        p_s_first = hit ? (uint32_t)__builtin_ctzll(hit) - (WS_IDS + pnk + pnsel) : 0u;
-      }
-      const int32_t csv_c = (i && lane < KSG_NCAND) ? r_csv[(ep * KSG_NCAND + lane) * KSG_SLOT_SVCS + p_s_first] : 0;
-      // pod i-1's node drawn (its word read in the same round as the sequence word: LDS runs
-      // one wave's reads in issue order), or the end
-      uint32_t xv_poll = ~0u;
-      for (uint32_t spin = 0;; ++spin) {
+      for (uint32_t spin = 0;; ++spin) {  // pod i-1's node drawn, or the end
         const uint32_t xn = ld_u(&ctl->xn_seq), st = ld_u(&ctl->stop);
-        asm volatile("" ::: "memory");
-        xv_poll = i ? L_cm[i - 1].xn : ~0u;
-        asm volatile("" ::"v"(xv_poll));  // (read in this round, not moved past the loop)
         if (xn >= i) break;
         if (st) {
           stopped = true;
@@ -1098,7 +1078,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         st_rel(&ctl->xseq, i + 1);
       }
       uint32_t res = 0;
-      const uint32_t xv = __builtin_amdgcn_readfirstlane(xv_poll);
+      const uint32_t xv = i ? __builtin_amdgcn_readfirstlane(L_cm[i - 1].xn) : ~0u;
       const uint32_t xnode = xv == ~0u ? ~0u : xv & 0x0fffffffu, xcid = xv == ~0u ? KSG_NO_CAND : xv >> 28;
       const bool do_check = xnode != ~0u && !__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE;
       const uint32_t xw = d.lo + (do_check ? xnode : 0u);
@@ -1114,14 +1094,11 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
                   ? (int32_t)(uint32_t)(r_csnap[(ep * KSG_NCAND + xcid) * KSG_CSNAP + 8 + (lane >> 1)] >> (32 * (lane & 1)))
                   : xhead(gld(d.scalar_cap + (size_t)lane * d.n_nodes + xw), gld(d.scalar_used + (size_t)lane * d.n_nodes + xw));
       if (do_check) {
-        if (xcid < KSG_NCAND) {  // (from the registers read ahead of the node)
-          const int b = (int)(xcid * KSG_CSNAP);
-          const uint64_t cap_c = readlane64(csall, b), cap_m = readlane64(csall, b + 1);
-          const uint64_t use_c = readlane64(csall, b + 2), use_m = readlane64(csall, b + 3);
-          const uint64_t inv_c = readlane64(csall, b + 4), inv_m = readlane64(csall, b + 5);
-          capv = (int64_t)(rl ? cap_m : cap_c);
-          usev = (int64_t)(rl ? use_m : use_c);
-          invv = __longlong_as_double((long long)(rl ? inv_m : inv_c));
+        if (xcid < KSG_NCAND) {
+          const uint64_t* cs = r_csnap + (ep * KSG_NCAND + xcid) * KSG_CSNAP;
+          capv = (int64_t)cs[rl];
+          usev = (int64_t)cs[2 + rl];
+          invv = __longlong_as_double((long long)cs[4 + rl]);
         } else {
           capv = gld((rl ? d.cap_mem : d.cap_cpu) + xw);
           usev = gld((rl ? d.used_mem : d.used_cpu) + xw);
@@ -1171,8 +1148,8 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         if (x_cnt_s) {
           // s's snapshot count on x: staged with pod i-1's services when pod i-1 is
           // a pod of s, else from L2 (the checkers may not have written it yet)
-          if (prev_ents && p_staged && xcid < KSG_NCAND)  // (read ahead of the node: p_s_first is that entry)
-            x_snapc = __builtin_amdgcn_readlane(csv_c, (int)xcid);
+          if (prev_ents && p_staged && xcid < KSG_NCAND)
+            x_snapc = r_csv[(ep * KSG_NCAND + xcid) * KSG_SLOT_SVCS + (uint32_t)__builtin_ctzll(prev_ents) - KSG_CL_SV - bns];
           else
             x_snapc = gld(d.svc_cnt + (size_t)s * d.n_nodes + xw);
           x_snapc = __builtin_amdgcn_readfirstlane(x_snapc);
