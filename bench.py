@@ -90,6 +90,7 @@ _STAGES_PLAIN = {
     16: ("checker0", "wait"), 17: ("checker0", "apply"), 18: ("checker0", "check"),
     19: ("checker1", "wait"), 20: ("checker1", "apply"), 21: ("checker1", "check"),
     22: ("checker0", "check_loads"), 23: ("checker0", "check_resources_lr"),  # (check = the rest)
+    14: ("checker0", "ext_fit"), 15: ("checker0", "ext_score"), 9: ("checker0", "ext_verdict"),  # (extension scores)
     24: ("producers_sum_over_waves", "ring_wait"), 25: ("producers_sum_over_waves", "loads"),
     26: ("producers_sum_over_waves", "draw_wait"), 27: ("producers_sum_over_waves", "stage"),
     28: ("xchecker", "wait_node"), 29: ("xchecker", "flags"), 30: ("xchecker", "bookkeeping_and_lists"),

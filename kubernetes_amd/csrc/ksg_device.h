@@ -403,6 +403,11 @@ __device__ __forceinline__ int32_t soft_taints(const KsgDev& d, const PodCtx& c,
 __device__ __forceinline__ int64_t taint_score(int32_t cnt, int32_t mx) {
   return mx == 0 ? 10 : 10 - (10 * (int64_t)cnt) / mx;
 }
+// the same in 32 bits (counts of a node's taints, at most 64): a 32-bit divide instead of
+// the 64-bit one's long expansion, for the resolvers' per-pod chain
+__device__ __forceinline__ int32_t taint_score_i32(int32_t cnt, int32_t mx) {
+  return mx == 0 ? 10 : 10 - (10 * cnt) / mx;
+}
 
 struct PtrLists {
   const uint32_t* ports_;

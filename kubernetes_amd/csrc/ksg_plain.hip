@@ -719,9 +719,11 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
                (uint32_t)__popcll(tw & ((1ULL << (S.node & 63)) - 1ULL));
         cstamp(c == 0 ? 22 : 40);  // (KSG_DEBUG & 8, checker 0: the check's loads; lane 40 is dropped)
         if (esc) {
-          // (extension scores) the slot's score for pod i now against the snapshot: T0 nodes
-          // drop (unfit / below M0) or rise above it; nodes outside T0 that the pod fitted at
-          // the snapshot can reach M0 (join T0) or pass it (BalancedAllocation rises)
+          // (extension scores) the slot's whole score for pod i now (es_snap_score's sum at the
+          // window's totals), against M0, the score every T0 node had at the snapshot: T0 nodes
+          // drop (unfit / below M0) or rise above it; nodes outside T0 that the pod fitted at the
+          // snapshot (so below M0 then) can reach M0 (join T0) or pass it (BalancedAllocation
+          // rises). No snapshot terms: now - M0 is es_delta's sum for a T0 node
           const bool in_t0 = (tw >> (S.node & 63)) & 1ULL;
           const int64_t now_c = (int64_t)((uint64_t)S.snp_c + (uint64_t)S.dl_c);
           const int64_t now_m = (int64_t)((uint64_t)S.snp_m + (uint64_t)S.dl_m);
@@ -739,64 +741,44 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           // ServiceSpreading: the window's entries of the pod's service here (maxCount fixed)
           int32_t snapc = 0, sdel = 0;
           if (spread_on && pv.s >= 0 && ((S.smask >> (pv.s & 31)) & 1u)) R.svc(S.ns, (uint32_t)pv.s, snapc, sdel);
+          cstamp(c == 0 ? 14 : 40);  // (checker 0, extension scores: fit and the window's service entries)
           const bool sp = spread_on && pv.s >= 0 && pv.smax > 0;
-          const int64_t fr_snap = (sp && sdel) ? frac10_f32((int64_t)pv.smax - snapc, pv.smax) : 0;
-          const int64_t fr_now = (sp && sdel) ? frac10_f32((int64_t)pv.smax - snapc - sdel, pv.smax) : 0;
-          // es_delta's and es_snap_score's terms once (the snapshot terms serve both): four
-          // independent LeastRequested terms (branch-free, so they interleave) and two
-          // BalancedAllocation terms
-          const int64_t tcn = (int64_t)((uint64_t)now_c + (uint64_t)pv.req_c), tmn = (int64_t)((uint64_t)now_m + (uint64_t)pv.req_m);
-          const int64_t tcs = (int64_t)((uint64_t)S.snp_c + (uint64_t)pv.req_c), tms = (int64_t)((uint64_t)S.snp_m + (uint64_t)pv.req_m);
-          int32_t lr_n = 0, lr_s = 0;
-          int64_t ba_n = 0, ba_s = 0;
-          if (d.w_lr) {
-            lr_n = (lr_win_nb(tcn, S.cap_c, S.inv_c) + lr_win_nb(tmn, S.cap_m, S.inv_m)) >> 1;
-            lr_s = (lr_win_nb(tcs, S.cap_c, S.inv_c) + lr_win_nb(tms, S.cap_m, S.inv_m)) >> 1;
-          }
-          if (d.w_bal) {
-            ba_n = balanced_score(tcn, S.cap_c, tmn, S.cap_m);
-            ba_s = balanced_score(tcs, S.cap_c, tms, S.cap_m);
-          }
-          int64_t dl = 0;  // (es_delta's sum, term for term)
-          if (d.w_lr) dl += (int64_t)d.w_lr * ((int64_t)lr_n - (int64_t)lr_s);
-          if (d.w_spread) dl += (int64_t)d.w_spread * (fr_now - fr_snap);
-          if (d.w_bal) dl += (int64_t)d.w_bal * (ba_n - ba_s);
           const uint64_t psoft = r_hdr[e].psoft;
           const int32_t tmx = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].tmax);
           const int32_t soft = __popcll(S.ntm & psoft);
           const bool at_max = d.w_taint != 0 && tmx > 0 && soft == tmx;
+          // two independent LeastRequested terms (branch-free, so they interleave), the
+          // BalancedAllocation term, then the service count (its load the last to be waited for)
+          const int64_t tcn = (int64_t)((uint64_t)now_c + (uint64_t)pv.req_c), tmn = (int64_t)((uint64_t)now_m + (uint64_t)pv.req_m);
+          int64_t now = S.sst;
+          if (d.w_lr) now += (int64_t)d.w_lr * ((lr_win_nb(tcn, S.cap_c, S.inv_c) + lr_win_nb(tmn, S.cap_m, S.inv_m)) >> 1);
+          if (d.w_bal) now += (int64_t)d.w_bal * balanced_score(tcn, S.cap_c, tmn, S.cap_m);
+          if (d.w_taint) now += (int64_t)d.w_taint * (d.ntaint ? taint_score_i32(soft, tmx) : 10);
+          if (d.w_spread) now += (int64_t)d.w_spread * (sp ? frac10_i32(pv.smax - (sdel ? snapc : e_cs) - sdel, pv.smax) : 10);
+          cstamp(c == 0 ? 15 : 40);  // (... the score)
           if (in_t0) {
             if (unfit) {
               drop = true;
               if (at_max) est |= 8u;  // (one fewer filtered node at the normalisation max)
-            } else if (dl < 0) {
+            } else if (now < m0) {
               drop = true;
-            } else if (dl > 0) {
+            } else if (now > m0) {
               est |= 2u;
-              esig = (int32_t)(m0 + dl);
+              esig = (int32_t)now;
             }
-          } else if (dl > 0 || (unfit && at_max)) {
+          } else if (unfit ? at_max : now >= m0) {
             if ((e_fw >> (S.node & 63)) & 1ULL) {  // fitted at the snapshot
               if (unfit) {
-                if (at_max) est |= 8u;  // (an unfit node off the max changes nothing)
+                est |= 8u;  // (an unfit node off the max changes nothing)
+              } else if (now > m0) {
+                est |= 2u;
+                esig = (int32_t)now;
               } else {
-                const int32_t cs = sdel ? snapc : e_cs;
-                const int64_t frs = sp ? frac10_f32((int64_t)pv.smax - cs, pv.smax) : 10;
-                int64_t now = S.sst;  // (es_snap_score's sum from the terms above, then the change)
-                if (d.w_lr) now += (int64_t)d.w_lr * lr_s;
-                if (d.w_spread) now += (int64_t)d.w_spread * frs;
-                if (d.w_bal) now += (int64_t)d.w_bal * ba_s;
-                if (d.w_taint) now += (int64_t)d.w_taint * (d.ntaint ? taint_score(soft, tmx) : 10);
-                now += dl;
-                if (now > m0) {
-                  est |= 2u;
-                  esig = (int32_t)now;
-                } else if (now == m0) {
-                  est |= 4u;
-                }
+                est |= 4u;
               }
             }
           }
+          cstamp(c == 0 ? 9 : 40);  // (... the verdict)
         } else if ((tw >> (S.node & 63)) & 1ULL) {
           // does the slot (a snapshot tie of the pod) score below M0 now?
           const int64_t now_c = (int64_t)((uint64_t)S.snp_c + (uint64_t)S.dl_c);
@@ -824,7 +806,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
             int32_t delta = 0, snapc = 0;
             R.svc(S.ns, (uint32_t)pv.s, snapc, delta);
             if (delta)
-              drop = frac10_f32((int64_t)pv.smax - snapc - delta, pv.smax) != frac10_f32((int64_t)pv.smax - snapc, pv.smax);
+              drop = frac10_i32(pv.smax - snapc - delta, pv.smax) != frac10_i32(pv.smax - snapc, pv.smax);
           }
         }
       }
@@ -880,7 +862,8 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       }
     }
     if constexpr (STAMP) {
-      if (d.dbgbuf && lane >= 16 && lane < 24) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
+      if (d.dbgbuf && ((lane >= 16 && lane < 24) || lane == 9 || lane == 14 || lane == 15))
+        atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
     }
     drain_stores();
     if (lane == 0) st_rel(&ctl->fin[c], 1u);
@@ -1105,6 +1088,17 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           invv = gld((rl ? d.inv10_mem : d.inv10_cpu) + xw);
         }
       }
+      // (extension scores) the pod's service count on x at the snapshot (the checkers write
+      // theirs back at the window's end), a non-candidate x's taints, static score and fit word
+      // (a candidate's were staged / read above): in flight over the replay and the check
+      const int32_t n_cs = (esc && do_check && s >= 0) ? gld(d.svc_cnt + (size_t)s * d.n_nodes + xw) : 0;
+      uint64_t n_fw = 0, n_ntm = 0;
+      int32_t n_sst = 0;
+      if (esc && do_check && xcid >= KSG_NCAND) {
+        n_ntm = d.ntaint ? gld(d.ntaint + xw) : 0ULL;
+        n_fw = gld(reinterpret_cast<const uint64_t*>(x.buf + x.efit_off) + (size_t)i * x.ostride + (xnode >> 6));
+        n_sst = d.has_static_score ? (int32_t)gld(d.static_score + xw) : 0;
+      }
       // commit i-1 into its slot (the committer's bookkeeping, replayed)
       uint32_t xslot = 0, bnk = 0, bns = 0, xkinds = 0;
       int32_t xdl[4];
@@ -1139,7 +1133,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         int32_t x_snapc = 0;
         if (res_on && !pv.zero_req)  // PodFitsResources: lanes 0 and 1
           xu = xd = (__ballot(lane < 2 && !(capv == 0 || capv - nowv >= reqv)) & 3ULL) != 0;
-        if (d.w_lr) {  // LeastRequested: one term per lane
+        if (d.w_lr && !esc) {  // LeastRequested: one term per lane (extension scores: below)
           const int32_t lrv = lr_win((lane < 2 ? nowv : usev) + reqv, capv, invv);
           const int32_t lr_now = __builtin_amdgcn_readlane(lrv, 0) + __builtin_amdgcn_readlane(lrv, 1);
           const int32_t lr_snap = __builtin_amdgcn_readlane(lrv, 2) + __builtin_amdgcn_readlane(lrv, 3);
@@ -1151,10 +1145,10 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           if (prev_ents && p_staged && xcid < KSG_NCAND)
             x_snapc = r_csv[(ep * KSG_NCAND + xcid) * KSG_SLOT_SVCS + (uint32_t)__builtin_ctzll(prev_ents) - KSG_CL_SV - bns];
           else
-            x_snapc = gld(d.svc_cnt + (size_t)s * d.n_nodes + xw);
+            x_snapc = esc ? n_cs : gld(d.svc_cnt + (size_t)s * d.n_nodes + xw);
           x_snapc = __builtin_amdgcn_readfirstlane(x_snapc);
-          if (spread_on) {  // ServiceSpreading under an unchanged maxCount: lane 0 now, lane 1 the snapshot
-            const int32_t fr = (int32_t)frac10_f32((int64_t)pv.smax - x_snapc - (lane == 0 ? (int32_t)x_cnt_s : 0),
+          if (spread_on && !esc) {  // ServiceSpreading under an unchanged maxCount: lane 0 now, lane 1 the snapshot
+            const int32_t fr = (int32_t)frac10_i32(pv.smax - x_snapc - (lane == 0 ? (int32_t)x_cnt_s : 0),
                                                    pv.smax);
             xd |= __builtin_amdgcn_readlane(fr, 0) != __builtin_amdgcn_readlane(fr, 1);
           }
@@ -1192,8 +1186,8 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           const double invm = __longlong_as_double((long long)readlane64((uint64_t)__double_as_longlong(invv), 1));
           const int64_t nowc = (int64_t)((uint64_t)usec + dlc), nowm = (int64_t)((uint64_t)usem + dlm);
           const bool sp = spread_on && s >= 0 && pv.smax > 0;
-          const int64_t fr_snap = (sp && x_cnt_s) ? frac10_f32((int64_t)pv.smax - x_snapc, pv.smax) : 0;
-          const int64_t fr_now = (sp && x_cnt_s) ? frac10_f32((int64_t)pv.smax - x_snapc - (int32_t)x_cnt_s, pv.smax) : 0;
+          const int64_t fr_snap = (sp && x_cnt_s) ? frac10_i32(pv.smax - x_snapc, pv.smax) : 0;
+          const int64_t fr_now = (sp && x_cnt_s) ? frac10_i32(pv.smax - x_snapc - (int32_t)x_cnt_s, pv.smax) : 0;
           // es_delta / es_snap_score lane-parallel (this wave's chain is the pod's): lanes 0..3 the
           // LeastRequested terms (cpu / memory, now / at the snapshot), lanes 0 / 1 BalancedAllocation
           // now / at the snapshot, one pass each instead of six calls one after another
@@ -1215,7 +1209,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           const int32_t tmx = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].tmax);
           // x's taints, static score, fit word and service count: prefetched for a candidate
           const bool cand_x = xcid < KSG_NCAND;
-          const uint64_t xntm = cand_x ? readlane64(c_ntm, (int)xcid) : (d.ntaint ? gld(d.ntaint + xw) : 0ULL);
+          const uint64_t xntm = cand_x ? readlane64(c_ntm, (int)xcid) : n_ntm;
           const int32_t soft = __popcll(xntm & psoft);
           const bool at_max = d.w_taint != 0 && tmx > 0 && soft == tmx;
           uint32_t es = 0;
@@ -1232,25 +1226,21 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
               sig = (int32_t)(m0 + dl);
             }
           } else if (dl > 0 || (xu && at_max)) {
-            const uint64_t fw =
-                cand_x ? readlane64(c_fw, (int)xcid)
-                       : gld(reinterpret_cast<const uint64_t*>(x.buf + x.efit_off) + (size_t)i * x.ostride + (xnode >> 6));
+            const uint64_t fw = cand_x ? readlane64(c_fw, (int)xcid) : n_fw;
             if ((fw >> (xnode & 63)) & 1ULL) {  // fitted at the snapshot
               if (xu) {
                 if (at_max) es |= 16u;  // (an unfit node off the max changes nothing)
               } else {
                 const int32_t cs = x_cnt_s ? x_snapc
                                            : !sp ? 0
-                                           : cand_x ? __builtin_amdgcn_readlane(c_cs, (int)xcid)
-                                                    : gld(d.svc_cnt + (size_t)s * d.n_nodes + xw);
-                const int64_t frs = sp ? frac10_f32((int64_t)pv.smax - cs, pv.smax) : 10;
-                const int32_t xsst = cand_x ? __builtin_amdgcn_readlane(c_sst, (int)xcid)
-                                            : d.has_static_score ? (int32_t)gld(d.static_score + xw) : 0;
+                                           : cand_x ? __builtin_amdgcn_readlane(c_cs, (int)xcid) : n_cs;
+                const int64_t frs = sp ? frac10_i32(pv.smax - cs, pv.smax) : 10;
+                const int32_t xsst = cand_x ? __builtin_amdgcn_readlane(c_sst, (int)xcid) : n_sst;
                 int64_t now = xsst;  // (es_snap_score's sum from the terms above, then the change)
                 if (d.w_lr) now += (int64_t)d.w_lr * lr_s;
                 if (d.w_spread) now += (int64_t)d.w_spread * frs;
                 if (d.w_bal) now += (int64_t)d.w_bal * ba_s;
-                if (d.w_taint) now += (int64_t)d.w_taint * (d.ntaint ? taint_score(soft, tmx) : 10);
+                if (d.w_taint) now += (int64_t)d.w_taint * (d.ntaint ? taint_score_i32(soft, tmx) : 10);
                 now += dl;
                 if (now > m0) {
                   es |= 4u;

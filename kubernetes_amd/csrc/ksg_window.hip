@@ -1175,7 +1175,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
         if (mm) {
           const int32_t delta = (int32_t)__popcll(mm);
           const int32_t snapc = __builtin_amdgcn_readlane(ls_scnt, (int)__builtin_ctzll(mm));
-          a_drop = frac10_f32((int64_t)pv.smax - snapc - delta, pv.smax) != frac10_f32((int64_t)pv.smax - snapc, pv.smax);
+          a_drop = frac10_i32(pv.smax - snapc - delta, pv.smax) != frac10_i32(pv.smax - snapc, pv.smax);
         }
       }
       a_drop = __builtin_amdgcn_readfirstlane((int)a_drop) != 0;
@@ -2139,8 +2139,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
                 int32_t delta = 0, snapc = 0;  // ServiceSpreading (spreading.go:72-86) under an unchanged maxCount
                 R.svc(S.ns, (uint32_t)pv.s, snapc, delta);
                 if (delta)
-                  drop = frac10_f32((int64_t)pv.smax - snapc - delta, pv.smax) !=
-                         frac10_f32((int64_t)pv.smax - snapc, pv.smax);
+                  drop = frac10_i32(pv.smax - snapc - delta, pv.smax) !=
+                         frac10_i32(pv.smax - snapc, pv.smax);
               }
               if (drop)
                 atomicOr(reinterpret_cast<unsigned long long*>(L_drop + (size_t)par * P * 64 + wd), nb);
@@ -2208,8 +2208,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
               int32_t delta = 0, snapc = 0;
               R.svc(S.ns, (uint32_t)pv.s, snapc, delta);
               if (delta)
-                drop = frac10_f32((int64_t)pv.smax - snapc - delta, pv.smax) !=
-                       frac10_f32((int64_t)pv.smax - snapc, pv.smax);
+                drop = frac10_i32(pv.smax - snapc - delta, pv.smax) !=
+                       frac10_i32(pv.smax - snapc, pv.smax);
             }
           }
         }
@@ -2480,7 +2480,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         if (x_cnt_s) {
           const int32_t x_snapc = __builtin_amdgcn_readfirstlane(xcv);
           if (spread_on) {  // ServiceSpreading under an unchanged maxCount: lane 0 now, lane 1 the snapshot
-            const int32_t fr = (int32_t)frac10_f32((int64_t)pv.smax - x_snapc - (lane == 0 ? (int32_t)x_cnt_s : 0),
+            const int32_t fr = (int32_t)frac10_i32(pv.smax - x_snapc - (lane == 0 ? (int32_t)x_cnt_s : 0),
                                                    pv.smax);
             xd |= __builtin_amdgcn_readlane(fr, 0) != __builtin_amdgcn_readlane(fr, 1);
           }
