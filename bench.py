@@ -93,7 +93,8 @@ _STAGES_PLAIN = {
     14: ("checker0", "ext_fit"), 15: ("checker0", "ext_score"), 9: ("checker0", "ext_verdict"),  # (extension scores)
     24: ("producers_sum_over_waves", "ring_wait"), 25: ("producers_sum_over_waves", "loads"),
     26: ("producers_sum_over_waves", "draw_wait"), 27: ("producers_sum_over_waves", "stage"),
-    28: ("xchecker", "wait_node"), 29: ("xchecker", "flags"), 30: ("xchecker", "bookkeeping_and_lists"),
+    28: ("xchecker", "wait_node"), 30: ("xchecker", "bookkeeping_and_lists"), 32: ("xchecker", "check"),
+    33: ("xchecker", "ext_score"), 29: ("xchecker", "post_and_flags"),
 }
 
 

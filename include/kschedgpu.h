@@ -337,7 +337,7 @@ int ksg_batch_totals(ksg_ctx* ctx, double* out24);
 
 /* Diagnostics: the window resolver's per-stage clock counters (s_memtime
  * cycles / 64, summed over every window since the context was created) for a
- * context created with KSG_DEBUG=8 in the environment; out32[32] (layout:
+ * context created with KSG_DEBUG=8 in the environment; out32[64] (layout:
  * DESIGN.md section 4, "resolver stages"). KSG_ERR_STATE when not enabled. */
 int ksg_debug_counters(ksg_ctx* ctx, int32_t* out32);
 

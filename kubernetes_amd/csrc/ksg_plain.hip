@@ -1017,6 +1017,9 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
       const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
       const int32_t peer0 = __builtin_amdgcn_readfirstlane(r_svc[e].peer[0]);
+      // (extension scores) the pod's PreferNoSchedule taints and TaintToleration max, ahead of the node
+      const uint64_t x_psoft = esc ? r_hdr[e].psoft : 0ULL;
+      const int32_t x_tmx = esc ? (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].tmax) : 0;
       const uint32_t prec = (i && lane < DW) ? r_rec[ep * DW + lane] : 0u;
       const bool p_staged = i && r_hdr[ep].pad != 0;
       const PodView pv = pod_view(rec);
@@ -1088,10 +1091,12 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           invv = gld((rl ? d.inv10_mem : d.inv10_cpu) + xw);
         }
       }
-      // (extension scores) the pod's service count on x at the snapshot (the checkers write
-      // theirs back at the window's end), a non-candidate x's taints, static score and fit word
-      // (a candidate's were staged / read above): in flight over the replay and the check
-      const int32_t n_cs = (esc && do_check && s >= 0) ? gld(d.svc_cnt + (size_t)s * d.n_nodes + xw) : 0;
+      // (extension scores) a non-candidate x's service count at the snapshot (the checkers write
+      // theirs back at the window's end), taints, static score and fit word (a candidate's were
+      // staged / read before the node: no load is waited for on the chain then): in flight over
+      // the replay and the check
+      const int32_t n_cs = (esc && do_check && s >= 0 && xcid >= KSG_NCAND) ? gld(d.svc_cnt + (size_t)s * d.n_nodes + xw) : 0;
+      const uint64_t x_t0w = (esc && do_check) ? r_t0[(size_t)e * P * 64 + (xnode >> 6)] : 0ULL;  // (x's T0 word)
       uint64_t n_fw = 0, n_ntm = 0;
       int32_t n_sst = 0;
       if (esc && do_check && xcid >= KSG_NCAND) {
@@ -1145,7 +1150,8 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           if (prev_ents && p_staged && xcid < KSG_NCAND)
             x_snapc = r_csv[(ep * KSG_NCAND + xcid) * KSG_SLOT_SVCS + (uint32_t)__builtin_ctzll(prev_ents) - KSG_CL_SV - bns];
           else
-            x_snapc = esc ? n_cs : gld(d.svc_cnt + (size_t)s * d.n_nodes + xw);
+            x_snapc = !esc ? gld(d.svc_cnt + (size_t)s * d.n_nodes + xw)
+                      : xcid < KSG_NCAND ? __builtin_amdgcn_readlane(c_cs, (int)xcid) : n_cs;
           x_snapc = __builtin_amdgcn_readfirstlane(x_snapc);
           if (spread_on && !esc) {  // ServiceSpreading under an unchanged maxCount: lane 0 now, lane 1 the snapshot
             const int32_t fr = (int32_t)frac10_i32(pv.smax - x_snapc - (lane == 0 ? (int32_t)x_cnt_s : 0),
@@ -1175,11 +1181,15 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           xu |= xh;
         }
         res = (xd ? 1u : 0u) | (flag_x ? 2u : 0u);
+        if constexpr (STAMP) {  // (lane 32: the check before the extension scores)
+          const uint64_t t_now = __builtin_amdgcn_s_memtime();
+          x_acc += lane == 32 ? t_now - x_last : 0ULL;
+          x_last = t_now;
+        }
         if (esc) {
           // (extension scores) x re-scored as the checkers do a slot: bit 0 drop (a T0 node unfit
           // or below M0), 4 rose above M0 (xsig), 8 joined T0, 16 normalisation stop
-          const uint64_t t0w = r_t0[(size_t)e * P * 64 + (xnode >> 6)];
-          const bool in_t0 = (t0w >> (xnode & 63)) & 1ULL;
+          const bool in_t0 = (x_t0w >> (xnode & 63)) & 1ULL;
           const int64_t capc = (int64_t)readlane64((uint64_t)capv, 0), capm = (int64_t)readlane64((uint64_t)capv, 1);
           const int64_t usec = (int64_t)readlane64((uint64_t)usev, 0), usem = (int64_t)readlane64((uint64_t)usev, 1);
           const double invc = __longlong_as_double((long long)readlane64((uint64_t)__double_as_longlong(invv), 0));
@@ -1205,8 +1215,8 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           if (d.w_lr) dl += (int64_t)d.w_lr * ((int64_t)lr_n - (int64_t)lr_s);
           if (d.w_spread) dl += (int64_t)d.w_spread * (fr_now - fr_snap);
           if (d.w_bal) dl += (int64_t)d.w_bal * ((int64_t)ba_n - (int64_t)ba_s);
-          const uint64_t psoft = r_hdr[e].psoft;
-          const int32_t tmx = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].tmax);
+          const uint64_t psoft = x_psoft;
+          const int32_t tmx = x_tmx;
           // x's taints, static score, fit word and service count: prefetched for a candidate
           const bool cand_x = xcid < KSG_NCAND;
           const uint64_t xntm = cand_x ? readlane64(c_ntm, (int)xcid) : n_ntm;
@@ -1252,6 +1262,11 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
             }
           }
           res = (edrop ? 1u : 0u) | (flag_x ? 2u : 0u) | es;
+          if constexpr (STAMP) {  // (lane 33: the extension scores)
+            const uint64_t t_now = __builtin_amdgcn_s_memtime();
+            x_acc += lane == 33 ? t_now - x_last : 0ULL;
+            x_last = t_now;
+          }
           if (lane == 0) ctl->xsig[par] = sig;
         }
       }
@@ -1291,7 +1306,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       flags(q, node, cid, slot, bns, prec);
     }
     if constexpr (STAMP) {
-      if (d.dbgbuf && lane >= 28 && lane < 32) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
+      if (d.dbgbuf && lane >= 28 && lane < 34) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
     }
     if (lane == 0) st_rel(&ctl->fin_x, 1u);
     return;
@@ -1419,8 +1434,14 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     // (LDS runs one wave's reads in issue order, so the round that finds both sequence words
     // posted has read the posted verdicts too: no second round of reads after the wait)
     struct Verd {
-      uint32_t cc0, cc1, xres, fw, m0l, m0h, m1l, m1h, dp0, dp1;
+      uint32_t cc0, cc1, xres, fw, m0l, m0h, m1l, m1h, dp0, dp1, esw;
     };
+    // (extension scores) lane w < 12: word w of the checkers' risen / joined / normalisation-stop
+    // masks (checker w/2 & 1, half w & 1), lane 12 the pod's TaintToleration max count: one read
+    const uint32_t* esp = lane < 4    ? &ctl->chk_rmsk[lane >> 1][par][lane & 1]
+                          : lane < 8  ? &ctl->chk_jmsk[(lane - 4) >> 1][par][lane & 1]
+                          : lane < 12 ? &ctl->chk_nmsk[(lane - 8) >> 1][par][lane & 1]
+                                      : reinterpret_cast<const uint32_t*>(&r_hdr[e].tcnt);
     auto verdict_reads = [&]() -> Verd {
       Verd v;
       v.cc0 = ctl->chk_cnt[0][par];
@@ -1433,6 +1454,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       v.m1h = ctl->chk_msk[1][par][1];
       v.dp0 = L_dpos[par * KSG_MAX_SLOTS + lane];
       v.dp1 = L_dpos[par * KSG_MAX_SLOTS + 64 + lane];
+      v.esw = esc ? *esp : 0u;
       return v;
     };
     bool hung = false;
@@ -1446,7 +1468,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       vd = verdict_reads();
       // (and in this round: the values are inputs here, so the reads are not moved past the loop)
       asm volatile("" ::"v"(vd.cc0), "v"(vd.cc1), "v"(vd.xres), "v"(vd.fw), "v"(vd.m0l), "v"(vd.m0h), "v"(vd.m1l),
-                   "v"(vd.m1h), "v"(vd.dp0), "v"(vd.dp1));
+                   "v"(vd.m1h), "v"(vd.dp0), "v"(vd.dp1), "v"(vd.esw));
       if ((cs >= i + 1 && xs >= i + 1) || (xpt & 8u)) break;
       if (spin > 16 * KSG_SPIN_LIMIT || hg) {
         hung = true;
@@ -1486,24 +1508,22 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     if (esc) {
       const uint64_t xb0 = (have_x && xslot < 64) ? 1ULL << (xslot & 63) : 0ULL;
       const uint64_t xb1 = (have_x && xslot >= 64) ? 1ULL << (xslot & 63) : 0ULL;
-      rm0 = (((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_rmsk[0][par][1]) << 32) |
-             (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_rmsk[0][par][0])) & ~xb0;
-      rm1 = (((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_rmsk[1][par][1]) << 32) |
-             (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_rmsk[1][par][0])) & ~xb1;
-      jm0 = (((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_jmsk[0][par][1]) << 32) |
-             (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_jmsk[0][par][0])) & ~xb0;
-      jm1 = (((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_jmsk[1][par][1]) << 32) |
-             (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_jmsk[1][par][0])) & ~xb1;
+      auto esw64 = [&](int w) -> uint64_t {  // (the poll round's words w, w + 1)
+        return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)vd.esw, w + 1) << 32) |
+               (uint32_t)__builtin_amdgcn_readlane((int)vd.esw, w);
+      };
+      rm0 = esw64(0) & ~xb0;
+      rm1 = esw64(2) & ~xb1;
+      jm0 = esw64(4) & ~xb0;
+      jm1 = esw64(6) & ~xb1;
       msk0 &= ~xb0;
       msk1 &= ~xb1;
       // the TaintToleration max falls once every filtered node at it stopped fitting: the
       // checkers' such slots (x's by the x-checker) against the count pass's node count
-      const uint64_t nm0 = (((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_nmsk[0][par][1]) << 32) |
-                            (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_nmsk[0][par][0])) & ~xb0;
-      const uint64_t nm1 = (((uint64_t)__builtin_amdgcn_readfirstlane(ctl->chk_nmsk[1][par][1]) << 32) |
-                            (uint32_t)__builtin_amdgcn_readfirstlane(ctl->chk_nmsk[1][par][0])) & ~xb1;
+      const uint64_t nm0 = esw64(8) & ~xb0;
+      const uint64_t nm1 = esw64(10) & ~xb1;
       const uint32_t gone = (uint32_t)__popcll(nm0) + (uint32_t)__popcll(nm1) + ((have_x && (xres & 16u)) ? 1u : 0u);
-      const int32_t tcnt = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].tcnt);
+      const int32_t tcnt = __builtin_amdgcn_readlane((int)vd.esw, 12);
       if (gone && (int32_t)gone >= tcnt) {
         resolved = i;  // every filtered node at the pod's TaintToleration max stopped fitting
         reason = KSG_STOP_SERVICE;

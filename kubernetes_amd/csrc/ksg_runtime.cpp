@@ -1517,8 +1517,8 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   // out-of-range payload layout (tests/test_gpu_serve.py: the server must reject it, not fault)
   c->dbg_corrupt = ((uint32_t)d.dbg >> 22) & 3u;
   if (d.dbg & (8 | 32)) {  // (32: the plain resolver's inconsistency record, ksg_plain.hip)
-    (void)hipMalloc(&d.dbgbuf, 128);
-    (void)hipMemset(d.dbgbuf, 0, 128);
+    (void)hipMalloc(&d.dbgbuf, 64 * sizeof(int32_t));
+    (void)hipMemset(d.dbgbuf, 0, 64 * sizeof(int32_t));
   }
   d.has_static_fit = ((c->cfg.predicates & KSG_PRED_LABELSPRESENCE) && c->cfg.n_presence > 0) ? 1 : 0;
   d.cap_cpu = cap_c;
@@ -2378,7 +2378,7 @@ int ksg_debug_counters(ksg_ctx* c, int32_t* out32) {
   if (!c->dev.dbgbuf) return fail(c, KSG_ERR_STATE, "debug counters need KSG_DEBUG=8 at ksg_create");
   (void)hipSetDevice(c->device);
   HIPCHK(c, hipStreamSynchronize(c->st));
-  HIPCHK(c, hipMemcpy(out32, c->dev.dbgbuf, 32 * sizeof(int32_t), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(out32, c->dev.dbgbuf, 64 * sizeof(int32_t), hipMemcpyDeviceToHost));
   return KSG_OK;
 }
 

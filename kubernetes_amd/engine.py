@@ -325,7 +325,7 @@ class DeviceScheduler:
     def debug_counters(self) -> np.ndarray:
         """KSG_DEBUG=8 contexts: the window resolver's per-stage cycle counters
         (cycles / 64, summed over every window so far)."""
-        o = np.zeros(32, np.int32)
+        o = np.zeros(64, np.int32)
         rc = self._lib.ksg_debug_counters(self._ctx, abi.ptr(o))
         if rc != abi.KSG_OK:
             self._err(rc)
