@@ -750,11 +750,11 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           // two independent LeastRequested terms (branch-free, so they interleave), the
           // BalancedAllocation term, then the service count (its load the last to be waited for)
           const int64_t tcn = (int64_t)((uint64_t)now_c + (uint64_t)pv.req_c), tmn = (int64_t)((uint64_t)now_m + (uint64_t)pv.req_m);
-          int64_t now = S.sst;
-          if (d.w_lr) now += (int64_t)d.w_lr * ((lr_win_nb(tcn, S.cap_c, S.inv_c) + lr_win_nb(tmn, S.cap_m, S.inv_m)) >> 1);
-          if (d.w_bal) now += (int64_t)d.w_bal * balanced_score(tcn, S.cap_c, tmn, S.cap_m);
-          if (d.w_taint) now += (int64_t)d.w_taint * (d.ntaint ? taint_score_i32(soft, tmx) : 10);
-          if (d.w_spread) now += (int64_t)d.w_spread * (sp ? frac10_i32(pv.smax - (sdel ? snapc : e_cs) - sdel, pv.smax) : 10);
+          int32_t now = S.sst;  // (int32: every window-path score sum stays below 2^30, use_window)
+          if (d.w_lr) now += (int32_t)d.w_lr * ((lr_win_nb(tcn, S.cap_c, S.inv_c) + lr_win_nb(tmn, S.cap_m, S.inv_m)) >> 1);
+          if (d.w_bal) now += d.w_bal * (int32_t)balanced_score(tcn, S.cap_c, tmn, S.cap_m);
+          if (d.w_taint) now += d.w_taint * (d.ntaint ? taint_score_i32(soft, tmx) : 10);
+          if (d.w_spread) now += (int32_t)d.w_spread * (sp ? frac10_i32(pv.smax - (sdel ? snapc : e_cs) - sdel, pv.smax) : 10);
           cstamp(c == 0 ? 15 : 40);  // (... the score)
           if (in_t0) {
             if (unfit) {
@@ -1196,8 +1196,8 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           const double invm = __longlong_as_double((long long)readlane64((uint64_t)__double_as_longlong(invv), 1));
           const int64_t nowc = (int64_t)((uint64_t)usec + dlc), nowm = (int64_t)((uint64_t)usem + dlm);
           const bool sp = spread_on && s >= 0 && pv.smax > 0;
-          const int64_t fr_snap = (sp && x_cnt_s) ? frac10_i32(pv.smax - x_snapc, pv.smax) : 0;
-          const int64_t fr_now = (sp && x_cnt_s) ? frac10_i32(pv.smax - x_snapc - (int32_t)x_cnt_s, pv.smax) : 0;
+          const int32_t fr_snap = (sp && x_cnt_s) ? frac10_i32(pv.smax - x_snapc, pv.smax) : 0;
+          const int32_t fr_now = (sp && x_cnt_s) ? frac10_i32(pv.smax - x_snapc - (int32_t)x_cnt_s, pv.smax) : 0;
           // es_delta / es_snap_score lane-parallel (this wave's chain is the pod's): lanes 0..3 the
           // LeastRequested terms (cpu / memory, now / at the snapshot), lanes 0 / 1 BalancedAllocation
           // now / at the snapshot, one pass each instead of six calls one after another
@@ -1211,10 +1211,10 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           const int32_t lr_n = (__builtin_amdgcn_readlane(lrv, 0) + __builtin_amdgcn_readlane(lrv, 1)) >> 1;
           const int32_t lr_s = (__builtin_amdgcn_readlane(lrv, 2) + __builtin_amdgcn_readlane(lrv, 3)) >> 1;
           const int32_t ba_n = __builtin_amdgcn_readlane(bav, 0), ba_s = __builtin_amdgcn_readlane(bav, 1);
-          int64_t dl = 0;  // (es_delta's sum, term for term)
-          if (d.w_lr) dl += (int64_t)d.w_lr * ((int64_t)lr_n - (int64_t)lr_s);
-          if (d.w_spread) dl += (int64_t)d.w_spread * (fr_now - fr_snap);
-          if (d.w_bal) dl += (int64_t)d.w_bal * ((int64_t)ba_n - (int64_t)ba_s);
+          int32_t dl = 0;  // (es_delta's sum, term for term; int32: window-path scores stay below 2^30)
+          if (d.w_lr) dl += (int32_t)d.w_lr * (lr_n - lr_s);
+          if (d.w_spread) dl += (int32_t)d.w_spread * (fr_now - fr_snap);
+          if (d.w_bal) dl += d.w_bal * (ba_n - ba_s);
           const uint64_t psoft = x_psoft;
           const int32_t tmx = x_tmx;
           // x's taints, static score, fit word and service count: prefetched for a candidate
@@ -1233,7 +1233,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
               edrop = true;
             } else if (dl > 0) {
               es |= 4u;
-              sig = (int32_t)(m0 + dl);
+              sig = m0 + dl;
             }
           } else if (dl > 0 || (xu && at_max)) {
             const uint64_t fw = cand_x ? readlane64(c_fw, (int)xcid) : n_fw;
@@ -1244,13 +1244,13 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
                 const int32_t cs = x_cnt_s ? x_snapc
                                            : !sp ? 0
                                            : cand_x ? __builtin_amdgcn_readlane(c_cs, (int)xcid) : n_cs;
-                const int64_t frs = sp ? frac10_i32(pv.smax - cs, pv.smax) : 10;
+                const int32_t frs = sp ? frac10_i32(pv.smax - cs, pv.smax) : 10;
                 const int32_t xsst = cand_x ? __builtin_amdgcn_readlane(c_sst, (int)xcid) : n_sst;
-                int64_t now = xsst;  // (es_snap_score's sum from the terms above, then the change)
-                if (d.w_lr) now += (int64_t)d.w_lr * lr_s;
-                if (d.w_spread) now += (int64_t)d.w_spread * frs;
-                if (d.w_bal) now += (int64_t)d.w_bal * ba_s;
-                if (d.w_taint) now += (int64_t)d.w_taint * (d.ntaint ? taint_score_i32(soft, tmx) : 10);
+                int32_t now = xsst;  // (es_snap_score's sum from the terms above, then the change)
+                if (d.w_lr) now += (int32_t)d.w_lr * lr_s;
+                if (d.w_spread) now += (int32_t)d.w_spread * frs;
+                if (d.w_bal) now += d.w_bal * ba_s;
+                if (d.w_taint) now += d.w_taint * (d.ntaint ? taint_score_i32(soft, tmx) : 10);
                 now += dl;
                 if (now > m0) {
                   es |= 4u;
