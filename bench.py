@@ -93,8 +93,12 @@ _STAGES_PLAIN = {
     14: ("checker0", "ext_fit"), 15: ("checker0", "ext_score"), 9: ("checker0", "ext_verdict"),  # (extension scores)
     24: ("producers_sum_over_waves", "ring_wait"), 25: ("producers_sum_over_waves", "loads"),
     26: ("producers_sum_over_waves", "draw_wait"), 27: ("producers_sum_over_waves", "stage"),
-    28: ("xchecker", "wait_node"), 30: ("xchecker", "bookkeeping_and_lists"), 32: ("xchecker", "check"),
-    33: ("xchecker", "ext_score"), 29: ("xchecker", "post_and_flags"),
+    28: ("xchecker", "wait_node"), 32: ("xchecker", "check"),
+    33: ("xchecker", "ext_score"), 29: ("xchecker", "post_and_replay"), 34: ("xchecker", "ring_wait"),
+    39: ("flagger", "wait"), 40: ("flagger", "flags"),
+    # (counts x 64 per pod: commits whose node's verdict the committer took from phase A's
+    # single-commit drop bitmap, and those the x-checker checked)
+    41: ("xchecker", "x_by_committer_x64"), 42: ("xchecker", "x_checked_x64"),
 }
 
 

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define KSG_ABI_VERSION 2
+#define KSG_ABI_VERSION 3
 
 /* ---- return codes ---------------------------------------------------- */
 #define KSG_OK 0
@@ -337,9 +337,14 @@ int ksg_batch_totals(ksg_ctx* ctx, double* out24);
 
 /* Diagnostics: the window resolver's per-stage clock counters (s_memtime
  * cycles / 64, summed over every window since the context was created) for a
- * context created with KSG_DEBUG=8 in the environment; out32[64] (layout:
- * DESIGN.md section 4, "resolver stages"). KSG_ERR_STATE when not enabled. */
-int ksg_debug_counters(ksg_ctx* ctx, int32_t* out32);
+ * context created with KSG_DEBUG=8 in the environment (layout: DESIGN.md
+ * section 4, "resolver stages"). The library holds KSG_DEBUG_COUNTER_WORDS
+ * words; it copies min(n_words, KSG_DEBUG_COUNTER_WORDS) of them into out and
+ * zero-fills the rest of out (ABI version 3: version 2's form took no length
+ * and wrote 64 words into a buffer its parameter name said held 32).
+ * KSG_ERR_STATE when not enabled. */
+#define KSG_DEBUG_COUNTER_WORDS 64
+int ksg_debug_counters(ksg_ctx* ctx, int32_t* out, uint32_t n_words);
 
 /* Diagnostics of the resident begin/commit server: out4[0] kernel launches,
  * [1] requests served (begin, commit, patch, exit), [2] 1 while resident,
@@ -431,10 +436,17 @@ int ksg_admit_pods(ksg_ctx* ctx, const ksg_admission_set* sets, uint32_t n_sets,
  * ScalarResources, priorities TaintTolerationPriority + NormalizeReduce and
  * BalancedResourceAllocation) and PARITY IS UNPINNED (no reference to run or
  * table to check against; the C restatement oracle/ksg_oracle.c is the checker).
- * Off unless ksg_set_extensions enables them, on one rank. Batches take the
- * speculative-window path unless a pod's extended-resource request is outside
- * [0, 2^16] (the exact one-pod-at-a-time kernels then). The reference's own
- * predicates and priorities are unchanged. */
+ * Off unless ksg_set_extensions enables them. On a node-sharded context the node
+ * state is replicated as usual and TaintTolerationPriority's NormalizeReduce max
+ * (over every shard's filtered nodes) is all-reduced (max) before the scores, per
+ * window on the window path and per pod on the per-pod path. Batches take the
+ * speculative-window path (otherwise the exact one-pod-at-a-time kernels) unless
+ *   - a pod's extended-resource request is outside [0, 2^16], or
+ *   - the config has a ServiceAntiAffinity priority, or
+ *   - TaintToleration scores (w_taint_toleration != 0) with max_taints > 64 (the
+ *     window path counts a node's taints as one 64-bit mask),
+ * on top of the window path's general conditions (ksg_set_window). The reference's
+ * own predicates and priorities are unchanged. */
 #define KSG_EXT_TAINTS (1u << 0) /* PodToleratesNodeTaints: NoSchedule / NoExecute taints */
 #define KSG_EXT_SCALAR (1u << 1) /* extended resources: allocatable >= used + request    */
 #define KSG_FAIL_TAINTS 8        /* fail codes after the reference's seven             */
@@ -454,15 +466,17 @@ typedef struct ksg_ext_config {
  * (Toleration.ToleratesTaint: effect empty or equal, key empty or equal,
  * operator Exists or value equal): hard = effect NoSchedule or NoExecute,
  * soft = effect PreferNoSchedule against the tolerations whose effect is empty
- * or PreferNoSchedule. Lists are (offset, count) into the call's id array. */
+ * or PreferNoSchedule. Lists are (offset, count) into the call's id array; each
+ * list is a set (a taint id repeated in one list is rejected with KSG_ERR_ARG:
+ * TaintTolerationPriority counts each untolerated taint of a node once). */
 typedef struct ksg_pod_ext {
   int64_t scalar[KSG_MAX_SCALAR]; /* extended resource requests (0: not requested)   */
   uint32_t hard_off, n_hard;
   uint32_t soft_off, n_soft;
 } ksg_pod_ext;
 
-/* Enable extensions; call before ksg_set_cluster (KSG_ERR_ARG for a sharded
- * context, n_scalar > KSG_MAX_SCALAR). */
+/* Enable extensions; call before ksg_set_cluster (every rank of a sharded
+ * context alike; KSG_ERR_ARG for n_scalar > KSG_MAX_SCALAR). */
 int ksg_set_extensions(ksg_ctx* ctx, const ksg_ext_config* ext);
 /* Per node, after ksg_set_cluster: scalar_cap[r * n_nodes + n] = allocatable of
  * resource r (0: none), node n's taint ids taint_ids[taint_off[n], + taint_n[n]).

@@ -23,6 +23,8 @@ KSG_ERR_STATE = -4
 KSG_ERR_NOPEER = -5
 KSG_ERR_RCCL = -6
 
+KSG_DEBUG_COUNTER_WORDS = 64  # ksg_debug_counters: words the library holds
+
 KSG_OUT_NOFIT = -1
 KSG_OUT_ERROR = -2
 KSG_OUT_NONODES = -3
@@ -263,7 +265,7 @@ def load_library() -> C.CDLL:
         "ksg_last_batch_kernel_ms": (C.c_int, [vp, vp]),
         "ksg_last_batch_host_us": (C.c_int, [vp, vp]),
         "ksg_batch_totals": (C.c_int, [vp, vp]),
-        "ksg_debug_counters": (C.c_int, [vp, vp]),
+        "ksg_debug_counters": (C.c_int, [vp, vp, U32]),
         "ksg_serve_stats": (C.c_int, [vp, vp]),
         "ksg_set_static_terms": (C.c_int, [vp, vp, vp, C.c_int]),
         "ksg_schedule_batch_draws": (C.c_int, [vp, vp, U32, vp, U32, vp, U32, P(U32), vp]),

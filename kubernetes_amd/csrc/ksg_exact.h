@@ -87,7 +87,8 @@ __device__ __forceinline__ SC scan_pod(const KsgDev& d, const PodCtx& c, uint32_
     }
     __syncthreads();
     const int32_t* dc = dglobal ? dglobal : s_dcount;
-    const int32_t tm = tt ? *s_tmax : 0;
+    // (sharded: the all-reduced max over every shard's filtered nodes, after the domain counts)
+    const int32_t tm = tt ? (dglobal ? dglobal[d.n_domains_total] : *s_tmax) : 0;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       SC v = s_score[j * KSG_NT + tid];

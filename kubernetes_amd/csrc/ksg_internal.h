@@ -194,6 +194,14 @@ struct KsgWinXchg {
   // resolver for the next window)
   uint32_t esc;
   uint32_t efit_off;
+  // the plain resolver without extensions, shards of up to 4 x 64 node words per lane
+  // (16,384 nodes): d1 != 0, phase A also writes per (pod i, word) the bitmap of the nodes that
+  // would stop scoring as they do (drop) for pod i if pod i-1 were committed there as the
+  // node's first commit of the window (uint64[wcap][ostride] at d1_off in a block); the
+  // committer answers "does commit i-1's node drop for pod i" from it for such a node
+  // (ksg_plain.hip, x_fast)
+  uint32_t d1;
+  uint32_t d1_off;
   int32_t* tmax;
   uint64_t* psoft;
   // ... and the count pass's histogram of the pods' soft-taint counts over their filtered

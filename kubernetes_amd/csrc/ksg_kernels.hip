@@ -125,9 +125,11 @@ __global__ __launch_bounds__(KSG_NT) void ksg_batch_kernel(KsgDev d, const ksg_p
 // Single-pod scan (begin / evaluate / sharded steps). Writes, per mode:
 //   EVAL : fail code and combined score of every node of the shard
 //   BEGIN: the exchange record {max score, tie count, error, tie words}
-// phase 0: complete pass; phase 1: only ServiceAntiAffinity domain counts
-// (partial over this shard, written to dpart); phase 2: complete pass with
-// all-reduced domain counts read from dglobal.
+// phase 0: complete pass; phase 1: only the terms normalised over every shard's
+// filtered nodes, partial over this shard: ServiceAntiAffinity's domain counts
+// (dpart[0, n_domains_total)) and the extension TaintTolerationPriority's max soft
+// count (dpart[n_domains_total]); phase 2: complete pass with the all-reduced
+// ones read from dglobal (sum of the counts, max of the max).
 // ============================================================================
 template <int R, bool ANTI, typename SC>
 __global__ __launch_bounds__(KSG_NT) void ksg_scan_kernel(KsgDev d, const ksg_pod* __restrict__ pods,
@@ -166,25 +168,28 @@ __global__ __launch_bounds__(KSG_NT) void ksg_scan_kernel(KsgDev d, const ksg_po
       hdr->error = 1;
     }
     if (phase == 1)
-      for (uint32_t k = tid; k < d.n_domains_total; k += KSG_NT) dpart[k] = 0;
+      for (uint32_t k = tid; k <= d.n_domains_total; k += KSG_NT) dpart[k] = 0;
     return;
   }
   const bool lds_dcount = ANTI && phase != 2;
-  if (lds_dcount || ext) {
+  if (lds_dcount || ext || phase == 1) {
     if (lds_dcount)
       for (uint32_t k = tid; k < d.n_domains_total; k += KSG_NT) s_dcount[k] = 0;
     if (tid == 0) *s_tmax = 0;
     __syncthreads();
   }
-  if (ANTI && phase == 1) {
-    // domain counts only (the sharded all-reduce needs them before any score)
+  if (phase == 1) {
+    // the normalised terms' inputs only (the sharded all-reduce needs them before any score)
     scan_pod<R, false, false, SC>(d, c, tid, wave, bit, s_score, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                                   nullptr);
-    const bool need = c.svc >= 0;
+    const bool need = ANTI && c.svc >= 0;
+    const bool tt = d.w_taint != 0 && ext != nullptr && !d.equal_fallback;
+    int32_t tmax = 0;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const uint32_t n = d.lo + j * KSG_NT + tid;
-      if (need && n < d.hi && s_score[j * KSG_NT + tid] != T::none) {
+      const bool fit = n < d.hi && s_score[j * KSG_NT + tid] != T::none;
+      if (need && fit) {
         const int32_t cnt = ld_mut(d.svc_cnt + (size_t)c.svc * d.n_nodes + n);
         if (cnt)
           for (uint32_t a = 0; a < d.n_anti; ++a) {
@@ -192,9 +197,15 @@ __global__ __launch_bounds__(KSG_NT) void ksg_scan_kernel(KsgDev d, const ksg_po
             if (dom >= 0) atomicAdd(&s_dcount[d.anti_dom_off[a] + dom], cnt);
           }
       }
+      if (tt && fit) tmax = max(tmax, soft_taints(d, c, (d.lo >> 6) + j * KSG_NWAVE + wave, bit));
+    }
+    if (tt) {
+      tmax = wave_max_i32(tmax);
+      if (lane == 0) atomicMax(s_tmax, tmax);
     }
     __syncthreads();
-    for (uint32_t k = tid; k < d.n_domains_total; k += KSG_NT) dpart[k] = s_dcount[k];
+    for (uint32_t k = tid; k < d.n_domains_total; k += KSG_NT) dpart[k] = ANTI ? s_dcount[k] : 0;
+    if (tid == 0) dpart[d.n_domains_total] = tt ? *s_tmax : 0;
     return;
   }
   const SC m = scan_pod<R, ANTI, false, SC>(d, c, tid, wave, bit, s_score, lds_dcount ? s_dcount : nullptr,

@@ -11,8 +11,8 @@
 // ix-th node, from the top, of T0 minus the committed nodes ("slots") whose
 // score for pod i fell below M0 ("drops"), ix = Int63() mod (k0 - drops).
 //
-// One workgroup of 8 waves, pipelined over the window's pods:
-//  PRODUCERS (waves 4..7) stage pod j into ring entry j mod RING: its record,
+// One workgroup of 12 waves (8 above 16k nodes), pipelined over the window's pods:
+//  PRODUCERS (waves 5..) stage pod j into ring entry j mod RING: its record,
 //    T0 by word with its prefix counts (T0 bits below each 64-word row and
 //    below each word inside its row: the ascending position of any node in T0
 //    is two LDS reads away), its draw r (splitmix64 at the pod's draw index =
@@ -29,15 +29,21 @@
 //    the dropping slots (a 64-bit mask per checker) and each drop's position in
 //    T0.
 //  X-CHECKER (wave 1) re-checks pod i against the node x of commit i-1 as of
-//    that commit (the checkers' view lags a commit): x's snapshot from the
-//    candidate staging when x is a candidate (LDS; else from L2), x's window
-//    delta and lists from its own replay of the committer's slot bookkeeping
-//    (node -> slot, list lengths, delta) and the table row / pod i-1's record.
-//    It posts "x drops" and "commit i-1 raised a service scalar of the pod",
-//    then applies commit i-1's service flags in commit order (a ServiceSpreading
-//    maxCount rise or a ServiceAffinity first peer ends the window at the next
-//    pod of that service; the window's first peers are recorded for the
-//    write-back).
+//    that commit (the checkers' view lags a commit): x's window delta and lists
+//    from its own replay of the committer's slot bookkeeping (node -> slot, list
+//    lengths, delta; the lists in its own rows L_xr), x's snapshot from the
+//    candidate staging. Round 5: before x is drawn it computes pod i's verdict
+//    on each of pod i-1's six staged candidates as of commit i-1 landing there
+//    (lane-parallel, off the chain), so for a candidate x (the usual case) it
+//    posts "x drops" / "commit i-1 raised a service scalar of the pod" as soon
+//    as x arrives; a non-candidate x (and the extended-resource build) is
+//    checked on arrival as before.
+//  FLAGGER (wave 4) applies each commit's service flags in commit order from
+//    the committer's published records (a ServiceSpreading maxCount rise or a
+//    ServiceAffinity first peer ends the window at the next pod of that
+//    service; the window's first peers are recorded for the write-back); round 4
+//    had the x-checker do this after each post, which kept it busy while the
+//    next node was being drawn.
 //  COMMITTER (wave 0) walks the window in order. Per pod i: the ring entry; the
 //    checkers' drops and the x-checker's verdict; the select: the staged
 //    prediction when nothing dropped, else T0's tp-th node ascending, tp the
@@ -62,16 +68,21 @@
 //   chk_seq[c], chk_msk,   checker c   committer, producers i               chk_seq[c] = i+1 release after
 //    chk_cnt, L_dpos                                                        the mask, count, positions
 //   xres[i & 1]            x-checker   committer           i                xseq = i+1 release after xres
-//   L_flag, L_peer,        x-checker   committer           commits <= i-2   program order in the x-checker,
-//    L_peerset, n_peer                 (reads at pod i)                     xseq >= i+1 acquired by the committer
+//   L_xr rows              x-checker   x-checker           commits <= i-1   program order (one wave)
+//   L_flag, L_peer,        flagger     committer           commits <= i-2   fseq = q+1 release after commit q's,
+//    L_peerset, n_peer                 (reads at pod i)                     fseq >= i-1 acquired by the committer
+//   L_peerset              flagger     x-checker (flag of  commits <= i-2   none: a stale bit only matters when
+//                                      commit i-1)                          commit i-2 set it, and then L_flag
+//                                                                           stops pod i anyway
 //   stop, resolved         committer   all                 —                stop = 1 release after resolved
-//   fin[c], fin_x          checkers,   committer           —                release after the write-back /
-//                          x-checker                                        the last first peers
+//   fin[c], fin_x, fin_f   checkers,   committer           —                release after the write-back /
+//                          x-checker, flagger                               the last first peers
 //
 // Ring entry e = j mod RING is rewritten for pod j once the checkers are done
-// with pod j-RING+2 (they apply commit j-RING while checking it) and the
+// with pod j-RING+2 (they apply commit j-RING while checking it), the
 // x-checker with pod j-RING+1 (it reads pod j-RING's record, candidates and
-// staged counts). The committer reads an entry only for its own pod. Every
+// staged counts) and the flagger with commit j-RING (its record and staged
+// counts). The committer reads an entry only for its own pod. Every
 // wait has a spin limit; a timed-out wait sets ctl->hang and the host fails
 // the batch.
 #include "ksg_resolver.h"
@@ -83,6 +94,17 @@
 // (extension scores) the node's static score and taint mask, (extended resources) the
 // headroom of kinds 0, 1 and of kinds 2, 3 (two int32 each)
 #define KSG_CSNAP 10
+// the x-checker's copy of each slot's lists (keys [0, 8), services [8, 20)), written by its own
+// replay of the commits: it reads them ahead of the committer's table rows being published
+#define KSG_XR_W 20
+// waves of the resolver workgroup: 0 committer, 1 x-checker, 2..3 checkers, 4 flagger (service
+// flags and first peers in commit order), 5.. producers: 12 waves (7 producers), 8 at P = 32,
+// where a producer's T0 copy needs the registers of two waves per SIMD
+__host__ __device__ constexpr uint32_t pl_nt(int P) { return P >= 32 ? 512u : 768u; }
+#define KSG_PL_FW KSG_RES_P0
+#define KSG_PL_P0 (KSG_PL_FW + 1)
+// the resolver's ring holds the d1 bitmaps up to P = 4 (16,384 nodes)
+__host__ __device__ constexpr bool pl_d1(uint32_t P) { return P <= 4; }
 
 // one per window pod; the first 16 bytes are the commit record (stored as one
 // 16-byte write), then the pod's answer and its drawn node (written apart)
@@ -110,8 +132,10 @@ struct alignas(16) PlCtl {
   uint32_t xseq;                         // pods the x-checker is done with
   uint32_t xres[2];                      // its verdict for the pod of parity p: bit 0 x drops, bit 1 flag
   uint32_t xn_seq;                       // pods whose drawn node is posted in L_cm[].xn
-  uint32_t fin_x;                        // the x-checker applied every commit's flags and first peers
+  uint32_t fin_x;                        // the x-checker is done
   uint32_t t_x, t_n;                     // KSG_DEBUG & 8: clock at the xres / xn posts
+  uint32_t fseq;                         // commits the flagger applied the service flags of
+  uint32_t fin_f;                        // the flagger applied every commit's flags and first peers
   // (extension scores) checker c's slots for the pod of parity p whose score ROSE above M0
   // (L_sig: the score) and non-T0 slots that JOINED T0 (L_dpos: their T0 position), and a
   // normalisation stop (a slot the pod fitted at its TaintToleration max no longer fits)
@@ -121,8 +145,8 @@ struct alignas(16) PlCtl {
   int32_t xsig[2];                       // (extension scores) x's score when it rose (xres bit 2)
 };
 struct PlLdsOff {
-  uint32_t ctl, r_hdr, r_t0, r_wp, r_lp, r_rec, r_mod, r_svc, r_cand, r_csnap, r_csv;  // ring
-  uint32_t clist, dpos, sig, cm, peer, pub, drw, flag, peerset;                        // window
+  uint32_t ctl, r_hdr, r_t0, r_wp, r_lp, r_rec, r_mod, r_svc, r_cand, r_csnap, r_csv, r_d1;  // ring
+  uint32_t clist, xrow, dpos, sig, cm, peer, pub, drw, flag, peerset;                  // window
   uint32_t total;
 };
 
@@ -141,9 +165,11 @@ __host__ __device__ inline PlLdsOff plain_lds_offsets(uint32_t P, uint32_t nflag
   o.r_cand = at;  at += win_al16((size_t)R * 8 * 4);            // candidate nodes (~0u: none)
   o.r_csnap = at; at += win_al16((size_t)R * KSG_NCAND * KSG_CSNAP * 8);  // [cand][cap c, m, used c, m, inv c, m, sst, taints]
   o.r_csv = at;   at += win_al16((size_t)R * KSG_NCAND * KSG_SLOT_SVCS * 4);  // [cand][service t] counts
+  o.r_d1 = at;    at += pl_d1(P) ? win_al16((size_t)R * P * 64 * 8) : 0u;   // single-commit drop bitmaps
   // fixed sizes first: every offset up to the commit records is a compile-time
   // constant for a given P (an LDS immediate, not a register the roles' loops keep)
   o.clist = at;   at += win_al16((size_t)KSG_MAX_SLOTS * KSG_CL_W * 4);
+  o.xrow = at;    at += win_al16((size_t)KSG_MAX_SLOTS * KSG_XR_W * 4);  // the x-checker's own slot lists
   o.dpos = at;    at += win_al16((size_t)2 * KSG_MAX_SLOTS * 4);
   o.sig = at;     at += win_al16((size_t)2 * KSG_MAX_SLOTS * 4);    // (extension scores) risen slots' scores
   o.cm = at;      at += win_al16((size_t)W * sizeof(PlCommit));
@@ -163,11 +189,13 @@ __host__ __device__ inline PlLdsOff plain_lds_offsets(uint32_t P, uint32_t nflag
 // ---------------------------------------------------------------------------
 // image of one pod at img + pod * stride: t0 uint64[P*64] (word q*64 + l), wp
 // uint16[P*64] (T0 bits below the word in its row), lp uint32[32][2] (per row:
-// T0 bits below it, up to its end), hdr int32 {m0, k0}
+// T0 bits below it, up to its end), hdr int32 {m0, k0}, and (KsgWinXchg.d1) d1
+// uint64[P*64]: the pod's single-commit drop bitmap by word
 __host__ __device__ constexpr uint32_t t0img_wp(uint32_t P) { return P * 64 * 8; }
 __host__ __device__ constexpr uint32_t t0img_lp(uint32_t P) { return P * 64 * 10; }
 __host__ __device__ constexpr uint32_t t0img_hdr(uint32_t P) { return P * 64 * 10 + 256; }
-__host__ __device__ constexpr uint32_t t0img_stride(uint32_t P) { return (P * 64 * 10 + 256 + 16 + 255) & ~255u; }
+__host__ __device__ constexpr uint32_t t0img_d1(uint32_t P) { return (P * 64 * 10 + 256 + 16 + 15) & ~15u; }
+__host__ __device__ constexpr uint32_t t0img_stride(uint32_t P) { return (t0img_d1(P) + P * 64 * 8 + 255) & ~255u; }
 
 // byte offsets of word w's best-score bitmap and best score in the (gathered)
 // phase-A blocks (KsgWinXchg), ~0u: no such word
@@ -181,6 +209,24 @@ __device__ __forceinline__ void xchg_word_at(const KsgWinXchg& x, uint32_t nword
   const uint32_t base = (uint32_t)(g * x.blk);
   b_at = ok ? base + i * 8 : ~0u;
   m_at = ok ? base + x.wcap * x.ostride * 8 + i * 4 : ~0u;
+}
+
+// (extension scores) pod i's fit word w (phase A's fit bitmaps at efit_off): in the
+// block of the rank that owns word w once the blocks are all-gathered (sharded)
+__device__ __forceinline__ const uint64_t* efit_word(const KsgWinXchg& x, uint32_t i, uint32_t w) {
+  uint32_t g = 0;
+  for (uint32_t r = 1; r < x.world; ++r)
+    if (w >= x.wlo[r] && x.nw[r] > 0) g = r;
+  return reinterpret_cast<const uint64_t*>(x.buf + (size_t)g * x.blk + x.efit_off) + (size_t)i * x.ostride + (w - x.wlo[g]);
+}
+
+// does the pod of resolver record `prec` (lane L holds dword L) list service s among its
+// services (the record's ids after its keys and nodeSelector pairs)? (wave-uniform)
+__device__ __forceinline__ bool pod_has_service(uint32_t prec, int32_t s) {
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const uint32_t npp = __builtin_amdgcn_readlane(prec, WS_NPP), nss = __builtin_amdgcn_readlane(prec, WS_NSS);
+  const uint32_t at = WS_IDS + (npp & 0xffff) + (npp >> 16) + (nss & 0xffff);
+  return s >= 0 && __ballot(lane - at < (nss >> 16) && lane < KSG_WIN_SUM_DWORDS && prec == (uint32_t)s) != 0;
 }
 
 template <int P>
@@ -213,6 +259,17 @@ __global__ __launch_bounds__(256) void ksg_win_t0_kernel(uint32_t nwords, uint32
   uint8_t* im = x.img + (size_t)j * x.img_stride;
   uint64_t* it0 = reinterpret_cast<uint64_t*>(im);
   uint16_t* iwp = reinterpret_cast<uint16_t*>(im + t0img_wp(P));
+  if (pl_d1(P) && x.d1) {  // (the single-commit drop bitmap: copied as it is)
+    uint64_t* id1 = reinterpret_cast<uint64_t*>(im + t0img_d1(P));
+#pragma unroll
+    for (uint32_t k = 0; k < RPW; ++k) {
+      const uint32_t q = wave + 4 * k;
+      if (q >= P) break;  // (wave-uniform)
+      uint32_t b_at = ~0u, m_at = ~0u;
+      xchg_word_at(x, nwords, q * 64 + lane, b_at, m_at);
+      id1[q * 64 + lane] = b_at != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + b_at + x.d1_off + (size_t)j * x.ostride * 8) : 0ULL;
+    }
+  }
 #pragma unroll
   for (uint32_t k = 0; k < RPW; ++k) {
     const uint32_t q = wave + 4 * k;
@@ -248,7 +305,7 @@ __global__ __launch_bounds__(256) void ksg_win_t0_kernel(uint32_t nwords, uint32
 // instantiation: their per-slot state would cost every other configuration
 // registers on the chain)
 template <int P, bool STAMP, bool XS>
-__global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
+__global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
                                                             const KsgWinSum* __restrict__ sums, const KsgWinXchg x,
                                                             uint64_t* rng_io, int32_t* __restrict__ out_batch) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -261,13 +318,14 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t nflag = (d.n_services + 31) / 32;
   constexpr uint32_t RING = win2_ring(P, false);
-  constexpr uint32_t NT = 512;
-  constexpr uint32_t NPW = NT / 64 - KSG_RES_P0;  // producer waves
+  constexpr uint32_t NT = pl_nt(P);
+  constexpr uint32_t NPW = NT / 64 - KSG_PL_P0;  // producer waves
   constexpr uint32_t DW = KSG_WIN_SUM_DWORDS;
   const PlLdsOff o = plain_lds_offsets(P, nflag, wcap);
   PlCtl* ctl = reinterpret_cast<PlCtl*>(smem + o.ctl);
   RingHdr* r_hdr = reinterpret_cast<RingHdr*>(smem + o.r_hdr);
   uint64_t* r_t0 = reinterpret_cast<uint64_t*>(smem + o.r_t0);
+  uint64_t* r_d1 = reinterpret_cast<uint64_t*>(smem + o.r_d1);  // (pl_d1(P): single-commit drop bitmaps)
   uint16_t* r_wp = reinterpret_cast<uint16_t*>(smem + o.r_wp);
   uint32_t* r_lp = reinterpret_cast<uint32_t*>(smem + o.r_lp);
   uint32_t* r_rec = reinterpret_cast<uint32_t*>(smem + o.r_rec);
@@ -286,6 +344,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   uint32_t* L_pub = reinterpret_cast<uint32_t*>(smem + o.pub);  // pods whose drawable bit is known
   uint32_t* L_drw = reinterpret_cast<uint32_t*>(smem + o.drw);  // drawable pods
   uint32_t* L_cl = reinterpret_cast<uint32_t*>(smem + o.clist);  // [slot][KSG_CL_W]
+  uint32_t* L_xr = reinterpret_cast<uint32_t*>(smem + o.xrow);   // [slot][KSG_XR_W] (the x-checker's)
   uint32_t* L_dpos = reinterpret_cast<uint32_t*>(smem + o.dpos);  // [parity][slot] drop positions in T0
   int32_t* L_sig = reinterpret_cast<int32_t*>(smem + o.sig);       // [parity][slot] (extension scores) risen scores
   const bool spread_on = d.w_spread != 0;
@@ -324,7 +383,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   // =========================================================================
   // producers
   // =========================================================================
-  if (wave >= KSG_RES_P0) {
+  if (wave >= KSG_PL_P0) {
     const uint32_t* recs = reinterpret_cast<const uint32_t*>(sums);
     uint64_t p_last = 0, p_acc = 0;  // KSG_DEBUG & 8: lanes 24..27 ring wait, loads, draw wait, the rest
     auto pstamp = [&](uint32_t k) {
@@ -335,17 +394,18 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       }
     };
     if constexpr (STAMP) p_last = __builtin_amdgcn_s_memtime();
-    for (uint32_t j = wave - KSG_RES_P0; j < n_pods; j += NPW) {
+    for (uint32_t j = wave - KSG_PL_P0; j < n_pods; j += NPW) {
       const uint32_t e = j % RING;
       // ring entry free: the checkers applied commit j - RING (while checking
-      // pod j - RING + 2); the x-checker of pod j - RING + 1 read its record
+      // pod j - RING + 2); the x-checker of pod j - RING + 1 read its record; the
+      // flagger applied commit j - RING's flags
       for (uint32_t spin = 0;; ++spin) {
         if (ld_acq(&ctl->stop)) return;
         if (spin > KSG_SPIN_LIMIT) {
           ctl->hang = 1;
           return;
         }
-        uint32_t done = ld_acq(&ctl->xseq);
+        uint32_t done = min(ld_acq(&ctl->xseq), ld_acq(&ctl->fseq) + 2u);
 #pragma unroll
         for (int c = 0; c < KSG_RES_NCHK; ++c) done = min(done, ld_acq(&ctl->chk_seq[c]));
         if (j < RING || done + RING >= j + 3) break;
@@ -358,12 +418,15 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       // then the LDS stores (T0 words, in-row prefixes, row prefixes, m0 / k0)
       const uint8_t* im = x.img + (size_t)j * x.img_stride;
       constexpr uint32_t NT0 = P * 64 * 8 / 16, NWP = P * 64 * 2 / 16;  // 16-byte chunks
-      constexpr uint32_t NC = (NT0 + NWP + 63) / 64;
+      constexpr uint32_t ND1 = pl_d1(P) ? P * 64 * 8 / 16 : 0;             // (the d1 bitmap's, after them)
+      constexpr uint32_t NC = (NT0 + NWP + ND1 + 63) / 64;
+      const uint32_t nch = NT0 + NWP + (x.d1 ? ND1 : 0u);
       uint4 ch[NC];
 #pragma unroll
       for (uint32_t k = 0; k < NC; ++k) {
         const uint32_t t = k * 64 + lane;
-        ch[k] = t < NT0 + NWP ? *reinterpret_cast<const uint4*>(im + (size_t)t * 16) : uint4{0, 0, 0, 0};
+        const uint8_t* src = t < NT0 + NWP ? im + (size_t)t * 16 : im + t0img_d1(P) + (size_t)(t - NT0 - NWP) * 16;
+        ch[k] = t < nch ? *reinterpret_cast<const uint4*>(src) : uint4{0, 0, 0, 0};
       }
       const uint32_t lpv = lane < 2 * P ? *reinterpret_cast<const uint32_t*>(im + t0img_lp(P) + lane * 4) : 0u;
       const int32_t m0 = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int32_t*>(im + t0img_hdr(P)));
@@ -376,11 +439,13 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       }
       uint4* e_t0 = reinterpret_cast<uint4*>(r_t0 + (size_t)e * P * 64);
       uint4* e_wp = reinterpret_cast<uint4*>(r_wp + (size_t)e * P * 64);
+      uint4* e_d1 = reinterpret_cast<uint4*>(r_d1 + (size_t)e * P * 64);
 #pragma unroll
       for (uint32_t k = 0; k < NC; ++k) {
         const uint32_t t = k * 64 + lane;
         if (t < NT0) e_t0[t] = ch[k];
         else if (t < NT0 + NWP) e_wp[t - NT0] = ch[k];
+        else if (t < nch) e_d1[t - NT0 - NWP] = ch[k];
       }
       if (lane < 2 * P) r_lp[e * 64 + lane] = lpv;
       // (the entry is read back below through other pointer types: no
@@ -546,7 +611,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   // =========================================================================
   // checkers (waves KSG_RES_C0 ..): lane l of checker c owns slot 64c + l
   // =========================================================================
-  if (wave >= KSG_RES_C0) {
+  if (wave >= KSG_RES_C0 && wave < KSG_RES_C0 + KSG_RES_NCHK) {
     __builtin_amdgcn_s_setprio(2);
     const uint32_t c = wave - KSG_RES_C0;
     const uint32_t my_slot = c * 64 + lane;
@@ -699,7 +764,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       uint64_t e_fw = 0;
       int32_t e_cs = 0;
       if (esc && S.node != ~0u) {
-        e_fw = gld(reinterpret_cast<const uint64_t*>(x.buf + x.efit_off) + (size_t)i * x.ostride + (S.node >> 6));
+        e_fw = gld(efit_word(x, i, S.node >> 6));
         const int32_t ps = (int32_t)__builtin_amdgcn_readfirstlane(r_rec[e * DW + WS_SVC]);
         if (spread_on && ps >= 0) e_cs = gld(d.svc_cnt + (size_t)ps * d.n_nodes + d.lo + S.node);
       }
@@ -871,9 +936,120 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   }
 
   // =========================================================================
+  // commit q's service flags (a ServiceSpreading maxCount rise: its snapshot count
+  // on the node plus the window's entries there above the snapshot max; a
+  // ServiceAffinity first peer) end the window at the next pod of that service; the
+  // window's first peer of a service is the earliest commit's node. One wave (the
+  // flagger), in commit order, from the committer's published commit records.
+  // =========================================================================
+  auto flags = [&](uint32_t q, uint32_t node, uint32_t cidx, uint32_t slot, uint32_t bns, uint32_t prec) {
+    const uint32_t nss = __builtin_amdgcn_readlane(prec, WS_NSS), npp = __builtin_amdgcn_readlane(prec, WS_NPP);
+    const uint32_t n_svcs = nss >> 16, n_sel = nss & 0xffff, pnk = (npp & 0xffff) + (npp >> 16);
+    if (!n_svcs) return;
+    const uint32_t wn = d.lo + node, eq = q % RING;
+    const bool sv_lane = lane < n_svcs;
+    const uint32_t my_sv =
+        (uint32_t)__shfl((int)prec, (int)min(WS_IDS + pnk + n_sel + (sv_lane ? lane : 0u), 63u), 64);
+    const bool staged = cidx < KSG_NCAND && r_hdr[eq].pad != 0;
+    int32_t mx = 0, peer = 0, cnt = 0;
+    if (sv_lane) {
+      cnt = staged ? r_csv[(eq * KSG_NCAND + cidx) * KSG_SLOT_SVCS + lane] : gld(d.svc_cnt + (size_t)my_sv * d.n_nodes + wn);
+      mx = r_svc[eq].max[lane];
+      peer = r_svc[eq].peer[lane];
+    }
+    // earlier window commits of each service on this node (table lanes KSG_CL_SV..)
+    const uint32_t ent = lane - KSG_CL_SV < bns ? L_cl[(size_t)slot * KSG_CL_W + lane] : ~0u;
+    uint32_t before = 0;
+    for (uint32_t t = 0; t < n_svcs; ++t) {
+      const uint32_t sv_t = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)t);
+      const uint32_t b_t = (uint32_t)__popcll(__ballot(ent == sv_t));
+      if (lane == t) before = b_t;
+    }
+    bool changed = sv_lane && aff_on && peer == -1 && !((L_peerset[my_sv >> 5] >> (my_sv & 31)) & 1u);
+    uint64_t pm = __ballot(sv_lane && peer == -1);
+    if (pm) {  // first commit of a service with no peer yet: its first peer
+      uint32_t n_peer = __builtin_amdgcn_readfirstlane(ctl->n_peer);
+      while (pm) {
+        const uint32_t b = __builtin_ctzll(pm);
+        pm &= pm - 1;
+        const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)b);
+        if (!((L_peerset[fsv >> 5] >> (fsv & 31)) & 1u)) {
+          if (lane == 0) {
+            L_peerset[fsv >> 5] |= 1u << (fsv & 31);
+            L_peer[2 * n_peer] = fsv;
+            L_peer[2 * n_peer + 1] = wn;
+          }
+          ++n_peer;
+          lds_fence();
+        }
+      }
+      if (lane == 0) ctl->n_peer = n_peer;
+    }
+    if (sv_lane && spread_on && cnt + (int32_t)before + 1 > mx) changed = true;  // maxCount rises
+    if (changed) atomicOr(&L_flag[my_sv >> 5], 1u << (my_sv & 31));
+  };
+  if (wave == KSG_PL_FW) {
+    // commit q's record (kind, slot, node, flags) is published with sel_seq > q; the ring
+    // entry of pod q stays until fseq > q (the producers wait for it)
+    auto flag_commit = [&](uint32_t q) {
+      const uint4 cmv = *reinterpret_cast<const uint4*>(&L_cm[q]);
+      if (__builtin_amdgcn_readfirstlane(cmv.x) != 1) return;
+      const uint32_t slot = __builtin_amdgcn_readfirstlane(cmv.y), node = __builtin_amdgcn_readfirstlane(cmv.z);
+      const uint32_t fl = __builtin_amdgcn_readfirstlane(cmv.w);
+      const uint32_t prec = lane < DW ? r_rec[(q % RING) * DW + lane] : 0u;
+      flags(q, node, (fl >> 1) & 7u, slot, (fl >> 16) & 0xffu, prec);
+    };
+    uint64_t f_last = 0, f_acc = 0;  // KSG_DEBUG & 8: lanes 39 wait, 40 flags
+    auto fstamp = [&](uint32_t k) {
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        f_acc += lane == k ? t_now - f_last : 0ULL;
+        f_last = t_now;
+      }
+    };
+    if constexpr (STAMP) f_last = __builtin_amdgcn_s_memtime();
+    uint32_t q = 0;
+    for (;; ++q) {
+      bool stopped = false;
+      for (uint32_t spin = 0;; ++spin) {
+        const uint32_t ss = ld_u(&ctl->sel_seq), st = ld_u(&ctl->stop);
+        if (ss > q) break;
+        if (st) {
+          stopped = true;
+          break;
+        }
+        if (spin > 16 * KSG_SPIN_LIMIT) {
+          ctl->hang = 1;
+          stopped = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      acq_lds();
+      if (stopped) break;
+      if (skew & 2u) __builtin_amdgcn_s_sleep(8);
+      fstamp(39);
+      flag_commit(q);
+      if (lane == 0) st_rel(&ctl->fseq, q + 1);
+      fstamp(40);
+    }
+    // the committer is done: pods [0, resolved) are decided; the first peers of the
+    // commits not applied yet still count (the window's end writes them)
+    const uint32_t R = __builtin_amdgcn_readfirstlane(ctl->resolved);
+    for (; q < R; ++q) flag_commit(q);
+    if constexpr (STAMP) {
+      if (d.dbgbuf && lane >= 39 && lane < 41) atomicAdd(d.dbgbuf + lane, (int32_t)(f_acc / 64));
+    }
+    if (lane == 0) st_rel(&ctl->fin_f, 1u);
+    return;
+  }
+
+  // =========================================================================
   // x-checker (wave 1): pod i against commit i-1's node x as of that commit
-  // (the checkers' view lags a commit), while the committer finishes commit
-  // i-1 and reads pod i; then commit i-1's service flags, in commit order
+  // (the checkers' view lags a commit). Without extended resources (XS) the
+  // verdicts on each of pod i-1's staged candidates are computed BEFORE x is
+  // drawn (x is usually one of them) and the one for x is posted as soon as x
+  // arrives; otherwise, or for a non-candidate x, x is checked on arrival.
   // =========================================================================
   if (wave == 1) {
     __builtin_amdgcn_s_setprio(2);
@@ -881,15 +1057,28 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     // at the node's requested total now (L < 2) or at the snapshot (L >= 2)
     const uint32_t rl = lane & 1;
     // the committer's slot bookkeeping, replayed: lane l holds slots l and 64 + l
-    // (node, list lengths, window delta after the commits replayed so far)
+    // (node, list lengths, window delta after the commits replayed so far); the
+    // slots' lists go into this wave's own rows (L_xr)
     uint32_t xcn0 = ~0u, xcn1 = ~0u, xsk0 = 0, xsk1 = 0, xss0 = 0, xss1 = 0, xn_slots = 0;
     uint32_t xsx0 = 0, xsx1 = 0;  // (extensions) extended resource kinds the window took on the slot
     int32_t xsd0[4] = {0, 0, 0, 0}, xsd1[4] = {0, 0, 0, 0};  // ... and its requests of each kind
     int64_t xdc0 = 0, xdm0 = 0, xdc1 = 0, xdm1 = 0;
+    // KSG_DEBUG & 8: lanes 28 wait for the node, 29 post + replay, 31 node hand-off, 32 / 33
+    // the check / extension scores, 34 ring wait; 41 / 42 (x 64) commits answered from the
+    // d1 bitmap by the committer / checked here
+    uint64_t x_last = 0, x_acc = 0;
+    auto xstamp = [&](uint32_t k) {
+      if constexpr (STAMP) {
+        const uint64_t t_now = __builtin_amdgcn_s_memtime();
+        x_acc += lane == k ? t_now - x_last : 0ULL;
+        x_last = t_now;
+      }
+    };
     auto replay = [&](uint32_t node, uint32_t prec, uint32_t& slot, uint32_t& bnk, uint32_t& bns, uint64_t& dlc,
                       uint64_t& dlm, uint32_t& xk, int32_t (&xd)[4]) {
       const PodView ppv = pod_view(prec);
-      const uint32_t p_svcs = (uint32_t)__builtin_amdgcn_readlane(prec, WS_NSS) >> 16;
+      const uint32_t p_nss = (uint32_t)__builtin_amdgcn_readlane(prec, WS_NSS);
+      const uint32_t p_svcs = p_nss >> 16, p_sel = p_nss & 0xffff;
       const uint64_t hit0 = __ballot(xcn0 == node), hit1 = __ballot(xcn1 == node);
       const bool in_c = (hit0 | hit1) != 0;
       bnk = bns = 0;
@@ -910,6 +1099,13 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         dlm = readlane64((uint64_t)(slot < 64 ? xdm0 : xdm1), (int)sl);
       } else {
         slot = xn_slots < KSG_MAX_SLOTS ? xn_slots++ : 0u;  // (a full table stops the committer)
+      }
+      // the pod's keys and service ids into this wave's row (record lane L holds dword L)
+      {
+        uint32_t* row = L_xr + (size_t)slot * KSG_XR_W;
+        const uint32_t kt = lane - WS_IDS, st_ = lane - (WS_IDS + ppv.nk + p_sel);
+        if (kt < ppv.nk && bnk + kt < KSG_SLOT_KEYS) row[bnk + kt] = prec;
+        if (st_ < p_svcs && bns + st_ < KSG_SLOT_SVCS) row[KSG_SLOT_KEYS + bns + st_] = prec;
       }
       dlc += (uint64_t)ppv.req_c;
       dlm += (uint64_t)ppv.req_m;
@@ -940,58 +1136,6 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         }
       }
     };
-    // commit q of a pod of services sv_t on node x (slot, bns entries before it):
-    // a maxCount rise (its snapshot count on x plus the window's entries there
-    // above the snapshot max) or the service's first peer in the window ends the
-    // window at the next pod of that service; the window's first peer of a
-    // service is the earliest commit's node (one wave, commit order)
-    auto flags = [&](uint32_t q, uint32_t node, uint32_t cidx, uint32_t slot, uint32_t bns, uint32_t prec) {
-      const uint32_t nss = __builtin_amdgcn_readlane(prec, WS_NSS), npp = __builtin_amdgcn_readlane(prec, WS_NPP);
-      const uint32_t n_svcs = nss >> 16, n_sel = nss & 0xffff, pnk = (npp & 0xffff) + (npp >> 16);
-      if (!n_svcs) return;
-      const uint32_t wn = d.lo + node, eq = q % RING;
-      const bool sv_lane = lane < n_svcs;
-      const uint32_t my_sv =
-          (uint32_t)__shfl((int)prec, (int)min(WS_IDS + pnk + n_sel + (sv_lane ? lane : 0u), 63u), 64);
-      const bool staged = cidx < KSG_NCAND && r_hdr[eq].pad != 0;
-      int32_t mx = 0, peer = 0, cnt = 0;
-      if (sv_lane) {
-        cnt = staged ? r_csv[(eq * KSG_NCAND + cidx) * KSG_SLOT_SVCS + lane] : gld(d.svc_cnt + (size_t)my_sv * d.n_nodes + wn);
-        mx = r_svc[eq].max[lane];
-        peer = r_svc[eq].peer[lane];
-      }
-      // earlier window commits of each service on this node (table lanes KSG_CL_SV..)
-      const uint32_t ent = lane - KSG_CL_SV < bns ? L_cl[(size_t)slot * KSG_CL_W + lane] : ~0u;
-      uint32_t before = 0;
-      for (uint32_t t = 0; t < n_svcs; ++t) {
-        const uint32_t sv_t = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)t);
-        const uint32_t b_t = (uint32_t)__popcll(__ballot(ent == sv_t));
-        if (lane == t) before = b_t;
-      }
-      bool changed = sv_lane && aff_on && peer == -1 && !((L_peerset[my_sv >> 5] >> (my_sv & 31)) & 1u);
-      uint64_t pm = __ballot(sv_lane && peer == -1);
-      if (pm) {  // first commit of a service with no peer yet: its first peer
-        uint32_t n_peer = __builtin_amdgcn_readfirstlane(ctl->n_peer);
-        while (pm) {
-          const uint32_t b = __builtin_ctzll(pm);
-          pm &= pm - 1;
-          const uint32_t fsv = (uint32_t)__builtin_amdgcn_readlane((int)my_sv, (int)b);
-          if (!((L_peerset[fsv >> 5] >> (fsv & 31)) & 1u)) {
-            if (lane == 0) {
-              L_peerset[fsv >> 5] |= 1u << (fsv & 31);
-              L_peer[2 * n_peer] = fsv;
-              L_peer[2 * n_peer + 1] = wn;
-            }
-            ++n_peer;
-            lds_fence();
-          }
-        }
-        if (lane == 0) ctl->n_peer = n_peer;
-      }
-      if (sv_lane && spread_on && cnt + (int32_t)before + 1 > mx) changed = true;  // maxCount rises
-      if (changed) atomicOr(&L_flag[my_sv >> 5], 1u << (my_sv & 31));
-    };
-    uint64_t x_last = 0, x_acc = 0;  // KSG_DEBUG & 8: lanes 28..30 wait, check, flags; 31 node hand-off
     if constexpr (STAMP) x_last = __builtin_amdgcn_s_memtime();
     uint32_t i = 0;
     for (; i < n_pods; ++i) {
@@ -1013,6 +1157,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       }
       acq_lds();
       if (stopped) break;
+      xstamp(34);
       // pods i's and i-1's records ahead of the node
       const uint32_t rec = lane < DW ? r_rec[e * DW + lane] : 0u;
       const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(r_hdr[e].m0);
@@ -1024,6 +1169,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       const bool p_staged = i && r_hdr[ep].pad != 0;
       const PodView pv = pod_view(rec);
       const int32_t s = pv.s;
+      const bool chk_pod = !__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE;
       // (extension scores) pod i's fit word, the node taints, static score and service count of
       // each of pod i-1's staged candidates (lane c), in flight while the node is drawn: the
       // drawn node is usually one of them, and its re-score then reads no L2 on the chain
@@ -1031,16 +1177,25 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       int32_t c_sst = 0, c_cs = 0;
       const uint32_t c_node = (esc && i > 0 && lane < KSG_NCAND) ? r_cand[ep * 8 + lane] : ~0u;
       if (c_node != ~0u) {
-        c_fw = gld(reinterpret_cast<const uint64_t*>(x.buf + x.efit_off) + (size_t)i * x.ostride + (c_node >> 6));
+        c_fw = gld(efit_word(x, i, c_node >> 6));
         const uint64_t* cs = r_csnap + (ep * KSG_NCAND + lane) * KSG_CSNAP;  // (staged by the producer)
         c_ntm = cs[7];
         c_sst = (int32_t)cs[6];
         c_cs = (spread_on && s >= 0) ? gld(d.svc_cnt + (size_t)s * d.n_nodes + d.lo + c_node) : 0;
       }
-      for (uint32_t spin = 0;; ++spin) {  // pod i-1's node drawn, or the end
-        const uint32_t xn = ld_u(&ctl->xn_seq), st = ld_u(&ctl->stop);
-        if (xn >= i) break;
-        if (st) {
+      // pod i-1's drawn node: its post and the node, read in one round (one wave's LDS reads
+      // complete in issue order: the round that sees the post has read the node too)
+      uint32_t xv = ~0u;
+      for (uint32_t spin = 0;; ++spin) {
+        const uint32_t xn = ld_rlx(&ctl->xn_seq), st = ld_rlx(&ctl->stop);
+        asm volatile("" ::: "memory");  // (the node read stays behind the post's)
+        const uint32_t xvr = L_cm[i ? i - 1 : 0].xn;
+        asm volatile("" ::"v"(xvr));
+        if (__builtin_amdgcn_readfirstlane(xn) >= i) {
+          xv = i ? (uint32_t)__builtin_amdgcn_readfirstlane(xvr) : ~0u;
+          break;
+        }
+        if (__builtin_amdgcn_readfirstlane(st)) {
           stopped = true;
           break;
         }
@@ -1063,10 +1218,30 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         ctl->xres[par] = 0;
         st_rel(&ctl->xseq, i + 1);
       }
-      uint32_t res = 0;
-      const uint32_t xv = i ? __builtin_amdgcn_readfirstlane(L_cm[i - 1].xn) : ~0u;
       const uint32_t xnode = xv == ~0u ? ~0u : xv & 0x0fffffffu, xcid = xv == ~0u ? KSG_NO_CAND : xv >> 28;
-      const bool do_check = xnode != ~0u && !__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE;
+      uint32_t xslot = 0, bnk = 0, bns = 0, xkinds = 0;
+      int32_t xdl[4];
+      uint64_t dlc = 0, dlm = 0;
+      if (!XS && pl_d1(P) && x.d1 && xnode != ~0u && i > 0 && chk_pod) {  // (the committer's x_fast, alike)
+        // a fresh x (no slot before commit i-1) under a pod i-1 of another service: phase A's
+        // single-commit drop bitmap answers for x, and the committer reads it itself (x_fast);
+        // only the replay is left here (off the chain)
+        const bool fresh = (__ballot(xcn0 == xnode) | __ballot(xcn1 == xnode)) == 0;
+        if (fresh && !pod_has_service(prec, s)) {
+          if (lane == 0) st_rel(&ctl->xseq, i + 1);  // (no verdict: the committer does not read it)
+          replay(xnode, prec, xslot, bnk, bns, dlc, dlm, xkinds, xdl);
+          if constexpr (STAMP) {
+            const uint64_t t_now = __builtin_amdgcn_s_memtime();
+            x_acc += lane == 29 ? t_now - x_last : 0ULL;
+            x_last = t_now;
+            x_acc += lane == 41 ? 64ULL : 0ULL;  // (pods whose x the committer answered)
+          }
+          continue;
+        }
+      }
+      if constexpr (STAMP) x_acc += (lane == 42 && xnode != ~0u && chk_pod) ? 64ULL : 0ULL;  // (x checked on arrival)
+      uint32_t res = 0;
+      const bool do_check = xnode != ~0u && chk_pod;
       const uint32_t xw = d.lo + (do_check ? xnode : 0u);
       // x's snapshot: staged for a candidate (LDS), else from L2 (in flight over
       // the bookkeeping below)
@@ -1101,36 +1276,24 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       int32_t n_sst = 0;
       if (esc && do_check && xcid >= KSG_NCAND) {
         n_ntm = d.ntaint ? gld(d.ntaint + xw) : 0ULL;
-        n_fw = gld(reinterpret_cast<const uint64_t*>(x.buf + x.efit_off) + (size_t)i * x.ostride + (xnode >> 6));
+        n_fw = gld(efit_word(x, i, xnode >> 6));
         n_sst = d.has_static_score ? (int32_t)gld(d.static_score + xw) : 0;
       }
       // commit i-1 into its slot (the committer's bookkeeping, replayed)
-      uint32_t xslot = 0, bnk = 0, bns = 0, xkinds = 0;
-      int32_t xdl[4];
-      uint64_t dlc = 0, dlm = 0;
       if (xnode != ~0u) replay(xnode, prec, xslot, bnk, bns, dlc, dlm, xkinds, xdl);
       if (do_check) {
-        // pod i-1's record: its keys and service ids follow the earlier commits' in the slot's lists
+        // the slot's lists with commit i-1's entries: this wave's row (just written by the replay)
         const uint32_t pnpp = __builtin_amdgcn_readlane(prec, WS_NPP), pnss = __builtin_amdgcn_readlane(prec, WS_NSS);
-        const uint32_t pnk = (pnpp & 0xffff) + (pnpp >> 16), pnsel = pnss & 0xffff, pns = pnss >> 16;
+        const uint32_t pnk = (pnpp & 0xffff) + (pnpp >> 16), pns = pnss >> 16;
         const uint32_t xnk = bnk + pnk, xns = bns + pns;
         // lane t < 8: key t of the slot; lane 8 + u (u < 12): its service u
         const uint32_t kt = lane - KSG_CL_KEY, ut = lane - KSG_CL_SV;
-        const bool from_row = (kt < KSG_SLOT_KEYS && kt < bnk) || (ut < KSG_SLOT_SVCS && ut < bns);
-        const uint32_t src = kt < KSG_SLOT_KEYS ? WS_IDS + (kt - bnk) : WS_IDS + pnk + pnsel + (ut - bns);
-        const uint32_t from_rec = (uint32_t)__shfl((int)prec, (int)min(src, 63u), 64);
-        const uint32_t rowv = from_row ? L_cl[(size_t)xslot * KSG_CL_W + lane] : 0u;
-        const uint32_t xcl = from_row ? rowv : from_rec;
+        const uint32_t xcl = lane < KSG_XR_W ? L_xr[(size_t)xslot * KSG_XR_W + lane] : ~0u;
         const uint32_t nk = pv.nk;
-        const bool s_ent = s >= 0 && ut < xns && xcl == (uint32_t)s;
+        const bool s_ent = s >= 0 && ut < KSG_SLOT_SVCS && ut < xns && xcl == (uint32_t)s;
         const uint64_t ents = __ballot(s_ent);
         const uint32_t x_cnt_s = (uint32_t)__popcll(ents);
         const uint64_t prev_ents = __ballot(s_ent && ut >= bns);  // commit i-1's entries of service s
-        if constexpr (STAMP) {
-          const uint64_t t_now = __builtin_amdgcn_s_memtime();
-          x_acc += lane == 30 ? t_now - x_last : 0ULL;
-          x_last = t_now;
-        }
         const int64_t reqv = rl ? pv.req_m : pv.req_c;
         const int64_t nowv = (int64_t)((uint64_t)usev + (rl ? dlm : dlc));  // requested total now
         bool xd = false, flag_x = false;
@@ -1167,7 +1330,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
           bool hit = false;
           for (uint32_t b = 0; b < nk; ++b) {
             const bool on = b < pv.n_ports ? ports_on : disk_on;
-            hit |= on && kt < xnk && xcl == (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b));
+            hit |= on && kt < KSG_SLOT_KEYS && kt < xnk && xcl == (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)(WS_IDS + b));
           }
           const bool kh = __ballot(hit) != 0;
           xd |= kh;
@@ -1275,38 +1438,14 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
         if constexpr (STAMP) ctl->t_x = (uint32_t)__builtin_amdgcn_s_memtime();
         st_rel(&ctl->xseq, i + 1);
       }
-      // off the chain now: commit i-1's service flags and first peers (the
-      // committer reads them for pod i+1 once this iteration is done)
-      if (xnode != ~0u) flags(i - 1, xnode, xcid, xslot, bns, prec);
       if constexpr (STAMP) {
         const uint64_t t_now = __builtin_amdgcn_s_memtime();
         x_acc += lane == 29 ? t_now - x_last : 0ULL;
         x_last = t_now;
       }
     }
-    // the committer is done: the commits from i-1 on were not replayed yet; their
-    // first peers still count (the window's end writes them)
-    for (uint32_t spin = 0; !ld_acq(&ctl->stop); ++spin) {
-      if (spin > 16 * KSG_SPIN_LIMIT) {
-        ctl->hang = 1;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    const uint32_t R = __builtin_amdgcn_readfirstlane(ctl->resolved);
-    for (uint32_t q = i >= 1 ? i - 1 : 0; q < R; ++q) {
-      if (__builtin_amdgcn_readfirstlane(L_cm[q].kind) != 1) continue;
-      const uint32_t node = __builtin_amdgcn_readfirstlane(L_cm[q].node);
-      const uint32_t cid = (__builtin_amdgcn_readfirstlane(L_cm[q].flags) >> 1) & 7u;
-      const uint32_t prec = lane < DW ? r_rec[(q % RING) * DW + lane] : 0u;
-      uint32_t slot, bnk, bns, xk;
-      int32_t xd[4];
-      uint64_t dlc, dlm;
-      replay(node, prec, slot, bnk, bns, dlc, dlm, xk, xd);
-      flags(q, node, cid, slot, bns, prec);
-    }
     if constexpr (STAMP) {
-      if (d.dbgbuf && lane >= 28 && lane < 34) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
+      if (d.dbgbuf && ((lane >= 28 && lane < 35) || lane == 41 || lane == 42)) atomicAdd(d.dbgbuf + lane, (int32_t)(x_acc / 64));
     }
     if (lane == 0) st_rel(&ctl->fin_x, 1u);
     return;
@@ -1324,6 +1463,12 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   int64_t dc0 = 0, dm0 = 0, dc1 = 0, dm1 = 0;  // their window deltas (current through the last commit)
   bool have_x = false;                   // commit i-1's node x (and its slot)
   uint32_t xnode = 0, xslot = 0;
+  // x took a new slot at commit i-1 (its first commit in the window), and pod i-1's record
+  // lane: with phase A's single-commit drop bitmaps (d1) this wave answers "does x drop for
+  // pod i" itself when pod i-1 is of another service than pod i (x_fast below)
+  bool x_fresh = false;
+  uint32_t xrec = 0;
+  const bool d1_on = !XS && pl_d1(P) && x.d1 != 0;
   uint64_t t_last = 0, t_acc = 0;
 #define KSG_STAMPP(k)                                        \
   if constexpr (STAMP) {                                     \
@@ -1343,7 +1488,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   // so; a compiler barrier keeps them behind it)
   struct Head {
     uint32_t rec, rmod, lp_ex, lp_in, cand, xlp, xwp, m0, k0, pred;
-    uint64_t t0x;
+    uint64_t t0x, d1x;
   };
   auto head_reads = [&](uint32_t e) -> Head {
     // (every lane reads, at a clamped index: no exec-mask branch between the reads; the
@@ -1358,6 +1503,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     // masked once they are back)
     const uint32_t xw = have_x ? xnode >> 6 : 0u;
     h.t0x = r_t0[(size_t)e * P * 64 + xw];
+    h.d1x = pl_d1(P) ? r_d1[(size_t)e * P * 64 + xw] : 0ULL;
     h.xlp = r_lp[e * 64 + (xw >> 6) * 2];
     h.xwp = r_wp[(size_t)e * P * 64 + xw];
     h.m0 = (uint32_t)r_hdr[e].m0;
@@ -1421,6 +1567,10 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     const int32_t s = pv.s;
     const uint32_t nss = __builtin_amdgcn_readlane(rec, WS_NSS);
     const uint32_t n_sel = nss & 0xffff, n_svcs = nss >> 16, nk = pv.nk;
+    // x's verdict from phase A's bitmap: x fresh (its state is the snapshot plus pod i-1) and
+    // pod i-1 of another service (x's service entries cannot move pod i's spreading term or
+    // raise its service's scalars); the x-checker only replays such a commit
+    const bool x_fast = d1_on && have_x && x_fresh && !pod_has_service(xrec, s);
     if (__builtin_amdgcn_readlane(rec, WS_NINL) > KSG_WIN_INLINE || nk > KSG_SLOT_KEYS || n_svcs > KSG_SLOT_SVCS) {
       resolved = i;  // lists longer than the record / a slot: the exact per-pod kernel takes it
       reason = i == 0 ? KSG_STOP_OVERSIZE : KSG_STOP_SLOT;
@@ -1460,7 +1610,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     bool hung = false;
     Verd vd;
     for (uint32_t spin = 0;; ++spin) {
-      const uint32_t xs = ld_rlx(&ctl->xseq), hg = ld_rlx(&ctl->hang);
+      const uint32_t xs = ld_rlx(&ctl->xseq), hg = ld_rlx(&ctl->hang), fs = ld_rlx(&ctl->fseq);
       uint32_t cs = ld_rlx(&ctl->chk_seq[0]);
 #pragma unroll
       for (int c = 1; c < KSG_RES_NCHK; ++c) cs = min(cs, ld_rlx(&ctl->chk_seq[c]));
@@ -1469,7 +1619,9 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
       // (and in this round: the values are inputs here, so the reads are not moved past the loop)
       asm volatile("" ::"v"(vd.cc0), "v"(vd.cc1), "v"(vd.xres), "v"(vd.fw), "v"(vd.m0l), "v"(vd.m0h), "v"(vd.m1l),
                    "v"(vd.m1h), "v"(vd.dp0), "v"(vd.dp1), "v"(vd.esw));
-      if ((cs >= i + 1 && xs >= i + 1) || (xpt & 8u)) break;
+      // (the flagger applied the flags of commits <= i-2: fseq >= i-1; the x-checker's verdict
+      // covers commit i-1's)
+      if ((cs >= i + 1 && (x_fast || xs >= i + 1) && fs + 1 >= i) || (xpt & 8u)) break;
       if (spin > 16 * KSG_SPIN_LIMIT || hg) {
         hung = true;
         break;
@@ -1483,7 +1635,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     KSG_STAMPP(2)
     if constexpr (STAMP) t_acc += lane == 6 ? (uint64_t)(uint32_t)((uint32_t)t_last - ctl->t_x) : 0ULL;
     const uint32_t cc0 = vd.cc0, cc1 = vd.cc1, fw = vd.fw;
-    const uint32_t xres = __builtin_amdgcn_readfirstlane(vd.xres);
+    const uint32_t xres = x_fast ? (uint32_t)((h.d1x >> (xnode & 63)) & 1ULL) : __builtin_amdgcn_readfirstlane(vd.xres);
     uint64_t msk0 = ((uint64_t)__builtin_amdgcn_readfirstlane(vd.m0h) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(vd.m0l);
     uint64_t msk1 = ((uint64_t)__builtin_amdgcn_readfirstlane(vd.m1h) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(vd.m1l);
     const uint32_t dp0 = vd.dp0, dp1 = vd.dp1;
@@ -1750,6 +1902,8 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
     have_x = true;
     xnode = woff;
     xslot = slot;
+    x_fresh = !in_c;
+    xrec = rec;
     ++n_draws;
     KSG_STAMPP(5)
   }
@@ -1761,7 +1915,7 @@ __global__ __launch_bounds__(512) void ksg_win_plain_kernel(KsgDev d, uint32_t w
   // x-checker records the last first peers
   bool drained = false;
   for (uint32_t spin = 0; spin <= 16 * KSG_SPIN_LIMIT; ++spin) {
-    bool done = ld_acq(&ctl->fin_x) != 0;
+    bool done = ld_acq(&ctl->fin_x) != 0 && ld_acq(&ctl->fin_f) != 0;
 #pragma unroll
     for (int c = 0; c < KSG_RES_NCHK; ++c) done = done && ld_acq(&ctl->fin[c]) != 0;
     if (done) {
@@ -1859,7 +2013,7 @@ static hipError_t win_plain_launch_x(const KsgDev& d, uint32_t wcap, size_t lds,
     (void)hipGetLastError();  // do not leave a sticky error behind
     once = true;
   }
-  hipLaunchKernelGGL((ksg_win_plain_kernel<PP, ST, XS>), dim3(1), dim3(512), lds, st, d, wcap, run, sums, x, rng,
+  hipLaunchKernelGGL((ksg_win_plain_kernel<PP, ST, XS>), dim3(1), dim3(pl_nt(PP)), lds, st, d, wcap, run, sums, x, rng,
                      out);
   return hipGetLastError();
 }
@@ -1877,8 +2031,11 @@ hipError_t ksg_launch_win_plain(const KsgDev& d, uint32_t P, uint32_t wcap, KsgW
                                 const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
   const size_t lds = plain_lds_offsets(P, (d.n_services + 31) / 32, wcap).total;
   // the debug instantiation: KSG_DEBUG & 8 (per-section s_memtime stamps), bits 16..19 (skews) or
-  // 24..27 (timing switches); the production one keeps no debug switch in a register
-  const bool stamp = (d.dbg & 8) != 0 || ((uint32_t)d.dbg & 0x0fff0000u) != 0;
+  // 24..27 (timing switches); the production one keeps no debug switch in a register. Bits 22 / 23
+  // (the runtime's request-corruption hook for the resident server's rejection test) and every
+  // other bit keep the production resolver: a fault-injection switch never changes which resolver
+  // build runs
+  const bool stamp = (d.dbg & 8) != 0 || ((uint32_t)d.dbg & KSG_DBG_RESOLVER_MASK) != 0;
 #define KSG_PLAIN_CASE(PP)                                                                  \
   if (P == PP)                                                                              \
     return stamp ? win_plain_launch<PP, true>(d, wcap, lds, run, sums, x, rng, out, st)    \

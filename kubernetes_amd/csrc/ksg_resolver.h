@@ -161,6 +161,12 @@ __host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag,
 #define KSG_STOP_OVERSIZE 4
 #define KSG_STOP_HANG 9        // a ring/draw wait exceeded KSG_SPIN_LIMIT polls (a bug): the host fails
 #define KSG_SPIN_LIMIT (1u << 22)
+// KSG_DEBUG bits that select a resolver's debug instantiation: 16..19 the per-role delay
+// skews (interleaving tests), 24..27 the plain resolver's timing switches. Bits 20..23 are
+// not resolver switches (22 / 23: the runtime's request-corruption hook for the resident
+// server's rejection test), so setting them never changes which resolver build runs.
+#define KSG_DBG_SKEW_MASK 0x000f0000u
+#define KSG_DBG_RESOLVER_MASK 0x0f0f0000u
 
 // a global-address-space load: global_load (vmcnt only), not flat_load, whose
 // lgkmcnt share would make every later LDS wait also wait for it

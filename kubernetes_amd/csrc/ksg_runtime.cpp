@@ -219,6 +219,7 @@ struct ksg_ctx {
   double last_wsum = 0;            // window capacity W summed over the launches
   bool dbg_fail_next = false;      // KSG_DEBUG & 16384: the next window batch fails after its device work
   uint32_t dbg_corrupt = 0;        // KSG_DEBUG bits 22 / 23: corrupt the next COMMIT / BEGIN request's layout
+  bool win_d1 = true;              // phase A's single-commit drop bitmaps (KSG_WIN_D1=0: off; ksg_plain.hip)
   double last_hus[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // host us per phase of the last batch (ksg_last_batch_host_us)
   double totals[24] = {};  // ksg_batch_totals: the per-batch diagnostics summed over batches
   int64_t max_cap = 0, min_cap = 0;
@@ -658,21 +659,53 @@ int allreduce_sum_i32(ksg_ctx* c, const int32_t* dsend, int32_t* drecv, uint32_t
   return KSG_OK;
 }
 
-// one pod through scan [+ dcount all-reduce] + record all-gather (device only)
+int allreduce_max_i32(ksg_ctx* c, const int32_t* dsend, int32_t* drecv, uint32_t n) {
+  if (c->comm) {
+    NCCLCHK(c, ncclAllReduce(dsend, drecv, n, ncclInt32, ncclMax, c->comm, c->st));
+    return KSG_OK;
+  }
+  if (!c->xfn) return fail(c, KSG_ERR_STATE, "sharded context has neither an RCCL communicator nor ksg_set_allgather");
+  const size_t bytes = (size_t)n * 4;
+  int rc;
+  if ((rc = grow_host(c, &c->h_xsend, &c->h_xsend_cap, bytes)) ||
+      (rc = grow_host(c, &c->h_xrecv, &c->h_xrecv_cap, bytes * (c->world + 1))))
+    return rc;
+  HIPCHK(c, hipMemcpyAsync(c->h_xsend, dsend, bytes, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(c, hipStreamSynchronize(c->st));
+  if ((rc = c->xfn(c->xuser, c->h_xsend, c->h_xrecv, (uint64_t)bytes)) != 0)
+    return fail(c, KSG_ERR_RCCL, "allgather callback returned %d", rc);
+  int32_t* all = reinterpret_cast<int32_t*>(c->h_xrecv);
+  int32_t* mx = all + (size_t)n * c->world;
+  for (uint32_t i = 0; i < n; ++i) {
+    int32_t m = all[i];
+    for (int g = 1; g < c->world; ++g) m = std::max(m, all[(size_t)g * n + i]);
+    mx[i] = m;
+  }
+  HIPCHK(c, hipMemcpyAsync(drecv, mx, bytes, hipMemcpyHostToDevice, c->st));
+  return KSG_OK;
+}
+
+// one pod through scan [+ the normalised terms' all-reduces] + record all-gather (device
+// only). On a sharded context ServiceAntiAffinity's domain counts and the extension
+// TaintTolerationPriority's max are over every shard's filtered nodes: a first pass writes
+// this shard's part (dpart: the counts, then the max), the all-reduces combine them (sum,
+// max) and the full pass reads the result (dglobal). dext: the pod's extension record.
 int scan_exchange(ksg_ctx* c, const ksg_pod* dpod, const uint32_t* dids, int mode, uint8_t* fail_out,
-                  int64_t* score_out) {
+                  int64_t* score_out, const ksg_pod_ext* dext) {
   const bool anti = anti_on(c);
-  if (anti && c->xchg) {
-    HIPCHK(c, ksg_launch_scan(c->R, true, c->dev, dpod, dids, mode, 1, nullptr, nullptr, c->d_rec_send,
-                              c->d_dpart, nullptr, c->st));
-    int rc = allreduce_sum_i32(c, c->d_dpart, c->d_dglobal, c->dev.n_domains_total);
+  const bool tt = dext != nullptr && c->ext.w_taint_toleration != 0;
+  if ((anti || tt) && c->xchg) {
+    HIPCHK(c, ksg_launch_scan(c->R, anti, c->dev, dpod, dids, mode, 1, nullptr, nullptr, c->d_rec_send,
+                              c->d_dpart, nullptr, c->st, dext));
+    const uint32_t D = c->dev.n_domains_total;
+    int rc = anti ? allreduce_sum_i32(c, c->d_dpart, c->d_dglobal, D) : KSG_OK;
+    if (!rc && tt) rc = allreduce_max_i32(c, c->d_dpart + D, c->d_dglobal + D, 1);
     if (rc) return rc;
-    HIPCHK(c, ksg_launch_scan(c->R, true, c->dev, dpod, dids, mode, 2, fail_out, score_out, c->d_rec_send,
-                              nullptr, c->d_dglobal, c->st));
+    HIPCHK(c, ksg_launch_scan(c->R, anti, c->dev, dpod, dids, mode, 2, fail_out, score_out, c->d_rec_send,
+                              nullptr, c->d_dglobal, c->st, dext));
   } else {
     HIPCHK(c, ksg_launch_scan(c->R, anti, c->dev, dpod, dids, mode, 0, fail_out, score_out, c->d_rec_send,
-                              nullptr, nullptr, c->st,
-                              (c->ext_on && dpod == c->one_pod) ? c->d_one_ext : nullptr));
+                              nullptr, nullptr, c->st, dext));
   }
   if (mode == KSG_MODE_BEGIN) {
     if (c->xchg) {
@@ -1516,9 +1549,10 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   // KSG_DEBUG bit 22 / 23: the next COMMIT / BEGIN posted to the resident server carries an
   // out-of-range payload layout (tests/test_gpu_serve.py: the server must reject it, not fault)
   c->dbg_corrupt = ((uint32_t)d.dbg >> 22) & 3u;
+  c->win_d1 = !(getenv("KSG_WIN_D1") && atoi(getenv("KSG_WIN_D1")) == 0);
   if (d.dbg & (8 | 32)) {  // (32: the plain resolver's inconsistency record, ksg_plain.hip)
-    (void)hipMalloc(&d.dbgbuf, 64 * sizeof(int32_t));
-    (void)hipMemset(d.dbgbuf, 0, 64 * sizeof(int32_t));
+    (void)hipMalloc(&d.dbgbuf, KSG_DEBUG_COUNTER_WORDS * sizeof(int32_t));
+    (void)hipMemset(d.dbgbuf, 0, KSG_DEBUG_COUNTER_WORDS * sizeof(int32_t));
   }
   d.has_static_fit = ((c->cfg.predicates & KSG_PRED_LABELSPRESENCE) && c->cfg.n_presence > 0) ? 1 : 0;
   d.cap_cpu = cap_c;
@@ -1571,8 +1605,8 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   if ((rc = dalloc(c, &c->d_rec_send, c->rec_bytes, nullptr)) ||
       (rc = dalloc(c, &c->d_rec_recv, (size_t)c->rec_bytes * c->world, nullptr)) ||
       (rc = dalloc(c, &c->d_fail, NN, nullptr)) || (rc = dalloc(c, &c->d_score, NN, nullptr)) ||
-      (rc = dalloc(c, &c->d_dpart, std::max<uint32_t>(c->D, 1), nullptr)) ||
-      (rc = dalloc(c, &c->d_dglobal, std::max<uint32_t>(c->D, 1), nullptr)) ||
+      (rc = dalloc(c, &c->d_dpart, (size_t)c->dev.n_domains_total + 1, nullptr)) ||  // (+ the TaintToleration max)
+      (rc = dalloc(c, &c->d_dglobal, (size_t)c->dev.n_domains_total + 1, nullptr)) ||
       (rc = dalloc(c, &c->d_shard_wlo, c->world, nullptr)))
     return rc;
   HIPCHK(c, hipMemcpyAsync(c->d_shard_wlo, c->shard_wlo_h.data(), c->world * 4, hipMemcpyHostToDevice, c->st));
@@ -1659,11 +1693,17 @@ int ksg_add_static_config(ksg_ctx* c, const ksg_config* extra) {
     weighted |= w != 0;
   }
   const bool do_fit = extra->n_presence > 0, do_score = extra->n_label_pref > 0;
-  uint8_t* tmp = nullptr;
   const size_t fb = (size_t)nw * 8;
-  HIPCHK(c, hipMalloc((void**)&tmp, fb + (size_t)N * 8));
-  uint64_t* xfit = reinterpret_cast<uint64_t*>(tmp);
-  int64_t* xscore = reinterpret_cast<int64_t*>(tmp + fb);
+  // the scratch pair, freed on every path out (an error return included)
+  struct Scratch {
+    uint8_t* p = nullptr;
+    ~Scratch() {
+      if (p) (void)hipFree(p);
+    }
+  } tmp;
+  HIPCHK(c, hipMalloc((void**)&tmp.p, fb + (size_t)N * 8));
+  uint64_t* xfit = reinterpret_cast<uint64_t*>(tmp.p);
+  int64_t* xscore = reinterpret_cast<int64_t*>(tmp.p + fb);
   KsgDev& d = c->dev;
   HIPCHK(c, ksg_launch_static_terms(sc, N, c->d_lbl_nodes, c->d_lbl_pairs, c->d_lbl_keys, c->n_pairs, nw, xfit, xscore,
                                     c->st));
@@ -1671,7 +1711,6 @@ int ksg_add_static_config(ksg_ctx* c, const ksg_config* extra) {
                                    do_fit ? xfit : nullptr, do_score ? xscore : nullptr, nw, N, d.has_static_fit,
                                    d.has_static_score, c->st));
   HIPCHK(c, hipStreamSynchronize(c->st));
-  (void)hipFree(tmp);
   if (do_fit) d.has_static_fit = 1;
   if (do_score) {
     d.has_static_score = 1;
@@ -1849,7 +1888,8 @@ int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int6
   if ((rc = srv_stop(c))) return rc;
   if ((rc = flush_patches(c))) return rc;
   if ((rc = ensure_map(c)) || (rc = upload_one(c, pod, ids, ext))) return rc;
-  if ((rc = scan_exchange(c, c->one_pod, c->one_ids, KSG_MODE_BEGIN, fail_codes ? c->d_fail : nullptr, nullptr)))
+  if ((rc = scan_exchange(c, c->one_pod, c->one_ids, KSG_MODE_BEGIN, fail_codes ? c->d_fail : nullptr, nullptr,
+                          c->ext_on ? c->d_one_ext : nullptr)))
     return rc;
   HIPCHK(c, ksg_launch_decide(c->dev, c->one_pod, c->one_ids, rec_buf(c), c->rec_bytes, c->world,
                               c->d_shard_wlo, 0, 0, c->d_rng, nullptr, 0, reinterpret_cast<int64_t*>(c->d_map),
@@ -2066,9 +2106,14 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     const bool etm = esc && c->ext.w_taint_toleration != 0;  // (the TaintToleration count pass)
     x.esc = esc ? 1u : 0u;
     x.efit_off = esc ? (uint32_t)fit_off : 0u;
-    x.blk = ((rr            ? fit_off + (size_t)W * x.ostride * 16
-              : anti || esc ? fit_off + (size_t)W * x.ostride * 8
-                            : (size_t)W * x.ostride * 12) +
+    // the plain resolver without extensions up to 16,384 nodes (its ring holds the bitmaps):
+    // phase A's single-commit drop bitmaps at the same offset
+    const bool d1 = !anti && !dext && c->win_d1 && c->nw <= 4 * 64;
+    x.d1 = d1 ? 1u : 0u;
+    x.d1_off = d1 ? (uint32_t)fit_off : 0u;
+    x.blk = ((rr                  ? fit_off + (size_t)W * x.ostride * 16
+              : anti || esc || d1 ? fit_off + (size_t)W * x.ostride * 8
+                                  : (size_t)W * x.ostride * 12) +
              255) & ~(size_t)255;
     if (esc) {
       if ((rc = grow(c, (void**)&c->d_etmax, &c->etmax_cap, W, sizeof(int32_t))) ||
@@ -2155,13 +2200,19 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
                                         x.ostride, c->d_dcnt, nullptr, x.dmb, nullptr, x.dz, c->st));
           if (c->xchg && (rc = allreduce_sum_i32(c, c->d_dcnt, c->d_dcnt, (uint32_t)dcnt_n))) return rc;
         }
-        if (etm)  // TaintToleration: each pod's max soft-taint count over its filtered nodes first
+        if (etm) {  // TaintToleration: each pod's max soft-taint count over its filtered nodes first
           HIPCHK(c, ksg_launch_win_eval(c->dev, 3, c->d_pods, c->d_ids, c->d_run, W, c->d_winsum, wbits, wmax,
                                         x.ostride, nullptr, nullptr, nullptr, nullptr, 0, c->st, dext, x.tmax,
                                         x.psoft, x.thist));
+          // sharded: over every shard's filtered nodes (the max, and the histogram of soft
+          // counts whose bin at the max the resolver's normalisation stop reads)
+          if (c->xchg && ((rc = allreduce_max_i32(c, x.tmax, x.tmax, W)) ||
+                          (rc = allreduce_sum_i32(c, x.thist, x.thist, W * KSG_TBINS))))
+            return rc;
+        }
         HIPCHK(c, ksg_launch_win_eval(c->dev, anti ? 2 : 0, c->d_pods, c->d_ids, c->d_run, W, c->d_winsum, wbits,
                                       wmax, x.ostride, c->d_dcnt,
-                                      (anti || esc) ? reinterpret_cast<uint64_t*>(c->d_xsend + fit_off) : nullptr,
+                                      (anti || esc || d1) ? reinterpret_cast<uint64_t*>(c->d_xsend + fit_off) : nullptr,
                                       x.dmb, rr ? reinterpret_cast<uint64_t*>(c->d_xsend + x.b_off) : nullptr, x.dz,
                                       c->st, dext, x.tmax, x.psoft));
         if (c->xchg && (rc = allgather(c, c->d_xsend, c->d_xrecv, x.blk))) return rc;
@@ -2218,9 +2269,12 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
           HIPCHK(c, ksg_launch_batch(c->R, anti, c->dev, c->d_pods + pos, c->d_ids, 1, c->d_rng,
                                      c->d_out + pos, c->st, dext ? dext + pos : nullptr));
         } else {
-          if ((rc = scan_exchange(c, c->d_pods + pos, c->d_ids, KSG_MODE_BEGIN, nullptr, nullptr))) return rc;
+          if ((rc = scan_exchange(c, c->d_pods + pos, c->d_ids, KSG_MODE_BEGIN, nullptr, nullptr,
+                                  dext ? dext + pos : nullptr)))
+            return rc;
           HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods + pos, c->d_ids, rec_buf(c), c->rec_bytes, c->world,
-                                      c->d_shard_wlo, 1, 0, c->d_rng, c->d_out, pos, c->d_summary, c->st));
+                                      c->d_shard_wlo, 1, 0, c->d_rng, c->d_out, pos, c->d_summary, c->st,
+                                      dext ? dext + pos : nullptr));
         }
         pos += 1;
         ++c->last_stats[3];
@@ -2233,9 +2287,11 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
     HIPCHK(c, ksg_launch_batch(c->R, anti_on(c), c->dev, c->d_pods, c->d_ids, n, c->d_rng, c->d_out, c->st, dext));
   } else {
     for (uint32_t i = 0; i < n; ++i) {
-      if ((rc = scan_exchange(c, c->d_pods + i, c->d_ids, KSG_MODE_BEGIN, nullptr, nullptr))) return rc;
+      if ((rc = scan_exchange(c, c->d_pods + i, c->d_ids, KSG_MODE_BEGIN, nullptr, nullptr, dext ? dext + i : nullptr)))
+        return rc;
       HIPCHK(c, ksg_launch_decide(c->dev, c->d_pods + i, c->d_ids, rec_buf(c), c->rec_bytes, c->world,
-                                  c->d_shard_wlo, 1, 0, c->d_rng, c->d_out, i, c->d_summary, c->st));
+                                  c->d_shard_wlo, 1, 0, c->d_rng, c->d_out, i, c->d_summary, c->st,
+                                  dext ? dext + i : nullptr));
     }
   }
   if (!tail_queued) {
@@ -2302,10 +2358,12 @@ int ksg_evaluate(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, uint8_t* f
   if ((rc = flush_patches(c))) return rc;
   if ((rc = upload_one(c, pod, ids, ext))) return rc;
   // errors surface through the BEGIN record, so run BEGIN first for the flag
-  if ((rc = scan_exchange(c, c->one_pod, c->one_ids, KSG_MODE_BEGIN, nullptr, nullptr))) return rc;
+  if ((rc = scan_exchange(c, c->one_pod, c->one_ids, KSG_MODE_BEGIN, nullptr, nullptr, c->ext_on ? c->d_one_ext : nullptr)))
+    return rc;
   HIPCHK(c, ksg_launch_decide(c->dev, c->one_pod, c->one_ids, rec_buf(c), c->rec_bytes, c->world,
                               c->d_shard_wlo, 0, 0, c->d_rng, nullptr, 0, c->d_summary, c->st));
-  if ((rc = scan_exchange(c, c->one_pod, c->one_ids, KSG_MODE_EVAL, c->d_fail, c->d_score))) return rc;
+  if ((rc = scan_exchange(c, c->one_pod, c->one_ids, KSG_MODE_EVAL, c->d_fail, c->d_score, c->ext_on ? c->d_one_ext : nullptr)))
+    return rc;
   int64_t summ[3];
   HIPCHK(c, hipMemcpyAsync(summ, c->d_summary, sizeof summ, hipMemcpyDeviceToHost, c->st));
   const size_t ns = c->hi - c->lo;
@@ -2371,14 +2429,16 @@ int ksg_serve_stats(ksg_ctx* c, uint64_t* out4) {
   return KSG_OK;
 }
 
-int ksg_debug_counters(ksg_ctx* c, int32_t* out32) {
-  if (!c || !out32) return KSG_ERR_ARG;
+int ksg_debug_counters(ksg_ctx* c, int32_t* out, uint32_t n_words) {
+  if (!c || (!out && n_words)) return KSG_ERR_ARG;
   KSG_LOCK(c);
   if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
   if (!c->dev.dbgbuf) return fail(c, KSG_ERR_STATE, "debug counters need KSG_DEBUG=8 at ksg_create");
   (void)hipSetDevice(c->device);
   HIPCHK(c, hipStreamSynchronize(c->st));
-  HIPCHK(c, hipMemcpy(out32, c->dev.dbgbuf, 64 * sizeof(int32_t), hipMemcpyDeviceToHost));
+  int32_t words[KSG_DEBUG_COUNTER_WORDS];
+  HIPCHK(c, hipMemcpy(words, c->dev.dbgbuf, sizeof(words), hipMemcpyDeviceToHost));
+  for (uint32_t k = 0; k < n_words; ++k) out[k] = k < KSG_DEBUG_COUNTER_WORDS ? words[k] : 0;
   return KSG_OK;
 }
 
@@ -2473,7 +2533,6 @@ int ksg_set_extensions(ksg_ctx* c, const ksg_ext_config* e) {
   KSG_LOCK(c);
   if (c->have_cluster) return fail(c, KSG_ERR_STATE, "ksg_set_extensions: call before ksg_set_cluster");
   if (int rs_ = srv_stop(c)) return rs_;  // (the resident server leaves the stream)
-  if (c->world > 1 || c->xchg) return fail(c, KSG_ERR_ARG, "extensions: one rank only");
   if ((e->filters & ~(KSG_EXT_TAINTS | KSG_EXT_SCALAR)) || e->n_scalar > KSG_MAX_SCALAR)
     return fail(c, KSG_ERR_ARG, "extensions: bad filters / n_scalar");
   c->ext = *e;
@@ -2555,11 +2614,27 @@ static int note_ext(ksg_ctx* c, const ksg_pod* p, const ksg_pod_ext* e, size_t n
   else c->ext_scalar.erase(p->uid);
   return KSG_OK;
 }
+// a taint list is a set: TaintTolerationPriority counts each untolerated taint of the node once,
+// and the window path counts a soft list as a bit mask while the exact kernels count its entries,
+// so a repeated id would make the answer depend on the path
+static bool has_repeat(const uint32_t* v, uint32_t n) {
+  if (n <= 64) {
+    for (uint32_t i = 1; i < n; ++i)
+      for (uint32_t j = 0; j < i; ++j)
+        if (v[i] == v[j]) return true;
+    return false;
+  }
+  std::vector<uint32_t> s(v, v + n);
+  std::sort(s.begin(), s.end());
+  return std::adjacent_find(s.begin(), s.end()) != s.end();
+}
 static int check_taint_ids(ksg_ctx* c, const ksg_pod_ext* e, const uint32_t* ids) {
   for (uint32_t i = 0; i < e->n_hard; ++i)
     if (ids[e->hard_off + i] >= c->ext.max_taints) return fail(c, KSG_ERR_CAPACITY, "taint id out of range");
   for (uint32_t i = 0; i < e->n_soft; ++i)
     if (ids[e->soft_off + i] >= c->ext.max_taints) return fail(c, KSG_ERR_CAPACITY, "taint id out of range");
+  if ((e->n_hard && has_repeat(ids + e->hard_off, e->n_hard)) || (e->n_soft && has_repeat(ids + e->soft_off, e->n_soft)))
+    return fail(c, KSG_ERR_ARG, "a taint id repeats in the pod's hard or soft list (each list is a set)");
   return KSG_OK;
 }
 
@@ -2635,7 +2710,7 @@ int ksg_schedule_begin_ext(ksg_ctx* c, const ksg_pod* pod, const ksg_pod_ext* ex
   int rc = KSG_OK;
   if (ext) {
     const size_t n_ids = call_ids_extent(c, pod);
-    if (!(rc = note_ext(c, pod, ext, n_ids))) rc = check_taint_ids(c, ext, ids);
+    if (!(rc = check_ext_range(c, ext, n_ids)) && !(rc = check_taint_ids(c, ext, ids))) rc = note_ext(c, pod, ext, n_ids);
   }
   if (!rc) rc = ksg_schedule_begin(c, pod, ids, max_score, tie_count, fail_codes);
   c->cur_ext = nullptr;

@@ -213,6 +213,26 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
     smax = c.spread_max;
   }
 
+  // ---- (plain, no extensions, wfit given: the single-commit drop bitmap, KsgWinXchg.d1) lane j:
+  // pod p0+j-1's requests and whether a conflict key of pod p0+j that its predicates check is
+  // one of pod p0+j-1's keys (a node that took pod p0+j-1 then conflicts for pod p0+j)
+  const bool d1_on = MODE == KSG_WIN_PLAIN && !EXT && wfit != nullptr;
+  int64_t prc = 0, prm = 0;
+  bool pkey = false;
+  if (d1_on && lane < np && p0 + lane > 0) {
+    const ksg_pod& q = pods[p0 + lane - 1];
+    const ksg_pod& p = pods[p0 + lane];
+    prc = q.milli_cpu;
+    prm = q.memory;
+    const uint32_t nq = q.n_ports + q.n_pds, np_ = p.n_ports + p.n_pds;
+    for (uint32_t b = 0; b < np_; ++b) {
+      if (!(b < p.n_ports ? (P & KSG_PRED_PODFITSPORTS) : (P & KSG_PRED_NODISKCONFLICT))) continue;
+      const uint32_t kb = b < p.n_ports ? ids[p.ports_off + b] : ids[p.pds_off + (b - p.n_ports)];
+      for (uint32_t a = 0; a < nq; ++a)
+        pkey |= (a < q.n_ports ? ids[q.ports_off + a] : ids[q.pds_off + (a - q.n_ports)]) == kb;
+    }
+  }
+
   // ---- per-pod service counts of this lane's node, all issued up front: the
   // service's node word first (svc_bits, one 8-byte load per wave), then a count
   // only where the node holds pods of the service (most counts are 0)
@@ -401,6 +421,27 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
           sc = s;
         }
       }
+      if (d1_on) {
+        // the x-checker's verdict (ksg_plain.hip) on this node for this pod if pod p0+j-1 were the
+        // node's first commit of the window: it no longer fits (resources, a shared key) or its
+        // LeastRequested term fell; the node's service entries cannot change it when pod p0+j-1
+        // is of another service (the committer takes this bitmap only then)
+        bool dr = false;
+        if (fit) {
+          const int64_t pcj = (int64_t)readlane64((uint64_t)prc, j), pmj = (int64_t)readlane64((uint64_t)prm, j);
+          const int64_t nowc = (int64_t)((uint64_t)usedc + (uint64_t)pcj), nowm = (int64_t)((uint64_t)usedm + (uint64_t)pmj);
+          if (res_on && !__builtin_amdgcn_readlane(zr, j))  // PodFitsResources (predicates.go:127-145)
+            dr = !((capc == 0 || capc - nowc >= rcj) && (capm == 0 || capm - nowm >= rmj));
+          if (d.w_lr) {  // LeastRequested (priorities.go:43-76)
+            const int32_t lr_now = lr_win(nowc + rcj, capc, inv_c) + lr_win(nowm + rmj, capm, inv_m);
+            const int32_t lr_snap = lr_win(usedc + rcj, capc, inv_c) + lr_win(usedm + rmj, capm, inv_m);
+            dr |= (lr_now >> 1) != (lr_snap >> 1);
+          }
+          dr |= __builtin_amdgcn_readlane((int)pkey, j) != 0;
+        }
+        const uint64_t db = __ballot(dr);
+        if (lane == (uint32_t)j) my_fit = db;
+      }
       int32_t m = wave_total_max(sc);
       if (d.empty_priorities) m = KSG_S32_NONE;  // prioritizeNodes returns nothing
       const uint64_t b = __ballot(m != KSG_S32_NONE && sc == m);
@@ -426,6 +467,7 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
     }
     if constexpr (EXT)
       if (wfit) wfit[(size_t)(p0 + lane) * ostride + w] = my_fit;
+    if (d1_on) wfit[(size_t)(p0 + lane) * ostride + w] = my_fit;  // (the single-commit drop bitmap)
   }
   if constexpr (EXT)
     if (psoft && w == 0 && lane < np) psoft[p0 + lane] = ps;
@@ -3158,7 +3200,7 @@ hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run
   const size_t lds =
       win_lds_offsets(P, (d.n_services + 31) / 32, wcap, x.fit_off != 0, x.rr ? x.dz : 0u, d.n_services).total;
   // the debug instantiation: stamps (KSG_DEBUG & 8) or skews (bits 16..19)
-  const bool stamp = (d.dbg & 8) != 0 || ((uint32_t)d.dbg & 0x000f0000u) != 0;
+  const bool stamp = (d.dbg & 8) != 0 || ((uint32_t)d.dbg & KSG_DBG_SKEW_MASK) != 0;
   const bool anti = x.fit_off != 0;
 #define KSG_RES_CASE(PP, AN)                                                                          \
   if (P == PP && anti == AN)                                                                          \

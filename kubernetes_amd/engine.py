@@ -160,8 +160,9 @@ class DeviceScheduler:
         cap = np.ascontiguousarray(scalar_cap, np.int64).reshape(-1)
         cap = cap if len(cap) else np.zeros(1, np.int64)
         ti = _u32(taint_ids if len(taint_ids) else np.zeros(1, np.uint32))
-        rc = self._lib.ksg_set_node_ext(self._ctx, self.n_nodes, abi.ptr(cap), abi.ptr(_u32(taint_off)),
-                                        abi.ptr(_u32(taint_n)), abi.ptr(ti), len(taint_ids))
+        toff, tn = _u32(taint_off), _u32(taint_n)  # (held: a converted copy must outlive the call)
+        rc = self._lib.ksg_set_node_ext(self._ctx, self.n_nodes, abi.ptr(cap), abi.ptr(toff), abi.ptr(tn), abi.ptr(ti),
+                                        len(taint_ids))
         if rc != abi.KSG_OK:
             self._err(rc)
 
@@ -325,8 +326,8 @@ class DeviceScheduler:
     def debug_counters(self) -> np.ndarray:
         """KSG_DEBUG=8 contexts: the window resolver's per-stage cycle counters
         (cycles / 64, summed over every window so far)."""
-        o = np.zeros(64, np.int32)
-        rc = self._lib.ksg_debug_counters(self._ctx, abi.ptr(o))
+        o = np.zeros(abi.KSG_DEBUG_COUNTER_WORDS, np.int32)
+        rc = self._lib.ksg_debug_counters(self._ctx, abi.ptr(o), len(o))
         if rc != abi.KSG_OK:
             self._err(rc)
         return o

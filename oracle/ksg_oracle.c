@@ -76,6 +76,9 @@ typedef struct orc {
   int64_t *scap, *sused;  /* [n_scalar][N] */
   uint32_t **ntaint, *nnt; /* per node taint ids */
   ksg_pod_ext pend_ext;
+  /* the node-sharded TaintToleration step (orc_evaluate_ext_tmax): the max soft-taint count
+   * over every shard's filtered nodes, supplied by the caller; -1: computed here */
+  int32_t tmax_given;
 } orc;
 
 #define NONE_SCORE (-0x7fffffffffffffffLL - 1)
@@ -149,6 +152,7 @@ orc *orc_create(const ksg_config *cfg, int faithful) {
   o->cfg = *cfg;
   if (o->cfg.max_conflict_keys == 0) o->cfg.max_conflict_keys = 1024;
   o->faithful = faithful;
+  o->tmax_given = -1;
   return o;
 }
 
@@ -427,11 +431,14 @@ static void ext_prioritize(const orc *o, const pctx *c, const uint8_t *fails, in
       if (!fails[n]) score[n] = go_add(score[n], go_mul(o->ext.w_balanced, balanced_score(tc[n], o->cap_c[n], tm[n], o->cap_m[n])));
   if (o->ext.w_taint_toleration && c->ext) {
     int32_t mx = 0;
-    for (uint32_t n = 0; n < o->N; ++n)
-      if (!fails[n]) {
-        int32_t k = soft_taints(o, c, n);
-        if (k > mx) mx = k;
-      }
+    if (o->tmax_given >= 0)
+      mx = o->tmax_given;
+    else
+      for (uint32_t n = 0; n < o->N; ++n)
+        if (!fails[n]) {
+          int32_t k = soft_taints(o, c, n);
+          if (k > mx) mx = k;
+        }
     for (uint32_t n = 0; n < o->N; ++n)
       if (!fails[n]) {
         int64_t v = mx == 0 ? 10 : 10 - (10 * (int64_t)soft_taints(o, c, n)) / mx;
@@ -965,6 +972,47 @@ int orc_evaluate_counts(orc *o, const ksg_pod *p, const uint32_t *ids, const int
   if (c.error) return KSG_ERR_NOPEER;
   for (uint32_t n = 0; n < o->N; ++n) o->fails[n] = (uint8_t)incr_fail_code(o, &c, n);
   (void)incr_prioritize(o, &c, o->fails, o->scores, dcount);
+  if (fail_out) memcpy(fail_out, o->fails, o->N);
+  if (score_out)
+    for (uint32_t n = 0; n < o->N; ++n) score_out[n] = o->fails[n] ? 0 : o->scores[n];
+  return KSG_OK;
+}
+
+/* The node-sharded TaintTolerationPriority step, restated (ksg_runtime.cpp scan_exchange,
+ * and the window path's count pass + all-reduce): NormalizeReduce's max is over every
+ * filtered node (parity unpinned: no reference code, kschedgpu.h "extensions"), so a
+ * shard [lo, hi) reports the max untolerated soft-taint count over ITS filtered nodes
+ * (*out), the shards' maxima are all-reduced (max) and every shard scores with the
+ * result (orc_evaluate_ext_tmax). */
+int orc_taint_max(orc *o, const ksg_pod *p, const ksg_pod_ext *e, const uint32_t *ids, uint32_t lo, uint32_t hi,
+                  int32_t *out) {
+  *out = 0;
+  pctx c;
+  c.p = p;
+  c.ids = ids;
+  c.ext = e;
+  resolve_affinity(o, &c);
+  if (c.error) return KSG_ERR_NOPEER;
+  if (hi > o->N) hi = o->N;
+  for (uint32_t n = lo; n < hi; ++n) {
+    if (incr_fail_code(o, &c, n)) continue;
+    int32_t k = e ? soft_taints(o, &c, n) : 0;
+    if (k > *out) *out = k;
+  }
+  return KSG_OK;
+}
+
+/* orc_evaluate_ext (incremental mode) with TaintTolerationPriority's max supplied */
+int orc_evaluate_ext_tmax(orc *o, const ksg_pod *p, const ksg_pod_ext *e, const uint32_t *ids, int32_t tmax,
+                          uint8_t *fail_out, int64_t *score_out) {
+  if (o->N == 0) return KSG_NONODES;
+  const int faithful = o->faithful;
+  o->faithful = 0;
+  o->tmax_given = tmax;
+  int r = evaluate_ext(o, p, e, ids);
+  o->tmax_given = -1;
+  o->faithful = faithful;
+  if (r < 0) return r;
   if (fail_out) memcpy(fail_out, o->fails, o->N);
   if (score_out)
     for (uint32_t n = 0; n < o->N; ++n) score_out[n] = o->fails[n] ? 0 : o->scores[n];

@@ -43,6 +43,8 @@ def load():
         "orc_evaluate": (C.c_int, [vp, vp, vp, vp, vp]),
         "orc_domain_counts": (C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, vp]),
         "orc_evaluate_counts": (C.c_int, [vp, vp, vp, vp, vp, vp]),
+        "orc_taint_max": (C.c_int, [vp, vp, vp, vp, C.c_uint32, C.c_uint32, P(C.c_int32)]),
+        "orc_evaluate_ext_tmax": (C.c_int, [vp, vp, vp, vp, C.c_int32, vp, vp]),
         "orc_schedule_begin": (C.c_int, [vp, vp, vp, C.c_size_t, P(C.c_int64), P(C.c_uint32), vp]),
         "orc_schedule_commit": (C.c_int, [vp, C.c_uint32, P(C.c_int32)]),
         "orc_schedule_batch": (C.c_int, [vp, vp, C.c_uint32, vp, C.c_uint32, P(C.c_uint64), vp]),
@@ -112,16 +114,16 @@ class OracleScheduler:
     def set_node_ext(self, scalar_cap, taint_off, taint_n, taint_ids):
         cap = np.ascontiguousarray(scalar_cap, np.int64).reshape(-1)
         cap = cap if len(cap) else np.zeros(1, np.int64)
-        self._lib.orc_set_node_ext(self._o, abi.ptr(cap), abi.ptr(_u32(taint_off)), abi.ptr(_u32(taint_n)),
-                                   abi.ptr(_u32(taint_ids)))
+        toff, tn, ti = _u32(taint_off), _u32(taint_n), _u32(taint_ids)  # (held across the call)
+        self._lib.orc_set_node_ext(self._o, abi.ptr(cap), abi.ptr(toff), abi.ptr(tn), abi.ptr(ti))
 
     def _ext(self, batch: PodBatch, i: int):
         return None if batch.ext is None else np.ascontiguousarray(batch.ext[i : i + 1], dtype=abi.POD_EXT_DTYPE)
 
     def add_pod(self, host_id: int, batch: PodBatch, i: int = 0):
         pod = np.ascontiguousarray(batch.pods[i : i + 1])
-        self._lib.orc_add_pod_ext(self._o, int(host_id), abi.ptr(pod), abi.ptr(self._ext(batch, i)),
-                                  abi.ptr(_u32(batch.ids)))
+        e, ids = self._ext(batch, i), _u32(batch.ids)  # (held: the pointers must outlive the call)
+        self._lib.orc_add_pod_ext(self._o, int(host_id), abi.ptr(pod), abi.ptr(e), abi.ptr(ids))
 
     def remove_pod(self, uid: int):
         rc = self._lib.orc_remove_pod(self._o, int(uid))
@@ -193,6 +195,26 @@ class OracleScheduler:
         dc = np.ascontiguousarray(dcount, np.int32)
         rc = self._lib.orc_evaluate_counts(self._o, abi.ptr(pod), abi.ptr(_u32(batch.ids)), abi.ptr(dc),
                                            abi.ptr(fails), abi.ptr(scores))
+        return rc, fails[: self.n_nodes], scores[: self.n_nodes]
+
+    def taint_max(self, batch: PodBatch, i: int, lo: int, hi: int) -> int:
+        """TaintTolerationPriority's max soft-taint count over the filtered nodes of
+        shard [lo, hi) (orc_taint_max; the sharded step's partial)."""
+        pod = np.ascontiguousarray(batch.pods[i : i + 1])
+        out = C.c_int32(0)
+        e, ids = self._ext(batch, i), _u32(batch.ids)  # (held: the pointers must outlive the call)
+        rc = self._lib.orc_taint_max(self._o, abi.ptr(pod), abi.ptr(e), abi.ptr(ids), lo, hi, C.byref(out))
+        assert rc == abi.KSG_OK or rc == abi.KSG_ERR_NOPEER, rc
+        return int(out.value)
+
+    def evaluate_tmax(self, batch: PodBatch, i: int, tmax: int):
+        """evaluate() with TaintTolerationPriority's max supplied (the all-reduced one)."""
+        pod = np.ascontiguousarray(batch.pods[i : i + 1])
+        fails = np.zeros(max(self.n_nodes, 1), np.uint8)
+        scores = np.zeros(max(self.n_nodes, 1), np.int64)
+        e, ids = self._ext(batch, i), _u32(batch.ids)  # (held: the pointers must outlive the call)
+        rc = self._lib.orc_evaluate_ext_tmax(self._o, abi.ptr(pod), abi.ptr(e), abi.ptr(ids), int(tmax), abi.ptr(fails),
+                                             abi.ptr(scores))
         return rc, fails[: self.n_nodes], scores[: self.n_nodes]
 
     def shard(self):

@@ -189,3 +189,32 @@ def test_config5_extensions_full_size_matches_restatement():
     for r in range(gx.shape[0]):
         np.add.at(sx[r], got[ok], c.batch.ext["scalar"][ok, r])
     assert np.array_equal(sx, gx) and (gx <= np.where(cap > 0, cap, 0)).all()
+
+
+@pytest.mark.parametrize("window", [0, 64])
+@pytest.mark.parametrize("which", ["soft", "hard"])
+def test_repeated_taint_id_is_rejected_on_every_path(window, which):
+    """A pod's hard / soft taint list is a set (include/kschedgpu.h, ksg_pod_ext): the
+    window path counts the soft list as a 64-bit mask and the exact kernels count its
+    entries, so a repeated id would make the placement depend on the window size
+    (ADVICE round 4). Every pod-taking entry point rejects it before any device work,
+    at window 0 and 64 alike, and the context stays usable."""
+    from kubernetes_amd.engine import KsgError
+    c = ExtCase("config2", 300, 120)
+    dev = c.load(DeviceScheduler(c.cfg, device=0))
+    dev.set_window(window)
+    ids = np.concatenate([c.batch.ids, np.array([0, 0], np.uint32)])
+    ext = c.batch.ext.copy()
+    ext[5][f"{which}_off"] = len(ids) - 2
+    ext[5][f"n_{which}"] = 2
+    bad = PodBatch(c.batch.pods, ids, ext)
+    for call in (lambda: dev.batch(bad, 77), lambda: dev.begin(bad, 5), lambda: dev.evaluate(bad, 5)):
+        with pytest.raises(KsgError) as ei:
+            call()
+        assert ei.value.code == abi.KSG_ERR_ARG and "repeats" in str(ei.value)
+    ok = PodBatch(c.batch.pods, c.batch.ids, c.batch.ext)  # the same batch with sets: schedules
+    orc = c.load(OracleScheduler(c.cfg))
+    got, sg = dev.batch(ok, 77)
+    want, sw = orc.batch(ok, 77)
+    assert np.array_equal(got, want) and sg == sw
+    dev.close()

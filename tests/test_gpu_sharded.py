@@ -37,12 +37,21 @@ class _Fuzz:
         self.view = type("View", (), {"arrays": arrays})()
 
 
+# extension variants (parity unpinned: the C restatement is the checker):
+# "ext:<config>:<variant>"
+_EXT_KW = {"all": dict(w_taint=1, w_bal=1), "taint": dict(w_taint=2, w_bal=0), "filters": dict(w_taint=0, w_bal=0)}
+
+
 def _make_case(name, nn, npods):
     from tests.families import FamilyCase
     from tests.helpers import Case
 
     if name.startswith("fam:"):
         return FamilyCase(name[4:], nn, npods)
+    if name.startswith("ext:"):
+        from tests.ext_cases import ExtCase
+        _, cfg, var = name.split(":")
+        return ExtCase(cfg, nn, npods, **_EXT_KW[var])
     return _Fuzz(nn) if name == "fuzz" else Case(name, nn, npods)
 
 
@@ -72,6 +81,8 @@ def _worker(rank, world, port, name, nn, npods, window, chunk, seed, q):
         used_c, used_m = dev.read_requested()
         lo, hi = dev.shard()
         stats = dev.last_batch_stats()
+        if getattr(dev, "n_scalar", 0):  # (extensions: the extended resources taken, on every rank)
+            stats = dict(stats, ext_used=dev.read_ext_used().tolist())
         dev.close()
         q.put((rank, out.tolist(), rng, used_c.tolist(), used_m.tolist(), lo, hi, stats, None))
     except Exception as e:  # report instead of hanging the parent
@@ -107,13 +118,15 @@ def _run(name, nn, npods, window, world=2, chunk=None, seed=1234):
     return res
 
 
-def _oracle(name, nn, npods, seed=1234):
+def _oracle(name, nn, npods, seed=1234, ext_used=False):
     from oracle.pyoracle import OracleScheduler
 
     case = _make_case(name, nn, npods)
     orc = OracleScheduler(case.cfg)
     want, st = _run_case(orc, case, seed)
     wc, wm = orc.read_requested()
+    if ext_used:
+        return want, st, wc, wm, orc.read_ext_used().tolist()
     return want, st, wc, wm
 
 
@@ -142,6 +155,34 @@ def test_sharded_batch_matches_oracle(name, nn, npods, window, world, chunk):
     if world == 2 and all(b > a for a, b in spans):
         lo1 = spans[1][0]  # both shards must have produced winners
         assert (want >= lo1).any() and ((want >= 0) & (want < lo1)).any()
+
+
+@pytest.mark.parametrize("name,nn,npods,window,world,chunk", [
+    ("ext:config2:all", 700, 900, 128, 2, None),     # window path: TaintToleration max + histogram all-reduced
+    ("ext:config2:all", 700, 400, 0, 2, None),       # per-pod path: scan phase 1 + the max all-reduce
+    ("ext:config2:taint", 1500, 700, 37, 3, 211),    # three ranks, ragged shards, windows cut by batches
+    ("ext:config2:filters", 5000, 1200, 128, 2, None),
+    ("ext:config4:all", 900, 300, 128, 2, None),     # ServiceAntiAffinity + extensions: both all-reduces per pod
+])
+def test_sharded_extensions_match_oracle(name, nn, npods, window, world, chunk):
+    """Extensions on a node-sharded context (parity unpinned): taints,
+    extended resources (GPU counts), BalancedAllocation and TaintToleration, whose
+    normalisation max is over every shard's filtered nodes. Every rank's placements, RNG
+    position, requested totals and extended-resource usage equal the C restatement's
+    single-process schedule."""
+    want, st, wc, wm, xu = _oracle(name, nn, npods, ext_used=True)
+    res = _run(name, nn, npods, window, world=world, chunk=chunk)
+    for rank, out, rng, uc, um, lo, hi, stats, _ in res:
+        got = np.asarray(out)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, f"rank {rank}: first mismatches at {bad[:8]}: {got[bad[:8]]} vs {want[bad[:8]]}"
+        assert rng == st
+        assert np.array_equal(np.asarray(uc), wc) and np.array_equal(np.asarray(um), wm)
+        assert stats["ext_used"] == xu
+        if window and "config4" not in name:
+            assert stats["windows"] > 0  # (the window path took it)
+    lo1 = res[1][5]  # both shards produced winners
+    assert (want >= lo1).any() and ((want >= 0) & (want < lo1)).any()
 
 
 @pytest.mark.parametrize("fuzz_seed", [2, 3, 6, 10, 11, 14])
@@ -190,6 +231,38 @@ def test_rccl_one_rank_batch_matches_oracle(name, nn, npods, window):
             assert dev.last_batch_stats()["windows"] > 0
     finally:
         dev.close()
+
+
+@pytest.mark.parametrize("window", [128, 0])
+def test_rccl_one_rank_config2_every_extension_matches_oracle(window):
+    """Config 2's shape (5,000 nodes) + taints, GPU counts, BalancedAllocation and
+    TaintToleration over a 1-rank RCCL communicator: the sharded exchange path's
+    ncclAllGather per window / per pod and the ncclAllReduce (max, sum) of the
+    TaintToleration terms, against the C restatement (parity unpinned)."""
+    from oracle.pyoracle import OracleScheduler
+    from tests.ext_cases import ExtCase
+
+    c = ExtCase("config2", 5000, 2400 if window else 600)
+    orc = c.load(OracleScheduler(c.cfg))
+    dev = c.load(_rccl_ctx(c.cfg))
+    try:
+        dev.set_window(window)
+        for i in range(0, 60, 3):  # placed pods with extended resource requests
+            dev.add_pod(i * 7, c.batch, i)
+            orc.add_pod(i * 7, c.batch, i)
+        from kubernetes_amd.engine import PodBatch
+        rest = PodBatch(c.batch.pods[60:], c.batch.ids, c.batch.ext[60:])
+        got, rg = dev.batch(rest, 99)
+        want, rw = orc.batch(rest, 99)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, f"first mismatches at {bad[:8]}: {got[bad[:8]]} vs {want[bad[:8]]}"
+        assert rg == rw
+        assert np.array_equal(dev.read_ext_used(), orc.read_ext_used())
+        if window:
+            assert dev.last_batch_stats()["windows"] > 0
+    finally:
+        dev.close()
+        orc.close()
 
 
 def test_rccl_one_rank_begin_commit_matches_oracle():

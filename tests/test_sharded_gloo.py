@@ -193,3 +193,78 @@ def test_two_rank_anti_affinity_domain_allreduce():
         assert split >= 20, split  # the reduction actually combines two shards
         assert np.array_equal(np.asarray(out), want), rank
         assert rng == st
+
+
+def _ext_worker(rank, world, port, nn, npods, seed, q):
+    """The extensions' sharded step (ksg_runtime.cpp scan_exchange and the window path's
+    count pass + all-reduce; parity unpinned): each rank takes the
+    pod's max untolerated soft-taint count over the filtered nodes of its own shard
+    (TaintTolerationPriority's NormalizeReduce max), the partials are all-reduced (MAX),
+    every rank scores its shard with the global max, the shard records go through the
+    product's winner rule, and every rank commits the winner with its extension record
+    (extended resources)."""
+    from tests.ext_cases import ExtCase
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c = ExtCase("config2", nn, npods, w_taint=2, w_bal=1)
+        n = c.case.view.arrays.n_nodes
+        lo, hi = shard_range(n, rank, world)
+        spans = [shard_range(n, g, world) for g in range(world)]
+        nwords_max = max((b + 63) // 64 - a // 64 for a, b in spans)
+        orc = c.load(OracleScheduler(c.cfg))
+        rng = seed
+        out, reduced_equal, split = [], True, 0
+        for i in range(len(c.batch)):
+            part = orc.taint_max(c.batch, i, lo, hi)
+            t = torch.tensor([part], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            glob = int(t.item())
+            reduced_equal &= glob == orc.taint_max(c.batch, i, 0, n)
+            split += int(part < glob)  # the other shard holds the max
+            rc, fails, scores = orc.evaluate_tmax(c.batch, i, glob)
+            rec = make_shard_record(fails[lo:hi], scores[lo:hi], lo, lo // 64, nwords_max, error=rc < 0)
+            gathered = [torch.zeros(len(rec), dtype=torch.uint8) for _ in range(world)]
+            dist.all_gather(gathered, torch.from_numpy(rec))
+            recs = np.stack([g.numpy() for g in gathered])
+            mrc, node, _, _, rng = merge_records(recs, n, rng_state=rng)
+            if mrc == abi.KSG_OK:
+                orc.add_pod(node, c.batch, i)
+                out.append(node)
+            else:
+                out.append(abi.KSG_OUT_NOFIT if mrc == abi.KSG_NOFIT else abi.KSG_OUT_ERROR)
+        q.put((rank, out, rng, reduced_equal, split, orc.read_ext_used().tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_extension_taint_max_allreduce():
+    """World-2 gloo rehearsal of the sharded extension path: the
+    all-reduced shard maxima equal the whole cluster's TaintToleration max for every pod,
+    and scoring each shard with it (plus BalancedAllocation and extended resources)
+    reproduces the single-process schedule and extended-resource usage."""
+    from tests.ext_cases import ExtCase
+
+    nn, npods, seed = 700, 300, 77
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ext_worker, args=(r, WORLD, port, nn, npods, seed, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(WORLD)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    c = ExtCase("config2", nn, npods, w_taint=2, w_bal=1)
+    orc = c.load(OracleScheduler(c.cfg))
+    want, st = orc.batch(c.batch, seed)
+    used = orc.read_ext_used().tolist()
+    for rank, out, rng, reduced_equal, split, ext_used in res:
+        assert reduced_equal, rank
+        assert np.array_equal(np.asarray(out), want), rank
+        assert split >= 3, split  # the reduction actually combines two shards
+        assert rng == st
+        assert ext_used == used
