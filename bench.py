@@ -44,9 +44,22 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 
+from tools.srcsha import kernel_src_sha  # noqa: E402
+
 HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md chip-level parameters
 CLOCK_MHZ = 2400.0  # MI355X max engine clock (MI355X_MICROARCH.md); the resolver's stamps count it
 BYTES_PER_NODE = {"config1": 32, "config2": 60, "config3": 60, "config4": 64, "config5": 84}
+
+
+def traffic_entry(tj, key, src_sha, stale):
+    """profiles/traffic.json's PMC entry for key, only when it was measured on the build of
+    these sources (its kernel_src_sha, tools/srcsha.py); an entry from another build is
+    appended to stale (reported as roofline.traffic_source.stale) and not used."""
+    ent = tj.get(key)
+    if ent and ent.get("kernel_src_sha") != src_sha:
+        stale.append({"entry": key, "source": ent.get("source"), "round": ent.get("round")})
+        return None
+    return ent
 
 
 def _dist_env():
@@ -389,18 +402,28 @@ def main():
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        ent = tj.get(f"{wl}:{n_nodes}:{kname}")
-        if ent:
-            traffic = ent["hbm_bytes_per_launch"]
     except (OSError, ValueError):
         pass
+    src_sha = kernel_src_sha()
+    stale = []
+
+    def counters(key):
+        return traffic_entry(tj, key, src_sha, stale)
+
+    ent = counters(f"{wl}:{n_nodes}:{kname}")
+    if ent:
+        traffic = ent["hbm_bytes_per_launch"]
+    traffic_source = {"kernel_src_sha": src_sha, "resolver": ent and {"source": ent["source"], "round": ent["round"]},
+                      "stale": stale}
     roofline = {"bound": "hbm", "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK, "traffic": traffic, "kernel": kname,
                 "kernel_ms_avg": kavg_s * 1e3, "bytes_per_node_pod": bpn, "alg_bytes_per_launch": alg_bytes}
     roofline.update(extra)
+    roofline["traffic_source"] = traffic_source
     filter_score = None
     if kk["launches"] > 0:
-        ent = tj.get(f"{wl}:{n_nodes}:ksg_win_score_kernel")  # phase A's counter-measured bytes (profiles/)
+        ent = counters(f"{wl}:{n_nodes}:ksg_win_score_kernel")  # phase A's counter-measured bytes (profiles/)
+        traffic_source["filter_score"] = ent and {"source": ent["source"], "round": ent["round"]}
         if ent:
             roofline["win_eval_traffic"] = ent["hbm_bytes_per_launch"]
             roofline["win_eval_traffic_GBps"] = ent["hbm_bytes_per_launch"] / ev_s / 1e9

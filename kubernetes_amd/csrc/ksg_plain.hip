@@ -751,7 +751,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
         if (lane == 0) {
           ctl->chk_cnt[c][par] = 0;
           ctl->chk_msk[c][par][0] = ctl->chk_msk[c][par][1] = 0;
-          st_rel(&ctl->chk_seq[c], i + 1);
+          st_post(&ctl->chk_seq[c], i + 1);
         }
         continue;
       }
@@ -893,7 +893,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
         ctl->chk_cnt[c][par] = (uint32_t)__popcll(dmsk);
         ctl->chk_msk[c][par][0] = (uint32_t)dmsk;
         ctl->chk_msk[c][par][1] = (uint32_t)(dmsk >> 32);
-        st_rel(&ctl->chk_seq[c], i + 1);
+        st_post(&ctl->chk_seq[c], i + 1);
       }
       cstamp(c == 0 ? 18 : 21);
     }
@@ -1030,7 +1030,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
       if (skew & 2u) __builtin_amdgcn_s_sleep(8);
       fstamp(39);
       flag_commit(q);
-      if (lane == 0) st_rel(&ctl->fseq, q + 1);
+      if (lane == 0) st_post(&ctl->fseq, q + 1);
       fstamp(40);
     }
     // the committer is done: pods [0, resolved) are decided; the first peers of the
@@ -1216,7 +1216,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
       if (skew & 2u) __builtin_amdgcn_s_sleep(8);
       if ((xpt & 1u) && lane == 0) {
         ctl->xres[par] = 0;
-        st_rel(&ctl->xseq, i + 1);
+        st_post(&ctl->xseq, i + 1);
       }
       const uint32_t xnode = xv == ~0u ? ~0u : xv & 0x0fffffffu, xcid = xv == ~0u ? KSG_NO_CAND : xv >> 28;
       uint32_t xslot = 0, bnk = 0, bns = 0, xkinds = 0;
@@ -1228,7 +1228,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
         // only the replay is left here (off the chain)
         const bool fresh = (__ballot(xcn0 == xnode) | __ballot(xcn1 == xnode)) == 0;
         if (fresh && !pod_has_service(prec, s)) {
-          if (lane == 0) st_rel(&ctl->xseq, i + 1);  // (no verdict: the committer does not read it)
+          if (lane == 0) st_post(&ctl->xseq, i + 1);  // (no verdict: the committer does not read it)
           replay(xnode, prec, xslot, bnk, bns, dlc, dlm, xkinds, xdl);
           if constexpr (STAMP) {
             const uint64_t t_now = __builtin_amdgcn_s_memtime();
@@ -1436,7 +1436,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
       if (lane == 0 && !(xpt & 1u)) {
         ctl->xres[par] = res;
         if constexpr (STAMP) ctl->t_x = (uint32_t)__builtin_amdgcn_s_memtime();
-        st_rel(&ctl->xseq, i + 1);
+        st_post(&ctl->xseq, i + 1);
       }
       if constexpr (STAMP) {
         const uint64_t t_now = __builtin_amdgcn_s_memtime();
@@ -1557,8 +1557,8 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
         L_cm[i].kind = 0;
         L_cm[i].out = __builtin_amdgcn_readlane(rec, WS_ERR) ? KSG_OUT_ERROR : KSG_OUT_NOFIT;
         L_cm[i].xn = ~0u;
-        st_rel(&ctl->xn_seq, i + 1);
-        st_rel(&ctl->sel_seq, i + 1);
+        st_post(&ctl->xn_seq, i + 1);
+        st_post(&ctl->sel_seq, i + 1);
       }
       have_x = false;  // pod i+1's checkers see every commit up to i-1
       continue;
@@ -1835,7 +1835,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
     if (lane == 0) {  // the x-checker takes the node's snapshot meanwhile
       L_cm[i].xn = woff | (cidx << 28);
       if constexpr (STAMP) ctl->t_n = (uint32_t)__builtin_amdgcn_s_memtime();
-      st_rel(&ctl->xn_seq, i + 1);
+      st_post(&ctl->xn_seq, i + 1);
     }
     KSG_STAMPP(3)
     // ---- AssumePod's slot
@@ -1881,7 +1881,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
       *reinterpret_cast<uint4*>(&L_cm[i]) =
           uint4{1u, slot, woff, (in_c ? 0u : 1u) | (cidx << 1) | (n_svcs << 8) | (base_ns << 16) | (base_nk << 24)};
       L_cm[i].out = (int32_t)wn;
-      st_rel(&ctl->sel_seq, i + 1);  // the checkers move on
+      st_post(&ctl->sel_seq, i + 1);  // the checkers move on
     }
     if ((int32_t)woff != pred) KSG_COUNTP(8, 64)
     if (lane == (slot & 63)) {  // this wave's counts and deltas of the slot

@@ -181,6 +181,20 @@ __device__ __forceinline__ uint32_t ld_acq(uint32_t* p) {
 __device__ __forceinline__ void st_rel(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// a sequence post publishing data THIS wave wrote to LDS before it: the LDS runs one wave's
+// instructions in issue order, so the data lands before the post without the release's
+// lgkmcnt(0) wait (which also waits for every LDS read in flight: an LDS round trip on the
+// chain). Readers poll with ld_rlx and read the data in the same round (in order too). A post
+// that publishes global memory, or another wave's writes, takes st_rel. (-DKSG_POST_RELEASE:
+// st_rel everywhere, for A/B runs)
+__device__ __forceinline__ void st_post(uint32_t* p, uint32_t v) {
+#ifdef KSG_POST_RELEASE
+  st_rel(p, v);
+#else
+  asm volatile("" ::: "memory");  // (the compiler keeps the data stores ahead of the post)
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
+}
 // polling: relaxed LDS loads issue back to back under one lgkmcnt wait (an
 // acquire load waits for each), then one LDS-only acquire once the wait is over
 // (no vmcnt wait on the poller's loads in flight)

@@ -1,0 +1,41 @@
+"""bench.py's counter bookkeeping (CPU): profiles/traffic.json entries are used only for the
+build they were measured on ("make every bench line's roofline reproducible")."""
+import json
+import os
+
+import bench
+from tools.srcsha import ROOT, kernel_src_sha
+
+
+def test_traffic_entry_from_another_build_is_refused():
+    sha = kernel_src_sha()
+    tj = {"config2:5000:ksg_win_plain_kernel": {"hbm_bytes_per_launch": 1.0, "source": "prof_old", "round": "r4",
+                                                 "kernel_src_sha": "0" * 16},
+          "config2:5000:ksg_win_score_kernel": {"hbm_bytes_per_launch": 2.0, "source": "prof_new", "round": "r5",
+                                                "kernel_src_sha": sha},
+          "config3:15000:ksg_win_score_kernel": {"hbm_bytes_per_launch": 3.0, "source": "prof_r2f_config3"}}
+    stale = []
+    assert bench.traffic_entry(tj, "config2:5000:ksg_win_plain_kernel", sha, stale) is None
+    assert bench.traffic_entry(tj, "config2:5000:ksg_win_score_kernel", sha, stale)["hbm_bytes_per_launch"] == 2.0
+    assert bench.traffic_entry(tj, "config3:15000:ksg_win_score_kernel", sha, stale) is None  # (untagged: refused)
+    assert bench.traffic_entry(tj, "config9:1:none", sha, stale) is None
+    assert [s["source"] for s in stale] == ["prof_old", "prof_r2f_config3"]
+
+
+def test_kernel_src_sha_tracks_the_sources(tmp_path):
+    # a copy of the tree's source layout: one changed byte changes the tag
+    for sub in ("kubernetes_amd/csrc", "include"):
+        os.makedirs(tmp_path / sub)
+    (tmp_path / "include" / "kschedgpu.h").write_text("x")
+    (tmp_path / "kubernetes_amd" / "csrc" / "a.hip").write_text("y")
+    a = kernel_src_sha(str(tmp_path))
+    (tmp_path / "kubernetes_amd" / "csrc" / "a.hip").write_text("z")
+    assert kernel_src_sha(str(tmp_path)) != a
+    assert len(kernel_src_sha(ROOT)) == 16
+
+
+def test_committed_traffic_entries_name_their_source():
+    with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
+        tj = json.load(f)
+    for key, ent in tj.items():
+        assert ent["hbm_bytes_per_launch"] > 0 and ent["source"], key

@@ -11,6 +11,10 @@ doubling is calibrated here for every access width the kernels use
 8-B loads -- FETCH_SIZE x 1024 is exactly half the bytes of the 128-B lines
 touched in each case.
 
+Each entry carries the round tag (KSG_ROUND, e.g. "r5") and the kernel sources' sha
+(tools/srcsha.py) of the tree it was measured on; bench.py takes an entry only when that
+sha is the current one.
+
 usage: tools/traffic_from_pmc.py <prof_dir> <workload> <n_nodes> [profiles/traffic.json]
 """
 import csv
@@ -18,6 +22,9 @@ import json
 import os
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from tools.srcsha import kernel_src_sha  # noqa: E402
 
 KERNELS = {"ksg_win_plain_kernel": "ksg_win_plain_kernel", "ksg_win_t0_kernel": "ksg_win_t0_kernel",
            "ksg_win_resolve_kernel": "ksg_win_resolve_kernel", "ksg_win_resolve2_kernel": "ksg_win_resolve2_kernel",
@@ -53,6 +60,7 @@ def main():
         wb = write.get(k, 0.0)
         tj[f"{wl}:{n_nodes}:{k}"] = {"hbm_bytes_per_launch": fb + wb, "fetch_bytes_per_launch": fb,
                                      "write_bytes_per_launch": wb, "source": os.path.basename(prof.rstrip("/")),
+                                     "round": os.environ.get("KSG_ROUND", ""), "kernel_src_sha": kernel_src_sha(),
                                      "note": "FETCH_SIZE KiB x1024 x2 (gfx950, calibrated: profiles/r3_fetch_calib.json) + WRITE_SIZE KiB x1024, mean per launch"}
         print(k, tj[f"{wl}:{n_nodes}:{k}"])
     with open(out, "w") as f:
