@@ -323,7 +323,7 @@ def main():
     assert tot1["batches"] - tot0["batches"] == args.steps
     kern_ms = [(tot1["device_ms"] - tot0["device_ms"]) / args.steps]
     host_us = {k_: tot1["host_us"][k_] - tot0["host_us"][k_] for k_ in tot1["host_us"]}
-    kk = {k_: tot1[k_] - tot0[k_] for k_ in ("eval_ms", "resolve_ms", "launches")}
+    kk = {k_: tot1[k_] - tot0[k_] for k_ in ("eval_ms", "resolve_ms", "launches", "t0_ms")}
     wstats = {k_: tot1[k_] - tot0[k_] for k_ in ("windows", "stops_service", "stops_exhausted", "stops_cache")}
     if dist is not None:
         import torch
@@ -374,8 +374,9 @@ def main():
         kname = ("ksg_win_plain_kernel" if plain else
                  "ksg_win_resolve_kernel" if anti else "ksg_win_resolve2_kernel")
         # phase A scores this rank's shard (N/world nodes) for the window's W pods
-        # (the capacity the library used: it shrinks W where windows stop early);
-        # with world > 1 its event window also holds the per-window all-gather.
+        # (the capacity the library used: it shrinks W where windows stop early); its
+        # events bracket the scoring kernel(s) only (the T0-image kernel and, with
+        # world > 1, the per-window all-gather are timed apart: win_t0_ms_avg).
         ev_s = kk["eval_ms"] / launches / 1e3 or float("nan")
         w_used = tot1["wcap_sum"] - tot0["wcap_sum"]
         w_mean = w_used / launches if w_used > 0 else float(wcap)
@@ -386,6 +387,7 @@ def main():
         extra = {"launches": launches, "pods_per_launch": pods_per_launch,
                  "timed_launch_stride": int(os.environ.get("KSG_KERNEL_EVENTS", "4") or 0),
                  "win_eval_ms_avg": kk["eval_ms"] / launches,
+                 "win_t0_ms_avg": kk["t0_ms"] / launches,
                  "win_eval_model_bytes_per_launch": ev_bytes,
                  "win_eval_pods_per_launch": w_mean,
                  "win_eval_model_GBps": ev_bytes / ev_s / 1e9,

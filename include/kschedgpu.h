@@ -305,7 +305,8 @@ int ksg_last_batch_stats(ksg_ctx* ctx, uint32_t* stats4);
 int ksg_last_batch_ms(ksg_ctx* ctx, double* ms);
 
 /* Window path of the last ksg_schedule_batch: out3[0] = device ms in the
- * snapshot-scoring kernel(s) (ksg_win_score_kernel), out3[1] = device ms in the
+ * snapshot-scoring kernel(s) (ksg_win_score_kernel, and its count pass; not the
+ * T0-image kernel: ksg_batch_totals [18]), out3[1] = device ms in the
  * resolver (ksg_win_plain_kernel, or with ServiceAntiAffinity
  * ksg_win_resolve2_kernel / ksg_win_resolve_kernel), out3[2] = resolver launches (windows are
  * chained on the device, so a round may end with launches that find the batch
@@ -332,7 +333,9 @@ int ksg_last_batch_host_us(ksg_ctx* ctx, double* out8);
  * ms (ksg_last_batch_ms), [2..4] ksg_last_batch_kernel_ms, [5..8]
  * ksg_last_batch_stats, [9..16] ksg_last_batch_host_us, [17] the window
  * capacity (pods phase A scores per launch) summed over the window-path
- * launches, [18..23] zero. */
+ * launches, [18] device ms between phase A and the resolver (the sharded
+ * exchange and the T0-image kernel, ksg_win_t0_kernel; sampled like
+ * ksg_last_batch_kernel_ms), [19..23] zero. */
 int ksg_batch_totals(ksg_ctx* ctx, double* out24);
 
 /* Diagnostics: the window resolver's per-stage clock counters (s_memtime

@@ -216,6 +216,7 @@ struct ksg_ctx {
   uint32_t last_stats[4] = {0, 0, 0, 0};  // windows, stops (service scalar), stops (ties exhausted)
   std::vector<hipEvent_t> wev;     // event pairs around the chained window kernels
   double last_kms[3] = {0, 0, 0};  // phase A ms, phase B ms, launches (window path)
+  double last_t0ms = 0;            // ... and between them: the exchange (sharded) and the T0 images
   double last_wsum = 0;            // window capacity W summed over the launches
   bool dbg_fail_next = false;      // KSG_DEBUG & 16384: the next window batch fails after its device work
   uint32_t dbg_corrupt = 0;        // KSG_DEBUG bits 22 / 23: corrupt the next COMMIT / BEGIN request's layout
@@ -1550,7 +1551,7 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   // out-of-range payload layout (tests/test_gpu_serve.py: the server must reject it, not fault)
   c->dbg_corrupt = ((uint32_t)d.dbg >> 22) & 3u;
   c->win_d1 = !(getenv("KSG_WIN_D1") && atoi(getenv("KSG_WIN_D1")) == 0);
-  if (d.dbg & (8 | 32)) {  // (32: the plain resolver's inconsistency record, ksg_plain.hip)
+  if (d.dbg & (8 | 32 | 64)) {  // (32: the plain resolver's inconsistency record, ksg_plain.hip; 64: phase-A stamps)
     (void)hipMalloc(&d.dbgbuf, KSG_DEBUG_COUNTER_WORDS * sizeof(int32_t));
     (void)hipMemset(d.dbgbuf, 0, KSG_DEBUG_COUNTER_WORDS * sizeof(int32_t));
   }
@@ -2055,7 +2056,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
   HIPCHK(c, hipMemcpyAsync(c->d_rng, rng_state, 8, hipMemcpyHostToDevice, c->st));
   HIPCHK(c, hipEventRecord(c->ev0, c->st));
   c->last_stats[0] = c->last_stats[1] = c->last_stats[2] = c->last_stats[3] = 0;
-  c->last_kms[0] = c->last_kms[1] = c->last_kms[2] = 0;
+  c->last_kms[0] = c->last_kms[1] = c->last_kms[2] = c->last_t0ms = 0;
   c->last_wsum = 0;
   hphase(1);
   const ksg_pod_ext* dext = nullptr;
@@ -2172,13 +2173,13 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       return (uint32_t)std::min(k, 8192.0);
     };
     uint32_t pos = 0, K = round_k(n);
-    c->last_kms[0] = c->last_kms[1] = c->last_kms[2] = 0;
+    c->last_kms[0] = c->last_kms[1] = c->last_kms[2] = c->last_t0ms = 0;
     c->last_wsum = 0;
     hphase(2);
     while (pos < n) {
-      if (c->wev.size() < 2 * (size_t)K + 1) {
+      if (c->wev.size() < 3 * (size_t)K + 1) {
         const size_t old = c->wev.size();
-        c->wev.resize(2 * (size_t)K + 1, nullptr);
+        c->wev.resize(3 * (size_t)K + 1, nullptr);
         for (size_t i = old; i < c->wev.size(); ++i) HIPCHK(c, hipEventCreateWithFlags(&c->wev[i], kTimingEvent));
       }
       // the sampled launches rotate from round to round (launches k with
@@ -2192,7 +2193,9 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       for (uint32_t k = 0; k < K; ++k) {
         // HIP events on this stream around the sampled launches (per-kernel device time)
         const bool evk = es && (k + ev_off) % es == 0;
-        if (evk && k > 0) HIPCHK(c, hipEventRecord(c->wev[2 * k], c->st));
+        // (launch k: events 3k before phase A, 3k+1 after it, 3k+2 before the resolver, 3k+3 =
+        // the next launch's 3(k+1) after it)
+        if (evk && k > 0) HIPCHK(c, hipEventRecord(c->wev[3 * k], c->st));
         if (anti) {
           // ServiceAntiAffinity: the pods' per-domain counts over their filtered nodes first
           // (into d_dcnt, zero: the previous resolver cleared it)
@@ -2215,11 +2218,12 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
                                       (anti || esc || d1) ? reinterpret_cast<uint64_t*>(c->d_xsend + fit_off) : nullptr,
                                       x.dmb, rr ? reinterpret_cast<uint64_t*>(c->d_xsend + x.b_off) : nullptr, x.dz,
                                       c->st, dext, x.tmax, x.psoft));
+        if (evk) HIPCHK(c, hipEventRecord(c->wev[3 * k + 1], c->st));
         if (c->xchg && (rc = allgather(c, c->d_xsend, c->d_xrecv, x.blk))) return rc;
         if (plain) HIPCHK(c, ksg_launch_win_t0(full, W, c->d_run, x, c->st));
-        if (evk) HIPCHK(c, hipEventRecord(c->wev[2 * k + 1], c->st));
+        if (evk) HIPCHK(c, hipEventRecord(c->wev[3 * k + 2], c->st));
         HIPCHK(c, ksg_launch_win_resolve(full, W, c->d_run, c->d_winsum, x, c->d_rng, c->d_out, c->st));
-        if (evk) HIPCHK(c, hipEventRecord(c->wev[2 * k + 2], c->st));
+        if (evk) HIPCHK(c, hipEventRecord(c->wev[3 * k + 3], c->st));
       }
       HIPCHK(c, hipMemcpyAsync(c->h_run, c->d_run, sizeof(KsgWinRun), hipMemcpyDeviceToHost, c->st));
       if ((rc = enqueue_tail())) return rc;
@@ -2236,19 +2240,22 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       // the sampled launches (every one of the round's launches is a sampling
       // candidate, including the ones after the batch was done, which return at
       // once, so the mean matches a kernel trace of the run), scaled to all K
-      double ea = 0.0, eb = 0.0;
+      double ea = 0.0, eb = 0.0, et = 0.0;
       uint32_t nt = 0;
       for (uint32_t k = es ? (es - ev_off) % es : 0u; es && k < K; k += es) {
-        float a = 0.f, b = 0.f;
-        HIPCHK(c, hipEventElapsedTime(&a, c->wev[2 * k], c->wev[2 * k + 1]));
-        HIPCHK(c, hipEventElapsedTime(&b, c->wev[2 * k + 1], c->wev[2 * k + 2]));
+        float a = 0.f, t0 = 0.f, b = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&a, c->wev[3 * k], c->wev[3 * k + 1]));
+        HIPCHK(c, hipEventElapsedTime(&t0, c->wev[3 * k + 1], c->wev[3 * k + 2]));
+        HIPCHK(c, hipEventElapsedTime(&b, c->wev[3 * k + 2], c->wev[3 * k + 3]));
         ea += a;
+        et += t0;
         eb += b;
         ++nt;
       }
       if (nt) {
         c->last_kms[0] += ea * K / nt;
         c->last_kms[1] += eb * K / nt;
+        c->last_t0ms += et * K / nt;
       }
       c->last_kms[2] += K;
       c->last_wsum += (double)W * K;
@@ -2338,6 +2345,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
   t[1] += c->last_ms;
   for (int q = 0; q < 3; ++q) t[2 + q] += c->last_kms[q];
   t[17] += c->last_wsum;
+  t[18] += c->last_t0ms;
   for (int q = 0; q < 4; ++q) t[5 + q] += c->last_stats[q];
   for (int q = 0; q < 8; ++q) t[9 + q] += c->last_hus[q];
   return KSG_OK;

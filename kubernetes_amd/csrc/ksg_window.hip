@@ -80,8 +80,13 @@
 // EXT: the extensions' filters (PodToleratesNodeTaints: static per (pod, node);
 // extended resources: allocatable >= used + request, monotone under commits
 // like cpu / memory), MODE PLAIN only
+#ifdef KSG_PA_WAVES  // (A/B builds: an occupancy floor for phase A)
+#define KSG_PA_ATTR __attribute__((amdgpu_waves_per_eu(KSG_PA_WAVES, 8)))
+#else
+#define KSG_PA_ATTR
+#endif
 template <int MODE, int KSG_PG, bool EXT = false>
-__global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, const ksg_pod* __restrict__ batch,
+__global__ __launch_bounds__(KSG_SC_NT) KSG_PA_ATTR void ksg_win_score_kernel(KsgDev d, const ksg_pod* __restrict__ batch,
                                                                  const uint32_t* __restrict__ ids,
                                                                  const KsgWinRun* __restrict__ run, uint32_t wcap,
                                                                  KsgWinSum* __restrict__ sums,
@@ -117,6 +122,12 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
   if ((w >= d.nwords && w != 0) || p0 >= n_pods) return;  // wave-uniform
   const bool has_word = w < d.nwords;
   const uint32_t np = min((uint32_t)KSG_PG, n_pods - p0);
+  // KSG_DEBUG & 64: per-wave phase-A stamps into dbgbuf[48..50] (cycles / 16): the loads (to
+  // the scoring loop, every load landed), scoring + stores, the wave count (tools/pa_stamps.py;
+  // a diagnostic: the vmcnt(0) it adds before the loop changes the schedule)
+  const bool pst = (d.dbg & 64) && d.dbgbuf;
+  const uint64_t ts0 = pst ? __builtin_amdgcn_s_memtime() : 0ULL;
+  uint64_t ts1 = 0;
   const uint32_t gw = d.wlo + w;  // global word
   const uint32_t n = gw * 64 + lane;
   const bool valid = has_word && n < d.hi;
@@ -294,6 +305,10 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
       mbz[j] = ((uint32_t)j < np && zrow >= 0) ? dmb[(size_t)(p0 + j) * dz + zrow] : KSG_S32_NONE;
   }
 
+  if (pst) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ts1 = __builtin_amdgcn_s_memtime();
+  }
   // ---- score every pod of the group on this word
   const int32_t w_lr = (int32_t)d.w_lr, w_spread = (int32_t)d.w_spread;  // (|w| < 2^30 / 10 on this path)
   int32_t my_max = KSG_S32_NONE;
@@ -471,6 +486,12 @@ __global__ __launch_bounds__(KSG_SC_NT) void ksg_win_score_kernel(KsgDev d, cons
   }
   if constexpr (EXT)
     if (psoft && w == 0 && lane < np) psoft[p0 + lane] = ps;
+  if (pst && lane == 0) {
+    const uint64_t ts2 = __builtin_amdgcn_s_memtime();
+    atomicAdd(d.dbgbuf + 48, (int32_t)((ts1 - ts0) >> 4));
+    atomicAdd(d.dbgbuf + 49, (int32_t)((ts2 - ts1) >> 4));
+    atomicAdd(d.dbgbuf + 50, 1);
+  }
 
   // ---- the resolver's record of each pod (one wave per pod group)
   if (w == 0) {

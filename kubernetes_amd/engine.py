@@ -297,7 +297,7 @@ class DeviceScheduler:
                 "resolve_ms": float(o[3]), "launches": int(o[4]), "windows": int(o[5]),
                 "stops_service": int(o[6]), "stops_exhausted": int(o[7]), "stops_cache": int(o[8]),
                 "host_us": {k: float(v) for k, v in zip(self.HOST_PHASES, o[9:17])},
-                "wcap_sum": float(o[17])}
+                "wcap_sum": float(o[17]), "t0_ms": float(o[18])}
 
     def set_static_terms(self, fit_words, score, weighted: bool):
         """ksg_set_static_terms: static node terms past the config's slots (after

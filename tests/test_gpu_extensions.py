@@ -159,9 +159,21 @@ def test_config5_extensions_full_size_matches_restatement():
     size-independent checks (usage == the placed pods' requests, no node above
     its allocatable). Parity unpinned: nothing in this reference vintage reads
     extended resources (pkg/api/resource_helpers.go:29-42)."""
+    _config5_full_size(w_taint=0, w_bal=0)
+
+
+def test_config5_extension_scores_full_size_matches_restatement():
+    """The same at full size with the extension SCORES on as well (TaintToleration weight 1,
+    BalancedResourceAllocation weight 1): the window path's per-pod TaintToleration max
+    count pass and the resolver's re-score of committed nodes (risers / joiners) over
+    100 windows-worth of 1,000-pod batches."""
+    _config5_full_size(w_taint=1, w_bal=1)
+
+
+def _config5_full_size(w_taint, w_bal):
     import os
 
-    c = ExtCase("config5", 100000, 100000, w_taint=0, w_bal=0)
+    c = ExtCase("config5", 100000, 100000, w_taint=w_taint, w_bal=w_bal)
     dev = c.load(DeviceScheduler(c.cfg, device=0))
     got, rng, windows = [], 1234, 0
     for s in range(0, len(c.batch), 1000):

@@ -243,6 +243,8 @@ def test_batch_totals_sum_the_per_batch_diagnostics():
     assert t1["batches"] == 2 and win == t1["windows"] > 0
     assert abs(t1["device_ms"] - dms) < 1e-9 and abs(t1["resolve_ms"] - res) < 1e-9
     assert t1["host_us"]["validate"] > 0
+    # phase A, the T0-image kernel and the resolver are timed apart (every 4th launch sampled)
+    assert t1["eval_ms"] > 0 and t1["t0_ms"] > 0 and t1["resolve_ms"] > 0
     dev.close()
 
 

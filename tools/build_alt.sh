@@ -1,11 +1,23 @@
-# A/B helper: build kubernetes_amd/_alt/libkschedgpu.so with ksg_plain.hip compiled under extra
-# defines (e.g. tools/build_alt.sh -DKSG_POST_RELEASE), the other objects from the main build;
-# load it with KSG_LIB=kubernetes_amd/_alt/libkschedgpu.so (abi.py).
+# A/B helper: build kubernetes_amd/_alt/<name>/libkschedgpu.so with one kernel source compiled
+# under extra defines, or from another git revision, the other objects from the main build
+# (run the main build first); load it with KSG_LIB=_alt/<name>/libkschedgpu.so (abi.py).
+# usage: tools/build_alt.sh <name> <plain|window> [REV|-] [hipcc defines...]
 set -e
 cd "$(dirname "$0")/.."
+NAME=$1; SRC=$2; REV=$3; shift 3
 O=kubernetes_amd/csrc/_obj
-mkdir -p kubernetes_amd/_alt
+D=kubernetes_amd/_alt/$NAME
+mkdir -p "$D"
+F=kubernetes_amd/csrc/ksg_$SRC.hip
+if [ "$REV" != "-" ]; then
+  git show "$REV:$F" > "$D/ksg_$SRC.hip"
+  F="$D/ksg_$SRC.hip"
+fi
 hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-strict-aliasing -Wall -Wno-unused-function \
-  "$@" -c kubernetes_amd/csrc/ksg_plain.hip -o $O/ksg_plain_alt.o
-hipcc --offload-arch=gfx950 -shared -fPIC $O/ksg_kernels.o $O/ksg_window.o $O/ksg_plain_alt.o $O/ksg_admit.o \
-  $O/ksg_serve.o $O/ksg_runtime.o -o kubernetes_amd/_alt/libkschedgpu.so -lrccl
+  -I kubernetes_amd/csrc -I include "$@" -c "$F" -o "$D/ksg_$SRC.o"
+objs=""
+for k in kernels window plain admit serve; do
+  if [ "$k" = "$SRC" ]; then objs="$objs $D/ksg_$k.o"; else objs="$objs $O/ksg_$k.o"; fi
+done
+hipcc --offload-arch=gfx950 -shared -fPIC $objs $O/ksg_runtime.o -o "$D/libkschedgpu.so" -lrccl
+rm -f "$D/ksg_$SRC.o" "$D/ksg_$SRC.hip"
