@@ -1490,6 +1490,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
     uint32_t rec, rmod, lp_ex, lp_in, cand, xlp, xwp, m0, k0, pred;
     uint64_t t0x, d1x;
   };
+  const uint32_t zv = opaque_v(0u);
   auto head_reads = [&](uint32_t e) -> Head {
     // (every lane reads, at a clamped index: no exec-mask branch between the reads; the
     // lanes past each array are masked once the reads are back)
@@ -1501,14 +1502,17 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
     h.cand = r_cand[e * 8 + min(lane, (uint32_t)KSG_NCAND - 1)];
     // (read whether or not there is an x: no branch between the reads, the word is
     // masked once they are back)
-    const uint32_t xw = have_x ? xnode >> 6 : 0u;
+    // (uniform words, read at an index offset by zv, a zero the compiler cannot see: it keeps
+    // them in VGPRs until their use instead of moving each to an SGPR right behind its read,
+    // which would wait for the read there, splitting this round in two)
+    const uint32_t xw = (have_x ? xnode >> 6 : 0u) + zv;
     h.t0x = r_t0[(size_t)e * P * 64 + xw];
     h.d1x = pl_d1(P) ? r_d1[(size_t)e * P * 64 + xw] : 0ULL;
     h.xlp = r_lp[e * 64 + (xw >> 6) * 2];
     h.xwp = r_wp[(size_t)e * P * 64 + xw];
-    h.m0 = (uint32_t)r_hdr[e].m0;
-    h.k0 = r_hdr[e].k0;
-    h.pred = (uint32_t)r_hdr[e].pred;
+    h.m0 = (uint32_t)r_hdr[e + zv].m0;
+    h.k0 = r_hdr[e + zv].k0;
+    h.pred = (uint32_t)r_hdr[e + zv].pred;
     __builtin_amdgcn_sched_barrier(0);  // (every read issued before any of them is used)
     return h;
   };
@@ -1543,9 +1547,9 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
     const uint32_t rec = lane < DW ? h.rec : 0u, rmod = h.rmod;
     const uint32_t lp_ex = lane < P ? h.lp_ex : 0u, lp_in = lane < P ? h.lp_in : 0u;
     const uint32_t cand = lane < KSG_NCAND ? h.cand : ~0u;
-    const uint32_t xpos0 = have_x ? h.xlp + h.xwp : 0u;
+    const uint32_t xpos0 = have_x ? __builtin_amdgcn_readfirstlane(h.xlp + h.xwp) : 0u;
     const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
-    const uint64_t t0x = have_x ? h.t0x : 0ULL;
+    const uint64_t t0x = have_x ? readlane64(h.t0x, 0) : 0ULL;
     const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(h.m0);
     const uint32_t k0 = __builtin_amdgcn_readfirstlane(h.k0);
     const int32_t pred = (int32_t)__builtin_amdgcn_readfirstlane(h.pred);
@@ -1635,7 +1639,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
     KSG_STAMPP(2)
     if constexpr (STAMP) t_acc += lane == 6 ? (uint64_t)(uint32_t)((uint32_t)t_last - ctl->t_x) : 0ULL;
     const uint32_t cc0 = vd.cc0, cc1 = vd.cc1, fw = vd.fw;
-    const uint32_t xres = x_fast ? (uint32_t)((h.d1x >> (xnode & 63)) & 1ULL) : __builtin_amdgcn_readfirstlane(vd.xres);
+    const uint32_t xres = x_fast ? (uint32_t)((readlane64(h.d1x, 0) >> (xnode & 63)) & 1ULL) : __builtin_amdgcn_readfirstlane(vd.xres);
     uint64_t msk0 = ((uint64_t)__builtin_amdgcn_readfirstlane(vd.m0h) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(vd.m0l);
     uint64_t msk1 = ((uint64_t)__builtin_amdgcn_readfirstlane(vd.m1h) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(vd.m1l);
     const uint32_t dp0 = vd.dp0, dp1 = vd.dp1;
