@@ -224,6 +224,7 @@ struct KsgWinXchg {
 #define KSG_HALT_OVERSIZE 4  // pod `pos` needs the exact per-pod path
 #define KSG_HALT_BADCOUNT 8  // resolver reported an impossible count (a bug)
 #define KSG_HALT_HANG 9      // a ring/draw wait timed out (a bug)
+#define KSG_HALT_BAD 10      // the resolver's selection left T0 / the shard (KSG_STOP_BAD)
 struct KsgWinRun {
   uint32_t pos;       // first pod of the next window
   uint32_t n;         // pods in the batch

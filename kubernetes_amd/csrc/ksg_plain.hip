@@ -129,6 +129,7 @@ struct alignas(16) PlCtl {
   uint32_t chk_msk[KSG_RES_NCHK][2][2];  // ... and its dropping slots (lane l: slot 64c + l)
   uint32_t fin[KSG_RES_NCHK];            // checker c applied every commit and wrote its slots back
   uint32_t hang;                         // a wait exceeded its spin limit (a bug)
+  uint32_t bad;                          // a producer found the T0 prefixes inconsistent (a bug)
   uint32_t xseq;                         // pods the x-checker is done with
   uint32_t xres[2];                      // its verdict for the pod of parity p: bit 0 x drops, bit 1 flag
   uint32_t xn_seq;                       // pods whose drawn node is posted in L_cm[].xn
@@ -521,7 +522,8 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
                 g[17] = (int32_t)e; g[18] = (int32_t)node;
               }
               node = ~0u;
-              ctl->hang = 1;
+              ctl->bad = 1;
+              ctl->hang = 1;  // (the other roles stop waiting)
             }
             if (lane == (uint32_t)c) cand_l = node;
             if (c == 0) cand0 = node;
@@ -1831,7 +1833,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
     }
     if (woff >= d.hi - d.lo) {  // (never: inconsistent prefixes or drop positions; the host fails the batch)
       resolved = i;
-      reason = KSG_STOP_HANG;
+      reason = KSG_STOP_BAD;
       break;
     }
     const uint64_t cm = __ballot(cand == woff);
@@ -1927,7 +1929,8 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
       break;
     }
   }
-  if (!drained || ld_acq(&ctl->hang)) reason = KSG_STOP_HANG;
+  if (ld_acq(&ctl->bad)) reason = KSG_STOP_BAD;
+  else if (!drained || ld_acq(&ctl->hang)) reason = KSG_STOP_HANG;
   if constexpr (STAMP) {
     if (d.dbgbuf && lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
   }
@@ -1963,6 +1966,8 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
     *rng_io = rng0 + (uint64_t)n_draws * ksg_rng_step(d.draws);
     if (reason == KSG_STOP_HANG) {
       run->halt = KSG_HALT_HANG;
+    } else if (reason == KSG_STOP_BAD) {
+      run->halt = KSG_HALT_BAD;
     } else if (reason == KSG_STOP_OVERSIZE) {
       run->halt = KSG_HALT_OVERSIZE;  // pod pos: the host runs the exact per-pod path, then resumes
     } else if (resolved == 0 || resolved > n_pods) {

@@ -160,6 +160,8 @@ __host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag,
 #define KSG_STOP_SLOT 3
 #define KSG_STOP_OVERSIZE 4
 #define KSG_STOP_HANG 9        // a ring/draw wait exceeded KSG_SPIN_LIMIT polls (a bug): the host fails
+#define KSG_STOP_BAD 10        // a selection outside T0 / the shard (inconsistent prefixes or drop positions:
+                               // a bug, or stale verdicts under the KSG_DEBUG timing switches): the host fails
 #define KSG_SPIN_LIMIT (1u << 22)
 // KSG_DEBUG bits that select a resolver's debug instantiation: 16..19 the per-role delay
 // skews (interleaving tests), 24..27 the plain resolver's timing switches. Bits 20..23 are

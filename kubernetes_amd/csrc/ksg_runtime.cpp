@@ -2266,6 +2266,10 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
         return fail(c, KSG_ERR_STATE, "window resolver: injected failure (KSG_DEBUG & 16384) at pod %u", r.pos);
       }
       if (r.halt == KSG_HALT_HANG) return fail(c, KSG_ERR_STATE, "window resolver: ring wait timed out at pod %u", r.pos);
+      if (r.halt == KSG_HALT_BAD)
+        return fail(c, KSG_ERR_STATE,
+                    "window resolver: selection outside T0 at pod %u (inconsistent prefixes or drop positions: a bug, "
+                    "or stale verdicts under the KSG_DEBUG timing switches)", r.pos);
       if (r.halt == KSG_HALT_BADCOUNT || r.pos < pos || r.pos > n)
         return fail(c, KSG_ERR_STATE, "window resolver: bad progress (halt %u, pos %u -> %u)", r.halt, pos, r.pos);
       pos = r.pos;
