@@ -112,6 +112,8 @@ _STAGES_PLAIN = {
     # (counts x 64 per pod: commits whose node's verdict the committer took from phase A's
     # single-commit drop bitmap, and those the x-checker checked)
     41: ("xchecker", "x_by_committer_x64"), 42: ("xchecker", "x_checked_x64"),
+    43: ("committer", "entry_not_staged_x64"),  # (pods whose ring entry the head round found unstaged)
+    44: ("committer", "entry_wait"),  # (cycles waiting for those entries, per pod of the run)
 }
 
 

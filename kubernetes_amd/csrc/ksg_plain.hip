@@ -97,6 +97,17 @@
 // the x-checker's copy of each slot's lists (keys [0, 8), services [8, 20)), written by its own
 // replay of the commits: it reads them ahead of the committer's table rows being published
 #define KSG_XR_W 20
+// poll pacing of the roles off the chain (s_sleep units of 64 cycles): every LDS request a
+// poller issues queues with the committer's (one LDS per CU for the workgroup's 12 waves)
+#ifndef KSG_PL_PROD_SLEEP
+#define KSG_PL_PROD_SLEEP 1  // producers waiting for a free ring entry (8 and 32 measured no faster)
+#endif
+#ifndef KSG_PL_CHK_SLEEP
+#define KSG_PL_CHK_SLEEP 2   // the checkers waiting for the commit they apply (0 measured the same)
+#endif
+#ifndef KSG_PL_XN_SLEEP
+#define KSG_PL_XN_SLEEP 0    // the x-checker waiting for the drawn node (1, 2 measured no faster)
+#endif
 // waves of the resolver workgroup: 0 committer, 1 x-checker, 2..3 checkers, 4 flagger (service
 // flags and first peers in commit order), 5.. producers: 12 waves (7 producers), 8 at P = 32,
 // where a producer's T0 copy needs the registers of two waves per SIMD
@@ -410,7 +421,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
 #pragma unroll
         for (int c = 0; c < KSG_RES_NCHK; ++c) done = min(done, ld_acq(&ctl->chk_seq[c]));
         if (j < RING || done + RING >= j + 3) break;
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(KSG_PL_PROD_SLEEP);  // (far ahead of the committer: poll the LDS rarely)
       }
       pstamp(24);
       if (skew & 8u) __builtin_amdgcn_s_sleep(8);
@@ -737,7 +748,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
           stopped = true;
           break;
         }
-        __builtin_amdgcn_s_sleep(2);  // (off the chain: leave the LDS to the committer)
+        if (KSG_PL_CHK_SLEEP) __builtin_amdgcn_s_sleep(KSG_PL_CHK_SLEEP);
       }
       acq_lds();
       cstamp(c == 0 ? 16 : 19);
@@ -1206,6 +1217,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
           stopped = true;
           break;
         }
+        if (KSG_PL_XN_SLEEP) __builtin_amdgcn_s_sleep(KSG_PL_XN_SLEEP);
       }
       acq_lds();
       if (stopped) break;
@@ -1523,7 +1535,9 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
     const uint32_t rd0 = ld_rlx(&r_hdr[e].ready);
     asm volatile("" ::: "memory");  // (the entry's reads stay behind the ready read)
     Head h = head_reads(e);
-    if (__builtin_amdgcn_readfirstlane(rd0) != i + 1) {
+    if (KSG_UNLIKELY(__builtin_amdgcn_readfirstlane(rd0) != i + 1)) {
+      KSG_COUNTP(43, 64)  // (pods whose entry was not staged yet when the head round read it)
+      const uint64_t tw0 = STAMP ? __builtin_amdgcn_s_memtime() : 0ULL;
       __builtin_amdgcn_s_setprio(0);  // a producer shares this SIMD: do not starve it
       bool hung = false;
       for (uint32_t spin = 0; ld_u(&r_hdr[e].ready) != i + 1; ++spin)
@@ -1532,13 +1546,14 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
           break;
         }
       __builtin_amdgcn_s_setprio(3);
-      if (hung) {
+      if (KSG_UNLIKELY(hung)) {
         resolved = i;
         reason = KSG_STOP_HANG;
         break;
       }
       acq_lds();
       h = head_reads(e);  // (the staged entry, read after the wait)
+      KSG_COUNTP(44, __builtin_amdgcn_s_memtime() - tw0)  // (the wait for it)
     }
     if constexpr (STAMP) {  // ring wait of the window's first 4 pods (lane 10) vs the rest (lane 11)
       const uint64_t t_now = __builtin_amdgcn_s_memtime();
@@ -1556,7 +1571,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
     const uint32_t k0 = __builtin_amdgcn_readfirstlane(h.k0);
     const int32_t pred = (int32_t)__builtin_amdgcn_readfirstlane(h.pred);
     KSG_STAMPP(13)  // (the head's LDS reads; lane 1: the rest of the head)
-    if (__builtin_amdgcn_readlane(rec, WS_ERR) || m0 == KSG_S32_NONE) {
+    if (KSG_UNLIKELY(__builtin_amdgcn_readlane(rec, WS_ERR) || m0 == KSG_S32_NONE)) {
       // ServiceAffinity peer error / nothing fit at the snapshot (commits only
       // remove fits): no draw, no commit
       if (lane == 0) {
@@ -1577,7 +1592,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
     // pod i-1 of another service (x's service entries cannot move pod i's spreading term or
     // raise its service's scalars); the x-checker only replays such a commit
     const bool x_fast = d1_on && have_x && x_fresh && !pod_has_service(xrec, s);
-    if (__builtin_amdgcn_readlane(rec, WS_NINL) > KSG_WIN_INLINE || nk > KSG_SLOT_KEYS || n_svcs > KSG_SLOT_SVCS) {
+    if (KSG_UNLIKELY(__builtin_amdgcn_readlane(rec, WS_NINL) > KSG_WIN_INLINE || nk > KSG_SLOT_KEYS || n_svcs > KSG_SLOT_SVCS)) {
       resolved = i;  // lists longer than the record / a slot: the exact per-pod kernel takes it
       reason = i == 0 ? KSG_STOP_OVERSIZE : KSG_STOP_SLOT;
       break;
@@ -1628,12 +1643,12 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
       // (the flagger applied the flags of commits <= i-2: fseq >= i-1; the x-checker's verdict
       // covers commit i-1's)
       if ((cs >= i + 1 && (x_fast || xs >= i + 1) && fs + 1 >= i) || (xpt & 8u)) break;
-      if (spin > 16 * KSG_SPIN_LIMIT || hg) {
+      if (KSG_UNLIKELY(spin > 16 * KSG_SPIN_LIMIT || hg)) {
         hung = true;
         break;
       }
     }
-    if (hung) {
+    if (KSG_UNLIKELY(hung)) {
       resolved = i;
       reason = KSG_STOP_HANG;
       break;
@@ -1646,7 +1661,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
     uint64_t msk1 = ((uint64_t)__builtin_amdgcn_readfirstlane(vd.m1h) << 32) | (uint32_t)__builtin_amdgcn_readfirstlane(vd.m1l);
     const uint32_t dp0 = vd.dp0, dp1 = vd.dp1;
     acq_lds();  // (the ES masks, signs and the drop positions read below: after the wait)
-    if (s >= 0 && (spread_on || aff_on) && ((xres & 2u) || ((__builtin_amdgcn_readfirstlane(fw) >> (s & 31)) & 1u))) {
+    if (KSG_UNLIKELY(s >= 0 && (spread_on || aff_on) && ((xres & 2u) || ((__builtin_amdgcn_readfirstlane(fw) >> (s & 31)) & 1u)))) {
       resolved = i;  // a service scalar this pod reads changed in the window
       reason = KSG_STOP_SERVICE;
       break;
@@ -1694,7 +1709,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
       dropped = (uint32_t)__popcll(msk0) + (uint32_t)__popcll(msk1) + (x_drop ? 1u : 0u);
     }
     const uint32_t n_add = (uint32_t)__popcll(jm0) + (uint32_t)__popcll(jm1);
-    if (dropped >= k0 && n_add == 0 && (rm0 | rm1) == 0) {
+    if (KSG_UNLIKELY(dropped >= k0 && n_add == 0 && (rm0 | rm1) == 0)) {
       resolved = i;  // every snapshot tie got worse: needs a fresh snapshot
       reason = KSG_STOP_EXHAUSTED;
       break;
@@ -1831,7 +1846,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
       }
       woff = t0_node(t0_minus_drops(k - 1 - ix));
     }
-    if (woff >= d.hi - d.lo) {  // (never: inconsistent prefixes or drop positions; the host fails the batch)
+    if (KSG_UNLIKELY(woff >= d.hi - d.lo)) {  // (never: inconsistent prefixes or drop positions; the host fails the batch)
       resolved = i;
       reason = KSG_STOP_BAD;
       break;
@@ -1855,7 +1870,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
       const uint32_t sl = slot & 63;
       base_nk = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? sk0 : sk1), (int)sl);
       base_ns = (uint32_t)__builtin_amdgcn_readlane((int)(slot < 64 ? ss0 : ss1), (int)sl);
-      if (base_nk + nk > KSG_SLOT_KEYS || base_ns + n_svcs > KSG_SLOT_SVCS) {
+      if (KSG_UNLIKELY(base_nk + nk > KSG_SLOT_KEYS || base_ns + n_svcs > KSG_SLOT_SVCS)) {
         resolved = i;  // this pod is redone (with the same draw) in the next window
         reason = KSG_STOP_SLOT;
         break;
@@ -1863,7 +1878,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
       base_dc = (int64_t)readlane64((uint64_t)(slot < 64 ? dc0 : dc1), (int)sl);
       base_dm = (int64_t)readlane64((uint64_t)(slot < 64 ? dm0 : dm1), (int)sl);
     } else {
-      if (n_slots == KSG_MAX_SLOTS) {
+      if (KSG_UNLIKELY(n_slots == KSG_MAX_SLOTS)) {
         resolved = i;
         reason = KSG_STOP_SLOT;
         break;
@@ -1932,7 +1947,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
   if (ld_acq(&ctl->bad)) reason = KSG_STOP_BAD;
   else if (!drained || ld_acq(&ctl->hang)) reason = KSG_STOP_HANG;
   if constexpr (STAMP) {
-    if (d.dbgbuf && lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
+    if (d.dbgbuf && (lane < 16 || lane == 43 || lane == 44)) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
   }
 #undef KSG_STAMPP
 #undef KSG_COUNTP

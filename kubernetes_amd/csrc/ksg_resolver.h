@@ -177,6 +177,9 @@ __device__ __forceinline__ T gld(const T* p) {
   return *(const __attribute__((address_space(1))) T*)p;
 }
 __device__ __forceinline__ void lds_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+// the resolvers' rare exits (stops, hangs, error records): laid out off the hot path, so the
+// common pod falls through without taken branches (each costs an instruction-buffer refill)
+#define KSG_UNLIKELY(c) __builtin_expect(!!(c), 0)
 __device__ __forceinline__ uint32_t ld_acq(uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
