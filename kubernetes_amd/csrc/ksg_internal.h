@@ -324,6 +324,10 @@ struct KsgSrvGrid {
   uint32_t quit;     // == the launch's epoch: the scan workgroups return
   uint32_t applied;  // the last control request the leader applied (a BEGIN waits for its ARG)
   uint32_t pad[14];
+  // (extensions) TaintToleration: each scan workgroup's max untolerated soft-taint count over its
+  // filtered nodes, tagged with the BEGIN's sequence number (seq << 32 | max): every workgroup
+  // reads all of them (the normalisation max over the whole shard) before it scores
+  uint64_t tmx[KSG_GSRV_MAXW];
 };
 struct KsgSrvArgs {
   KsgSrvBox* box;        // device address of the mapped box

@@ -839,8 +839,8 @@ uint32_t srv_npt(const ksg_ctx* c) { return c->hi - c->lo > c->srv_npt4_min ? 4u
 bool srv_grid(const ksg_ctx* c) {
   const uint32_t n = c->hi - c->lo, per = KSG_GSRV_NT * srv_npt(c);
   // (extensions: the filters and BalancedAllocation are per node; TaintToleration normalises over
-  // the filtered set, a reduction across the scan workgroups: the one-workgroup server takes it)
-  return c->srv_grid_on && !anti_on(c) && !(c->ext_on && (c->ext.w_taint_toleration || !c->srv_grid_ext)) &&
+  // the filtered set: the scan workgroups exchange their maxima through device memory)
+  return c->srv_grid_on && !anti_on(c) && !(c->ext_on && !c->srv_grid_ext) &&
          n > c->srv_grid_min &&
          (n + per - 1) / per <= KSG_GSRV_MAXW;
 }

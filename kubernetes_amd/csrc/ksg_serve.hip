@@ -693,6 +693,7 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
   __shared__ uint64_t s_tw[NW];
   __shared__ uint32_t s_kind, s_seq, s_ready;
   __shared__ KsgPatch s_pt[64];
+  __shared__ int32_t s_tmw[NWV], s_gtm;  // (extensions) TaintToleration maxima: per wave, over the shard
 
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -802,6 +803,14 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
           if (tid == 0) grid_mark(a, 1 + w, T, 4);
           if ((a.stamps & 1u) && tid == 0) s_ready = (uint32_t)wall_clock64();
           const bool res_on = (d.preds & KSG_PRED_PODFITSRESOURCES) && !c.zero_req;
+          // (extensions) TaintTolerationPriority (ksg_exact.h scan_pod): the node's count of the
+          // pod's untolerated PreferNoSchedule taints, normalised by the max over the shard's
+          // filtered nodes (NormalizeReduce(10, reverse)) -- a max across the scan workgroups
+          const bool ttg = EXT && c.ext != nullptr && d.w_taint != 0 && !d.equal_fallback;
+          uint64_t psoft = 0;  // (taint ids < 64 with the per-node masks: the pod's soft ids as a mask)
+          if (ttg && d.ntaint)
+            for (uint32_t t = 0; t < c.ext->n_soft; ++t) psoft |= 1ULL << (c.ids[c.ext->soft_off + t] & 63);
+          int32_t soft[NPT];
 #pragma unroll
           for (int j = 0; j < NPT; ++j) {
             int f;
@@ -809,6 +818,9 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
             const int32_t s = eval_node(d, c, n, bit, s_wm, NW, j * NWV + wave, res_on, capc[j], capm[j], usedc[j],
                                         usedm[j], invc[j], invm[j], ss[j], cnt[j], s_tab, n_tab, f);
             sc[j] = (valid[j] && f == KSG_FAIL_NONE) ? s : KSG_S32_NONE;
+            soft[j] = !ttg ? 0
+                      : d.ntaint ? __popcll(d.ntaint[nn[j]] & psoft)
+                                 : soft_taints(d, c, nn[j] >> 6, 1ULL << (nn[j] & 63));
             if (want_fail) {  // four nodes' codes per dword, straight into host memory
               const uint32_t fb = valid[j] ? (uint32_t)f : 0u;
               const uint32_t b0 = __shfl(fb, (int)((lane * 4 + 0) & 63), 64), b1 = __shfl(fb, (int)((lane * 4 + 1) & 63), 64);
@@ -817,6 +829,52 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
               if (lane < 16 && dw.lo + off < dw.hi)  // (shard-relative; the area is 4-padded)
                 *reinterpret_cast<volatile uint32_t*>(a.fail + w * NODES + off) = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
             }
+          }
+          if (ttg) {
+            int32_t lm = 0;
+#pragma unroll
+            for (int j = 0; j < NPT; ++j) lm = sc[j] != KSG_S32_NONE ? max(lm, soft[j]) : lm;
+            lm = wave_max_i32(lm);
+            if (lane == 0) s_tmw[wave] = lm;
+            __syncthreads();
+            if (wave == 0) {
+              int32_t wmx = s_tmw[0];
+#pragma unroll
+              for (uint32_t q = 1; q < NWV; ++q) wmx = max(wmx, s_tmw[q]);
+              if (lane == 0) agent_st64(&a.grid->tmx[w], ((uint64_t)T << 32) | (uint32_t)wmx);
+              // every scan workgroup's, tagged with this BEGIN (lane q reads workgroups q, q + 64, ...)
+              const uint32_t G = a.n_workers;
+              const uint64_t tq = wall_clock64();
+              int32_t gm = 0;
+              bool ok = true;
+              for (;;) {
+                bool all = true;
+                int32_t mx = 0;
+                for (uint32_t q = lane; q < G; q += 64) {
+                  const uint64_t v = __hip_atomic_load(&a.grid->tmx[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                  all = all && (uint32_t)(v >> 32) == T;
+                  mx = max(mx, (int32_t)(uint32_t)v);
+                }
+                if (__ballot(!all) == 0) {
+                  gm = wave_max_i32(mx);
+                  break;
+                }
+                if (wall_clock64() - tq > KSG_GSRV_WAIT || ld_mut(&a.grid->quit) == a.epoch) {
+                  ok = false;  // (a workgroup left: this launch cannot serve the BEGIN)
+                  break;
+                }
+              }
+              if (lane == 0) {
+                s_gtm = gm;
+                if (!ok) s_kind = 0;
+              }
+            }
+            __syncthreads();
+            if (s_kind == 0) return;
+            const int32_t gtm = s_gtm;
+#pragma unroll
+            for (int j = 0; j < NPT; ++j)
+              if (sc[j] != KSG_S32_NONE) sc[j] += d.w_taint * taint_score_i32(soft[j], gtm);
           }
         }
       }
