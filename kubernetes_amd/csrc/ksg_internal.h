@@ -297,6 +297,7 @@ enum { KSG_SRVH_KIND = 0, KSG_SRVH_ARG, KSG_SRVH_RSV, KSG_SRVH_FLAGS, KSG_SRVH_P
 #define KSG_GSRV_NT 256
 #define KSG_GSRV_MAXW 255  // scan workgroups: shards up to 65,280 nodes (261,120 at 4 nodes per thread)
 #define KSG_GSRV_TIEW 16   // tie words of a scan workgroup at 4 nodes per thread
+#define KSG_GSRV_MAXD 64   // ServiceAntiAffinity label domains (all anti priorities) the grid server takes
 struct alignas(64) KsgSrvPart {
   uint32_t seq;     // the BEGIN this part answers (its 16-B store comes last)
   int32_t max;      // best score over the workgroup's nodes (KSG_S32_NONE: none fits)
@@ -328,6 +329,9 @@ struct KsgSrvGrid {
   // filtered nodes, tagged with the BEGIN's sequence number (seq << 32 | max): every workgroup
   // reads all of them (the normalisation max over the whole shard) before it scores
   uint64_t tmx[KSG_GSRV_MAXW];
+  // ServiceAntiAffinity: each scan workgroup's counts of the pod's service pods on its filtered
+  // labelled nodes, per domain, tagged likewise ([workgroup][domain]: seq << 32 | count)
+  uint64_t dcx[KSG_GSRV_MAXW * KSG_GSRV_MAXD];
 };
 struct KsgSrvArgs {
   KsgSrvBox* box;        // device address of the mapped box

@@ -185,6 +185,7 @@ struct ksg_ctx {
   std::vector<int32_t> svc_cnt;                    // S*N
   std::vector<std::unordered_map<uint32_t, int32_t>> svc_ext;
   std::vector<int32_t> svc_max, svc_total, svc_peer;
+  std::vector<int32_t> h_aff_pair;  // [affinity label][node] (ServiceAffinity, one rank; ksg_set_cluster)
   std::vector<std::map<uint64_t, uint32_t>> svc_members;  // seq -> host
   std::unordered_map<uint64_t, PodRec> pods;
   uint64_t seq = 0;
@@ -840,7 +841,9 @@ bool srv_grid(const ksg_ctx* c) {
   const uint32_t n = c->hi - c->lo, per = KSG_GSRV_NT * srv_npt(c);
   // (extensions: the filters and BalancedAllocation are per node; TaintToleration normalises over
   // the filtered set: the scan workgroups exchange their maxima through device memory)
-  return c->srv_grid_on && !anti_on(c) && !(c->ext_on && !c->srv_grid_ext) &&
+  // (ServiceAntiAffinity: the domain counts likewise, up to KSG_GSRV_MAXD domains, without extensions)
+  return c->srv_grid_on && !(anti_on(c) && (c->ext_on || c->dev.n_domains_total > KSG_GSRV_MAXD)) &&
+         !(c->ext_on && !c->srv_grid_ext) &&
          n > c->srv_grid_min &&
          (n + per - 1) / per <= KSG_GSRV_MAXW;
 }
@@ -1490,6 +1493,15 @@ int ksg_set_cluster(ksg_ctx* c, const ksg_node* nodes, uint32_t n_nodes, const u
   memcpy(sc.aff_key, c->cfg.aff_key, sizeof sc.aff_key);
   HIPCHK(c, ksg_launch_static(sc, n_nodes, dn, dnp, dpk, ddom, n_pairs, c->nw, sfit, sscore, anti_dom, aff_pair,
                               (unsigned long long*)pairmap, c->st));
+  // (ServiceAffinity: a host copy of each node's pair per affinity label, so the drop-in server's
+  // BEGIN carries a pod's requirements already resolved from its service's first peer)
+  c->h_aff_pair.clear();
+  if ((c->cfg.predicates & KSG_PRED_SERVICEAFFINITY) && c->cfg.n_aff_labels > 0 && c->world == 1) {
+    c->h_aff_pair.resize((size_t)c->cfg.n_aff_labels * NN);
+    HIPCHK(c, hipMemcpyAsync(c->h_aff_pair.data(), aff_pair, c->h_aff_pair.size() * sizeof(int32_t),
+                             hipMemcpyDeviceToHost, c->st));
+    HIPCHK(c, hipStreamSynchronize(c->st));
+  }
   // ServiceAntiAffinity re-rank (one anti priority, one rank, few domains, an
   // LDS count per service): the nodes of each domain row, row D = unlabelled
   c->d_zmap = nullptr;
@@ -1861,7 +1873,24 @@ int ksg_schedule_begin(ksg_ctx* c, const ksg_pod* pod, const uint32_t* ids, int6
     // (an all-zero record for the plain entry point of an extensions context)
     static const ksg_pod_ext zero_ext{};
     const ksg_pod_ext* xr = c->ext_on ? (c->cur_ext ? c->cur_ext : &zero_ext) : nullptr;
-    if (srv_put_pod(c, pod, ids, ext, xr, hdr)) {
+    // ServiceAffinity (predicates.go:257-324): the labels the pod's nodeSelector does not give come
+    // from its service's first peer's node; resolved here from the host mirror (svc_peer, kept equal
+    // to the device's) so the scan workgroups skip that dependent chain (pod_resolve then finds
+    // every requirement given; an unlabelled peer leaves -1, which it resolves to the same -1)
+    ksg_pod rp;
+    const ksg_pod* sp = pod;
+    if (!c->h_aff_pair.empty() && pod->service >= 0 && (uint32_t)pod->service < c->S) {
+      const int32_t peer = c->svc_peer[pod->service];
+      bool given = true;
+      for (uint32_t j = 0; j < c->cfg.n_aff_labels && j < KSG_MAX_AFF; ++j) given = given && pod->aff_pair[j] != -1;
+      if (!given && peer >= 0 && (uint32_t)peer < c->N) {
+        rp = *pod;
+        for (uint32_t j = 0; j < c->cfg.n_aff_labels && j < KSG_MAX_AFF; ++j)
+          if (rp.aff_pair[j] == -1) rp.aff_pair[j] = c->h_aff_pair[(size_t)j * c->N + (uint32_t)peer];
+        sp = &rp;
+      }
+    }
+    if (srv_put_pod(c, sp, ids, ext, xr, hdr)) {
       if ((rc = flush_patches(c)) || (!c->srv_running && (rc = srv_flush_patches(c)))) return rc;
       if (fail_codes) hdr[KSG_SRVH_FLAGS] |= KSG_SRVF_WANT_FAIL;
       uint32_t r[4];

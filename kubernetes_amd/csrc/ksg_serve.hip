@@ -635,6 +635,7 @@ __device__ __forceinline__ void st_applied(const KsgSrvArgs& a, uint32_t seq) {
 }
 // scan workgroups' backstop beyond the leader's idle limit (wall_clock64 ticks, 100 MHz: 10 ms)
 #define KSG_GSRV_WAIT 1000000ull
+#define KSG_GSRV_ANTI_REG 2  // anti priorities whose node domains a scan thread keeps in registers
 // KSG_SERVE_DEBUG: workgroup `slot` reached `stage` of request `seq` (host memory, read after a fault)
 __device__ __forceinline__ void grid_mark(const KsgSrvArgs& a, uint32_t slot, uint32_t seq, uint32_t stage) {
   if (a.stamps & 2u)
@@ -694,6 +695,7 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
   __shared__ uint32_t s_kind, s_seq, s_ready;
   __shared__ KsgPatch s_pt[64];
   __shared__ int32_t s_tmw[NWV], s_gtm;  // (extensions) TaintToleration maxima: per wave, over the shard
+  __shared__ int32_t s_dc[KSG_GSRV_MAXD], s_dtot[KSG_GSRV_MAXD];  // anti-affinity domain counts: here, over the shard
 
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -738,6 +740,9 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
       int64_t capc[NPT], capm[NPT], usedc[NPT], usedm[NPT];
       double invc[NPT], invm[NPT];
       int32_t ss[NPT], cnt[NPT];
+      // ServiceAntiAffinity: the nodes' label domains of the first KSG_GSRV_ANTI_REG anti priorities
+      // (static), in flight with the rest
+      int32_t domr[NPT][KSG_GSRV_ANTI_REG];
 #pragma unroll
       for (int j = 0; j < NPT; ++j) {
         capc[j] = d.cap_cpu[nn[j]];
@@ -745,6 +750,9 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
         invc[j] = d.w_lr ? d.inv10_cpu[nn[j]] : 0.0;
         invm[j] = d.w_lr ? d.inv10_mem[nn[j]] : 0.0;
         ss[j] = d.has_static_score ? (int32_t)d.static_score[nn[j]] : 0;
+#pragma unroll
+        for (int q = 0; q < KSG_GSRV_ANTI_REG; ++q)
+          domr[j][q] = (uint32_t)q < d.n_anti && d.n_domains_total > 0 ? d.anti_domain[(size_t)q * d.n_nodes + nn[j]] : -1;
       }
       grid_load_ext(a.box->ext, s_req, tid);
       if (wave == 0) {  // the control requests posted before this BEGIN are applied (commits it must see)
@@ -776,7 +784,13 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
         const uint32_t* pay = s_req + KSG_SRV_HDR_DW;
         const ksg_pod& p = *reinterpret_cast<const ksg_pod*>(pay);
         const uint32_t* ids = pay + s_req[KSG_SRVH_IDS_AT];
-        const bool need_cnt = d.w_spread && p.service >= 0 && !d.equal_fallback;
+        // ServiceAntiAffinity (spreading.go:104-168): the pod's service pods on the shard's filtered
+        // labelled nodes per domain, summed over the scan workgroups before any node is scored
+        // (the host keeps the grid to <= KSG_GSRV_MAXD domains and no extensions)
+        const bool anti_g = d.n_anti > 0 && d.n_domains_total > 0 && !d.equal_fallback;
+        const bool need_cnt = (d.w_spread || anti_g) && p.service >= 0 && !d.equal_fallback;
+        if (anti_g)
+          for (uint32_t k = tid; k < d.n_domains_total; k += KSG_GSRV_NT) s_dc[k] = 0;  // (the barrier below)
 #pragma unroll
         for (int j = 0; j < NPT; ++j)
           cnt[j] = need_cnt ? ld_mut(d.svc_cnt + (size_t)p.service * d.n_nodes + nn[j]) : 0;
@@ -818,6 +832,15 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
             const int32_t s = eval_node(d, c, n, bit, s_wm, NW, j * NWV + wave, res_on, capc[j], capm[j], usedc[j],
                                         usedm[j], invc[j], invm[j], ss[j], cnt[j], s_tab, n_tab, f);
             sc[j] = (valid[j] && f == KSG_FAIL_NONE) ? s : KSG_S32_NONE;
+            if (anti_g && sc[j] != KSG_S32_NONE && cnt[j] != 0) {
+#pragma unroll
+              for (int q = 0; q < KSG_GSRV_ANTI_REG; ++q)  // (compile-time indices: the domains stay in registers)
+                if ((uint32_t)q < d.n_anti && domr[j][q] >= 0) atomicAdd(&s_dc[d.anti_dom_off[q] + domr[j][q]], cnt[j]);
+              for (uint32_t q = KSG_GSRV_ANTI_REG; q < d.n_anti; ++q) {
+                const int32_t dom = d.anti_domain[(size_t)q * d.n_nodes + nn[j]];
+                if (dom >= 0) atomicAdd(&s_dc[d.anti_dom_off[q] + dom], cnt[j]);
+              }
+            }
             soft[j] = !ttg ? 0
                       : d.ntaint ? __popcll(d.ntaint[nn[j]] & psoft)
                                  : soft_taints(d, c, nn[j] >> 6, 1ULL << (nn[j] & 63));
@@ -828,6 +851,53 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
               const uint32_t off = j * KSG_GSRV_NT + wave * 64 + lane * 4;
               if (lane < 16 && dw.lo + off < dw.hi)  // (shard-relative; the area is 4-padded)
                 *reinterpret_cast<volatile uint32_t*>(a.fail + w * NODES + off) = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+            }
+          }
+          if (anti_g) {
+            __syncthreads();  // (every node's counts in s_dc)
+            if (wave == 0) {
+              const uint32_t D = d.n_domains_total, G = a.n_workers;
+              if (lane < D) agent_st64(&a.grid->dcx[(size_t)w * KSG_GSRV_MAXD + lane], ((uint64_t)T << 32) | (uint32_t)s_dc[lane]);
+              // lane k sums domain k over every scan workgroup's counts, tagged with this BEGIN
+              const uint64_t tq = wall_clock64();
+              int32_t tot = 0;
+              bool ok = true;
+              for (;;) {
+                bool all = true;
+                tot = 0;
+                if (lane < D)
+                  for (uint32_t q = 0; q < G; ++q) {
+                    const uint64_t v = __hip_atomic_load(&a.grid->dcx[(size_t)q * KSG_GSRV_MAXD + lane], __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+                    all = all && (uint32_t)(v >> 32) == T;
+                    tot += (int32_t)(uint32_t)v;
+                  }
+                if (__ballot(!all) == 0) break;
+                if (wall_clock64() - tq > KSG_GSRV_WAIT || ld_mut(&a.grid->quit) == a.epoch) {
+                  ok = false;  // (a workgroup left: this launch cannot serve the BEGIN)
+                  break;
+                }
+              }
+              // each domain's term, int(10 * float32(n - count) / float32(n)) (10 when n == 0), once
+              const int64_t tot_n = c.svc_total;
+              if (lane < D) s_dtot[lane] = tot_n > 0 ? (int32_t)frac10_f32(tot_n - tot, tot_n) : 10;
+              if (lane == 0 && !ok) s_kind = 0;
+            }
+            __syncthreads();
+            if (s_kind == 0) return;
+            // (anti_term from the per-domain terms: unlabelled nodes score 0, spreading.go:164-166)
+#pragma unroll
+            for (int j = 0; j < NPT; ++j) {
+              int32_t at = 0;
+#pragma unroll
+              for (int q = 0; q < KSG_GSRV_ANTI_REG; ++q)
+                if ((uint32_t)q < d.n_anti && domr[j][q] >= 0)
+                  at += (int32_t)d.w_anti[q] * s_dtot[d.anti_dom_off[q] + domr[j][q]];
+              for (uint32_t q = KSG_GSRV_ANTI_REG; q < d.n_anti; ++q) {
+                const int32_t dom = d.anti_domain[(size_t)q * d.n_nodes + nn[j]];
+                at += dom >= 0 ? (int32_t)d.w_anti[q] * s_dtot[d.anti_dom_off[q] + dom] : 0;
+              }
+              if (sc[j] != KSG_S32_NONE) sc[j] += at;
             }
           }
           if (ttg) {

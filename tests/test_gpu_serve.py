@@ -81,6 +81,8 @@ def _drive(case, dev, orc, seed, n_pods, *, evaluate_every=0, batch_at=(), churn
     ("config2", 5000, 500, False),    # R = 8 (config 2's node count)
     ("config2", 5000, 500, True),
     ("config4", 900, 400, False),     # ServiceAffinity + ServiceAntiAffinity
+    ("config4", 900, 400, True),      # ... on the grid server: the domain counts exchanged (round 5)
+    ("config4", 5000, 300, True),     # ... config 4's node count, 20 scan workgroups
     ("config3", 15000, 200, False),   # R = 16
     ("config3", 15000, 200, True),
     ("config2", 30000, 120, True),    # past the one-workgroup server's 16,384 nodes (4 nodes per thread)
@@ -155,7 +157,7 @@ def test_serve_matches_launch_per_call_path(monkeypatch):
 
 
 @pytest.mark.parametrize("name,nn,npods,churn", [("config2", 2000, 300, 0.0), ("config1", 700, 300, 0.2),
-                                                 ("config2", 5000, 200, 0.1)])
+                                                 ("config2", 5000, 200, 0.1), ("config4", 3000, 250, 0.1)])
 def test_serve_grid_four_nodes_per_thread(name, nn, npods, churn, monkeypatch):
     """The grid server's 4-nodes-per-thread scan workgroups (the default past
     16,384 nodes) forced at small sizes: partial last workgroups, fail codes,
