@@ -1293,8 +1293,27 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
         n_fw = gld(efit_word(x, i, xnode >> 6));
         n_sst = d.has_static_score ? (int32_t)gld(d.static_score + xw) : 0;
       }
-      // commit i-1 into its slot (the committer's bookkeeping, replayed)
-      if (xnode != ~0u) replay(xnode, prec, xslot, bnk, bns, dlc, dlm, xkinds, xdl);
+      // commit i-1 into its slot (the committer's bookkeeping, replayed). A fresh x (its first
+      // commit in the window, no slot yet) is checked from pod i-1's own record -- the slot holds
+      // exactly that pod -- and replayed after the verdict is posted, off the committer's chain
+      const bool x_new = xnode != ~0u && (__ballot(xcn0 == xnode) | __ballot(xcn1 == xnode)) == 0;
+      uint32_t fx_cl = ~0u;  // (fresh x) the row the replay would write: pod i-1's keys, then its services
+      if (x_new) {
+        const PodView xpv = pod_view(prec);
+        const uint32_t xnss = __builtin_amdgcn_readlane(prec, WS_NSS);
+        const uint32_t psel = xnss & 0xffff, psv = xnss >> 16;
+        const uint32_t src = lane < KSG_SLOT_KEYS ? WS_IDS + lane : WS_IDS + xpv.nk + psel + (lane - KSG_SLOT_KEYS);
+        const uint32_t v = (uint32_t)__shfl((int)prec, (int)min(src, 63u), 64);
+        fx_cl = (lane < KSG_SLOT_KEYS ? lane < xpv.nk : (lane < KSG_XR_W && lane - KSG_SLOT_KEYS < psv)) ? v : ~0u;
+        bnk = bns = 0;
+        dlc = (uint64_t)xpv.req_c;
+        dlm = (uint64_t)xpv.req_m;
+        xkinds = XS ? xpv.xm : 0u;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xdl[r] = XS ? (int32_t)__builtin_amdgcn_readlane(prec, WS_XREQ + r) : 0;
+      } else if (xnode != ~0u) {
+        replay(xnode, prec, xslot, bnk, bns, dlc, dlm, xkinds, xdl);
+      }
       if (do_check) {
         // the slot's lists with commit i-1's entries: this wave's row (just written by the replay)
         const uint32_t pnpp = __builtin_amdgcn_readlane(prec, WS_NPP), pnss = __builtin_amdgcn_readlane(prec, WS_NSS);
@@ -1302,7 +1321,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
         const uint32_t xnk = bnk + pnk, xns = bns + pns;
         // lane t < 8: key t of the slot; lane 8 + u (u < 12): its service u
         const uint32_t kt = lane - KSG_CL_KEY, ut = lane - KSG_CL_SV;
-        const uint32_t xcl = lane < KSG_XR_W ? L_xr[(size_t)xslot * KSG_XR_W + lane] : ~0u;
+        const uint32_t xcl = x_new ? fx_cl : lane < KSG_XR_W ? L_xr[(size_t)xslot * KSG_XR_W + lane] : ~0u;
         const uint32_t nk = pv.nk;
         const bool s_ent = s >= 0 && ut < KSG_SLOT_SVCS && ut < xns && xcl == (uint32_t)s;
         const uint64_t ents = __ballot(s_ent);
@@ -1452,6 +1471,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
         if constexpr (STAMP) ctl->t_x = (uint32_t)__builtin_amdgcn_s_memtime();
         st_post(&ctl->xseq, i + 1);
       }
+      if (x_new) replay(xnode, prec, xslot, bnk, bns, dlc, dlm, xkinds, xdl);  // (after the post)
       if constexpr (STAMP) {
         const uint64_t t_now = __builtin_amdgcn_s_memtime();
         x_acc += lane == 29 ? t_now - x_last : 0ULL;
