@@ -601,7 +601,17 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
         e_tm = x.tmax ? x.tmax[j] : 0;
         e_tc = (x.thist && e_tm > 0) ? x.thist[(size_t)j * KSG_TBINS + e_tm] : 0;
       }
+      // the committer's pod scalars (RingHdr::ps / pfl)
+      const int32_t h_s = __builtin_amdgcn_readlane(rec, WS_SVC);
+      const bool h_over = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NINL) > KSG_WIN_INLINE || nk > KSG_SLOT_KEYS ||
+                          n_svcs > KSG_SLOT_SVCS;
+      const uint32_t h_prv = (j > 0 && lane < DW) ? recs[(size_t)(j - 1) * DW + lane] : 0u;
+      const bool h_prev_s = j > 0 && pod_has_service(h_prv, h_s);
+      const uint32_t h_pfl = (drawable ? 0u : 1u) | (h_prev_s ? 2u : 0u) | (h_over ? 4u : 0u) | (min(nk, 255u) << 8) |
+                             (min(n_svcs, 255u) << 16) | (min(n_sel, 255u) << 24);
       if (lane == 0) {
+        r_hdr[e].ps = h_s;
+        r_hdr[e].pfl = h_pfl;
         r_hdr[e].psoft = e_ps;
         r_hdr[e].tmax = e_tm;
         r_hdr[e].tcnt = e_tc;
@@ -1497,11 +1507,9 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
   int64_t dc0 = 0, dm0 = 0, dc1 = 0, dm1 = 0;  // their window deltas (current through the last commit)
   bool have_x = false;                   // commit i-1's node x (and its slot)
   uint32_t xnode = 0, xslot = 0;
-  // x took a new slot at commit i-1 (its first commit in the window), and pod i-1's record
-  // lane: with phase A's single-commit drop bitmaps (d1) this wave answers "does x drop for
+  // x took a new slot at commit i-1 (its first commit in the window): with phase A's single-commit drop bitmaps (d1) this wave answers "does x drop for
   // pod i" itself when pod i-1 is of another service than pod i (x_fast below)
   bool x_fresh = false;
-  uint32_t xrec = 0;
   const bool d1_on = !XS && pl_d1(P) && x.d1 != 0;
   uint64_t t_last = 0, t_acc = 0;
 #define KSG_STAMPP(k)                                        \
@@ -1521,7 +1529,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
   // issue order, so what they return is the staged entry whenever that ready read says
   // so; a compiler barrier keeps them behind it)
   struct Head {
-    uint32_t rec, rmod, lp_ex, lp_in, cand, xlp, xwp, m0, k0, pred;
+    uint32_t rec, rmod, lp_ex, lp_in, cand, xlp, xwp, k0, pred, ps, pfl;
     uint64_t t0x, d1x;
   };
   const uint32_t zv = opaque_v(0u);
@@ -1544,9 +1552,10 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
     h.d1x = pl_d1(P) ? r_d1[(size_t)e * P * 64 + xw] : 0ULL;
     h.xlp = r_lp[e * 64 + (xw >> 6) * 2];
     h.xwp = r_wp[(size_t)e * P * 64 + xw];
-    h.m0 = (uint32_t)r_hdr[e + zv].m0;
     h.k0 = r_hdr[e + zv].k0;
     h.pred = (uint32_t)r_hdr[e + zv].pred;
+    h.ps = (uint32_t)r_hdr[e + zv].ps;
+    h.pfl = r_hdr[e + zv].pfl;
     __builtin_amdgcn_sched_barrier(0);  // (every read issued before any of them is used)
     return h;
   };
@@ -1587,11 +1596,11 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
     const uint32_t xpos0 = have_x ? __builtin_amdgcn_readfirstlane(h.xlp + h.xwp) : 0u;
     const uint64_t* t0e = r_t0 + (size_t)e * P * 64;
     const uint64_t t0x = have_x ? readlane64(h.t0x, 0) : 0ULL;
-    const int32_t m0 = (int32_t)__builtin_amdgcn_readfirstlane(h.m0);
     const uint32_t k0 = __builtin_amdgcn_readfirstlane(h.k0);
     const int32_t pred = (int32_t)__builtin_amdgcn_readfirstlane(h.pred);
+    const uint32_t pfl = __builtin_amdgcn_readfirstlane(h.pfl);
     KSG_STAMPP(13)  // (the head's LDS reads; lane 1: the rest of the head)
-    if (KSG_UNLIKELY(__builtin_amdgcn_readlane(rec, WS_ERR) || m0 == KSG_S32_NONE)) {
+    if (KSG_UNLIKELY(pfl & 1u)) {
       // ServiceAffinity peer error / nothing fit at the snapshot (commits only
       // remove fits): no draw, no commit
       if (lane == 0) {
@@ -1605,14 +1614,13 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
       continue;
     }
     const PodView pv = pod_view(rec);
-    const int32_t s = pv.s;
-    const uint32_t nss = __builtin_amdgcn_readlane(rec, WS_NSS);
-    const uint32_t n_sel = nss & 0xffff, n_svcs = nss >> 16, nk = pv.nk;
+    const int32_t s = (int32_t)__builtin_amdgcn_readfirstlane(h.ps);  // (staged: RingHdr::ps / pfl)
+    const uint32_t n_sel = pfl >> 24, n_svcs = (pfl >> 16) & 0xffu, nk = (pfl >> 8) & 0xffu;
     // x's verdict from phase A's bitmap: x fresh (its state is the snapshot plus pod i-1) and
     // pod i-1 of another service (x's service entries cannot move pod i's spreading term or
     // raise its service's scalars); the x-checker only replays such a commit
-    const bool x_fast = d1_on && have_x && x_fresh && !pod_has_service(xrec, s);
-    if (KSG_UNLIKELY(__builtin_amdgcn_readlane(rec, WS_NINL) > KSG_WIN_INLINE || nk > KSG_SLOT_KEYS || n_svcs > KSG_SLOT_SVCS)) {
+    const bool x_fast = d1_on && have_x && x_fresh && !(pfl & 2u);
+    if (KSG_UNLIKELY(pfl & 4u)) {
       resolved = i;  // lists longer than the record / a slot: the exact per-pod kernel takes it
       reason = i == 0 ? KSG_STOP_OVERSIZE : KSG_STOP_SLOT;
       break;
@@ -1944,7 +1952,6 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
     xnode = woff;
     xslot = slot;
     x_fresh = !in_c;
-    xrec = rec;
     ++n_draws;
     KSG_STAMPP(5)
   }

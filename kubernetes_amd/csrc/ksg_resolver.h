@@ -68,6 +68,12 @@ struct alignas(16) RingHdr {
   uint64_t psoft;                        // (extension scores) the pod's untolerated soft taints (mask)
   int32_t tmax;                          // ... its TaintToleration max over its filtered nodes
   int32_t tcnt;                          // ... and how many of them hold it
+  // (plain resolver) the pod's scalars the committer branches on, staged so its head reads two
+  // words instead of the record's lanes: the service, and flags -- bit 0 no draw (error / nothing
+  // fit), 1 the previous pod is of this pod's service, 2 lists longer than the record / a slot,
+  // bits 8..15 conflict keys, 16..23 services, 24..31 selector pairs (each capped at 255)
+  int32_t ps;
+  uint32_t pfl;
 };
 struct alignas(16) RingSvc {  // per service entry t of the pod (t < n_svcs)
   int32_t cnt[KSG_SLOT_SVCS];   // svc_cnt[sv][pred] at the snapshot
