@@ -60,6 +60,6 @@ PY
     timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY \
       --output-format csv -d $OUT -o run -- python3 bench.py --no-cpu-baseline --no-stages --workload $WL --steps 3 --warmup 1 "$@" \
       > $OUT.json 2> $OUT.err || { tail $OUT.err; exit 1; }
-    ls $OUT/*/ ;;
+    ls $OUT ;;
   *) echo "unknown step $STEP"; exit 2 ;;
 esac
