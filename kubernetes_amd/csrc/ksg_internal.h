@@ -177,8 +177,9 @@ struct KsgWinXchg {
   // domain row), the best score without the anti term over the pod's filtered
   // nodes (dmb, int32[wcap][dz]; row dz-1 = unlabelled nodes), and the score pass
   // the bitmap of filtered nodes at their row's best (uint64[wcap][ostride] at
-  // b_off); zmap = uint64[dz][nw], the nodes of each domain row. The resolver
-  // resets dmb to KSG_S32_NONE for the next window.
+  // b_off) and how many of them each row holds (dmb's second half, int32[wcap][dz]);
+  // zmap = uint64[dz][nw], the nodes of each domain row. The resolver resets the row
+  // bests to KSG_S32_NONE and the counts to 0 for the next window.
   // the plain resolver (no ServiceAntiAffinity): per window pod, its T0 image
   // (ksg_plain.hip, ksg_win_t0_kernel) at img + pod * img_stride
   uint8_t* img;

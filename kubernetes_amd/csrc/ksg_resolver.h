@@ -38,6 +38,14 @@ __host__ __device__ constexpr uint32_t win_ring(uint32_t P) { return P <= 8 ? 16
 __host__ __device__ constexpr uint32_t win2_ring(uint32_t P, bool anti) {
   return anti || P <= 8 ? win_ring(P) : P == 16 ? 8u : 5u;
 }
+// Shards past 32k nodes (P > 8): the re-rank's per-domain node bitmaps (one P * 512 B bitmap per
+// domain row) are read from their HBM copy (x.zmap, L2-resident: rows x words x 8 B) instead of
+// LDS; past 64k nodes (P > 16) the pod's fit-at-the-snapshot and best-per-row (B) bitmaps are
+// read from phase A's output rows (x.buf, one row per window pod) instead of ring copies. T0 and
+// the drop bitmap stay in LDS (the committer reads them every pod).
+__host__ __device__ constexpr bool win2_zg(uint32_t P) { return P > 8; }
+__host__ __device__ constexpr bool win2_zg_words(uint32_t nwords) { return nwords > 8 * 64; }  // (P > 8)
+__host__ __device__ constexpr bool win2_fg(uint32_t P) { return P > 16; }
 #define KSG_SLOT_KEYS 8
 #define KSG_SLOT_SVCS 12
 #define KSG_MAX_SLOTS (64 * KSG_RES_NCHK)

@@ -2164,10 +2164,11 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       x.dcnt = c->d_dcnt;
       x.dcnt_n = (uint32_t)dcnt_n;
     }
-    if (rr) {  // (the resolver resets the row bests to KSG_S32_NONE for the next window)
-      const size_t dmb_n = (size_t)W * c->dev.rr_dz;
-      if ((rc = grow(c, (void**)&c->d_dmb, &c->dmb_cap, dmb_n, sizeof(int32_t)))) return rc;
+    if (rr) {  // (the resolver resets the row bests to KSG_S32_NONE and the B counts to 0 for the next window)
+      const size_t dmb_n = (size_t)W * c->dev.rr_dz;  // [W][dz] row bests, then [W][dz] B nodes per row
+      if ((rc = grow(c, (void**)&c->d_dmb, &c->dmb_cap, 2 * dmb_n, sizeof(int32_t)))) return rc;
       HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)c->d_dmb, (int)0x80000000, dmb_n, c->st));
+      HIPCHK(c, hipMemsetAsync(c->d_dmb + dmb_n, 0, dmb_n * sizeof(int32_t), c->st));
       x.rr = 1;
       x.dz = c->dev.rr_dz;
       x.dmb = c->d_dmb;

@@ -468,6 +468,16 @@ __global__ __launch_bounds__(KSG_SC_NT) KSG_PA_ATTR void ksg_win_score_kernel(Ks
         if (dmb) {  // filtered nodes at their domain row's best score without the anti term
           const uint64_t bz = __ballot(fit && zrow >= 0 && base == mbz[j]);
           if (lane == (uint32_t)j) my_bz = bz;
+          // ... and, past 32k nodes per shard (win2_zg: the resolver keeps no row bitmaps in LDS
+          // to count them over), how many per row (dmb's second half, [wcap][dz] int32, zeroed by
+          // the resolver for the next window), one atomic per (wave, row)
+          if (win2_zg_words(d.nwords))
+          for (uint64_t pend = bz; pend;) {
+            const int32_t zz = __builtin_amdgcn_readlane(zrow, (int)__builtin_ctzll(pend));
+            const uint64_t mine = __ballot(zrow == zz) & pend;
+            if (lane == 0) atomicAdd(dmb + (size_t)wcap * dz + (size_t)(p0 + j) * dz + zz, (int32_t)__popcll(mine));
+            pend &= ~mine;
+          }
         }
       }
     }
@@ -1528,6 +1538,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
   if (rr) {  // the producers staged this window's domain counts and row bests: reset them for the next
     for (uint32_t t = lane; t < x.dcnt_n; t += 64) x.dcnt[t] = 0;
     for (uint32_t t = lane; t < wcap * dz; t += 64) x.dmb[t] = KSG_S32_NONE;
+    for (uint32_t t = lane; t < wcap * dz; t += 64) x.dmb[(size_t)wcap * dz + t] = 0;  // (B counts per row)
   }
   if constexpr (STAMP) {
     if (d.dbgbuf && lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
@@ -1676,6 +1687,7 @@ struct WinLdsOff2 {
   uint32_t total;
 };
 
+
 // (rr: the re-rank's arrays; -1: iff dz > 0; the kernel passes a constant)
 __host__ __device__ inline WinLdsOff2 win2_lds_offsets(uint32_t P, uint32_t nflag, uint32_t W, uint32_t dz = 0,
                                                        uint32_t nsvc = 0, int rr_ = -1) {
@@ -1693,8 +1705,9 @@ __host__ __device__ inline WinLdsOff2 win2_lds_offsets(uint32_t P, uint32_t nfla
   const bool rr = rr_ < 0 ? dz != 0 : rr_ != 0;
   o.clist = at;   at += win_al16((size_t)KSG_MAX_SLOTS * KSG_CL_W * 4);
   o.drop = at;    at += rr ? win_al16((size_t)2 * P * 64 * 8) : 0u;  // (the re-rank's drop bitmap)
-  o.r_fit = at;   at += rr ? win_al16((size_t)R * P * 64 * 8) : 0u;
-  o.r_b = at;     at += rr ? win_al16((size_t)R * P * 64 * 8) : 0u;
+  // (P > 16: the fit and B bitmaps are read from phase A's output instead, win2_fg)
+  o.r_fit = at;   at += rr && !win2_fg(P) ? win_al16((size_t)R * P * 64 * 8) : 0u;
+  o.r_b = at;     at += rr && !win2_fg(P) ? win_al16((size_t)R * P * 64 * 8) : 0u;
   o.r_mb = at;    at += rr ? win_al16((size_t)R * KSG_RR_MAXZ * 4) : 0u;
   o.r_dc = at;    at += rr ? win_al16((size_t)R * KSG_RR_MAXZ * 4) : 0u;
   o.dca = at;     at += rr ? win_al16((size_t)KSG_RES_NCHK * 2 * KSG_RR_MAXZ * 4) : 0u;
@@ -1709,7 +1722,7 @@ __host__ __device__ inline WinLdsOff2 win2_lds_offsets(uint32_t P, uint32_t nfla
   o.drw = at;     at += win_al16((size_t)((W + 31) / 32) * 4);
   o.flag = at;    at += win_al16((size_t)nflag * 4);
   o.peerset = at; at += win_al16((size_t)nflag * 4);
-  o.zm = at;      at += win_al16((size_t)dz * P * 64 * 8);
+  o.zm = at;      at += win2_zg(P) ? 0u : win_al16((size_t)dz * P * 64 * 8);  // (P > 8: from HBM, win2_zg)
   o.nsv = at;     at += rr ? win_al16((size_t)nsvc * 4) : 0u;
   o.total = at;
   return o;
@@ -1809,6 +1822,19 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   // producers): another interleaving of the hand-offs than the natural one (tests/test_gpu_fuzz.py)
   // (the debug instantiation only: the production one keeps no debug switch in a register)
   const uint32_t skew = STAMP ? ((uint32_t)d.dbg >> 16) & 15u : 0u;
+  // (P > 8 / P > 16, win2_zg / win2_fg) the domain rows' node bitmaps and the pod's fit / B bitmaps
+  // from HBM: word w of domain row r (x.zmap), word w of window pod j's phase-A row at byte offset
+  // off (x.fit_off, x.b_off; the re-rank runs on one rank, so word w sits at w * 8); words past
+  // the shard read 0, as their LDS copies do
+  constexpr bool ZG = ANTI && win2_zg(P), FG = ANTI && win2_fg(P);
+  auto zm_word = [&](uint32_t r, uint32_t w) -> uint64_t {
+    if constexpr (ZG) return w < nwords ? gld(x.zmap + (size_t)r * d.nw + d.wlo + w) : 0ULL;
+    else return L_zm[(size_t)r * P * 64 + w];
+  };
+  auto pa_word = [&](uint32_t off, uint32_t j, uint32_t w) -> uint64_t {
+    return w < nwords ? gld(reinterpret_cast<const uint64_t*>(x.buf + off + (size_t)j * x.ostride * 8 + (size_t)w * 8))
+                      : 0ULL;
+  };
 
   for (uint32_t t = tid; t < RING; t += NT) r_hdr[t].ready = 0;
   if (tid == 0) *ctl = WinCtl2{};
@@ -1823,10 +1849,11 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   if constexpr (ANTI)
     for (uint32_t w = tid; w < 2 * P * 64u; w += NT) L_drop[w] = 0;
   if constexpr (ANTI) {
-    for (uint32_t t = tid; t < dz * P * 64; t += NT) {
-      const uint32_t row = t / (P * 64), w = t % (P * 64);
-      L_zm[t] = w < nwords ? x.zmap[(size_t)row * d.nw + d.wlo + w] : 0ULL;
-    }
+    if constexpr (!ZG)
+      for (uint32_t t = tid; t < dz * P * 64; t += NT) {
+        const uint32_t row = t / (P * 64), w = t % (P * 64);
+        L_zm[t] = w < nwords ? x.zmap[(size_t)row * d.nw + d.wlo + w] : 0ULL;
+      }
     for (uint32_t t = tid; t < d.n_services; t += NT) L_nsv[t] = 0;
   }
   __syncthreads();
@@ -2000,19 +2027,26 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         uint64_t bw[P];
 #pragma unroll
         for (int q = 0; q < P; ++q) {
-          r_fit[(size_t)e * P * 64 + lane * P + q] =
-              wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + x.fit_off + j * row_b) : 0ULL;
           bw[q] = wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + x.b_off + j * row_b) : 0ULL;
-          r_b[(size_t)e * P * 64 + lane * P + q] = bw[q];
+          if constexpr (!FG) {
+            r_fit[(size_t)e * P * 64 + lane * P + q] =
+                wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + x.fit_off + j * row_b) : 0ULL;
+            r_b[(size_t)e * P * 64 + lane * P + q] = bw[q];
+          }
         }
-        // B nodes per domain row (the committer's re-rank subtracts the drops)
+        // B nodes per domain row (the committer's re-rank subtracts the drops): counted here over
+        // the LDS row bitmaps, past 32k nodes by phase A (win2_zg)
         int32_t kz = 0;
-        for (uint32_t rw = 0; rw < dz; ++rw) {
-          uint32_t c1 = 0;
+        if constexpr (ZG) {
+          if (lane < dz) kz = x.dmb[(size_t)wcap * dz + (size_t)j * dz + lane];
+        } else {
+          for (uint32_t rw = 0; rw < dz; ++rw) {
+            uint32_t c1 = 0;
 #pragma unroll
-          for (int q = 0; q < P; ++q) c1 += __popcll(bw[q] & L_zm[(size_t)rw * P * 64 + lane * P + q]);
-          const uint32_t tr = wave_total_add(c1);
-          if (lane == rw) kz = (int32_t)tr;
+            for (int q = 0; q < P; ++q) c1 += __popcll(bw[q] & L_zm[(size_t)rw * P * 64 + lane * P + q]);
+            const uint32_t tr = wave_total_add(c1);
+            if (lane == rw) kz = (int32_t)tr;
+          }
         }
         if (lane < dz) r_kz[e * KSG_RR_MAXZ + lane] = kz;
         if (lane < dz) {
@@ -2178,8 +2212,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
           const uint32_t wd = S.node >> 6;
           const uint64_t nb = 1ULL << (S.node & 63);
           const bool in_t0 = (r_t0[(size_t)e * P * 64 + wd] & nb) != 0;
-          const bool in_b = (r_b[(size_t)e * P * 64 + wd] & nb) != 0;
-          const bool fsnap = pv.s >= 0 && (r_fit[(size_t)e * P * 64 + wd] & nb) != 0;
+          const bool in_b = ((FG ? pa_word(x.b_off, i, wd) : r_b[(size_t)e * P * 64 + wd]) & nb) != 0;
+          const bool fsnap = pv.s >= 0 && ((FG ? pa_word(x.fit_off, i, wd) : r_fit[(size_t)e * P * 64 + wd]) & nb) != 0;
           if (in_b || fsnap) {
             const int64_t now_c = (int64_t)((uint64_t)S.snp_c + (uint64_t)S.dl_c);
             const int64_t now_m = (int64_t)((uint64_t)S.snp_m + (uint64_t)S.dl_m);
@@ -2569,7 +2603,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
           // service's window commits there; the domain count of x's row moves by
           // the difference, or the window ends if the pod no longer fits a
           // labelled x that held pods of its service at the snapshot
-          if (s >= 0 && ((r_fit[(size_t)e * P * 64 + (xnode >> 6)] >> (xnode & 63)) & 1ULL)) {
+          const uint64_t xfw = FG ? pa_word(x.fit_off, i, xnode >> 6) : r_fit[(size_t)e * P * 64 + (xnode >> 6)];
+          if (s >= 0 && ((xfw >> (xnode & 63)) & 1ULL)) {
             const PodView qv = pod_view(prec);
             const int64_t befv = (int64_t)((uint64_t)nowv - (uint64_t)(rl ? qv.req_m : qv.req_c));
             bool fa = true, fb = true;
@@ -2853,7 +2888,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       const int64_t aa = lane + 1 < dz ? (int64_t)d.w_anti[0] * frac10_f32((int64_t)nn - cz, nn) : 0;
       uint64_t lw[P];
 #pragma unroll
-      for (int q = 0; q < P; ++q) lw[q] = r_b[(size_t)e * P * 64 + lane * P + q] & ~dww[q];
+      for (int q = 0; q < P; ++q)
+        lw[q] = (FG ? pa_word(x.b_off, i, lane * P + q) : r_b[(size_t)e * P * 64 + lane * P + q]) & ~dww[q];
       // live B nodes per row: the producer's count minus the checkers' drops
       // minus x if it is a B node the checkers kept and the x-checker dropped
       bool x_new = false;
@@ -2890,12 +2926,30 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       const uint32_t ix = umod64_32(r, k2);
       uint64_t sw[P];
       uint32_t cl = 0;
+      if constexpr (ZG) {  // the selected rows' nodes from HBM: one round of loads per row, then live B
 #pragma unroll
-      for (int q = 0; q < P; ++q) {
-        uint64_t m = 0;
-        for (uint64_t zz = zsel; zz; zz &= zz - 1) m |= L_zm[(size_t)__builtin_ctzll(zz) * P * 64 + lane * P + q];
-        sw[q] = lw[q] & m;
-        cl += __popcll(sw[q]);
+        for (int q = 0; q < P; ++q) sw[q] = 0;
+        for (uint64_t zz = zsel; zz; zz &= zz - 1) {
+          const uint32_t zr = (uint32_t)__builtin_ctzll(zz);
+          uint64_t zw[P];
+#pragma unroll
+          for (int q = 0; q < P; ++q) zw[q] = zm_word(zr, lane * P + q);
+#pragma unroll
+          for (int q = 0; q < P; ++q) sw[q] |= zw[q];
+        }
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+          sw[q] &= lw[q];
+          cl += __popcll(sw[q]);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+          uint64_t m = 0;
+          for (uint64_t zz = zsel; zz; zz &= zz - 1) m |= L_zm[(size_t)__builtin_ctzll(zz) * P * 64 + lane * P + q];
+          sw[q] = lw[q] & m;
+          cl += __popcll(sw[q]);
+        }
       }
       const uint32_t incl = dpp_scan_add(cl);
       woff = select_in_lanes<P>(sw, cl, incl, k2 - 1 - ix, lane);
@@ -3062,6 +3116,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
   if constexpr (ANTI) {  // the producers staged this window's domain counts and row bests: reset them for the next
     for (uint32_t t = lane; t < x.dcnt_n; t += 64) x.dcnt[t] = 0;
     for (uint32_t t = lane; t < wcap * dz; t += 64) x.dmb[t] = KSG_S32_NONE;
+    for (uint32_t t = lane; t < wcap * dz; t += 64) x.dmb[(size_t)wcap * dz + t] = 0;  // (B counts per row)
   }
   if constexpr (STAMP) {
     if (d.dbgbuf && lane < 16) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
@@ -3148,9 +3203,10 @@ hipError_t ksg_launch_win_eval(const KsgDev& d, int mode, const ksg_pod* batch, 
 uint32_t ksg_win_max_window(const KsgDev& d) {
   const uint32_t P = win_P(d);
   if (P == 0) return 0;
-  if (d.n_anti > 0 && d.n_domains_total > 0 && P > 8) return 0;  // anti-affinity: up to 32k nodes
   const uint32_t nflag = (d.n_services + 31) / 32;
   const bool anti = d.n_anti > 0 && d.n_domains_total > 0;
+  // anti-affinity without the re-rank (the LDS-slot resolver): up to 32k nodes per shard
+  if (anti && P > 8 && !(d.rr_dz && !(d.dbg & 4096))) return 0;
   uint32_t lo = 0, hi = 4096;
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1) / 2;
@@ -3215,6 +3271,8 @@ hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run
     KSG_RES2A_CASE(2)
     KSG_RES2A_CASE(4)
     KSG_RES2A_CASE(8)
+    KSG_RES2A_CASE(16)
+    KSG_RES2A_CASE(32)
 #undef KSG_RES2A_CASE
     return hipErrorInvalidValue;
   }

@@ -303,6 +303,29 @@ def test_full_size_matches_oracle(name, nn, npods):
     dev.close()
 
 
+@pytest.mark.parametrize("nn,npods", [
+    (40000, 3000),   # P = 16: the domain rows' node bitmaps from HBM (win2_zg)
+    (70000, 2000),   # P = 32: the fit and best-per-row bitmaps from phase A's rows too (win2_fg)
+])
+def test_anti_affinity_large_shard_window_matches_oracle(nn, npods):
+    """ServiceAntiAffinity (config 4's policy) past 32k nodes on one shard takes the window
+    path (the re-rank resolver with its large bitmaps off LDS), not the exact kernel: every
+    decision, the RNG position and the committed totals against the incremental oracle."""
+    case = Case("config4", nn, npods)
+    dev, orc = _pair(case)
+    got, sg = run_batch(dev, case, chunk=1000)
+    st = dev.last_batch_stats()
+    want, sw = run_batch(orc, case, chunk=1000)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"first mismatches at {bad[:8]}: gpu {got[bad[:8]]} oracle {want[bad[:8]]}"
+    assert sg == sw
+    gc, gm = dev.read_requested()
+    wc, wm = orc.read_requested()
+    assert np.array_equal(gc, wc) and np.array_equal(gm, wm)
+    assert st["windows"] > 0, st
+    dev.close()
+
+
 def test_config2_prefix_matches_faithful_restatement():
     """bench.py's cpu_baseline check as a test: the reference's own cost structure
     (faithful mode: per-pod MapPodsToMachines regroup, greedy CheckPodsExceedingCapacity,
