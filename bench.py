@@ -89,6 +89,8 @@ _STAGES2 = {
     24: ("producers_sum_over_waves", "ring_wait"), 25: ("producers_sum_over_waves", "loads"),
     26: ("producers_sum_over_waves", "draw_wait"), 27: ("producers_sum_over_waves", "stage"),
     28: ("xchecker", "wait_node"), 29: ("xchecker", "check"), 30: ("xchecker", "bookkeeping_and_lists"),
+    # (ServiceAntiAffinity re-ranks: their count x 64 per pod and their cycles)
+    9: ("committer", "rerank_x64"), 12: ("committer", "rerank_cycles"),
 }
 
 

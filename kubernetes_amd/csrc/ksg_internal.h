@@ -37,10 +37,11 @@
 #define KSG_SCORE_NONE (-0x7fffffffffffffffLL - 1)
 #define KSG_S32_NONE ((int32_t)0x80000000)
 // combined scores: int32 on the window path, which the host takes only while no
-// |score| can reach this bound (and at most KSG_WIN_MAX_ANTI anti-affinity
-// priorities carry a weight); int64 and wrapping like Go's int on the exact
+// |score| can reach this bound; int64 and wrapping like Go's int on the exact
 // kernels otherwise (KsgDev.wide)
 #define KSG_SCORE_BOUND (1LL << 30)
+// anti-affinity priorities whose node domains phase A keeps in registers (the
+// rest, up to the policy's KSG_MAX_ANTI, are loaded where they are used)
 #define KSG_WIN_MAX_ANTI 4
 // largest capacity / requested total the window path accepts (lr_win's bound,
 // ksg_device.h)

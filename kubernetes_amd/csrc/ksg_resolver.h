@@ -363,10 +363,8 @@ __device__ __forceinline__ bool slot_drops(const KsgDev& d, const WinSlots& S, u
 // (spreading.go:130-151): not a monotone change, the window must end there.
 __device__ __forceinline__ bool anti_counts_move(const KsgDev& d, uint32_t node, int32_t s) {
   bool labelled = false;
-#pragma unroll
-  for (int a = 0; a < KSG_WIN_MAX_ANTI; ++a)
-    if ((uint32_t)a < d.n_anti && d.w_anti[a] != 0 && d.anti_domain[(size_t)a * d.n_nodes + d.lo + node] >= 0)
-      labelled = true;
+  for (uint32_t a = 0; a < d.n_anti && !labelled; ++a)
+    if (d.w_anti[a] != 0 && d.anti_domain[(size_t)a * d.n_nodes + d.lo + node] >= 0) labelled = true;
   return labelled && d.svc_cnt[(size_t)s * d.n_nodes + d.lo + node] > 0;
 }
 

@@ -749,8 +749,8 @@ bool use_window(ksg_ctx* c, const ksg_pod* pods, uint32_t n) {
         for (uint32_t r = 0; r < c->ext.n_scalar; ++r)
           if (c->cur_ext[i].scalar[r] < 0 || c->cur_ext[i].scalar[r] > KSG_WIN_XREQ_BOUND) return false;
   }
-  // int64 combined scores / more anti-affinity priorities than phase A keeps in registers
-  if (c->dev.wide || c->dev.n_anti > KSG_WIN_MAX_ANTI) return false;
+  // int64 combined scores
+  if (c->dev.wide) return false;
   // monotonicity under commits needs non-negative pod-dependent weights
   if (c->cfg.w_least_requested < 0 || c->cfg.w_service_spreading < 0) return false;
   // lr_win (ksg_device.h) is exact for 0 <= capacity, requested totals <= 2^49

@@ -293,6 +293,21 @@ __global__ __launch_bounds__(KSG_SC_NT) KSG_PA_ATTR void ksg_win_score_kernel(Ks
           s += (int64_t)d.w_anti[a] * (tj > 0 ? frac10_f32((int64_t)tj - pcs[j][a], tj) : 10);
       aterm[j] = s;
     }
+    // priorities past the first KSG_WIN_MAX_ANTI (policies with more): their domain and counts
+    // loaded here, one priority at a time
+    for (uint32_t a = KSG_WIN_MAX_ANTI; a < d.n_anti; ++a) {
+      if (d.w_anti[a] == 0) continue;
+      const int32_t da = valid ? d.anti_domain[(size_t)a * d.n_nodes + n] : -1;
+      int32_t pc[KSG_PG];
+#pragma unroll
+      for (int j = 0; j < KSG_PG; ++j)
+        pc[j] = ((uint32_t)j < np && da >= 0) ? dcnt[(size_t)(p0 + j) * d.n_domains_total + d.anti_dom_off[a] + da] : 0;
+#pragma unroll
+      for (int j = 0; j < KSG_PG; ++j) {
+        const int32_t tj = __builtin_amdgcn_readlane(tot, j);
+        if (da >= 0) aterm[j] += (int64_t)d.w_anti[a] * (tj > 0 ? frac10_f32((int64_t)tj - pc[j], tj) : 10);
+      }
+    }
   }
   // re-rank (dmb != nullptr): this node's domain row for the first anti priority
   // (dz - 1: unlabelled), and in the score pass each pod's best score without
@@ -386,6 +401,18 @@ __global__ __launch_bounds__(KSG_SC_NT) KSG_PA_ATTR void ksg_win_score_kernel(Ks
           while (pend) {
             const int32_t dd = __builtin_amdgcn_readlane(dom[a], (int)__builtin_ctzll(pend));
             const bool mine = ((pend >> lane) & 1ULL) && dom[a] == dd;
+            const uint32_t sum = wave_total_add(mine ? (uint32_t)cj : 0u);
+            if (lane == 0) atomicAdd(dcnt + (size_t)(p0 + j) * d.n_domains_total + d.anti_dom_off[a] + dd, (int32_t)sum);
+            pend &= ~__ballot(mine);
+          }
+        }
+        for (uint32_t a = KSG_WIN_MAX_ANTI; a < d.n_anti; ++a) {  // (priorities past the first few)
+          if (d.w_anti[a] == 0) continue;
+          const int32_t da = valid ? d.anti_domain[(size_t)a * d.n_nodes + n] : -1;
+          uint64_t pend = __ballot(cj != 0 && da >= 0);
+          while (pend) {
+            const int32_t dd = __builtin_amdgcn_readlane(da, (int)__builtin_ctzll(pend));
+            const bool mine = ((pend >> lane) & 1ULL) && da == dd;
             const uint32_t sum = wave_total_add(mine ? (uint32_t)cj : 0u);
             if (lane == 0) atomicAdd(dcnt + (size_t)(p0 + j) * d.n_domains_total + d.anti_dom_off[a] + dd, (int32_t)sum);
             pend &= ~__ballot(mine);
@@ -2875,6 +2902,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       // row's term is recomputed and the tie set is the live best-per-row nodes
       // of the rows whose best + term is the maximum
       KSG_COUNT2(9, 64)
+      const uint64_t t_rr = STAMP ? __builtin_amdgcn_s_memtime() : 0ULL;
       const int32_t nn = (int32_t)__builtin_amdgcn_readlane(rec, WS_STOT) + (int32_t)mv_n;
       const uint32_t xz = __builtin_amdgcn_readfirstlane(ctl->xdz[par]);
       const int32_t xc = (int32_t)__builtin_amdgcn_readfirstlane(ctl->xdc[par]);
@@ -2953,6 +2981,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       }
       const uint32_t incl = dpp_scan_add(cl);
       woff = select_in_lanes<P>(sw, cl, incl, k2 - 1 - ix, lane);
+      KSG_COUNT2(12, __builtin_amdgcn_s_memtime() - t_rr)  // (the re-rank's cycles)
     } else if (dropped == 0) {
       woff = (uint32_t)pred;  // staged by the producer
     } else if constexpr (!ANTI) {

@@ -111,6 +111,10 @@ def test_family_windows_match_oracle(family):
         assert sg == sw, (family, window)
         gc, gm = dev.read_requested()
         assert np.array_equal(gc, wc) and np.array_equal(gm, wm), (family, window)
+        if family in ("many_anti", "past_caps") and window:
+            # six / twenty ServiceAntiAffinity priorities: the window path (phase A keeps the
+            # first four priorities' domains in registers and loads the rest)
+            assert dev.last_batch_stats()["windows"] > 0, (family, window)
         if family == "negative" and window:
             # negative LeastRequested / ServiceSpreading weights break the window path's
             # monotonicity: every batch must have taken the exact kernel
