@@ -144,7 +144,8 @@ __host__ __device__ inline WinLdsOff win_lds_offsets(uint32_t P, uint32_t nflag,
   o.r_rec = at;   at += win_al16((size_t)KSG_RING * KSG_WIN_SUM_DWORDS * 4);
   o.r_mod = at;   at += win_al16((size_t)KSG_RING * 64 * 4);
   o.r_svc = at;   at += win_al16((size_t)KSG_RING * sizeof(RingSvc));
-  o.r_fit = at;   at += anti ? win_al16((size_t)KSG_RING * P * 64 * 8) : 0u;  // fit bitmaps (anti-affinity)
+  // fit bitmaps (anti-affinity; past 64k nodes read from phase A's rows instead, win2_fg)
+  o.r_fit = at;   at += anti && !win2_fg(P) ? win_al16((size_t)KSG_RING * P * 64 * 8) : 0u;
   o.s_meta = at;  at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(SlotMeta));
   o.s_cap = at;   at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(I64x2));
   o.s_snp = at;   at += win_al16((size_t)KSG_MAX_SLOTS * sizeof(I64x2));

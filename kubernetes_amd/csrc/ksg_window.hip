@@ -688,6 +688,22 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
   uint32_t* r_mod = reinterpret_cast<uint32_t*>(smem + o.r_mod);
   RingSvc* r_svc = reinterpret_cast<RingSvc*>(smem + o.r_svc);
   uint64_t* r_fit = reinterpret_cast<uint64_t*>(smem + o.r_fit);
+  // pod j's fit-at-the-snapshot word w: its ring copy, or past 64k nodes (win2_fg) phase A's row
+  // (the rank that scored word w wrote it at its block of the exchanged buffer)
+  auto fit_word = [&](uint32_t e, uint32_t j, uint32_t w) -> uint64_t {
+    if constexpr (win2_fg(P)) {
+      uint32_t g = 0;
+      for (uint32_t r = 1; r < x.world; ++r)
+        if (w >= x.wlo[r] && x.nw[r] > 0) g = r;
+      const uint32_t iw = w - x.wlo[g];
+      return (w < nwords && iw < x.nw[g])
+                 ? gld(reinterpret_cast<const uint64_t*>(x.buf + (size_t)g * x.blk + (size_t)iw * 8 + x.fit_off +
+                                                         (size_t)j * x.ostride * 8))
+                 : 0ULL;
+    } else {
+      return r_fit[(size_t)e * P * 64 + w];
+    }
+  };
   const WinSlots S{reinterpret_cast<SlotMeta*>(smem + o.s_meta), reinterpret_cast<I64x2*>(smem + o.s_cap),
                    reinterpret_cast<I64x2*>(smem + o.s_snp),     reinterpret_cast<I64x2*>(smem + o.s_dl),
                    reinterpret_cast<F64x2*>(smem + o.s_inv),     reinterpret_cast<uint32_t*>(smem + o.keys),
@@ -852,10 +868,11 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
 #pragma unroll
       for (int q = 0; q < P; ++q) r_t0[(size_t)e * P * 64 + lane * P + q] = t0[q];
       if (anti_on) {
+        if constexpr (!win2_fg(P))
 #pragma unroll
-        for (int q = 0; q < P; ++q)
-          r_fit[(size_t)e * P * 64 + lane * P + q] =
-              wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + x.fit_off + j * row_b) : 0ULL;
+          for (int q = 0; q < P; ++q)
+            r_fit[(size_t)e * P * 64 + lane * P + q] =
+                wb_at[q] != ~0u ? *reinterpret_cast<const uint64_t*>(x.buf + wb_at[q] + x.fit_off + j * row_b) : 0ULL;
         if (rr) {  // the re-rank's inputs: best-per-row words, best per row, domain counts
 #pragma unroll
           for (int q = 0; q < P; ++q)
@@ -931,7 +948,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
                        1ULL << (nd & 63));
             t0_drop = drop && in_t0;
           }
-          const bool fit_snap = anti_on && pv.s >= 0 && ((r_fit[(size_t)e * P * 64 + (nd >> 6)] >> (nd & 63)) & 1ULL);
+          const bool fit_snap = anti_on && pv.s >= 0 && ((fit_word(e, i, nd >> 6) >> (nd & 63)) & 1ULL);
           bool fits_now = false;
           if (fit_snap) {
             fits_now = slot_fits_now(S, sl, pv, rec, res_on, ports_on, disk_on);
@@ -1306,7 +1323,7 @@ __global__ __launch_bounds__(win_res_nt(P)) void ksg_win_resolve_kernel(KsgDev d
     }
     bool ls_counts = false;  // (re-rank) the last slot's node is still among the pod's filtered nodes
     if (anti_on && pv.s >= 0 && !chk_stop && ls_valid &&
-        ((r_fit[(size_t)e * P * 64 + (ls_node >> 6)] >> (ls_node & 63)) & 1ULL)) {
+        ((fit_word(e, i, ls_node >> 6) >> (ls_node & 63)) & 1ULL)) {
       // the last slot, from the register copy: does the pod still fit it?
       const int64_t now_c = (int64_t)((uint64_t)ls_snp_c + (uint64_t)ls_dl_c);
       const int64_t now_m = (int64_t)((uint64_t)ls_snp_m + (uint64_t)ls_dl_m);
@@ -3234,8 +3251,8 @@ uint32_t ksg_win_max_window(const KsgDev& d) {
   if (P == 0) return 0;
   const uint32_t nflag = (d.n_services + 31) / 32;
   const bool anti = d.n_anti > 0 && d.n_domains_total > 0;
-  // anti-affinity without the re-rank (the LDS-slot resolver): up to 32k nodes per shard
-  if (anti && P > 8 && !(d.rr_dz && !(d.dbg & 4096))) return 0;
+  // the LDS-slot resolver with the re-rank (KSG_DEBUG & 4096, a comparison path): up to 32k nodes
+  if (anti && P > 8 && d.rr_dz && (d.dbg & 4096)) return 0;
   uint32_t lo = 0, hi = 4096;
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1) / 2;
@@ -3318,6 +3335,8 @@ hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run
   KSG_RES_CASE(2, true)
   KSG_RES_CASE(4, true)
   KSG_RES_CASE(8, true)
+  KSG_RES_CASE(16, true)
+  KSG_RES_CASE(32, true)
 #undef KSG_RES_CASE
   return hipErrorInvalidValue;
 }

@@ -303,14 +303,19 @@ def test_full_size_matches_oracle(name, nn, npods):
     dev.close()
 
 
+@pytest.mark.parametrize("rerank", [True, False])
 @pytest.mark.parametrize("nn,npods", [
     (40000, 3000),   # P = 16: the domain rows' node bitmaps from HBM (win2_zg)
     (70000, 2000),   # P = 32: the fit and best-per-row bitmaps from phase A's rows too (win2_fg)
 ])
-def test_anti_affinity_large_shard_window_matches_oracle(nn, npods):
+def test_anti_affinity_large_shard_window_matches_oracle(nn, npods, rerank, monkeypatch):
     """ServiceAntiAffinity (config 4's policy) past 32k nodes on one shard takes the window
-    path (the re-rank resolver with its large bitmaps off LDS), not the exact kernel: every
-    decision, the RNG position and the committed totals against the incremental oracle."""
+    path, not the exact kernel: the re-rank resolver with its large bitmaps off LDS, and
+    without the re-rank (KSG_DEBUG & 2048: the LDS-slot resolver, the one multi-priority and
+    sharded anti-affinity contexts take) -- every decision, the RNG position and the committed
+    totals against the incremental oracle."""
+    if not rerank:
+        monkeypatch.setenv("KSG_DEBUG", "2048")
     case = Case("config4", nn, npods)
     dev, orc = _pair(case)
     got, sg = run_batch(dev, case, chunk=1000)
@@ -323,6 +328,27 @@ def test_anti_affinity_large_shard_window_matches_oracle(nn, npods):
     wc, wm = orc.read_requested()
     assert np.array_equal(gc, wc) and np.array_equal(gm, wm)
     assert st["windows"] > 0, st
+    dev.close()
+
+
+def test_many_anti_priorities_large_shard_window_matches_oracle():
+    """Six ServiceAntiAffinity priorities (tests/families.py many_anti) at 40k nodes: the
+    window path (phase A past its four register-held priorities, the LDS-slot resolver at
+    P = 16) against the oracle."""
+    from tests.families import FamilyCase
+
+    case = FamilyCase("many_anti", 40000, 1500)
+    orc = case.load(OracleScheduler(case.cfg))
+    want, sw = orc.batch(case.batch, 4242)
+    wc, wm = orc.read_requested()
+    dev = case.load(DeviceScheduler(case.cfg, device=0))
+    got, sg = dev.batch(case.batch, 4242)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"first mismatches at {bad[:8]}: gpu {got[bad[:8]]} oracle {want[bad[:8]]}"
+    assert sg == sw
+    gc, gm = dev.read_requested()
+    assert np.array_equal(gc, wc) and np.array_equal(gm, wm)
+    assert dev.last_batch_stats()["windows"] > 0
     dev.close()
 
 
