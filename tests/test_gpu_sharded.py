@@ -139,6 +139,7 @@ def _oracle(name, nn, npods, seed=1234, ext_used=False):
     ("config4", 900, 500, 128, 2, None),     # ServiceAntiAffinity: per-pod path + domain all-reduce
     ("config1", 500, 1000, 128, 2, None),    # BASELINE config 1
     ("config3", 15000, 50000, 128, 2, 1000), # BASELINE config 3 at full size, 1000-pod batches
+    ("config4", 70000, 1000, 128, 2, 500),   # ServiceAntiAffinity, 35k-node shards: the LDS-slot resolver at P = 16
 ] + [(f"fam:{f}", 700, 400, 64, 2, None) for f in ("multi_service", "namespaces", "negative", "big_weights",
                                                    "existing_hosts", "invalid_selectors")])
 def test_sharded_batch_matches_oracle(name, nn, npods, window, world, chunk):
