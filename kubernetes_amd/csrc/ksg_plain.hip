@@ -605,8 +605,10 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
       const int32_t h_s = __builtin_amdgcn_readlane(rec, WS_SVC);
       const bool h_over = (uint32_t)__builtin_amdgcn_readlane(rec, WS_NINL) > KSG_WIN_INLINE || nk > KSG_SLOT_KEYS ||
                           n_svcs > KSG_SLOT_SVCS;
-      const uint32_t h_prv = (j > 0 && lane < DW) ? recs[(size_t)(j - 1) * DW + lane] : 0u;
-      const bool h_prev_s = j > 0 && pod_has_service(h_prv, h_s);
+      // (pod j-1 of pod j's service: read only where the committer takes the d1 bitmap)
+      const bool h_d1 = !XS && pl_d1(P) && x.d1 != 0 && j > 0;
+      const uint32_t h_prv = (h_d1 && lane < DW) ? recs[(size_t)(j - 1) * DW + lane] : 0u;
+      const bool h_prev_s = h_d1 && pod_has_service(h_prv, h_s);
       const uint32_t h_pfl = (drawable ? 0u : 1u) | (h_prev_s ? 2u : 0u) | (h_over ? 4u : 0u) | (min(nk, 255u) << 8) |
                              (min(n_svcs, 255u) << 16) | (min(n_sel, 255u) << 24);
       if (lane == 0) {
