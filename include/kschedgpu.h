@@ -109,10 +109,10 @@ typedef struct ksg_config {
                                    (generic_scheduler.go:141-143)                       */
   /* Priority weights are Go ints (plugin/pkg/scheduler/api/types.go:46: int64 on
    * the reference's platform) and combined scores wrap like Go's int
-   * (generic_scheduler.go:145-159). While 10 * sum|w| + |w_equal| < 2^30 and at
-   * most 4 ServiceAntiAffinity priorities carry a weight, the window path runs
-   * with int32 scores; otherwise every batch takes the exact kernels with int64
-   * (wrapping) combined scores. */
+   * (generic_scheduler.go:145-159). While 10 * sum|w| + |w_equal| < 2^30 the
+   * window path runs with int32 scores (any number of ServiceAntiAffinity
+   * priorities, any shard size up to 131,072 nodes); otherwise every batch takes
+   * the exact kernels with int64 (wrapping) combined scores. */
   int64_t w_least_requested;    /* LeastRequestedPriority weight, 0 = absent/skipped    */
   int64_t w_service_spreading;  /* ServiceSpreadingPriority weight                       */
   int64_t w_equal;              /* EqualPriority weight (DefaultProvider: 0, skipped)    */
