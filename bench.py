@@ -91,6 +91,7 @@ _STAGES2 = {
     28: ("xchecker", "wait_node"), 29: ("xchecker", "check"), 30: ("xchecker", "bookkeeping_and_lists"),
     # (ServiceAntiAffinity re-ranks: their count x 64 per pod and their cycles)
     9: ("committer", "rerank_x64"), 12: ("committer", "rerank_cycles"),
+    22: ("checker0", "check_record"), 23: ("checker0", "check_slot"),  # (check = these + the row sums and post)
 }
 
 

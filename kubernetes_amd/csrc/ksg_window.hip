@@ -2251,10 +2251,13 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         // service the slot adds to its row's count while the pod still fits it
         bool drop = false, t0d = false, astop = false;
         uint32_t ks = 0;
+        cstamp(c == 0 ? 22 : 40);  // (checker 0: the pod's record; lane 40 is dropped)
         if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE && S.node != ~0u) {
           const PodView pv = pod_view(rec);
           const uint32_t wd = S.node >> 6;
           const uint64_t nb = 1ULL << (S.node & 63);
+          SlotRow R;  // the slot's lists, in registers (in flight with the slot's T0 / B / fit words)
+          R.load(my_cl);
           const bool in_t0 = (r_t0[(size_t)e * P * 64 + wd] & nb) != 0;
           const bool in_b = ((FG ? pa_word(x.b_off, i, wd) : r_b[(size_t)e * P * 64 + wd]) & nb) != 0;
           const bool fsnap = pv.s >= 0 && ((FG ? pa_word(x.fit_off, i, wd) : r_fit[(size_t)e * P * 64 + wd]) & nb) != 0;
@@ -2264,8 +2267,6 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
             bool nofit = false;
             if (res_on && !pv.zero_req)  // PodFitsResources (predicates.go:127-145)
               nofit = !((S.cap_c == 0 || S.cap_c - now_c >= pv.req_c) && (S.cap_m == 0 || S.cap_m - now_m >= pv.req_m));
-            SlotRow R;  // the slot's lists, in registers
-            R.load(my_cl);
             if (!nofit && pv.nk && S.nk)  // PodFitsPorts / NoDiskConflict vs the window's keys
               nofit |= R.key_hit(S.nk, rec, pv.nk, pv.n_ports, ports_on, disk_on);
             if (in_b) {
@@ -2298,6 +2299,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
             }
           }
         }
+        cstamp(c == 0 ? 23 : 40);  // (checker 0: the slot's check)
         cntd = __popcll(__ballot(t0d));
         int32_t ddrop = 0;  // B drops of this lane's row (unlabelled nodes: row dz-1)
         for (uint64_t dm = __ballot(drop); dm; dm &= dm - 1) {
@@ -2364,7 +2366,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
           ctl->chk_msk[c][par][0] = (uint32_t)dmsk;
           ctl->chk_msk[c][par][1] = (uint32_t)(dmsk >> 32);
         }
-        st_rel(&ctl->chk_seq[c], i + 1);
+        st_post(&ctl->chk_seq[c], i + 1);
       }
       cstamp(c == 0 ? 18 : 21);
     }
@@ -2398,7 +2400,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       }
     }
     if constexpr (STAMP) {
-      if (d.dbgbuf && lane >= 16 && lane < 22) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
+      if (d.dbgbuf && lane >= 16 && lane < 24) atomicAdd(d.dbgbuf + lane, (int32_t)(t_acc / 64));
     }
     drain_stores();
     if (lane == 0) st_rel(&ctl->fin[c], 1u);
@@ -2686,7 +2688,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         }
         ctl->xres[par] = res;
         if constexpr (STAMP) ctl->t_x = (uint32_t)__builtin_amdgcn_s_memtime();
-        st_rel(&ctl->xseq, i + 1);
+        st_post(&ctl->xseq, i + 1);
       }
       // off the chain now: commit i-1's service flags and first peers (the
       // committer reads them for pod i+1 once this iteration is done)
@@ -2809,8 +2811,8 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         L_cm[i].kind = 0;
         L_cm[i].out = __builtin_amdgcn_readlane(rec, WS_ERR) ? KSG_OUT_ERROR : KSG_OUT_NOFIT;
         L_cm[i].xn = ~0u;
-        st_rel(&ctl->xn_seq, i + 1);
-        st_rel(&ctl->sel_seq, i + 1);
+        st_post(&ctl->xn_seq, i + 1);
+        st_post(&ctl->sel_seq, i + 1);
       }
       have_x = false;  // pod i+1's checkers see every commit up to i-1
       prev_sv = ~0u;
@@ -3069,7 +3071,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     if (lane == 0) {  // the x-checker loads the node's snapshot meanwhile
       L_cm[i].xn = woff;
       if constexpr (STAMP) ctl->t_n = (uint32_t)__builtin_amdgcn_s_memtime();
-      st_rel(&ctl->xn_seq, i + 1);
+      st_post(&ctl->xn_seq, i + 1);
     }
     KSG_STAMP2(3)
     // ---- AssumePod's slot
@@ -3114,7 +3116,7 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
       *reinterpret_cast<uint4*>(&L_cm[i]) =
           uint4{1u, slot, woff, (in_c ? 0u : 1u) | ((int32_t)woff == pred ? 2u : 0u) | (n_svcs << 8)};
       L_cm[i].out = (int32_t)(d.lo + woff);
-      st_rel(&ctl->sel_seq, i + 1);  // the checkers and the x-checker move on
+      st_post(&ctl->sel_seq, i + 1);  // the checkers and the x-checker move on
     }
     if ((int32_t)woff != pred) KSG_COUNT2(8, 64)
     if (lane == (slot & 63)) {  // this wave's counts and deltas of the slot
