@@ -2272,9 +2272,11 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
             if (in_b) {
               drop = nofit;
               if (!drop && d.w_lr) {  // LeastRequested (priorities.go:43-76)
-                const int32_t lr_now = lr_win(now_c + pv.req_c, S.cap_c, S.inv_c) + lr_win(now_m + pv.req_m, S.cap_m, S.inv_m);
+                // (branch-free terms: the four interleave)
+                const int32_t lr_now =
+                    lr_win_nb(now_c + pv.req_c, S.cap_c, S.inv_c) + lr_win_nb(now_m + pv.req_m, S.cap_m, S.inv_m);
                 const int32_t lr_snap =
-                    lr_win(S.snp_c + pv.req_c, S.cap_c, S.inv_c) + lr_win(S.snp_m + pv.req_m, S.cap_m, S.inv_m);
+                    lr_win_nb(S.snp_c + pv.req_c, S.cap_c, S.inv_c) + lr_win_nb(S.snp_m + pv.req_m, S.cap_m, S.inv_m);
                 drop = (lr_now >> 1) != (lr_snap >> 1);
               }
               if (!drop && spread_on && pv.s >= 0 && ((S.smask >> (pv.s & 31)) & 1u)) {
