@@ -2303,22 +2303,17 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
         }
         cstamp(c == 0 ? 23 : 40);  // (checker 0: the slot's check)
         cntd = __popcll(__ballot(t0d));
-        int32_t ddrop = 0;  // B drops of this lane's row (unlabelled nodes: row dz-1)
-        for (uint64_t dm = __ballot(drop); dm; dm &= dm - 1) {
-          const uint32_t rw = (uint32_t)__builtin_amdgcn_readlane((int)S.row, (int)__builtin_ctzll(dm));
-          if (lane == (rw != ~0u ? rw : dz - 1)) ++ddrop;
+        // per domain row: the B drops (unlabelled nodes: row dz-1) and the window commits of the
+        // pod's service on slots it still fits, summed by LDS atomics after the rows are zeroed
+        // (one wave's LDS operations run in issue order)
+        int32_t* const ddr = L_ddr + (c * 2 + par) * KSG_RR_MAXZ;
+        int32_t* const dca = L_dca + (c * 2 + par) * KSG_RR_MAXZ;
+        if (lane < dz) {
+          ddr[lane] = 0;
+          dca[lane] = 0;
         }
-        if (lane < dz) L_ddr[(c * 2 + par) * KSG_RR_MAXZ + lane] = ddrop;
-        int32_t dadd = 0;
-        uint64_t pm = __ballot(ks != 0 && S.row != ~0u);
-        while (pm) {
-          const int b = (int)__builtin_ctzll(pm);
-          pm &= pm - 1;
-          const uint32_t zz = (uint32_t)__builtin_amdgcn_readlane((int)S.row, b);
-          const int32_t kk = __builtin_amdgcn_readlane((int)ks, b);
-          if (lane == zz) dadd += kk;
-        }
-        if (lane < dz) L_dca[(c * 2 + par) * KSG_RR_MAXZ + lane] = dadd;
+        if (drop) atomicAdd(&ddr[S.row != ~0u ? S.row : dz - 1], 1);
+        if (ks != 0 && S.row != ~0u) atomicAdd(&dca[S.row], (int32_t)ks);
         const uint32_t ast = __ballot(astop) != 0;
         if (lane == 0) ctl->chk_stop[c][par] = ast;
       } else if (!__builtin_amdgcn_readlane(rec, WS_ERR) && m0 != KSG_S32_NONE) {
