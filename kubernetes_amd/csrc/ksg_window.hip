@@ -2141,14 +2141,18 @@ __global__ __launch_bounds__(512) void ksg_win_resolve2_kernel(KsgDev d, uint32_
     // counts into the table (the x-checker applies the service flags, in commit
     // order)
     auto apply = [&](uint32_t p) {
-      const uint32_t kind = __builtin_amdgcn_readfirstlane(L_cm[p].kind);
-      const uint32_t slot = __builtin_amdgcn_readfirstlane(L_cm[p].slot);
+      // (the commit record's 16 bytes and the pod's record in one round of LDS reads)
+      const uint4 cmv = *reinterpret_cast<const uint4*>(&L_cm[p]);
+      const uint32_t ep = p % RING;
+      const uint32_t prec_l = r_rec[ep * DW + min(lane, DW - 1)];
+      const uint32_t kind = __builtin_amdgcn_readfirstlane(cmv.x);
+      const uint32_t slot = __builtin_amdgcn_readfirstlane(cmv.y);
       if (kind != 1 || (slot >> 6) != c) return;
-      const uint32_t woff = __builtin_amdgcn_readfirstlane(L_cm[p].node);
-      const uint32_t fl = __builtin_amdgcn_readfirstlane(L_cm[p].flags);
+      const uint32_t woff = __builtin_amdgcn_readfirstlane(cmv.z);
+      const uint32_t fl = __builtin_amdgcn_readfirstlane(cmv.w);
       const bool fresh = (fl & 1u) != 0, is_pred = (fl & 2u) != 0;
-      const uint32_t ol = slot & 63, ep = p % RING, wn = d.lo + woff;
-      const uint32_t prec = lane < DW ? r_rec[ep * DW + lane] : 0u;
+      const uint32_t ol = slot & 63, wn = d.lo + woff;
+      const uint32_t prec = lane < DW ? prec_l : 0u;
       const PodView ppv = pod_view(prec);
       const uint32_t nss = __builtin_amdgcn_readlane(prec, WS_NSS);
       const uint32_t n_sel = nss & 0xffff, n_svcs = nss >> 16, nk = ppv.nk;
