@@ -195,6 +195,11 @@ def _stage_breakdown(cfg, view, args, step_batch, anti, ext=None):
     plain = not any(int(cfg.w_anti[a]) != 0 for a in range(int(cfg.n_anti)))
     for lane, (role, st) in (_STAGES_PLAIN if plain else _STAGES2).items():
         out.setdefault(role, {})[st] = round(float(c[lane]) / pods, 1)
+    nwin = float(c[54]) / 64
+    if plain and nwin > 0:  # the fused launch's window start (10-ns ticks, s_memrealtime), per window
+        out["window_start_us"] = {"windows": int(nwin),
+                                  "to_first_group_scored": round(float(c[52]) / 64 / nwin / 100, 2),
+                                  "to_first_entry_staged": round(float(c[53]) / 64 / nwin / 100, 2)}
     return out
 
 

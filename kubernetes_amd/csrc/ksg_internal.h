@@ -235,6 +235,24 @@ struct KsgWinRun {
   uint32_t stops[4];  // windows ended early, by stop reason 1..3
 };
 
+// The fused window launch (ksg_plain.hip, ksg_win_plain_kernel<..., FUSED>): one
+// launch per window instead of phase A + T0 images + resolver. Block 0 resolves
+// the window; blocks 1.. score it (ksg_score.h, outputs write-through) in pod-group
+// order, and after each (pod group, word group) task add 1 to cnt[set][group][xcd
+// shard]; a resolver producer waits for the 8 shards of its pod's group to sum to
+// the word groups, then builds the pod's T0 image itself. The run record has two
+// slots: launch k reads slot k & 1 and its block 0 writes the outcome into slot
+// (k + 1) & 1 (a scoring block still starting up never reads the window's own
+// outcome), and zeroes counter set (k + 1) & 1 for launch k + 1.
+struct KsgFused {
+  const ksg_pod* batch;  // the batch's pods and id lists (device)
+  const uint32_t* ids;
+  KsgWinRun* run_out;    // slot (k + 1) & 1
+  uint32_t* cnt;         // uint32[2][ngroups][8]
+  uint32_t set;          // k & 1
+  uint32_t ngroups;      // counter rows per set (>= pod groups in a window)
+};
+
 // one record of the per-pod winner exchange (all-gathered across ranks)
 typedef ksg_shard_record KsgRecordHdr;  // public layout (include/kschedgpu.h)
 // followed by nwords_max uint64 tie words (bit set = node at max_score)

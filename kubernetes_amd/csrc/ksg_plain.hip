@@ -86,6 +86,7 @@
 // wait has a spin limit; a timed-out wait sets ctl->hang and the host fails
 // the batch.
 #include "ksg_resolver.h"
+#include "ksg_score.h"
 
 #define KSG_NCAND 6     // candidate nodes staged per pod (0, 1 or 2 drops)
 #define KSG_CSV_MAX 10  // services of a pod whose counts on the candidates are staged (6 x 10 lanes)
@@ -316,13 +317,100 @@ __global__ __launch_bounds__(256) void ksg_win_t0_kernel(uint32_t nwords, uint32
 // XS: extended resources re-checked on the slots (extensions; a separate
 // instantiation: their per-slot state would cost every other configuration
 // registers on the chain)
-template <int P, bool STAMP, bool XS>
+// ---------------------------------------------------------------------------
+// the fused launch's scoring blocks (KsgFused, ksg_internal.h)
+// ---------------------------------------------------------------------------
+// pods per phase-A wave in the fused launch: 4 up to 512 words per shard (P <= 8), 8 above
+__host__ __device__ constexpr int pl_pg(int P) { return P <= 8 ? 4 : 8; }
+
+// Blocks 1.. of the fused launch: every (pod group, word group) task of the window, pod group
+// major, so the resolver's first pods are scored first. Word groups are split into 8 contiguous
+// ranges, one per block % 8 (the hardware deals blocks round-robin to the 8 XCDs: a word group's
+// node state is fetched into one XCD's L2 for every pod group; speed only, nothing depends on the
+// placement). One wave = one 64-node word x pl_pg(P) pods (ksg_score.h); its outputs are stored
+// write-through, every wave drains them, and after the block's barrier one lane adds 1 to the
+// group's counter shard (MI355X_MICROARCH.md, visibility: sc1 stores + vmcnt(0) + an agent
+// atomic, read with sc1 loads).
+// one scoring task (KSG_FUSED_NOINLINE, an A/B build: a separate function, so its registers do
+// not add to the resolver's pressure in the same kernel, at the price of a call frame in scratch)
+#ifdef KSG_FUSED_NOINLINE
+#define KSG_FUSED_TASK_ATTR __attribute__((noinline))
+#else
+#define KSG_FUSED_TASK_ATTR __forceinline__
+#endif
+template <int P>
+__device__ KSG_FUSED_TASK_ATTR void fused_score_task(const KsgDev& d, const KsgFused& f, uint32_t pos,
+                                                           uint32_t n_batch, uint32_t wcap, uint32_t w, uint32_t p0,
+                                                           KsgWinSum* sums, uint64_t* wbits, int32_t* wmax,
+                                                           uint32_t ostride, uint64_t* wd1, uint32_t* rec_lds) {
+  win_score_wave<KSG_WIN_PLAIN, pl_pg(P), false, true>(d, f.batch, f.ids, pos, n_batch, wcap, w, p0, sums, wbits, wmax,
+                                                      ostride, nullptr, wd1, nullptr, nullptr, 0u, nullptr, nullptr,
+                                                      nullptr, nullptr, rec_lds);
+}
+
+template <int P>
+__device__ __forceinline__ void fused_score_blocks(const KsgDev& d, uint32_t wcap, const KsgWinRun* run,
+                                                   const KsgWinSum* sums_c, const KsgWinXchg& x, const KsgFused& f,
+                                                   char* smem) {
+  constexpr uint32_t NWV = pl_nt(P) / 64;
+  constexpr int PGF = pl_pg(P);
+  const uint32_t pos = run->pos, n_batch = run->n;
+  if (run->halt || pos >= n_batch) return;
+  const uint32_t n_pods = min(wcap, n_batch - pos);
+  const uint32_t ngrp = (n_pods + PGF - 1) / PGF;
+  const uint32_t nwg = (d.nwords + NWV - 1) / NWV;
+  const uint32_t b = blockIdx.x, xs = b & 7u;
+  const uint32_t nbx = (gridDim.x - xs + 7u) / 8u - (xs == 0 ? 1u : 0u);  // (block 0 resolves)
+  const uint32_t ix = (b >> 3) - (xs == 0 ? 1u : 0u);
+  const uint32_t wg0 = nwg * xs / 8u, nwx = nwg * (xs + 1u) / 8u - wg0;
+  const uint32_t wave = threadIdx.x >> 6;
+  uint32_t* rec_lds = reinterpret_cast<uint32_t*>(smem) + wave * PGF * KSG_WIN_SUM_DWORDS;
+  KsgWinSum* sums = const_cast<KsgWinSum*>(sums_c);
+  uint64_t* wbits = reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(x.buf));
+  int32_t* wmax = reinterpret_cast<int32_t*>(const_cast<uint8_t*>(x.buf) + (size_t)x.wcap * x.ostride * 8);
+  uint64_t* wd1 = x.d1 ? reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(x.buf) + x.d1_off) : nullptr;
+  for (uint32_t t = ix; t < nwx * ngrp; t += nbx) {
+    const uint32_t g = t / nwx, wgp = wg0 + (t - g * nwx);
+    const uint32_t w = __builtin_amdgcn_readfirstlane(wgp * NWV + wave);
+    fused_score_task<P>(d, f, pos, n_batch, wcap, w, g * PGF, sums, wbits, wmax, x.ostride, wd1, rec_lds);
+    drain_stores();  // (every storing wave: its write-through stores have landed)
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_fetch_add(f.cnt + ((size_t)f.set * f.ngroups + g) * 8u + xs, 1u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// has pod group g of the fused launch been scored (all word groups, summed over the 8 shards)?
+// (wave-uniform; sc1 loads of the counters)
+__device__ __forceinline__ bool fused_group_done(const KsgFused& f, uint32_t g, uint32_t nwg) {
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const uint32_t v = lane < 8 ? ld_mut(f.cnt + ((size_t)f.set * f.ngroups + g) * 8u + lane) : 0u;
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s += (uint32_t)__builtin_amdgcn_readlane((int)v, k);
+  return s >= nwg;
+}
+
+template <int P, bool STAMP, bool XS, bool FUSED>
 __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
                                                             const KsgWinSum* __restrict__ sums, const KsgWinXchg x,
-                                                            uint64_t* rng_io, int32_t* __restrict__ out_batch) {
+                                                            uint64_t* rng_io, int32_t* __restrict__ out_batch,
+                                                            const KsgFused f) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if constexpr (FUSED) {
+    if (blockIdx.x != 0) {
+      fused_score_blocks<P>(d, wcap, run, sums, x, f, smem);
+      return;
+    }
+  }
+  // (the fused launch: the window's outcome goes into the next launch's slot)
+  KsgWinRun* const run_out = FUSED ? f.run_out : run;
   const uint32_t pos = run->pos, n_batch = run->n;
-  if (run->halt || pos >= n_batch) return;  // the chain is done (uniform, before any barrier)
+  if (run->halt || pos >= n_batch) {  // the chain is done (uniform, before any barrier)
+    if (FUSED && threadIdx.x == 0) *run_out = *run;
+    return;
+  }
   const uint32_t n_pods = min(wcap, n_batch - pos);
   int32_t* __restrict__ out = out_batch + pos;
   const uint32_t tid = threadIdx.x;
@@ -332,6 +420,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
   constexpr uint32_t RING = win2_ring(P, false);
   constexpr uint32_t NT = pl_nt(P);
   constexpr uint32_t NPW = NT / 64 - KSG_PL_P0;  // producer waves
+  const uint32_t f_nwg = FUSED ? (d.nwords + NT / 64 - 1) / (NT / 64) : 0u;  // (fused: word groups per pod group)
   constexpr uint32_t DW = KSG_WIN_SUM_DWORDS;
   const PlLdsOff o = plain_lds_offsets(P, nflag, wcap);
   PlCtl* ctl = reinterpret_cast<PlCtl*>(smem + o.ctl);
@@ -381,6 +470,8 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
 
   for (uint32_t t = tid; t < RING; t += NT) r_hdr[t].ready = 0;
   if (tid == 0) *ctl = PlCtl{};
+  if constexpr (FUSED)  // the next launch's counters (launch k - 1, their last user, has ended)
+    for (uint32_t t = tid; t < f.ngroups * 8u; t += NT) st_mut(f.cnt + (size_t)(f.set ^ 1u) * f.ngroups * 8u + t, 0u);
   for (uint32_t w = tid; w < nflag; w += NT) {
     L_flag[w] = 0;
     L_peerset[w] = 0;
@@ -406,6 +497,10 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
       }
     };
     if constexpr (STAMP) p_last = __builtin_amdgcn_s_memtime();
+    // (KSG_DEBUG & 8, fused: 10-ns ticks from the block's start to pod 0's group scored and on to
+    // its ring entry staged, summed over windows into dbgbuf[52..54])
+    const uint64_t f_t0 = (STAMP && FUSED) ? __builtin_amdgcn_s_memrealtime() : 0ULL;
+    uint64_t f_tg = 0;
     for (uint32_t j = wave - KSG_PL_P0; j < n_pods; j += NPW) {
       const uint32_t e = j % RING;
       // ring entry free: the checkers applied commit j - RING (while checking
@@ -425,7 +520,79 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
       }
       pstamp(24);
       if (skew & 8u) __builtin_amdgcn_s_sleep(8);
-      const uint32_t rec = lane < DW ? recs[(size_t)j * DW + lane] : 0u;
+      uint32_t rec, lpv, k0;
+      int32_t m0;
+      if constexpr (FUSED) {
+        // pod j's group scored by the worker blocks (and pod j-1's: its record is read below)
+        const uint32_t g = j / (uint32_t)pl_pg(P);
+        const uint32_t g_lo = (j > 0 && j % (uint32_t)pl_pg(P) == 0) ? g - 1u : g;
+        for (uint32_t spin = 0;; ++spin) {
+          if (ld_acq(&ctl->stop)) return;
+          if (spin > KSG_SPIN_LIMIT) {
+            ctl->hang = 1;
+            return;
+          }
+          if (fused_group_done(f, g, f_nwg) && (g_lo == g || fused_group_done(f, g_lo, f_nwg))) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        rec = lane < DW ? ld_mut(recs + (size_t)j * DW + lane) : 0u;
+        // pod j's T0 image, built here from phase A's per-word results (sc1 loads of the worker
+        // blocks' write-through stores): m0 = the best word maximum, T0 = the words' bitmaps at
+        // m0, their in-row prefixes, the row prefixes (lane 2q: T0 bits below row q, 2q + 1:
+        // through it) and k0; the single-commit drop bitmaps copied as they are
+        const int32_t* pm = reinterpret_cast<const int32_t*>(x.buf + (size_t)x.wcap * x.ostride * 8) + (size_t)j * x.ostride;
+        const uint64_t* pb = reinterpret_cast<const uint64_t*>(x.buf) + (size_t)j * x.ostride;
+        const uint64_t* pd = reinterpret_cast<const uint64_t*>(x.buf + x.d1_off) + (size_t)j * x.ostride;
+        int32_t mw[P];
+        int32_t lm = KSG_S32_NONE;
+        // up to 8 rows (P <= 8) the bitmaps are loaded with the maxima, one round of loads
+        constexpr bool ONE = P <= 8;
+        uint64_t b1[ONE ? P : 1];
+#pragma unroll
+        for (uint32_t q = 0; q < P; ++q) {
+          const uint32_t wq = q * 64 + lane;
+          mw[q] = wq < d.nwords ? ld_mut(pm + wq) : KSG_S32_NONE;
+          if constexpr (ONE) b1[q] = wq < d.nwords ? ld_mut(pb + wq) : 0ULL;
+          lm = mw[q] > lm ? mw[q] : lm;
+        }
+        m0 = wave_total_max(lm);
+        if constexpr (STAMP) {
+          if (j == 0) f_tg = __builtin_amdgcn_s_memrealtime();
+        }
+        uint64_t* f_t0 = r_t0 + (size_t)e * P * 64;
+        uint16_t* f_wp = r_wp + (size_t)e * P * 64;
+        uint64_t* f_d1 = r_d1 + (size_t)e * P * 64;
+        const bool cp_d1 = pl_d1(P) && x.d1 != 0;
+        constexpr uint32_t QC = P < 8 ? P : 8;  // rows whose loads are in flight together
+        uint32_t below = 0;
+        lpv = 0;
+#pragma unroll
+        for (uint32_t q0 = 0; q0 < P; q0 += QC) {
+          uint64_t bw[QC], dw[QC];
+#pragma unroll
+          for (uint32_t k = 0; k < QC; ++k) {
+            const uint32_t wq = (q0 + k) * 64 + lane;
+            if constexpr (ONE) bw[k] = (m0 != KSG_S32_NONE && mw[q0 + k] == m0) ? b1[q0 + k] : 0ULL;
+            else bw[k] = (m0 != KSG_S32_NONE && wq < d.nwords && mw[q0 + k] == m0) ? ld_mut(pb + wq) : 0ULL;
+            dw[k] = (cp_d1 && wq < d.nwords) ? ld_mut(pd + wq) : 0ULL;
+          }
+#pragma unroll
+          for (uint32_t k = 0; k < QC; ++k) {
+            const uint32_t q = q0 + k;
+            const uint32_t c1 = (uint32_t)__popcll(bw[k]);
+            const uint32_t in1 = dpp_scan_add(c1);
+            const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)in1, 63);
+            f_t0[q * 64 + lane] = bw[k];
+            f_wp[q * 64 + lane] = (uint16_t)(in1 - c1);
+            if (cp_d1) f_d1[q * 64 + lane] = dw[k];
+            if (lane == 2 * q) lpv = below;
+            if (lane == 2 * q + 1) lpv = below + tot;
+            below += tot;
+          }
+        }
+        k0 = below;
+      } else {
+      rec = lane < DW ? recs[(size_t)j * DW + lane] : 0u;
       // the pod's T0 image into the ring entry: 16-byte loads, all in flight,
       // then the LDS stores (T0 words, in-row prefixes, row prefixes, m0 / k0)
       const uint8_t* im = x.img + (size_t)j * x.img_stride;
@@ -440,15 +607,9 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
         const uint8_t* src = t < NT0 + NWP ? im + (size_t)t * 16 : im + t0img_d1(P) + (size_t)(t - NT0 - NWP) * 16;
         ch[k] = t < nch ? *reinterpret_cast<const uint4*>(src) : uint4{0, 0, 0, 0};
       }
-      const uint32_t lpv = lane < 2 * P ? *reinterpret_cast<const uint32_t*>(im + t0img_lp(P) + lane * 4) : 0u;
-      const int32_t m0 = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int32_t*>(im + t0img_hdr(P)));
-      const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane(*reinterpret_cast<const int32_t*>(im + t0img_hdr(P) + 4));
-      const bool drawable = __builtin_amdgcn_readlane(rec, WS_ERR) == 0 && m0 != KSG_S32_NONE;
-      const uint32_t wj = j >> 5, bj = 1u << (j & 31);
-      if (lane == 0) {  // the drawable bit first, then "known" (readers read them in that order)
-        if (drawable) atomicOr(&L_drw[wj], bj);
-        atomicOr(&L_pub[wj], bj);
-      }
+      lpv = lane < 2 * P ? *reinterpret_cast<const uint32_t*>(im + t0img_lp(P) + lane * 4) : 0u;
+      m0 = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int32_t*>(im + t0img_hdr(P)));
+      k0 = (uint32_t)__builtin_amdgcn_readfirstlane(*reinterpret_cast<const int32_t*>(im + t0img_hdr(P) + 4));
       uint4* e_t0 = reinterpret_cast<uint4*>(r_t0 + (size_t)e * P * 64);
       uint4* e_wp = reinterpret_cast<uint4*>(r_wp + (size_t)e * P * 64);
       uint4* e_d1 = reinterpret_cast<uint4*>(r_d1 + (size_t)e * P * 64);
@@ -458,6 +619,13 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
         if (t < NT0) e_t0[t] = ch[k];
         else if (t < NT0 + NWP) e_wp[t - NT0] = ch[k];
         else if (t < nch) e_d1[t - NT0 - NWP] = ch[k];
+      }
+      }
+      const bool drawable = __builtin_amdgcn_readlane(rec, WS_ERR) == 0 && m0 != KSG_S32_NONE;
+      const uint32_t wj = j >> 5, bj = 1u << (j & 31);
+      if (lane == 0) {  // the drawable bit first, then "known" (readers read them in that order)
+        if (drawable) atomicOr(&L_drw[wj], bj);
+        atomicOr(&L_pub[wj], bj);
       }
       if (lane < 2 * P) r_lp[e * 64 + lane] = lpv;
       // (the entry is read back below through other pointer types: no
@@ -607,7 +775,9 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
                           n_svcs > KSG_SLOT_SVCS;
       // (pod j-1 of pod j's service: read only where the committer takes the d1 bitmap)
       const bool h_d1 = !XS && pl_d1(P) && x.d1 != 0 && j > 0;
-      const uint32_t h_prv = (h_d1 && lane < DW) ? recs[(size_t)(j - 1) * DW + lane] : 0u;
+      const uint32_t h_prv = (h_d1 && lane < DW) ? (FUSED ? ld_mut(recs + (size_t)(j - 1) * DW + lane)
+                                                          : recs[(size_t)(j - 1) * DW + lane])
+                                                 : 0u;
       const bool h_prev_s = h_d1 && pod_has_service(h_prv, h_s);
       const uint32_t h_pfl = (drawable ? 0u : 1u) | (h_prev_s ? 2u : 0u) | (h_over ? 4u : 0u) | (min(nk, 255u) << 8) |
                              (min(n_svcs, 255u) << 16) | (min(n_sel, 255u) << 24);
@@ -624,6 +794,14 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
         r_hdr[e].pred = (int32_t)cand0;
         r_hdr[e].pad = csv_on ? 1u : 0u;  // the candidates' service counts are staged
         st_rel(&r_hdr[e].ready, j + 1);
+      }
+      if constexpr (STAMP && FUSED) {
+        if (j == 0 && lane == 0 && d.dbgbuf) {
+          const uint64_t t_r = __builtin_amdgcn_s_memrealtime();
+          atomicAdd(d.dbgbuf + 52, (int32_t)(f_tg - f_t0));
+          atomicAdd(d.dbgbuf + 53, (int32_t)(t_r - f_tg));
+          atomicAdd(d.dbgbuf + 54, 1);
+        }
       }
       pstamp(27);
     }
@@ -2008,19 +2186,21 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
   }
   if (lane == 0) {
     *rng_io = rng0 + (uint64_t)n_draws * ksg_rng_step(d.draws);
+    KsgWinRun r = *run;
     if (reason == KSG_STOP_HANG) {
-      run->halt = KSG_HALT_HANG;
+      r.halt = KSG_HALT_HANG;
     } else if (reason == KSG_STOP_BAD) {
-      run->halt = KSG_HALT_BAD;
+      r.halt = KSG_HALT_BAD;
     } else if (reason == KSG_STOP_OVERSIZE) {
-      run->halt = KSG_HALT_OVERSIZE;  // pod pos: the host runs the exact per-pod path, then resumes
+      r.halt = KSG_HALT_OVERSIZE;  // pod pos: the host runs the exact per-pod path, then resumes
     } else if (resolved == 0 || resolved > n_pods) {
-      run->halt = KSG_HALT_BADCOUNT;
+      r.halt = KSG_HALT_BADCOUNT;
     } else {
-      run->pos = pos + resolved;
-      run->windows += 1;
-      if (reason >= 1 && reason <= 3) run->stops[reason] += 1;
+      r.pos = pos + resolved;
+      r.windows += 1;
+      if (reason >= 1 && reason <= 3) r.stops[reason] += 1;
     }
+    *run_out = r;
   }
 }
 
@@ -2055,19 +2235,19 @@ hipError_t ksg_launch_win_t0(const KsgDev& d, uint32_t wcap, const KsgWinRun* ru
   return hipGetLastError();
 }
 
-template <int PP, bool ST, bool XS>
+template <int PP, bool ST, bool XS, bool FU = false>
 static hipError_t win_plain_launch_x(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run,
                                      const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
-                                     hipStream_t st) {
+                                     hipStream_t st, const KsgFused& f = KsgFused{}, uint32_t grid = 1) {
   static bool once = false;
   if (!once) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_plain_kernel<PP, ST, XS>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_plain_kernel<PP, ST, XS, FU>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipGetLastError();  // do not leave a sticky error behind
     once = true;
   }
-  hipLaunchKernelGGL((ksg_win_plain_kernel<PP, ST, XS>), dim3(1), dim3(pl_nt(PP)), lds, st, d, wcap, run, sums, x, rng,
-                     out);
+  hipLaunchKernelGGL((ksg_win_plain_kernel<PP, ST, XS, FU>), dim3(grid), dim3(pl_nt(PP)), lds, st, d, wcap, run, sums,
+                     x, rng, out, f);
   return hipGetLastError();
 }
 
@@ -2100,5 +2280,36 @@ hipError_t ksg_launch_win_plain(const KsgDev& d, uint32_t P, uint32_t wcap, KsgW
   KSG_PLAIN_CASE(16)
   KSG_PLAIN_CASE(32)
 #undef KSG_PLAIN_CASE
+  return hipErrorInvalidValue;
+}
+
+// the fused window launch (KsgFused): block 0 resolves, blocks 1 .. grid-1 score the window
+// (no ServiceAntiAffinity, no extensions, one rank); run = this launch's slot
+bool ksg_win_fused_ok(const KsgDev& d) { return plain_P(d) >= 1 && d.nwords > 0; }
+
+uint32_t ksg_win_fused_groups(const KsgDev& d, uint32_t wcap) {
+  const uint32_t pg = (uint32_t)pl_pg((int)plain_P(d));
+  return (wcap + pg - 1) / pg;
+}
+
+hipError_t ksg_launch_win_fused(const KsgDev& d, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
+                                const KsgWinXchg& x, uint64_t* rng, int32_t* out, const KsgFused& f, uint32_t grid,
+                                hipStream_t st) {
+  const uint32_t P = plain_P(d);
+  // (the scoring blocks stage their pods' records in LDS: waves x pods x 192 B)
+  const size_t lds = std::max<size_t>(plain_lds_offsets(P, (d.n_services + 31) / 32, wcap).total,
+                                      (size_t)(pl_nt(P) / 64) * pl_pg((int)P) * sizeof(KsgWinSum));
+  const bool stamp = (d.dbg & 8) != 0 || ((uint32_t)d.dbg & KSG_DBG_RESOLVER_MASK) != 0;
+#define KSG_FUSED_CASE(PP)                                                                                  \
+  if (P == PP)                                                                                              \
+    return stamp ? win_plain_launch_x<PP, true, false, true>(d, wcap, lds, run, sums, x, rng, out, st, f, grid) \
+                 : win_plain_launch_x<PP, false, false, true>(d, wcap, lds, run, sums, x, rng, out, st, f, grid);
+  KSG_FUSED_CASE(1)
+  KSG_FUSED_CASE(2)
+  KSG_FUSED_CASE(4)
+  KSG_FUSED_CASE(8)
+  KSG_FUSED_CASE(16)
+  KSG_FUSED_CASE(32)
+#undef KSG_FUSED_CASE
   return hipErrorInvalidValue;
 }

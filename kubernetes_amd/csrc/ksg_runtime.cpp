@@ -53,6 +53,11 @@ hipError_t ksg_launch_win_t0(const KsgDev& d, uint32_t wcap, const KsgWinRun* ru
 uint32_t ksg_win_t0_stride(const KsgDev& d);
 hipError_t ksg_launch_win_resolve(const KsgDev& d, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
                                   const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st);
+bool ksg_win_fused_ok(const KsgDev& d);
+uint32_t ksg_win_fused_groups(const KsgDev& d, uint32_t wcap);
+hipError_t ksg_launch_win_fused(const KsgDev& d, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
+                                const KsgWinXchg& x, uint64_t* rng, int32_t* out, const KsgFused& f, uint32_t grid,
+                                hipStream_t st);
 uint32_t ksg_win_max_window(const KsgDev& d);
 hipError_t ksg_launch_decide(const KsgDev& d, const ksg_pod* pods, const uint32_t* ids,
                              const uint8_t* records, uint32_t rec_bytes, uint32_t world,
@@ -88,6 +93,11 @@ struct PodRec {
 };
 
 constexpr uint32_t kMaxNodesPerShard = KSG_R_MAX * KSG_NT;
+// the fused window launch's control block: two KsgWinRun slots, then the pod groups'
+// counters uint32[2][kFctlGroups][8] (a window of up to 4 x kFctlGroups pods)
+constexpr uint32_t kFctlGroups = 1024;
+constexpr size_t kFctlRuns = 2 * sizeof(KsgWinRun);
+constexpr size_t kFctlBytes = kFctlRuns + (size_t)2 * kFctlGroups * 8 * sizeof(uint32_t);
 
 // Timing-only events: no system-scope fence when they complete. A default
 // hipEventRecord writes back and invalidates the caches, which costs the
@@ -222,6 +232,12 @@ struct ksg_ctx {
   bool dbg_fail_next = false;      // KSG_DEBUG & 16384: the next window batch fails after its device work
   uint32_t dbg_corrupt = 0;        // KSG_DEBUG bits 22 / 23: corrupt the next COMMIT / BEGIN request's layout
   bool win_d1 = true;              // phase A's single-commit drop bitmaps (KSG_WIN_D1=0: off; ksg_plain.hip)
+  // the fused window launch (KsgFused, ksg_plain.hip): one launch per window on one rank without
+  // ServiceAntiAffinity or extensions (KSG_FUSED=0: phase A, T0 images and resolver apart)
+  bool win_fused = true;
+  uint32_t fused_grid = 0;          // its blocks: one per CU (KSG_FUSED_GRID overrides)
+  uint8_t* d_fctl = nullptr;        // KsgWinRun[2], then the counters uint32[2][groups][8]
+  uint8_t* h_fctl = nullptr;        // pinned: the round's first slot and zeroed counters
   double last_hus[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // host us per phase of the last batch (ksg_last_batch_host_us)
   double totals[24] = {};  // ksg_batch_totals: the per-batch diagnostics summed over batches
   int64_t max_cap = 0, min_cap = 0;
@@ -1274,6 +1290,18 @@ static int create_impl(const ksg_config* cfg, int device, int rank, int world, c
     return bail(rc);
   if ((e = hipHostMalloc((void**)&c->h_run, sizeof(KsgWinRun), hipHostMallocDefault)) != hipSuccess)
     return bail(fail(c, KSG_ERR_HIP, "hipHostMalloc: %s", hipGetErrorString(e)));
+  c->win_fused = !(getenv("KSG_FUSED") && atoi(getenv("KSG_FUSED")) == 0);
+  {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || cus < 16) cus = 0;
+    c->fused_grid = (uint32_t)cus;
+    if (const char* fg = getenv("KSG_FUSED_GRID")) c->fused_grid = (uint32_t)std::min(std::max(atoi(fg), 9), 4096);
+    if (c->fused_grid == 0) c->win_fused = false;
+  }
+  if ((e = hipMalloc((void**)&c->d_fctl, kFctlBytes)) != hipSuccess ||
+      (e = hipHostMalloc((void**)&c->h_fctl, kFctlBytes, hipHostMallocDefault)) != hipSuccess)
+    return bail(fail(c, KSG_ERR_HIP, "fused window control: %s", hipGetErrorString(e)));
+  memset(c->h_fctl, 0, kFctlBytes);
   *out = c;
   return KSG_OK;
 }
@@ -1330,6 +1358,8 @@ int ksg_destroy(ksg_ctx* c) {
   if (c->comm) ncclCommDestroy(c->comm);
   if (c->h_xsend) (void)hipHostFree(c->h_xsend);
   if (c->h_run) (void)hipHostFree(c->h_run);
+  if (c->h_fctl) (void)hipHostFree(c->h_fctl);
+  if (c->d_fctl) (void)hipFree(c->d_fctl);
   if (c->h_up) (void)hipHostFree(c->h_up);
   if (c->h_dn) (void)hipHostFree(c->h_dn);
   if (c->h_map) (void)hipHostFree(c->h_map);
@@ -2184,6 +2214,12 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       if ((rc = grow(c, (void**)&c->d_t0img, &c->t0img_cap, (size_t)W * x.img_stride, 1))) return rc;
       x.img = c->d_t0img;
     }
+    // one launch per window (KsgFused): one rank, no ServiceAntiAffinity, no extensions
+    const uint32_t fgroups = plain && !c->xchg && !dext && c->win_fused && ksg_win_fused_ok(full)
+                                 ? ksg_win_fused_groups(full, W) : 0u;
+    const bool fused = fgroups > 0 && fgroups <= kFctlGroups;
+    KsgWinRun* const fruns = reinterpret_cast<KsgWinRun*>(c->d_fctl);
+    uint32_t* const fcnt = reinterpret_cast<uint32_t*>(c->d_fctl + kFctlRuns);
     uint64_t* wbits = reinterpret_cast<uint64_t*>(c->d_xsend);
     int32_t* wmax = reinterpret_cast<int32_t*>(c->d_xsend + (size_t)W * x.ostride * 8);
     // Windows are chained on the device: each kernel reads the window's start
@@ -2218,14 +2254,29 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       const uint32_t es = std::min(c->ev_stride, K);  // (a short round still times one launch)
       const uint32_t ev_off = es ? c->ev_phase++ % es : 0u;
       *c->h_run = KsgWinRun{pos, n, 0, 0, {0, 0, 0, 0}};
-      HIPCHK(c, hipMemcpyAsync(c->d_run, c->h_run, sizeof(KsgWinRun), hipMemcpyHostToDevice, c->st));
+      if (fused) {  // slot 0 and both counter sets (the launches zero the next set as they go)
+        *reinterpret_cast<KsgWinRun*>(c->h_fctl) = *c->h_run;
+        HIPCHK(c, hipMemcpyAsync(c->d_fctl, c->h_fctl, kFctlRuns + (size_t)2 * fgroups * 8 * sizeof(uint32_t),
+                                 hipMemcpyHostToDevice, c->st));
+      } else {
+        HIPCHK(c, hipMemcpyAsync(c->d_run, c->h_run, sizeof(KsgWinRun), hipMemcpyHostToDevice, c->st));
+      }
       HIPCHK(c, hipEventRecord(c->wev[0], c->st));
       for (uint32_t k = 0; k < K; ++k) {
         // HIP events on this stream around the sampled launches (per-kernel device time)
         const bool evk = es && (k + ev_off) % es == 0;
         // (launch k: events 3k before phase A, 3k+1 after it, 3k+2 before the resolver, 3k+3 =
-        // the next launch's 3(k+1) after it)
+        // the next launch's 3(k+1) after it; the fused launch: 3k before it, 3k+3 after it)
         if (evk && k > 0) HIPCHK(c, hipEventRecord(c->wev[3 * k], c->st));
+        if (fused) {
+          // the counter rows: fgroups per set, set k & 1 (the host zeroed both for launch 0; each
+          // launch's block 0 zeroes the other set for the next launch)
+          KsgFused f{c->d_pods, c->d_ids, fruns + ((k + 1) & 1), fcnt, k & 1u, fgroups};
+          HIPCHK(c, ksg_launch_win_fused(full, W, fruns + (k & 1), c->d_winsum, x, c->d_rng, c->d_out, f,
+                                         c->fused_grid, c->st));
+          if (evk) HIPCHK(c, hipEventRecord(c->wev[3 * k + 3], c->st));
+          continue;
+        }
         if (anti) {
           // ServiceAntiAffinity: the pods' per-domain counts over their filtered nodes first
           // (into d_dcnt, zero: the previous resolver cleared it)
@@ -2255,7 +2306,8 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
         HIPCHK(c, ksg_launch_win_resolve(full, W, c->d_run, c->d_winsum, x, c->d_rng, c->d_out, c->st));
         if (evk) HIPCHK(c, hipEventRecord(c->wev[3 * k + 3], c->st));
       }
-      HIPCHK(c, hipMemcpyAsync(c->h_run, c->d_run, sizeof(KsgWinRun), hipMemcpyDeviceToHost, c->st));
+      HIPCHK(c, hipMemcpyAsync(c->h_run, fused ? fruns + (K & 1) : c->d_run, sizeof(KsgWinRun), hipMemcpyDeviceToHost,
+                               c->st));
       if ((rc = enqueue_tail())) return rc;
       hphase(3);
       if ((rc = overlap_work())) return rc;  // the host mirror catches up while the device works
@@ -2274,9 +2326,13 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       uint32_t nt = 0;
       for (uint32_t k = es ? (es - ev_off) % es : 0u; es && k < K; k += es) {
         float a = 0.f, t0 = 0.f, b = 0.f;
-        HIPCHK(c, hipEventElapsedTime(&a, c->wev[3 * k], c->wev[3 * k + 1]));
-        HIPCHK(c, hipEventElapsedTime(&t0, c->wev[3 * k + 1], c->wev[3 * k + 2]));
-        HIPCHK(c, hipEventElapsedTime(&b, c->wev[3 * k + 2], c->wev[3 * k + 3]));
+        if (fused) {  // (one kernel: its whole time is the resolver's, phase A runs inside it)
+          HIPCHK(c, hipEventElapsedTime(&b, c->wev[3 * k], c->wev[3 * k + 3]));
+        } else {
+          HIPCHK(c, hipEventElapsedTime(&a, c->wev[3 * k], c->wev[3 * k + 1]));
+          HIPCHK(c, hipEventElapsedTime(&t0, c->wev[3 * k + 1], c->wev[3 * k + 2]));
+          HIPCHK(c, hipEventElapsedTime(&b, c->wev[3 * k + 2], c->wev[3 * k + 3]));
+        }
         ea += a;
         et += t0;
         eb += b;
