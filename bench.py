@@ -228,6 +228,10 @@ def main():
     ap.add_argument("--ext-filters-only", action="store_true",
                     help="with --extensions: the filters only (taints, extended resources), TaintToleration and "
                          "BalancedResourceAllocation weights 0")
+    ap.add_argument("--prefix-pods", type=int, default=0,
+                    help="place this many of the workload's first pods (untimed, 5,000-pod batches) before the "
+                         "warm-up, so the timed steps run on the late-run state (fuller nodes, FitErrors); the "
+                         "cpu_baseline legs start from the same state (the prefix's placements added as pods)")
     ap.add_argument("--no-stages", action="store_true",
                     help="skip the resolver's per-stage cycle breakdown (a second, untimed run with KSG_DEBUG=8)")
     args = ap.parse_args()
@@ -236,7 +240,8 @@ def main():
     if world != args.gpus and world > 1:
         raise SystemExit(f"WORLD_SIZE={world} but --gpus={args.gpus}")
     wl = args.workload or ("config2" if world == 1 else "config3")
-    n_pods = (args.warmup + args.steps) * args.batch
+    pre = max(0, args.prefix_pods)
+    n_pods = pre + (args.warmup + args.steps) * args.batch
 
     from kubernetes_amd import ingest, workload
     from kubernetes_amd.engine import DeviceScheduler, PodBatch
@@ -262,8 +267,6 @@ def main():
         rec, ids_x = inter.pod_records(batch.ids, tols, scal)
         batch = PodBatch(batch.pods, ids_x, rec)
         ext = (ecfg.compile(max(len(inter.taints), 1)), node_arrays)
-        if world > 1:
-            raise SystemExit("--extensions runs on one rank")
 
     def load_cluster(s):
         """set_cluster (+ the extensions, which must be enabled before it)."""
@@ -303,11 +306,19 @@ def main():
         sched.set_window(args.window)
     load_cluster(sched)
 
+    def pod_slice(lo, hi):
+        return PodBatch(batch.pods[lo:hi], batch.ids, None if batch.ext is None else batch.ext[lo:hi])
+
     def step_batch(s):
-        sl = slice(s * args.batch, (s + 1) * args.batch)
-        return PodBatch(batch.pods[sl], batch.ids, None if batch.ext is None else batch.ext[sl])
+        return pod_slice(pre + s * args.batch, pre + (s + 1) * args.batch)
 
     rng = workload.TIEBREAK_SEED
+    out_pre = []  # (--prefix-pods) the untimed prefix's placements
+    for lo in range(0, pre, 5000):
+        o, rng = sched.batch(pod_slice(lo, min(pre, lo + 5000)), rng)
+        out_pre.append(o)
+    out_pre = np.concatenate(out_pre) if out_pre else np.zeros(0, np.int32)
+    rng_pre = rng
     outs = []
     for s in range(args.warmup):
         o, rng = sched.batch(step_batch(s), rng)
@@ -470,62 +481,70 @@ def main():
     if not args.no_cpu_baseline and world == 1:
         from oracle.pyoracle import OracleScheduler
 
-        orc = load_cluster(OracleScheduler(cfg, faithful=True))
-        r = workload.TIEBREAK_SEED
+        n_run = n_pods - pre  # (the pods after the prefix: warm-up + timed)
+
+        def cpu_ctx(faithful):
+            """An oracle at the state the GPU's warm-up started from: the prefix's placements
+            added as pods on their nodes (ksg_add_pod's form), in placement order."""
+            o_ = load_cluster(OracleScheduler(cfg, faithful=faithful))
+            for i in np.flatnonzero(out_pre >= 0):
+                o_.add_pod(int(out_pre[i]), batch, int(i))
+            return o_
+
+        orc = cpu_ctx(True)
+        r = rng_pre
         done = 0
         t_c = time.perf_counter()
         chunk = 50
         cpu_out = []
-        while done < n_pods and time.perf_counter() - t_c < args.cpu_seconds:
-            sub = PodBatch(batch.pods[done:done + chunk], batch.ids,
-                           None if batch.ext is None else batch.ext[done:done + chunk])
-            o, r = orc.batch(sub, r)
+        while done < n_run and time.perf_counter() - t_c < args.cpu_seconds:
+            o, r = orc.batch(pod_slice(pre + done, pre + min(n_run, done + chunk)), r)
             cpu_out.append(o)
-            done += len(sub)
+            done += len(o)
         cpu_s = time.perf_counter() - t_c
         cpu_out = np.concatenate(cpu_out)
         agree = bool(np.array_equal(cpu_out, out[:done]))
         # the stronger CPU design point beside it: the same restatement in incremental
         # mode (closed forms over SoA, no per-pod re-list), one thread, a bounded prefix
-        inc = load_cluster(OracleScheduler(cfg, faithful=False))
-        r = workload.TIEBREAK_SEED
+        inc = cpu_ctx(False)
+        r = rng_pre
         done_i = 0
         t_i = time.perf_counter()
-        while done_i < n_pods and time.perf_counter() - t_i < min(args.cpu_seconds, 5.0):
-            o, r = inc.batch(PodBatch(batch.pods[done_i:done_i + 200], batch.ids,
-                                      None if batch.ext is None else batch.ext[done_i:done_i + 200]), r)
+        while done_i < n_run and time.perf_counter() - t_i < min(args.cpu_seconds, 5.0):
+            o, r = inc.batch(pod_slice(pre + done_i, pre + min(n_run, done_i + 200)), r)
             done_i += len(o)
         inc_s = time.perf_counter() - t_i
         inc.close()
         # ... and node-sharded over this process's CPU share (OMP_NUM_THREADS: 16 on the
         # GPU box, whose os.cpu_count() is the whole machine's), SURVEY.md 8(d) "CPU timing" ii
         nthr = max(1, min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
-        mt = load_cluster(OracleScheduler(cfg, faithful=False))
-        r = workload.TIEBREAK_SEED
+        mt = cpu_ctx(False)
+        r = rng_pre
         done_m = 0
         mt_out = [np.zeros(0, np.int32)]
         t_m = time.perf_counter()
         # the whole run's pods (warm-up + timed) when they fit the budget: this leg is also the
         # decision check of every pod the GPU placed, extension records included
-        while done_m < n_pods and time.perf_counter() - t_m < max(args.cpu_seconds, 30.0):
-            o, r = mt.batch_mt(PodBatch(batch.pods[done_m:done_m + 500], batch.ids,
-                                        None if batch.ext is None else batch.ext[done_m:done_m + 500]), r, nthr)
+        while done_m < n_run and time.perf_counter() - t_m < max(args.cpu_seconds, 30.0):
+            o, r = mt.batch_mt(pod_slice(pre + done_m, pre + min(n_run, done_m + 500)), r, nthr)
             mt_out.append(o)
             done_m += len(o)
         mt_s = max(time.perf_counter() - t_m, 1e-9)
-        mt_all = done_m == n_pods and r == rng  # (and the generator state after the last timed step)
+        mt_all = done_m == n_run and r == rng  # (and the generator state after the last timed step)
         mt.close()
         mt_agree = bool(np.array_equal(np.concatenate(mt_out), out[:done_m]))
+        start = (f"from the state after the first {pre} pods (the GPU's placements added)" if pre
+                 else "from an empty cluster")
         cpu = {"value": done / cpu_s, "unit": "pods/s", "cores": 1, "kind": "port",
-               "sample": f"first {done} pods of the same {wl} workload on {n_nodes} nodes from an empty cluster "
+               "sample": f"first {done} pods of the same {wl} workload on {n_nodes} nodes {start} "
                          f"({cpu_s:.1f}s, faithful mode: per-pod MapPodsToMachines regroup, per-node predicate "
                          f"rescans, HostPriorityList sort); decisions identical to GPU: {agree}",
                "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
                "incremental": {"value": done_i / inc_s, "unit": "pods/s", "cores": 1,
-                               "sample": f"first {done_i} pods, incremental mode (SoA closed forms, "
+                               "sample": f"first {done_i} pods {start}, incremental mode (SoA closed forms, "
                                          f"no per-pod re-list), {inc_s:.1f}s"},
                "incremental_nproc": {"value": done_m / mt_s, "unit": "pods/s", "cores": nthr,
-                                     "sample": f"first {done_m} of the run's {n_pods} pods (warm-up + timed), "
+                                     "sample": f"first {done_m} of the run's {n_run} pods (warm-up + timed) {start}, "
                                                f"incremental mode, each pod's node loop split over {nthr} threads "
                                                f"(node-rank shards, two spin barriers per pod; ServiceAntiAffinity "
                                                f"configs run 1 thread), {mt_s:.1f}s; decisions identical to GPU: "
@@ -556,6 +575,8 @@ def main():
                                    " + extensions (taints/tolerations, GPU/FPGA counts, TaintToleration, "
                                    "BalancedResourceAllocation; parity unpinned)") if ext else ""),
                    "nodes": n_nodes, "pods_per_step": args.batch,
+                   "prefix_pods": pre, "placed_in_prefix": int((out_pre >= 0).sum()),
+                   "timed_pods": [pre + args.warmup * args.batch, n_pods],
                    "placed_in_timed": int((timed >= 0).sum()), "fit_errors_in_timed": int((timed == -1).sum()),
                    "snapshots_in_timed": wstats,
                    "exchange": None if world == 1 else args.transport,

@@ -280,6 +280,23 @@ int ksg_schedule_batch_draws(ksg_ctx* ctx, const ksg_pod* pods, uint32_t n, cons
                              uint32_t n_ids, const uint64_t* draws, uint32_t n_draws, uint32_t* draws_used,
                              int32_t* out_nodes);
 
+/* Bind rejected in batch mode. The reference binds each pod before it schedules
+ * the next: a rejected Bind means no AssumePod for that pod, but its rand.Int()
+ * was already drawn (plugin/pkg/scheduler/scheduler.go:93-118,
+ * pkg/scheduler/generic_scheduler.go:94). A batch committed every placement on
+ * the device, so when the caller binds pods[0..n) of the last batch in order and
+ * pod k's Bind (out_nodes[k] >= 0) is rejected, this call undoes the commits of
+ * pods k..n-1 (newest first), leaving the state of pods 0..k-1 committed.
+ * *draws_kept = the draws pods 0..k consumed (pod k's stays consumed): with
+ * ksg_schedule_batch_draws the caller puts draws[*draws_kept .. draws_used) back
+ * at the front of its FIFO; rng_state (optional, ksg_schedule_batch's splitmix64
+ * state) is stepped back over the draws of pods k+1..n-1. The caller then
+ * re-batches pods k+1..n-1. pods / out_nodes are the last batch's arrays; every
+ * rank of a sharded context makes the same call. KSG_ERR_ARG (nothing changed)
+ * when k >= n, pod k found no node, or a placed pod's uid is not committed. */
+int ksg_batch_unwind(ksg_ctx* ctx, const ksg_pod* pods, const int32_t* out_nodes, uint32_t n, uint32_t k,
+                     uint64_t* rng_state, uint32_t* draws_kept);
+
 /* Introspection (HostPriorityList): per-node fail code and combined score for
  * a pod, without committing. score_out[i] is meaningful where fail_out[i]==0. */
 int ksg_evaluate(ksg_ctx* ctx, const ksg_pod* pod, const uint32_t* ids,
@@ -305,10 +322,13 @@ int ksg_last_batch_stats(ksg_ctx* ctx, uint32_t* stats4);
 int ksg_last_batch_ms(ksg_ctx* ctx, double* ms);
 
 /* Window path of the last ksg_schedule_batch: out3[0] = device ms in the
- * snapshot-scoring kernel(s) (ksg_win_score_kernel, and its count pass; not the
+ * snapshot-scoring kernel(s) (ksg_win_score_kernel, its count passes and, on a
+ * sharded context, the count passes' all-reduces; not the all-gather or the
  * T0-image kernel: ksg_batch_totals [18]), out3[1] = device ms in the
  * resolver (ksg_win_plain_kernel, or with ServiceAntiAffinity
- * ksg_win_resolve2_kernel / ksg_win_resolve_kernel), out3[2] = resolver launches (windows are
+ * ksg_win_resolve2_kernel / ksg_win_resolve_kernel; the fused window launch of
+ * one plain rank scores the window inside the resolver's launch, so its whole
+ * time is here and out3[0] is 0), out3[2] = resolver launches (windows are
  * chained on the device, so a round may end with launches that find the batch
  * done and return at once); from HIP events recorded on the context's stream
  * around every 4th launch of a round, the sampled positions rotating from round
@@ -334,8 +354,8 @@ int ksg_last_batch_host_us(ksg_ctx* ctx, double* out8);
  * ksg_last_batch_stats, [9..16] ksg_last_batch_host_us, [17] the window
  * capacity (pods phase A scores per launch) summed over the window-path
  * launches, [18] device ms between phase A and the resolver (the sharded
- * exchange and the T0-image kernel, ksg_win_t0_kernel; sampled like
- * ksg_last_batch_kernel_ms), [19..23] zero. */
+ * all-gather and the T0-image kernel, ksg_win_t0_kernel; the count passes'
+ * all-reduces are in [2]; sampled like ksg_last_batch_kernel_ms), [19..23] zero. */
 int ksg_batch_totals(ksg_ctx* ctx, double* out24);
 
 /* Diagnostics: the window resolver's per-stage clock counters (s_memtime

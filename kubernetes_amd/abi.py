@@ -200,6 +200,7 @@ EXPORTS = [
     "ksg_serve_stats",
     "ksg_set_static_terms",
     "ksg_schedule_batch_draws",
+    "ksg_batch_unwind",
     "ksg_shard",
     "ksg_read_requested",
     "ksg_shard_range",
@@ -269,6 +270,7 @@ def load_library() -> C.CDLL:
         "ksg_serve_stats": (C.c_int, [vp, vp]),
         "ksg_set_static_terms": (C.c_int, [vp, vp, vp, C.c_int]),
         "ksg_schedule_batch_draws": (C.c_int, [vp, vp, U32, vp, U32, vp, U32, P(U32), vp]),
+        "ksg_batch_unwind": (C.c_int, [vp, vp, vp, U32, U32, vp, P(U32)]),
         "ksg_shard": (C.c_int, [vp, P(U32), P(U32)]),
         "ksg_read_requested": (C.c_int, [vp, vp, vp]),
         "ksg_shard_range": (C.c_int, [U32, C.c_int, C.c_int, P(U32), P(U32)]),

@@ -2775,6 +2775,37 @@ int ksg_schedule_batch_draws(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const 
   return rc;
 }
 
+// A rejected Bind in batch mode (scheduler.go:107-112: no AssumePod for pod k, its rand.Int()
+// already drawn at generic_scheduler.go:94, pod k + 1 scheduled against the state without it).
+// The batch committed pods 0..n-1 in order, so undoing the commits of pods n-1 down to k leaves
+// exactly the state after pods 0..k-1; pods k+1..n-1 are then re-batched by the caller with the
+// draws they had consumed put back (a splitmix64 state is stepped back over them instead).
+int ksg_batch_unwind(ksg_ctx* c, const ksg_pod* pods, const int32_t* out_nodes, uint32_t n, uint32_t k,
+                     uint64_t* rng_state, uint32_t* draws_kept) {
+  if (!c || !pods || !out_nodes || !draws_kept || k >= n) return KSG_ERR_ARG;
+  KSG_LOCK(c);
+  if (c->pending) return fail(c, KSG_ERR_STATE, "schedule_begin pending");
+  if (out_nodes[k] < 0) return fail(c, KSG_ERR_ARG, "pod %u found no node: there was no Bind to reject", k);
+  if (int rs = cluster_ok(c)) return rs;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (int rc0 = flush_deferred(c)) return rc0;  // (the batch's commits into the host mirror)
+  // (validate every uid before removing any: a failed call changes nothing)
+  for (uint32_t i = k; i < n; ++i)
+    if (out_nodes[i] >= 0 && !c->pods.count(pods[i].uid))
+      return fail(c, KSG_ERR_ARG, "pod %u (uid %llu) is not a committed pod of this context", i,
+                  (unsigned long long)pods[i].uid);
+  uint32_t kept = 0, back = 0;
+  for (uint32_t i = 0; i <= k; ++i) kept += out_nodes[i] >= 0 ? 1u : 0u;
+  for (uint32_t i = n; i-- > k;) {  // newest first
+    if (out_nodes[i] < 0) continue;
+    if (i > k) ++back;
+    if (int rc = remove_pod_impl(c, pods[i].uid)) return rc;
+  }
+  if (rng_state) *rng_state -= (uint64_t)back * ksg_rng_step(nullptr);
+  *draws_kept = kept;
+  return flush_patches(c);
+}
+
 int ksg_schedule_batch_ext(ksg_ctx* c, const ksg_pod* pods, const ksg_pod_ext* ext, uint32_t n, const uint32_t* ids,
                            uint32_t n_ids, uint64_t* rng_state, int32_t* out_nodes) {
   if (!c || (n && (!pods || !out_nodes)) || !rng_state) return KSG_ERR_ARG;

@@ -796,7 +796,8 @@ __global__ __launch_bounds__(KSG_GSRV_NT) void ksg_serve_grid_kernel(KsgDev d, K
           cnt[j] = need_cnt ? ld_mut(d.svc_cnt + (size_t)p.service * d.n_nodes + nn[j]) : 0;
         PodCtx c;
         pod_resolve(d, p, ids, c);
-        // (extensions: the filters and BalancedAllocation; the host keeps TaintToleration off this server)
+        // (extensions: the filters, BalancedAllocation and TaintToleration, whose normalisation max
+        // is exchanged across the scan workgroups through grid->tmx)
         c.ext = (EXT && (s_req[KSG_SRVH_FLAGS] & KSG_SRVF_EXT))
                     ? reinterpret_cast<const ksg_pod_ext*>(pay + s_req[KSG_SRVH_EXT_AT])
                     : nullptr;

@@ -242,6 +242,21 @@ class DeviceScheduler:
             self._err(rc)
         return out[:n], int(used.value)
 
+    def batch_unwind(self, batch: PodBatch, out, k: int, rng_state=None):
+        """ksg_batch_unwind: pod k's Bind was rejected (scheduler.go:107-112). Undoes the
+        commits of pods k..n-1 of the last batch; -> (draws pods 0..k consumed, the
+        rng_state stepped back over pods k+1..n-1's draws, or None)."""
+        n = len(batch)
+        pods = np.ascontiguousarray(batch.pods, dtype=abi.POD_DTYPE)
+        o = np.ascontiguousarray(out, dtype=np.int32)
+        kept = C.c_uint32(0)
+        st = C.c_uint64(0 if rng_state is None else int(rng_state))
+        rc = self._lib.ksg_batch_unwind(self._ctx, abi.ptr(pods), abi.ptr(o), n, int(k),
+                                        None if rng_state is None else C.byref(st), C.byref(kept))
+        if rc != abi.KSG_OK:
+            self._err(rc)
+        return int(kept.value), (None if rng_state is None else st.value)
+
     def evaluate(self, batch: PodBatch, i: int = 0):
         """Per-node (fail code, combined score) of the shard, no commit."""
         pod = np.ascontiguousarray(batch.pods[i : i + 1])

@@ -138,6 +138,15 @@ def build(family: str, nn: int, npods: int, seed: int = 7) -> workload.Workload:
                                               ("region", 2)))]
         cfg = _policy(_DEFAULT_PREDS, [{"name": "LeastRequestedPriority", "weight": 1},
                                        {"name": "ServiceSpreadingPriority", "weight": 1}] + anti, "ma")
+    elif family == "four_anti":
+        # four ServiceAntiAffinity priorities over 50 label domains (8 + 2 + 32 + 8): within
+        # the grid drop-in server's 64, with priorities past its register-held two
+        pods = workload.make_pods(npods, rng, n_apps=6)
+        services = workload.make_services(6)
+        anti = [{"name": f"Anti{i}-{lab}", "weight": w, "argument": {"serviceAntiAffinity": {"label": lab}}}
+                for i, (lab, w) in enumerate((("zone", 1), ("region", 2), ("rack", 1), ("zone", 3)))]
+        cfg = _policy(_DEFAULT_PREDS, [{"name": "LeastRequestedPriority", "weight": 1},
+                                       {"name": "ServiceSpreadingPriority", "weight": 1}] + anti, "fa")
     elif family == "existing_hosts":
         pods = workload.make_pods(npods + npods // 3, rng, n_apps=4)
         services = workload.make_services(4)

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 from kubernetes_amd import abi
-from kubernetes_amd.engine import DeviceScheduler
+from kubernetes_amd.engine import DeviceScheduler, PodBatch
 from oracle.pyoracle import OracleScheduler
 from tests.helpers import Case
 
@@ -53,5 +53,82 @@ def test_caller_draws_rejects_short_or_negative_lists():
             dev.batch_draws(case.batch, np.zeros(5, np.uint64))  # fewer values than pods
         with pytest.raises(Exception):
             dev.batch_draws(case.batch, np.full(20, 1 << 63, np.uint64))  # not rand.Int() values
+    finally:
+        dev.close()
+
+
+def _slice(b: PodBatch, lo: int, hi: int) -> PodBatch:
+    return PodBatch(b.pods[lo:hi].copy(), b.ids, None if b.ext is None else b.ext[lo:hi].copy())
+
+
+@pytest.mark.parametrize("name,nn,window", [("config2", 3000, None), ("config4", 900, None), ("config2", 1200, 0)])
+def test_batch_bind_rejection_matches_sequential(name, nn, window):
+    """A 1,000-pod batch whose pod k's Bind is rejected (scheduler.go:107-112): ksg_batch_unwind
+    undoes pods k..n-1, pods k+1..n-1 are re-batched with the draws they had used put back. The
+    placements and the final state equal the C restatement's begin / commit pod by pod with pod
+    k's commit skipped (its begin abandoned) and its draw consumed (generic_scheduler.go:94)."""
+    n = 1000
+    case = Case(name, nn, n)
+    draws = np.random.default_rng(nn + 1).integers(0, 1 << 63, size=2 * n, dtype=np.uint64)
+    dev = DeviceScheduler(case.cfg, device=0)
+    orc = OracleScheduler(case.cfg)
+    try:
+        if window is not None:
+            dev.set_window(window)
+        dev.set_cluster(case.view.arrays)
+        orc.set_cluster(case.view.arrays)
+        out, used = dev.batch_draws(case.batch, draws)
+        if window is None:
+            assert dev.last_batch_windows() > 0
+        placed = np.flatnonzero(out >= 0)
+        k = int(placed[len(placed) // 3])  # a placed pod well inside the batch
+        kept, _ = dev.batch_unwind(case.batch, out, k)
+        assert kept == int(np.count_nonzero(out[: k + 1] >= 0))
+        out2, used2 = dev.batch_draws(_slice(case.batch, k + 1, n), draws[kept:])
+        got = np.concatenate([out[: k + 1], out2])
+        k_used = 0
+        for i in range(n):
+            rc, _, ties, _ = orc.begin(case.batch, i, want_fail=False)
+            if rc != abi.KSG_OK:
+                assert got[i] < 0, f"pod {i}: {got[i]}"
+                continue
+            r = int(draws[k_used])
+            k_used += 1
+            if i == k:
+                continue  # Bind rejected: no AssumePod, the draw stays consumed
+            assert got[i] == orc.commit(r % ties), f"pod {i}"
+        assert kept + used2 == k_used
+        gc, gm = dev.read_requested()
+        wc, wm = orc.read_requested()
+        assert np.array_equal(gc, wc) and np.array_equal(gm, wm)
+    finally:
+        dev.close()
+
+
+def test_batch_bind_rejection_splitmix_state():
+    """The splitmix64 form: the state comes back stepped over pods k+1..n-1's draws, so the
+    re-batch equals the oracle's batch of pods 0..k-1, one draw for pod k, then pods k+1..n-1."""
+    n = 600
+    case = Case("config2", 2000, n)
+    dev = DeviceScheduler(case.cfg, device=0)
+    orc = OracleScheduler(case.cfg)
+    try:
+        dev.set_cluster(case.view.arrays)
+        orc.set_cluster(case.view.arrays)
+        seed = 0x1234_5678_9ABC
+        out, st = dev.batch(case.batch, seed)
+        k = int(np.flatnonzero(out >= 0)[n // 2])
+        kept, st_k = dev.batch_unwind(case.batch, out, k, rng_state=st)
+        out2, st2 = dev.batch(_slice(case.batch, k + 1, n), st_k)
+        w1, s1 = orc.batch(_slice(case.batch, 0, k), seed)
+        assert np.array_equal(out[:k], w1)
+        assert kept == int(np.count_nonzero(w1 >= 0)) + 1
+        w2, s2 = orc.batch(_slice(case.batch, k + 1, n), s1 + 0x9E3779B97F4A7C15 & (2**64 - 1))
+        assert np.array_equal(out2, w2) and st2 == s2
+        gc, gm = dev.read_requested()
+        wc, wm = orc.read_requested()
+        assert np.array_equal(gc, wc) and np.array_equal(gm, wm)
+        with pytest.raises(Exception):  # pod k is no longer committed: a second unwind is refused
+            dev.batch_unwind(case.batch, out, k)
     finally:
         dev.close()

@@ -102,6 +102,31 @@ def test_serve_begin_commit_matches_oracle(name, nn, npods, grid, monkeypatch):
     dev.close()
 
 
+@pytest.mark.parametrize("family,nn,npods,grid", [
+    ("four_anti", 900, 300, True),   # 50 domains: the grid server, anti priorities past its two in registers
+    ("four_anti", 3000, 200, True),  # (12 scan workgroups)
+    ("many_anti", 900, 300, False),  # 84 domains > KSG_GSRV_MAXD: the one-workgroup server instead
+])
+def test_serve_anti_priorities_grid_or_fallback(family, nn, npods, grid, monkeypatch):
+    """Several ServiceAntiAffinity priorities through begin / commit with the grid server
+    asked for: up to KSG_GSRV_MAXD label domains it serves them, the
+    priorities past KSG_GSRV_ANTI_REG loading their domains from HBM (ksg_serve.hip); past
+    that many domains srv_grid() falls back to the one-workgroup server. Both match the oracle."""
+    from tests.families import FamilyCase
+
+    monkeypatch.setenv("KSG_SERVE_GRID", "1")
+    case = FamilyCase(family, nn, npods)
+    dev = DeviceScheduler(case.cfg, device=0)
+    orc = OracleScheduler(case.cfg)
+    dev.set_cluster(case.view.arrays)
+    orc.set_cluster(case.view.arrays)
+    _drive(case, dev, orc, seed=nn + 3, n_pods=npods, churn=0.05)
+    st = dev.serve_stats()
+    assert st["eligible"] and st["requests"] >= npods, st
+    assert st["grid"] == grid, st
+    dev.close()
+
+
 @pytest.mark.parametrize("name,nn,npods", [("config2", 1500, 400), ("config4", 700, 300), ("config2", 3000, 300)])
 def test_serve_interleaved_with_add_remove_evaluate_batch(name, nn, npods):
     """Mirror patches through the server, and evaluate / batch taking the stream."""
