@@ -111,6 +111,7 @@ def test_window_path_with_extension_filters_matches_oracle(name, nn, npods, kw, 
     (300, dict(w_taint=0, w_bal=3), False),   # filters + BalancedAllocation
     (3000, dict(w_taint=0, w_bal=0), False),
     (2000, dict(w_taint=0, w_bal=2), True),   # ... at 4 nodes per thread
+    (30000, dict(), False),                   # TaintToleration past 16,384 nodes: 30 scan workgroups of 1,024
 ])
 def test_begin_commit_evaluate_remove_with_extensions(nn, kw, npt4, monkeypatch):
     monkeypatch.setenv("KSG_SERVE_GRID_EXT", "1")

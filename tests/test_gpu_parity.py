@@ -213,21 +213,27 @@ def test_kernel_time_sampling_strides(monkeypatch):
     nothing. The decisions never depend on it."""
     case = Case("config2", 600, 400)
     res = {}
-    for stride in ("1", "4", "0"):
+    # (default: the fused window launch, phase A inside the resolver's launch, so eval_ms is 0;
+    # KSG_FUSED=0: phase A launched and timed apart)
+    for stride, fused in (("1", "1"), ("4", "1"), ("0", "1"), ("1", "0"), ("4", "0")):
         monkeypatch.setenv("KSG_KERNEL_EVENTS", stride)
+        monkeypatch.setenv("KSG_FUSED", fused)
         dev, orc = _pair(case, 128)
         got, sg = run_batch(dev, case)
-        res[stride] = (got, sg, dev.last_batch_kernel_ms())
+        res[stride + fused] = (got, sg, dev.last_batch_kernel_ms())
         dev.close()
-    assert all(np.array_equal(res["1"][0], r[0]) and res["1"][1] == r[1] for r in res.values())
-    for stride in ("1", "4"):
-        k = res[stride][2]
-        assert k["launches"] > 0 and k["resolve_ms"] > 0 and k["eval_ms"] > 0
-    assert res["0"][2]["resolve_ms"] == 0 and res["0"][2]["launches"] > 0
+    assert all(np.array_equal(res["11"][0], r[0]) and res["11"][1] == r[1] for r in res.values())
+    for key in ("11", "41", "10", "40"):
+        k = res[key][2]
+        assert k["launches"] > 0 and k["resolve_ms"] > 0
+        assert (k["eval_ms"] > 0) == (key[1] == "0"), (key, k)
+    assert res["01"][2]["resolve_ms"] == 0 and res["01"][2]["launches"] > 0
 
 
-def test_batch_totals_sum_the_per_batch_diagnostics():
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_batch_totals_sum_the_per_batch_diagnostics(fused, monkeypatch):
     """ksg_batch_totals = the per-batch diagnostics summed over batches."""
+    monkeypatch.setenv("KSG_FUSED", fused)
     case = Case("config2", 500, 300)
     dev, _ = _pair(case, 128)
     dev.set_cluster(case.view.arrays)
@@ -243,8 +249,12 @@ def test_batch_totals_sum_the_per_batch_diagnostics():
     assert t1["batches"] == 2 and win == t1["windows"] > 0
     assert abs(t1["device_ms"] - dms) < 1e-9 and abs(t1["resolve_ms"] - res) < 1e-9
     assert t1["host_us"]["validate"] > 0
-    # phase A, the T0-image kernel and the resolver are timed apart (every 4th launch sampled)
-    assert t1["eval_ms"] > 0 and t1["t0_ms"] > 0 and t1["resolve_ms"] > 0
+    # phase A, the T0-image kernel and the resolver are timed apart (every 4th launch sampled);
+    # the fused window launch (the default on one plain rank) is one kernel: all resolver time
+    if fused == "0":
+        assert t1["eval_ms"] > 0 and t1["t0_ms"] > 0 and t1["resolve_ms"] > 0
+    else:
+        assert t1["eval_ms"] == 0 and t1["t0_ms"] == 0 and t1["resolve_ms"] > 0
     dev.close()
 
 
