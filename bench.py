@@ -200,6 +200,12 @@ def _stage_breakdown(cfg, view, args, step_batch, anti, ext=None):
         out["window_start_us"] = {"windows": int(nwin),
                                   "to_first_group_scored": round(float(c[52]) / 64 / nwin / 100, 2),
                                   "to_first_entry_staged": round(float(c[53]) / 64 / nwin / 100, 2)}
+        ntask = float(c[61]) / 64
+        if ntask > 0:  # the first scoring task's timeline from block 0's start (us, per window)
+            out["window_start_us"]["first_task"] = {
+                k_: round(float(c[i]) / 64 / ntask / 100, 2)
+                for i, k_ in ((56, "block_start"), (57, "task_start"), (58, "scored"), (59, "drained"),
+                              (60, "counted"))}
     return out
 
 

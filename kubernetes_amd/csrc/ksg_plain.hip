@@ -348,10 +348,12 @@ __device__ KSG_FUSED_TASK_ATTR void fused_score_task(const KsgDev& d, const KsgF
                                                       nullptr, nullptr, rec_lds);
 }
 
-template <int P>
+template <int P, bool STAMP>
 __device__ __forceinline__ void fused_score_blocks(const KsgDev& d, uint32_t wcap, const KsgWinRun* run,
                                                    const KsgWinSum* sums_c, const KsgWinXchg& x, const KsgFused& f,
                                                    char* smem) {
+  // (KSG_DEBUG & 8: the first task's timeline in 10-ns ticks from block 0's start, dbgbuf[55])
+  const uint32_t t_b0 = STAMP ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
   constexpr uint32_t NWV = pl_nt(P) / 64;
   constexpr int PGF = pl_pg(P);
   const uint32_t pos = run->pos, n_batch = run->n;
@@ -372,12 +374,30 @@ __device__ __forceinline__ void fused_score_blocks(const KsgDev& d, uint32_t wca
   for (uint32_t t = ix; t < nwx * ngrp; t += nbx) {
     const uint32_t g = t / nwx, wgp = wg0 + (t - g * nwx);
     const uint32_t w = __builtin_amdgcn_readfirstlane(wgp * NWV + wave);
+    const uint32_t t_k0 = STAMP ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
     fused_score_task<P>(d, f, pos, n_batch, wcap, w, g * PGF, sums, wbits, wmax, x.ostride, wd1, rec_lds);
+    const uint32_t t_k1 = STAMP ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
     drain_stores();  // (every storing wave: its write-through stores have landed)
     __syncthreads();
-    if (threadIdx.x == 0)
+    const uint32_t t_k2 = STAMP ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
+    if (threadIdx.x == 0) {
       __hip_atomic_fetch_add(f.cnt + ((size_t)f.set * f.ngroups + g) * 8u + xs, 1u, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
+      if constexpr (STAMP) {
+        // the first task (group 0, word group 0): block start, task start, scored (wave 0), drained
+        // and barrier, counter added, each from block 0's start (dbgbuf[55], written by block 0)
+        if (t == ix && g == 0 && wgp == 0 && d.dbgbuf) {
+          const uint32_t t_k3 = (uint32_t)__builtin_amdgcn_s_memrealtime();
+          const uint32_t base = (uint32_t)__hip_atomic_load(d.dbgbuf + 55, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          atomicAdd(d.dbgbuf + 56, (int32_t)(t_b0 - base));
+          atomicAdd(d.dbgbuf + 57, (int32_t)(t_k0 - base));
+          atomicAdd(d.dbgbuf + 58, (int32_t)(t_k1 - base));
+          atomicAdd(d.dbgbuf + 59, (int32_t)(t_k2 - base));
+          atomicAdd(d.dbgbuf + 60, (int32_t)(t_k3 - base));
+          atomicAdd(d.dbgbuf + 61, 1);
+        }
+      }
+    }
   }
 }
 
@@ -400,9 +420,12 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if constexpr (FUSED) {
     if (blockIdx.x != 0) {
-      fused_score_blocks<P>(d, wcap, run, sums, x, f, smem);
+      fused_score_blocks<P, STAMP>(d, wcap, run, sums, x, f, smem);
       return;
     }
+    if (STAMP && threadIdx.x == 0 && d.dbgbuf)  // (block 0's start for the scoring blocks' stamps)
+      __hip_atomic_store(d.dbgbuf + 55, (int32_t)(uint32_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
   }
   // (the fused launch: the window's outcome goes into the next launch's slot)
   KsgWinRun* const run_out = FUSED ? f.run_out : run;

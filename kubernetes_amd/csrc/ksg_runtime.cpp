@@ -236,6 +236,10 @@ struct ksg_ctx {
   // ServiceAntiAffinity or extensions (KSG_FUSED=0: phase A, T0 images and resolver apart)
   bool win_fused = true;
   uint32_t fused_grid = 0;          // its blocks: one per CU (KSG_FUSED_GRID overrides)
+  // ... up to this many 64-node words per shard (KSG_FUSED_MAX_WORDS): past them the scoring blocks,
+  // one per CU under the resolver's LDS, are too few waves to hide phase A's load latency (config 5,
+  // 100k nodes, same box: 255k fused against 385k apart)
+  uint32_t fused_max_words = 512;
   uint8_t* d_fctl = nullptr;        // KsgWinRun[2], then the counters uint32[2][groups][8]
   uint8_t* h_fctl = nullptr;        // pinned: the round's first slot and zeroed counters
   double last_hus[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // host us per phase of the last batch (ksg_last_batch_host_us)
@@ -1297,6 +1301,7 @@ static int create_impl(const ksg_config* cfg, int device, int rank, int world, c
     c->fused_grid = (uint32_t)cus;
     if (const char* fg = getenv("KSG_FUSED_GRID")) c->fused_grid = (uint32_t)std::min(std::max(atoi(fg), 9), 4096);
     if (c->fused_grid == 0) c->win_fused = false;
+    if (const char* fw = getenv("KSG_FUSED_MAX_WORDS")) c->fused_max_words = (uint32_t)std::max(atoi(fw), 0);
   }
   if ((e = hipMalloc((void**)&c->d_fctl, kFctlBytes)) != hipSuccess ||
       (e = hipHostMalloc((void**)&c->h_fctl, kFctlBytes, hipHostMallocDefault)) != hipSuccess)
@@ -2215,7 +2220,8 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
       x.img = c->d_t0img;
     }
     // one launch per window (KsgFused): one rank, no ServiceAntiAffinity, no extensions
-    const uint32_t fgroups = plain && !c->xchg && !dext && c->win_fused && ksg_win_fused_ok(full)
+    const uint32_t fgroups = plain && !c->xchg && !dext && c->win_fused && full.nwords <= c->fused_max_words &&
+                                     ksg_win_fused_ok(full)
                                  ? ksg_win_fused_groups(full, W) : 0u;
     const bool fused = fgroups > 0 && fgroups <= kFctlGroups;
     KsgWinRun* const fruns = reinterpret_cast<KsgWinRun*>(c->d_fctl);

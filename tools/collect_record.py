@@ -1,8 +1,8 @@
-"""Fold one record run (tools/gpu_r5_record.sh <tag> prof / bench / sq, tools/gpu_r5_dropin.sh) from
+"""Fold one record run (tools/gpu_record.sh <tag> prof / bench / sq, tools/gpu_dropin.sh) from
 gpurun_out/ into profiles/: the PMC passes into profiles/traffic.json (round and source sha
 tags, tools/traffic_from_pmc.py), the bench lines, kernel-trace stats, SQ fractions
 (tools/sq_summary.py) and drop-in records under profiles/<round>_*; prints the table rows.
-usage: python tools/collect_record.py <tag> [round=r5]"""
+usage: python tools/collect_record.py <tag> [round=r6]"""
 import glob
 import json
 import os
@@ -20,7 +20,7 @@ def last_json(path):
     return json.loads(open(path).read().strip().splitlines()[-1])
 
 
-def main(tag, rnd="r5"):
+def main(tag, rnd="r6"):
     env = dict(os.environ, KSG_ROUND=rnd)
     for wl in WLS:
         d = os.path.join(OUT, f"prof_{tag}_{wl}")

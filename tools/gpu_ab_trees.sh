@@ -1,6 +1,6 @@
 # Same-box A/B of whole trees (tools/build_tree.sh): the current tree against _ab/<name> trees,
 # interleaved (rep x workload x tree), each bench line without CPU baseline or stage rerun.
-# usage: REPS=2 WLS="config5 config3" tools/gpu_r6_ab_trees.sh <tag> <name>...
+# usage: REPS=2 WLS="config5 config3" tools/gpu_ab_trees.sh <tag> <name>...
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 TAG=$1; shift

@@ -1,6 +1,6 @@
-# Round-5: drop-in per-pod latency from C (ksg_schedule_begin + ksg_schedule_commit) for the given
+drop-in per-pod latency from C (ksg_schedule_begin + ksg_schedule_commit) for the given
 # tools/bin/dropin_latency argument sets ("nodes pods warmup want_fail ext policy"), one JSON line
-# each into gpurun_out/<tag>_dropin.jsonl. usage: tools/gpu_r5_dropin.sh <tag> "<args>" ...
+# each into gpurun_out/<tag>_dropin.jsonl. usage: tools/gpu_dropin.sh <tag> "<args>" ...
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 TAG=$1; shift

@@ -1,6 +1,6 @@
-# Round-6 quick check on the GPU box: selected -m gpu tests (pytest -k expression in $K, files
+# Quick check on the GPU box: selected -m gpu tests (pytest -k expression in $K, files
 # in $FILES), then the default bench (config 2 unless BENCH_ARGS) under each ENV spec given.
-# usage: K='expr' FILES='tests/x.py ...' tools/gpu_r6_quick.sh <tag> [name:VAR=val[,VAR=val] ...]
+# usage: K='expr' FILES='tests/x.py ...' tools/gpu_quick.sh <tag> [name:VAR=val[,VAR=val] ...]
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 TAG=${1:-r6q}; shift

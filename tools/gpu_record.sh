@@ -1,9 +1,9 @@
-# Round-5 record run on the GPU box, in steps (each GPU step under its own time limit; the
-# first failure ends the script). usage: tools/gpu_r5_record.sh <tag> <step> [args]
+# Record run on the GPU box, in steps (each GPU step under its own time limit; the
+# first failure ends the script). usage: KSG_ROUND=r6 tools/gpu_record.sh <tag> <step> [args]
 #   tests                 pytest -m gpu (every GPU test) and __graft_entry__.smoke()
 #   bench <wl> [args]     one bench.py line (default shape, CPU baseline included) -> <tag>_bench_<wl>.json
 #   prof <wl> [args]      rocprofv3 kernel-trace stats, then one PMC pass each for FETCH_SIZE and
-#                         WRITE_SIZE, folded into profiles/traffic.json (KSG_ROUND=r5, the sources' sha)
+#                         WRITE_SIZE, folded into profiles/traffic.json (KSG_ROUND, default r6; the sources' sha)
 #   sq <wl>               one PMC pass of 8 SQ counters (busy / issue / wait fractions)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -45,7 +45,7 @@ PY
       || { tail $OUT/bench_write.err; exit 1; }
     NN=$(python3 -c "import json,sys; print(json.loads(open('$OUT/bench_kt.json').read().strip().splitlines()[-1])['config']['nodes'])")
     mv $OUT/fetch/*/run_counter_collection.csv $OUT/fetch/ 2>/dev/null; mv $OUT/write/*/run_counter_collection.csv $OUT/write/ 2>/dev/null
-    KSG_ROUND=r5 python3 tools/traffic_from_pmc.py $OUT $WL $NN profiles/traffic.json && cp profiles/traffic.json gpurun_out/${TAG}_traffic.json
+    KSG_ROUND=${KSG_ROUND:-r6} python3 tools/traffic_from_pmc.py $OUT $WL $NN profiles/traffic.json && cp profiles/traffic.json gpurun_out/${TAG}_traffic.json
     python3 - $OUT <<'PY'
 import csv, glob, sys
 f = sorted(glob.glob(sys.argv[1] + "/kt/**/*kernel_stats.csv", recursive=True))

@@ -1,9 +1,9 @@
-# Round-6 GPU call in steps (each its own time limit; the first failure ends the call):
+# GPU call in steps (each its own time limit; the first failure ends the call):
 #   tests <k-expr> <files...>  : selected -m gpu tests
 #   kt <tag> [bench args]      : rocprofv3 kernel + memory-copy trace of one bench run (no PMC)
-#   ab <tag> <trees...>        : same-box tree A/B (tools/gpu_r6_ab_trees.sh; REPS / WLS env)
+#   ab <tag> <trees...>        : same-box tree A/B (tools/gpu_ab_trees.sh; REPS / WLS env)
 #   bench <tag> [bench args]   : one bench line (with CPU baselines and stages)
-# usage: tools/gpu_r6_run.sh "<step>" "<step>" ...
+# usage: tools/gpu_run.sh "<step>" "<step>" ...
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -26,7 +26,7 @@ for step in "$@"; do
       echo "kt $tag done" ;;
     ab)
       tag=$1; shift
-      bash tools/gpu_r6_ab_trees.sh $tag "$@" || exit 1 ;;
+      bash tools/gpu_ab_trees.sh $tag "$@" || exit 1 ;;
     bench)
       tag=$1; shift
       timeout -k 10 400 python bench.py "$@" > gpurun_out/bench_$tag.json 2> gpurun_out/bench_$tag.err \

@@ -1,4 +1,4 @@
-"""Fold one rocprofv3 SQ counter pass (tools/gpu_r5_record.sh sq) into per-kernel fractions.
+"""Fold one rocprofv3 SQ counter pass (tools/gpu_record.sh sq) into per-kernel fractions.
 
 Each dispatch's counters are summed per kernel; the fractions are of SQ_WAVE_CYCLES (the
 wave-resident quad-cycles; ACTIVE_INST_ANY + WAIT_ANY + WAIT_INST_ANY ~ WAVE_CYCLES, disjoint,
