@@ -284,6 +284,11 @@ def main():
                     help="skip the resolver's per-stage cycle breakdown (a second, untimed run with KSG_DEBUG=8)")
     args = ap.parse_args()
 
+    # HIP events around every 8th window launch (the library's default is every 4th): each event
+    # record between two dependent launches adds ~4.5 us to the gap between them (kernel trace:
+    # 0 us between launches without one), so the sampled kernel times cost the timed region
+    # ~0.7 % instead of ~1.5 %; KSG_KERNEL_EVENTS in the environment overrides
+    os.environ.setdefault("KSG_KERNEL_EVENTS", "8")
     world, rank, local_rank = _dist_env()
     if world != args.gpus and world > 1:
         raise SystemExit(f"WORLD_SIZE={world} but --gpus={args.gpus}")
@@ -461,7 +466,7 @@ def main():
         # (HIP events around every timed_launch_stride-th launch of a round, the
         # sampled mean scaled to all launches; KSG_KERNEL_EVENTS=N sets the stride)
         extra = {"launches": launches, "pods_per_launch": pods_per_launch,
-                 "timed_launch_stride": int(os.environ.get("KSG_KERNEL_EVENTS", "4") or 0),
+                 "timed_launch_stride": int(os.environ.get("KSG_KERNEL_EVENTS", "8") or 0),
                  "win_eval_ms_avg": kk["eval_ms"] / launches,
                  "win_t0_ms_avg": kk["t0_ms"] / launches,
                  "win_eval_model_bytes_per_launch": ev_bytes,

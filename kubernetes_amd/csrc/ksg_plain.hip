@@ -338,14 +338,20 @@ __host__ __device__ constexpr int pl_pg(int P) { return P <= 8 ? 4 : 8; }
 #else
 #define KSG_FUSED_TASK_ATTR __forceinline__
 #endif
-template <int P>
+template <int PG>
 __device__ KSG_FUSED_TASK_ATTR void fused_score_task(const KsgDev& d, const KsgFused& f, uint32_t pos,
                                                            uint32_t n_batch, uint32_t wcap, uint32_t w, uint32_t p0,
                                                            KsgWinSum* sums, uint64_t* wbits, int32_t* wmax,
                                                            uint32_t ostride, uint64_t* wd1, uint32_t* rec_lds) {
-  win_score_wave<KSG_WIN_PLAIN, pl_pg(P), false, true>(d, f.batch, f.ids, pos, n_batch, wcap, w, p0, sums, wbits, wmax,
-                                                      ostride, nullptr, wd1, nullptr, nullptr, 0u, nullptr, nullptr,
-                                                      nullptr, nullptr, rec_lds);
+  win_score_wave<KSG_WIN_PLAIN, PG, false, true>(d, f.batch, f.ids, pos, n_batch, wcap, w, p0, sums, wbits, wmax,
+                                                 ostride, nullptr, wd1, nullptr, nullptr, 0u, nullptr, nullptr,
+                                                 nullptr, nullptr, rec_lds);
+}
+
+// arrivals that complete pod group g's counter: group 0 is scored one pod per task (the
+// resolver's first pod waits for it: a quarter of a task's scoring time), the others a group per task
+__host__ __device__ constexpr uint32_t fused_group_arrivals(uint32_t g, uint32_t nwg, uint32_t pg) {
+  return g == 0 ? nwg * pg : nwg;
 }
 
 template <int P, bool STAMP>
@@ -371,11 +377,21 @@ __device__ __forceinline__ void fused_score_blocks(const KsgDev& d, uint32_t wca
   uint64_t* wbits = reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(x.buf));
   int32_t* wmax = reinterpret_cast<int32_t*>(const_cast<uint8_t*>(x.buf) + (size_t)x.wcap * x.ostride * 8);
   uint64_t* wd1 = x.d1 ? reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(x.buf) + x.d1_off) : nullptr;
-  for (uint32_t t = ix; t < nwx * ngrp; t += nbx) {
-    const uint32_t g = t / nwx, wgp = wg0 + (t - g * nwx);
+  // tasks of this XCD's word groups: group 0 as PGF one-pod tasks per word group first, then
+  // groups 1.. a group per task
+  const uint32_t nsplit = nwx * (uint32_t)PGF;
+  for (uint32_t t = ix; t < nsplit + nwx * (ngrp - 1u); t += nbx) {
+    const bool one = t < nsplit;
+    const uint32_t sp = t / nwx;                        // (one: the pod; else the group - 1 past them)
+    const uint32_t u = one ? t : t - nsplit;
+    const uint32_t g = one ? 0u : 1u + (u / nwx);
+    const uint32_t wgp = wg0 + (u - (one ? sp : g - 1u) * nwx);
     const uint32_t w = __builtin_amdgcn_readfirstlane(wgp * NWV + wave);
     const uint32_t t_k0 = STAMP ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
-    fused_score_task<P>(d, f, pos, n_batch, wcap, w, g * PGF, sums, wbits, wmax, x.ostride, wd1, rec_lds);
+    if (one)
+      fused_score_task<1>(d, f, pos, n_batch, wcap, w, sp, sums, wbits, wmax, x.ostride, wd1, rec_lds);
+    else
+      fused_score_task<PGF>(d, f, pos, n_batch, wcap, w, g * PGF, sums, wbits, wmax, x.ostride, wd1, rec_lds);
     const uint32_t t_k1 = STAMP ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
     drain_stores();  // (every storing wave: its write-through stores have landed)
     __syncthreads();
@@ -403,29 +419,30 @@ __device__ __forceinline__ void fused_score_blocks(const KsgDev& d, uint32_t wca
 
 // has pod group g of the fused launch been scored (all word groups, summed over the 8 shards)?
 // (wave-uniform; sc1 loads of the counters)
+template <int P>
 __device__ __forceinline__ bool fused_group_done(const KsgFused& f, uint32_t g, uint32_t nwg) {
   const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   const uint32_t v = lane < 8 ? ld_mut(f.cnt + ((size_t)f.set * f.ngroups + g) * 8u + lane) : 0u;
   uint32_t s = 0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) s += (uint32_t)__builtin_amdgcn_readlane((int)v, k);
-  return s >= nwg;
+  return s >= fused_group_arrivals(g, nwg, (uint32_t)pl_pg(P));
 }
 
+// the resolver's body; two kernels below: the plain launch (no fused-launch argument at all, so
+// its code and register allocation are the resolver's alone) and the fused window launch
 template <int P, bool STAMP, bool XS, bool FUSED>
-__global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
-                                                            const KsgWinSum* __restrict__ sums, const KsgWinXchg x,
-                                                            uint64_t* rng_io, int32_t* __restrict__ out_batch,
-                                                            const KsgFused f) {
+__device__ __forceinline__ void win_plain_body(const KsgDev d, uint32_t wcap, KsgWinRun* run,
+                                               const KsgWinSum* __restrict__ sums, const KsgWinXchg x,
+                                               uint64_t* rng_io, int32_t* __restrict__ out_batch, const KsgFused f) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint32_t t_blk0 = 0;  // (KSG_DEBUG & 8, fused: block 0's start, the base of the scoring blocks' stamps)
   if constexpr (FUSED) {
     if (blockIdx.x != 0) {
       fused_score_blocks<P, STAMP>(d, wcap, run, sums, x, f, smem);
       return;
     }
-    if (STAMP && threadIdx.x == 0 && d.dbgbuf)  // (block 0's start for the scoring blocks' stamps)
-      __hip_atomic_store(d.dbgbuf + 55, (int32_t)(uint32_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (STAMP) t_blk0 = (uint32_t)__builtin_amdgcn_s_memrealtime();
   }
   // (the fused launch: the window's outcome goes into the next launch's slot)
   KsgWinRun* const run_out = FUSED ? f.run_out : run;
@@ -434,6 +451,9 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
     if (FUSED && threadIdx.x == 0) *run_out = *run;
     return;
   }
+  // (a mailbox in dbgbuf[55] while the window runs: the committer clears it at the window's end)
+  if (FUSED && STAMP && threadIdx.x == 0 && d.dbgbuf)
+    __hip_atomic_store(d.dbgbuf + 55, (int32_t)t_blk0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t n_pods = min(wcap, n_batch - pos);
   int32_t* __restrict__ out = out_batch + pos;
   const uint32_t tid = threadIdx.x;
@@ -555,7 +575,7 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
             ctl->hang = 1;
             return;
           }
-          if (fused_group_done(f, g, f_nwg) && (g_lo == g || fused_group_done(f, g_lo, f_nwg))) break;
+          if (fused_group_done<P>(f, g, f_nwg) && (g_lo == g || fused_group_done<P>(f, g_lo, f_nwg))) break;
           __builtin_amdgcn_s_sleep(1);
         }
         rec = lane < DW ? ld_mut(recs + (size_t)j * DW + lane) : 0u;
@@ -2209,6 +2229,8 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
   }
   if (lane == 0) {
     *rng_io = rng0 + (uint64_t)n_draws * ksg_rng_step(d.draws);
+    if constexpr (STAMP && FUSED)  // (the scoring blocks' stamp base, a mailbox, not a counter)
+      if (d.dbgbuf) __hip_atomic_store(d.dbgbuf + 55, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     KsgWinRun r = *run;
     if (reason == KSG_STOP_HANG) {
       r.halt = KSG_HALT_HANG;
@@ -2221,10 +2243,29 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint3
     } else {
       r.pos = pos + resolved;
       r.windows += 1;
-      if (reason >= 1 && reason <= 3) r.stops[reason] += 1;
+      // (constant indices: a dynamic one puts r in scratch, and the compiler then budgets the
+      // whole kernel's registers for a higher occupancy it never gets: config 5 -4 %)
+      r.stops[1] += reason == 1 ? 1u : 0u;
+      r.stops[2] += reason == 2 ? 1u : 0u;
+      r.stops[3] += reason == 3 ? 1u : 0u;
     }
     *run_out = r;
   }
+}
+
+template <int P, bool STAMP, bool XS>
+__global__ __launch_bounds__(pl_nt(P)) void ksg_win_plain_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
+                                                            const KsgWinSum* __restrict__ sums, const KsgWinXchg x,
+                                                            uint64_t* rng_io, int32_t* __restrict__ out_batch) {
+  win_plain_body<P, STAMP, XS, false>(d, wcap, run, sums, x, rng_io, out_batch, KsgFused{});
+}
+
+template <int P, bool STAMP>
+__global__ __launch_bounds__(pl_nt(P)) void ksg_win_fused_kernel(KsgDev d, uint32_t wcap, KsgWinRun* run,
+                                                            const KsgWinSum* __restrict__ sums, const KsgWinXchg x,
+                                                            uint64_t* rng_io, int32_t* __restrict__ out_batch,
+                                                            const KsgFused f) {
+  win_plain_body<P, STAMP, false, true>(d, wcap, run, sums, x, rng_io, out_batch, f);
 }
 
 // ---------------------------------------------------------------------------
@@ -2262,15 +2303,20 @@ template <int PP, bool ST, bool XS, bool FU = false>
 static hipError_t win_plain_launch_x(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run,
                                      const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
                                      hipStream_t st, const KsgFused& f = KsgFused{}, uint32_t grid = 1) {
+  const void* fn = FU ? reinterpret_cast<const void*>(ksg_win_fused_kernel<PP, ST>)
+                      : reinterpret_cast<const void*>(ksg_win_plain_kernel<PP, ST, XS>);
   static bool once = false;
   if (!once) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(ksg_win_plain_kernel<PP, ST, XS, FU>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipGetLastError();  // do not leave a sticky error behind
     once = true;
   }
-  hipLaunchKernelGGL((ksg_win_plain_kernel<PP, ST, XS, FU>), dim3(grid), dim3(pl_nt(PP)), lds, st, d, wcap, run, sums,
-                     x, rng, out, f);
+  if constexpr (FU)
+    hipLaunchKernelGGL((ksg_win_fused_kernel<PP, ST>), dim3(grid), dim3(pl_nt(PP)), lds, st, d, wcap, run, sums, x,
+                       rng, out, f);
+  else
+    hipLaunchKernelGGL((ksg_win_plain_kernel<PP, ST, XS>), dim3(grid), dim3(pl_nt(PP)), lds, st, d, wcap, run, sums,
+                       x, rng, out);
   return hipGetLastError();
 }
 

@@ -57,7 +57,7 @@ def test_committed_traffic_covers_the_current_build():
     need += [(w, "ksg_win_score_kernel") for w, _ in need]
     tagged = {ent.get("kernel_src_sha") for ent in tj.values()}
     if sha not in tagged:  # (a source change after the last record: the bench lines say so in traffic_source.stale)
-        pytest.skip(f"kernel sources {sha} changed since the last PMC record: run tools/gpu_r5_record.sh <tag> prof")
+        pytest.skip(f"kernel sources {sha} changed since the last PMC record: run tools/gpu_record.sh <tag> prof")
     for w, k in need:
         ent = tj.get(f"{w}:{k}")
         assert ent is not None and ent.get("kernel_src_sha") == sha, (w, k, ent and ent.get("kernel_src_sha"), sha)

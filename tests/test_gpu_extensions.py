@@ -173,10 +173,19 @@ def test_config5_extension_scores_full_size_matches_restatement():
     _config5_full_size(w_taint=1, w_bal=1)
 
 
-def _config5_full_size(w_taint, w_bal):
+def test_config2_every_extension_full_size_matches_restatement():
+    """BASELINE config 2 at its full size (5,000 nodes, 10,000 pods) with the default filter set
+    and every extension (taints and tolerations, GPU / FPGA counts, TaintToleration 1,
+    BalancedResourceAllocation 1), the shape of `bench.py --extensions`, over ten 1,000-pod
+    batches on the window path (it was checked on the GPU only up to
+    1,200 pods)."""
+    _config5_full_size(w_taint=1, w_bal=1, name="config2", nn=5000, npods=10000)
+
+
+def _config5_full_size(w_taint, w_bal, name="config5", nn=100000, npods=100000):
     import os
 
-    c = ExtCase("config5", 100000, 100000, w_taint=w_taint, w_bal=w_bal)
+    c = ExtCase(name, nn, npods, w_taint=w_taint, w_bal=w_bal)
     dev = c.load(DeviceScheduler(c.cfg, device=0))
     got, rng, windows = [], 1234, 0
     for s in range(0, len(c.batch), 1000):
