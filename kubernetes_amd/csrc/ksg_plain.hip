@@ -2271,6 +2271,69 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_fused_kernel(KsgDev d, uint3
 // ---------------------------------------------------------------------------
 // host launcher
 // ---------------------------------------------------------------------------
+// The plain resolver past 512 words per shard (P = 16, 32: config 5's 100,000 nodes) is
+// instantiated in its own translation unit, ksg_plain_large.hip, which includes this file with
+// KSG_PLAIN_LARGE_TU and is compiled with the max-ILP machine scheduler: its default schedule
+// holds the P = 32 production resolver to 137 VGPRs (3 waves per SIMD, an occupancy the LDS never
+// allows) and measured 3.5 % slower at config 5 than with 181 (same box, profiles/r6_ab_trees.json
+// ab5); the fused and small-shard kernels keep the default schedule (config 2: -1 % under max-ILP).
+template <int PP, bool ST, bool XS, bool FU = false>
+static hipError_t win_plain_launch_x(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run,
+                                     const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
+                                     hipStream_t st, const KsgFused& f = KsgFused{}, uint32_t grid = 1) {
+  // (each branch names only its own kernel: a kernel template instantiated in both translation
+  // units would be registered twice, with two schedules)
+  const void* fn;
+  if constexpr (FU) fn = reinterpret_cast<const void*>(ksg_win_fused_kernel<PP, ST>);
+  else fn = reinterpret_cast<const void*>(ksg_win_plain_kernel<PP, ST, XS>);
+  static bool once = false;
+  if (!once) {
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipGetLastError();  // do not leave a sticky error behind
+    once = true;
+  }
+  if constexpr (FU)
+    hipLaunchKernelGGL((ksg_win_fused_kernel<PP, ST>), dim3(grid), dim3(pl_nt(PP)), lds, st, d, wcap, run, sums, x,
+                       rng, out, f);
+  else
+    hipLaunchKernelGGL((ksg_win_plain_kernel<PP, ST, XS>), dim3(grid), dim3(pl_nt(PP)), lds, st, d, wcap, run, sums,
+                       x, rng, out);
+  return hipGetLastError();
+}
+
+template <int PP, bool ST>
+static hipError_t win_plain_launch(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run, const KsgWinSum* sums,
+                                   const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
+  // (extensions) extended resources on the slots
+  if (x.exts != nullptr && (((d.ext_filters & KSG_EXT_SCALAR) && d.n_scalar > 0) || x.esc))
+    return win_plain_launch_x<PP, ST, true>(d, wcap, lds, run, sums, x, rng, out, st);
+  return win_plain_launch_x<PP, ST, false>(d, wcap, lds, run, sums, x, rng, out, st);
+}
+
+// the debug instantiation: KSG_DEBUG & 8 (per-section s_memtime stamps), bits 16..19 (skews) or
+// 24..27 (timing switches); the production one keeps no debug switch in a register. Bits 22 / 23
+// (the runtime's request-corruption hook for the resident server's rejection test) and every
+// other bit keep the production resolver: a fault-injection switch never changes which resolver
+// build runs
+static bool plain_stamp(const KsgDev& d) { return (d.dbg & 8) != 0 || ((uint32_t)d.dbg & KSG_DBG_RESOLVER_MASK) != 0; }
+
+#define KSG_PLAIN_CASE(PP)                                                                         \
+  if (P == PP)                                                                                     \
+    return plain_stamp(d) ? win_plain_launch<PP, true>(d, wcap, lds, run, sums, x, rng, out, st) \
+                          : win_plain_launch<PP, false>(d, wcap, lds, run, sums, x, rng, out, st);
+
+hipError_t ksg_launch_win_plain_large(const KsgDev& d, uint32_t P, uint32_t wcap, size_t lds, KsgWinRun* run,
+                                      const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
+                                      hipStream_t st)
+#ifdef KSG_PLAIN_LARGE_TU
+{
+  KSG_PLAIN_CASE(16)
+  KSG_PLAIN_CASE(32)
+  return hipErrorInvalidValue;
+}
+#else
+    ;  // (ksg_plain_large.hip)
+
 static uint32_t plain_P(const KsgDev& d);
 uint32_t ksg_win_plain_lds(const KsgDev& d, uint32_t wcap) {
   return plain_lds_offsets(plain_P(d), (d.n_services + 31) / 32, wcap).total;
@@ -2299,56 +2362,14 @@ hipError_t ksg_launch_win_t0(const KsgDev& d, uint32_t wcap, const KsgWinRun* ru
   return hipGetLastError();
 }
 
-template <int PP, bool ST, bool XS, bool FU = false>
-static hipError_t win_plain_launch_x(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run,
-                                     const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
-                                     hipStream_t st, const KsgFused& f = KsgFused{}, uint32_t grid = 1) {
-  const void* fn = FU ? reinterpret_cast<const void*>(ksg_win_fused_kernel<PP, ST>)
-                      : reinterpret_cast<const void*>(ksg_win_plain_kernel<PP, ST, XS>);
-  static bool once = false;
-  if (!once) {
-    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)hipGetLastError();  // do not leave a sticky error behind
-    once = true;
-  }
-  if constexpr (FU)
-    hipLaunchKernelGGL((ksg_win_fused_kernel<PP, ST>), dim3(grid), dim3(pl_nt(PP)), lds, st, d, wcap, run, sums, x,
-                       rng, out, f);
-  else
-    hipLaunchKernelGGL((ksg_win_plain_kernel<PP, ST, XS>), dim3(grid), dim3(pl_nt(PP)), lds, st, d, wcap, run, sums,
-                       x, rng, out);
-  return hipGetLastError();
-}
-
-template <int PP, bool ST>
-static hipError_t win_plain_launch(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run, const KsgWinSum* sums,
-                                   const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
-  // (extensions) extended resources on the slots
-  if (x.exts != nullptr && (((d.ext_filters & KSG_EXT_SCALAR) && d.n_scalar > 0) || x.esc))
-    return win_plain_launch_x<PP, ST, true>(d, wcap, lds, run, sums, x, rng, out, st);
-  return win_plain_launch_x<PP, ST, false>(d, wcap, lds, run, sums, x, rng, out, st);
-}
-
 hipError_t ksg_launch_win_plain(const KsgDev& d, uint32_t P, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
                                 const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
   const size_t lds = plain_lds_offsets(P, (d.n_services + 31) / 32, wcap).total;
-  // the debug instantiation: KSG_DEBUG & 8 (per-section s_memtime stamps), bits 16..19 (skews) or
-  // 24..27 (timing switches); the production one keeps no debug switch in a register. Bits 22 / 23
-  // (the runtime's request-corruption hook for the resident server's rejection test) and every
-  // other bit keep the production resolver: a fault-injection switch never changes which resolver
-  // build runs
-  const bool stamp = (d.dbg & 8) != 0 || ((uint32_t)d.dbg & KSG_DBG_RESOLVER_MASK) != 0;
-#define KSG_PLAIN_CASE(PP)                                                                  \
-  if (P == PP)                                                                              \
-    return stamp ? win_plain_launch<PP, true>(d, wcap, lds, run, sums, x, rng, out, st)    \
-                 : win_plain_launch<PP, false>(d, wcap, lds, run, sums, x, rng, out, st);
   KSG_PLAIN_CASE(1)
   KSG_PLAIN_CASE(2)
   KSG_PLAIN_CASE(4)
   KSG_PLAIN_CASE(8)
-  KSG_PLAIN_CASE(16)
-  KSG_PLAIN_CASE(32)
-#undef KSG_PLAIN_CASE
+  if (P == 16 || P == 32) return ksg_launch_win_plain_large(d, P, wcap, lds, run, sums, x, rng, out, st);
   return hipErrorInvalidValue;
 }
 
@@ -2368,7 +2389,7 @@ hipError_t ksg_launch_win_fused(const KsgDev& d, uint32_t wcap, KsgWinRun* run, 
   // (the scoring blocks stage their pods' records in LDS: waves x pods x 192 B)
   const size_t lds = std::max<size_t>(plain_lds_offsets(P, (d.n_services + 31) / 32, wcap).total,
                                       (size_t)(pl_nt(P) / 64) * pl_pg((int)P) * sizeof(KsgWinSum));
-  const bool stamp = (d.dbg & 8) != 0 || ((uint32_t)d.dbg & KSG_DBG_RESOLVER_MASK) != 0;
+  const bool stamp = plain_stamp(d);
 #define KSG_FUSED_CASE(PP)                                                                                  \
   if (P == PP)                                                                                              \
     return stamp ? win_plain_launch_x<PP, true, false, true>(d, wcap, lds, run, sums, x, rng, out, st, f, grid) \
@@ -2382,3 +2403,5 @@ hipError_t ksg_launch_win_fused(const KsgDev& d, uint32_t wcap, KsgWinRun* run, 
 #undef KSG_FUSED_CASE
   return hipErrorInvalidValue;
 }
+#endif  // KSG_PLAIN_LARGE_TU
+#undef KSG_PLAIN_CASE

@@ -17,8 +17,13 @@ for s in kernels window plain admit serve; do
   hipcc $F -c "$C/ksg_$s.hip" -o "$C/_obj/ksg_$s.o" & pids="$pids $!"
 done
 hipcc $F -c "$C/ksg_runtime.cpp" -o "$C/_obj/ksg_runtime.o" & pids="$pids $!"
+L=""
+if [ -f "$C/ksg_plain_large.hip" ]; then  # (round 6: the large-shard resolvers under the max-ILP scheduler)
+  hipcc $F -mllvm -amdgpu-sched-strategy=max-ilp -c "$C/ksg_plain_large.hip" -o "$C/_obj/ksg_plain_large.o" & pids="$pids $!"
+  L="$C/_obj/ksg_plain_large.o"
+fi
 for p in $pids; do wait $p; done
-hipcc --offload-arch=gfx950 -shared -fPIC $C/_obj/ksg_{kernels,window,plain,admit,serve}.o $C/_obj/ksg_runtime.o \
+hipcc --offload-arch=gfx950 -shared -fPIC $C/_obj/ksg_{kernels,window,plain,admit,serve}.o $L $C/_obj/ksg_runtime.o \
   -o "$D/kubernetes_amd/libkschedgpu.so" -lrccl
 rm -rf "$C/_obj"
 # (its tests and docs are not needed on the box)
