@@ -4,9 +4,12 @@
 A "step" is one batch of `--batch` pods scheduled in order through the hot path
 (filter every node, score, argmax + reference tie-break, commit) by
 ksg_schedule_batch: windows of pods are scored against a snapshot on all CUs
-(ksg_win_score_kernel) and resolved in order, exactly, by one workgroup
-(ksg_win_plain_kernel, fed by ksg_win_t0_kernel's per-pod T0 images;
-ksg_win_resolve2_kernel / ksg_win_resolve_kernel with ServiceAntiAffinity);
+and resolved in order, exactly, by one workgroup. Up to 32,768 nodes on one rank
+(configs 1-3) that is one launch per window, ksg_win_fused_kernel (block 0
+resolves while the other blocks score the window); past that, sharded, or with
+the extensions, three: ksg_win_score_kernel, ksg_win_t0_kernel (per-pod T0
+images) and ksg_win_plain_kernel; with ServiceAntiAffinity the count / score
+passes and ksg_win_resolve2_kernel / ksg_win_resolve_kernel;
 node state is resident in HBM before the timed region (the C ABI copies the
 batch descriptors in, ~B*88 bytes, inside the step).
 
@@ -445,7 +448,10 @@ def main():
         kavg_s = kk["resolve_ms"] / launches / 1e3 or float("nan")
         # the in-order resolver: the plain one without ServiceAntiAffinity (ksg_plain.hip),
         # else the LDS-slot one or the register-slot re-rank (ksg_window.hip)
-        kname = ("ksg_win_plain_kernel" if plain else
+        # the fused window launch (one plain rank, no extensions): phase A runs inside the
+        # resolver's launch, one kernel per window (ksg_win_fused_kernel)
+        fused = kk["eval_ms"] == 0 and plain and world == 1
+        kname = ("ksg_win_fused_kernel" if fused else "ksg_win_plain_kernel" if plain else
                  "ksg_win_resolve_kernel" if anti else "ksg_win_resolve2_kernel")
         # phase A scores this rank's shard (N/world nodes) for the window's W pods
         # (the capacity the library used: it shrinks W where windows stop early); its
@@ -454,9 +460,7 @@ def main():
         ev_s = kk["eval_ms"] / launches / 1e3 or float("nan")
         w_used = tot1["wcap_sum"] - tot0["wcap_sum"]
         w_mean = w_used / launches if w_used > 0 else float(wcap)
-        # the fused window launch (one plain rank, no extensions): phase A runs inside the
-        # resolver's launch; its standalone time from an untimed KSG_FUSED=0 side run
-        fused = kk["eval_ms"] == 0 and plain and world == 1
+        # (fused: phase A's standalone time from an untimed KSG_FUSED=0 side run)
         side = _phase_a_standalone(cfg, view, args, step_batch, ext) if fused else None
         if side:
             ev_s = side["eval_ms_avg"] / 1e3
@@ -476,7 +480,7 @@ def main():
                  "fused_window_launch": bool(fused)}
         if fused:
             extra["win_eval_source"] = ("untimed KSG_FUSED=0 side run over the first steps: phase A's own "
-                                        "events; in the timed run it scores inside ksg_win_plain_kernel")
+                                        "events; in the timed run it scores inside ksg_win_fused_kernel")
             extra["unfused_side_run"] = side
     else:
         pods_per_launch = args.batch

@@ -51,8 +51,8 @@ def test_committed_traffic_covers_the_current_build():
     with open(os.path.join(ROOT, "profiles", "traffic.json")) as f:
         tj = json.load(f)
     sha = kernel_src_sha()
-    need = [("config1:500", "ksg_win_plain_kernel"), ("config2:5000", "ksg_win_plain_kernel"),
-            ("config3:15000", "ksg_win_plain_kernel"), ("config4:5000", "ksg_win_resolve2_kernel"),
+    need = [("config1:500", "ksg_win_fused_kernel"), ("config2:5000", "ksg_win_fused_kernel"),
+            ("config3:15000", "ksg_win_fused_kernel"), ("config4:5000", "ksg_win_resolve2_kernel"),
             ("config5:100000", "ksg_win_plain_kernel")]
     need += [(w, "ksg_win_score_kernel") for w, _ in need]
     tagged = {ent.get("kernel_src_sha") for ent in tj.values()}

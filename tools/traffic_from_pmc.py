@@ -26,7 +26,8 @@ from collections import defaultdict
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from tools.srcsha import kernel_src_sha  # noqa: E402
 
-KERNELS = {"ksg_win_plain_kernel": "ksg_win_plain_kernel", "ksg_win_t0_kernel": "ksg_win_t0_kernel",
+KERNELS = {"ksg_win_plain_kernel": "ksg_win_plain_kernel", "ksg_win_fused_kernel": "ksg_win_fused_kernel",
+           "ksg_win_t0_kernel": "ksg_win_t0_kernel",
            "ksg_win_resolve_kernel": "ksg_win_resolve_kernel", "ksg_win_resolve2_kernel": "ksg_win_resolve2_kernel",
            "ksg_win_resolve3_kernel": "ksg_win_resolve3_kernel", "ksg_win_score_kernel": "ksg_win_score_kernel",
            "ksg_batch_kernel": "ksg_batch_kernel"}
