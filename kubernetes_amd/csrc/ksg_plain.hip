@@ -2271,9 +2271,10 @@ __global__ __launch_bounds__(pl_nt(P)) void ksg_win_fused_kernel(KsgDev d, uint3
 // ---------------------------------------------------------------------------
 // host launcher
 // ---------------------------------------------------------------------------
-// The plain resolver past 512 words per shard (P = 16, 32: config 5's 100,000 nodes) is
-// instantiated in its own translation unit, ksg_plain_large.hip, which includes this file with
-// KSG_PLAIN_LARGE_TU and is compiled with the max-ILP machine scheduler: its default schedule
+// The plain resolver past 512 words per shard (P = 16, 32: config 5's 100,000 nodes) and the
+// extension (XS) resolvers are instantiated in their own translation unit, ksg_plain_large.hip,
+// which includes this file with KSG_PLAIN_LARGE_TU and is compiled with the max-ILP machine
+// scheduler: its default schedule
 // holds the P = 32 production resolver to 137 VGPRs (3 waves per SIMD, an occupancy the LDS never
 // allows) and measured 3.5 % slower at config 5 than with 181 (same box, profiles/r6_ab_trees.json
 // ab5); the fused and small-shard kernels keep the default schedule (config 2: -1 % under max-ILP).
@@ -2301,13 +2302,9 @@ static hipError_t win_plain_launch_x(const KsgDev& d, uint32_t wcap, size_t lds,
   return hipGetLastError();
 }
 
-template <int PP, bool ST>
-static hipError_t win_plain_launch(const KsgDev& d, uint32_t wcap, size_t lds, KsgWinRun* run, const KsgWinSum* sums,
-                                   const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
-  // (extensions) extended resources on the slots
-  if (x.exts != nullptr && (((d.ext_filters & KSG_EXT_SCALAR) && d.n_scalar > 0) || x.esc))
-    return win_plain_launch_x<PP, ST, true>(d, wcap, lds, run, sums, x, rng, out, st);
-  return win_plain_launch_x<PP, ST, false>(d, wcap, lds, run, sums, x, rng, out, st);
+// (extensions) extended resources / extension scores re-checked on the slots: the XS instantiation
+static bool plain_xs(const KsgDev& d, const KsgWinXchg& x) {
+  return x.exts != nullptr && (((d.ext_filters & KSG_EXT_SCALAR) && d.n_scalar > 0) || x.esc);
 }
 
 // the debug instantiation: KSG_DEBUG & 8 (per-section s_memtime stamps), bits 16..19 (skews) or
@@ -2317,18 +2314,29 @@ static hipError_t win_plain_launch(const KsgDev& d, uint32_t wcap, size_t lds, K
 // build runs
 static bool plain_stamp(const KsgDev& d) { return (d.dbg & 8) != 0 || ((uint32_t)d.dbg & KSG_DBG_RESOLVER_MASK) != 0; }
 
-#define KSG_PLAIN_CASE(PP)                                                                         \
-  if (P == PP)                                                                                     \
-    return plain_stamp(d) ? win_plain_launch<PP, true>(d, wcap, lds, run, sums, x, rng, out, st) \
-                          : win_plain_launch<PP, false>(d, wcap, lds, run, sums, x, rng, out, st);
+#define KSG_PLAIN_CASE(PP, XS)                                                                              \
+  if (P == PP)                                                                                              \
+    return plain_stamp(d) ? win_plain_launch_x<PP, true, XS>(d, wcap, lds, run, sums, x, rng, out, st)    \
+                          : win_plain_launch_x<PP, false, XS>(d, wcap, lds, run, sums, x, rng, out, st);
 
-hipError_t ksg_launch_win_plain_large(const KsgDev& d, uint32_t P, uint32_t wcap, size_t lds, KsgWinRun* run,
-                                      const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
-                                      hipStream_t st)
+// the max-ILP translation unit's share: P = 16, 32, and the extension (XS) resolvers at every P
+// (config 2 + every extension: 230k -> 235k pods/s under max-ILP, same box, profiles/r6_ab_trees.json ab7)
+hipError_t ksg_launch_win_plain_ilp(const KsgDev& d, uint32_t P, uint32_t wcap, size_t lds, KsgWinRun* run,
+                                    const KsgWinSum* sums, const KsgWinXchg& x, uint64_t* rng, int32_t* out,
+                                    hipStream_t st)
 #ifdef KSG_PLAIN_LARGE_TU
 {
-  KSG_PLAIN_CASE(16)
-  KSG_PLAIN_CASE(32)
+  if (plain_xs(d, x)) {
+    KSG_PLAIN_CASE(1, true)
+    KSG_PLAIN_CASE(2, true)
+    KSG_PLAIN_CASE(4, true)
+    KSG_PLAIN_CASE(8, true)
+    KSG_PLAIN_CASE(16, true)
+    KSG_PLAIN_CASE(32, true)
+  } else {
+    KSG_PLAIN_CASE(16, false)
+    KSG_PLAIN_CASE(32, false)
+  }
   return hipErrorInvalidValue;
 }
 #else
@@ -2365,11 +2373,11 @@ hipError_t ksg_launch_win_t0(const KsgDev& d, uint32_t wcap, const KsgWinRun* ru
 hipError_t ksg_launch_win_plain(const KsgDev& d, uint32_t P, uint32_t wcap, KsgWinRun* run, const KsgWinSum* sums,
                                 const KsgWinXchg& x, uint64_t* rng, int32_t* out, hipStream_t st) {
   const size_t lds = plain_lds_offsets(P, (d.n_services + 31) / 32, wcap).total;
-  KSG_PLAIN_CASE(1)
-  KSG_PLAIN_CASE(2)
-  KSG_PLAIN_CASE(4)
-  KSG_PLAIN_CASE(8)
-  if (P == 16 || P == 32) return ksg_launch_win_plain_large(d, P, wcap, lds, run, sums, x, rng, out, st);
+  if (P >= 16 || plain_xs(d, x)) return ksg_launch_win_plain_ilp(d, P, wcap, lds, run, sums, x, rng, out, st);
+  KSG_PLAIN_CASE(1, false)
+  KSG_PLAIN_CASE(2, false)
+  KSG_PLAIN_CASE(4, false)
+  KSG_PLAIN_CASE(8, false)
   return hipErrorInvalidValue;
 }
 
