@@ -56,8 +56,12 @@ def test_committed_traffic_covers_the_current_build():
             ("config5:100000", "ksg_win_plain_kernel")]
     need += [(w, "ksg_win_score_kernel") for w, _ in need]
     tagged = {ent.get("kernel_src_sha") for ent in tj.values()}
-    if sha not in tagged:  # (a source change after the last record: the bench lines say so in traffic_source.stale)
-        pytest.skip(f"kernel sources {sha} changed since the last PMC record: run tools/gpu_record.sh <tag> prof")
+    if sha not in tagged and os.environ.get("KSG_TRAFFIC_STALE_OK") == "1":
+        # (an explicit opt-out while kernels are being changed between two records; ADVICE round 5:
+        # a plain skip would make this guard a no-op)
+        pytest.skip(f"kernel sources {sha} changed since the last PMC record (KSG_TRAFFIC_STALE_OK=1)")
+    assert sha in tagged, (f"kernel sources {sha} changed since the last PMC record: "
+                           "run tools/gpu_record.sh <tag> prof <workload> for every default workload")
     for w, k in need:
         ent = tj.get(f"{w}:{k}")
         assert ent is not None and ent.get("kernel_src_sha") == sha, (w, k, ent and ent.get("kernel_src_sha"), sha)
