@@ -279,6 +279,9 @@ def main():
     ap.add_argument("--ext-filters-only", action="store_true",
                     help="with --extensions: the filters only (taints, extended resources), TaintToleration and "
                          "BalancedResourceAllocation weights 0")
+    ap.add_argument("--ext-taints-only", action="store_true",
+                    help="with --extensions --ext-filters-only: no extended resources either (taints and "
+                         "tolerations only: with ServiceAntiAffinity, config 4, the window path takes them)")
     ap.add_argument("--prefix-pods", type=int, default=0,
                     help="place this many of the workload's first pods (untimed, 5,000-pod batches) before the "
                          "warm-up, so the timed steps run on the late-run state (fuller nodes, FitErrors); the "
@@ -317,7 +320,8 @@ def main():
 
         fo = args.ext_filters_only
         ecfg, node_taints, node_scalar, tols, scal = workload.extension_data(n_nodes, n_pods, w_taint=0 if fo else 1,
-                                                                             w_bal=0 if fo else 1)
+                                                                             w_bal=0 if fo else 1,
+                                                                             gpus=not (fo and args.ext_taints_only))
         inter = ExtInterner(ecfg)
         node_arrays = inter.node_arrays(node_taints, node_scalar)
         rec, ids_x = inter.pod_records(batch.ids, tols, scal)
@@ -652,7 +656,9 @@ def main():
         "data": "synthetic (seeded splitmix64 scheduler_perf-style cluster; SURVEY.md 8(d))",
         "config": {"workload": f"{wl}: {n_nodes} nodes, {n_pods} pods, "
                                + ("DefaultProvider" if wl in ("config2", "config3", "config5") else wl)
-                               + ((" + extension filters (taints/tolerations, GPU/FPGA counts; scoring "
+                               + ((" + extension filters (taints/tolerations; scoring extensions off; parity "
+                                   "unpinned)" if args.ext_filters_only and args.ext_taints_only else
+                                   " + extension filters (taints/tolerations, GPU/FPGA counts; scoring "
                                    "extensions off; parity unpinned, window path)" if args.ext_filters_only else
                                    " + extensions (taints/tolerations, GPU/FPGA counts, TaintToleration, "
                                    "BalancedResourceAllocation; parity unpinned)") if ext else ""),

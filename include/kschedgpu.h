@@ -465,7 +465,10 @@ int ksg_admit_pods(ksg_ctx* ctx, const ksg_admission_set* sets, uint32_t n_sets,
  * window on the window path and per pod on the per-pod path. Batches take the
  * speculative-window path (otherwise the exact one-pod-at-a-time kernels) unless
  *   - a pod's extended-resource request is outside [0, 2^16], or
- *   - the config has a ServiceAntiAffinity priority, or
+ *   - the config has a ServiceAntiAffinity priority and either extension score
+ *     is on or a pod of the batch requests an extended resource (with both
+ *     scores off and no requests the filters are static per (pod, node) and the
+ *     anti-affinity window path takes them, round 6), or
  *   - TaintToleration scores (w_taint_toleration != 0) with max_taints > 64 (the
  *     window path counts a node's taints as one 64-bit mask),
  * on top of the window path's general conditions (ksg_set_window). The reference's

@@ -762,7 +762,17 @@ bool use_window(ksg_ctx* c, const ksg_pod* pods, uint32_t n) {
   // ServiceAntiAffinity, negative requests and requests past 2^16 take the exact
   // kernels.
   if (c->ext_on) {
-    if (anti_on(c)) return false;
+    // ServiceAntiAffinity with the extensions: the window path only for the static filters —
+    // PodToleratesNodeTaints, and extended resources no pod of the batch requests (a zero request
+    // fits whatever the node's usage) — with both extension scores off: the anti-affinity
+    // resolvers re-check nothing extension-specific on the window's committed nodes
+    if (anti_on(c)) {
+      if (c->ext.w_taint_toleration != 0 || c->ext.w_balanced != 0) return false;
+      if (c->cur_ext)
+        for (uint32_t i = 0; i < n; ++i)
+          for (uint32_t r = 0; r < c->ext.n_scalar; ++r)
+            if (c->cur_ext[i].scalar[r] != 0) return false;
+    }
     if (c->ext.w_taint_toleration != 0 && !c->dev.ntaint) return false;
     if (c->cur_ext)
       for (uint32_t i = 0; i < n; ++i)
@@ -2287,7 +2297,7 @@ int ksg_schedule_batch(ksg_ctx* c, const ksg_pod* pods, uint32_t n, const uint32
           // ServiceAntiAffinity: the pods' per-domain counts over their filtered nodes first
           // (into d_dcnt, zero: the previous resolver cleared it)
           HIPCHK(c, ksg_launch_win_eval(c->dev, 1, c->d_pods, c->d_ids, c->d_run, W, c->d_winsum, wbits, wmax,
-                                        x.ostride, c->d_dcnt, nullptr, x.dmb, nullptr, x.dz, c->st));
+                                        x.ostride, c->d_dcnt, nullptr, x.dmb, nullptr, x.dz, c->st, dext));
           if (c->xchg && (rc = allreduce_sum_i32(c, c->d_dcnt, c->d_dcnt, (uint32_t)dcnt_n))) return rc;
         }
         if (etm) {  // TaintToleration: each pod's max soft-taint count over its filtered nodes first

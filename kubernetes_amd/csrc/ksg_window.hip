@@ -2741,7 +2741,14 @@ hipError_t ksg_launch_win_eval(const KsgDev& d, int mode, const ksg_pod* batch, 
   if (exts && mode == KSG_WIN_TMAX) {  // extensions: the TaintToleration count pass
     if (small) KSG_EVAL_LAUNCH_X(KSG_WIN_TMAX, KSG_PG_SMALL);
     else KSG_EVAL_LAUNCH_X(KSG_WIN_TMAX, KSG_PG_LARGE);
-  } else if (exts) {  // extensions (plain mode only: the host keeps ServiceAntiAffinity off this path)
+  } else if (exts && mode == KSG_WIN_COUNT) {  // ServiceAntiAffinity with the extension filters (round 6:
+    // taints only, no extension scores, no extended-resource requests in the batch; use_window)
+    if (small) KSG_EVAL_LAUNCH_X(KSG_WIN_COUNT, KSG_PG_SMALL);
+    else KSG_EVAL_LAUNCH_X(KSG_WIN_COUNT, KSG_PG_LARGE);
+  } else if (exts && mode == KSG_WIN_ANTI) {
+    if (small) KSG_EVAL_LAUNCH_X(KSG_WIN_ANTI, KSG_PG_SMALL);
+    else KSG_EVAL_LAUNCH_X(KSG_WIN_ANTI, KSG_PG_LARGE);
+  } else if (exts) {  // extensions, plain mode
     if (small) KSG_EVAL_LAUNCH_X(KSG_WIN_PLAIN, KSG_PG_SMALL);
     else KSG_EVAL_LAUNCH_X(KSG_WIN_PLAIN, KSG_PG_LARGE);
   } else if (mode == KSG_WIN_COUNT) {

@@ -1,4 +1,4 @@
-drop-in per-pod latency from C (ksg_schedule_begin + ksg_schedule_commit) for the given
+# Drop-in per-pod latency from C (ksg_schedule_begin + ksg_schedule_commit) for the given
 # tools/bin/dropin_latency argument sets ("nodes pods warmup want_fail ext policy"), one JSON line
 # each into gpurun_out/<tag>_dropin.jsonl. usage: tools/gpu_dropin.sh <tag> "<args>" ...
 set -o pipefail
