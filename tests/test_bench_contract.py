@@ -65,3 +65,23 @@ def test_committed_traffic_covers_the_current_build():
     for w, k in need:
         ent = tj.get(f"{w}:{k}")
         assert ent is not None and ent.get("kernel_src_sha") == sha, (w, k, ent and ent.get("kernel_src_sha"), sha)
+
+
+def test_fill_traffic_takes_only_entries_of_the_lines_own_sources():
+    """tools/fill_traffic.py: a recorded line's counter fields come from profiles/traffic.json
+    entries measured on the same kernel sources as the line (its traffic_source.kernel_src_sha);
+    an entry of other sources is refused and listed as stale."""
+    from tools.fill_traffic import fill
+    line = {"config": {"workload": "config2: 5000 nodes, 10000 pods, DefaultProvider", "nodes": 5000},
+            "roofline": {"kernel": "ksg_win_fused_kernel", "traffic": None,
+                         "traffic_source": {"kernel_src_sha": "a" * 16}},
+            "filter_score": {"ms_avg": 0.01, "basis": "byte_model", "bytes_per_launch": 1.0, "frac": 0.0}}
+    tj = {"config2:5000:ksg_win_fused_kernel": {"hbm_bytes_per_launch": 2.0e6, "source": "p", "round": "r6",
+                                                "kernel_src_sha": "a" * 16},
+          "config2:5000:ksg_win_score_kernel": {"hbm_bytes_per_launch": 8.0e5, "source": "q", "round": "r5",
+                                                "kernel_src_sha": "b" * 16}}
+    d = fill(json.loads(json.dumps(line)), tj)
+    assert d["roofline"]["traffic"] == 2.0e6
+    assert d["filter_score"]["basis"] == "byte_model"  # (the score entry is from other sources)
+    assert [s["source"] for s in d["roofline"]["traffic_source"]["stale"]] == ["q"]
+    assert d["traffic_filled_after_run"]
