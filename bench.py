@@ -4,7 +4,7 @@
 A "step" is one batch of `--batch` pods scheduled in order through the hot path
 (filter every node, score, argmax + reference tie-break, commit) by
 ksg_schedule_batch: windows of pods are scored against a snapshot on all CUs
-and resolved in order, exactly, by one workgroup. Up to 32,768 nodes on one rank
+and resolved in order, exactly, by one workgroup. Up to 65,536 nodes on one rank
 (configs 1-3) that is one launch per window, ksg_win_fused_kernel (block 0
 resolves while the other blocks score the window); past that, sharded, or with
 the extensions, three: ksg_win_score_kernel, ksg_win_t0_kernel (per-pod T0

@@ -236,10 +236,11 @@ struct ksg_ctx {
   // ServiceAntiAffinity or extensions (KSG_FUSED=0: phase A, T0 images and resolver apart)
   bool win_fused = true;
   uint32_t fused_grid = 0;          // its blocks: one per CU (KSG_FUSED_GRID overrides)
-  // ... up to this many 64-node words per shard (KSG_FUSED_MAX_WORDS): past them the scoring blocks,
-  // one per CU under the resolver's LDS, are too few waves to hide phase A's load latency (config 5,
-  // 100k nodes, same box: 255k fused against 385k apart)
-  uint32_t fused_max_words = 512;
+  // ... up to this many 64-node words per shard (KSG_FUSED_MAX_WORDS; 65,536 nodes): past them the
+  // scoring blocks, one per CU under the resolver's LDS, are too few waves to hide phase A's load
+  // latency (config 5, 100k nodes, same box: 255k fused against 385k apart; 45k nodes: 492k fused
+  // against 465k, profiles/r6_fused_threshold.json)
+  uint32_t fused_max_words = 1024;
   uint8_t* d_fctl = nullptr;        // KsgWinRun[2], then the counters uint32[2][groups][8]
   uint8_t* h_fctl = nullptr;        // pinned: the round's first slot and zeroed counters
   double last_hus[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // host us per phase of the last batch (ksg_last_batch_host_us)

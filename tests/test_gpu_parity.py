@@ -207,6 +207,27 @@ def test_batch_uid_reuse_after_no_fit_and_in_batch_duplicates():
         dev.close()
 
 
+@pytest.mark.parametrize("max_words", ["1024", "512"])
+def test_fused_launch_at_p16_matches_oracle(max_words, monkeypatch):
+    """40,000 nodes (625 words, P = 16): the fused window launch by default since round 6
+    (KSG_FUSED_MAX_WORDS 1024), three launches with the gate at 512; both bit-exact against the
+    oracle, and the launch form asserted from the kernel events (the fused launch has no phase-A
+    events of its own)."""
+    monkeypatch.setenv("KSG_KERNEL_EVENTS", "1")
+    monkeypatch.setenv("KSG_FUSED_MAX_WORDS", max_words)
+    case = Case("config2", 40000, 1500)
+    dev, orc = _pair(case, 128)
+    got, sg = run_batch(dev, case, chunk=500)
+    want, sw = run_batch(orc, case, chunk=500)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"first mismatches at {bad[:8]}: gpu {got[bad[:8]]} oracle {want[bad[:8]]}"
+    assert sg == sw
+    k = dev.last_batch_kernel_ms()
+    assert k["launches"] > 0 and k["resolve_ms"] > 0
+    assert (k["eval_ms"] == 0) == (max_words == "1024"), k
+    dev.close()
+
+
 def test_kernel_time_sampling_strides(monkeypatch):
     """ksg_last_batch_kernel_ms: HIP events around every N-th window launch
     (KSG_KERNEL_EVENTS=N at context creation), scaled to all launches; 0 times
